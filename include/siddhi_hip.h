@@ -1,0 +1,133 @@
+/*
+ * siddhi_hip.h — C-ABI of libsiddhi_hip.so, the MI355X (gfx950) batch NFA
+ * matcher that replaces siddhi-core's pattern/sequence runtime
+ * (io.siddhi.core.query.input.stream.state) behind the unchanged
+ * SiddhiManager / SiddhiAppRuntime / InputHandler / StreamCallback API.
+ *
+ * Each entry point names the reference interface it replaces. The Java host
+ * (JNI shim) or the Python mirror (siddhi_amd/) calls these;
+ * no torch types cross this boundary.
+ *
+ * Threading: calls on one handle are serialised by the caller (the reference
+ * serialises a query under patternSyncObject, MultiProcessStreamReceiver.java:158).
+ * Independent handles may run concurrently, each on its own HIP stream.
+ * Results come back through sh_drain; the library never calls back.
+ */
+#ifndef SIDDHI_HIP_H
+#define SIDDHI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "sh_query.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes (the JNI shim maps them to SiddhiAppCreationException /
+   SiddhiAppRuntimeException; SH_E_UNSUPPORTED at compile time means the host
+   keeps the stock Java runtime for that app) */
+#define SH_OK 0
+#define SH_E_INVALID_ARG (-1)
+#define SH_E_OOM (-2)
+#define SH_E_HIP (-3)
+#define SH_E_UNSUPPORTED (-4)
+#define SH_E_STATE_OVERFLOW (-5)
+#define SH_E_MORE (-6)
+#define SH_E_NO_DEVICE (-7)
+
+typedef struct sh_handle sh_handle;
+
+/* One InputHandler.send(Event[]) call, packed as SoA (columns in the stream
+   definition's attribute order, each in its natural width: INT/STRING-id ->
+   int32, LONG -> int64, FLOAT -> float, DOUBLE -> double, BOOL -> uint8). */
+typedef struct sh_batch {
+    int32_t stream;              /* app stream index                                */
+    int32_t on_device;           /* 1: every pointer below is a device (HBM) pointer */
+    int64_t n;                   /* events in this send() call                      */
+    const int64_t* ts;           /* event timestamps (ms)                           */
+    const int32_t* keys;         /* partition key ids (attr.toString() dictionary), -1 = null key; NULL if unpartitioned */
+    const void* const* cols;     /* n_attrs column pointers                         */
+    const uint8_t* const* nulls; /* per column null mask (1 = null) or NULL          */
+} sh_batch;
+
+/* Match output: the ordered stream StreamCallback.receive(Event[]) would see.
+   Caller-provided buffers with a capacity; SH_E_MORE if more remain. */
+typedef struct sh_match_buf {
+    int64_t capacity;            /* rows the buffers below can hold                 */
+    int64_t count;               /* out: rows written                               */
+    int32_t* query;              /* out: query index that emitted the row           */
+    uint64_t* trigger_seq;       /* out: global input sequence number of the event being processed */
+    int64_t* ts;                 /* out: output Event timestamp (StateEvent ts)      */
+    int64_t* values;             /* out: count x n_out raw 8-byte values (row-major) */
+    uint8_t* nulls;              /* out: count x n_out null flags                    */
+    int32_t n_out;               /* columns per row = max outputs over the app's queries */
+    int32_t pad;
+} sh_match_buf;
+
+/* Replaces SiddhiAppParser/QueryParser -> StateInputStreamParser.parseInputStream
+   (core/util/parser/StateInputStreamParser.java:76-146): lowers every query's
+   state-element tree to the device NFA table. */
+int sh_compile(const sh_app_desc* app, sh_handle** out);
+
+/* Replaces InputHandler.send(Event[]) -> StreamJunction.sendEvent ->
+   [PartitionStreamReceiver.receive] -> Pattern/Sequence*ProcessStreamReceiver.receive
+   (core/stream/input/InputHandler.java:85-96, core/partition/PartitionStreamReceiver.java:176-216,
+   core/query/input/MultiProcessStreamReceiver.java:155-183). */
+int sh_push_batch(sh_handle* h, const sh_batch* batch);
+
+/* Replaces the playback clock advance TimestampGeneratorImpl.setCurrentTimestamp
+   -> Scheduler.onTimeChange (core/util/timestamp/TimestampGeneratorImpl.java:105-121,
+   core/util/Scheduler.java:74-99). */
+int sh_advance_time(sh_handle* h, int64_t now_ms);
+
+/* Replaces OutputRateLimiter.sendToCallBacks -> StreamCallback.receive
+   (core/query/output/ratelimit/OutputRateLimiter.java:63-106): ordered matches. */
+int sh_drain(sh_handle* h, sh_match_buf* out);
+
+/* Number of rows sh_drain would return right now (forces pending device work). */
+int64_t sh_pending(sh_handle* h);
+
+/* Replaces SiddhiAppRuntime.shutdown for the matcher's state. */
+void sh_destroy(sh_handle* h);
+
+const char* sh_last_error(sh_handle* h);
+
+/* ---- device-resident bulk path (bench / throughput) ----------------------
+   Matches on `n` events already resident in HBM for a single-stream app,
+   starting from fresh per-key state, writing the ordered match stream to
+   device buffers. Times only device work; the caller owns all buffers. */
+typedef struct sh_device_run {
+    int64_t n;                   /* events                                         */
+    const int64_t* d_ts;
+    const int32_t* d_keys;       /* partition key ids (dense 0..n_keys-1)           */
+    int32_t n_keys;
+    int32_t pad;
+    const void* const* d_cols;   /* device column pointers, stream attribute order  */
+    int64_t out_capacity;        /* rows the output buffers hold                    */
+    uint64_t* d_out_seq;         /* out: trigger_seq per match (ordered)            */
+    int64_t* d_out_values;       /* out: out_capacity x n_out raw values            */
+    int64_t out_count;           /* out: matches produced                           */
+    void* stream;                /* hipStream_t to run on (NULL = default)          */
+} sh_device_run;
+
+int sh_run_device(sh_handle* h, sh_device_run* run);
+
+/* kernel timing of the last sh_run_device call (HIP events on run->stream) */
+typedef struct sh_kernel_times {
+    float segment_ms;            /* radix segment by (key, seq)                    */
+    float advance_ms;            /* per-key NFA state advance                       */
+    float emit_ms;               /* match compaction / ordered placement            */
+    float total_ms;
+    int64_t advance_launches;
+} sh_kernel_times;
+int sh_last_kernel_times(sh_handle* h, sh_kernel_times* t);
+
+/* library / device info */
+const char* sh_version(void);
+int sh_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIDDHI_HIP_H */

@@ -1,0 +1,130 @@
+"""ctypes mirror of include/sh_query.h and include/siddhi_hip.h (the C-ABI boundary)."""
+import ctypes as C
+
+SH_DESC_VERSION = 1
+
+SH_OK = 0
+SH_E_INVALID_ARG = -1
+SH_E_OOM = -2
+SH_E_HIP = -3
+SH_E_UNSUPPORTED = -4
+SH_E_STATE_OVERFLOW = -5
+SH_E_MORE = -6
+SH_E_NO_DEVICE = -7
+
+STATUS_NAMES = {0: "OK", -1: "INVALID_ARG", -2: "OOM", -3: "HIP", -4: "UNSUPPORTED",
+                -5: "STATE_OVERFLOW", -6: "MORE", -7: "NO_DEVICE"}
+
+
+class sh_expr(C.Structure):
+    _fields_ = [("op", C.c_int32), ("type", C.c_int32), ("lhs", C.c_int32), ("rhs", C.c_int32),
+                ("third", C.c_int32), ("ltype", C.c_int32), ("rtype", C.c_int32),
+                ("slot", C.c_int32), ("chain", C.c_int32), ("attr", C.c_int32),
+                ("is_null", C.c_int32), ("pad", C.c_int32), ("cval", C.c_int64)]
+
+
+class sh_state_elem(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("child0", C.c_int32), ("child1", C.c_int32),
+                ("stream", C.c_int32), ("filter", C.c_int32), ("slot", C.c_int32),
+                ("min_count", C.c_int32), ("max_count", C.c_int32), ("waiting_ms", C.c_int64)]
+
+
+class sh_output_attr(C.Structure):
+    _fields_ = [("expr", C.c_int32), ("agg", C.c_int32), ("type", C.c_int32), ("pad", C.c_int32)]
+
+
+class sh_stream_def(C.Structure):
+    _fields_ = [("n_attrs", C.c_int32), ("pad", C.c_int32), ("attr_types", C.POINTER(C.c_int32))]
+
+
+class sh_query_desc(C.Structure):
+    _fields_ = [("state_type", C.c_int32), ("root", C.c_int32), ("n_elems", C.c_int32),
+                ("n_exprs", C.c_int32), ("n_outputs", C.c_int32), ("n_slots", C.c_int32),
+                ("partition", C.c_int32), ("output_stream", C.c_int32), ("within_ms", C.c_int64),
+                ("elems", C.POINTER(sh_state_elem)), ("exprs", C.POINTER(sh_expr)),
+                ("outputs", C.POINTER(sh_output_attr))]
+
+
+class sh_app_desc(C.Structure):
+    _fields_ = [("version", C.c_int32), ("n_streams", C.c_int32), ("n_queries", C.c_int32),
+                ("n_partitions", C.c_int32), ("playback", C.c_int32), ("pad", C.c_int32),
+                ("streams", C.POINTER(sh_stream_def)), ("queries", C.POINTER(sh_query_desc)),
+                ("partition_streams", C.POINTER(C.c_uint8))]
+
+
+class sh_batch(C.Structure):
+    _fields_ = [("stream", C.c_int32), ("on_device", C.c_int32), ("n", C.c_int64),
+                ("ts", C.c_void_p), ("keys", C.c_void_p),
+                ("cols", C.POINTER(C.c_void_p)), ("nulls", C.POINTER(C.c_void_p))]
+
+
+class sh_match_buf(C.Structure):
+    _fields_ = [("capacity", C.c_int64), ("count", C.c_int64),
+                ("query", C.POINTER(C.c_int32)), ("trigger_seq", C.POINTER(C.c_uint64)),
+                ("ts", C.POINTER(C.c_int64)), ("values", C.POINTER(C.c_int64)),
+                ("nulls", C.POINTER(C.c_uint8)), ("n_out", C.c_int32), ("pad", C.c_int32)]
+
+
+class sh_device_run(C.Structure):
+    _fields_ = [("n", C.c_int64), ("d_ts", C.c_void_p), ("d_keys", C.c_void_p),
+                ("n_keys", C.c_int32), ("pad", C.c_int32), ("d_cols", C.POINTER(C.c_void_p)),
+                ("out_capacity", C.c_int64), ("d_out_seq", C.c_void_p),
+                ("d_out_values", C.c_void_p), ("out_count", C.c_int64), ("stream", C.c_void_p)]
+
+
+class sh_kernel_times(C.Structure):
+    _fields_ = [("segment_ms", C.c_float), ("advance_ms", C.c_float), ("emit_ms", C.c_float),
+                ("total_ms", C.c_float), ("advance_launches", C.c_int64)]
+
+
+# every symbol include/siddhi_hip.h declares (checked by tests/test_abi.py)
+EXPORTED = ["sh_compile", "sh_push_batch", "sh_advance_time", "sh_drain", "sh_pending",
+            "sh_destroy", "sh_last_error", "sh_run_device", "sh_last_kernel_times",
+            "sh_version", "sh_device_count"]
+
+
+def bind_product(lib):
+    lib.sh_compile.argtypes = [C.POINTER(sh_app_desc), C.POINTER(C.c_void_p)]
+    lib.sh_compile.restype = C.c_int
+    lib.sh_push_batch.argtypes = [C.c_void_p, C.POINTER(sh_batch)]
+    lib.sh_push_batch.restype = C.c_int
+    lib.sh_advance_time.argtypes = [C.c_void_p, C.c_int64]
+    lib.sh_advance_time.restype = C.c_int
+    lib.sh_drain.argtypes = [C.c_void_p, C.POINTER(sh_match_buf)]
+    lib.sh_drain.restype = C.c_int
+    lib.sh_pending.argtypes = [C.c_void_p]
+    lib.sh_pending.restype = C.c_int64
+    lib.sh_destroy.argtypes = [C.c_void_p]
+    lib.sh_destroy.restype = None
+    lib.sh_last_error.argtypes = [C.c_void_p]
+    lib.sh_last_error.restype = C.c_char_p
+    lib.sh_run_device.argtypes = [C.c_void_p, C.POINTER(sh_device_run)]
+    lib.sh_run_device.restype = C.c_int
+    lib.sh_last_kernel_times.argtypes = [C.c_void_p, C.POINTER(sh_kernel_times)]
+    lib.sh_last_kernel_times.restype = C.c_int
+    lib.sh_version.argtypes = []
+    lib.sh_version.restype = C.c_char_p
+    lib.sh_device_count.argtypes = []
+    lib.sh_device_count.restype = C.c_int
+    return lib
+
+
+def bind_oracle(lib):
+    lib.ref_create.argtypes = [C.POINTER(sh_app_desc), C.c_char_p, C.c_int]
+    lib.ref_create.restype = C.c_void_p
+    lib.ref_start.argtypes = [C.c_void_p]
+    lib.ref_start.restype = None
+    lib.ref_send.argtypes = [C.c_void_p, C.POINTER(sh_batch), C.c_uint64]
+    lib.ref_send.restype = C.c_int
+    lib.ref_advance_time.argtypes = [C.c_void_p, C.c_int64]
+    lib.ref_advance_time.restype = C.c_int
+    lib.ref_out_count.argtypes = [C.c_void_p]
+    lib.ref_out_count.restype = C.c_int64
+    lib.ref_out_read.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+    lib.ref_out_read.restype = C.c_int
+    lib.ref_out_clear.argtypes = [C.c_void_p]
+    lib.ref_out_clear.restype = None
+    lib.ref_destroy.argtypes = [C.c_void_p]
+    lib.ref_destroy.restype = None
+    return lib

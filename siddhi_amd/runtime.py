@@ -1,0 +1,340 @@
+"""Host-side mirror of siddhi-core's public API for the pattern/sequence path.
+
+Same names, argument meaning and error behaviour as
+  core/SiddhiManager.java:93                       createSiddhiAppRuntime
+  core/SiddhiAppRuntime.java:115-144               getInputHandler / addCallback / start / shutdown
+  core/stream/input/InputHandler.java:65-96        send(Object[]) / send(long, Object[]) / send(Event[])
+  core/stream/output/StreamCallback.java           receive(Event[])
+  core/query/output/callback/QueryCallback.java    receive(timestamp, inEvents, removeEvents)
+  core/event/Event.java                            Event(timestamp, data, isExpired)
+
+The matcher itself runs behind the C-ABI (libsiddhi_hip.so) through an engine
+object; the default engine is the HIP one (siddhi_amd._native.HipEngine), which
+fails loudly when the extension is missing.
+
+Time: `send(Object[])` stamps events with the runtime clock. Outside
+@app:playback the reference uses System.currentTimeMillis(); this mirror keeps a
+virtual clock advanced by `SiddhiAppRuntime.sleep(ms)` so that tests written with
+Thread.sleep are deterministic ("time").
+"""
+from __future__ import annotations
+
+import struct
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+
+from . import compiler as cp
+from .compiler import (BOOL, DOUBLE, FLOAT, INT, LONG, OBJECT, STRING, CompiledApp,
+                       SiddhiAppValidationException, SiddhiParserException, UnsupportedQuery)
+
+__all__ = ["SiddhiManager", "SiddhiAppRuntime", "InputHandler", "StreamCallback", "QueryCallback",
+           "Event", "SiddhiAppCreationException", "SiddhiAppRuntimeException"]
+
+
+class SiddhiAppCreationException(Exception):
+    pass
+
+
+class SiddhiAppRuntimeException(Exception):
+    pass
+
+
+class Event:
+    """core/event/Event.java"""
+
+    __slots__ = ("timestamp", "data", "is_expired")
+
+    def __init__(self, timestamp: int = -1, data=None, is_expired: bool = False):
+        self.timestamp = timestamp
+        self.data = list(data) if data is not None else []
+        self.is_expired = is_expired
+
+    def getTimestamp(self):
+        return self.timestamp
+
+    def getData(self, i=None):
+        return self.data if i is None else self.data[i]
+
+    def isExpired(self):
+        return self.is_expired
+
+    def __repr__(self):
+        return f"Event{{timestamp={self.timestamp}, data={self.data}, isExpired={self.is_expired}}}"
+
+
+class StreamCallback:
+    """core/stream/output/StreamCallback.java — override receive(events)."""
+
+    def receive(self, events: List[Event]):  # pragma: no cover - user hook
+        raise NotImplementedError
+
+
+class QueryCallback:
+    """core/query/output/callback/QueryCallback.java — override receive(ts, in, remove)."""
+
+    def receive(self, timestamp: int, in_events: Optional[List[Event]],
+                remove_events: Optional[List[Event]]):  # pragma: no cover - user hook
+        raise NotImplementedError
+
+
+class _FnStreamCallback(StreamCallback):
+    def __init__(self, fn):
+        self.fn = fn
+
+    def receive(self, events):
+        self.fn(events)
+
+
+class _FnQueryCallback(QueryCallback):
+    def __init__(self, fn):
+        self.fn = fn
+
+    def receive(self, timestamp, in_events, remove_events):
+        self.fn(timestamp, in_events, remove_events)
+
+
+# ---------------------------------------------------------------- value packing
+_NP = {STRING: np.int32, INT: np.int32, LONG: np.int64, FLOAT: np.float32,
+       DOUBLE: np.float64, BOOL: np.uint8, OBJECT: np.int64}
+
+
+def _to_float32(x) -> float:
+    return struct.unpack("<f", struct.pack("<f", float(x)))[0]
+
+
+def decode_value(bits: int, typ: int, strings: cp.StringDict):
+    """raw 8-byte value -> Python value (Java boxing of the output attribute)."""
+    if typ == STRING:
+        return strings.str(int(np.int32(np.int64(bits))))
+    if typ == INT:
+        return int(np.int32(np.int64(bits)))
+    if typ == LONG:
+        return int(bits)
+    if typ == FLOAT:
+        return struct.unpack("<f", struct.pack("<I", int(bits) & 0xFFFFFFFF))[0]
+    if typ == DOUBLE:
+        return struct.unpack("<d", struct.pack("<q", int(bits)))[0]
+    if typ == BOOL:
+        return bool(bits)
+    return int(bits)
+
+
+class KeyDict:
+    """Partition keys: ValuePartitionExecutor.execute = attr.toString()
+    (core/partition/executor/ValuePartitionExecutor.java:34-40). Two values share a
+    partition iff their Java toString() is equal; ids are dense in first-seen order."""
+
+    def __init__(self):
+        self.ids: Dict[object, int] = {}
+
+    def key(self, value, typ) -> int:
+        if value is None:
+            return -1
+        if typ == FLOAT:
+            f = _to_float32(value)
+            k = ("nan",) if f != f else ("f", struct.pack("<f", f))
+        elif typ == DOUBLE:
+            f = float(value)
+            k = ("nan",) if f != f else ("d", struct.pack("<d", f))
+        elif typ == BOOL:
+            k = ("b", bool(value))
+        elif typ in (INT, LONG):
+            k = ("i", int(value))
+        else:
+            k = ("s", str(value))
+        i = self.ids.get(k)
+        if i is None:
+            i = len(self.ids)
+            self.ids[k] = i
+        return i
+
+
+# ---------------------------------------------------------------- runtime
+class InputHandler:
+    """core/stream/input/InputHandler.java"""
+
+    def __init__(self, rt: "SiddhiAppRuntime", stream: str):
+        self.rt = rt
+        self.stream = stream
+        self.stream_id = rt._stream_index[stream]
+
+    def getStreamId(self):
+        return self.stream
+
+    def send(self, *args):
+        """send(Object[] data) | send(long timestamp, Object[] data) | send(Event) | send(Event[])"""
+        if len(args) == 2:
+            ts, data = args
+            self.rt._send(self.stream_id, [int(ts)], [list(data)])
+            return
+        (x,) = args
+        if isinstance(x, Event):
+            self.rt._send(self.stream_id, [x.timestamp], [x.data])
+        elif isinstance(x, (list, tuple)) and x and isinstance(x[0], Event):
+            self.rt._send(self.stream_id, [e.timestamp for e in x], [e.data for e in x])
+        else:
+            self.rt._send(self.stream_id, [None], [list(x)])
+
+    def send_batch(self, timestamps, rows):
+        """One send(Event[]) call from parallel lists of timestamps and data rows."""
+        self.rt._send(self.stream_id, list(timestamps), [list(r) for r in rows])
+
+
+class SiddhiAppRuntime:
+    """core/SiddhiAppRuntime.java (pattern/sequence apps)."""
+
+    def __init__(self, compiled: CompiledApp, engine_factory: Callable):
+        self.compiled = compiled
+        self.app = compiled.app
+        self.strings = compiled.strings
+        self.keys = KeyDict()
+        self._stream_index = {n: i for i, n in enumerate(self.app.stream_order)}
+        self._stream_cbs: Dict[str, List[StreamCallback]] = {}
+        self._query_cbs: Dict[int, List[QueryCallback]] = {}
+        self._query_by_name = {q.query.name: i for i, q in enumerate(compiled.queries)
+                               if q.query.name}
+        self._engine = engine_factory(compiled)
+        self._started = False
+        self._seq = 0
+        self.clock = 0 if self.app.playback else 1_000_000_000_000
+        self.name = self.app.name
+
+    # -- API
+    def getName(self):
+        return self.name
+
+    def getInputHandler(self, stream: str) -> InputHandler:
+        if stream not in self._stream_index:
+            raise SiddhiAppRuntimeException(f"stream {stream} is not defined")
+        return InputHandler(self, stream)
+
+    def addCallback(self, name: str, cb):
+        if name in self._query_by_name:
+            if callable(cb) and not isinstance(cb, QueryCallback):
+                cb = _FnQueryCallback(cb)
+            self._query_cbs.setdefault(self._query_by_name[name], []).append(cb)
+            return
+        if callable(cb) and not isinstance(cb, StreamCallback):
+            cb = _FnStreamCallback(cb)
+        self._stream_cbs.setdefault(name, []).append(cb)
+
+    def start(self):
+        if not self._started:
+            self._engine.start()
+            self._started = True
+
+    def shutdown(self):
+        if self._engine is not None:
+            self._engine.close()
+            self._engine = None
+
+    def sleep(self, ms: int):
+        """Thread.sleep stand-in: advances the virtual clock (and fires due timers)."""
+        self.clock += int(ms)
+        if not self.app.playback and self._engine is not None:
+            self._engine.advance_time(self.clock)
+            self._deliver()
+
+    def advance_time(self, now: int):
+        self.clock = max(self.clock, int(now))
+        self._engine.advance_time(self.clock)
+        self._deliver()
+
+    # -- internals
+    def _pack(self, stream_id: int, ts: List[Optional[int]], rows: List[list]):
+        sd = self.app.streams[self.app.stream_order[stream_id]]
+        n = len(rows)
+        tsa = np.empty(n, dtype=np.int64)
+        for i, t in enumerate(ts):
+            tsa[i] = self.clock if t is None else t
+        cols, nulls = [], []
+        for ai, (aname, typ) in enumerate(sd.attrs):
+            col = np.zeros(n, dtype=_NP[typ])
+            nm = None
+            for i, r in enumerate(rows):
+                v = r[ai] if ai < len(r) else None
+                if v is None:
+                    if nm is None:
+                        nm = np.zeros(n, dtype=np.uint8)
+                    nm[i] = 1
+                    continue
+                if typ == STRING:
+                    col[i] = self.strings.id(v)
+                elif typ == BOOL:
+                    col[i] = 1 if v else 0
+                else:
+                    col[i] = v
+            cols.append(col)
+            nulls.append(nm)
+        keys = None
+        for p, spec in enumerate(self.app.partitions):
+            sname = self.app.stream_order[stream_id]
+            if sname in spec:
+                ai = sd.index(spec[sname])
+                typ = sd.attrs[ai][1]
+                keys = np.array([self.keys.key(r[ai], typ) for r in rows], dtype=np.int32)
+        return tsa, cols, nulls, keys
+
+    def _send(self, stream_id: int, ts, rows):
+        if not self._started:
+            raise SiddhiAppRuntimeException("SiddhiAppRuntime not started")
+        if not rows:
+            return
+        tsa, cols, nulls, keys = self._pack(stream_id, ts, rows)
+        if self.app.playback:
+            self.clock = max(self.clock, int(tsa[-1]))
+        first = self._seq
+        self._seq += len(rows)
+        self._engine.send(stream_id, tsa, cols, nulls, keys, first)
+        self._deliver()
+
+    def _deliver(self):
+        res = self._engine.drain()
+        if res is None or len(res["query"]) == 0:
+            return
+        qs, tss, vals, nls, groups = res["query"], res["ts"], res["values"], res["nulls"], res["group"]
+        # group consecutive rows by callback chunk (sendToCallBacks call)
+        i = 0
+        n = len(qs)
+        while i < n:
+            j = i + 1
+            while j < n and groups[j] == groups[i] and qs[j] == qs[i]:
+                j += 1
+            q = int(qs[i])
+            cq = self.compiled.queries[q]
+            evs = []
+            for k in range(i, j):
+                data = [None if nls[k, c] else decode_value(int(vals[k, c]), cq.out_types[c], self.strings)
+                        for c in range(len(cq.out_types))]
+                evs.append(Event(int(tss[k]), data))
+            for cb in self._query_cbs.get(q, []):
+                cb.receive(evs[-1].timestamp, evs, None)
+            for cb in self._stream_cbs.get(cq.query.output, []):
+                cb.receive(evs)
+            i = j
+
+
+class SiddhiManager:
+    """core/SiddhiManager.java"""
+
+    def __init__(self, engine_factory: Optional[Callable] = None):
+        if engine_factory is None:
+            from ._native import HipEngine  # raises ImportError when the extension is absent
+            engine_factory = HipEngine
+        self._engine_factory = engine_factory
+        self._runtimes = []
+
+    def createSiddhiAppRuntime(self, app: str) -> SiddhiAppRuntime:
+        try:
+            compiled = cp.compile_app(app)
+        except (SiddhiParserException, SiddhiAppValidationException, UnsupportedQuery) as e:
+            raise SiddhiAppCreationException(str(e)) from e
+        rt = SiddhiAppRuntime(compiled, self._engine_factory)
+        self._runtimes.append(rt)
+        return rt
+
+    def shutdown(self):
+        for rt in self._runtimes:
+            rt.shutdown()
+        self._runtimes = []
