@@ -432,6 +432,8 @@ class Parser:
         elif self.kw("events"):
             self.next()
         self.expect_kw("into")
+        if self.op("#"):
+            raise UnsupportedQuery("inner-stream outputs (#Stream) are out of scope")
         out = self.ident()
         return Query(name, st, root, within, sel, star, out)
 

@@ -221,6 +221,9 @@ class SiddhiAppRuntime:
 
     def start(self):
         if not self._started:
+            if not self.app.playback:
+                # wall-clock apps: the scheduler's "now" at start (partitionCreated)
+                self._engine.advance_time(self.clock)
             self._engine.start()
             self._started = True
 

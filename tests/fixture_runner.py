@@ -1,0 +1,134 @@
+"""Replays a golden fixture (tests/golden/fixtures.json) through the API mirror
+with a given engine (HIP product or CPU oracle) and checks the asserted outputs."""
+from __future__ import annotations
+
+import json
+import os
+import struct
+
+from siddhi_amd import SiddhiManager
+from siddhi_amd.compiler import UnsupportedQuery
+from siddhi_amd.runtime import SiddhiAppCreationException
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FIXTURES = os.path.join(HERE, "golden", "fixtures.json")
+
+
+def load_fixtures():
+    with open(FIXTURES) as fh:
+        return [f for f in json.load(fh) if "skipped" not in f]
+
+
+def py_value(v):
+    if isinstance(v, dict):
+        if "f" in v:
+            return float(v["f"])
+        if "d" in v:
+            return float(v["d"])
+        if "l" in v:
+            return int(v["l"])
+    return v
+
+
+def same(expected, got) -> bool:
+    if isinstance(expected, dict):
+        if "f" in expected:
+            if not isinstance(got, float):
+                return False
+            return struct.pack("<f", float(expected["f"])) == struct.pack("<f", got)
+        if "d" in expected:
+            return isinstance(got, float) and float(expected["d"]) == got
+        if "l" in expected:
+            return isinstance(got, int) and not isinstance(got, bool) and got == expected["l"]
+    if expected is None:
+        return got is None
+    if isinstance(expected, bool):
+        return got is expected
+    if isinstance(expected, int):
+        return isinstance(got, int) and not isinstance(got, bool) and got == expected
+    return expected == got
+
+
+def same_row(exp, got) -> bool:
+    return len(exp) == len(got) and all(same(e, g) for e, g in zip(exp, got))
+
+
+class Unsupported(Exception):
+    pass
+
+
+def run_fixture(fx, engine_factory):
+    """Returns the list of output events the fixture's callback received."""
+    mgr = SiddhiManager(engine_factory=engine_factory)
+    try:
+        rt = mgr.createSiddhiAppRuntime(fx["app"])
+    except SiddhiAppCreationException as e:
+        if isinstance(e.__cause__, UnsupportedQuery):
+            raise Unsupported(str(e))
+        raise
+    got = []
+    cb = fx["callback"]
+    if cb["kind"] == "query":
+        rt.addCallback(cb["name"], lambda ts, i, r: got.extend(i or []))
+    else:
+        rt.addCallback(cb["name"], lambda evs: got.extend(evs))
+    handlers = {}
+    rt.start()
+    try:
+        for a in fx["actions"]:
+            if a[0] == "send":
+                _, stream, ts, vals = a
+                h = handlers.get(stream) or rt.getInputHandler(stream)
+                handlers[stream] = h
+                vals = [py_value(v) for v in vals]
+                if ts is None:
+                    h.send(vals)
+                else:
+                    h.send(ts, vals)
+            elif a[0] == "sleep":
+                rt.sleep(a[1])
+            elif a[0] == "wait_in_events":
+                sleep, retry = a[1], a[2]
+                count = 0
+                while True:
+                    rt.sleep(sleep)
+                    count += 1
+                    if len(got) == 1 or count == retry:
+                        break
+            elif a[0] == "wait_for_events":
+                sleep, expected, timeout = a[1], a[2], a[3]
+                waited = 0
+                while len(got) < expected and waited < timeout:
+                    rt.sleep(sleep)
+                    waited += sleep
+    finally:
+        rt.shutdown()
+    return got
+
+
+def check_fixture(fx, got):
+    """Returns a list of mismatch descriptions (empty = parity)."""
+    errs = []
+    data = [e.data for e in got]
+    if len(data) != fx["expect_count"]:
+        errs.append(f"event count {len(data)} != expected {fx['expect_count']}")
+    used = set()
+    for r in fx["expect_rows"]:
+        g = r["guard"]
+        if g is not None and not r.get("first_of_callback"):
+            if g - 1 >= len(data):
+                if g <= fx["expect_count"]:
+                    errs.append(f"missing event #{g}: expected {r['row']}")
+                continue
+            if not same_row(r["row"], data[g - 1]):
+                errs.append(f"event #{g}: expected {r['row']} got {data[g - 1]}")
+            used.add(g - 1)
+        else:
+            ok = False
+            for k, d in enumerate(data):
+                if same_row(r["row"], d):
+                    ok = True
+                    break
+            if not ok and fx["expect_count"] > 0:
+                errs.append(f"expected row {r['row']} not emitted (got {data})")
+    return errs
