@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Benchmark: input events/sec for the partitioned pattern query (config C2).
+
+Workload (BASELINE.json configs[1]):
+  partition with (symbol of StockStream) begin
+    from every e1=StockStream[price>20] -> e2=StockStream[symbol==e1.symbol and price>e1.price]
+    within 1 sec select e1.symbol as symbol, e1.price as p1, e2.price as p2, e2.volume as v2
+    insert into Out; end;
+  100M synthetic ticks, 10,000 symbols, R = 100 ev/ms, resident in HBM.
+
+A step = one full pass of the matcher over the 100M events from fresh per-key
+state (radix segment -> per-key NFA advance -> ordered match placement), with
+the ordered match stream written to HBM.
+
+Multi-GPU (torchrun): one process per GPU, weak scaling: each rank owns a
+disjoint symbol range (its own 100M-event stream); partitions never cross
+ranks, so there is no data-path collective. value = all ranks' events / the
+max-over-ranks step time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--events", type=int, default=100_000_000)
+    ap.add_argument("--keys", type=int, default=10_000)
+    ap.add_argument("--rate", type=int, default=100)
+    ap.add_argument("--cpu-sample", type=int, default=2_000_000,
+                    help="events of the same workload timed on the CPU oracle (0 = skip)")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device(f"cuda:{local}")
+
+    from siddhi_amd import compiler, synth
+    from siddhi_amd.device_run import DeviceRunner
+
+    n, K = args.events, args.keys
+    # each rank: its own stream over its own symbol range (weak scaling)
+    ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=2, seed=synth.SEED + 2 + 7919 * rank)
+    compiled = compiler.compile_app(synth.C2_QUERY)
+    runner = DeviceRunner(compiled, device=str(dev))
+    t_ts = torch.from_numpy(ts).to(dev)
+    t_k = torch.from_numpy(keys).to(dev)
+    t_p = torch.from_numpy(price).to(dev)
+    t_v = torch.from_numpy(vol).to(dev)
+    cols = [t_k, t_p, t_v]
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        return runner.run(t_ts, t_k, cols, K, stream=stream)
+
+    for _ in range(args.warmup):
+        m, _, _ = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    seg = adv = emt = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m, oseq, ovals = step()
+        kt = runner.kernel_times()
+        seg += kt["segment_ms"]
+        adv += kt["advance_ms"]
+        emt += kt["emit_ms"]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    ms_step = dt * 1000.0 / args.steps
+    events_total = n * world
+    value = events_total * args.steps / dt
+
+    # algorithmic bytes: event columns the query reads
+    # (ts 8 + symbol 4 + price 4 + volume 8 = 24 B) + emitted record
+    # (trigger seq 8 + symbol 4 + p1 4 + p2 4 + v2 8 = 28 B)
+    b_alg = 24 * n + 28 * m
+    adv_ms = adv / args.steps
+    seg_ms = seg / args.steps
+    emt_ms = emt / args.steps
+    peak = 8.0e12
+    achieved = b_alg / (adv_ms / 1000.0)
+    pipeline = b_alg / ((seg_ms + adv_ms + emt_ms) / 1000.0)
+
+    verified = None
+    if not args.no_verify and rank == 0:
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        from c2_check import c2_expected
+        eseq, evals = c2_expected(ts, keys, price, vol)
+        verified = bool(m == len(eseq) and np.array_equal(oseq.cpu().numpy(), eseq)
+                        and np.array_equal(ovals.cpu().numpy(), evals))
+
+    traffic = None
+    prof = os.path.join(HERE, "profiles", "pmc_advance.json")
+    if os.path.exists(prof):
+        try:
+            pj = json.load(open(prof))
+            if pj.get("events") == n and pj.get("keys") == K:
+                traffic = pj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and args.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        from oracle_engine import run_stock_oracle
+        s = min(args.cpu_sample, n)
+        t1 = time.perf_counter()
+        run_stock_oracle(compiled, ts[:s], keys[:s], price[:s], vol[:s], batch=4096)
+        cdt = time.perf_counter() - t1
+        cpu = {"value": s / cdt, "unit": "events/s", "cores": 1, "kind": "port",
+               "sample": f"first {s} events of the same C2 stream, send(Event[]) batches of 4096, "
+                         f"C++ restatement of siddhi-core's processors (oracle/), 1 thread"}
+
+    if rank == 0:
+        line = {
+            "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
+            "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic",
+            "config": {"workload": "C2: every e1[price>20] -> e2[symbol==e1.symbol and price>e1.price] "
+                                   "within 1 sec, partition with (symbol of StockStream)",
+                       "events_per_gpu": n, "symbols_per_gpu": K, "rate_ev_per_ms": args.rate,
+                       "matches_per_gpu": int(m), "parallelism": f"key-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",
+                         "frac": achieved / peak, "traffic": traffic, "kernel": "k_advance",
+                         "algorithmic_bytes": b_alg, "pipeline_GBps": pipeline / 1e9,
+                         "pipeline_frac": pipeline / peak},
+            "phase_ms": {"segment": seg_ms, "advance": adv_ms, "emit": emt_ms},
+            "cpu_baseline": cpu,
+            "verified_vs_restatement": verified,
+        }
+        print(json.dumps(line))
+    runner.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

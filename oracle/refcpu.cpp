@@ -241,6 +241,8 @@ struct Holder {
     std::function<S*()> factory;
     S* single = nullptr;
     std::unordered_map<int64_t, S*> states;
+    int64_t ckey = INT64_MIN;  // one-entry lookup cache (same semantics as the map)
+    S* cst = nullptr;
     S* get();
     void ret(S* s);
     ~Holder() {
@@ -650,9 +652,16 @@ S* Holder<S>::get() {
         if (!single) single = factory();
         return single;
     }
-    S*& p = states[app->flow.key];
+    const int64_t key = app->flow.key;
+    if (cst && ckey == key) {
+        cst->use++;
+        return cst;
+    }
+    S*& p = states[key];
     if (!p) p = factory();
     p->use++;
+    ckey = key;
+    cst = p;
     return p;
 }
 template <class S>
@@ -662,6 +671,7 @@ void Holder<S>::ret(S* s) {
     if (s->use == 0 && s->canDestroy()) {
         auto it = states.find(app->flow.key);
         if (it != states.end() && it->second == s) states.erase(it);
+        if (cst == s) cst = nullptr;
         app->zombies.push_back(s);
     }
 }

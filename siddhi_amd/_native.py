@@ -1,0 +1,125 @@
+"""Product engine: ctypes binding of the in-tree libsiddhi_hip.so (C-ABI).
+
+Fails loudly: importing this module raises ImportError when the extension is
+missing, and every processing call raises when the HIP runtime reports no
+device (the matcher has no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsiddhi_hip.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libsiddhi_hip.so is not built ({LIB_PATH}); run `python -m siddhi_amd.build` "
+                      "or __graft_entry__.build()")
+
+_lib = abi.bind_product(C.CDLL(LIB_PATH))
+
+
+def lib():
+    return _lib
+
+
+class HipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{abi.STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def check(h, rc):
+    if rc not in (abi.SH_OK, abi.SH_E_MORE):
+        msg = _lib.sh_last_error(h).decode() if h else ""
+        raise HipError(rc, msg)
+    return rc
+
+
+class CompiledHandle:
+    """RAII wrapper of sh_handle*."""
+
+    def __init__(self, compiled):
+        self.compiled = compiled
+        self.desc = compiled.descriptor()
+        h = C.c_void_p()
+        rc = _lib.sh_compile(C.byref(self.desc), C.byref(h))
+        self.h = h
+        if rc != abi.SH_OK:
+            msg = _lib.sh_last_error(h).decode() if h.value else ""
+            if h.value:
+                _lib.sh_destroy(h)
+                self.h = None
+            raise HipError(rc, msg)
+
+    def close(self):
+        if self.h:
+            _lib.sh_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HipEngine:
+    """Engine protocol (start/send/advance_time/drain/close) over libsiddhi_hip.so."""
+
+    def __init__(self, compiled):
+        self.handle = CompiledHandle(compiled)
+        self.h = self.handle.h
+        self.n_out = max([len(q.outs) for q in compiled.queries] + [1])
+
+    def start(self):
+        pass
+
+    def send(self, stream, tsa, cols, nulls, keys, first_seq):
+        tsa = np.ascontiguousarray(tsa, dtype=np.int64)
+        n = len(tsa)
+        cp = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
+        npp = (C.c_void_p * max(1, len(cols)))(*[(m.ctypes.data if m is not None else None) for m in nulls])
+        b = abi.sh_batch()
+        b.stream = stream
+        b.on_device = 0
+        b.n = n
+        b.ts = tsa.ctypes.data
+        b.keys = keys.ctypes.data if keys is not None else None
+        b.cols = cp
+        b.nulls = npp if any(m is not None for m in nulls) else None
+        check(self.h, _lib.sh_push_batch(self.h, C.byref(b)))
+
+    def advance_time(self, now):
+        check(self.h, _lib.sh_advance_time(self.h, int(now)))
+
+    def drain(self):
+        n = _lib.sh_pending(self.h)
+        if n < 0:
+            check(self.h, int(n))
+        q = np.zeros(n, np.int32)
+        seq = np.zeros(n, np.uint64)
+        ts = np.zeros(n, np.int64)
+        vals = np.zeros((n, self.n_out), np.int64)
+        nls = np.zeros((n, self.n_out), np.uint8)
+        if n:
+            mb = abi.sh_match_buf()
+            mb.capacity = n
+            mb.query = q.ctypes.data_as(C.POINTER(C.c_int32))
+            mb.trigger_seq = seq.ctypes.data_as(C.POINTER(C.c_uint64))
+            mb.ts = ts.ctypes.data_as(C.POINTER(C.c_int64))
+            mb.values = vals.ctypes.data_as(C.POINTER(C.c_int64))
+            mb.nulls = nls.ctypes.data_as(C.POINTER(C.c_uint8))
+            mb.n_out = self.n_out
+            check(self.h, _lib.sh_drain(self.h, C.byref(mb)))
+        # one callback chunk per (send, query): the device path keeps arrival
+        # order; chunking of callbacks is cosmetic
+        grp = np.zeros(n, np.int32)
+        return dict(query=q, seq=seq, ts=ts, values=vals, nulls=nls, group=grp)
+
+    def close(self):
+        self.handle.close()

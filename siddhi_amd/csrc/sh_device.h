@@ -1,0 +1,69 @@
+// sh_device.h — host<->kernel structures and launch entry points of the
+// gfx950 matcher (implemented in sh_kernels.hip, called from sh_host.cpp).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "sh_program.h"
+
+#define SHD_NULL_ROW 0xFFFFFFFFu
+
+// Column stores of every stream (device pointers). Lives in device memory;
+// kernels take a pointer to it.
+struct shd_cols {
+    const void* col[SHP_MAX_STREAMS][32];
+    const uint8_t* nul[SHP_MAX_STREAMS][32];
+};
+
+// One device batch of events in arrival order.
+struct shd_batch {
+    const int64_t* ts;       // [n]
+    const uint8_t* stream;   // [n] or NULL (single stream 0)
+    const uint32_t* row;     // [n] row in the stream's column store, or NULL (row = row_base + i)
+    const int32_t* keys;     // [n] partition key (dense), -1 = null key; NULL -> key 0
+    uint32_t row_base;
+    int32_t pad;
+    uint64_t seq_base;       // global sequence number of event 0
+    int64_t n;
+};
+
+// Emission buffers.
+struct shd_emit {
+    uint64_t* tmp;           // temp records: [cap][3 + n_out] words
+    unsigned long long* tmp_ctr;  // atomic record counter
+    int64_t tmp_cap;
+    uint32_t* match_cnt;     // [n] matches triggered by local event i (pre-zeroed)
+    int32_t* err;            // [0]: state overflow, [1]: temp overflow
+};
+
+// scratch for the radix segment
+struct shd_segment_ws {
+    uint32_t* keys_a;
+    uint32_t* keys_b;
+    uint32_t* idx_a;
+    uint32_t* idx_b;
+    uint32_t* hist;          // [256 * nblocks]
+    uint32_t* scan_tmp;      // scan block sums (3 levels)
+    uint32_t* seg_off;       // [3n + 2]: flags, positions, segment list + count
+    int64_t cap;
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+// all launches are asynchronous on `stream` (hipStream_t)
+size_t shd_scan_tmp_words(int64_t n);
+// stable radix segment by (key, arrival): perm / sorted keys (both NULL for an
+// unpartitioned batch) and the segment list in ws->seg_off[2n .. 3n] (+ count at [3n])
+int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
+                const uint32_t** perm_out, const uint32_t** skeys_out);
+int shd_advance(const shp_program* dprog, const shp_layout* lay, uint8_t* kstate, int32_t nkeys,
+                const shd_batch* b, const uint32_t* perm, const uint32_t* skeys,
+                const uint32_t* seg_off, const shd_cols* dcols, const shd_emit* em, void* stream);
+int shd_emit_place(const shd_emit* em, int32_t n_out, int64_t n_events, uint32_t* offsets,
+                   uint32_t* scan_tmp, int64_t n_records, const shd_batch* b, uint64_t* out_seq,
+                   int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, void* stream);
+int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, void* stream);
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,750 @@
+// sh_host.cpp — host side of libsiddhi_hip.so: the C-ABI (include/siddhi_hip.h),
+// lowering of the app descriptor to the device NFA program, HBM residency of
+// event columns and per-key state, and the launch sequence
+//   radix segment -> per-key advance -> ordered placement.
+//
+// The product path has no CPU fallback: without a device every call that
+// needs one returns SH_E_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/siddhi_hip.h"
+#include "sh_device.h"
+
+#define SH_VERSION_STR "siddhi_hip 0.1 (gfx950)"
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t need) {
+        if (need <= bytes) return 0;
+        size_t nb = std::max(need, bytes * 2);
+        void* q = nullptr;
+        if (hipMalloc(&q, nb) != hipSuccess) return SH_E_OOM;
+        if (p) {
+            hipMemcpy(q, p, bytes, hipMemcpyDeviceToDevice);
+            hipFree(p);
+        }
+        p = q;
+        bytes = nb;
+        return 0;
+    }
+    int ensure_fresh(size_t need) {  // no content preservation
+        if (need <= bytes) return 0;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t nb = std::max(need, (size_t)4096);
+        if (hipMalloc(&p, nb) != hipSuccess) return SH_E_OOM;
+        bytes = nb;
+        return 0;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const {
+        return (T*)p;
+    }
+};
+
+int type_width(int t) {
+    switch (t) {
+        case SH_T_LONG:
+        case SH_T_DOUBLE: return 8;
+        case SH_T_BOOL: return 1;
+        default: return 4;
+    }
+}
+
+// ----------------------------------------------------------- lowering
+struct Lowering {
+    const sh_query_desc* q;
+    shp_program P;
+    std::string err;
+    std::vector<int> chain;  // stream element indices in slot order
+
+    int add_const(int64_t v, int type, int isnull) {
+        for (int i = 0; i < P.n_const; i++)
+            if (P.consts[i] == v && P.const_type[i] == type && P.const_null[i] == isnull) return i;
+        if (P.n_const >= 64) {
+            err = "too many constants";
+            return -1;
+        }
+        P.consts[P.n_const] = v;
+        P.const_type[P.n_const] = (uint8_t)type;
+        P.const_null[P.n_const] = (uint8_t)isnull;
+        return P.n_const++;
+    }
+    bool emit(uint8_t op, uint8_t a, uint8_t b, uint8_t c, int32_t x) {
+        if (P.n_code >= SHP_MAX_CODE) {
+            err = "expression program too long";
+            return false;
+        }
+        shp_instr& in = P.code[P.n_code++];
+        in.op = op;
+        in.a = a;
+        in.b = b;
+        in.c = c;
+        in.x = x;
+        return true;
+    }
+    static int dom_for(int op, int lt, int rt) {
+        if (lt == SH_T_STRING || rt == SH_T_STRING) return DOM_STR;
+        if (lt == SH_T_BOOL || rt == SH_T_BOOL) return DOM_BOOL;
+        auto rk = [](int t) {
+            switch (t) {
+                case SH_T_INT: return 0;
+                case SH_T_LONG: return 1;
+                case SH_T_FLOAT: return 2;
+                default: return 3;
+            }
+        };
+        int r = std::max(rk(lt), rk(rt));
+        // Equal/NotEqual FloatLong & LongFloat compare as double
+        // (EqualCompareConditionExpressionExecutorFloatLong.java)
+        bool fl = (lt == SH_T_FLOAT && rt == SH_T_LONG) || (lt == SH_T_LONG && rt == SH_T_FLOAT);
+        if ((op == SH_OP_EQ || op == SH_OP_NE) && fl) r = 3;
+        return r == 0 ? DOM_I32 : r == 1 ? DOM_I64 : r == 2 ? DOM_F32 : DOM_F64;
+    }
+    // postfix emission of an sh_expr tree
+    bool gen(int e, int depth) {
+        if (e < 0 || e >= q->n_exprs) {
+            err = "bad expression index";
+            return false;
+        }
+        if (depth > SHP_MAX_STACK - 2) {
+            err = "expression too deep";
+            return false;
+        }
+        const sh_expr& x = q->exprs[e];
+        switch (x.op) {
+            case SH_OP_CONST: {
+                int c = add_const(x.cval, x.type, x.is_null);
+                return c >= 0 && emit(OPC_CONST, 0, 0, 0, c);
+            }
+            case SH_OP_VAR:
+                if (x.slot < 0 || x.slot >= P.n_states) {
+                    err = "variable slot out of range";
+                    return false;
+                }
+                return emit(OPC_VAR, (uint8_t)x.slot, (uint8_t)x.attr, (uint8_t)x.type, x.chain);
+            case SH_OP_IS_NULL_STREAM:
+                return emit(OPC_ISNULL_STREAM, (uint8_t)x.slot, 0, 0, x.chain);
+            case SH_OP_NOT:
+                return gen(x.lhs, depth + 1) && emit(OPC_NOT, 0, 0, 0, 0);
+            case SH_OP_BOOL_VAR:
+                return gen(x.lhs, depth + 1) && emit(OPC_BOOLV, 0, 0, 0, 0);
+            case SH_OP_IS_NULL:
+                return gen(x.lhs, depth + 1) && emit(OPC_ISNULL, 0, 0, 0, 0);
+            case SH_OP_AND:
+            case SH_OP_OR:
+                return gen(x.lhs, depth + 1) && gen(x.rhs, depth + 2) &&
+                       emit(x.op == SH_OP_AND ? OPC_AND : OPC_OR, 0, 0, 0, 0);
+            case SH_OP_EQ:
+            case SH_OP_NE:
+            case SH_OP_GT:
+            case SH_OP_GE:
+            case SH_OP_LT:
+            case SH_OP_LE: {
+                int lt = q->exprs[x.lhs].type, rt = q->exprs[x.rhs].type;
+                return gen(x.lhs, depth + 1) && gen(x.rhs, depth + 2) &&
+                       emit(OPC_CMP, (uint8_t)x.op, (uint8_t)dom_for(x.op, lt, rt), 0, 0);
+            }
+            case SH_OP_ADD:
+            case SH_OP_SUB:
+            case SH_OP_MUL:
+            case SH_OP_DIV:
+            case SH_OP_MOD:
+                return gen(x.lhs, depth + 1) && gen(x.rhs, depth + 2) &&
+                       emit(OPC_ARITH, (uint8_t)x.op, (uint8_t)x.type, 0, 0);
+            case SH_OP_IF_THEN_ELSE:
+                return gen(x.lhs, depth + 1) && gen(x.rhs, depth + 2) && gen(x.third, depth + 3) &&
+                       emit(OPC_SELECT, 0, 0, 0, 0) && emit(OPC_CAST, 0, (uint8_t)x.type, 0, 0);
+        }
+        err = "unsupported expression operator";
+        return false;
+    }
+    // flatten `Next(...)` chains of stream states, `every` allowed on the start
+    // state only (the shapes of configs C1/C2/C5)
+    bool flatten(int e, bool first) {
+        const sh_state_elem& el = q->elems[e];
+        switch (el.kind) {
+            case SH_E_NEXT:
+                return flatten(el.child0, first) && flatten(el.child1, false);
+            case SH_E_EVERY: {
+                if (!first || !chain.empty() || q->elems[el.child0].kind != SH_E_STREAM) {
+                    err = "device engine: `every` is supported on the start state only";
+                    return false;
+                }
+                P.every_start = 1;
+                chain.push_back(el.child0);
+                return true;
+            }
+            case SH_E_STREAM:
+                chain.push_back(e);
+                return true;
+            default:
+                err = "device engine: count / logical / absent states are not lowered yet";
+                return false;
+        }
+    }
+};
+
+}  // namespace
+
+struct sh_handle {
+    std::string err;
+    bool has_device = false;
+    sh_app_desc app{};
+    std::vector<std::vector<int32_t>> stream_types;
+    int32_t n_out = 0;
+    int32_t partitioned = 0;
+    shp_program prog{};
+    shp_layout lay{};
+    hipStream_t stream = nullptr;      // active stream
+    hipStream_t own_stream = nullptr;  // created by sh_compile
+    DevBuf d_prog, d_cols_desc, d_kstate, d_err;
+    int32_t nkeys_alloc = 0;
+    // column stores (streaming path)
+    struct Store {
+        std::vector<DevBuf> cols, nuls;
+        std::vector<bool> has_nul;
+        int64_t rows = 0;
+    };
+    std::vector<Store> stores;
+    // staged (pushed, not yet processed) events
+    std::vector<int64_t> st_ts;
+    std::vector<uint8_t> st_stream;
+    std::vector<uint32_t> st_row;
+    std::vector<int32_t> st_key;
+    int32_t max_key = 0;
+    uint64_t seq_next = 0;  // global sequence of the next staged event
+    uint64_t seq_staged0 = 0;
+    // workspaces
+    DevBuf w_ts, w_stream, w_row, w_key, w_keys_a, w_keys_b, w_idx_a, w_idx_b, w_hist, w_scan, w_seg;
+    DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls;
+    int64_t tmp_cap = 0;
+    // drained output queue (host)
+    std::vector<int32_t> o_query;
+    std::vector<uint64_t> o_seq;
+    std::vector<int64_t> o_ts;
+    std::vector<int64_t> o_vals;
+    std::vector<uint8_t> o_nulls;
+    int64_t o_read = 0;
+    sh_kernel_times times{};
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+static int fail(sh_handle* h, int code, const std::string& m) {
+    if (h) h->err = m;
+    return code;
+}
+
+static bool device_available() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return false;
+    return n > 0;
+}
+
+extern "C" {
+
+const char* sh_version(void) { return SH_VERSION_STR; }
+
+int sh_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* sh_last_error(sh_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int sh_compile(const sh_app_desc* app, sh_handle** out) {
+    if (!app || !out) return SH_E_INVALID_ARG;
+    *out = nullptr;
+    sh_handle* h = new sh_handle();
+    *out = h;
+    if (app->version != SH_DESC_VERSION) return fail(h, SH_E_INVALID_ARG, "descriptor version mismatch");
+    h->app = *app;
+    if (app->n_streams < 1 || app->n_streams > SHP_MAX_STREAMS)
+        return fail(h, SH_E_UNSUPPORTED, "device engine: 1..8 streams per app");
+    for (int s = 0; s < app->n_streams; s++) {
+        const sh_stream_def& sd = app->streams[s];
+        if (sd.n_attrs > 32) return fail(h, SH_E_UNSUPPORTED, "device engine: at most 32 attributes per stream");
+        h->stream_types.emplace_back(sd.attr_types, sd.attr_types + sd.n_attrs);
+    }
+    if (app->n_queries != 1) return fail(h, SH_E_UNSUPPORTED, "device engine: one pattern query per app (round 1)");
+    const sh_query_desc& q = app->queries[0];
+    if (q.state_type != SH_PATTERN) return fail(h, SH_E_UNSUPPORTED, "device engine: sequences are not lowered yet");
+    Lowering L;
+    L.q = &q;
+    memset(&L.P, 0, sizeof(L.P));
+    if (!L.flatten(q.root, true)) return fail(h, SH_E_UNSUPPORTED, L.err);
+    shp_program& P = L.P;
+    P.n_states = (int32_t)L.chain.size();
+    if (P.n_states < 1 || P.n_states > SHP_MAX_STATES)
+        return fail(h, SH_E_UNSUPPORTED, "device engine: 1..8 states per pattern");
+    P.within_ms = q.within_ms;
+    P.n_streams = app->n_streams;
+    for (int k = 0; k < P.n_states; k++) {
+        const sh_state_elem& el = q.elems[L.chain[k]];
+        if (el.slot != k) return fail(h, SH_E_INVALID_ARG, "state slots are not in chain order");
+        P.state_stream[k] = el.stream;
+    }
+    // receivers: PatternSingle updates its only state; PatternMulti updates all
+    // states of the stream in setup order and processes them in reverse
+    // (PatternMultiProcessStreamReceiver.java:34-51)
+    for (int s = 0; s < app->n_streams; s++) {
+        int c = 0;
+        for (int k = 0; k < P.n_states; k++)
+            if (P.state_stream[k] == s) P.upd_state[s][c++] = k;
+        P.upd_count[s] = c;
+        P.proc_count[s] = c;
+        for (int i = 0; i < c; i++) P.proc_state[s][i] = P.upd_state[s][c - 1 - i];
+        P.stream_nattr[s] = app->streams[s].n_attrs;
+        for (int a = 0; a < app->streams[s].n_attrs; a++) P.attr_type[s][a] = app->streams[s].attr_types[a];
+    }
+    for (int k = 0; k < P.n_states; k++) {
+        const sh_state_elem& el = q.elems[L.chain[k]];
+        if (el.filter >= 0) {
+            P.filter_pc[k] = P.n_code;
+            if (!L.gen(el.filter, 0)) return fail(h, SH_E_UNSUPPORTED, L.err);
+            P.filter_len[k] = P.n_code - P.filter_pc[k];
+        } else {
+            P.filter_pc[k] = -1;
+            P.filter_len[k] = 0;
+        }
+    }
+    if (q.n_outputs > SHP_MAX_OUT) return fail(h, SH_E_UNSUPPORTED, "device engine: at most 16 output attributes");
+    P.n_out = q.n_outputs;
+    for (int o = 0; o < q.n_outputs; o++) {
+        const sh_output_attr& oa = q.outputs[o];
+        P.out_agg[o] = oa.agg;
+        P.out_type[o] = oa.type;
+        if (oa.expr >= 0) {
+            P.out_pc[o] = P.n_code;
+            if (!L.gen(oa.expr, 0)) return fail(h, SH_E_UNSUPPORTED, L.err);
+            P.out_len[o] = P.n_code - P.out_pc[o];
+            P.out_arg_type[o] = q.exprs[oa.expr].type;
+        } else {
+            P.out_pc[o] = -1;
+            P.out_len[o] = 0;
+        }
+    }
+    h->prog = P;
+    h->n_out = P.n_out;
+    h->partitioned = q.partition >= 0;
+    if (h->partitioned) {
+        for (int k = 0; k < P.n_states; k++) {
+            int s = P.state_stream[k];
+            if (!app->partition_streams[q.partition * app->n_streams + s])
+                return fail(h, SH_E_UNSUPPORTED, "device engine: every stream of a partitioned query must be keyed");
+        }
+    }
+    // per-key state layout
+    shp_layout& Y = h->lay;
+    const char* capenv = getenv("SH_PARTIAL_CAP");
+    Y.cap = capenv ? atoi(capenv) : 64;
+    Y.rec_words = 2 + (P.n_states + 1) / 2;
+    Y.list_bytes = (int64_t)Y.cap * Y.rec_words * 8;
+    Y.off_lists = (int64_t)(1 + SHP_MAX_STATES) * 8;
+    Y.off_agg = Y.off_lists + (int64_t)(P.n_states > 1 ? P.n_states - 1 : 0) * 2 * Y.list_bytes;
+    Y.key_bytes = Y.off_agg + (int64_t)P.n_out * 5 * 8;
+    Y.key_bytes = (Y.key_bytes + 63) & ~63ll;
+
+    h->has_device = device_available();
+    if (!h->has_device) return SH_OK;  // compile is host-only; processing needs a device
+    hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    h->stream = h->own_stream;
+    for (auto& e : h->ev) hipEventCreate(&e);
+    if (h->d_prog.ensure(sizeof(shp_program)) || h->d_cols_desc.ensure(sizeof(shd_cols)) || h->d_err.ensure(64))
+        return fail(h, SH_E_OOM, "hipMalloc failed");
+    hipMemcpy(h->d_prog.p, &h->prog, sizeof(shp_program), hipMemcpyHostToDevice);
+    h->stores.resize(app->n_streams);
+    for (int s = 0; s < app->n_streams; s++) {
+        h->stores[s].cols.resize(h->stream_types[s].size());
+        h->stores[s].nuls.resize(h->stream_types[s].size());
+        h->stores[s].has_nul.assign(h->stream_types[s].size(), false);
+    }
+    return SH_OK;
+}
+
+void sh_destroy(sh_handle* h) {
+    if (!h) return;
+    if (h->has_device) {
+        hipStreamSynchronize(h->stream);
+        DevBuf* bufs[] = {&h->d_prog, &h->d_cols_desc, &h->d_kstate, &h->d_err, &h->w_ts, &h->w_stream, &h->w_row,
+                          &h->w_key, &h->w_keys_a, &h->w_keys_b, &h->w_idx_a, &h->w_idx_b, &h->w_hist, &h->w_scan,
+                          &h->w_seg, &h->w_cnt, &h->w_off, &h->w_tmp, &h->w_ctr, &h->w_oseq, &h->w_ots,
+                          &h->w_ovals, &h->w_onulls};
+        for (DevBuf* b : bufs) b->release();
+        for (auto& st : h->stores) {
+            for (auto& c : st.cols) c.release();
+            for (auto& c : st.nuls) c.release();
+        }
+        for (auto& e : h->ev)
+            if (e) hipEventDestroy(e);
+        hipStreamDestroy(h->own_stream);
+    }
+    delete h;
+}
+
+int sh_push_batch(sh_handle* h, const sh_batch* b) {
+    if (!h || !b) return SH_E_INVALID_ARG;
+    if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
+    if (b->stream < 0 || b->stream >= h->app.n_streams) return fail(h, SH_E_INVALID_ARG, "bad stream index");
+    if (b->on_device) return fail(h, SH_E_UNSUPPORTED, "device batches go through sh_run_device");
+    if (b->n <= 0) return SH_OK;
+    auto& st = h->stores[b->stream];
+    const auto& types = h->stream_types[b->stream];
+    const int64_t r0 = st.rows;
+    for (size_t a = 0; a < types.size(); a++) {
+        const int w = type_width(types[a]);
+        if (st.cols[a].ensure((size_t)(r0 + b->n) * w)) return fail(h, SH_E_OOM, "column store");
+        hipMemcpyAsync((uint8_t*)st.cols[a].p + r0 * w, b->cols[a], b->n * w, hipMemcpyHostToDevice, h->stream);
+        const uint8_t* nm = b->nulls ? b->nulls[a] : nullptr;
+        if (nm || st.has_nul[a]) {
+            if (!st.has_nul[a]) {
+                if (st.nuls[a].ensure((size_t)(r0 + b->n))) return fail(h, SH_E_OOM, "null mask");
+                hipMemsetAsync(st.nuls[a].p, 0, r0, h->stream);
+                st.has_nul[a] = true;
+            } else if (st.nuls[a].ensure((size_t)(r0 + b->n))) {
+                return fail(h, SH_E_OOM, "null mask");
+            }
+            if (nm)
+                hipMemcpyAsync((uint8_t*)st.nuls[a].p + r0, nm, b->n, hipMemcpyHostToDevice, h->stream);
+            else
+                hipMemsetAsync((uint8_t*)st.nuls[a].p + r0, 0, b->n, h->stream);
+        }
+    }
+    // the async copies above read caller memory: complete them before returning
+    hipStreamSynchronize(h->stream);
+    st.rows += b->n;
+    for (int64_t i = 0; i < b->n; i++) {
+        h->st_ts.push_back(b->ts[i]);
+        h->st_stream.push_back((uint8_t)b->stream);
+        h->st_row.push_back((uint32_t)(r0 + i));
+        int32_t k = h->partitioned ? (b->keys ? b->keys[i] : -1) : 0;
+        h->st_key.push_back(k);
+        if (k + 1 > h->max_key) h->max_key = k + 1;
+    }
+    h->seq_next += b->n;
+    return SH_OK;
+}
+
+int sh_advance_time(sh_handle* h, int64_t now_ms) {
+    (void)now_ms;
+    if (!h) return SH_E_INVALID_ARG;
+    return SH_OK;  // no timer states are lowered to the device engine yet
+}
+
+static int ensure_keys(sh_handle* h, int32_t nkeys) {
+    if (nkeys <= h->nkeys_alloc) return 0;
+    int32_t nk = std::max(nkeys, h->nkeys_alloc * 2);
+    size_t old = (size_t)h->nkeys_alloc * h->lay.key_bytes;
+    if (h->d_kstate.ensure((size_t)nk * h->lay.key_bytes)) return SH_E_OOM;
+    hipMemsetAsync((uint8_t*)h->d_kstate.p + old, 0, (size_t)nk * h->lay.key_bytes - old, h->stream);
+    h->nkeys_alloc = nk;
+    return 0;
+}
+
+static int ensure_ws(sh_handle* h, int64_t n) {
+    const int64_t tiles = (n + 4095) / 4096;
+    int rc = 0;
+    rc |= h->w_keys_a.ensure_fresh(n * 4);
+    rc |= h->w_keys_b.ensure_fresh(n * 4);
+    rc |= h->w_idx_a.ensure_fresh(n * 4);
+    rc |= h->w_idx_b.ensure_fresh(n * 4);
+    rc |= h->w_hist.ensure_fresh(256 * tiles * 4 + 64);
+    size_t sw = std::max(shd_scan_tmp_words(256 * tiles), shd_scan_tmp_words(n));
+    rc |= h->w_scan.ensure_fresh(sw * 4 + 64);
+    rc |= h->w_seg.ensure_fresh((3 * n + 4) * 4);
+    rc |= h->w_cnt.ensure_fresh(n * 4 + 4);
+    rc |= h->w_off.ensure_fresh(n * 4 + 4);
+    rc |= h->w_ctr.ensure_fresh(64);
+    return rc ? SH_E_OOM : 0;
+}
+
+// segment -> advance -> place for one device batch; fills outputs into the
+// w_o* buffers (or caller-provided device buffers) and returns the match count
+static int run_batch(sh_handle* h, const shd_batch& B, int32_t nkeys, const shd_cols& cols, uint64_t* out_seq,
+                     int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, int64_t out_cap, int64_t* n_matches,
+                     bool timed) {
+    hipStream_t st = h->stream;
+    const int64_t n = B.n;
+    if (ensure_ws(h, n)) return fail(h, SH_E_OOM, "workspace");
+    hipMemcpyAsync(h->d_cols_desc.p, &cols, sizeof(shd_cols), hipMemcpyHostToDevice, st);
+    if (h->tmp_cap < n + (1 << 16)) {
+        h->tmp_cap = n + (1 << 16);
+        if (h->w_tmp.ensure_fresh((size_t)h->tmp_cap * (3 + h->n_out) * 8)) return fail(h, SH_E_OOM, "emit buffer");
+    }
+    // keep a copy of the key state: an emit-buffer overflow restores and reruns
+    DevBuf backup;
+    const size_t kbytes = (size_t)nkeys * h->lay.key_bytes;
+    for (int attempt = 0; attempt < 8; attempt++) {
+        if (attempt == 0 && !timed) {
+            if (backup.ensure_fresh(kbytes)) return fail(h, SH_E_OOM, "state backup");
+            hipMemcpyAsync(backup.p, h->d_kstate.p, kbytes, hipMemcpyDeviceToDevice, st);
+        }
+        hipMemsetAsync(h->w_cnt.p, 0, n * 4, st);
+        hipMemsetAsync(h->w_ctr.p, 0, 8, st);
+        hipMemsetAsync(h->d_err.p, 0, 8, st);
+        if (timed) hipEventRecord(h->ev[0], st);
+        shd_segment_ws ws;
+        ws.keys_a = h->w_keys_a.as<uint32_t>();
+        ws.keys_b = h->w_keys_b.as<uint32_t>();
+        ws.idx_a = h->w_idx_a.as<uint32_t>();
+        ws.idx_b = h->w_idx_b.as<uint32_t>();
+        ws.hist = h->w_hist.as<uint32_t>();
+        ws.scan_tmp = h->w_scan.as<uint32_t>();
+        ws.seg_off = h->w_seg.as<uint32_t>();
+        ws.cap = n;
+        const uint32_t* perm = nullptr;
+        const uint32_t* skeys = nullptr;
+        int rc = shd_segment(&B, nkeys, &ws, st, &perm, &skeys);
+        if (rc) return fail(h, SH_E_HIP, "segment launch failed");
+        if (timed) hipEventRecord(h->ev[1], st);
+        shd_emit em;
+        em.tmp = h->w_tmp.as<uint64_t>();
+        em.tmp_ctr = h->w_ctr.as<unsigned long long>();
+        em.tmp_cap = h->tmp_cap;
+        em.match_cnt = h->w_cnt.as<uint32_t>();
+        em.err = h->d_err.as<int32_t>();
+        rc = shd_advance(h->d_prog.as<shp_program>(), &h->lay, h->d_kstate.as<uint8_t>(), nkeys, &B, perm, skeys,
+                         ws.seg_off, h->d_cols_desc.as<shd_cols>(), &em, st);
+        if (rc) return fail(h, SH_E_HIP, "advance launch failed");
+        if (timed) hipEventRecord(h->ev[2], st);
+        int32_t herr[2] = {0, 0};
+        unsigned long long nrec = 0;
+        hipMemcpyAsync(herr, h->d_err.p, 8, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(&nrec, h->w_ctr.p, 8, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in advance");
+        if (herr[0] == 2) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
+        if (herr[0]) return fail(h, SH_E_STATE_OVERFLOW, "partial-match list overflow (raise SH_PARTIAL_CAP)");
+        if (herr[1]) {
+            // emit buffer too small: restore state, grow, rerun
+            if (timed) {
+                h->tmp_cap *= 4;
+                if (h->w_tmp.ensure_fresh((size_t)h->tmp_cap * (3 + h->n_out) * 8))
+                    return fail(h, SH_E_OOM, "emit buffer");
+                hipMemsetAsync(h->d_kstate.p, 0, kbytes, st);  // timed runs start from fresh state
+                continue;
+            }
+            hipMemcpyAsync(h->d_kstate.p, backup.p, kbytes, hipMemcpyDeviceToDevice, st);
+            h->tmp_cap *= 4;
+            if (h->w_tmp.ensure_fresh((size_t)h->tmp_cap * (3 + h->n_out) * 8))
+                return fail(h, SH_E_OOM, "emit buffer");
+            continue;
+        }
+        // total matches = sum of per-event counts (<= nrec, chunk tails unused)
+        if (timed) hipEventRecord(h->ev[2], st);
+        rc = shd_emit_place(&em, h->n_out, n, h->w_off.as<uint32_t>(), h->w_scan.as<uint32_t>(), (int64_t)nrec, &B,
+                            nullptr, nullptr, nullptr, nullptr, st);
+        (void)rc;
+        uint32_t last_off = 0, last_cnt = 0;
+        hipMemcpyAsync(&last_off, h->w_off.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(&last_cnt, h->w_cnt.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, st);
+        hipStreamSynchronize(st);
+        const int64_t total = (int64_t)last_off + last_cnt;
+        *n_matches = total;
+        if (total > out_cap) {
+            backup.release();
+            return SH_E_MORE;
+        }
+        // placement into the ordered output
+        rc = shd_emit_place(&em, h->n_out, 0, h->w_off.as<uint32_t>(), h->w_scan.as<uint32_t>(), (int64_t)nrec, &B,
+                            out_seq, out_ts, out_vals, out_nulls, st);
+        if (timed) hipEventRecord(h->ev[3], st);
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in placement");
+        if (timed) {
+            hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
+            hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
+            hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
+            hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
+            h->times.advance_launches++;
+        }
+        backup.release();
+        return SH_OK;
+    }
+    backup.release();
+    return fail(h, SH_E_OOM, "emit buffer kept overflowing");
+}
+
+static shd_cols store_cols(sh_handle* h) {
+    shd_cols c;
+    memset(&c, 0, sizeof(c));
+    for (int s = 0; s < h->app.n_streams; s++)
+        for (size_t a = 0; a < h->stream_types[s].size(); a++) {
+            c.col[s][a] = h->stores[s].cols[a].p;
+            c.nul[s][a] = h->stores[s].has_nul[a] ? (const uint8_t*)h->stores[s].nuls[a].p : nullptr;
+        }
+    return c;
+}
+
+// process every staged event
+static int flush(sh_handle* h) {
+    const int64_t n = (int64_t)h->st_ts.size();
+    if (n == 0) return SH_OK;
+    if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device");
+    h->stream = h->own_stream;
+    hipStream_t st = h->stream;
+    int32_t nkeys = std::max(1, h->max_key);
+    if (ensure_keys(h, nkeys)) return fail(h, SH_E_OOM, "key state");
+    if (h->w_ts.ensure_fresh(n * 8) || h->w_stream.ensure_fresh(n) || h->w_row.ensure_fresh(n * 4) ||
+        h->w_key.ensure_fresh(n * 4))
+        return fail(h, SH_E_OOM, "staging");
+    hipMemcpyAsync(h->w_ts.p, h->st_ts.data(), n * 8, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_stream.p, h->st_stream.data(), n, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_row.p, h->st_row.data(), n * 4, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_key.p, h->st_key.data(), n * 4, hipMemcpyHostToDevice, st);
+    shd_batch B;
+    B.ts = h->w_ts.as<int64_t>();
+    B.stream = h->w_stream.as<uint8_t>();
+    B.row = h->w_row.as<uint32_t>();
+    B.keys = h->partitioned ? h->w_key.as<int32_t>() : nullptr;
+    B.row_base = 0;
+    B.seq_base = h->seq_staged0;
+    B.n = n;
+    shd_cols cols = store_cols(h);
+    int64_t cap = std::max<int64_t>(n, 1024);
+    int64_t nm = 0;
+    int rc;
+    for (;;) {
+        if (h->w_oseq.ensure_fresh(cap * 8) || h->w_ots.ensure_fresh(cap * 8) ||
+            h->w_ovals.ensure_fresh(cap * std::max(1, h->n_out) * 8) ||
+            h->w_onulls.ensure_fresh(cap * std::max(1, h->n_out)))
+            return fail(h, SH_E_OOM, "output buffers");
+        rc = run_batch(h, B, nkeys, cols, h->w_oseq.as<uint64_t>(), h->w_ots.as<int64_t>(), h->w_ovals.as<int64_t>(),
+                       h->w_onulls.as<uint8_t>(), cap, &nm, false);
+        if (rc == SH_E_MORE) {
+            // the state advanced already; rerunning would double-advance: outputs
+            // sized from the count are produced by the placement below instead
+            cap = nm;
+            if (h->w_oseq.ensure_fresh(cap * 8) || h->w_ots.ensure_fresh(cap * 8) ||
+                h->w_ovals.ensure_fresh(cap * std::max(1, h->n_out) * 8) ||
+                h->w_onulls.ensure_fresh(cap * std::max(1, h->n_out)))
+                return fail(h, SH_E_OOM, "output buffers");
+            shd_emit em;
+            em.tmp = h->w_tmp.as<uint64_t>();
+            em.tmp_ctr = h->w_ctr.as<unsigned long long>();
+            em.tmp_cap = h->tmp_cap;
+            em.match_cnt = h->w_cnt.as<uint32_t>();
+            em.err = h->d_err.as<int32_t>();
+            unsigned long long nrec = 0;
+            hipMemcpy(&nrec, h->w_ctr.p, 8, hipMemcpyDeviceToHost);
+            shd_emit_place(&em, h->n_out, 0, h->w_off.as<uint32_t>(), h->w_scan.as<uint32_t>(), (int64_t)nrec, &B,
+                           h->w_oseq.as<uint64_t>(), h->w_ots.as<int64_t>(), h->w_ovals.as<int64_t>(),
+                           h->w_onulls.as<uint8_t>(), st);
+            hipStreamSynchronize(st);
+            rc = SH_OK;
+        }
+        break;
+    }
+    if (rc) return rc;
+    // D2H into the host output queue
+    size_t base = h->o_seq.size();
+    h->o_query.resize(base + nm, 0);
+    h->o_seq.resize(base + nm);
+    h->o_ts.resize(base + nm);
+    h->o_vals.resize((base + nm) * h->n_out);
+    h->o_nulls.resize((base + nm) * h->n_out);
+    if (nm) {
+        hipMemcpy(h->o_seq.data() + base, h->w_oseq.p, nm * 8, hipMemcpyDeviceToHost);
+        hipMemcpy(h->o_ts.data() + base, h->w_ots.p, nm * 8, hipMemcpyDeviceToHost);
+        if (h->n_out) {
+            hipMemcpy(h->o_vals.data() + base * h->n_out, h->w_ovals.p, nm * h->n_out * 8, hipMemcpyDeviceToHost);
+            hipMemcpy(h->o_nulls.data() + base * h->n_out, h->w_onulls.p, nm * h->n_out, hipMemcpyDeviceToHost);
+        }
+    }
+    h->st_ts.clear();
+    h->st_stream.clear();
+    h->st_row.clear();
+    h->st_key.clear();
+    h->seq_staged0 = h->seq_next;
+    return SH_OK;
+}
+
+int64_t sh_pending(sh_handle* h) {
+    if (!h) return SH_E_INVALID_ARG;
+    int rc = flush(h);
+    if (rc) return rc;
+    return (int64_t)h->o_seq.size() - h->o_read;
+}
+
+int sh_drain(sh_handle* h, sh_match_buf* out) {
+    if (!h || !out) return SH_E_INVALID_ARG;
+    int rc = flush(h);
+    if (rc) return rc;
+    const int64_t avail = (int64_t)h->o_seq.size() - h->o_read;
+    const int64_t k = std::min(avail, out->capacity);
+    const int no = out->n_out;
+    for (int64_t i = 0; i < k; i++) {
+        const int64_t r = h->o_read + i;
+        if (out->query) out->query[i] = h->o_query[r];
+        if (out->trigger_seq) out->trigger_seq[i] = h->o_seq[r];
+        if (out->ts) out->ts[i] = h->o_ts[r];
+        for (int c = 0; c < no; c++) {
+            const bool has = c < h->n_out;
+            if (out->values) out->values[i * no + c] = has ? h->o_vals[r * h->n_out + c] : 0;
+            if (out->nulls) out->nulls[i * no + c] = has ? h->o_nulls[r * h->n_out + c] : 1;
+        }
+    }
+    out->count = k;
+    h->o_read += k;
+    if (h->o_read == (int64_t)h->o_seq.size()) {
+        h->o_query.clear();
+        h->o_seq.clear();
+        h->o_ts.clear();
+        h->o_vals.clear();
+        h->o_nulls.clear();
+        h->o_read = 0;
+    }
+    return avail > k ? SH_E_MORE : SH_OK;
+}
+
+int sh_run_device(sh_handle* h, sh_device_run* run) {
+    if (!h || !run) return SH_E_INVALID_ARG;
+    if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device");
+    if (h->app.n_streams != 1) return fail(h, SH_E_UNSUPPORTED, "sh_run_device: single-stream apps only");
+    if (run->n <= 0 || run->n > 0x7FFFFFFFll) return fail(h, SH_E_INVALID_ARG, "sh_run_device: 1 <= n < 2^31");
+    h->stream = run->stream ? (hipStream_t)run->stream : h->own_stream;
+    const int32_t nkeys = h->partitioned ? std::max(1, run->n_keys) : 1;
+    // fresh per-key state
+    if (ensure_keys(h, nkeys)) return fail(h, SH_E_OOM, "key state");
+    hipMemsetAsync(h->d_kstate.p, 0, (size_t)nkeys * h->lay.key_bytes, h->stream);
+    shd_batch B;
+    B.ts = run->d_ts;
+    B.stream = nullptr;
+    B.row = nullptr;
+    B.keys = h->partitioned ? run->d_keys : nullptr;
+    B.row_base = 0;
+    B.seq_base = 0;
+    B.n = run->n;
+    shd_cols cols;
+    memset(&cols, 0, sizeof(cols));
+    for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = run->d_cols[a];
+    int64_t nm = 0;
+    h->times = sh_kernel_times{};
+    int rc = run_batch(h, B, nkeys, cols, run->d_out_seq, nullptr, run->d_out_values, nullptr, run->out_capacity,
+                       &nm, true);
+    run->out_count = nm;
+    return rc;
+}
+
+int sh_last_kernel_times(sh_handle* h, sh_kernel_times* t) {
+    if (!h || !t) return SH_E_INVALID_ARG;
+    *t = h->times;
+    return SH_OK;
+}
+
+}  // extern "C"

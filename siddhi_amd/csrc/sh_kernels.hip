@@ -1,0 +1,885 @@
+// sh_kernels.hip — gfx950 kernels of the batch NFA matcher.
+//
+//  (1) predicate evaluation      : typed postfix VM (vm_eval) run per
+//                                  (partial, event) inside the advance kernel
+//  (2) radix segment             : k_digit_hist / k_digit_scatter (stable LSD
+//                                  radix sort of (key, arrival index), 8-bit
+//                                  digits, wave64 ballot ranking) + k_seg_mark
+//  (3) per-key state advance     : k_advance, one lane per partition key walks
+//                                  its segment in arrival order with the
+//                                  pending / new-and-every lists in HBM
+//  (4) spawn / compaction        : partial spawn + list compaction in
+//                                  k_advance, ordered match placement via an
+//                                  exclusive scan of per-event match counts
+//  (5) within expiry             : break-early head expiry per event (k_advance)
+//
+// Semantics follow core/query/input/stream/state/StreamPreStateProcessor.java
+// (expireEvents :325-361, updateState :307-323, processAndReturn :363-403),
+// StreamPostStateProcessor.java:64-83, the Pattern*ProcessStreamReceiver
+// stabilizeStates/eventSequence rules and the executor conversion/null rules.
+#include <hip/hip_runtime.h>
+
+#include "../../include/sh_query.h"
+#include "sh_device.h"
+
+#define TPB 256
+#define RADIX_ITEMS 16
+#define RADIX_TILE (TPB * RADIX_ITEMS)
+#define SCAN_ITEMS 4
+#define SCAN_TILE (TPB * SCAN_ITEMS)
+
+// ------------------------------------------------------------------ scan
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// block-wide exclusive scan of one value per thread; returns block total in *total
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total) {
+    __shared__ uint32_t wsum[TPB / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < TPB / 64; i++) {
+        uint32_t s = wsum[i];
+        if (i < w) off += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
+__global__ void __launch_bounds__(TPB) k_scan_tiles(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                    int64_t n, uint32_t* __restrict__ tile_sums) {
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; j++) {
+        v[j] = (base + j < n) ? in[base + j] : 0u;
+        s += v[j];
+    }
+    uint32_t tot;
+    uint32_t off = block_excl_scan(s, &tot);
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; j++) {
+        if (base + j < n) out[base + j] = off;
+        off += v[j];
+    }
+    if (threadIdx.x == 0 && tile_sums) tile_sums[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(TPB) k_scan_add(uint32_t* __restrict__ out, int64_t n,
+                                                  const uint32_t* __restrict__ tile_off) {
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+    const uint32_t add = tile_off[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; j++)
+        if (base + j < n) out[base + j] += add;
+}
+
+static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+extern "C" size_t shd_scan_tmp_words(int64_t n) {
+    size_t words = 0;
+    int64_t m = ceil_div(n, SCAN_TILE);
+    while (m > 1) {
+        words += 2 * (size_t)m + 2;
+        m = ceil_div(m, SCAN_TILE);
+    }
+    return words + 4;
+}
+
+// exclusive scan of n uint32 (in may equal out); tmp >= shd_scan_tmp_words(n)
+extern "C" int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n <= 0) return 0;
+    int64_t tiles = ceil_div(n, SCAN_TILE);
+    if (tiles == 1) {
+        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(TPB), 0, st, in, out, n, (uint32_t*)nullptr);
+        return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
+    uint32_t* sums = tmp;
+    uint32_t* sums_scanned = tmp + tiles + 1;
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)tiles), dim3(TPB), 0, st, in, out, n, sums);
+    int rc = shd_exclusive_scan(sums, sums_scanned, tiles, tmp + 2 * tiles + 2, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)tiles), dim3(TPB), 0, st, out, n, (const uint32_t*)sums_scanned);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// ------------------------------------------------------------------ radix segment
+// digit histogram per tile, digit-major: hist[d * ntiles + tile]
+__global__ void __launch_bounds__(TPB) k_digit_hist(const uint32_t* __restrict__ keys, const int32_t* __restrict__ raw,
+                                                    uint32_t sentinel, int64_t n, int shift,
+                                                    uint32_t* __restrict__ hist, int64_t ntiles) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * RADIX_TILE;
+#pragma unroll 4
+    for (int j = 0; j < RADIX_ITEMS; j++) {
+        int64_t i = base + j * TPB + threadIdx.x;
+        if (i < n) {
+            uint32_t k;
+            if (keys) {
+                k = keys[i];
+            } else {
+                int32_t r = raw ? raw[i] : 0;
+                k = r < 0 ? sentinel : (uint32_t)r;
+            }
+            atomicAdd(&h[(k >> shift) & 0xFF], 1u);
+        }
+    }
+    __syncthreads();
+    hist[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// stable scatter: elements of a tile are ranked in arrival order within their digit
+__global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ raw,
+                                                       uint32_t sentinel, const uint32_t* __restrict__ idx_in, int64_t n,
+                                                       int shift, const uint32_t* __restrict__ offs, int64_t ntiles,
+                                                       uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out) {
+    __shared__ uint32_t running[256];
+    __shared__ uint32_t wcnt[TPB / 64][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    running[threadIdx.x] = offs[(int64_t)threadIdx.x * ntiles + blockIdx.x];
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int64_t base = (int64_t)blockIdx.x * RADIX_TILE;
+    for (int j = 0; j < RADIX_ITEMS; j++) {
+#pragma unroll
+        for (int q = 0; q < TPB / 64; q++) wcnt[q][threadIdx.x] = 0;
+        __syncthreads();
+        const int64_t i = base + j * TPB + threadIdx.x;
+        const bool valid = i < n;
+        uint32_t k = 0, id = 0;
+        if (valid) {
+            if (keys_in) {
+                k = keys_in[i];
+            } else {
+                int32_t r = raw ? raw[i] : 0;
+                k = r < 0 ? sentinel : (uint32_t)r;
+            }
+            id = idx_in ? idx_in[i] : (uint32_t)i;
+        }
+        const uint32_t d = (k >> shift) & 0xFF;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(valid && bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t rank = __popcll(peers & lt_mask);
+        if (valid && rank == 0) wcnt[w][d] = __popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pre = 0;
+            for (int q = 0; q < w; q++) pre += wcnt[q][d];
+            const uint32_t dst = running[d] + pre + rank;
+            keys_out[dst] = k;
+            idx_out[dst] = id;
+        }
+        __syncthreads();
+        uint32_t add = 0;
+#pragma unroll
+        for (int q = 0; q < TPB / 64; q++) add += wcnt[q][threadIdx.x];
+        running[threadIdx.x] += add;
+        __syncthreads();
+    }
+}
+
+// segment starts: flag positions where the (sorted) key changes; sentinel excluded
+__global__ void k_seg_flags(const uint32_t* __restrict__ skeys, int64_t n, uint32_t sentinel,
+                            uint32_t* __restrict__ flags) {
+    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    uint32_t k = skeys ? skeys[p] : 0u;
+    bool start = (p == 0) || (skeys && skeys[p - 1] != k);
+    flags[p] = (start && k != sentinel) ? 1u : 0u;
+}
+
+__global__ void k_seg_compact(const uint32_t* __restrict__ flags, const uint32_t* __restrict__ pos, int64_t n,
+                              uint32_t* __restrict__ seg_list, uint32_t* __restrict__ nseg) {
+    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    if (flags[p]) seg_list[pos[p]] = (uint32_t)p;
+    if (p == n - 1) *nseg = pos[p] + flags[p];
+}
+
+// ------------------------------------------------------------------ expression VM
+struct VmVal {
+    int64_t b;
+    uint8_t t;
+    uint8_t null;
+};
+
+__device__ __forceinline__ float bits_f32(int64_t b) { return __int_as_float((int32_t)(uint32_t)b); }
+__device__ __forceinline__ double bits_f64(int64_t b) { return __longlong_as_double(b); }
+__device__ __forceinline__ int64_t f32_bits(float f) { return (int64_t)(uint32_t)__float_as_int(f); }
+__device__ __forceinline__ int64_t f64_bits(double d) { return __double_as_longlong(d); }
+
+__device__ __forceinline__ int64_t to_i64(const VmVal& v) {
+    return v.t == SH_T_LONG ? v.b : (int64_t)(int32_t)v.b;  // only INT/LONG reach here
+}
+__device__ __forceinline__ float to_f32(const VmVal& v) {
+    switch (v.t) {
+        case SH_T_INT: return (float)(int32_t)v.b;
+        case SH_T_LONG: return (float)v.b;
+        case SH_T_FLOAT: return bits_f32(v.b);
+        default: return (float)bits_f64(v.b);
+    }
+}
+__device__ __forceinline__ double to_f64(const VmVal& v) {
+    switch (v.t) {
+        case SH_T_INT: return (double)(int32_t)v.b;
+        case SH_T_LONG: return (double)v.b;
+        case SH_T_FLOAT: return (double)bits_f32(v.b);
+        default: return bits_f64(v.b);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ bool cmp_op(int op, T a, T b) {
+    switch (op) {
+        case SH_OP_EQ: return a == b;
+        case SH_OP_NE: return a != b;
+        case SH_OP_GT: return a > b;
+        case SH_OP_GE: return a >= b;
+        case SH_OP_LT: return a < b;
+        default: return a <= b;
+    }
+}
+
+__device__ __forceinline__ int64_t load_attr(const shd_cols* C, int s, int a, int type, uint32_t row) {
+    const void* p = C->col[s][a];
+    switch (type) {
+        case SH_T_LONG: return ((const int64_t*)p)[row];
+        case SH_T_FLOAT: return (int64_t)(uint32_t)((const uint32_t*)p)[row];
+        case SH_T_DOUBLE: return ((const int64_t*)p)[row];
+        case SH_T_BOOL: return ((const uint8_t*)p)[row] ? 1 : 0;
+        default: return (int64_t)((const int32_t*)p)[row];
+    }
+}
+
+// Evaluate `len` instructions at `pc`. rows[slot] = row of the slot's event
+// (SHD_NULL_ROW when the slot is empty). Chains are length 1 for stream
+// states, so chain index 0 / CURRENT address the event and anything else is null
+// (StateEvent.getStreamEvent, StateEvent.java:138-182).
+__device__ VmVal vm_eval(const shp_program* __restrict__ P, int pc, int len, const uint32_t* rows,
+                         const shd_cols* __restrict__ C) {
+    VmVal st[SHP_MAX_STACK];
+    int sp = 0;
+    for (int k = 0; k < len; k++) {
+        const shp_instr in = P->code[pc + k];
+        switch (in.op) {
+            case OPC_CONST: {
+                VmVal v;
+                v.b = P->consts[in.x];
+                v.t = P->const_type[in.x];
+                v.null = P->const_null[in.x];
+                st[sp++] = v;
+                break;
+            }
+            case OPC_VAR: {
+                VmVal v;
+                v.t = in.c;
+                const uint32_t row = rows[in.a];
+                if (row == SHD_NULL_ROW || !(in.x == 0 || in.x == SH_CHAIN_CURRENT)) {
+                    v.null = 1;
+                    v.b = 0;
+                } else {
+                    const int s = P->state_stream[in.a];
+                    const uint8_t* nm = C->nul[s][in.b];
+                    v.null = nm ? nm[row] : 0;
+                    v.b = load_attr(C, s, in.b, in.c, row);
+                }
+                st[sp++] = v;
+                break;
+            }
+            case OPC_AND: {
+                VmVal r = st[--sp], l = st[--sp];
+                VmVal o;
+                o.t = SH_T_BOOL;
+                o.null = 0;
+                o.b = (!l.null && l.b && !r.null && r.b) ? 1 : 0;
+                st[sp++] = o;
+                break;
+            }
+            case OPC_OR: {
+                VmVal r = st[--sp], l = st[--sp];
+                VmVal o;
+                o.t = SH_T_BOOL;
+                o.null = 0;
+                o.b = ((!l.null && l.b) || (!r.null && r.b)) ? 1 : 0;
+                st[sp++] = o;
+                break;
+            }
+            case OPC_NOT: {
+                VmVal l = st[--sp];
+                VmVal o;
+                o.t = SH_T_BOOL;
+                o.null = 0;
+                o.b = (!l.null && l.b) ? 0 : 1;  // Not(null) = true
+                st[sp++] = o;
+                break;
+            }
+            case OPC_BOOLV: {
+                VmVal l = st[--sp];
+                VmVal o;
+                o.t = SH_T_BOOL;
+                o.null = 0;
+                o.b = (!l.null && l.b) ? 1 : 0;
+                st[sp++] = o;
+                break;
+            }
+            case OPC_ISNULL: {
+                VmVal l = st[--sp];
+                VmVal o;
+                o.t = SH_T_BOOL;
+                o.null = 0;
+                o.b = l.null ? 1 : 0;
+                st[sp++] = o;
+                break;
+            }
+            case OPC_ISNULL_STREAM: {
+                VmVal o;
+                o.t = SH_T_BOOL;
+                o.null = 0;
+                o.b = (rows[in.a] == SHD_NULL_ROW || !(in.x == 0 || in.x == SH_CHAIN_CURRENT)) ? 1 : 0;
+                st[sp++] = o;
+                break;
+            }
+            case OPC_CMP: {
+                VmVal r = st[--sp], l = st[--sp];
+                bool res = false;
+                if (!l.null && !r.null) {
+                    switch (in.b) {
+                        case DOM_I32: res = cmp_op<int32_t>(in.a, (int32_t)l.b, (int32_t)r.b); break;
+                        case DOM_I64: res = cmp_op<int64_t>(in.a, to_i64(l), to_i64(r)); break;
+                        case DOM_F32: res = cmp_op<float>(in.a, to_f32(l), to_f32(r)); break;
+                        case DOM_F64: res = cmp_op<double>(in.a, to_f64(l), to_f64(r)); break;
+                        case DOM_BOOL: res = cmp_op<int>(in.a, l.b != 0, r.b != 0); break;
+                        default: res = cmp_op<int32_t>(in.a, (int32_t)l.b, (int32_t)r.b); break;
+                    }
+                }
+                VmVal o;
+                o.t = SH_T_BOOL;
+                o.null = 0;
+                o.b = res ? 1 : 0;
+                st[sp++] = o;
+                break;
+            }
+            case OPC_ARITH: {
+                VmVal r = st[--sp], l = st[--sp];
+                VmVal o;
+                o.t = in.b;
+                o.null = 0;
+                o.b = 0;
+                if (l.null || r.null) {
+                    o.null = 1;
+                } else if (in.b == SH_T_INT) {
+                    const uint32_t a = (uint32_t)l.b, b = (uint32_t)r.b;
+                    const int32_t sa = (int32_t)a, sb = (int32_t)b;
+                    int32_t res = 0;
+                    switch (in.a) {
+                        case SH_OP_ADD: res = (int32_t)(a + b); break;
+                        case SH_OP_SUB: res = (int32_t)(a - b); break;
+                        case SH_OP_MUL: res = (int32_t)(a * b); break;
+                        case SH_OP_DIV:
+                            if (sb == 0) o.null = 1;
+                            else res = (sa == INT32_MIN && sb == -1) ? INT32_MIN : sa / sb;
+                            break;
+                        default:
+                            if (sb == 0) o.null = 1;
+                            else res = (sb == -1) ? 0 : sa % sb;
+                    }
+                    o.b = res;
+                } else if (in.b == SH_T_LONG) {
+                    const uint64_t a = (uint64_t)to_i64(l), b = (uint64_t)to_i64(r);
+                    const int64_t sa = (int64_t)a, sb = (int64_t)b;
+                    int64_t res = 0;
+                    switch (in.a) {
+                        case SH_OP_ADD: res = (int64_t)(a + b); break;
+                        case SH_OP_SUB: res = (int64_t)(a - b); break;
+                        case SH_OP_MUL: res = (int64_t)(a * b); break;
+                        case SH_OP_DIV:
+                            if (sb == 0) o.null = 1;
+                            else res = (sa == INT64_MIN && sb == -1) ? INT64_MIN : sa / sb;
+                            break;
+                        default:
+                            if (sb == 0) o.null = 1;
+                            else res = (sb == -1) ? 0 : sa % sb;
+                    }
+                    o.b = res;
+                } else if (in.b == SH_T_FLOAT) {
+                    const float a = to_f32(l), b = to_f32(r);
+                    float res = 0.f;
+                    switch (in.a) {
+                        case SH_OP_ADD: res = __fadd_rn(a, b); break;
+                        case SH_OP_SUB: res = __fsub_rn(a, b); break;
+                        case SH_OP_MUL: res = __fmul_rn(a, b); break;
+                        case SH_OP_DIV:
+                            if (b == 0.0f) o.null = 1;
+                            else res = __fdiv_rn(a, b);
+                            break;
+                        default:
+                            if (b == 0.0f) o.null = 1;
+                            else res = fmodf(a, b);
+                    }
+                    o.b = f32_bits(res);
+                } else {
+                    const double a = to_f64(l), b = to_f64(r);
+                    double res = 0.0;
+                    switch (in.a) {
+                        case SH_OP_ADD: res = __dadd_rn(a, b); break;
+                        case SH_OP_SUB: res = __dsub_rn(a, b); break;
+                        case SH_OP_MUL: res = __dmul_rn(a, b); break;
+                        case SH_OP_DIV:
+                            if (b == 0.0) o.null = 1;
+                            else res = __ddiv_rn(a, b);
+                            break;
+                        default:
+                            if (b == 0.0) o.null = 1;
+                            else res = fmod(a, b);
+                    }
+                    o.b = f64_bits(res);
+                }
+                st[sp++] = o;
+                break;
+            }
+            case OPC_SELECT: {
+                VmVal e = st[--sp], t = st[--sp], c = st[--sp];
+                st[sp++] = (!c.null && c.b) ? t : e;
+                break;
+            }
+            case OPC_CAST: {
+                st[sp - 1].t = in.b;
+                break;
+            }
+        }
+    }
+    return st[sp - 1];
+}
+
+// ------------------------------------------------------------------ per-key state
+// key block layout (8-byte words):
+//   [0] flags: bit0 initialized, bit1 start template pending, bit2 start template in new-and-every
+//   [1 .. n]   list counts: word 1+k = pending count of state k | (nae count << 32)
+//   off_lists: per state k in 1..n-1: pending[cap] then nae[cap]; record = ts, ts0, rows[n] (u32)
+//   off_agg:   per output: dsum, lsum, cnt, mx bits, mx null
+struct KeyView {
+    uint64_t* base;
+    const shp_layout* L;
+    __device__ uint64_t* list(int k, int which) const {  // which 0 pending, 1 nae
+        return (uint64_t*)((uint8_t*)base + L->off_lists + ((int64_t)(k - 1) * 2 + which) * L->list_bytes);
+    }
+    __device__ uint64_t* rec(uint64_t* lst, int i) const { return lst + (int64_t)i * L->rec_words; }
+    __device__ uint32_t pcount(int k) const { return (uint32_t)base[1 + k]; }
+    __device__ uint32_t ncount(int k) const { return (uint32_t)(base[1 + k] >> 32); }
+    __device__ void set_counts(int k, uint32_t p, uint32_t n) const { base[1 + k] = (uint64_t)p | ((uint64_t)n << 32); }
+};
+
+__device__ __forceinline__ void rec_copy(uint64_t* dst, const uint64_t* src, int words) {
+    for (int i = 0; i < words; i++) dst[i] = src[i];
+}
+
+struct Emitter {
+    const shd_emit* em;
+    uint64_t* chunk;
+    int64_t used, cap;
+    int rec_words;
+};
+
+#define EMIT_CHUNK 64
+
+__device__ __forceinline__ uint64_t* emit_slot(Emitter& E) {
+    if (E.used == E.cap) {
+        unsigned long long at = atomicAdd(E.em->tmp_ctr, (unsigned long long)EMIT_CHUNK);
+        if ((int64_t)at + EMIT_CHUNK > E.em->tmp_cap) {
+            atomicExch(&E.em->err[1], 1);
+            return nullptr;
+        }
+        E.chunk = E.em->tmp + (int64_t)at * E.rec_words;
+        E.used = 0;
+        E.cap = EMIT_CHUNK;
+    }
+    uint64_t* r = E.chunk + E.used * E.rec_words;
+    E.used++;
+    return r;
+}
+
+// QuerySelector.processNoGroupBy / processInBatchNoGroupBy for one match + the
+// Sum/Avg/Count/Max/Min aggregators (per partition key, match order)
+__device__ void emit_match(const shp_program* __restrict__ P, const KeyView& K, Emitter& E, const uint32_t* rows,
+                           const shd_cols* __restrict__ C, uint32_t local_i, uint32_t ordinal, int64_t ts) {
+    uint64_t* r = emit_slot(E);
+    uint64_t nullmask = 0;
+    uint64_t* agg = (uint64_t*)((uint8_t*)K.base + K.L->off_agg);
+    for (int o = 0; o < P->n_out; o++) {
+        const int aggk = P->out_agg[o];
+        VmVal v;
+        if (P->out_pc[o] >= 0)
+            v = vm_eval(P, P->out_pc[o], P->out_len[o], rows, C);
+        else {
+            v.null = 0;
+            v.b = 1;
+            v.t = SH_T_BOOL;
+        }
+        int64_t outb = v.b;
+        bool outnull = v.null;
+        if (aggk != SH_AGG_NONE) {
+            uint64_t* a = agg + o * 5;
+            double dsum = __longlong_as_double((long long)a[0]);
+            int64_t lsum = (int64_t)a[1];
+            int64_t cnt = (int64_t)a[2];
+            switch (aggk) {
+                case SH_AGG_SUM:
+                    if (!v.null) {
+                        if (v.t == SH_T_INT || v.t == SH_T_LONG)
+                            lsum += to_i64(v);
+                        else
+                            dsum = __dadd_rn(dsum, to_f64(v));
+                        cnt++;
+                    }
+                    outnull = false;
+                    outb = (P->out_type[o] == SH_T_LONG) ? lsum : f64_bits(dsum);
+                    break;
+                case SH_AGG_AVG:
+                    if (!v.null) {
+                        dsum = __dadd_rn(dsum, to_f64(v));
+                        cnt++;
+                    }
+                    outnull = cnt == 0;
+                    outb = outnull ? 0 : f64_bits(__ddiv_rn(dsum, (double)cnt));
+                    break;
+                case SH_AGG_COUNT:
+                    cnt++;
+                    outnull = false;
+                    outb = cnt;
+                    break;
+                default: {  // MAX / MIN
+                    if (!v.null) {
+                        VmVal m;
+                        m.b = (int64_t)a[3];
+                        m.t = v.t;
+                        m.null = (uint8_t)a[4];
+                        bool better = m.null;
+                        if (!better) {
+                            const int op = aggk == SH_AGG_MAX ? SH_OP_GT : SH_OP_LT;
+                            switch (v.t) {
+                                case SH_T_INT: better = cmp_op<int32_t>(op, (int32_t)v.b, (int32_t)m.b); break;
+                                case SH_T_LONG: better = cmp_op<int64_t>(op, v.b, m.b); break;
+                                case SH_T_FLOAT: better = cmp_op<float>(op, bits_f32(v.b), bits_f32(m.b)); break;
+                                default: better = cmp_op<double>(op, bits_f64(v.b), bits_f64(m.b)); break;
+                            }
+                        }
+                        if (better) {
+                            a[3] = (uint64_t)v.b;
+                            a[4] = 0;
+                        }
+                    }
+                    outnull = a[4] != 0;
+                    outb = (int64_t)a[3];
+                }
+            }
+            a[0] = (uint64_t)__double_as_longlong(dsum);
+            a[1] = (uint64_t)lsum;
+            a[2] = (uint64_t)cnt;
+        }
+        if (r) r[3 + o] = (uint64_t)outb;
+        if (outnull) nullmask |= (1ull << o);
+    }
+    if (r) {
+        r[0] = (uint64_t)local_i | ((uint64_t)ordinal << 32);
+        r[1] = (uint64_t)ts;
+        r[2] = nullmask;
+    }
+}
+
+__device__ __forceinline__ bool expired(const uint64_t* rec, int64_t now, int64_t within) {
+    const int64_t ts0 = (int64_t)rec[1];
+    const int64_t d = ts0 - now;
+    return (d < 0 ? -d : d) > within;
+}
+
+// ------------------------------------------------------------------ advance kernel
+// One lane per key segment: replays StreamPreStateProcessor / StreamPostStateProcessor
+// for a PATTERN chain over the key's events in arrival order.
+__global__ void __launch_bounds__(TPB) k_advance(const shp_program* __restrict__ P, shp_layout L,
+                                                 uint8_t* __restrict__ kstate, shd_batch B,
+                                                 const uint32_t* __restrict__ perm, const uint32_t* __restrict__ skeys,
+                                                 const uint32_t* __restrict__ seg_list, const uint32_t* __restrict__ nseg,
+                                                 const shd_cols* __restrict__ C, shd_emit EM, int32_t nkeys) {
+    const uint32_t sidx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sidx >= *nseg) return;
+    const uint32_t beg = seg_list[sidx];
+    const uint32_t key = skeys ? skeys[beg] : 0u;
+    if (key >= (uint32_t)nkeys) {  // key id outside the allocated key state
+        atomicExch(&EM.err[0], 2);
+        return;
+    }
+    KeyView K;
+    K.base = (uint64_t*)(kstate + (int64_t)key * L.key_bytes);
+    K.L = &L;
+    const int n = P->n_states;
+    const int rw = L.rec_words;
+    const int64_t within = P->within_ms;
+    Emitter E;
+    E.em = &EM;
+    E.chunk = nullptr;
+    E.used = 0;
+    E.cap = 0;
+    E.rec_words = 3 + P->n_out;
+    uint64_t flags = K.base[0];
+    if (!(flags & 1ull)) {
+        // initPartition -> StreamPreStateProcessor.init: start template into new-and-every
+        flags = 1ull | 4ull;
+        for (int k = 1; k < n; k++) K.set_counts(k, 0, 0);
+    }
+    uint32_t rows[SHP_MAX_STATES];
+    for (int64_t p = beg; p < B.n; p++) {
+        if (p != beg && skeys && skeys[p] != key) break;
+        const uint32_t i = perm ? perm[p] : (uint32_t)p;
+        const int64_t t = B.ts[i];
+        const int s = B.stream ? B.stream[i] : 0;
+        const uint32_t row = B.row ? B.row[i] : B.row_base + i;
+        uint32_t nmatch = 0;
+        // (5) within expiry on every state (PatternMultiProcessStreamReceiver.stabilizeStates)
+        if (within >= 0) {
+            for (int k = 1; k < n; k++) {
+                uint32_t pc = K.pcount(k), nc = K.ncount(k);
+                uint64_t* pl = K.list(k, 0);
+                uint32_t e = 0;
+                while (e < pc && expired(K.rec(pl, e), t, within)) e++;  // break at first live
+                if (e) {
+                    for (uint32_t q = e; q < pc; q++) rec_copy(K.rec(pl, q - e), K.rec(pl, q), rw);
+                    pc -= e;
+                }
+                uint64_t* nl = K.list(k, 1);
+                uint32_t wpos = 0;
+                for (uint32_t q = 0; q < nc; q++) {
+                    if (!expired(K.rec(nl, q), t, within)) {
+                        if (wpos != q) rec_copy(K.rec(nl, wpos), K.rec(nl, q), rw);
+                        wpos++;
+                    }
+                }
+                K.set_counts(k, pc, wpos);
+            }
+        }
+        // updateState for the states this stream drives
+        for (int u = 0; u < P->upd_count[s]; u++) {
+            const int k = P->upd_state[s][u];
+            if (k == 0) {
+                if (flags & 4ull) flags = (flags | 2ull) & ~4ull;
+                continue;
+            }
+            uint32_t pc = K.pcount(k), nc = K.ncount(k);
+            if (!nc) continue;
+            uint64_t* nl = K.list(k, 1);
+            // stable insertion sort by StateEvent timestamp (-1 last)
+            for (uint32_t a = 1; a < nc; a++) {
+                uint64_t tmp[2 + SHP_MAX_STATES / 2 + 1];
+                rec_copy(tmp, K.rec(nl, a), rw);
+                const int64_t ta = (int64_t)tmp[0];
+                int32_t b = (int32_t)a - 1;
+                while (b >= 0) {
+                    const int64_t tb = (int64_t)K.rec(nl, b)[0];
+                    const bool gt = (tb == -1) ? (ta != -1) : (ta != -1 && tb > ta);
+                    if (!gt) break;
+                    rec_copy(K.rec(nl, b + 1), K.rec(nl, b), rw);
+                    b--;
+                }
+                rec_copy(K.rec(nl, b + 1), tmp, rw);
+            }
+            if (pc + nc > (uint32_t)L.cap) {
+                atomicExch(&EM.err[0], 1);
+                nc = L.cap - pc;
+            }
+            uint64_t* pl = K.list(k, 0);
+            for (uint32_t q = 0; q < nc; q++) rec_copy(K.rec(pl, pc + q), K.rec(nl, q), rw);
+            K.set_counts(k, pc + nc, 0);
+        }
+        // processAndReturn in eventSequence order (later states first)
+        for (int u = 0; u < P->proc_count[s]; u++) {
+            const int k = P->proc_state[s][u];
+            if (k == 0) {
+                if (!(flags & 2ull)) continue;
+                for (int q = 0; q < n; q++) rows[q] = SHD_NULL_ROW;
+                rows[0] = row;
+                bool pass = true;
+                if (P->filter_pc[0] >= 0) {
+                    VmVal v = vm_eval(P, P->filter_pc[0], P->filter_len[0], rows, C);
+                    pass = !v.null && v.b;
+                }
+                if (!pass) continue;
+                flags &= ~2ull;                       // template leaves pending (stateChanged)
+                if (P->every_start) flags |= 4ull;    // addEveryState: fresh clone into new-and-every
+                if (n == 1) {
+                    emit_match(P, K, E, rows, C, i, nmatch++, t);
+                } else {
+                    uint32_t pc = K.pcount(1), nc = K.ncount(1);
+                    if (nc >= (uint32_t)L.cap) {
+                        atomicExch(&EM.err[0], 1);
+                        continue;
+                    }
+                    uint64_t* r = K.rec(K.list(1, 1), nc);
+                    r[0] = (uint64_t)t;   // StateEvent ts := matched event ts
+                    r[1] = (uint64_t)t;   // start-state event ts (within)
+                    uint32_t* rr = (uint32_t*)(r + 2);
+                    for (int q = 0; q < n; q++) rr[q] = rows[q];
+                    K.set_counts(1, pc, nc + 1);
+                }
+                continue;
+            }
+            uint32_t pc = K.pcount(k);
+            if (!pc) continue;
+            uint64_t* pl = K.list(k, 0);
+            uint32_t w = 0;
+            for (uint32_t q = 0; q < pc; q++) {
+                uint64_t* r = K.rec(pl, q);
+                uint32_t* rr = (uint32_t*)(r + 2);
+                for (int z = 0; z < n; z++) rows[z] = rr[z];
+                rows[k] = row;
+                bool pass = true;
+                if (P->filter_pc[k] >= 0) {
+                    VmVal v = vm_eval(P, P->filter_pc[k], P->filter_len[k], rows, C);
+                    pass = !v.null && v.b;
+                }
+                if (pass) {
+                    if (k == n - 1) {
+                        emit_match(P, K, E, rows, C, i, nmatch++, t);
+                    } else {
+                        uint32_t npc = K.pcount(k + 1), nnc = K.ncount(k + 1);
+                        if (nnc >= (uint32_t)L.cap) {
+                            atomicExch(&EM.err[0], 1);
+                        } else {
+                            uint64_t* d = K.rec(K.list(k + 1, 1), nnc);
+                            d[0] = (uint64_t)t;
+                            d[1] = r[1];
+                            uint32_t* dr = (uint32_t*)(d + 2);
+                            for (int z = 0; z < n; z++) dr[z] = rows[z];
+                            K.set_counts(k + 1, npc, nnc + 1);
+                        }
+                    }
+                } else {
+                    if (w != q) rec_copy(K.rec(pl, w), r, rw);
+                    w++;
+                }
+            }
+            K.set_counts(k, w, K.ncount(k));
+        }
+        if (nmatch) EM.match_cnt[i] = nmatch;
+    }
+    K.base[0] = flags;
+    for (int64_t q = E.used; q < E.cap; q++) E.chunk[q * E.rec_words] = ~0ull;  // unused tail
+}
+
+// ------------------------------------------------------------------ ordered placement
+__global__ void k_place(const uint64_t* __restrict__ tmp, int64_t nrec, int rec_words, int n_out,
+                        const uint32_t* __restrict__ offsets, uint64_t seq_base, uint64_t* __restrict__ out_seq,
+                        int64_t* __restrict__ out_ts, int64_t* __restrict__ out_vals, uint8_t* __restrict__ out_nulls) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    const uint64_t* rec = tmp + r * rec_words;
+    const uint64_t h = rec[0];
+    if (h == ~0ull) return;  // unused slot of a partially filled chunk
+    const uint32_t li = (uint32_t)h, ord = (uint32_t)(h >> 32);
+    const int64_t dst = (int64_t)offsets[li] + ord;
+    if (out_seq) out_seq[dst] = seq_base + li;
+    if (out_ts) out_ts[dst] = (int64_t)rec[1];
+    for (int o = 0; o < n_out; o++) {
+        if (out_vals) out_vals[dst * n_out + o] = (int64_t)rec[3 + o];
+        if (out_nulls) out_nulls[dst * n_out + o] = (uint8_t)((rec[2] >> o) & 1);
+    }
+}
+
+// ------------------------------------------------------------------ host entry points
+static uint32_t g_bits_for(uint32_t maxkey) {
+    uint32_t b = 0;
+    while (b < 32 && (maxkey >> b)) b++;
+    return b;
+}
+
+extern "C" int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
+                           const uint32_t** perm_out, const uint32_t** skeys_out) {
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t n = b->n;
+    const uint32_t sentinel = (uint32_t)nkeys;
+    const int64_t ntiles = ceil_div(n, RADIX_TILE);
+    const uint32_t bits = g_bits_for(sentinel);
+    const int passes = b->keys ? (int)((bits + 7) / 8) : 0;
+    const uint32_t* kin = nullptr;
+    const uint32_t* iin = nullptr;
+    uint32_t* kout = ws->keys_a;
+    uint32_t* iout = ws->idx_a;
+    for (int ps = 0; ps < passes; ps++) {
+        const int shift = ps * 8;
+        hipLaunchKernelGGL(k_digit_hist, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, b->keys, sentinel, n, shift,
+                           ws->hist, ntiles);
+        int rc = shd_exclusive_scan(ws->hist, ws->hist, 256 * ntiles, ws->scan_tmp, stream);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_digit_scatter, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, b->keys, sentinel, iin, n,
+                           shift, (const uint32_t*)ws->hist, ntiles, kout, iout);
+        kin = kout;
+        iin = iout;
+        kout = (kout == ws->keys_a) ? ws->keys_b : ws->keys_a;
+        iout = (iout == ws->idx_a) ? ws->idx_b : ws->idx_a;
+    }
+    // kin/iin: sorted keys / permutation (NULL when nothing to sort: single key)
+    *perm_out = iin;
+    *skeys_out = kin;
+    uint32_t* flags = ws->seg_off;          // [n]
+    uint32_t* pos = ws->seg_off + n;        // [n]
+    uint32_t* seg_list = ws->seg_off + 2 * n;  // [n + 1]
+    const unsigned g = (unsigned)ceil_div(n, TPB);
+    hipLaunchKernelGGL(k_seg_flags, dim3(g), dim3(TPB), 0, st, kin, n, kin ? sentinel : 0xFFFFFFFFu, flags);
+    int rc = shd_exclusive_scan(flags, pos, n, ws->scan_tmp, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_seg_compact, dim3(g), dim3(TPB), 0, st, (const uint32_t*)flags, (const uint32_t*)pos, n,
+                       seg_list, seg_list + n);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int shd_advance(const shp_program* dprog, const shp_layout* lay, uint8_t* kstate, int32_t nkeys,
+                           const shd_batch* b, const uint32_t* perm, const uint32_t* skeys, const uint32_t* seg_off,
+                           const shd_cols* dcols, const shd_emit* em, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t n = b->n;
+    const uint32_t* seg_list = seg_off + 2 * n;
+    const uint32_t* nseg = seg_list + n;
+    // the segment count is only known on device: size the grid for the worst
+    // case (every key present), lanes past *nseg exit at once
+    int64_t maxseg = n < (int64_t)nkeys ? n : (int64_t)nkeys;
+    if (maxseg < 1) maxseg = 1;
+    const unsigned g = (unsigned)ceil_div(maxseg, TPB);
+    hipLaunchKernelGGL(k_advance, dim3(g), dim3(TPB), 0, st, dprog, *lay, kstate, *b, perm, skeys, seg_list, nseg,
+                       dcols, *em, nkeys);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int shd_emit_place(const shd_emit* em, int32_t n_out, int64_t n_events, uint32_t* offsets,
+                              uint32_t* scan_tmp, int64_t n_records, const shd_batch* b, uint64_t* out_seq,
+                              int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n_events > 0) {  // offsets of each event's matches in the ordered output
+        int rc = shd_exclusive_scan(em->match_cnt, offsets, n_events, scan_tmp, stream);
+        if (rc) return rc;
+    }
+    const bool any_out = out_seq || out_ts || out_vals || out_nulls;
+    if (n_records > 0 && any_out) {
+        hipLaunchKernelGGL(k_place, dim3((unsigned)ceil_div(n_records, TPB)), dim3(TPB), 0, st,
+                           (const uint64_t*)em->tmp, n_records, 3 + n_out, n_out, (const uint32_t*)offsets,
+                           b->seq_base, out_seq, out_ts, out_vals, out_nulls);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}

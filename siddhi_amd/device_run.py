@@ -1,0 +1,53 @@
+"""Device-resident bulk path (sh_run_device) driven with torch-allocated HBM
+buffers. torch is plumbing here (allocation, streams); the matcher runs in
+libsiddhi_hip.so."""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import abi
+from ._native import CompiledHandle, check, lib
+
+
+class DeviceRunner:
+    def __init__(self, compiled, device="cuda:0"):
+        self.compiled = compiled
+        self.device = torch.device(device)
+        self.handle = CompiledHandle(compiled)
+        self.n_out = max(1, len(compiled.queries[0].outs))
+        self._out_cap = 0
+
+    def run(self, ts, keys, cols, n_keys, out_capacity=None, stream=None):
+        """ts/keys/cols: device tensors (int64 / int32 / stream attribute order).
+        Returns (n_matches, out_seq[n], out_values[n, n_out]) as device tensors."""
+        n = ts.numel()
+        cap = out_capacity or n
+        if self._out_cap < cap:
+            self.out_seq = torch.empty(cap, dtype=torch.int64, device=self.device)
+            self.out_vals = torch.empty(cap * self.n_out, dtype=torch.int64, device=self.device)
+            self._out_cap = cap
+        cp = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
+        r = abi.sh_device_run()
+        r.n = n
+        r.d_ts = ts.data_ptr()
+        r.d_keys = keys.data_ptr()
+        r.n_keys = int(n_keys)
+        r.d_cols = cp
+        r.out_capacity = self._out_cap
+        r.d_out_seq = self.out_seq.data_ptr()
+        r.d_out_values = self.out_vals.data_ptr()
+        r.stream = stream.cuda_stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        rc = lib().sh_run_device(self.handle.h, C.byref(r))
+        check(self.handle.h, rc)
+        m = int(r.out_count)
+        return m, self.out_seq[:m], self.out_vals[: m * self.n_out].view(m, self.n_out)
+
+    def kernel_times(self):
+        t = abi.sh_kernel_times()
+        lib().sh_last_kernel_times(self.handle.h, C.byref(t))
+        return dict(segment_ms=t.segment_ms, advance_ms=t.advance_ms, emit_ms=t.emit_ms, total_ms=t.total_ms)
+
+    def close(self):
+        self.handle.close()

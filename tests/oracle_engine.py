@@ -98,3 +98,21 @@ class OracleEngine:
             self.close()
         except Exception:
             pass
+
+
+def run_stock_oracle(compiled, ts, keys, price, vol, batch=4096, partitioned=True):
+    """Drive the oracle with send(Event[]) calls of `batch` events over the
+    StockStream columns; returns (seq, ts, values[n, n_out], nulls) of all matches."""
+    eng = OracleEngine(compiled)
+    eng.start()
+    n = len(ts)
+    sym = keys.astype(np.int32)
+    for b0 in range(0, n, batch):
+        b1 = min(n, b0 + batch)
+        cols = [np.ascontiguousarray(sym[b0:b1]), np.ascontiguousarray(price[b0:b1]),
+                np.ascontiguousarray(vol[b0:b1])]
+        eng.send(0, np.ascontiguousarray(ts[b0:b1]), cols, [None, None, None],
+                 np.ascontiguousarray(sym[b0:b1]) if partitioned else None, b0)
+    out = eng.drain()
+    eng.close()
+    return out["seq"], out["ts"], out["values"], out["nulls"]

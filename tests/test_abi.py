@@ -1,0 +1,71 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol
+include/siddhi_hip.h declares, lowers supported apps and refuses the rest."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from siddhi_amd import abi, build, compiler, synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    path = build.build()
+    return abi.bind_product(C.CDLL(path))
+
+
+def test_header_declares_exactly_the_exported_symbols(lib):
+    hdr = open(os.path.join(ROOT, "include", "siddhi_hip.h")).read()
+    declared = set(re.findall(r"\b(sh_[a-z_]+)\s*\(", hdr))
+    assert declared == set(abi.EXPORTED)
+    out = subprocess.run(["nm", "-D", "--defined-only", build.OUT], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (sh_[a-z_]+)", out))
+    assert declared <= exported
+
+
+def _compile(lib, text):
+    ca = compiler.compile_app(text)
+    d = ca.descriptor()
+    h = C.c_void_p()
+    rc = lib.sh_compile(C.byref(d), C.byref(h))
+    return rc, h, ca
+
+
+def test_c2_query_lowers(lib):
+    rc, h, _ = _compile(lib, synth.C2_QUERY)
+    assert rc == abi.SH_OK, lib.sh_last_error(h)
+    lib.sh_destroy(h)
+
+
+@pytest.mark.parametrize("text", [
+    "define stream S (a int); from every e1=S, e2=S[a>e1.a]+, e3=S select e1.a as a insert into O;",
+    "define stream S (a int); define stream T (a int); from e1=S and e2=T -> e3=S select e3.a as a insert into O;",
+])
+def test_unlowered_shapes_are_refused(lib, text):
+    rc, h, _ = _compile(lib, text)
+    assert rc == abi.SH_E_UNSUPPORTED
+    assert lib.sh_last_error(h)
+    lib.sh_destroy(h)
+
+
+def test_no_cpu_fallback_without_device(lib):
+    if lib.sh_device_count() > 0:
+        pytest.skip("a GPU is present")
+    rc, h, _ = _compile(lib, synth.C2_QUERY)
+    assert rc == abi.SH_OK
+    import numpy as np
+    ts = np.zeros(1, np.int64)
+    cols = [np.zeros(1, np.int32), np.zeros(1, np.float32), np.zeros(1, np.int64)]
+    cp = (C.c_void_p * 3)(*[c.ctypes.data for c in cols])
+    keys = np.zeros(1, np.int32)
+    b = abi.sh_batch(stream=0, on_device=0, n=1, ts=ts.ctypes.data, keys=keys.ctypes.data, cols=cp, nulls=None)
+    assert lib.sh_push_batch(h, C.byref(b)) == abi.SH_E_NO_DEVICE
+    lib.sh_destroy(h)
+
+
+def test_version_string(lib):
+    assert b"gfx950" in lib.sh_version()

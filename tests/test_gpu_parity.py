@@ -1,0 +1,193 @@
+"""GPU parity: libsiddhi_hip.so (through the C-ABI) vs the reference's fixtures,
+the CPU oracle, and the vectorised C2 restatement. Bit-exact: same events,
+same order, same selected attributes (raw 8-byte values)."""
+import random
+
+import numpy as np
+import pytest
+
+from c2_check import c2_expected
+from fixture_runner import Unsupported, check_fixture, load_fixtures, run_fixture
+from oracle_engine import OracleEngine, run_stock_oracle
+from siddhi_amd import SiddhiManager, compiler, synth
+
+pytestmark = pytest.mark.gpu
+
+FIXTURES = load_fixtures()
+
+
+def hip_factory(compiled):
+    from siddhi_amd._native import HipEngine, HipError
+    try:
+        return HipEngine(compiled)
+    except HipError as e:
+        if e.code == -4:
+            raise Unsupported(str(e))
+        raise
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from siddhi_amd._native import lib
+    assert lib().sh_device_count() > 0
+
+
+def _rows(evs):
+    return [(e.timestamp, e.data) for e in evs]
+
+
+@pytest.mark.parametrize("fx", FIXTURES, ids=[f["id"] for f in FIXTURES])
+def test_fixture_on_gpu(fx):
+    try:
+        got = run_fixture(fx, hip_factory)
+    except Unsupported as e:
+        pytest.skip(f"not lowered to the device engine: {e}")
+    errs = check_fixture(fx, got)
+    assert not errs, f"{fx['source']}: {errs}"
+    ref = run_fixture(fx, OracleEngine)
+    assert _rows(got) == _rows(ref)
+
+
+def _run_engine(factory, app, sends):
+    mgr = SiddhiManager(engine_factory=factory)
+    rt = mgr.createSiddhiAppRuntime(app)
+    got = []
+    rt.addCallback("query1", lambda ts, i, r: got.extend(i or []))
+    rt.start()
+    hs = {}
+    for stream, batch in sends:
+        h = hs.setdefault(stream, rt.getInputHandler(stream))
+        h.send_batch([t for t, _ in batch], [d for _, d in batch])
+    rt.shutdown()
+    return [(e.timestamp, e.data) for e in got]
+
+
+def _random_case(rng):
+    n_states = rng.randint(2, 4)
+    streams = ["S1", "S2"]
+    pick = [rng.choice(streams) if rng.random() < 0.5 else "S1" for _ in range(n_states)]
+    filters = []
+    for k in range(n_states):
+        opts = ["price > {c}f", "x < {c}", "price >= 10.5", "not (x == {c})", "volume % 3 != 1"]
+        if k > 0:
+            e = f"e{rng.randrange(k)}"
+            opts += [f"price > {e}.price", f"x < {e}.x + {{c}}", f"sym == {e}.sym and price > {e}.price",
+                     f"price * 2 > {e}.price + x", f"(x / 2) >= {e}.x or price < {e}.price",
+                     f"volume > {e}.volume", f"{e}.price - price < {{c}}.0"]
+        f = rng.choice(opts).format(c=rng.randint(1, 20))
+        if rng.random() < 0.2:
+            f = f"{f} and {rng.choice(['x > 2', 'price < 19.0f', 'sym != sym'])}"
+        filters.append(f if rng.random() < 0.9 else None)
+    parts = []
+    for k in range(n_states):
+        src = f"e{k}={pick[k]}" + (f"[{filters[k]}]" if filters[k] else "")
+        if k == 0 and rng.random() < 0.6:
+            src = "every " + src
+        parts.append(src)
+    within = rng.choice([None, None, 3, 8, 20])
+    pattern = " -> ".join(parts) + (f" within {within} milliseconds" if within else "")
+    sel = [f"e0.sym as a", f"e{n_states - 1}.price as b", f"e{rng.randrange(n_states)}.x as c"]
+    if rng.random() < 0.3:
+        sel.append(f"sum(e{n_states - 1}.price) as d")
+    if rng.random() < 0.2:
+        sel.append(f"avg(e0.x) as e")
+    partitioned = rng.random() < 0.5
+    defs = ("define stream S1 (sym string, price float, volume long, x int); "
+            "define stream S2 (sym string, price float, volume long, x int); ")
+    q = f"@info(name = 'query1') from {pattern} select {', '.join(sel)} insert into Out;"
+    used = sorted(set(pick))
+    if partitioned:
+        app = defs + "partition with (" + ", ".join(f"sym of {s}" for s in used) + ") begin " + q + " end;"
+    else:
+        app = defs + q
+    syms = [f"K{i}" for i in range(rng.choice([1, 3, 7]))]
+    t = 1000
+    sends = []
+    n_ev = rng.randint(50, 600)
+    i = 0
+    while i < n_ev:
+        s = rng.choice(used)
+        b = []
+        for _ in range(rng.randint(1, 40)):
+            t += rng.choice([0, 0, 1, 1, 2, 5])
+            b.append((t, [rng.choice(syms), float(rng.randint(0, 40)) + rng.choice([0.0, 0.5, 0.25]),
+                          rng.randint(0, 9), rng.randint(-3, 25)]))
+            i += 1
+        sends.append((s, b))
+    return app, sends
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_random_chain_patterns_vs_oracle(seed):
+    rng = random.Random(1000 + seed)
+    app, sends = _random_case(rng)
+    ref = _run_engine(OracleEngine, app, sends)
+    got = _run_engine(hip_factory, app, sends)
+    assert len(got) == len(ref), app
+    for g, r in zip(got, ref):
+        assert g[0] == r[0]
+        for a, b in zip(g[1], r[1]):
+            assert (a == b) or (a != a and b != b), (app, g, r)
+
+
+def test_c2_push_api_vs_oracle():
+    n, keys = 120_000, 500
+    ts, k, p, v = synth.stock_stream(n, keys, 100)
+    ca = compiler.compile_app(synth.C2_QUERY)
+    seq, ots, vals, _ = run_stock_oracle(ca, ts, k, p, v)
+    from siddhi_amd._native import HipEngine
+    eng = HipEngine(compiler.compile_app(synth.C2_QUERY))
+    parts = []
+    for b0 in range(0, n, 4096):
+        b1 = min(n, b0 + 4096)
+        eng.send(0, ts[b0:b1], [k[b0:b1].copy(), p[b0:b1].copy(), v[b0:b1].copy()], [None] * 3,
+                 k[b0:b1].copy(), b0)
+        if (b0 // 4096) % 7 == 3:   # drain at uneven points: state must carry across flushes
+            parts.append(eng.drain())
+    parts.append(eng.drain())
+    eng.close()
+    gseq = np.concatenate([x["seq"] for x in parts])
+    gts = np.concatenate([x["ts"] for x in parts])
+    gvals = np.concatenate([x["values"] for x in parts])
+    assert len(gseq) == len(seq) > 0
+    assert np.array_equal(gseq, seq)
+    assert np.array_equal(gts, ots)
+    assert np.array_equal(gvals, vals)
+
+
+def _run_device_c2(n, keys, rate=100):
+    import torch
+    from siddhi_amd.device_run import DeviceRunner
+    ts, k, p, v = synth.stock_stream(n, keys, rate)
+    runner = DeviceRunner(compiler.compile_app(synth.C2_QUERY))
+    dev = torch.device("cuda:0")
+    tts = torch.from_numpy(ts).to(dev)
+    tk = torch.from_numpy(k).to(dev)
+    tp = torch.from_numpy(p).to(dev)
+    tv = torch.from_numpy(v).to(dev)
+    m, oseq, ovals = runner.run(tts, tk, [tk, tp, tv], keys)
+    torch.cuda.synchronize()
+    res = (m, oseq.cpu().numpy(), ovals.cpu().numpy())
+    runner.close()
+    return (ts, k, p, v), res
+
+
+def test_c2_device_run_vs_oracle():
+    (ts, k, p, v), (m, oseq, ovals) = _run_device_c2(400_000, 2_000)
+    ca = compiler.compile_app(synth.C2_QUERY)
+    seq, ots, vals, _ = run_stock_oracle(ca, ts, k, p, v)
+    assert m == len(seq) > 0
+    assert np.array_equal(oseq, seq.astype(np.int64))
+    assert np.array_equal(ovals, vals)
+
+
+@pytest.mark.parametrize("n,keys", [(10_000_000, 10_000), (100_000_000, 10_000)])
+def test_c2_full_size_vs_vectorised_restatement(n, keys):
+    (ts, k, p, v), (m, oseq, ovals) = _run_device_c2(n, keys)
+    eseq, evals = c2_expected(ts, k, p, v)
+    assert m == len(eseq) > 0
+    assert np.array_equal(oseq, eseq)
+    assert np.array_equal(ovals, evals)
