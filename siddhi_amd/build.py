@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libsiddhi_hip.so")
-SOURCES = ["sh_host.cpp", "sh_kernels.hip"]
+SOURCES = ["sh_host.cpp", "sh_kernels.hip", "sh_window.hip"]
 # exact IEEE arithmetic like the JVM: no FMA contraction, no flush-to-zero,
 # correctly rounded f32 division
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950", "-ffp-contract=off",

@@ -48,6 +48,16 @@ struct shd_segment_ws {
     int64_t cap;
 };
 
+// scratch of the window engine (sh_window.hip)
+struct shd_window_ws {
+    int64_t* sts;            // [n] timestamps in key-segment order
+    void* scol[32];          // [n] per attribute, key-segment order
+    int32_t* match_pos;      // [n] consuming position of the partial opened at p, -1 none
+    uint32_t* cnt;           // [n] matches per event (arrival index)
+    uint32_t* off;           // [n] exclusive scan of cnt
+    int32_t* flag;           // [1] non-monotone timestamps seen
+};
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -63,6 +73,15 @@ int shd_advance(const shp_program* dprog, const shp_layout* lay, uint8_t* kstate
 int shd_emit_place(const shd_emit* em, int32_t n_out, int64_t n_events, uint32_t* offsets,
                    uint32_t* scan_tmp, int64_t n_records, const shd_batch* b, uint64_t* out_seq,
                    int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, void* stream);
+// window engine for `every e1=S[f1] -> e2=S[f2] within W`: 0 ok, 1 = fall back
+// (timestamps decrease inside a key), 2 = output capacity too small, <0 error
+int shd_window(const shp_program* dprog, const shp_program* hprog, const shd_batch* b, int32_t nkeys,
+               const uint32_t* perm, const uint32_t* skeys, const void* const* cols, shd_window_ws* ws,
+               shd_cols* d_sorted_desc, uint32_t* scan_tmp, uint64_t* out_seq, int64_t* out_ts,
+               int64_t* out_vals, uint8_t* out_nulls, int64_t out_cap, int64_t* n_matches, void* stream,
+               void* ev_mid);
+int shd_relayout(const uint8_t* src, const shp_layout* A, uint8_t* dst, const shp_layout* B, int32_t nkeys,
+                 int32_t n_states, int32_t n_out, void* stream);
 int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, void* stream);
 #ifdef __cplusplus
 }

@@ -234,6 +234,8 @@ struct sh_handle {
     // workspaces
     DevBuf w_ts, w_stream, w_row, w_key, w_keys_a, w_keys_b, w_idx_a, w_idx_b, w_hist, w_scan, w_seg;
     DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls;
+    DevBuf v_sts, v_mpos, v_flag;
+    DevBuf v_scol[32];
     int64_t tmp_cap = 0;
     // drained output queue (host)
     std::vector<int32_t> o_query;
@@ -245,6 +247,16 @@ struct sh_handle {
     sh_kernel_times times{};
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
+
+static void set_layout(shp_layout& Y, const shp_program& P, int32_t cap) {
+    Y.cap = cap;
+    Y.rec_words = 2 + (P.n_states + 1) / 2;
+    Y.list_bytes = (int64_t)Y.cap * Y.rec_words * 8;
+    Y.off_lists = (int64_t)(1 + SHP_MAX_STATES) * 8;
+    Y.off_agg = Y.off_lists + (int64_t)(P.n_states > 1 ? P.n_states - 1 : 0) * 2 * Y.list_bytes;
+    Y.key_bytes = Y.off_agg + (int64_t)P.n_out * 5 * 8;
+    Y.key_bytes = (Y.key_bytes + 63) & ~63ll;
+}
 
 static int fail(sh_handle* h, int code, const std::string& m) {
     if (h) h->err = m;
@@ -341,6 +353,17 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
             P.out_len[o] = 0;
         }
     }
+    // the data-parallel window engine (sh_window.hip) covers
+    // `every e1=S[f1] -> e2=S[f2] within W` without aggregators
+    {
+        bool agg = false;
+        for (int o = 0; o < P.n_out; o++) agg |= P.out_agg[o] != SH_AGG_NONE;
+        P.window_ok = (P.n_states == 2 && P.every_start && P.within_ms >= 0 && !agg &&
+                       P.state_stream[0] == P.state_stream[1] && app->n_streams == 1)
+                          ? 1
+                          : 0;
+        if (getenv("SH_DISABLE_WINDOW")) P.window_ok = 0;
+    }
     h->prog = P;
     h->n_out = P.n_out;
     h->partitioned = q.partition >= 0;
@@ -352,15 +375,8 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
         }
     }
     // per-key state layout
-    shp_layout& Y = h->lay;
     const char* capenv = getenv("SH_PARTIAL_CAP");
-    Y.cap = capenv ? atoi(capenv) : 64;
-    Y.rec_words = 2 + (P.n_states + 1) / 2;
-    Y.list_bytes = (int64_t)Y.cap * Y.rec_words * 8;
-    Y.off_lists = (int64_t)(1 + SHP_MAX_STATES) * 8;
-    Y.off_agg = Y.off_lists + (int64_t)(P.n_states > 1 ? P.n_states - 1 : 0) * 2 * Y.list_bytes;
-    Y.key_bytes = Y.off_agg + (int64_t)P.n_out * 5 * 8;
-    Y.key_bytes = (Y.key_bytes + 63) & ~63ll;
+    set_layout(h->lay, P, capenv ? atoi(capenv) : 32);
 
     h->has_device = device_available();
     if (!h->has_device) return SH_OK;  // compile is host-only; processing needs a device
@@ -383,6 +399,10 @@ void sh_destroy(sh_handle* h) {
     if (!h) return;
     if (h->has_device) {
         hipStreamSynchronize(h->stream);
+        h->v_sts.release();
+        h->v_mpos.release();
+        h->v_flag.release();
+        for (auto& b : h->v_scol) b.release();
         DevBuf* bufs[] = {&h->d_prog, &h->d_cols_desc, &h->d_kstate, &h->d_err, &h->w_ts, &h->w_stream, &h->w_row,
                           &h->w_key, &h->w_keys_a, &h->w_keys_b, &h->w_idx_a, &h->w_idx_b, &h->w_hist, &h->w_scan,
                           &h->w_seg, &h->w_cnt, &h->w_off, &h->w_tmp, &h->w_ctr, &h->w_oseq, &h->w_ots,
@@ -490,8 +510,8 @@ static int run_batch(sh_handle* h, const shd_batch& B, int32_t nkeys, const shd_
     }
     // keep a copy of the key state: an emit-buffer overflow restores and reruns
     DevBuf backup;
-    const size_t kbytes = (size_t)nkeys * h->lay.key_bytes;
-    for (int attempt = 0; attempt < 8; attempt++) {
+    for (int attempt = 0; attempt < 24; attempt++) {
+        const size_t kbytes = (size_t)nkeys * h->lay.key_bytes;
         if (attempt == 0 && !timed) {
             if (backup.ensure_fresh(kbytes)) return fail(h, SH_E_OOM, "state backup");
             hipMemcpyAsync(backup.p, h->d_kstate.p, kbytes, hipMemcpyDeviceToDevice, st);
@@ -530,7 +550,34 @@ static int run_batch(sh_handle* h, const shd_batch& B, int32_t nkeys, const shd_
         hipMemcpyAsync(&nrec, h->w_ctr.p, 8, hipMemcpyDeviceToHost, st);
         if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in advance");
         if (herr[0] == 2) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
-        if (herr[0]) return fail(h, SH_E_STATE_OVERFLOW, "partial-match list overflow (raise SH_PARTIAL_CAP)");
+        if (herr[0]) {
+            // a partial-match list outgrew its capacity: grow every key's lists x4
+            // (the reference's lists are unbounded LinkedLists) and rerun the batch
+            if (h->lay.cap >= (1 << 20)) return fail(h, SH_E_STATE_OVERFLOW, "partial-match list overflow");
+            shp_layout old = h->lay, nl;
+            set_layout(nl, h->prog, old.cap * 4);
+            DevBuf fresh;
+            if (fresh.ensure_fresh((size_t)h->nkeys_alloc * nl.key_bytes)) return fail(h, SH_E_OOM, "state growth");
+            if (timed) {
+                hipMemsetAsync(fresh.p, 0, (size_t)h->nkeys_alloc * nl.key_bytes, st);
+            } else {
+                hipMemcpyAsync(h->d_kstate.p, backup.p, kbytes, hipMemcpyDeviceToDevice, st);
+                shd_relayout(h->d_kstate.as<uint8_t>(), &old, fresh.as<uint8_t>(), &nl, h->nkeys_alloc,
+                             h->prog.n_states, h->n_out, st);
+            }
+            hipStreamSynchronize(st);
+            h->d_kstate.release();
+            h->d_kstate = fresh;
+            fresh.p = nullptr;
+            fresh.bytes = 0;
+            h->lay = nl;
+            if (!timed) {
+                const size_t nkb = (size_t)nkeys * h->lay.key_bytes;
+                if (backup.ensure_fresh(nkb)) return fail(h, SH_E_OOM, "state backup");
+                hipMemcpyAsync(backup.p, h->d_kstate.p, nkb, hipMemcpyDeviceToDevice, st);
+            }
+            continue;
+        }
         if (herr[1]) {
             // emit buffer too small: restore state, grow, rerun
             if (timed) {
@@ -735,6 +782,56 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
     for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = run->d_cols[a];
     int64_t nm = 0;
     h->times = sh_kernel_times{};
+    if (h->prog.window_ok) {
+        const int64_t n = run->n;
+        hipStream_t st = h->stream;
+        if (ensure_ws(h, n)) return fail(h, SH_E_OOM, "workspace");
+        shd_window_ws wws;
+        memset(&wws, 0, sizeof(wws));
+        if (h->v_sts.ensure_fresh(n * 8) || h->v_mpos.ensure_fresh(n * 4) || h->v_flag.ensure_fresh(64))
+            return fail(h, SH_E_OOM, "window workspace");
+        for (size_t a = 0; a < h->stream_types[0].size(); a++) {
+            if (h->v_scol[a].ensure_fresh(n * type_width(h->stream_types[0][a])))
+                return fail(h, SH_E_OOM, "window workspace");
+            wws.scol[a] = h->v_scol[a].p;
+        }
+        wws.sts = h->v_sts.as<int64_t>();
+        wws.match_pos = h->v_mpos.as<int32_t>();
+        wws.cnt = h->w_cnt.as<uint32_t>();
+        wws.off = h->w_off.as<uint32_t>();
+        wws.flag = h->v_flag.as<int32_t>();
+        hipEventRecord(h->ev[0], st);
+        shd_segment_ws ws;
+        ws.keys_a = h->w_keys_a.as<uint32_t>();
+        ws.keys_b = h->w_keys_b.as<uint32_t>();
+        ws.idx_a = h->w_idx_a.as<uint32_t>();
+        ws.idx_b = h->w_idx_b.as<uint32_t>();
+        ws.hist = h->w_hist.as<uint32_t>();
+        ws.scan_tmp = h->w_scan.as<uint32_t>();
+        ws.seg_off = h->w_seg.as<uint32_t>();
+        ws.cap = n;
+        const uint32_t* perm = nullptr;
+        const uint32_t* skeys = nullptr;
+        if (shd_segment(&B, nkeys, &ws, st, &perm, &skeys)) return fail(h, SH_E_HIP, "segment launch failed");
+        hipEventRecord(h->ev[1], st);
+        int wrc = shd_window(h->d_prog.as<shp_program>(), &h->prog, &B, nkeys, perm, skeys, run->d_cols, &wws,
+                             h->d_cols_desc.as<shd_cols>(), h->w_scan.as<uint32_t>(), run->d_out_seq, nullptr,
+                             run->d_out_values, nullptr, run->out_capacity, &nm, st, h->ev[2]);
+        hipEventRecord(h->ev[3], st);
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in window engine");
+        if (wrc < 0) return fail(h, SH_E_HIP, "window engine launch failed");
+        run->out_count = nm;
+        if (wrc == 2) return fail(h, SH_E_MORE, "output capacity too small");
+        if (wrc == 0) {
+            hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
+            hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
+            hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
+            hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
+            h->times.advance_launches = 1;
+            return SH_OK;
+        }
+        // wrc == 1: timestamps decrease inside a key -> sequential per-key engine
+    }
     int rc = run_batch(h, B, nkeys, cols, run->d_out_seq, nullptr, run->d_out_values, nullptr, run->out_capacity,
                        &nm, true);
     run->out_count = nm;

@@ -44,6 +44,7 @@ struct shp_instr {
 struct shp_program {
     int32_t n_states;                 // chain length
     int32_t every_start;              // `every` wraps exactly the start state
+    int32_t window_ok;                // shape runs on the window engine (sh_window.hip)
     int64_t within_ms;                // -1: none
     int32_t n_streams;
     int32_t n_out;

@@ -1,0 +1,185 @@
+// sh_window.hip — the data-parallel "window" engine for two-state patterns
+//     every e1=S[f1] -> e2=S[f2(e1, e2)] within W      (configs C1, C2, C5 rules)
+//
+// For this shape the per-key NFA of StreamPreStateProcessor reduces to: every
+// event i of a key with f1(i) opens one partial (the start template is always
+// re-armed by `every`, StreamPostStateProcessor.java:77-79); the partial becomes
+// pending at the key's next event (updateState, :307-323) and is consumed by the
+// first later event j of the key with f2(i, j), unless an event k <= j of the key
+// expired it first (|ts_i - ts_k| > W, expireEvents :325-361). With non-decreasing
+// timestamps per key the pending list is in creation (= ts) order, so the
+// break-early expiry scan removes exactly the over-age partials, and matches at j
+// leave in pending (= creation) order. The host checks non-decreasing timestamps
+// on the device first (k_ts_check) and falls back to the sequential per-key
+// engine (sh_kernels.hip) when they are not.
+//
+// Every candidate is then independent: one lane per event scans forward in its
+// key segment (stable radix segment output) — massively parallel and coalesced.
+#include <hip/hip_runtime.h>
+
+#include "../../include/sh_query.h"
+#include "sh_device.h"
+#include "sh_vm.h"
+
+#include <string.h>
+
+#define WTPB 256
+
+static int64_t wceil(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+__global__ void k_ts_check(const int64_t* __restrict__ ts, const uint32_t* __restrict__ perm,
+                           const uint32_t* __restrict__ skeys, int64_t n, uint32_t sentinel, int32_t* __restrict__ flag) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t k = skeys ? skeys[p] : 0u;
+        if (k == sentinel || (skeys && skeys[p - 1] != k)) continue;
+        const int64_t a = ts[perm ? perm[p - 1] : p - 1], b = ts[perm ? perm[p] : p];
+        if (b < a) atomicExch(flag, 1);
+    }
+}
+
+// gather a column into key-segment order
+template <typename T>
+__global__ void k_permute(const T* __restrict__ src, const uint32_t* __restrict__ perm, int64_t n, T* __restrict__ dst) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x)
+        dst[p] = src[perm[p]];
+}
+
+// one lane per event: candidate test + forward scan for the consuming event
+__global__ void __launch_bounds__(WTPB) k_window(const shp_program* __restrict__ P, const int64_t* __restrict__ sts,
+                                                 const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ perm,
+                                                 int64_t n, uint32_t sentinel, const shd_cols* __restrict__ C,
+                                                 int32_t* __restrict__ match_pos, uint32_t* __restrict__ cnt) {
+    const int64_t within = P->within_ms;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t key = skeys ? skeys[p] : 0u;
+        if (key == sentinel) continue;
+        uint32_t rows[2];
+        rows[0] = (uint32_t)p;
+        rows[1] = SHD_NULL_ROW;
+        if (P->filter_pc[0] >= 0) {
+            VmVal v = vm_eval(P, P->filter_pc[0], P->filter_len[0], rows, C);
+            if (v.null || !v.b) continue;
+        }
+        const int64_t t0 = sts[p];
+        for (int64_t q = p + 1; q < n; q++) {
+            if (skeys && skeys[q] != key) break;
+            const int64_t d = sts[q] - t0;
+            if ((d < 0 ? -d : d) > within) break;  // expired before event q is matched
+            rows[1] = (uint32_t)q;
+            bool pass = true;
+            if (P->filter_pc[1] >= 0) {
+                VmVal v = vm_eval(P, P->filter_pc[1], P->filter_len[1], rows, C);
+                pass = !v.null && v.b;
+            }
+            if (pass) {
+                match_pos[p] = (int32_t)q;
+                atomicAdd(&cnt[perm ? perm[q] : (uint32_t)q], 1u);
+                break;
+            }
+        }
+    }
+}
+
+// rank of partial p among the partials consumed by the same event (creation
+// order), then the ordered write of the selected attributes
+__global__ void __launch_bounds__(WTPB) k_window_place(const shp_program* __restrict__ P, const int64_t* __restrict__ sts,
+                                                       const uint32_t* __restrict__ skeys,
+                                                       const uint32_t* __restrict__ perm, int64_t n,
+                                                       const shd_cols* __restrict__ C,
+                                                       const int32_t* __restrict__ match_pos,
+                                                       const uint32_t* __restrict__ off, uint64_t seq_base,
+                                                       uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_ts,
+                                                       int64_t* __restrict__ out_vals, uint8_t* __restrict__ out_nulls) {
+    const int64_t within = P->within_ms;
+    const int n_out = P->n_out;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t q = match_pos[p];
+        if (q < 0) continue;
+        const uint32_t key = skeys ? skeys[p] : 0u;
+        const int64_t tq = sts[q];
+        uint32_t rank = 0;
+        for (int64_t r = p - 1; r >= 0; r--) {
+            if (skeys && skeys[r] != key) break;
+            if (tq - sts[r] > within) break;  // older partials expired before q
+            if (match_pos[r] == q) rank++;
+        }
+        const uint32_t j = perm ? perm[q] : (uint32_t)q;
+        const int64_t dst = (int64_t)off[j] + rank;
+        if (out_seq) out_seq[dst] = seq_base + j;
+        if (out_ts) out_ts[dst] = tq;
+        uint32_t rows[2] = {(uint32_t)p, (uint32_t)q};
+        for (int o = 0; o < n_out; o++) {
+            VmVal v = vm_eval(P, P->out_pc[o], P->out_len[o], rows, C);
+            if (out_vals) out_vals[dst * n_out + o] = v.b;
+            if (out_nulls) out_nulls[dst * n_out + o] = v.null;
+        }
+    }
+}
+
+static unsigned grid_for(int64_t n) {
+    int64_t g = wceil(n, WTPB);
+    if (g > 65536 * 4) g = 65536 * 4;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+
+// Runs the window engine on a segmented single-stream batch. Returns 0, or 1 when
+// timestamps decrease inside a key (caller falls back), <0 on HIP errors.
+extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, const shd_batch* b, int32_t nkeys,
+                          const uint32_t* perm, const uint32_t* skeys, const void* const* cols,
+                          shd_window_ws* ws, shd_cols* d_sorted_desc, uint32_t* scan_tmp, uint64_t* out_seq,
+                          int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, int64_t out_cap,
+                          int64_t* n_matches, void* stream, void* ev_mid_) {
+    hipEvent_t ev_mid = (hipEvent_t)ev_mid_;
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t n = b->n;
+    const uint32_t sentinel = skeys ? (uint32_t)nkeys : 0xFFFFFFFFu;
+    const unsigned g = grid_for(n);
+    hipMemsetAsync(ws->flag, 0, 4, st);
+    hipLaunchKernelGGL(k_ts_check, dim3(g), dim3(WTPB), 0, st, b->ts, perm, skeys, n, sentinel, ws->flag);
+    int32_t hflag = 0;
+    hipMemcpyAsync(&hflag, ws->flag, 4, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return -3;
+    if (hflag) return 1;
+    // key-segment-ordered copies of ts and every column of the stream
+    shd_cols sc;
+    memset(&sc, 0, sizeof(sc));
+    const int64_t* sts = b->ts;
+    if (perm) {
+        hipLaunchKernelGGL(k_permute<int64_t>, dim3(g), dim3(WTPB), 0, st, b->ts, perm, n, ws->sts);
+        sts = ws->sts;
+        for (int a = 0; a < hprog->stream_nattr[0]; a++) {
+            const int t = hprog->attr_type[0][a];
+            void* dst = ws->scol[a];
+            if (t == SH_T_LONG || t == SH_T_DOUBLE)
+                hipLaunchKernelGGL(k_permute<int64_t>, dim3(g), dim3(WTPB), 0, st, (const int64_t*)cols[a], perm, n,
+                                   (int64_t*)dst);
+            else if (t == SH_T_BOOL)
+                hipLaunchKernelGGL(k_permute<uint8_t>, dim3(g), dim3(WTPB), 0, st, (const uint8_t*)cols[a], perm, n,
+                                   (uint8_t*)dst);
+            else
+                hipLaunchKernelGGL(k_permute<int32_t>, dim3(g), dim3(WTPB), 0, st, (const int32_t*)cols[a], perm, n,
+                                   (int32_t*)dst);
+            sc.col[0][a] = dst;
+        }
+    } else {
+        for (int a = 0; a < hprog->stream_nattr[0]; a++) sc.col[0][a] = cols[a];
+    }
+    hipMemcpyAsync(d_sorted_desc, &sc, sizeof(sc), hipMemcpyHostToDevice, st);
+    hipMemsetAsync(ws->match_pos, 0xFF, n * 4, st);
+    hipMemsetAsync(ws->cnt, 0, n * 4, st);
+    hipLaunchKernelGGL(k_window, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n, sentinel,
+                       (const shd_cols*)d_sorted_desc, ws->match_pos, ws->cnt);
+    if (ev_mid) hipEventRecord(ev_mid, st);
+    int rc = shd_exclusive_scan(ws->cnt, ws->off, n, scan_tmp, stream);
+    if (rc) return rc;
+    uint32_t lo = 0, lc = 0;
+    hipMemcpyAsync(&lo, ws->off + (n - 1), 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(&lc, ws->cnt + (n - 1), 4, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return -3;
+    *n_matches = (int64_t)lo + lc;
+    if (*n_matches > out_cap) return 2;
+    hipLaunchKernelGGL(k_window_place, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n,
+                       (const shd_cols*)d_sorted_desc, (const int32_t*)ws->match_pos, (const uint32_t*)ws->off,
+                       b->seq_base, out_seq, out_ts, out_vals, out_nulls);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
