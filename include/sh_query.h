@@ -166,6 +166,9 @@ typedef struct sh_app_desc {
        each batch (ValuePartitionExecutor: key = attr.toString()); a stream
        participates in partition p iff partition_streams[p*n_streams+s] != 0 */
     const uint8_t* partition_streams;
+    /* partition_attr[p*n_streams+s]: attribute index of stream s that keys
+       partition p (`partition with (attr of Stream)`), -1 if not keyed */
+    const int32_t* partition_attr;
 } sh_app_desc;
 
 #ifdef __cplusplus

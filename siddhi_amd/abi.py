@@ -49,7 +49,8 @@ class sh_app_desc(C.Structure):
     _fields_ = [("version", C.c_int32), ("n_streams", C.c_int32), ("n_queries", C.c_int32),
                 ("n_partitions", C.c_int32), ("playback", C.c_int32), ("pad", C.c_int32),
                 ("streams", C.POINTER(sh_stream_def)), ("queries", C.POINTER(sh_query_desc)),
-                ("partition_streams", C.POINTER(C.c_uint8))]
+                ("partition_streams", C.POINTER(C.c_uint8)),
+                ("partition_attr", C.POINTER(C.c_int32))]
 
 
 class sh_batch(C.Structure):

@@ -1058,10 +1058,12 @@ class CompiledApp:
         ns = len(app.stream_order)
         np_ = len(app.partitions)
         ps = (ctypes.c_uint8 * max(1, np_ * ns))()
+        pa = (ctypes.c_int32 * max(1, np_ * ns))()
         for p, spec in enumerate(app.partitions):
             for s, name in enumerate(app.stream_order):
                 ps[p * ns + s] = 1 if name in spec else 0
-        keep += [streams, qs, ps]
+                pa[p * ns + s] = app.streams[name].index(spec[name]) if name in spec else -1
+        keep += [streams, qs, ps, pa]
         d = abi.sh_app_desc()
         d.version = abi.SH_DESC_VERSION
         d.n_streams = ns
@@ -1071,6 +1073,7 @@ class CompiledApp:
         d.streams = streams
         d.queries = qs
         d.partition_streams = ps
+        d.partition_attr = pa
         self._keep = keep
         return d
 

@@ -69,7 +69,7 @@ int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* str
                 const uint32_t** perm_out, const uint32_t** skeys_out);
 int shd_advance(const shp_program* dprog, const shp_layout* lay, uint8_t* kstate, int32_t nkeys,
                 const shd_batch* b, const uint32_t* perm, const uint32_t* skeys,
-                const uint32_t* seg_off, const shd_cols* dcols, const shd_emit* em, void* stream);
+                const uint32_t* seg_off, const shd_cols* dcols, const shd_emit* em, void* stream, int fast_ok);
 int shd_emit_place(const shd_emit* em, int32_t n_out, int64_t n_events, uint32_t* offsets,
                    uint32_t* scan_tmp, int64_t n_records, const shd_batch* b, uint64_t* out_seq,
                    int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, void* stream);

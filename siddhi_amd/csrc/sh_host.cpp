@@ -175,6 +175,98 @@ struct Lowering {
         err = "unsupported expression operator";
         return false;
     }
+    // ---- register-only filters: conjunction of `attr op attr|const|attr(aop)const`
+    const sh_app_desc* app = nullptr;
+    static bool is_var(const sh_expr& x) {
+        return x.op == SH_OP_VAR && (x.chain == 0 || x.chain == SH_CHAIN_CURRENT);
+    }
+    void conjuncts(int e, std::vector<int>& out) {
+        const sh_expr& x = q->exprs[e];
+        if (x.op == SH_OP_AND) {
+            conjuncts(x.lhs, out);
+            conjuncts(x.rhs, out);
+        } else {
+            out.push_back(e);
+        }
+    }
+    // `a.k == b.k` on the attribute that keys the query's partition is always
+    // true inside one partition (same key <=> same toString() for these types)
+    bool partition_tautology(const sh_expr& c) {
+        if (c.op != SH_OP_EQ || q->partition < 0 || !app || !app->partition_attr) return false;
+        const sh_expr& l = q->exprs[c.lhs];
+        const sh_expr& r = q->exprs[c.rhs];
+        if (!is_var(l) || !is_var(r) || l.type != r.type) return false;
+        if (!(l.type == SH_T_STRING || l.type == SH_T_INT || l.type == SH_T_LONG || l.type == SH_T_BOOL)) return false;
+        const int ns = app->n_streams;
+        const int sl = P.state_stream[l.slot], sr = P.state_stream[r.slot];
+        return app->partition_attr[q->partition * ns + sl] == l.attr &&
+               app->partition_attr[q->partition * ns + sr] == r.attr;
+    }
+    static int mirror(int op) {
+        switch (op) {
+            case SH_OP_GT: return SH_OP_LT;
+            case SH_OP_GE: return SH_OP_LE;
+            case SH_OP_LT: return SH_OP_GT;
+            case SH_OP_LE: return SH_OP_GE;
+            default: return op;
+        }
+    }
+    bool fast_filter(int root, int k) {
+        std::vector<int> cs;
+        conjuncts(root, cs);
+        int nt = 0;
+        for (int e : cs) {
+            const sh_expr& c = q->exprs[e];
+            if (c.op < SH_OP_EQ || c.op > SH_OP_LE) return false;
+            if (partition_tautology(c)) continue;
+            if (nt >= SHP_MAX_TERMS) return false;
+            int li = c.lhs, ri = c.rhs, op = c.op;
+            if (!is_var(q->exprs[li])) {
+                std::swap(li, ri);
+                op = mirror(op);
+            }
+            const sh_expr& l = q->exprs[li];
+            const sh_expr& r = q->exprs[ri];
+            if (!is_var(l)) return false;
+            shp_term t;
+            memset(&t, 0, sizeof(t));
+            t.op = (uint8_t)op;
+            t.dom = (uint8_t)dom_for(op, l.type, r.type);
+            t.lslot = (uint8_t)l.slot;
+            t.lattr = (uint8_t)l.attr;
+            t.ltype = (uint8_t)l.type;
+            if (is_var(r)) {
+                t.rkind = 0;
+                t.rslot = (uint8_t)r.slot;
+                t.rattr = (uint8_t)r.attr;
+                t.rtype = (uint8_t)r.type;
+            } else if (r.op == SH_OP_CONST) {
+                if (r.is_null) return false;
+                t.rkind = 1;
+                t.ctype = (uint8_t)r.type;
+                t.c = r.cval;
+            } else if (r.op == SH_OP_ADD || r.op == SH_OP_SUB || r.op == SH_OP_MUL) {
+                const sh_expr& a = q->exprs[r.lhs];
+                const sh_expr& b = q->exprs[r.rhs];
+                if (!is_var(a) || b.op != SH_OP_CONST || b.is_null) return false;
+                t.rkind = 2;
+                t.rslot = (uint8_t)a.slot;
+                t.rattr = (uint8_t)a.attr;
+                t.rtype = (uint8_t)a.type;
+                t.aop = (uint8_t)r.op;
+                t.atype = (uint8_t)r.type;
+                t.ctype = (uint8_t)b.type;
+                t.c = b.cval;
+            } else {
+                return false;
+            }
+            if (t.ltype == SH_T_OBJECT || t.rtype == SH_T_OBJECT) return false;
+            P.terms[k][nt++] = t;
+        }
+        P.filter_nterms[k] = nt;
+        P.filter_fast[k] = 1;
+        return true;
+    }
     // flatten `Next(...)` chains of stream states, `every` allowed on the start
     // state only (the shapes of configs C1/C2/C5)
     bool flatten(int e, bool first) {
@@ -300,6 +392,7 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
     if (q.state_type != SH_PATTERN) return fail(h, SH_E_UNSUPPORTED, "device engine: sequences are not lowered yet");
     Lowering L;
     L.q = &q;
+    L.app = app;
     memset(&L.P, 0, sizeof(L.P));
     if (!L.flatten(q.root, true)) return fail(h, SH_E_UNSUPPORTED, L.err);
     shp_program& P = L.P;
@@ -337,8 +430,28 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
             P.filter_len[k] = 0;
         }
     }
+    for (int k = 0; k < P.n_states; k++) {
+        const sh_state_elem& el = q.elems[L.chain[k]];
+        P.filter_fast[k] = 0;
+        if (el.filter >= 0) {
+            if (!getenv("SH_DISABLE_FAST_FILTER")) L.fast_filter(el.filter, k);
+        } else {
+            P.filter_fast[k] = 1;  // no filter: empty conjunction
+            P.filter_nterms[k] = 0;
+        }
+    }
     if (q.n_outputs > SHP_MAX_OUT) return fail(h, SH_E_UNSUPPORTED, "device engine: at most 16 output attributes");
     P.n_out = q.n_outputs;
+    P.out_fast = getenv("SH_DISABLE_FAST_FILTER") ? 0 : 1;
+    for (int o = 0; o < q.n_outputs; o++) {
+        const sh_output_attr& oa = q.outputs[o];
+        if (oa.agg != SH_AGG_NONE || oa.expr < 0 || !Lowering::is_var(q.exprs[oa.expr])) {
+            P.out_fast = 0;
+        } else {
+            P.out_slot[o] = q.exprs[oa.expr].slot;
+            P.out_attr[o] = q.exprs[oa.expr].attr;
+        }
+    }
     for (int o = 0; o < q.n_outputs; o++) {
         const sh_output_attr& oa = q.outputs[o];
         P.out_agg[o] = oa.agg;
@@ -540,8 +653,11 @@ static int run_batch(sh_handle* h, const shd_batch& B, int32_t nkeys, const shd_
         em.tmp_cap = h->tmp_cap;
         em.match_cnt = h->w_cnt.as<uint32_t>();
         em.err = h->d_err.as<int32_t>();
+        bool fast_ok = true;  // register-only filters need null-free columns
+        for (int s2 = 0; s2 < SHP_MAX_STREAMS; s2++)
+            for (int a = 0; a < 32; a++) fast_ok = fast_ok && cols.nul[s2][a] == nullptr;
         rc = shd_advance(h->d_prog.as<shp_program>(), &h->lay, h->d_kstate.as<uint8_t>(), nkeys, &B, perm, skeys,
-                         ws.seg_off, h->d_cols_desc.as<shd_cols>(), &em, st);
+                         ws.seg_off, h->d_cols_desc.as<shd_cols>(), &em, st, fast_ok ? 1 : 0);
         if (rc) return fail(h, SH_E_HIP, "advance launch failed");
         if (timed) hipEventRecord(h->ev[2], st);
         int32_t herr[2] = {0, 0};

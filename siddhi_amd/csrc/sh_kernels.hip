@@ -366,7 +366,8 @@ __global__ void __launch_bounds__(TPB) k_advance(const shp_program* __restrict__
                                                  uint8_t* __restrict__ kstate, shd_batch B,
                                                  const uint32_t* __restrict__ perm, const uint32_t* __restrict__ skeys,
                                                  const uint32_t* __restrict__ seg_list, const uint32_t* __restrict__ nseg,
-                                                 const shd_cols* __restrict__ C, shd_emit EM, int32_t nkeys) {
+                                                 const shd_cols* __restrict__ C, shd_emit EM, int32_t nkeys,
+                                                 int fast_ok) {
     const uint32_t sidx = blockIdx.x * blockDim.x + threadIdx.x;
     if (sidx >= *nseg) return;
     const uint32_t beg = seg_list[sidx];
@@ -463,12 +464,7 @@ __global__ void __launch_bounds__(TPB) k_advance(const shp_program* __restrict__
                 if (!(flags & 2ull)) continue;
                 for (int q = 0; q < n; q++) rows[q] = SHD_NULL_ROW;
                 rows[0] = row;
-                bool pass = true;
-                if (P->filter_pc[0] >= 0) {
-                    VmVal v = vm_eval(P, P->filter_pc[0], P->filter_len[0], rows, C);
-                    pass = !v.null && v.b;
-                }
-                if (!pass) continue;
+                if (!filter_pass(P, 0, rows, C, fast_ok)) continue;
                 flags &= ~2ull;                       // template leaves pending (stateChanged)
                 if (P->every_start) flags |= 4ull;    // addEveryState: fresh clone into new-and-every
                 if (n == 1) {
@@ -497,12 +493,7 @@ __global__ void __launch_bounds__(TPB) k_advance(const shp_program* __restrict__
                 uint32_t* rr = (uint32_t*)(r + 2);
                 for (int z = 0; z < n; z++) rows[z] = rr[z];
                 rows[k] = row;
-                bool pass = true;
-                if (P->filter_pc[k] >= 0) {
-                    VmVal v = vm_eval(P, P->filter_pc[k], P->filter_len[k], rows, C);
-                    pass = !v.null && v.b;
-                }
-                if (pass) {
+                if (filter_pass(P, k, rows, C, fast_ok)) {
                     if (k == n - 1) {
                         emit_match(P, K, E, rows, C, i, nmatch++, t);
                     } else {
@@ -629,7 +620,7 @@ extern "C" int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws
 
 extern "C" int shd_advance(const shp_program* dprog, const shp_layout* lay, uint8_t* kstate, int32_t nkeys,
                            const shd_batch* b, const uint32_t* perm, const uint32_t* skeys, const uint32_t* seg_off,
-                           const shd_cols* dcols, const shd_emit* em, void* stream) {
+                           const shd_cols* dcols, const shd_emit* em, void* stream, int fast_ok) {
     hipStream_t st = (hipStream_t)stream;
     const int64_t n = b->n;
     const uint32_t* seg_list = seg_off + 2 * n;
@@ -640,7 +631,7 @@ extern "C" int shd_advance(const shp_program* dprog, const shp_layout* lay, uint
     if (maxseg < 1) maxseg = 1;
     const unsigned g = (unsigned)ceil_div(maxseg, TPB);
     hipLaunchKernelGGL(k_advance, dim3(g), dim3(TPB), 0, st, dprog, *lay, kstate, *b, perm, skeys, seg_list, nseg,
-                       dcols, *em, nkeys);
+                       dcols, *em, nkeys, fast_ok);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

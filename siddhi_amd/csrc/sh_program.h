@@ -41,6 +41,22 @@ struct shp_instr {
     int32_t x;
 };
 
+// A conjunct `lhs op rhs` of a filter that needs no stack machine:
+// lhs is an attribute, rhs an attribute, a constant, or `attribute (aop) constant`.
+struct shp_term {
+    uint8_t op;     // SH_OP_EQ..SH_OP_LE
+    uint8_t dom;    // compare domain (enum shp_dom)
+    uint8_t lslot, lattr, ltype;
+    uint8_t rkind;  // 0: attribute, 1: constant, 2: attribute (aop) constant
+    uint8_t rslot, rattr, rtype;
+    uint8_t aop;    // SH_OP_ADD/SUB/MUL for rkind 2
+    uint8_t atype;  // arithmetic result type for rkind 2
+    uint8_t ctype;  // constant type
+    int64_t c;      // constant raw bits
+};
+
+#define SHP_MAX_TERMS 4
+
 struct shp_program {
     int32_t n_states;                 // chain length
     int32_t every_start;              // `every` wraps exactly the start state
@@ -51,6 +67,14 @@ struct shp_program {
     int32_t state_stream[SHP_MAX_STATES];
     int32_t filter_pc[SHP_MAX_STATES];   // -1: no filter
     int32_t filter_len[SHP_MAX_STATES];
+    // register-only form of the filters: conjunction of shp_term (no nulls)
+    int32_t filter_fast[SHP_MAX_STATES];
+    int32_t filter_nterms[SHP_MAX_STATES];
+    shp_term terms[SHP_MAX_STATES][SHP_MAX_TERMS];
+    // projection-only select: output o reads attribute (out_slot, out_attr)
+    int32_t out_fast;
+    int32_t out_slot[SHP_MAX_OUT];
+    int32_t out_attr[SHP_MAX_OUT];
     // per stream: which states update (stabilizeStates) and the processing order
     // (eventSequence: reverse of setup order), PatternSingle/MultiProcessStreamReceiver
     int32_t upd_count[SHP_MAX_STREAMS];

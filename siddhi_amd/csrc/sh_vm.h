@@ -53,6 +53,97 @@ __device__ __forceinline__ bool cmp_op(int op, T a, T b) {
     }
 }
 
+
+// typed compare in a promotion domain (operands non-null)
+__device__ __forceinline__ bool vm_cmp(int op, int dom, const VmVal& l, const VmVal& r) {
+    switch (dom) {
+        case DOM_I32: return cmp_op<int32_t>(op, (int32_t)l.b, (int32_t)r.b);
+        case DOM_I64: return cmp_op<int64_t>(op, to_i64(l), to_i64(r));
+        case DOM_F32: return cmp_op<float>(op, to_f32(l), to_f32(r));
+        case DOM_F64: return cmp_op<double>(op, to_f64(l), to_f64(r));
+        case DOM_BOOL: return cmp_op<int>(op, l.b != 0, r.b != 0);
+        default: return cmp_op<int32_t>(op, (int32_t)l.b, (int32_t)r.b);
+    }
+}
+
+// arithmetic in result type rt (math/{add,subtract,multiply,divide,mod}/*)
+__device__ __forceinline__ VmVal vm_arith(int aop, int rt, const VmVal& l, const VmVal& r) {
+    VmVal o;
+    o.t = (uint8_t)rt;
+    o.null = 0;
+    o.b = 0;
+    if (l.null || r.null) {
+        o.null = 1;
+    } else if (rt == SH_T_INT) {
+        const uint32_t a = (uint32_t)l.b, b = (uint32_t)r.b;
+        const int32_t sa = (int32_t)a, sb = (int32_t)b;
+        int32_t res = 0;
+        switch (aop) {
+            case SH_OP_ADD: res = (int32_t)(a + b); break;
+            case SH_OP_SUB: res = (int32_t)(a - b); break;
+            case SH_OP_MUL: res = (int32_t)(a * b); break;
+            case SH_OP_DIV:
+                if (sb == 0) o.null = 1;
+                else res = (sa == INT32_MIN && sb == -1) ? INT32_MIN : sa / sb;
+                break;
+            default:
+                if (sb == 0) o.null = 1;
+                else res = (sb == -1) ? 0 : sa % sb;
+        }
+        o.b = res;
+    } else if (rt == SH_T_LONG) {
+        const uint64_t a = (uint64_t)to_i64(l), b = (uint64_t)to_i64(r);
+        const int64_t sa = (int64_t)a, sb = (int64_t)b;
+        int64_t res = 0;
+        switch (aop) {
+            case SH_OP_ADD: res = (int64_t)(a + b); break;
+            case SH_OP_SUB: res = (int64_t)(a - b); break;
+            case SH_OP_MUL: res = (int64_t)(a * b); break;
+            case SH_OP_DIV:
+                if (sb == 0) o.null = 1;
+                else res = (sa == INT64_MIN && sb == -1) ? INT64_MIN : sa / sb;
+                break;
+            default:
+                if (sb == 0) o.null = 1;
+                else res = (sb == -1) ? 0 : sa % sb;
+        }
+        o.b = res;
+    } else if (rt == SH_T_FLOAT) {
+        const float a = to_f32(l), b = to_f32(r);
+        float res = 0.f;
+        switch (aop) {
+            case SH_OP_ADD: res = __fadd_rn(a, b); break;
+            case SH_OP_SUB: res = __fsub_rn(a, b); break;
+            case SH_OP_MUL: res = __fmul_rn(a, b); break;
+            case SH_OP_DIV:
+                if (b == 0.0f) o.null = 1;
+                else res = __fdiv_rn(a, b);
+                break;
+            default:
+                if (b == 0.0f) o.null = 1;
+                else res = fmodf(a, b);
+        }
+        o.b = f32_bits(res);
+    } else {
+        const double a = to_f64(l), b = to_f64(r);
+        double res = 0.0;
+        switch (aop) {
+            case SH_OP_ADD: res = __dadd_rn(a, b); break;
+            case SH_OP_SUB: res = __dsub_rn(a, b); break;
+            case SH_OP_MUL: res = __dmul_rn(a, b); break;
+            case SH_OP_DIV:
+                if (b == 0.0) o.null = 1;
+                else res = __ddiv_rn(a, b);
+                break;
+            default:
+                if (b == 0.0) o.null = 1;
+                else res = fmod(a, b);
+        }
+        o.b = f64_bits(res);
+    }
+    return o;
+}
+
 __device__ __forceinline__ int64_t load_attr(const shd_cols* C, int s, int a, int type, uint32_t row) {
     const void* p = C->col[s][a];
     switch (type) {
@@ -154,100 +245,16 @@ __device__ inline VmVal vm_eval(const shp_program* __restrict__ P, int pc, int l
             }
             case OPC_CMP: {
                 VmVal r = st[--sp], l = st[--sp];
-                bool res = false;
-                if (!l.null && !r.null) {
-                    switch (in.b) {
-                        case DOM_I32: res = cmp_op<int32_t>(in.a, (int32_t)l.b, (int32_t)r.b); break;
-                        case DOM_I64: res = cmp_op<int64_t>(in.a, to_i64(l), to_i64(r)); break;
-                        case DOM_F32: res = cmp_op<float>(in.a, to_f32(l), to_f32(r)); break;
-                        case DOM_F64: res = cmp_op<double>(in.a, to_f64(l), to_f64(r)); break;
-                        case DOM_BOOL: res = cmp_op<int>(in.a, l.b != 0, r.b != 0); break;
-                        default: res = cmp_op<int32_t>(in.a, (int32_t)l.b, (int32_t)r.b); break;
-                    }
-                }
                 VmVal o;
                 o.t = SH_T_BOOL;
                 o.null = 0;
-                o.b = res ? 1 : 0;
+                o.b = (!l.null && !r.null && vm_cmp(in.a, in.b, l, r)) ? 1 : 0;
                 st[sp++] = o;
                 break;
             }
             case OPC_ARITH: {
                 VmVal r = st[--sp], l = st[--sp];
-                VmVal o;
-                o.t = in.b;
-                o.null = 0;
-                o.b = 0;
-                if (l.null || r.null) {
-                    o.null = 1;
-                } else if (in.b == SH_T_INT) {
-                    const uint32_t a = (uint32_t)l.b, b = (uint32_t)r.b;
-                    const int32_t sa = (int32_t)a, sb = (int32_t)b;
-                    int32_t res = 0;
-                    switch (in.a) {
-                        case SH_OP_ADD: res = (int32_t)(a + b); break;
-                        case SH_OP_SUB: res = (int32_t)(a - b); break;
-                        case SH_OP_MUL: res = (int32_t)(a * b); break;
-                        case SH_OP_DIV:
-                            if (sb == 0) o.null = 1;
-                            else res = (sa == INT32_MIN && sb == -1) ? INT32_MIN : sa / sb;
-                            break;
-                        default:
-                            if (sb == 0) o.null = 1;
-                            else res = (sb == -1) ? 0 : sa % sb;
-                    }
-                    o.b = res;
-                } else if (in.b == SH_T_LONG) {
-                    const uint64_t a = (uint64_t)to_i64(l), b = (uint64_t)to_i64(r);
-                    const int64_t sa = (int64_t)a, sb = (int64_t)b;
-                    int64_t res = 0;
-                    switch (in.a) {
-                        case SH_OP_ADD: res = (int64_t)(a + b); break;
-                        case SH_OP_SUB: res = (int64_t)(a - b); break;
-                        case SH_OP_MUL: res = (int64_t)(a * b); break;
-                        case SH_OP_DIV:
-                            if (sb == 0) o.null = 1;
-                            else res = (sa == INT64_MIN && sb == -1) ? INT64_MIN : sa / sb;
-                            break;
-                        default:
-                            if (sb == 0) o.null = 1;
-                            else res = (sb == -1) ? 0 : sa % sb;
-                    }
-                    o.b = res;
-                } else if (in.b == SH_T_FLOAT) {
-                    const float a = to_f32(l), b = to_f32(r);
-                    float res = 0.f;
-                    switch (in.a) {
-                        case SH_OP_ADD: res = __fadd_rn(a, b); break;
-                        case SH_OP_SUB: res = __fsub_rn(a, b); break;
-                        case SH_OP_MUL: res = __fmul_rn(a, b); break;
-                        case SH_OP_DIV:
-                            if (b == 0.0f) o.null = 1;
-                            else res = __fdiv_rn(a, b);
-                            break;
-                        default:
-                            if (b == 0.0f) o.null = 1;
-                            else res = fmodf(a, b);
-                    }
-                    o.b = f32_bits(res);
-                } else {
-                    const double a = to_f64(l), b = to_f64(r);
-                    double res = 0.0;
-                    switch (in.a) {
-                        case SH_OP_ADD: res = __dadd_rn(a, b); break;
-                        case SH_OP_SUB: res = __dsub_rn(a, b); break;
-                        case SH_OP_MUL: res = __dmul_rn(a, b); break;
-                        case SH_OP_DIV:
-                            if (b == 0.0) o.null = 1;
-                            else res = __ddiv_rn(a, b);
-                            break;
-                        default:
-                            if (b == 0.0) o.null = 1;
-                            else res = fmod(a, b);
-                    }
-                    o.b = f64_bits(res);
-                }
-                st[sp++] = o;
+                st[sp++] = vm_arith(in.a, in.b, l, r);
                 break;
             }
             case OPC_SELECT: {
@@ -264,3 +271,49 @@ __device__ inline VmVal vm_eval(const shp_program* __restrict__ P, int pc, int l
     return st[sp - 1];
 }
 
+
+// register-only filter: conjunction of shp_term over non-null columns
+// (null masks are absent on this path; empty slots compare as null -> false)
+__device__ __forceinline__ bool terms_pass(const shp_program* __restrict__ P, int k, const uint32_t* rows,
+                                           const shd_cols* __restrict__ C) {
+    const int nt = P->filter_nterms[k];
+    for (int t = 0; t < nt; t++) {
+        const shp_term T = P->terms[k][t];
+        const uint32_t lr = rows[T.lslot];
+        if (lr == SHD_NULL_ROW) return false;
+        VmVal l, r;
+        l.t = T.ltype;
+        l.null = 0;
+        l.b = load_attr(C, P->state_stream[T.lslot], T.lattr, T.ltype, lr);
+        if (T.rkind == 1) {
+            r.t = T.ctype;
+            r.null = 0;
+            r.b = T.c;
+        } else {
+            const uint32_t rr = rows[T.rslot];
+            if (rr == SHD_NULL_ROW) return false;
+            r.t = T.rtype;
+            r.null = 0;
+            r.b = load_attr(C, P->state_stream[T.rslot], T.rattr, T.rtype, rr);
+            if (T.rkind == 2) {
+                VmVal c;
+                c.t = T.ctype;
+                c.null = 0;
+                c.b = T.c;
+                r = vm_arith(T.aop, T.atype, r, c);
+                if (r.null) return false;
+            }
+        }
+        if (!vm_cmp(T.op, T.dom, l, r)) return false;
+    }
+    return true;
+}
+
+// filter of state k: register path when lowered and no column carries nulls
+__device__ __forceinline__ bool filter_pass(const shp_program* __restrict__ P, int k, const uint32_t* rows,
+                                            const shd_cols* __restrict__ C, bool fast_ok) {
+    if (fast_ok && P->filter_fast[k]) return terms_pass(P, k, rows, C);
+    if (P->filter_pc[k] < 0) return true;
+    VmVal v = vm_eval(P, P->filter_pc[k], P->filter_len[k], rows, C);
+    return !v.null && v.b;
+}

@@ -48,30 +48,25 @@ __global__ void k_permute(const T* __restrict__ src, const uint32_t* __restrict_
 __global__ void __launch_bounds__(WTPB) k_window(const shp_program* __restrict__ P, const int64_t* __restrict__ sts,
                                                  const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ perm,
                                                  int64_t n, uint32_t sentinel, const shd_cols* __restrict__ C,
-                                                 int32_t* __restrict__ match_pos, uint32_t* __restrict__ cnt) {
+                                                 int32_t* __restrict__ match_pos, uint32_t* __restrict__ cnt,
+                                                 int fast_ok, int32_t* __restrict__ flag) {
     const int64_t within = P->within_ms;
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t key = skeys ? skeys[p] : 0u;
         if (key == sentinel) continue;
+        // the reduction to a forward scan needs non-decreasing timestamps per key
+        if (p > 0 && (!skeys || skeys[p - 1] == key) && sts[p] < sts[p - 1]) atomicExch(flag, 1);
         uint32_t rows[2];
         rows[0] = (uint32_t)p;
         rows[1] = SHD_NULL_ROW;
-        if (P->filter_pc[0] >= 0) {
-            VmVal v = vm_eval(P, P->filter_pc[0], P->filter_len[0], rows, C);
-            if (v.null || !v.b) continue;
-        }
+        if (!filter_pass(P, 0, rows, C, fast_ok)) continue;
         const int64_t t0 = sts[p];
         for (int64_t q = p + 1; q < n; q++) {
             if (skeys && skeys[q] != key) break;
             const int64_t d = sts[q] - t0;
             if ((d < 0 ? -d : d) > within) break;  // expired before event q is matched
             rows[1] = (uint32_t)q;
-            bool pass = true;
-            if (P->filter_pc[1] >= 0) {
-                VmVal v = vm_eval(P, P->filter_pc[1], P->filter_len[1], rows, C);
-                pass = !v.null && v.b;
-            }
-            if (pass) {
+            if (filter_pass(P, 1, rows, C, fast_ok)) {
                 match_pos[p] = (int32_t)q;
                 atomicAdd(&cnt[perm ? perm[q] : (uint32_t)q], 1u);
                 break;
@@ -89,7 +84,8 @@ __global__ void __launch_bounds__(WTPB) k_window_place(const shp_program* __rest
                                                        const int32_t* __restrict__ match_pos,
                                                        const uint32_t* __restrict__ off, uint64_t seq_base,
                                                        uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_ts,
-                                                       int64_t* __restrict__ out_vals, uint8_t* __restrict__ out_nulls) {
+                                                       int64_t* __restrict__ out_vals, uint8_t* __restrict__ out_nulls,
+                                                       int fast_ok) {
     const int64_t within = P->within_ms;
     const int n_out = P->n_out;
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
@@ -108,10 +104,18 @@ __global__ void __launch_bounds__(WTPB) k_window_place(const shp_program* __rest
         if (out_seq) out_seq[dst] = seq_base + j;
         if (out_ts) out_ts[dst] = tq;
         uint32_t rows[2] = {(uint32_t)p, (uint32_t)q};
-        for (int o = 0; o < n_out; o++) {
-            VmVal v = vm_eval(P, P->out_pc[o], P->out_len[o], rows, C);
-            if (out_vals) out_vals[dst * n_out + o] = v.b;
-            if (out_nulls) out_nulls[dst * n_out + o] = v.null;
+        if (P->out_fast && fast_ok) {
+            for (int o = 0; o < n_out; o++) {
+                const int sl = P->out_slot[o], at = P->out_attr[o];
+                if (out_vals) out_vals[dst * n_out + o] = load_attr(C, P->state_stream[sl], at, P->attr_type[P->state_stream[sl]][at], rows[sl]);
+                if (out_nulls) out_nulls[dst * n_out + o] = 0;
+            }
+        } else {
+            for (int o = 0; o < n_out; o++) {
+                VmVal v = vm_eval(P, P->out_pc[o], P->out_len[o], rows, C);
+                if (out_vals) out_vals[dst * n_out + o] = v.b;
+                if (out_nulls) out_nulls[dst * n_out + o] = v.null;
+            }
         }
     }
 }
@@ -135,11 +139,6 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
     const uint32_t sentinel = skeys ? (uint32_t)nkeys : 0xFFFFFFFFu;
     const unsigned g = grid_for(n);
     hipMemsetAsync(ws->flag, 0, 4, st);
-    hipLaunchKernelGGL(k_ts_check, dim3(g), dim3(WTPB), 0, st, b->ts, perm, skeys, n, sentinel, ws->flag);
-    int32_t hflag = 0;
-    hipMemcpyAsync(&hflag, ws->flag, 4, hipMemcpyDeviceToHost, st);
-    if (hipStreamSynchronize(st) != hipSuccess) return -3;
-    if (hflag) return 1;
     // key-segment-ordered copies of ts and every column of the stream
     shd_cols sc;
     memset(&sc, 0, sizeof(sc));
@@ -168,18 +167,21 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
     hipMemsetAsync(ws->match_pos, 0xFF, n * 4, st);
     hipMemsetAsync(ws->cnt, 0, n * 4, st);
     hipLaunchKernelGGL(k_window, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n, sentinel,
-                       (const shd_cols*)d_sorted_desc, ws->match_pos, ws->cnt);
+                       (const shd_cols*)d_sorted_desc, ws->match_pos, ws->cnt, 1, ws->flag);
     if (ev_mid) hipEventRecord(ev_mid, st);
     int rc = shd_exclusive_scan(ws->cnt, ws->off, n, scan_tmp, stream);
     if (rc) return rc;
     uint32_t lo = 0, lc = 0;
+    int32_t hflag = 0;
     hipMemcpyAsync(&lo, ws->off + (n - 1), 4, hipMemcpyDeviceToHost, st);
     hipMemcpyAsync(&lc, ws->cnt + (n - 1), 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(&hflag, ws->flag, 4, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return -3;
+    if (hflag) return 1;  // timestamps decrease inside a key: caller falls back
     *n_matches = (int64_t)lo + lc;
     if (*n_matches > out_cap) return 2;
     hipLaunchKernelGGL(k_window_place, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n,
                        (const shd_cols*)d_sorted_desc, (const int32_t*)ws->match_pos, (const uint32_t*)ws->off,
-                       b->seq_base, out_seq, out_ts, out_vals, out_nulls);
+                       b->seq_base, out_seq, out_ts, out_vals, out_nulls, 1);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
