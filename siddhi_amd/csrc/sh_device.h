@@ -48,11 +48,19 @@ struct shd_segment_ws {
     int64_t cap;
 };
 
+// columns carried through the radix segment (moved with their key)
+struct shd_payload {
+    int32_t n;
+    int32_t pad;
+    const void* src[8];      // arrival-order columns
+    void* dst[8];            // key-segment-order output
+    uint8_t width[8];        // 1, 4 or 8 bytes
+};
+
 // scratch of the window engine (sh_window.hip)
 struct shd_window_ws {
-    int64_t* sts;            // [n] timestamps in key-segment order
-    void* scol[32];          // [n] per attribute, key-segment order
     int32_t* match_pos;      // [n] consuming position of the partial opened at p, -1 none
+    uint32_t* cnt_s;         // [n] matches per event (key-segment position)
     uint32_t* cnt;           // [n] matches per event (arrival index)
     uint32_t* off;           // [n] exclusive scan of cnt
     int32_t* flag;           // [1] non-monotone timestamps seen
@@ -67,6 +75,11 @@ size_t shd_scan_tmp_words(int64_t n);
 // unpartitioned batch) and the segment list in ws->seg_off[2n .. 3n] (+ count at [3n])
 int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
                 const uint32_t** perm_out, const uint32_t** skeys_out);
+// as shd_segment, also moving `carry` columns into key-segment order; `mid`
+// holds one intermediate buffer per carried column (multi-pass ping-pong)
+int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
+                        const uint32_t** perm_out, const uint32_t** skeys_out, const shd_payload* carry,
+                        void* const* mid);
 int shd_advance(const shp_program* dprog, const shp_layout* lay, uint8_t* kstate, int32_t nkeys,
                 const shd_batch* b, const uint32_t* perm, const uint32_t* skeys,
                 const uint32_t* seg_off, const shd_cols* dcols, const shd_emit* em, void* stream, int fast_ok);
@@ -76,10 +89,10 @@ int shd_emit_place(const shd_emit* em, int32_t n_out, int64_t n_events, uint32_t
 // window engine for `every e1=S[f1] -> e2=S[f2] within W`: 0 ok, 1 = fall back
 // (timestamps decrease inside a key), 2 = output capacity too small, <0 error
 int shd_window(const shp_program* dprog, const shp_program* hprog, const shd_batch* b, int32_t nkeys,
-               const uint32_t* perm, const uint32_t* skeys, const void* const* cols, shd_window_ws* ws,
-               shd_cols* d_sorted_desc, uint32_t* scan_tmp, uint64_t* out_seq, int64_t* out_ts,
-               int64_t* out_vals, uint8_t* out_nulls, int64_t out_cap, int64_t* n_matches, void* stream,
-               void* ev_mid);
+               const uint32_t* perm, const uint32_t* skeys, const int64_t* sts, const void* const* scols,
+               shd_window_ws* ws, shd_cols* d_sorted_desc, uint32_t* scan_tmp, uint64_t* out_seq,
+               int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, int64_t out_cap, int64_t* n_matches,
+               void* stream, void* ev_mid);
 int shd_relayout(const uint8_t* src, const shp_layout* A, uint8_t* dst, const shp_layout* B, int32_t nkeys,
                  int32_t n_states, int32_t n_out, void* stream);
 int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, void* stream);

@@ -326,8 +326,8 @@ struct sh_handle {
     // workspaces
     DevBuf w_ts, w_stream, w_row, w_key, w_keys_a, w_keys_b, w_idx_a, w_idx_b, w_hist, w_scan, w_seg;
     DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls;
-    DevBuf v_sts, v_mpos, v_flag;
-    DevBuf v_scol[32];
+    DevBuf v_sts, v_mpos, v_flag, v_cnts, v_mid_ts;
+    DevBuf v_scol[32], v_mid[32];
     int64_t tmp_cap = 0;
     // drained output queue (host)
     std::vector<int32_t> o_query;
@@ -515,7 +515,10 @@ void sh_destroy(sh_handle* h) {
         h->v_sts.release();
         h->v_mpos.release();
         h->v_flag.release();
+        h->v_cnts.release();
+        h->v_mid_ts.release();
         for (auto& b : h->v_scol) b.release();
+        for (auto& b : h->v_mid) b.release();
         DevBuf* bufs[] = {&h->d_prog, &h->d_cols_desc, &h->d_kstate, &h->d_err, &h->w_ts, &h->w_stream, &h->w_row,
                           &h->w_key, &h->w_keys_a, &h->w_keys_b, &h->w_idx_a, &h->w_idx_b, &h->w_hist, &h->w_scan,
                           &h->w_seg, &h->w_cnt, &h->w_off, &h->w_tmp, &h->w_ctr, &h->w_oseq, &h->w_ots,
@@ -898,21 +901,39 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
     for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = run->d_cols[a];
     int64_t nm = 0;
     h->times = sh_kernel_times{};
-    if (h->prog.window_ok) {
+    if (h->prog.window_ok && h->stream_types[0].size() <= 7) {
         const int64_t n = run->n;
         hipStream_t st = h->stream;
         if (ensure_ws(h, n)) return fail(h, SH_E_OOM, "workspace");
+        const int na = (int)h->stream_types[0].size();
+        const bool sorted = h->partitioned;  // unpartitioned: one segment, arrival order
         shd_window_ws wws;
         memset(&wws, 0, sizeof(wws));
-        if (h->v_sts.ensure_fresh(n * 8) || h->v_mpos.ensure_fresh(n * 4) || h->v_flag.ensure_fresh(64))
+        if (h->v_mpos.ensure_fresh(n * 4) || h->v_flag.ensure_fresh(64) || h->v_cnts.ensure_fresh(n * 4))
             return fail(h, SH_E_OOM, "window workspace");
-        for (size_t a = 0; a < h->stream_types[0].size(); a++) {
-            if (h->v_scol[a].ensure_fresh(n * type_width(h->stream_types[0][a])))
+        shd_payload carry;
+        memset(&carry, 0, sizeof(carry));
+        void* mid[8] = {nullptr};
+        if (sorted) {
+            if (h->v_sts.ensure_fresh(n * 8) || h->v_mid_ts.ensure_fresh(n * 8))
                 return fail(h, SH_E_OOM, "window workspace");
-            wws.scol[a] = h->v_scol[a].p;
+            carry.n = 1 + na;
+            carry.src[0] = run->d_ts;
+            carry.dst[0] = h->v_sts.p;
+            carry.width[0] = 8;
+            mid[0] = h->v_mid_ts.p;
+            for (int a = 0; a < na; a++) {
+                const int w = type_width(h->stream_types[0][a]);
+                if (h->v_scol[a].ensure_fresh(n * w) || h->v_mid[a].ensure_fresh(n * w))
+                    return fail(h, SH_E_OOM, "window workspace");
+                carry.src[1 + a] = run->d_cols[a];
+                carry.dst[1 + a] = h->v_scol[a].p;
+                carry.width[1 + a] = (uint8_t)w;
+                mid[1 + a] = h->v_mid[a].p;
+            }
         }
-        wws.sts = h->v_sts.as<int64_t>();
         wws.match_pos = h->v_mpos.as<int32_t>();
+        wws.cnt_s = h->v_cnts.as<uint32_t>();
         wws.cnt = h->w_cnt.as<uint32_t>();
         wws.off = h->w_off.as<uint32_t>();
         wws.flag = h->v_flag.as<int32_t>();
@@ -928,9 +949,13 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
         ws.cap = n;
         const uint32_t* perm = nullptr;
         const uint32_t* skeys = nullptr;
-        if (shd_segment(&B, nkeys, &ws, st, &perm, &skeys)) return fail(h, SH_E_HIP, "segment launch failed");
+        if (shd_segment_payload(&B, nkeys, &ws, st, &perm, &skeys, sorted ? &carry : nullptr, mid))
+            return fail(h, SH_E_HIP, "segment launch failed");
         hipEventRecord(h->ev[1], st);
-        int wrc = shd_window(h->d_prog.as<shp_program>(), &h->prog, &B, nkeys, perm, skeys, run->d_cols, &wws,
+        const int64_t* sts = sorted ? h->v_sts.as<int64_t>() : run->d_ts;
+        const void* scols[32];
+        for (int a = 0; a < na; a++) scols[a] = sorted ? (const void*)h->v_scol[a].p : run->d_cols[a];
+        int wrc = shd_window(h->d_prog.as<shp_program>(), &h->prog, &B, nkeys, perm, skeys, sts, scols, &wws,
                              h->d_cols_desc.as<shd_cols>(), h->w_scan.as<uint32_t>(), run->d_out_seq, nullptr,
                              run->d_out_values, nullptr, run->out_capacity, &nm, st, h->ev[2]);
         hipEventRecord(h->ev[3], st);

@@ -22,6 +22,8 @@
 #include "../../include/sh_query.h"
 #include "sh_device.h"
 
+#include <string.h>
+
 #define TPB 256
 #define RADIX_ITEMS 16
 #define RADIX_TILE (TPB * RADIX_ITEMS)
@@ -148,7 +150,8 @@ __global__ void __launch_bounds__(TPB) k_digit_hist(const uint32_t* __restrict__
 __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ raw,
                                                        uint32_t sentinel, const uint32_t* __restrict__ idx_in, int64_t n,
                                                        int shift, const uint32_t* __restrict__ offs, int64_t ntiles,
-                                                       uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out) {
+                                                       uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out,
+                                                       shd_payload PL) {
     __shared__ uint32_t running[256];
     __shared__ uint32_t wcnt[TPB / 64][256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -188,6 +191,15 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
             const uint32_t dst = running[d] + pre + rank;
             keys_out[dst] = k;
             idx_out[dst] = id;
+            // carried columns move with their key (pass 1 reads them in arrival order)
+            for (int c = 0; c < PL.n; c++) {
+                if (PL.width[c] == 8)
+                    ((uint64_t*)PL.dst[c])[dst] = ((const uint64_t*)PL.src[c])[i];
+                else if (PL.width[c] == 4)
+                    ((uint32_t*)PL.dst[c])[dst] = ((const uint32_t*)PL.src[c])[i];
+                else
+                    ((uint8_t*)PL.dst[c])[dst] = ((const uint8_t*)PL.src[c])[i];
+            }
         }
         __syncthreads();
         uint32_t add = 0;
@@ -578,8 +590,9 @@ static uint32_t g_bits_for(uint32_t maxkey) {
     return b;
 }
 
-extern "C" int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
-                           const uint32_t** perm_out, const uint32_t** skeys_out) {
+extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
+                                   const uint32_t** perm_out, const uint32_t** skeys_out, const shd_payload* carry,
+                                   void* const* mid) {
     hipStream_t st = (hipStream_t)stream;
     const int64_t n = b->n;
     const uint32_t sentinel = (uint32_t)nkeys;
@@ -596,8 +609,23 @@ extern "C" int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws
                            ws->hist, ntiles);
         int rc = shd_exclusive_scan(ws->hist, ws->hist, 256 * ntiles, ws->scan_tmp, stream);
         if (rc) return rc;
+        // payload ping-pong: pass ps reads the previous pass's output (or the
+        // original columns) and writes `mid` (odd distance to the last pass) or
+        // the final arrays
+        shd_payload PL;
+        memset(&PL, 0, sizeof(PL));
+        if (carry) {
+            PL = *carry;
+            const bool last = ps == passes - 1;
+            const bool to_mid = ((passes - 1 - ps) & 1) != 0;
+            for (int c = 0; c < carry->n; c++) {
+                const void* src = (ps == 0) ? carry->src[c] : (((passes - ps) & 1) ? mid[c] : carry->dst[c]);
+                PL.src[c] = src;
+                PL.dst[c] = last ? carry->dst[c] : (to_mid ? mid[c] : carry->dst[c]);
+            }
+        }
         hipLaunchKernelGGL(k_digit_scatter, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, b->keys, sentinel, iin, n,
-                           shift, (const uint32_t*)ws->hist, ntiles, kout, iout);
+                           shift, (const uint32_t*)ws->hist, ntiles, kout, iout, PL);
         kin = kout;
         iin = iout;
         kout = (kout == ws->keys_a) ? ws->keys_b : ws->keys_a;
@@ -616,6 +644,11 @@ extern "C" int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws
     hipLaunchKernelGGL(k_seg_compact, dim3(g), dim3(TPB), 0, st, (const uint32_t*)flags, (const uint32_t*)pos, n,
                        seg_list, seg_list + n);
     return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
+                           const uint32_t** perm_out, const uint32_t** skeys_out) {
+    return shd_segment_payload(b, nkeys, ws, stream, perm_out, skeys_out, nullptr, nullptr);
 }
 
 extern "C" int shd_advance(const shp_program* dprog, const shp_layout* lay, uint8_t* kstate, int32_t nkeys,

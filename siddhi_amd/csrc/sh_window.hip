@@ -68,11 +68,18 @@ __global__ void __launch_bounds__(WTPB) k_window(const shp_program* __restrict__
             rows[1] = (uint32_t)q;
             if (filter_pass(P, 1, rows, C, fast_ok)) {
                 match_pos[p] = (int32_t)q;
-                atomicAdd(&cnt[perm ? perm[q] : (uint32_t)q], 1u);
+                atomicAdd(&cnt[q], 1u);  // key-segment space: neighbouring lanes hit neighbouring words
                 break;
             }
         }
     }
+}
+
+// per-event match counts back to arrival order (inverse of the segment permutation)
+__global__ void k_cnt_scatter(const uint32_t* __restrict__ cnt_s, const uint32_t* __restrict__ perm, int64_t n,
+                              uint32_t* __restrict__ cnt) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+        cnt[perm[q]] = cnt_s[q];
 }
 
 // rank of partial p among the partials consumed by the same event (creation
@@ -126,10 +133,12 @@ static unsigned grid_for(int64_t n) {
     return (unsigned)(g < 1 ? 1 : g);
 }
 
-// Runs the window engine on a segmented single-stream batch. Returns 0, or 1 when
-// timestamps decrease inside a key (caller falls back), <0 on HIP errors.
+// Runs the window engine on a segmented single-stream batch whose timestamps and
+// columns are already in key-segment order (shd_segment_payload). Returns 0, 1 when
+// timestamps decrease inside a key (caller falls back), 2 when out_cap is too
+// small, <0 on HIP errors.
 extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, const shd_batch* b, int32_t nkeys,
-                          const uint32_t* perm, const uint32_t* skeys, const void* const* cols,
+                          const uint32_t* perm, const uint32_t* skeys, const int64_t* sts, const void* const* scols,
                           shd_window_ws* ws, shd_cols* d_sorted_desc, uint32_t* scan_tmp, uint64_t* out_seq,
                           int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, int64_t out_cap,
                           int64_t* n_matches, void* stream, void* ev_mid_) {
@@ -138,37 +147,18 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
     const int64_t n = b->n;
     const uint32_t sentinel = skeys ? (uint32_t)nkeys : 0xFFFFFFFFu;
     const unsigned g = grid_for(n);
-    hipMemsetAsync(ws->flag, 0, 4, st);
-    // key-segment-ordered copies of ts and every column of the stream
     shd_cols sc;
     memset(&sc, 0, sizeof(sc));
-    const int64_t* sts = b->ts;
-    if (perm) {
-        hipLaunchKernelGGL(k_permute<int64_t>, dim3(g), dim3(WTPB), 0, st, b->ts, perm, n, ws->sts);
-        sts = ws->sts;
-        for (int a = 0; a < hprog->stream_nattr[0]; a++) {
-            const int t = hprog->attr_type[0][a];
-            void* dst = ws->scol[a];
-            if (t == SH_T_LONG || t == SH_T_DOUBLE)
-                hipLaunchKernelGGL(k_permute<int64_t>, dim3(g), dim3(WTPB), 0, st, (const int64_t*)cols[a], perm, n,
-                                   (int64_t*)dst);
-            else if (t == SH_T_BOOL)
-                hipLaunchKernelGGL(k_permute<uint8_t>, dim3(g), dim3(WTPB), 0, st, (const uint8_t*)cols[a], perm, n,
-                                   (uint8_t*)dst);
-            else
-                hipLaunchKernelGGL(k_permute<int32_t>, dim3(g), dim3(WTPB), 0, st, (const int32_t*)cols[a], perm, n,
-                                   (int32_t*)dst);
-            sc.col[0][a] = dst;
-        }
-    } else {
-        for (int a = 0; a < hprog->stream_nattr[0]; a++) sc.col[0][a] = cols[a];
-    }
+    for (int a = 0; a < hprog->stream_nattr[0]; a++) sc.col[0][a] = scols[a];
     hipMemcpyAsync(d_sorted_desc, &sc, sizeof(sc), hipMemcpyHostToDevice, st);
+    hipMemsetAsync(ws->flag, 0, 4, st);
     hipMemsetAsync(ws->match_pos, 0xFF, n * 4, st);
-    hipMemsetAsync(ws->cnt, 0, n * 4, st);
+    uint32_t* cnt_s = perm ? ws->cnt_s : ws->cnt;
+    hipMemsetAsync(cnt_s, 0, n * 4, st);
     hipLaunchKernelGGL(k_window, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n, sentinel,
-                       (const shd_cols*)d_sorted_desc, ws->match_pos, ws->cnt, 1, ws->flag);
+                       (const shd_cols*)d_sorted_desc, ws->match_pos, cnt_s, 1, ws->flag);
     if (ev_mid) hipEventRecord(ev_mid, st);
+    if (perm) hipLaunchKernelGGL(k_cnt_scatter, dim3(g), dim3(WTPB), 0, st, (const uint32_t*)cnt_s, perm, n, ws->cnt);
     int rc = shd_exclusive_scan(ws->cnt, ws->off, n, scan_tmp, stream);
     if (rc) return rc;
     uint32_t lo = 0, lc = 0;
