@@ -146,35 +146,60 @@ __global__ void __launch_bounds__(TPB) k_digit_hist(const uint32_t* __restrict__
     hist[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
-// stable scatter: elements of a tile are ranked in arrival order within their digit
+// stable scatter: elements of a tile are ranked in arrival order within their
+// digit, staged in LDS in digit order, and written out as contiguous runs per
+// digit (coalesced), for the key, the arrival index and every carried column
+__device__ __forceinline__ uint32_t load_key(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ raw,
+                                             uint32_t sentinel, int64_t i) {
+    if (keys_in) return keys_in[i];
+    const int32_t r = raw ? raw[i] : 0;
+    return r < 0 ? sentinel : (uint32_t)r;
+}
+
 __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ raw,
                                                        uint32_t sentinel, const uint32_t* __restrict__ idx_in, int64_t n,
                                                        int shift, const uint32_t* __restrict__ offs, int64_t ntiles,
                                                        uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out,
                                                        shd_payload PL) {
     __shared__ uint32_t running[256];
+    __shared__ uint32_t tstart[256];
+    __shared__ uint32_t gbase[256];
     __shared__ uint32_t wcnt[TPB / 64][256];
+    __shared__ uint8_t dig[RADIX_TILE];
+    __shared__ uint64_t stage[RADIX_TILE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    running[threadIdx.x] = offs[(int64_t)threadIdx.x * ntiles + blockIdx.x];
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t base = (int64_t)blockIdx.x * RADIX_TILE;
+    const int64_t tile_n = (n - base) < RADIX_TILE ? (n - base) : RADIX_TILE;
+    // tile histogram -> tile-local digit starts
+    running[threadIdx.x] = 0;
+    gbase[threadIdx.x] = offs[(int64_t)threadIdx.x * ntiles + blockIdx.x];
+    __syncthreads();
+    uint32_t key[RADIX_ITEMS];
+#pragma unroll
+    for (int j = 0; j < RADIX_ITEMS; j++) {
+        const int64_t i = base + j * TPB + threadIdx.x;
+        key[j] = (i < n) ? load_key(keys_in, raw, sentinel, i) : 0u;
+        if (i < n) atomicAdd(&running[(key[j] >> shift) & 0xFF], 1u);
+    }
+    __syncthreads();
+    {
+        uint32_t tot;
+        const uint32_t c = running[threadIdx.x];
+        const uint32_t ex = block_excl_scan(c, &tot);
+        tstart[threadIdx.x] = ex;
+        running[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    // stable rank of every element inside its digit (arrival order)
+    uint32_t lp[RADIX_ITEMS];
     for (int j = 0; j < RADIX_ITEMS; j++) {
 #pragma unroll
         for (int q = 0; q < TPB / 64; q++) wcnt[q][threadIdx.x] = 0;
         __syncthreads();
         const int64_t i = base + j * TPB + threadIdx.x;
         const bool valid = i < n;
-        uint32_t k = 0, id = 0;
-        if (valid) {
-            if (keys_in) {
-                k = keys_in[i];
-            } else {
-                int32_t r = raw ? raw[i] : 0;
-                k = r < 0 ? sentinel : (uint32_t)r;
-            }
-            id = idx_in ? idx_in[i] : (uint32_t)i;
-        }
-        const uint32_t d = (k >> shift) & 0xFF;
+        const uint32_t d = (key[j] >> shift) & 0xFF;
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
@@ -188,18 +213,8 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
         if (valid) {
             uint32_t pre = 0;
             for (int q = 0; q < w; q++) pre += wcnt[q][d];
-            const uint32_t dst = running[d] + pre + rank;
-            keys_out[dst] = k;
-            idx_out[dst] = id;
-            // carried columns move with their key (pass 1 reads them in arrival order)
-            for (int c = 0; c < PL.n; c++) {
-                if (PL.width[c] == 8)
-                    ((uint64_t*)PL.dst[c])[dst] = ((const uint64_t*)PL.src[c])[i];
-                else if (PL.width[c] == 4)
-                    ((uint32_t*)PL.dst[c])[dst] = ((const uint32_t*)PL.src[c])[i];
-                else
-                    ((uint8_t*)PL.dst[c])[dst] = ((const uint8_t*)PL.src[c])[i];
-            }
+            lp[j] = tstart[d] + running[d] + pre + rank;
+            dig[lp[j]] = (uint8_t)d;
         }
         __syncthreads();
         uint32_t add = 0;
@@ -208,6 +223,38 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
         running[threadIdx.x] += add;
         __syncthreads();
     }
+    // write-out through LDS: contiguous runs per digit
+#define SH_STAGE_OUT(T, SRCEXPR, DST)                                                           \
+    {                                                                                           \
+        for (int j = 0; j < RADIX_ITEMS; j++) {                                                 \
+            const int64_t i = base + j * TPB + threadIdx.x;                                     \
+            if (i < n) stage[lp[j]] = (uint64_t)(SRCEXPR);                                      \
+        }                                                                                       \
+        __syncthreads();                                                                        \
+        for (int m = 0; m < RADIX_ITEMS; m++) {                                                 \
+            const int l = m * TPB + threadIdx.x;                                                \
+            if (l < tile_n) {                                                                   \
+                const uint32_t d = dig[l];                                                      \
+                ((T*)(DST))[gbase[d] + (uint32_t)l - tstart[d]] = (T)stage[l];                  \
+            }                                                                                   \
+        }                                                                                       \
+        __syncthreads();                                                                        \
+    }
+    SH_STAGE_OUT(uint32_t, key[j], keys_out);
+    SH_STAGE_OUT(uint32_t, (idx_in ? idx_in[i] : (uint32_t)i), idx_out);
+    for (int c = 0; c < PL.n; c++) {
+        if (PL.width[c] == 8) {
+            const uint64_t* src = (const uint64_t*)PL.src[c];
+            SH_STAGE_OUT(uint64_t, src[i], PL.dst[c]);
+        } else if (PL.width[c] == 4) {
+            const uint32_t* src = (const uint32_t*)PL.src[c];
+            SH_STAGE_OUT(uint32_t, src[i], PL.dst[c]);
+        } else {
+            const uint8_t* src = (const uint8_t*)PL.src[c];
+            SH_STAGE_OUT(uint8_t, src[i], PL.dst[c]);
+        }
+    }
+#undef SH_STAGE_OUT
 }
 
 // segment starts: flag positions where the (sorted) key changes; sentinel excluded

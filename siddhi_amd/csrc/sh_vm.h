@@ -317,3 +317,40 @@ __device__ __forceinline__ bool filter_pass(const shp_program* __restrict__ P, i
     VmVal v = vm_eval(P, P->filter_pc[k], P->filter_len[k], rows, C);
     return !v.null && v.b;
 }
+
+// two-slot form for the window engine: rows live in two scalars (no local array,
+// no scratch)
+__device__ __forceinline__ bool terms_pass2(const shp_program* __restrict__ P, int k, uint32_t r0, uint32_t r1,
+                                            const shd_cols* __restrict__ C) {
+    const int nt = P->filter_nterms[k];
+    for (int t = 0; t < nt; t++) {
+        const shp_term T = P->terms[k][t];
+        const uint32_t lr = T.lslot ? r1 : r0;
+        if (lr == SHD_NULL_ROW) return false;
+        VmVal l, r;
+        l.t = T.ltype;
+        l.null = 0;
+        l.b = load_attr(C, P->state_stream[T.lslot], T.lattr, T.ltype, lr);
+        if (T.rkind == 1) {
+            r.t = T.ctype;
+            r.null = 0;
+            r.b = T.c;
+        } else {
+            const uint32_t rr = T.rslot ? r1 : r0;
+            if (rr == SHD_NULL_ROW) return false;
+            r.t = T.rtype;
+            r.null = 0;
+            r.b = load_attr(C, P->state_stream[T.rslot], T.rattr, T.rtype, rr);
+            if (T.rkind == 2) {
+                VmVal c;
+                c.t = T.ctype;
+                c.null = 0;
+                c.b = T.c;
+                r = vm_arith(T.aop, T.atype, r, c);
+                if (r.null) return false;
+            }
+        }
+        if (!vm_cmp(T.op, T.dom, l, r)) return false;
+    }
+    return true;
+}

@@ -45,6 +45,7 @@ __global__ void k_permute(const T* __restrict__ src, const uint32_t* __restrict_
 }
 
 // one lane per event: candidate test + forward scan for the consuming event
+template <bool FAST>
 __global__ void __launch_bounds__(WTPB) k_window(const shp_program* __restrict__ P, const int64_t* __restrict__ sts,
                                                  const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ perm,
                                                  int64_t n, uint32_t sentinel, const shd_cols* __restrict__ C,
@@ -59,14 +60,19 @@ __global__ void __launch_bounds__(WTPB) k_window(const shp_program* __restrict__
         uint32_t rows[2];
         rows[0] = (uint32_t)p;
         rows[1] = SHD_NULL_ROW;
-        if (!filter_pass(P, 0, rows, C, fast_ok)) continue;
+        if (FAST) {
+            if (!terms_pass2(P, 0, (uint32_t)p, SHD_NULL_ROW, C)) continue;
+        } else if (!filter_pass(P, 0, rows, C, fast_ok)) {
+            continue;
+        }
         const int64_t t0 = sts[p];
         for (int64_t q = p + 1; q < n; q++) {
             if (skeys && skeys[q] != key) break;
             const int64_t d = sts[q] - t0;
             if ((d < 0 ? -d : d) > within) break;  // expired before event q is matched
             rows[1] = (uint32_t)q;
-            if (filter_pass(P, 1, rows, C, fast_ok)) {
+            const bool pass = FAST ? terms_pass2(P, 1, (uint32_t)p, (uint32_t)q, C) : filter_pass(P, 1, rows, C, fast_ok);
+            if (pass) {
                 match_pos[p] = (int32_t)q;
                 atomicAdd(&cnt[q], 1u);  // key-segment space: neighbouring lanes hit neighbouring words
                 break;
@@ -84,6 +90,7 @@ __global__ void k_cnt_scatter(const uint32_t* __restrict__ cnt_s, const uint32_t
 
 // rank of partial p among the partials consumed by the same event (creation
 // order), then the ordered write of the selected attributes
+template <bool FAST>
 __global__ void __launch_bounds__(WTPB) k_window_place(const shp_program* __restrict__ P, const int64_t* __restrict__ sts,
                                                        const uint32_t* __restrict__ skeys,
                                                        const uint32_t* __restrict__ perm, int64_t n,
@@ -110,14 +117,15 @@ __global__ void __launch_bounds__(WTPB) k_window_place(const shp_program* __rest
         const int64_t dst = (int64_t)off[j] + rank;
         if (out_seq) out_seq[dst] = seq_base + j;
         if (out_ts) out_ts[dst] = tq;
-        uint32_t rows[2] = {(uint32_t)p, (uint32_t)q};
-        if (P->out_fast && fast_ok) {
+        if (FAST) {
             for (int o = 0; o < n_out; o++) {
                 const int sl = P->out_slot[o], at = P->out_attr[o];
-                if (out_vals) out_vals[dst * n_out + o] = load_attr(C, P->state_stream[sl], at, P->attr_type[P->state_stream[sl]][at], rows[sl]);
+                const int s = P->state_stream[sl];
+                if (out_vals) out_vals[dst * n_out + o] = load_attr(C, s, at, P->attr_type[s][at], sl ? (uint32_t)q : (uint32_t)p);
                 if (out_nulls) out_nulls[dst * n_out + o] = 0;
             }
         } else {
+            uint32_t rows[2] = {(uint32_t)p, (uint32_t)q};
             for (int o = 0; o < n_out; o++) {
                 VmVal v = vm_eval(P, P->out_pc[o], P->out_len[o], rows, C);
                 if (out_vals) out_vals[dst * n_out + o] = v.b;
@@ -155,8 +163,13 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
     hipMemsetAsync(ws->match_pos, 0xFF, n * 4, st);
     uint32_t* cnt_s = perm ? ws->cnt_s : ws->cnt;
     hipMemsetAsync(cnt_s, 0, n * 4, st);
-    hipLaunchKernelGGL(k_window, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n, sentinel,
-                       (const shd_cols*)d_sorted_desc, ws->match_pos, cnt_s, 1, ws->flag);
+    const bool fast = hprog->filter_fast[0] && hprog->filter_fast[1] && hprog->out_fast;
+    if (fast)
+        hipLaunchKernelGGL(k_window<true>, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n, sentinel,
+                           (const shd_cols*)d_sorted_desc, ws->match_pos, cnt_s, 1, ws->flag);
+    else
+        hipLaunchKernelGGL(k_window<false>, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n, sentinel,
+                           (const shd_cols*)d_sorted_desc, ws->match_pos, cnt_s, 1, ws->flag);
     if (ev_mid) hipEventRecord(ev_mid, st);
     if (perm) hipLaunchKernelGGL(k_cnt_scatter, dim3(g), dim3(WTPB), 0, st, (const uint32_t*)cnt_s, perm, n, ws->cnt);
     int rc = shd_exclusive_scan(ws->cnt, ws->off, n, scan_tmp, stream);
@@ -170,8 +183,13 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
     if (hflag) return 1;  // timestamps decrease inside a key: caller falls back
     *n_matches = (int64_t)lo + lc;
     if (*n_matches > out_cap) return 2;
-    hipLaunchKernelGGL(k_window_place, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n,
-                       (const shd_cols*)d_sorted_desc, (const int32_t*)ws->match_pos, (const uint32_t*)ws->off,
-                       b->seq_base, out_seq, out_ts, out_vals, out_nulls, 1);
+    if (fast)
+        hipLaunchKernelGGL(k_window_place<true>, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n,
+                           (const shd_cols*)d_sorted_desc, (const int32_t*)ws->match_pos, (const uint32_t*)ws->off,
+                           b->seq_base, out_seq, out_ts, out_vals, out_nulls, 1);
+    else
+        hipLaunchKernelGGL(k_window_place<false>, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n,
+                           (const shd_cols*)d_sorted_desc, (const int32_t*)ws->match_pos, (const uint32_t*)ws->off,
+                           b->seq_base, out_seq, out_ts, out_vals, out_nulls, 1);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

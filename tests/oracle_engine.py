@@ -116,3 +116,18 @@ def run_stock_oracle(compiled, ts, keys, price, vol, batch=4096, partitioned=Tru
     out = eng.drain()
     eng.close()
     return out["seq"], out["ts"], out["values"], out["nulls"]
+
+
+def run_columns_oracle(compiled, ts, cols, keys, batch=4096):
+    """Single-stream app: drive the oracle with send(Event[]) batches over the
+    given arrival-order columns; returns (seq, ts, values, nulls)."""
+    eng = OracleEngine(compiled)
+    eng.start()
+    n = len(ts)
+    for b0 in range(0, n, batch):
+        b1 = min(n, b0 + batch)
+        eng.send(0, np.ascontiguousarray(ts[b0:b1]), [np.ascontiguousarray(c[b0:b1]) for c in cols],
+                 [None] * len(cols), np.ascontiguousarray(keys[b0:b1]) if keys is not None else None, b0)
+    out = eng.drain()
+    eng.close()
+    return out["seq"], out["ts"], out["values"], out["nulls"]

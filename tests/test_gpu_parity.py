@@ -8,7 +8,7 @@ import pytest
 
 from c2_check import c2_expected
 from fixture_runner import Unsupported, check_fixture, load_fixtures, run_fixture
-from oracle_engine import OracleEngine, run_stock_oracle
+from oracle_engine import OracleEngine, run_columns_oracle, run_stock_oracle
 from siddhi_amd import SiddhiManager, compiler, synth
 
 pytestmark = pytest.mark.gpu
@@ -191,3 +191,54 @@ def test_c2_full_size_vs_vectorised_restatement(n, keys):
     assert m == len(eseq) > 0
     assert np.array_equal(oseq, eseq)
     assert np.array_equal(ovals, evals)
+
+
+def _window_case(rng):
+    """Random `every e1=S[f1] -> e2=S[f2] within W` over one stream (window engine)."""
+    f1 = rng.choice(["price > {c}f", "x < {c}", "volume >= {c}L", "price > 10.0 and x != {c}",
+                     "x % 3 == 1", "price * 2.0f > {c}f"]).format(c=rng.randint(0, 20))
+    f2 = rng.choice(["price > e1.price", "x <= e1.x", "sym == e1.sym and price < e1.price",
+                     "price > e1.price * 1.05", "x < e1.x + {c}", "volume != e1.volume and x > e1.x",
+                     "price + 1.0f > e1.price", "(x / 2) > e1.x"]).format(c=rng.randint(0, 5))
+    w = rng.choice([0, 1, 5, 40, 1000])
+    partitioned = rng.random() < 0.7
+    sel = ["e1.sym as a", "e1.price as b", "e2.price as c", "e2.volume as d", "e1.x as e"]
+    if rng.random() < 0.3:
+        sel.append("e2.x * 2 as f")
+    q = (f"@info(name = 'query1') from every e1=S[{f1}] -> e2=S[{f2}] within {w} milliseconds "
+         f"select {', '.join(sel)} insert into Out;")
+    defs = "define stream S (sym string, price float, volume long, x int); "
+    app = defs + (f"partition with (sym of S) begin {q} end;" if partitioned else q)
+    return app, partitioned
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_window_engine_vs_oracle(seed):
+    import torch
+    from siddhi_amd.device_run import DeviceRunner
+    rng = random.Random(7000 + seed)
+    app, partitioned = _window_case(rng)
+    nk = rng.choice([1, 4, 50, 300])
+    n = rng.choice([2000, 20000, 60000])
+    nprng = np.random.default_rng(seed)
+    keys = nprng.integers(0, nk, n).astype(np.int32)
+    ts = (1000 + np.cumsum(nprng.choice([0, 0, 1, 2, 3], n))).astype(np.int64)
+    price = (nprng.integers(0, 40, n) + nprng.choice([0.0, 0.5, 0.25], n)).astype(np.float32)
+    vol = nprng.integers(0, 6, n).astype(np.int64)
+    x = nprng.integers(-3, 25, n).astype(np.int32)
+    strings = compiler.StringDict()
+    for i in range(nk):
+        strings.id(f"K{i}")
+    ca = compiler.compile_app(app, strings)
+    seq, ots, vals, nulls = run_columns_oracle(ca, ts, [keys, price, vol, x], keys if partitioned else None)
+    runner = DeviceRunner(compiler.compile_app(app, strings))
+    dev = torch.device("cuda:0")
+    cols = [torch.from_numpy(c).to(dev) for c in (keys, price, vol, x)]
+    m, oseq, ovals = runner.run(torch.from_numpy(ts).to(dev), cols[0], cols, nk)
+    torch.cuda.synchronize()
+    oseq, ovals = oseq.cpu().numpy(), ovals.cpu().numpy()
+    runner.close()
+    assert m == len(seq), app
+    assert np.array_equal(oseq, seq.astype(np.int64)), app
+    nn = ~nulls.astype(bool)
+    assert np.array_equal(ovals[nn], vals[nn]), app
