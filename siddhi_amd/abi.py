@@ -107,6 +107,13 @@ def bind_product(lib):
     lib.sh_version.restype = C.c_char_p
     lib.sh_device_count.argtypes = []
     lib.sh_device_count.restype = C.c_int
+    # diagnostics of the hipRTC window kernels (not part of the reference-facing ABI)
+    lib.shx_jit_status.argtypes = [C.c_void_p]
+    lib.shx_jit_status.restype = C.c_int
+    lib.shx_jit_compile.argtypes = [C.c_void_p]
+    lib.shx_jit_compile.restype = C.c_int
+    lib.shx_jit_source.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+    lib.shx_jit_source.restype = C.c_int64
     return lib
 
 

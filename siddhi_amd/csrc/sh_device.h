@@ -87,12 +87,14 @@ int shd_emit_place(const shd_emit* em, int32_t n_out, int64_t n_events, uint32_t
                    uint32_t* scan_tmp, int64_t n_records, const shd_batch* b, uint64_t* out_seq,
                    int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, void* stream);
 // window engine for `every e1=S[f1] -> e2=S[f2] within W`: 0 ok, 1 = fall back
-// (timestamps decrease inside a key), 2 = output capacity too small, <0 error
+// (timestamps decrease inside a key), 2 = output capacity too small, <0 error;
+// `jit` (const shj_window*, sh_jit.h) selects the hipRTC-specialised kernels
+// when non-NULL, else the ahead-of-time ones
 int shd_window(const shp_program* dprog, const shp_program* hprog, const shd_batch* b, int32_t nkeys,
                const uint32_t* perm, const uint32_t* skeys, const int64_t* sts, const void* const* scols,
                shd_window_ws* ws, shd_cols* d_sorted_desc, uint32_t* scan_tmp, uint64_t* out_seq,
                int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, int64_t out_cap, int64_t* n_matches,
-               void* stream, void* ev_mid);
+               void* stream, void* ev_mid, const void* jit);
 int shd_relayout(const uint8_t* src, const shp_layout* A, uint8_t* dst, const shp_layout* B, int32_t nkeys,
                  int32_t n_states, int32_t n_out, void* stream);
 int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, void* stream);

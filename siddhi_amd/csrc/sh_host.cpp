@@ -16,6 +16,7 @@
 
 #include "../../include/siddhi_hip.h"
 #include "sh_device.h"
+#include "sh_jit.h"
 
 #define SH_VERSION_STR "siddhi_hip 0.1 (gfx950)"
 
@@ -338,6 +339,10 @@ struct sh_handle {
     int64_t o_read = 0;
     sh_kernel_times times{};
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // hipRTC-specialised window kernels (sh_jit.cpp): 0 untried, 1 loaded, <0 unavailable
+    int jit_state = 0;
+    shj_window jit{};
+    std::string jit_err;
 };
 
 static void set_layout(shp_layout& Y, const shp_program& P, int32_t cap) {
@@ -955,9 +960,18 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
         const int64_t* sts = sorted ? h->v_sts.as<int64_t>() : run->d_ts;
         const void* scols[32];
         for (int a = 0; a < na; a++) scols[a] = sorted ? (const void*)h->v_scol[a].p : run->d_cols[a];
+        if (h->jit_state == 0) {
+            if (getenv("SH_DISABLE_JIT")) {
+                h->jit_state = -1;
+                h->jit_err = "disabled by SH_DISABLE_JIT";
+            } else {
+                h->jit_state = shj_window_load(&h->prog, &h->jit, &h->jit_err) == 0 ? 1 : -1;
+            }
+        }
         int wrc = shd_window(h->d_prog.as<shp_program>(), &h->prog, &B, nkeys, perm, skeys, sts, scols, &wws,
                              h->d_cols_desc.as<shd_cols>(), h->w_scan.as<uint32_t>(), run->d_out_seq, nullptr,
-                             run->d_out_values, nullptr, run->out_capacity, &nm, st, h->ev[2]);
+                             run->d_out_values, nullptr, run->out_capacity, &nm, st, h->ev[2],
+                             h->jit_state == 1 ? &h->jit : nullptr);
         hipEventRecord(h->ev[3], st);
         if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in window engine");
         if (wrc < 0) return fail(h, SH_E_HIP, "window engine launch failed");
@@ -977,6 +991,30 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
                        &nm, true);
     run->out_count = nm;
     return rc;
+}
+
+// ---- diagnostics of the hipRTC path (not part of the reference-facing ABI)
+int shx_jit_status(sh_handle* h) { return h ? h->jit_state : 0; }
+
+// compile-only check of the specialised kernels (no device needed)
+int shx_jit_compile(sh_handle* h) {
+    if (!h) return SH_E_INVALID_ARG;
+    shj_window w;
+    std::string err;
+    if (!h->prog.window_ok) return fail(h, SH_E_UNSUPPORTED, "not a window-shaped program");
+    if (shj_window_compile(&h->prog, &w, &err)) return fail(h, SH_E_HIP, err);
+    return SH_OK;
+}
+
+int64_t shx_jit_source(sh_handle* h, char* buf, int64_t len) {
+    std::string src;
+    if (!h || shj_window_source(&h->prog, &src)) return -1;
+    if (buf && len > 0) {
+        const int64_t k = std::min<int64_t>(len - 1, (int64_t)src.size());
+        memcpy(buf, src.data(), k);
+        buf[k] = 0;
+    }
+    return (int64_t)src.size();
 }
 
 int sh_last_kernel_times(sh_handle* h, sh_kernel_times* t) {

@@ -19,6 +19,7 @@
 
 #include "../../include/sh_query.h"
 #include "sh_device.h"
+#include "sh_jit.h"
 #include "sh_vm.h"
 
 #include <string.h>
@@ -149,7 +150,8 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
                           const uint32_t* perm, const uint32_t* skeys, const int64_t* sts, const void* const* scols,
                           shd_window_ws* ws, shd_cols* d_sorted_desc, uint32_t* scan_tmp, uint64_t* out_seq,
                           int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, int64_t out_cap,
-                          int64_t* n_matches, void* stream, void* ev_mid_) {
+                          int64_t* n_matches, void* stream, void* ev_mid_, const void* jit_) {
+    const shj_window* jit = (const shj_window*)jit_;
     hipEvent_t ev_mid = (hipEvent_t)ev_mid_;
     hipStream_t st = (hipStream_t)stream;
     const int64_t n = b->n;
@@ -164,7 +166,16 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
     uint32_t* cnt_s = perm ? ws->cnt_s : ws->cnt;
     hipMemsetAsync(cnt_s, 0, n * 4, st);
     const bool fast = hprog->filter_fast[0] && hprog->filter_fast[1] && hprog->out_fast;
-    if (fast)
+    uint32_t tiles_per_xcd = 0, ntiles = 0;
+    const unsigned jg = shj_tiles(n, &tiles_per_xcd, &ntiles);
+    if (jit) {
+        const shd_cols* dc = d_sorted_desc;
+        void* args[] = {(void*)&sts, (void*)&skeys, (void*)&n, (void*)&sentinel, (void*)&dc, (void*)&ws->match_pos,
+                        (void*)&cnt_s, (void*)&ws->flag, (void*)&tiles_per_xcd, (void*)&ntiles};
+        if (hipModuleLaunchKernel((hipFunction_t)jit->match, jg, 1, 1, shj_tile_size(), 1, 1, 0, st, args, nullptr) !=
+            hipSuccess)
+            return -3;
+    } else if (fast)
         hipLaunchKernelGGL(k_window<true>, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n, sentinel,
                            (const shd_cols*)d_sorted_desc, ws->match_pos, cnt_s, 1, ws->flag);
     else
@@ -183,7 +194,18 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
     if (hflag) return 1;  // timestamps decrease inside a key: caller falls back
     *n_matches = (int64_t)lo + lc;
     if (*n_matches > out_cap) return 2;
-    if (fast)
+    if (jit) {
+        const shd_cols* dc = d_sorted_desc;
+        const int32_t* mp = ws->match_pos;
+        const uint32_t* off = ws->off;
+        uint64_t seq_base = b->seq_base;
+        void* args[] = {(void*)&sts,     (void*)&skeys,    (void*)&perm,    (void*)&n,         (void*)&dc,
+                        (void*)&mp,      (void*)&off,      (void*)&seq_base, (void*)&out_seq,  (void*)&out_ts,
+                        (void*)&out_vals, (void*)&out_nulls, (void*)&tiles_per_xcd, (void*)&ntiles};
+        if (hipModuleLaunchKernel((hipFunction_t)jit->place, jg, 1, 1, shj_tile_size(), 1, 1, 0, st, args, nullptr) !=
+            hipSuccess)
+            return -3;
+    } else if (fast)
         hipLaunchKernelGGL(k_window_place<true>, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n,
                            (const shd_cols*)d_sorted_desc, (const int32_t*)ws->match_pos, (const uint32_t*)ws->off,
                            b->seq_base, out_seq, out_ts, out_vals, out_nulls, 1);

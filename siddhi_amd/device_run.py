@@ -49,5 +49,12 @@ class DeviceRunner:
         lib().sh_last_kernel_times(self.handle.h, C.byref(t))
         return dict(segment_ms=t.segment_ms, advance_ms=t.advance_ms, emit_ms=t.emit_ms, total_ms=t.total_ms)
 
+    def jit_status(self):
+        """1: hipRTC-specialised window kernels ran, -1: ahead-of-time kernels, 0: not tried."""
+        return lib().shx_jit_status(self.handle.h)
+
+    def last_error(self):
+        return lib().sh_last_error(self.handle.h).decode()
+
     def close(self):
         self.handle.close()

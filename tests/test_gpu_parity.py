@@ -9,6 +9,7 @@ import pytest
 from c2_check import c2_expected
 from fixture_runner import Unsupported, check_fixture, load_fixtures, run_fixture
 from oracle_engine import OracleEngine, run_columns_oracle, run_stock_oracle
+from window_cases import window_case
 from siddhi_amd import SiddhiManager, compiler, synth
 
 pytestmark = pytest.mark.gpu
@@ -193,31 +194,16 @@ def test_c2_full_size_vs_vectorised_restatement(n, keys):
     assert np.array_equal(ovals, evals)
 
 
-def _window_case(rng):
-    """Random `every e1=S[f1] -> e2=S[f2] within W` over one stream (window engine)."""
-    f1 = rng.choice(["price > {c}f", "x < {c}", "volume >= {c}L", "price > 10.0 and x != {c}",
-                     "x % 3 == 1", "price * 2.0f > {c}f"]).format(c=rng.randint(0, 20))
-    f2 = rng.choice(["price > e1.price", "x <= e1.x", "sym == e1.sym and price < e1.price",
-                     "price > e1.price * 1.05", "x < e1.x + {c}", "volume != e1.volume and x > e1.x",
-                     "price + 1.0f > e1.price", "(x / 2) > e1.x"]).format(c=rng.randint(0, 5))
-    w = rng.choice([0, 1, 5, 40, 1000])
-    partitioned = rng.random() < 0.7
-    sel = ["e1.sym as a", "e1.price as b", "e2.price as c", "e2.volume as d", "e1.x as e"]
-    if rng.random() < 0.3:
-        sel.append("e2.x * 2 as f")
-    q = (f"@info(name = 'query1') from every e1=S[{f1}] -> e2=S[{f2}] within {w} milliseconds "
-         f"select {', '.join(sel)} insert into Out;")
-    defs = "define stream S (sym string, price float, volume long, x int); "
-    app = defs + (f"partition with (sym of S) begin {q} end;" if partitioned else q)
-    return app, partitioned
-
-
+@pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
 @pytest.mark.parametrize("seed", range(24))
-def test_window_engine_vs_oracle(seed):
+def test_window_engine_vs_oracle(seed, jit, monkeypatch):
+    """hipRTC-specialised kernels (sh_jit.cpp) and the ahead-of-time ones."""
     import torch
     from siddhi_amd.device_run import DeviceRunner
+    if not jit:
+        monkeypatch.setenv("SH_DISABLE_JIT", "1")
     rng = random.Random(7000 + seed)
-    app, partitioned = _window_case(rng)
+    app, partitioned = window_case(rng)
     nk = rng.choice([1, 4, 50, 300])
     n = rng.choice([2000, 20000, 60000])
     nprng = np.random.default_rng(seed)
@@ -236,6 +222,7 @@ def test_window_engine_vs_oracle(seed):
     cols = [torch.from_numpy(c).to(dev) for c in (keys, price, vol, x)]
     m, oseq, ovals = runner.run(torch.from_numpy(ts).to(dev), cols[0], cols, nk)
     torch.cuda.synchronize()
+    assert runner.jit_status() == (1 if jit else -1), runner.last_error()
     oseq, ovals = oseq.cpu().numpy(), ovals.cpu().numpy()
     runner.close()
     assert m == len(seq), app

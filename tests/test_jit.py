@@ -1,0 +1,57 @@
+"""hipRTC code generation of the window kernels (sh_jit.cpp), checked on the CPU:
+the specialised source is generated and compiles for gfx950 for the C2 query and
+for the random window-engine queries the GPU parity tests run."""
+import ctypes as C
+import random
+
+import pytest
+
+from siddhi_amd import abi, build, compiler, synth
+from window_cases import window_case
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return abi.bind_product(C.CDLL(build.build()))
+
+
+def _handle(lib, text, strings=None):
+    d = compiler.compile_app(text, strings).descriptor()
+    h = C.c_void_p()
+    assert lib.sh_compile(C.byref(d), C.byref(h)) == abi.SH_OK, lib.sh_last_error(h)
+    return h
+
+
+def _source(lib, h):
+    n = lib.shx_jit_source(h, None, 0)
+    assert n > 0
+    buf = C.create_string_buffer(n + 1)
+    lib.shx_jit_source(h, buf, n + 1)
+    return buf.value.decode()
+
+
+def test_c2_specialised_source(lib):
+    h = _handle(lib, synth.C2_QUERY)
+    src = _source(lib, h)
+    # partition-key tautology `symbol == e1.symbol` folded: only price staged
+    assert "s_c1[SHJ_SPAN]" in src and "s_c0[" not in src
+    assert "vm_cmp(7, 2," in src  # price > ... compared in the float domain
+    assert lib.shx_jit_compile(h) == abi.SH_OK, lib.sh_last_error(h)
+    lib.sh_destroy(h)
+
+
+def test_non_window_shape_has_no_source(lib):
+    h = _handle(lib, "define stream S (a int); from e1=S[a > 1] -> e2=S[a > e1.a] -> e3=S[a > e2.a] "
+                     "select e1.a as x insert into Out;")
+    assert lib.shx_jit_source(h, None, 0) == -1
+    assert lib.shx_jit_compile(h) == abi.SH_E_UNSUPPORTED
+    lib.sh_destroy(h)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_window_queries_compile(lib, seed):
+    app, _ = window_case(random.Random(7000 + seed))
+    strings = compiler.StringDict()
+    h = _handle(lib, app, strings)
+    assert lib.shx_jit_compile(h) == abi.SH_OK, (app, lib.sh_last_error(h))
+    lib.sh_destroy(h)
