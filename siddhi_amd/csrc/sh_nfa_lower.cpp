@@ -1,0 +1,566 @@
+// sh_nfa_lower.cpp — lowers an sh_app_desc (the query-api StateElement trees)
+// into the general engine's NFA table (sh_nfa.h). Restates, per query,
+// StateInputStreamParser.parseInputStream / parse
+// (core/util/parser/StateInputStreamParser.java:76-408):
+//   - one receiver per stream: Single if the stream feeds one state, Multi(k)
+//     otherwise, eventSequence = slots in reverse (:91-110);
+//   - parse() builds the pre/post processor graph: Next links post -> next pre
+//     (NextStateElement), Every links the last post back to the first pre and sets
+//     withinEvery on the whole sub-tree, Logical creates a partner pair and parses
+//     element 2 before element 1 (:350-361), Count wraps a stream state;
+//   - StateStreamRuntime.setCommonProcessor: root first's thisLast = root last,
+//     setQuerySelector, then setup() wires receivers (StateStreamRuntime.java:38-98);
+//   - InnerStateRuntime init/reset/update orders (state/runtime/*.java) become flat
+//     sequences of pre-state ids.
+// Pure host C++: linked into libsiddhi_hip.so (sh_compile) and into the CPU test
+// harness tests/nfa_host.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "sh_nfa.h"
+#include "sh_nfa_lower.h"
+
+namespace {
+
+struct LProc {
+    int kind = NF_K_STREAM;
+    int stateId = -1;
+    bool isStart = false;
+    int stream = -1;
+    int withinEvery = -1;
+    int thisLast = -1;   // proc id
+    int partner = -1;    // proc id
+    int ltype = 0;
+    int nextPre = -1, nextEveryPre = -1, callbackPre = -1;
+    bool toSel = false;
+    int minc = 0, maxc = 0;
+    int64_t waiting = -1;
+    int filter = -1;
+};
+
+struct LInner {
+    enum { BASIC, NEXT, EVERY, LOGICAL } type = BASIC;
+    int first = -1, last = -1;  // proc ids
+    LInner* a = nullptr;        // NEXT: cur, EVERY: in, LOGICAL: in1
+    LInner* b = nullptr;        // NEXT: nxt, LOGICAL: in2
+    std::vector<std::pair<int, int>> ssr;  // (stream, proc)
+};
+
+struct QueryLowering {
+    const sh_app_desc* app;
+    const sh_query_desc* q;
+    nf_table* T;
+    nf_query* Q;
+    std::string err;
+    std::vector<LProc> procs;
+    std::vector<std::unique_ptr<LInner>> inners;
+    std::vector<int> pres;       // parse order
+    std::vector<int> startup;    // absent pres
+    int slotCounter = 0;
+    std::map<int, int> uses;     // stream -> states fed
+
+    LInner* newInner() {
+        inners.emplace_back(new LInner());
+        return inners.back().get();
+    }
+    int newProc(int kind) {
+        procs.emplace_back();
+        procs.back().kind = kind;
+        return (int)procs.size() - 1;
+    }
+    // setNextStatePre (StreamPost / CountPost / LogicalPost)
+    void setNextStatePre(int post, int p) {
+        LProc& o = procs[post];
+        o.nextPre = p;
+        if (o.kind == NF_K_COUNT) {
+            if (o.isStart && q->state_type == SH_SEQUENCE && o.minc == 0) procs[p].callbackPre = post;
+        } else if (o.kind == NF_K_LOGICAL) {
+            procs[o.partner].nextPre = p;
+        }
+    }
+    void setNextEveryStatePre(int post, int p) {
+        LProc& o = procs[post];
+        o.nextEveryPre = p;
+        if (o.kind == NF_K_LOGICAL) procs[o.partner].nextEveryPre = p;
+    }
+
+    LInner* parse(int ei, int pre, std::vector<int>& list, bool isStart) {
+        if (ei < 0 || ei >= q->n_elems) {
+            err = "bad state element index";
+            return nullptr;
+        }
+        const sh_state_elem& e = q->elems[ei];
+        switch (e.kind) {
+            case SH_E_STREAM:
+            case SH_E_ABSENT_STREAM: {
+                if (e.stream < 0 || e.stream >= app->n_streams) {
+                    err = "bad stream index";
+                    return nullptr;
+                }
+                const int stateIndex = slotCounter++;
+                if (stateIndex != e.slot) {
+                    err = "slot mismatch between descriptor and parse order";
+                    return nullptr;
+                }
+                if (pre < 0) {
+                    if (e.kind == SH_E_ABSENT_STREAM) {
+                        pre = newProc(NF_K_ABSENT);
+                        procs[pre].waiting = e.waiting_ms;
+                        startup.push_back(pre);
+                    } else {
+                        pre = newProc(NF_K_STREAM);
+                    }
+                } else if (e.kind == SH_E_ABSENT_STREAM) {
+                    err = "device engine: absent states inside count / logical (AbsentLogicalPreStateProcessor) "
+                          "are not lowered";
+                    return nullptr;
+                }
+                LProc& P = procs[pre];
+                P.stateId = stateIndex;
+                P.isStart = isStart;
+                P.stream = e.stream;
+                P.filter = e.filter;
+                P.thisLast = pre;
+                uses[e.stream]++;
+                LInner* in = newInner();
+                in->first = in->last = pre;
+                in->ssr.push_back({e.stream, pre});
+                list.push_back(pre);
+                return in;
+            }
+            case SH_E_NEXT: {
+                LInner* cur = parse(e.child0, -1, list, isStart);
+                if (!cur) return nullptr;
+                LInner* nxt = parse(e.child1, -1, list, false);
+                if (!nxt) return nullptr;
+                setNextStatePre(cur->last, nxt->first);
+                LInner* ni = newInner();
+                ni->type = LInner::NEXT;
+                ni->a = cur;
+                ni->b = nxt;
+                ni->first = cur->first;
+                ni->last = nxt->last;
+                ni->ssr = cur->ssr;
+                ni->ssr.insert(ni->ssr.end(), nxt->ssr.begin(), nxt->ssr.end());
+                return ni;
+            }
+            case SH_E_EVERY: {
+                std::vector<int> wl;
+                LInner* in = parse(e.child0, -1, wl, isStart);
+                if (!in) return nullptr;
+                LInner* ev = newInner();
+                ev->type = LInner::EVERY;
+                ev->a = in;
+                ev->first = in->first;
+                ev->last = in->last;
+                ev->ssr = in->ssr;
+                setNextEveryStatePre(ev->last, ev->first);
+                for (int p : wl) procs[p].withinEvery = ev->first;
+                list.insert(list.end(), wl.begin(), wl.end());
+                return ev;
+            }
+            case SH_E_LOGICAL_AND:
+            case SH_E_LOGICAL_OR: {
+                if (e.child0 < 0 || e.child1 < 0) {
+                    err = "bad logical element";
+                    return nullptr;
+                }
+                const sh_state_elem& e1 = q->elems[e.child0];
+                const sh_state_elem& e2 = q->elems[e.child1];
+                if (e1.kind == SH_E_ABSENT_STREAM || e2.kind == SH_E_ABSENT_STREAM) {
+                    err = "device engine: logical absent states (AbsentLogicalPreStateProcessor) are not lowered";
+                    return nullptr;
+                }
+                const int p1 = newProc(NF_K_LOGICAL);
+                const int p2 = newProc(NF_K_LOGICAL);
+                procs[p1].ltype = procs[p2].ltype = e.kind;
+                procs[p1].partner = p2;
+                procs[p2].partner = p1;
+                LInner* in2 = parse(e.child1, p2, list, isStart);
+                if (!in2) return nullptr;
+                LInner* in1 = parse(e.child0, p1, list, isStart);
+                if (!in1) return nullptr;
+                LInner* li = newInner();
+                li->type = LInner::LOGICAL;
+                li->a = in1;
+                li->b = in2;
+                li->first = in1->first;
+                li->last = in2->last;
+                li->ssr = in2->ssr;
+                li->ssr.insert(li->ssr.end(), in1->ssr.begin(), in1->ssr.end());
+                return li;
+            }
+            case SH_E_COUNT: {
+                const int cp = newProc(NF_K_COUNT);
+                procs[cp].minc = e.min_count == SH_ANY ? 0 : e.min_count;
+                procs[cp].maxc = e.max_count == SH_ANY ? INT32_MAX : e.max_count;
+                LInner* in = parse(e.child0, cp, list, isStart);
+                if (!in) return nullptr;
+                LInner* ci = newInner();  // CountInnerStateRuntime: same first / last / ssr
+                ci->first = in->first;
+                ci->last = in->last;
+                ci->ssr = in->ssr;
+                return ci;
+            }
+        }
+        err = "unknown state element";
+        return nullptr;
+    }
+
+    // InnerStateRuntime orders
+    void initSeq(LInner* n, std::vector<int>& out) {
+        switch (n->type) {
+            case LInner::NEXT:
+                initSeq(n->a, out);
+                initSeq(n->b, out);
+                return;
+            case LInner::EVERY: initSeq(n->a, out); return;
+            case LInner::LOGICAL:
+                initSeq(n->b, out);
+                initSeq(n->a, out);
+                return;
+            default: out.push_back(n->first);
+        }
+    }
+    void resetSeq(LInner* n, std::vector<int>& out) {
+        switch (n->type) {
+            case LInner::NEXT:
+                resetSeq(n->b, out);
+                resetSeq(n->a, out);
+                return;
+            case LInner::LOGICAL: resetSeq(n->b, out); return;
+            default: out.push_back(n->first);  // Every inherits: first processor only
+        }
+    }
+    void updateSeq(LInner* n, std::vector<int>& out) {
+        switch (n->type) {
+            case LInner::NEXT:
+                updateSeq(n->a, out);
+                updateSeq(n->b, out);
+                return;
+            case LInner::LOGICAL: updateSeq(n->b, out); return;
+            default: out.push_back(n->first);
+        }
+    }
+    void setQuerySelector(LInner* n) {
+        switch (n->type) {
+            case LInner::NEXT: setQuerySelector(n->b); return;
+            case LInner::EVERY: setQuerySelector(n->a); return;
+            case LInner::LOGICAL:
+                setQuerySelector(n->b);
+                setQuerySelector(n->a);
+                return;
+            default: procs[n->last].toSel = true;
+        }
+    }
+    // setup(): receiver.setNext(first) + stateProcessorsForStream
+    void setup(LInner* n, std::vector<std::pair<int, int>>& order) {
+        switch (n->type) {
+            case LInner::NEXT:
+                setup(n->a, order);
+                setup(n->b, order);
+                return;
+            case LInner::EVERY: setup(n->a, order); return;
+            case LInner::LOGICAL:
+                setup(n->b, order);
+                setup(n->a, order);
+                return;
+            default: order.push_back(n->ssr[0]);
+        }
+    }
+
+    // ---------------------------------------------------------- expressions
+    int add_const(int64_t v, int type, int isnull) {
+        for (int i = 0; i < T->n_const; i++)
+            if (T->consts[i] == v && T->const_type[i] == type && T->const_null[i] == isnull) return i;
+        if (T->n_const >= NF_MAX_CONST) {
+            err = "too many constants";
+            return -1;
+        }
+        T->consts[T->n_const] = v;
+        T->const_type[T->n_const] = (uint8_t)type;
+        T->const_null[T->n_const] = (uint8_t)isnull;
+        return T->n_const++;
+    }
+    bool emit(uint8_t op, uint8_t a, uint8_t b, uint8_t c, int32_t x) {
+        if (T->n_code >= NF_MAX_CODE) {
+            err = "expression programs too long";
+            return false;
+        }
+        shp_instr& in = T->code[T->n_code++];
+        in.op = op;
+        in.a = a;
+        in.b = b;
+        in.c = c;
+        in.x = x;
+        return true;
+    }
+    static int dom_for(int op, int lt, int rt) {
+        if (lt == SH_T_STRING || rt == SH_T_STRING) return DOM_STR;
+        if (lt == SH_T_BOOL || rt == SH_T_BOOL) return DOM_BOOL;
+        auto rk = [](int t) {
+            switch (t) {
+                case SH_T_INT: return 0;
+                case SH_T_LONG: return 1;
+                case SH_T_FLOAT: return 2;
+                default: return 3;
+            }
+        };
+        int r = std::max(rk(lt), rk(rt));
+        bool fl = (lt == SH_T_FLOAT && rt == SH_T_LONG) || (lt == SH_T_LONG && rt == SH_T_FLOAT);
+        if ((op == SH_OP_EQ || op == SH_OP_NE) && fl) r = 3;
+        return r == 0 ? DOM_I32 : r == 1 ? DOM_I64 : r == 2 ? DOM_F32 : DOM_F64;
+    }
+    int max_depth = 0;
+    bool gen(int e, int depth) {
+        if (e < 0 || e >= q->n_exprs) {
+            err = "bad expression index";
+            return false;
+        }
+        if (depth > NF_STACK - 2) {
+            err = "expression too deep";
+            return false;
+        }
+        const sh_expr& x = q->exprs[e];
+        switch (x.op) {
+            case SH_OP_CONST: {
+                int c = add_const(x.cval, x.type, x.is_null);
+                return c >= 0 && emit(OPC_CONST, 0, 0, 0, c);
+            }
+            case SH_OP_VAR:
+                if (x.slot < 0 || x.slot >= q->n_slots) {
+                    err = "variable slot out of range";
+                    return false;
+                }
+                if (x.type == SH_T_OBJECT) {
+                    err = "device engine: object attributes are not lowered";
+                    return false;
+                }
+                return emit(OPC_VAR, (uint8_t)x.slot, (uint8_t)x.attr, (uint8_t)x.type, x.chain);
+            case SH_OP_IS_NULL_STREAM: return emit(OPC_ISNULL_STREAM, (uint8_t)x.slot, 0, 0, x.chain);
+            case SH_OP_NOT: return gen(x.lhs, depth + 1) && emit(OPC_NOT, 0, 0, 0, 0);
+            case SH_OP_BOOL_VAR: return gen(x.lhs, depth + 1) && emit(OPC_BOOLV, 0, 0, 0, 0);
+            case SH_OP_IS_NULL: return gen(x.lhs, depth + 1) && emit(OPC_ISNULL, 0, 0, 0, 0);
+            case SH_OP_AND:
+            case SH_OP_OR:
+                return gen(x.lhs, depth + 1) && gen(x.rhs, depth + 2) &&
+                       emit(x.op == SH_OP_AND ? OPC_AND : OPC_OR, 0, 0, 0, 0);
+            case SH_OP_EQ:
+            case SH_OP_NE:
+            case SH_OP_GT:
+            case SH_OP_GE:
+            case SH_OP_LT:
+            case SH_OP_LE: {
+                int lt = q->exprs[x.lhs].type, rt = q->exprs[x.rhs].type;
+                return gen(x.lhs, depth + 1) && gen(x.rhs, depth + 2) &&
+                       emit(OPC_CMP, (uint8_t)x.op, (uint8_t)dom_for(x.op, lt, rt), 0, 0);
+            }
+            case SH_OP_ADD:
+            case SH_OP_SUB:
+            case SH_OP_MUL:
+            case SH_OP_DIV:
+            case SH_OP_MOD:
+                return gen(x.lhs, depth + 1) && gen(x.rhs, depth + 2) &&
+                       emit(OPC_ARITH, (uint8_t)x.op, (uint8_t)x.type, 0, 0);
+            case SH_OP_IF_THEN_ELSE:
+                return gen(x.lhs, depth + 1) && gen(x.rhs, depth + 2) && gen(x.third, depth + 3) &&
+                       emit(OPC_SELECT, 0, 0, 0, 0) && emit(OPC_CAST, 0, (uint8_t)x.type, 0, 0);
+        }
+        err = "unsupported expression operator";
+        return false;
+    }
+
+    bool run() {
+        memset(Q, 0, sizeof(*Q));
+        Q->state_type = q->state_type;
+        Q->within = q->within_ms;
+        if (q->n_slots < 1 || q->n_slots > NF_MAX_PROC) {
+            err = "device engine: 1..16 states per query";
+            return false;
+        }
+        // receivers: count stream uses first (a pre-pass over the element list)
+        std::map<int, int> suse;
+        for (int i = 0; i < q->n_elems; i++)
+            if (q->elems[i].kind == SH_E_STREAM || q->elems[i].kind == SH_E_ABSENT_STREAM) suse[q->elems[i].stream]++;
+        std::vector<int> list;
+        LInner* root = parse(q->root, -1, list, true);
+        if (!root) return false;
+        if ((int)procs.size() != q->n_slots || slotCounter != q->n_slots) {
+            err = "state count mismatch";
+            return false;
+        }
+        // proc id -> state id
+        std::vector<int> sid(procs.size());
+        for (size_t i = 0; i < procs.size(); i++) sid[i] = procs[i].stateId;
+        auto S = [&](int p) { return p < 0 ? -1 : sid[p]; };
+        procs[root->first].thisLast = root->last;
+        setQuerySelector(root);
+        if (q->within_ms >= 0)
+            for (auto& P : procs)
+                if (P.isStart) Q->start_ids[Q->n_start++] = (int8_t)P.stateId;
+        std::vector<std::pair<int, int>> order;
+        setup(root, order);
+        for (auto& kv : suse) {
+            nf_receiver& R = Q->recv[kv.first];
+            R.present = 1;
+            R.n_next = (int8_t)kv.second;
+            R.multi = kv.second > 1;
+            for (int i = 0; i < NF_MAX_PROC; i++) R.next_procs[i] = -1;
+            for (int i = 0; i < kv.second; i++) R.event_seq[i] = (int8_t)(kv.second - 1 - i);
+        }
+        for (auto& sp : order) {
+            nf_receiver& R = Q->recv[sp.first];
+            const int p = sp.second;
+            if (R.multi) {
+                for (int i = 0; i < R.n_next; i++)
+                    if (R.next_procs[i] < 0) {
+                        R.next_procs[i] = (int8_t)S(p);
+                        break;
+                    }
+                R.has_selector = procs[p].toSel;
+            } else {
+                R.next_procs[0] = (int8_t)S(p);
+                R.has_selector = procs[procs[p].thisLast].toSel;
+            }
+            R.for_stream[R.n_for++] = (int8_t)S(p);
+        }
+        std::vector<int> seq;
+        initSeq(root, seq);
+        Q->n_init = (int)seq.size();
+        for (size_t i = 0; i < seq.size(); i++) Q->init_seq[i] = (int8_t)S(seq[i]);
+        seq.clear();
+        resetSeq(root, seq);
+        Q->n_reset = (int)seq.size();
+        for (size_t i = 0; i < seq.size(); i++) Q->reset_seq[i] = (int8_t)S(seq[i]);
+        seq.clear();
+        updateSeq(root, seq);
+        Q->n_update = (int)seq.size();
+        for (size_t i = 0; i < seq.size(); i++) Q->update_seq[i] = (int8_t)S(seq[i]);
+        Q->n_startup = (int)startup.size();
+        for (size_t i = 0; i < startup.size(); i++) Q->startup[i] = (int8_t)S(startup[i]);
+        Q->n_proc = (int)procs.size();
+        for (auto& P : procs) {
+            nf_proc& D = Q->proc[P.stateId];
+            D.kind = (int8_t)P.kind;
+            D.is_start = P.isStart;
+            D.stream = (int8_t)P.stream;
+            D.within_every = (int8_t)S(P.withinEvery);
+            D.this_last = (int8_t)S(P.thisLast);
+            D.partner = (int8_t)S(P.partner);
+            D.logical_type = (int8_t)P.ltype;
+            D.next_pre = (int8_t)S(P.nextPre);
+            D.next_every_pre = (int8_t)S(P.nextEveryPre);
+            D.callback_pre = (int8_t)S(P.callbackPre);
+            D.to_selector = P.toSel;
+            D.min_count = P.minc;
+            D.max_count = P.maxc;
+            D.waiting = P.waiting;
+            Q->slot_stream[P.stateId] = (int8_t)P.stream;
+            if (P.filter >= 0) {
+                D.filter_pc = T->n_code;
+                if (!gen(P.filter, 0)) return false;
+                D.filter_len = T->n_code - D.filter_pc;
+            } else {
+                D.filter_pc = -1;
+                D.filter_len = 0;
+            }
+        }
+        if (q->n_outputs > NF_MAX_OUT) {
+            err = "device engine: at most 16 output attributes";
+            return false;
+        }
+        Q->n_out = q->n_outputs;
+        for (int o = 0; o < q->n_outputs; o++) {
+            const sh_output_attr& oa = q->outputs[o];
+            Q->out_agg[o] = oa.agg;
+            Q->out_type[o] = oa.type;
+            if (oa.agg != SH_AGG_NONE) Q->contains_agg = 1;
+            if (oa.expr >= 0) {
+                Q->out_pc[o] = T->n_code;
+                if (!gen(oa.expr, 0)) return false;
+                Q->out_len[o] = T->n_code - Q->out_pc[o];
+            } else {
+                Q->out_pc[o] = -1;
+                Q->out_len[o] = 0;
+            }
+        }
+        return true;
+    }
+};
+
+}  // namespace
+
+int nf_lower(const sh_app_desc* app, nf_table* T, std::string* err) {
+    memset(T, 0, sizeof(*T));
+    if (app->n_queries < 1 || app->n_queries > NF_MAX_QUERIES) {
+        *err = "device engine: 1..16 queries per app";
+        return -1;
+    }
+    if (app->n_streams < 1 || app->n_streams > NF_MAX_STREAMS) {
+        *err = "device engine: 1..8 streams per app";
+        return -1;
+    }
+    T->n_queries = app->n_queries;
+    T->n_streams = app->n_streams;
+    T->playback = app->playback;
+    for (int s = 0; s < app->n_streams; s++) {
+        if (app->streams[s].n_attrs > NF_MAX_ATTRS) {
+            *err = "device engine: at most 32 attributes per stream";
+            return -1;
+        }
+        T->stream_nattr[s] = app->streams[s].n_attrs;
+        for (int a = 0; a < app->streams[s].n_attrs; a++) T->attr_type[s][a] = (int8_t)app->streams[s].attr_types[a];
+    }
+    // every query in partition 0, or every query unpartitioned
+    int np = 0, nu = 0;
+    for (int i = 0; i < app->n_queries; i++) {
+        if (app->queries[i].partition == 0)
+            np++;
+        else if (app->queries[i].partition < 0)
+            nu++;
+    }
+    if (np + nu != app->n_queries || (np && nu)) {
+        *err = "device engine: all queries in one partition, or none partitioned";
+        return -1;
+    }
+    T->partitioned = np > 0;
+    for (int i = 0; i < app->n_queries; i++) {
+        QueryLowering L;
+        L.app = app;
+        L.q = &app->queries[i];
+        L.T = T;
+        L.Q = &T->q[i];
+        if (!L.run()) {
+            *err = "query " + std::to_string(i) + ": " + L.err;
+            return -1;
+        }
+        if (T->partitioned) {
+            for (int p = 0; p < T->q[i].n_proc; p++) {
+                const int s = T->q[i].proc[p].stream;
+                if (!app->partition_streams[s]) {
+                    *err = "device engine: every stream of a partitioned query must be keyed";
+                    return -1;
+                }
+            }
+        }
+        for (int p = 0; p < T->q[i].n_proc; p++)
+            if (T->q[i].proc[p].kind == NF_K_ABSENT) T->has_absent = 1;
+    }
+    nf_set_caps(T, 16, 32, 64, 32, 8);
+    return 0;
+}
+
+void nf_set_caps(nf_table* T, int list_cap, int se_cap, int node_cap, int hold_cap, int sched_cap) {
+    int64_t w = 1;  // key header word: bit 0 = partition seen (initPartition done)
+    for (int i = 0; i < T->n_queries; i++) {
+        nf_query& Q = T->q[i];
+        nf_set_layout(Q, Q.n_proc, list_cap, se_cap, node_cap, hold_cap, sched_cap);
+        Q.q_off = w;
+        w += Q.lay.words;
+    }
+    T->key_words = w;
+}

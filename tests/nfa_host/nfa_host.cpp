@@ -1,0 +1,396 @@
+// nfa_host.cpp — TEST INFRASTRUCTURE: the general engine's per-key logic
+// (siddhi_amd/csrc/sh_nfa.h, the code k_nfa runs on the GPU) compiled for the
+// CPU, driven exactly like sh_host.cpp drives k_nfa: each flush is segmented by
+// key (stable), one NfLane walks each key segment, emissions are ordered by
+// their (run index, ordinal) tag, playback timers run the same selection rule.
+// tests/ use it to diff the kernel logic against the oracle without a GPU. The
+// product (libsiddhi_hip.so) never runs this code on the host.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../siddhi_amd/csrc/sh_nfa.h"
+#include "../../siddhi_amd/csrc/sh_nfa_lower.h"
+#include "../../include/siddhi_hip.h"
+
+namespace {
+
+struct HostSink {
+    std::vector<uint64_t> recs;
+    int words = 0;
+    uint64_t* slot(int w) {
+        words = w;
+        recs.resize(recs.size() + w);
+        return recs.data() + recs.size() - w;
+    }
+};
+
+struct Ev {
+    int64_t ts;
+    uint32_t row;
+    uint64_t seq;
+    int stream;
+    uint32_t local;
+    uint32_t batch;
+};
+struct SegEvents {
+    const std::vector<Ev>* v;
+    int64_t ts(int64_t k) const { return (*v)[k].ts; }
+    uint32_t row(int64_t k) const { return (*v)[k].row; }
+    uint64_t seq(int64_t k) const { return (*v)[k].seq; }
+    int stream(int64_t k) const { return (*v)[k].stream; }
+    uint32_t local(int64_t k) const { return (*v)[k].local; }
+    uint32_t batch(int64_t k) const { return (*v)[k].batch; }
+};
+
+struct OutRow {
+    int32_t query;
+    uint64_t seq;
+    int64_t ts;
+    std::vector<int64_t> v;
+    std::vector<uint8_t> nul;
+};
+
+}  // namespace
+
+struct nfh {
+    nf_table T;
+    std::string err;
+    // column stores
+    std::vector<std::vector<std::vector<uint8_t>>> cols, nuls;
+    std::vector<std::vector<bool>> has_nul;
+    std::vector<int64_t> rows;
+    std::vector<uint64_t> kstate;
+    int32_t nkeys = 0;
+    int64_t clock = 0;
+    uint64_t tick = 1;
+    bool started = false;
+    std::vector<OutRow> out;
+    int caps[5] = {16, 32, 64, 32, 8};
+};
+
+static int width(int t) {
+    switch (t) {
+        case SH_T_LONG:
+        case SH_T_DOUBLE: return 8;
+        case SH_T_BOOL: return 1;
+        default: return 4;
+    }
+}
+
+static nf_cols host_cols(nfh* h) {
+    nf_cols c;
+    memset(&c, 0, sizeof(c));
+    for (int s = 0; s < h->T.n_streams; s++)
+        for (int a = 0; a < h->T.stream_nattr[s]; a++) {
+            c.col[s][a] = h->cols[s][a].data();
+            c.nul[s][a] = h->has_nul[s][a] ? h->nuls[s][a].data() : nullptr;
+        }
+    return c;
+}
+
+static void ensure_keys(nfh* h, int32_t n) {
+    if (n <= h->nkeys) return;
+    h->kstate.resize((size_t)n * h->T.key_words, 0);
+    h->nkeys = n;
+}
+
+// grow every capacity named by the error bits; re-lay every key block
+static bool grow(nfh* h, uint32_t err) {
+    int c[5];
+    memcpy(c, h->caps, sizeof(c));
+    if (err & NF_E_LIST) c[0] *= 2;
+    if (err & NF_E_SE) c[1] *= 2;
+    if (err & NF_E_NODE) c[2] *= 2;
+    if (err & NF_E_HOLD) c[3] *= 2;
+    if (err & NF_E_SCHED) c[4] *= 2;
+    if (c[0] > 60000 || c[1] > (1 << 22) || c[2] > (1 << 24) || c[3] > (1 << 22) || c[4] > (1 << 20)) return false;
+    nf_table old = h->T;
+    nf_set_caps(&h->T, c[0], c[1], c[2], c[3], c[4]);
+    std::vector<uint64_t> ns((size_t)h->nkeys * h->T.key_words, 0);
+    for (int32_t k = 0; k < h->nkeys; k++) {
+        const uint64_t* src = h->kstate.data() + (size_t)k * old.key_words;
+        uint64_t* dst = ns.data() + (size_t)k * h->T.key_words;
+        dst[0] = src[0];
+        for (int q = 0; q < h->T.n_queries; q++) {
+            const nf_query& A = old.q[q];
+            const nf_query& B = h->T.q[q];
+            const uint64_t* s = src + A.q_off;
+            uint64_t* d = dst + B.q_off;
+            for (int w = 0; w < NF_QH_WORDS; w++) d[w] = s[w];
+            for (int w = 0; w < A.n_proc * NF_PS_WORDS; w++) d[B.lay.off_pstate + w] = s[A.lay.off_pstate + w];
+            for (int p = 0; p < A.n_proc; p++)
+                for (int wh = 0; wh < 2; wh++) {
+                    const uint32_t* sl = (const uint32_t*)(s + A.lay.off_lists) + ((int64_t)p * 2 + wh) * A.lay.list_cap;
+                    uint32_t* dl = (uint32_t*)(d + B.lay.off_lists) + ((int64_t)p * 2 + wh) * B.lay.list_cap;
+                    for (int i = 0; i < A.lay.list_cap; i++) dl[i] = sl[i];
+                }
+            for (int w = 0; w < A.n_out * 5; w++) d[B.lay.off_agg + w] = s[A.lay.off_agg + w];
+            for (int w = 0; w < 3; w++) d[B.lay.off_hold + w] = s[A.lay.off_hold + w];
+            for (int w = 0; w < A.lay.hold_cap; w++) d[B.lay.off_hold + 3 + w] = s[A.lay.off_hold + 3 + w];
+            for (int p = 0; p < A.n_proc; p++) {
+                const uint64_t* sq = s + A.lay.off_sched + (int64_t)p * (2 + A.lay.sched_cap);
+                uint64_t* dq = d + B.lay.off_sched + (int64_t)p * (2 + B.lay.sched_cap);
+                const uint32_t head = (uint32_t)sq[0], n = (uint32_t)(sq[0] >> 32);
+                dq[0] = (uint64_t)n << 32;  // re-based ring
+                dq[1] = sq[1];
+                for (uint32_t i = 0; i < n; i++) dq[2 + i] = sq[2 + (head + i) % A.lay.sched_cap];
+            }
+            for (int64_t w = 0; w < (int64_t)A.lay.se_cap * A.lay.se_words; w++) d[B.lay.off_se + w] = s[A.lay.off_se + w];
+            for (int64_t w = 0; w < (int64_t)A.lay.node_cap * 2; w++) d[B.lay.off_node + w] = s[A.lay.off_node + w];
+        }
+    }
+    h->kstate.swap(ns);
+    memcpy(h->caps, c, sizeof(c));
+    return true;
+}
+
+static void take_records(nfh* h, HostSink& sink, int32_t nq) {
+    // records are appended per lane; order them by (tag index, ordinal)
+    struct R {
+        uint64_t tag;
+        size_t off;
+        int words;
+    };
+    std::vector<R> rs;
+    size_t off = 0;
+    while (off < sink.recs.size()) {
+        const uint64_t* r = sink.recs.data() + off;
+        const int q = (int)(r[2] >> 32);
+        const int w = NF_REC_HDR + h->T.q[q].n_out;
+        rs.push_back({r[0], off, w});
+        off += w;
+    }
+    std::stable_sort(rs.begin(), rs.end(), [](const R& a, const R& b) {
+        const uint32_t ia = (uint32_t)a.tag, ib = (uint32_t)b.tag;
+        if (ia != ib) return ia < ib;
+        return (a.tag >> 32) < (b.tag >> 32);
+    });
+    (void)nq;
+    for (auto& x : rs) {
+        const uint64_t* r = sink.recs.data() + x.off;
+        OutRow o;
+        o.query = (int32_t)(r[2] >> 32);
+        o.ts = (int64_t)r[1];
+        o.seq = r[3];
+        const int n = h->T.q[o.query].n_out;
+        for (int c = 0; c < n; c++) {
+            o.v.push_back((int64_t)r[NF_REC_HDR + c]);
+            o.nul.push_back((uint8_t)((r[2] >> c) & 1));
+        }
+        h->out.push_back(std::move(o));
+    }
+}
+
+static NfLane<HostSink> make_lane(nfh* h, const nf_cols* C, HostSink* sink, int32_t key) {
+    NfLane<HostSink> L;
+    memset(&L, 0, sizeof(L));
+    L.T = &h->T;
+    L.C = C;
+    L.kb = h->kstate.data() + (size_t)key * h->T.key_words;
+    L.sink = sink;
+    L.partitioned = h->T.partitioned;
+    L.clock = h->clock;
+    return L;
+}
+
+// Scheduler.onTimeChange for every scheduler (absent pre-state), in creation order
+static int timers(nfh* h, int64_t now) {
+    if (!h->T.has_absent) return 0;
+    for (int attempt = 0; attempt < 40; attempt++) {
+        std::vector<uint64_t> backup = h->kstate;
+        const size_t out0 = h->out.size();
+        uint32_t err = 0;
+        nf_cols C = host_cols(h);
+        for (int q = 0; q < h->T.n_queries && !err; q++) {
+            const nf_query& Q = h->T.q[q];
+            for (int p = 0; p < Q.n_proc && !err; p++) {
+                if (Q.proc[p].kind != NF_K_ABSENT) continue;
+                // due keys: head <= now; one key per distinct due time (TreeMultimap
+                // with a zero comparator), the earliest-registered wins
+                struct Cand {
+                    int64_t t;
+                    uint64_t stamp;
+                    int32_t key;
+                };
+                std::vector<Cand> cs;
+                for (int32_t k = 0; k < h->nkeys; k++) {
+                    NfLane<HostSink> L = make_lane(h, &C, nullptr, k);
+                    L.Q = &Q;
+                    L.qb = L.kb + Q.q_off;
+                    int64_t t;
+                    if (!(L.sched(p)[1] >> 63) && h->T.partitioned) continue;
+                    if (L.sched_head(p, &t) && t <= now) cs.push_back({t, L.sched(p)[1] & ~(1ull << 63), k});
+                }
+                std::sort(cs.begin(), cs.end(), [](const Cand& a, const Cand& b) {
+                    if (a.t != b.t) return a.t < b.t;
+                    return a.stamp < b.stamp;
+                });
+                HostSink sink;
+                uint32_t rank = 0;
+                for (size_t i = 0; i < cs.size(); i++) {
+                    if (i && cs[i].t == cs[i - 1].t) continue;
+                    NfLane<HostSink> L = make_lane(h, &C, &sink, cs[i].key);
+                    L.Q = &Q;
+                    L.qb = L.kb + Q.q_off;
+                    L.qi = q;
+                    L.tag_index = rank++;
+                    L.stamp = (h->tick << 40) | L.tag_index;
+                    L.send_timer_events(p, now);
+                    err |= L.err;
+                }
+                h->tick++;
+                if (!err) take_records(h, sink, h->T.n_queries);
+            }
+        }
+        if (!err) return 0;
+        h->kstate.swap(backup);
+        h->out.resize(out0);
+        if ((err & (NF_E_UNSUP | NF_E_EMIT | NF_E_KEY)) || !grow(h, err)) {
+            h->err = "state overflow / unsupported in timers";
+            return -5;
+        }
+    }
+    return -5;
+}
+
+extern "C" {
+
+nfh* nfh_create(const sh_app_desc* d, char* err, int errlen) {
+    nfh* h = new nfh();
+    std::string e;
+    if (nf_lower(d, &h->T, &e)) {
+        if (err && errlen > 0) snprintf(err, errlen, "%s", e.c_str());
+        delete h;
+        return nullptr;
+    }
+    h->cols.resize(d->n_streams);
+    h->nuls.resize(d->n_streams);
+    h->has_nul.resize(d->n_streams);
+    h->rows.assign(d->n_streams, 0);
+    for (int s = 0; s < d->n_streams; s++) {
+        h->cols[s].resize(d->streams[s].n_attrs);
+        h->nuls[s].resize(d->streams[s].n_attrs);
+        h->has_nul[s].assign(d->streams[s].n_attrs, false);
+    }
+    nf_set_caps(&h->T, h->caps[0], h->caps[1], h->caps[2], h->caps[3], h->caps[4]);
+    return h;
+}
+
+int nfh_start(nfh* h) {
+    if (h->started) return 0;
+    h->started = true;
+    if (h->T.partitioned) return 0;
+    ensure_keys(h, 1);
+    nf_cols C = host_cols(h);
+    HostSink sink;
+    NfLane<HostSink> L = make_lane(h, &C, &sink, 0);
+    L.kb[0] |= 1ull;
+    for (int q = 0; q < h->T.n_queries; q++) {
+        L.Q = &h->T.q[q];
+        L.qb = L.kb + L.Q->q_off;
+        L.qi = q;
+        L.stamp = h->tick << 40;
+        L.init_partition();
+    }
+    h->tick++;
+    return L.err ? -5 : 0;
+}
+
+int nfh_advance_time(nfh* h, int64_t now) {
+    if (now < h->clock) return 0;
+    h->clock = now;
+    return timers(h, now);
+}
+
+int nfh_send(nfh* h, const sh_batch* b, uint64_t first_seq) {
+    if (b->n <= 0) return 0;
+    const int s = b->stream;
+    const int64_t r0 = h->rows[s];
+    for (int a = 0; a < h->T.stream_nattr[s]; a++) {
+        const int w = width(h->T.attr_type[s][a]);
+        auto& col = h->cols[s][a];
+        col.resize((size_t)(r0 + b->n) * w);
+        memcpy(col.data() + r0 * w, b->cols[a], (size_t)b->n * w);
+        const uint8_t* nm = b->nulls ? b->nulls[a] : nullptr;
+        auto& nc = h->nuls[s][a];
+        nc.resize((size_t)(r0 + b->n), 0);
+        if (nm) {
+            memcpy(nc.data() + r0, nm, b->n);
+            h->has_nul[s][a] = true;
+        }
+    }
+    h->rows[s] += b->n;
+    // InputHandler.send in playback: clock -> last timestamp, due timers first
+    if (h->T.playback) {
+        int rc = nfh_advance_time(h, b->ts[b->n - 1]);
+        if (rc) return rc;
+    }
+    // stable segment by key (null keys dropped)
+    std::vector<Ev> evs;
+    int32_t maxk = 0;
+    for (int64_t i = 0; i < b->n; i++) {
+        int32_t k = h->T.partitioned ? (b->keys ? b->keys[i] : 0) : 0;
+        if (k < 0) continue;
+        maxk = std::max(maxk, k + 1);
+    }
+    ensure_keys(h, std::max(maxk, 1));
+    std::vector<std::vector<Ev>> byKey(std::max(maxk, 1));
+    for (int64_t i = 0; i < b->n; i++) {
+        int32_t k = h->T.partitioned ? (b->keys ? b->keys[i] : 0) : 0;
+        if (k < 0) continue;
+        byKey[k].push_back({b->ts[i], (uint32_t)(r0 + i), first_seq + i, s, (uint32_t)i, 0});
+    }
+    for (int attempt = 0; attempt < 40; attempt++) {
+        std::vector<uint64_t> backup = h->kstate;
+        nf_cols C = host_cols(h);
+        HostSink sink;
+        uint32_t err = 0;
+        for (size_t k = 0; k < byKey.size() && !err; k++) {
+            if (byKey[k].empty()) continue;
+            NfLane<HostSink> L = make_lane(h, &C, &sink, (int32_t)k);
+            SegEvents E{&byKey[k]};
+            nf_process_segment(L, E, 0, (int64_t)byKey[k].size(), h->tick, nullptr);
+            err |= L.err;
+        }
+        if (!err) {
+            h->tick++;
+            take_records(h, sink, h->T.n_queries);
+            return 0;
+        }
+        h->kstate.swap(backup);
+        if ((err & (NF_E_UNSUP | NF_E_EMIT | NF_E_KEY)) || !grow(h, err)) {
+            h->err = (err & NF_E_UNSUP) ? "unsupported reference behaviour" : "state overflow";
+            return -5;
+        }
+    }
+    return -5;
+}
+
+int64_t nfh_out_count(nfh* h) { return (int64_t)h->out.size(); }
+
+int nfh_out_read(nfh* h, int64_t start, int64_t count, int32_t* query, uint64_t* seq, int64_t* ts, int64_t* values,
+                 uint8_t* nulls, int32_t n_out) {
+    if (start < 0 || start + count > (int64_t)h->out.size()) return -1;
+    for (int64_t i = 0; i < count; i++) {
+        const OutRow& r = h->out[start + i];
+        if (query) query[i] = r.query;
+        if (seq) seq[i] = r.seq;
+        if (ts) ts[i] = r.ts;
+        for (int c = 0; c < n_out; c++) {
+            const bool has = c < (int)r.v.size();
+            if (values) values[i * n_out + c] = has ? r.v[c] : 0;
+            if (nulls) nulls[i * n_out + c] = has ? r.nul[c] : 1;
+        }
+    }
+    return 0;
+}
+
+const char* nfh_last_error(nfh* h) { return h->err.c_str(); }
+
+void nfh_destroy(nfh* h) { delete h; }
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+"""Engine adapter over tests/nfa_host/libnfahost.so — TEST INFRASTRUCTURE.
+
+libnfahost.so is the general engine's per-key kernel logic (siddhi_amd/csrc/sh_nfa.h,
+the code k_nfa runs on the GPU) compiled for the CPU. The CPU test suite drives it
+with the reference's fixtures and randomized apps and diffs it against the oracle,
+so the kernel logic is checked without a GPU. The product never uses it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from siddhi_amd import abi
+from oracle_engine import make_batch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DIR = os.path.join(HERE, "nfa_host")
+SO = os.path.join(DIR, "libnfahost.so")
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        subprocess.run(["make", "-s", "-C", DIR], check=True)
+        lib = C.CDLL(SO)
+        lib.nfh_create.argtypes = [C.POINTER(abi.sh_app_desc), C.c_char_p, C.c_int]
+        lib.nfh_create.restype = C.c_void_p
+        lib.nfh_start.argtypes = [C.c_void_p]
+        lib.nfh_start.restype = C.c_int
+        lib.nfh_send.argtypes = [C.c_void_p, C.POINTER(abi.sh_batch), C.c_uint64]
+        lib.nfh_send.restype = C.c_int
+        lib.nfh_advance_time.argtypes = [C.c_void_p, C.c_int64]
+        lib.nfh_advance_time.restype = C.c_int
+        lib.nfh_out_count.argtypes = [C.c_void_p]
+        lib.nfh_out_count.restype = C.c_int64
+        lib.nfh_out_read.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]
+        lib.nfh_out_read.restype = C.c_int
+        lib.nfh_last_error.argtypes = [C.c_void_p]
+        lib.nfh_last_error.restype = C.c_char_p
+        lib.nfh_destroy.argtypes = [C.c_void_p]
+        lib.nfh_destroy.restype = None
+        _lib = lib
+    return _lib
+
+
+class NfaUnsupported(Exception):
+    pass
+
+
+class NfaHostEngine:
+    def __init__(self, compiled):
+        self.lib = load()
+        self.compiled = compiled
+        self.desc = compiled.descriptor()
+        err = C.create_string_buffer(512)
+        self.h = self.lib.nfh_create(C.byref(self.desc), err, 512)
+        if not self.h:
+            raise NfaUnsupported(err.value.decode())
+        self.n_out = max([len(q.outs) for q in compiled.queries] + [1])
+        self.read = 0
+
+    def start(self):
+        self._check(self.lib.nfh_start(self.h))
+
+    def _check(self, rc):
+        if rc != 0:
+            raise RuntimeError(f"nfa_host rc={rc}: {self.lib.nfh_last_error(self.h).decode()}")
+
+    def send(self, stream, tsa, cols, nulls, keys, first_seq):
+        tsa = np.ascontiguousarray(tsa, dtype=np.int64)
+        b, keep = make_batch(stream, tsa, cols, nulls, keys)
+        self._check(self.lib.nfh_send(self.h, C.byref(b), first_seq))
+
+    def advance_time(self, now):
+        self._check(self.lib.nfh_advance_time(self.h, int(now)))
+
+    def drain(self):
+        total = self.lib.nfh_out_count(self.h)
+        n = total - self.read
+        q = np.zeros(n, np.int32)
+        seq = np.zeros(n, np.uint64)
+        ts = np.zeros(n, np.int64)
+        vals = np.zeros((n, self.n_out), np.int64)
+        nls = np.zeros((n, self.n_out), np.uint8)
+        if n:
+            self.lib.nfh_out_read(self.h, self.read, n, q.ctypes.data, seq.ctypes.data, ts.ctypes.data,
+                                  vals.ctypes.data, nls.ctypes.data, self.n_out)
+        self.read = total
+        return dict(query=q, seq=seq, ts=ts, values=vals, nulls=nls, group=np.zeros(n, np.int32))
+
+    def close(self):
+        if self.h:
+            self.lib.nfh_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
