@@ -388,7 +388,6 @@ struct NfLane {
     int qi;
     int partitioned;
     // transient processing state (thread-local in the reference)
-    uint8_t returned[NF_MAX_PROC];  // StreamPostStateProcessor.isEventReturned
     int in_holder;                   // ReturnEventHolder active (Multi receiver)
     uint32_t h_first, h_last;        // current holder's chunk
     int h_has;
@@ -399,6 +398,10 @@ struct NfLane {
     uint64_t stamp;                  // processing-order stamp for scheduler registration
     uint32_t err;
 
+    // StreamPostStateProcessor.isEventReturned of every post of the query: a field
+    // of the processor object, so it persists across events (query header word 3)
+    NF_HD bool returned(int p) const { return (qb[3] >> p) & 1; }
+    NF_HD void set_returned(int p, bool v) { qb[3] = v ? (qb[3] | (1ull << p)) : (qb[3] & ~(1ull << p)); }
     // ---------------------------------------------------------- arena access
     NF_HD uint64_t* pst(int p) const { return qb + Q->lay.off_pstate + (int64_t)p * NF_PS_WORDS; }
     NF_HD uint32_t* list(int p, int which) const {
@@ -1046,7 +1049,7 @@ struct NfLane {
         se_set_ts(s, nd_ts(n));
         if (P.to_selector) {
             ch_reset(c);
-            returned[p] = 1;
+            set_returned(p, true);
         }
         if (P.next_pre >= 0) add_state(P.next_pre, s);
         if (P.next_every_pre >= 0) add_every_state(P.next_every_pre, s);
@@ -1058,7 +1061,7 @@ struct NfLane {
         if (P.to_selector) {
             state_changed(p);
             ch_reset(c);
-            returned[p] = 1;
+            set_returned(p, true);
         }
         if (P.next_pre >= 0) add_state(P.next_pre, s);
         if (P.next_every_pre >= 0) add_every_state(P.next_every_pre, s);
@@ -1098,7 +1101,7 @@ struct NfLane {
                         state_changed(p);
                 } else {
                     stream_post(p, s, c);
-                    if (Q->proc[P.partner].to_selector && P.this_last == P.partner) returned[P.partner] = 1;
+                    if (Q->proc[P.partner].to_selector && P.this_last == P.partner) set_returned(P.partner, true);
                 }
                 break;
             }
@@ -1108,7 +1111,7 @@ struct NfLane {
                 state_changed(p);
                 const uint32_t n = se_ev(s, p);
                 se_set_ts(s, nd_ts(n));
-                returned[p] = 1;
+                set_returned(p, true);
                 if (P.is_start && P.next_every_pre == p) add_every_state(p, s);
                 pget(p);
                 const int64_t t = nd_ts(n) + P.waiting;
@@ -1156,8 +1159,8 @@ struct NfLane {
                 ps_setf(p, NF_PS_SUCCESS, false);
                 process_se(p, s);
                 const int tl = P.this_last;
-                if (returned[tl]) {
-                    returned[tl] = 0;
+                if (returned(tl)) {
+                    set_returned(tl, false);
                     ch_add(ret, s);
                 }
                 bool erased = false;
@@ -1197,8 +1200,8 @@ struct NfLane {
             se_set_ev(s, p, ne);
             process_se(p, s);
             const int tl = P.this_last;
-            if (returned[tl]) {
-                returned[tl] = 0;
+            if (returned(tl)) {
+                set_returned(tl, false);
                 ch_add(ret, s);
             }
             if (ps_flag(p, NF_PS_CHANGED)) {

@@ -547,8 +547,20 @@ int nf_lower(const sh_app_desc* app, nf_table* T, std::string* err) {
                 }
             }
         }
-        for (int p = 0; p < T->q[i].n_proc; p++)
-            if (T->q[i].proc[p].kind == NF_K_ABSENT) T->has_absent = 1;
+        for (int p = 0; p < T->q[i].n_proc; p++) {
+            const nf_proc& P = T->q[i].proc[p];
+            if (P.kind == NF_K_ABSENT) T->has_absent = 1;
+            // CountPreStateProcessor.addState with minCount 0 raises the final count
+            // post's isEventReturned outside that state's own processing; the flag is
+            // consumed by whichever partition key processes the state next, so the
+            // result depends on the global cross-key processing order
+            if (T->partitioned && P.kind == NF_K_COUNT && P.min_count == 0 && P.to_selector) {
+                *err = "query " + std::to_string(i) +
+                       ": device engine: a final count state with min 0 inside a partition (cross-key "
+                       "isEventReturned hand-off) stays on the reference runtime";
+                return -1;
+            }
+        }
     }
     nf_set_caps(T, 16, 32, 64, 32, 8);
     return 0;
