@@ -70,6 +70,12 @@ typedef struct sh_match_buf {
    state-element tree to the device NFA table. */
 int sh_compile(const sh_app_desc* app, sh_handle** out);
 
+/* Replaces SiddhiAppRuntime.start -> StateStreamRuntime.initPartition for
+   unpartitioned queries (core/query/input/stream/state/StateStreamRuntime.java:90-97,
+   AbsentStreamPreStateProcessor.partitionCreated :303-314): arms start states and
+   absent-state timers at the current clock. Call once, before the first batch. */
+int sh_start(sh_handle* h);
+
 /* Replaces InputHandler.send(Event[]) -> StreamJunction.sendEvent ->
    [PartitionStreamReceiver.receive] -> Pattern/Sequence*ProcessStreamReceiver.receive
    (core/stream/input/InputHandler.java:85-96, core/partition/PartitionStreamReceiver.java:176-216,

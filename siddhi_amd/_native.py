@@ -77,7 +77,7 @@ class HipEngine:
         self.n_out = max([len(q.outs) for q in compiled.queries] + [1])
 
     def start(self):
-        pass
+        check(self.h, _lib.sh_start(self.h))
 
     def send(self, stream, tsa, cols, nulls, keys, first_seq):
         tsa = np.ascontiguousarray(tsa, dtype=np.int64)

@@ -79,7 +79,7 @@ class sh_kernel_times(C.Structure):
 
 
 # every symbol include/siddhi_hip.h declares (checked by tests/test_abi.py)
-EXPORTED = ["sh_compile", "sh_push_batch", "sh_advance_time", "sh_drain", "sh_pending",
+EXPORTED = ["sh_start", "sh_compile", "sh_push_batch", "sh_advance_time", "sh_drain", "sh_pending",
             "sh_destroy", "sh_last_error", "sh_run_device", "sh_last_kernel_times",
             "sh_version", "sh_device_count"]
 
@@ -87,6 +87,8 @@ EXPORTED = ["sh_compile", "sh_push_batch", "sh_advance_time", "sh_drain", "sh_pe
 def bind_product(lib):
     lib.sh_compile.argtypes = [C.POINTER(sh_app_desc), C.POINTER(C.c_void_p)]
     lib.sh_compile.restype = C.c_int
+    lib.sh_start.argtypes = [C.c_void_p]
+    lib.sh_start.restype = C.c_int
     lib.sh_push_batch.argtypes = [C.c_void_p, C.POINTER(sh_batch)]
     lib.sh_push_batch.restype = C.c_int
     lib.sh_advance_time.argtypes = [C.c_void_p, C.c_int64]

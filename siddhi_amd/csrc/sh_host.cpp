@@ -11,12 +11,16 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../include/siddhi_hip.h"
 #include "sh_device.h"
 #include "sh_jit.h"
+#include "sh_nfa.h"
+#include "sh_nfa_dev.h"
+#include "sh_nfa_lower.h"
 
 #define SH_VERSION_STR "siddhi_hip 0.1 (gfx950)"
 
@@ -326,7 +330,7 @@ struct sh_handle {
     uint64_t seq_staged0 = 0;
     // workspaces
     DevBuf w_ts, w_stream, w_row, w_key, w_keys_a, w_keys_b, w_idx_a, w_idx_b, w_hist, w_scan, w_seg;
-    DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls;
+    DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls, w_oq;
     DevBuf v_sts, v_mpos, v_flag, v_cnts, v_mid_ts;
     DevBuf v_scol[32], v_mid[32];
     int64_t tmp_cap = 0;
@@ -343,6 +347,17 @@ struct sh_handle {
     int jit_state = 0;
     shj_window jit{};
     std::string jit_err;
+    // ---- general engine (sh_nfa.h): mode 1
+    int mode = 0;                 // 0: chain / window engines, 1: general NFA engine
+    nf_table* T = nullptr;        // host copy of the NFA table
+    DevBuf d_T, d_T_old, d_ncols, n_kstate, n_kstate2, n_save, n_recs, n_ctr, n_err, n_cand, n_sel, n_bid;
+    int caps[5] = {16, 32, 64, 32, 8};
+    int32_t n_nkeys = 0;          // key blocks allocated
+    int64_t rec_cap = 0;
+    int64_t clock = 0;            // TimestampGeneratorImpl current time
+    uint64_t tick = 1;            // processing-phase counter (scheduler registration order)
+    bool started = false;
+    uint32_t batch_id = 0;
 };
 
 static void set_layout(shp_layout& Y, const shp_program& P, int32_t cap) {
@@ -378,20 +393,9 @@ int sh_device_count(void) {
 
 const char* sh_last_error(sh_handle* h) { return h ? h->err.c_str() : "null handle"; }
 
-int sh_compile(const sh_app_desc* app, sh_handle** out) {
-    if (!app || !out) return SH_E_INVALID_ARG;
-    *out = nullptr;
-    sh_handle* h = new sh_handle();
-    *out = h;
-    if (app->version != SH_DESC_VERSION) return fail(h, SH_E_INVALID_ARG, "descriptor version mismatch");
-    h->app = *app;
-    if (app->n_streams < 1 || app->n_streams > SHP_MAX_STREAMS)
-        return fail(h, SH_E_UNSUPPORTED, "device engine: 1..8 streams per app");
-    for (int s = 0; s < app->n_streams; s++) {
-        const sh_stream_def& sd = app->streams[s];
-        if (sd.n_attrs > 32) return fail(h, SH_E_UNSUPPORTED, "device engine: at most 32 attributes per stream");
-        h->stream_types.emplace_back(sd.attr_types, sd.attr_types + sd.n_attrs);
-    }
+// chain / window engines: PATTERN chains of stream states in one query
+// (k_advance, sh_window.hip); returns SH_E_UNSUPPORTED for anything else
+static int compile_chain(sh_handle* h, const sh_app_desc* app) {
     if (app->n_queries != 1) return fail(h, SH_E_UNSUPPORTED, "device engine: one pattern query per app (round 1)");
     const sh_query_desc& q = app->queries[0];
     if (q.state_type != SH_PATTERN) return fail(h, SH_E_UNSUPPORTED, "device engine: sequences are not lowered yet");
@@ -496,6 +500,50 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
     const char* capenv = getenv("SH_PARTIAL_CAP");
     set_layout(h->lay, P, capenv ? atoi(capenv) : 32);
 
+    return SH_OK;
+}
+
+// general engine (sh_nfa.h): every other lowered shape
+static int compile_nfa(sh_handle* h, const sh_app_desc* app) {
+    nf_table* T = new nf_table();
+    std::string err;
+    if (nf_lower(app, T, &err)) {
+        delete T;
+        return fail(h, SH_E_UNSUPPORTED, err);
+    }
+    const char* capenv = getenv("SH_NFA_CAPS");  // list,se,node,hold,sched (tests: force growth)
+    if (capenv) sscanf(capenv, "%d,%d,%d,%d,%d", &h->caps[0], &h->caps[1], &h->caps[2], &h->caps[3], &h->caps[4]);
+    nf_set_caps(T, h->caps[0], h->caps[1], h->caps[2], h->caps[3], h->caps[4]);
+    h->T = T;
+    h->mode = 1;
+    int nout = 0;
+    for (int q = 0; q < T->n_queries; q++) nout = std::max(nout, T->q[q].n_out);
+    h->n_out = nout;
+    h->partitioned = T->partitioned;
+    return SH_OK;
+}
+
+int sh_compile(const sh_app_desc* app, sh_handle** out) {
+    if (!app || !out) return SH_E_INVALID_ARG;
+    *out = nullptr;
+    sh_handle* h = new sh_handle();
+    *out = h;
+    if (app->version != SH_DESC_VERSION) return fail(h, SH_E_INVALID_ARG, "descriptor version mismatch");
+    h->app = *app;
+    if (app->n_streams < 1 || app->n_streams > SHP_MAX_STREAMS)
+        return fail(h, SH_E_UNSUPPORTED, "device engine: 1..8 streams per app");
+    for (int s = 0; s < app->n_streams; s++) {
+        const sh_stream_def& sd = app->streams[s];
+        if (sd.n_attrs > 32) return fail(h, SH_E_UNSUPPORTED, "device engine: at most 32 attributes per stream");
+        h->stream_types.emplace_back(sd.attr_types, sd.attr_types + sd.n_attrs);
+    }
+    int rc = compile_chain(h, app);
+    if (rc == SH_E_UNSUPPORTED) {
+        const std::string chain_err = h->err;
+        rc = compile_nfa(h, app);
+        if (rc) h->err = chain_err + "; " + h->err;
+    }
+    if (rc) return rc;
     h->has_device = device_available();
     if (!h->has_device) return SH_OK;  // compile is host-only; processing needs a device
     hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
@@ -504,6 +552,12 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
     if (h->d_prog.ensure(sizeof(shp_program)) || h->d_cols_desc.ensure(sizeof(shd_cols)) || h->d_err.ensure(64))
         return fail(h, SH_E_OOM, "hipMalloc failed");
     hipMemcpy(h->d_prog.p, &h->prog, sizeof(shp_program), hipMemcpyHostToDevice);
+    if (h->mode == 1) {
+        if (h->d_T.ensure(sizeof(nf_table)) || h->d_ncols.ensure(sizeof(nf_cols)) || h->n_err.ensure(64) ||
+            h->n_ctr.ensure(64))
+            return fail(h, SH_E_OOM, "hipMalloc failed");
+        hipMemcpy(h->d_T.p, h->T, sizeof(nf_table), hipMemcpyHostToDevice);
+    }
     h->stores.resize(app->n_streams);
     for (int s = 0; s < app->n_streams; s++) {
         h->stores[s].cols.resize(h->stream_types[s].size());
@@ -529,6 +583,9 @@ void sh_destroy(sh_handle* h) {
                           &h->w_seg, &h->w_cnt, &h->w_off, &h->w_tmp, &h->w_ctr, &h->w_oseq, &h->w_ots,
                           &h->w_ovals, &h->w_onulls};
         for (DevBuf* b : bufs) b->release();
+        DevBuf* nbufs[] = {&h->d_T, &h->d_T_old, &h->d_ncols, &h->n_kstate, &h->n_kstate2, &h->n_save, &h->n_recs,
+                           &h->n_ctr, &h->n_err, &h->n_cand, &h->n_sel, &h->n_bid, &h->w_oq};
+        for (DevBuf* b : nbufs) b->release();
         for (auto& st : h->stores) {
             for (auto& c : st.cols) c.release();
             for (auto& c : st.nuls) c.release();
@@ -537,8 +594,13 @@ void sh_destroy(sh_handle* h) {
             if (e) hipEventDestroy(e);
         hipStreamDestroy(h->own_stream);
     }
+    delete h->T;
     delete h;
 }
+
+static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0);
+static int nf_start(sh_handle* h);
+static int nf_timers(sh_handle* h, int64_t now);
 
 int sh_push_batch(sh_handle* h, const sh_batch* b) {
     if (!h || !b) return SH_E_INVALID_ARG;
@@ -571,6 +633,7 @@ int sh_push_batch(sh_handle* h, const sh_batch* b) {
     // the async copies above read caller memory: complete them before returning
     hipStreamSynchronize(h->stream);
     st.rows += b->n;
+    if (h->mode == 1) return nf_push(h, b, r0);
     for (int64_t i = 0; i < b->n; i++) {
         h->st_ts.push_back(b->ts[i]);
         h->st_stream.push_back((uint8_t)b->stream);
@@ -584,9 +647,23 @@ int sh_push_batch(sh_handle* h, const sh_batch* b) {
 }
 
 int sh_advance_time(sh_handle* h, int64_t now_ms) {
-    (void)now_ms;
     if (!h) return SH_E_INVALID_ARG;
-    return SH_OK;  // no timer states are lowered to the device engine yet
+    if (h->mode != 1) return SH_OK;  // the chain / window engines have no timer states
+    if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
+    if (!h->started) {
+        int rc = nf_start(h);
+        if (rc) return rc;
+    }
+    if (now_ms < h->clock) return SH_OK;  // TimestampGeneratorImpl: time never goes back
+    h->clock = now_ms;
+    return nf_timers(h, now_ms);
+}
+
+int sh_start(sh_handle* h) {
+    if (!h) return SH_E_INVALID_ARG;
+    if (h->mode != 1) return SH_OK;
+    if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
+    return nf_start(h);
 }
 
 static int ensure_keys(sh_handle* h, int32_t nkeys) {
@@ -751,6 +828,363 @@ static int run_batch(sh_handle* h, const shd_batch& B, int32_t nkeys, const shd_
     return fail(h, SH_E_OOM, "emit buffer kept overflowing");
 }
 
+// ================================================================ general engine (mode 1)
+// sh_nfa.h lanes over the radix segment; emissions are placed by an exclusive
+// scan of per-run counts. A lane error (an arena / list / queue / emission
+// buffer full) restores the touched keys' blocks, grows the capacity and replays.
+static nf_cols nf_store_cols(sh_handle* h) {
+    nf_cols c;
+    memset(&c, 0, sizeof(c));
+    for (int s = 0; s < h->app.n_streams; s++)
+        for (size_t a = 0; a < h->stream_types[s].size(); a++) {
+            c.col[s][a] = h->stores[s].cols[a].p;
+            c.nul[s][a] = h->stores[s].has_nul[a] ? (const uint8_t*)h->stores[s].nuls[a].p : nullptr;
+        }
+    return c;
+}
+
+static int nf_ensure_keys(sh_handle* h, int32_t nkeys) {
+    if (nkeys <= h->n_nkeys) return 0;
+    const int32_t nk = std::max(nkeys, h->n_nkeys * 2);
+    const size_t kb = (size_t)h->T->key_words * 8;
+    const size_t old = (size_t)h->n_nkeys * kb, need = (size_t)nk * kb;
+    hipStreamSynchronize(h->stream);
+    if (h->n_kstate.ensure(need)) return SH_E_OOM;
+    hipMemsetAsync((uint8_t*)h->n_kstate.p + old, 0, need - old, h->stream);
+    h->n_nkeys = nk;
+    return 0;
+}
+
+static int nf_upload_table(sh_handle* h) {
+    return hipMemcpyAsync(h->d_T.p, h->T, sizeof(nf_table), hipMemcpyHostToDevice, h->stream) == hipSuccess
+               ? 0
+               : SH_E_HIP;
+}
+
+// grow the capacities named by `err` and re-lay every key block
+static int nf_grow(sh_handle* h, uint32_t err) {
+    int c[5];
+    memcpy(c, h->caps, sizeof(c));
+    if (err & NF_E_LIST) c[0] *= 2;
+    if (err & NF_E_SE) c[1] *= 2;
+    if (err & NF_E_NODE) c[2] *= 2;
+    if (err & NF_E_HOLD) c[3] *= 2;
+    if (err & NF_E_SCHED) c[4] *= 2;
+    if (c[0] > 60000 || c[1] > (1 << 22) || c[2] > (1 << 24) || c[3] > (1 << 22) || c[4] > (1 << 20))
+        return fail(h, SH_E_STATE_OVERFLOW, "partial-match state overflow");
+    std::unique_ptr<nf_table> old(new nf_table(*h->T));
+    nf_set_caps(h->T, c[0], c[1], c[2], c[3], c[4]);
+    memcpy(h->caps, c, sizeof(c));
+    hipStream_t st = h->stream;
+    if (h->d_T_old.ensure(sizeof(nf_table))) return fail(h, SH_E_OOM, "table");
+    hipMemcpyAsync(h->d_T_old.p, old.get(), sizeof(nf_table), hipMemcpyHostToDevice, st);
+    nf_upload_table(h);
+    if (h->n_nkeys > 0) {
+        DevBuf fresh;
+        if (fresh.ensure_fresh((size_t)h->n_nkeys * h->T->key_words * 8)) return fail(h, SH_E_OOM, "state growth");
+        nfd_relayout(h->d_T_old.as<nf_table>(), h->d_T.as<nf_table>(), h->n_kstate.as<uint64_t>(),
+                     fresh.as<uint64_t>(), h->n_nkeys, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "relayout");
+        h->n_kstate.release();
+        h->n_kstate = fresh;
+        fresh.p = nullptr;
+        fresh.bytes = 0;
+    } else {
+        hipStreamSynchronize(st);
+    }
+    return SH_OK;
+}
+
+static int nf_ensure_recs(sh_handle* h, int64_t cap) {
+    const int stride = NF_REC_HDR + std::max(1, h->n_out);
+    if (cap <= h->rec_cap) return 0;
+    hipStreamSynchronize(h->stream);
+    if (h->n_recs.ensure_fresh((size_t)cap * stride * 8)) return SH_E_OOM;
+    h->rec_cap = cap;
+    return 0;
+}
+
+static nfd_emit nf_emit(sh_handle* h) {
+    nfd_emit em;
+    em.recs = h->n_recs.as<uint64_t>();
+    em.ctr = h->n_ctr.as<unsigned long long>();
+    em.cap = h->rec_cap;
+    em.stride = NF_REC_HDR + std::max(1, h->n_out);
+    em.pad = 0;
+    em.match_cnt = h->w_cnt.as<uint32_t>();
+    em.err = h->n_err.as<unsigned>();
+    return em;
+}
+
+// scan the per-index counts, place the records, append them to the host queue
+// (or to the caller's device buffers); returns the number of rows
+static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_seq, int64_t* d_vals, int64_t cap) {
+    hipStream_t st = h->stream;
+    unsigned long long nrec = 0;
+    hipMemcpyAsync(&nrec, h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
+    if (shd_exclusive_scan(h->w_cnt.as<uint32_t>(), h->w_off.as<uint32_t>(), n_idx, h->w_scan.as<uint32_t>(), st))
+        return fail(h, SH_E_HIP, "scan");
+    uint32_t last_off = 0, last_cnt = 0;
+    hipMemcpyAsync(&last_off, h->w_off.as<uint32_t>() + (n_idx - 1), 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(&last_cnt, h->w_cnt.as<uint32_t>() + (n_idx - 1), 4, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error before placement");
+    const int64_t total = (int64_t)last_off + last_cnt;
+    *rows_out = total;
+    if (total == 0) return SH_OK;
+    const int stride = NF_REC_HDR + std::max(1, h->n_out);
+    const int no = std::max(1, h->n_out);
+    if (d_seq) {  // device-resident output (sh_run_device)
+        if (total > cap) return SH_E_MORE;
+        if (h->w_onulls.ensure_fresh(total * no) || h->w_ots.ensure_fresh(total * 8) ||
+            h->w_oq.ensure_fresh(total * 4))
+            return fail(h, SH_E_OOM, "output buffers");
+        nfd_place(h->n_recs.as<uint64_t>(), (int64_t)nrec, stride, h->w_off.as<uint32_t>(), no, h->w_oq.as<int32_t>(),
+                  d_seq, h->w_ots.as<int64_t>(), d_vals, h->w_onulls.as<uint8_t>(), st);
+        return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "placement");
+    }
+    if (h->w_oseq.ensure_fresh(total * 8) || h->w_ots.ensure_fresh(total * 8) || h->w_ovals.ensure_fresh(total * no * 8) ||
+        h->w_onulls.ensure_fresh(total * no) || h->w_oq.ensure_fresh(total * 4))
+        return fail(h, SH_E_OOM, "output buffers");
+    nfd_place(h->n_recs.as<uint64_t>(), (int64_t)nrec, stride, h->w_off.as<uint32_t>(), no, h->w_oq.as<int32_t>(),
+              h->w_oseq.as<uint64_t>(), h->w_ots.as<int64_t>(), h->w_ovals.as<int64_t>(), h->w_onulls.as<uint8_t>(), st);
+    const size_t base = h->o_seq.size();
+    h->o_query.resize(base + total);
+    h->o_seq.resize(base + total);
+    h->o_ts.resize(base + total);
+    h->o_vals.resize((base + total) * h->n_out);
+    h->o_nulls.resize((base + total) * h->n_out);
+    hipMemcpyAsync(h->o_query.data() + base, h->w_oq.p, total * 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(h->o_seq.data() + base, h->w_oseq.p, total * 8, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(h->o_ts.data() + base, h->w_ots.p, total * 8, hipMemcpyDeviceToHost, st);
+    if (h->n_out) {
+        if (no == h->n_out) {
+            hipMemcpyAsync(h->o_vals.data() + base * h->n_out, h->w_ovals.p, total * no * 8, hipMemcpyDeviceToHost, st);
+            hipMemcpyAsync(h->o_nulls.data() + base * h->n_out, h->w_onulls.p, total * no, hipMemcpyDeviceToHost, st);
+        }
+    }
+    return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "output copy");
+}
+
+// one or more send() calls resident on the device, processed by k_nfa_run
+static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& cols, uint64_t* d_seq,
+                      int64_t* d_vals, int64_t cap, int64_t* n_rows) {
+    hipStream_t st = h->stream;
+    const int64_t n = B.n;
+    if (ensure_ws(h, n)) return fail(h, SH_E_OOM, "workspace");
+    if (nf_ensure_keys(h, nkeys)) return fail(h, SH_E_OOM, "key state");
+    if (nf_ensure_recs(h, std::max<int64_t>(h->rec_cap, n + 4096))) return fail(h, SH_E_OOM, "emission buffer");
+    hipMemcpyAsync(h->d_ncols.p, &cols, sizeof(nf_cols), hipMemcpyHostToDevice, st);
+    shd_segment_ws ws;
+    ws.keys_a = h->w_keys_a.as<uint32_t>();
+    ws.keys_b = h->w_keys_b.as<uint32_t>();
+    ws.idx_a = h->w_idx_a.as<uint32_t>();
+    ws.idx_b = h->w_idx_b.as<uint32_t>();
+    ws.hist = h->w_hist.as<uint32_t>();
+    ws.scan_tmp = h->w_scan.as<uint32_t>();
+    ws.seg_off = h->w_seg.as<uint32_t>();
+    ws.cap = n;
+    const uint32_t* perm = nullptr;
+    const uint32_t* skeys = nullptr;
+    hipEventRecord(h->ev[0], st);
+    if (shd_segment(&B, nkeys, &ws, st, &perm, &skeys)) return fail(h, SH_E_HIP, "segment launch failed");
+    hipEventRecord(h->ev[1], st);
+    const uint32_t* seg_list = ws.seg_off + 2 * n;
+    const uint32_t* nseg = seg_list + n;
+    const int64_t max_seg = std::max<int64_t>(1, std::min<int64_t>(n, nkeys));
+    nfd_events E;
+    E.ts = B.ts;
+    E.stream = B.stream;
+    E.row = B.row;
+    E.bid = h->n_bid.as<uint32_t>();
+    E.perm = perm;
+    E.seq_base = B.seq_base;
+    if (!B.row) return fail(h, SH_E_INVALID_ARG, "row ids required");
+    for (int attempt = 0; attempt < 64; attempt++) {
+        const size_t kw = (size_t)h->T->key_words;
+        if (h->n_save.ensure_fresh((size_t)max_seg * kw * 8)) return fail(h, SH_E_OOM, "save area");
+        nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, seg_list, nseg, skeys, max_seg, h->n_save.as<uint64_t>(), 0,
+                 st);
+        hipMemsetAsync(h->w_cnt.p, 0, n * 4, st);
+        hipMemsetAsync(h->n_ctr.p, 0, 8, st);
+        hipMemsetAsync(h->n_err.p, 0, 4, st);
+        nfd_emit em = nf_emit(h);
+        if (nfd_run(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), &E, n, seg_list, nseg,
+                    skeys, nkeys, max_seg, h->tick, h->clock, &em, st))
+            return fail(h, SH_E_HIP, "k_nfa_run launch failed");
+        hipEventRecord(h->ev[2], st);
+        unsigned err = 0;
+        hipMemcpyAsync(&err, h->n_err.p, 4, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_run");
+        if (!err) {
+            h->tick++;
+            int rc = nf_place(h, n, n_rows, d_seq, d_vals, cap);
+            hipEventRecord(h->ev[3], st);
+            hipStreamSynchronize(st);
+            hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
+            hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
+            hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
+            hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
+            h->times.advance_launches = attempt + 1;
+            return rc;
+        }
+        if (err & NF_E_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
+        if (err & NF_E_UNSUP)
+            return fail(h, SH_E_UNSUPPORTED, "CountPreStateProcessor.startStateReset recursion (reference overflows)");
+        // restore the touched keys, grow, replay
+        nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, seg_list, nseg, skeys, max_seg, h->n_save.as<uint64_t>(), 1,
+                 st);
+        if (err & NF_E_EMIT) {
+            if (nf_ensure_recs(h, h->rec_cap * 4)) return fail(h, SH_E_OOM, "emission buffer");
+        }
+        if (err & ~(unsigned)NF_E_EMIT) {
+            int rc = nf_grow(h, err);
+            if (rc) return rc;
+        }
+    }
+    return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
+}
+
+// Scheduler.onTimeChange(now) for every scheduler (absent pre-state) in creation order
+static int nf_timers(sh_handle* h, int64_t now) {
+    if (!h->T->has_absent || h->n_nkeys == 0) return SH_OK;
+    hipStream_t st = h->stream;
+    const nf_cols cols = nf_store_cols(h);
+    hipMemcpyAsync(h->d_ncols.p, &cols, sizeof(nf_cols), hipMemcpyHostToDevice, st);
+    for (int q = 0; q < h->T->n_queries; q++) {
+        for (int p = 0; p < h->T->q[q].n_proc; p++) {
+            if (h->T->q[q].proc[p].kind != NF_K_ABSENT) continue;
+            const int32_t nkeys = h->n_nkeys;
+            // due keys
+            if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");
+            hipMemsetAsync(h->n_ctr.p, 0, 8, st);
+            nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, now, h->n_cand.as<nfd_cand>(),
+                    h->n_ctr.as<unsigned long long>(), nkeys, st);
+            unsigned long long nc = 0;
+            hipMemcpyAsync(&nc, h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
+            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
+            if (nc == 0) continue;
+            std::vector<nfd_cand> cs(nc);
+            hipMemcpy(cs.data(), h->n_cand.p, nc * sizeof(nfd_cand), hipMemcpyDeviceToHost);
+            // TreeMultimap<Long, SchedulerState> with a zero comparator: one key per
+            // distinct due time, the first in keyOrder (earliest registration)
+            std::sort(cs.begin(), cs.end(), [](const nfd_cand& a, const nfd_cand& b) {
+                if (a.t != b.t) return a.t < b.t;
+                return a.stamp < b.stamp;
+            });
+            std::vector<int32_t> sel;
+            for (size_t i = 0; i < cs.size(); i++)
+                if (i == 0 || cs[i].t != cs[i - 1].t) sel.push_back(cs[i].key);
+            const int32_t ns = (int32_t)sel.size();
+            if (h->n_sel.ensure_fresh((size_t)ns * 4) || h->n_save.ensure_fresh((size_t)ns * h->T->key_words * 8))
+                return fail(h, SH_E_OOM, "timer keys");
+            hipMemcpyAsync(h->n_sel.p, sel.data(), (size_t)ns * 4, hipMemcpyHostToDevice, st);
+            if (ensure_ws(h, ns)) return fail(h, SH_E_OOM, "workspace");
+            if (nf_ensure_recs(h, std::max<int64_t>(h->rec_cap, ns + 4096))) return fail(h, SH_E_OOM, "emission");
+            for (int attempt = 0;; attempt++) {
+                if (attempt > 64) return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
+                const size_t kw = (size_t)h->T->key_words;
+                if (h->n_save.ensure_fresh((size_t)ns * kw * 8)) return fail(h, SH_E_OOM, "save area");
+                nfd_save_keys(h->n_kstate.as<uint64_t>(), (int64_t)kw, h->n_sel.as<int32_t>(), ns,
+                              h->n_save.as<uint64_t>(), 0, st);
+                hipMemsetAsync(h->w_cnt.p, 0, (size_t)ns * 4, st);
+                hipMemsetAsync(h->n_ctr.p, 0, 8, st);
+                hipMemsetAsync(h->n_err.p, 0, 4, st);
+                nfd_emit em = nf_emit(h);
+                nfd_timer(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), q, p,
+                          h->n_sel.as<int32_t>(), ns, now, h->tick, h->clock, &em, st);
+                unsigned err = 0;
+                hipMemcpyAsync(&err, h->n_err.p, 4, hipMemcpyDeviceToHost, st);
+                if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_timer");
+                if (!err) break;
+                if (err & NF_E_UNSUP) return fail(h, SH_E_UNSUPPORTED, "startStateReset recursion");
+                nfd_save_keys(h->n_kstate.as<uint64_t>(), (int64_t)kw, h->n_sel.as<int32_t>(), ns,
+                              h->n_save.as<uint64_t>(), 1, st);
+                if (err & NF_E_EMIT && nf_ensure_recs(h, h->rec_cap * 4)) return fail(h, SH_E_OOM, "emission");
+                if (err & ~(unsigned)NF_E_EMIT) {
+                    int rc = nf_grow(h, err);
+                    if (rc) return rc;
+                }
+            }
+            h->tick++;
+            int64_t rows = 0;
+            int rc = nf_place(h, ns, &rows, nullptr, nullptr, 0);
+            if (rc) return rc;
+        }
+    }
+    return SH_OK;
+}
+
+static int nf_start(sh_handle* h) {
+    if (h->started) return SH_OK;
+    h->started = true;
+    if (h->T->partitioned) return SH_OK;
+    if (nf_ensure_keys(h, 1)) return fail(h, SH_E_OOM, "key state");
+    const nf_cols cols = nf_store_cols(h);
+    hipMemcpyAsync(h->d_ncols.p, &cols, sizeof(nf_cols), hipMemcpyHostToDevice, h->stream);
+    hipMemsetAsync(h->n_err.p, 0, 4, h->stream);
+    if (nf_ensure_recs(h, 4096)) return fail(h, SH_E_OOM, "emission");
+    nfd_emit em = nf_emit(h);
+    nfd_start(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), h->tick, h->clock, &em,
+              h->stream);
+    unsigned err = 0;
+    hipMemcpyAsync(&err, h->n_err.p, 4, hipMemcpyDeviceToHost, h->stream);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_start");
+    h->tick++;
+    return err ? fail(h, SH_E_STATE_OVERFLOW, "start state overflow") : SH_OK;
+}
+
+// InputHandler.send(Event[]) on the general engine: playback clock + due timers
+// first (InputHandler.java:85-96), then the batch
+static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0) {
+    if (!h->started) {
+        int rc = nf_start(h);
+        if (rc) return rc;
+    }
+    if (h->app.playback) {
+        const int64_t last = b->ts[b->n - 1];
+        if (last >= h->clock) {
+            h->clock = last;
+            int rc = nf_timers(h, last);
+            if (rc) return rc;
+        }
+    }
+    const int64_t n = b->n;
+    hipStream_t st = h->stream;
+    std::vector<uint8_t> sv(n, (uint8_t)b->stream);
+    std::vector<uint32_t> rows(n);
+    std::vector<int32_t> keys(n, 0);
+    int32_t nk = 1;
+    for (int64_t i = 0; i < n; i++) {
+        rows[i] = (uint32_t)(r0 + i);
+        if (h->partitioned) {
+            keys[i] = b->keys ? b->keys[i] : -1;
+            nk = std::max(nk, keys[i] + 1);
+        }
+    }
+    if (h->w_ts.ensure_fresh(n * 8) || h->w_stream.ensure_fresh(n) || h->w_row.ensure_fresh(n * 4) ||
+        h->w_key.ensure_fresh(n * 4) || h->n_bid.ensure_fresh(n * 4))
+        return fail(h, SH_E_OOM, "staging");
+    hipMemcpyAsync(h->w_ts.p, b->ts, n * 8, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_stream.p, sv.data(), n, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_row.p, rows.data(), n * 4, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_key.p, keys.data(), n * 4, hipMemcpyHostToDevice, st);
+    hipMemsetAsync(h->n_bid.p, 0, n * 4, st);
+    shd_batch B;
+    B.ts = h->w_ts.as<int64_t>();
+    B.stream = h->w_stream.as<uint8_t>();
+    B.row = h->w_row.as<uint32_t>();
+    B.keys = h->partitioned ? h->w_key.as<int32_t>() : nullptr;
+    B.row_base = 0;
+    B.pad = 0;
+    B.seq_base = h->seq_next;
+    B.n = n;
+    int64_t nrows = 0;
+    int rc = nf_process(h, B, nk, nf_store_cols(h), nullptr, nullptr, 0, &nrows);
+    h->seq_next += n;
+    h->seq_staged0 = h->seq_next;
+    return rc;
+}
+
 static shd_cols store_cols(sh_handle* h) {
     shd_cols c;
     memset(&c, 0, sizeof(c));
@@ -764,6 +1198,7 @@ static shd_cols store_cols(sh_handle* h) {
 
 // process every staged event
 static int flush(sh_handle* h) {
+    if (h->mode == 1) return SH_OK;  // the general engine processes each send() at once
     const int64_t n = (int64_t)h->st_ts.size();
     if (n == 0) return SH_OK;
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device");

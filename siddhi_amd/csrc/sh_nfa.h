@@ -827,60 +827,96 @@ struct NfLane {
         }
         pret(p);
     }
-    // addState (:204-227) and the Count / Logical / Absent overrides
-    NF_HD void add_state(int p, uint32_t s) {
-        pget(p);
-        const nf_proc& P = Q->proc[p];
-        switch (P.kind) {
-            case NF_K_COUNT:
-                // CountPreStateProcessor.addState (:114-138)
-                if (Q->state_type == SH_SEQUENCE) {
-                    if (lcount(p, 1) == 0) lpush(p, 1, s);
-                } else {
-                    lpush(p, 1, s);
-                }
-                if (P.min_count == 0 && !se_ev(s, p)) {
-                    uint32_t* c = cur(p);
-                    ch_clear(c);
-                    ch_add(c, s);
-                    min_count_reached(p, s, c);
-                    ch_clear(c);
-                }
-                break;
-            case NF_K_LOGICAL:
-                // LogicalPreStateProcessor.addState (:43-66)
-                if (P.is_start || Q->state_type == SH_SEQUENCE) {
-                    if (lcount(p, 1) == 0) lpush(p, 1, s);
-                    if (P.partner >= 0 && nae_empty(P.partner)) add_to_nae(P.partner, s);
-                } else {
-                    lpush(p, 1, s);
-                    if (P.partner >= 0) add_to_nae(P.partner, s);
-                }
-                break;
-            case NF_K_ABSENT:
-                // AbsentStreamPreStateProcessor.addState (:95-114)
-                if (!ps_flag(p, NF_PS_INACTIVE)) {
+    // addState (:204-227) and the Count / Logical / Absent overrides.
+    // CountPreStateProcessor.addState with minCount 0 calls processMinCountReached,
+    // which adds the same StateEvent to the next state (and so on down a chain of
+    // min-0 counts): iterative here, with an explicit stack (no device recursion).
+    NF_HD void add_state(int p0, uint32_t s) {
+        int8_t stk[NF_MAX_PROC + 1];
+        int top = 0;
+        stk[top++] = (int8_t)p0;
+        bool resume = false;  // top frame returns from its nested add_state
+        while (top > 0) {
+            const int p = stk[top - 1];
+            const nf_proc& P = Q->proc[p];
+            if (resume) {
+                // processMinCountReached, after nextStatePreProcessor.addState
+                if (P.next_every_pre >= 0) add_every_state(P.next_every_pre, s);
+                ch_clear(cur(p));
+                pret(p);
+                top--;
+                continue;
+            }
+            pget(p);
+            bool nested = false;
+            switch (P.kind) {
+                case NF_K_COUNT:
+                    // CountPreStateProcessor.addState (:114-138)
                     if (Q->state_type == SH_SEQUENCE) {
-                        lset(p, 1, 0);
-                        lpush(p, 1, s);
+                        if (lcount(p, 1) == 0) lpush(p, 1, s);
                     } else {
                         lpush(p, 1, s);
                     }
-                    if (!P.is_start) {
-                        const int64_t t = se_ts(s) + P.waiting;
-                        pst(p)[0] = (uint64_t)t;
-                        notify_at(p, t);
+                    if (P.min_count == 0 && !se_ev(s, p)) {
+                        uint32_t* c = cur(p);
+                        ch_clear(c);
+                        ch_add(c, s);
+                        // CountPostStateProcessor.processMinCountReached (:66-78)
+                        if (P.to_selector) {
+                            state_changed(p);
+                            ch_reset(c);
+                            set_returned(p, true);
+                        }
+                        if (P.next_pre >= 0 && top <= NF_MAX_PROC) {
+                            stk[top++] = (int8_t)P.next_pre;
+                            nested = true;
+                        } else {
+                            if (P.next_every_pre >= 0) add_every_state(P.next_every_pre, s);
+                            ch_clear(c);
+                        }
                     }
-                }
-                break;
-            default:
-                if (Q->state_type == SH_SEQUENCE) {
-                    if (lcount(p, 1) == 0) lpush(p, 1, s);
-                } else {
-                    lpush(p, 1, s);
-                }
+                    break;
+                case NF_K_LOGICAL:
+                    // LogicalPreStateProcessor.addState (:43-66)
+                    if (P.is_start || Q->state_type == SH_SEQUENCE) {
+                        if (lcount(p, 1) == 0) lpush(p, 1, s);
+                        if (P.partner >= 0 && nae_empty(P.partner)) add_to_nae(P.partner, s);
+                    } else {
+                        lpush(p, 1, s);
+                        if (P.partner >= 0) add_to_nae(P.partner, s);
+                    }
+                    break;
+                case NF_K_ABSENT:
+                    // AbsentStreamPreStateProcessor.addState (:95-114)
+                    if (!ps_flag(p, NF_PS_INACTIVE)) {
+                        if (Q->state_type == SH_SEQUENCE) {
+                            lset(p, 1, 0);
+                            lpush(p, 1, s);
+                        } else {
+                            lpush(p, 1, s);
+                        }
+                        if (!P.is_start) {
+                            const int64_t t = se_ts(s) + P.waiting;
+                            pst(p)[0] = (uint64_t)t;
+                            notify_at(p, t);
+                        }
+                    }
+                    break;
+                default:
+                    if (Q->state_type == SH_SEQUENCE) {
+                        if (lcount(p, 1) == 0) lpush(p, 1, s);
+                    } else {
+                        lpush(p, 1, s);
+                    }
+            }
+            if (nested) {
+                resume = false;
+                continue;
+            }
+            pret(p);
+            top--;
+            resume = top > 0;  // every frame below the top is waiting in processMinCountReached
         }
-        pret(p);
     }
     NF_HD bool nae_empty(int p) {
         pget(p);

@@ -1,0 +1,355 @@
+// sh_nfa.hip — gfx950 kernels of the general per-key NFA engine (sh_nfa.h).
+//
+//   k_nfa_run    one lane per partition-key segment of a flushed batch set
+//                (segments come from the radix segment in sh_kernels.hip); the
+//                lane replays the key's events through the query processor graph
+//                and writes emission records through a chunked sink
+//   k_nfa_due    scheduler scan: keys whose FIFO head is due (Scheduler.onTimeChange)
+//   k_nfa_timer  one lane per selected key: sendTimerEvents
+//   k_nfa_place  ordered placement of emission records (exclusive scan of counts)
+//   k_nfa_save / k_nfa_load   copy the touched keys' blocks (replay after growth)
+//   k_nfa_relayout            re-lays every key block into grown capacities
+//
+// Latency-bound by design: the parallelism is the number of keys present in a
+// flush (C3: 1M keys, C4: 10M keys); per-key work is pointer chasing in the key's
+// own arena, which stays L2-resident while its lane runs.
+#include <hip/hip_runtime.h>
+
+#include "sh_nfa.h"
+#include "sh_nfa_dev.h"
+
+#define NF_TPB 128
+#define NF_SINK_CHUNK 16
+
+struct DevSink {
+    uint64_t* buf;
+    unsigned long long* ctr;
+    int64_t cap;       // records
+    int stride;        // words per record
+    uint64_t* chunk;
+    int used, n;
+    __device__ uint64_t* slot(int) {
+        if (used == n) {
+            unsigned long long at = atomicAdd(ctr, (unsigned long long)NF_SINK_CHUNK);
+            if ((int64_t)at + NF_SINK_CHUNK > cap) return nullptr;
+            chunk = buf + (int64_t)at * stride;
+            used = 0;
+            n = NF_SINK_CHUNK;
+        }
+        uint64_t* r = chunk + (int64_t)used * stride;
+        used++;
+        return r;
+    }
+    __device__ void finish() {
+        for (int i = used; i < n; i++) chunk[(int64_t)i * stride] = ~0ull;
+    }
+};
+
+struct DevEvents {
+    const int64_t* ts;
+    const uint8_t* stream;
+    const uint32_t* row;
+    const uint32_t* bid;
+    const uint32_t* perm;   // key-segment position -> arrival index (NULL: identity)
+    uint64_t seq_base;
+    __device__ uint32_t at(int64_t k) const { return perm ? perm[k] : (uint32_t)k; }
+    __device__ int64_t ts_(int64_t k) const { return ts[at(k)]; }
+    __device__ uint32_t row_(int64_t k) const { return row[at(k)]; }
+};
+// the Events interface of nf_process_segment / NfLane::receive
+struct DevEv {
+    const DevEvents* E;
+    __device__ int64_t ts(int64_t k) const { return E->ts[E->at(k)]; }
+    __device__ uint32_t row(int64_t k) const { return E->row[E->at(k)]; }
+    __device__ uint64_t seq(int64_t k) const { return E->seq_base + E->at(k); }
+    __device__ int stream(int64_t k) const { return E->stream ? E->stream[E->at(k)] : 0; }
+    __device__ uint32_t local(int64_t k) const { return E->at(k); }
+    __device__ uint32_t batch(int64_t k) const { return E->bid ? E->bid[E->at(k)] : 0u; }
+};
+
+__device__ inline void lane_init(NfLane<DevSink>& L, const nf_table* T, const nf_cols* C, uint64_t* kb,
+                                 DevSink* sink, int64_t clock) {
+    L.T = T;
+    L.C = C;
+    L.kb = kb;
+    L.sink = sink;
+    L.Q = nullptr;
+    L.qb = nullptr;
+    L.qi = 0;
+    L.partitioned = T->partitioned;
+    L.in_holder = 0;
+    L.h_first = L.h_last = 0;
+    L.h_has = 0;
+    L.cur_seq = 0;
+    L.tag_index = 0;
+    L.ordinal = 0;
+    L.clock = clock;
+    L.stamp = 0;
+    L.err = 0;
+}
+
+__global__ void __launch_bounds__(NF_TPB) k_nfa_run(const nf_table* __restrict__ T, const nf_cols* __restrict__ C,
+                                                    uint64_t* __restrict__ kstate, DevEvents E, int64_t n,
+                                                    const uint32_t* __restrict__ seg_list,
+                                                    const uint32_t* __restrict__ nseg,
+                                                    const uint32_t* __restrict__ skeys, int32_t nkeys, uint64_t tick,
+                                                    int64_t clock, nfd_emit EM) {
+    const uint32_t sidx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sidx >= *nseg) return;
+    const uint32_t beg = seg_list[sidx];
+    const uint32_t key = skeys ? skeys[beg] : 0u;
+    if (key >= (uint32_t)nkeys) {
+        atomicOr(EM.err, (unsigned)NF_E_KEY);
+        return;
+    }
+    int64_t end = beg + 1;
+    if (skeys)
+        while (end < n && skeys[end] == key) end++;
+    else
+        end = n;
+    DevSink sink;
+    sink.buf = EM.recs;
+    sink.ctr = EM.ctr;
+    sink.cap = EM.cap;
+    sink.stride = EM.stride;
+    sink.chunk = nullptr;
+    sink.used = sink.n = 0;
+    NfLane<DevSink> L;
+    lane_init(L, T, C, kstate + (int64_t)key * T->key_words, &sink, clock);
+    DevEv ev{&E};
+    nf_process_segment(L, ev, (int64_t)beg, end, tick, EM.match_cnt);
+    if (sink.chunk) sink.finish();
+    if (L.err) atomicOr(EM.err, L.err);
+}
+
+// unpartitioned apps: StateStreamRuntime.initPartition at SiddhiAppRuntime.start
+__global__ void k_nfa_start(const nf_table* __restrict__ T, const nf_cols* __restrict__ C, uint64_t* __restrict__ kstate,
+                            uint64_t tick, int64_t clock, nfd_emit EM) {
+    if (blockIdx.x * blockDim.x + threadIdx.x != 0) return;
+    NfLane<DevSink> L;
+    lane_init(L, T, C, kstate, nullptr, clock);
+    L.kb[0] |= 1ull;
+    for (int q = 0; q < T->n_queries; q++) {
+        L.Q = &T->q[q];
+        L.qb = L.kb + L.Q->q_off;
+        L.qi = q;
+        L.stamp = tick << 40;
+        L.init_partition();
+    }
+    if (L.err) atomicOr(EM.err, L.err);
+}
+
+// Scheduler.onTimeChange, first half: every key whose queue head is due
+__global__ void __launch_bounds__(256) k_nfa_due(const nf_table* __restrict__ T, int q, int p,
+                                                 const uint64_t* __restrict__ kstate, int32_t nkeys, int64_t now,
+                                                 nfd_cand* __restrict__ cand, unsigned long long* __restrict__ ctr,
+                                                 int64_t cap) {
+    const int32_t key = blockIdx.x * blockDim.x + threadIdx.x;
+    if (key >= nkeys) return;
+    const nf_query& Q = T->q[q];
+    const uint64_t* kb = kstate + (int64_t)key * T->key_words;
+    const uint64_t* sq = kb + Q.q_off + Q.lay.off_sched + (int64_t)p * (2 + Q.lay.sched_cap);
+    const uint32_t head = (uint32_t)sq[0], cnt = (uint32_t)(sq[0] >> 32);
+    if (!cnt) return;
+    if (T->partitioned && !(sq[1] >> 63)) return;
+    const int64_t t = (int64_t)sq[2 + head];
+    if (t > now) return;
+    unsigned long long at = atomicAdd(ctr, 1ull);
+    if ((int64_t)at >= cap) return;
+    cand[at].t = t;
+    cand[at].stamp = sq[1] & ~(1ull << 63);
+    cand[at].key = key;
+    cand[at].pad = 0;
+}
+
+// Scheduler.onTimeChange, second half: sendTimerEvents for each selected key
+// (rank = position in due-time order = emission order)
+__global__ void __launch_bounds__(NF_TPB) k_nfa_timer(const nf_table* __restrict__ T, const nf_cols* __restrict__ C,
+                                                      uint64_t* __restrict__ kstate, int q, int p,
+                                                      const int32_t* __restrict__ keys, int32_t nsel, int64_t now,
+                                                      uint64_t tick, int64_t clock, nfd_emit EM) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nsel) return;
+    DevSink sink;
+    sink.buf = EM.recs;
+    sink.ctr = EM.ctr;
+    sink.cap = EM.cap;
+    sink.stride = EM.stride;
+    sink.chunk = nullptr;
+    sink.used = sink.n = 0;
+    NfLane<DevSink> L;
+    lane_init(L, T, C, kstate + (int64_t)keys[r] * T->key_words, &sink, clock);
+    L.Q = &T->q[q];
+    L.qb = L.kb + L.Q->q_off;
+    L.qi = q;
+    L.tag_index = (uint32_t)r;
+    L.stamp = (tick << 40) | (uint64_t)r;
+    L.send_timer_events(p, now);
+    if (L.ordinal) EM.match_cnt[r] = L.ordinal;
+    if (sink.chunk) sink.finish();
+    if (L.err) atomicOr(EM.err, L.err);
+}
+
+__global__ void __launch_bounds__(256) k_nfa_place(const uint64_t* __restrict__ recs, int64_t nrec, int stride,
+                                                   const uint32_t* __restrict__ offsets, int n_out,
+                                                   int32_t* __restrict__ out_query, uint64_t* __restrict__ out_seq,
+                                                   int64_t* __restrict__ out_ts, int64_t* __restrict__ out_vals,
+                                                   uint8_t* __restrict__ out_nulls) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrec) return;
+    const uint64_t* r = recs + i * stride;
+    const uint64_t tag = r[0];
+    if (tag == ~0ull) return;
+    const int64_t dst = (int64_t)offsets[(uint32_t)tag] + (int64_t)(tag >> 32);
+    const int q = (int)(r[2] >> 32);
+    out_query[dst] = q;
+    out_seq[dst] = r[3];
+    out_ts[dst] = (int64_t)r[1];
+    for (int c = 0; c < n_out; c++) {
+        const bool has = c < stride - NF_REC_HDR;
+        out_vals[dst * n_out + c] = has ? (int64_t)r[NF_REC_HDR + c] : 0;
+        out_nulls[dst * n_out + c] = has ? (uint8_t)((r[2] >> c) & 1) : 1;
+    }
+}
+
+// blocks of the keys touched by this flush <-> compact save area
+__global__ void k_nfa_save(const uint64_t* __restrict__ kstate, int64_t key_words, const uint32_t* __restrict__ seg_list,
+                           const uint32_t* __restrict__ nseg, const uint32_t* __restrict__ skeys,
+                           uint64_t* __restrict__ save, int dir) {
+    const uint32_t s = blockIdx.x;
+    if (s >= *nseg) return;
+    const uint32_t key = skeys ? skeys[seg_list[s]] : 0u;
+    uint64_t* kb = (uint64_t*)kstate + (int64_t)key * key_words;
+    uint64_t* sv = save + (int64_t)s * key_words;
+    for (int64_t w = threadIdx.x; w < key_words; w += blockDim.x) {
+        if (dir == 0)
+            sv[w] = kb[w];
+        else
+            kb[w] = sv[w];
+    }
+}
+
+__global__ void k_nfa_save_keys(uint64_t* __restrict__ kstate, int64_t key_words, const int32_t* __restrict__ keys,
+                                uint64_t* __restrict__ save, int dir) {
+    const int32_t s = blockIdx.x;
+    uint64_t* kb = kstate + (int64_t)keys[s] * key_words;
+    uint64_t* sv = save + (int64_t)s * key_words;
+    for (int64_t w = threadIdx.x; w < key_words; w += blockDim.x) {
+        if (dir == 0)
+            sv[w] = kb[w];
+        else
+            kb[w] = sv[w];
+    }
+}
+
+// re-lay one key block from table A's layout into table B's (capacities grown)
+__global__ void k_nfa_relayout(const nf_table* __restrict__ A, const nf_table* __restrict__ B,
+                               const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, int32_t nkeys) {
+    const int32_t key = blockIdx.x;
+    if (key >= nkeys) return;
+    const uint64_t* s0 = src + (int64_t)key * A->key_words;
+    uint64_t* d0 = dst + (int64_t)key * B->key_words;
+    const int t = threadIdx.x, nt = blockDim.x;
+    for (int64_t w = t; w < B->key_words; w += nt) d0[w] = 0;
+    __syncthreads();
+    if (t == 0) d0[0] = s0[0];
+    for (int q = 0; q < A->n_queries; q++) {
+        const nf_query& QA = A->q[q];
+        const nf_query& QB = B->q[q];
+        const uint64_t* s = s0 + QA.q_off;
+        uint64_t* d = d0 + QB.q_off;
+        for (int w = t; w < NF_QH_WORDS; w += nt) d[w] = s[w];
+        for (int w = t; w < QA.n_proc * NF_PS_WORDS; w += nt) d[QB.lay.off_pstate + w] = s[QA.lay.off_pstate + w];
+        for (int64_t i = t; i < (int64_t)QA.n_proc * 2 * QA.lay.list_cap; i += nt) {
+            const int64_t pl = i / QA.lay.list_cap, e = i % QA.lay.list_cap;
+            ((uint32_t*)(d + QB.lay.off_lists))[pl * QB.lay.list_cap + e] = ((const uint32_t*)(s + QA.lay.off_lists))[i];
+        }
+        for (int w = t; w < QA.n_out * 5; w += nt) d[QB.lay.off_agg + w] = s[QA.lay.off_agg + w];
+        for (int w = t; w < 3 + QA.lay.hold_cap; w += nt) d[QB.lay.off_hold + w] = s[QA.lay.off_hold + w];
+        for (int p = 0; p < QA.n_proc; p++) {
+            const uint64_t* sq = s + QA.lay.off_sched + (int64_t)p * (2 + QA.lay.sched_cap);
+            uint64_t* dq = d + QB.lay.off_sched + (int64_t)p * (2 + QB.lay.sched_cap);
+            const uint32_t head = (uint32_t)sq[0], n = (uint32_t)(sq[0] >> 32);
+            if (t == 0) {
+                dq[0] = (uint64_t)n << 32;
+                dq[1] = sq[1];
+            }
+            for (uint32_t i = t; i < n; i += nt) dq[2 + i] = sq[2 + (head + i) % QA.lay.sched_cap];
+        }
+        for (int64_t w = t; w < (int64_t)QA.lay.se_cap * QA.lay.se_words; w += nt) d[QB.lay.off_se + w] = s[QA.lay.off_se + w];
+        for (int64_t w = t; w < (int64_t)QA.lay.node_cap * 2; w += nt) d[QB.lay.off_node + w] = s[QA.lay.off_node + w];
+    }
+}
+
+static inline unsigned nf_blocks(int64_t n, int tpb) { return (unsigned)((n + tpb - 1) / tpb); }
+
+extern "C" int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, const nfd_events* ev, int64_t n,
+                       const uint32_t* seg_list, const uint32_t* nseg, const uint32_t* skeys, int32_t nkeys,
+                       int64_t max_segments, uint64_t tick, int64_t clock, const nfd_emit* em, void* stream) {
+    DevEvents E;
+    E.ts = ev->ts;
+    E.stream = ev->stream;
+    E.row = ev->row;
+    E.bid = ev->bid;
+    E.perm = ev->perm;
+    E.seq_base = ev->seq_base;
+    if (max_segments < 1) max_segments = 1;
+    hipLaunchKernelGGL(k_nfa_run, dim3(nf_blocks(max_segments, NF_TPB)), dim3(NF_TPB), 0, (hipStream_t)stream, dT, dC,
+                       kstate, E, n, seg_list, nseg, skeys, nkeys, tick, clock, *em);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_start(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, uint64_t tick, int64_t clock,
+                         const nfd_emit* em, void* stream) {
+    hipLaunchKernelGGL(k_nfa_start, dim3(1), dim3(64), 0, (hipStream_t)stream, dT, dC, kstate, tick, clock, *em);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_due(const nf_table* dT, int q, int p, const uint64_t* kstate, int32_t nkeys, int64_t now,
+                       nfd_cand* cand, unsigned long long* ctr, int64_t cap, void* stream) {
+    if (nkeys <= 0) return 0;
+    hipLaunchKernelGGL(k_nfa_due, dim3(nf_blocks(nkeys, 256)), dim3(256), 0, (hipStream_t)stream, dT, q, p, kstate,
+                       nkeys, now, cand, ctr, cap);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_timer(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, int q, int p, const int32_t* keys,
+                         int32_t nsel, int64_t now, uint64_t tick, int64_t clock, const nfd_emit* em, void* stream) {
+    if (nsel <= 0) return 0;
+    hipLaunchKernelGGL(k_nfa_timer, dim3(nf_blocks(nsel, NF_TPB)), dim3(NF_TPB), 0, (hipStream_t)stream, dT, dC,
+                       kstate, q, p, keys, nsel, now, tick, clock, *em);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_place(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets, int n_out,
+                         int32_t* out_query, uint64_t* out_seq, int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls,
+                         void* stream) {
+    if (nrec <= 0) return 0;
+    hipLaunchKernelGGL(k_nfa_place, dim3(nf_blocks(nrec, 256)), dim3(256), 0, (hipStream_t)stream, recs, nrec, stride,
+                       offsets, n_out, out_query, out_seq, out_ts, out_vals, out_nulls);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_save(uint64_t* kstate, int64_t key_words, const uint32_t* seg_list, const uint32_t* nseg,
+                        const uint32_t* skeys, int64_t max_segments, uint64_t* save, int dir, void* stream) {
+    if (max_segments < 1) return 0;
+    hipLaunchKernelGGL(k_nfa_save, dim3((unsigned)max_segments), dim3(256), 0, (hipStream_t)stream, kstate, key_words,
+                       seg_list, nseg, skeys, save, dir);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_relayout(const nf_table* dA, const nf_table* dB, const uint64_t* src, uint64_t* dst, int32_t nkeys,
+                            void* stream) {
+    if (nkeys <= 0) return 0;
+    hipLaunchKernelGGL(k_nfa_relayout, dim3((unsigned)nkeys), dim3(256), 0, (hipStream_t)stream, dA, dB, src, dst,
+                       nkeys);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_save_keys(uint64_t* kstate, int64_t key_words, const int32_t* keys, int32_t nkeys, uint64_t* save,
+                             int dir, void* stream) {
+    if (nkeys < 1) return 0;
+    hipLaunchKernelGGL(k_nfa_save_keys, dim3((unsigned)nkeys), dim3(256), 0, (hipStream_t)stream, kstate, key_words,
+                       keys, save, dir);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}

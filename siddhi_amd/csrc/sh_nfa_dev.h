@@ -1,0 +1,58 @@
+// sh_nfa_dev.h — host <-> kernel interface of the general engine (sh_nfa.hip),
+// called from sh_host.cpp.
+#pragma once
+#include <stdint.h>
+
+#include "sh_nfa.h"
+
+// emission sink (device pointers)
+struct nfd_emit {
+    uint64_t* recs;                // [cap][stride] records (sh_nfa.h NF_REC_HDR layout)
+    unsigned long long* ctr;       // records handed out (chunked)
+    int64_t cap;
+    int32_t stride;                // NF_REC_HDR + max n_out
+    int32_t pad;
+    uint32_t* match_cnt;           // [n] emissions per run-first index (pre-zeroed)
+    unsigned* err;                 // OR of nf_err bits
+};
+
+// events of one flush in arrival order (device pointers)
+struct nfd_events {
+    const int64_t* ts;
+    const uint8_t* stream;         // NULL: stream 0
+    const uint32_t* row;
+    const uint32_t* bid;           // send() call id per event, NULL: one call
+    const uint32_t* perm;          // key-segment position -> arrival index, NULL: identity
+    uint64_t seq_base;
+};
+
+struct nfd_cand {
+    int64_t t;
+    uint64_t stamp;
+    int32_t key;
+    int32_t pad;
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, const nfd_events* ev, int64_t n,
+            const uint32_t* seg_list, const uint32_t* nseg, const uint32_t* skeys, int32_t nkeys, int64_t max_segments,
+            uint64_t tick, int64_t clock, const nfd_emit* em, void* stream);
+int nfd_start(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, uint64_t tick, int64_t clock,
+              const nfd_emit* em, void* stream);
+int nfd_due(const nf_table* dT, int q, int p, const uint64_t* kstate, int32_t nkeys, int64_t now, nfd_cand* cand,
+            unsigned long long* ctr, int64_t cap, void* stream);
+int nfd_timer(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, int q, int p, const int32_t* keys, int32_t nsel,
+              int64_t now, uint64_t tick, int64_t clock, const nfd_emit* em, void* stream);
+int nfd_place(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets, int n_out, int32_t* out_query,
+              uint64_t* out_seq, int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, void* stream);
+int nfd_save(uint64_t* kstate, int64_t key_words, const uint32_t* seg_list, const uint32_t* nseg, const uint32_t* skeys,
+             int64_t max_segments, uint64_t* save, int dir, void* stream);
+int nfd_save_keys(uint64_t* kstate, int64_t key_words, const int32_t* keys, int32_t nkeys, uint64_t* save, int dir,
+                  void* stream);
+int nfd_relayout(const nf_table* dA, const nf_table* dB, const uint64_t* src, uint64_t* dst, int32_t nkeys,
+                 void* stream);
+#ifdef __cplusplus
+}
+#endif

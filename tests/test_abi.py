@@ -42,8 +42,26 @@ def test_c2_query_lowers(lib):
 
 
 @pytest.mark.parametrize("text", [
+    # C3 (sequence + Kleene count) and a logical pattern: the general engine
     "define stream S (a int); from every e1=S, e2=S[a>e1.a]+, e3=S select e1.a as a insert into O;",
     "define stream S (a int); define stream T (a int); from e1=S and e2=T -> e3=S select e3.a as a insert into O;",
+    # C4: logical + absent, playback, partitioned
+    "@app:playback define stream L (u string, ip int); define stream T (u string, amt float); "
+    "define stream O (u string); partition with (u of L, u of T, u of O) begin "
+    "from (e1=L and e2=T) -> not O for 5 sec select e1.u as u, e2.amt as a insert into A; end;",
+])
+def test_general_engine_lowers(lib, text):
+    rc, h, _ = _compile(lib, text)
+    assert rc == abi.SH_OK, lib.sh_last_error(h)
+    lib.sh_destroy(h)
+
+
+@pytest.mark.parametrize("text", [
+    # AbsentLogicalPreStateProcessor (`A and not B for T`) is not lowered
+    "define stream S (a int); define stream T (a int); from e1=S and not T for 1 sec select e1.a as a insert into O;",
+    # a final min-0 count inside a partition hands isEventReturned across keys
+    "define stream S (k int, a int); partition with (k of S) begin "
+    "from every e1=S -> e2=S[a > e1.a]<0:2> select e1.a as a insert into O; end;",
 ])
 def test_unlowered_shapes_are_refused(lib, text):
     rc, h, _ = _compile(lib, text)
