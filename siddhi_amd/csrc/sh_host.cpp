@@ -650,12 +650,9 @@ int sh_advance_time(sh_handle* h, int64_t now_ms) {
     if (!h) return SH_E_INVALID_ARG;
     if (h->mode != 1) return SH_OK;  // the chain / window engines have no timer states
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
-    if (!h->started) {
-        int rc = nf_start(h);
-        if (rc) return rc;
-    }
     if (now_ms < h->clock) return SH_OK;  // TimestampGeneratorImpl: time never goes back
     h->clock = now_ms;
+    if (!h->started) return SH_OK;  // schedulers exist from SiddhiAppRuntime.start on
     return nf_timers(h, now_ms);
 }
 

