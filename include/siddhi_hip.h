@@ -108,7 +108,7 @@ typedef struct sh_device_run {
     const int64_t* d_ts;
     const int32_t* d_keys;       /* partition key ids (dense 0..n_keys-1)           */
     int32_t n_keys;
-    int32_t pad;
+    int32_t batch_events;        /* events per send(Event[]) call (0: one call)     */
     const void* const* d_cols;   /* device column pointers, stream attribute order  */
     int64_t out_capacity;        /* rows the output buffers hold                    */
     uint64_t* d_out_seq;         /* out: trigger_seq per match (ordered)            */

@@ -964,7 +964,7 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
 
 // one or more send() calls resident on the device, processed by k_nfa_run
 static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& cols, uint64_t* d_seq,
-                      int64_t* d_vals, int64_t cap, int64_t* n_rows) {
+                      int64_t* d_vals, int64_t cap, int64_t* n_rows, bool fresh = false, int64_t batch_events = 0) {
     hipStream_t st = h->stream;
     const int64_t n = B.n;
     if (ensure_ws(h, n)) return fail(h, SH_E_OOM, "workspace");
@@ -992,15 +992,17 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     E.ts = B.ts;
     E.stream = B.stream;
     E.row = B.row;
-    E.bid = h->n_bid.as<uint32_t>();
+    E.bid = fresh ? nullptr : h->n_bid.as<uint32_t>();
     E.perm = perm;
     E.seq_base = B.seq_base;
-    if (!B.row) return fail(h, SH_E_INVALID_ARG, "row ids required");
+    E.batch_events = batch_events;
     for (int attempt = 0; attempt < 64; attempt++) {
         const size_t kw = (size_t)h->T->key_words;
-        if (h->n_save.ensure_fresh((size_t)max_seg * kw * 8)) return fail(h, SH_E_OOM, "save area");
-        nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, seg_list, nseg, skeys, max_seg, h->n_save.as<uint64_t>(), 0,
-                 st);
+        if (!fresh) {
+            if (h->n_save.ensure_fresh((size_t)max_seg * kw * 8)) return fail(h, SH_E_OOM, "save area");
+            nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, seg_list, nseg, skeys, max_seg, h->n_save.as<uint64_t>(),
+                     0, st);
+        }
         hipMemsetAsync(h->w_cnt.p, 0, n * 4, st);
         hipMemsetAsync(h->n_ctr.p, 0, 8, st);
         hipMemsetAsync(h->n_err.p, 0, 4, st);
@@ -1027,15 +1029,24 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
         if (err & NF_E_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
         if (err & NF_E_UNSUP)
             return fail(h, SH_E_UNSUPPORTED, "CountPreStateProcessor.startStateReset recursion (reference overflows)");
-        // restore the touched keys, grow, replay
-        nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, seg_list, nseg, skeys, max_seg, h->n_save.as<uint64_t>(), 1,
-                 st);
+        // restore the touched keys (or the fresh state), grow, replay
+        if (!fresh)
+            nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, seg_list, nseg, skeys, max_seg,
+                     h->n_save.as<uint64_t>(), 1, st);
         if (err & NF_E_EMIT) {
             if (nf_ensure_recs(h, h->rec_cap * 4)) return fail(h, SH_E_OOM, "emission buffer");
         }
         if (err & ~(unsigned)NF_E_EMIT) {
             int rc = nf_grow(h, err);
             if (rc) return rc;
+        }
+        if (fresh) {
+            hipMemsetAsync(h->n_kstate.p, 0, (size_t)nkeys * h->T->key_words * 8, st);
+            if (!h->T->partitioned) {
+                h->started = false;
+                int rc = nf_start(h);
+                if (rc) return rc;
+            }
         }
     }
     return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
@@ -1321,6 +1332,35 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
     if (h->app.n_streams != 1) return fail(h, SH_E_UNSUPPORTED, "sh_run_device: single-stream apps only");
     if (run->n <= 0 || run->n > 0x7FFFFFFFll) return fail(h, SH_E_INVALID_ARG, "sh_run_device: 1 <= n < 2^31");
     h->stream = run->stream ? (hipStream_t)run->stream : h->own_stream;
+    if (h->mode == 1) {
+        // general engine from fresh per-key state; the events arrive as send()
+        // calls of run->batch_events
+        if (h->T->has_absent) return fail(h, SH_E_UNSUPPORTED, "sh_run_device: absent states need sh_push_batch");
+        const int32_t nkeys = h->partitioned ? std::max(1, run->n_keys) : 1;
+        if (nf_ensure_keys(h, nkeys)) return fail(h, SH_E_OOM, "key state");
+        hipMemsetAsync(h->n_kstate.p, 0, (size_t)nkeys * h->T->key_words * 8, h->stream);
+        h->started = false;
+        int rc = nf_start(h);
+        if (rc) return rc;
+        nf_cols cols;
+        memset(&cols, 0, sizeof(cols));
+        for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = run->d_cols[a];
+        shd_batch B;
+        B.ts = run->d_ts;
+        B.stream = nullptr;
+        B.row = nullptr;
+        B.keys = h->partitioned ? run->d_keys : nullptr;
+        B.row_base = 0;
+        B.pad = 0;
+        B.seq_base = 0;
+        B.n = run->n;
+        int64_t rows = 0;
+        h->times = sh_kernel_times{};
+        rc = nf_process(h, B, nkeys, cols, run->d_out_seq, run->d_out_values, run->out_capacity, &rows, true,
+                        run->batch_events);
+        run->out_count = rows;
+        return rc;
+    }
     const int32_t nkeys = h->partitioned ? std::max(1, run->n_keys) : 1;
     // fresh per-key state
     if (ensure_keys(h, nkeys)) return fail(h, SH_E_OOM, "key state");

@@ -52,19 +52,20 @@ struct DevEvents {
     const uint32_t* bid;
     const uint32_t* perm;   // key-segment position -> arrival index (NULL: identity)
     uint64_t seq_base;
+    int64_t batch_events;
     __device__ uint32_t at(int64_t k) const { return perm ? perm[k] : (uint32_t)k; }
-    __device__ int64_t ts_(int64_t k) const { return ts[at(k)]; }
-    __device__ uint32_t row_(int64_t k) const { return row[at(k)]; }
 };
 // the Events interface of nf_process_segment / NfLane::receive
 struct DevEv {
     const DevEvents* E;
     __device__ int64_t ts(int64_t k) const { return E->ts[E->at(k)]; }
-    __device__ uint32_t row(int64_t k) const { return E->row[E->at(k)]; }
+    __device__ uint32_t row(int64_t k) const { return E->row ? E->row[E->at(k)] : E->at(k); }
     __device__ uint64_t seq(int64_t k) const { return E->seq_base + E->at(k); }
     __device__ int stream(int64_t k) const { return E->stream ? E->stream[E->at(k)] : 0; }
     __device__ uint32_t local(int64_t k) const { return E->at(k); }
-    __device__ uint32_t batch(int64_t k) const { return E->bid ? E->bid[E->at(k)] : 0u; }
+    __device__ uint32_t batch(int64_t k) const {
+        return E->bid ? E->bid[E->at(k)] : (E->batch_events ? (uint32_t)(E->at(k) / E->batch_events) : 0u);
+    }
 };
 
 __device__ inline void lane_init(NfLane<DevSink>& L, const nf_table* T, const nf_cols* C, uint64_t* kb,
@@ -293,6 +294,7 @@ extern "C" int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, 
     E.bid = ev->bid;
     E.perm = ev->perm;
     E.seq_base = ev->seq_base;
+    E.batch_events = ev->batch_events;
     if (max_segments < 1) max_segments = 1;
     hipLaunchKernelGGL(k_nfa_run, dim3(nf_blocks(max_segments, NF_TPB)), dim3(NF_TPB), 0, (hipStream_t)stream, dT, dC,
                        kstate, E, n, seg_list, nseg, skeys, nkeys, tick, clock, *em);

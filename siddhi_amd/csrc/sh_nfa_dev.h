@@ -24,6 +24,7 @@ struct nfd_events {
     const uint32_t* bid;           // send() call id per event, NULL: one call
     const uint32_t* perm;          // key-segment position -> arrival index, NULL: identity
     uint64_t seq_base;
+    int64_t batch_events;          // bid == NULL: send() call = arrival index / batch_events (0: one call)
 };
 
 struct nfd_cand {

@@ -16,11 +16,12 @@ class DeviceRunner:
         self.compiled = compiled
         self.device = torch.device(device)
         self.handle = CompiledHandle(compiled)
-        self.n_out = max(1, len(compiled.queries[0].outs))
+        self.n_out = max([1] + [len(q.outs) for q in compiled.queries])
         self._out_cap = 0
 
-    def run(self, ts, keys, cols, n_keys, out_capacity=None, stream=None):
-        """ts/keys/cols: device tensors (int64 / int32 / stream attribute order).
+    def run(self, ts, keys, cols, n_keys, out_capacity=None, stream=None, batch_events=4096):
+        """ts/keys/cols: device tensors (int64 / int32 / stream attribute order);
+        the events arrive as send(Event[]) calls of `batch_events`.
         Returns (n_matches, out_seq[n], out_values[n, n_out]) as device tensors."""
         n = ts.numel()
         cap = out_capacity or n
@@ -34,6 +35,7 @@ class DeviceRunner:
         r.d_ts = ts.data_ptr()
         r.d_keys = keys.data_ptr()
         r.n_keys = int(n_keys)
+        r.batch_events = int(batch_events)
         r.d_cols = cp
         r.out_capacity = self._out_cap
         r.d_out_seq = self.out_seq.data_ptr()

@@ -58,3 +58,58 @@ def test_random_apps_on_gpu_vs_oracle(seed):
 def test_random_apps_on_gpu_with_growth(seed, monkeypatch):
     monkeypatch.setenv("SH_NFA_CAPS", "2,2,2,2,2")
     _check(seed)
+
+
+def _c3_run(n, keys, rate=1000):
+    import numpy as np
+    import torch
+    from siddhi_amd import compiler, synth
+    from siddhi_amd.device_run import DeviceRunner
+    ts, k, p, v = synth.stock_stream(n, keys, rate, config_index=3)
+    runner = DeviceRunner(compiler.compile_app(synth.C3_QUERY))
+    dev = torch.device("cuda:0")
+    tk = torch.from_numpy(k).to(dev)
+    m, oseq, ovals = runner.run(torch.from_numpy(ts).to(dev), tk,
+                                [tk, torch.from_numpy(p).to(dev), torch.from_numpy(v).to(dev)], keys)
+    torch.cuda.synchronize()
+    res = (m, oseq.cpu().numpy(), ovals.cpu().numpy())
+    runner.close()
+    return (ts, k, p, v), res
+
+
+@pytest.mark.parametrize("n,keys", [(200_000, 2_000), (2_000_000, 100_000)])
+def test_c3_device_run_vs_oracle(n, keys):
+    """C3 (sequence + Kleene count, partitioned) through sh_run_device, send() calls of 4096."""
+    import numpy as np
+    from siddhi_amd import compiler, synth
+    from oracle_engine import run_stock_oracle
+    (ts, k, p, v), (m, oseq, ovals) = _c3_run(n, keys)
+    seq, _, vals, _ = run_stock_oracle(compiler.compile_app(synth.C3_QUERY), ts, k, p, v, batch=4096)
+    assert m == len(seq) > 0
+    assert np.array_equal(oseq, seq.astype(np.int64))
+    assert np.array_equal(ovals, vals)
+
+
+def test_c3_full_size_key_subset_vs_oracle():
+    """C3 at BASELINE size (100M events, 1M keys): partitions are independent, so the
+    device output restricted to a random subset of keys must equal the oracle run on
+    that subset's events (each event its own send(), global sequence numbers kept)."""
+    import numpy as np
+    from siddhi_amd import compiler, synth
+    from oracle_engine import OracleEngine
+    (ts, k, p, v), (m, oseq, ovals) = _c3_run(100_000_000, 1_000_000)
+    rng = np.random.default_rng(3)
+    subset = np.zeros(1_000_000, bool)
+    subset[rng.choice(1_000_000, 1500, replace=False)] = True
+    idx = np.nonzero(subset[k])[0]
+    eng = OracleEngine(compiler.compile_app(synth.C3_QUERY))
+    eng.start()
+    for i in idx:
+        sl = slice(i, i + 1)
+        eng.send(0, ts[sl], [k[sl].copy(), p[sl].copy(), v[sl].copy()], [None] * 3, k[sl].copy(), int(i))
+    ref = eng.drain()
+    eng.close()
+    sel = subset[k[oseq]]
+    assert sel.sum() == len(ref["seq"]) > 0
+    assert np.array_equal(oseq[sel], ref["seq"].astype(np.int64))
+    assert np.array_equal(ovals[sel], ref["values"])
