@@ -395,10 +395,10 @@ const char* sh_last_error(sh_handle* h) { return h ? h->err.c_str() : "null hand
 
 // chain / window engines: PATTERN chains of stream states in one query
 // (k_advance, sh_window.hip); returns SH_E_UNSUPPORTED for anything else
-static int compile_chain(sh_handle* h, const sh_app_desc* app) {
-    if (app->n_queries != 1) return fail(h, SH_E_UNSUPPORTED, "device engine: one pattern query per app (round 1)");
-    const sh_query_desc& q = app->queries[0];
-    if (q.state_type != SH_PATTERN) return fail(h, SH_E_UNSUPPORTED, "device engine: sequences are not lowered yet");
+// (errors are reported through h->err; h is only used for that)
+static int lower_chain(sh_handle* h, const sh_app_desc* app, int qi, shp_program& Pout) {
+    const sh_query_desc& q = app->queries[qi];
+    if (q.state_type != SH_PATTERN) return fail(h, SH_E_UNSUPPORTED, "chain engine: sequences go to the general engine");
     Lowering L;
     L.q = &q;
     L.app = app;
@@ -486,16 +486,25 @@ static int compile_chain(sh_handle* h, const sh_app_desc* app) {
                           : 0;
         if (getenv("SH_DISABLE_WINDOW")) P.window_ok = 0;
     }
-    h->prog = P;
-    h->n_out = P.n_out;
-    h->partitioned = q.partition >= 0;
-    if (h->partitioned) {
+    if (q.partition >= 0) {
         for (int k = 0; k < P.n_states; k++) {
             int s = P.state_stream[k];
             if (!app->partition_streams[q.partition * app->n_streams + s])
                 return fail(h, SH_E_UNSUPPORTED, "device engine: every stream of a partitioned query must be keyed");
         }
     }
+    Pout = P;
+    return SH_OK;
+}
+
+static int compile_chain(sh_handle* h, const sh_app_desc* app) {
+    if (app->n_queries != 1) return fail(h, SH_E_UNSUPPORTED, "chain engine: one query per app");
+    shp_program P;
+    int rc = lower_chain(h, app, 0, P);
+    if (rc) return rc;
+    h->prog = P;
+    h->n_out = P.n_out;
+    h->partitioned = app->queries[0].partition >= 0;
     // per-key state layout
     const char* capenv = getenv("SH_PARTIAL_CAP");
     set_layout(h->lay, P, capenv ? atoi(capenv) : 32);
