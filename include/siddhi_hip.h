@@ -115,6 +115,7 @@ typedef struct sh_device_run {
     int64_t* d_out_values;       /* out: out_capacity x n_out raw values            */
     int64_t out_count;           /* out: matches produced                           */
     void* stream;                /* hipStream_t to run on (NULL = default)          */
+    int32_t* d_out_query;        /* out (optional): query index per match (ordered) */
 } sh_device_run;
 
 int sh_run_device(sh_handle* h, sh_device_run* run);

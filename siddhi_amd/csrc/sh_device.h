@@ -97,6 +97,9 @@ int shd_window(const shp_program* dprog, const shp_program* hprog, const shd_bat
                void* stream, void* ev_mid, const void* jit);
 int shd_relayout(const uint8_t* src, const shp_layout* A, uint8_t* dst, const shp_layout* B, int32_t nkeys,
                  int32_t n_states, int32_t n_out, void* stream);
+int shd_sort_pairs(const uint32_t* keys, const uint32_t* vals, int64_t n, int bits, uint32_t* const* kbuf,
+                   uint32_t* const* vbuf, uint32_t* hist, uint32_t* scan_tmp, void* stream,
+                   const uint32_t** keys_out, const uint32_t** vals_out);
 int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, void* stream);
 #ifdef __cplusplus
 }

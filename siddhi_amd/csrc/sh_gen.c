@@ -46,3 +46,23 @@ int sh_gen_stock(int64_t n, int32_t n_keys, int64_t rate_per_ms, uint64_t seed, 
     free(walk);
     return 0;
 }
+
+/* C5: card transactions. Cards uniform over [0, n_cards), amount lognormal(4, 1)
+ * rounded to 0.01 (at least 0.01) and stored as float, merchant uniform over
+ * [0, n_merchants), ts_i = t0 + floor(i / R). Returns 0 on success. */
+int sh_gen_txn(int64_t n, int32_t n_cards, int32_t n_merchants, int64_t rate_per_ms, uint64_t seed, int64_t t0,
+               int64_t* ts, int32_t* card, float* amount, int32_t* merchant) {
+    uint64_t s = seed;
+    for (int64_t i = 0; i < n; i++) {
+        card[i] = (int32_t)(splitmix64(&s) % (uint64_t)n_cards);
+        double u1 = u01(&s), u2 = u01(&s);
+        if (u1 < 1e-300) u1 = 1e-300;
+        const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+        double a = floor(exp(4.0 + z) * 100.0 + 0.5) / 100.0;
+        if (a < 0.01) a = 0.01;
+        amount[i] = (float)a;
+        merchant[i] = (int32_t)(splitmix64(&s) % (uint64_t)n_merchants);
+        ts[i] = t0 + i / rate_per_ms;
+    }
+    return 0;
+}

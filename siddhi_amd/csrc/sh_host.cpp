@@ -21,6 +21,7 @@
 #include "sh_nfa.h"
 #include "sh_nfa_dev.h"
 #include "sh_nfa_lower.h"
+#include "sh_rules.h"
 
 #define SH_VERSION_STR "siddhi_hip 0.1 (gfx950)"
 
@@ -358,6 +359,17 @@ struct sh_handle {
     uint64_t tick = 1;            // processing-phase counter (scheduler registration order)
     bool started = false;
     uint32_t batch_id = 0;
+    // ---- batch-compiled rule sets (sh_rules.hip): sh_run_device on mode 2, or
+    // on any app every query of which is window-shaped
+    bool has_rules = false;
+    bool r_partitioned = false;
+    int32_t r_nout = 0;
+    std::vector<shr_rule> r_rules;
+    std::vector<int64_t> r_ixval;
+    std::vector<uint32_t> r_ixstart, r_ixrule, r_free;
+    shr_table r_tab{};
+    DevBuf rd_rules, rd_ixval, rd_ixstart, rd_ixrule, rd_free, rd_tab;
+    DevBuf r_rec, r_keys, r_g, r_sk, r_sv, r_hist, r_scan, r_run;
 };
 
 static void set_layout(shp_layout& Y, const shp_program& P, int32_t cap) {
@@ -512,6 +524,131 @@ static int compile_chain(sh_handle* h, const sh_app_desc* app) {
     return SH_OK;
 }
 
+// ---- batch-compiled rule sets: every query `every e1=S[f1] -> e2=S[f2] within W`
+// with register filters and a projection, all over stream 0 and one partition
+static bool ix_term_ok(const shp_term& X) {
+    if (X.op != SH_OP_EQ || X.rkind != 1 || X.lslot != 0) return false;
+    const bool li = X.ltype == SH_T_INT || X.ltype == SH_T_LONG;
+    const bool ci = X.ctype == SH_T_INT || X.ctype == SH_T_LONG;
+    if (li && ci) return X.dom == DOM_I32 || X.dom == DOM_I64;
+    return X.ltype == X.ctype && (X.ltype == SH_T_STRING || X.ltype == SH_T_BOOL);
+}
+
+// index key of a constant, as rule_ix_key (sh_rules.hip) keys attribute values
+static int64_t ix_const_key(int type, int64_t c) {
+    if (type == SH_T_LONG) return c;
+    if (type == SH_T_BOOL) return c != 0;
+    return (int64_t)(int32_t)c;
+}
+
+static int compile_rules(sh_handle* h, const sh_app_desc* app) {
+    if (app->n_queries < 2 || app->n_streams != 1)
+        return fail(h, SH_E_UNSUPPORTED, "rule engine: two or more queries over one stream");
+    const int part = app->queries[0].partition;
+    std::vector<shr_rule> rules(app->n_queries);
+    std::unique_ptr<sh_handle> tmp(new sh_handle());
+    std::unique_ptr<shp_program> P(new shp_program());
+    for (int qi = 0; qi < app->n_queries; qi++) {
+        if (lower_chain(tmp.get(), app, qi, *P))
+            return fail(h, SH_E_UNSUPPORTED, "rule engine: query " + std::to_string(qi) + ": " + tmp->err);
+        if (!P->window_ok || !P->filter_fast[0] || !P->filter_fast[1] || !P->out_fast ||
+            app->queries[qi].partition != part)
+            return fail(h, SH_E_UNSUPPORTED, "rule engine: query " + std::to_string(qi) +
+                                                 " is not `every e1=S[f1] -> e2=S[f2] within W` with register "
+                                                 "filters and a projection in the common partition");
+        shr_rule& R = rules[qi];
+        memset(&R, 0, sizeof(R));
+        R.within = P->within_ms;
+        R.query = qi;
+        R.n_out = P->n_out;
+        for (int k = 0; k < 2; k++) {
+            R.nt[k] = P->filter_nterms[k];
+            for (int t = 0; t < R.nt[k]; t++) R.t[k][t] = P->terms[k][t];
+        }
+        for (int o = 0; o < P->n_out; o++) {
+            R.out_slot[o] = (int8_t)P->out_slot[o];
+            R.out_attr[o] = (int8_t)P->out_attr[o];
+        }
+    }
+    // predicate index: the slot-0 attribute most start filters compare for
+    // equality with a constant
+    const int na = app->streams[0].n_attrs;
+    std::vector<int> votes(na, 0);
+    for (const shr_rule& R : rules) {
+        std::vector<bool> seen(na, false);
+        for (int t = 0; t < R.nt[0]; t++) {
+            const shp_term& X = R.t[0][t];
+            if (ix_term_ok(X) && X.lattr < na && !seen[X.lattr]) {
+                seen[X.lattr] = true;
+                votes[X.lattr]++;
+            }
+        }
+    }
+    int ix = -1;
+    for (int a = 0; a < na; a++)
+        if (votes[a] > 0 && (ix < 0 || votes[a] > votes[ix])) ix = a;
+    std::vector<std::pair<int64_t, uint32_t>> ent;
+    h->r_free.clear();
+    for (uint32_t r = 0; r < (uint32_t)rules.size(); r++) {
+        int t = -1;
+        for (int k = 0; ix >= 0 && k < rules[r].nt[0]; k++)
+            if (ix_term_ok(rules[r].t[0][k]) && rules[r].t[0][k].lattr == ix) {
+                t = k;
+                break;
+            }
+        if (t < 0)
+            h->r_free.push_back(r);
+        else
+            ent.emplace_back(ix_const_key(rules[r].t[0][t].ctype, rules[r].t[0][t].c), r);
+    }
+    std::sort(ent.begin(), ent.end());
+    h->r_ixval.clear();
+    h->r_ixstart.clear();
+    h->r_ixrule.clear();
+    for (size_t i = 0; i < ent.size(); i++) {
+        if (i == 0 || ent[i].first != ent[i - 1].first) {
+            h->r_ixval.push_back(ent[i].first);
+            h->r_ixstart.push_back((uint32_t)i);
+        }
+        h->r_ixrule.push_back(ent[i].second);
+    }
+    h->r_ixstart.push_back((uint32_t)ent.size());
+    memset(&h->r_tab, 0, sizeof(h->r_tab));
+    h->r_tab.n_rules = (int32_t)rules.size();
+    h->r_tab.ix_attr = h->r_ixval.empty() ? -1 : ix;
+    h->r_tab.n_ix = (int32_t)h->r_ixval.size();
+    h->r_tab.n_free = (int32_t)h->r_free.size();
+    for (int a = 0; a < na && a < 32; a++) h->r_tab.attr_type[a] = app->streams[0].attr_types[a];
+    h->r_nout = 0;
+    for (const shr_rule& R : rules) h->r_nout = std::max(h->r_nout, R.n_out);
+    h->r_rules.swap(rules);
+    h->r_partitioned = part >= 0;
+    h->has_rules = true;
+    return SH_OK;
+}
+
+static int upload_rules(sh_handle* h) {
+    const size_t nr = h->r_rules.size();
+    if (h->rd_rules.ensure(nr * sizeof(shr_rule)) || h->rd_ixval.ensure(8 * h->r_ixval.size() + 8) ||
+        h->rd_ixstart.ensure(4 * h->r_ixstart.size() + 4) || h->rd_ixrule.ensure(4 * h->r_ixrule.size() + 4) ||
+        h->rd_free.ensure(4 * h->r_free.size() + 4) || h->rd_tab.ensure(sizeof(shr_table)))
+        return fail(h, SH_E_OOM, "hipMalloc failed");
+    hipMemcpy(h->rd_rules.p, h->r_rules.data(), nr * sizeof(shr_rule), hipMemcpyHostToDevice);
+    if (!h->r_ixval.empty()) hipMemcpy(h->rd_ixval.p, h->r_ixval.data(), 8 * h->r_ixval.size(), hipMemcpyHostToDevice);
+    hipMemcpy(h->rd_ixstart.p, h->r_ixstart.data(), 4 * h->r_ixstart.size(), hipMemcpyHostToDevice);
+    if (!h->r_ixrule.empty())
+        hipMemcpy(h->rd_ixrule.p, h->r_ixrule.data(), 4 * h->r_ixrule.size(), hipMemcpyHostToDevice);
+    if (!h->r_free.empty()) hipMemcpy(h->rd_free.p, h->r_free.data(), 4 * h->r_free.size(), hipMemcpyHostToDevice);
+    shr_table t = h->r_tab;
+    t.rules = h->rd_rules.as<shr_rule>();
+    t.ix_val = h->rd_ixval.as<int64_t>();
+    t.ix_start = h->rd_ixstart.as<uint32_t>();
+    t.ix_rule = h->rd_ixrule.as<uint32_t>();
+    t.free_rule = h->rd_free.as<uint32_t>();
+    hipMemcpy(h->rd_tab.p, &t, sizeof(t), hipMemcpyHostToDevice);
+    return SH_OK;
+}
+
 // general engine (sh_nfa.h): every other lowered shape
 static int compile_nfa(sh_handle* h, const sh_app_desc* app) {
     nf_table* T = new nf_table();
@@ -549,8 +686,19 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
     int rc = compile_chain(h, app);
     if (rc == SH_E_UNSUPPORTED) {
         const std::string chain_err = h->err;
+        const bool rules = compile_rules(h, app) == SH_OK;
+        const std::string rules_err = rules ? std::string() : h->err;
         rc = compile_nfa(h, app);
-        if (rc) h->err = chain_err + "; " + h->err;
+        if (rc && rules) {
+            // rule sets beyond the general engine's query table: bulk path only
+            rc = SH_OK;
+            h->mode = 2;
+            h->n_out = h->r_nout;
+            h->partitioned = h->r_partitioned;
+            h->err.clear();
+        } else if (rc) {
+            h->err = chain_err + "; " + rules_err + "; " + h->err;
+        }
     }
     if (rc) return rc;
     h->has_device = device_available();
@@ -567,6 +715,7 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
             return fail(h, SH_E_OOM, "hipMalloc failed");
         hipMemcpy(h->d_T.p, h->T, sizeof(nf_table), hipMemcpyHostToDevice);
     }
+    if (h->has_rules && upload_rules(h)) return SH_E_OOM;
     h->stores.resize(app->n_streams);
     for (int s = 0; s < app->n_streams; s++) {
         h->stores[s].cols.resize(h->stream_types[s].size());
@@ -593,7 +742,9 @@ void sh_destroy(sh_handle* h) {
                           &h->w_ovals, &h->w_onulls};
         for (DevBuf* b : bufs) b->release();
         DevBuf* nbufs[] = {&h->d_T, &h->d_T_old, &h->d_ncols, &h->n_kstate, &h->n_kstate2, &h->n_save, &h->n_recs,
-                           &h->n_ctr, &h->n_err, &h->n_cand, &h->n_sel, &h->n_bid, &h->w_oq};
+                           &h->n_ctr, &h->n_err, &h->n_cand, &h->n_sel, &h->n_bid, &h->w_oq,
+                           &h->rd_rules, &h->rd_ixval, &h->rd_ixstart, &h->rd_ixrule, &h->rd_free, &h->rd_tab,
+                           &h->r_rec, &h->r_keys, &h->r_g, &h->r_sk, &h->r_sv, &h->r_hist, &h->r_scan, &h->r_run};
         for (DevBuf* b : nbufs) b->release();
         for (auto& st : h->stores) {
             for (auto& c : st.cols) c.release();
@@ -616,6 +767,9 @@ int sh_push_batch(sh_handle* h, const sh_batch* b) {
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
     if (b->stream < 0 || b->stream >= h->app.n_streams) return fail(h, SH_E_INVALID_ARG, "bad stream index");
     if (b->on_device) return fail(h, SH_E_UNSUPPORTED, "device batches go through sh_run_device");
+    if (h->mode == 2)
+        return fail(h, SH_E_UNSUPPORTED, "rule sets larger than the general engine's query table run through "
+                                         "sh_run_device only");
     if (b->n <= 0) return SH_OK;
     auto& st = h->stores[b->stream];
     const auto& types = h->stream_types[b->stream];
@@ -1335,12 +1489,189 @@ int sh_drain(sh_handle* h, sh_match_buf* out) {
     return avail > k ? SH_E_MORE : SH_OK;
 }
 
+static int bits_for(uint64_t v) {
+    int b = 0;
+    while (b < 64 && (v >> b)) b++;
+    return b;
+}
+
+static shd_segment_ws seg_ws(sh_handle* h, int64_t n) {
+    shd_segment_ws ws;
+    ws.keys_a = h->w_keys_a.as<uint32_t>();
+    ws.keys_b = h->w_keys_b.as<uint32_t>();
+    ws.idx_a = h->w_idx_a.as<uint32_t>();
+    ws.idx_b = h->w_idx_b.as<uint32_t>();
+    ws.hist = h->w_hist.as<uint32_t>();
+    ws.scan_tmp = h->w_scan.as<uint32_t>();
+    ws.seg_off = h->w_seg.as<uint32_t>();
+    ws.cap = n;
+    return ws;
+}
+
+// ts and every column of stream 0 moved into key-segment order by the segment
+static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid) {
+    const int64_t n = run->n;
+    const int na = (int)h->stream_types[0].size();
+    memset(carry, 0, sizeof(*carry));
+    if (h->v_sts.ensure_fresh(n * 8) || h->v_mid_ts.ensure_fresh(n * 8)) return SH_E_OOM;
+    carry->n = 1 + na;
+    carry->src[0] = run->d_ts;
+    carry->dst[0] = h->v_sts.p;
+    carry->width[0] = 8;
+    mid[0] = h->v_mid_ts.p;
+    for (int a = 0; a < na; a++) {
+        const int w = type_width(h->stream_types[0][a]);
+        if (h->v_scol[a].ensure_fresh(n * w) || h->v_mid[a].ensure_fresh(n * w)) return SH_E_OOM;
+        carry->src[1 + a] = run->d_cols[a];
+        carry->dst[1 + a] = h->v_scol[a].p;
+        carry->width[1 + a] = (uint8_t)w;
+        mid[1 + a] = h->v_mid[a].p;
+    }
+    return SH_OK;
+}
+
+// batch-compiled rule sets (sh_rules.hip) over HBM-resident columns
+static int run_rules(sh_handle* h, sh_device_run* run) {
+    hipStream_t st = h->stream;
+    const int64_t n = run->n;
+    const int na = (int)h->stream_types[0].size();
+    if (na > 7) return fail(h, SH_E_UNSUPPORTED, "rule engine: at most 7 attributes per stream");
+    const bool sorted = h->r_partitioned;
+    const int32_t nkeys = sorted ? std::max(1, run->n_keys) : 1;
+    if (ensure_ws(h, n) || h->v_flag.ensure_fresh(64)) return fail(h, SH_E_OOM, "workspace");
+    h->times = sh_kernel_times{};
+    shd_batch B;
+    memset(&B, 0, sizeof(B));
+    B.ts = run->d_ts;
+    B.keys = sorted ? run->d_keys : nullptr;
+    B.n = n;
+    shd_payload carry;
+    void* mid[8] = {nullptr};
+    if (sorted && carry_setup(h, run, &carry, mid)) return fail(h, SH_E_OOM, "rule workspace");
+    hipEventRecord(h->ev[0], st);
+    shd_segment_ws ws = seg_ws(h, n);
+    const uint32_t* perm = nullptr;
+    const uint32_t* skeys = nullptr;
+    if (shd_segment_payload(&B, nkeys, &ws, st, &perm, &skeys, sorted ? &carry : nullptr, mid))
+        return fail(h, SH_E_HIP, "segment launch failed");
+    hipEventRecord(h->ev[1], st);
+    const int64_t* sts = sorted ? h->v_sts.as<int64_t>() : run->d_ts;
+    shd_cols sc;
+    memset(&sc, 0, sizeof(sc));
+    for (int a = 0; a < na; a++) sc.col[0][a] = sorted ? (const void*)h->v_scol[a].p : run->d_cols[a];
+    hipMemcpyAsync(h->d_cols_desc.p, &sc, sizeof(sc), hipMemcpyHostToDevice, st);
+    const shd_cols* dC = h->d_cols_desc.as<shd_cols>();
+    const shr_table* dT = h->rd_tab.as<shr_table>();
+    const uint32_t sentinel = sorted ? (uint32_t)nkeys : 0xFFFFFFFFu;
+    uint32_t* cnt = h->w_cnt.as<uint32_t>();
+    uint32_t* off = h->w_off.as<uint32_t>();
+    hipMemsetAsync(h->v_flag.p, 0, 4, st);
+    if (shr_count(dT, sts, skeys, n, sentinel, dC, cnt, h->v_flag.as<int32_t>(), st) ||
+        shd_exclusive_scan(cnt, off, n, h->w_scan.as<uint32_t>(), st))
+        return fail(h, SH_E_HIP, "rule scan launch failed");
+    uint32_t lo = 0, lc = 0;
+    int32_t flag = 0;
+    hipMemcpyAsync(&lo, off + (n - 1), 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(&lc, cnt + (n - 1), 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(&flag, h->v_flag.p, 4, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the rule scan");
+    if (flag) return fail(h, SH_E_UNSUPPORTED, "rule engine: timestamps decrease inside a key");
+    const int64_t m = (int64_t)lo + lc;
+    run->out_count = m;
+    if (m > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
+    if (m > 0) {
+        const int64_t mt = (m + 4095) / 4096;
+        const size_t sw = std::max(shd_scan_tmp_words(256 * mt), (size_t)16);
+        if (h->r_rec.ensure_fresh((size_t)m * 12) || h->r_keys.ensure_fresh((size_t)m * 12) ||
+            h->r_g.ensure_fresh((size_t)m * 8) || h->r_sk.ensure_fresh((size_t)m * 8) ||
+            h->r_sv.ensure_fresh((size_t)m * 8) || h->r_hist.ensure_fresh((size_t)256 * mt * 4 + 64) ||
+            h->r_scan.ensure_fresh(sw * 4 + 64))
+            return fail(h, SH_E_OOM, "match records");
+        uint32_t* rec_p = h->r_rec.as<uint32_t>();
+        uint32_t* rec_q = rec_p + m;
+        uint32_t* rec_r = rec_q + m;
+        if (shr_write(dT, sts, skeys, n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, st))
+            return fail(h, SH_E_HIP, "rule write launch failed");
+        // PartitionStreamReceiver runs inside each send() call
+        const int64_t batch = run->batch_events > 0 ? run->batch_events : 0;
+        const uint32_t* flags = nullptr;
+        const uint32_t* rid = nullptr;
+        const uint32_t* rfirst = nullptr;
+        if (sorted) {
+            if (h->r_run.ensure_fresh((size_t)n * 12)) return fail(h, SH_E_OOM, "run ids");
+            uint32_t* f = h->r_run.as<uint32_t>();
+            if (shr_run_ids(run->d_keys, n, batch, f, f + n, f + 2 * n, h->w_scan.as<uint32_t>(), st))
+                return fail(h, SH_E_HIP, "run id launch failed");
+            flags = f;
+            rid = f + n;
+            rfirst = f + 2 * n;
+        }
+        // order key (run, query, consuming event), least significant first; the
+        // records are in (opening event, rule) order, which the stable sort keeps
+        // among equal keys (creation order of the partials a consumer takes)
+        const int64_t runlen = batch > 0 ? std::min(batch, n) : n;
+        const int qbits = bits_for((uint64_t)(runlen - 1));
+        const int rbits = bits_for((uint64_t)(h->r_rules.size() - 1));
+        const int nbits = bits_for((uint64_t)(n - 1));
+        const bool packed = qbits + rbits <= 32;
+        uint32_t* k0 = h->r_keys.as<uint32_t>();
+        uint32_t* k1 = k0 + m;
+        uint32_t* k2 = k1 + m;
+        if (shr_keys(rec_q, rec_r, m, perm, flags, rid, rfirst, batch, qbits, packed ? 1 : 0, k0, k1, k2, st))
+            return fail(h, SH_E_HIP, "rule key launch failed");
+        const uint32_t* stage_key[3];
+        int stage_bits[3];
+        int ns = 0;
+        if (packed) {
+            stage_key[ns] = k0;
+            stage_bits[ns++] = qbits + rbits;
+        } else {
+            stage_key[ns] = k0;
+            stage_bits[ns++] = qbits;
+            stage_key[ns] = k1;
+            stage_bits[ns++] = rbits;
+        }
+        stage_key[ns] = packed ? k1 : k2;
+        stage_bits[ns++] = nbits;
+        const uint32_t* order = nullptr;
+        uint32_t* gk = h->r_g.as<uint32_t>();
+        uint32_t* gv = gk + m;
+        uint32_t* kb[2] = {h->r_sk.as<uint32_t>(), h->r_sk.as<uint32_t>() + m};
+        uint32_t* vb[2] = {h->r_sv.as<uint32_t>(), h->r_sv.as<uint32_t>() + m};
+        for (int s = 0; s < ns; s++) {
+            if (stage_bits[s] == 0) continue;
+            const uint32_t* ko = nullptr;
+            const uint32_t* vo = nullptr;
+            if (shr_gather(stage_key[s], order, m, gk, gv, st) ||
+                shd_sort_pairs(gk, gv, m, stage_bits[s], kb, vb, h->r_hist.as<uint32_t>(), h->r_scan.as<uint32_t>(),
+                               st, &ko, &vo))
+                return fail(h, SH_E_HIP, "rule sort launch failed");
+            order = vo;
+        }
+        hipEventRecord(h->ev[2], st);
+        if (shr_place(dT, order, m, rec_p, rec_q, rec_r, perm, sts, dC, 0, std::max(1, h->n_out), run->d_out_seq,
+                      run->d_out_query, nullptr, run->d_out_values, st))
+            return fail(h, SH_E_HIP, "rule placement launch failed");
+    } else {
+        hipEventRecord(h->ev[2], st);
+    }
+    hipEventRecord(h->ev[3], st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the rule engine");
+    hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
+    hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
+    hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
+    hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
+    h->times.advance_launches = 1;
+    return SH_OK;
+}
+
 int sh_run_device(sh_handle* h, sh_device_run* run) {
     if (!h || !run) return SH_E_INVALID_ARG;
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device");
     if (h->app.n_streams != 1) return fail(h, SH_E_UNSUPPORTED, "sh_run_device: single-stream apps only");
     if (run->n <= 0 || run->n > 0x7FFFFFFFll) return fail(h, SH_E_INVALID_ARG, "sh_run_device: 1 <= n < 2^31");
     h->stream = run->stream ? (hipStream_t)run->stream : h->own_stream;
+    if (h->has_rules && (h->mode == 2 || !getenv("SH_DISABLE_RULES"))) return run_rules(h, run);
     if (h->mode == 1) {
         // general engine from fresh per-key state; the events arrive as send()
         // calls of run->batch_events
@@ -1368,6 +1699,10 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
         rc = nf_process(h, B, nkeys, cols, run->d_out_seq, run->d_out_values, run->out_capacity, &rows, true,
                         run->batch_events);
         run->out_count = rows;
+        if (rc == SH_OK && run->d_out_query && rows > 0) {
+            hipMemcpyAsync(run->d_out_query, h->w_oq.p, rows * 4, hipMemcpyDeviceToDevice, h->stream);
+            hipStreamSynchronize(h->stream);
+        }
         return rc;
     }
     const int32_t nkeys = h->partitioned ? std::max(1, run->n_keys) : 1;
@@ -1458,6 +1793,7 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
         if (wrc < 0) return fail(h, SH_E_HIP, "window engine launch failed");
         run->out_count = nm;
         if (wrc == 2) return fail(h, SH_E_MORE, "output capacity too small");
+        if (wrc == 0 && run->d_out_query && nm > 0) hipMemsetAsync(run->d_out_query, 0, nm * 4, st);
         if (wrc == 0) {
             hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
             hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
@@ -1471,6 +1807,10 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
     int rc = run_batch(h, B, nkeys, cols, run->d_out_seq, nullptr, run->d_out_values, nullptr, run->out_capacity,
                        &nm, true);
     run->out_count = nm;
+    if (rc == SH_OK && run->d_out_query && nm > 0) {
+        hipMemsetAsync(run->d_out_query, 0, nm * 4, h->stream);
+        hipStreamSynchronize(h->stream);
+    }
     return rc;
 }
 

@@ -693,6 +693,35 @@ extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segmen
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// stable LSD radix sort of (key, value) pairs by the low `bits` of the key
+// (vals NULL: identity); the result lies in the kbuf / vbuf ping-pong buffers,
+// which must not alias the inputs
+extern "C" int shd_sort_pairs(const uint32_t* keys, const uint32_t* vals, int64_t n, int bits, uint32_t* const* kbuf,
+                              uint32_t* const* vbuf, uint32_t* hist, uint32_t* scan_tmp, void* stream,
+                              const uint32_t** keys_out, const uint32_t** vals_out) {
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t ntiles = ceil_div(n, RADIX_TILE);
+    const int passes = (bits + 7) / 8;
+    const uint32_t* kin = keys;
+    const uint32_t* vin = vals;
+    shd_payload PL;
+    memset(&PL, 0, sizeof(PL));
+    for (int ps = 0; ps < passes && n > 0; ps++) {
+        const int shift = ps * 8;
+        hipLaunchKernelGGL(k_digit_hist, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
+                           0xFFFFFFFFu, n, shift, hist, ntiles);
+        int rc = shd_exclusive_scan(hist, hist, 256 * ntiles, scan_tmp, stream);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_digit_scatter, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
+                           0xFFFFFFFFu, vin, n, shift, (const uint32_t*)hist, ntiles, kbuf[ps & 1], vbuf[ps & 1], PL);
+        kin = kbuf[ps & 1];
+        vin = vbuf[ps & 1];
+    }
+    *keys_out = kin;
+    *vals_out = vin;
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 extern "C" int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
                            const uint32_t** perm_out, const uint32_t** skeys_out) {
     return shd_segment_payload(b, nkeys, ws, stream, perm_out, skeys_out, nullptr, nullptr);

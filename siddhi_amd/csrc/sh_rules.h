@@ -1,0 +1,61 @@
+// sh_rules.h — the batch-compiled rule table (config C5) shared by the host
+// lowering (sh_host.cpp compile_rules) and the gfx950 kernels (sh_rules.hip).
+#pragma once
+#include <stdint.h>
+
+#include "sh_device.h"
+#include "sh_program.h"
+
+// one query `every e1=S[f1] -> e2=S[f2(e1, e2)] within W select <projection>`
+struct shr_rule {
+    int64_t within;                     // ms (the window shape requires `within`)
+    int32_t query;                      // query index in the app (junction subscription order)
+    int32_t n_out;
+    int32_t nt[2];                      // conjuncts of f1 (slot 0) and of f2 (slots 0, 1)
+    shp_term t[2][SHP_MAX_TERMS];
+    int8_t out_slot[SHP_MAX_OUT];
+    int8_t out_attr[SHP_MAX_OUT];
+};
+
+struct shr_table {
+    int32_t n_rules;
+    int32_t ix_attr;                    // indexed slot-0 attribute, -1: no index
+    int32_t n_ix;                       // distinct indexed constants
+    int32_t n_free;                     // rules without the indexed conjunct
+    int32_t attr_type[32];              // stream attribute types
+    const shr_rule* rules;              // device [n_rules]
+    const int64_t* ix_val;              // device [n_ix], ascending
+    const uint32_t* ix_start;           // device [n_ix + 1]
+    const uint32_t* ix_rule;            // device rule ids grouped by constant (ascending inside a group)
+    const uint32_t* free_rule;          // device [n_free], ascending
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+// matches opened at every key-segment position (cnt[p]); flag := 1 when a key's
+// timestamps decrease (the window reduction does not hold)
+int shr_count(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
+              const shd_cols* dC, uint32_t* cnt, int32_t* flag, void* stream);
+// the same scan, writing (opening, consuming, rule) records at off[p]
+int shr_write(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
+              const shd_cols* dC, const uint32_t* cnt, const uint32_t* off, uint32_t* rec_p, uint32_t* rec_q,
+              uint32_t* rec_r, void* stream);
+// PartitionStreamReceiver runs of an arrival-order key array: flags[i] (run
+// start), rid[i] (exclusive scan of flags), rfirst[run] (first arrival index)
+int shr_run_ids(const int32_t* akeys, int64_t n, int64_t batch, uint32_t* flags, uint32_t* rid, uint32_t* rfirst,
+                uint32_t* scan_tmp, void* stream);
+// order keys of the records: packed -> k0 = rule << qbits | offset in run,
+// k1 = run; else k0 = offset in run, k1 = rule, k2 = run
+int shr_keys(const uint32_t* rec_q, const uint32_t* rec_r, int64_t m, const uint32_t* perm, const uint32_t* flags,
+             const uint32_t* rid, const uint32_t* rfirst, int64_t batch, int qbits, int packed, uint32_t* k0,
+             uint32_t* k1, uint32_t* k2, void* stream);
+// gk[i] = key[order[i]], gv[i] = order[i] (order NULL: identity)
+int shr_gather(const uint32_t* key, const uint32_t* order, int64_t m, uint32_t* gk, uint32_t* gv, void* stream);
+// ordered output rows from the sorted record order
+int shr_place(const shr_table* dT, const uint32_t* order, int64_t m, const uint32_t* rec_p, const uint32_t* rec_q,
+              const uint32_t* rec_r, const uint32_t* perm, const int64_t* sts, const shd_cols* dC, uint64_t seq_base,
+              int n_out, uint64_t* out_seq, int32_t* out_query, int64_t* out_ts, int64_t* out_vals, void* stream);
+#ifdef __cplusplus
+}
+#endif

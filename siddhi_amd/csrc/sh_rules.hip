@@ -1,0 +1,284 @@
+// sh_rules.hip — batch-compiled rule sets (config C5): R queries
+//     every e1=S[f1_r] -> e2=S[f2_r(e1, e2)] within W_r          r = 0 .. R-1
+// over one stream and one `partition with (key of S)` (or none), lowered
+// together into one rule table (sh_rules.h) that shares a single radix segment.
+//
+// Every rule has the window-engine shape (sh_window.hip): with non-decreasing
+// timestamps per key, rule r's partial opened at event p (f1_r) is consumed by
+// the first later event q of the key with f2_r(p, q), unless ts_q - ts_p > W_r.
+// Each query owns its processor state, so rules meet only in the output order:
+// PartitionStreamReceiver.receive(Event[]) (core/partition/PartitionStreamReceiver.java:176-216)
+// splits a send() call into runs of consecutive same-key events (a null-key event
+// is dropped without ending the run) and sends each run to every query of the
+// partition in subscription order, and a Multi receiver hands a run's matches to
+// the callbacks after the whole run (core/query/input/MultiProcessStreamReceiver.java:95-122).
+// A match is therefore ordered by (run, query, consuming event, opening event);
+// an unpartitioned app sees each send() call as one run.
+//
+// Predicate index: the host picks the slot-0 attribute that the most start
+// filters compare for equality with an integral / string / bool constant
+// (`merchant == M_r`) and groups the rules by that constant; a lane
+// binary-searches its event's value and evaluates only the rules of that group
+// plus the rules without such a conjunct. Every conjunct is still evaluated, so
+// the index only prunes.
+//
+// Pipeline (sh_host.cpp run_rules): segment (sh_kernels.hip) -> k_rules_scan<0>
+// (matches per opening event) -> exclusive scan -> k_rules_scan<1> (records in
+// (opening event, rule) order) -> run ids -> k_rules_keys -> stable LSD radix
+// sort of the records by (run, query, consuming event) -> k_rules_place.
+#include <hip/hip_runtime.h>
+
+#include "../../include/sh_query.h"
+#include "sh_device.h"
+#include "sh_rules.h"
+#include "sh_vm.h"
+
+#define RTPB 256
+
+static unsigned rgrid(int64_t n) {
+    int64_t g = (n + RTPB - 1) / RTPB;
+    if (g > 65536 * 8) g = 65536 * 8;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+
+// conjunction of register terms over the two slots (rows in key-segment order)
+__device__ __forceinline__ bool rule_terms(const shp_term* __restrict__ T, int nt, uint32_t r0, uint32_t r1,
+                                           const shd_cols* __restrict__ C) {
+    for (int t = 0; t < nt; t++) {
+        const shp_term X = T[t];
+        const uint32_t lr = X.lslot ? r1 : r0;
+        if (lr == SHD_NULL_ROW) return false;
+        VmVal l, r;
+        l.t = X.ltype;
+        l.null = 0;
+        l.b = load_attr(C, 0, X.lattr, X.ltype, lr);
+        if (X.rkind == 1) {
+            r.t = X.ctype;
+            r.null = 0;
+            r.b = X.c;
+        } else {
+            const uint32_t rr = X.rslot ? r1 : r0;
+            if (rr == SHD_NULL_ROW) return false;
+            r.t = X.rtype;
+            r.null = 0;
+            r.b = load_attr(C, 0, X.rattr, X.rtype, rr);
+            if (X.rkind == 2) {
+                VmVal c;
+                c.t = X.ctype;
+                c.null = 0;
+                c.b = X.c;
+                r = vm_arith(X.aop, X.atype, r, c);
+                if (r.null) return false;
+            }
+        }
+        if (!vm_cmp(X.op, X.dom, l, r)) return false;
+    }
+    return true;
+}
+
+// index key of an attribute value (the host keys the constants the same way)
+__device__ __forceinline__ int64_t rule_ix_key(int type, int64_t raw) {
+    if (type == SH_T_LONG) return raw;
+    if (type == SH_T_BOOL) return raw != 0;
+    return (int64_t)(int32_t)raw;
+}
+
+// WRITE = 0: matches opened at every key-segment position p -> cnt[p]
+// WRITE = 1: the same scan, writing (p, q, rule) records from off[p] on
+template <int WRITE>
+__global__ void __launch_bounds__(RTPB) k_rules_scan(const shr_table* __restrict__ RT, const int64_t* __restrict__ sts,
+                                                     const uint32_t* __restrict__ skeys, int64_t n, uint32_t sentinel,
+                                                     const shd_cols* __restrict__ C, uint32_t* __restrict__ cnt,
+                                                     const uint32_t* __restrict__ off, uint32_t* __restrict__ rec_p,
+                                                     uint32_t* __restrict__ rec_q, uint32_t* __restrict__ rec_r,
+                                                     int32_t* __restrict__ flag) {
+    const int ix_attr = RT->ix_attr;
+    const int n_ix = RT->n_ix;
+    const uint32_t n_free = (uint32_t)RT->n_free;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        if (WRITE && cnt[p] == 0) continue;
+        const uint32_t key = skeys ? skeys[p] : 0u;
+        if (key == sentinel) continue;
+        const int64_t t0 = sts[p];
+        if (!WRITE && p > 0 && (!skeys || skeys[p - 1] == key) && t0 < sts[p - 1]) atomicExch(flag, 1);
+        uint32_t lo = 0, hi = 0;
+        if (ix_attr >= 0) {
+            const int ty = RT->attr_type[ix_attr];
+            const int64_t x = rule_ix_key(ty, load_attr(C, 0, ix_attr, ty, (uint32_t)p));
+            int a = 0, b = n_ix;
+            while (a < b) {
+                const int m = (a + b) >> 1;
+                if (RT->ix_val[m] < x)
+                    a = m + 1;
+                else
+                    b = m;
+            }
+            if (a < n_ix && RT->ix_val[a] == x) {
+                lo = RT->ix_start[a];
+                hi = RT->ix_start[a + 1];
+            }
+        }
+        const uint32_t nsel = hi - lo, total = nsel + n_free;
+        uint32_t c = 0;
+        const uint32_t o = WRITE ? off[p] : 0u;
+        for (uint32_t k = 0; k < total; k++) {
+            const uint32_t r = k < nsel ? RT->ix_rule[lo + k] : RT->free_rule[k - nsel];
+            const shr_rule* R = RT->rules + r;
+            if (!rule_terms(R->t[0], R->nt[0], (uint32_t)p, SHD_NULL_ROW, C)) continue;
+            const int64_t W = R->within;
+            for (int64_t q = p + 1; q < n; q++) {
+                if (skeys && skeys[q] != key) break;
+                const int64_t d = sts[q] - t0;
+                if (W >= 0 && (d < 0 ? -d : d) > W) break;  // expired before event q is matched
+                if (rule_terms(R->t[1], R->nt[1], (uint32_t)p, (uint32_t)q, C)) {
+                    if (WRITE) {
+                        rec_p[o + c] = (uint32_t)p;
+                        rec_q[o + c] = (uint32_t)q;
+                        rec_r[o + c] = r;
+                    }
+                    c++;
+                    break;
+                }
+            }
+        }
+        if (!WRITE) cnt[p] = c;
+    }
+}
+
+// start of a PartitionStreamReceiver run: the first keyed event of a send() call,
+// or a keyed event whose key differs from the previous keyed event of the call
+__global__ void k_run_flags(const int32_t* __restrict__ akeys, int64_t n, int64_t batch, uint32_t* __restrict__ flags) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t k = akeys[i];
+        uint32_t f = 0;
+        if (k >= 0) {
+            const int64_t b0 = batch > 0 ? i - i % batch : 0;
+            int64_t j = i - 1;
+            while (j >= b0 && akeys[j] < 0) j--;
+            f = (j < b0 || akeys[j] != k) ? 1u : 0u;
+        }
+        flags[i] = f;
+    }
+}
+
+__global__ void k_run_first(const uint32_t* __restrict__ flags, const uint32_t* __restrict__ rid, int64_t n,
+                            uint32_t* __restrict__ rfirst) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (flags[i]) rfirst[rid[i]] = (uint32_t)i;
+}
+
+__global__ void k_rules_keys(const uint32_t* __restrict__ rec_q, const uint32_t* __restrict__ rec_r, int64_t m,
+                             const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
+                             const uint32_t* __restrict__ rid, const uint32_t* __restrict__ rfirst, int64_t batch,
+                             int qbits, int packed, uint32_t* __restrict__ k0, uint32_t* __restrict__ k1,
+                             uint32_t* __restrict__ k2) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t q = rec_q[i];
+        const uint32_t qa = perm ? perm[q] : q;
+        uint32_t run, qoff;
+        if (flags) {
+            run = rid[qa] + flags[qa] - 1u;
+            qoff = qa - rfirst[run];
+        } else if (batch > 0) {
+            run = (uint32_t)(qa / batch);
+            qoff = (uint32_t)(qa % batch);
+        } else {
+            run = 0;
+            qoff = qa;
+        }
+        if (packed) {
+            k0[i] = (rec_r[i] << qbits) | qoff;
+            k1[i] = run;
+        } else {
+            k0[i] = qoff;
+            k1[i] = rec_r[i];
+            k2[i] = run;
+        }
+    }
+}
+
+__global__ void k_gather_key(const uint32_t* __restrict__ key, const uint32_t* __restrict__ order, int64_t m,
+                             uint32_t* __restrict__ gk, uint32_t* __restrict__ gv) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = order ? order[i] : (uint32_t)i;
+        gk[i] = key[s];
+        gv[i] = s;
+    }
+}
+
+__global__ void k_rules_place(const shr_table* __restrict__ RT, const uint32_t* __restrict__ order, int64_t m,
+                              const uint32_t* __restrict__ rec_p, const uint32_t* __restrict__ rec_q,
+                              const uint32_t* __restrict__ rec_r, const uint32_t* __restrict__ perm,
+                              const int64_t* __restrict__ sts, const shd_cols* __restrict__ C, uint64_t seq_base,
+                              int n_out, uint64_t* __restrict__ out_seq, int32_t* __restrict__ out_query,
+                              int64_t* __restrict__ out_ts, int64_t* __restrict__ out_vals) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t id = order ? order[i] : (uint32_t)i;
+        const uint32_t p = rec_p[id], q = rec_q[id];
+        const shr_rule* R = RT->rules + rec_r[id];
+        if (out_seq) out_seq[i] = seq_base + (perm ? perm[q] : q);
+        if (out_query) out_query[i] = R->query;
+        if (out_ts) out_ts[i] = sts[q];
+        if (out_vals)
+            for (int o = 0; o < n_out; o++) {
+                int64_t v = 0;
+                if (o < R->n_out) {
+                    const int a = R->out_attr[o];
+                    v = load_attr(C, 0, a, RT->attr_type[a], R->out_slot[o] ? q : p);
+                }
+                out_vals[i * n_out + o] = v;
+            }
+    }
+}
+
+static int rules_ok() { return hipGetLastError() == hipSuccess ? 0 : -3; }
+
+extern "C" int shr_count(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
+                         const shd_cols* dC, uint32_t* cnt, int32_t* flag, void* stream) {
+    hipLaunchKernelGGL(k_rules_scan<0>, dim3(rgrid(n)), dim3(RTPB), 0, (hipStream_t)stream, dT, sts, skeys, n,
+                       sentinel, dC, cnt, (const uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                       (uint32_t*)nullptr, flag);
+    return rules_ok();
+}
+
+extern "C" int shr_write(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
+                         const shd_cols* dC, const uint32_t* cnt, const uint32_t* off, uint32_t* rec_p,
+                         uint32_t* rec_q, uint32_t* rec_r, void* stream) {
+    hipLaunchKernelGGL(k_rules_scan<1>, dim3(rgrid(n)), dim3(RTPB), 0, (hipStream_t)stream, dT, sts, skeys, n,
+                       sentinel, dC, (uint32_t*)cnt, off, rec_p, rec_q, rec_r, (int32_t*)nullptr);
+    return rules_ok();
+}
+
+extern "C" int shr_run_ids(const int32_t* akeys, int64_t n, int64_t batch, uint32_t* flags, uint32_t* rid,
+                           uint32_t* rfirst, uint32_t* scan_tmp, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_run_flags, dim3(rgrid(n)), dim3(RTPB), 0, st, akeys, n, batch, flags);
+    int rc = shd_exclusive_scan(flags, rid, n, scan_tmp, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_run_first, dim3(rgrid(n)), dim3(RTPB), 0, st, (const uint32_t*)flags, (const uint32_t*)rid,
+                       n, rfirst);
+    return rules_ok();
+}
+
+extern "C" int shr_keys(const uint32_t* rec_q, const uint32_t* rec_r, int64_t m, const uint32_t* perm,
+                        const uint32_t* flags, const uint32_t* rid, const uint32_t* rfirst, int64_t batch, int qbits,
+                        int packed, uint32_t* k0, uint32_t* k1, uint32_t* k2, void* stream) {
+    hipLaunchKernelGGL(k_rules_keys, dim3(rgrid(m)), dim3(RTPB), 0, (hipStream_t)stream, rec_q, rec_r, m, perm, flags,
+                       rid, rfirst, batch, qbits, packed, k0, k1, k2);
+    return rules_ok();
+}
+
+extern "C" int shr_gather(const uint32_t* key, const uint32_t* order, int64_t m, uint32_t* gk, uint32_t* gv,
+                          void* stream) {
+    hipLaunchKernelGGL(k_gather_key, dim3(rgrid(m)), dim3(RTPB), 0, (hipStream_t)stream, key, order, m, gk, gv);
+    return rules_ok();
+}
+
+extern "C" int shr_place(const shr_table* dT, const uint32_t* order, int64_t m, const uint32_t* rec_p,
+                         const uint32_t* rec_q, const uint32_t* rec_r, const uint32_t* perm, const int64_t* sts,
+                         const shd_cols* dC, uint64_t seq_base, int n_out, uint64_t* out_seq, int32_t* out_query,
+                         int64_t* out_ts, int64_t* out_vals, void* stream) {
+    hipLaunchKernelGGL(k_rules_place, dim3(rgrid(m)), dim3(RTPB), 0, (hipStream_t)stream, dT, order, m, rec_p, rec_q,
+                       rec_r, perm, sts, dC, seq_base, n_out, out_seq, out_query, out_ts, out_vals);
+    return rules_ok();
+}

@@ -19,15 +19,17 @@ class DeviceRunner:
         self.n_out = max([1] + [len(q.outs) for q in compiled.queries])
         self._out_cap = 0
 
-    def run(self, ts, keys, cols, n_keys, out_capacity=None, stream=None, batch_events=4096):
+    def run(self, ts, keys, cols, n_keys, out_capacity=None, stream=None, batch_events=4096, with_query=False):
         """ts/keys/cols: device tensors (int64 / int32 / stream attribute order);
         the events arrive as send(Event[]) calls of `batch_events`.
-        Returns (n_matches, out_seq[n], out_values[n, n_out]) as device tensors."""
+        Returns (n_matches, out_seq[n], out_values[n, n_out]) as device tensors,
+        plus out_query[n] (emitting query index) when `with_query`."""
         n = ts.numel()
         cap = out_capacity or n
         if self._out_cap < cap:
             self.out_seq = torch.empty(cap, dtype=torch.int64, device=self.device)
             self.out_vals = torch.empty(cap * self.n_out, dtype=torch.int64, device=self.device)
+            self.out_q = torch.empty(cap, dtype=torch.int32, device=self.device)
             self._out_cap = cap
         cp = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
         r = abi.sh_device_run()
@@ -41,10 +43,12 @@ class DeviceRunner:
         r.d_out_seq = self.out_seq.data_ptr()
         r.d_out_values = self.out_vals.data_ptr()
         r.stream = stream.cuda_stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        r.d_out_query = self.out_q.data_ptr() if with_query else None
         rc = lib().sh_run_device(self.handle.h, C.byref(r))
         check(self.handle.h, rc)
         m = int(r.out_count)
-        return m, self.out_seq[:m], self.out_vals[: m * self.n_out].view(m, self.n_out)
+        res = (m, self.out_seq[:m], self.out_vals[: m * self.n_out].view(m, self.n_out))
+        return res + (self.out_q[:m],) if with_query else res
 
     def kernel_times(self):
         t = abi.sh_kernel_times()

@@ -1,0 +1,66 @@
+"""GPU parity of the batch-compiled rule engine (sh_rules.hip, config C5) through
+sh_run_device, bit-exact against the CPU oracle: same rows, same order (same-key
+run, query, consuming event, opening event), same query ids and values. At C5
+size the device output is checked against the vectorised restatement
+(tests/c5_check.py, itself checked against the oracle on CPU)."""
+import numpy as np
+import pytest
+
+from c5_check import c5_expected
+from rules_cases import CASES, card_strings, case_data, oracle_run
+from siddhi_amd import compiler, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _device_run(text, n_cards, ts, card, amount, merchant, batch, partitioned=True):
+    import torch
+    from siddhi_amd.device_run import DeviceRunner
+    runner = DeviceRunner(compiler.compile_app(text, card_strings(n_cards)))
+    dev = torch.device("cuda:0")
+    cols = [torch.from_numpy(c).to(dev) for c in (card, amount, merchant)]
+    m, seq, vals, q = runner.run(torch.from_numpy(ts).to(dev), cols[0], cols, n_cards if partitioned else 1,
+                                 batch_events=batch, with_query=True)
+    torch.cuda.synchronize()
+    res = (seq.cpu().numpy(), vals.cpu().numpy(), q.cpu().numpy())
+    runner.close()
+    return res
+
+
+@pytest.mark.parametrize("general", [False, True], ids=["rules", "general"])
+@pytest.mark.parametrize("ci", range(len(CASES)))
+def test_rule_sets_vs_oracle(ci, general, monkeypatch):
+    case = CASES[ci]
+    n, cards, nr, rate, batch, merchants, partitioned, free, seed = case
+    if general:
+        if nr > 16:
+            pytest.skip("the general engine's query table holds 16 queries")
+        monkeypatch.setenv("SH_DISABLE_RULES", "1")
+    text, rules, (ts, card, amount, merchant) = case_data(case)
+    ref = oracle_run(text, cards, ts, card, amount, merchant, batch, partitioned)
+    seq, vals, q = _device_run(text, cards, ts, card, amount, merchant, batch, partitioned)
+    assert len(seq) == len(ref["seq"]) > 0
+    assert np.array_equal(seq, ref["seq"].astype(np.int64))
+    assert np.array_equal(q, ref["query"])
+    assert np.array_equal(vals[:, :2], ref["values"][:, :2])
+
+
+def test_c5_large_vs_vectorised_restatement():
+    """1,000 rules (BASELINE distributions), 20M card transactions, 200k cards."""
+    n, cards = 20_000_000, 200_000
+    ts, card, amount, merchant = synth.txn_stream(n, cards, 100)
+    rules = synth.c5_rules()
+    text = synth.c5_query(rules)
+    seq, vals, q = _device_run(text, cards, ts, card, amount, merchant, 4096)
+    eseq, erule, evals = c5_expected(ts, card, amount, merchant, rules)
+    assert len(seq) == len(eseq) > 0
+    assert np.array_equal(seq, eseq)
+    assert np.array_equal(q, erule)
+    assert np.array_equal(vals[:, :2], evals)
