@@ -38,12 +38,98 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2_000_000,
                     help="events of the same workload timed on the CPU oracle (0 = skip)")
     ap.add_argument("--no-verify", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
+                    help="c2 (default, BASELINE.json configs[1]); c3 / c5 measure the other configs")
+    ap.add_argument("--rules", type=int, default=1000, help="c5: rule count")
+    args = ap.parse_args()
+    if args.config == "c5" and args.keys == 10_000:
+        args.keys = 1_000_000
+    if args.config == "c3" and args.keys == 10_000:
+        args.keys = 1_000_000
+        if args.rate == 100:
+            args.rate = 1000
+    return args
+
+
+def log(msg):
+    """progress on stderr (long phases must keep writing, or the run looks hung)"""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def workload(args, rank):
+    """Synthetic stream, compiled app, columns, bytes and checks of one config."""
+    from siddhi_amd import compiler, synth
+    n, K = args.events, args.keys
+    if args.config == "c5":
+        ts, card, amount, merchant = synth.txn_stream(n, K, args.rate, seed=synth.SEED + 5 + 7919 * rank)
+        rules = synth.c5_rules(args.rules)
+        text = synth.c5_query(rules)
+        strings = compiler.StringDict()
+        compiled = compiler.compile_app(text, strings)
+
+        def verify(oseq, ovals, oq):
+            sys.path.insert(0, os.path.join(HERE, "tests"))
+            from c5_check import c5_expected
+            eseq, erule, evals = c5_expected(ts, card, amount, merchant, rules)
+            return bool(np.array_equal(oseq, eseq) and np.array_equal(oq, erule)
+                        and np.array_equal(ovals[:, :2], evals))
+
+        def cpu(s):
+            sys.path.insert(0, os.path.join(HERE, "tests"))
+            from oracle_engine import run_columns_oracle
+            run_columns_oracle(compiled, ts[:s], [card[:s], amount[:s], merchant[:s]], card[:s], batch=4096)
+
+        return dict(
+            ts=ts, keys=card, cols=[card, amount, merchant], compiled=compiled, verify=verify, cpu=cpu,
+            b_event=20, b_match=20, cpu_sample=min(args.cpu_sample, 4096),
+            desc=f"C5: {args.rules} fraud rules `every e1=Txn[amount > A and merchant == M] -> "
+                 f"e2=Txn[card == e1.card and amount > e1.amount * F] within W sec`, one partition (card of Txn)",
+            key_name="cards_per_gpu", bytes_note="event: ts 8 + card 4 + amount 4 + merchant 4 = 20 B; "
+            "match: seq 8 + query 4 + card 4 + amount 4 = 20 B")
+    ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=3 if args.config == "c3" else 2,
+                                              seed=synth.SEED + (3 if args.config == "c3" else 2) + 7919 * rank)
+    if args.config == "c3":
+        compiled = compiler.compile_app(synth.C3_QUERY)
+
+        def verify(oseq, ovals, oq):
+            return None  # C3 parity: tests/test_gpu_nfa.py (oracle, key subsets at full size)
+
+        def cpu(s):
+            sys.path.insert(0, os.path.join(HERE, "tests"))
+            from oracle_engine import run_stock_oracle
+            run_stock_oracle(compiled, ts[:s], keys[:s], price[:s], vol[:s], batch=4096)
+
+        return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, verify=verify, cpu=cpu,
+                    b_event=16, b_match=20, cpu_sample=args.cpu_sample,
+                    desc="C3: every e1=S, e2=S[price>e1.price]+, e3=S[price<e2[last].price], "
+                         "partition with (symbol of S)", key_name="keys_per_gpu",
+                    bytes_note="event: ts 8 + symbol 4 + price 4 = 16 B; match: seq 8 + 3 x price 4 = 20 B")
+    compiled = compiler.compile_app(synth.C2_QUERY)
+
+    def verify(oseq, ovals, oq):
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        from c2_check import c2_expected
+        eseq, evals = c2_expected(ts, keys, price, vol)
+        return bool(len(oseq) == len(eseq) and np.array_equal(oseq, eseq) and np.array_equal(ovals, evals))
+
+    def cpu(s):
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        from oracle_engine import run_stock_oracle
+        run_stock_oracle(compiled, ts[:s], keys[:s], price[:s], vol[:s], batch=4096)
+
+    return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, verify=verify, cpu=cpu,
+                b_event=24, b_match=28, cpu_sample=args.cpu_sample,
+                desc="C2: every e1[price>20] -> e2[symbol==e1.symbol and price>e1.price] within 1 sec, "
+                     "partition with (symbol of StockStream)", key_name="symbols_per_gpu",
+                bytes_note="event: ts 8 + symbol 4 + price 4 + volume 8 = 24 B; "
+                           "match: seq 8 + symbol 4 + p1 4 + p2 4 + v2 8 = 28 B")
+
+
+import numpy as np  # noqa: E402
 
 
 def main():
     args = parse()
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -55,26 +141,25 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device(f"cuda:{local}")
 
-    from siddhi_amd import compiler, synth
     from siddhi_amd.device_run import DeviceRunner
 
     n, K = args.events, args.keys
-    # each rank: its own stream over its own symbol range (weak scaling)
-    ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=2, seed=synth.SEED + 2 + 7919 * rank)
-    compiled = compiler.compile_app(synth.C2_QUERY)
-    runner = DeviceRunner(compiled, device=str(dev))
-    t_ts = torch.from_numpy(ts).to(dev)
-    t_k = torch.from_numpy(keys).to(dev)
-    t_p = torch.from_numpy(price).to(dev)
-    t_v = torch.from_numpy(vol).to(dev)
-    cols = [t_k, t_p, t_v]
+    log(f"generating {args.config} workload: {n} events, {K} keys")
+    W = workload(args, rank)   # each rank: its own stream over its own key range (weak scaling)
+    runner = DeviceRunner(W["compiled"], device=str(dev))
+    t_ts = torch.from_numpy(W["ts"]).to(dev)
+    cols = [torch.from_numpy(c).to(dev) for c in W["cols"]]
+    t_k = cols[0]
     stream = torch.cuda.current_stream(dev)
+    with_q = args.config == "c5"
 
     def step():
-        return runner.run(t_ts, t_k, cols, K, stream=stream)
+        r = runner.run(t_ts, t_k, cols, K, stream=stream, with_query=with_q)
+        return r if with_q else r + (None,)
 
+    log("warmup")
     for _ in range(args.warmup):
-        m, _, _ = step()
+        m, _, _, _ = step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -82,7 +167,7 @@ def main():
     seg = adv = emt = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        m, oseq, ovals = step()
+        m, oseq, ovals, oq = step()
         kt = runner.kernel_times()
         seg += kt["segment_ms"]
         adv += kt["advance_ms"]
@@ -100,10 +185,9 @@ def main():
     events_total = n * world
     value = events_total * args.steps / dt
 
-    # algorithmic bytes: event columns the query reads
-    # (ts 8 + symbol 4 + price 4 + volume 8 = 24 B) + emitted record
-    # (trigger seq 8 + symbol 4 + p1 4 + p2 4 + v2 8 = 28 B)
-    b_alg = 24 * n + 28 * m
+    # algorithmic bytes: event columns the query reads + the
+    # emitted records (see W["bytes_note"])
+    b_alg = W["b_event"] * n + W["b_match"] * m
     adv_ms = adv / args.steps
     seg_ms = seg / args.steps
     emt_ms = emt / args.steps
@@ -117,16 +201,13 @@ def main():
 
     verified = None
     if not args.no_verify and rank == 0:
-        sys.path.insert(0, os.path.join(HERE, "tests"))
-        from c2_check import c2_expected
-        eseq, evals = c2_expected(ts, keys, price, vol)
-        verified = bool(m == len(eseq) and np.array_equal(oseq.cpu().numpy(), eseq)
-                        and np.array_equal(ovals.cpu().numpy(), evals))
+        log("verifying the full output against the vectorised restatement")
+        verified = W["verify"](oseq.cpu().numpy(), ovals.cpu().numpy(), oq.cpu().numpy() if oq is not None else None)
 
     # HBM bytes per step from the committed rocprofv3 PMC passes of this
     # workload (scripts/pmc_traffic.py), when they match the configuration
     traffic = None
-    prof = os.path.join(HERE, "profiles", "pmc_c2.json")
+    prof = os.path.join(HERE, "profiles", f"pmc_{args.config}.json")
     if os.path.exists(prof):
         try:
             pj = json.load(open(prof))
@@ -137,15 +218,14 @@ def main():
 
     cpu = None
     if rank == 0 and args.cpu_sample > 0:
-        sys.path.insert(0, os.path.join(HERE, "tests"))
-        from oracle_engine import run_stock_oracle
-        s = min(args.cpu_sample, n)
+        s = min(W["cpu_sample"], n)
+        log(f"CPU baseline on {s} events")
         t1 = time.perf_counter()
-        run_stock_oracle(compiled, ts[:s], keys[:s], price[:s], vol[:s], batch=4096)
+        W["cpu"](s)
         cdt = time.perf_counter() - t1
         cpu = {"value": s / cdt, "unit": "events/s", "cores": 1, "kind": "port",
-               "sample": f"first {s} events of the same C2 stream, send(Event[]) batches of 4096, "
-                         f"C++ restatement of siddhi-core's processors (oracle/), 1 thread"}
+               "sample": f"first {s} events of the same {args.config.upper()} stream, send(Event[]) batches of "
+                         f"4096, C++ restatement of siddhi-core's processors (oracle/), 1 thread"}
 
     if rank == 0:
         line = {
@@ -153,14 +233,12 @@ def main():
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic",
-            "config": {"workload": "C2: every e1[price>20] -> e2[symbol==e1.symbol and price>e1.price] "
-                                   "within 1 sec, partition with (symbol of StockStream)",
-                       "events_per_gpu": n, "symbols_per_gpu": K, "rate_ev_per_ms": args.rate,
-                       "matches_per_gpu": int(m), "parallelism": f"key-sharded x{world}"},
+            "config": {"workload": W["desc"], "events_per_gpu": n, W["key_name"]: K, "rate_ev_per_ms": args.rate,
+                       "matches_per_gpu": int(m), "parallelism": f"key-sharded x{world}",
+                       "bytes": W["bytes_note"]},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": traffic,
-                         "kernel": "matcher step (all kernels: radix segment, shj_match, count scatter, scan, "
-                                   "shj_place)",
+                         "kernel": "matcher step (every kernel of one pass, HIP events on the launch stream)",
                          "kernels_ms_per_step": step_kernels_ms, "algorithmic_bytes": b_alg,
                          "match_kernel_only_GBps": match_only / 1e9},
             "phase_ms": {"segment": seg_ms, "advance": adv_ms, "emit": emt_ms},
