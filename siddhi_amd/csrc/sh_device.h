@@ -57,6 +57,17 @@ struct shd_payload {
     uint8_t width[8];        // 1, 4 or 8 bytes
 };
 
+// arrival-tile directory of a tile-major segment: run of key k in tile a is
+// [dstart[a*K1+k], dend[a*K1+k]) (empty when equal)
+struct shd_tiles {
+    const uint32_t* dstart;
+    const uint32_t* dend;
+    uint32_t K1;             // keys + 1 (the null-key sentinel bucket)
+    uint32_t ntile;
+    int32_t shift;           // log2 events per tile
+    int32_t pad;
+};
+
 // scratch of the window engine (sh_window.hip)
 struct shd_window_ws {
     int32_t* match_pos;      // [n] consuming position of the partial opened at p, -1 none
@@ -76,10 +87,12 @@ size_t shd_scan_tmp_words(int64_t n);
 int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
                 const uint32_t** perm_out, const uint32_t** skeys_out);
 // as shd_segment, also moving `carry` columns into key-segment order; `mid`
-// holds one intermediate buffer per carried column (multi-pass ping-pong)
+// holds one intermediate buffer per carried column (multi-pass ping-pong).
+// tile_shift >= 12 sorts each arrival tile of 2^tile_shift events by key in its
+// own region ((tile, key, arrival) order); want_segments = 0 skips the segment list
 int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
                         const uint32_t** perm_out, const uint32_t** skeys_out, const shd_payload* carry,
-                        void* const* mid);
+                        void* const* mid, int tile_shift, int want_segments);
 int shd_advance(const shp_program* dprog, const shp_layout* lay, uint8_t* kstate, int32_t nkeys,
                 const shd_batch* b, const uint32_t* perm, const uint32_t* skeys,
                 const uint32_t* seg_off, const shd_cols* dcols, const shd_emit* em, void* stream, int fast_ok);
@@ -94,7 +107,9 @@ int shd_window(const shp_program* dprog, const shp_program* hprog, const shd_bat
                const uint32_t* perm, const uint32_t* skeys, const int64_t* sts, const void* const* scols,
                shd_window_ws* ws, shd_cols* d_sorted_desc, uint32_t* scan_tmp, uint64_t* out_seq,
                int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, int64_t out_cap, int64_t* n_matches,
-               void* stream, void* ev_mid, const void* jit);
+               void* stream, void* ev_mid, const void* jit, const shd_tiles* tiles);
+int shd_tile_dir(const uint32_t* skeys, int64_t n, int shift, uint32_t K1, uint32_t ntile, uint32_t* ds,
+                 uint32_t* de, void* stream);
 int shd_relayout(const uint8_t* src, const shp_layout* A, uint8_t* dst, const shp_layout* B, int32_t nkeys,
                  int32_t n_states, int32_t n_out, void* stream);
 int shd_sort_pairs(const uint32_t* keys, const uint32_t* vals, int64_t n, int bits, uint32_t* const* kbuf,

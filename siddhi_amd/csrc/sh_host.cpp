@@ -332,7 +332,7 @@ struct sh_handle {
     // workspaces
     DevBuf w_ts, w_stream, w_row, w_key, w_keys_a, w_keys_b, w_idx_a, w_idx_b, w_hist, w_scan, w_seg;
     DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls, w_oq;
-    DevBuf v_sts, v_mpos, v_flag, v_cnts, v_mid_ts;
+    DevBuf v_sts, v_mpos, v_flag, v_cnts, v_mid_ts, v_dir;
     DevBuf v_scol[32], v_mid[32];
     int64_t tmp_cap = 0;
     // drained output queue (host)
@@ -734,6 +734,7 @@ void sh_destroy(sh_handle* h) {
         h->v_flag.release();
         h->v_cnts.release();
         h->v_mid_ts.release();
+        h->v_dir.release();
         for (auto& b : h->v_scol) b.release();
         for (auto& b : h->v_mid) b.release();
         DevBuf* bufs[] = {&h->d_prog, &h->d_cols_desc, &h->d_kstate, &h->d_err, &h->w_ts, &h->w_stream, &h->w_row,
@@ -837,7 +838,9 @@ static int ensure_keys(sh_handle* h, int32_t nkeys) {
 }
 
 static int ensure_ws(sh_handle* h, int64_t n) {
-    const int64_t tiles = (n + 4095) / 4096;
+    // radix blocks of 4096, padded to whole arrival tiles (<= 2^20 events) for
+    // the tile-major segment layout
+    const int64_t tiles = (n + 4095) / 4096 + 256;
     int rc = 0;
     rc |= h->w_keys_a.ensure_fresh(n * 4);
     rc |= h->w_keys_b.ensure_fresh(n * 4);
@@ -1509,25 +1512,47 @@ static shd_segment_ws seg_ws(sh_handle* h, int64_t n) {
 }
 
 // ts and every column of stream 0 moved into key-segment order by the segment
-static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid) {
+// A 4-byte column that is the key array itself (the partition attribute, passed
+// as the same device buffer) is not carried: its key-segment order is the
+// sorted key array (*alias = that attribute, -1 if none). Null-key events
+// (sorted to the sentinel bucket) are never read.
+static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid, int* alias) {
     const int64_t n = run->n;
     const int na = (int)h->stream_types[0].size();
     memset(carry, 0, sizeof(*carry));
+    *alias = -1;
     if (h->v_sts.ensure_fresh(n * 8) || h->v_mid_ts.ensure_fresh(n * 8)) return SH_E_OOM;
-    carry->n = 1 + na;
-    carry->src[0] = run->d_ts;
-    carry->dst[0] = h->v_sts.p;
-    carry->width[0] = 8;
-    mid[0] = h->v_mid_ts.p;
+    int c = 0;
+    carry->src[c] = run->d_ts;
+    carry->dst[c] = h->v_sts.p;
+    carry->width[c] = 8;
+    mid[c++] = h->v_mid_ts.p;
     for (int a = 0; a < na; a++) {
         const int w = type_width(h->stream_types[0][a]);
+        if (*alias < 0 && w == 4 && run->d_cols[a] == (const void*)run->d_keys && !getenv("SH_NO_KEY_ALIAS")) {
+            *alias = a;
+            continue;
+        }
         if (h->v_scol[a].ensure_fresh(n * w) || h->v_mid[a].ensure_fresh(n * w)) return SH_E_OOM;
-        carry->src[1 + a] = run->d_cols[a];
-        carry->dst[1 + a] = h->v_scol[a].p;
-        carry->width[1 + a] = (uint8_t)w;
-        mid[1 + a] = h->v_mid[a].p;
+        carry->src[c] = run->d_cols[a];
+        carry->dst[c] = h->v_scol[a].p;
+        carry->width[c] = (uint8_t)w;
+        mid[c++] = h->v_mid[a].p;
     }
+    carry->n = c;
     return SH_OK;
+}
+
+// log2 of the arrival tile (0: untiled) for a partitioned window run: tiles of
+// 2^19 events when the stream spans several and the directory stays small
+// (SH_TILE_SHIFT overrides, for tests)
+static int tile_shift_for(int64_t n, int32_t nkeys) {
+    int shift = 19;
+    if (const char* e = getenv("SH_TILE_SHIFT")) shift = atoi(e);
+    if (shift < 12 || shift > 24) return 0;
+    const int64_t ntile = (n + ((int64_t)1 << shift) - 1) >> shift;
+    if (ntile < 2 || ntile * ((int64_t)nkeys + 1) > ((int64_t)1 << 26)) return 0;
+    return shift;
 }
 
 // batch-compiled rule sets (sh_rules.hip) over HBM-resident columns
@@ -1547,18 +1572,20 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
     B.n = n;
     shd_payload carry;
     void* mid[8] = {nullptr};
-    if (sorted && carry_setup(h, run, &carry, mid)) return fail(h, SH_E_OOM, "rule workspace");
+    int alias = -1;
+    if (sorted && carry_setup(h, run, &carry, mid, &alias)) return fail(h, SH_E_OOM, "rule workspace");
     hipEventRecord(h->ev[0], st);
     shd_segment_ws ws = seg_ws(h, n);
     const uint32_t* perm = nullptr;
     const uint32_t* skeys = nullptr;
-    if (shd_segment_payload(&B, nkeys, &ws, st, &perm, &skeys, sorted ? &carry : nullptr, mid))
+    if (shd_segment_payload(&B, nkeys, &ws, st, &perm, &skeys, sorted ? &carry : nullptr, mid, 0, 0))
         return fail(h, SH_E_HIP, "segment launch failed");
     hipEventRecord(h->ev[1], st);
     const int64_t* sts = sorted ? h->v_sts.as<int64_t>() : run->d_ts;
     shd_cols sc;
     memset(&sc, 0, sizeof(sc));
     for (int a = 0; a < na; a++) sc.col[0][a] = sorted ? (const void*)h->v_scol[a].p : run->d_cols[a];
+    if (alias >= 0) sc.col[0][alias] = skeys;
     hipMemcpyAsync(h->d_cols_desc.p, &sc, sizeof(sc), hipMemcpyHostToDevice, st);
     const shd_cols* dC = h->d_cols_desc.as<shd_cols>();
     const shr_table* dT = h->rd_tab.as<shr_table>();
@@ -1733,49 +1760,42 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
         if (h->v_mpos.ensure_fresh(n * 4) || h->v_flag.ensure_fresh(64) || h->v_cnts.ensure_fresh(n * 4))
             return fail(h, SH_E_OOM, "window workspace");
         shd_payload carry;
-        memset(&carry, 0, sizeof(carry));
         void* mid[8] = {nullptr};
-        if (sorted) {
-            if (h->v_sts.ensure_fresh(n * 8) || h->v_mid_ts.ensure_fresh(n * 8))
-                return fail(h, SH_E_OOM, "window workspace");
-            carry.n = 1 + na;
-            carry.src[0] = run->d_ts;
-            carry.dst[0] = h->v_sts.p;
-            carry.width[0] = 8;
-            mid[0] = h->v_mid_ts.p;
-            for (int a = 0; a < na; a++) {
-                const int w = type_width(h->stream_types[0][a]);
-                if (h->v_scol[a].ensure_fresh(n * w) || h->v_mid[a].ensure_fresh(n * w))
-                    return fail(h, SH_E_OOM, "window workspace");
-                carry.src[1 + a] = run->d_cols[a];
-                carry.dst[1 + a] = h->v_scol[a].p;
-                carry.width[1 + a] = (uint8_t)w;
-                mid[1 + a] = h->v_mid[a].p;
-            }
-        }
+        int alias = -1;
+        if (sorted && carry_setup(h, run, &carry, mid, &alias)) return fail(h, SH_E_OOM, "window workspace");
         wws.match_pos = h->v_mpos.as<int32_t>();
         wws.cnt_s = h->v_cnts.as<uint32_t>();
         wws.cnt = h->w_cnt.as<uint32_t>();
         wws.off = h->w_off.as<uint32_t>();
         wws.flag = h->v_flag.as<int32_t>();
+        // arrival tiles: the sorted order becomes (tile, key, arrival), so the
+        // count scatter and the ordered placement touch one tile's output window
+        // at a time (L2 / Infinity-Cache resident) instead of the whole stream
+        const int tshift = sorted ? tile_shift_for(n, nkeys) : 0;
         hipEventRecord(h->ev[0], st);
-        shd_segment_ws ws;
-        ws.keys_a = h->w_keys_a.as<uint32_t>();
-        ws.keys_b = h->w_keys_b.as<uint32_t>();
-        ws.idx_a = h->w_idx_a.as<uint32_t>();
-        ws.idx_b = h->w_idx_b.as<uint32_t>();
-        ws.hist = h->w_hist.as<uint32_t>();
-        ws.scan_tmp = h->w_scan.as<uint32_t>();
-        ws.seg_off = h->w_seg.as<uint32_t>();
-        ws.cap = n;
+        shd_segment_ws ws = seg_ws(h, n);
         const uint32_t* perm = nullptr;
         const uint32_t* skeys = nullptr;
-        if (shd_segment_payload(&B, nkeys, &ws, st, &perm, &skeys, sorted ? &carry : nullptr, mid))
+        if (shd_segment_payload(&B, nkeys, &ws, st, &perm, &skeys, sorted ? &carry : nullptr, mid, tshift, 0))
             return fail(h, SH_E_HIP, "segment launch failed");
+        shd_tiles TL;
+        memset(&TL, 0, sizeof(TL));
+        if (tshift) {
+            TL.K1 = (uint32_t)nkeys + 1;
+            TL.ntile = (uint32_t)((n + ((int64_t)1 << tshift) - 1) >> tshift);
+            TL.shift = tshift;
+            const size_t words = (size_t)TL.ntile * TL.K1;
+            if (h->v_dir.ensure_fresh(words * 8)) return fail(h, SH_E_OOM, "tile directory");
+            TL.dstart = h->v_dir.as<uint32_t>();
+            TL.dend = h->v_dir.as<uint32_t>() + words;
+            if (shd_tile_dir(skeys, n, tshift, TL.K1, TL.ntile, (uint32_t*)TL.dstart, (uint32_t*)TL.dend, st))
+                return fail(h, SH_E_HIP, "tile directory launch failed");
+        }
         hipEventRecord(h->ev[1], st);
         const int64_t* sts = sorted ? h->v_sts.as<int64_t>() : run->d_ts;
         const void* scols[32];
         for (int a = 0; a < na; a++) scols[a] = sorted ? (const void*)h->v_scol[a].p : run->d_cols[a];
+        if (alias >= 0) scols[alias] = skeys;  // the partition column in key-segment order is the sorted key
         if (h->jit_state == 0) {
             if (getenv("SH_DISABLE_JIT")) {
                 h->jit_state = -1;
@@ -1787,7 +1807,7 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
         int wrc = shd_window(h->d_prog.as<shp_program>(), &h->prog, &B, nkeys, perm, skeys, sts, scols, &wws,
                              h->d_cols_desc.as<shd_cols>(), h->w_scan.as<uint32_t>(), run->d_out_seq, nullptr,
                              run->d_out_values, nullptr, run->out_capacity, &nm, st, h->ev[2],
-                             h->jit_state == 1 ? &h->jit : nullptr);
+                             h->jit_state == 1 ? &h->jit : nullptr, tshift ? &TL : nullptr);
         hipEventRecord(h->ev[3], st);
         if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in window engine");
         if (wrc < 0) return fail(h, SH_E_HIP, "window engine launch failed");

@@ -308,7 +308,8 @@ bool generate(const shp_program& P, std::string& src) {
 extern "C" __global__ void __launch_bounds__(SHJ_TILE)
 shj_match(const int64_t* __restrict__ sts, const uint32_t* __restrict__ skeys, int64_t n, uint32_t sentinel,
           const shd_cols* __restrict__ C, int32_t* __restrict__ match_pos, uint32_t* __restrict__ cnt,
-          int32_t* __restrict__ flag, uint32_t tiles_per_xcd, uint32_t ntiles) {
+          int32_t* __restrict__ flag, uint32_t tiles_per_xcd, uint32_t ntiles, shd_tiles TL) {
+const TileDir D = tile_dir(TL);
 __shared__ int64_t s_ts[SHJ_SPAN];
 __shared__ uint32_t s_key[SHJ_SPAN];
 )";
@@ -332,7 +333,11 @@ if (p >= n) return;
 const uint32_t key = s_key[threadIdx.x];
 if (key == sentinel) return;
 const int64_t t0 = s_ts[threadIdx.x];
-if (p > 0) {  // the reduction to a forward scan needs non-decreasing timestamps per key
+// the reduction to a forward scan needs non-decreasing timestamps per key
+if (D.on()) {
+    const int64_t pp = key_pred(D, skeys, p, key);
+    if (pp >= 0 && t0 < sts[pp]) atomicExch(flag, 1);
+} else if (p > 0) {
     uint32_t kp;
     int64_t tp;
     if (threadIdx.x) { kp = s_key[threadIdx.x - 1]; tp = s_ts[threadIdx.x - 1]; }
@@ -343,7 +348,10 @@ if (p > 0) {  // the reduction to a forward scan needs non-decreasing timestamps
     src += decl_attrs(a0_m, 0) + load_attrs(P, a0_m, 0, "p", &a1_m, "threadIdx.x");
     src += "{\nbool ok = true;\n" + f0 + "if (!ok) return;\n}\n";
     src += decl_attrs(a1_m, 1);
-    src += R"(for (int64_t q = p + 1; q < n; q++) {
+    src += R"(uint32_t ta = D.on() ? D.tile(p) : 0u;
+int64_t qend = D.on() ? (int64_t)D.de[D.at(ta, key)] : n;
+for (int64_t q = p + 1;; q++) {
+    if (q >= qend && !(D.on() && D.next(ta, key, q, qend))) break;
     uint32_t kq;
     int64_t tq;
     if (q < lim) {
@@ -377,7 +385,8 @@ shj_place(const int64_t* __restrict__ sts, const uint32_t* __restrict__ skeys, c
           int64_t n, const shd_cols* __restrict__ C, const int32_t* __restrict__ match_pos,
           const uint32_t* __restrict__ off, uint64_t seq_base, uint64_t* __restrict__ out_seq,
           int64_t* __restrict__ out_ts, int64_t* __restrict__ out_vals, uint8_t* __restrict__ out_nulls,
-          uint32_t tiles_per_xcd, uint32_t ntiles) {
+          uint32_t tiles_per_xcd, uint32_t ntiles, shd_tiles TL) {
+const TileDir D = tile_dir(TL);
 __shared__ int64_t s_ts[SHJ_SPAN];
 __shared__ uint32_t s_key[SHJ_SPAN];
 __shared__ int32_t s_mp[SHJ_SPAN];
@@ -402,7 +411,10 @@ if (q < 0) return;
 const uint32_t key = s_key[p - lo];
 const int64_t tq = (q < hi) ? s_ts[q - lo] : sts[q];
 uint32_t rank = 0;  // partials of the key consumed by q before this one (creation order)
-for (int64_t r = p - 1; r >= 0; r--) {
+uint32_t ta = D.on() ? D.tile(p) : 0u;
+int64_t rbeg = D.on() ? (int64_t)D.ds[D.at(ta, key)] : 0;
+for (int64_t r = p - 1;; r--) {
+    if (r < rbeg && !(D.on() && D.prev(ta, key, r, rbeg))) break;
     uint32_t kr;
     int64_t tr;
     int32_t mr;

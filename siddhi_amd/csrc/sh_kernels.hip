@@ -120,10 +120,20 @@ extern "C" int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, 
 }
 
 // ------------------------------------------------------------------ radix segment
-// digit histogram per tile, digit-major: hist[d * ntiles + tile]
+// Histogram layout. Global (sub_shift < 0): digit-major, hist[d * ntiles + blk],
+// so the exclusive scan orders all blocks by digit. Arrival-tile-major
+// (sub_shift >= 0, 2^sub_shift blocks per arrival tile): hist[(tile, d, blk in
+// tile)], so the scan keeps every arrival tile in its own region and sorts each
+// tile by key: the stable LSD passes then produce (tile, key, arrival) order.
+__device__ __forceinline__ int64_t hist_idx(uint32_t d, uint32_t blk, int64_t ntiles, int sub_shift) {
+    if (sub_shift < 0) return (int64_t)d * ntiles + blk;
+    return ((((int64_t)(blk >> sub_shift)) * 256 + d) << sub_shift) + (blk & ((1u << sub_shift) - 1u));
+}
+
+// digit histogram per block (layout: hist_idx)
 __global__ void __launch_bounds__(TPB) k_digit_hist(const uint32_t* __restrict__ keys, const int32_t* __restrict__ raw,
                                                     uint32_t sentinel, int64_t n, int shift,
-                                                    uint32_t* __restrict__ hist, int64_t ntiles) {
+                                                    uint32_t* __restrict__ hist, int64_t ntiles, int sub_shift) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
@@ -143,7 +153,7 @@ __global__ void __launch_bounds__(TPB) k_digit_hist(const uint32_t* __restrict__
         }
     }
     __syncthreads();
-    hist[(int64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+    hist[hist_idx(threadIdx.x, blockIdx.x, ntiles, sub_shift)] = h[threadIdx.x];
 }
 
 // stable scatter: elements of a tile are ranked in arrival order within their
@@ -160,7 +170,7 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
                                                        uint32_t sentinel, const uint32_t* __restrict__ idx_in, int64_t n,
                                                        int shift, const uint32_t* __restrict__ offs, int64_t ntiles,
                                                        uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out,
-                                                       shd_payload PL) {
+                                                       shd_payload PL, int sub_shift) {
     __shared__ uint32_t running[256];
     __shared__ uint32_t tstart[256];
     __shared__ uint32_t gbase[256];
@@ -173,7 +183,7 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
     const int64_t tile_n = (n - base) < RADIX_TILE ? (n - base) : RADIX_TILE;
     // tile histogram -> tile-local digit starts
     running[threadIdx.x] = 0;
-    gbase[threadIdx.x] = offs[(int64_t)threadIdx.x * ntiles + blockIdx.x];
+    gbase[threadIdx.x] = offs[hist_idx(threadIdx.x, blockIdx.x, ntiles, sub_shift)];
     __syncthreads();
     uint32_t key[RADIX_ITEMS];
 #pragma unroll
@@ -639,11 +649,14 @@ static uint32_t g_bits_for(uint32_t maxkey) {
 
 extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
                                    const uint32_t** perm_out, const uint32_t** skeys_out, const shd_payload* carry,
-                                   void* const* mid) {
+                                   void* const* mid, int tile_shift, int want_segments) {
     hipStream_t st = (hipStream_t)stream;
     const int64_t n = b->n;
     const uint32_t sentinel = (uint32_t)nkeys;
-    const int64_t ntiles = ceil_div(n, RADIX_TILE);
+    // arrival tiles of 2^tile_shift events (0: one global segment order)
+    const int sub_shift = tile_shift >= 12 ? tile_shift - 12 : -1;
+    int64_t ntiles = ceil_div(n, RADIX_TILE);
+    if (sub_shift >= 0) ntiles = ceil_div(ntiles, (int64_t)1 << sub_shift) << sub_shift;
     const uint32_t bits = g_bits_for(sentinel);
     const int passes = b->keys ? (int)((bits + 7) / 8) : 0;
     const uint32_t* kin = nullptr;
@@ -653,7 +666,7 @@ extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segmen
     for (int ps = 0; ps < passes; ps++) {
         const int shift = ps * 8;
         hipLaunchKernelGGL(k_digit_hist, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, b->keys, sentinel, n, shift,
-                           ws->hist, ntiles);
+                           ws->hist, ntiles, sub_shift);
         int rc = shd_exclusive_scan(ws->hist, ws->hist, 256 * ntiles, ws->scan_tmp, stream);
         if (rc) return rc;
         // payload ping-pong: pass ps reads the previous pass's output (or the
@@ -672,7 +685,7 @@ extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segmen
             }
         }
         hipLaunchKernelGGL(k_digit_scatter, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, b->keys, sentinel, iin, n,
-                           shift, (const uint32_t*)ws->hist, ntiles, kout, iout, PL);
+                           shift, (const uint32_t*)ws->hist, ntiles, kout, iout, PL, sub_shift);
         kin = kout;
         iin = iout;
         kout = (kout == ws->keys_a) ? ws->keys_b : ws->keys_a;
@@ -681,6 +694,7 @@ extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segmen
     // kin/iin: sorted keys / permutation (NULL when nothing to sort: single key)
     *perm_out = iin;
     *skeys_out = kin;
+    if (!want_segments) return hipGetLastError() == hipSuccess ? 0 : -3;
     uint32_t* flags = ws->seg_off;          // [n]
     uint32_t* pos = ws->seg_off + n;        // [n]
     uint32_t* seg_list = ws->seg_off + 2 * n;  // [n + 1]
@@ -709,11 +723,12 @@ extern "C" int shd_sort_pairs(const uint32_t* keys, const uint32_t* vals, int64_
     for (int ps = 0; ps < passes && n > 0; ps++) {
         const int shift = ps * 8;
         hipLaunchKernelGGL(k_digit_hist, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
-                           0xFFFFFFFFu, n, shift, hist, ntiles);
+                           0xFFFFFFFFu, n, shift, hist, ntiles, -1);
         int rc = shd_exclusive_scan(hist, hist, 256 * ntiles, scan_tmp, stream);
         if (rc) return rc;
         hipLaunchKernelGGL(k_digit_scatter, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
-                           0xFFFFFFFFu, vin, n, shift, (const uint32_t*)hist, ntiles, kbuf[ps & 1], vbuf[ps & 1], PL);
+                           0xFFFFFFFFu, vin, n, shift, (const uint32_t*)hist, ntiles, kbuf[ps & 1], vbuf[ps & 1], PL,
+                           -1);
         kin = kbuf[ps & 1];
         vin = vbuf[ps & 1];
     }
@@ -724,7 +739,7 @@ extern "C" int shd_sort_pairs(const uint32_t* keys, const uint32_t* vals, int64_
 
 extern "C" int shd_segment(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
                            const uint32_t** perm_out, const uint32_t** skeys_out) {
-    return shd_segment_payload(b, nkeys, ws, stream, perm_out, skeys_out, nullptr, nullptr);
+    return shd_segment_payload(b, nkeys, ws, stream, perm_out, skeys_out, nullptr, nullptr, 0, 1);
 }
 
 extern "C" int shd_advance(const shp_program* dprog, const shp_layout* lay, uint8_t* kstate, int32_t nkeys,

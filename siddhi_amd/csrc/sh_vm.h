@@ -354,3 +354,69 @@ __device__ __forceinline__ bool terms_pass2(const shp_program* __restrict__ P, i
     }
     return true;
 }
+
+// Arrival-tile-major segments (shd_tiles): the events of a key are spread over
+// the runs [dstart, dend) of that key in consecutive arrival tiles. A forward
+// scan that leaves its run continues at the key's run in the next non-empty
+// tile, a backward scan at the previous one; untiled segments keep one run per
+// key and the scans stop at the key change.
+struct TileDir {
+    const uint32_t* ds;
+    const uint32_t* de;
+    uint32_t K1, ntile;
+    int32_t shift;
+    __device__ bool on() const { return ds != nullptr; }
+    __device__ uint32_t tile(int64_t p) const { return (uint32_t)(p >> shift); }
+    __device__ size_t at(uint32_t a, uint32_t key) const { return (size_t)a * K1 + key; }
+    // next non-empty run of `key` after tile a (a advances); false when none
+    __device__ bool next(uint32_t& a, uint32_t key, int64_t& q, int64_t& qend) const {
+        while (++a < ntile) {
+            const size_t e = at(a, key);
+            const uint32_t s0 = ds[e], e0 = de[e];
+            if (e0 > s0) {
+                q = s0;
+                qend = e0;
+                return true;
+            }
+        }
+        return false;
+    }
+    // previous non-empty run of `key` before tile a (a decreases); false when none
+    __device__ bool prev(uint32_t& a, uint32_t key, int64_t& r, int64_t& rbeg) const {
+        while (a > 0) {
+            a--;
+            const size_t e = at(a, key);
+            const uint32_t s0 = ds[e], e0 = de[e];
+            if (e0 > s0) {
+                r = (int64_t)e0 - 1;
+                rbeg = s0;
+                return true;
+            }
+        }
+        return false;
+    }
+};
+
+__device__ __forceinline__ TileDir tile_dir(const shd_tiles& T) {
+    TileDir d;
+    d.ds = T.dstart;
+    d.de = T.dend;
+    d.K1 = T.K1;
+    d.ntile = T.ntile;
+    d.shift = T.shift;
+    return d;
+}
+
+// position of the previous event of p's key (-1: none); the same-key
+// predecessor check of the non-decreasing-timestamp premise
+__device__ __forceinline__ int64_t key_pred(const TileDir& D, const uint32_t* __restrict__ skeys, int64_t p,
+                                            uint32_t key) {
+    if (D.on()) {
+        uint32_t a = D.tile(p);
+        if ((int64_t)D.ds[D.at(a, key)] < p) return p - 1;
+        int64_t r, rb;
+        return D.prev(a, key, r, rb) ? r : -1;
+    }
+    if (p == 0 || (skeys && skeys[p - 1] != key)) return -1;
+    return p - 1;
+}

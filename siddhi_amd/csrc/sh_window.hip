@@ -45,19 +45,34 @@ __global__ void k_permute(const T* __restrict__ src, const uint32_t* __restrict_
         dst[p] = src[perm[p]];
 }
 
+// build the tile directory of a tile-major segment (pre-zeroed)
+__global__ void k_tile_dir(const uint32_t* __restrict__ skeys, int64_t n, int shift, uint32_t K1,
+                           uint32_t* __restrict__ ds, uint32_t* __restrict__ de) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t key = skeys[p];
+        const int64_t a = p >> shift;
+        const int64_t tb = a << shift;
+        const int64_t te = (n < tb + ((int64_t)1 << shift)) ? n : tb + ((int64_t)1 << shift);
+        if (p == tb || skeys[p - 1] != key) ds[(size_t)a * K1 + key] = (uint32_t)p;
+        if (p == te - 1 || skeys[p + 1] != key) de[(size_t)a * K1 + key] = (uint32_t)(p + 1);
+    }
+}
+
 // one lane per event: candidate test + forward scan for the consuming event
 template <bool FAST>
 __global__ void __launch_bounds__(WTPB) k_window(const shp_program* __restrict__ P, const int64_t* __restrict__ sts,
                                                  const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ perm,
                                                  int64_t n, uint32_t sentinel, const shd_cols* __restrict__ C,
                                                  int32_t* __restrict__ match_pos, uint32_t* __restrict__ cnt,
-                                                 int fast_ok, int32_t* __restrict__ flag) {
+                                                 int fast_ok, int32_t* __restrict__ flag, shd_tiles TL) {
     const int64_t within = P->within_ms;
+    const TileDir D = tile_dir(TL);
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t key = skeys ? skeys[p] : 0u;
         if (key == sentinel) continue;
         // the reduction to a forward scan needs non-decreasing timestamps per key
-        if (p > 0 && (!skeys || skeys[p - 1] == key) && sts[p] < sts[p - 1]) atomicExch(flag, 1);
+        const int64_t pp = key_pred(D, skeys, p, key);
+        if (pp >= 0 && sts[p] < sts[pp]) atomicExch(flag, 1);
         uint32_t rows[2];
         rows[0] = (uint32_t)p;
         rows[1] = SHD_NULL_ROW;
@@ -67,7 +82,10 @@ __global__ void __launch_bounds__(WTPB) k_window(const shp_program* __restrict__
             continue;
         }
         const int64_t t0 = sts[p];
-        for (int64_t q = p + 1; q < n; q++) {
+        uint32_t a = D.on() ? D.tile(p) : 0u;
+        int64_t qend = D.on() ? (int64_t)D.de[D.at(a, key)] : n;
+        for (int64_t q = p + 1;; q++) {
+            if (q >= qend && !(D.on() && D.next(a, key, q, qend))) break;
             if (skeys && skeys[q] != key) break;
             const int64_t d = sts[q] - t0;
             if ((d < 0 ? -d : d) > within) break;  // expired before event q is matched
@@ -100,16 +118,20 @@ __global__ void __launch_bounds__(WTPB) k_window_place(const shp_program* __rest
                                                        const uint32_t* __restrict__ off, uint64_t seq_base,
                                                        uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_ts,
                                                        int64_t* __restrict__ out_vals, uint8_t* __restrict__ out_nulls,
-                                                       int fast_ok) {
+                                                       int fast_ok, shd_tiles TL) {
     const int64_t within = P->within_ms;
     const int n_out = P->n_out;
+    const TileDir D = tile_dir(TL);
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
         const int32_t q = match_pos[p];
         if (q < 0) continue;
         const uint32_t key = skeys ? skeys[p] : 0u;
         const int64_t tq = sts[q];
         uint32_t rank = 0;
-        for (int64_t r = p - 1; r >= 0; r--) {
+        uint32_t a = D.on() ? D.tile(p) : 0u;
+        int64_t rbeg = D.on() ? (int64_t)D.ds[D.at(a, key)] : 0;
+        for (int64_t r = p - 1;; r--) {
+            if (r < rbeg && !(D.on() && D.prev(a, key, r, rbeg))) break;
             if (skeys && skeys[r] != key) break;
             if (tq - sts[r] > within) break;  // older partials expired before q
             if (match_pos[r] == q) rank++;
@@ -150,7 +172,7 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
                           const uint32_t* perm, const uint32_t* skeys, const int64_t* sts, const void* const* scols,
                           shd_window_ws* ws, shd_cols* d_sorted_desc, uint32_t* scan_tmp, uint64_t* out_seq,
                           int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, int64_t out_cap,
-                          int64_t* n_matches, void* stream, void* ev_mid_, const void* jit_) {
+                          int64_t* n_matches, void* stream, void* ev_mid_, const void* jit_, const shd_tiles* tiles) {
     const shj_window* jit = (const shj_window*)jit_;
     hipEvent_t ev_mid = (hipEvent_t)ev_mid_;
     hipStream_t st = (hipStream_t)stream;
@@ -166,21 +188,25 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
     uint32_t* cnt_s = perm ? ws->cnt_s : ws->cnt;
     hipMemsetAsync(cnt_s, 0, n * 4, st);
     const bool fast = hprog->filter_fast[0] && hprog->filter_fast[1] && hprog->out_fast;
+    shd_tiles TL;
+    memset(&TL, 0, sizeof(TL));
+    if (tiles && skeys) TL = *tiles;
     uint32_t tiles_per_xcd = 0, ntiles = 0;
     const unsigned jg = shj_tiles(n, &tiles_per_xcd, &ntiles);
     if (jit) {
         const shd_cols* dc = d_sorted_desc;
-        void* args[] = {(void*)&sts, (void*)&skeys, (void*)&n, (void*)&sentinel, (void*)&dc, (void*)&ws->match_pos,
-                        (void*)&cnt_s, (void*)&ws->flag, (void*)&tiles_per_xcd, (void*)&ntiles};
+        void* args[] = {(void*)&sts,   (void*)&skeys, (void*)&n,     (void*)&sentinel,      (void*)&dc,
+                        (void*)&ws->match_pos, (void*)&cnt_s, (void*)&ws->flag, (void*)&tiles_per_xcd,
+                        (void*)&ntiles, (void*)&TL};
         if (hipModuleLaunchKernel((hipFunction_t)jit->match, jg, 1, 1, shj_tile_size(), 1, 1, 0, st, args, nullptr) !=
             hipSuccess)
             return -3;
     } else if (fast)
         hipLaunchKernelGGL(k_window<true>, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n, sentinel,
-                           (const shd_cols*)d_sorted_desc, ws->match_pos, cnt_s, 1, ws->flag);
+                           (const shd_cols*)d_sorted_desc, ws->match_pos, cnt_s, 1, ws->flag, TL);
     else
         hipLaunchKernelGGL(k_window<false>, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n, sentinel,
-                           (const shd_cols*)d_sorted_desc, ws->match_pos, cnt_s, 1, ws->flag);
+                           (const shd_cols*)d_sorted_desc, ws->match_pos, cnt_s, 1, ws->flag, TL);
     if (ev_mid) hipEventRecord(ev_mid, st);
     if (perm) hipLaunchKernelGGL(k_cnt_scatter, dim3(g), dim3(WTPB), 0, st, (const uint32_t*)cnt_s, perm, n, ws->cnt);
     int rc = shd_exclusive_scan(ws->cnt, ws->off, n, scan_tmp, stream);
@@ -201,17 +227,27 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
         uint64_t seq_base = b->seq_base;
         void* args[] = {(void*)&sts,     (void*)&skeys,    (void*)&perm,    (void*)&n,         (void*)&dc,
                         (void*)&mp,      (void*)&off,      (void*)&seq_base, (void*)&out_seq,  (void*)&out_ts,
-                        (void*)&out_vals, (void*)&out_nulls, (void*)&tiles_per_xcd, (void*)&ntiles};
+                        (void*)&out_vals, (void*)&out_nulls, (void*)&tiles_per_xcd, (void*)&ntiles, (void*)&TL};
         if (hipModuleLaunchKernel((hipFunction_t)jit->place, jg, 1, 1, shj_tile_size(), 1, 1, 0, st, args, nullptr) !=
             hipSuccess)
             return -3;
     } else if (fast)
         hipLaunchKernelGGL(k_window_place<true>, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n,
                            (const shd_cols*)d_sorted_desc, (const int32_t*)ws->match_pos, (const uint32_t*)ws->off,
-                           b->seq_base, out_seq, out_ts, out_vals, out_nulls, 1);
+                           b->seq_base, out_seq, out_ts, out_vals, out_nulls, 1, TL);
     else
         hipLaunchKernelGGL(k_window_place<false>, dim3(g), dim3(WTPB), 0, st, dprog, sts, skeys, perm, n,
                            (const shd_cols*)d_sorted_desc, (const int32_t*)ws->match_pos, (const uint32_t*)ws->off,
-                           b->seq_base, out_seq, out_ts, out_vals, out_nulls, 1);
+                           b->seq_base, out_seq, out_ts, out_vals, out_nulls, 1, TL);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// directory of a tile-major segment (shd_tiles): ds / de hold ntile * K1 words
+extern "C" int shd_tile_dir(const uint32_t* skeys, int64_t n, int shift, uint32_t K1, uint32_t ntile, uint32_t* ds,
+                            uint32_t* de, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    hipMemsetAsync(ds, 0, (size_t)ntile * K1 * 4, st);
+    hipMemsetAsync(de, 0, (size_t)ntile * K1 * 4, st);
+    hipLaunchKernelGGL(k_tile_dir, dim3(grid_for(n)), dim3(WTPB), 0, st, skeys, n, shift, K1, ds, de);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -179,7 +179,9 @@ def _run_device_c2(n, keys, rate=100):
     return (ts, k, p, v), res
 
 
-def test_c2_device_run_vs_oracle():
+@pytest.mark.parametrize("tiles", [19, 13], ids=["default", "tiles8192"])
+def test_c2_device_run_vs_oracle(tiles, monkeypatch):
+    monkeypatch.setenv("SH_TILE_SHIFT", str(tiles))
     (ts, k, p, v), (m, oseq, ovals) = _run_device_c2(400_000, 2_000)
     ca = compiler.compile_app(synth.C2_QUERY)
     seq, ots, vals, _ = run_stock_oracle(ca, ts, k, p, v)
@@ -197,14 +199,17 @@ def test_c2_full_size_vs_vectorised_restatement(n, keys):
     assert np.array_equal(ovals, evals)
 
 
+@pytest.mark.parametrize("tiles", [0, 12], ids=["untiled", "tiles4096"])
 @pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
 @pytest.mark.parametrize("seed", range(24))
-def test_window_engine_vs_oracle(seed, jit, monkeypatch):
-    """hipRTC-specialised kernels (sh_jit.cpp) and the ahead-of-time ones."""
+def test_window_engine_vs_oracle(seed, jit, tiles, monkeypatch):
+    """hipRTC-specialised kernels (sh_jit.cpp) and the ahead-of-time ones, on one
+    global key segment and on arrival tiles of 4,096 events (scans cross tiles)."""
     import torch
     from siddhi_amd.device_run import DeviceRunner
     if not jit:
         monkeypatch.setenv("SH_DISABLE_JIT", "1")
+    monkeypatch.setenv("SH_TILE_SHIFT", str(tiles))
     rng = random.Random(7000 + seed)
     app, partitioned = window_case(rng)
     nk = rng.choice([1, 4, 50, 300])
