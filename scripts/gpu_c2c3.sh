@@ -1,0 +1,19 @@
+#!/bin/bash
+# window-engine parity (tiled / untiled, jit / aot), C3 parity, benches, kernel stats
+cd "${GRAFT_REPO_ROOT:-$(dirname $0)/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/prof
+S=scripts/gpu_step.sh
+$S 900 gpurun_out/c2_tests.log python -u -m pytest tests/test_gpu_parity.py -k "window or c2" -x -q --timeout 300 --timeout-method thread -p no:cacheprovider || exit $?
+tail -n 2 gpurun_out/c2_tests.log
+grep -q "failed" gpurun_out/c2_tests.log && exit 1
+$S 900 gpurun_out/c3_tests.log python -u -m pytest tests/test_gpu_nfa.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider || exit $?
+tail -n 2 gpurun_out/c3_tests.log
+grep -q "failed" gpurun_out/c3_tests.log && exit 1
+$S 600 gpurun_out/bench.log python -u bench.py --steps 5 --warmup 2 --cpu-sample 200000 || exit $?
+tail -n 1 gpurun_out/bench.log
+$S 600 gpurun_out/bench_c3.log python -u bench.py --config c3 --steps 2 --warmup 1 --cpu-sample 200000 || exit $?
+tail -n 1 gpurun_out/bench_c3.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+    python bench.py --steps 3 --warmup 1 --cpu-sample 0 --no-verify > gpurun_out/prof/bench_prof.log 2>&1 || exit $?
+python scripts/show_prof.py

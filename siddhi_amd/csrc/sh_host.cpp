@@ -1129,14 +1129,27 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
 }
 
 // one or more send() calls resident on the device, processed by k_nfa_run
-static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& cols, uint64_t* d_seq,
-                      int64_t* d_vals, int64_t cap, int64_t* n_rows, bool fresh = false, int64_t batch_events = 0) {
+static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid, int* alias);
+
+// `carry` (sh_run_device, single stream): ts and the stream-0 columns are moved
+// into key-segment order by the segment, so each lane streams its own events
+static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& cols_in, uint64_t* d_seq,
+                      int64_t* d_vals, int64_t cap, int64_t* n_rows, bool fresh = false, int64_t batch_events = 0,
+                      const sh_device_run* carry_run = nullptr) {
     hipStream_t st = h->stream;
     const int64_t n = B.n;
     if (ensure_ws(h, n)) return fail(h, SH_E_OOM, "workspace");
     if (nf_ensure_keys(h, nkeys)) return fail(h, SH_E_OOM, "key state");
     if (nf_ensure_recs(h, std::max<int64_t>(h->rec_cap, n + 4096))) return fail(h, SH_E_OOM, "emission buffer");
-    hipMemcpyAsync(h->d_ncols.p, &cols, sizeof(nf_cols), hipMemcpyHostToDevice, st);
+    nf_cols cols = cols_in;
+    shd_payload carry;
+    void* mid[8] = {nullptr};
+    int alias = -1;
+    const bool sorted_cols = carry_run && B.keys && h->stream_types[0].size() <= 7;
+    if (sorted_cols) {
+        if (carry_setup(h, carry_run, &carry, mid, &alias)) return fail(h, SH_E_OOM, "sorted columns");
+        for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = h->v_scol[a].p;
+    }
     shd_segment_ws ws;
     ws.keys_a = h->w_keys_a.as<uint32_t>();
     ws.keys_b = h->w_keys_b.as<uint32_t>();
@@ -1149,7 +1162,10 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     const uint32_t* perm = nullptr;
     const uint32_t* skeys = nullptr;
     hipEventRecord(h->ev[0], st);
-    if (shd_segment(&B, nkeys, &ws, st, &perm, &skeys)) return fail(h, SH_E_HIP, "segment launch failed");
+    if (shd_segment_payload(&B, nkeys, &ws, st, &perm, &skeys, sorted_cols ? &carry : nullptr, mid, 0, 1))
+        return fail(h, SH_E_HIP, "segment launch failed");
+    if (sorted_cols && alias >= 0) cols.col[0][alias] = skeys;
+    hipMemcpyAsync(h->d_ncols.p, &cols, sizeof(nf_cols), hipMemcpyHostToDevice, st);
     hipEventRecord(h->ev[1], st);
     const uint32_t* seg_list = ws.seg_off + 2 * n;
     const uint32_t* nseg = seg_list + n;
@@ -1162,6 +1178,8 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     E.perm = perm;
     E.seq_base = B.seq_base;
     E.batch_events = batch_events;
+    E.sts = sorted_cols ? h->v_sts.as<int64_t>() : nullptr;
+    E.sorted_rows = sorted_cols ? 1 : 0;
     for (int attempt = 0; attempt < 64; attempt++) {
         const size_t kw = (size_t)h->T->key_words;
         if (!fresh) {
@@ -1724,7 +1742,7 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
         int64_t rows = 0;
         h->times = sh_kernel_times{};
         rc = nf_process(h, B, nkeys, cols, run->d_out_seq, run->d_out_values, run->out_capacity, &rows, true,
-                        run->batch_events);
+                        run->batch_events, getenv("SH_NFA_GATHER") ? nullptr : run);
         run->out_count = rows;
         if (rc == SH_OK && run->d_out_query && rows > 0) {
             hipMemcpyAsync(run->d_out_query, h->w_oq.p, rows * 4, hipMemcpyDeviceToDevice, h->stream);

@@ -53,13 +53,20 @@ struct DevEvents {
     const uint32_t* perm;   // key-segment position -> arrival index (NULL: identity)
     uint64_t seq_base;
     int64_t batch_events;
+    const int64_t* sts;
+    int32_t sorted_rows;
     __device__ uint32_t at(int64_t k) const { return perm ? perm[k] : (uint32_t)k; }
 };
 // the Events interface of nf_process_segment / NfLane::receive
 struct DevEv {
     const DevEvents* E;
-    __device__ int64_t ts(int64_t k) const { return E->ts[E->at(k)]; }
-    __device__ uint32_t row(int64_t k) const { return E->row ? E->row[E->at(k)] : E->at(k); }
+    // key-segment-ordered copies (sh_run_device) make a lane's reads sequential
+    // instead of one gather through perm per event
+    __device__ int64_t ts(int64_t k) const { return E->sts ? E->sts[k] : E->ts[E->at(k)]; }
+    __device__ uint32_t row(int64_t k) const {
+        if (E->sorted_rows) return (uint32_t)k;
+        return E->row ? E->row[E->at(k)] : E->at(k);
+    }
     __device__ uint64_t seq(int64_t k) const { return E->seq_base + E->at(k); }
     __device__ int stream(int64_t k) const { return E->stream ? E->stream[E->at(k)] : 0; }
     __device__ uint32_t local(int64_t k) const { return E->at(k); }
@@ -295,6 +302,8 @@ extern "C" int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, 
     E.perm = ev->perm;
     E.seq_base = ev->seq_base;
     E.batch_events = ev->batch_events;
+    E.sts = ev->sts;
+    E.sorted_rows = ev->sorted_rows;
     if (max_segments < 1) max_segments = 1;
     hipLaunchKernelGGL(k_nfa_run, dim3(nf_blocks(max_segments, NF_TPB)), dim3(NF_TPB), 0, (hipStream_t)stream, dT, dC,
                        kstate, E, n, seg_list, nseg, skeys, nkeys, tick, clock, *em);

@@ -25,6 +25,9 @@ struct nfd_events {
     const uint32_t* perm;          // key-segment position -> arrival index, NULL: identity
     uint64_t seq_base;
     int64_t batch_events;          // bid == NULL: send() call = arrival index / batch_events (0: one call)
+    const int64_t* sts;            // timestamps in key-segment order (NULL: gather ts through perm)
+    int32_t sorted_rows;           // 1: column rows are key-segment positions (columns carried by the segment)
+    int32_t pad;
 };
 
 struct nfd_cand {
