@@ -249,10 +249,273 @@ std::string col_ptrs(const shp_program& P, const std::set<int>& attrs) {
     return s;
 }
 
+// ---- consumer-side ("extremum") form of the window reduction
+//
+// A partial opened at i is consumed at the first later event j of its key with
+// f2(i, j), provided ts_j - ts_i <= W (timestamps are non-decreasing per key, so
+// no event between them expired it). When f2 is a conjunction of terms on e2
+// only, terms on e1 only and at most one ordering comparison X(e2) op Y(e1),
+//   i is consumed at j  <=>  f1(i) && f2(i, j) && !(ext_{q in (i, j), q2(q)} X(q) op Y(i))
+// with ext = max for > / >= and min for < / <= over the events q strictly
+// between i and j that pass the e2-only terms q2 (NaN never compares true and is
+// left out). One lane per consumer j walks back over its key's events inside
+// the window, keeping ext as it goes; the walk yields the partials j consumes,
+// newest first, so counting and ordered placement need no per-partial state.
+struct ExtForm {
+    std::vector<shp_term> f1, ionly, qonly;
+    bool cross = false;
+    shp_term ct{};
+    bool q_left = true;  // the e2 side is the term's left operand
+    int op = 0;          // X(e2) op Y(e1) after mirroring
+    int dom = 0;
+};
+
+int mirror_op(int op) {
+    switch (op) {
+        case SH_OP_GT: return SH_OP_LT;
+        case SH_OP_GE: return SH_OP_LE;
+        case SH_OP_LT: return SH_OP_GT;
+        case SH_OP_LE: return SH_OP_GE;
+        default: return op;
+    }
+}
+
+bool ext_form(const shp_program& P, ExtForm& F) {
+    if (!P.window_ok) return false;
+    for (int k = 0; k < 2; k++)
+        if (!P.filter_fast[k] && P.filter_pc[k] >= 0) return false;
+    if (P.filter_fast[0])
+        for (int t = 0; t < P.filter_nterms[0]; t++) {
+            const shp_term& T = P.terms[0][t];
+            if (T.lslot || (T.rkind != 1 && T.rslot)) return false;
+            F.f1.push_back(T);
+        }
+    if (P.filter_fast[1])
+        for (int t = 0; t < P.filter_nterms[1]; t++) {
+            const shp_term& T = P.terms[1][t];
+            const bool rconst = T.rkind == 1;
+            if (rconst || T.lslot == T.rslot) {
+                (T.lslot ? F.qonly : F.ionly).push_back(T);
+                continue;
+            }
+            if (F.cross) return false;  // one ordering comparison across the slots at most
+            if (T.op != SH_OP_GT && T.op != SH_OP_GE && T.op != SH_OP_LT && T.op != SH_OP_LE) return false;
+            if (T.dom != DOM_I32 && T.dom != DOM_I64 && T.dom != DOM_F32 && T.dom != DOM_F64) return false;
+            F.cross = true;
+            F.ct = T;
+            F.q_left = T.lslot == 1;
+            F.op = F.q_left ? T.op : mirror_op(T.op);
+            F.dom = T.dom;
+        }
+    return true;
+}
+
+const char* dom_ctype(int dom) {
+    switch (dom) {
+        case DOM_I32: return "int32_t";
+        case DOM_I64: return "int64_t";
+        case DOM_F32: return "float";
+        default: return "double";
+    }
+}
+
+std::string dom_conv(int dom, const std::string& v) {
+    switch (dom) {
+        case DOM_I32: return "(int32_t)" + v + ".b";
+        case DOM_I64: return "to_i64(" + v + ")";
+        case DOM_F32: return "to_f32(" + v + ")";
+        default: return "to_f64(" + v + ")";
+    }
+}
+
+// statements defining VmVal `name` for one operand of T; slot s reads
+// attributes from variables pfx[s]<attr> (recorded in need[s])
+struct SideGen {
+    std::string pfx[2];
+    std::set<int>* need[2];
+    int tmp = 0;
+    std::string attr(int slot, int a) {
+        need[slot]->insert(a);
+        return pfx[slot] + std::to_string(a);
+    }
+    std::string vm(const std::string& name, int type, const std::string& bits) {
+        return "VmVal " + name + "; " + name + ".t = " + std::to_string(type) + "; " + name + ".null = 0; " + name +
+               ".b = " + bits + ";\n";
+    }
+    std::string left(const shp_term& T, const std::string& name) { return vm(name, T.ltype, attr(T.lslot, T.lattr)); }
+    std::string right(const shp_term& T, const std::string& name) {
+        if (T.rkind == 1) return vm(name, T.ctype, lit64(T.c));
+        std::string s = vm(name, T.rtype, attr(T.rslot, T.rattr));
+        if (T.rkind == 2) {
+            const std::string c = name + "c";
+            s += vm(c, T.ctype, lit64(T.c));
+            s += name + " = vm_arith(" + std::to_string(T.aop) + ", " + std::to_string(T.atype) + ", " + name + ", " +
+                 c + ");\n";
+        }
+        return s;
+    }
+    // conjunction of terms: clears `ok` when one fails
+    std::string terms(const std::vector<shp_term>& ts, const std::string& ok) {
+        std::string s;
+        for (const shp_term& T : ts) {
+            const std::string l = "tl" + std::to_string(tmp), r = "tr" + std::to_string(tmp);
+            tmp++;
+            s += "if (" + ok + ") {\n" + left(T, l) + right(T, r) + "if (" + r + ".null || !vm_cmp(" +
+                 std::to_string(T.op) + ", " + std::to_string(T.dom) + ", " + l + ", " + r + ")) " + ok +
+                 " = false;\n}\n";
+        }
+        return s;
+    }
+    // the e2 side X and the e1 side Y of the cross term, in the compare domain
+    std::string xval(const ExtForm& F, const std::string& out) {
+        const std::string v = "xv" + std::to_string(tmp++);
+        std::string s = F.q_left ? left(F.ct, v) : right(F.ct, v);
+        return s + "const " + dom_ctype(F.dom) + " " + out + " = " + dom_conv(F.dom, v) + ";\n";
+    }
+    std::string yval(const ExtForm& F, const std::string& out) {
+        const std::string v = "yv" + std::to_string(tmp++);
+        std::string s = F.q_left ? right(F.ct, v) : left(F.ct, v);
+        return s + "const " + dom_ctype(F.dom) + " " + out + " = " + dom_conv(F.dom, v) + ";\n";
+    }
+};
+
 std::string xcd_tile() {
     return "const uint32_t tile = (blockIdx.x & 7u) * tiles_per_xcd + (blockIdx.x >> 3);\n"
            "if (tile >= ntiles) return;\n"
            "const int64_t b0 = (int64_t)tile * SHJ_TILE;\n";
+}
+
+std::string load_set(const shp_program& P, const std::set<int>& attrs, const std::string& pfx, const std::string& row,
+                     const std::set<int>* staged, const std::string& lds_row) {
+    std::string s;
+    for (int a : attrs) {
+        const int t = P.attr_type[0][a];
+        const std::string x = pfx + std::to_string(a);
+        if (staged && staged->count(a))
+            s += x + " = " + raw_of(t, "s_c" + std::to_string(a) + "[" + lds_row + "]") + ";\n";
+        else
+            s += x + " = " + raw_of(t, "c" + std::to_string(a) + "[" + row + "]") + ";\n";
+    }
+    return s;
+}
+
+// shj_count / shj_emit: the consumer-side walk (ExtForm) over a tile of the key
+// segment staged in LDS with a backward halo. `outs` writes the select list of
+// the partial in x0_* and the consumer in x1_* to row `dst`.
+std::string gen_ext(const shp_program& P, const ExtForm& F, const std::string& outs, const std::set<int>& out0,
+                    const std::set<int>& out1) {
+    std::set<int> need_r, need_q;
+    SideGen gq, gi;  // gq: e1 = walked event (x0_), e2 = consumer (x1_); gi: both = walked event
+    gq.pfx[0] = "x0_";
+    gq.pfx[1] = "x1_";
+    gq.need[0] = &need_r;
+    gq.need[1] = &need_q;
+    gi.pfx[0] = gi.pfx[1] = "x0_";
+    gi.need[0] = gi.need[1] = &need_r;
+    gi.tmp = 1000;
+    const std::string DT = F.cross ? dom_ctype(F.dom) : "int32_t";
+    // consumer: e2-only terms and X(consumer)
+    std::string qhead = "bool qok = true;\n" + gq.terms(F.qonly, "qok");
+    if (F.cross) qhead += "if (qok) {\n" + gq.xval(F, "xq_") + "xq = xq_;\n}\n";
+    // walked event as a pending partial
+    std::string cand = "bool ok = true;\n" + gq.terms(F.f1, "ok") + gq.terms(F.ionly, "ok");
+    if (F.cross)
+        cand += "if (ok) {\n" + gq.yval(F, "y") + "ok = cmp_op<" + DT + ">(" + std::to_string(F.op) +
+                ", xq, y) && !(hasM && cmp_op<" + DT + ">(" + std::to_string(F.op) + ", M, y));\n}\n";
+    else
+        cand += "ok = ok && !hasM;\n";
+    // walked event as an event between the partial and the consumer
+    std::string mid = "bool mk = true;\n" + gi.terms(F.qonly, "mk");
+    // once ext has reached X(consumer) no older partial can be consumed (for >:
+    // y < X(j) and y >= ext are then disjoint; likewise >=, <, <=): stop there
+    std::string stop;
+    if (F.cross) {
+        const bool mx = F.op == SH_OP_GT || F.op == SH_OP_GE;
+        mid += "if (mk) {\n" + gi.xval(F, "xr") + "if (xr == xr && (!hasM || xr " + (mx ? ">" : "<") +
+               " M)) M = xr;\nif (xr == xr) hasM = true;\n}\n";
+        stop = std::string("    if (xq != xq || (hasM && M ") + (mx ? ">=" : "<=") + " xq)) break;\n";
+    } else {
+        mid += "if (mk) hasM = true;\n";
+        stop = "    if (hasM) break;\n";
+    }
+    std::set<int> staged = need_r;
+    staged.insert(need_q.begin(), need_q.end());
+    std::set<int> all = staged;
+    all.insert(out0.begin(), out0.end());
+    all.insert(out1.begin(), out1.end());
+    std::set<int> dec0 = need_r, dec1 = need_q;
+    dec0.insert(out0.begin(), out0.end());
+    dec1.insert(out1.begin(), out1.end());
+    std::set<int> extra0;  // select-list attributes of the partial not read by the walk
+    for (int a : out0)
+        if (!need_r.count(a)) extra0.insert(a);
+
+    auto head = [&](const std::string& name, const std::string& params) {
+        std::string s = "\nextern \"C\" __global__ void __launch_bounds__(SHJ_TILE)\n" + name + "(" + params +
+                        ") {\nconst TileDir D = tile_dir(TL);\n__shared__ int64_t s_ts[SHJ_SPAN];\n"
+                        "__shared__ uint32_t s_key[SHJ_SPAN];\n";
+        for (int a : staged)
+            s += "__shared__ " + std::string(col_ctype(P.attr_type[0][a])) + " s_c" + std::to_string(a) +
+                 "[SHJ_SPAN];\n";
+        s += xcd_tile() + col_ptrs(P, all);
+        s += "const int64_t lo = b0 > SHJ_HALO ? b0 - SHJ_HALO : 0;\n"
+             "const int64_t hi = (n < b0 + SHJ_TILE) ? n : b0 + SHJ_TILE;\n"
+             "for (int i = threadIdx.x; i < SHJ_SPAN; i += SHJ_TILE) {\n"
+             "    const int64_t gi = lo + i;\n"
+             "    if (gi < hi) {\n        s_ts[i] = sts[gi];\n        s_key[i] = skeys[gi];\n";
+        for (int a : staged) s += "        s_c" + std::to_string(a) + "[i] = c" + std::to_string(a) + "[gi];\n";
+        s += "    }\n}\n__syncthreads();\nconst int64_t p = b0 + threadIdx.x;\nif (p >= n) return;\n"
+             "const uint32_t key = s_key[p - lo];\nconst uint32_t j = perm ? perm[p] : (uint32_t)p;\n";
+        return s;
+    };
+    auto walk = [&](bool count, const std::string& on_consumed) {
+        std::string s = "const int64_t tq = s_ts[p - lo];\n" + decl_attrs(dec0, 0) + decl_attrs(dec1, 1) +
+                        load_set(P, dec1, "x1_", "p", &staged, "p - lo") + DT + " xq = 0;\n" + qhead +
+                        "bool hasM = false;\n" + DT + " M = 0;\n";
+        s += R"(uint32_t ta = D.on() ? D.tile(p) : 0u;
+int64_t rbeg = D.on() ? (int64_t)D.ds[D.at(ta, key)] : 0;
+bool first = true;
+for (int64_t r = p - 1;; r--) {
+    if (r < rbeg && !(D.on() && D.prev(ta, key, r, rbeg))) break;
+    const bool in_lds = r >= lo;
+    const uint32_t kr = in_lds ? s_key[r - lo] : skeys[r];
+    if (kr != key) break;
+    const int64_t tr = in_lds ? s_ts[r - lo] : sts[r];
+)";
+        if (count) s += "    if (first && tq < tr) atomicExch(flag, 1);\n";
+        s += "    first = false;\n    if (tq - tr > SHJ_W || !qok) break;\n";
+        s += "    if (in_lds) {\n" + load_set(P, need_r, "x0_", "r", &staged, "r - lo") + "    } else {\n" +
+             load_set(P, need_r, "x0_", "r", nullptr, "") + "    }\n";
+        s += "    {\n" + cand + "    if (ok) {\n" + on_consumed + "    }\n    }\n";
+        s += "    {\n" + mid + "    }\n" + stop + "}\n";
+        return s;
+    };
+
+    std::string src;
+    src += head("shj_count",
+                "const int64_t* __restrict__ sts, const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ "
+                "perm, int64_t n, uint32_t sentinel, const shd_cols* __restrict__ C, uint32_t* __restrict__ cnt, "
+                "int32_t* __restrict__ flag, uint32_t tiles_per_xcd, uint32_t ntiles, shd_tiles TL");
+    src += "if (key == sentinel) { cnt[j] = 0u; return; }\nuint32_t c = 0;\n";
+    src += walk(true, "        c++;\n");
+    src += "cnt[j] = c;\n}\n";
+
+    src += head("shj_emit",
+                "const int64_t* __restrict__ sts, const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ "
+                "perm, int64_t n, uint32_t sentinel, const shd_cols* __restrict__ C, const uint32_t* __restrict__ "
+                "cnt, const uint32_t* __restrict__ off, uint64_t seq_base, uint64_t* __restrict__ out_seq, "
+                "int64_t* __restrict__ out_ts, int64_t* __restrict__ out_vals, uint8_t* __restrict__ out_nulls, "
+                "uint32_t tiles_per_xcd, uint32_t ntiles, shd_tiles TL");
+    src += "if (key == sentinel) return;\nconst uint32_t c = cnt[j];\nif (c == 0u) return;\n"
+           "const int64_t base = (int64_t)off[j];\nuint32_t k = 0;\n";
+    std::string put = "        const int64_t dst = base + (int64_t)(c - 1u - k);\n        k++;\n"
+                      "        if (out_seq) out_seq[dst] = seq_base + j;\n        if (out_ts) out_ts[dst] = tq;\n";
+    put += load_set(P, extra0, "x0_", "r", nullptr, "");
+    put += outs;
+    put += "        if (k == c) break;\n";
+    src += walk(false, put);
+    src += "}\n";
+    return src;
 }
 
 // Prints the two specialised kernels of a window-shaped program; false when a
@@ -432,6 +695,10 @@ if (out_ts) out_ts[dst] = tq;
     src += decl_attrs(h.need[0], 0) + load_attrs(P, h.need[0], 0, "p", nullptr, "");
     src += decl_attrs(h.need[1], 1) + load_attrs(P, h.need[1], 1, "q", nullptr, "");
     src += outs + "}\n";
+
+    // ------------------------------------------------------------------ consumer-side walk
+    ExtForm F;
+    if (!getenv("SH_NO_EXT") && ext_form(P, F)) src += gen_ext(P, F, outs, h.need[0], h.need[1]);
     return true;
 }
 
@@ -440,7 +707,7 @@ struct Entry {
     std::string err;
     std::vector<char> code;   // gfx950 code object
     hipModule_t mod = nullptr;
-    hipFunction_t match = nullptr, place = nullptr;
+    hipFunction_t match = nullptr, place = nullptr, count = nullptr, emit = nullptr;
 };
 
 std::mutex g_mu;
@@ -518,9 +785,17 @@ int shj_window_load(const shp_program* hp, shj_window* out, std::string* err) {
             e->mod = nullptr;
             return -3;
         }
+        if (hipModuleGetFunction(&e->count, e->mod, "shj_count") != hipSuccess ||
+            hipModuleGetFunction(&e->emit, e->mod, "shj_emit") != hipSuccess) {
+            e->count = nullptr;
+            e->emit = nullptr;
+            (void)hipGetLastError();
+        }
     }
     out->match = e->match;
     out->place = e->place;
+    out->count = e->count;
+    out->emit = e->emit;
     return 0;
 }
 

@@ -12,6 +12,8 @@ struct shj_window {
     size_t code_size;
     void* match;          // hipFunction_t shj_match (after shj_window_load)
     void* place;          // hipFunction_t shj_place
+    void* count;          // hipFunction_t shj_count (consumer-side walk), NULL when the filter has no such form
+    void* emit;           // hipFunction_t shj_emit
 };
 
 // generated source for a window-shaped program (0), -1 if it has no straight-line form

@@ -22,6 +22,7 @@
 #include "sh_jit.h"
 #include "sh_vm.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 #define WTPB 256
@@ -184,15 +185,49 @@ extern "C" int shd_window(const shp_program* dprog, const shp_program* hprog, co
     for (int a = 0; a < hprog->stream_nattr[0]; a++) sc.col[0][a] = scols[a];
     hipMemcpyAsync(d_sorted_desc, &sc, sizeof(sc), hipMemcpyHostToDevice, st);
     hipMemsetAsync(ws->flag, 0, 4, st);
-    hipMemsetAsync(ws->match_pos, 0xFF, n * 4, st);
     uint32_t* cnt_s = perm ? ws->cnt_s : ws->cnt;
-    hipMemsetAsync(cnt_s, 0, n * 4, st);
     const bool fast = hprog->filter_fast[0] && hprog->filter_fast[1] && hprog->out_fast;
     shd_tiles TL;
     memset(&TL, 0, sizeof(TL));
     if (tiles && skeys) TL = *tiles;
     uint32_t tiles_per_xcd = 0, ntiles = 0;
     const unsigned jg = shj_tiles(n, &tiles_per_xcd, &ntiles);
+    if (jit && jit->count && jit->emit && skeys && !getenv("SH_NO_EXT")) {
+        // consumer-side walk (sh_jit.cpp ExtForm): per-consumer counts straight
+        // into arrival order, exclusive scan, then the ordered write
+        const shd_cols* dc = d_sorted_desc;
+        void* args[] = {(void*)&sts, (void*)&skeys, (void*)&perm, (void*)&n, (void*)&sentinel, (void*)&dc,
+                        (void*)&ws->cnt, (void*)&ws->flag, (void*)&tiles_per_xcd, (void*)&ntiles, (void*)&TL};
+        if (hipModuleLaunchKernel((hipFunction_t)jit->count, jg, 1, 1, shj_tile_size(), 1, 1, 0, st, args, nullptr) !=
+            hipSuccess)
+            return -3;
+        if (ev_mid) hipEventRecord(ev_mid, st);
+        int rc = shd_exclusive_scan(ws->cnt, ws->off, n, scan_tmp, stream);
+        if (rc) return rc;
+        uint32_t lo = 0, lc = 0;
+        int32_t hflag = 0;
+        hipMemcpyAsync(&lo, ws->off + (n - 1), 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(&lc, ws->cnt + (n - 1), 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(&hflag, ws->flag, 4, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return -3;
+        if (hflag) return 1;
+        *n_matches = (int64_t)lo + lc;
+        if (*n_matches > out_cap) return 2;
+        const uint32_t* cnt = ws->cnt;
+        const uint32_t* off = ws->off;
+        uint64_t seq_base = b->seq_base;
+        void* eargs[] = {(void*)&sts,     (void*)&skeys,    (void*)&perm,     (void*)&n,       (void*)&sentinel,
+                         (void*)&dc,      (void*)&cnt,      (void*)&off,      (void*)&seq_base, (void*)&out_seq,
+                         (void*)&out_ts,  (void*)&out_vals, (void*)&out_nulls, (void*)&tiles_per_xcd,
+                         (void*)&ntiles,  (void*)&TL};
+        if (*n_matches > 0 &&
+            hipModuleLaunchKernel((hipFunction_t)jit->emit, jg, 1, 1, shj_tile_size(), 1, 1, 0, st, eargs, nullptr) !=
+                hipSuccess)
+            return -3;
+        return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
+    hipMemsetAsync(ws->match_pos, 0xFF, n * 4, st);
+    hipMemsetAsync(cnt_s, 0, n * 4, st);
     if (jit) {
         const shd_cols* dc = d_sorted_desc;
         void* args[] = {(void*)&sts,   (void*)&skeys, (void*)&n,     (void*)&sentinel,      (void*)&dc,
