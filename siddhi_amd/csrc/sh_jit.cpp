@@ -42,8 +42,20 @@
 
 namespace {
 
-constexpr int kTile = 256;   // events per workgroup (one lane each)
-constexpr int kHalo = 256;   // staged events beyond the tile (forward for match, backward for place)
+// events per workgroup (one lane each) and staged events beyond the tile
+// (forward for match, backward for place / the consumer walk); SH_JIT_TILE /
+// SH_JIT_HALO override them (tile 64..1024, powers of two; halo 0..1024)
+int env_int(const char* name, int def, int lo, int hi) {
+    const char* e = getenv(name);
+    if (!e) return def;
+    const int v = atoi(e);
+    return v < lo || v > hi ? def : v;
+}
+const int kTile = [] {
+    const int t = env_int("SH_JIT_TILE", 256, 64, 1024);
+    return (t & (t - 1)) ? 256 : t;
+}();
+const int kHalo = env_int("SH_JIT_HALO", 256, 0, 1024);
 
 const char* col_ctype(int t) {
     switch (t) {
