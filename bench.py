@@ -38,8 +38,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2_000_000,
                     help="events of the same workload timed on the CPU oracle (0 = skip)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
-                    help="c2 (default, BASELINE.json configs[1]); c3 / c5 measure the other configs")
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2 (default, BASELINE.json configs[1]); c3 / c4 / c5 measure the other configs")
+    ap.add_argument("--seconds", type=int, default=100, help="c4: stream duration (playback seconds)")
     ap.add_argument("--rules", type=int, default=1000, help="c5: rule count")
     args = ap.parse_args()
     if args.config == "c5" and args.keys == 10_000:
@@ -48,6 +49,8 @@ def parse():
         args.keys = 1_000_000
         if args.rate == 100:
             args.rate = 1000
+    if args.config == "c4" and args.keys == 10_000:
+        args.keys = 10_000_000
     return args
 
 
@@ -128,6 +131,81 @@ def workload(args, rank):
 import numpy as np  # noqa: E402
 
 
+def main_c4(args, torch, dist, world, rank, dev):
+    """C4 (BASELINE.json configs[3]): `(e1=Login and e2=Txn) -> not Logout for 5 sec`
+    partitioned by user, playback time. Absent states need the playback scheduler,
+    so this config runs through the streaming C-ABI (sh_push_batch per send(Event[])
+    batch, sh_advance_time, sh_drain): host buffers cross PCIe inside the timed
+    region, unlike C2's HBM-resident sh_run_device. A step = one fresh engine
+    start + the whole stream + the drain of every match."""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    from c4_cases import run_c4
+    from siddhi_amd import compiler, synth
+    from siddhi_amd._native import HipEngine
+    log(f"generating c4 workload: {args.keys} users over {args.seconds} s")
+    blocks = synth.c4_stream(args.keys, seconds=args.seconds, seed=synth.SEED + 4 + 7919 * rank)
+    n = sum(len(b[1]) for b in blocks)
+    c = compiler.compile_app(synth.C4_QUERY)
+
+    def step():
+        eng = HipEngine(c)
+        t = time.perf_counter()
+        out = run_c4(eng, blocks, progress=log)
+        dt = time.perf_counter() - t
+        eng.close()
+        return len(out["seq"]), dt
+
+    for i in range(args.warmup):
+        log(f"warmup {i}")
+        step()
+    if world > 1:
+        dist.barrier()
+    tot, m = 0.0, 0
+    for i in range(args.steps):
+        m, dt = step()
+        tot += dt
+        log(f"step {i}: {dt * 1000:.0f} ms, {m} matches")
+    dt_t = torch.tensor([tot], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    tot = float(dt_t.item())
+    value = n * world * args.steps / tot
+    cpu = None
+    if rank == 0 and args.cpu_sample > 0:
+        from oracle_engine import OracleEngine
+        acc, sub = 0, []
+        for b in blocks:
+            if acc >= args.cpu_sample:
+                break
+            sub.append(b)
+            acc += len(b[1])
+        log(f"CPU baseline on {acc} events")
+        t1 = time.perf_counter()
+        run_c4(OracleEngine(c), sub)
+        cdt = time.perf_counter() - t1
+        cpu = {"value": acc / cdt, "unit": "events/s", "cores": 1, "kind": "port",
+               "sample": f"first {acc} events of the same C4 stream (its own send(Event[]) batches), C++ "
+                         f"restatement of siddhi-core's processors (oracle/), 1 thread"}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
+            "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": tot * 1000.0 / args.steps, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic",
+            "config": {"workload": "C4: (e1=Login and e2=Txn) -> not Logout for 5 sec, partition with (user of "
+                                   "Login, user of Txn, user of Logout), @app:playback",
+                       "events_per_gpu": n, "users_per_gpu": args.keys, "seconds": args.seconds,
+                       "send_calls": len(blocks), "matches_per_gpu": int(m),
+                       "path": "streaming C-ABI from host buffers (PCIe-inclusive)",
+                       "parallelism": f"key-sharded x{world}"},
+            "roofline": None,
+            "cpu_baseline": cpu,
+            "verified_vs_restatement": None,
+            "parity": "tests/test_gpu_c4.py (whole streams up to 400k users vs the oracle)"}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     import torch
@@ -140,6 +218,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     dev = torch.device(f"cuda:{local}")
+    if args.config == "c4":
+        return main_c4(args, torch, dist, world, rank, dev)
 
     from siddhi_amd.device_run import DeviceRunner
 

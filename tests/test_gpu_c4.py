@@ -1,0 +1,34 @@
+"""C4 (BASELINE.json configs[3]): `(e1=Login and e2=Txn) -> not Logout for 5 sec`,
+partitioned by user, playback time — the general engine (k_nfa_run, k_nfa_due,
+k_nfa_timer) through the streaming C-ABI (sh_push_batch / sh_advance_time /
+sh_drain) against the oracle, bit-exact (same rows, same order, same values).
+Absence timers couple keys (Scheduler's TreeMultimap fires one key per distinct
+due time, Scheduler.java:74-99), so parity is checked on whole streams, never on
+key subsets."""
+import pytest
+
+from c4_cases import run_c4, same_output
+from oracle_engine import OracleEngine
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("users,seconds", [(2_000, 5), (50_000, 20), (400_000, 60)])
+def test_c4_streaming_vs_oracle(users, seconds):
+    from siddhi_amd import compiler, synth
+    from siddhi_amd._native import HipEngine
+    c = compiler.compile_app(synth.C4_QUERY)
+    blocks = synth.c4_stream(users, seconds=seconds)
+    ref = run_c4(OracleEngine(c), blocks)
+    eng = HipEngine(c)
+    got = run_c4(eng, blocks)
+    eng.close()
+    assert len(ref["seq"]) > 0
+    assert same_output(got, ref), (len(got["seq"]), len(ref["seq"]))
