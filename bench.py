@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default, BASELINE.json configs[1]); c3 / c4 / c5 measure the other configs")
     ap.add_argument("--seconds", type=int, default=100, help="c4: stream duration (playback seconds)")
+    ap.add_argument("--c4-calls", type=int, default=0, help="c4: send only the first N calls (profiling; 0 = all)")
     ap.add_argument("--rules", type=int, default=1000, help="c5: rule count")
     args = ap.parse_args()
     if args.config == "c5" and args.keys == 10_000:
@@ -144,6 +145,8 @@ def main_c4(args, torch, dist, world, rank, dev):
     from siddhi_amd._native import HipEngine
     log(f"generating c4 workload: {args.keys} users over {args.seconds} s")
     blocks = synth.c4_stream(args.keys, seconds=args.seconds, seed=synth.SEED + 4 + 7919 * rank)
+    if args.c4_calls:
+        blocks = blocks[:args.c4_calls]
     n = sum(len(b[1]) for b in blocks)
     c = compiler.compile_app(synth.C4_QUERY)
 

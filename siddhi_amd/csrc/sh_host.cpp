@@ -64,6 +64,33 @@ struct DevBuf {
     }
 };
 
+// page-locked host staging: async copies from / to it run as plain DMA
+// (pageable copies go through the runtime's bounce buffers, ~20 us each)
+struct PinBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t need) {  // no content preservation
+        if (need <= bytes) return 0;
+        release();
+        size_t nb = std::max(need * 2, (size_t)1 << 16);
+        if (hipHostMalloc(&p, nb, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return SH_E_OOM;
+        }
+        bytes = nb;
+        return 0;
+    }
+    void release() {
+        if (p) hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as(size_t byte_off = 0) const {
+        return (T*)((uint8_t*)p + byte_off);
+    }
+};
+
 int type_width(int t) {
     switch (t) {
         case SH_T_LONG:
@@ -352,6 +379,10 @@ struct sh_handle {
     int mode = 0;                 // 0: chain / window engines, 1: general NFA engine
     nf_table* T = nullptr;        // host copy of the NFA table
     DevBuf d_T, d_T_old, d_ncols, n_kstate, n_kstate2, n_save, n_recs, n_ctr, n_err, n_cand, n_sel, n_bid;
+    // pinned staging of the streaming path: pin_in = one send() call's uploads,
+    // pin_rd = small read-backs + the nf_cols image, pin_out = placed rows
+    PinBuf pin_in, pin_rd, pin_out;
+    DevBuf n_tmin, n_slot_s, n_slot_k;  // device tie-break of due keys
     int caps[5] = {16, 32, 64, 32, 8};
     int32_t n_nkeys = 0;          // key blocks allocated
     int64_t rec_cap = 0;
@@ -729,6 +760,12 @@ void sh_destroy(sh_handle* h) {
     if (!h) return;
     if (h->has_device) {
         hipStreamSynchronize(h->stream);
+        h->pin_in.release();
+        h->pin_rd.release();
+        h->pin_out.release();
+        h->n_tmin.release();
+        h->n_slot_s.release();
+        h->n_slot_k.release();
         h->v_sts.release();
         h->v_mpos.release();
         h->v_flag.release();
@@ -775,10 +812,18 @@ int sh_push_batch(sh_handle* h, const sh_batch* b) {
     auto& st = h->stores[b->stream];
     const auto& types = h->stream_types[b->stream];
     const int64_t r0 = st.rows;
+    size_t pin_need = 0;
+    for (size_t a = 0; a < types.size(); a++) pin_need += (size_t)b->n * type_width(types[a]);
+    if (h->pin_in.ensure(pin_need)) return fail(h, SH_E_OOM, "pinned staging");
+    size_t pin_off = 0;
     for (size_t a = 0; a < types.size(); a++) {
         const int w = type_width(types[a]);
         if (st.cols[a].ensure((size_t)(r0 + b->n) * w)) return fail(h, SH_E_OOM, "column store");
-        hipMemcpyAsync((uint8_t*)st.cols[a].p + r0 * w, b->cols[a], b->n * w, hipMemcpyHostToDevice, h->stream);
+        // through pinned staging (the sync below completes the copy before reuse)
+        memcpy(h->pin_in.as<void>(pin_off), b->cols[a], (size_t)b->n * w);
+        hipMemcpyAsync((uint8_t*)st.cols[a].p + r0 * w, h->pin_in.as<void>(pin_off), b->n * w, hipMemcpyHostToDevice,
+                       h->stream);
+        pin_off += (size_t)b->n * w;
         const uint8_t* nm = b->nulls ? b->nulls[a] : nullptr;
         if (nm || st.has_nul[a]) {
             if (!st.has_nul[a]) {
@@ -1079,18 +1124,38 @@ static nfd_emit nf_emit(sh_handle* h) {
     return em;
 }
 
+// pinned read-back slots (pin_rd): 0 nrec u64, 8 last_off u32, 12 last_cnt u32,
+// 16 err u32, 24 due-candidate count u64; the nf_cols image from byte 64
+enum { PR_NREC = 0, PR_LOFF = 8, PR_LCNT = 12, PR_ERR = 16, PR_NC = 24, PR_TMIN = 32, PR_COLS = 64 };
+// due-key backlogs at least this large are tie-broken on the device when their
+// due times span at most kTieBreakSlots milliseconds (SH_TIEBREAK_MIN overrides)
+static const int64_t kDeviceTieBreak = [] {
+    const char* e = getenv("SH_TIEBREAK_MIN");
+    return e ? (int64_t)atoll(e) : (int64_t)4096;
+}();
+static const int64_t kTieBreakSlots = (int64_t)1 << 22;
+static int pin_rd_ready(sh_handle* h) { return h->pin_rd.ensure(PR_COLS + sizeof(nf_cols)); }
+
+// upload the nf_cols image through pinned memory (the caller synchronises the
+// stream before the slot is written again)
+static void nf_put_cols(sh_handle* h, const nf_cols& cols) {
+    memcpy(h->pin_rd.as<nf_cols>(PR_COLS), &cols, sizeof(nf_cols));
+    hipMemcpyAsync(h->d_ncols.p, h->pin_rd.as<nf_cols>(PR_COLS), sizeof(nf_cols), hipMemcpyHostToDevice, h->stream);
+}
+
 // scan the per-index counts, place the records, append them to the host queue
 // (or to the caller's device buffers); returns the number of rows
 static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_seq, int64_t* d_vals, int64_t cap) {
     hipStream_t st = h->stream;
-    unsigned long long nrec = 0;
-    hipMemcpyAsync(&nrec, h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
+    if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
+    hipMemcpyAsync(h->pin_rd.as<void>(PR_NREC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
     if (shd_exclusive_scan(h->w_cnt.as<uint32_t>(), h->w_off.as<uint32_t>(), n_idx, h->w_scan.as<uint32_t>(), st))
         return fail(h, SH_E_HIP, "scan");
-    uint32_t last_off = 0, last_cnt = 0;
-    hipMemcpyAsync(&last_off, h->w_off.as<uint32_t>() + (n_idx - 1), 4, hipMemcpyDeviceToHost, st);
-    hipMemcpyAsync(&last_cnt, h->w_cnt.as<uint32_t>() + (n_idx - 1), 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(h->pin_rd.as<void>(PR_LOFF), h->w_off.as<uint32_t>() + (n_idx - 1), 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(h->pin_rd.as<void>(PR_LCNT), h->w_cnt.as<uint32_t>() + (n_idx - 1), 4, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error before placement");
+    const unsigned long long nrec = *h->pin_rd.as<unsigned long long>(PR_NREC);
+    const uint32_t last_off = *h->pin_rd.as<uint32_t>(PR_LOFF), last_cnt = *h->pin_rd.as<uint32_t>(PR_LCNT);
     const int64_t total = (int64_t)last_off + last_cnt;
     *rows_out = total;
     if (total == 0) return SH_OK;
@@ -1116,16 +1181,27 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
     h->o_ts.resize(base + total);
     h->o_vals.resize((base + total) * h->n_out);
     h->o_nulls.resize((base + total) * h->n_out);
-    hipMemcpyAsync(h->o_query.data() + base, h->w_oq.p, total * 4, hipMemcpyDeviceToHost, st);
-    hipMemcpyAsync(h->o_seq.data() + base, h->w_oseq.p, total * 8, hipMemcpyDeviceToHost, st);
-    hipMemcpyAsync(h->o_ts.data() + base, h->w_ots.p, total * 8, hipMemcpyDeviceToHost, st);
-    if (h->n_out) {
-        if (no == h->n_out) {
-            hipMemcpyAsync(h->o_vals.data() + base * h->n_out, h->w_ovals.p, total * no * 8, hipMemcpyDeviceToHost, st);
-            hipMemcpyAsync(h->o_nulls.data() + base * h->n_out, h->w_onulls.p, total * no, hipMemcpyDeviceToHost, st);
-        }
+    // rows come back through pinned staging, then into the host queue
+    const size_t b_q = 0, b_seq = b_q + ((size_t)total * 4 + 7) / 8 * 8, b_ts = b_seq + (size_t)total * 8,
+                 b_v = b_ts + (size_t)total * 8, b_n = b_v + (size_t)total * no * 8, b_end = b_n + (size_t)total * no;
+    if (h->pin_out.ensure(b_end)) return fail(h, SH_E_OOM, "pinned staging");
+    hipMemcpyAsync(h->pin_out.as<void>(b_q), h->w_oq.p, total * 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(h->pin_out.as<void>(b_seq), h->w_oseq.p, total * 8, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(h->pin_out.as<void>(b_ts), h->w_ots.p, total * 8, hipMemcpyDeviceToHost, st);
+    const bool vals = h->n_out && no == h->n_out;
+    if (vals) {
+        hipMemcpyAsync(h->pin_out.as<void>(b_v), h->w_ovals.p, total * no * 8, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(h->pin_out.as<void>(b_n), h->w_onulls.p, total * no, hipMemcpyDeviceToHost, st);
     }
-    return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "output copy");
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "output copy");
+    memcpy(h->o_query.data() + base, h->pin_out.as<void>(b_q), total * 4);
+    memcpy(h->o_seq.data() + base, h->pin_out.as<void>(b_seq), total * 8);
+    memcpy(h->o_ts.data() + base, h->pin_out.as<void>(b_ts), total * 8);
+    if (vals) {
+        memcpy(h->o_vals.data() + base * h->n_out, h->pin_out.as<void>(b_v), total * no * 8);
+        memcpy(h->o_nulls.data() + base * h->n_out, h->pin_out.as<void>(b_n), total * no);
+    }
+    return SH_OK;
 }
 
 // one or more send() calls resident on the device, processed by k_nfa_run
@@ -1165,7 +1241,8 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     if (shd_segment_payload(&B, nkeys, &ws, st, &perm, &skeys, sorted_cols ? &carry : nullptr, mid, 0, 1))
         return fail(h, SH_E_HIP, "segment launch failed");
     if (sorted_cols && alias >= 0) cols.col[0][alias] = skeys;
-    hipMemcpyAsync(h->d_ncols.p, &cols, sizeof(nf_cols), hipMemcpyHostToDevice, st);
+    if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
+    nf_put_cols(h, cols);
     hipEventRecord(h->ev[1], st);
     const uint32_t* seg_list = ws.seg_off + 2 * n;
     const uint32_t* nseg = seg_list + n;
@@ -1195,9 +1272,9 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
                     skeys, nkeys, max_seg, h->tick, h->clock, &em, st))
             return fail(h, SH_E_HIP, "k_nfa_run launch failed");
         hipEventRecord(h->ev[2], st);
-        unsigned err = 0;
-        hipMemcpyAsync(&err, h->n_err.p, 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(h->pin_rd.as<void>(PR_ERR), h->n_err.p, 4, hipMemcpyDeviceToHost, st);
         if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_run");
+        const unsigned err = *h->pin_rd.as<unsigned>(PR_ERR);
         if (!err) {
             h->tick++;
             int rc = nf_place(h, n, n_rows, d_seq, d_vals, cap);
@@ -1240,8 +1317,8 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
 static int nf_timers(sh_handle* h, int64_t now) {
     if (!h->T->has_absent || h->n_nkeys == 0) return SH_OK;
     hipStream_t st = h->stream;
-    const nf_cols cols = nf_store_cols(h);
-    hipMemcpyAsync(h->d_ncols.p, &cols, sizeof(nf_cols), hipMemcpyHostToDevice, st);
+    if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
+    nf_put_cols(h, nf_store_cols(h));
     for (int q = 0; q < h->T->n_queries; q++) {
         for (int p = 0; p < h->T->q[q].n_proc; p++) {
             if (h->T->q[q].proc[p].kind != NF_K_ABSENT) continue;
@@ -1251,25 +1328,52 @@ static int nf_timers(sh_handle* h, int64_t now) {
             hipMemsetAsync(h->n_ctr.p, 0, 8, st);
             nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, now, h->n_cand.as<nfd_cand>(),
                     h->n_ctr.as<unsigned long long>(), nkeys, st);
-            unsigned long long nc = 0;
-            hipMemcpyAsync(&nc, h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
+            hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
             if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
+            const unsigned long long nc = *h->pin_rd.as<unsigned long long>(PR_NC);
             if (nc == 0) continue;
-            std::vector<nfd_cand> cs(nc);
-            hipMemcpy(cs.data(), h->n_cand.p, nc * sizeof(nfd_cand), hipMemcpyDeviceToHost);
             // TreeMultimap<Long, SchedulerState> with a zero comparator: one key per
             // distinct due time, the first in keyOrder (earliest registration)
-            std::sort(cs.begin(), cs.end(), [](const nfd_cand& a, const nfd_cand& b) {
-                if (a.t != b.t) return a.t < b.t;
-                return a.stamp < b.stamp;
-            });
             std::vector<int32_t> sel;
-            for (size_t i = 0; i < cs.size(); i++)
-                if (i == 0 || cs[i].t != cs[i - 1].t) sel.push_back(cs[i].key);
+            bool picked = false;
+            if ((int64_t)nc >= kDeviceTieBreak) {
+                // large backlog of due keys: pick on the device (slot per due time)
+                if (h->n_tmin.ensure_fresh(8)) return fail(h, SH_E_OOM, "timer tie-break");
+                nfd_cand_tmin(h->n_cand.as<nfd_cand>(), (int64_t)nc, h->n_tmin.as<unsigned long long>(), st);
+                hipMemcpyAsync(h->pin_rd.as<void>(PR_TMIN), h->n_tmin.p, 8, hipMemcpyDeviceToHost, st);
+                if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_cand_tmin");
+                const int64_t tmin = (int64_t)*h->pin_rd.as<unsigned long long>(PR_TMIN);
+                const int64_t range = now - tmin + 1;
+                if (tmin >= 0 && range > 0 && range <= kTieBreakSlots) {
+                    if (h->n_slot_s.ensure_fresh((size_t)range * 8) || h->n_slot_k.ensure_fresh((size_t)range * 4) ||
+                        h->pin_out.ensure((size_t)range * 4))
+                        return fail(h, SH_E_OOM, "timer tie-break");
+                    nfd_cand_select(h->n_cand.as<nfd_cand>(), (int64_t)nc, tmin, range,
+                                    h->n_slot_s.as<unsigned long long>(), h->n_slot_k.as<int32_t>(), st);
+                    hipMemcpyAsync(h->pin_out.p, h->n_slot_k.p, (size_t)range * 4, hipMemcpyDeviceToHost, st);
+                    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_cand_select");
+                    const int32_t* sk = h->pin_out.as<int32_t>();
+                    for (int64_t r = 0; r < range; r++)
+                        if (sk[r] >= 0) sel.push_back(sk[r]);
+                    picked = true;
+                }
+            }
+            if (!picked) {
+                std::vector<nfd_cand> cs(nc);
+                hipMemcpy(cs.data(), h->n_cand.p, nc * sizeof(nfd_cand), hipMemcpyDeviceToHost);
+                std::sort(cs.begin(), cs.end(), [](const nfd_cand& a, const nfd_cand& b) {
+                    if (a.t != b.t) return a.t < b.t;
+                    return a.stamp < b.stamp;
+                });
+                for (size_t i = 0; i < cs.size(); i++)
+                    if (i == 0 || cs[i].t != cs[i - 1].t) sel.push_back(cs[i].key);
+            }
             const int32_t ns = (int32_t)sel.size();
             if (h->n_sel.ensure_fresh((size_t)ns * 4) || h->n_save.ensure_fresh((size_t)ns * h->T->key_words * 8))
                 return fail(h, SH_E_OOM, "timer keys");
-            hipMemcpyAsync(h->n_sel.p, sel.data(), (size_t)ns * 4, hipMemcpyHostToDevice, st);
+            if (h->pin_out.ensure((size_t)ns * 4)) return fail(h, SH_E_OOM, "pinned staging");
+            memcpy(h->pin_out.p, sel.data(), (size_t)ns * 4);  // read by the copy before the loop's sync
+            hipMemcpyAsync(h->n_sel.p, h->pin_out.p, (size_t)ns * 4, hipMemcpyHostToDevice, st);
             if (ensure_ws(h, ns)) return fail(h, SH_E_OOM, "workspace");
             if (nf_ensure_recs(h, std::max<int64_t>(h->rec_cap, ns + 4096))) return fail(h, SH_E_OOM, "emission");
             for (int attempt = 0;; attempt++) {
@@ -1284,9 +1388,9 @@ static int nf_timers(sh_handle* h, int64_t now) {
                 nfd_emit em = nf_emit(h);
                 nfd_timer(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), q, p,
                           h->n_sel.as<int32_t>(), ns, now, h->tick, h->clock, &em, st);
-                unsigned err = 0;
-                hipMemcpyAsync(&err, h->n_err.p, 4, hipMemcpyDeviceToHost, st);
+                hipMemcpyAsync(h->pin_rd.as<void>(PR_ERR), h->n_err.p, 4, hipMemcpyDeviceToHost, st);
                 if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_timer");
+                const unsigned err = *h->pin_rd.as<unsigned>(PR_ERR);
                 if (!err) break;
                 if (err & NF_E_UNSUP) return fail(h, SH_E_UNSUPPORTED, "startStateReset recursion");
                 nfd_save_keys(h->n_kstate.as<uint64_t>(), (int64_t)kw, h->n_sel.as<int32_t>(), ns,
@@ -1342,12 +1446,18 @@ static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0) {
     }
     const int64_t n = b->n;
     hipStream_t st = h->stream;
-    std::vector<uint8_t> sv(n, (uint8_t)b->stream);
-    std::vector<uint32_t> rows(n);
-    std::vector<int32_t> keys(n, 0);
+    // staged in pinned memory (pin_in; the column copies of this call are complete)
+    const size_t o_ts = 0, o_rows = (size_t)n * 8, o_keys = o_rows + (size_t)n * 4, o_sv = o_keys + (size_t)n * 4;
+    if (h->pin_in.ensure(o_sv + (size_t)n)) return fail(h, SH_E_OOM, "pinned staging");
+    uint8_t* sv = h->pin_in.as<uint8_t>(o_sv);
+    uint32_t* rows = h->pin_in.as<uint32_t>(o_rows);
+    int32_t* keys = h->pin_in.as<int32_t>(o_keys);
+    memset(sv, (uint8_t)b->stream, (size_t)n);
+    memcpy(h->pin_in.as<int64_t>(o_ts), b->ts, (size_t)n * 8);
     int32_t nk = 1;
     for (int64_t i = 0; i < n; i++) {
         rows[i] = (uint32_t)(r0 + i);
+        keys[i] = 0;
         if (h->partitioned) {
             keys[i] = b->keys ? b->keys[i] : -1;
             nk = std::max(nk, keys[i] + 1);
@@ -1356,10 +1466,10 @@ static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0) {
     if (h->w_ts.ensure_fresh(n * 8) || h->w_stream.ensure_fresh(n) || h->w_row.ensure_fresh(n * 4) ||
         h->w_key.ensure_fresh(n * 4) || h->n_bid.ensure_fresh(n * 4))
         return fail(h, SH_E_OOM, "staging");
-    hipMemcpyAsync(h->w_ts.p, b->ts, n * 8, hipMemcpyHostToDevice, st);
-    hipMemcpyAsync(h->w_stream.p, sv.data(), n, hipMemcpyHostToDevice, st);
-    hipMemcpyAsync(h->w_row.p, rows.data(), n * 4, hipMemcpyHostToDevice, st);
-    hipMemcpyAsync(h->w_key.p, keys.data(), n * 4, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_ts.p, h->pin_in.as<int64_t>(o_ts), n * 8, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_stream.p, sv, n, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_row.p, rows, n * 4, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_key.p, keys, n * 4, hipMemcpyHostToDevice, st);
     hipMemsetAsync(h->n_bid.p, 0, n * 4, st);
     shd_batch B;
     B.ts = h->w_ts.as<int64_t>();

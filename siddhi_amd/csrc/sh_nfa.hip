@@ -170,6 +170,30 @@ __global__ void __launch_bounds__(256) k_nfa_due(const nf_table* __restrict__ T,
     cand[at].pad = 0;
 }
 
+// Scheduler.onTimeChange tie-break on the device for a large backlog of due
+// keys: the earliest registration stamp per distinct due time (TreeMultimap with
+// a zero value comparator keeps one scheduler per time), slot = t - tmin
+__global__ void __launch_bounds__(256) k_cand_tmin(const nfd_cand* __restrict__ cand, int64_t nc,
+                                                   unsigned long long* __restrict__ tmin) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nc) atomicMin(tmin, (unsigned long long)cand[i].t);
+}
+
+__global__ void __launch_bounds__(256) k_cand_slot(const nfd_cand* __restrict__ cand, int64_t nc, int64_t tmin,
+                                                   unsigned long long* __restrict__ slot_stamp) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nc) atomicMin(&slot_stamp[cand[i].t - tmin], (unsigned long long)cand[i].stamp);
+}
+
+__global__ void __launch_bounds__(256) k_cand_pick(const nfd_cand* __restrict__ cand, int64_t nc, int64_t tmin,
+                                                   const unsigned long long* __restrict__ slot_stamp,
+                                                   int32_t* __restrict__ slot_key) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nc) return;
+    const int64_t s = cand[i].t - tmin;
+    if (slot_stamp[s] == (unsigned long long)cand[i].stamp) slot_key[s] = cand[i].key;
+}
+
 // Scheduler.onTimeChange, second half: sendTimerEvents for each selected key
 // (rank = position in due-time order = emission order)
 __global__ void __launch_bounds__(NF_TPB) k_nfa_timer(const nf_table* __restrict__ T, const nf_cols* __restrict__ C,
@@ -321,6 +345,25 @@ extern "C" int nfd_due(const nf_table* dT, int q, int p, const uint64_t* kstate,
     if (nkeys <= 0) return 0;
     hipLaunchKernelGGL(k_nfa_due, dim3(nf_blocks(nkeys, 256)), dim3(256), 0, (hipStream_t)stream, dT, q, p, kstate,
                        nkeys, now, cand, ctr, cap);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_cand_tmin(const nfd_cand* cand, int64_t nc, unsigned long long* tmin, void* stream) {
+    if (nc <= 0) return 0;
+    hipMemsetAsync(tmin, 0xFF, 8, (hipStream_t)stream);
+    hipLaunchKernelGGL(k_cand_tmin, dim3(nf_blocks(nc, 256)), dim3(256), 0, (hipStream_t)stream, cand, nc, tmin);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_cand_select(const nfd_cand* cand, int64_t nc, int64_t tmin, int64_t range,
+                               unsigned long long* slot_stamp, int32_t* slot_key, void* stream) {
+    if (nc <= 0 || range <= 0) return 0;
+    hipMemsetAsync(slot_stamp, 0xFF, (size_t)range * 8, (hipStream_t)stream);
+    hipMemsetAsync(slot_key, 0xFF, (size_t)range * 4, (hipStream_t)stream);
+    hipLaunchKernelGGL(k_cand_slot, dim3(nf_blocks(nc, 256)), dim3(256), 0, (hipStream_t)stream, cand, nc, tmin,
+                       slot_stamp);
+    hipLaunchKernelGGL(k_cand_pick, dim3(nf_blocks(nc, 256)), dim3(256), 0, (hipStream_t)stream, cand, nc, tmin,
+                       slot_stamp, slot_key);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -47,6 +47,11 @@ int nfd_start(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, uint64_t 
               const nfd_emit* em, void* stream);
 int nfd_due(const nf_table* dT, int q, int p, const uint64_t* kstate, int32_t nkeys, int64_t now, nfd_cand* cand,
             unsigned long long* ctr, int64_t cap, void* stream);
+// device tie-break of a due-key backlog: tmin of the candidates, then per due
+// time t (slot t - tmin of `range`) the key with the earliest stamp (-1: none)
+int nfd_cand_tmin(const nfd_cand* cand, int64_t nc, unsigned long long* tmin, void* stream);
+int nfd_cand_select(const nfd_cand* cand, int64_t nc, int64_t tmin, int64_t range, unsigned long long* slot_stamp,
+                    int32_t* slot_key, void* stream);
 int nfd_timer(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, int q, int p, const int32_t* keys, int32_t nsel,
               int64_t now, uint64_t tick, int64_t clock, const nfd_emit* em, void* stream);
 int nfd_place(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets, int n_out, int32_t* out_query,
