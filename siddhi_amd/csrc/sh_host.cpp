@@ -383,6 +383,7 @@ struct sh_handle {
     // pin_rd = small read-backs + the nf_cols image, pin_out = placed rows
     PinBuf pin_in, pin_rd, pin_out;
     DevBuf n_tmin, n_slot_s, n_slot_k;  // device tie-break of due keys
+    DevBuf n_armed;                     // per key: may hold a scheduler entry (nf_cols.sched_armed)
     int caps[5] = {16, 32, 64, 32, 8};
     int32_t n_nkeys = 0;          // key blocks allocated
     int64_t rec_cap = 0;
@@ -764,6 +765,7 @@ void sh_destroy(sh_handle* h) {
         h->pin_rd.release();
         h->pin_out.release();
         h->n_tmin.release();
+        h->n_armed.release();
         h->n_slot_s.release();
         h->n_slot_k.release();
         h->v_sts.release();
@@ -1040,6 +1042,12 @@ static int run_batch(sh_handle* h, const shd_batch& B, int32_t nkeys, const shd_
 // sh_nfa.h lanes over the radix segment; emissions are placed by an exclusive
 // scan of per-run counts. A lane error (an arena / list / queue / emission
 // buffer full) restores the touched keys' blocks, grows the capacity and replays.
+// the due scan's key filter (SH_NO_ARMED: scan every key)
+static uint8_t* armed_flags(sh_handle* h) {
+    static const bool off = getenv("SH_NO_ARMED") != nullptr;
+    return off ? nullptr : h->n_armed.as<uint8_t>();
+}
+
 static nf_cols nf_store_cols(sh_handle* h) {
     nf_cols c;
     memset(&c, 0, sizeof(c));
@@ -1048,6 +1056,7 @@ static nf_cols nf_store_cols(sh_handle* h) {
             c.col[s][a] = h->stores[s].cols[a].p;
             c.nul[s][a] = h->stores[s].has_nul[a] ? (const uint8_t*)h->stores[s].nuls[a].p : nullptr;
         }
+    c.sched_armed = armed_flags(h);
     return c;
 }
 
@@ -1059,6 +1068,8 @@ static int nf_ensure_keys(sh_handle* h, int32_t nkeys) {
     hipStreamSynchronize(h->stream);
     if (h->n_kstate.ensure(need)) return SH_E_OOM;
     hipMemsetAsync((uint8_t*)h->n_kstate.p + old, 0, need - old, h->stream);
+    if (h->n_armed.ensure((size_t)nk)) return SH_E_OOM;
+    hipMemsetAsync((uint8_t*)h->n_armed.p + h->n_nkeys, 0, (size_t)(nk - h->n_nkeys), h->stream);
     h->n_nkeys = nk;
     return 0;
 }
@@ -1218,6 +1229,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     if (nf_ensure_keys(h, nkeys)) return fail(h, SH_E_OOM, "key state");
     if (nf_ensure_recs(h, std::max<int64_t>(h->rec_cap, n + 4096))) return fail(h, SH_E_OOM, "emission buffer");
     nf_cols cols = cols_in;
+    cols.sched_armed = armed_flags(h);  // after any key growth above
     shd_payload carry;
     void* mid[8] = {nullptr};
     int alias = -1;
@@ -1319,6 +1331,9 @@ static int nf_timers(sh_handle* h, int64_t now) {
     hipStream_t st = h->stream;
     if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
     nf_put_cols(h, nf_store_cols(h));
+    int n_absent = 0;  // a key's armed flag may be cleared only when it has one scheduler
+    for (int q = 0; q < h->T->n_queries; q++)
+        for (int p = 0; p < h->T->q[q].n_proc; p++) n_absent += h->T->q[q].proc[p].kind == NF_K_ABSENT;
     for (int q = 0; q < h->T->n_queries; q++) {
         for (int p = 0; p < h->T->q[q].n_proc; p++) {
             if (h->T->q[q].proc[p].kind != NF_K_ABSENT) continue;
@@ -1327,7 +1342,7 @@ static int nf_timers(sh_handle* h, int64_t now) {
             if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");
             hipMemsetAsync(h->n_ctr.p, 0, 8, st);
             nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, now, h->n_cand.as<nfd_cand>(),
-                    h->n_ctr.as<unsigned long long>(), nkeys, st);
+                    h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0, st);
             hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
             if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
             const unsigned long long nc = *h->pin_rd.as<unsigned long long>(PR_NC);

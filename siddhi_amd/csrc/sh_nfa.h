@@ -150,6 +150,10 @@ struct nf_table {
 struct nf_cols {
     const void* col[NF_MAX_STREAMS][NF_MAX_ATTRS];
     const uint8_t* nul[NF_MAX_STREAMS][NF_MAX_ATTRS];
+    // per key: set when the key registers a scheduler entry, cleared by the due
+    // scan when its queues are empty, so the scan skips keys that never armed one
+    // (NULL: every key is scanned)
+    uint8_t* sched_armed;
 };
 
 // ------------------------------------------------------------------ layout
@@ -397,6 +401,7 @@ struct NfLane {
     int64_t clock;                   // playback clock (TimestampGeneratorImpl)
     uint64_t stamp;                  // processing-order stamp for scheduler registration
     uint32_t err;
+    int32_t key;                     // partition key id of kb
 
     // StreamPostStateProcessor.isEventReturned of every post of the query: a field
     // of the processor object, so it persists across events (query header word 3)
@@ -1455,6 +1460,7 @@ struct NfLane {
         if (!(q[1] >> 63)) q[1] = (1ull << 63) | (stamp & ~(1ull << 63));
         q[2 + (head + n) % Q->lay.sched_cap] = (uint64_t)t;
         q[0] = (uint64_t)head | ((uint64_t)(n + 1) << 32);
+        if (C && C->sched_armed) C->sched_armed[key] = 1;
     }
     NF_HD bool sched_head(int p, int64_t* t) const {
         const uint64_t* q = sched(p);

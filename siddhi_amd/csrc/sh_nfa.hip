@@ -76,7 +76,8 @@ struct DevEv {
 };
 
 __device__ inline void lane_init(NfLane<DevSink>& L, const nf_table* T, const nf_cols* C, uint64_t* kb,
-                                 DevSink* sink, int64_t clock) {
+                                 DevSink* sink, int64_t clock, int32_t key) {
+    L.key = key;
     L.T = T;
     L.C = C;
     L.kb = kb;
@@ -123,7 +124,7 @@ __global__ void __launch_bounds__(NF_TPB) k_nfa_run(const nf_table* __restrict__
     sink.chunk = nullptr;
     sink.used = sink.n = 0;
     NfLane<DevSink> L;
-    lane_init(L, T, C, kstate + (int64_t)key * T->key_words, &sink, clock);
+    lane_init(L, T, C, kstate + (int64_t)key * T->key_words, &sink, clock, (int32_t)key);
     DevEv ev{&E};
     nf_process_segment(L, ev, (int64_t)beg, end, tick, EM.match_cnt);
     if (sink.chunk) sink.finish();
@@ -135,7 +136,7 @@ __global__ void k_nfa_start(const nf_table* __restrict__ T, const nf_cols* __res
                             uint64_t tick, int64_t clock, nfd_emit EM) {
     if (blockIdx.x * blockDim.x + threadIdx.x != 0) return;
     NfLane<DevSink> L;
-    lane_init(L, T, C, kstate, nullptr, clock);
+    lane_init(L, T, C, kstate, nullptr, clock, 0);
     L.kb[0] |= 1ull;
     for (int q = 0; q < T->n_queries; q++) {
         L.Q = &T->q[q];
@@ -151,14 +152,18 @@ __global__ void k_nfa_start(const nf_table* __restrict__ T, const nf_cols* __res
 __global__ void __launch_bounds__(256) k_nfa_due(const nf_table* __restrict__ T, int q, int p,
                                                  const uint64_t* __restrict__ kstate, int32_t nkeys, int64_t now,
                                                  nfd_cand* __restrict__ cand, unsigned long long* __restrict__ ctr,
-                                                 int64_t cap) {
+                                                 int64_t cap, uint8_t* __restrict__ armed, int clear_armed) {
     const int32_t key = blockIdx.x * blockDim.x + threadIdx.x;
     if (key >= nkeys) return;
+    if (armed && !armed[key]) return;  // never registered since its queues were last empty
     const nf_query& Q = T->q[q];
     const uint64_t* kb = kstate + (int64_t)key * T->key_words;
     const uint64_t* sq = kb + Q.q_off + Q.lay.off_sched + (int64_t)p * (2 + Q.lay.sched_cap);
     const uint32_t head = (uint32_t)sq[0], cnt = (uint32_t)(sq[0] >> 32);
-    if (!cnt) return;
+    if (!cnt) {
+        if (armed && clear_armed) armed[key] = 0;
+        return;
+    }
     if (T->partitioned && !(sq[1] >> 63)) return;
     const int64_t t = (int64_t)sq[2 + head];
     if (t > now) return;
@@ -210,7 +215,7 @@ __global__ void __launch_bounds__(NF_TPB) k_nfa_timer(const nf_table* __restrict
     sink.chunk = nullptr;
     sink.used = sink.n = 0;
     NfLane<DevSink> L;
-    lane_init(L, T, C, kstate + (int64_t)keys[r] * T->key_words, &sink, clock);
+    lane_init(L, T, C, kstate + (int64_t)keys[r] * T->key_words, &sink, clock, keys[r]);
     L.Q = &T->q[q];
     L.qb = L.kb + L.Q->q_off;
     L.qi = q;
@@ -341,10 +346,11 @@ extern "C" int nfd_start(const nf_table* dT, const nf_cols* dC, uint64_t* kstate
 }
 
 extern "C" int nfd_due(const nf_table* dT, int q, int p, const uint64_t* kstate, int32_t nkeys, int64_t now,
-                       nfd_cand* cand, unsigned long long* ctr, int64_t cap, void* stream) {
+                       nfd_cand* cand, unsigned long long* ctr, int64_t cap, uint8_t* armed, int clear_armed,
+                       void* stream) {
     if (nkeys <= 0) return 0;
     hipLaunchKernelGGL(k_nfa_due, dim3(nf_blocks(nkeys, 256)), dim3(256), 0, (hipStream_t)stream, dT, q, p, kstate,
-                       nkeys, now, cand, ctr, cap);
+                       nkeys, now, cand, ctr, cap, armed, clear_armed);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -45,8 +45,11 @@ int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, const nfd_e
             uint64_t tick, int64_t clock, const nfd_emit* em, void* stream);
 int nfd_start(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, uint64_t tick, int64_t clock,
               const nfd_emit* em, void* stream);
+// armed (may be NULL): per-key maybe-registered flags (nf_cols.sched_armed);
+// clear_armed: the scan covers the key's only absent processor, so an empty
+// queue clears the flag
 int nfd_due(const nf_table* dT, int q, int p, const uint64_t* kstate, int32_t nkeys, int64_t now, nfd_cand* cand,
-            unsigned long long* ctr, int64_t cap, void* stream);
+            unsigned long long* ctr, int64_t cap, uint8_t* armed, int clear_armed, void* stream);
 // device tie-break of a due-key backlog: tmin of the candidates, then per due
 // time t (slot t - tmin of `range`) the key with the earliest stamp (-1: none)
 int nfd_cand_tmin(const nfd_cand* cand, int64_t nc, unsigned long long* tmin, void* stream);
