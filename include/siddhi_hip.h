@@ -82,6 +82,17 @@ int sh_start(sh_handle* h);
    core/query/input/MultiProcessStreamReceiver.java:155-183). */
 int sh_push_batch(sh_handle* h, const sh_batch* batch);
 
+/* Registers attr.toString() of partition key ids [first_key, first_key + n) as
+   UTF-16 (offsets[0..n] index into utf16): the ids the host put in sh_batch.keys
+   (ValuePartitionExecutor.execute, core/partition/executor/ValuePartitionExecutor.java:34-40).
+   Their String.hashCode / compareTo fix the iteration order of the playback
+   scheduler's state map (PartitionStateHolder.states, a HashMap<String, ...>,
+   util/snapshot/state/PartitionStateHolder.java:36), which decides the one
+   state per due time Scheduler.onTimeChange fires (util/Scheduler.java:75-87).
+   Call before the ids first appear in a batch; an unregistered id is taken to
+   be its decimal digits. */
+int sh_set_partition_keys(sh_handle* h, int32_t first_key, int32_t n, const uint16_t* utf16, const int64_t* offsets);
+
 /* Replaces the playback clock advance TimestampGeneratorImpl.setCurrentTimestamp
    -> Scheduler.onTimeChange (core/util/timestamp/TimestampGeneratorImpl.java:105-121,
    core/util/Scheduler.java:74-99). */

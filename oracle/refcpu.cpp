@@ -36,8 +36,10 @@
 //   executor/VariableExpressionExecutor.java,
 //   executor/function/IfThenElseFunctionExecutor.java           -> eval()
 //   util/Scheduler.java:74-206, util/timestamp/TimestampGeneratorImpl.java -> Scheduler
+//   java.util.HashMap iteration order of PartitionStateHolder.states    -> jhashmap.h
 //   util/parser/StateInputStreamParser.java:76-408               -> QueryRT::parse
 #include "refcpu.h"
+#include "jhashmap.h"
 
 #include <algorithm>
 #include <cmath>
@@ -243,6 +245,9 @@ struct Holder {
     std::unordered_map<int64_t, S*> states;
     int64_t ckey = INT64_MIN;  // one-entry lookup cache (same semantics as the map)
     S* cst = nullptr;
+    // PartitionStateHolder.states as a java.util.HashMap (iteration order), kept
+    // only where the order is observable (the Scheduler's holder)
+    JHashMap* order = nullptr;
     S* get();
     void ret(S* s);
     ~Holder() {
@@ -410,10 +415,9 @@ struct Scheduler {
     App* app = nullptr;
     AbsentPre* target = nullptr;  // EntryValveProcessor -> absent pre-processor
     Holder<SchedState> holder;
-    // HashMap<String,...> iteration order of partition keys is needed for
-    // cross-key tie breaking (Scheduler.java:77-86); keys are replayed in
-    // insertion order here ("parity unpinned").
-    std::vector<int64_t> keyOrder;
+    // PartitionStateHolder.states in java.util.HashMap order: onTimeChange walks
+    // it and keeps the first state per due time (Scheduler.java:77-86)
+    JHashMap order;
     void notifyAt(int64_t t);
     void onTimeChange(int64_t now);
     void sendTimerEvents(SchedState* st, int64_t now);
@@ -631,12 +635,33 @@ struct App {
     Flow flow;
     ReturnHolder* holder = nullptr;
     uint64_t curSeq = 0;
+    uint64_t nextSeq = 0;  // sequence number of the next input event
     int32_t cbGroup = 0;
     int64_t clock = 0;  // TimestampGeneratorImpl current time (playback)
     std::vector<OutRow> out;
     std::vector<StateBase*> zombies;  // destroyed states still referenced in-frame
     std::vector<Scheduler*> schedulers;
     std::string err;
+    // attr.toString() of every partition key id (ValuePartitionExecutor.java:34-40),
+    // UTF-16; an id never registered reads as its decimal digits
+    std::vector<std::u16string> keyStr;
+    std::vector<uint8_t> keyHas;
+    std::vector<int32_t> keyHashes;  // String.hashCode cache (valid where keyHas)
+    std::u16string keyString(int64_t k) const {
+        if (k >= 0 && k < (int64_t)keyStr.size() && keyHas[k]) return keyStr[k];
+        std::string d = std::to_string(k);
+        return std::u16string(d.begin(), d.end());
+    }
+    int32_t keyHash(int64_t k) const {
+        if (k >= 0 && k < (int64_t)keyHas.size() && keyHas[k]) return keyHashes[k];
+        const std::u16string s = keyString(k);
+        return java_string_hash((const uint16_t*)s.data(), (int64_t)s.size());
+    }
+    int keyCompare(int64_t a, int64_t b) const {
+        const std::u16string x = keyString(a), y = keyString(b);
+        return java_string_compare((const uint16_t*)x.data(), (int64_t)x.size(), (const uint16_t*)y.data(),
+                                   (int64_t)y.size());
+    }
     ~App() {
         for (auto* z : zombies) delete z;
     }
@@ -653,6 +678,7 @@ S* Holder<S>::get() {
         return single;
     }
     const int64_t key = app->flow.key;
+    if (order) order->computeIfAbsent(key);  // states.computeIfAbsent(partitionFlowId, ...)
     if (cst && ckey == key) {
         cst->use++;
         return cst;
@@ -671,6 +697,7 @@ void Holder<S>::ret(S* s) {
     if (s->use == 0 && s->canDestroy()) {
         auto it = states.find(app->flow.key);
         if (it != states.end() && it->second == s) states.erase(it);
+        if (order) order->remove(app->flow.key, true);  // removeState -> HashMap.remove
         if (cst == s) cst = nullptr;
         app->zombies.push_back(s);
     }
@@ -1628,22 +1655,16 @@ void AbsentPost::processSE(const SE& se, Chunk<StateEvent>& c) {
 // Scheduler.java:74-99,171-206 (event-time mode)
 void Scheduler::notifyAt(int64_t t) {
     SchedState* st = holder.get();
-    if (holder.partitioned && st->toNotify.empty()) {
-        int64_t k = app->flow.key;
-        if (std::find(keyOrder.begin(), keyOrder.end(), k) == keyOrder.end()) keyOrder.push_back(k);
-    }
     st->toNotify.push_back(t);
     holder.ret(st);
 }
+// sendTimerEvents works on the state object it was handed (no getState)
 void Scheduler::sendTimerEvents(SchedState* st, int64_t now) {
-    (void)st;
-    SchedState* s = holder.get();
-    while (!s->toNotify.empty() && s->toNotify.front() <= now) {
-        int64_t t = s->toNotify.front();
-        s->toNotify.pop_front();
+    while (!st->toNotify.empty() && st->toNotify.front() <= now) {
+        int64_t t = st->toNotify.front();
+        st->toNotify.pop_front();
         target->processTimer(t);
     }
-    holder.ret(s);
 }
 void Scheduler::onTimeChange(int64_t now) {
     if (!holder.partitioned) {
@@ -1653,29 +1674,34 @@ void Scheduler::onTimeChange(int64_t now) {
         if (due) sendTimerEvents(st, now);
         return;
     }
+    // getAllStates(): every state is in use until returnAllStates
+    for (auto& kv : holder.states) kv.second->use++;
     // sortedExpires: TreeMultimap<Long, SchedulerState> with compareTo()==0 for
-    // states => at most one state survives per distinct due time
+    // states => the first state in HashMap iteration order per distinct due time
     std::map<int64_t, int64_t> sorted;
-    for (int64_t k : keyOrder) {
-        auto it = holder.states.find(k);
-        if (it == holder.states.end()) continue;
-        SchedState* st = it->second;
-        if (!st->toNotify.empty() && st->toNotify.front() <= now) {
-            int64_t t = st->toNotify.front();
-            if (!sorted.count(t)) sorted[t] = k;
-        }
-    }
+    order.forEach([&](int64_t k) {
+        SchedState* st = holder.states[k];
+        if (!st->toNotify.empty() && st->toNotify.front() <= now) sorted.emplace(st->toNotify.front(), k);
+    });
     for (auto& kv : sorted) {
         int64_t saved = app->flow.key;
         app->flow.key = kv.second;
-        sendTimerEvents(nullptr, now);
+        sendTimerEvents(holder.states[kv.second], now);
         app->flow.key = saved;
     }
-    // drop keys whose queue drained
-    std::vector<int64_t> keep;
-    for (int64_t k : keyOrder)
-        if (holder.states.count(k)) keep.push_back(k);
-    keyOrder.swap(keep);
+    // returnAllStates(): in iteration order, iterator.remove() of every state that
+    // canDestroy (HashIterator.remove -> removeNode(..., movable = false))
+    for (int64_t k : order.keys()) {
+        auto it = holder.states.find(k);
+        SchedState* st = it->second;
+        st->use--;
+        if (st->use == 0 && st->canDestroy()) {
+            holder.states.erase(it);
+            if (holder.cst == st) holder.cst = nullptr;
+            app->zombies.push_back(st);
+            order.remove(k, false);
+        }
+    }
 }
 
 // ------------------------------------------------------------ selector
@@ -1961,6 +1987,12 @@ Inner* QueryRT::parse(int ei, StreamPre* pre, StreamPost* post, std::vector<Stre
                     s->holder.app = app;
                     s->holder.partitioned = partition >= 0;
                     s->holder.factory = []() { return new SchedState(); };
+                    if (partition >= 0) {
+                        s->holder.order = &s->order;
+                        App* ap = app;
+                        s->order.string_hash = [ap](int64_t k) { return ap->keyHash(k); };
+                        s->order.compare = [ap](int64_t a, int64_t b) { return ap->keyCompare(a, b); };
+                    }
                     app->schedulers.push_back(s);
                     ap->sched = s;
                     pre = ap;
@@ -2223,8 +2255,11 @@ int ref_send(ref_app* ra, const sh_batch* b, uint64_t first_seq) {
     }
     if (rows.empty()) return SH_OK;
     // InputHandler.send: playback clock moves to the batch's last timestamp and
-    // fires due timers BEFORE the batch (InputHandler.java:85-96)
+    // fires due timers BEFORE the batch (InputHandler.java:85-96); rows a timer
+    // emits carry the batch's first sequence number as their trigger
+    a.nextSeq = first_seq;
     if (a.d.playback) ref_advance_time(ra, rows.back()->ts);
+    a.nextSeq = first_seq + (uint64_t)rows.size();
     for (int sub : a.subs[s]) {
         if (sub >= 0) {
             QueryRT* q = a.queries[sub].get();
@@ -2264,10 +2299,28 @@ int ref_send(ref_app* ra, const sh_batch* b, uint64_t first_seq) {
     return SH_OK;
 }
 
+int ref_set_partition_keys(ref_app* ra, int32_t first, int32_t n, const uint16_t* utf16, const int64_t* offsets) {
+    if (!ra || first < 0 || n < 0 || (n && (!utf16 || !offsets))) return SH_E_INVALID_ARG;
+    App& a = ra->a;
+    const size_t need = (size_t)first + (size_t)n;
+    if (a.keyStr.size() < need) {
+        a.keyStr.resize(need);
+        a.keyHas.resize(need, 0);
+        a.keyHashes.resize(need, 0);
+    }
+    for (int32_t i = 0; i < n; i++) {
+        a.keyStr[first + i].assign((const char16_t*)utf16 + offsets[i], (size_t)(offsets[i + 1] - offsets[i]));
+        a.keyHas[first + i] = 1;
+        a.keyHashes[first + i] = java_string_hash(utf16 + offsets[i], offsets[i + 1] - offsets[i]);
+    }
+    return SH_OK;
+}
+
 int ref_advance_time(ref_app* ra, int64_t now) {
     App& a = ra->a;
     if (now < a.clock) return SH_OK;  // TimestampGeneratorImpl: time never goes back
     a.clock = now;
+    a.curSeq = a.nextSeq;
     for (Scheduler* s : a.schedulers) s->onTimeChange(now);
     a.flow.key = INT64_MIN;
     a.flushZombies();

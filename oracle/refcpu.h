@@ -29,6 +29,10 @@ ref_app* ref_create(const sh_app_desc* app, char* err, int errlen);
 void ref_start(ref_app* a);
 /* one InputHandler.send(Event[]) call; events get sequence numbers first_seq.. */
 int ref_send(ref_app* a, const sh_batch* b, uint64_t first_seq);
+/* attr.toString() of partition key ids [first, first+n) as UTF-16 (n+1
+   offsets into utf16): hashCode / compareTo of the keys fix the iteration
+   order of the scheduler's HashMap (jhashmap.h) */
+int ref_set_partition_keys(ref_app* a, int32_t first, int32_t n, const uint16_t* utf16, const int64_t* offsets);
 /* playback clock / timer advance (Scheduler.onTimeChange) */
 int ref_advance_time(ref_app* a, int64_t now);
 /* emitted output rows so far (ordered as StreamCallback would see them) */

@@ -94,6 +94,14 @@ class HipEngine:
         b.nulls = npp if any(m is not None for m in nulls) else None
         check(self.h, _lib.sh_push_batch(self.h, C.byref(b)))
 
+    def set_partition_keys(self, first, strings=None, utf16=None, offsets=None):
+        """attr.toString() of key ids first.. (a list of str, or packed UTF-16 + offsets)"""
+        from .javastr import pack_utf16
+        if utf16 is None:
+            utf16, offsets = pack_utf16(strings)
+        n = len(offsets) - 1
+        check(self.h, _lib.sh_set_partition_keys(self.h, int(first), int(n), utf16.ctypes.data, offsets.ctypes.data))
+
     def advance_time(self, now):
         check(self.h, _lib.sh_advance_time(self.h, int(now)))
 

@@ -82,7 +82,7 @@ class sh_kernel_times(C.Structure):
 # every symbol include/siddhi_hip.h declares (checked by tests/test_abi.py)
 EXPORTED = ["sh_start", "sh_compile", "sh_push_batch", "sh_advance_time", "sh_drain", "sh_pending",
             "sh_destroy", "sh_last_error", "sh_run_device", "sh_last_kernel_times",
-            "sh_version", "sh_device_count"]
+            "sh_version", "sh_device_count", "sh_set_partition_keys"]
 
 
 def bind_product(lib):
@@ -102,6 +102,8 @@ def bind_product(lib):
     lib.sh_destroy.restype = None
     lib.sh_last_error.argtypes = [C.c_void_p]
     lib.sh_last_error.restype = C.c_char_p
+    lib.sh_set_partition_keys.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+    lib.sh_set_partition_keys.restype = C.c_int
     lib.sh_run_device.argtypes = [C.c_void_p, C.POINTER(sh_device_run)]
     lib.sh_run_device.restype = C.c_int
     lib.sh_last_kernel_times.argtypes = [C.c_void_p, C.POINTER(sh_kernel_times)]
@@ -117,6 +119,10 @@ def bind_product(lib):
     lib.shx_jit_compile.restype = C.c_int
     lib.shx_jit_source.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
     lib.shx_jit_source.restype = C.c_int64
+    lib.shx_bucket_compile.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+    lib.shx_bucket_compile.restype = C.c_int
+    lib.shx_bucket_status.argtypes = [C.c_void_p]
+    lib.shx_bucket_status.restype = C.c_int
     return lib
 
 
@@ -127,6 +133,8 @@ def bind_oracle(lib):
     lib.ref_start.restype = None
     lib.ref_send.argtypes = [C.c_void_p, C.POINTER(sh_batch), C.c_uint64]
     lib.ref_send.restype = C.c_int
+    lib.ref_set_partition_keys.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+    lib.ref_set_partition_keys.restype = C.c_int
     lib.ref_advance_time.argtypes = [C.c_void_p, C.c_int64]
     lib.ref_advance_time.restype = C.c_int
     lib.ref_out_count.argtypes = [C.c_void_p]

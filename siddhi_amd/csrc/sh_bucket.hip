@@ -1,0 +1,360 @@
+// sh_bucket.hip — bucketed window engine: the data movement around the hipRTC
+// matcher (shb_match, sh_jit.cpp) for partitioned
+//   every e1=S[f1] -> e2=S[f2(e1,e2)] within W        (C2)
+//
+// A partial opened at event i is consumed at the first later event j of its
+// key with f2(i, j) while ts_j - ts_i <= W (StreamPreStateProcessor.java:325-403:
+// break-early expiry then processAndReturn, every event a consumer candidate).
+// The reference walks one global per-query pending list per event; here:
+//
+//  k_bk_hist    arrival tile T x key bucket b counts (b = key & 255)
+//  (scan)       -> base[b][T]: where tile T's events of bucket b land
+//  k_bk_scatter stable partition of the stream into 256 buckets, moving only
+//               the packed (ts | local key) word and the columns the matcher
+//               reads; tiles are ranked with wave ballots (sh_wave.h) and
+//               staged through LDS so every bucket run is written contiguously
+//  shb_match    (hipRTC) per bucket chunk + halo in LDS: per-consumer walk back
+//               over its key -> partials consumed per event (u8, bucket order),
+//               their e1-side select values (match stream), prefix sums at the
+//               (bucket, tile) segment starts
+//  k_bk_cum / k_bk_ttot  matches before each segment / per arrival tile
+//  k_bk_emit    per arrival tile: re-rank the tile's events by bucket, gather
+//               each consumer's count and match-stream position, scan in arrival
+//               order and write the ordered rows (trigger seq + select values)
+//
+// HBM bytes per event: hist 4 + scatter 16 read / 8 written (C2) + matcher 8
+// + emitter 16 + the match rows; no pass moves the event row more than once.
+#include <hip/hip_runtime.h>
+
+#include "../../include/sh_query.h"
+#include "sh_device.h"
+#include "sh_wave.h"
+
+#define BK_TPB 1024
+#define BK_ITEMS (SHB_TILE / BK_TPB)
+
+static_assert(BK_ITEMS == 16, "tile / threads");
+
+// raw 8-byte value of a column element (the VmVal bits sh_vm.h load_attr forms)
+__device__ __forceinline__ int64_t bk_raw(const void* p, int64_t i, int type) {
+    switch (type) {
+        case SH_T_LONG:
+        case SH_T_DOUBLE: return ((const int64_t*)p)[i];
+        case SH_T_FLOAT: return (int64_t)((const uint32_t*)p)[i];
+        case SH_T_BOOL: return ((const uint8_t*)p)[i] ? 1 : 0;
+        default: return (int64_t)((const int32_t*)p)[i];
+    }
+}
+
+// ---------------------------------------------------------------- histogram
+__global__ void __launch_bounds__(BK_TPB) k_bk_hist(const int32_t* __restrict__ keys, int64_t n, int32_t nkeys,
+                                                    int32_t nt, uint32_t* __restrict__ cnt,
+                                                    int32_t* __restrict__ flag) {
+    __shared__ uint32_t h[SHB_NB];
+    if (threadIdx.x < SHB_NB) h[threadIdx.x] = 0u;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x << SHB_TILE_SHIFT;
+    bool bad = false;
+#pragma unroll 4
+    for (int j = 0; j < BK_ITEMS; j++) {
+        const int64_t i = b0 + j * BK_TPB + threadIdx.x;
+        if (i < n) {
+            const int32_t k = keys[i];
+            if (k >= nkeys) bad = true;
+            else if (k >= 0) atomicAdd(&h[k & (SHB_NB - 1)], 1u);
+        }
+    }
+    if (bad) atomicOr(flag, SHB_F_KEY);
+    __syncthreads();
+    if (threadIdx.x < SHB_NB) cnt[(int64_t)threadIdx.x * nt + blockIdx.x] = h[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(int64_t)SHB_NB * nt] = 0u;
+}
+
+// ---------------------------------------------------------------- partition
+__global__ void __launch_bounds__(BK_TPB) k_bk_scatter(const int32_t* __restrict__ keys,
+                                                       const int64_t* __restrict__ ts, shb_plan P) {
+    __shared__ uint32_t wcnt[BK_TPB / 64][256];
+    __shared__ uint32_t run[256], tstart[256], gbase[256];
+    __shared__ uint32_t ws[BK_TPB / 64];
+    __shared__ uint32_t stage[SHB_TILE];
+    __shared__ uint8_t dig[SHB_TILE];
+    const int64_t b0 = (int64_t)blockIdx.x << SHB_TILE_SHIFT;
+    if (threadIdx.x < 256) {
+        run[threadIdx.x] = 0u;
+        gbase[threadIdx.x] = P.base[(int64_t)threadIdx.x * P.nt + blockIdx.x];
+    }
+    __syncthreads();
+    int32_t key[BK_ITEMS];
+#pragma unroll
+    for (int j = 0; j < BK_ITEMS; j++) {
+        const int64_t i = b0 + j * BK_TPB + threadIdx.x;
+        key[j] = (i < P.n) ? keys[i] : -1;
+        if (key[j] >= 0) atomicAdd(&run[key[j] & (SHB_NB - 1)], 1u);
+    }
+    __syncthreads();
+    uint32_t nvalid;
+    {
+        const uint32_t c = threadIdx.x < 256 ? run[threadIdx.x] : 0u;
+        const uint32_t ex = shw_block_excl<BK_TPB>(c, ws, &nvalid);
+        if (threadIdx.x < 256) {
+            tstart[threadIdx.x] = ex;
+            run[threadIdx.x] = 0u;
+        }
+    }
+    __syncthreads();
+    uint32_t lp[BK_ITEMS];
+    for (int j = 0; j < BK_ITEMS; j++) {
+        const bool valid = key[j] >= 0;
+        const uint32_t d = (uint32_t)key[j] & (SHB_NB - 1);
+        const uint32_t r = shw_rank8<BK_TPB>(d, valid, wcnt, run);
+        lp[j] = tstart[d] + r;
+        if (valid) dig[lp[j]] = (uint8_t)d;
+        // the emitter restores arrival order from this rank (no re-ranking there)
+        const int64_t i = b0 + j * BK_TPB + threadIdx.x;
+        if (i < P.n) P.rk[i] = (uint16_t)r;
+    }
+    // packed (ts - tbase) << kb | key >> 8
+    const int64_t lim = (int64_t)1 << (32 - P.kb);
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < BK_ITEMS; j++) {
+        if (key[j] < 0) continue;
+        const int64_t i = b0 + j * BK_TPB + threadIdx.x;
+        const int64_t dt = ts[i] - P.tbase;
+        if (dt < 0 || dt >= lim) bad = true;
+        stage[lp[j]] = ((uint32_t)dt << P.kb) | ((uint32_t)key[j] >> 8);
+    }
+    if (bad) atomicOr(P.flag, SHB_F_TS);
+    __syncthreads();
+#define BK_WRITE_OUT(T, DST, EXPR)                                                   \
+    {                                                                                \
+        for (int m = 0; m < BK_ITEMS; m++) {                                         \
+            const uint32_t l = (uint32_t)(m * BK_TPB + threadIdx.x);                 \
+            if (l < nvalid) {                                                        \
+                const uint32_t d = dig[l];                                           \
+                ((T*)(DST))[EXPR(gbase[d] + l - tstart[d])] = (T)stage[l];           \
+            }                                                                        \
+        }                                                                            \
+        __syncthreads();                                                             \
+    }
+#define BK_ID(x) (x)
+#define BK_LO(x) (2u * (x))
+#define BK_HI(x) (2u * (x) + 1u)
+    BK_WRITE_OUT(uint32_t, P.w0, BK_ID);
+    for (int c = 0; c < P.n_staged; c++) {
+        const int w = P.st_width[c];
+        const int halves = w == 8 ? 2 : 1;
+        for (int hh = 0; hh < halves; hh++) {
+#pragma unroll
+            for (int j = 0; j < BK_ITEMS; j++) {
+                if (key[j] < 0) continue;
+                const int64_t i = b0 + j * BK_TPB + threadIdx.x;
+                uint32_t v;
+                if (w == 8) v = ((const uint32_t*)P.st_src[c])[2 * i + hh];
+                else if (w == 4) v = ((const uint32_t*)P.st_src[c])[i];
+                else v = ((const uint8_t*)P.st_src[c])[i];
+                stage[lp[j]] = v;
+            }
+            __syncthreads();
+            if (w == 8) {
+                if (hh == 0) BK_WRITE_OUT(uint32_t, P.st_dst[c], BK_LO)
+                else BK_WRITE_OUT(uint32_t, P.st_dst[c], BK_HI)
+            } else if (w == 4) {
+                BK_WRITE_OUT(uint32_t, P.st_dst[c], BK_ID)
+            } else {
+                BK_WRITE_OUT(uint8_t, P.st_dst[c], BK_ID)
+            }
+        }
+    }
+#undef BK_WRITE_OUT
+#undef BK_ID
+#undef BK_LO
+#undef BK_HI
+}
+
+// ---------------------------------------------------------------- segment sums
+// cum[b][T] = matches of bucket b before the start of its tile-T segment: the
+// scanned chunk totals (ctot, exclusive over chunk ids) + the matcher's
+// within-chunk prefix at the segment start (psum)
+__device__ __forceinline__ int64_t bk_gch(uint32_t bs, int b, uint32_t ch) {
+    return (int64_t)(bs / SHB_CH) + ch + b;
+}
+
+__global__ void __launch_bounds__(256) k_bk_cum(shb_plan P) {
+    const int b = blockIdx.x;
+    const uint32_t bs = P.base[(int64_t)b * P.nt];
+    const uint32_t nb = P.base[(int64_t)(b + 1) * P.nt] - bs;
+    const uint32_t nch = (nb + SHB_CH - 1) / SHB_CH;
+    const uint32_t c0 = P.ctot[bk_gch(bs, b, 0)];
+    const uint32_t tot = P.ctot[bk_gch(bs, b, nch)] - c0;
+    uint32_t* row = P.cum + (int64_t)b * (P.nt + 1);
+    for (int T = threadIdx.x; T < P.nt; T += 256) {
+        const uint32_t x = P.base[(int64_t)b * P.nt + T] - bs;
+        row[T] = x >= nb ? tot : P.ctot[bk_gch(bs, b, x / SHB_CH)] - c0 + P.psum[(int64_t)b * P.nt + T];
+    }
+    if (threadIdx.x == 0) row[P.nt] = tot;
+}
+
+// matches per arrival tile: sum over buckets of the tile's segment
+__global__ void __launch_bounds__(256) k_bk_ttot(shb_plan P) {
+    const int64_t T = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (T > P.nt) return;
+    if (T == P.nt) {
+        P.ttot[T] = 0u;
+        return;
+    }
+    uint32_t s = 0;
+    for (int b = 0; b < SHB_NB; b++) {
+        const uint32_t* row = P.cum + (int64_t)b * (P.nt + 1);
+        s += row[T + 1] - row[T];
+    }
+    P.ttot[T] = s;
+}
+
+// ---------------------------------------------------------------- emitter
+// per event (registers): bucket d | count << 8 | rank << 16, and its
+// match-stream position; the select list lives in LDS (uniform per output)
+__global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ keys, shb_plan P, shb_out O,
+                                                    uint64_t seq_base, uint64_t* __restrict__ out_seq,
+                                                    int64_t* __restrict__ out_vals, int64_t out_cap) {
+    __shared__ uint32_t run[256], lstart[256], segx[256], bstart[256], psum[256];
+    __shared__ uint32_t ws[BK_TPB / 64];
+    __shared__ uint32_t S[SHB_TILE];
+    __shared__ int32_t o_kind[SHB_MAX_OUT], o_type[SHB_MAX_OUT];
+    __shared__ const void* o_src[SHB_MAX_OUT];
+    const int T = blockIdx.x;
+    const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
+    const int tile_n = (int)((P.n - b0) < SHB_TILE ? (P.n - b0) : SHB_TILE);
+    if (threadIdx.x < 256) {
+        const int b = threadIdx.x;
+        run[b] = 0u;
+        const uint32_t bs = P.base[(int64_t)b * P.nt];
+        bstart[b] = bs;
+        segx[b] = P.base[(int64_t)b * P.nt + T] - bs;
+        psum[b] = P.psum[(int64_t)b * P.nt + T];
+    }
+    if (threadIdx.x < SHB_MAX_OUT) {
+#pragma unroll
+        for (int o = 0; o < SHB_MAX_OUT; o++)
+            if (o == (int)threadIdx.x) {
+                o_kind[o] = O.kind[o];
+                o_type[o] = O.type[o];
+                o_src[o] = O.src[o];
+            }
+    }
+    // per event (registers): bucket d | count << 8 | rank << 16 (~0u: no key)
+    uint32_t pk[BK_ITEMS];
+#pragma unroll
+    for (int j = 0; j < BK_ITEMS; j++) {
+        const int l = j * BK_TPB + threadIdx.x;
+        const int32_t k = (l < tile_n) ? keys[b0 + l] : -1;
+        const uint32_t r = (l < tile_n) ? (uint32_t)P.rk[b0 + l] : 0u;
+        pk[j] = k >= 0 ? (((uint32_t)k & (SHB_NB - 1)) | (r << 16)) : ~0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < BK_ITEMS; j++)
+        if (pk[j] != ~0u) atomicAdd(&run[pk[j] & 0xFFu], 1u);
+    // counts of the events' consumers, gathered all at once
+#pragma unroll
+    for (int j = 0; j < BK_ITEMS; j++) {
+        if (pk[j] == ~0u) continue;
+        const uint32_t d = pk[j] & 0xFFu, r = pk[j] >> 16;
+        pk[j] |= (uint32_t)P.cnt[bstart[d] + segx[d] + r] << 8;
+    }
+    __syncthreads();
+    uint32_t nvalid;
+    {
+        const uint32_t c = threadIdx.x < 256 ? run[threadIdx.x] : 0u;
+        const uint32_t ex = shw_block_excl<BK_TPB>(c, ws, &nvalid);
+        if (threadIdx.x < 256) lstart[threadIdx.x] = ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < BK_ITEMS; j++) {
+        if (pk[j] == ~0u) continue;
+        const uint32_t d = pk[j] & 0xFFu, r = pk[j] >> 16;
+        S[lstart[d] + r] = (pk[j] >> 8) & 0xFFu;
+    }
+    __syncthreads();
+    shw_lds_excl_scan<BK_TPB, BK_ITEMS>(S, (int)nvalid, ws);
+    // match-stream position: region of the event's matcher chunk + the prefix
+    // inside that chunk (segment start: the matcher's psum; chunk start: 0)
+    uint32_t mpos[BK_ITEMS];
+#pragma unroll
+    for (int j = 0; j < BK_ITEMS; j++) {
+        mpos[j] = 0u;
+        if (pk[j] == ~0u) continue;
+        const uint32_t d = pk[j] & 0xFFu, r = pk[j] >> 16;
+        const uint32_t x = segx[d] + r;
+        const uint32_t ch = x / SHB_CH;
+        const uint32_t hx = (ch * SHB_CH > segx[d]) ? ch * SHB_CH : segx[d];
+        const uint32_t wp = S[lstart[d] + r] - S[lstart[d] + (hx - segx[d])] + (hx == segx[d] ? psum[d] : 0u);
+        mpos[j] = (uint32_t)(bk_gch(bstart[d], (int)d, ch) * SHB_SPAN) + wp;
+    }
+    __syncthreads();
+    // output offsets: scan of the counts in arrival order
+#pragma unroll
+    for (int j = 0; j < BK_ITEMS; j++) {
+        const int l = j * BK_TPB + threadIdx.x;
+        if (l < tile_n) S[l] = pk[j] == ~0u ? 0u : (pk[j] >> 8) & 0xFFu;
+    }
+    __syncthreads();
+    shw_lds_excl_scan<BK_TPB, BK_ITEMS>(S, tile_n, ws);
+    const uint32_t tb = P.ttot[T];
+    const int no = O.n_out;
+#pragma unroll
+    for (int j = 0; j < BK_ITEMS; j++) {
+        if (pk[j] == ~0u) continue;
+        const uint32_t c = (pk[j] >> 8) & 0xFFu;
+        if (!c) continue;
+        const int l = j * BK_TPB + threadIdx.x;
+        const int64_t i = b0 + l;
+        const int64_t row0 = (int64_t)tb + S[l];
+        if (row0 + c > out_cap) continue;  // the host reports SH_E_MORE
+        if (out_seq)
+            for (uint32_t k = 0; k < c; k++) out_seq[row0 + k] = seq_base + (uint64_t)i;
+        if (!out_vals) continue;
+        for (int o = 0; o < no; o++) {
+            const void* src = o_src[o];
+            const int ty = o_type[o];
+            if (o_kind[o] == 1) {
+                const int64_t v = bk_raw(src, i, ty);
+                for (uint32_t k = 0; k < c; k++) out_vals[(row0 + k) * no + o] = v;
+            } else {
+                for (uint32_t k = 0; k < c; k++) out_vals[(row0 + k) * no + o] = bk_raw(src, (int64_t)mpos[j] + k, ty);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- launches
+static int bk_ok() { return hipGetLastError() == hipSuccess ? 0 : -3; }
+
+extern "C" int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_plan* P, uint32_t* scan_tmp,
+                             void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t cells = (int64_t)SHB_NB * P->nt + 1;
+    hipLaunchKernelGGL(k_bk_hist, dim3(P->nt), dim3(BK_TPB), 0, st, keys, P->n, nkeys, P->nt, P->base, P->flag);
+    if (bk_ok()) return -3;
+    if (shd_exclusive_scan(P->base, P->base, cells, scan_tmp, stream)) return -3;
+    hipLaunchKernelGGL(k_bk_scatter, dim3(P->nt), dim3(BK_TPB), 0, st, keys, ts, *P);
+    return bk_ok();
+}
+
+extern "C" int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (shd_exclusive_scan(P->ctot, P->ctot, P->n_gch + 1, scan_tmp, stream)) return -3;
+    hipLaunchKernelGGL(k_bk_cum, dim3(SHB_NB), dim3(256), 0, st, *P);
+    if (bk_ok()) return -3;
+    hipLaunchKernelGGL(k_bk_ttot, dim3((P->nt + 1 + 255) / 256), dim3(256), 0, st, *P);
+    if (bk_ok()) return -3;
+    return shd_exclusive_scan(P->ttot, P->ttot, (int64_t)P->nt + 1, scan_tmp, stream);
+}
+
+extern "C" int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, uint64_t seq_base,
+                        uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
+    hipLaunchKernelGGL(k_bk_emit, dim3(P->nt), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O, seq_base, out_seq,
+                       out_vals, out_cap);
+    return bk_ok();
+}

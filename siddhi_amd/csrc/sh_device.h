@@ -77,6 +77,64 @@ struct shd_window_ws {
     int32_t* flag;           // [1] non-monotone timestamps seen
 };
 
+// ---- bucketed window engine (sh_bucket.hip + the hipRTC matcher shb_match)
+// Partitioned `every e1=S[f1] -> e2=S[f2] within W`: events are moved once into
+// SHB_NB key buckets (bucket = key & (SHB_NB-1), arrival order kept inside a
+// bucket), the matcher walks each consumer's key back through an LDS-resident
+// chunk of its bucket, and the emitter restores arrival order per arrival tile.
+#define SHB_NB 256
+#define SHB_TILE_SHIFT 14
+#define SHB_TILE (1 << SHB_TILE_SHIFT)
+#define SHB_CH 4096
+#define SHB_HALO 1024
+#define SHB_SPAN (SHB_CH + SHB_HALO)
+#define SHB_MAX_STAGED 4
+#define SHB_MAX_MS 4
+#define SHB_MAX_OUT 16
+// flag bits raised on the device (any bit: rerun on the general window path)
+#define SHB_F_TS 1        // timestamp outside the packed range
+#define SHB_F_KEY 2       // key id >= n_keys
+#define SHB_F_MONO 4      // timestamps decrease inside a key
+#define SHB_F_COUNT 8     // one consumer takes > 255 partials
+#define SHB_F_HALO 16     // a walk reached the halo start
+
+struct shb_plan {
+    int64_t n;
+    int64_t tbase;            // packed ts = ts - tbase in the high (32 - kb) bits of w0
+    int32_t nt;               // arrival tiles of SHB_TILE events
+    int32_t kb;               // local key bits: w0 low bits = key >> log2(SHB_NB)
+    int32_t grid_g;           // matcher grid = SHB_NB * grid_g; a workgroup takes chunks c, c + grid_g, ...
+    int64_t n_gch;            // matcher chunk ids: chunk c of bucket b = bs / SHB_CH + c + b
+    int32_t n_staged;
+    int32_t pad;
+    const void* st_src[SHB_MAX_STAGED];  // arrival-order columns moved into bucket order
+    void* st_dst[SHB_MAX_STAGED];
+    int32_t st_width[SHB_MAX_STAGED];
+    int32_t n_ms;             // match-stream columns (e1-side select values)
+    void* ms[SHB_MAX_MS];     // [n_gch * SHB_SPAN] each, natural width
+    int32_t ms_width[SHB_MAX_MS];
+    uint32_t* w0;             // bucket order: packed ts | local key
+    uint16_t* rk;             // arrival order: rank of the event inside its (tile, bucket) segment
+    uint32_t* base;           // [SHB_NB * nt + 1]: (bucket, tile) counts -> exclusive scan
+    uint8_t* cnt;             // bucket order: partials consumed per event
+    uint32_t* psum;           // [SHB_NB * nt]: within-chunk prefix at each (bucket, tile) segment start
+    uint32_t* ctot;           // [n_gch + 1]: matches per matcher chunk -> exclusive scan
+    uint32_t* cum;            // [SHB_NB * (nt + 1)]: matches of a bucket before each segment
+    uint32_t* ttot;           // [nt + 1]: matches per arrival tile -> exclusive scan
+    int32_t* flag;
+    unsigned long long* prof; // diagnostics (SH_BK_PROFILE): clock ticks per matcher phase, NULL off
+};
+
+// select list of the emitter: value o comes from match-stream column idx[o]
+// (kind 0) or from the consumer event's attribute idx[o] (kind 1)
+struct shb_out {
+    int32_t n_out;
+    int32_t pad;
+    int32_t kind[SHB_MAX_OUT];
+    int32_t type[SHB_MAX_OUT];    // sh_type: raw-value conversion
+    const void* src[SHB_MAX_OUT]; // kind 0: match-stream column, kind 1: consumer column
+};
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -116,6 +174,12 @@ int shd_sort_pairs(const uint32_t* keys, const uint32_t* vals, int64_t n, int bi
                    uint32_t* const* vbuf, uint32_t* hist, uint32_t* scan_tmp, void* stream,
                    const uint32_t** keys_out, const uint32_t** vals_out);
 int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, void* stream);
+// bucketed window engine launch steps (sh_bucket.hip), all async on `stream`
+int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_plan* P, uint32_t* scan_tmp,
+                  void* stream);
+int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream);
+int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, uint64_t seq_base, uint64_t* out_seq,
+             int64_t* out_vals, int64_t out_cap, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -18,6 +18,7 @@
 #include "../../include/siddhi_hip.h"
 #include "sh_device.h"
 #include "sh_jit.h"
+#include "sh_jmap.h"
 #include "sh_nfa.h"
 #include "sh_nfa_dev.h"
 #include "sh_nfa_lower.h"
@@ -384,6 +385,14 @@ struct sh_handle {
     PinBuf pin_in, pin_rd, pin_out;
     DevBuf n_tmin, n_slot_s, n_slot_k;  // device tie-break of due keys
     DevBuf n_armed;                     // per key: may hold a scheduler entry (nf_cols.sched_armed)
+    // scheduler maps' iteration order (sh_jmap.h): host models fed by the
+    // launches' getState history, per-key ranks uploaded for the due-key pick
+    bool sm_on = false;
+    ShSchedModels sm;
+    DevBuf n_sev, n_sev_ctr, n_rk_keys, n_rk_vals;
+    std::vector<DevBuf> n_rank;         // by scheduler id, [n_nkeys] u64
+    PinBuf pin_sev, pin_rk;
+    int64_t sev_cap = 0;
     int caps[5] = {16, 32, 64, 32, 8};
     int32_t n_nkeys = 0;          // key blocks allocated
     int64_t rec_cap = 0;
@@ -402,6 +411,15 @@ struct sh_handle {
     shr_table r_tab{};
     DevBuf rd_rules, rd_ixval, rd_ixstart, rd_ixrule, rd_free, rd_tab;
     DevBuf r_rec, r_keys, r_g, r_sk, r_sv, r_hist, r_scan, r_run;
+    // ---- bucketed window engine (sh_bucket.hip + shb_match): 0 untried, 1 loaded, <0 unavailable
+    int bk_state = 0;
+    int32_t part_attr0 = -1;  // stream-0 attribute keying query 0's partition
+    int bk_last = 0;          // 1: the last sh_run_device ran on the bucketed engine
+    shj_bucket bk{};
+    std::string bk_err;
+    DevBuf bk_w0, bk_rk, bk_base, bk_cnt, bk_psum, bk_ctot, bk_cum, bk_ttot, bk_flag, bk_prof;
+    DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS];
+    PinBuf bk_rd;
 };
 
 static void set_layout(shp_layout& Y, const shp_program& P, int32_t cap) {
@@ -549,6 +567,9 @@ static int compile_chain(sh_handle* h, const sh_app_desc* app) {
     h->prog = P;
     h->n_out = P.n_out;
     h->partitioned = app->queries[0].partition >= 0;
+    h->part_attr0 = (h->partitioned && app->partition_attr)
+                        ? app->partition_attr[app->queries[0].partition * app->n_streams + 0]
+                        : -1;
     // per-key state layout
     const char* capenv = getenv("SH_PARTIAL_CAP");
     set_layout(h->lay, P, capenv ? atoi(capenv) : 32);
@@ -698,6 +719,15 @@ static int compile_nfa(sh_handle* h, const sh_app_desc* app) {
     for (int q = 0; q < T->n_queries; q++) nout = std::max(nout, T->q[q].n_out);
     h->n_out = nout;
     h->partitioned = T->partitioned;
+    if (T->partitioned && T->has_absent && !getenv("SH_NO_MAP_ORDER")) {
+        std::vector<int> ids;
+        for (int q = 0; q < T->n_queries; q++)
+            for (int p = 0; p < T->q[q].n_proc; p++)
+                if (T->q[q].proc[p].kind == NF_K_ABSENT) ids.push_back(q * NF_MAX_PROC + p);
+        h->sm_on = true;
+        h->sm.init(ids, NF_MAX_QUERIES * NF_MAX_PROC);
+        h->n_rank.resize(NF_MAX_QUERIES * NF_MAX_PROC);
+    }
     return SH_OK;
 }
 
@@ -854,6 +884,12 @@ int sh_push_batch(sh_handle* h, const sh_batch* b) {
         if (k + 1 > h->max_key) h->max_key = k + 1;
     }
     h->seq_next += b->n;
+    return SH_OK;
+}
+
+int sh_set_partition_keys(sh_handle* h, int32_t first_key, int32_t n, const uint16_t* utf16, const int64_t* offsets) {
+    if (!h || first_key < 0 || n < 0 || (n && (!utf16 || !offsets))) return SH_E_INVALID_ARG;
+    h->sm.set_keys(first_key, n, utf16, offsets);
     return SH_OK;
 }
 
@@ -1048,6 +1084,7 @@ static uint8_t* armed_flags(sh_handle* h) {
     return off ? nullptr : h->n_armed.as<uint8_t>();
 }
 
+static int bits_for(uint64_t v);
 static nf_cols nf_store_cols(sh_handle* h) {
     nf_cols c;
     memset(&c, 0, sizeof(c));
@@ -1057,6 +1094,11 @@ static nf_cols nf_store_cols(sh_handle* h) {
             c.nul[s][a] = h->stores[s].has_nul[a] ? (const uint8_t*)h->stores[s].nuls[a].p : nullptr;
         }
     c.sched_armed = armed_flags(h);
+    if (h->sm_on) {
+        c.sev = h->n_sev.as<uint64_t>();
+        c.sev_ctr = h->n_sev_ctr.as<unsigned long long>();
+        c.sev_cap = (uint64_t)h->sev_cap;
+    }
     return c;
 }
 
@@ -1070,8 +1112,79 @@ static int nf_ensure_keys(sh_handle* h, int32_t nkeys) {
     hipMemsetAsync((uint8_t*)h->n_kstate.p + old, 0, need - old, h->stream);
     if (h->n_armed.ensure((size_t)nk)) return SH_E_OOM;
     hipMemsetAsync((uint8_t*)h->n_armed.p + h->n_nkeys, 0, (size_t)(nk - h->n_nkeys), h->stream);
+    if (h->sm_on)
+        for (int s : h->sm.used)
+            if (h->n_rank[s].ensure((size_t)nk * 8)) return SH_E_OOM;
     h->n_nkeys = nk;
     return 0;
+}
+
+// scheduler-history buffer for a launch processing `events` events / keys
+static int nf_sev_ready(sh_handle* h, int64_t events) {
+    if (!h->sm_on) return 0;
+    const int64_t need = std::max<int64_t>(4096, 2 * (events + 64) * (int64_t)h->sm.used.size());
+    if (need > h->sev_cap) {
+        hipStreamSynchronize(h->stream);
+        if (h->n_sev.ensure_fresh((size_t)need * 16) || h->n_sev_ctr.ensure_fresh(64)) return SH_E_OOM;
+        h->sev_cap = need;
+    }
+    return hipMemsetAsync(h->n_sev_ctr.p, 0, 8, h->stream) == hipSuccess ? 0 : SH_E_HIP;
+}
+
+// replay the launch's getState history on the host models and upload the
+// changed ranks (before the next due scan, on the same stream)
+static int nf_sev_apply(sh_handle* h) {
+    if (!h->sm_on) return SH_OK;
+    hipStream_t st = h->stream;
+    if (h->pin_sev.ensure(64)) return fail(h, SH_E_OOM, "pinned staging");
+    hipMemcpyAsync(h->pin_sev.p, h->n_sev_ctr.p, 8, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+    const int64_t n = (int64_t)*h->pin_sev.as<unsigned long long>();
+    if (n == 0) return SH_OK;
+    if (h->pin_sev.ensure((size_t)n * 16)) return fail(h, SH_E_OOM, "pinned staging");
+    hipMemcpyAsync(h->pin_sev.p, h->n_sev.p, (size_t)n * 16, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+    if (!h->sm.apply(h->pin_sev.as<uint64_t>(), (size_t)n))
+        return fail(h, SH_E_UNSUPPORTED, "more than 2^26 scheduler map bins (keys waiting on one absent state)");
+    // ranks: whole array after a resize, else the touched keys
+    std::vector<int32_t> ks;
+    std::vector<uint64_t> vs;
+    for (int s : h->sm.used) {
+        ShJMap& M = h->sm.maps[s];
+        if (M.rerank_all) {
+            const int32_t nk = h->n_nkeys;
+            if (h->pin_rk.ensure((size_t)nk * 8)) return fail(h, SH_E_OOM, "pinned staging");
+            uint64_t* r = h->pin_rk.as<uint64_t>();
+            for (int32_t k = 0; k < nk; k++) r[k] = M.present(k) ? M.rank(k) : ~0ull;
+            hipMemcpyAsync(h->n_rank[s].p, r, (size_t)nk * 8, hipMemcpyHostToDevice, st);
+            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "rank upload");
+        } else if (!M.dirty.empty()) {
+            ks.clear();
+            vs.clear();
+            std::sort(M.dirty.begin(), M.dirty.end());
+            M.dirty.erase(std::unique(M.dirty.begin(), M.dirty.end()), M.dirty.end());
+            for (int32_t k : M.dirty)
+                if (M.present(k) && k < h->n_nkeys) {
+                    ks.push_back(k);
+                    vs.push_back(M.rank(k));
+                }
+            const size_t m = ks.size();
+            if (m) {
+                if (h->pin_rk.ensure(m * 12) || h->n_rk_keys.ensure_fresh(m * 4) || h->n_rk_vals.ensure_fresh(m * 8))
+                    return fail(h, SH_E_OOM, "rank upload");
+                memcpy(h->pin_rk.p, vs.data(), m * 8);
+                memcpy(h->pin_rk.as<uint8_t>(m * 8), ks.data(), m * 4);
+                hipMemcpyAsync(h->n_rk_vals.p, h->pin_rk.p, m * 8, hipMemcpyHostToDevice, st);
+                hipMemcpyAsync(h->n_rk_keys.p, h->pin_rk.as<uint8_t>(m * 8), m * 4, hipMemcpyHostToDevice, st);
+                nfd_rank_scatter(h->n_rk_keys.as<int32_t>(), h->n_rk_vals.as<uint64_t>(), (int64_t)m,
+                                 h->n_rank[s].as<uint64_t>(), st);
+                if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "rank upload");
+            }
+        }
+        M.rerank_all = false;
+        M.dirty.clear();
+    }
+    return SH_OK;
 }
 
 static int nf_upload_table(sh_handle* h) {
@@ -1279,6 +1392,18 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
         hipMemsetAsync(h->w_cnt.p, 0, n * 4, st);
         hipMemsetAsync(h->n_ctr.p, 0, 8, st);
         hipMemsetAsync(h->n_err.p, 0, 4, st);
+        if (h->sm_on) {
+            if (nf_sev_ready(h, n)) return fail(h, SH_E_OOM, "scheduler history");
+            if (cols.sev != h->n_sev.as<uint64_t>() || cols.sev_cap != (uint64_t)h->sev_cap) {
+                // the buffer moved: refresh the column image
+                cols = nf_store_cols(h);
+                if (sorted_cols) {
+                    for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = h->v_scol[a].p;
+                    if (alias >= 0) cols.col[0][alias] = skeys;
+                }
+                nf_put_cols(h, cols);
+            }
+        }
         nfd_emit em = nf_emit(h);
         if (nfd_run(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), &E, n, seg_list, nseg,
                     skeys, nkeys, max_seg, h->tick, h->clock, &em, st))
@@ -1289,6 +1414,8 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
         const unsigned err = *h->pin_rd.as<unsigned>(PR_ERR);
         if (!err) {
             h->tick++;
+            int src = nf_sev_apply(h);
+            if (src) return src;
             int rc = nf_place(h, n, n_rows, d_seq, d_vals, cap);
             hipEventRecord(h->ev[3], st);
             hipStreamSynchronize(st);
@@ -1309,7 +1436,12 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
         if (err & NF_E_EMIT) {
             if (nf_ensure_recs(h, h->rec_cap * 4)) return fail(h, SH_E_OOM, "emission buffer");
         }
-        if (err & ~(unsigned)NF_E_EMIT) {
+        if (err & NF_E_SEV) {
+            hipStreamSynchronize(st);
+            if (h->n_sev.ensure_fresh((size_t)h->sev_cap * 4 * 16)) return fail(h, SH_E_OOM, "scheduler history");
+            h->sev_cap *= 4;
+        }
+        if (err & ~(unsigned)(NF_E_EMIT | NF_E_SEV)) {
             int rc = nf_grow(h, err);
             if (rc) return rc;
         }
@@ -1342,7 +1474,8 @@ static int nf_timers(sh_handle* h, int64_t now) {
             if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");
             hipMemsetAsync(h->n_ctr.p, 0, 8, st);
             nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, now, h->n_cand.as<nfd_cand>(),
-                    h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0, st);
+                    h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0,
+                    h->sm_on ? h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>() : nullptr, st);
             hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
             if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
             const unsigned long long nc = *h->pin_rd.as<unsigned long long>(PR_NC);
@@ -1400,23 +1533,39 @@ static int nf_timers(sh_handle* h, int64_t now) {
                 hipMemsetAsync(h->w_cnt.p, 0, (size_t)ns * 4, st);
                 hipMemsetAsync(h->n_ctr.p, 0, 8, st);
                 hipMemsetAsync(h->n_err.p, 0, 4, st);
+                if (h->sm_on) {
+                    const void* sev0 = h->n_sev.p;
+                    const int64_t cap0 = h->sev_cap;
+                    if (nf_sev_ready(h, ns)) return fail(h, SH_E_OOM, "scheduler history");
+                    if (sev0 != h->n_sev.p || cap0 != h->sev_cap || attempt > 0) nf_put_cols(h, nf_store_cols(h));
+                }
                 nfd_emit em = nf_emit(h);
                 nfd_timer(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), q, p,
-                          h->n_sel.as<int32_t>(), ns, now, h->tick, h->clock, &em, st);
+                          h->n_sel.as<int32_t>(), ns, now, h->tick, h->clock, h->seq_next, &em, st);
                 hipMemcpyAsync(h->pin_rd.as<void>(PR_ERR), h->n_err.p, 4, hipMemcpyDeviceToHost, st);
                 if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_timer");
-                const unsigned err = *h->pin_rd.as<unsigned>(PR_ERR);
+                unsigned err = *h->pin_rd.as<unsigned>(PR_ERR);
                 if (!err) break;
                 if (err & NF_E_UNSUP) return fail(h, SH_E_UNSUPPORTED, "startStateReset recursion");
                 nfd_save_keys(h->n_kstate.as<uint64_t>(), (int64_t)kw, h->n_sel.as<int32_t>(), ns,
                               h->n_save.as<uint64_t>(), 1, st);
                 if (err & NF_E_EMIT && nf_ensure_recs(h, h->rec_cap * 4)) return fail(h, SH_E_OOM, "emission");
+                if (err & NF_E_SEV) {
+                    hipStreamSynchronize(st);
+                    if (h->n_sev.ensure_fresh((size_t)h->sev_cap * 4 * 16)) return fail(h, SH_E_OOM, "history");
+                    h->sev_cap *= 4;
+                    err &= ~(unsigned)NF_E_SEV;
+                }
                 if (err & ~(unsigned)NF_E_EMIT) {
                     int rc = nf_grow(h, err);
                     if (rc) return rc;
                 }
             }
             h->tick++;
+            {
+                int src = nf_sev_apply(h);
+                if (src) return src;
+            }
             int64_t rows = 0;
             int rc = nf_place(h, ns, &rows, nullptr, nullptr, 0);
             if (rc) return rc;
@@ -1835,6 +1984,139 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
     return SH_OK;
 }
 
+// bucketed window engine (sh_bucket.hip): partitioned window programs with a
+// consumer-side form and a null-free projection; 0 ok, 1 = not applicable or a
+// premise failed on the device (the caller runs the general window path),
+// SH_E_MORE = output capacity too small (out_count = matches), <0 error
+static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
+    static const bool off = getenv("SH_DISABLE_BUCKET") != nullptr;
+    h->bk_last = 0;
+    const shp_program& P = h->prog;
+    const int64_t n = run->n;
+    if (off || !h->partitioned || nkeys < 1024 || !P.out_fast || n < SHB_TILE) return 1;
+    const int kb = std::max(0, bits_for((uint64_t)(nkeys - 1)) - 8);
+    if (kb > 8) return 1;
+    // select list: e2-side values (and e1's partition attribute, equal to e2's
+    // for these types) from the consumer row; other e1-side values ride the match stream
+    shb_out O;
+    memset(&O, 0, sizeof(O));
+    O.n_out = P.n_out;
+    int ms[SHB_MAX_MS], n_ms = 0;
+    const int part_attr = h->part_attr0;
+    for (int o = 0; o < P.n_out; o++) {
+        const int a = P.out_attr[o], t = P.attr_type[0][a];
+        O.type[o] = t;
+        const bool fold = a == part_attr && (t == SH_T_STRING || t == SH_T_INT || t == SH_T_LONG || t == SH_T_BOOL);
+        if (P.out_slot[o] == 1 || fold) {
+            O.kind[o] = 1;
+            O.src[o] = run->d_cols[a];
+            continue;
+        }
+        int m = 0;
+        while (m < n_ms && ms[m] != a) m++;
+        if (m == n_ms) {
+            if (n_ms == SHB_MAX_MS) return 1;
+            ms[n_ms++] = a;
+        }
+        O.kind[o] = 0;
+        O.src[o] = (const void*)(intptr_t)m;  // resolved below
+    }
+    if (h->bk_state == 0) {
+        const int lrc = shj_bucket_load(&P, ms, n_ms, &h->bk, &h->bk_err);
+        h->bk_state = lrc == 0 ? 1 : (lrc == -1 ? -2 : -1);  // -2: no consumer-side form (not applicable)
+    }
+    if (h->bk_state != 1) return 1;
+    hipStream_t st = h->stream;
+    shb_plan B;
+    memset(&B, 0, sizeof(B));
+    B.n = n;
+    B.nt = (int32_t)((n + SHB_TILE - 1) / SHB_TILE);
+    B.kb = kb;
+    B.n_gch = n / SHB_CH + SHB_NB + 2;
+    B.grid_g = (int32_t)((n / SHB_NB + SHB_CH - 1) / SHB_CH) + 2;
+    const int64_t cells = (int64_t)SHB_NB * B.nt;
+    if (ensure_ws(h, std::max<int64_t>(n, cells + 1)) || h->bk_w0.ensure_fresh(n * 4) || h->bk_rk.ensure_fresh(n * 2) ||
+        h->bk_base.ensure_fresh((cells + 1) * 4) || h->bk_cnt.ensure_fresh(n) || h->bk_psum.ensure_fresh(cells * 4) ||
+        h->bk_ctot.ensure_fresh((B.n_gch + 1) * 4) || h->bk_cum.ensure_fresh((cells + SHB_NB) * 4) ||
+        h->bk_ttot.ensure_fresh((B.nt + 1) * 4) || h->bk_flag.ensure_fresh(64) || h->bk_rd.ensure(64))
+        return fail(h, SH_E_OOM, "bucket workspace");
+    B.n_staged = h->bk.n_staged;
+    for (int k = 0; k < B.n_staged; k++) {
+        const int a = h->bk.staged_attr[k];
+        const int w = type_width(P.attr_type[0][a]);
+        if (h->bk_st[k].ensure_fresh(n * w)) return fail(h, SH_E_OOM, "bucket workspace");
+        B.st_src[k] = run->d_cols[a];
+        B.st_dst[k] = h->bk_st[k].p;
+        B.st_width[k] = w;
+    }
+    B.n_ms = n_ms;
+    for (int m = 0; m < n_ms; m++) {
+        const int w = type_width(P.attr_type[0][ms[m]]);
+        if (h->bk_ms[m].ensure_fresh(B.n_gch * SHB_SPAN * w)) return fail(h, SH_E_OOM, "match stream");
+        B.ms[m] = h->bk_ms[m].p;
+        B.ms_width[m] = w;
+    }
+    for (int o = 0; o < O.n_out; o++)
+        if (O.kind[o] == 0) O.src[o] = B.ms[(int)(intptr_t)O.src[o]];
+    B.w0 = h->bk_w0.as<uint32_t>();
+    B.rk = h->bk_rk.as<uint16_t>();
+    B.base = h->bk_base.as<uint32_t>();
+    B.cnt = h->bk_cnt.as<uint8_t>();
+    B.psum = h->bk_psum.as<uint32_t>();
+    B.ctot = h->bk_ctot.as<uint32_t>();
+    B.cum = h->bk_cum.as<uint32_t>();
+    B.ttot = h->bk_ttot.as<uint32_t>();
+    B.flag = h->bk_flag.as<int32_t>();
+    static const bool prof = getenv("SH_BK_PROFILE") != nullptr;
+    if (prof) {
+        if (h->bk_prof.ensure_fresh(64)) return fail(h, SH_E_OOM, "profile");
+        hipMemsetAsync(h->bk_prof.p, 0, 64, h->stream);
+        B.prof = h->bk_prof.as<unsigned long long>();
+    }
+    // packed timestamps: ts - tbase in 32 - kb bits, centred on the first event
+    hipMemcpyAsync(h->bk_rd.p, run->d_ts, 8, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "bucket: timestamp read");
+    B.tbase = *h->bk_rd.as<int64_t>() - ((int64_t)1 << (31 - kb));
+    hipEventRecord(h->ev[0], st);
+    hipMemsetAsync(B.flag, 0, 4, st);
+    hipMemsetAsync(B.ctot, 0, (B.n_gch + 1) * 4, st);
+    if (shb_partition(run->d_keys, run->d_ts, nkeys, &B, h->w_scan.as<uint32_t>(), st))
+        return fail(h, SH_E_HIP, "bucket partition launch failed");
+    hipEventRecord(h->ev[1], st);
+    void* args[] = {&B};
+    if (hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.grid_g), 1, 1, 512, 1, 1, 0, st,
+                              args, nullptr) != hipSuccess)
+        return fail(h, SH_E_HIP, "shb_match launch failed");
+    if (shb_finish(&B, h->w_scan.as<uint32_t>(), st)) return fail(h, SH_E_HIP, "bucket scan launch failed");
+    hipEventRecord(h->ev[2], st);
+    if (shb_emit(run->d_keys, &B, &O, 0, run->d_out_seq, run->d_out_values, run->out_capacity, st))
+        return fail(h, SH_E_HIP, "bucket emit launch failed");
+    hipEventRecord(h->ev[3], st);
+    hipMemcpyAsync(h->bk_rd.as<void>(0), B.flag, 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(h->bk_rd.as<void>(8), B.ttot + B.nt, 4, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in bucket engine");
+    const int32_t flag = *h->bk_rd.as<int32_t>(0);
+    const int64_t total = *h->bk_rd.as<uint32_t>(8);
+    if (B.prof) {
+        unsigned long long pr[8];
+        hipMemcpy(pr, B.prof, 64, hipMemcpyDeviceToHost);
+        fprintf(stderr, "[shb_match clock ticks, sum over workgroups] load %llu rank %llu walk %llu scan+psum %llu emit %llu\n",
+                pr[0], pr[1], pr[2], pr[3], pr[4]);
+    }
+    if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
+    if (flag) return 1;
+    run->out_count = total;
+    if (total > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
+    if (run->d_out_query && total > 0) hipMemsetAsync(run->d_out_query, 0, total * 4, st);
+    hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
+    hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
+    hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
+    hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
+    h->times.advance_launches = 1;
+    h->bk_last = 1;
+    return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "bucket engine");
+}
+
 int sh_run_device(sh_handle* h, sh_device_run* run) {
     if (!h || !run) return SH_E_INVALID_ARG;
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device");
@@ -1892,6 +2174,10 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
     for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = run->d_cols[a];
     int64_t nm = 0;
     h->times = sh_kernel_times{};
+    if (h->prog.window_ok) {
+        const int brc = run_bucket(h, run, nkeys);
+        if (brc != 1) return brc;
+    }
     if (h->prog.window_ok && h->stream_types[0].size() <= 7) {
         const int64_t n = run->n;
         hipStream_t st = h->stream;
@@ -1987,6 +2273,42 @@ int shx_jit_compile(sh_handle* h) {
     std::string err;
     if (!h->prog.window_ok) return fail(h, SH_E_UNSUPPORTED, "not a window-shaped program");
     if (shj_window_compile(&h->prog, &w, &err)) return fail(h, SH_E_HIP, err);
+    return SH_OK;
+}
+
+// 1: the last sh_run_device ran on the bucketed engine; 0: another engine;
+// -1: its matcher could not be built (message in sh_last_error)
+int shx_bucket_status(sh_handle* h) {
+    if (!h) return 0;
+    if (h->bk_state < 0) {
+        h->err = h->bk_err;
+        return -1;
+    }
+    return h->bk_last;
+}
+
+// compile-only check of the bucketed matcher shb_match (no device needed)
+int shx_bucket_compile(sh_handle* h, char* buf, int64_t len) {
+    if (!h) return SH_E_INVALID_ARG;
+    const shp_program& P = h->prog;
+    if (!P.window_ok || !P.out_fast) return fail(h, SH_E_UNSUPPORTED, "not a window-shaped projection");
+    int ms[SHB_MAX_MS], n_ms = 0;
+    for (int o = 0; o < P.n_out; o++) {
+        const int a = P.out_attr[o], t = P.attr_type[0][a];
+        const bool fold = a == h->part_attr0 && (t == SH_T_STRING || t == SH_T_INT || t == SH_T_LONG || t == SH_T_BOOL);
+        if (P.out_slot[o] == 1 || fold) continue;
+        int m = 0;
+        while (m < n_ms && ms[m] != a) m++;
+        if (m == n_ms && n_ms < SHB_MAX_MS) ms[n_ms++] = a;
+    }
+    std::string src, err;
+    if (shj_bucket_source(&P, ms, n_ms, &src)) return fail(h, SH_E_UNSUPPORTED, "no consumer-side form");
+    if (buf && len > 0) {
+        const int64_t k = std::min<int64_t>(len - 1, (int64_t)src.size());
+        memcpy(buf, src.data(), k);
+        buf[k] = 0;
+    }
+    if (shj_bucket_compile(&P, ms, n_ms, &err)) return fail(h, SH_E_HIP, err);
     return SH_OK;
 }
 

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <set>
@@ -714,6 +715,227 @@ if (out_ts) out_ts[dst] = tq;
     return true;
 }
 
+// ---- bucketed window engine matcher (sh_bucket.hip drives it)
+//
+// shb_match: one workgroup per (bucket, chunk): the chunk's SHB_CH events of the
+// bucket plus SHB_HALO earlier ones are staged in LDS (packed ts | local key and
+// the staged columns), stably re-sorted by local key with ballot ranking, and
+// every event of the chunk walks back over its key as a consumer (ExtForm): the
+// partials it consumes are counted (u8, bucket order), a scan over the chunk
+// places their e1-side select values in the chunk's match-stream region, and the
+// prefix at each (bucket, tile) segment start goes to psum for the emitter.
+bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& ms_attrs, std::vector<int>& staged_out,
+                std::string& src) {
+    std::set<int> need_r, need_q;
+    SideGen gq, gi;
+    gq.pfx[0] = "x0_";
+    gq.pfx[1] = "x1_";
+    gq.need[0] = &need_r;
+    gq.need[1] = &need_q;
+    gi.pfx[0] = gi.pfx[1] = "x0_";
+    gi.need[0] = gi.need[1] = &need_r;
+    gi.tmp = 1000;
+    const std::string DT = F.cross ? dom_ctype(F.dom) : "int32_t";
+    std::string qhead = "bool qok = true;\n" + gq.terms(F.qonly, "qok");
+    if (F.cross) qhead += "if (qok) {\n" + gq.xval(F, "xq_") + "xq = xq_;\n}\n";
+    std::string cand = "bool ok = true;\n" + gq.terms(F.f1, "ok") + gq.terms(F.ionly, "ok");
+    if (F.cross)
+        cand += "if (ok) {\n" + gq.yval(F, "y") + "ok = cmp_op<" + DT + ">(" + std::to_string(F.op) +
+                ", xq, y) && !(hasM && cmp_op<" + DT + ">(" + std::to_string(F.op) + ", M, y));\n}\n";
+    else
+        cand += "ok = ok && !hasM;\n";
+    std::string mid = "bool mk = true;\n" + gi.terms(F.qonly, "mk");
+    std::string stop;
+    if (F.cross) {
+        const bool mx = F.op == SH_OP_GT || F.op == SH_OP_GE;
+        mid += "if (mk) {\n" + gi.xval(F, "xr") + "if (xr == xr && (!hasM || xr " + (mx ? ">" : "<") +
+               " M)) M = xr;\nif (xr == xr) hasM = true;\n}\n";
+        stop = std::string("    if (xq != xq || (hasM && M ") + (mx ? ">=" : "<=") + " xq)) { stopped = true; break; }\n";
+    } else {
+        mid += "if (mk) hasM = true;\n";
+        stop = "    if (hasM) { stopped = true; break; }\n";
+    }
+    std::set<int> staged = need_r;
+    staged.insert(need_q.begin(), need_q.end());
+    for (int a : ms_attrs) staged.insert(a);
+    if (staged.size() > SHB_MAX_STAGED) return false;
+    staged_out.assign(staged.begin(), staged.end());
+    auto sidx = [&](int a) { return (int)(std::find(staged_out.begin(), staged_out.end(), a) - staged_out.begin()); };
+    auto lds = [&](int a) { return "s_a" + std::to_string(a); };
+    auto loads = [&](const std::set<int>& attrs, const std::string& pfx, const std::string& row) {
+        std::string s;
+        for (int a : attrs)
+            s += pfx + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], lds(a) + "[" + row + "]") + ";\n";
+        return s;
+    };
+    auto walk = [&](bool count, const std::string& on_consumed) {
+        std::string s = "const uint32_t wq = s_w0[i];\nconst uint32_t key = wq & kmask;\n"
+                        "const int64_t tq = (int64_t)(wq >> kb);\n" +
+                        decl_attrs(need_r, 0) + decl_attrs(need_q, 1) + loads(need_q, "x1_", "i") + DT +
+                        " xq = 0;\n" + qhead + "bool hasM = false;\n" + DT + " M = 0;\nbool first = true;\n"
+                        "bool stopped = false;\n";
+        s += "for (int r = sp - 1; r >= 0; r--) {\n"
+             "    const int o = (int)s_perm[r];\n    const uint32_t wr = s_w0[o];\n"
+             "    if ((wr & kmask) != key) break;\n    const int64_t tr = (int64_t)(wr >> kb);\n";
+        if (count) s += "    if (first && tq < tr) atomicOr(P.flag, SHB_F_MONO);\n";
+        s += "    first = false;\n    if (tq - tr > SHJ_W || !qok) { stopped = true; break; }\n";
+        s += loads(need_r, "x0_", "o");
+        s += "    {\n" + cand + "    if (ok) {\n" + on_consumed + "    }\n    }\n";
+        s += "    {\n" + mid + "    }\n" + stop + "}\n";
+        if (count) s += "if (!stopped && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n";
+        return s;
+    };
+    std::string ms_put;
+    for (size_t m = 0; m < ms_attrs.size(); m++) {
+        const int a = ms_attrs[m];
+        ms_put += "        ((" + std::string(col_ctype(P.attr_type[0][a])) + "*)P.ms[" + std::to_string(m) +
+                  "])[dst] = " + lds(a) + "[o];\n";
+    }
+    (void)sidx;
+
+    src = SHJ_HEADERS;
+    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_TPB 512\n";
+    src += R"(
+extern "C" __global__ void __launch_bounds__(SHB_TPB) shb_match(shb_plan P) {
+__shared__ uint32_t s_w0[SHB_SPAN];
+__shared__ uint16_t s_perm[SHB_SPAN];
+__shared__ uint16_t s_pre[SHB_CH];
+__shared__ uint32_t wcnt[SHB_TPB / 64][256];
+__shared__ uint32_t run[256], tstart[256], ws[SHB_TPB / 64];
+)";
+    for (int a : staged_out)
+        src += "__shared__ " + std::string(col_ctype(P.attr_type[0][a])) + " " + lds(a) + "[SHB_SPAN];\n";
+    for (size_t k = 0; k < staged_out.size(); k++) {
+        const int a = staged_out[k];
+        const std::string ct = col_ctype(P.attr_type[0][a]);
+        src += "const " + ct + "* __restrict__ g_a" + std::to_string(a) + " = (const " + ct + "*)P.st_dst[" +
+               std::to_string(k) + "];\n";
+    }
+    src += R"(
+const int b = (int)(blockIdx.x % SHB_NB);
+const uint32_t bs = P.base[(int64_t)b * P.nt];
+const int64_t nb = (int64_t)P.base[(int64_t)(b + 1) * P.nt] - bs;
+const int kb = P.kb;
+const uint32_t kmask = (1u << kb) - 1u;
+const uint32_t* __restrict__ row = P.base + (int64_t)b * P.nt;
+for (int64_t c = blockIdx.x / SHB_NB; c * SHB_CH < nb; c += P.grid_g) {
+const int64_t cs = c * SHB_CH;
+const int64_t hs = cs > SHB_HALO ? cs - SHB_HALO : 0;
+const int64_t he = (cs + SHB_CH < nb) ? cs + SHB_CH : nb;
+const int L = (int)(he - hs), hl = (int)(cs - hs), nc = L - hl;
+__syncthreads();
+if (threadIdx.x < 256) run[threadIdx.x] = 0u;
+__syncthreads();
+unsigned long long t_prev = wall_clock64();
+#define SHB_PROF(ph) if (P.prof && threadIdx.x == 0) { const unsigned long long t_now = wall_clock64(); atomicAdd(&P.prof[ph], t_now - t_prev); t_prev = t_now; }
+// stage the chunk and its halo; local-key histogram
+for (int i = threadIdx.x; i < L; i += SHB_TPB) {
+    const int64_t g = (int64_t)bs + hs + i;
+    const uint32_t w = P.w0[g];
+    s_w0[i] = w;
+    atomicAdd(&run[w & kmask], 1u);
+)";
+    for (int a : staged_out) src += "    " + lds(a) + "[i] = g_a" + std::to_string(a) + "[g];\n";
+    src += R"(}
+__syncthreads();
+{
+    uint32_t tot;
+    const uint32_t ex = shw_block_excl<SHB_TPB>(threadIdx.x < 256 ? run[threadIdx.x] : 0u, ws, &tot);
+    if (threadIdx.x < 256) {
+        tstart[threadIdx.x] = ex;
+        run[threadIdx.x] = 0u;
+    }
+}
+SHB_PROF(0)
+// stable sort of the span by local key (wave-ballot ranking)
+for (int r0 = 0; r0 < L; r0 += SHB_TPB) {
+    const int i = r0 + (int)threadIdx.x;
+    const bool valid = i < L;
+    const uint32_t d = valid ? (s_w0[i] & kmask) : 0u;
+    const uint32_t rk = shw_rank8<SHB_TPB>(d, valid, wcnt, run);
+    if (valid) s_perm[tstart[d] + rk] = (uint16_t)i;
+}
+__syncthreads();
+SHB_PROF(1)
+// consumers (chunk events) in sorted order: partials taken per event
+for (int sp = threadIdx.x; sp < L; sp += SHB_TPB) {
+const int i = (int)s_perm[sp];
+if (i < hl) continue;
+uint32_t c_ = 0;
+)";
+    src += walk(true, "        c_++;\n");
+    src += R"(if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);
+s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);
+}
+__syncthreads();
+SHB_PROF(2)
+// exclusive prefix of the counts over the chunk (arrival order inside the
+// bucket); the counts go out as bytes, 8 per thread
+uint32_t total;
+{
+    const int p0 = (int)threadIdx.x * (SHB_CH / SHB_TPB);
+    uint32_t v[SHB_CH / SHB_TPB];
+    uint32_t sum = 0;
+    uint64_t packed = 0;
+#pragma unroll
+    for (int q = 0; q < SHB_CH / SHB_TPB; q++) {
+        v[q] = (p0 + q < nc) ? (uint32_t)s_pre[p0 + q] : 0u;
+        sum += v[q];
+        packed |= (uint64_t)v[q] << (8 * q);
+    }
+    uint32_t off = shw_block_excl<SHB_TPB>(sum, ws, &total);
+    if (p0 + (SHB_CH / SHB_TPB) <= nc && (((int64_t)bs + cs + p0) & 7) == 0) {
+        *(uint64_t*)(P.cnt + (int64_t)bs + cs + p0) = packed;
+    } else {
+        for (int q = 0; q < SHB_CH / SHB_TPB; q++)
+            if (p0 + q < nc) P.cnt[(int64_t)bs + cs + p0 + q] = (uint8_t)v[q];
+    }
+#pragma unroll
+    for (int q = 0; q < SHB_CH / SHB_TPB; q++) {
+        if (p0 + q < nc) s_pre[p0 + q] = (uint16_t)off;
+        off += v[q];
+    }
+}
+__syncthreads();
+const int64_t gch = (int64_t)(bs / SHB_CH) + c + b;
+if (threadIdx.x == 0) P.ctot[gch] = total;
+// prefix at every (bucket, tile) segment start inside the chunk: first tile
+// whose segment starts at or after cs (two parallel search rounds)
+{
+    const int stride = (P.nt + SHB_TPB - 1) / SHB_TPB;
+    const int tc = (int)threadIdx.x * stride;
+    const int n1 = __syncthreads_count(tc < P.nt && (int64_t)(row[tc] - bs) < cs);
+    int t0 = 0;
+    if (n1 > 0) {
+        const int lo = (n1 - 1) * stride;
+        const int tf = lo + 1 + (int)threadIdx.x;
+        const int n2 = __syncthreads_count((int)threadIdx.x < stride && tf < P.nt && (int64_t)(row[tf] - bs) < cs);
+        t0 = lo + 1 + n2;
+    }
+    for (int T = t0 + (int)threadIdx.x; T < P.nt; T += SHB_TPB) {
+        const int64_t x = (int64_t)(row[T] - bs);
+        if (x >= he) break;
+        P.psum[(int64_t)b * P.nt + T] = s_pre[x - cs];
+    }
+}
+SHB_PROF(3)
+// the partials again, their e1-side select values into the chunk's region
+const int64_t rbase = gch * SHB_SPAN;
+for (int sp = threadIdx.x; sp < L; sp += SHB_TPB) {
+const int i = (int)s_perm[sp];
+if (i < hl) continue;
+const uint32_t off = s_pre[i - hl];
+const uint32_t cn = ((i + 1 < L) ? (uint32_t)s_pre[i + 1 - hl] : total) - off;
+if (cn == 0u) continue;
+uint32_t k = 0;
+)";
+    std::string put = "        const int64_t dst = rbase + (int64_t)off + (int64_t)(cn - 1u - k);\n        k++;\n" + ms_put +
+                      "        if (k == cn) break;\n";
+    src += walk(false, put);
+    src += "}\n__syncthreads();\nSHB_PROF(4)\n}\n}\n";
+    return true;
+}
+
 struct Entry {
     int status = 0;           // 0 ok, <0 failed (message in err)
     std::string err;
@@ -809,6 +1031,57 @@ int shj_window_load(const shp_program* hp, shj_window* out, std::string* err) {
     out->count = e->count;
     out->emit = e->emit;
     return 0;
+}
+
+int shj_bucket_load(const shp_program* hp, const int* ms_attrs, int n_ms, shj_bucket* out, std::string* err) {
+    memset(out, 0, sizeof(*out));
+    ExtForm F;
+    if (!hp->window_ok || !ext_form(*hp, F)) {
+        if (err) *err = "no consumer-side form";
+        return -1;
+    }
+    std::vector<int> ms(ms_attrs, ms_attrs + n_ms), staged;
+    std::string src;
+    if (!gen_bucket(*hp, F, ms, staged, src)) {
+        if (err) *err = "too many staged columns";
+        return -1;
+    }
+    Entry* e = compile(src);
+    if (e->status) {
+        if (err) *err = e->err;
+        return e->status;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!e->mod) {
+        if (hipModuleLoadData(&e->mod, e->code.data()) != hipSuccess ||
+            hipModuleGetFunction(&e->match, e->mod, "shb_match") != hipSuccess) {
+            if (err) *err = "hipModuleLoadData/GetFunction (shb_match) failed";
+            e->mod = nullptr;
+            return -3;
+        }
+    }
+    out->match = e->match;
+    out->n_staged = (int)staged.size();
+    for (size_t k = 0; k < staged.size(); k++) out->staged_attr[k] = staged[k];
+    return 0;
+}
+
+int shj_bucket_source(const shp_program* hp, const int* ms_attrs, int n_ms, std::string* src) {
+    ExtForm F;
+    if (!hp->window_ok || !ext_form(*hp, F)) return -1;
+    std::vector<int> ms(ms_attrs, ms_attrs + n_ms), staged;
+    return gen_bucket(*hp, F, ms, staged, *src) ? 0 : -1;
+}
+
+int shj_bucket_compile(const shp_program* hp, const int* ms_attrs, int n_ms, std::string* err) {
+    std::string src;
+    if (shj_bucket_source(hp, ms_attrs, n_ms, &src)) {
+        if (err) *err = "no consumer-side form";
+        return -1;
+    }
+    Entry* e = compile(src);
+    if (e->status && err) *err = e->err;
+    return e->status;
 }
 
 unsigned shj_tiles(int64_t n, uint32_t* tiles_per_xcd, uint32_t* ntiles) {

@@ -25,3 +25,14 @@ int shj_window_load(const shp_program* hp, shj_window* out, std::string* err);
 // grid of the XCD-major tile mapping for n events; returns the workgroup count
 unsigned shj_tiles(int64_t n, uint32_t* tiles_per_xcd, uint32_t* ntiles);
 int shj_tile_size(void);
+
+// bucketed window engine matcher (shb_match); ms_attrs: stream attributes the
+// match stream carries (e1-side select values), in match-stream column order
+struct shj_bucket {
+    void* match;          // hipFunction_t shb_match
+    int n_staged;         // columns the partition moves into bucket order
+    int staged_attr[4];
+};
+int shj_bucket_load(const shp_program* hp, const int* ms_attrs, int n_ms, shj_bucket* out, std::string* err);
+int shj_bucket_source(const shp_program* hp, const int* ms_attrs, int n_ms, std::string* src);
+int shj_bucket_compile(const shp_program* hp, const int* ms_attrs, int n_ms, std::string* err);

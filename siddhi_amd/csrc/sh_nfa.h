@@ -33,6 +33,7 @@
 #include "sh_program.h"
 
 #if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
 #define NF_HD __host__ __device__
 #else
 #define NF_HD
@@ -154,7 +155,16 @@ struct nf_cols {
     // scan when its queues are empty, so the scan skips keys that never armed one
     // (NULL: every key is scanned)
     uint8_t* sched_armed;
+    // scheduler-map history of this launch for the host's HashMap-order model
+    // (sh_jmap.h): 2 words per record, [0] processing stamp, [1] key | scheduler
+    // (query * NF_MAX_PROC + proc) << 32 | kind << 48 (NF_SEV_*); NULL: off
+    uint64_t* sev;
+    unsigned long long* sev_ctr;
+    uint64_t sev_cap;
 };
+#define NF_SEV_INSERT 0  // getState added the key (computeIfAbsent)
+#define NF_SEV_CALL 1    // getState of a present key (lazy resize only)
+#define NF_SEV_REMOVE 2  // queue drained: returnAllStates removes the state
 
 // ------------------------------------------------------------------ layout
 #define NF_PS_WORDS 4
@@ -375,7 +385,8 @@ enum nf_err {
     NF_E_SCHED = 16,  // scheduler queue full
     NF_E_EMIT = 32,   // emission buffer full
     NF_E_UNSUP = 64,  // a reference behaviour outside the lowered subset (recursion)
-    NF_E_KEY = 128    // key id out of range
+    NF_E_KEY = 128,   // key id out of range
+    NF_E_SEV = 256    // scheduler-history buffer full
 };
 
 // ------------------------------------------------------------------ the lane
@@ -1444,12 +1455,28 @@ struct NfLane {
     }
 
     // ---------------------------------------------------------- scheduler
-    // Scheduler.notifyAt (util/Scheduler.java:171-206, event-time mode): the key's
-    // FIFO queue of notification times for absent pre-state p
-    // The scheduler's keyOrder (HashMap iteration stand-in) is a
-    // registration stamp: set when the key enters keyOrder, cleared when its
-    // state is destroyed at the end of onTimeChange.
+    // Scheduler.notifyAt (util/Scheduler.java:113-127, event-time mode): the key's
+    // FIFO queue of notification times for absent pre-state p. Word 1 of the
+    // queue marks the key's presence in the scheduler's state map (set by the
+    // getState that adds it, cleared when onTimeChange's returnAllStates drops
+    // the drained state); every getState is recorded for the host's model of
+    // that map's iteration order (sh_jmap.h), which ranks the keys for the
+    // one-state-per-due-time pick.
     NF_HD uint64_t* sched(int p) const { return qb + Q->lay.off_sched + (int64_t)p * (2 + Q->lay.sched_cap); }
+    NF_HD void sched_record(int p, int kind) {
+        if (!C || !C->sev || !partitioned) return;
+#if defined(__HIP_DEVICE_COMPILE__)
+        const unsigned long long at = atomicAdd(C->sev_ctr, 1ull);
+#else
+        const unsigned long long at = (*C->sev_ctr)++;
+#endif
+        if (at >= C->sev_cap) {
+            err |= NF_E_SEV;
+            return;
+        }
+        C->sev[2 * at] = stamp;
+        C->sev[2 * at + 1] = (uint64_t)(uint32_t)key | ((uint64_t)(qi * NF_MAX_PROC + p) << 32) | ((uint64_t)kind << 48);
+    }
     NF_HD void notify_at(int p, int64_t t) {
         uint64_t* q = sched(p);
         uint32_t head = (uint32_t)q[0], n = (uint32_t)(q[0] >> 32);
@@ -1457,7 +1484,9 @@ struct NfLane {
             err |= NF_E_SCHED;
             return;
         }
-        if (!(q[1] >> 63)) q[1] = (1ull << 63) | (stamp & ~(1ull << 63));
+        const bool added = !(q[1] >> 63);
+        if (added) q[1] = (1ull << 63) | (stamp & ~(1ull << 63));
+        sched_record(p, added ? NF_SEV_INSERT : NF_SEV_CALL);
         q[2 + (head + n) % Q->lay.sched_cap] = (uint64_t)t;
         q[0] = (uint64_t)head | ((uint64_t)(n + 1) << 32);
         if (C && C->sched_armed) C->sched_armed[key] = 1;
@@ -1565,9 +1594,11 @@ struct NfLane {
             sched_pop(p);
             process_timer(p, t);
         }
-        // SchedulerState.canDestroy -> destroyed on return; onTimeChange then drops
-        // the key from keyOrder
-        if (partitioned && (uint32_t)(sched(p)[0] >> 32) == 0) sched(p)[1] = 0;
+        // SchedulerState.canDestroy: returnAllStates drops the drained state
+        if (partitioned && (uint32_t)(sched(p)[0] >> 32) == 0) {
+            sched(p)[1] = 0;
+            sched_record(p, NF_SEV_REMOVE);
+        }
     }
 
     // ---------------------------------------------------------- receivers
@@ -1767,7 +1798,7 @@ NF_HD void nf_process_segment(NfLane<Sink>& L, const Events& ev, int64_t beg, in
                 L.Q = &T->q[q];
                 L.qb = L.kb + L.Q->q_off;
                 L.qi = q;
-                L.stamp = (tick << 40) | ((uint64_t)ev.local(k) * 2);
+                L.stamp = (tick << 32) | ((uint64_t)ev.local(k) * 2);
                 L.init_partition();
             }
         }
@@ -1778,7 +1809,7 @@ NF_HD void nf_process_segment(NfLane<Sink>& L, const Events& ev, int64_t beg, in
             L.Q = Q;
             L.qb = L.kb + Q->q_off;
             L.qi = q;
-            L.stamp = (tick << 40) | ((uint64_t)ev.local(k) * 2 + 1);
+            L.stamp = (tick << 32) | ((uint64_t)ev.local(k) * 2 + 1);
             L.receive(Q->recv[s], ev, k, e);
         }
         if (L.ordinal && match_cnt) match_cnt[ev.local(k)] = L.ordinal;

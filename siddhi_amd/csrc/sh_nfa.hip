@@ -142,7 +142,7 @@ __global__ void k_nfa_start(const nf_table* __restrict__ T, const nf_cols* __res
         L.Q = &T->q[q];
         L.qb = L.kb + L.Q->q_off;
         L.qi = q;
-        L.stamp = tick << 40;
+        L.stamp = tick << 32;
         L.init_partition();
     }
     if (L.err) atomicOr(EM.err, L.err);
@@ -152,7 +152,8 @@ __global__ void k_nfa_start(const nf_table* __restrict__ T, const nf_cols* __res
 __global__ void __launch_bounds__(256) k_nfa_due(const nf_table* __restrict__ T, int q, int p,
                                                  const uint64_t* __restrict__ kstate, int32_t nkeys, int64_t now,
                                                  nfd_cand* __restrict__ cand, unsigned long long* __restrict__ ctr,
-                                                 int64_t cap, uint8_t* __restrict__ armed, int clear_armed) {
+                                                 int64_t cap, uint8_t* __restrict__ armed, int clear_armed,
+                                                 const uint64_t* __restrict__ rank) {
     const int32_t key = blockIdx.x * blockDim.x + threadIdx.x;
     if (key >= nkeys) return;
     if (armed && !armed[key]) return;  // never registered since its queues were last empty
@@ -170,7 +171,8 @@ __global__ void __launch_bounds__(256) k_nfa_due(const nf_table* __restrict__ T,
     unsigned long long at = atomicAdd(ctr, 1ull);
     if ((int64_t)at >= cap) return;
     cand[at].t = t;
-    cand[at].stamp = sq[1] & ~(1ull << 63);
+    // position of the key's state in the scheduler map's iteration order
+    cand[at].stamp = rank ? rank[key] : (sq[1] & ~(1ull << 63));
     cand[at].key = key;
     cand[at].pad = 0;
 }
@@ -204,7 +206,7 @@ __global__ void __launch_bounds__(256) k_cand_pick(const nfd_cand* __restrict__ 
 __global__ void __launch_bounds__(NF_TPB) k_nfa_timer(const nf_table* __restrict__ T, const nf_cols* __restrict__ C,
                                                       uint64_t* __restrict__ kstate, int q, int p,
                                                       const int32_t* __restrict__ keys, int32_t nsel, int64_t now,
-                                                      uint64_t tick, int64_t clock, nfd_emit EM) {
+                                                      uint64_t tick, int64_t clock, uint64_t seq, nfd_emit EM) {
     const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nsel) return;
     DevSink sink;
@@ -220,7 +222,8 @@ __global__ void __launch_bounds__(NF_TPB) k_nfa_timer(const nf_table* __restrict
     L.qb = L.kb + L.Q->q_off;
     L.qi = q;
     L.tag_index = (uint32_t)r;
-    L.stamp = (tick << 40) | (uint64_t)r;
+    L.cur_seq = seq;  // rows a timer emits: the next input event's sequence number
+    L.stamp = (tick << 32) | (uint64_t)r;
     L.send_timer_events(p, now);
     if (L.ordinal) EM.match_cnt[r] = L.ordinal;
     if (sink.chunk) sink.finish();
@@ -347,10 +350,10 @@ extern "C" int nfd_start(const nf_table* dT, const nf_cols* dC, uint64_t* kstate
 
 extern "C" int nfd_due(const nf_table* dT, int q, int p, const uint64_t* kstate, int32_t nkeys, int64_t now,
                        nfd_cand* cand, unsigned long long* ctr, int64_t cap, uint8_t* armed, int clear_armed,
-                       void* stream) {
+                       const uint64_t* rank, void* stream) {
     if (nkeys <= 0) return 0;
     hipLaunchKernelGGL(k_nfa_due, dim3(nf_blocks(nkeys, 256)), dim3(256), 0, (hipStream_t)stream, dT, q, p, kstate,
-                       nkeys, now, cand, ctr, cap, armed, clear_armed);
+                       nkeys, now, cand, ctr, cap, armed, clear_armed, rank);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -358,6 +361,18 @@ extern "C" int nfd_cand_tmin(const nfd_cand* cand, int64_t nc, unsigned long lon
     if (nc <= 0) return 0;
     hipMemsetAsync(tmin, 0xFF, 8, (hipStream_t)stream);
     hipLaunchKernelGGL(k_cand_tmin, dim3(nf_blocks(nc, 256)), dim3(256), 0, (hipStream_t)stream, cand, nc, tmin);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+__global__ void k_rank_scatter(const int32_t* __restrict__ keys, const uint64_t* __restrict__ ranks, int64_t n,
+                               uint64_t* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[keys[i]] = ranks[i];
+}
+
+extern "C" int nfd_rank_scatter(const int32_t* keys, const uint64_t* ranks, int64_t n, uint64_t* dst, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_rank_scatter, dim3(nf_blocks(n, 256)), dim3(256), 0, (hipStream_t)stream, keys, ranks, n, dst);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -374,10 +389,11 @@ extern "C" int nfd_cand_select(const nfd_cand* cand, int64_t nc, int64_t tmin, i
 }
 
 extern "C" int nfd_timer(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, int q, int p, const int32_t* keys,
-                         int32_t nsel, int64_t now, uint64_t tick, int64_t clock, const nfd_emit* em, void* stream) {
+                         int32_t nsel, int64_t now, uint64_t tick, int64_t clock, uint64_t seq, const nfd_emit* em,
+                         void* stream) {
     if (nsel <= 0) return 0;
     hipLaunchKernelGGL(k_nfa_timer, dim3(nf_blocks(nsel, NF_TPB)), dim3(NF_TPB), 0, (hipStream_t)stream, dT, dC,
-                       kstate, q, p, keys, nsel, now, tick, clock, *em);
+                       kstate, q, p, keys, nsel, now, tick, clock, seq, *em);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -48,15 +48,21 @@ int nfd_start(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, uint64_t 
 // armed (may be NULL): per-key maybe-registered flags (nf_cols.sched_armed);
 // clear_armed: the scan covers the key's only absent processor, so an empty
 // queue clears the flag
+// rank (may be NULL): per key, its position in the scheduler map's iteration
+// order (sh_jmap.h); NULL ranks by registration stamp (one key: unpartitioned)
 int nfd_due(const nf_table* dT, int q, int p, const uint64_t* kstate, int32_t nkeys, int64_t now, nfd_cand* cand,
-            unsigned long long* ctr, int64_t cap, uint8_t* armed, int clear_armed, void* stream);
+            unsigned long long* ctr, int64_t cap, uint8_t* armed, int clear_armed, const uint64_t* rank,
+            void* stream);
+// dst[keys[i]] = ranks[i]
+int nfd_rank_scatter(const int32_t* keys, const uint64_t* ranks, int64_t n, uint64_t* dst, void* stream);
 // device tie-break of a due-key backlog: tmin of the candidates, then per due
 // time t (slot t - tmin of `range`) the key with the earliest stamp (-1: none)
 int nfd_cand_tmin(const nfd_cand* cand, int64_t nc, unsigned long long* tmin, void* stream);
 int nfd_cand_select(const nfd_cand* cand, int64_t nc, int64_t tmin, int64_t range, unsigned long long* slot_stamp,
                     int32_t* slot_key, void* stream);
+// seq: trigger sequence number of the rows the timers emit (the next input event's)
 int nfd_timer(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, int q, int p, const int32_t* keys, int32_t nsel,
-              int64_t now, uint64_t tick, int64_t clock, const nfd_emit* em, void* stream);
+              int64_t now, uint64_t tick, int64_t clock, uint64_t seq, const nfd_emit* em, void* stream);
 int nfd_place(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets, int n_out, int32_t* out_query,
               uint64_t* out_seq, int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, void* stream);
 int nfd_save(uint64_t* kstate, int64_t key_words, const uint32_t* seg_list, const uint32_t* nseg, const uint32_t* skeys,

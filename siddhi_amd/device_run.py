@@ -59,6 +59,10 @@ class DeviceRunner:
         """1: hipRTC-specialised window kernels ran, -1: ahead-of-time kernels, 0: not tried."""
         return lib().shx_jit_status(self.handle.h)
 
+    def bucket_status(self):
+        """1: the last run took the bucketed window engine (sh_bucket.hip)."""
+        return lib().shx_bucket_status(self.handle.h)
+
     def last_error(self):
         return lib().sh_last_error(self.handle.h).decode()
 

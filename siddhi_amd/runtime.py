@@ -25,6 +25,7 @@ from typing import Callable, Dict, List, Optional
 import numpy as np
 
 from . import compiler as cp
+from . import javastr
 from .compiler import (BOOL, DOUBLE, FLOAT, INT, LONG, OBJECT, STRING, CompiledApp,
                        SiddhiAppValidationException, SiddhiParserException, UnsupportedQuery)
 
@@ -123,31 +124,43 @@ def decode_value(bits: int, typ: int, strings: cp.StringDict):
 class KeyDict:
     """Partition keys: ValuePartitionExecutor.execute = attr.toString()
     (core/partition/executor/ValuePartitionExecutor.java:34-40). Two values share a
-    partition iff their Java toString() is equal; ids are dense in first-seen order."""
+    partition iff their Java toString() is equal; ids are dense in first-seen order
+    and `text[id]` is that toString() (handed to the library: the scheduler's
+    HashMap<String, ...> order depends on it)."""
 
     def __init__(self):
-        self.ids: Dict[object, int] = {}
+        self.ids: Dict[str, int] = {}
+        self.text: List[str] = []
+        self.registered = 0  # ids [0, registered) already handed to the engine
+
+    @staticmethod
+    def java_text(value, typ) -> str:
+        if typ == FLOAT:
+            return javastr.java_float_to_string(value)
+        if typ == DOUBLE:
+            return javastr.java_double_to_string(value)
+        if typ == BOOL:
+            return "true" if value else "false"
+        if typ in (INT, LONG):
+            return str(int(value))
+        return str(value)
 
     def key(self, value, typ) -> int:
         if value is None:
             return -1
-        if typ == FLOAT:
-            f = _to_float32(value)
-            k = ("nan",) if f != f else ("f", struct.pack("<f", f))
-        elif typ == DOUBLE:
-            f = float(value)
-            k = ("nan",) if f != f else ("d", struct.pack("<d", f))
-        elif typ == BOOL:
-            k = ("b", bool(value))
-        elif typ in (INT, LONG):
-            k = ("i", int(value))
-        else:
-            k = ("s", str(value))
-        i = self.ids.get(k)
+        t = self.java_text(value, typ)
+        i = self.ids.get(t)
         if i is None:
-            i = len(self.ids)
-            self.ids[k] = i
+            i = len(self.text)
+            self.ids[t] = i
+            self.text.append(t)
         return i
+
+    def flush_new(self, engine):
+        """register ids added since the last call with the engine"""
+        if self.registered < len(self.text) and hasattr(engine, "set_partition_keys"):
+            engine.set_partition_keys(self.registered, self.text[self.registered:])
+        self.registered = len(self.text)
 
 
 # ---------------------------------------------------------------- runtime
@@ -285,6 +298,7 @@ class SiddhiAppRuntime:
         if not rows:
             return
         tsa, cols, nulls, keys = self._pack(stream_id, ts, rows)
+        self.keys.flush_new(self._engine)
         if self.app.playback:
             self.clock = max(self.clock, int(tsa[-1]))
         first = self._seq

@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "../../siddhi_amd/csrc/sh_jmap.h"
 #include "../../siddhi_amd/csrc/sh_nfa.h"
 #include "../../siddhi_amd/csrc/sh_nfa_lower.h"
 #include "../../include/siddhi_hip.h"
@@ -70,6 +71,12 @@ struct nfh {
     bool started = false;
     std::vector<OutRow> out;
     int caps[5] = {16, 32, 64, 32, 8};
+    // scheduler-map order models (as sh_host.cpp keeps them)
+    bool sm_on = false;
+    ShSchedModels sm;
+    std::vector<uint64_t> sev;
+    unsigned long long sev_n = 0;
+    uint64_t next_seq = 0;  // sequence number of the next input event
 };
 
 static int width(int t) {
@@ -89,7 +96,29 @@ static nf_cols host_cols(nfh* h) {
             c.col[s][a] = h->cols[s][a].data();
             c.nul[s][a] = h->has_nul[s][a] ? h->nuls[s][a].data() : nullptr;
         }
+    if (h->sm_on) {
+        if (h->sev.size() < (1u << 20)) h->sev.resize(1u << 20);
+        h->sev_n = 0;
+        c.sev = h->sev.data();
+        c.sev_ctr = &h->sev_n;
+        c.sev_cap = h->sev.size() / 2;
+    }
     return c;
+}
+
+// a launch's getState history -> the order models
+static int apply_history(nfh* h) {
+    if (!h->sm_on || h->sev_n == 0) return 0;
+    if (!h->sm.apply(h->sev.data(), (size_t)h->sev_n)) {
+        h->err = "scheduler map beyond the rank encoding";
+        return -4;
+    }
+    for (int s : h->sm.used) {
+        h->sm.maps[s].dirty.clear();
+        h->sm.maps[s].rerank_all = false;
+    }
+    h->sev_n = 0;
+    return 0;
 }
 
 static void ensure_keys(nfh* h, int32_t n) {
@@ -194,6 +223,7 @@ static NfLane<HostSink> make_lane(nfh* h, const nf_cols* C, HostSink* sink, int3
     L.sink = sink;
     L.partitioned = h->T.partitioned;
     L.clock = h->clock;
+    L.key = key;
     return L;
 }
 
@@ -223,7 +253,11 @@ static int timers(nfh* h, int64_t now) {
                     L.qb = L.kb + Q.q_off;
                     int64_t t;
                     if (!(L.sched(p)[1] >> 63) && h->T.partitioned) continue;
-                    if (L.sched_head(p, &t) && t <= now) cs.push_back({t, L.sched(p)[1] & ~(1ull << 63), k});
+                    // rank: the key's position in the scheduler map's iteration order
+                    const bool stamp_order = getenv("SH_NFAH_STAMP_ORDER") != nullptr;  // test control
+                    const uint64_t rank = (h->sm_on && !stamp_order) ? h->sm.maps[q * NF_MAX_PROC + p].rank(k)
+                                                                     : (L.sched(p)[1] & ~(1ull << 63));
+                    if (L.sched_head(p, &t) && t <= now) cs.push_back({t, rank, k});
                 }
                 std::sort(cs.begin(), cs.end(), [](const Cand& a, const Cand& b) {
                     if (a.t != b.t) return a.t < b.t;
@@ -238,12 +272,17 @@ static int timers(nfh* h, int64_t now) {
                     L.qb = L.kb + Q.q_off;
                     L.qi = q;
                     L.tag_index = rank++;
-                    L.stamp = (h->tick << 40) | L.tag_index;
+                    L.cur_seq = h->next_seq;
+                    L.stamp = (h->tick << 32) | L.tag_index;
                     L.send_timer_events(p, now);
                     err |= L.err;
                 }
                 h->tick++;
-                if (!err) take_records(h, sink, h->T.n_queries);
+                if (!err) {
+                    take_records(h, sink, h->T.n_queries);
+                    const int rc = apply_history(h);
+                    if (rc) return rc;
+                }
             }
         }
         if (!err) return 0;
@@ -277,7 +316,20 @@ nfh* nfh_create(const sh_app_desc* d, char* err, int errlen) {
         h->has_nul[s].assign(d->streams[s].n_attrs, false);
     }
     nf_set_caps(&h->T, h->caps[0], h->caps[1], h->caps[2], h->caps[3], h->caps[4]);
+    if (h->T.partitioned && h->T.has_absent) {
+        std::vector<int> ids;
+        for (int q = 0; q < h->T.n_queries; q++)
+            for (int p = 0; p < h->T.q[q].n_proc; p++)
+                if (h->T.q[q].proc[p].kind == NF_K_ABSENT) ids.push_back(q * NF_MAX_PROC + p);
+        h->sm_on = true;
+        h->sm.init(ids, NF_MAX_QUERIES * NF_MAX_PROC);
+    }
     return h;
+}
+
+int nfh_set_partition_keys(nfh* h, int32_t first, int32_t n, const uint16_t* utf16, const int64_t* offsets) {
+    h->sm.set_keys(first, n, utf16, offsets);
+    return 0;
 }
 
 int nfh_start(nfh* h) {
@@ -293,7 +345,7 @@ int nfh_start(nfh* h) {
         L.Q = &h->T.q[q];
         L.qb = L.kb + L.Q->q_off;
         L.qi = q;
-        L.stamp = h->tick << 40;
+        L.stamp = h->tick << 32;
         L.init_partition();
     }
     h->tick++;
@@ -325,10 +377,12 @@ int nfh_send(nfh* h, const sh_batch* b, uint64_t first_seq) {
     }
     h->rows[s] += b->n;
     // InputHandler.send in playback: clock -> last timestamp, due timers first
+    h->next_seq = first_seq;
     if (h->T.playback) {
         int rc = nfh_advance_time(h, b->ts[b->n - 1]);
         if (rc) return rc;
     }
+    h->next_seq = first_seq + (uint64_t)b->n;
     // stable segment by key (null keys dropped)
     std::vector<Ev> evs;
     int32_t maxk = 0;
@@ -359,7 +413,7 @@ int nfh_send(nfh* h, const sh_batch* b, uint64_t first_seq) {
         if (!err) {
             h->tick++;
             take_records(h, sink, h->T.n_queries);
-            return 0;
+            return apply_history(h);
         }
         h->kstate.swap(backup);
         if ((err & (NF_E_UNSUP | NF_E_EMIT | NF_E_KEY)) || !grow(h, err)) {

@@ -42,6 +42,8 @@ def load():
         lib.nfh_out_read.restype = C.c_int
         lib.nfh_last_error.argtypes = [C.c_void_p]
         lib.nfh_last_error.restype = C.c_char_p
+        lib.nfh_set_partition_keys.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        lib.nfh_set_partition_keys.restype = C.c_int
         lib.nfh_destroy.argtypes = [C.c_void_p]
         lib.nfh_destroy.restype = None
         _lib = lib
@@ -75,6 +77,13 @@ class NfaHostEngine:
         tsa = np.ascontiguousarray(tsa, dtype=np.int64)
         b, keep = make_batch(stream, tsa, cols, nulls, keys)
         self._check(self.lib.nfh_send(self.h, C.byref(b), first_seq))
+
+    def set_partition_keys(self, first, strings=None, utf16=None, offsets=None):
+        from siddhi_amd.javastr import pack_utf16
+        if utf16 is None:
+            utf16, offsets = pack_utf16(strings)
+        self.lib.nfh_set_partition_keys(self.h, int(first), int(len(offsets) - 1), utf16.ctypes.data,
+                                        offsets.ctypes.data)
 
     def advance_time(self, now):
         self._check(self.lib.nfh_advance_time(self.h, int(now)))

@@ -70,6 +70,15 @@ class OracleEngine:
         if rc != 0:
             raise RuntimeError(f"ref_send -> {rc}")
 
+    def set_partition_keys(self, first, strings=None, utf16=None, offsets=None):
+        from siddhi_amd.javastr import pack_utf16
+        if utf16 is None:
+            utf16, offsets = pack_utf16(strings)
+        n = len(offsets) - 1
+        rc = self.lib.ref_set_partition_keys(self.h, int(first), int(n), utf16.ctypes.data, offsets.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"ref_set_partition_keys -> {rc}")
+
     def advance_time(self, now):
         self.lib.ref_advance_time(self.h, int(now))
 

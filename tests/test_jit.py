@@ -55,3 +55,26 @@ def test_random_window_queries_compile(lib, seed):
     h = _handle(lib, app, strings)
     assert lib.shx_jit_compile(h) == abi.SH_OK, (app, lib.sh_last_error(h))
     lib.sh_destroy(h)
+
+
+def test_c2_bucket_matcher_compiles(lib):
+    """shb_match (bucketed window engine) for C2: only price is staged and the
+    match stream carries e1.price (e1.symbol is the partition key, taken from e2)"""
+    h = _handle(lib, synth.C2_QUERY)
+    buf = C.create_string_buffer(1 << 20)
+    rc = lib.shx_bucket_compile(h, buf, 1 << 20)
+    src = buf.value.decode()
+    assert rc == abi.SH_OK, (lib.sh_last_error(h), src[-3000:])
+    assert "s_a1[SHB_SPAN]" in src and "s_a0[" not in src and "s_a2[" not in src
+    assert "P.ms[0])[dst] = s_a1[o]" in src
+    lib.sh_destroy(h)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_window_queries_bucket_compile(lib, seed):
+    app, _ = window_case(random.Random(7000 + seed))
+    strings = compiler.StringDict()
+    h = _handle(lib, app, strings)
+    rc = lib.shx_bucket_compile(h, None, 0)
+    assert rc in (abi.SH_OK, abi.SH_E_UNSUPPORTED), (app, lib.sh_last_error(h))
+    lib.sh_destroy(h)
