@@ -413,7 +413,8 @@ struct SchedState : StateBase {
 
 struct Scheduler {
     App* app = nullptr;
-    AbsentPre* target = nullptr;  // EntryValveProcessor -> absent pre-processor
+    // EntryValveProcessor -> the absent pre-processor's process(TIMER chunk)
+    std::function<void(int64_t)> target;
     Holder<SchedState> holder;
     // PartitionStateHolder.states in java.util.HashMap order: onTimeChange walks
     // it and keeps the first state per due time (Scheduler.java:77-86)
@@ -421,6 +422,10 @@ struct Scheduler {
     void notifyAt(int64_t t);
     void onTimeChange(int64_t now);
     void sendTimerEvents(SchedState* st, int64_t now);
+    // wall-clock mode (Scheduler.EventCaller): earliest queued notify time, and
+    // every state due at `now` fired on its own (no TreeMultimap collapse)
+    int64_t nextDue() const;
+    void fireAllDue(int64_t now);
 };
 
 struct AbsentPre : StreamPre {
@@ -440,6 +445,33 @@ struct AbsentPre : StreamPre {
 };
 
 struct AbsentPost : StreamPost {
+    void processSE(const SE& se, Chunk<StateEvent>& c) override;
+};
+
+// AbsentLogicalPreStateProcessor.java:65-420 / AbsentLogicalPostStateProcessor.java:37-49
+struct LogicalAbsentState : PreState {
+    int64_t lastArrivalTime = 0;
+    bool active = true;
+    bool canDestroy() override { return PreState::canDestroy() && lastArrivalTime == 0; }
+};
+struct AbsentLogicalPre : LogicalPre {
+    int64_t waitingTime;
+    Scheduler* sched = nullptr;
+    AbsentLogicalPre(int lt, int64_t w) : LogicalPre(lt), waitingTime(w) { kind = K_ABSENT_LOGICAL; }
+    PreState* newState() override { return new LogicalAbsentState(); }
+    void updateLastArrivalTime(int64_t ts);
+    void addStateImpl(const SE& se, PreState* st) override;
+    void addEveryState(const SE& se) override;
+    void processTimer(int64_t t);  // process(ComplexEventChunk) with a TIMER event
+    bool waitingTimePassed(int64_t now, StateEvent* se);
+    void sendEvent(const SE& se, LogicalAbsentState* st);
+    void setActive(bool a);
+    Chunk<StateEvent> processAndReturn(const Ref<StreamEvent>& sev) override;
+    void partitionCreated();
+    bool partnerCanProceed(StateEvent* se) override;
+};
+struct AbsentLogicalPost : LogicalPost {
+    explicit AbsentLogicalPost(int t) : LogicalPost(t) {}
     void processSE(const SE& se, Chunk<StateEvent>& c) override;
 };
 
@@ -1652,6 +1684,222 @@ void AbsentPost::processSE(const SE& se, Chunk<StateEvent>& c) {
     (void)c;
 }
 
+
+// ------------------------------------------------------------ AbsentLogical
+// AbsentLogicalPreStateProcessor.java:65-420 (event-time semantics)
+// StateEvent.addEvent (StateEvent.java:212-222): append to the slot's chain
+static void addEventToSlot(StateEvent* se, int slot, const Ref<StreamEvent>& ev) {
+    if (!se->ev[slot]) {
+        se->ev[slot] = ev;
+        return;
+    }
+    StreamEvent* x = se->ev[slot].get();
+    while (x->next) x = x->next.get();
+    x->next = ev;
+}
+// :67-76
+void AbsentLogicalPre::updateLastArrivalTime(int64_t ts) {
+    LogicalAbsentState* st = (LogicalAbsentState*)holder.get();
+    st->lastArrivalTime = ts;
+    holder.ret(st);
+}
+// :78-98
+void AbsentLogicalPre::addStateImpl(const SE& se, PreState* pst) {
+    LogicalAbsentState* st = (LogicalAbsentState*)pst;
+    if (!st->active) return;
+    LogicalPre::addStateImpl(se, pst);
+    if (!isStart && waitingTime != -1) {
+        sched->notifyAt(se->ts + waitingTime);
+        if (partner->kind == K_ABSENT_LOGICAL) {
+            AbsentLogicalPre* pa = (AbsentLogicalPre*)partner;
+            pa->sched->notifyAt(se->ts + pa->waitingTime);
+        }
+    }
+}
+// :100-118
+void AbsentLogicalPre::addEveryState(const SE& se) {
+    SE c = q->copyStateEvent(se);
+    c->type = CURRENT;
+    if (c->ev[stateId]) c->ts = c->ev[stateId]->ts;  // the last arrived event's timestamp
+    c->ev[stateId] = Ref<StreamEvent>();
+    c->ev[partner->stateId] = Ref<StreamEvent>();
+    PreState* st = holder.get();
+    st->nae.push_back(c);
+    partner->addToNae(c);
+    holder.ret(st);
+}
+// :120-209
+void AbsentLogicalPre::processTimer(int64_t currentTime) {
+    LogicalAbsentState* st = (LogicalAbsentState*)holder.get();
+    if (!st->active) {
+        holder.ret(st);
+        return;
+    }
+    bool notProcessed = true;
+    Chunk<StateEvent> retc;
+    if (currentTime >= st->lastArrivalTime + waitingTime) {
+        if (isStart && stateType == SH_SEQUENCE && st->nae.empty() && st->pending.empty()) {
+            SE se = q->newStateEvent();
+            addState(se);
+        } else if (stateType == SH_SEQUENCE && !st->nae.empty()) {
+            resetState();
+        }
+        updateState();
+        SE expired;
+        for (auto it = st->pending.begin(); it != st->pending.end();) {
+            SE se = *it;
+            if (isExpired(se.get(), currentTime)) {  // within
+                expired = se;
+                it = st->pending.erase(it);
+                continue;
+            }
+            if (waitingTimePassed(currentTime, se.get())) {
+                it = st->pending.erase(it);
+                const bool partnerIn = (bool)se->ev[partner->stateId];
+                if (logicalType == SH_E_LOGICAL_OR && !partnerIn) {
+                    // OR: the partner never arrived
+                    addEventToSlot(se.get(), stateId, Ref<StreamEvent>(new StreamEvent()));
+                    retc.add(se);
+                } else if (logicalType == SH_E_LOGICAL_AND && partnerIn) {
+                    // AND: the partner arrived but could not send out
+                    retc.add(se);
+                } else if (logicalType == SH_E_LOGICAL_AND && !partnerIn) {
+                    // AND: the partner has not arrived; it may proceed later
+                    addEventToSlot(se.get(), stateId, Ref<StreamEvent>(new StreamEvent()));
+                }
+                continue;
+            }
+            ++it;
+        }
+        if (expired && withinEvery) {
+            withinEvery->addEveryState(expired);
+            withinEvery->updateState();
+        }
+        retc.reset();
+        notProcessed = !retc.first;
+        while (retc.hasNext()) {
+            SE se = retc.next();
+            retc.remove();
+            se->ts = currentTime;
+            sendEvent(se, st);
+        }
+        st->lastArrivalTime = 0;
+    }
+    if (thisPost->nextEveryPre || (notProcessed && isStart)) {
+        // every, or an unanswered start state: wait again
+        const int64_t nextBreak =
+            st->lastArrivalTime == 0 ? q->app->clock + waitingTime : st->lastArrivalTime + waitingTime;
+        sched->notifyAt(nextBreak);
+    }
+    holder.ret(st);
+}
+// :220-228
+bool AbsentLogicalPre::waitingTimePassed(int64_t now, StateEvent* se) {
+    if (!se->ev[stateId]) return now >= se->ts + waitingTime;
+    return now >= se->ev[stateId]->ts + waitingTime;  // re-added by `every`
+}
+// :230-251
+void AbsentLogicalPre::sendEvent(const SE& se, LogicalAbsentState* st) {
+    if (thisPost->nextProc) {
+        Chunk<StateEvent> c(se, se);
+        thisPost->nextProc->process(c);
+    }
+    if (thisPost->nextPre) thisPost->nextPre->addState(se);
+    if (thisPost->nextEveryPre) {
+        thisPost->nextEveryPre->addEveryState(se);
+    } else if (isStart) {
+        st->active = false;
+        if (logicalType == SH_E_LOGICAL_OR && partner->kind == K_ABSENT_LOGICAL)
+            ((AbsentLogicalPre*)partner)->setActive(false);
+    }
+    if (thisPost->callbackPre) thisPost->callbackPre->startStateReset();
+}
+void AbsentLogicalPre::setActive(bool a) {
+    LogicalAbsentState* st = (LogicalAbsentState*)holder.get();
+    st->active = a;
+    holder.ret(st);
+}
+// :262-320
+Chunk<StateEvent> AbsentLogicalPre::processAndReturn(const Ref<StreamEvent>& sev) {
+    Chunk<StateEvent> ret;
+    LogicalAbsentState* st = (LogicalAbsentState*)holder.get();
+    if (!st->active) {
+        holder.ret(st);
+        return ret;
+    }
+    for (auto it = st->pending.begin(); it != st->pending.end();) {
+        SE se = *it;
+        if (logicalType == SH_E_LOGICAL_OR && se->ev[partner->stateId]) {
+            it = st->pending.erase(it);
+            continue;
+        }
+        Ref<StreamEvent> currentStreamEvent = se->ev[stateId];
+        se->ev[stateId] = QueryRT::copyStreamEvent(sev);
+        processSE(se);
+        if (waitingTime != -1 ||
+            (stateType == SH_SEQUENCE && logicalType == SH_E_LOGICAL_AND && thisPost->nextEveryPre))
+            se->ev[stateId] = currentStreamEvent;  // back to the original state
+        bool erased = false;
+        if (thisLast->returned) {
+            // passed the filter: no longer an absence candidate
+            thisLast->returned = false;
+            it = st->pending.erase(it);
+            erased = true;
+            if (stateType == SH_SEQUENCE) partner->pendingList()->remove(se);
+        }
+        if (!st->changed) {
+            se->ev[stateId] = currentStreamEvent;
+            if (stateType == SH_SEQUENCE && !erased) {
+                it = st->pending.erase(it);
+                erased = true;
+            }
+        }
+        if (!erased) ++it;
+    }
+    holder.ret(st);
+    return ret;
+}
+// :333-351
+void AbsentLogicalPre::partitionCreated() {
+    LogicalAbsentState* st = (LogicalAbsentState*)holder.get();
+    if (!st->started) {
+        st->started = true;
+        if (isStart && waitingTime != -1 && st->active) sched->notifyAt(q->app->clock + waitingTime);
+    }
+    holder.ret(st);
+}
+// :353-388
+bool AbsentLogicalPre::partnerCanProceed(StateEvent* se) {
+    LogicalAbsentState* st = (LogicalAbsentState*)holder.get();
+    bool process;
+    if (stateType == SH_SEQUENCE && !thisPost->nextEveryPre && st->lastArrivalTime > 0) {
+        process = false;
+    } else if (waitingTime == -1) {
+        // no `for`: proceed while this absent state has not seen its event
+        if (!thisPost->nextEveryPre) {
+            process = !se->ev[stateId];
+        } else if (st->lastArrivalTime > 0) {
+            process = false;
+            st->lastArrivalTime = 0;
+            init();
+        } else {
+            process = true;
+        }
+    } else {
+        process = (bool)se->ev[stateId];
+    }
+    holder.ret(st);
+    return process;
+}
+// AbsentLogicalPostStateProcessor.java:37-49
+void AbsentLogicalPost::processSE(const SE& se, Chunk<StateEvent>& c) {
+    (void)c;
+    thisPre->stateChanged();
+    StreamEvent* s = se->ev[stateId].get();
+    returned = true;  // tells the pre-processor the absent event arrived
+    ((AbsentLogicalPre*)thisPre)->updateLastArrivalTime(s->ts);
+}
+
 // Scheduler.java:74-99,171-206 (event-time mode)
 void Scheduler::notifyAt(int64_t t) {
     SchedState* st = holder.get();
@@ -1663,7 +1911,38 @@ void Scheduler::sendTimerEvents(SchedState* st, int64_t now) {
     while (!st->toNotify.empty() && st->toNotify.front() <= now) {
         int64_t t = st->toNotify.front();
         st->toNotify.pop_front();
-        target->processTimer(t);
+        target(t);
+    }
+}
+int64_t Scheduler::nextDue() const {
+    int64_t t = INT64_MAX;
+    if (holder.single && !holder.single->toNotify.empty()) t = holder.single->toNotify.front();
+    for (auto& kv : holder.states)
+        if (!kv.second->toNotify.empty()) t = std::min(t, kv.second->toNotify.front());
+    return t;
+}
+// Scheduler.java:285-300 outside playback: each state's EventCaller runs at its
+// head's due time and drains every notify time <= the current time. States due
+// at the same instant are independent callers; they run in HashMap order here.
+void Scheduler::fireAllDue(int64_t now) {
+    std::vector<int64_t> due;
+    if (holder.partitioned) {
+        order.forEach([&](int64_t k) {
+            SchedState* st = holder.states[k];
+            if (!st->toNotify.empty() && st->toNotify.front() <= now) due.push_back(k);
+        });
+    } else {
+        SchedState* st = holder.single;
+        if (st && !st->toNotify.empty() && st->toNotify.front() <= now) sendTimerEvents(st, now);
+        return;
+    }
+    for (int64_t k : due) {
+        auto it = holder.states.find(k);
+        if (it == holder.states.end()) continue;
+        int64_t saved = app->flow.key;
+        if (holder.partitioned) app->flow.key = k;
+        sendTimerEvents(it->second, now);
+        app->flow.key = saved;
     }
 }
 void Scheduler::onTimeChange(int64_t now) {
@@ -1983,7 +2262,7 @@ Inner* QueryRT::parse(int ei, StreamPre* pre, StreamPost* post, std::vector<Stre
                     Scheduler* s = new Scheduler();
                     scheds.emplace_back(s);
                     s->app = app;
-                    s->target = ap;
+                    s->target = [ap](int64_t t) { ap->processTimer(t); };
                     s->holder.app = app;
                     s->holder.partitioned = partition >= 0;
                     s->holder.factory = []() { return new SchedState(); };
@@ -2057,18 +2336,37 @@ Inner* QueryRT::parse(int ei, StreamPre* pre, StreamPost* post, std::vector<Stre
             int lt = e.kind;
             const sh_state_elem& e1 = elems[e.child0];
             const sh_state_elem& e2 = elems[e.child1];
-            if (e1.kind == SH_E_ABSENT_STREAM || e2.kind == SH_E_ABSENT_STREAM) {
-                err = "logical absent states (AbsentLogicalPreStateProcessor) not restated yet";
-                return nullptr;
-            }
-            LogicalPre* p1 = own<LogicalPre>(lt);
+            // an absent element gets AbsentLogicalPre/Post + its own scheduler
+            // (StateInputStreamParser.java:289-344); element 1's scheduler first
+            auto make = [&](const sh_state_elem& x) -> LogicalPre* {
+                if (x.kind != SH_E_ABSENT_STREAM) return own<LogicalPre>(lt);
+                AbsentLogicalPre* ap = own<AbsentLogicalPre>(lt, x.waiting_ms);
+                startupPres.push_back(ap);
+                Scheduler* s = new Scheduler();
+                scheds.emplace_back(s);
+                s->app = app;
+                s->target = [ap](int64_t t) { ap->processTimer(t); };
+                s->holder.app = app;
+                s->holder.partitioned = partition >= 0;
+                s->holder.factory = []() { return new SchedState(); };
+                if (partition >= 0) {
+                    s->holder.order = &s->order;
+                    App* a2 = app;
+                    s->order.string_hash = [a2](int64_t k) { return a2->keyHash(k); };
+                    s->order.compare = [a2](int64_t a, int64_t b) { return a2->keyCompare(a, b); };
+                }
+                app->schedulers.push_back(s);
+                ap->sched = s;
+                return ap;
+            };
+            LogicalPre* p1 = make(e1);
             p1->q = this;
             p1->stateType = st;
-            LogicalPost* o1 = own<LogicalPost>(lt);
-            LogicalPre* p2 = own<LogicalPre>(lt);
+            LogicalPost* o1 = e1.kind == SH_E_ABSENT_STREAM ? own<AbsentLogicalPost>(lt) : own<LogicalPost>(lt);
+            LogicalPre* p2 = make(e2);
             p2->q = this;
             p2->stateType = st;
-            LogicalPost* o2 = own<LogicalPost>(lt);
+            LogicalPost* o2 = e2.kind == SH_E_ABSENT_STREAM ? own<AbsentLogicalPost>(lt) : own<LogicalPost>(lt);
             o1->partnerPre = p2;
             o2->partnerPre = p1;
             o1->partnerPost = o2;
@@ -2158,8 +2456,10 @@ bool QueryRT::build() {
 // StateStreamRuntime.initPartition, StateStreamRuntime.java:90-97
 void QueryRT::initPartition() {
     root->init();
-    for (StreamPre* p : startupPres)
+    for (StreamPre* p : startupPres) {
         if (p->kind == K_ABSENT) ((AbsentPre*)p)->partitionCreated();
+        if (p->kind == K_ABSENT_LOGICAL) ((AbsentLogicalPre*)p)->partitionCreated();
+    }
 }
 
 }  // namespace ref
@@ -2319,8 +2619,23 @@ int ref_set_partition_keys(ref_app* ra, int32_t first, int32_t n, const uint16_t
 int ref_advance_time(ref_app* ra, int64_t now) {
     App& a = ra->a;
     if (now < a.clock) return SH_OK;  // TimestampGeneratorImpl: time never goes back
-    a.clock = now;
     a.curSeq = a.nextSeq;
+    if (!a.d.playback) {
+        // wall clock: the clock passes through every queued notify time in
+        // order and each due state fires at exactly its due time
+        for (;;) {
+            int64_t t = INT64_MAX;
+            for (Scheduler* s : a.schedulers) t = std::min(t, s->nextDue());
+            if (t > now) break;
+            a.clock = std::max(a.clock, t);
+            for (Scheduler* s : a.schedulers) s->fireAllDue(a.clock);
+            a.flow.key = INT64_MIN;
+        }
+        a.clock = now;
+        a.flushZombies();
+        return SH_OK;
+    }
+    a.clock = now;
     for (Scheduler* s : a.schedulers) s->onTimeChange(now);
     a.flow.key = INT64_MIN;
     a.flushZombies();

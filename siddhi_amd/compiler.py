@@ -517,6 +517,11 @@ class Parser:
             right = self.stateful(st)
             if isinstance(left, SCount) or isinstance(right, SCount):
                 self.err("counts cannot be logical operands")
+            if right.absent and not left.absent:
+                # a present/absent mix puts the absent element first
+                # (SiddhiQLBaseVisitorImpl.visitLogical_absent_stateful_source:
+                # State.logicalNotAnd(absent, present) / logicalOr(absent, present))
+                left, right = right, left
             return SLogical(kind, left, right)
         return left
 

@@ -830,7 +830,8 @@ void sh_destroy(sh_handle* h) {
 
 static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0);
 static int nf_start(sh_handle* h);
-static int nf_timers(sh_handle* h, int64_t now);
+static int nf_timers(sh_handle* h, int64_t now, bool wall = false);
+static int nf_next_due(sh_handle* h, int64_t* out);
 
 int sh_push_batch(sh_handle* h, const sh_batch* b) {
     if (!h || !b) return SH_E_INVALID_ARG;
@@ -898,8 +899,25 @@ int sh_advance_time(sh_handle* h, int64_t now_ms) {
     if (h->mode != 1) return SH_OK;  // the chain / window engines have no timer states
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
     if (now_ms < h->clock) return SH_OK;  // TimestampGeneratorImpl: time never goes back
+    if (!h->started) {
+        h->clock = now_ms;
+        return SH_OK;  // schedulers exist from SiddhiAppRuntime.start on
+    }
+    if (!h->app.playback) {
+        // wall clock: the clock passes through every queued notify time in order
+        for (;;) {
+            int64_t t;
+            int rc = nf_next_due(h, &t);
+            if (rc) return rc;
+            if (t > now_ms) break;
+            h->clock = std::max(h->clock, t);
+            rc = nf_timers(h, h->clock, true);
+            if (rc) return rc;
+        }
+        h->clock = now_ms;
+        return SH_OK;
+    }
     h->clock = now_ms;
-    if (!h->started) return SH_OK;  // schedulers exist from SiddhiAppRuntime.start on
     return nf_timers(h, now_ms);
 }
 
@@ -1457,8 +1475,38 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
 }
 
-// Scheduler.onTimeChange(now) for every scheduler (absent pre-state) in creation order
-static int nf_timers(sh_handle* h, int64_t now) {
+// earliest queued notify time over every scheduler and key (INT64_MAX: none)
+static int nf_next_due(sh_handle* h, int64_t* out) {
+    *out = INT64_MAX;
+    if (!h->T->has_absent || h->n_nkeys == 0) return SH_OK;
+    hipStream_t st = h->stream;
+    if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
+    const int32_t nkeys = h->n_nkeys;
+    if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand)) || h->n_tmin.ensure_fresh(8))
+        return fail(h, SH_E_OOM, "candidates");
+    for (int q = 0; q < h->T->n_queries; q++) {
+        for (int p = 0; p < h->T->q[q].n_proc; p++) {
+            if (h->T->q[q].proc[p].kind != NF_K_ABSENT) continue;
+            hipMemsetAsync(h->n_ctr.p, 0, 8, st);
+            nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, INT64_MAX,
+                    h->n_cand.as<nfd_cand>(), h->n_ctr.as<unsigned long long>(), nkeys, nullptr, 0, nullptr, st);
+            hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
+            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
+            const int64_t nc = (int64_t)*h->pin_rd.as<unsigned long long>(PR_NC);
+            if (nc == 0) continue;
+            nfd_cand_tmin(h->n_cand.as<nfd_cand>(), nc, h->n_tmin.as<unsigned long long>(), st);
+            hipMemcpyAsync(h->pin_rd.as<void>(PR_TMIN), h->n_tmin.p, 8, hipMemcpyDeviceToHost, st);
+            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_cand_tmin");
+            *out = std::min(*out, (int64_t)*h->pin_rd.as<unsigned long long>(PR_TMIN));
+        }
+    }
+    return SH_OK;
+}
+
+// Scheduler.onTimeChange(now) for every scheduler (absent pre-state) in creation
+// order. wall: the EventCaller form outside playback (Scheduler.java:285-300) --
+// every due key fires on its own, no collapse of equal due times.
+static int nf_timers(sh_handle* h, int64_t now, bool wall) {
     if (!h->T->has_absent || h->n_nkeys == 0) return SH_OK;
     hipStream_t st = h->stream;
     if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
@@ -1484,7 +1532,7 @@ static int nf_timers(sh_handle* h, int64_t now) {
             // distinct due time, the first in keyOrder (earliest registration)
             std::vector<int32_t> sel;
             bool picked = false;
-            if ((int64_t)nc >= kDeviceTieBreak) {
+            if ((int64_t)nc >= kDeviceTieBreak && !wall) {
                 // large backlog of due keys: pick on the device (slot per due time)
                 if (h->n_tmin.ensure_fresh(8)) return fail(h, SH_E_OOM, "timer tie-break");
                 nfd_cand_tmin(h->n_cand.as<nfd_cand>(), (int64_t)nc, h->n_tmin.as<unsigned long long>(), st);
@@ -1514,7 +1562,7 @@ static int nf_timers(sh_handle* h, int64_t now) {
                     return a.stamp < b.stamp;
                 });
                 for (size_t i = 0; i < cs.size(); i++)
-                    if (i == 0 || cs[i].t != cs[i - 1].t) sel.push_back(cs[i].key);
+                    if (wall || i == 0 || cs[i].t != cs[i - 1].t) sel.push_back(cs[i].key);
             }
             const int32_t ns = (int32_t)sel.size();
             if (h->n_sel.ensure_fresh((size_t)ns * 4) || h->n_save.ensure_fresh((size_t)ns * h->T->key_words * 8))
@@ -2280,6 +2328,7 @@ int shx_jit_compile(sh_handle* h) {
 // -1: its matcher could not be built (message in sh_last_error)
 int shx_bucket_status(sh_handle* h) {
     if (!h) return 0;
+    if (h->bk_state == -2) return 0;  // no consumer-side form: not applicable
     if (h->bk_state < 0) {
         h->err = h->bk_err;
         return -1;

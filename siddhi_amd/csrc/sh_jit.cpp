@@ -768,20 +768,29 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
             s += pfx + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], lds(a) + "[" + row + "]") + ";\n";
         return s;
     };
+    // walk back over the consumer's key in the sorted span, SHB_U events per
+    // step: the step's LDS loads are issued together (no dependent chain)
     auto walk = [&](bool count, const std::string& on_consumed) {
-        std::string s = "const uint32_t wq = s_w0[i];\nconst uint32_t key = wq & kmask;\n"
+        std::string s = "const uint32_t wq = s_ws[sp];\nconst uint32_t key = wq & kmask;\n"
                         "const int64_t tq = (int64_t)(wq >> kb);\n" +
-                        decl_attrs(need_r, 0) + decl_attrs(need_q, 1) + loads(need_q, "x1_", "i") + DT +
+                        decl_attrs(need_r, 0) + decl_attrs(need_q, 1) + loads(need_q, "x1_", "sp") + DT +
                         " xq = 0;\n" + qhead + "bool hasM = false;\n" + DT + " M = 0;\nbool first = true;\n"
-                        "bool stopped = false;\n";
-        s += "for (int r = sp - 1; r >= 0; r--) {\n"
-             "    const int o = (int)s_perm[r];\n    const uint32_t wr = s_w0[o];\n"
-             "    if ((wr & kmask) != key) break;\n    const int64_t tr = (int64_t)(wr >> kb);\n";
+                        "bool stopped = !qok, ran_off = false;\n";
+        s += "for (int r = sp - 1; r >= 0 && !stopped && !ran_off; r -= SHB_U) {\n    uint32_t wv[SHB_U];\n";
+        for (int a : need_r) s += "    " + std::string(col_ctype(P.attr_type[0][a])) + " av" + std::to_string(a) + "[SHB_U];\n";
+        s += "#pragma unroll\n    for (int u = 0; u < SHB_U; u++) {\n        const int o = r - u < 0 ? 0 : r - u;\n"
+             "        wv[u] = s_ws[o];\n";
+        for (int a : need_r) s += "        av" + std::to_string(a) + "[u] = " + lds(a) + "[o];\n";
+        s += "    }\n#pragma unroll\n    for (int u = 0; u < SHB_U; u++) {\n"
+             "    const int o = r - u;\n"
+             "    if (o < 0 || (wv[u] & kmask) != key) { ran_off = true; break; }\n"
+             "    const int64_t tr = (int64_t)(wv[u] >> kb);\n";
         if (count) s += "    if (first && tq < tr) atomicOr(P.flag, SHB_F_MONO);\n";
-        s += "    first = false;\n    if (tq - tr > SHJ_W || !qok) { stopped = true; break; }\n";
-        s += loads(need_r, "x0_", "o");
+        s += "    first = false;\n    if (tq - tr > SHJ_W) { stopped = true; break; }\n";
+        for (int a : need_r)
+            s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
         s += "    {\n" + cand + "    if (ok) {\n" + on_consumed + "    }\n    }\n";
-        s += "    {\n" + mid + "    }\n" + stop + "}\n";
+        s += "    {\n" + mid + "    }\n" + stop + "    }\n}\n";
         if (count) s += "if (!stopped && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n";
         return s;
     };
@@ -794,11 +803,11 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     (void)sidx;
 
     src = SHJ_HEADERS;
-    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_TPB 512\n";
+    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_TPB 512\n#define SHB_U 4\n";
     src += R"(
 extern "C" __global__ void __launch_bounds__(SHB_TPB) shb_match(shb_plan P) {
-__shared__ uint32_t s_w0[SHB_SPAN];
-__shared__ uint16_t s_perm[SHB_SPAN];
+__shared__ uint32_t s_ws[SHB_SPAN];
+__shared__ uint16_t s_idx[SHB_SPAN];
 __shared__ uint16_t s_pre[SHB_CH];
 __shared__ uint32_t wcnt[SHB_TPB / 64][256];
 __shared__ uint32_t run[256], tstart[256], ws[SHB_TPB / 64];
@@ -828,15 +837,9 @@ if (threadIdx.x < 256) run[threadIdx.x] = 0u;
 __syncthreads();
 unsigned long long t_prev = wall_clock64();
 #define SHB_PROF(ph) if (P.prof && threadIdx.x == 0) { const unsigned long long t_now = wall_clock64(); atomicAdd(&P.prof[ph], t_now - t_prev); t_prev = t_now; }
-// stage the chunk and its halo; local-key histogram
-for (int i = threadIdx.x; i < L; i += SHB_TPB) {
-    const int64_t g = (int64_t)bs + hs + i;
-    const uint32_t w = P.w0[g];
-    s_w0[i] = w;
-    atomicAdd(&run[w & kmask], 1u);
-)";
-    for (int a : staged_out) src += "    " + lds(a) + "[i] = g_a" + std::to_string(a) + "[g];\n";
-    src += R"(}
+// local-key histogram of the chunk and its halo
+const uint32_t* __restrict__ gw = P.w0 + (int64_t)bs + hs;
+for (int i = threadIdx.x; i < L; i += SHB_TPB) atomicAdd(&run[gw[i] & kmask], 1u);
 __syncthreads();
 {
     uint32_t tot;
@@ -847,19 +850,31 @@ __syncthreads();
     }
 }
 SHB_PROF(0)
-// stable sort of the span by local key (wave-ballot ranking)
+// stable sort of the span by local key (wave-ballot ranking), staged in sorted
+// order: the walks read consecutive LDS words
 for (int r0 = 0; r0 < L; r0 += SHB_TPB) {
     const int i = r0 + (int)threadIdx.x;
     const bool valid = i < L;
-    const uint32_t d = valid ? (s_w0[i] & kmask) : 0u;
+    const uint32_t w = valid ? gw[i] : 0u;
+)";
+    for (int a : staged_out)
+        src += "    const " + std::string(col_ctype(P.attr_type[0][a])) + " v" + std::to_string(a) + " = valid ? g_a" +
+               std::to_string(a) + "[(int64_t)bs + hs + i] : 0;\n";
+    src += R"(    const uint32_t d = w & kmask;
     const uint32_t rk = shw_rank8<SHB_TPB>(d, valid, wcnt, run);
-    if (valid) s_perm[tstart[d] + rk] = (uint16_t)i;
+    if (valid) {
+        const int pos = (int)(tstart[d] + rk);
+        s_ws[pos] = w;
+        s_idx[pos] = (uint16_t)i;
+)";
+    for (int a : staged_out) src += "        " + lds(a) + "[pos] = v" + std::to_string(a) + ";\n";
+    src += R"(    }
 }
 __syncthreads();
 SHB_PROF(1)
 // consumers (chunk events) in sorted order: partials taken per event
 for (int sp = threadIdx.x; sp < L; sp += SHB_TPB) {
-const int i = (int)s_perm[sp];
+const int i = (int)s_idx[sp];
 if (i < hl) continue;
 uint32_t c_ = 0;
 )";
@@ -922,7 +937,7 @@ SHB_PROF(3)
 // the partials again, their e1-side select values into the chunk's region
 const int64_t rbase = gch * SHB_SPAN;
 for (int sp = threadIdx.x; sp < L; sp += SHB_TPB) {
-const int i = (int)s_perm[sp];
+const int i = (int)s_idx[sp];
 if (i < hl) continue;
 const uint32_t off = s_pre[i - hl];
 const uint32_t cn = ((i + 1 < L) ? (uint32_t)s_pre[i + 1 - hl] : total) - off;
@@ -930,7 +945,7 @@ if (cn == 0u) continue;
 uint32_t k = 0;
 )";
     std::string put = "        const int64_t dst = rbase + (int64_t)off + (int64_t)(cn - 1u - k);\n        k++;\n" + ms_put +
-                      "        if (k == cn) break;\n";
+                      "        if (k == cn) { stopped = true; break; }\n";
     src += walk(false, put);
     src += "}\n__syncthreads();\nSHB_PROF(4)\n}\n}\n";
     return true;

@@ -3,7 +3,7 @@ tests and bench.py: feed synth.c4_stream's send(Event[]) batches to any engine
 of the start/send/advance_time/drain protocol."""
 import numpy as np
 
-from siddhi_amd import synth
+from siddhi_amd import javastr, synth
 
 
 def register_users(engine, blocks):
@@ -45,3 +45,32 @@ def same_output(a, b):
     return (len(a["seq"]) == len(b["seq"]) and np.array_equal(a["seq"], b["seq"])
             and np.array_equal(a["query"], b["query"]) and np.array_equal(a["ts"], b["ts"])
             and np.array_equal(a["values"], b["values"]) and np.array_equal(a["nulls"], b["nulls"]))
+
+
+def ties(blocks):
+    """due milliseconds shared by more than one user (fired one per call)"""
+    due = {}
+    for st, ts, cols, keys in blocks:
+        if st == 1:
+            for t in np.unique(ts):
+                due[int(t)] = due.get(int(t), 0) + int((ts == t).sum())
+    return sum(1 for v in due.values() if v > 1)
+
+
+class CollidingNames:
+    """engine wrapper registering user names built from "Aa"/"BB" blocks, which
+    all share one String.hashCode per length: bins overflow into trees"""
+
+    def __init__(self, eng, n):
+        self.eng = eng
+        names = []
+        for u in range(n):
+            bits = format(u, "014b")
+            names.append("".join("Aa" if b == "0" else "BB" for b in bits[-9:]) + str(u // 512))
+        self.utf16, self.offs = javastr.pack_utf16(names)
+
+    def set_partition_keys(self, first, strings=None, utf16=None, offsets=None):
+        self.eng.set_partition_keys(0, utf16=self.utf16, offsets=self.offs)
+
+    def __getattr__(self, name):
+        return getattr(self.eng, name)

@@ -53,6 +53,17 @@ def same_row(exp, got) -> bool:
     return len(exp) == len(got) and all(same(e, g) for e, g in zip(exp, got))
 
 
+def row_matches(r, got) -> bool:
+    """asserted row: whole data array (`row`) or asserted fields (`fields`, per-index)"""
+    if r.get("fields") is not None:
+        return all(int(k) < len(got) and same(v, got[int(k)]) for k, v in r["fields"].items())
+    return same_row(r["row"], got)
+
+
+def row_text(r):
+    return r["row"] if r.get("fields") is None else {"fields": r["fields"]}
+
+
 class Unsupported(Exception):
     pass
 
@@ -118,17 +129,17 @@ def check_fixture(fx, got):
         if g is not None and not r.get("first_of_callback"):
             if g - 1 >= len(data):
                 if g <= fx["expect_count"]:
-                    errs.append(f"missing event #{g}: expected {r['row']}")
+                    errs.append(f"missing event #{g}: expected {row_text(r)}")
                 continue
-            if not same_row(r["row"], data[g - 1]):
-                errs.append(f"event #{g}: expected {r['row']} got {data[g - 1]}")
+            if not row_matches(r, data[g - 1]):
+                errs.append(f"event #{g}: expected {row_text(r)} got {data[g - 1]}")
             used.add(g - 1)
         else:
             ok = False
             for k, d in enumerate(data):
-                if same_row(r["row"], d):
+                if row_matches(r, d):
                     ok = True
                     break
             if not ok and fx["expect_count"] > 0:
-                errs.append(f"expected row {r['row']} not emitted (got {data})")
+                errs.append(f"expected row {row_text(r)} not emitted (got {data})")
     return errs

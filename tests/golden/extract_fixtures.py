@@ -35,7 +35,15 @@ FILES = [
     "query/pattern/absent/EveryAbsentPatternTestCase.java",
     "query/pattern/absent/AbsentWithEveryPatternTestCase.java",
     "query/sequence/absent/AbsentSequenceTestCase.java",
+    "query/pattern/absent/LogicalAbsentPatternTestCase.java",
+    "query/sequence/absent/LogicalAbsentSequenceTestCase.java",
+    "query/sequence/absent/EveryAbsentSequenceTestCase.java",
+    "query/sequence/absent/AbsentWithEverySequenceTestCase.java",
 ]
+
+# `long now = System.currentTimeMillis();` in playback tests: any base works (the
+# asserted outputs depend on differences only); a fixed one keeps fixtures stable
+TIME_BASE = 1_700_000_000_000
 
 TOKEN = re.compile(r'''
     (?P<ws>\s+|//[^\n]*|/\*.*?\*/)
@@ -173,6 +181,7 @@ def interpret(body):
     expect_count = None
     rows = []
     started = False
+    shut = False
     i = 0
     n = len(toks)
     # guard tracking for assertArrayEquals: last `case K:` or `== K` seen in callback
@@ -184,8 +193,52 @@ def interpret(body):
         raise Skip("persistence test (next row, SURVEY 8f)")
     if "getInputHandler" not in body:
         raise Skip("no input handler")
+    tv = {}  # long time variables of the test body (playback timestamps)
     while i < n:
         k, t, _ = toks[i]
+        # long X = System.currentTimeMillis(); / long X = 123L;
+        if k == "id" and t == "long" and toks[i + 1][0] == "id" and toks[i + 2][1] == "=":
+            var = toks[i + 1][1]
+            if toks[i + 3][1] == "System.currentTimeMillis":
+                tv[var] = TIME_BASE
+                i += 7
+                continue
+            j = i + 3
+            expr = []
+            while toks[j][1] != ";":
+                expr.append(toks[j])
+                j += 1
+            tv[var] = int_expr(expr, tv)
+            i = j + 1
+            continue
+        # X += e; X -= e; X = e; X++; ++X;
+        if k == "id" and t in tv and toks[i + 1][1] in ("+=", "=", "-", "++"):
+            op = toks[i + 1][1]
+            if op == "++":
+                tv[t] += 1
+                i += 2
+                continue
+            if op == "-" and toks[i + 2][1] == "=":
+                j = i + 3
+                sign = -1
+            elif op == "-":
+                i += 1
+                continue
+            else:
+                j = i + 2
+                sign = 1
+            expr = []
+            while toks[j][1] != ";":
+                expr.append(toks[j])
+                j += 1
+            v = int_expr(expr, tv)
+            tv[t] = tv[t] + sign * v if op in ("+=", "-") else v
+            i = j + 1
+            continue
+        if t == "++" and toks[i + 1][0] == "id" and toks[i + 1][1] in tv and toks[i + 2][1] == ";":
+            tv[toks[i + 1][1]] += 1
+            i += 3
+            continue
         if t == "{":
             depth += 1
         elif t == "}":
@@ -259,19 +312,38 @@ def interpret(body):
             h = t.split(".")[0]
             j = i + 2
             ts = None
-            if toks[j][0] == "num":
+            if toks[j][0] == "num" and toks[j + 1][1] == ",":
                 ts = int(value(toks[j])["l"]) if isinstance(value(toks[j]), dict) else int(value(toks[j]))
                 j += 2
+            elif toks[j][1] != "new":
+                # a timestamp expression over the time variables: ++now, now++, now + 100
+                depth0 = 0
+                expr = []
+                while not (toks[j][1] == "," and depth0 == 0):
+                    if toks[j][1] == "(":
+                        depth0 += 1
+                    elif toks[j][1] == ")":
+                        depth0 -= 1
+                    expr.append(toks[j])
+                    j += 1
+                ts = ts_expr(expr, tv)
+                j += 1
             if toks[j][1] != "new":
                 raise Skip("send of non-literal event")
             if toks[j + 1][1] == "Event":
                 raise Skip("send(Event[])")
             vals, j = parse_object_array(toks, j)
-            actions.append(["send", handlers[h], ts, vals])
+            if not shut:
+                actions.append(["send", handlers[h], ts, vals])
             i = j
             continue
+        if k == "id" and t.endswith(".shutdown") and started and in_callback_depth is None:
+            # the runtime is gone: later sleeps and sends reach nothing (count
+            # assertions after this point are still read)
+            shut = True
         if t == "Thread.sleep" and toks[i + 2][0] == "num":
-            actions.append(["sleep", int(toks[i + 2][1].rstrip("lL"))])
+            if not shut:
+                actions.append(["sleep", int(toks[i + 2][1].rstrip("lL"))])
             i += 3
             continue
         if in_callback_depth is not None:
@@ -279,6 +351,18 @@ def interpret(body):
                 guard = int(toks[i + 1][1])
             if t == "==" and toks[i + 1][0] == "num" and toks[i - 1][1] in ("inEventCount", ")", "count"):
                 guard = int(toks[i + 1][1])
+            if t.endswith("assertEquals") and toks[i + 1][1] == "(":
+                # assertEquals(event.getData(k), literal) / assertEquals(literal, event.getData(k))
+                fld = field_assert(toks, i + 2)
+                if fld is not None:
+                    idx, val, j = fld
+                    if rows and rows[-1].get("fields") is not None and rows[-1]["guard"] == guard:
+                        rows[-1]["fields"][str(idx)] = val
+                    else:
+                        rows.append({"guard": guard, "fields": {str(idx): val}, "row": None,
+                                     "first_of_callback": False})
+                    i = j
+                    continue
             if t.endswith("assertArrayEquals") and toks[i + 1][1] == "(":
                 vals, j = parse_object_array(toks, i + 2)
                 # which event: inEvents[0] / events[0] / event
@@ -296,6 +380,13 @@ def interpret(body):
                     j += 2
                 else:
                     msg = ""
+                if toks[j][0] == "id" and toks[j + 1][1] == "," and toks[j + 2][0] == "num" and \
+                        toks[j + 3][1] == ")" and toks[j][1].startswith(("inEventCount", "count", "eventCount")):
+                    # assertEquals(inEventCount, N)
+                    if toks[j][1].startswith("inEventCount") or expect_count is None:
+                        expect_count = int(toks[j + 2][1])
+                    i = j + 3
+                    continue
                 if toks[j][0] == "num" and toks[j + 1][1] == ",":
                     var = toks[j + 2][1]
                     if ("success" in msg or msg == "" or "in event" in msg) and (
@@ -317,6 +408,63 @@ def interpret(body):
         raise Skip("no asserted event count")
     return {"app": app, "actions": actions, "callback": callbacks[0],
             "expect_count": expect_count, "expect_rows": rows}
+
+
+def int_expr(expr, tv):
+    """integer arithmetic over numbers and time variables (no side effects)"""
+    parts = []
+    for k, t, _ in expr:
+        if k == "num":
+            parts.append(t.rstrip("lL"))
+        elif k == "id" and t in tv:
+            parts.append(str(tv[t]))
+        elif t in ("+", "-", "*", "/", "(", ")"):
+            parts.append("//" if t == "/" else t)
+        elif k == "id" and t in ("long", "int"):
+            continue
+        else:
+            raise Skip(f"timestamp expression near {t}")
+    return int(eval("".join(parts), {"__builtins__": {}}, {}))
+
+
+def ts_expr(expr, tv):
+    """send(ts, ...) first argument: ++X, X++, X, or an arithmetic expression"""
+    ts = [t for _, t, _ in expr]
+    if len(ts) == 2 and ts[0] == "++" and ts[1] in tv:
+        tv[ts[1]] += 1
+        return tv[ts[1]]
+    if len(ts) == 2 and ts[1] == "++" and ts[0] in tv:
+        v = tv[ts[0]]
+        tv[ts[0]] += 1
+        return v
+    return int_expr(expr, tv)
+
+
+def field_assert(toks, j):
+    """(index, literal value, next index) of assertEquals(e.getData(k), v) in either order, else None"""
+    def getdata(at):
+        if toks[at][0] == "id" and toks[at][1].endswith(".getData") and toks[at + 1][1] == "(" and \
+                toks[at + 2][0] == "num" and toks[at + 3][1] == ")":
+            return int(toks[at + 2][1]), at + 4
+        return None
+    g = getdata(j)
+    if g is not None and toks[g[1]][1] == ",":
+        try:
+            v = value(toks[g[1] + 1])
+        except ValueError:
+            return None
+        if toks[g[1] + 2][1] != ")":
+            return None
+        return g[0], v, g[1] + 3
+    if toks[j + 1][1] == ",":
+        g = getdata(j + 2)
+        if g is not None and toks[g[1]][1] == ")":
+            try:
+                v = value(toks[j])
+            except ValueError:
+                return None
+            return g[0], v, g[1] + 1
+    return None
 
 
 def concat(toks, i, strs, stop=";"):

@@ -227,8 +227,10 @@ static NfLane<HostSink> make_lane(nfh* h, const nf_cols* C, HostSink* sink, int3
     return L;
 }
 
-// Scheduler.onTimeChange for every scheduler (absent pre-state), in creation order
-static int timers(nfh* h, int64_t now) {
+// Scheduler.onTimeChange for every scheduler (absent pre-state), in creation order.
+// wall: the EventCaller form (outside playback) -- every due key fires, no
+// collapse of equal due times
+static int timers(nfh* h, int64_t now, bool wall = false) {
     if (!h->T.has_absent) return 0;
     for (int attempt = 0; attempt < 40; attempt++) {
         std::vector<uint64_t> backup = h->kstate;
@@ -266,7 +268,7 @@ static int timers(nfh* h, int64_t now) {
                 HostSink sink;
                 uint32_t rank = 0;
                 for (size_t i = 0; i < cs.size(); i++) {
-                    if (i && cs[i].t == cs[i - 1].t) continue;
+                    if (i && cs[i].t == cs[i - 1].t && !wall) continue;
                     NfLane<HostSink> L = make_lane(h, &C, &sink, cs[i].key);
                     L.Q = &Q;
                     L.qb = L.kb + Q.q_off;
@@ -352,8 +354,42 @@ int nfh_start(nfh* h) {
     return L.err ? -5 : 0;
 }
 
+// earliest queued notify time over every scheduler and key
+static int64_t next_due(nfh* h) {
+    int64_t tmin = INT64_MAX;
+    if (!h->T.has_absent) return tmin;
+    nf_cols C = host_cols(h);
+    for (int q = 0; q < h->T.n_queries; q++) {
+        const nf_query& Q = h->T.q[q];
+        for (int p = 0; p < Q.n_proc; p++) {
+            if (Q.proc[p].kind != NF_K_ABSENT) continue;
+            for (int32_t k = 0; k < h->nkeys; k++) {
+                NfLane<HostSink> L = make_lane(h, &C, nullptr, k);
+                L.Q = &Q;
+                L.qb = L.kb + Q.q_off;
+                int64_t t;
+                if (!(L.sched(p)[1] >> 63) && h->T.partitioned) continue;
+                if (L.sched_head(p, &t)) tmin = std::min(tmin, t);
+            }
+        }
+    }
+    return tmin;
+}
+
 int nfh_advance_time(nfh* h, int64_t now) {
     if (now < h->clock) return 0;
+    if (!h->T.playback) {
+        // wall clock: step through every queued notify time
+        for (;;) {
+            const int64_t t = next_due(h);
+            if (t > now) break;
+            h->clock = std::max(h->clock, t);
+            const int rc = timers(h, h->clock, true);
+            if (rc) return rc;
+        }
+        h->clock = now;
+        return 0;
+    }
     h->clock = now;
     return timers(h, now);
 }

@@ -7,7 +7,7 @@ due time, Scheduler.java:74-99), so parity is checked on whole streams, never on
 key subsets."""
 import pytest
 
-from c4_cases import run_c4, same_output
+from c4_cases import CollidingNames, run_c4, same_output, ties
 from oracle_engine import OracleEngine
 
 pytestmark = pytest.mark.gpu
@@ -32,3 +32,34 @@ def test_c4_streaming_vs_oracle(users, seconds):
     eng.close()
     assert len(ref["seq"]) > 0
     assert same_output(got, ref), (len(got["seq"]), len(ref["seq"]))
+
+
+def test_c4_ties_follow_map_order_on_gpu():
+    """>= 1,000 users share due milliseconds: the device picks one key per due
+    time in java.util.HashMap order (the product's order model, sh_jmap.h)"""
+    from siddhi_amd import compiler, synth
+    from siddhi_amd._native import HipEngine
+    c = compiler.compile_app(synth.C4_QUERY)
+    blocks = synth.c4_stream(5_000, seconds=5)
+    assert ties(blocks) > 100
+    ref = run_c4(OracleEngine(c), blocks)
+    eng = HipEngine(c)
+    got = run_c4(eng, blocks)
+    eng.close()
+    assert len(ref["seq"]) > 1000
+    assert same_output(got, ref)
+
+
+def test_c4_colliding_names_on_gpu():
+    """user names sharing String.hashCode: treeified bins, compareTo order"""
+    from siddhi_amd import compiler, synth
+    from siddhi_amd._native import HipEngine
+    n = 2000
+    c = compiler.compile_app(synth.C4_QUERY)
+    blocks = synth.c4_stream(n, seconds=10)
+    ref = run_c4(CollidingNames(OracleEngine(c), n), blocks)
+    eng = HipEngine(c)
+    got = run_c4(CollidingNames(eng, n), blocks)
+    eng.close()
+    assert len(ref["seq"]) > 500
+    assert same_output(got, ref)

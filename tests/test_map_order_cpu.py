@@ -13,10 +13,9 @@ cross-key tie."""
 import os
 import subprocess
 
-import numpy as np
 import pytest
 
-from c4_cases import run_c4, same_output
+from c4_cases import CollidingNames, run_c4, same_output, ties
 from nfa_host_engine import NfaHostEngine
 from oracle_engine import OracleEngine
 from siddhi_amd import compiler, javastr, synth
@@ -38,52 +37,23 @@ def test_java_string_hash_known_values():
     assert javastr.java_string_hash("polygenelubricants") == -2147483648
 
 
-def _ties(blocks):
-    """due milliseconds shared by more than one user (fired one per call)"""
-    due = {}
-    for st, ts, cols, keys in blocks:
-        if st == 1:
-            for t in np.unique(ts):
-                due[int(t)] = due.get(int(t), 0) + int((ts == t).sum())
-    return sum(1 for v in due.values() if v > 1)
-
-
 @pytest.mark.parametrize("users,seconds", [(5_000, 5), (2_000, 10)])
 def test_c4_ties_follow_map_order(users, seconds):
     c = compiler.compile_app(synth.C4_QUERY)
     blocks = synth.c4_stream(users, seconds=seconds)
-    assert _ties(blocks) > 100
+    assert ties(blocks) > 100
     ref = run_c4(OracleEngine(c), blocks)
     got = run_c4(NfaHostEngine(c), blocks)
     assert len(ref["seq"]) > 1000
     assert same_output(got, ref)
 
 
-class _CollidingNames:
-    """engine wrapper registering user names built from "Aa"/"BB" blocks, which
-    all share one String.hashCode per length: bins overflow into trees"""
-
-    def __init__(self, eng, n):
-        self.eng = eng
-        names = []
-        for u in range(n):
-            bits = format(u, "014b")
-            names.append("".join("Aa" if b == "0" else "BB" for b in bits[-9:]) + str(u // 512))
-        self.utf16, self.offs = javastr.pack_utf16(names)
-
-    def set_partition_keys(self, first, strings=None, utf16=None, offsets=None):
-        self.eng.set_partition_keys(0, utf16=self.utf16, offsets=self.offs)
-
-    def __getattr__(self, name):
-        return getattr(self.eng, name)
-
-
 def test_c4_colliding_names_follow_map_order():
     n = 2000
     c = compiler.compile_app(synth.C4_QUERY)
     blocks = synth.c4_stream(n, seconds=10)
-    ref = run_c4(_CollidingNames(OracleEngine(c), n), blocks)
-    got = run_c4(_CollidingNames(NfaHostEngine(c), n), blocks)
+    ref = run_c4(CollidingNames(OracleEngine(c), n), blocks)
+    got = run_c4(CollidingNames(NfaHostEngine(c), n), blocks)
     assert len(ref["seq"]) > 500
     assert same_output(got, ref)
 
