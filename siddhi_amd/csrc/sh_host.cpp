@@ -723,7 +723,7 @@ static int compile_nfa(sh_handle* h, const sh_app_desc* app) {
         std::vector<int> ids;
         for (int q = 0; q < T->n_queries; q++)
             for (int p = 0; p < T->q[q].n_proc; p++)
-                if (T->q[q].proc[p].kind == NF_K_ABSENT) ids.push_back(q * NF_MAX_PROC + p);
+                if (nf_has_sched(T->q[q].proc[p])) ids.push_back(q * NF_MAX_PROC + p);
         h->sm_on = true;
         h->sm.init(ids, NF_MAX_QUERIES * NF_MAX_PROC);
         h->n_rank.resize(NF_MAX_QUERIES * NF_MAX_PROC);
@@ -1485,8 +1485,8 @@ static int nf_next_due(sh_handle* h, int64_t* out) {
     if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand)) || h->n_tmin.ensure_fresh(8))
         return fail(h, SH_E_OOM, "candidates");
     for (int q = 0; q < h->T->n_queries; q++) {
-        for (int p = 0; p < h->T->q[q].n_proc; p++) {
-            if (h->T->q[q].proc[p].kind != NF_K_ABSENT) continue;
+        for (int si = 0; si < h->T->q[q].n_sched; si++) {
+            const int p = h->T->q[q].sched_seq[si];
             hipMemsetAsync(h->n_ctr.p, 0, 8, st);
             nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, INT64_MAX,
                     h->n_cand.as<nfd_cand>(), h->n_ctr.as<unsigned long long>(), nkeys, nullptr, 0, nullptr, st);
@@ -1513,10 +1513,11 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
     nf_put_cols(h, nf_store_cols(h));
     int n_absent = 0;  // a key's armed flag may be cleared only when it has one scheduler
     for (int q = 0; q < h->T->n_queries; q++)
-        for (int p = 0; p < h->T->q[q].n_proc; p++) n_absent += h->T->q[q].proc[p].kind == NF_K_ABSENT;
+        for (int p = 0; p < h->T->q[q].n_proc; p++) n_absent += nf_has_sched(h->T->q[q].proc[p]);
     for (int q = 0; q < h->T->n_queries; q++) {
-        for (int p = 0; p < h->T->q[q].n_proc; p++) {
-            if (h->T->q[q].proc[p].kind != NF_K_ABSENT) continue;
+        // Scheduler creation order (the TimestampGenerator's listener order)
+        for (int si = 0; si < h->T->q[q].n_sched; si++) {
+            const int p = h->T->q[q].sched_seq[si];
             const int32_t nkeys = h->n_nkeys;
             // due keys
             if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");

@@ -70,11 +70,16 @@ struct nf_proc {
     int8_t next_every_pre;  // post.nextEveryStatePreProcessor, -1
     int8_t callback_pre;    // post.callbackPreStateProcessor (a CountPre), -1
     int8_t to_selector;     // post.nextProcessor is the QuerySelector
-    int8_t pad;
+    int8_t absent_logical;  // Logical: AbsentLogicalPre/PostStateProcessor (own scheduler)
     int32_t min_count, max_count;
-    int64_t waiting;        // Absent: waitingTime (ms)
+    int64_t waiting;        // Absent / absent logical: waitingTime (ms), -1: no `for`
     int32_t filter_pc, filter_len;  // FilterProcessor between pre and post (-1: none)
 };
+
+// the pre owns a Scheduler (AbsentStreamPre / AbsentLogicalPre)
+NF_INL bool nf_has_sched(const nf_proc& P) {
+    return P.kind == NF_K_ABSENT || (P.kind == NF_K_LOGICAL && P.absent_logical);
+}
 
 // Per stream: the ProcessStreamReceiver of this query (StateInputStreamParser.java:91-110)
 struct nf_receiver {
@@ -116,6 +121,8 @@ struct nf_query {
     int32_t n_start;
     int32_t n_init, n_reset, n_update;
     int32_t n_startup;      // startup absent pres (partitionCreated)
+    int32_t n_sched;        // scheduler-owning pres, in Scheduler creation order
+    int8_t sched_seq[NF_MAX_PROC];
     int8_t start_ids[NF_MAX_PROC];
     int8_t init_seq[NF_MAX_SEQ];
     int8_t reset_seq[NF_MAX_SEQ];
@@ -374,6 +381,9 @@ NF_INL NfVal nf_arith(int aop, int rt, const NfVal& l, const NfVal& r) {
 // [1] output timestamp, [2] null mask (low 32) | query << 32, [3] trigger seq,
 // [4..] raw output values.
 #define NF_REC_HDR 4
+// row of an empty StreamEvent (`new StreamEvent()` added by an absent logical
+// state): every attribute reads as null
+#define NF_ROW_NULL 0x7FFFFFFFu
 
 // errors raised by a lane (the host grows the named capacity and replays)
 enum nf_err {
@@ -561,7 +571,8 @@ struct NfLane {
         if (!partitioned) return;
         const int32_t u = ps_use(p) - 1;
         ps_set_use(p, u);
-        if (u == 0 && cur(p)[0] == 0 && lcount(p, 0) == 0 && lcount(p, 1) == 0 && !ps_flag(p, NF_PS_INIT))
+        if (u == 0 && cur(p)[0] == 0 && lcount(p, 0) == 0 && lcount(p, 1) == 0 && !ps_flag(p, NF_PS_INIT) &&
+            !(Q->proc[p].absent_logical && pst(p)[0] != 0))
             ps_setf(p, NF_PS_ALIVE, false);  // canDestroy -> destroyed
     }
 
@@ -716,9 +727,14 @@ struct NfLane {
                     } else {
                         const int strm = Q->slot_stream[in.a];
                         const uint32_t row = nd_row(n);
-                        const uint8_t* nm = C->nul[strm][in.b];
-                        v.null = nm ? nm[row] : 0;
-                        v.b = load_attr(strm, in.b, in.c, row);
+                        if (row == NF_ROW_NULL) {
+                            v.null = 1;
+                            v.b = 0;
+                        } else {
+                            const uint8_t* nm = C->nul[strm][in.b];
+                            v.null = nm ? nm[row] : 0;
+                            v.b = load_attr(strm, in.b, in.c, row);
+                        }
                     }
                     st[sp++] = v;
                     break;
@@ -829,8 +845,9 @@ struct NfLane {
     }
     NF_HD bool next_is_absent(int p) const {
         const int np = Q->proc[p].next_pre;
-        return np >= 0 && Q->proc[np].kind == NF_K_ABSENT;
+        return np >= 0 && nf_has_sched(Q->proc[np]);
     }
+    NF_HD bool is_alog(int p) const { return p >= 0 && Q->proc[p].kind == NF_K_LOGICAL && Q->proc[p].absent_logical; }
     // StreamPreStateProcessor.init (:178-194)
     NF_HD void init(int p) {
         const nf_proc& P = Q->proc[p];
@@ -893,6 +910,8 @@ struct NfLane {
                     }
                     break;
                 case NF_K_LOGICAL:
+                    // AbsentLogicalPreStateProcessor.addState (:78-98): inactive -> no-op
+                    if (P.absent_logical && ps_flag(p, NF_PS_INACTIVE)) break;
                     // LogicalPreStateProcessor.addState (:43-66)
                     if (P.is_start || Q->state_type == SH_SEQUENCE) {
                         if (lcount(p, 1) == 0) lpush(p, 1, s);
@@ -900,6 +919,10 @@ struct NfLane {
                     } else {
                         lpush(p, 1, s);
                         if (P.partner >= 0) add_to_nae(P.partner, s);
+                    }
+                    if (P.absent_logical && !P.is_start && P.waiting != -1) {
+                        notify_at(p, se_ts(s) + P.waiting);
+                        if (is_alog(P.partner)) notify_at(P.partner, se_ts(s) + Q->proc[P.partner].waiting);
                     }
                     break;
                 case NF_K_ABSENT:
@@ -951,6 +974,19 @@ struct NfLane {
         uint32_t c = copy_se(src);
         if (!c) return;
         se_set_type(c, NF_CURRENT);
+        if (P.absent_logical) {
+            // AbsentLogicalPreStateProcessor.addEveryState (:100-118): the last
+            // arrived event's time, only this slot and the partner's cleared
+            const uint32_t n = se_ev(c, p);
+            if (n) se_set_ts(c, nd_ts(n));
+            se_set_ev(c, p, 0);
+            se_set_ev(c, P.partner, 0);
+            pget(p);
+            lpush(p, 1, c);
+            add_to_nae(P.partner, c);
+            pret(p);
+            return;
+        }
         for (int i = p; i < Q->n_proc; i++) se_set_ev(c, i, 0);
         pget(p);
         lpush(p, 1, c);
@@ -1145,9 +1181,20 @@ struct NfLane {
                 break;
             }
             case NF_K_LOGICAL: {
+                if (P.absent_logical) {
+                    // AbsentLogicalPostStateProcessor.process (:37-49): the absent
+                    // event arrived
+                    state_changed(p);
+                    set_returned(p, true);
+                    pget(p);
+                    pst(p)[0] = (uint64_t)nd_ts(se_ev(s, p));  // updateLastArrivalTime
+                    pret(p);
+                    break;
+                }
                 // LogicalPostStateProcessor.process (:59-87)
                 if (P.logical_type == SH_E_LOGICAL_AND) {
-                    if (se_ev(s, P.partner))
+                    const bool go = is_alog(P.partner) ? partner_can_proceed(P.partner, s) : se_ev(s, P.partner) != 0;
+                    if (go)
                         stream_post(p, s, c);
                     else
                         state_changed(p);
@@ -1179,6 +1226,7 @@ struct NfLane {
     // returns the chunk of returned StateEvents (first id, linked through next)
     NF_HD uint32_t process_and_return(int p, int64_t ts, uint32_t row) {
         const nf_proc& P = Q->proc[p];
+        if (P.absent_logical) return alog_process_and_return(p, ts, row);
         uint32_t ret[4] = {0, 0, 0, 0};
         pget(p);
         if (P.kind == NF_K_ABSENT && ps_flag(p, NF_PS_INACTIVE)) {
@@ -1513,7 +1561,7 @@ struct NfLane {
             ps_setf(p, NF_PS_STARTED, true);
             if (P.is_start && P.waiting != -1 && !ps_flag(p, NF_PS_INACTIVE)) {
                 const int64_t t = clock + P.waiting;
-                pst(p)[0] = (uint64_t)t;
+                if (!P.absent_logical) pst(p)[0] = (uint64_t)t;  // AbsentLogical (:333-351): no lastArrivalTime
                 notify_at(p, t);
             }
         }
@@ -1523,6 +1571,10 @@ struct NfLane {
     // at `now` (:150-227)
     NF_HD void process_timer(int p, int64_t now) {
         const nf_proc& P = Q->proc[p];
+        if (P.absent_logical) {
+            alog_process_timer(p, now);
+            return;
+        }
         pget(p);
         if (ps_flag(p, NF_PS_INACTIVE)) {
             pret(p);
@@ -1586,6 +1638,191 @@ struct NfLane {
             ps_setf(p, NF_PS_INACTIVE, true);
         if (P.callback_pre >= 0) start_state_reset(P.callback_pre);
     }
+    // ---------------------------------------------------------- absent logical
+    // AbsentLogicalPreStateProcessor (query/input/stream/state/
+    // AbsentLogicalPreStateProcessor.java): a LogicalPre whose element is `not S
+    // [for T]`; its state word 0 is lastArrivalTime, INACTIVE is !active.
+    // StateEvent.addEvent(slot, new StreamEvent()) (StateEvent.java:212-222)
+    NF_HD void add_empty_event(uint32_t s, int slot) {
+        const uint32_t ne = new_node(-1, NF_ROW_NULL);
+        if (!ne) return;
+        uint32_t h = se_ev(s, slot);
+        if (!h) {
+            se_set_ev(s, slot, ne);
+            return;
+        }
+        while (nd_next(h)) h = nd_next(h);
+        nd_set_next(h, ne);
+    }
+    // :220-228
+    NF_HD bool alog_waiting_passed(int p, int64_t now, uint32_t s) const {
+        const uint32_t n = se_ev(s, p);
+        if (!n) return now >= se_ts(s) + Q->proc[p].waiting;
+        return now >= nd_ts(n) + Q->proc[p].waiting;  // re-added by `every`
+    }
+    // :120-209 (a TIMER event at `now`)
+    NF_HD void alog_process_timer(int p, int64_t now) {
+        const nf_proc& P = Q->proc[p];
+        pget(p);
+        if (ps_flag(p, NF_PS_INACTIVE)) {
+            pret(p);
+            return;
+        }
+        bool not_processed = true;
+        if (now >= (int64_t)pst(p)[0] + P.waiting) {
+            if (P.is_start && Q->state_type == SH_SEQUENCE && lcount(p, 1) == 0 && lcount(p, 0) == 0) {
+                uint32_t s = new_se();
+                if (s) add_state(p, s);
+            } else if (Q->state_type == SH_SEQUENCE && lcount(p, 1) != 0) {
+                reset_state(p);
+            }
+            update_state(p);
+            uint32_t retc[4] = {0, 0, 0, 0};
+            uint32_t expired = 0;
+            uint32_t* pl = list(p, 0);
+            for (uint32_t i = 0; i < lcount(p, 0);) {
+                const uint32_t ev = pl[i];
+                if (is_expired(ev, now)) {
+                    expired = ev;
+                    lerase(p, 0, i);
+                    continue;
+                }
+                if (alog_waiting_passed(p, now, ev)) {
+                    lerase(p, 0, i);
+                    const bool partner_in = se_ev(ev, P.partner) != 0;
+                    if (P.logical_type == SH_E_LOGICAL_OR && !partner_in) {
+                        add_empty_event(ev, p);  // OR: the partner never arrived
+                        ch_add(retc, ev);
+                    } else if (P.logical_type == SH_E_LOGICAL_AND && partner_in) {
+                        ch_add(retc, ev);  // AND: the partner arrived but could not send out
+                    } else if (P.logical_type == SH_E_LOGICAL_AND) {
+                        add_empty_event(ev, p);  // AND: the partner may proceed later
+                    }
+                    continue;
+                }
+                i++;
+            }
+            if (expired && P.within_every >= 0) {
+                add_every_state(P.within_every, expired);
+                update_state(P.within_every);
+            }
+            ch_reset(retc);
+            not_processed = retc[0] == 0;
+            while (ch_has_next(retc)) {
+                const uint32_t s = ch_next(retc);
+                ch_remove(retc);
+                se_set_ts(s, now);
+                alog_send(p, s);
+            }
+            pst(p)[0] = 0;
+        }
+        if (P.next_every_pre >= 0 || (not_processed && P.is_start)) {
+            // every, or an unanswered start state: wait again
+            const int64_t lat = (int64_t)pst(p)[0];
+            notify_at(p, lat == 0 ? clock + P.waiting : lat + P.waiting);
+        }
+        pret(p);
+    }
+    // :230-251
+    NF_HD void alog_send(int p, uint32_t s) {
+        const nf_proc& P = Q->proc[p];
+        if (P.to_selector) {
+            uint32_t c[4] = {s, s, 0, 0};
+            selector_process(c);
+        }
+        if (P.next_pre >= 0) add_state(P.next_pre, s);
+        if (P.next_every_pre >= 0) {
+            add_every_state(P.next_every_pre, s);
+        } else if (P.is_start) {
+            ps_setf(p, NF_PS_INACTIVE, true);
+            if (P.logical_type == SH_E_LOGICAL_OR && is_alog(P.partner)) {
+                pget(P.partner);
+                ps_setf(P.partner, NF_PS_INACTIVE, true);  // setActive(false)
+                pret(P.partner);
+            }
+        }
+        if (P.callback_pre >= 0) start_state_reset(P.callback_pre);
+    }
+    // :262-320 (returns an empty chunk)
+    NF_HD uint32_t alog_process_and_return(int p, int64_t ts, uint32_t row) {
+        const nf_proc& P = Q->proc[p];
+        pget(p);
+        if (ps_flag(p, NF_PS_INACTIVE)) {
+            pret(p);
+            return 0;
+        }
+        uint32_t* pl = list(p, 0);
+        for (uint32_t i = 0; i < lcount(p, 0);) {
+            const uint32_t s = pl[i];
+            if (P.logical_type == SH_E_LOGICAL_OR && se_ev(s, P.partner)) {
+                lerase(p, 0, i);
+                continue;
+            }
+            const uint32_t cur_ev = se_ev(s, p);
+            const uint32_t ne = new_node(ts, row);
+            if (!ne) break;
+            se_set_ev(s, p, ne);
+            process_se(p, s);
+            if (P.waiting != -1 ||
+                (Q->state_type == SH_SEQUENCE && P.logical_type == SH_E_LOGICAL_AND && P.next_every_pre >= 0))
+                se_set_ev(s, p, cur_ev);  // back to the original state
+            bool erased = false;
+            const int tl = P.this_last;
+            if (returned(tl)) {
+                // passed the filter: no longer an absence candidate
+                set_returned(tl, false);
+                lerase(p, 0, i);
+                erased = true;
+                if (Q->state_type == SH_SEQUENCE) {
+                    pget(P.partner);
+                    const uint32_t n = lcount(P.partner, 0);
+                    const uint32_t* ql = list(P.partner, 0);
+                    for (uint32_t k = 0; k < n; k++) {
+                        if (ql[k] == s) {
+                            lerase(P.partner, 0, k);
+                            break;
+                        }
+                    }
+                    pret(P.partner);
+                }
+            }
+            if (!ps_flag(p, NF_PS_CHANGED)) {
+                se_set_ev(s, p, cur_ev);
+                if (Q->state_type == SH_SEQUENCE && !erased) {
+                    lerase(p, 0, i);
+                    erased = true;
+                }
+            }
+            if (!erased) i++;
+        }
+        pret(p);
+        return 0;
+    }
+    // :353-388, asked by the partner's LogicalPostStateProcessor (AND)
+    NF_HD bool partner_can_proceed(int p, uint32_t s) {
+        const nf_proc& P = Q->proc[p];
+        pget(p);
+        bool go;
+        if (Q->state_type == SH_SEQUENCE && P.next_every_pre < 0 && (int64_t)pst(p)[0] > 0) {
+            go = false;
+        } else if (P.waiting == -1) {
+            // no `for`: proceed while this absent state has not seen its event
+            if (P.next_every_pre < 0) {
+                go = se_ev(s, p) == 0;
+            } else if ((int64_t)pst(p)[0] > 0) {
+                go = false;
+                pst(p)[0] = 0;
+                init(p);
+            } else {
+                go = true;
+            }
+        } else {
+            go = se_ev(s, p) != 0;
+        }
+        pret(p);
+        return go;
+    }
+
     // Scheduler.sendTimerEvents for this key (Scheduler.java:171-206): every queued
     // notification <= now, in FIFO order
     NF_HD void send_timer_events(int p, int64_t now) {

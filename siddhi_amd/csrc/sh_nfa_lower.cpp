@@ -40,6 +40,7 @@ struct LProc {
     int minc = 0, maxc = 0;
     int64_t waiting = -1;
     int filter = -1;
+    bool alog = false;   // AbsentLogicalPreStateProcessor (a Logical pre with its own scheduler)
 };
 
 struct LInner {
@@ -59,7 +60,8 @@ struct QueryLowering {
     std::vector<LProc> procs;
     std::vector<std::unique_ptr<LInner>> inners;
     std::vector<int> pres;       // parse order
-    std::vector<int> startup;    // absent pres
+    std::vector<int> startup;    // absent pres (partitionCreated order)
+    std::vector<int> schedOrder; // scheduler-owning pres in Scheduler creation order
     int slotCounter = 0;
     std::map<int, int> uses;     // stream -> states fed
 
@@ -111,12 +113,12 @@ struct QueryLowering {
                         pre = newProc(NF_K_ABSENT);
                         procs[pre].waiting = e.waiting_ms;
                         startup.push_back(pre);
+                        schedOrder.push_back(pre);
                     } else {
                         pre = newProc(NF_K_STREAM);
                     }
-                } else if (e.kind == SH_E_ABSENT_STREAM) {
-                    err = "device engine: absent states inside count / logical (AbsentLogicalPreStateProcessor) "
-                          "are not lowered";
+                } else if (e.kind == SH_E_ABSENT_STREAM && !procs[pre].alog) {
+                    err = "device engine: absent states inside counts are not lowered";
                     return nullptr;
                 }
                 LProc& P = procs[pre];
@@ -171,12 +173,19 @@ struct QueryLowering {
                 }
                 const sh_state_elem& e1 = q->elems[e.child0];
                 const sh_state_elem& e2 = q->elems[e.child1];
-                if (e1.kind == SH_E_ABSENT_STREAM || e2.kind == SH_E_ABSENT_STREAM) {
-                    err = "device engine: logical absent states (AbsentLogicalPreStateProcessor) are not lowered";
-                    return nullptr;
-                }
+                // an absent element gets AbsentLogicalPre/Post and its own scheduler,
+                // element 1's first (StateInputStreamParser.java:289-344)
                 const int p1 = newProc(NF_K_LOGICAL);
                 const int p2 = newProc(NF_K_LOGICAL);
+                const int pe[2] = {p1, p2};
+                const sh_state_elem* ee[2] = {&e1, &e2};
+                for (int k = 0; k < 2; k++) {
+                    if (ee[k]->kind != SH_E_ABSENT_STREAM) continue;
+                    procs[pe[k]].alog = true;
+                    procs[pe[k]].waiting = ee[k]->waiting_ms;
+                    startup.push_back(pe[k]);
+                    schedOrder.push_back(pe[k]);
+                }
                 procs[p1].ltype = procs[p2].ltype = e.kind;
                 procs[p1].partner = p2;
                 procs[p2].partner = p1;
@@ -442,6 +451,8 @@ struct QueryLowering {
         for (size_t i = 0; i < seq.size(); i++) Q->update_seq[i] = (int8_t)S(seq[i]);
         Q->n_startup = (int)startup.size();
         for (size_t i = 0; i < startup.size(); i++) Q->startup[i] = (int8_t)S(startup[i]);
+        Q->n_sched = (int)schedOrder.size();
+        for (size_t i = 0; i < schedOrder.size(); i++) Q->sched_seq[i] = (int8_t)S(schedOrder[i]);
         Q->n_proc = (int)procs.size();
         for (auto& P : procs) {
             nf_proc& D = Q->proc[P.stateId];
@@ -459,6 +470,7 @@ struct QueryLowering {
             D.min_count = P.minc;
             D.max_count = P.maxc;
             D.waiting = P.waiting;
+            D.absent_logical = P.alog;
             Q->slot_stream[P.stateId] = (int8_t)P.stream;
             if (P.filter >= 0) {
                 D.filter_pc = T->n_code;
@@ -549,7 +561,7 @@ int nf_lower(const sh_app_desc* app, nf_table* T, std::string* err) {
         }
         for (int p = 0; p < T->q[i].n_proc; p++) {
             const nf_proc& P = T->q[i].proc[p];
-            if (P.kind == NF_K_ABSENT) T->has_absent = 1;
+            if (nf_has_sched(P)) T->has_absent = 1;
             // CountPreStateProcessor.addState with minCount 0 raises the final count
             // post's isEventReturned outside that state's own processing; the flag is
             // consumed by whichever partition key processes the state next, so the

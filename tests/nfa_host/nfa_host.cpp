@@ -239,8 +239,8 @@ static int timers(nfh* h, int64_t now, bool wall = false) {
         nf_cols C = host_cols(h);
         for (int q = 0; q < h->T.n_queries && !err; q++) {
             const nf_query& Q = h->T.q[q];
-            for (int p = 0; p < Q.n_proc && !err; p++) {
-                if (Q.proc[p].kind != NF_K_ABSENT) continue;
+            for (int si = 0; si < Q.n_sched && !err; si++) {
+                const int p = Q.sched_seq[si];
                 // due keys: head <= now; one key per distinct due time (TreeMultimap
                 // with a zero comparator), the earliest-registered wins
                 struct Cand {
@@ -322,7 +322,7 @@ nfh* nfh_create(const sh_app_desc* d, char* err, int errlen) {
         std::vector<int> ids;
         for (int q = 0; q < h->T.n_queries; q++)
             for (int p = 0; p < h->T.q[q].n_proc; p++)
-                if (h->T.q[q].proc[p].kind == NF_K_ABSENT) ids.push_back(q * NF_MAX_PROC + p);
+                if (nf_has_sched(h->T.q[q].proc[p])) ids.push_back(q * NF_MAX_PROC + p);
         h->sm_on = true;
         h->sm.init(ids, NF_MAX_QUERIES * NF_MAX_PROC);
     }
@@ -361,8 +361,8 @@ static int64_t next_due(nfh* h) {
     nf_cols C = host_cols(h);
     for (int q = 0; q < h->T.n_queries; q++) {
         const nf_query& Q = h->T.q[q];
-        for (int p = 0; p < Q.n_proc; p++) {
-            if (Q.proc[p].kind != NF_K_ABSENT) continue;
+        for (int si = 0; si < Q.n_sched; si++) {
+            const int p = Q.sched_seq[si];
             for (int32_t k = 0; k < h->nkeys; k++) {
                 NfLane<HostSink> L = make_lane(h, &C, nullptr, k);
                 L.Q = &Q;

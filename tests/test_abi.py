@@ -49,16 +49,18 @@ def test_c2_query_lowers(lib):
     "@app:playback define stream L (u string, ip int); define stream T (u string, amt float); "
     "define stream O (u string); partition with (u of L, u of T, u of O) begin "
     "from (e1=L and e2=T) -> not O for 5 sec select e1.u as u, e2.amt as a insert into A; end;",
+    "define stream S (a int); define stream T (a int); from e1=S and not T for 1 sec select e1.a as a insert into O;",
+    "define stream S (a int); define stream T (a int); from every (not S for 1 sec or not T for 2 sec) -> e3=S "
+    "select e3.a as a insert into O;",
 ])
 def test_general_engine_lowers(lib, text):
+    """includes AbsentLogicalPreStateProcessor (`A and not B for T`)"""
     rc, h, _ = _compile(lib, text)
     assert rc == abi.SH_OK, lib.sh_last_error(h)
     lib.sh_destroy(h)
 
 
 @pytest.mark.parametrize("text", [
-    # AbsentLogicalPreStateProcessor (`A and not B for T`) is not lowered
-    "define stream S (a int); define stream T (a int); from e1=S and not T for 1 sec select e1.a as a insert into O;",
     # a final min-0 count inside a partition hands isEventReturned across keys
     "define stream S (k int, a int); partition with (k of S) begin "
     "from every e1=S -> e2=S[a > e1.a]<0:2> select e1.a as a insert into O; end;",

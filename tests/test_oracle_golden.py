@@ -12,19 +12,7 @@ from oracle_engine import OracleEngine
 
 FIXTURES = load_fixtures()
 
-# Known oracle gaps (tracked in DESIGN.md "parity status"):
-#  - AbsentLogicalPreStateProcessor (`A and not B for T` …) is not restated yet
-#  - wall-clock `every not X for T` timer re-arming is modelled in event time; the
-#    reference's ScheduledExecutorService timing differs for these tests
-KNOWN_GAPS = {
-    "AbsentPatternTestCase.testQueryAbsent6",
-    "EveryAbsentPatternTestCase.testQueryAbsent1",
-    "EveryAbsentPatternTestCase.testQueryAbsent7",
-    "EveryAbsentPatternTestCase.testQueryAbsent13",
-    "EveryAbsentPatternTestCase.testQueryAbsent14",
-    "EveryAbsentPatternTestCase.testQueryAbsent22",
-    "AbsentWithEveryPatternTestCase.testQuery8",
-}
+KNOWN_GAPS = set()
 
 
 @pytest.mark.parametrize("fx", FIXTURES, ids=[f["id"] for f in FIXTURES])
