@@ -12,10 +12,14 @@ A step = one full pass of the matcher over the 100M events from fresh per-key
 state (radix segment -> per-key NFA advance -> ordered match placement), with
 the ordered match stream written to HBM.
 
-Multi-GPU (torchrun): one process per GPU, weak scaling: each rank owns a
-disjoint symbol range (its own 100M-event stream); partitions never cross
-ranks, so there is no data-path collective. value = all ranks' events / the
-max-over-ranks step time.
+Multi-GPU (torchrun, C2): one process per GPU, strong scaling over ONE
+100M-event stream. Every rank ingests an arrival-contiguous slice; a step
+routes the slice's events to the ranks owning their symbols (mix32(key) %
+world, one RCCL all-to-all of packed records), runs the matcher on the owned
+events, sends every match row back to the rank holding its trigger event (a
+second all-to-all) and k-way merges the runs by trigger sequence
+(siddhi_amd/shard.py, include/siddhi_shard.h). value = the stream's events /
+the max-over-ranks step time. Other configs at N > 1: independent replicas.
 """
 import argparse
 import json
@@ -38,12 +42,22 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2_000_000,
                     help="events of the same workload timed on the CPU oracle (0 = skip)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
-                    help="c2 (default, BASELINE.json configs[1]); c3 / c4 / c5 measure the other configs")
+    ap.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default="c2",
+                    help="c2 (default, BASELINE.json configs[1]); c1 / c3 / c4 / c5 measure the other configs")
     ap.add_argument("--seconds", type=int, default=100, help="c4: stream duration (playback seconds)")
     ap.add_argument("--c4-calls", type=int, default=0, help="c4: send only the first N calls (profiling; 0 = all)")
     ap.add_argument("--rules", type=int, default=1000, help="c5: rule count")
     args = ap.parse_args()
+    if args.config == "c1":
+        # BASELINE.json configs[0]: 10M ticks, 100 symbols, R = 1 ev/ms, no partition
+        if args.events == 100_000_000:
+            args.events = 10_000_000
+        if args.keys == 10_000:
+            args.keys = 100
+        if args.rate == 100:
+            args.rate = 1
+        if args.cpu_sample == 2_000_000:
+            args.cpu_sample = 300_000
     if args.config == "c5" and args.keys == 10_000:
         args.keys = 1_000_000
     if args.config == "c3" and args.keys == 10_000:
@@ -90,6 +104,27 @@ def workload(args, rank):
                  f"e2=Txn[card == e1.card and amount > e1.amount * F] within W sec`, one partition (card of Txn)",
             key_name="cards_per_gpu", bytes_note="event: ts 8 + card 4 + amount 4 + merchant 4 = 20 B; "
             "match: seq 8 + query 4 + card 4 + amount 4 = 20 B")
+    if args.config == "c1":
+        ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=1, seed=synth.SEED + 1 + 7919 * rank)
+        compiled = compiler.compile_app(synth.C1_QUERY)
+
+        def verify(oseq, ovals, oq):
+            sys.path.insert(0, os.path.join(HERE, "tests"))
+            from c2_check import c2_expected
+            eseq, evals = c2_expected(ts, keys, price, vol)
+            return bool(len(oseq) == len(eseq) and np.array_equal(oseq, eseq) and np.array_equal(ovals, evals))
+
+        def cpu(s):
+            sys.path.insert(0, os.path.join(HERE, "tests"))
+            from oracle_engine import run_columns_oracle
+            run_columns_oracle(compiled, ts[:s], [keys[:s], price[:s], vol[:s]], None, batch=4096)
+
+        return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, verify=verify, cpu=cpu,
+                    run_keys=np.zeros(n, np.int32), n_keys=1, b_event=24, b_match=28, cpu_sample=args.cpu_sample,
+                    desc="C1: every e1[price>20] -> e2[symbol==e1.symbol and price>e1.price] within 1 sec, "
+                         "no partition (BASELINE.json configs[0])", key_name="symbols_per_gpu",
+                    bytes_note="event: ts 8 + symbol 4 + price 4 + volume 8 = 24 B; "
+                               "match: seq 8 + symbol 4 + p1 4 + p2 4 + v2 8 = 28 B")
     ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=3 if args.config == "c3" else 2,
                                               seed=synth.SEED + (3 if args.config == "c3" else 2) + 7919 * rank)
     if args.config == "c3":
@@ -194,7 +229,8 @@ def main_c4(args, torch, dist, world, rank, dev):
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": tot * 1000.0 / args.steps, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic",
+            "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic", "nproc": os.cpu_count(),
+            "ingest": {"path": "host buffers of every send(Event[]) call cross PCIe inside the timed step"},
             "config": {"workload": "C4: (e1=Login and e2=Txn) -> not Logout for 5 sec, partition with (user of "
                                    "Login, user of Txn, user of Logout), @app:playback",
                        "events_per_gpu": n, "users_per_gpu": args.keys, "seconds": args.seconds,
@@ -207,6 +243,74 @@ def main_c4(args, torch, dist, world, rank, dev):
             "parity": "tests/test_gpu_c4.py (whole streams up to 400k users vs the oracle)"}))
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_sharded(args, torch, dist, world, rank, dev):
+    """C2 over `world` GPUs: one stream, key-sharded step (module docstring)."""
+    from siddhi_amd import compiler, shard, synth
+    from siddhi_amd.device_run import DeviceRunner
+    n, K = args.events, args.keys
+    log(f"rank {rank}: generating the C2 stream ({n} events, {K} symbols), slice {rank}/{world}")
+    ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=2, seed=synth.SEED + 2)
+    b = shard.slice_bounds(n, world)
+    lo, hi = b[rank], b[rank + 1]
+    d_ts = torch.from_numpy(ts[lo:hi].copy()).to(dev)
+    d_k = torch.from_numpy(keys[lo:hi].copy()).to(dev)
+    d_p = torch.from_numpy(price[lo:hi].copy()).to(dev)
+    d_v = torch.from_numpy(vol[lo:hi].copy()).to(dev)
+    compiled = compiler.compile_app(synth.C2_QUERY)
+    runner = DeviceRunner(compiled, device=str(dev))
+    stream = torch.cuda.current_stream(dev)
+    step = shard.KeyShardedStep(world, rank, shard.HipShardOps(str(dev)),
+                                lambda t, k, c, nk: runner.run(t, k, c, nk, stream=stream), n_out=4)
+
+    def one():
+        return step.run(d_ts, d_k, [d_k, d_p, d_v], lo, K, key_attr=0)
+
+    log("warmup")
+    for _ in range(args.warmup):
+        one()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        seq, vals = one()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    m_t = torch.tensor([int(seq.numel())], dtype=torch.int64, device=dev)
+    dist.all_reduce(m_t)
+    m = int(m_t.item())
+    verified = None
+    if not args.no_verify and rank == 0:
+        log("verifying rank 0's ordered rows against the vectorised restatement")
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        from c2_check import c2_expected
+        eseq, evals = c2_expected(ts, keys, price, vol)
+        sel = (eseq >= lo) & (eseq < hi)
+        verified = bool(np.array_equal(seq.cpu().numpy(), eseq[sel]) and np.array_equal(vals.cpu().numpy(), evals[sel]))
+    if rank == 0:
+        print(json.dumps({
+            "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
+            "value": n * args.steps / dt, "unit": "events/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt * 1000.0 / args.steps, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic",
+            "nproc": os.cpu_count(),
+            "config": {"workload": "C2: every e1[price>20] -> e2[symbol==e1.symbol and price>e1.price] within 1 "
+                                   "sec, partition with (symbol of StockStream); one stream split by symbol",
+                       "events_total": n, "symbols": K, "rate_ev_per_ms": args.rate, "matches_total": m,
+                       "parallelism": f"key-sharded x{world}: RCCL all-to-all route + return, k-way merge",
+                       "rank0_slice": [lo, hi], "rank0_step": step.last},
+            "roofline": None,
+            "cpu_baseline": None,
+            "verified_vs_restatement": verified}))
+    runner.close()
+    dist.destroy_process_group()
 
 
 def main():
@@ -223,6 +327,8 @@ def main():
     dev = torch.device(f"cuda:{local}")
     if args.config == "c4":
         return main_c4(args, torch, dist, world, rank, dev)
+    if args.config == "c2" and world > 1:
+        return main_sharded(args, torch, dist, world, rank, dev)
 
     from siddhi_amd.device_run import DeviceRunner
 
@@ -230,9 +336,17 @@ def main():
     log(f"generating {args.config} workload: {n} events, {K} keys")
     W = workload(args, rank)   # each rank: its own stream over its own key range (weak scaling)
     runner = DeviceRunner(W["compiled"], device=str(dev))
+    # host -> device ingest of the input columns (outside the timed region:
+    # the timed step starts from HBM-resident events)
+    torch.cuda.synchronize(dev)
+    t_in = time.perf_counter()
     t_ts = torch.from_numpy(W["ts"]).to(dev)
     cols = [torch.from_numpy(c).to(dev) for c in W["cols"]]
-    t_k = cols[0]
+    t_k = torch.from_numpy(W["run_keys"]).to(dev) if "run_keys" in W else cols[0]
+    torch.cuda.synchronize(dev)
+    ingest_s = time.perf_counter() - t_in
+    ingest_bytes = W["ts"].nbytes + sum(c.nbytes for c in W["cols"])
+    K = W.get("n_keys", K)
     stream = torch.cuda.current_stream(dev)
     with_q = args.config == "c5"
 
@@ -315,8 +429,14 @@ def main():
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic",
-            "config": {"workload": W["desc"], "events_per_gpu": n, W["key_name"]: K, "rate_ev_per_ms": args.rate,
+            # C2 at N > 1 splits the same 100M stream (main_sharded): strong
+            "scaling": "strong" if args.config in ("c1", "c2") else "weak",
+            "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic",
+            "nproc": os.cpu_count(),
+            "ingest": {"bytes": ingest_bytes, "ms": ingest_s * 1000.0, "GBps": ingest_bytes / ingest_s / 1e9,
+                       "path": "pageable host numpy -> HBM (torch .to), before the timed steps"},
+            "config": {"workload": W["desc"], "events_per_gpu": n, W["key_name"]: args.keys,
+                       "rate_ev_per_ms": args.rate,
                        "matches_per_gpu": int(m), "parallelism": f"key-sharded x{world}",
                        "bytes": W["bytes_note"]},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",

@@ -32,6 +32,7 @@
 
 #define BK_TPB 1024
 #define BK_ITEMS (SHB_TILE / BK_TPB)
+#define BK_ROWMAP 2048  // rows per 1,024-event block written row-parallel
 
 static_assert(BK_ITEMS == 16, "tile / threads");
 
@@ -222,6 +223,9 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
     __shared__ uint32_t S[SHB_TILE];
     __shared__ int32_t o_kind[SHB_MAX_OUT], o_type[SHB_MAX_OUT];
     __shared__ const void* o_src[SHB_MAX_OUT];
+    __shared__ uint16_t evmap[BK_ROWMAP];
+    __shared__ uint32_t blk_mpos[BK_TPB];
+    __shared__ uint32_t s_tot;
     const int T = blockIdx.x;
     const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
     const int tile_n = (int)((P.n - b0) < SHB_TILE ? (P.n - b0) : SHB_TILE);
@@ -303,15 +307,59 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
     shw_lds_excl_scan<BK_TPB, BK_ITEMS>(S, tile_n, ws);
     const uint32_t tb = P.ttot[T];
     const int no = O.n_out;
+    // the rows are written row-parallel, one 1,024-event block at a time: each
+    // event enters its rows into the block's row -> event map, then thread t
+    // writes row r0 + t (consecutive lanes, consecutive rows: coalesced)
+    {
+        const int l = tile_n - 1;
+        if (l >= 0 && (l & (BK_TPB - 1)) == (int)threadIdx.x) {
+            const uint32_t pl = pk[l / BK_TPB];
+            s_tot = S[l] + (pl == ~0u ? 0u : (pl >> 8) & 0xFFu);
+        }
+    }
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < BK_ITEMS; j++) {
-        if (pk[j] == ~0u) continue;
-        const uint32_t c = (pk[j] >> 8) & 0xFFu;
+        const int lb = j * BK_TPB;
+        if (lb >= tile_n) break;  // uniform
+        const int l = lb + threadIdx.x;
+        const uint32_t r0 = S[lb];
+        const uint32_t r1 = lb + BK_TPB < tile_n ? S[lb + BK_TPB] : s_tot;
+        const uint32_t R = r1 - r0;
+        const uint32_t c = pk[j] == ~0u ? 0u : (pk[j] >> 8) & 0xFFu;
+        if (R <= BK_ROWMAP) {
+            if (c) {
+                const uint32_t at = S[l] - r0;
+                for (uint32_t k = 0; k < c; k++) evmap[at + k] = (uint16_t)threadIdx.x;
+            }
+            blk_mpos[threadIdx.x] = mpos[j];
+            __syncthreads();
+            for (uint32_t t = threadIdx.x; t < R; t += BK_TPB) {
+                const int e = evmap[t];
+                const int le = lb + e;
+                const uint32_t k = r0 + t - S[le];
+                const int64_t i = b0 + le;
+                const int64_t row = (int64_t)tb + r0 + t;
+                if (row >= out_cap) continue;  // the host reports SH_E_MORE
+                if (out_seq) out_seq[row] = seq_base + (uint64_t)i;
+                if (!out_vals) continue;
+                // output descriptors straight from the kernel arguments (scalar
+                // registers: uniform branches)
+#pragma unroll
+                for (int o = 0; o < SHB_MAX_OUT; o++) {
+                    if (o >= no) break;
+                    out_vals[row * no + o] = O.kind[o] == 1 ? bk_raw(O.src[o], i, O.type[o])
+                                                            : bk_raw(O.src[o], (int64_t)blk_mpos[e] + k, O.type[o]);
+                }
+            }
+            __syncthreads();
+            continue;
+        }
+        // a dense block (more rows than the map holds): event-parallel writes
         if (!c) continue;
-        const int l = j * BK_TPB + threadIdx.x;
         const int64_t i = b0 + l;
         const int64_t row0 = (int64_t)tb + S[l];
-        if (row0 + c > out_cap) continue;  // the host reports SH_E_MORE
+        if (row0 + c > out_cap) continue;
         if (out_seq)
             for (uint32_t k = 0; k < c; k++) out_seq[row0 + k] = seq_base + (uint64_t)i;
         if (!out_vals) continue;

@@ -385,6 +385,10 @@ struct sh_handle {
     PinBuf pin_in, pin_rd, pin_out;
     DevBuf n_tmin, n_slot_s, n_slot_k;  // device tie-break of due keys
     DevBuf n_armed;                     // per key: may hold a scheduler entry (nf_cols.sched_armed)
+    // the armed-key list of the due pass (two buffers, swapped per pass; counts
+    // in n_klist_n[0..1]) and the log of keys armed since the last pass
+    DevBuf n_klist[2], n_klist_n, n_arm_log, n_arm_ctr;
+    int klist_cur = 0;
     // scheduler maps' iteration order (sh_jmap.h): host models fed by the
     // launches' getState history, per-key ranks uploaded for the due-key pick
     bool sm_on = false;
@@ -796,6 +800,11 @@ void sh_destroy(sh_handle* h) {
         h->pin_out.release();
         h->n_tmin.release();
         h->n_armed.release();
+        h->n_klist[0].release();
+        h->n_klist[1].release();
+        h->n_klist_n.release();
+        h->n_arm_log.release();
+        h->n_arm_ctr.release();
         h->n_slot_s.release();
         h->n_slot_k.release();
         h->v_sts.release();
@@ -1112,6 +1121,11 @@ static nf_cols nf_store_cols(sh_handle* h) {
             c.nul[s][a] = h->stores[s].has_nul[a] ? (const uint8_t*)h->stores[s].nuls[a].p : nullptr;
         }
     c.sched_armed = armed_flags(h);
+    if (c.sched_armed && h->n_arm_log.p) {
+        c.arm_log = h->n_arm_log.as<int32_t>();
+        c.arm_ctr = h->n_arm_ctr.as<unsigned long long>();
+        c.arm_cap = (uint64_t)h->n_nkeys;
+    }
     if (h->sm_on) {
         c.sev = h->n_sev.as<uint64_t>();
         c.sev_ctr = h->n_sev_ctr.as<unsigned long long>();
@@ -1130,6 +1144,14 @@ static int nf_ensure_keys(sh_handle* h, int32_t nkeys) {
     hipMemsetAsync((uint8_t*)h->n_kstate.p + old, 0, need - old, h->stream);
     if (h->n_armed.ensure((size_t)nk)) return SH_E_OOM;
     hipMemsetAsync((uint8_t*)h->n_armed.p + h->n_nkeys, 0, (size_t)(nk - h->n_nkeys), h->stream);
+    if (h->n_klist[0].ensure((size_t)nk * 4) || h->n_klist[1].ensure((size_t)nk * 4) ||
+        h->n_arm_log.ensure((size_t)nk * 4))
+        return SH_E_OOM;
+    if (!h->n_klist_n.p) {
+        if (h->n_klist_n.ensure(16) || h->n_arm_ctr.ensure(8)) return SH_E_OOM;
+        hipMemsetAsync(h->n_klist_n.p, 0, 16, h->stream);
+        hipMemsetAsync(h->n_arm_ctr.p, 0, 8, h->stream);
+    }
     if (h->sm_on)
         for (int s : h->sm.used)
             if (h->n_rank[s].ensure((size_t)nk * 8)) return SH_E_OOM;
@@ -1361,6 +1383,11 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     if (nf_ensure_recs(h, std::max<int64_t>(h->rec_cap, n + 4096))) return fail(h, SH_E_OOM, "emission buffer");
     nf_cols cols = cols_in;
     cols.sched_armed = armed_flags(h);  // after any key growth above
+    if (cols.sched_armed && h->n_arm_log.p) {
+        cols.arm_log = h->n_arm_log.as<int32_t>();
+        cols.arm_ctr = h->n_arm_ctr.as<unsigned long long>();
+        cols.arm_cap = (uint64_t)h->n_nkeys;
+    }
     shd_payload carry;
     void* mid[8] = {nullptr};
     int alias = -1;
@@ -1511,6 +1538,7 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
     hipStream_t st = h->stream;
     if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
     nf_put_cols(h, nf_store_cols(h));
+    bool first_pass = true;
     int n_absent = 0;  // a key's armed flag may be cleared only when it has one scheduler
     for (int q = 0; q < h->T->n_queries; q++)
         for (int p = 0; p < h->T->q[q].n_proc; p++) n_absent += nf_has_sched(h->T->q[q].proc[p]);
@@ -1522,9 +1550,32 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
             // due keys
             if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");
             hipMemsetAsync(h->n_ctr.p, 0, 8, st);
-            nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, now, h->n_cand.as<nfd_cand>(),
-                    h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0,
-                    h->sm_on ? h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>() : nullptr, st);
+            const uint64_t* rank = h->sm_on ? h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>() : nullptr;
+            if (armed_flags(h) && h->n_arm_log.p) {
+                // the armed-key list (+ the keys armed since the last pass on the
+                // first scheduler's pass, which also rebuilds the list)
+                unsigned long long* ln = h->n_klist_n.as<unsigned long long>();
+                const int c = h->klist_cur;
+                if (first_pass) {
+                    hipMemsetAsync(ln + (c ^ 1), 0, 8, st);
+                    nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
+                                 ln + c, h->n_arm_log.as<int32_t>(), h->n_arm_ctr.as<unsigned long long>(), now,
+                                 h->n_cand.as<nfd_cand>(), h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h),
+                                 n_absent == 1 ? 1 : 0, rank, h->n_klist[c ^ 1].as<int32_t>(), ln + (c ^ 1),
+                                 (int64_t)nkeys, st);
+                    hipMemsetAsync(h->n_arm_ctr.p, 0, 8, st);
+                    h->klist_cur ^= 1;
+                    first_pass = false;
+                } else {
+                    nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
+                                 ln + c, nullptr, nullptr, now, h->n_cand.as<nfd_cand>(),
+                                 h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), 0, rank, nullptr, nullptr,
+                                 (int64_t)nkeys, st);
+                }
+            } else {
+                nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, now, h->n_cand.as<nfd_cand>(),
+                        h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0, rank, st);
+            }
             hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
             if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
             const unsigned long long nc = *h->pin_rd.as<unsigned long long>(PR_NC);

@@ -745,16 +745,17 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     else
         cand += "ok = ok && !hasM;\n";
     std::string mid = "bool mk = true;\n" + gi.terms(F.qonly, "mk");
-    std::string stop;
+    std::string stop, stop_cond;
     if (F.cross) {
         const bool mx = F.op == SH_OP_GT || F.op == SH_OP_GE;
         mid += "if (mk) {\n" + gi.xval(F, "xr") + "if (xr == xr && (!hasM || xr " + (mx ? ">" : "<") +
                " M)) M = xr;\nif (xr == xr) hasM = true;\n}\n";
-        stop = std::string("    if (xq != xq || (hasM && M ") + (mx ? ">=" : "<=") + " xq)) { stopped = true; break; }\n";
+        stop_cond = std::string("xq != xq || (hasM && M ") + (mx ? ">=" : "<=") + " xq)";
     } else {
         mid += "if (mk) hasM = true;\n";
-        stop = "    if (hasM) { stopped = true; break; }\n";
+        stop_cond = "hasM";
     }
+    stop = "    if (" + stop_cond + ") { stopped = true; break; }\n";
     std::set<int> staged = need_r;
     staged.insert(need_q.begin(), need_q.end());
     for (int a : ms_attrs) staged.insert(a);
@@ -768,31 +769,68 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
             s += pfx + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], lds(a) + "[" + row + "]") + ";\n";
         return s;
     };
-    // walk back over the consumer's key in the sorted span, SHB_U events per
-    // step: the step's LDS loads are issued together (no dependent chain)
-    auto walk = [&](bool count, const std::string& on_consumed) {
-        std::string s = "const uint32_t wq = s_ws[sp];\nconst uint32_t key = wq & kmask;\n"
-                        "const int64_t tq = (int64_t)(wq >> kb);\n" +
-                        decl_attrs(need_r, 0) + decl_attrs(need_q, 1) + loads(need_q, "x1_", "sp") + DT +
-                        " xq = 0;\n" + qhead + "bool hasM = false;\n" + DT + " M = 0;\nbool first = true;\n"
-                        "bool stopped = !qok, ran_off = false;\n";
-        s += "for (int r = sp - 1; r >= 0 && !stopped && !ran_off; r -= SHB_U) {\n    uint32_t wv[SHB_U];\n";
-        for (int a : need_r) s += "    " + std::string(col_ctype(P.attr_type[0][a])) + " av" + std::to_string(a) + "[SHB_U];\n";
-        s += "#pragma unroll\n    for (int u = 0; u < SHB_U; u++) {\n        const int o = r - u < 0 ? 0 : r - u;\n"
-             "        wv[u] = s_ws[o];\n";
-        for (int a : need_r) s += "        av" + std::to_string(a) + "[u] = " + lds(a) + "[o];\n";
-        s += "    }\n#pragma unroll\n    for (int u = 0; u < SHB_U; u++) {\n"
-             "    const int o = r - u;\n"
-             "    if (o < 0 || (wv[u] & kmask) != key) { ran_off = true; break; }\n"
-             "    const int64_t tr = (int64_t)(wv[u] >> kb);\n";
+    // the consumer walk back over its key in the sorted span. The first SHB_D
+    // predecessors are loaded together (one LDS latency for the common case);
+    // a walk that goes on past them continues one event at a time. The count
+    // walk records which of the first SHB_D predecessors it consumed (u16 mask,
+    // SHB_MOVF: went past SHB_D), so the emit phase rarely walks again.
+    auto elem = [&](bool count, const std::string& on_consumed, const std::string& wexpr,
+                    const std::string& aexpr) {
+        std::string s = "    if (o < 0 || ((" + wexpr + ") & kmask) != key) { ran_off = true; break; }\n"
+                        "    const int64_t tr = (int64_t)((" + wexpr + ") >> kb);\n";
         if (count) s += "    if (first && tq < tr) atomicOr(P.flag, SHB_F_MONO);\n";
         s += "    first = false;\n    if (tq - tr > SHJ_W) { stopped = true; break; }\n";
+        for (int a : need_r) {
+            std::string ae = aexpr;
+            size_t at = ae.find("@");
+            ae.replace(at, 1, std::to_string(a));
+            s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], ae) + ";\n";
+        }
+        s += "    {\n" + cand + "    if (ok) {\n" + on_consumed + "    }\n    }\n";
+        s += "    {\n" + mid + "    }\n" + stop;
+        return s;
+    };
+    auto head = [&]() {
+        return "const uint32_t wq = s_ws[sp];\nconst uint32_t key = wq & kmask;\n"
+               "const int64_t tq = (int64_t)(wq >> kb);\n" +
+               decl_attrs(need_r, 0) + decl_attrs(need_q, 1) + loads(need_q, "x1_", "sp") + DT + " xq = 0;\n" +
+               qhead + "bool hasM = false;\n" + DT + " M = 0;\nbool first = true;\n"
+               "bool stopped = !qok, ran_off = false;\n";
+    };
+    auto slow = [&](bool count, const std::string& on_consumed, const std::string& from) {
+        return "for (int o = " + from + "; !stopped && !ran_off; o--) {\n" +
+               elem(count, on_consumed, "s_ws[o < 0 ? 0 : o]", "s_a@[o]") + "}\n";
+    };
+    auto walk_count = [&]() {
+        std::string s = head() + "uint32_t mask = 0u;\nif (!stopped) {\nuint32_t wv[SHB_D];\n";
+        for (int a : need_r)
+            s += std::string(col_ctype(P.attr_type[0][a])) + " av" + std::to_string(a) + "[SHB_D];\n";
+        s += "#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n    const int o = sp - 1 - u < 0 ? 0 : sp - 1 - u;\n"
+             "    wv[u] = s_ws[o];\n";
+        for (int a : need_r) s += "    av" + std::to_string(a) + "[u] = " + lds(a) + "[o];\n";
+        // break-free: a `live` predicate instead of early exits, so the unrolled
+        // loop compiles to straight-line vector code (no exec-mask juggling on
+        // the CU's shared scalar unit)
+        s += "}\nbool live = true, mono = false;\n#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n"
+             "    const int o = sp - 1 - u;\n"
+             "    const bool same = o >= 0 && (wv[u] & kmask) == key;\n"
+             "    const int64_t tr = (int64_t)(wv[u] >> kb);\n"
+             "    if (live && !same) { live = false; ran_off = true; }\n"
+             "    if (live && tq - tr > SHJ_W) { live = false; stopped = true; }\n"
+             "    if (live && first && tq < tr) mono = true;\n"
+             "    if (live) {\n    first = false;\n";
         for (int a : need_r)
             s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
-        s += "    {\n" + cand + "    if (ok) {\n" + on_consumed + "    }\n    }\n";
-        s += "    {\n" + mid + "    }\n" + stop + "    }\n}\n";
-        if (count) s += "if (!stopped && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n";
+        s += "    {\n" + cand + "    if (ok) {\n        c_++;\n        mask |= 1u << u;\n    }\n    }\n";
+        s += "    {\n" + mid + "    }\n    if (" + stop_cond + ") { stopped = true; live = false; }\n    }\n}\n"
+             "if (mono) atomicOr(P.flag, SHB_F_MONO);\n";
+        s += "}\nif (!stopped && !ran_off) {\n    mask = SHB_MOVF;\n" +
+             slow(true, "        c_++;\n", "sp - 1 - SHB_D") + "}\n";
+        s += "if (!stopped && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n";
         return s;
+    };
+    auto walk = [&](bool count, const std::string& on_consumed) {
+        return head() + slow(count, on_consumed, "sp - 1");
     };
     std::string ms_put;
     for (size_t m = 0; m < ms_attrs.size(); m++) {
@@ -803,12 +841,14 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     (void)sidx;
 
     src = SHJ_HEADERS;
-    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_TPB 512\n#define SHB_U 4\n";
+    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_TPB 512\n#define SHB_D 15\n#define SHB_MOVF 0x8000u\n"
+           "#define SHB_NR (SHB_SPAN / SHB_TPB)\nstatic_assert(SHB_SPAN % SHB_TPB == 0, \"span\");\n";
     src += R"(
 extern "C" __global__ void __launch_bounds__(SHB_TPB) shb_match(shb_plan P) {
 __shared__ uint32_t s_ws[SHB_SPAN];
 __shared__ uint16_t s_idx[SHB_SPAN];
 __shared__ uint16_t s_pre[SHB_CH];
+__shared__ uint16_t s_msk[SHB_CH];
 __shared__ uint32_t wcnt[SHB_TPB / 64][256];
 __shared__ uint32_t run[256], tstart[256], ws[SHB_TPB / 64];
 )";
@@ -837,9 +877,24 @@ if (threadIdx.x < 256) run[threadIdx.x] = 0u;
 __syncthreads();
 unsigned long long t_prev = wall_clock64();
 #define SHB_PROF(ph) if (P.prof && threadIdx.x == 0) { const unsigned long long t_now = wall_clock64(); atomicAdd(&P.prof[ph], t_now - t_prev); t_prev = t_now; }
-// local-key histogram of the chunk and its halo
+// the chunk and its halo into registers (all loads in flight together);
+// local-key histogram
 const uint32_t* __restrict__ gw = P.w0 + (int64_t)bs + hs;
-for (int i = threadIdx.x; i < L; i += SHB_TPB) atomicAdd(&run[gw[i] & kmask], 1u);
+uint32_t wr[SHB_NR];
+)";
+    for (int a : staged_out)
+        src += std::string(col_ctype(P.attr_type[0][a])) + " vr" + std::to_string(a) + "[SHB_NR];\n";
+    src += R"(#pragma unroll
+for (int k = 0; k < SHB_NR; k++) {
+    const int i = k * SHB_TPB + (int)threadIdx.x;
+    wr[k] = i < L ? gw[i] : 0u;
+)";
+    for (int a : staged_out)
+        src += "    vr" + std::to_string(a) + "[k] = i < L ? g_a" + std::to_string(a) + "[(int64_t)bs + hs + i] : 0;\n";
+    src += R"(}
+#pragma unroll
+for (int k = 0; k < SHB_NR; k++)
+    if (k * SHB_TPB + (int)threadIdx.x < L) atomicAdd(&run[wr[k] & kmask], 1u);
 __syncthreads();
 {
     uint32_t tot;
@@ -852,14 +907,15 @@ __syncthreads();
 SHB_PROF(0)
 // stable sort of the span by local key (wave-ballot ranking), staged in sorted
 // order: the walks read consecutive LDS words
-for (int r0 = 0; r0 < L; r0 += SHB_TPB) {
-    const int i = r0 + (int)threadIdx.x;
+#pragma unroll
+for (int k = 0; k < SHB_NR; k++) {
+    const int i = k * SHB_TPB + (int)threadIdx.x;
     const bool valid = i < L;
-    const uint32_t w = valid ? gw[i] : 0u;
+    const uint32_t w = wr[k];
 )";
     for (int a : staged_out)
-        src += "    const " + std::string(col_ctype(P.attr_type[0][a])) + " v" + std::to_string(a) + " = valid ? g_a" +
-               std::to_string(a) + "[(int64_t)bs + hs + i] : 0;\n";
+        src += "    const " + std::string(col_ctype(P.attr_type[0][a])) + " v" + std::to_string(a) + " = vr" +
+               std::to_string(a) + "[k];\n";
     src += R"(    const uint32_t d = w & kmask;
     const uint32_t rk = shw_rank8<SHB_TPB>(d, valid, wcnt, run);
     if (valid) {
@@ -878,9 +934,10 @@ const int i = (int)s_idx[sp];
 if (i < hl) continue;
 uint32_t c_ = 0;
 )";
-    src += walk(true, "        c_++;\n");
+    src += walk_count();
     src += R"(if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);
 s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);
+s_msk[i - hl] = (uint16_t)mask;
 }
 __syncthreads();
 SHB_PROF(2)
@@ -946,7 +1003,10 @@ uint32_t k = 0;
 )";
     std::string put = "        const int64_t dst = rbase + (int64_t)off + (int64_t)(cn - 1u - k);\n        k++;\n" + ms_put +
                       "        if (k == cn) { stopped = true; break; }\n";
-    src += walk(false, put);
+    src += "const uint32_t mk = s_msk[i - hl];\nif (!(mk & SHB_MOVF)) {\n    uint32_t m = mk;\n"
+           "    while (m) {\n        const int o = sp - __ffs(m);\n        m &= m - 1u;\n"
+           "        const int64_t dst = rbase + (int64_t)off + (int64_t)(cn - 1u - k);\n        k++;\n" +
+           ms_put + "    }\n} else {\n" + walk(false, put) + "}\n";
     src += "}\n__syncthreads();\nSHB_PROF(4)\n}\n}\n";
     return true;
 }

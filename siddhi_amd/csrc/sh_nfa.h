@@ -162,6 +162,11 @@ struct nf_cols {
     // scan when its queues are empty, so the scan skips keys that never armed one
     // (NULL: every key is scanned)
     uint8_t* sched_armed;
+    // keys whose flag went 0 -> 1 since the last due pass (the device due list
+    // takes them in, sh_host.cpp nf_timers); NULL: off
+    int32_t* arm_log;
+    unsigned long long* arm_ctr;
+    uint64_t arm_cap;
     // scheduler-map history of this launch for the host's HashMap-order model
     // (sh_jmap.h): 2 words per record, [0] processing stamp, [1] key | scheduler
     // (query * NF_MAX_PROC + proc) << 32 | kind << 48 (NF_SEV_*); NULL: off
@@ -1537,7 +1542,17 @@ struct NfLane {
         sched_record(p, added ? NF_SEV_INSERT : NF_SEV_CALL);
         q[2 + (head + n) % Q->lay.sched_cap] = (uint64_t)t;
         q[0] = (uint64_t)head | ((uint64_t)(n + 1) << 32);
-        if (C && C->sched_armed) C->sched_armed[key] = 1;
+        if (C && C->sched_armed && !C->sched_armed[key]) {
+            C->sched_armed[key] = 1;
+            if (C->arm_log) {
+#if defined(__HIP_DEVICE_COMPILE__)
+                const unsigned long long at = atomicAdd(C->arm_ctr, 1ull);
+#else
+                const unsigned long long at = (*C->arm_ctr)++;
+#endif
+                if (at < C->arm_cap) C->arm_log[at] = key;  // one entry per key per episode: never full
+            }
+        }
     }
     NF_HD bool sched_head(int p, int64_t* t) const {
         const uint64_t* q = sched(p);

@@ -15,6 +15,8 @@
 // own arena, which stays L2-resident while its lane runs.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "sh_nfa.h"
 #include "sh_nfa_dev.h"
 
@@ -175,6 +177,76 @@ __global__ void __launch_bounds__(256) k_nfa_due(const nf_table* __restrict__ T,
     cand[at].stamp = rank ? rank[key] : (sq[1] & ~(1ull << 63));
     cand[at].key = key;
     cand[at].pad = 0;
+}
+
+// The due pass over the armed-key list instead of every key: the list holds
+// every key that may have a queued notification (armed flag set), the arm log
+// the keys armed since the last pass. Survivors (non-empty queue, or every key
+// when `drop` is off) go to lout; a drained key leaves the list and clears its
+// flag. Scheduler.onTimeChange's head-peek per state (Scheduler.java:74-99).
+__global__ void __launch_bounds__(256) k_nfa_due_list(const nf_table* __restrict__ T, int q, int p,
+                                                      const uint64_t* __restrict__ kstate,
+                                                      const int32_t* __restrict__ lin,
+                                                      const unsigned long long* __restrict__ lin_n,
+                                                      const int32_t* __restrict__ alog,
+                                                      const unsigned long long* __restrict__ alog_n, int64_t now,
+                                                      nfd_cand* __restrict__ cand, unsigned long long* __restrict__ ctr,
+                                                      int64_t cap, uint8_t* __restrict__ armed, int drop,
+                                                      const uint64_t* __restrict__ rank, int32_t* __restrict__ lout,
+                                                      unsigned long long* __restrict__ lout_n) {
+    const int64_t n1 = (int64_t)*lin_n, n2 = alog ? (int64_t)*alog_n : 0;
+    const nf_query& Q = T->q[q];
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    // uniform trip count per wave (ballots below)
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n1 + n2; i0 += stride) {
+        const int64_t i = i0 + lane;
+        bool keep = false, due = false;
+        int32_t key = -1;
+        int64_t t = 0;
+        uint64_t stamp = 0;
+        if (i < n1 + n2) {
+            key = i < n1 ? lin[i] : alog[i - n1];
+            const uint64_t* kb = kstate + (int64_t)key * T->key_words;
+            const uint64_t* sq = kb + Q.q_off + Q.lay.off_sched + (int64_t)p * (2 + Q.lay.sched_cap);
+            const uint32_t head = (uint32_t)sq[0], cnt = (uint32_t)(sq[0] >> 32);
+            if (!cnt && drop) {
+                armed[key] = 0;
+            } else {
+                keep = true;
+                if (cnt && (!T->partitioned || (sq[1] >> 63))) {
+                    t = (int64_t)sq[2 + head];
+                    due = t <= now;
+                    stamp = rank ? rank[key] : (sq[1] & ~(1ull << 63));
+                }
+            }
+        }
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        if (lout) {
+            const uint64_t km = __ballot(keep);
+            unsigned long long base = 0;
+            if (km) {
+                const int leader = __ffsll((long long)km) - 1;
+                if (lane == leader) base = atomicAdd(lout_n, (unsigned long long)__popcll(km));
+                base = __shfl(base, leader);
+            }
+            if (keep) lout[base + __popcll(km & lt)] = key;
+        }
+        const uint64_t dm = __ballot(due);
+        if (dm) {
+            const int leader = __ffsll((long long)dm) - 1;
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(dm));
+            base = __shfl(base, leader);
+            const unsigned long long at = base + __popcll(dm & lt);
+            if (due && (int64_t)at < cap) {
+                cand[at].t = t;
+                cand[at].stamp = stamp;
+                cand[at].key = key;
+                cand[at].pad = 0;
+            }
+        }
+    }
 }
 
 // Scheduler.onTimeChange tie-break on the device for a large backlog of due
@@ -354,6 +426,17 @@ extern "C" int nfd_due(const nf_table* dT, int q, int p, const uint64_t* kstate,
     if (nkeys <= 0) return 0;
     hipLaunchKernelGGL(k_nfa_due, dim3(nf_blocks(nkeys, 256)), dim3(256), 0, (hipStream_t)stream, dT, q, p, kstate,
                        nkeys, now, cand, ctr, cap, armed, clear_armed, rank);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_due_list(const nf_table* dT, int q, int p, const uint64_t* kstate, const int32_t* lin,
+                            const unsigned long long* lin_n, const int32_t* alog, const unsigned long long* alog_n,
+                            int64_t now, nfd_cand* cand, unsigned long long* ctr, int64_t cap, uint8_t* armed,
+                            int drop, const uint64_t* rank, int32_t* lout, unsigned long long* lout_n,
+                            int64_t max_items, void* stream) {
+    const int64_t blocks = std::min<int64_t>(std::max<int64_t>(nf_blocks(max_items, 256), 1), 2048);
+    hipLaunchKernelGGL(k_nfa_due_list, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dT, q, p, kstate,
+                       lin, lin_n, alog, alog_n, now, cand, ctr, cap, armed, drop, rank, lout, lout_n);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -53,6 +53,14 @@ int nfd_start(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, uint64_t 
 int nfd_due(const nf_table* dT, int q, int p, const uint64_t* kstate, int32_t nkeys, int64_t now, nfd_cand* cand,
             unsigned long long* ctr, int64_t cap, uint8_t* armed, int clear_armed, const uint64_t* rank,
             void* stream);
+// the due pass over the armed-key list (lin, count in device memory) plus the
+// keys armed since the last pass (alog, may be NULL); survivors to lout (may be
+// NULL: scan only); drop: a drained key leaves the list and clears its flag.
+// max_items bounds the launch (grid-stride).
+int nfd_due_list(const nf_table* dT, int q, int p, const uint64_t* kstate, const int32_t* lin,
+                 const unsigned long long* lin_n, const int32_t* alog, const unsigned long long* alog_n, int64_t now,
+                 nfd_cand* cand, unsigned long long* ctr, int64_t cap, uint8_t* armed, int drop, const uint64_t* rank,
+                 int32_t* lout, unsigned long long* lout_n, int64_t max_items, void* stream);
 // dst[keys[i]] = ranks[i]
 int nfd_rank_scatter(const int32_t* keys, const uint64_t* ranks, int64_t n, uint64_t* dst, void* stream);
 // device tie-break of a due-key backlog: tmin of the candidates, then per due

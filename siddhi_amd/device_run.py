@@ -26,26 +26,32 @@ class DeviceRunner:
         plus out_query[n] (emitting query index) when `with_query`."""
         n = ts.numel()
         cap = out_capacity or n
-        if self._out_cap < cap:
-            self.out_seq = torch.empty(cap, dtype=torch.int64, device=self.device)
-            self.out_vals = torch.empty(cap * self.n_out, dtype=torch.int64, device=self.device)
-            self.out_q = torch.empty(cap, dtype=torch.int32, device=self.device)
-            self._out_cap = cap
-        cp = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
-        r = abi.sh_device_run()
-        r.n = n
-        r.d_ts = ts.data_ptr()
-        r.d_keys = keys.data_ptr()
-        r.n_keys = int(n_keys)
-        r.batch_events = int(batch_events)
-        r.d_cols = cp
-        r.out_capacity = self._out_cap
-        r.d_out_seq = self.out_seq.data_ptr()
-        r.d_out_values = self.out_vals.data_ptr()
-        r.stream = stream.cuda_stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
-        r.d_out_query = self.out_q.data_ptr() if with_query else None
-        rc = lib().sh_run_device(self.handle.h, C.byref(r))
-        check(self.handle.h, rc)
+        for attempt in range(2):
+            if self._out_cap < cap:
+                self.out_seq = torch.empty(cap, dtype=torch.int64, device=self.device)
+                self.out_vals = torch.empty(cap * self.n_out, dtype=torch.int64, device=self.device)
+                self.out_q = torch.empty(cap, dtype=torch.int32, device=self.device)
+                self._out_cap = cap
+            cp = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
+            r = abi.sh_device_run()
+            r.n = n
+            r.d_ts = ts.data_ptr()
+            r.d_keys = keys.data_ptr()
+            r.n_keys = int(n_keys)
+            r.batch_events = int(batch_events)
+            r.d_cols = cp
+            r.out_capacity = self._out_cap
+            r.d_out_seq = self.out_seq.data_ptr()
+            r.d_out_values = self.out_vals.data_ptr()
+            r.stream = stream.cuda_stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+            r.d_out_query = self.out_q.data_ptr() if with_query else None
+            rc = lib().sh_run_device(self.handle.h, C.byref(r))
+            if rc == abi.SH_E_MORE and attempt == 0 and int(r.out_count) > self._out_cap:
+                # more matches than events: grow the output to the reported count and rerun
+                cap = int(r.out_count)
+                continue
+            check(self.handle.h, rc)
+            break
         m = int(r.out_count)
         res = (m, self.out_seq[:m], self.out_vals[: m * self.n_out].view(m, self.n_out))
         return res + (self.out_q[:m],) if with_query else res

@@ -1,15 +1,40 @@
-"""Key sharding across GPUs (one process per GPU).
+"""Key-sharded multi-GPU path (one process per GPU, torch.distributed over RCCL).
 
-Partitions never interact in the reference (per-key state, PartitionSyncStateHolder),
-so a partitioned app shards by key with no data-path collective: rank =
-mix32(key id) % world. Each rank runs its own matcher handle; the per-rank ordered
-match streams are merged by trigger sequence number.
+Partitions never interact in the reference: every partition key has its own
+state (core/partition/PartitionRuntimeImpl.java:346-364, PartitionStateHolder),
+so ONE arrival-ordered stream is split across the ranks by key: rank r owns the
+keys with mix32(key id) % world == r. Every rank ingests an arrival-contiguous
+slice of the stream (global sequence numbers seq0 .. seq0 + n). A step:
+
+  1. route   owner rank of every event of the slice; stable owner-major
+             positions (shs_route) and packed records (shs_pack: the event
+             columns + the global sequence number, 32 B per C2 event)
+  2. shuffle one all-to-all of the records (RCCL), split sizes exchanged first
+  3. match   the owner unpacks (shs_unpack; received runs are laid out by
+             source rank, so arrival order holds) and runs its own matcher on
+             the events of its keys (sh_run_device)
+  4. return  each match row goes back to the rank whose slice holds its trigger
+             event (shs_rows_home: the rows are already grouped by source
+             rank), one all-to-all of (seq, values)
+  5. merge   k-way merge of the owners' ordered runs by trigger sequence
+             (shs_merge): rank r ends with the reference's output order for its
+             slice, so the ranks' outputs concatenated are the single-process
+             output.
+
+Step 3 is the only compute; 2 and 4 are the only collectives (no collective
+inside the matcher). Scaling is strong: the stream is fixed, the ranks split it.
+The device kernels live in libsiddhi_hip.so (include/siddhi_shard.h); tests can
+drive the same orchestration with other ops / matchers on CPU over gloo.
 """
+from __future__ import annotations
+
+import ctypes as C
+
 import numpy as np
 
 
 def mix32(x):
-    """splitmix-style 32-bit finaliser (vectorised)."""
+    """splitmix-style 32-bit finaliser (vectorised; = shs_owner's hash)."""
     x = np.asarray(x, dtype=np.uint64) & np.uint64(0xFFFFFFFF)
     x = (x ^ (x >> np.uint64(16))) * np.uint64(0x85EBCA6B) & np.uint64(0xFFFFFFFF)
     x = (x ^ (x >> np.uint64(13))) * np.uint64(0xC2B2AE35) & np.uint64(0xFFFFFFFF)
@@ -26,10 +51,184 @@ def split(keys, world):
     return [np.nonzero(s == r)[0] for r in range(world)]
 
 
-def merge(parts):
-    """k-way merge of per-rank ordered outputs: list of (seq, *columns) tuples of
-    arrays, each ordered by seq. Rows sharing a seq come from one rank and keep
-    their order (stable sort)."""
-    seqs = np.concatenate([p[0] for p in parts])
-    order = np.argsort(seqs, kind="stable")
-    return tuple(np.concatenate([p[i] for p in parts])[order] for i in range(len(parts[0])))
+def slice_bounds(n_total, world):
+    """arrival-contiguous ingest slices: rank r holds [b[r], b[r+1])"""
+    return [n_total * r // world for r in range(world + 1)]
+
+
+def _width(t):
+    return t.element_size()
+
+
+class HipShardOps:
+    """The device kernels of include/siddhi_shard.h on torch-allocated HBM."""
+
+    def __init__(self, device):
+        import torch
+        from ._native import lib
+        self.torch = torch
+        self.device = torch.device(device)
+        self.lib = lib()
+        L = self.lib
+        L.shs_route_scratch_bytes.argtypes = [C.c_int64, C.c_int32]
+        L.shs_route_scratch_bytes.restype = C.c_int64
+        L.shs_route.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.shs_route.restype = C.c_int
+        L.shs_record_words.argtypes = [C.c_int32, C.c_void_p]
+        L.shs_record_words.restype = C.c_int32
+        L.shs_pack.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                               C.c_void_p]
+        L.shs_pack.restype = C.c_int
+        L.shs_unpack.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.shs_unpack.restype = C.c_int
+        L.shs_rows_home.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
+                                    C.c_void_p]
+        L.shs_rows_home.restype = C.c_int
+        L.shs_merge.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                C.c_void_p]
+        L.shs_merge.restype = C.c_int
+        self._scratch = None
+
+    def _stream(self):
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    @staticmethod
+    def _check(rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed with status {rc}")
+
+    def route(self, keys, world):
+        torch = self.torch
+        n = keys.numel()
+        need = int(self.lib.shs_route_scratch_bytes(n, world))
+        if self._scratch is None or self._scratch.numel() < need:
+            self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+        pos = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        counts = (C.c_int64 * world)()
+        self._check(self.lib.shs_route(keys.data_ptr(), n, world, pos.data_ptr(), self._scratch.data_ptr(),
+                                       counts, self._stream()), "shs_route")
+        return pos, [int(c) for c in counts]
+
+    def record_words(self, widths):
+        w = (C.c_int32 * len(widths))(*widths)
+        return int(self.lib.shs_record_words(len(widths), w))
+
+    def pack(self, pos, cols, seq0):
+        torch = self.torch
+        n = cols[0].numel()
+        widths = [_width(c) for c in cols]
+        stride = self.record_words(widths)
+        rec = torch.empty(max(n * stride, 1), dtype=torch.int32, device=self.device)
+        cp = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
+        wp = (C.c_int32 * len(cols))(*widths)
+        self._check(self.lib.shs_pack(pos.data_ptr(), n, len(cols), cp, wp, seq0, rec.data_ptr(), self._stream()),
+                    "shs_pack")
+        return rec[: n * stride], stride
+
+    def unpack(self, rec, n, like):
+        torch = self.torch
+        cols = [torch.empty(n, dtype=c.dtype, device=self.device) for c in like]
+        seq = torch.empty(n, dtype=torch.int64, device=self.device)
+        cp = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
+        wp = (C.c_int32 * len(cols))(*[_width(c) for c in cols])
+        self._check(self.lib.shs_unpack(rec.data_ptr(), n, len(cols), cp, wp, seq.data_ptr(), self._stream()),
+                    "shs_unpack")
+        return cols, seq
+
+    def rows_home(self, oseq, m, seq_base, gseq, src_off, world):
+        offs = (C.c_int64 * (world + 1))(*src_off)
+        counts = (C.c_int64 * world)()
+        self._check(self.lib.shs_rows_home(oseq.data_ptr(), m, seq_base, gseq.data_ptr(), offs, world, counts,
+                                           self._stream()), "shs_rows_home")
+        return [int(c) for c in counts]
+
+    def merge(self, seq, vals, n_out, run_off):
+        torch = self.torch
+        m = run_off[-1]
+        seq_out = torch.empty(max(m, 1), dtype=torch.int64, device=self.device)
+        vals_out = torch.empty(max(m * n_out, 1), dtype=torch.int64, device=self.device)
+        offs = (C.c_int64 * len(run_off))(*run_off)
+        self._check(self.lib.shs_merge(seq.data_ptr(), vals.data_ptr(), n_out, offs, len(run_off) - 1,
+                                       seq_out.data_ptr(), vals_out.data_ptr(), self._stream()), "shs_merge")
+        return seq_out[:m], vals_out[: m * n_out].view(m, n_out)
+
+
+class TorchComm:
+    """the step's two exchanges over torch.distributed (RCCL "nccl" on GPUs, gloo
+    on CPU): all_to_all_single with per-rank split sizes"""
+
+    def __init__(self, world, group=None):
+        import torch.distributed as dist
+        self.dist, self.world, self.group = dist, world, group
+
+    def counts(self, counts, device):
+        import torch
+        send = torch.tensor(counts, dtype=torch.int64, device=device)
+        recv = torch.empty(self.world, dtype=torch.int64, device=device)
+        self.dist.all_to_all_single(recv, send, group=self.group)
+        return [int(x) for x in recv.cpu().tolist()]
+
+    def exchange(self, send, send_counts, recv_counts, per):
+        import torch
+        n = sum(recv_counts) * per
+        recv = torch.empty(max(n, 1), dtype=send.dtype, device=send.device)[:n]
+        self.dist.all_to_all_single(recv, send, output_split_sizes=[c * per for c in recv_counts],
+                                    input_split_sizes=[c * per for c in send_counts], group=self.group)
+        return recv
+
+
+class KeyShardedStep:
+    """One sharded pass on this rank (see the module docstring).
+
+    matcher(ts, keys, cols, n_keys) -> (m, local_seq[m] ascending (event index
+    into the received events), values[m, n_out]) runs on the received events.
+    comm: the two all-to-all exchanges (TorchComm by default).
+    """
+
+    def __init__(self, world, rank, ops, matcher, n_out, comm=None):
+        self.world, self.rank = world, rank
+        self.ops, self.matcher, self.n_out = ops, matcher, n_out
+        self.comm = comm if comm is not None else TorchComm(world)
+        self.last = {}
+
+    def run(self, ts, keys, cols, seq0, n_keys, key_attr=None):
+        """ts / keys / cols: this rank's ingest slice (arrival order), seq0 its
+        first global sequence number; key_attr: index of the attribute column
+        that holds the partition key ids (then `keys` travels once). Returns
+        (seq[m], values[m, n_out]) of the rows triggered by the slice's events,
+        in the reference's order."""
+        dev = ts.device
+        world = self.world
+        # 1. route + pack (columns: ts, [keys,] then the attribute columns)
+        pos, send_counts = self.ops.route(keys, world)
+        allc = [ts] + ([] if key_attr is not None else [keys]) + list(cols)
+        rec, stride = self.ops.pack(pos, allc, seq0)
+        # 2. shuffle
+        recv_counts = self.comm.counts(send_counts, dev)
+        rrec = self.comm.exchange(rec, send_counts, recv_counts, stride)
+        n_recv = sum(recv_counts)
+        ucols, gseq = self.ops.unpack(rrec, n_recv, allc)
+        if key_attr is not None:
+            r_ts, r_cols = ucols[0], ucols[1:]
+            r_keys = r_cols[key_attr]
+        else:
+            r_ts, r_keys, r_cols = ucols[0], ucols[1], ucols[2:]
+        # 3. match on the owned keys' events
+        m, oseq, ovals = self.matcher(r_ts, r_keys, r_cols, n_keys)
+        # 4. rows back to the ranks holding their trigger events
+        src_off = [0]
+        for c in recv_counts:
+            src_off.append(src_off[-1] + c)
+        oseq = oseq[:m].contiguous()
+        ovals = ovals[:m].contiguous().view(-1)
+        row_counts = self.ops.rows_home(oseq, m, 0, gseq, src_off, world)
+        back_counts = self.comm.counts(row_counts, dev)
+        hseq = self.comm.exchange(oseq, row_counts, back_counts, 1)
+        hvals = self.comm.exchange(ovals, row_counts, back_counts, self.n_out)
+        # 5. k-way merge of the owners' runs by trigger sequence
+        run_off = [0]
+        for c in back_counts:
+            run_off.append(run_off[-1] + c)
+        seq, vals = self.ops.merge(hseq, hvals, self.n_out, run_off)
+        self.last = dict(sent=send_counts, received=recv_counts, matches_here=m, rows_home=run_off[-1])
+        return seq, vals

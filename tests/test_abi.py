@@ -18,6 +18,27 @@ def lib():
     return abi.bind_product(C.CDLL(path))
 
 
+def test_shard_header_symbols_are_exported(lib):
+    """include/siddhi_shard.h (key-sharded multi-GPU path) is implemented by the
+    same library"""
+    hdr = open(os.path.join(ROOT, "include", "siddhi_shard.h")).read()
+    declared = set(re.findall(r"\b(shs_[a-z_]+)\s*\(", hdr))
+    assert len(declared) >= 8
+    out = subprocess.run(["nm", "-D", "--defined-only", build.OUT], capture_output=True, text=True).stdout
+    assert declared <= set(re.findall(r" T (shs_[a-z_]+)", out))
+
+
+def test_shard_owner_matches_python_hash(lib):
+    import ctypes
+    import numpy as np
+    from siddhi_amd import shard
+    lib.shs_owner.argtypes = [ctypes.c_int32, ctypes.c_int32]
+    lib.shs_owner.restype = ctypes.c_int32
+    keys = np.arange(0, 50_000, 7, dtype=np.int32)
+    for world in (1, 2, 3, 8):
+        assert [lib.shs_owner(int(k), world) for k in keys] == list(shard.shard_of(keys, world))
+
+
 def test_header_declares_exactly_the_exported_symbols(lib):
     hdr = open(os.path.join(ROOT, "include", "siddhi_hip.h")).read()
     declared = set(re.findall(r"\b(sh_[a-z_]+)\s*\(", hdr))
