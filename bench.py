@@ -131,7 +131,10 @@ def workload(args, rank):
         compiled = compiler.compile_app(synth.C3_QUERY)
 
         def verify(oseq, ovals, oq):
-            return None  # C3 parity: tests/test_gpu_nfa.py (oracle, key subsets at full size)
+            sys.path.insert(0, os.path.join(HERE, "tests"))
+            from c3_check import c3_expected
+            eseq, evals = c3_expected(ts, keys, price)
+            return bool(len(oseq) == len(eseq) and np.array_equal(oseq, eseq) and np.array_equal(ovals, evals))
 
         def cpu(s):
             sys.path.insert(0, os.path.join(HERE, "tests"))

@@ -389,6 +389,7 @@ struct sh_handle {
     // in n_klist_n[0..1]) and the log of keys armed since the last pass
     DevBuf n_klist[2], n_klist_n, n_arm_log, n_arm_ctr;
     int klist_cur = 0;
+    int seq3_last = 0;                  // the last general-engine run took k_seq3
     // scheduler maps' iteration order (sh_jmap.h): host models fed by the
     // launches' getState history, per-key ranks uploaded for the due-key pick
     bool sm_on = false;
@@ -1450,8 +1451,15 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
             }
         }
         nfd_emit em = nf_emit(h);
-        if (nfd_run(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), &E, n, seg_list, nseg,
-                    skeys, nkeys, max_seg, h->tick, h->clock, &em, st))
+        // the rise-and-fall sequence engine: fresh single-query runs of that shape
+        const bool seq3 = fresh && h->T->n_queries == 1 && h->T->q[0].s3 && !getenv("SH_NO_SEQ3");
+        h->seq3_last = seq3 ? 1 : 0;
+        if (seq3) {
+            if (nfd_seq3(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), &E, n, seg_list, nseg, skeys, nkeys, max_seg,
+                         &em, st))
+                return fail(h, SH_E_HIP, "k_seq3 launch failed");
+        } else if (nfd_run(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), &E, n,
+                           seg_list, nseg, skeys, nkeys, max_seg, h->tick, h->clock, &em, st))
             return fail(h, SH_E_HIP, "k_nfa_run launch failed");
         hipEventRecord(h->ev[2], st);
         hipMemcpyAsync(h->pin_rd.as<void>(PR_ERR), h->n_err.p, 4, hipMemcpyDeviceToHost, st);
@@ -2387,6 +2395,11 @@ int shx_bucket_status(sh_handle* h) {
     }
     return h->bk_last;
 }
+
+// 1: the last general-engine sh_run_device took the rise-and-fall sequence engine
+int shx_seq3_status(sh_handle* h) { return h ? h->seq3_last : 0; }
+// 1: the compiled app has the rise-and-fall sequence shape (no device needed)
+int shx_seq3_shape(sh_handle* h) { return h && h->T && h->T->n_queries == 1 && h->T->q[0].s3 ? 1 : 0; }
 
 // compile-only check of the bucketed matcher shb_match (no device needed)
 int shx_bucket_compile(sh_handle* h, char* buf, int64_t len) {

@@ -134,6 +134,13 @@ struct nf_query {
     int32_t out_pc[NF_MAX_OUT], out_len[NF_MAX_OUT], out_agg[NF_MAX_OUT], out_type[NF_MAX_OUT];
     nf_layout lay;
     int64_t q_off;          // word offset of this query's block inside a key block
+    // rise-and-fall sequence `every e1=S, e2=S[f2(e2, e1)]+, e3=S[f3(e3, e2[last])]`
+    // (no within, one stream): the per-key state reduces to one partial (k_seq3)
+    int8_t s3;
+    int8_t s3_op2, s3_dom2, s3_op3, s3_dom3;
+    int8_t s3_a2, s3_t2, s3_e1a, s3_e1t;      // f2: x.a2 (type t2) op2 e1.e1a (type e1t)
+    int8_t s3_a3, s3_t3, s3_la, s3_lt;        // f3: x.a3 (type t3) op3 last.la (type lt)
+    int8_t s3_out_slot[NF_MAX_OUT], s3_out_attr[NF_MAX_OUT], s3_out_type[NF_MAX_OUT];
 };
 
 struct nf_table {

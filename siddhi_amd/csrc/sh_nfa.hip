@@ -133,6 +133,104 @@ __global__ void __launch_bounds__(NF_TPB) k_nfa_run(const nf_table* __restrict__
     if (L.err) atomicOr(EM.err, L.err);
 }
 
+// The rise-and-fall sequence (nf_query.s3, sh_nfa_lower.cpp detect_seq3): one
+// lane per key segment, the key's single partial in registers. Per event x:
+//   hit = (a last e2 exists) && f3(x, last)        -> emit (e1, last, x)
+//   else if f2(x, e1) -> last = x (the e2 run grows)
+//   else              -> e1 = x (every: the new start partial)
+// Fresh per-key state each run (sh_run_device); emission records and per-event
+// counts as k_nfa_run writes them, so k_nfa_place orders the rows.
+__device__ __forceinline__ NfVal s3_val(const nf_cols* C, int a, int t, uint32_t row) {
+    NfVal v;
+    v.t = (uint8_t)t;
+    const uint8_t* nm = C->nul[0][a];
+    v.null = nm ? nm[row] : 0;
+    const void* p = C->col[0][a];
+    switch (t) {
+        case SH_T_LONG:
+        case SH_T_DOUBLE: v.b = ((const int64_t*)p)[row]; break;
+        case SH_T_FLOAT: v.b = (int64_t)((const uint32_t*)p)[row]; break;
+        case SH_T_BOOL: v.b = ((const uint8_t*)p)[row] ? 1 : 0; break;
+        default: v.b = (int64_t)((const int32_t*)p)[row];
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(NF_TPB) k_seq3(const nf_table* __restrict__ T, const nf_cols* __restrict__ C,
+                                                 DevEvents E, int64_t n, const uint32_t* __restrict__ seg_list,
+                                                 const uint32_t* __restrict__ nseg,
+                                                 const uint32_t* __restrict__ skeys, int32_t nkeys, nfd_emit EM) {
+    const uint32_t sidx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sidx >= *nseg) return;
+    const uint32_t beg = seg_list[sidx];
+    const uint32_t key = skeys ? skeys[beg] : 0u;
+    if (key >= (uint32_t)nkeys) {
+        atomicOr(EM.err, (unsigned)NF_E_KEY);
+        return;
+    }
+    int64_t end = beg + 1;
+    if (skeys)
+        while (end < n && skeys[end] == key) end++;
+    else
+        end = n;
+    const nf_query& Q = T->q[0];
+    DevSink sink;
+    sink.buf = EM.recs;
+    sink.ctr = EM.ctr;
+    sink.cap = EM.cap;
+    sink.stride = EM.stride;
+    sink.chunk = nullptr;
+    sink.used = sink.n = 0;
+    DevEv ev{&E};
+    bool has_last = false;
+    uint32_t e1_row = 0, last_row = 0;
+    NfVal e1v, lastv;
+    e1v.b = lastv.b = 0;
+    e1v.t = lastv.t = 0;
+    e1v.null = lastv.null = 1;
+    bool fail = false;
+    for (int64_t k = beg; k < end; k++) {
+        const uint32_t row = ev.row(k);
+        bool hit = false;
+        if (has_last) {
+            const NfVal x3 = s3_val(C, Q.s3_a3, Q.s3_t3, row);
+            hit = !x3.null && !lastv.null && nf_cmp(Q.s3_op3, Q.s3_dom3, x3, lastv);
+        }
+        if (hit) {
+            uint64_t* r = sink.slot(0);
+            if (!r) {
+                fail = true;
+                break;
+            }
+            const uint32_t loc = ev.local(k);
+            r[0] = (uint64_t)loc;
+            r[1] = (uint64_t)ev.ts(k);
+            uint64_t nulls = 0;
+            for (int o = 0; o < Q.n_out; o++) {
+                const int sl = Q.s3_out_slot[o];
+                const NfVal v = s3_val(C, Q.s3_out_attr[o], Q.s3_out_type[o], sl == 0 ? e1_row : sl == 1 ? last_row : row);
+                r[NF_REC_HDR + o] = (uint64_t)v.b;
+                if (v.null) nulls |= 1ull << o;
+            }
+            r[2] = nulls;  // query 0
+            r[3] = ev.seq(k);
+            EM.match_cnt[loc] = 1;
+        }
+        const NfVal x2 = s3_val(C, Q.s3_a2, Q.s3_t2, row);
+        if (!hit && k > (int64_t)beg && !x2.null && !e1v.null && nf_cmp(Q.s3_op2, Q.s3_dom2, x2, e1v)) {
+            has_last = true;
+            last_row = row;
+            lastv = s3_val(C, Q.s3_la, Q.s3_lt, row);
+        } else {
+            has_last = false;
+            e1_row = row;
+            e1v = s3_val(C, Q.s3_e1a, Q.s3_e1t, row);
+        }
+    }
+    if (sink.chunk) sink.finish();
+    if (fail) atomicOr(EM.err, (unsigned)NF_E_EMIT);
+}
+
 // unpartitioned apps: StateStreamRuntime.initPartition at SiddhiAppRuntime.start
 __global__ void k_nfa_start(const nf_table* __restrict__ T, const nf_cols* __restrict__ C, uint64_t* __restrict__ kstate,
                             uint64_t tick, int64_t clock, nfd_emit EM) {
@@ -411,6 +509,25 @@ extern "C" int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, 
     if (max_segments < 1) max_segments = 1;
     hipLaunchKernelGGL(k_nfa_run, dim3(nf_blocks(max_segments, NF_TPB)), dim3(NF_TPB), 0, (hipStream_t)stream, dT, dC,
                        kstate, E, n, seg_list, nseg, skeys, nkeys, tick, clock, *em);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int nfd_seq3(const nf_table* dT, const nf_cols* dC, const nfd_events* ev, int64_t n,
+                        const uint32_t* seg_list, const uint32_t* nseg, const uint32_t* skeys, int32_t nkeys,
+                        int64_t max_segments, const nfd_emit* em, void* stream) {
+    DevEvents E;
+    E.ts = ev->ts;
+    E.stream = ev->stream;
+    E.row = ev->row;
+    E.bid = ev->bid;
+    E.perm = ev->perm;
+    E.seq_base = ev->seq_base;
+    E.batch_events = ev->batch_events;
+    E.sts = ev->sts;
+    E.sorted_rows = ev->sorted_rows;
+    if (max_segments < 1) max_segments = 1;
+    hipLaunchKernelGGL(k_seq3, dim3(nf_blocks(max_segments, NF_TPB)), dim3(NF_TPB), 0, (hipStream_t)stream, dT, dC, E,
+                       n, seg_list, nseg, skeys, nkeys, *em);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -383,6 +384,104 @@ struct QueryLowering {
         return false;
     }
 
+    // The rise-and-fall sequence (C3's shape):
+    //   from every e1=S, e2=S[x.a op2 e1.b]+, e3=S[x.c op3 e2[last].d]
+    // SEQUENCE keeps at most one partial per state (StreamPreStateProcessor /
+    // CountPreStateProcessor.addState add to an empty new-and-every list only,
+    // resetState clears every pending list per event), the e3 match sets slot 2
+    // of the shared StateEvent before the count state sees it and drops it
+    // (CountPreStateProcessor.java:60-68), and `every` re-arms e1 at every event.
+    // Per key this is one partial (e1, last e2) — k_seq3 (sh_nfa.hip) runs it.
+    void detect_seq3() {
+        Q->s3 = 0;
+        if (q->state_type != SH_SEQUENCE || q->within_ms >= 0 || q->n_slots != 3 || q->n_outputs < 1) return;
+        // flatten the NEXT chain
+        std::vector<int> chain;
+        std::function<bool(int)> flat = [&](int e) -> bool {
+            if (e < 0 || e >= q->n_elems) return false;
+            const sh_state_elem& x = q->elems[e];
+            if (x.kind == SH_E_NEXT) return flat(x.child0) && flat(x.child1);
+            chain.push_back(e);
+            return true;
+        };
+        if (!flat(q->root) || chain.size() != 3) return;
+        const sh_state_elem& ev = q->elems[chain[0]];
+        const sh_state_elem& cn = q->elems[chain[1]];
+        const sh_state_elem& c3 = q->elems[chain[2]];
+        if (ev.kind != SH_E_EVERY || cn.kind != SH_E_COUNT || c3.kind != SH_E_STREAM) return;
+        if (ev.child0 < 0 || cn.child0 < 0) return;
+        const sh_state_elem& a = q->elems[ev.child0];
+        const sh_state_elem& b = q->elems[cn.child0];
+        if (a.kind != SH_E_STREAM || b.kind != SH_E_STREAM || a.filter >= 0 || b.filter < 0 || c3.filter < 0) return;
+        if (a.slot != 0 || b.slot != 1 || c3.slot != 2 || a.stream != b.stream || b.stream != c3.stream) return;
+        if (cn.min_count != 1 || cn.max_count != SH_ANY) return;
+        auto var = [&](int e, int slot, bool current_only, int* attr, int* type) {
+            if (e < 0 || e >= q->n_exprs) return false;
+            const sh_expr& x = q->exprs[e];
+            if (x.op != SH_OP_VAR || x.slot != slot || x.type == SH_T_OBJECT) return false;
+            if (current_only ? x.chain != SH_CHAIN_CURRENT : (x.chain != 0 && x.chain != SH_CHAIN_CURRENT)) return false;
+            *attr = x.attr;
+            *type = x.type;
+            return true;
+        };
+        auto mirror = [](int op) {
+            switch (op) {
+                case SH_OP_GT: return (int)SH_OP_LT;
+                case SH_OP_GE: return (int)SH_OP_LE;
+                case SH_OP_LT: return (int)SH_OP_GT;
+                case SH_OP_LE: return (int)SH_OP_GE;
+                default: return op;
+            }
+        };
+        // filter = CMP(x.attr of `self` slot, other slot's attr), either operand order
+        auto cmpf = [&](int e, int self, int other, bool other_current, int* op, int* xa, int* xt, int* oa, int* ot) {
+            if (e < 0 || e >= q->n_exprs) return false;
+            const sh_expr& x = q->exprs[e];
+            if (x.op < SH_OP_EQ || x.op > SH_OP_LE) return false;
+            if (var(x.lhs, self, false, xa, xt) && var(x.rhs, other, other_current, oa, ot)) {
+                *op = x.op;
+                return true;
+            }
+            if (var(x.rhs, self, false, xa, xt) && var(x.lhs, other, other_current, oa, ot)) {
+                *op = mirror(x.op);
+                return true;
+            }
+            return false;
+        };
+        int op2, a2, t2, e1a, e1t, op3, a3, t3, la, lt;
+        // the e2 event inside its own filter is the chain's current event
+        if (!cmpf(b.filter, 1, 0, false, &op2, &a2, &t2, &e1a, &e1t)) return;
+        if (q->exprs[q->exprs[b.filter].lhs].slot == 1 ? q->exprs[q->exprs[b.filter].lhs].chain != SH_CHAIN_CURRENT
+                                                       : q->exprs[q->exprs[b.filter].rhs].chain != SH_CHAIN_CURRENT)
+            return;
+        if (!cmpf(c3.filter, 2, 1, true, &op3, &a3, &t3, &la, &lt)) return;
+        if (q->n_outputs > NF_MAX_OUT) return;
+        for (int o = 0; o < q->n_outputs; o++) {
+            const sh_output_attr& oa = q->outputs[o];
+            if (oa.agg != SH_AGG_NONE || oa.expr < 0) return;
+            const sh_expr& x = q->exprs[oa.expr];
+            int at, ty;
+            if (x.op != SH_OP_VAR || x.slot < 0 || x.slot > 2) return;
+            if (!var(oa.expr, x.slot, x.slot == 1, &at, &ty)) return;
+            Q->s3_out_slot[o] = (int8_t)x.slot;
+            Q->s3_out_attr[o] = (int8_t)at;
+            Q->s3_out_type[o] = (int8_t)ty;
+        }
+        Q->s3_op2 = (int8_t)op2;
+        Q->s3_dom2 = (int8_t)dom_for(op2, t2, e1t);
+        Q->s3_a2 = (int8_t)a2;
+        Q->s3_t2 = (int8_t)t2;
+        Q->s3_e1a = (int8_t)e1a;
+        Q->s3_e1t = (int8_t)e1t;
+        Q->s3_op3 = (int8_t)op3;
+        Q->s3_dom3 = (int8_t)dom_for(op3, t3, lt);
+        Q->s3_a3 = (int8_t)a3;
+        Q->s3_t3 = (int8_t)t3;
+        Q->s3_la = (int8_t)la;
+        Q->s3_lt = (int8_t)lt;
+        Q->s3 = 1;
+    }
+
     bool run() {
         memset(Q, 0, sizeof(*Q));
         Q->state_type = q->state_type;
@@ -485,6 +584,7 @@ struct QueryLowering {
             err = "device engine: at most 16 output attributes";
             return false;
         }
+        detect_seq3();
         Q->n_out = q->n_outputs;
         for (int o = 0; o < q->n_outputs; o++) {
             const sh_output_attr& oa = q->outputs[o];

@@ -69,6 +69,10 @@ class DeviceRunner:
         """1: the last run took the bucketed window engine (sh_bucket.hip)."""
         return lib().shx_bucket_status(self.handle.h)
 
+    def seq3_status(self):
+        """1: the last run took the rise-and-fall sequence engine (k_seq3)."""
+        return lib().shx_seq3_status(self.handle.h)
+
     def last_error(self):
         return lib().sh_last_error(self.handle.h).decode()
 

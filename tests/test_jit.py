@@ -78,3 +78,24 @@ def test_random_window_queries_bucket_compile(lib, seed):
     rc = lib.shx_bucket_compile(h, None, 0)
     assert rc in (abi.SH_OK, abi.SH_E_UNSUPPORTED), (app, lib.sh_last_error(h))
     lib.sh_destroy(h)
+
+
+def test_c3_has_the_rise_and_fall_sequence_shape(lib):
+    """C3 lowers to the k_seq3 engine; near misses (a filter on e1, `within`,
+    e2[last] read from a different position) stay on the general engine"""
+    h = _handle(lib, synth.C3_QUERY)
+    assert lib.shx_seq3_shape(h) == 1
+    lib.sh_destroy(h)
+    base = ("define stream S (symbol string, price float, volume long); partition with (symbol of S) begin "
+            "from every e1=S{e1f}, e2=S[price>e1.price]+, e3=S[price<e2[last].price]{w} "
+            "select e1.price as p1, e2[last].price as peak, e3.price as p3 insert into Out; end;")
+    for e1f, w, want in [("", "", 1), ("[price > 1.0f]", "", 0), ("", " within 1 sec", 0)]:
+        h = _handle(lib, base.format(e1f=e1f, w=w))
+        assert lib.shx_seq3_shape(h) == want, (e1f, w)
+        lib.sh_destroy(h)
+    mixed = ("define stream S (symbol string, price float, volume long); partition with (symbol of S) begin "
+             "from every e1=S, e2=S[volume >= e1.volume]+, e3=S[e2[last].price > price] "
+             "select e3.volume as v3, e1.symbol as s, e2[last].volume as lv insert into Out; end;")
+    h = _handle(lib, mixed)
+    assert lib.shx_seq3_shape(h) == 1
+    lib.sh_destroy(h)
