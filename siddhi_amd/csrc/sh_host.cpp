@@ -1370,7 +1370,8 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
 }
 
 // one or more send() calls resident on the device, processed by k_nfa_run
-static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid, int* alias);
+static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid, int* alias,
+                       bool used_only = false);
 
 // `carry` (sh_run_device, single stream): ts and the stream-0 columns are moved
 // into key-segment order by the segment, so each lane streams its own events
@@ -1394,8 +1395,9 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     int alias = -1;
     const bool sorted_cols = carry_run && B.keys && h->stream_types[0].size() <= 7;
     if (sorted_cols) {
-        if (carry_setup(h, carry_run, &carry, mid, &alias)) return fail(h, SH_E_OOM, "sorted columns");
-        for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = h->v_scol[a].p;
+        if (carry_setup(h, carry_run, &carry, mid, &alias, true)) return fail(h, SH_E_OOM, "sorted columns");
+        for (size_t a = 0; a < h->stream_types[0].size(); a++)
+            if (a >= 32 || ((h->T->attr_used[0] >> a) & 1u)) cols.col[0][a] = h->v_scol[a].p;
     }
     shd_segment_ws ws;
     ws.keys_a = h->w_keys_a.as<uint32_t>();
@@ -1444,7 +1446,8 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
                 // the buffer moved: refresh the column image
                 cols = nf_store_cols(h);
                 if (sorted_cols) {
-                    for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = h->v_scol[a].p;
+                    for (size_t a = 0; a < h->stream_types[0].size(); a++)
+                        if (a >= 32 || ((h->T->attr_used[0] >> a) & 1u)) cols.col[0][a] = h->v_scol[a].p;
                     if (alias >= 0) cols.col[0][alias] = skeys;
                 }
                 nf_put_cols(h, cols);
@@ -1916,7 +1919,8 @@ static shd_segment_ws seg_ws(sh_handle* h, int64_t n) {
 // as the same device buffer) is not carried: its key-segment order is the
 // sorted key array (*alias = that attribute, -1 if none). Null-key events
 // (sorted to the sentinel bucket) are never read.
-static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid, int* alias) {
+static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid, int* alias,
+                       bool used_only) {
     const int64_t n = run->n;
     const int na = (int)h->stream_types[0].size();
     memset(carry, 0, sizeof(*carry));
@@ -1929,6 +1933,7 @@ static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carr
     mid[c++] = h->v_mid_ts.p;
     for (int a = 0; a < na; a++) {
         const int w = type_width(h->stream_types[0][a]);
+        if (used_only && h->T && a < 32 && !((h->T->attr_used[0] >> a) & 1u)) continue;  // no expression reads it
         if (*alias < 0 && w == 4 && run->d_cols[a] == (const void*)run->d_keys && !getenv("SH_NO_KEY_ALIAS")) {
             *alias = a;
             continue;

@@ -745,14 +745,28 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     else
         cand += "ok = ok && !hasM;\n";
     std::string mid = "bool mk = true;\n" + gi.terms(F.qonly, "mk");
+    // unguarded (straight-line) forms for the predicated fast walk: the guarded
+    // blocks only compute values, so they may run for every element
+    auto unguard = [](std::string t) {
+        for (const char* g : {"if (ok) {", "if (mk) {"}) {
+            size_t at;
+            while ((at = t.find(g)) != std::string::npos) t.replace(at, strlen(g), "{");
+        }
+        return t;
+    };
+    const std::string cand_fast = unguard(cand);
+    std::string mid_fast = "bool mk = true;\n" + unguard(gi.terms(F.qonly, "mk"));
     std::string stop, stop_cond;
     if (F.cross) {
         const bool mx = F.op == SH_OP_GT || F.op == SH_OP_GE;
         mid += "if (mk) {\n" + gi.xval(F, "xr") + "if (xr == xr && (!hasM || xr " + (mx ? ">" : "<") +
                " M)) M = xr;\nif (xr == xr) hasM = true;\n}\n";
         stop_cond = std::string("xq != xq || (hasM && M ") + (mx ? ">=" : "<=") + " xq)";
+        mid_fast += "{\n" + unguard(gi.xval(F, "xr")) + "const uint32_t upd = (act && mk && xr == xr) ? 1u : 0u;\nM = (upd && (!hasM || xr " +
+                    (mx ? ">" : "<") + " M)) ? xr : M;\nhasM |= upd;\n}\n";
     } else {
         mid += "if (mk) hasM = true;\n";
+        mid_fast += "hasM |= (act && mk) ? 1u : 0u;\n";
         stop_cond = "hasM";
     }
     stop = "    if (" + stop_cond + ") { stopped = true; break; }\n";
@@ -794,8 +808,8 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
         return "const uint32_t wq = s_ws[sp];\nconst uint32_t key = wq & kmask;\n"
                "const int64_t tq = (int64_t)(wq >> kb);\n" +
                decl_attrs(need_r, 0) + decl_attrs(need_q, 1) + loads(need_q, "x1_", "sp") + DT + " xq = 0;\n" +
-               qhead + "bool hasM = false;\n" + DT + " M = 0;\nbool first = true;\n"
-               "bool stopped = !qok, ran_off = false;\n";
+               qhead + "uint32_t hasM = 0u;\n" + DT + " M = 0;\nuint32_t first = 1u;\n"
+               "uint32_t stopped = qok ? 0u : 1u, ran_off = 0u;\n";
     };
     auto slow = [&](bool count, const std::string& on_consumed, const std::string& from) {
         return "for (int o = " + from + "; !stopped && !ran_off; o--) {\n" +
@@ -811,18 +825,23 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
         // break-free: a `live` predicate instead of early exits, so the unrolled
         // loop compiles to straight-line vector code (no exec-mask juggling on
         // the CU's shared scalar unit)
-        s += "}\nbool live = true, mono = false;\n#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n"
+        // the loop-carried flags are 0/1 words (vector registers), not lane masks
+        s += "}\nuint32_t live = 1u, mono = 0u;\n#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n"
              "    const int o = sp - 1 - u;\n"
-             "    const bool same = o >= 0 && (wv[u] & kmask) == key;\n"
+             "    const uint32_t same = (o >= 0 && (wv[u] & kmask) == key) ? 1u : 0u;\n"
              "    const int64_t tr = (int64_t)(wv[u] >> kb);\n"
-             "    if (live && !same) { live = false; ran_off = true; }\n"
-             "    if (live && tq - tr > SHJ_W) { live = false; stopped = true; }\n"
-             "    if (live && first && tq < tr) mono = true;\n"
-             "    if (live) {\n    first = false;\n";
+             "    const uint32_t inwin = (tq - tr <= SHJ_W) ? 1u : 0u;\n"
+             "    ran_off |= live & (same ^ 1u);\n"
+             "    stopped |= live & same & (inwin ^ 1u);\n"
+             "    const uint32_t act = live & same & inwin;\n"
+             "    mono |= act & first & ((tq < tr) ? 1u : 0u);\n"
+             "    first &= act ^ 1u;\n";
         for (int a : need_r)
             s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
-        s += "    {\n" + cand + "    if (ok) {\n        c_++;\n        mask |= 1u << u;\n    }\n    }\n";
-        s += "    {\n" + mid + "    }\n    if (" + stop_cond + ") { stopped = true; live = false; }\n    }\n}\n"
+        s += "    {\n" + cand_fast +
+             "    const uint32_t cons = act & (ok ? 1u : 0u);\n    c_ += cons;\n    mask |= cons << u;\n    }\n";
+        s += "    {\n" + mid_fast + "    }\n    {\n    const uint32_t st = (act && (" + stop_cond +
+             ")) ? 1u : 0u;\n    stopped |= st;\n    live = act & (st ^ 1u);\n    }\n}\n"
              "if (mono) atomicOr(P.flag, SHB_F_MONO);\n";
         s += "}\nif (!stopped && !ran_off) {\n    mask = SHB_MOVF;\n" +
              slow(true, "        c_++;\n", "sp - 1 - SHB_D") + "}\n";
@@ -841,10 +860,10 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     (void)sidx;
 
     src = SHJ_HEADERS;
-    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_TPB 512\n#define SHB_D 15\n#define SHB_MOVF 0x8000u\n"
+    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_TPB 512\n#define SHB_D 10\n#define SHB_MOVF 0x8000u\n"
            "#define SHB_NR (SHB_SPAN / SHB_TPB)\nstatic_assert(SHB_SPAN % SHB_TPB == 0, \"span\");\n";
     src += R"(
-extern "C" __global__ void __launch_bounds__(SHB_TPB) shb_match(shb_plan P) {
+extern "C" __global__ void __launch_bounds__(SHB_TPB, 4) shb_match(shb_plan P) {
 __shared__ uint32_t s_ws[SHB_SPAN];
 __shared__ uint16_t s_idx[SHB_SPAN];
 __shared__ uint16_t s_pre[SHB_CH];

@@ -152,6 +152,7 @@ struct nf_table {
     int32_t pad;
     int64_t key_words;      // words per key block: 1 header word + every query block
     int32_t stream_nattr[NF_MAX_STREAMS];
+    uint32_t attr_used[NF_MAX_STREAMS];  // attributes any filter / select reads (bit per attribute)
     int8_t attr_type[NF_MAX_STREAMS][NF_MAX_ATTRS];
     int32_t n_code, n_const;
     shp_instr code[NF_MAX_CODE];

@@ -156,24 +156,34 @@ __device__ __forceinline__ NfVal s3_val(const nf_cols* C, int a, int t, uint32_t
     return v;
 }
 
+#define S3_U 8
 __global__ void __launch_bounds__(NF_TPB) k_seq3(const nf_table* __restrict__ T, const nf_cols* __restrict__ C,
                                                  DevEvents E, int64_t n, const uint32_t* __restrict__ seg_list,
                                                  const uint32_t* __restrict__ nseg,
                                                  const uint32_t* __restrict__ skeys, int32_t nkeys, nfd_emit EM) {
     const uint32_t sidx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (sidx >= *nseg) return;
+    const uint32_t ns = *nseg;
+    if (sidx >= ns) return;
     const uint32_t beg = seg_list[sidx];
     const uint32_t key = skeys ? skeys[beg] : 0u;
     if (key >= (uint32_t)nkeys) {
         atomicOr(EM.err, (unsigned)NF_E_KEY);
         return;
     }
-    int64_t end = beg + 1;
-    if (skeys)
-        while (end < n && skeys[end] == key) end++;
-    else
+    // segments are listed in order; only the last one may be followed by the
+    // null-key run
+    int64_t end;
+    if (!skeys) {
         end = n;
+    } else if (sidx + 1 < ns) {
+        end = seg_list[sidx + 1];
+    } else {
+        end = beg + 1;
+        while (end < n && skeys[end] == key) end++;
+    }
     const nf_query& Q = T->q[0];
+    const bool same2 = Q.s3_e1a == Q.s3_a2 && Q.s3_e1t == Q.s3_t2;  // e1's operand is x's f2 operand
+    const bool same3 = Q.s3_la == Q.s3_a3 && Q.s3_lt == Q.s3_t3;
     DevSink sink;
     sink.buf = EM.recs;
     sink.ctr = EM.ctr;
@@ -182,49 +192,60 @@ __global__ void __launch_bounds__(NF_TPB) k_seq3(const nf_table* __restrict__ T,
     sink.chunk = nullptr;
     sink.used = sink.n = 0;
     DevEv ev{&E};
-    bool has_last = false;
+    bool has_last = false, has_e1 = false;
     uint32_t e1_row = 0, last_row = 0;
     NfVal e1v, lastv;
     e1v.b = lastv.b = 0;
     e1v.t = lastv.t = 0;
     e1v.null = lastv.null = 1;
     bool fail = false;
-    for (int64_t k = beg; k < end; k++) {
-        const uint32_t row = ev.row(k);
-        bool hit = false;
-        if (has_last) {
-            const NfVal x3 = s3_val(C, Q.s3_a3, Q.s3_t3, row);
-            hit = !x3.null && !lastv.null && nf_cmp(Q.s3_op3, Q.s3_dom3, x3, lastv);
+    for (int64_t k0 = beg; k0 < end && !fail; k0 += S3_U) {
+        // the block's operands together (independent loads in flight)
+        NfVal x2v[S3_U], x3v[S3_U];
+#pragma unroll
+        for (int u = 0; u < S3_U; u++) {
+            const int64_t k = k0 + u < end ? k0 + u : end - 1;
+            const uint32_t row = ev.row(k);
+            x2v[u] = s3_val(C, Q.s3_a2, Q.s3_t2, row);
+            x3v[u] = s3_val(C, Q.s3_a3, Q.s3_t3, row);
         }
-        if (hit) {
-            uint64_t* r = sink.slot(0);
-            if (!r) {
-                fail = true;
-                break;
+#pragma unroll
+        for (int u = 0; u < S3_U; u++) {
+            const int64_t k = k0 + u;
+            if (k >= end) break;
+            const uint32_t row = ev.row(k);
+            const bool hit = has_last && !x3v[u].null && !lastv.null && nf_cmp(Q.s3_op3, Q.s3_dom3, x3v[u], lastv);
+            if (hit) {
+                uint64_t* r = sink.slot(0);
+                if (!r) {
+                    fail = true;
+                    break;
+                }
+                const uint32_t loc = ev.local(k);
+                r[0] = (uint64_t)loc;
+                r[1] = (uint64_t)ev.ts(k);
+                uint64_t nulls = 0;
+                for (int o = 0; o < Q.n_out; o++) {
+                    const int sl = Q.s3_out_slot[o];
+                    const NfVal v =
+                        s3_val(C, Q.s3_out_attr[o], Q.s3_out_type[o], sl == 0 ? e1_row : sl == 1 ? last_row : row);
+                    r[NF_REC_HDR + o] = (uint64_t)v.b;
+                    if (v.null) nulls |= 1ull << o;
+                }
+                r[2] = nulls;  // query 0
+                r[3] = ev.seq(k);
+                EM.match_cnt[loc] = 1;
             }
-            const uint32_t loc = ev.local(k);
-            r[0] = (uint64_t)loc;
-            r[1] = (uint64_t)ev.ts(k);
-            uint64_t nulls = 0;
-            for (int o = 0; o < Q.n_out; o++) {
-                const int sl = Q.s3_out_slot[o];
-                const NfVal v = s3_val(C, Q.s3_out_attr[o], Q.s3_out_type[o], sl == 0 ? e1_row : sl == 1 ? last_row : row);
-                r[NF_REC_HDR + o] = (uint64_t)v.b;
-                if (v.null) nulls |= 1ull << o;
+            if (!hit && has_e1 && !x2v[u].null && !e1v.null && nf_cmp(Q.s3_op2, Q.s3_dom2, x2v[u], e1v)) {
+                has_last = true;
+                last_row = row;
+                lastv = same3 ? x3v[u] : s3_val(C, Q.s3_la, Q.s3_lt, row);
+            } else {
+                has_last = false;
+                has_e1 = true;
+                e1_row = row;
+                e1v = same2 ? x2v[u] : s3_val(C, Q.s3_e1a, Q.s3_e1t, row);
             }
-            r[2] = nulls;  // query 0
-            r[3] = ev.seq(k);
-            EM.match_cnt[loc] = 1;
-        }
-        const NfVal x2 = s3_val(C, Q.s3_a2, Q.s3_t2, row);
-        if (!hit && k > (int64_t)beg && !x2.null && !e1v.null && nf_cmp(Q.s3_op2, Q.s3_dom2, x2, e1v)) {
-            has_last = true;
-            last_row = row;
-            lastv = s3_val(C, Q.s3_la, Q.s3_lt, row);
-        } else {
-            has_last = false;
-            e1_row = row;
-            e1v = s3_val(C, Q.s3_e1a, Q.s3_e1t, row);
         }
     }
     if (sink.chunk) sink.finish();

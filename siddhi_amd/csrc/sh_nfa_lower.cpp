@@ -640,6 +640,21 @@ int nf_lower(const sh_app_desc* app, nf_table* T, std::string* err) {
         return -1;
     }
     T->partitioned = np > 0;
+    // attributes read by any expression (sh_run_device carries only these through the segment)
+    for (int i = 0; i < app->n_queries; i++) {
+        const sh_query_desc& qd = app->queries[i];
+        std::vector<int> slot_stream(qd.n_slots > 0 ? qd.n_slots : 1, -1);
+        for (int e = 0; e < qd.n_elems; e++)
+            if ((qd.elems[e].kind == SH_E_STREAM || qd.elems[e].kind == SH_E_ABSENT_STREAM) && qd.elems[e].slot >= 0 &&
+                qd.elems[e].slot < qd.n_slots)
+                slot_stream[qd.elems[e].slot] = qd.elems[e].stream;
+        for (int x = 0; x < qd.n_exprs; x++) {
+            const sh_expr& ex = qd.exprs[x];
+            if (ex.op != SH_OP_VAR || ex.slot < 0 || ex.slot >= qd.n_slots || ex.attr < 0 || ex.attr >= 32) continue;
+            const int st = slot_stream[ex.slot];
+            if (st >= 0 && st < NF_MAX_STREAMS) T->attr_used[st] |= 1u << ex.attr;
+        }
+    }
     for (int i = 0; i < app->n_queries; i++) {
         QueryLowering L;
         L.app = app;

@@ -1,0 +1,76 @@
+"""C3 (BASELINE.json configs[2]) on the rise-and-fall sequence engine (k_seq3,
+sh_nfa.hip) through sh_run_device: bit-exact against the oracle at 300k events
+(with price ties), against the vectorised restatement tests/c3_check.py
+(pinned to the oracle in tests/test_c3_checker.py) at the full 100M events /
+1M keys, and the general engine on the same input (SH_NO_SEQ3) for the shape's
+near relatives."""
+import os
+
+import numpy as np
+import pytest
+
+from c3_check import c3_expected
+from oracle_engine import run_columns_oracle, run_stock_oracle
+from siddhi_amd import compiler, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _gpu(text, ts, cols, keys, nk):
+    import torch
+    from siddhi_amd.device_run import DeviceRunner
+    runner = DeviceRunner(compiler.compile_app(text))
+    dev = torch.device("cuda:0")
+    m, oseq, ovals = runner.run(torch.from_numpy(ts).to(dev), torch.from_numpy(keys).to(dev),
+                                [torch.from_numpy(c).to(dev) for c in cols], nk)
+    torch.cuda.synchronize()
+    r = (oseq.cpu().numpy(), ovals.cpu().numpy(), runner.seq3_status())
+    runner.close()
+    return r
+
+
+@pytest.mark.parametrize("ties,engine", [(False, "seq3"), (True, "seq3"), (False, "general")])
+def test_c3_vs_oracle(ties, engine, monkeypatch):
+    if engine == "general":
+        monkeypatch.setenv("SH_NO_SEQ3", "1")
+    n, nk = 300_000, 5_000
+    ts, k, p, v = synth.stock_stream(n, nk, 1000, config_index=3)
+    if ties:
+        p = np.random.default_rng(3).integers(0, 5, n).astype(np.float32)
+    seq, _, vals, _ = run_stock_oracle(compiler.compile_app(synth.C3_QUERY), ts, k, p, v)
+    gseq, gvals, st = _gpu(synth.C3_QUERY, ts, [k, p, v], k, nk)
+    assert st == (1 if engine == "seq3" else 0)
+    assert len(gseq) == len(seq) > 0
+    assert np.array_equal(gseq, seq.astype(np.int64)) and np.array_equal(gvals, vals)
+
+
+def test_c3_full_size_vs_restatement():
+    n, nk = 100_000_000, 1_000_000
+    ts, k, p, v = synth.stock_stream(n, nk, 1000, config_index=3)
+    gseq, gvals, st = _gpu(synth.C3_QUERY, ts, [k, p, v], k, nk)
+    assert st == 1
+    eseq, evals = c3_expected(ts, k, p)
+    assert len(gseq) == len(eseq) > 0
+    assert np.array_equal(gseq, eseq) and np.array_equal(gvals, evals)
+
+
+def test_mixed_attribute_shape_vs_oracle():
+    """other attributes / operators / select columns of the same shape"""
+    text = ("define stream S (symbol string, price float, volume long); partition with (symbol of S) begin "
+            "from every e1=S, e2=S[volume >= e1.volume]+, e3=S[e2[last].price > price] "
+            "select e3.volume as v3, e1.symbol as s, e2[last].volume as lv, e1.price as p1 insert into Out; end;")
+    n, nk = 200_000, 3_000
+    ts, k, p, v = synth.stock_stream(n, nk, 100, config_index=3)
+    v = np.random.default_rng(9).integers(0, 4, n).astype(np.int64)
+    seq, _, vals, _ = run_columns_oracle(compiler.compile_app(text), ts, [k, p, v], k)
+    gseq, gvals, st = _gpu(text, ts, [k, p, v], k, nk)
+    assert st == 1
+    assert len(gseq) == len(seq) > 0
+    assert np.array_equal(gseq, seq.astype(np.int64)) and np.array_equal(gvals, vals)
