@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--rate", type=int, default=100)
     ap.add_argument("--cpu-sample", type=int, default=2_000_000,
                     help="events of the same workload timed on the CPU oracle (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads for partitioned configs without timers (events split by key; "
+                         "0 = 1 thread, except C5: min(16, nproc))")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default, BASELINE.json configs[1]); c1 / c3 / c4 / c5 measure the other configs")
@@ -92,14 +95,15 @@ def workload(args, rank):
             return bool(np.array_equal(oseq, eseq) and np.array_equal(oq, erule)
                         and np.array_equal(ovals[:, :2], evals))
 
-        def cpu(s):
+        def cpu(s, idx=None):
             sys.path.insert(0, os.path.join(HERE, "tests"))
             from oracle_engine import run_columns_oracle
-            run_columns_oracle(compiled, ts[:s], [card[:s], amount[:s], merchant[:s]], card[:s], batch=4096)
+            ix = np.arange(s) if idx is None else idx
+            run_columns_oracle(compiled, ts[ix], [card[ix], amount[ix], merchant[ix]], card[ix], batch=4096)
 
         return dict(
             ts=ts, keys=card, cols=[card, amount, merchant], compiled=compiled, verify=verify, cpu=cpu,
-            b_event=20, b_match=20, cpu_sample=min(args.cpu_sample, 4096),
+            b_event=20, b_match=20, cpu_sample=min(args.cpu_sample, 1_000_000), cpu_split=True,
             desc=f"C5: {args.rules} fraud rules `every e1=Txn[amount > A and merchant == M] -> "
                  f"e2=Txn[card == e1.card and amount > e1.amount * F] within W sec`, one partition (card of Txn)",
             key_name="cards_per_gpu", bytes_note="event: ts 8 + card 4 + amount 4 + merchant 4 = 20 B; "
@@ -136,13 +140,14 @@ def workload(args, rank):
             eseq, evals = c3_expected(ts, keys, price)
             return bool(len(oseq) == len(eseq) and np.array_equal(oseq, eseq) and np.array_equal(ovals, evals))
 
-        def cpu(s):
+        def cpu(s, idx=None):
             sys.path.insert(0, os.path.join(HERE, "tests"))
             from oracle_engine import run_stock_oracle
-            run_stock_oracle(compiled, ts[:s], keys[:s], price[:s], vol[:s], batch=4096)
+            ix = np.arange(s) if idx is None else idx
+            run_stock_oracle(compiled, ts[ix], keys[ix], price[ix], vol[ix], batch=4096)
 
         return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, verify=verify, cpu=cpu,
-                    b_event=16, b_match=20, cpu_sample=args.cpu_sample,
+                    b_event=16, b_match=20, cpu_sample=args.cpu_sample, cpu_split=True,
                     desc="C3: every e1=S, e2=S[price>e1.price]+, e3=S[price<e2[last].price], "
                          "partition with (symbol of S)", key_name="keys_per_gpu",
                     bytes_note="event: ts 8 + symbol 4 + price 4 = 16 B; match: seq 8 + 3 x price 4 = 20 B")
@@ -154,13 +159,14 @@ def workload(args, rank):
         eseq, evals = c2_expected(ts, keys, price, vol)
         return bool(len(oseq) == len(eseq) and np.array_equal(oseq, eseq) and np.array_equal(ovals, evals))
 
-    def cpu(s):
+    def cpu(s, idx=None):
         sys.path.insert(0, os.path.join(HERE, "tests"))
         from oracle_engine import run_stock_oracle
-        run_stock_oracle(compiled, ts[:s], keys[:s], price[:s], vol[:s], batch=4096)
+        ix = np.arange(s) if idx is None else idx
+        run_stock_oracle(compiled, ts[ix], keys[ix], price[ix], vol[ix], batch=4096)
 
     return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, verify=verify, cpu=cpu,
-                b_event=24, b_match=28, cpu_sample=args.cpu_sample,
+                b_event=24, b_match=28, cpu_sample=args.cpu_sample, cpu_split=True,
                 desc="C2: every e1[price>20] -> e2[symbol==e1.symbol and price>e1.price] within 1 sec, "
                      "partition with (symbol of StockStream)", key_name="symbols_per_gpu",
                 bytes_note="event: ts 8 + symbol 4 + price 4 + volume 8 = 24 B; "
@@ -419,13 +425,27 @@ def main():
     cpu = None
     if rank == 0 and args.cpu_sample > 0:
         s = min(W["cpu_sample"], n)
-        log(f"CPU baseline on {s} events")
+        threads = args.cpu_threads or (min(16, os.cpu_count() or 1) if args.config == "c5" else 1)
+        if not W.get("cpu_split"):
+            threads = 1
+        log(f"CPU baseline on {s} events, {threads} thread(s)")
         t1 = time.perf_counter()
-        W["cpu"](s)
+        if threads == 1:
+            W["cpu"](s)
+        else:
+            # partitions are independent (no timers): the sample's events split by
+            # key over threads, each with its own oracle instance (ctypes releases
+            # the GIL inside the restatement)
+            from concurrent.futures import ThreadPoolExecutor
+            part = W["keys"][:s] % threads
+            idxs = [np.flatnonzero(part == t) for t in range(threads)]
+            with ThreadPoolExecutor(threads) as ex:
+                list(ex.map(lambda ix: W["cpu"](s, ix), idxs))
         cdt = time.perf_counter() - t1
-        cpu = {"value": s / cdt, "unit": "events/s", "cores": 1, "kind": "port",
+        cpu = {"value": s / cdt, "unit": "events/s", "cores": threads, "kind": "port",
                "sample": f"first {s} events of the same {args.config.upper()} stream, send(Event[]) batches of "
-                         f"4096, C++ restatement of siddhi-core's processors (oracle/), 1 thread"}
+                         f"4096, C++ restatement of siddhi-core's processors (oracle/), {threads} thread(s)"
+                         + (" over key-disjoint sub-streams" if threads > 1 else "")}
 
     if rank == 0:
         line = {

@@ -18,3 +18,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
     python bench.py --config c3 --steps 3 --warmup 1 --cpu-sample 0 --no-verify > gpurun_out/prof_c3/bench.log 2>&1
 echo "c3 prof rc=$?"
 grep '^{' gpurun_out/prof_c3/bench.log | cut -c1-300
+# PMC: calibration streams, then the C2 step (separate passes per counter)
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_cal_$c -o cal -- python scripts/pmc_calib.py > gpurun_out/pmc_cal_$c.log 2>&1 || { echo "cal $c failed"; exit 1; }
+done
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_c2_$c -o c2 -- python bench.py --steps 1 --warmup 0 --cpu-sample 0 --no-verify > gpurun_out/pmc_c2_$c.log 2>&1 || { echo "pmc $c failed"; exit 1; }
+done
+echo "pmc done"

@@ -345,12 +345,20 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
                 if (!out_vals) continue;
                 // output descriptors straight from the kernel arguments (scalar
                 // registers: uniform branches)
-#pragma unroll
-                for (int o = 0; o < SHB_MAX_OUT; o++) {
-                    if (o >= no) break;
-                    out_vals[row * no + o] = O.kind[o] == 1 ? bk_raw(O.src[o], i, O.type[o])
-                                                            : bk_raw(O.src[o], (int64_t)blk_mpos[e] + k, O.type[o]);
+                if (no == 4) {
+                    // a 32-byte row as two 16-byte stores: consecutive lanes fill whole lines
+                    const int64_t mp = (int64_t)blk_mpos[e] + k;
+                    const int64_t v0 = bk_raw(O.src[0], O.kind[0] == 1 ? i : mp, O.type[0]);
+                    const int64_t v1 = bk_raw(O.src[1], O.kind[1] == 1 ? i : mp, O.type[1]);
+                    const int64_t v2 = bk_raw(O.src[2], O.kind[2] == 1 ? i : mp, O.type[2]);
+                    const int64_t v3 = bk_raw(O.src[3], O.kind[3] == 1 ? i : mp, O.type[3]);
+                    longlong2* dst = (longlong2*)(out_vals + row * 4);
+                    dst[0] = make_longlong2(v0, v1);
+                    dst[1] = make_longlong2(v2, v3);
+                    continue;
                 }
+                for (int o = 0; o < no; o++)
+                    out_vals[row * no + o] = bk_raw(O.src[o], O.kind[o] == 1 ? i : (int64_t)blk_mpos[e] + k, O.type[o]);
             }
             __syncthreads();
             continue;

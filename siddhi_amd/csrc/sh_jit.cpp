@@ -754,7 +754,13 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
         }
         return t;
     };
-    const std::string cand_fast = unguard(cand);
+    // (a guarded `ok = expr` must become `ok = ok && expr` once unguarded)
+    std::string cand_fast = "bool ok = true;\n" + unguard(gq.terms(F.f1, "ok")) + unguard(gq.terms(F.ionly, "ok"));
+    if (F.cross)
+        cand_fast += "{\n" + unguard(gq.yval(F, "y")) + "ok = ok && cmp_op<" + DT + ">(" + std::to_string(F.op) +
+                     ", xq, y) && !(hasM && cmp_op<" + DT + ">(" + std::to_string(F.op) + ", M, y));\n}\n";
+    else
+        cand_fast += "ok = ok && !hasM;\n";
     std::string mid_fast = "bool mk = true;\n" + unguard(gi.terms(F.qonly, "mk"));
     std::string stop, stop_cond;
     if (F.cross) {

@@ -775,3 +775,35 @@ extern "C" int shd_emit_place(const shd_emit* em, int32_t n_out, int64_t n_event
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+// ------------------------------------------------------------------ PMC calibration
+// Known-byte streams in the access widths the matcher kernels use (4 and 8 bytes
+// per lane, coalesced), so FETCH_SIZE / WRITE_SIZE can be scaled by a measured
+// factor instead of an assumed one (MI355X_MICROARCH.md, HBM: "other access
+// widths are uncalibrated"). Diagnostics only (scripts/pmc_calib.py).
+template <typename T>
+__global__ void k_cal_read(const T* __restrict__ src, int64_t n, T* __restrict__ sink) {
+    T acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        acc ^= src[i];
+    if (acc == (T)0x5A5A5A5A) sink[0] = acc;  // keeps the loads; practically never stores
+}
+template <typename T>
+__global__ void k_cal_write(T* __restrict__ dst, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = (T)i;
+}
+
+// kind: 0 read 4 B/lane, 1 read 8 B/lane, 2 write 4 B/lane, 3 write 8 B/lane; bytes of buf
+extern "C" int shx_pmc_calibrate(int kind, void* buf, int64_t bytes, void* sink, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 g(4096), b(256);
+    switch (kind) {
+        case 0: hipLaunchKernelGGL(k_cal_read<uint32_t>, g, b, 0, st, (const uint32_t*)buf, bytes / 4, (uint32_t*)sink); break;
+        case 1: hipLaunchKernelGGL(k_cal_read<uint64_t>, g, b, 0, st, (const uint64_t*)buf, bytes / 8, (uint64_t*)sink); break;
+        case 2: hipLaunchKernelGGL(k_cal_write<uint32_t>, g, b, 0, st, (uint32_t*)buf, bytes / 4); break;
+        case 3: hipLaunchKernelGGL(k_cal_write<uint64_t>, g, b, 0, st, (uint64_t*)buf, bytes / 8); break;
+        default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
