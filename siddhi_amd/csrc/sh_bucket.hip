@@ -75,43 +75,69 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_hist(const int32_t* __restrict__ 
 __global__ void __launch_bounds__(BK_TPB) k_bk_scatter(const int32_t* __restrict__ keys,
                                                        const int64_t* __restrict__ ts, shb_plan P) {
     __shared__ uint32_t wcnt[BK_TPB / 64][256];
-    __shared__ uint32_t run[256], tstart[256], gbase[256];
+    __shared__ uint32_t tstart[256], gbase[256];
     __shared__ uint32_t ws[BK_TPB / 64];
     __shared__ uint32_t stage[SHB_TILE];
     __shared__ uint8_t dig[SHB_TILE];
     const int64_t b0 = (int64_t)blockIdx.x << SHB_TILE_SHIFT;
-    if (threadIdx.x < 256) {
-        run[threadIdx.x] = 0u;
-        gbase[threadIdx.x] = P.base[(int64_t)threadIdx.x * P.nt + blockIdx.x];
-    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int c = threadIdx.x; c < (BK_TPB / 64) * 256; c += BK_TPB) (&wcnt[0][0])[c] = 0u;
+    if (threadIdx.x < 256) gbase[threadIdx.x] = P.base[(int64_t)threadIdx.x * P.nt + blockIdx.x];
     __syncthreads();
+    // each wave ranks its own contiguous 1,024 events (16 rounds of 64): the
+    // rank of an event among the wave's same-bucket events before it, from 8
+    // ballots per round and the wave's running counts (no block barrier)
     int32_t key[BK_ITEMS];
+    uint32_t rw[BK_ITEMS];
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
 #pragma unroll
     for (int j = 0; j < BK_ITEMS; j++) {
-        const int64_t i = b0 + j * BK_TPB + threadIdx.x;
+        const int64_t i = b0 + (int64_t)w * (64 * BK_ITEMS) + j * 64 + lane;
         key[j] = (i < P.n) ? keys[i] : -1;
-        if (key[j] >= 0) atomicAdd(&run[key[j] & (SHB_NB - 1)], 1u);
     }
-    __syncthreads();
-    uint32_t nvalid;
-    {
-        const uint32_t c = threadIdx.x < 256 ? run[threadIdx.x] : 0u;
-        const uint32_t ex = shw_block_excl<BK_TPB>(c, ws, &nvalid);
-        if (threadIdx.x < 256) {
-            tstart[threadIdx.x] = ex;
-            run[threadIdx.x] = 0u;
-        }
-    }
-    __syncthreads();
-    uint32_t lp[BK_ITEMS];
+#pragma unroll
     for (int j = 0; j < BK_ITEMS; j++) {
         const bool valid = key[j] >= 0;
         const uint32_t d = (uint32_t)key[j] & (SHB_NB - 1);
-        const uint32_t r = shw_rank8<BK_TPB>(d, valid, wcnt, run);
-        lp[j] = tstart[d] + r;
-        if (valid) dig[lp[j]] = (uint8_t)d;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bb = 0; bb < 8; bb++) {
+            const bool bit = (d >> bb) & 1u;
+            const uint64_t m = __ballot(valid && bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t r = (uint32_t)__popcll(peers & lt);
+        const uint32_t base = valid ? wcnt[w][d] : 0u;
+        rw[j] = valid ? ((base + r) | (d << 16)) : ~0u;  // wave rank | bucket << 16
+        if (valid && r == 0) wcnt[w][d] = base + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // per bucket: the waves' exclusive offsets and the tile total, then the
+    // buckets' starts
+    uint32_t nvalid;
+    {
+        uint32_t tot = 0;
+        if (threadIdx.x < 256) {
+#pragma unroll
+            for (int q = 0; q < BK_TPB / 64; q++) {
+                const uint32_t c = wcnt[q][threadIdx.x];
+                wcnt[q][threadIdx.x] = tot;
+                tot += c;
+            }
+        }
+        const uint32_t ex = shw_block_excl<BK_TPB>(threadIdx.x < 256 ? tot : 0u, ws, &nvalid);
+        if (threadIdx.x < 256) tstart[threadIdx.x] = ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < BK_ITEMS; j++) {
+        const bool valid = rw[j] != ~0u;
+        const uint32_t d = (rw[j] >> 16) & (SHB_NB - 1);
+        const uint32_t r = valid ? wcnt[w][d] + (rw[j] & 0xFFFFu) : 0u;  // rank among the tile's bucket-d events
+        rw[j] = valid ? tstart[d] + r : ~0u;                  // the event's slot in the staged tile
+        if (valid) dig[rw[j]] = (uint8_t)d;
         // the emitter restores arrival order from this rank (no re-ranking there)
-        const int64_t i = b0 + j * BK_TPB + threadIdx.x;
+        const int64_t i = b0 + (int64_t)w * (64 * BK_ITEMS) + j * 64 + lane;
         if (i < P.n) P.rk[i] = (uint16_t)r;
     }
     // packed (ts - tbase) << kb | key >> 8
@@ -119,11 +145,11 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_scatter(const int32_t* __restrict
     bool bad = false;
 #pragma unroll
     for (int j = 0; j < BK_ITEMS; j++) {
-        if (key[j] < 0) continue;
-        const int64_t i = b0 + j * BK_TPB + threadIdx.x;
+        if (rw[j] == ~0u) continue;
+        const int64_t i = b0 + (int64_t)w * (64 * BK_ITEMS) + j * 64 + lane;
         const int64_t dt = ts[i] - P.tbase;
         if (dt < 0 || dt >= lim) bad = true;
-        stage[lp[j]] = ((uint32_t)dt << P.kb) | ((uint32_t)key[j] >> 8);
+        stage[rw[j]] = ((uint32_t)dt << P.kb) | ((uint32_t)keys[i] >> 8);  // key reloaded (L2)
     }
     if (bad) atomicOr(P.flag, SHB_F_TS);
     __syncthreads();
@@ -143,24 +169,24 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_scatter(const int32_t* __restrict
 #define BK_HI(x) (2u * (x) + 1u)
     BK_WRITE_OUT(uint32_t, P.w0, BK_ID);
     for (int c = 0; c < P.n_staged; c++) {
-        const int w = P.st_width[c];
-        const int halves = w == 8 ? 2 : 1;
+        const int wd = P.st_width[c];
+        const int halves = wd == 8 ? 2 : 1;
         for (int hh = 0; hh < halves; hh++) {
 #pragma unroll
             for (int j = 0; j < BK_ITEMS; j++) {
-                if (key[j] < 0) continue;
-                const int64_t i = b0 + j * BK_TPB + threadIdx.x;
+                if (rw[j] == ~0u) continue;
+                const int64_t i = b0 + (int64_t)w * (64 * BK_ITEMS) + j * 64 + lane;
                 uint32_t v;
-                if (w == 8) v = ((const uint32_t*)P.st_src[c])[2 * i + hh];
-                else if (w == 4) v = ((const uint32_t*)P.st_src[c])[i];
+                if (wd == 8) v = ((const uint32_t*)P.st_src[c])[2 * i + hh];
+                else if (wd == 4) v = ((const uint32_t*)P.st_src[c])[i];
                 else v = ((const uint8_t*)P.st_src[c])[i];
-                stage[lp[j]] = v;
+                stage[rw[j]] = v;
             }
             __syncthreads();
-            if (w == 8) {
+            if (wd == 8) {
                 if (hh == 0) BK_WRITE_OUT(uint32_t, P.st_dst[c], BK_LO)
                 else BK_WRITE_OUT(uint32_t, P.st_dst[c], BK_HI)
-            } else if (w == 4) {
+            } else if (wd == 4) {
                 BK_WRITE_OUT(uint32_t, P.st_dst[c], BK_ID)
             } else {
                 BK_WRITE_OUT(uint8_t, P.st_dst[c], BK_ID)

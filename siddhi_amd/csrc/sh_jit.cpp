@@ -821,19 +821,23 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
         return "for (int o = " + from + "; !stopped && !ran_off; o--) {\n" +
                elem(count, on_consumed, "s_ws[o < 0 ? 0 : o]", "s_a@[o]") + "}\n";
     };
+    // the count walk: blocks of SHB_D predecessors, each loaded together and
+    // walked with 0/1 word predicates (straight-line vector code: no exec-mask
+    // juggling on the CU's shared scalar unit); the block loop runs while any
+    // lane of the wave still walks (a uniform exit). Consumed predecessors at
+    // distance < 31 go to a 32-bit mask for the emit phase (SHB_MOVF: beyond).
     auto walk_count = [&]() {
-        std::string s = head() + "uint32_t mask = 0u;\nif (!stopped) {\nuint32_t wv[SHB_D];\n";
+        std::string s = head() + "uint32_t mask = 0u;\nuint32_t live = stopped ? 0u : 1u, mono = 0u;\n"
+                                 "for (int base = 0; __ballot(live != 0u) != 0ull; base += SHB_D) {\n"
+                                 "uint32_t wv[SHB_D];\n";
         for (int a : need_r)
             s += std::string(col_ctype(P.attr_type[0][a])) + " av" + std::to_string(a) + "[SHB_D];\n";
-        s += "#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n    const int o = sp - 1 - u < 0 ? 0 : sp - 1 - u;\n"
-             "    wv[u] = s_ws[o];\n";
+        s += "#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n    const int o0 = sp - 1 - base - u;\n"
+             "    const int o = o0 < 0 ? 0 : o0;\n    wv[u] = s_ws[o];\n";
         for (int a : need_r) s += "    av" + std::to_string(a) + "[u] = " + lds(a) + "[o];\n";
-        // break-free: a `live` predicate instead of early exits, so the unrolled
-        // loop compiles to straight-line vector code (no exec-mask juggling on
-        // the CU's shared scalar unit)
-        // the loop-carried flags are 0/1 words (vector registers), not lane masks
-        s += "}\nuint32_t live = 1u, mono = 0u;\n#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n"
-             "    const int o = sp - 1 - u;\n"
+        s += "}\n#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n"
+             "    const int step = base + u;\n"
+             "    const int o = sp - 1 - step;\n"
              "    const uint32_t same = (o >= 0 && (wv[u] & kmask) == key) ? 1u : 0u;\n"
              "    const int64_t tr = (int64_t)(wv[u] >> kb);\n"
              "    const uint32_t inwin = (tq - tr <= SHJ_W) ? 1u : 0u;\n"
@@ -845,12 +849,11 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
         for (int a : need_r)
             s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
         s += "    {\n" + cand_fast +
-             "    const uint32_t cons = act & (ok ? 1u : 0u);\n    c_ += cons;\n    mask |= cons << u;\n    }\n";
+             "    const uint32_t cons = act & (ok ? 1u : 0u);\n    c_ += cons;\n"
+             "    mask |= step < 31 ? (cons << step) : (cons ? SHB_MOVF : 0u);\n    }\n";
         s += "    {\n" + mid_fast + "    }\n    {\n    const uint32_t st = (act && (" + stop_cond +
-             ")) ? 1u : 0u;\n    stopped |= st;\n    live = act & (st ^ 1u);\n    }\n}\n"
+             ")) ? 1u : 0u;\n    stopped |= st;\n    live = act & (st ^ 1u);\n    }\n}\n}\n"
              "if (mono) atomicOr(P.flag, SHB_F_MONO);\n";
-        s += "}\nif (!stopped && !ran_off) {\n    mask = SHB_MOVF;\n" +
-             slow(true, "        c_++;\n", "sp - 1 - SHB_D") + "}\n";
         s += "if (!stopped && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n";
         return s;
     };
@@ -866,15 +869,17 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     (void)sidx;
 
     src = SHJ_HEADERS;
-    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_TPB 512\n#define SHB_D 10\n#define SHB_MOVF 0x8000u\n"
-           "#define SHB_NR (SHB_SPAN / SHB_TPB)\nstatic_assert(SHB_SPAN % SHB_TPB == 0, \"span\");\n";
+    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_TPB 512\n#define SHB_D 8\n#define SHB_MOVF 0x80000000u\n"
+           "#define SHB_NR (SHB_SPAN / SHB_TPB)\nstatic_assert(SHB_SPAN % SHB_TPB == 0 && SHB_NR * SHB_TPB == SHB_SPAN, \"span\");\n";
     src += R"(
 extern "C" __global__ void __launch_bounds__(SHB_TPB, 4) shb_match(shb_plan P) {
 __shared__ uint32_t s_ws[SHB_SPAN];
 __shared__ uint16_t s_idx[SHB_SPAN];
 __shared__ uint16_t s_pre[SHB_CH];
-__shared__ uint16_t s_msk[SHB_CH];
-__shared__ uint32_t wcnt[SHB_TPB / 64][256];
+__shared__ uint32_t u_buf[SHB_CH];  // rank phase: per-wave key counts; then the consumed masks
+uint32_t (*const wcnt)[256] = (uint32_t(*)[256])u_buf;
+uint32_t* const s_msk = u_buf;
+static_assert((SHB_TPB / 64) * 256 <= SHB_CH, "wcnt fits u_buf");
 __shared__ uint32_t run[256], tstart[256], ws[SHB_TPB / 64];
 )";
     for (int a : staged_out)
@@ -902,55 +907,76 @@ if (threadIdx.x < 256) run[threadIdx.x] = 0u;
 __syncthreads();
 unsigned long long t_prev = wall_clock64();
 #define SHB_PROF(ph) if (P.prof && threadIdx.x == 0) { const unsigned long long t_now = wall_clock64(); atomicAdd(&P.prof[ph], t_now - t_prev); t_prev = t_now; }
-// the chunk and its halo into registers (all loads in flight together);
-// local-key histogram
+// the chunk and its halo into registers (all loads in flight together): wave v
+// owns the contiguous events [v * SHB_NR * 64, (v + 1) * SHB_NR * 64)
 const uint32_t* __restrict__ gw = P.w0 + (int64_t)bs + hs;
+const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
 uint32_t wr[SHB_NR];
 )";
     for (int a : staged_out)
         src += std::string(col_ctype(P.attr_type[0][a])) + " vr" + std::to_string(a) + "[SHB_NR];\n";
     src += R"(#pragma unroll
 for (int k = 0; k < SHB_NR; k++) {
-    const int i = k * SHB_TPB + (int)threadIdx.x;
+    const int i = (wv * SHB_NR + k) * 64 + lane;
     wr[k] = i < L ? gw[i] : 0u;
 )";
     for (int a : staged_out)
         src += "    vr" + std::to_string(a) + "[k] = i < L ? g_a" + std::to_string(a) + "[(int64_t)bs + hs + i] : 0;\n";
     src += R"(}
-#pragma unroll
-for (int k = 0; k < SHB_NR; k++)
-    if (k * SHB_TPB + (int)threadIdx.x < L) atomicAdd(&run[wr[k] & kmask], 1u);
+for (int c = (int)threadIdx.x; c < (SHB_TPB / 64) * 256; c += SHB_TPB) (&wcnt[0][0])[c] = 0u;
 __syncthreads();
+SHB_PROF(0)
+// stable sort of the span by local key, staged in sorted order (the walks read
+// consecutive LDS words): each wave ranks its own events (8 ballots per round,
+// running per-key counts of the wave), one block pass combines the waves
+uint32_t rw[SHB_NR];
 {
-    uint32_t tot;
-    const uint32_t ex = shw_block_excl<SHB_TPB>(threadIdx.x < 256 ? run[threadIdx.x] : 0u, ws, &tot);
-    if (threadIdx.x < 256) {
-        tstart[threadIdx.x] = ex;
-        run[threadIdx.x] = 0u;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+    for (int k = 0; k < SHB_NR; k++) {
+        const int i = (wv * SHB_NR + k) * 64 + lane;
+        const bool valid = i < L;
+        const uint32_t d = wr[k] & kmask;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bb = 0; bb < 8; bb++) {
+            const bool bit = (d >> bb) & 1u;
+            const uint64_t m = __ballot(valid && bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t r = (uint32_t)__popcll(peers & lt);
+        const uint32_t base = valid ? wcnt[wv][d] : 0u;
+        rw[k] = valid ? ((base + r) | (d << 16)) : ~0u;
+        if (valid && r == 0) wcnt[wv][d] = base + (uint32_t)__popcll(peers);
     }
 }
-SHB_PROF(0)
-// stable sort of the span by local key (wave-ballot ranking), staged in sorted
-// order: the walks read consecutive LDS words
+__syncthreads();
+{
+    uint32_t tot = 0, all;
+    if (threadIdx.x < 256) {
+#pragma unroll
+        for (int q = 0; q < SHB_TPB / 64; q++) {
+            const uint32_t c = wcnt[q][threadIdx.x];
+            wcnt[q][threadIdx.x] = tot;
+            tot += c;
+        }
+    }
+    const uint32_t ex = shw_block_excl<SHB_TPB>(threadIdx.x < 256 ? tot : 0u, ws, &all);
+    if (threadIdx.x < 256) tstart[threadIdx.x] = ex;
+}
+__syncthreads();
 #pragma unroll
 for (int k = 0; k < SHB_NR; k++) {
-    const int i = k * SHB_TPB + (int)threadIdx.x;
-    const bool valid = i < L;
-    const uint32_t w = wr[k];
+    if (rw[k] == ~0u) continue;
+    const int i = (wv * SHB_NR + k) * 64 + lane;
+    const uint32_t d = (rw[k] >> 16) & 0xFFu;
+    const int pos = (int)(tstart[d] + wcnt[wv][d] + (rw[k] & 0xFFFFu));
+    s_ws[pos] = wr[k];
+    s_idx[pos] = (uint16_t)i;
+
 )";
-    for (int a : staged_out)
-        src += "    const " + std::string(col_ctype(P.attr_type[0][a])) + " v" + std::to_string(a) + " = vr" +
-               std::to_string(a) + "[k];\n";
-    src += R"(    const uint32_t d = w & kmask;
-    const uint32_t rk = shw_rank8<SHB_TPB>(d, valid, wcnt, run);
-    if (valid) {
-        const int pos = (int)(tstart[d] + rk);
-        s_ws[pos] = w;
-        s_idx[pos] = (uint16_t)i;
-)";
-    for (int a : staged_out) src += "        " + lds(a) + "[pos] = v" + std::to_string(a) + ";\n";
-    src += R"(    }
-}
+    for (int a : staged_out) src += "    " + lds(a) + "[pos] = vr" + std::to_string(a) + "[k];\n";
+    src += R"(}
 __syncthreads();
 SHB_PROF(1)
 // consumers (chunk events) in sorted order: partials taken per event
@@ -962,7 +988,7 @@ uint32_t c_ = 0;
     src += walk_count();
     src += R"(if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);
 s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);
-s_msk[i - hl] = (uint16_t)mask;
+s_msk[i - hl] = mask;
 }
 __syncthreads();
 SHB_PROF(2)
