@@ -30,7 +30,7 @@
 #include "sh_device.h"
 #include "sh_wave.h"
 
-#define BK_TPB 1024
+#define BK_TPB 512
 #define BK_ITEMS (SHB_TILE / BK_TPB)
 #define BK_ROWMAP 2048  // rows per 1,024-event block written row-parallel
 

@@ -83,7 +83,7 @@ struct shd_window_ws {
 // bucket), the matcher walks each consumer's key back through an LDS-resident
 // chunk of its bucket, and the emitter restores arrival order per arrival tile.
 #define SHB_NB 256
-#define SHB_TILE_SHIFT 14
+#define SHB_TILE_SHIFT 13
 #define SHB_TILE (1 << SHB_TILE_SHIFT)
 #define SHB_CH 4096
 #define SHB_HALO 1024
