@@ -167,7 +167,8 @@ typedef struct sh_app_desc {
        participates in partition p iff partition_streams[p*n_streams+s] != 0 */
     const uint8_t* partition_streams;
     /* partition_attr[p*n_streams+s]: attribute index of stream s that keys
-       partition p (`partition with (attr of Stream)`), -1 if not keyed */
+       partition p (`partition with (attr of Stream)`), -1 if not keyed or
+       range-partitioned (keys computed by the host from the ranges) */
     const int32_t* partition_attr;
 } sh_app_desc;
 

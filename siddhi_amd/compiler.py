@@ -9,7 +9,7 @@ This mirrors, for the pattern/sequence hot path only, what the reference does in
   modules/siddhi-core/.../util/parser/SelectorParser.java:215                 (select default index 0)
 
 Supported: `define stream`, `@app:playback`, `@info(name=...)`, `partition with
-(attr of Stream, ...) begin ... end`, pattern (`->`) and sequence (`,`) queries with
+(attr of Stream | cond as 'label' or ... of Stream, ...) begin ... end`, pattern (`->`) and sequence (`,`) queries with
 `every`, `within`, filters, logical `and`/`or`, `not X for T`, counts `<m:n>` `+` `*` `?`,
 `e[i]` / `e[last]` / `e[last-k]` references, `select ... [as ...]` with
 sum/avg/count/max/min, `insert [current events] into`.
@@ -189,13 +189,21 @@ class Query:
 
 
 @dataclass
+class RangeSpec:
+    """range partition of one stream: (condition, label) in declaration order
+    (core/partition/executor/RangePartitionExecutor.java; PartitionParser builds one
+    executor per range, evaluated in this order)"""
+    ranges: List[Tuple[object, str]]
+
+
+@dataclass
 class App:
     name: Optional[str]
     playback: bool
     streams: Dict[str, StreamDef]
     stream_order: List[str]
     queries: List[Query]
-    partitions: List[Dict[str, str]]   # per partition: stream -> attribute name
+    partitions: List[Dict[str, object]]   # per partition: stream -> attribute name | RangeSpec
     output_streams: List[str] = field(default_factory=list)
 
 
@@ -347,14 +355,30 @@ class Parser:
         self.expect_op("(")
         spec = {}
         while True:
-            attr = self.ident()
-            if self.op("."):
-                raise UnsupportedQuery("range/expression partitions are out of scope")
-            if not self.kw("of"):
-                raise UnsupportedQuery("range partitions are out of scope")
-            self.next()
-            stream = self.ident()
-            spec[stream] = attr
+            # partition_with_stream (SiddhiQL.g4): `attr of S` (value partition) or
+            # `cond as 'label' (or cond as 'label')* of S` (range partition)
+            e = self.expr()
+            if self.kw("as"):
+                ranges = []
+                while True:
+                    self.expect_kw("as")
+                    tk = self.peek()
+                    if tk.kind != "str":
+                        self.err("expected a range label string")
+                    self.next()
+                    ranges.append((e, bytes(tk.text[1:-1], "utf-8").decode("unicode_escape")))
+                    if self.kw("or"):
+                        self.next()
+                        e = self.expr()
+                        continue
+                    break
+                self.expect_kw("of")
+                spec[self.ident()] = RangeSpec(ranges)
+            else:
+                if not isinstance(e, EVar) or e.stream is not None or e.index is not None:
+                    self.err("expected `attribute of Stream` or `condition as 'label' of Stream`")
+                self.expect_kw("of")
+                spec[self.ident()] = e.name
             if self.op(","):
                 self.next()
                 continue
@@ -1067,7 +1091,9 @@ class CompiledApp:
         for p, spec in enumerate(app.partitions):
             for s, name in enumerate(app.stream_order):
                 ps[p * ns + s] = 1 if name in spec else 0
-                pa[p * ns + s] = app.streams[name].index(spec[name]) if name in spec else -1
+                # -1 for a range partition: the host computes the keys from the ranges
+                pa[p * ns + s] = (app.streams[name].index(spec[name])
+                                  if name in spec and isinstance(spec[name], str) else -1)
         keep += [streams, qs, ps, pa]
         d = abi.sh_app_desc()
         d.version = abi.SH_DESC_VERSION
@@ -1095,7 +1121,13 @@ def compile_app(text: str, strings: Optional[StringDict] = None) -> CompiledApp:
             for sname in spec:
                 if sname not in app.streams:
                     raise SiddhiAppValidationException(f"partition stream {sname} undefined")
-                if app.streams[sname].index(spec[sname]) < 0:
+                if isinstance(spec[sname], RangeSpec):
+                    from .hostexpr import RangeEvaluator
+                    ev = RangeEvaluator(app.streams[sname], sname)
+                    probe = [None] * len(app.streams[sname].attrs)
+                    for cond, _ in spec[sname].ranges:
+                        ev.cond(cond, probe)  # validates attributes and types on an all-null row
+                elif app.streams[sname].index(spec[sname]) < 0:
                     raise SiddhiAppValidationException(f"partition attribute {spec[sname]} undefined")
         root, outs = low.lower_query(q)
         if q.output not in out_streams:

@@ -26,6 +26,7 @@ import numpy as np
 
 from . import compiler as cp
 from . import javastr
+from .hostexpr import RangeEvaluator
 from .compiler import (BOOL, DOUBLE, FLOAT, INT, LONG, OBJECT, STRING, CompiledApp,
                        SiddhiAppValidationException, SiddhiParserException, UnsupportedQuery)
 
@@ -210,6 +211,8 @@ class SiddhiAppRuntime:
         self._engine = engine_factory(compiled)
         self._started = False
         self._seq = 0
+        self._range_ev: Dict[str, RangeEvaluator] = {}
+        self._labels = None
         self.clock = 0 if self.app.playback else 1_000_000_000_000
         self.name = self.app.name
 
@@ -286,15 +289,43 @@ class SiddhiAppRuntime:
         keys = None
         for p, spec in enumerate(self.app.partitions):
             sname = self.app.stream_order[stream_id]
-            if sname in spec:
+            if sname in spec and isinstance(spec[sname], cp.RangeSpec):
+                # the range labels are the partition keys (RangePartitionExecutor.execute)
+                keys = np.array([self.keys.key(lb, STRING) for lb in self._labels], dtype=np.int32)
+            elif sname in spec:
                 ai = sd.index(spec[sname])
                 typ = sd.attrs[ai][1]
                 keys = np.array([self.keys.key(r[ai], typ) for r in rows], dtype=np.int32)
         return tsa, cols, nulls, keys
 
+    def _range_expand(self, stream_id: int, ts, rows):
+        """Range partitions (PartitionStreamReceiver.receive, core/partition/
+        PartitionStreamReceiver.java:176-272): every range executor is evaluated per
+        event in declaration order and the event goes to the partition of each range
+        whose condition holds (none: dropped); consecutive same-key events form one
+        chunk. Returns the expanded (ts, rows, labels)."""
+        sname = self.app.stream_order[stream_id]
+        for spec in self.app.partitions:
+            rs = spec.get(sname)
+            if isinstance(rs, cp.RangeSpec):
+                ev = self._range_ev.get(sname)
+                if ev is None:
+                    ev = self._range_ev[sname] = RangeEvaluator(self.app.streams[sname], sname)
+                ots, orows, labels = [], [], []
+                for t, r in zip(ts, rows):
+                    for cond, label in rs.ranges:
+                        if ev.cond(cond, r):
+                            ots.append(t)
+                            orows.append(r)
+                            labels.append(label)
+                return ots, orows, labels
+        return ts, rows, None
+
     def _send(self, stream_id: int, ts, rows):
         if not self._started:
             raise SiddhiAppRuntimeException("SiddhiAppRuntime not started")
+        ts, rows, labels = self._range_expand(stream_id, ts, rows)
+        self._labels = labels
         if not rows:
             return
         tsa, cols, nulls, keys = self._pack(stream_id, ts, rows)
