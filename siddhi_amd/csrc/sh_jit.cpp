@@ -43,6 +43,8 @@
 
 namespace {
 
+int type_width(int t) { return t == SH_T_LONG || t == SH_T_DOUBLE ? 8 : (t == SH_T_BOOL ? 1 : 4); }
+
 // events per workgroup (one lane each) and staged events beyond the tile
 // (forward for match, backward for place / the consumer walk); SH_JIT_TILE /
 // SH_JIT_HALO override them (tile 64..1024, powers of two; halo 0..1024)
@@ -857,6 +859,56 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
         s += "if (!stopped && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n";
         return s;
     };
+    // the count walk for a floating-point ordering term: ext starts as NaN (no
+    // compare with NaN holds, and maxNum/minNum skip a NaN operand), so the
+    // `hasM` flag, the NaN tests on X and the per-step premise checks drop out;
+    // times compare as the packed 32-bit values (in window: tr >= tq - W)
+    const bool fdom = F.cross && (F.dom == DOM_F32 || F.dom == DOM_F64);
+    auto walk_count_f = [&]() {
+        const bool mx = F.op == SH_OP_GT || F.op == SH_OP_GE;
+        const std::string opn = std::to_string(F.op);
+        const std::string ext = F.dom == DOM_F32 ? (mx ? "__builtin_fmaxf" : "__builtin_fminf")
+                                                 : (mx ? "__builtin_fmax" : "__builtin_fmin");
+        std::string cand_f = "bool ok = true;\n" + unguard(gq.terms(F.f1, "ok")) + unguard(gq.terms(F.ionly, "ok")) +
+                             "{\n" + unguard(gq.yval(F, "y")) + "ok = ok && cmp_op<" + DT + ">(" + opn +
+                             ", xq, y) && !cmp_op<" + DT + ">(" + opn + ", Mx, y);\n}\n";
+        std::string mid_f = "bool mk = true;\n" + unguard(gi.terms(F.qonly, "mk")) + "{\n" + unguard(gi.xval(F, "xr")) +
+                            "Mx = (act && mk) ? " + ext + "(Mx, xr) : Mx;\n}\n";
+        std::string s = head() +
+                        "const uint32_t tq32 = wq >> kb;\n"
+                        "const uint32_t tlo = tq32 > SHB_WLIM ? tq32 - SHB_WLIM : 0u;\n" + DT +
+                        " Mx = " + (F.dom == DOM_F32 ? "__builtin_nanf(\"\")" : "__builtin_nan(\"\")") + ";\n"
+                        "uint32_t mask = 0u, cext = 0u, roff = 0u;\n"
+                        "uint32_t live = (qok && xq == xq) ? 1u : 0u;\n"
+                        "if (live && sp >= 1) {\n"
+                        "    const uint32_t wp = s_ws[sp - 1];\n"
+                        "    if (((wp ^ wq) & kmask) == 0u && (wp >> kb) > tq32) atomicOr(P.flag, SHB_F_MONO);\n"
+                        "}\n"
+                        "for (int base = 0; __ballot(live != 0u) != 0ull; base += SHB_D) {\n"
+                        "uint32_t wv[SHB_D];\n";
+        for (int a : need_r)
+            s += std::string(col_ctype(P.attr_type[0][a])) + " av" + std::to_string(a) + "[SHB_D];\n";
+        s += "#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n    const int o0 = sp - 1 - base - u;\n"
+             "    const int o = o0 < 0 ? 0 : o0;\n    wv[u] = s_ws[o];\n";
+        for (int a : need_r) s += "    av" + std::to_string(a) + "[u] = " + lds(a) + "[o];\n";
+        s += "}\n#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n"
+             "    const int step = base + u;\n"
+             "    const uint32_t same = (u < sp - base && ((wv[u] ^ wq) & kmask) == 0u) ? 1u : 0u;\n"
+             "    roff |= live & (same ^ 1u);\n"
+             "    const uint32_t act = live & same & ((wv[u] >> kb) >= tlo ? 1u : 0u);\n";
+        for (int a : need_r)
+            s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
+        s += "    {\n" + cand_f +
+             "    const uint32_t cons = act & (ok ? 1u : 0u);\n"
+             "    if (step < 31) mask |= cons << step;\n"
+             "    else { cext += cons; mask |= cons ? SHB_MOVF : 0u; }\n    }\n";
+        s += "    {\n" + mid_f + "    }\n    live = act & (cmp_op<" + DT + ">(" + (mx ? std::to_string(SH_OP_GE)
+                                                                                  : std::to_string(SH_OP_LE)) +
+             ", Mx, xq) ? 0u : 1u);\n}\n}\n"
+             "c_ = (uint32_t)__popc(mask & ~SHB_MOVF) + cext;\n"
+             "if (roff && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n";
+        return s;
+    };
     auto walk = [&](bool count, const std::string& on_consumed) {
         return head() + slow(count, on_consumed, "sp - 1");
     };
@@ -869,7 +921,9 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     (void)sidx;
 
     src = SHJ_HEADERS;
-    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_TPB 512\n#define SHB_D 8\n#define SHB_MOVF 0x80000000u\n"
+    const int64_t wlim = P.within_ms < 0 ? 0 : (P.within_ms > 0xFFFFFFFFll ? 0xFFFFFFFFll : P.within_ms);
+    src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_WLIM " + std::to_string(wlim) +
+           "u\n#define SHB_TPB 512\n#define SHB_D 8\n#define SHB_MOVF 0x80000000u\n"
            "#define SHB_NR (SHB_SPAN / SHB_TPB)\nstatic_assert(SHB_SPAN % SHB_TPB == 0 && SHB_NR * SHB_TPB == SHB_SPAN, \"span\");\n";
     src += R"(
 extern "C" __global__ void __launch_bounds__(SHB_TPB, 4) shb_match(shb_plan P) {
@@ -927,7 +981,7 @@ for (int c = (int)threadIdx.x; c < (SHB_TPB / 64) * 256; c += SHB_TPB) (&wcnt[0]
 __syncthreads();
 SHB_PROF(0)
 // stable sort of the span by local key, staged in sorted order (the walks read
-// consecutive LDS words): each wave ranks its own events (8 ballots per round,
+// consecutive LDS words): each wave ranks its own events (kb ballots per round,
 // running per-key counts of the wave), one block pass combines the waves
 uint32_t rw[SHB_NR];
 {
@@ -940,9 +994,11 @@ uint32_t rw[SHB_NR];
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int bb = 0; bb < 8; bb++) {
-            const bool bit = (d >> bb) & 1u;
-            const uint64_t m = __ballot(valid && bit);
-            peers &= bit ? m : ~m;
+            if (bb < kb) {  // uniform: the local key has kb bits
+                const bool bit = (d >> bb) & 1u;
+                const uint64_t m = __ballot(valid && bit);
+                peers &= bit ? m : ~m;
+            }
         }
         const uint32_t r = (uint32_t)__popcll(peers & lt);
         const uint32_t base = valid ? wcnt[wv][d] : 0u;
@@ -985,7 +1041,7 @@ const int i = (int)s_idx[sp];
 if (i < hl) continue;
 uint32_t c_ = 0;
 )";
-    src += walk_count();
+    src += fdom ? walk_count_f() : walk_count();
     src += R"(if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);
 s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);
 s_msk[i - hl] = mask;
@@ -1058,7 +1114,8 @@ uint32_t k = 0;
            "    while (m) {\n        const int o = sp - __ffs(m);\n        m &= m - 1u;\n"
            "        const int64_t dst = rbase + (int64_t)off + (int64_t)(cn - 1u - k);\n        k++;\n" +
            ms_put + "    }\n} else {\n" + walk(false, put) + "}\n";
-    src += "}\n__syncthreads();\nSHB_PROF(4)\n}\n}\n";
+    src += "}\n__syncthreads();\n";
+    src += "SHB_PROF(4)\n}\n}\n";
     return true;
 }
 
