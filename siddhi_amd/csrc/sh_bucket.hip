@@ -272,7 +272,6 @@ __global__ void __launch_bounds__(256) k_bk_ttot(shb_plan P) {
 // ---------------------------------------------------------------- emitter
 // per event (registers): bucket d | count << 8 | rank << 16, and its
 // match-stream position; the select list lives in LDS (uniform per output)
-template <int MODE, int G>
 __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ keys, shb_plan P, shb_out O,
                                                     uint64_t seq_base, uint64_t* __restrict__ out_seq,
                                                     int64_t* __restrict__ out_vals, int64_t out_cap) {
@@ -281,8 +280,8 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
     __shared__ uint32_t S[SHB_TILE];
     __shared__ int32_t o_kind[SHB_MAX_OUT], o_type[SHB_MAX_OUT];
     __shared__ const void* o_src[SHB_MAX_OUT];
-    __shared__ uint16_t evmap[BK_ROWMAP * G];
-    __shared__ uint32_t blk_mpos[BK_TPB * G];
+    __shared__ uint16_t evmap[BK_ROWMAP];
+    __shared__ uint32_t blk_mpos[BK_TPB];
     __shared__ uint32_t s_tot;
     const int T = blockIdx.x;
     const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
@@ -365,51 +364,6 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
     shw_lds_excl_scan<BK_TPB, BK_ITEMS>(S, tile_n, ws);
     const uint32_t tb = P.ttot[T];
     const int no = O.n_out;
-    if (MODE == 1) {
-        // event-parallel writes: the lanes of a wave hold consecutive events, so
-        // their rows are consecutive; no barrier after the scans
-#pragma unroll
-        for (int j = 0; j < BK_ITEMS; j++) {
-            const int l = j * BK_TPB + threadIdx.x;
-            const uint32_t c = (l < tile_n && pk[j] != ~0u) ? (pk[j] >> 8) & 0xFFu : 0u;
-            if (!c) continue;
-            const int64_t i = b0 + l;
-            const int64_t row0 = (int64_t)tb + S[l];
-            if (row0 + c > out_cap) continue;  // the host reports SH_E_MORE
-            if (out_seq)
-                for (uint32_t k = 0; k < c; k++) out_seq[row0 + k] = seq_base + (uint64_t)i;
-            if (!out_vals) continue;
-            if (no == 4) {
-                const bool m0 = O.kind[0] == 0, m1 = O.kind[1] == 0, m2 = O.kind[2] == 0, m3 = O.kind[3] == 0;
-                const int64_t e0 = m0 ? 0 : bk_raw(O.src[0], i, O.type[0]);
-                const int64_t e1 = m1 ? 0 : bk_raw(O.src[1], i, O.type[1]);
-                const int64_t e2 = m2 ? 0 : bk_raw(O.src[2], i, O.type[2]);
-                const int64_t e3 = m3 ? 0 : bk_raw(O.src[3], i, O.type[3]);
-                for (uint32_t k = 0; k < c; k++) {
-                    const int64_t mp = (int64_t)mpos[j] + k;
-                    const int64_t v0 = m0 ? bk_raw(O.src[0], mp, O.type[0]) : e0;
-                    const int64_t v1 = m1 ? bk_raw(O.src[1], mp, O.type[1]) : e1;
-                    const int64_t v2 = m2 ? bk_raw(O.src[2], mp, O.type[2]) : e2;
-                    const int64_t v3 = m3 ? bk_raw(O.src[3], mp, O.type[3]) : e3;
-                    longlong2* dst = (longlong2*)(out_vals + (row0 + k) * 4);
-                    dst[0] = make_longlong2(v0, v1);
-                    dst[1] = make_longlong2(v2, v3);
-                }
-                continue;
-            }
-            for (int o = 0; o < no; o++) {
-                const void* src = O.src[o];
-                const int ty = O.type[o];
-                if (O.kind[o] == 1) {
-                    const int64_t v = bk_raw(src, i, ty);
-                    for (uint32_t k = 0; k < c; k++) out_vals[(row0 + k) * no + o] = v;
-                } else {
-                    for (uint32_t k = 0; k < c; k++) out_vals[(row0 + k) * no + o] = bk_raw(src, (int64_t)mpos[j] + k, ty);
-                }
-            }
-        }
-        return;
-    }
     // the rows are written row-parallel, one 1,024-event block at a time: each
     // event enters its rows into the block's row -> event map, then thread t
     // writes row r0 + t (consecutive lanes, consecutive rows: coalesced)
@@ -421,96 +375,67 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
         }
     }
     __syncthreads();
-    // one super-block of G * BK_TPB events at a time: its events enter their
-    // rows into the row -> event map, then thread t writes rows r0 + t,
-    // r0 + t + BK_TPB, ... (two rows per round: all loads, then all stores)
-    auto put_row = [&](uint32_t t, int lb, uint32_t r0, int64_t& row, int64_t& i, int64_t* v, int& nv) {
-        const int e = evmap[t];
-        const int le = lb + e;
-        const uint32_t k = r0 + t - S[le];
-        i = b0 + le;
-        row = (int64_t)tb + r0 + t;
-        const int64_t mp = (int64_t)blk_mpos[e] + k;
-        nv = no <= 4 ? no : 0;
 #pragma unroll
-        for (int o = 0; o < 4; o++)
-            if (o < no) v[o] = bk_raw(O.src[o], O.kind[o] == 1 ? i : mp, O.type[o]);
-    };
-    auto store_row = [&](int64_t row, int64_t i, const int64_t* v, uint32_t t, int lb, uint32_t r0) {
-        if (row >= out_cap) return;  // the host reports SH_E_MORE
-        if (out_seq) out_seq[row] = seq_base + (uint64_t)i;
-        if (!out_vals) return;
-        if (no == 4) {
-            // a 32-byte row as two 16-byte stores: consecutive lanes fill whole lines
-            longlong2* dst = (longlong2*)(out_vals + row * 4);
-            dst[0] = make_longlong2(v[0], v[1]);
-            dst[1] = make_longlong2(v[2], v[3]);
-            return;
-        }
-        if (no < 4) {
-            for (int o = 0; o < no; o++) out_vals[row * no + o] = v[o];
-            return;
-        }
-        const int e = evmap[t];
-        const uint32_t k = r0 + t - S[lb + e];
-        for (int o = 0; o < no; o++)
-            out_vals[row * no + o] = bk_raw(O.src[o], O.kind[o] == 1 ? i : (int64_t)blk_mpos[e] + k, O.type[o]);
-    };
-#pragma unroll
-    for (int g = 0; g < BK_ITEMS / G; g++) {
-        const int lb = g * G * BK_TPB;
+    for (int j = 0; j < BK_ITEMS; j++) {
+        const int lb = j * BK_TPB;
         if (lb >= tile_n) break;  // uniform
-        const int le_end = lb + G * BK_TPB;
+        const int l = lb + threadIdx.x;
         const uint32_t r0 = S[lb];
-        const uint32_t r1 = le_end < tile_n ? S[le_end] : s_tot;
+        const uint32_t r1 = lb + BK_TPB < tile_n ? S[lb + BK_TPB] : s_tot;
         const uint32_t R = r1 - r0;
-        if (R <= (uint32_t)(BK_ROWMAP * G)) {
-#pragma unroll
-            for (int jj = 0; jj < G; jj++) {
-                const int j = g * G + jj;
-                const int l = lb + jj * BK_TPB + threadIdx.x;
-                const uint32_t c = (l < tile_n && pk[j] != ~0u) ? (pk[j] >> 8) & 0xFFu : 0u;
-                if (c) {
-                    const uint32_t at = S[l] - r0;
-                    for (uint32_t k = 0; k < c; k++) evmap[at + k] = (uint16_t)(jj * BK_TPB + threadIdx.x);
-                }
-                blk_mpos[jj * BK_TPB + threadIdx.x] = mpos[j];
+        const uint32_t c = pk[j] == ~0u ? 0u : (pk[j] >> 8) & 0xFFu;
+        if (R <= BK_ROWMAP) {
+            if (c) {
+                const uint32_t at = S[l] - r0;
+                for (uint32_t k = 0; k < c; k++) evmap[at + k] = (uint16_t)threadIdx.x;
             }
+            blk_mpos[threadIdx.x] = mpos[j];
             __syncthreads();
-            for (uint32_t t = threadIdx.x; t < R; t += 2 * BK_TPB) {
-                int64_t rowA, iA, vA[4], rowB = 0, iB = 0, vB[4];
-                int nA, nB;
-                put_row(t, lb, r0, rowA, iA, vA, nA);
-                const bool hasB = t + BK_TPB < R;
-                if (hasB) put_row(t + BK_TPB, lb, r0, rowB, iB, vB, nB);
-                store_row(rowA, iA, vA, t, lb, r0);
-                if (hasB) store_row(rowB, iB, vB, t + BK_TPB, lb, r0);
+            for (uint32_t t = threadIdx.x; t < R; t += BK_TPB) {
+                const int e = evmap[t];
+                const int le = lb + e;
+                const uint32_t k = r0 + t - S[le];
+                const int64_t i = b0 + le;
+                const int64_t row = (int64_t)tb + r0 + t;
+                if (row >= out_cap) continue;  // the host reports SH_E_MORE
+                if (out_seq) out_seq[row] = seq_base + (uint64_t)i;
+                if (!out_vals) continue;
+                // output descriptors straight from the kernel arguments (scalar
+                // registers: uniform branches)
+                if (no == 4) {
+                    // a 32-byte row as two 16-byte stores: consecutive lanes fill whole lines
+                    const int64_t mp = (int64_t)blk_mpos[e] + k;
+                    const int64_t v0 = bk_raw(O.src[0], O.kind[0] == 1 ? i : mp, O.type[0]);
+                    const int64_t v1 = bk_raw(O.src[1], O.kind[1] == 1 ? i : mp, O.type[1]);
+                    const int64_t v2 = bk_raw(O.src[2], O.kind[2] == 1 ? i : mp, O.type[2]);
+                    const int64_t v3 = bk_raw(O.src[3], O.kind[3] == 1 ? i : mp, O.type[3]);
+                    longlong2* dst = (longlong2*)(out_vals + row * 4);
+                    dst[0] = make_longlong2(v0, v1);
+                    dst[1] = make_longlong2(v2, v3);
+                    continue;
+                }
+                for (int o = 0; o < no; o++)
+                    out_vals[row * no + o] = bk_raw(O.src[o], O.kind[o] == 1 ? i : (int64_t)blk_mpos[e] + k, O.type[o]);
             }
             __syncthreads();
             continue;
         }
-        // a dense super-block (more rows than the map holds): event-parallel writes
-#pragma unroll
-        for (int jj = 0; jj < G; jj++) {
-            const int j = g * G + jj;
-            const int l = lb + jj * BK_TPB + threadIdx.x;
-            const uint32_t c = (l < tile_n && pk[j] != ~0u) ? (pk[j] >> 8) & 0xFFu : 0u;
-            if (!c) continue;
-            const int64_t i = b0 + l;
-            const int64_t row0 = (int64_t)tb + S[l];
-            if (row0 + c > out_cap) continue;
-            if (out_seq)
-                for (uint32_t k = 0; k < c; k++) out_seq[row0 + k] = seq_base + (uint64_t)i;
-            if (!out_vals) continue;
-            for (int o = 0; o < no; o++) {
-                const void* src = o_src[o];
-                const int ty = o_type[o];
-                if (o_kind[o] == 1) {
-                    const int64_t v = bk_raw(src, i, ty);
-                    for (uint32_t k = 0; k < c; k++) out_vals[(row0 + k) * no + o] = v;
-                } else {
-                    for (uint32_t k = 0; k < c; k++) out_vals[(row0 + k) * no + o] = bk_raw(src, (int64_t)mpos[j] + k, ty);
-                }
+        // a dense block (more rows than the map holds): event-parallel writes
+        if (!c) continue;
+        const int64_t i = b0 + l;
+        const int64_t row0 = (int64_t)tb + S[l];
+        if (row0 + c > out_cap) continue;
+        if (out_seq)
+            for (uint32_t k = 0; k < c; k++) out_seq[row0 + k] = seq_base + (uint64_t)i;
+        if (!out_vals) continue;
+        for (int o = 0; o < no; o++) {
+            const void* src = o_src[o];
+            const int ty = o_type[o];
+            if (o_kind[o] == 1) {
+                const int64_t v = bk_raw(src, i, ty);
+                for (uint32_t k = 0; k < c; k++) out_vals[(row0 + k) * no + o] = v;
+            } else {
+                for (uint32_t k = 0; k < c; k++) out_vals[(row0 + k) * no + o] = bk_raw(src, (int64_t)mpos[j] + k, ty);
             }
         }
     }
@@ -548,23 +473,7 @@ extern "C" int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream) {
 
 extern "C" int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, uint64_t seq_base,
                         uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
-    // default: row-parallel writes through a row map per super-block of
-    // SH_BK_EMIT_G (1, 2, 4; default 2) x 512 events; SH_BK_EMIT=1: event-parallel
-    // writes (measured slower: 2.77 vs 1.84 ms on C2)
-    static const int mode = getenv("SH_BK_EMIT") ? atoi(getenv("SH_BK_EMIT")) : 0;
-    static const int gsz = getenv("SH_BK_EMIT_G") ? atoi(getenv("SH_BK_EMIT_G")) : 2;
-    hipStream_t st = (hipStream_t)stream;
-    if (mode == 1)
-        hipLaunchKernelGGL((k_bk_emit<1, 1>), dim3(P->nt), dim3(BK_TPB), 0, st, keys, *P, *O, seq_base, out_seq,
-                           out_vals, out_cap);
-    else if (gsz == 4)
-        hipLaunchKernelGGL((k_bk_emit<0, 4>), dim3(P->nt), dim3(BK_TPB), 0, st, keys, *P, *O, seq_base, out_seq,
-                           out_vals, out_cap);
-    else if (gsz == 1)
-        hipLaunchKernelGGL((k_bk_emit<0, 1>), dim3(P->nt), dim3(BK_TPB), 0, st, keys, *P, *O, seq_base, out_seq,
-                           out_vals, out_cap);
-    else
-        hipLaunchKernelGGL((k_bk_emit<0, 2>), dim3(P->nt), dim3(BK_TPB), 0, st, keys, *P, *O, seq_base, out_seq,
-                           out_vals, out_cap);
+    hipLaunchKernelGGL(k_bk_emit, dim3(P->nt), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O, seq_base, out_seq,
+                       out_vals, out_cap);
     return bk_ok();
 }

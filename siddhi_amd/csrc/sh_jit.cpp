@@ -827,7 +827,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     // walked with 0/1 word predicates (straight-line vector code: no exec-mask
     // juggling on the CU's shared scalar unit); the block loop runs while any
     // lane of the wave still walks (a uniform exit). Consumed predecessors at
-    // distance < 31 go to a 32-bit mask for the emit phase (SHB_MOVF: beyond).
+    // distance < 15 go to a 16-bit mask for the emit phase (SHB_MOVF: beyond).
     auto walk_count = [&]() {
         std::string s = head() + "uint32_t mask = 0u;\nuint32_t live = stopped ? 0u : 1u, mono = 0u;\n"
                                  "for (int base = 0; __ballot(live != 0u) != 0ull; base += SHB_D) {\n"
@@ -852,7 +852,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
             s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
         s += "    {\n" + cand_fast +
              "    const uint32_t cons = act & (ok ? 1u : 0u);\n    c_ += cons;\n"
-             "    mask |= step < 31 ? (cons << step) : (cons ? SHB_MOVF : 0u);\n    }\n";
+             "    mask |= step < SHB_MSTEPS ? (cons << step) : (cons ? SHB_MOVF : 0u);\n    }\n";
         s += "    {\n" + mid_fast + "    }\n    {\n    const uint32_t st = (act && (" + stop_cond +
              ")) ? 1u : 0u;\n    stopped |= st;\n    live = act & (st ^ 1u);\n    }\n}\n}\n"
              "if (mono) atomicOr(P.flag, SHB_F_MONO);\n";
@@ -900,7 +900,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
             s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
         s += "    {\n" + cand_f +
              "    const uint32_t cons = act & (ok ? 1u : 0u);\n"
-             "    if (step < 31) mask |= cons << step;\n"
+             "    if (step < SHB_MSTEPS) mask |= cons << step;\n"
              "    else { cext += cons; mask |= cons ? SHB_MOVF : 0u; }\n    }\n";
         s += "    {\n" + mid_f + "    }\n    live = act & (cmp_op<" + DT + ">(" + (mx ? std::to_string(SH_OP_GE)
                                                                                   : std::to_string(SH_OP_LE)) +
@@ -923,17 +923,19 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     src = SHJ_HEADERS;
     const int64_t wlim = P.within_ms < 0 ? 0 : (P.within_ms > 0xFFFFFFFFll ? 0xFFFFFFFFll : P.within_ms);
     src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_WLIM " + std::to_string(wlim) +
-           "u\n#define SHB_TPB 512\n#define SHB_D 8\n#define SHB_MOVF 0x80000000u\n"
+           "u\n#define SHB_TPB 512\n#define SHB_D 8\n#define SHB_MOVF 0x8000u\n#define SHB_MSTEPS 15\n"
            "#define SHB_NR (SHB_SPAN / SHB_TPB)\nstatic_assert(SHB_SPAN % SHB_TPB == 0 && SHB_NR * SHB_TPB == SHB_SPAN, \"span\");\n";
     src += R"(
 extern "C" __global__ void __launch_bounds__(SHB_TPB, 4) shb_match(shb_plan P) {
 __shared__ uint32_t s_ws[SHB_SPAN];
-__shared__ uint16_t s_idx[SHB_SPAN];
+// the chunk's consumers in sorted order: sorted position | (arrival - hl) << 16
+__shared__ uint32_t s_cons[SHB_CH];
 __shared__ uint16_t s_pre[SHB_CH];
-__shared__ uint32_t u_buf[SHB_CH];  // rank phase: per-wave key counts; then the consumed masks
+__shared__ uint32_t u_buf[(SHB_TPB / 64) * 256];  // rank phase: per-wave key counts; then the u16 consumed masks
 uint32_t (*const wcnt)[256] = (uint32_t(*)[256])u_buf;
-uint32_t* const s_msk = u_buf;
-static_assert((SHB_TPB / 64) * 256 <= SHB_CH, "wcnt fits u_buf");
+uint16_t* const s_msk = (uint16_t*)u_buf;
+static_assert((SHB_TPB / 64) * 256 * 4 >= SHB_CH * 2, "masks fit u_buf");
+// run: halo events per local key, then their inclusive prefix over the keys
 __shared__ uint32_t run[256], tstart[256], ws[SHB_TPB / 64];
 )";
     for (int a : staged_out)
@@ -1003,7 +1005,11 @@ uint32_t rw[SHB_NR];
         const uint32_t r = (uint32_t)__popcll(peers & lt);
         const uint32_t base = valid ? wcnt[wv][d] : 0u;
         rw[k] = valid ? ((base + r) | (d << 16)) : ~0u;
-        if (valid && r == 0) wcnt[wv][d] = base + (uint32_t)__popcll(peers);
+        const uint64_t hal = peers & __ballot(i < hl);  // this round's halo events of key d
+        if (valid && r == 0) {
+            wcnt[wv][d] = base + (uint32_t)__popcll(peers);
+            if (hal) atomicAdd(&run[d], (uint32_t)__popcll(hal));
+        }
     }
 }
 __syncthreads();
@@ -1017,8 +1023,13 @@ __syncthreads();
             tot += c;
         }
     }
-    const uint32_t ex = shw_block_excl<SHB_TPB>(threadIdx.x < 256 ? tot : 0u, ws, &all);
-    if (threadIdx.x < 256) tstart[threadIdx.x] = ex;
+    // one scan for both: span events (low 16 bits) and halo events (high 16 bits) per key
+    const uint32_t h = threadIdx.x < 256 ? run[threadIdx.x] : 0u;
+    const uint32_t ex = shw_block_excl<SHB_TPB>(threadIdx.x < 256 ? (tot | (h << 16)) : 0u, ws, &all);
+    if (threadIdx.x < 256) {
+        tstart[threadIdx.x] = ex & 0xFFFFu;
+        run[threadIdx.x] = (ex >> 16) + h;
+    }
 }
 __syncthreads();
 #pragma unroll
@@ -1028,7 +1039,9 @@ for (int k = 0; k < SHB_NR; k++) {
     const uint32_t d = (rw[k] >> 16) & 0xFFu;
     const int pos = (int)(tstart[d] + wcnt[wv][d] + (rw[k] & 0xFFFFu));
     s_ws[pos] = wr[k];
-    s_idx[pos] = (uint16_t)i;
+    // a key's halo events precede its chunk events in sorted order, so the
+    // consumer's rank is its position less the halo events of keys <= d
+    if (i >= hl) s_cons[pos - (int)run[d]] = (uint32_t)pos | ((uint32_t)(i - hl) << 16);
 
 )";
     for (int a : staged_out) src += "    " + lds(a) + "[pos] = vr" + std::to_string(a) + "[k];\n";
@@ -1036,15 +1049,15 @@ for (int k = 0; k < SHB_NR; k++) {
 __syncthreads();
 SHB_PROF(1)
 // consumers (chunk events) in sorted order: partials taken per event
-for (int sp = threadIdx.x; sp < L; sp += SHB_TPB) {
-const int i = (int)s_idx[sp];
-if (i < hl) continue;
+for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {
+const uint32_t cw = s_cons[ci];
+const int sp = (int)(cw & 0xFFFFu), i = hl + (int)(cw >> 16);
 uint32_t c_ = 0;
 )";
     src += fdom ? walk_count_f() : walk_count();
     src += R"(if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);
 s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);
-s_msk[i - hl] = mask;
+s_msk[i - hl] = (uint16_t)mask;
 }
 __syncthreads();
 SHB_PROF(2)
@@ -1100,9 +1113,9 @@ if (threadIdx.x == 0) P.ctot[gch] = total;
 SHB_PROF(3)
 // the partials again, their e1-side select values into the chunk's region
 const int64_t rbase = gch * SHB_SPAN;
-for (int sp = threadIdx.x; sp < L; sp += SHB_TPB) {
-const int i = (int)s_idx[sp];
-if (i < hl) continue;
+for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {
+const uint32_t cw = s_cons[ci];
+const int sp = (int)(cw & 0xFFFFu), i = hl + (int)(cw >> 16);
 const uint32_t off = s_pre[i - hl];
 const uint32_t cn = ((i + 1 < L) ? (uint32_t)s_pre[i + 1 - hl] : total) - off;
 if (cn == 0u) continue;
