@@ -48,14 +48,28 @@ __device__ __forceinline__ int64_t bk_raw(const void* p, int64_t i, int type) {
     }
 }
 
+// XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs, so
+// block `bid` takes tile (bid % 8) * per + bid / 8 and each XCD walks a
+// contiguous run of arrival tiles; the (bucket, tile) segments of neighbouring
+// tiles share cache lines (partial-line writes of the scatter, count and
+// match-stream gathers of the emitter) and now meet in the same L2. -1: none.
+__device__ __forceinline__ int bk_tile(int nt) {
+    const int per = (nt + 7) >> 3;
+    const int t = (int)(blockIdx.x & 7u) * per + (int)(blockIdx.x >> 3);
+    return t < nt ? t : -1;
+}
+static inline unsigned bk_grid(int nt) { return 8u * (unsigned)((nt + 7) >> 3); }
+
 // ---------------------------------------------------------------- histogram
 __global__ void __launch_bounds__(BK_TPB) k_bk_hist(const int32_t* __restrict__ keys, int64_t n, int32_t nkeys,
                                                     int32_t nt, uint32_t* __restrict__ cnt,
                                                     int32_t* __restrict__ flag) {
     __shared__ uint32_t h[SHB_NB];
+    const int T = bk_tile(nt);
+    if (T < 0) return;
     if (threadIdx.x < SHB_NB) h[threadIdx.x] = 0u;
     __syncthreads();
-    const int64_t b0 = (int64_t)blockIdx.x << SHB_TILE_SHIFT;
+    const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
     bool bad = false;
 #pragma unroll 4
     for (int j = 0; j < BK_ITEMS; j++) {
@@ -68,8 +82,8 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_hist(const int32_t* __restrict__ 
     }
     if (bad) atomicOr(flag, SHB_F_KEY);
     __syncthreads();
-    if (threadIdx.x < SHB_NB) cnt[(int64_t)threadIdx.x * nt + blockIdx.x] = h[threadIdx.x];
-    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(int64_t)SHB_NB * nt] = 0u;
+    if (threadIdx.x < SHB_NB) cnt[(int64_t)threadIdx.x * nt + T] = h[threadIdx.x];
+    if (T == 0 && threadIdx.x == 0) cnt[(int64_t)SHB_NB * nt] = 0u;
 }
 
 // ---------------------------------------------------------------- partition
@@ -81,10 +95,12 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
     __shared__ uint32_t ws[BK_TPB / 64];
     __shared__ uint32_t stage[SHB_TILE];
     __shared__ uint8_t dig[SHB_TILE];
-    const int64_t b0 = (int64_t)blockIdx.x << SHB_TILE_SHIFT;
+    const int T = bk_tile(P.nt);
+    if (T < 0) return;
+    const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int c = threadIdx.x; c < (BK_TPB / 64) * 256; c += BK_TPB) (&wcnt[0][0])[c] = 0u;
-    if (threadIdx.x < 256) gbase[threadIdx.x] = P.base[(int64_t)threadIdx.x * P.nt + blockIdx.x];
+    if (threadIdx.x < 256) gbase[threadIdx.x] = P.base[(int64_t)threadIdx.x * P.nt + T];
     __syncthreads();
     // every load of the tile is issued up front (keys, timestamps and the first
     // staged column when it is 4 bytes wide): one HBM round trip per tile; the
@@ -134,21 +150,34 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
     // each wave ranks its own contiguous 1,024 events (16 rounds of 64): the
     // rank of an event among the wave's same-bucket events before it, from 8
     // ballots per round and the wave's running counts (no block barrier)
+    // the leader lane of each bucket group adds the group to the wave's running
+    // count with a returning LDS atomic (the rounds' atomics issue back to back);
+    // the group reads its base from the leader afterwards
+    {
+        uint32_t old[BK_ITEMS];
 #pragma unroll
-    for (int j = 0; j < BK_ITEMS; j++) {
-        const bool valid = key[j] >= 0;
-        const uint32_t d = (uint32_t)key[j] & (SHB_NB - 1);
-        uint64_t peers = __ballot(valid);
+        for (int j = 0; j < BK_ITEMS; j++) {
+            const bool valid = key[j] >= 0;
+            const uint32_t d = (uint32_t)key[j] & (SHB_NB - 1);
+            uint64_t peers = __ballot(valid);
 #pragma unroll
-        for (int bb = 0; bb < 8; bb++) {
-            const bool bit = (d >> bb) & 1u;
-            const uint64_t m = __ballot(valid && bit);
-            peers &= bit ? m : ~m;
+            for (int bb = 0; bb < 8; bb++) {
+                const bool bit = (d >> bb) & 1u;
+                const uint64_t m = __ballot(valid && bit);
+                peers &= bit ? m : ~m;
+            }
+            const uint32_t r = (uint32_t)__popcll(peers & lt);
+            old[j] = 0u;
+            if (valid && r == 0) old[j] = atomicAdd(&wcnt[w][d], (uint32_t)__popcll(peers));
+            // rank | leader lane << 8 | bucket << 16 (~0u: no key)
+            rw[j] = valid ? (r | ((uint32_t)(__ffsll((unsigned long long)peers) - 1) << 8) | (d << 16)) : ~0u;
         }
-        const uint32_t r = (uint32_t)__popcll(peers & lt);
-        const uint32_t base = valid ? wcnt[w][d] : 0u;
-        rw[j] = valid ? ((base + r) | (d << 16)) : ~0u;  // wave rank | bucket << 16
-        if (valid && r == 0) wcnt[w][d] = base + (uint32_t)__popcll(peers);
+#pragma unroll
+        for (int j = 0; j < BK_ITEMS; j++) {
+            const uint32_t ld = rw[j] == ~0u ? (uint32_t)lane : (rw[j] >> 8) & 63u;
+            const uint32_t base = (uint32_t)__shfl((int)old[j], (int)ld);
+            if (rw[j] != ~0u) rw[j] = ((base + (rw[j] & 0xFFu)) & 0xFFFFu) | (rw[j] & 0xFF0000u);  // wave rank | bucket << 16
+        }
     }
     __syncthreads();
     // per bucket: the waves' exclusive offsets and the tile total, then the
@@ -283,7 +312,8 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
     __shared__ uint16_t evmap[BK_ROWMAP];
     __shared__ uint32_t blk_mpos[BK_TPB];
     __shared__ uint32_t s_tot;
-    const int T = blockIdx.x;
+    const int T = bk_tile(P.nt);
+    if (T < 0) return;
     const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
     const int tile_n = (int)((P.n - b0) < SHB_TILE ? (P.n - b0) : SHB_TILE);
     if (threadIdx.x < 256) {
@@ -448,16 +478,16 @@ extern "C" int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nke
                              void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const int64_t cells = (int64_t)SHB_NB * P->nt + 1;
-    hipLaunchKernelGGL(k_bk_hist, dim3(P->nt), dim3(BK_TPB), 0, st, keys, P->n, nkeys, P->nt, P->base, P->flag);
+    hipLaunchKernelGGL(k_bk_hist, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, P->n, nkeys, P->nt, P->base, P->flag);
     if (bk_ok()) return -3;
     if (shd_exclusive_scan(P->base, P->base, cells, scan_tmp, stream)) return -3;
     // SH_BK_SCAT=1: no occupancy bound on the scatter (more registers, one
     // workgroup per CU); default: 4 waves per SIMD (two workgroups per CU)
     static const int scat = getenv("SH_BK_SCAT") ? atoi(getenv("SH_BK_SCAT")) : 4;
     if (scat == 1)
-        hipLaunchKernelGGL(k_bk_scatter<1>, dim3(P->nt), dim3(BK_TPB), 0, st, keys, ts, *P);
+        hipLaunchKernelGGL(k_bk_scatter<1>, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, *P);
     else
-        hipLaunchKernelGGL(k_bk_scatter<4>, dim3(P->nt), dim3(BK_TPB), 0, st, keys, ts, *P);
+        hipLaunchKernelGGL(k_bk_scatter<4>, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, *P);
     return bk_ok();
 }
 
@@ -473,7 +503,7 @@ extern "C" int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream) {
 
 extern "C" int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, uint64_t seq_base,
                         uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
-    hipLaunchKernelGGL(k_bk_emit, dim3(P->nt), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O, seq_base, out_seq,
+    hipLaunchKernelGGL(k_bk_emit, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O, seq_base, out_seq,
                        out_vals, out_cap);
     return bk_ok();
 }
