@@ -45,6 +45,8 @@ def parse():
                     help="CPU baseline threads for partitioned configs without timers (events split by key; "
                          "0 = 1 thread, except C5: min(16, nproc))")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--columns", action="store_true",
+                    help="c2: typed output columns (d_out_cols) instead of the raw 8-byte rows (d_out_values)")
     ap.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default, BASELINE.json configs[1]); c1 / c3 / c4 / c5 measure the other configs")
     ap.add_argument("--seconds", type=int, default=100, help="c4: stream duration (playback seconds)")
@@ -359,8 +361,13 @@ def main():
     stream = torch.cuda.current_stream(dev)
     with_q = args.config == "c5"
 
+    # --columns: the match stream as typed columns (sh_device_run.d_out_cols: seq 8
+    # + symbol 4 + p1 4 + p2 4 + v2 8 bytes per match) instead of raw 8-byte rows;
+    # fewer bytes but more store instructions (measured slower: 2.25 vs 1.83 ms emit)
+    use_cols = args.config == "c2" and args.columns
+
     def step():
-        r = runner.run(t_ts, t_k, cols, K, stream=stream, with_query=with_q)
+        r = runner.run(t_ts, t_k, cols, K, stream=stream, with_query=with_q, columns=use_cols)
         return r if with_q else r + (None,)
 
     log("warmup")
@@ -408,7 +415,12 @@ def main():
     verified = None
     if not args.no_verify and rank == 0:
         log("verifying the full output against the vectorised restatement")
-        verified = W["verify"](oseq.cpu().numpy(), ovals.cpu().numpy(), oq.cpu().numpy() if oq is not None else None)
+        if use_cols:
+            from siddhi_amd.device_run import columns_to_raw
+            ovals_np = columns_to_raw([c.cpu().numpy() for c in ovals], runner.out_types)
+        else:
+            ovals_np = ovals.cpu().numpy()
+        verified = W["verify"](oseq.cpu().numpy(), ovals_np, oq.cpu().numpy() if oq is not None else None)
 
     # HBM bytes per step from the committed rocprofv3 PMC passes of this
     # workload (scripts/pmc_traffic.py), when they match the configuration
@@ -460,6 +472,7 @@ def main():
                        "path": "pageable host numpy -> HBM (torch .to), before the timed steps"},
             "config": {"workload": W["desc"], "events_per_gpu": n, W["key_name"]: args.keys,
                        "rate_ev_per_ms": args.rate,
+                       "output": "typed columns (d_out_cols)" if use_cols else "raw 8-byte rows (d_out_values)",
                        "matches_per_gpu": int(m), "parallelism": f"key-sharded x{world}",
                        "bytes": W["bytes_note"]},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",

@@ -127,6 +127,11 @@ typedef struct sh_device_run {
     int64_t out_count;           /* out: matches produced                           */
     void* stream;                /* hipStream_t to run on (NULL = default)          */
     int32_t* d_out_query;        /* out (optional): query index per match (ordered) */
+    /* out (optional): the select values as typed columns, one device pointer per
+       output attribute in its natural width (long/double 8 B, int/float/string id
+       4 B, bool 1 B), ordered like d_out_seq. When set, d_out_values may be NULL
+       and is not written; the row-major raw layout stays the default. */
+    void* const* d_out_cols;
 } sh_device_run;
 
 int sh_run_device(sh_handle* h, sh_device_run* run);

@@ -26,6 +26,7 @@
 // + emitter 16 + the match rows; no pass moves the event row more than once.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "../../include/sh_query.h"
 #include "sh_device.h"
@@ -59,6 +60,13 @@ __device__ __forceinline__ int bk_tile(int nt) {
     return t < nt ? t : -1;
 }
 static inline unsigned bk_grid(int nt) { return 8u * (unsigned)((nt + 7) >> 3); }
+
+// one typed output column element (sh_device_run.d_out_cols): natural width
+__device__ __forceinline__ void bk_put(void* col, int w, int64_t row, int64_t v) {
+    if (w == 8) ((int64_t*)col)[row] = v;
+    else if (w == 4) ((uint32_t*)col)[row] = (uint32_t)v;
+    else ((uint8_t*)col)[row] = (uint8_t)v;
+}
 
 // ---------------------------------------------------------------- histogram
 __global__ void __launch_bounds__(BK_TPB) k_bk_hist(const int32_t* __restrict__ keys, int64_t n, int32_t nkeys,
@@ -429,23 +437,34 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
                 const int64_t row = (int64_t)tb + r0 + t;
                 if (row >= out_cap) continue;  // the host reports SH_E_MORE
                 if (out_seq) out_seq[row] = seq_base + (uint64_t)i;
-                if (!out_vals) continue;
+                if (!out_vals && !O.use_cols) continue;
                 // output descriptors straight from the kernel arguments (scalar
                 // registers: uniform branches)
                 if (no == 4) {
-                    // a 32-byte row as two 16-byte stores: consecutive lanes fill whole lines
                     const int64_t mp = (int64_t)blk_mpos[e] + k;
                     const int64_t v0 = bk_raw(O.src[0], O.kind[0] == 1 ? i : mp, O.type[0]);
                     const int64_t v1 = bk_raw(O.src[1], O.kind[1] == 1 ? i : mp, O.type[1]);
                     const int64_t v2 = bk_raw(O.src[2], O.kind[2] == 1 ? i : mp, O.type[2]);
                     const int64_t v3 = bk_raw(O.src[3], O.kind[3] == 1 ? i : mp, O.type[3]);
+                    if (O.use_cols) {
+                        // typed columns: consecutive lanes, consecutive elements of each column
+                        bk_put(O.cols[0], O.colw[0], row, v0);
+                        bk_put(O.cols[1], O.colw[1], row, v1);
+                        bk_put(O.cols[2], O.colw[2], row, v2);
+                        bk_put(O.cols[3], O.colw[3], row, v3);
+                        continue;
+                    }
+                    // a 32-byte row as two 16-byte stores: consecutive lanes fill whole lines
                     longlong2* dst = (longlong2*)(out_vals + row * 4);
                     dst[0] = make_longlong2(v0, v1);
                     dst[1] = make_longlong2(v2, v3);
                     continue;
                 }
-                for (int o = 0; o < no; o++)
-                    out_vals[row * no + o] = bk_raw(O.src[o], O.kind[o] == 1 ? i : (int64_t)blk_mpos[e] + k, O.type[o]);
+                for (int o = 0; o < no; o++) {
+                    const int64_t v = bk_raw(O.src[o], O.kind[o] == 1 ? i : (int64_t)blk_mpos[e] + k, O.type[o]);
+                    if (O.use_cols) bk_put(O.cols[o], O.colw[o], row, v);
+                    else out_vals[row * no + o] = v;
+                }
             }
             __syncthreads();
             continue;
@@ -457,15 +476,14 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
         if (row0 + c > out_cap) continue;
         if (out_seq)
             for (uint32_t k = 0; k < c; k++) out_seq[row0 + k] = seq_base + (uint64_t)i;
-        if (!out_vals) continue;
+        if (!out_vals && !O.use_cols) continue;
         for (int o = 0; o < no; o++) {
             const void* src = o_src[o];
             const int ty = o_type[o];
-            if (o_kind[o] == 1) {
-                const int64_t v = bk_raw(src, i, ty);
-                for (uint32_t k = 0; k < c; k++) out_vals[(row0 + k) * no + o] = v;
-            } else {
-                for (uint32_t k = 0; k < c; k++) out_vals[(row0 + k) * no + o] = bk_raw(src, (int64_t)mpos[j] + k, ty);
+            for (uint32_t k = 0; k < c; k++) {
+                const int64_t v = bk_raw(src, o_kind[o] == 1 ? i : (int64_t)mpos[j] + k, ty);
+                if (O.use_cols) bk_put(O.cols[o], O.colw[o], row0 + k, v);
+                else out_vals[(row0 + k) * no + o] = v;
             }
         }
     }
@@ -505,5 +523,29 @@ extern "C" int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O
                         uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
     hipLaunchKernelGGL(k_bk_emit, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O, seq_base, out_seq,
                        out_vals, out_cap);
+    return bk_ok();
+}
+
+// ---------------------------------------------------------------- typed columns
+// raw 8-byte rows -> typed columns, for engines that write rows
+__global__ void __launch_bounds__(256) k_narrow_rows(const int64_t* __restrict__ vals, int32_t n_out, int64_t m,
+                                                     shb_out O) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= m) return;
+    for (int o = 0; o < n_out; o++) bk_put(O.cols[o], O.colw[o], r, vals[r * n_out + o]);
+}
+
+extern "C" int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, void* const* cols, const int32_t* w,
+                               void* stream) {
+    if (m <= 0) return 0;
+    if (n_out > SHB_MAX_OUT) return -1;
+    shb_out O;
+    memset(&O, 0, sizeof(O));
+    for (int o = 0; o < n_out; o++) {
+        O.cols[o] = cols[o];
+        O.colw[o] = w[o];
+    }
+    hipLaunchKernelGGL(k_narrow_rows, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, vals, n_out,
+                       m, O);
     return bk_ok();
 }

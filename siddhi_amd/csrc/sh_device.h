@@ -133,6 +133,10 @@ struct shb_out {
     int32_t kind[SHB_MAX_OUT];
     int32_t type[SHB_MAX_OUT];    // sh_type: raw-value conversion
     const void* src[SHB_MAX_OUT]; // kind 0: match-stream column, kind 1: consumer column
+    void* cols[SHB_MAX_OUT];      // typed output columns (use_cols), natural width
+    int32_t colw[SHB_MAX_OUT];    // their widths: 8, 4 or 1 bytes
+    int32_t use_cols;             // 1: write cols instead of raw 8-byte rows
+    int32_t pad2;
 };
 
 #ifdef __cplusplus
@@ -180,6 +184,8 @@ int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_pla
 int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream);
 int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, uint64_t seq_base, uint64_t* out_seq,
              int64_t* out_vals, int64_t out_cap, void* stream);
+// raw 8-byte rows [m x n_out] -> typed columns of widths w[o] (8, 4 or 1 bytes)
+int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, void* const* cols, const int32_t* w, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -425,6 +425,10 @@ struct sh_handle {
     DevBuf bk_w0, bk_rk, bk_base, bk_cnt, bk_psum, bk_ctot, bk_cum, bk_ttot, bk_flag, bk_prof;
     DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS];
     PinBuf bk_rd;
+    // typed output columns (sh_device_run.d_out_cols) for engines that write rows
+    DevBuf w_colrows;
+    bool cols_rows = false;
+    std::vector<int32_t> out_types;  // per select position over the queries (-2: types differ)
 };
 
 static void set_layout(shp_layout& Y, const shp_program& P, int32_t cap) {
@@ -743,6 +747,12 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
     *out = h;
     if (app->version != SH_DESC_VERSION) return fail(h, SH_E_INVALID_ARG, "descriptor version mismatch");
     h->app = *app;
+    for (int32_t q = 0; q < app->n_queries; q++)
+        for (int32_t o = 0; o < app->queries[q].n_outputs; o++) {
+            const int32_t t = app->queries[q].outputs[o].type;
+            if ((int32_t)h->out_types.size() <= o) h->out_types.push_back(t);
+            else if (h->out_types[o] != t) h->out_types[o] = -2;
+        }
     if (app->n_streams < 1 || app->n_streams > SHP_MAX_STREAMS)
         return fail(h, SH_E_UNSUPPORTED, "device engine: 1..8 streams per app");
     for (int s = 0; s < app->n_streams; s++) {
@@ -2171,6 +2181,13 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     }
     for (int o = 0; o < O.n_out; o++)
         if (O.kind[o] == 0) O.src[o] = B.ms[(int)(intptr_t)O.src[o]];
+    if (run->d_out_cols) {
+        O.use_cols = 1;
+        for (int o = 0; o < O.n_out; o++) {
+            O.cols[o] = run->d_out_cols[o];
+            O.colw[o] = type_width(O.type[o]);
+        }
+    }
     B.w0 = h->bk_w0.as<uint32_t>();
     B.rk = h->bk_rk.as<uint16_t>();
     B.base = h->bk_base.as<uint32_t>();
@@ -2230,14 +2247,30 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "bucket engine");
 }
 
-int sh_run_device(sh_handle* h, sh_device_run* run) {
-    if (!h || !run) return SH_E_INVALID_ARG;
+// typed output columns requested: engines that write raw rows write them into a
+// workspace that sh_run_device narrows afterwards (the bucketed engine writes
+// the columns itself)
+static int rows_for_cols(sh_handle* h, sh_device_run* run) {
+    if (!run->d_out_cols || h->cols_rows) return SH_OK;
+    if (h->w_colrows.ensure((size_t)std::max<int64_t>(1, run->out_capacity) * std::max(1, h->n_out) * 8))
+        return fail(h, SH_E_OOM, "typed-column row workspace");
+    run->d_out_values = h->w_colrows.as<int64_t>();
+    h->cols_rows = true;
+    return SH_OK;
+}
+
+static int run_device_impl(sh_handle* h, sh_device_run* run) {
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device");
     if (h->app.n_streams != 1) return fail(h, SH_E_UNSUPPORTED, "sh_run_device: single-stream apps only");
     if (run->n <= 0 || run->n > 0x7FFFFFFFll) return fail(h, SH_E_INVALID_ARG, "sh_run_device: 1 <= n < 2^31");
     h->stream = run->stream ? (hipStream_t)run->stream : h->own_stream;
-    if (h->has_rules && (h->mode == 2 || !getenv("SH_DISABLE_RULES"))) return run_rules(h, run);
+    if (h->has_rules && (h->mode == 2 || !getenv("SH_DISABLE_RULES"))) {
+        const int crc = rows_for_cols(h, run);
+        return crc ? crc : run_rules(h, run);
+    }
     if (h->mode == 1) {
+        const int crc = rows_for_cols(h, run);
+        if (crc) return crc;
         // general engine from fresh per-key state; the events arrive as send()
         // calls of run->batch_events
         if (h->T->has_absent) return fail(h, SH_E_UNSUPPORTED, "sh_run_device: absent states need sh_push_batch");
@@ -2290,6 +2323,10 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
     if (h->prog.window_ok) {
         const int brc = run_bucket(h, run, nkeys);
         if (brc != 1) return brc;
+    }
+    {
+        const int crc = rows_for_cols(h, run);
+        if (crc) return crc;
     }
     if (h->prog.window_ok && h->stream_types[0].size() <= 7) {
         const int64_t n = run->n;
@@ -2373,6 +2410,32 @@ int sh_run_device(sh_handle* h, sh_device_run* run) {
         hipMemsetAsync(run->d_out_query, 0, nm * 4, h->stream);
         hipStreamSynchronize(h->stream);
     }
+    return rc;
+}
+
+int sh_run_device(sh_handle* h, sh_device_run* run) {
+    if (!h || !run) return SH_E_INVALID_ARG;
+    if (!run->d_out_cols) return run_device_impl(h, run);
+    // typed columns: one output type per select position across the app's queries
+    int32_t w[SHB_MAX_OUT];
+    if (h->n_out > SHB_MAX_OUT) return fail(h, SH_E_UNSUPPORTED, "typed columns: too many select values");
+    for (int o = 0; o < h->n_out; o++) {
+        const int t = o < (int)h->out_types.size() ? h->out_types[o] : SH_T_LONG;
+        if (t == -2) return fail(h, SH_E_UNSUPPORTED, "typed columns: queries select different types at one position");
+        w[o] = type_width(t);
+    }
+    int64_t* user_vals = run->d_out_values;
+    h->cols_rows = false;
+    int rc = run_device_impl(h, run);
+    if (h->cols_rows) {
+        if (rc == SH_OK && run->out_count > 0) {
+            if (shd_narrow_rows(h->w_colrows.as<int64_t>(), h->n_out, run->out_count, run->d_out_cols, w, h->stream) ||
+                hipStreamSynchronize(h->stream) != hipSuccess)
+                rc = fail(h, SH_E_HIP, "typed-column narrowing failed");
+        }
+        h->cols_rows = false;
+    }
+    run->d_out_values = user_vals;
     return rc;
 }
 

@@ -5,10 +5,30 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
 import torch
 
 from . import abi
+from . import compiler as cp
 from ._native import CompiledHandle, check, lib
+
+
+_TORCH = {cp.LONG: torch.int64, cp.DOUBLE: torch.float64, cp.INT: torch.int32, cp.STRING: torch.int32,
+          cp.FLOAT: torch.float32, cp.BOOL: torch.uint8}
+
+
+def columns_to_raw(cols, types):
+    """typed output columns (numpy) -> the raw 8-byte row values of d_out_values
+    (sh_vm.h load_attr: float bits zero-extended, int / string id sign-extended)"""
+    out = np.empty((len(cols[0]) if cols else 0, len(cols)), dtype=np.int64)
+    for o, (c, t) in enumerate(zip(cols, types)):
+        if t == cp.FLOAT:
+            out[:, o] = c.view(np.uint32).astype(np.int64)
+        elif t == cp.DOUBLE:
+            out[:, o] = c.view(np.int64)
+        else:
+            out[:, o] = c.astype(np.int64)
+    return out
 
 
 class DeviceRunner:
@@ -17,21 +37,33 @@ class DeviceRunner:
         self.device = torch.device(device)
         self.handle = CompiledHandle(compiled)
         self.n_out = max([1] + [len(q.outs) for q in compiled.queries])
+        self.out_types = list(compiled.queries[0].out_types) if compiled.queries else []
         self._out_cap = 0
+        self._col_cap = 0
 
-    def run(self, ts, keys, cols, n_keys, out_capacity=None, stream=None, batch_events=4096, with_query=False):
+    def run(self, ts, keys, cols, n_keys, out_capacity=None, stream=None, batch_events=4096, with_query=False,
+            columns=False):
         """ts/keys/cols: device tensors (int64 / int32 / stream attribute order);
         the events arrive as send(Event[]) calls of `batch_events`.
         Returns (n_matches, out_seq[n], out_values[n, n_out]) as device tensors,
-        plus out_query[n] (emitting query index) when `with_query`."""
+        plus out_query[n] (emitting query index) when `with_query`. With
+        `columns`, out_values is a list of typed columns (sh_device_run.d_out_cols:
+        natural width per select attribute) instead of the raw 8-byte rows."""
         n = ts.numel()
         cap = out_capacity or n
         for attempt in range(2):
             if self._out_cap < cap:
                 self.out_seq = torch.empty(cap, dtype=torch.int64, device=self.device)
-                self.out_vals = torch.empty(cap * self.n_out, dtype=torch.int64, device=self.device)
+                self.out_vals = (torch.empty(0, dtype=torch.int64, device=self.device) if columns else
+                                 torch.empty(cap * self.n_out, dtype=torch.int64, device=self.device))
                 self.out_q = torch.empty(cap, dtype=torch.int32, device=self.device)
                 self._out_cap = cap
+            if columns and (self._col_cap < self._out_cap or not hasattr(self, "out_cols")):
+                self.out_cols = [torch.empty(self._out_cap, dtype=_TORCH[t], device=self.device)
+                                 for t in self.out_types]
+                self._col_cap = self._out_cap
+            if not columns and self.out_vals.numel() < self._out_cap * self.n_out:
+                self.out_vals = torch.empty(self._out_cap * self.n_out, dtype=torch.int64, device=self.device)
             cp = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
             r = abi.sh_device_run()
             r.n = n
@@ -42,7 +74,10 @@ class DeviceRunner:
             r.d_cols = cp
             r.out_capacity = self._out_cap
             r.d_out_seq = self.out_seq.data_ptr()
-            r.d_out_values = self.out_vals.data_ptr()
+            r.d_out_values = None if columns else self.out_vals.data_ptr()
+            if columns:
+                ocp = (C.c_void_p * len(self.out_cols))(*[c.data_ptr() for c in self.out_cols])
+                r.d_out_cols = ocp
             r.stream = stream.cuda_stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
             r.d_out_query = self.out_q.data_ptr() if with_query else None
             rc = lib().sh_run_device(self.handle.h, C.byref(r))
@@ -53,6 +88,9 @@ class DeviceRunner:
             check(self.handle.h, rc)
             break
         m = int(r.out_count)
+        if columns:
+            res = (m, self.out_seq[:m], [c[:m] for c in self.out_cols])
+            return res + (self.out_q[:m],) if with_query else res
         res = (m, self.out_seq[:m], self.out_vals[: m * self.n_out].view(m, self.n_out))
         return res + (self.out_q[:m],) if with_query else res
 

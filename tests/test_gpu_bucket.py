@@ -25,17 +25,24 @@ def _device():
         pytest.skip("no GPU")
 
 
-def _run(app, strings, ts, cols, keys, nk):
+def _run(app, strings, ts, cols, keys, nk, columns=False):
+    """columns: typed output columns (d_out_cols), returned as raw rows for comparison"""
     import torch
-    from siddhi_amd.device_run import DeviceRunner
+    from siddhi_amd.device_run import DeviceRunner, columns_to_raw
     runner = DeviceRunner(compiler.compile_app(app, strings))
     dev = torch.device("cuda:0")
     tcols = [torch.from_numpy(c).to(dev) for c in cols]
-    m, oseq, ovals = runner.run(torch.from_numpy(ts).to(dev), torch.from_numpy(keys).to(dev), tcols, nk)
+    m, oseq, ovals = runner.run(torch.from_numpy(ts).to(dev), torch.from_numpy(keys).to(dev), tcols, nk,
+                                columns=columns)
     torch.cuda.synchronize()
     status = runner.bucket_status()
     err = runner.last_error()
-    res = (m, oseq.cpu().numpy(), ovals.cpu().numpy())
+    if columns:
+        assert [c.dtype for c in ovals] == [{0: torch.int32, 1: torch.int32, 2: torch.int64, 3: torch.float32,
+                                             4: torch.float64, 5: torch.uint8}[t] for t in runner.out_types]
+        res = (m, oseq.cpu().numpy(), columns_to_raw([c.cpu().numpy() for c in ovals], runner.out_types))
+    else:
+        res = (m, oseq.cpu().numpy(), ovals.cpu().numpy())
     runner.close()
     return res, status, err
 
@@ -52,12 +59,16 @@ def test_c2_bucket_vs_oracle():
     assert np.array_equal(ovals, vals)
 
 
-@pytest.mark.parametrize("n,nk,bucketed", [(10_000_000, 10_000, 1), (100_000_000, 10_000, 1), (3_000_000, 60_000, 0)])
-def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed):
+@pytest.mark.parametrize("n,nk,bucketed,columns", [(10_000_000, 10_000, 1, False), (100_000_000, 10_000, 1, False),
+                                                   (100_000_000, 10_000, 1, True), (3_000_000, 60_000, 0, False),
+                                                   (3_000_000, 60_000, 0, True)])
+def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed, columns):
     """60k symbols at 100 ev/ms: a key's previous event is often beyond the
-    matcher's halo (SHB_HALO bucket events), so the run falls back -- exactly"""
+    matcher's halo (SHB_HALO bucket events), so the run falls back -- exactly.
+    `columns`: typed output columns (the bucketed engine writes them itself, the
+    fallback's rows are narrowed)"""
     ts, k, p, v = synth.stock_stream(n, nk, 100)
-    (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk)
+    (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk, columns)
     assert status == bucketed, err
     eseq, evals = c2_expected(ts, k, p, v)
     assert m == len(eseq) > 0
