@@ -110,30 +110,24 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
     for (int c = threadIdx.x; c < (BK_TPB / 64) * 256; c += BK_TPB) (&wcnt[0][0])[c] = 0u;
     if (threadIdx.x < 256) gbase[threadIdx.x] = P.base[(int64_t)threadIdx.x * P.nt + T];
     __syncthreads();
-    // every load of the tile is issued up front (keys, timestamps and the first
-    // staged column when it is 4 bytes wide): one HBM round trip per tile; the
-    // packed word (ts - tbase) << kb | key >> 8 is formed in registers
+    // the keys and timestamps of the tile are loaded up front (one HBM round
+    // trip); the packed word (ts - tbase) << kb | key >> 8 is formed in registers
     int32_t key[BK_ITEMS];
-    uint32_t rw[BK_ITEMS], wp[BK_ITEMS], v0[BK_ITEMS];
-    const bool pre0 = P.n_staged > 0 && P.st_width[0] == 4;  // uniform
-    const uint32_t* __restrict__ src0 = (const uint32_t*)P.st_src[0];
+    // (staged columns are loaded after the packed words are written: prefetching
+    // them as well spills registers at two workgroups per CU)
+    uint32_t rw[BK_ITEMS], wp[BK_ITEMS];
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     {
         int64_t tv[BK_ITEMS];
         const int64_t e0 = b0 + (int64_t)w * (64 * BK_ITEMS) + lane;
         if (b0 + SHB_TILE <= P.n) {
-            // a full tile: unpredicated loads at immediate offsets from three bases
+            // a full tile: unpredicated loads at immediate offsets from two bases
             const int32_t* __restrict__ pk = keys + e0;
             const int64_t* __restrict__ pt = ts + e0;
-            const uint32_t* __restrict__ pv = src0 + e0;
 #pragma unroll
             for (int j = 0; j < BK_ITEMS; j++) {
                 key[j] = pk[j * 64];
                 tv[j] = pt[j * 64];
-            }
-            if (pre0) {
-#pragma unroll
-                for (int j = 0; j < BK_ITEMS; j++) v0[j] = pv[j * 64];
             }
         } else {
 #pragma unroll
@@ -142,7 +136,6 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
                 const bool in = i < P.n;
                 key[j] = in ? keys[i] : -1;
                 tv[j] = in ? ts[i] : P.tbase;
-                v0[j] = (in && pre0) ? src0[i] : 0u;
             }
         }
         const int64_t lim = (int64_t)1 << (32 - P.kb);
@@ -152,6 +145,8 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
             const int64_t dt = tv[j] - P.tbase;
             if (key[j] >= 0 && (dt < 0 || dt >= lim)) bad = true;
             wp[j] = ((uint32_t)dt << P.kb) | ((uint32_t)key[j] >> 8);
+            // the key is not needed past this point: bucket << 16 (~0u: no key)
+            rw[j] = key[j] >= 0 ? ((uint32_t)key[j] & (SHB_NB - 1)) << 16 : ~0u;
         }
         if (bad) atomicOr(P.flag, SHB_F_TS);
     }
@@ -165,8 +160,8 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
         uint32_t old[BK_ITEMS];
 #pragma unroll
         for (int j = 0; j < BK_ITEMS; j++) {
-            const bool valid = key[j] >= 0;
-            const uint32_t d = (uint32_t)key[j] & (SHB_NB - 1);
+            const bool valid = rw[j] != ~0u;
+            const uint32_t d = (rw[j] >> 16) & (SHB_NB - 1);
             uint64_t peers = __ballot(valid);
 #pragma unroll
             for (int bb = 0; bb < 8; bb++) {
@@ -222,7 +217,7 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
     __syncthreads();
 #define BK_WRITE_OUT(T, DST, EXPR)                                                   \
     {                                                                                \
-        for (int m = 0; m < BK_ITEMS; m++) {                                         \
+        _Pragma("unroll 4") for (int m = 0; m < BK_ITEMS; m++) {                     \
             const uint32_t l = (uint32_t)(m * BK_TPB + threadIdx.x);                 \
             if (l < nvalid) {                                                        \
                 const uint32_t d = dig[l];                                           \
@@ -244,8 +239,7 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
                 if (rw[j] == ~0u) continue;
                 const int64_t i = b0 + (int64_t)w * (64 * BK_ITEMS) + j * 64 + lane;
                 uint32_t v;
-                if (c == 0 && pre0) v = v0[j];  // prefetched with the keys
-                else if (wd == 8) v = ((const uint32_t*)P.st_src[c])[2 * i + hh];
+                if (wd == 8) v = ((const uint32_t*)P.st_src[c])[2 * i + hh];
                 else if (wd == 4) v = ((const uint32_t*)P.st_src[c])[i];
                 else v = ((const uint8_t*)P.st_src[c])[i];
                 stage[rw[j]] = v;

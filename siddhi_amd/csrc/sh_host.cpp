@@ -429,6 +429,7 @@ struct sh_handle {
     DevBuf w_colrows;
     bool cols_rows = false;
     std::vector<int32_t> out_types;  // per select position over the queries (-2: types differ)
+    uint64_t fp = 0;                 // compiled-program fingerprint (snapshot images)
 };
 
 static void set_layout(shp_layout& Y, const shp_program& P, int32_t cap) {
@@ -740,6 +741,21 @@ static int compile_nfa(sh_handle* h, const sh_app_desc* app) {
     return SH_OK;
 }
 
+// FNV-1a over the lowered program as compiled (before any capacity growth):
+// snapshot images restore only into a handle compiled from the same app
+static uint64_t fnv1a(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
+    const uint8_t* b = (const uint8_t*)p;
+    for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+static uint64_t program_fingerprint(const sh_handle* h) {
+    uint64_t f = fnv1a(&h->mode, sizeof(h->mode));
+    if (h->mode == 1 && h->T) return fnv1a(h->T, sizeof(nf_table), f);
+    f = fnv1a(&h->prog, sizeof(h->prog), f);
+    for (const auto& t : h->stream_types) f = fnv1a(t.data(), t.size() * sizeof(int32_t), f);
+    return f;
+}
+
 int sh_compile(const sh_app_desc* app, sh_handle** out) {
     if (!app || !out) return SH_E_INVALID_ARG;
     *out = nullptr;
@@ -778,6 +794,7 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
         }
     }
     if (rc) return rc;
+    h->fp = program_fingerprint(h);
     h->has_device = device_available();
     if (!h->has_device) return SH_OK;  // compile is host-only; processing needs a device
     hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
