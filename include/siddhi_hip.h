@@ -146,6 +146,21 @@ typedef struct sh_kernel_times {
 } sh_kernel_times;
 int sh_last_kernel_times(sh_handle* h, sh_kernel_times* t);
 
+/* Snapshot of the matcher state -- replaces the State.snapshot() maps of the
+   pattern processors collected by SiddhiAppRuntime.snapshot() / persist()
+   (core/util/snapshot/SnapshotService.java:90-187; state/StreamPreStateProcessor.java:
+   450-469): every partial match with the events it holds, scheduler queues and
+   their HashMap-order models, per-key aggregates, the playback clock, sequence
+   counters and undelivered output, as one opaque versioned image. Pending send()s
+   are processed first. buf == NULL or cap < size: *size is set and SH_E_MORE
+   returned. */
+int sh_snapshot(sh_handle* h, void* buf, int64_t cap, int64_t* size);
+/* Restore an image into a handle compiled from the same app that has not
+   processed events yet (SiddhiAppRuntime.restore(byte[]) / restoreLastRevision,
+   SnapshotService.java:333-430). SH_E_INVALID_ARG: another app's image or a
+   damaged one. */
+int sh_restore(sh_handle* h, const void* buf, int64_t size);
+
 /* library / device info */
 const char* sh_version(void);
 int sh_device_count(void);

@@ -5,8 +5,10 @@ host-side mirror of the SiddhiManager / SiddhiAppRuntime / InputHandler /
 StreamCallback API plus the SiddhiQL subset compiler that lowers apps to the
 boundary descriptor (include/sh_query.h).
 """
-from .runtime import (Event, InputHandler, QueryCallback, SiddhiAppCreationException,
-                      SiddhiAppRuntime, SiddhiAppRuntimeException, SiddhiManager, StreamCallback)
+from .runtime import (Event, InMemoryPersistenceStore, InputHandler, NoPersistenceStoreException, QueryCallback,
+                      SiddhiAppCreationException, SiddhiAppRuntime, SiddhiAppRuntimeException, SiddhiManager,
+                      StreamCallback)
 
 __all__ = ["SiddhiManager", "SiddhiAppRuntime", "InputHandler", "StreamCallback", "QueryCallback",
-           "Event", "SiddhiAppCreationException", "SiddhiAppRuntimeException"]
+           "Event", "SiddhiAppCreationException", "SiddhiAppRuntimeException", "InMemoryPersistenceStore",
+           "NoPersistenceStoreException"]

@@ -105,6 +105,20 @@ class HipEngine:
     def advance_time(self, now):
         check(self.h, _lib.sh_advance_time(self.h, int(now)))
 
+    def snapshot(self) -> bytes:
+        """the matcher state image (sh_snapshot)"""
+        size = C.c_int64(0)
+        rc = _lib.sh_snapshot(self.h, None, 0, C.byref(size))
+        if rc != abi.SH_E_MORE:
+            check(self.h, rc)
+        buf = C.create_string_buffer(max(1, size.value))
+        check(self.h, _lib.sh_snapshot(self.h, buf, size.value, C.byref(size)))
+        return buf.raw[: size.value]
+
+    def restore(self, image: bytes):
+        """load an image taken from an engine of the same app (sh_restore)"""
+        check(self.h, _lib.sh_restore(self.h, image, len(image)))
+
     def drain(self):
         n = _lib.sh_pending(self.h)
         if n < 0:

@@ -82,7 +82,7 @@ class sh_kernel_times(C.Structure):
 # every symbol include/siddhi_hip.h declares (checked by tests/test_abi.py)
 EXPORTED = ["sh_start", "sh_compile", "sh_push_batch", "sh_advance_time", "sh_drain", "sh_pending",
             "sh_destroy", "sh_last_error", "sh_run_device", "sh_last_kernel_times",
-            "sh_version", "sh_device_count", "sh_set_partition_keys"]
+            "sh_version", "sh_device_count", "sh_set_partition_keys", "sh_snapshot", "sh_restore"]
 
 
 def bind_product(lib):
@@ -108,6 +108,10 @@ def bind_product(lib):
     lib.sh_run_device.restype = C.c_int
     lib.sh_last_kernel_times.argtypes = [C.c_void_p, C.POINTER(sh_kernel_times)]
     lib.sh_last_kernel_times.restype = C.c_int
+    lib.sh_snapshot.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+    lib.sh_snapshot.restype = C.c_int
+    lib.sh_restore.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    lib.sh_restore.restype = C.c_int
     lib.sh_version.argtypes = []
     lib.sh_version.restype = C.c_char_p
     lib.sh_device_count.argtypes = []

@@ -303,8 +303,9 @@ __global__ void __launch_bounds__(256) k_bk_ttot(shb_plan P) {
 // ---------------------------------------------------------------- emitter
 // per event (registers): bucket d | count << 8 | rank << 16, and its
 // match-stream position; the select list lives in LDS (uniform per output)
+template <bool COLS>  // COLS: typed output columns (OC.cols), else raw 8-byte rows
 __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ keys, shb_plan P, shb_out O,
-                                                    uint64_t seq_base, uint64_t* __restrict__ out_seq,
+                                                    shb_cols OC, uint64_t seq_base, uint64_t* __restrict__ out_seq,
                                                     int64_t* __restrict__ out_vals, int64_t out_cap) {
     __shared__ uint32_t run[256], lstart[256], segx[256], bstart[256], psum[256];
     __shared__ uint32_t ws[BK_TPB / 64];
@@ -431,7 +432,7 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
                 const int64_t row = (int64_t)tb + r0 + t;
                 if (row >= out_cap) continue;  // the host reports SH_E_MORE
                 if (out_seq) out_seq[row] = seq_base + (uint64_t)i;
-                if (!out_vals && !O.use_cols) continue;
+                if (!out_vals && !COLS) continue;
                 // output descriptors straight from the kernel arguments (scalar
                 // registers: uniform branches)
                 if (no == 4) {
@@ -440,12 +441,12 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
                     const int64_t v1 = bk_raw(O.src[1], O.kind[1] == 1 ? i : mp, O.type[1]);
                     const int64_t v2 = bk_raw(O.src[2], O.kind[2] == 1 ? i : mp, O.type[2]);
                     const int64_t v3 = bk_raw(O.src[3], O.kind[3] == 1 ? i : mp, O.type[3]);
-                    if (O.use_cols) {
+                    if (COLS) {
                         // typed columns: consecutive lanes, consecutive elements of each column
-                        bk_put(O.cols[0], O.colw[0], row, v0);
-                        bk_put(O.cols[1], O.colw[1], row, v1);
-                        bk_put(O.cols[2], O.colw[2], row, v2);
-                        bk_put(O.cols[3], O.colw[3], row, v3);
+                        bk_put(OC.cols[0], OC.colw[0], row, v0);
+                        bk_put(OC.cols[1], OC.colw[1], row, v1);
+                        bk_put(OC.cols[2], OC.colw[2], row, v2);
+                        bk_put(OC.cols[3], OC.colw[3], row, v3);
                         continue;
                     }
                     // a 32-byte row as two 16-byte stores: consecutive lanes fill whole lines
@@ -456,7 +457,7 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
                 }
                 for (int o = 0; o < no; o++) {
                     const int64_t v = bk_raw(O.src[o], O.kind[o] == 1 ? i : (int64_t)blk_mpos[e] + k, O.type[o]);
-                    if (O.use_cols) bk_put(O.cols[o], O.colw[o], row, v);
+                    if (COLS) bk_put(OC.cols[o], OC.colw[o], row, v);
                     else out_vals[row * no + o] = v;
                 }
             }
@@ -470,13 +471,13 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
         if (row0 + c > out_cap) continue;
         if (out_seq)
             for (uint32_t k = 0; k < c; k++) out_seq[row0 + k] = seq_base + (uint64_t)i;
-        if (!out_vals && !O.use_cols) continue;
+        if (!out_vals && !COLS) continue;
         for (int o = 0; o < no; o++) {
             const void* src = o_src[o];
             const int ty = o_type[o];
             for (uint32_t k = 0; k < c; k++) {
                 const int64_t v = bk_raw(src, o_kind[o] == 1 ? i : (int64_t)mpos[j] + k, ty);
-                if (O.use_cols) bk_put(O.cols[o], O.colw[o], row0 + k, v);
+                if (COLS) bk_put(OC.cols[o], OC.colw[o], row0 + k, v);
                 else out_vals[(row0 + k) * no + o] = v;
             }
         }
@@ -513,33 +514,37 @@ extern "C" int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream) {
     return shd_exclusive_scan(P->ttot, P->ttot, (int64_t)P->nt + 1, scan_tmp, stream);
 }
 
-extern "C" int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, uint64_t seq_base,
-                        uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
-    hipLaunchKernelGGL(k_bk_emit, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O, seq_base, out_seq,
-                       out_vals, out_cap);
+extern "C" int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, const shb_cols* OC,
+                        uint64_t seq_base, uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
+    if (OC && OC->use)
+        hipLaunchKernelGGL(k_bk_emit<true>, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O,
+                           *OC, seq_base, out_seq, out_vals, out_cap);
+    else
+        hipLaunchKernelGGL(k_bk_emit<false>, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O,
+                           shb_cols{}, seq_base, out_seq, out_vals, out_cap);
     return bk_ok();
 }
 
 // ---------------------------------------------------------------- typed columns
 // raw 8-byte rows -> typed columns, for engines that write rows
 __global__ void __launch_bounds__(256) k_narrow_rows(const int64_t* __restrict__ vals, int32_t n_out, int64_t m,
-                                                     shb_out O) {
+                                                     shb_cols OC) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= m) return;
-    for (int o = 0; o < n_out; o++) bk_put(O.cols[o], O.colw[o], r, vals[r * n_out + o]);
+    for (int o = 0; o < n_out; o++) bk_put(OC.cols[o], OC.colw[o], r, vals[r * n_out + o]);
 }
 
 extern "C" int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, void* const* cols, const int32_t* w,
                                void* stream) {
     if (m <= 0) return 0;
     if (n_out > SHB_MAX_OUT) return -1;
-    shb_out O;
-    memset(&O, 0, sizeof(O));
+    shb_cols OC;
+    memset(&OC, 0, sizeof(OC));
     for (int o = 0; o < n_out; o++) {
-        O.cols[o] = cols[o];
-        O.colw[o] = w[o];
+        OC.cols[o] = cols[o];
+        OC.colw[o] = w[o];
     }
     hipLaunchKernelGGL(k_narrow_rows, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, vals, n_out,
-                       m, O);
+                       m, OC);
     return bk_ok();
 }

@@ -133,10 +133,14 @@ struct shb_out {
     int32_t kind[SHB_MAX_OUT];
     int32_t type[SHB_MAX_OUT];    // sh_type: raw-value conversion
     const void* src[SHB_MAX_OUT]; // kind 0: match-stream column, kind 1: consumer column
-    void* cols[SHB_MAX_OUT];      // typed output columns (use_cols), natural width
+};
+
+// typed output columns (sh_device_run.d_out_cols) instead of raw 8-byte rows
+struct shb_cols {
+    void* cols[SHB_MAX_OUT];      // natural width per select value
     int32_t colw[SHB_MAX_OUT];    // their widths: 8, 4 or 1 bytes
-    int32_t use_cols;             // 1: write cols instead of raw 8-byte rows
-    int32_t pad2;
+    int32_t use;                  // 1: write the columns
+    int32_t pad;
 };
 
 #ifdef __cplusplus
@@ -182,8 +186,8 @@ int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* t
 int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_plan* P, uint32_t* scan_tmp,
                   void* stream);
 int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream);
-int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, uint64_t seq_base, uint64_t* out_seq,
-             int64_t* out_vals, int64_t out_cap, void* stream);
+int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base,
+             uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream);
 // raw 8-byte rows [m x n_out] -> typed columns of widths w[o] (8, 4 or 1 bytes)
 int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, void* const* cols, const int32_t* w, void* stream);
 #ifdef __cplusplus

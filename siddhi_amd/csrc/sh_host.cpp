@@ -2198,11 +2198,13 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     }
     for (int o = 0; o < O.n_out; o++)
         if (O.kind[o] == 0) O.src[o] = B.ms[(int)(intptr_t)O.src[o]];
+    shb_cols OC;
+    memset(&OC, 0, sizeof(OC));
     if (run->d_out_cols) {
-        O.use_cols = 1;
+        OC.use = 1;
         for (int o = 0; o < O.n_out; o++) {
-            O.cols[o] = run->d_out_cols[o];
-            O.colw[o] = type_width(O.type[o]);
+            OC.cols[o] = run->d_out_cols[o];
+            OC.colw[o] = type_width(O.type[o]);
         }
     }
     B.w0 = h->bk_w0.as<uint32_t>();
@@ -2236,7 +2238,7 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
         return fail(h, SH_E_HIP, "shb_match launch failed");
     if (shb_finish(&B, h->w_scan.as<uint32_t>(), st)) return fail(h, SH_E_HIP, "bucket scan launch failed");
     hipEventRecord(h->ev[2], st);
-    if (shb_emit(run->d_keys, &B, &O, 0, run->d_out_seq, run->d_out_values, run->out_capacity, st))
+    if (shb_emit(run->d_keys, &B, &O, &OC, 0, run->d_out_seq, run->d_out_values, run->out_capacity, st))
         return fail(h, SH_E_HIP, "bucket emit launch failed");
     hipEventRecord(h->ev[3], st);
     hipMemcpyAsync(h->bk_rd.as<void>(0), B.flag, 4, hipMemcpyDeviceToHost, st);
@@ -2525,6 +2527,289 @@ int64_t shx_jit_source(sh_handle* h, char* buf, int64_t len) {
 int sh_last_kernel_times(sh_handle* h, sh_kernel_times* t) {
     if (!h || !t) return SH_E_INVALID_ARG;
     *t = h->times;
+    return SH_OK;
+}
+
+// ---- snapshot / restore (State.snapshot / restore of the pattern processors,
+// StreamPreStateProcessor.java:450-469, driven by SnapshotService.java:90-187,
+// 333-430): one opaque, versioned image of everything the matcher carries between
+// calls -- partial matches and their events (the column stores they index), the
+// schedulers (queues, armed-key lists, HashMap-order models), per-key aggregates,
+// the playback clock, sequence counters and undelivered output.
+}  // extern "C"
+
+namespace {
+const uint32_t kSnapMagic = 0x31534853u;  // "SHS1"
+const uint32_t kSnapVersion = 1;
+
+struct SnapW {
+    std::vector<uint8_t> b;
+    bool bad = false;
+    void raw(const void* p, size_t n) {
+        const uint8_t* q = (const uint8_t*)p;
+        b.insert(b.end(), q, q + n);
+    }
+    template <class T>
+    void put(const T& v) {
+        raw(&v, sizeof(T));
+    }
+    template <class T>
+    void vec(const std::vector<T>& v) {
+        put<uint64_t>(v.size());
+        if (!v.empty()) raw(v.data(), v.size() * sizeof(T));
+    }
+    void dev(const DevBuf& d, size_t n) {
+        put<uint64_t>(n);
+        if (!n) return;
+        if (!d.p || d.bytes < n) {
+            bad = true;
+            return;
+        }
+        const size_t at = b.size();
+        b.resize(at + n);
+        if (hipMemcpy(b.data() + at, d.p, n, hipMemcpyDeviceToHost) != hipSuccess) bad = true;
+    }
+};
+
+struct SnapR {
+    const uint8_t* p;
+    size_t n, at = 0;
+    bool bad = false;
+    bool raw(void* d, size_t k) {
+        if (bad || k > n - at) {
+            bad = true;
+            return false;
+        }
+        memcpy(d, p + at, k);
+        at += k;
+        return true;
+    }
+    template <class T>
+    T get() {
+        T v{};
+        raw(&v, sizeof(T));
+        return v;
+    }
+    template <class T>
+    void vec(std::vector<T>& v) {
+        const uint64_t k = get<uint64_t>();
+        if (bad || k > (n - at) / sizeof(T)) {
+            bad = true;
+            return;
+        }
+        v.resize(k);
+        if (k) raw(v.data(), k * sizeof(T));
+    }
+    // restores n bytes into d (grown as needed); returns the byte count
+    uint64_t dev(DevBuf& d) {
+        const uint64_t k = get<uint64_t>();
+        if (bad || k > n - at) {
+            bad = true;
+            return 0;
+        }
+        if (!k) return 0;
+        if (d.ensure(k) || hipMemcpy(d.p, p + at, k, hipMemcpyHostToDevice) != hipSuccess) bad = true;
+        at += k;
+        return k;
+    }
+};
+
+void put_jmap(SnapW& w, const ShJMap& M) {
+    w.vec(M.h);
+    w.vec(M.nx);
+    w.vec(M.pv);
+    w.vec(M.pa);
+    w.vec(M.lf);
+    w.vec(M.rt);
+    w.vec(M.fl);
+    w.vec(M.code);
+    w.vec(M.tab);
+    w.put(M.size);
+    w.put(M.threshold);
+    w.put(M.ord);
+    std::vector<int32_t> irr(M.irregular.begin(), M.irregular.end());
+    std::sort(irr.begin(), irr.end());
+    w.vec(irr);
+    w.vec(M.dirty);
+    w.put<uint8_t>(M.rerank_all ? 1 : 0);
+}
+
+void get_jmap(SnapR& r, ShJMap& M) {
+    r.vec(M.h);
+    r.vec(M.nx);
+    r.vec(M.pv);
+    r.vec(M.pa);
+    r.vec(M.lf);
+    r.vec(M.rt);
+    r.vec(M.fl);
+    r.vec(M.code);
+    r.vec(M.tab);
+    M.size = r.get<int32_t>();
+    M.threshold = r.get<int32_t>();
+    M.ord = r.get<uint64_t>();
+    std::vector<int32_t> irr;
+    r.vec(irr);
+    M.irregular = std::unordered_set<int32_t>(irr.begin(), irr.end());
+    r.vec(M.dirty);
+    M.rerank_all = r.get<uint8_t>() != 0;
+}
+}  // namespace
+
+static int snapshot_image(sh_handle* h, SnapW& w) {
+    if (h->mode == 2) return fail(h, SH_E_UNSUPPORTED, "snapshot: rule sets run through sh_run_device only");
+    int rc = flush(h);  // pending send()s are processed first
+    if (rc) return rc;
+    if (h->has_device && hipStreamSynchronize(h->stream) != hipSuccess) return fail(h, SH_E_HIP, "snapshot sync");
+    w.put(kSnapMagic);
+    w.put(kSnapVersion);
+    w.put<int32_t>(h->mode);
+    w.put(h->fp);
+    w.put(h->seq_next);
+    w.put(h->seq_staged0);
+    w.put(h->max_key);
+    w.put(h->clock);
+    w.put(h->tick);
+    w.put<uint8_t>(h->started ? 1 : 0);
+    w.put(h->batch_id);
+    w.vec(h->o_query);
+    w.vec(h->o_seq);
+    w.vec(h->o_ts);
+    w.vec(h->o_vals);
+    w.vec(h->o_nulls);
+    w.put(h->o_read);
+    w.put<int32_t>((int32_t)h->stores.size());
+    for (size_t s = 0; s < h->stores.size(); s++) {
+        const auto& st = h->stores[s];
+        w.put(st.rows);
+        w.put<int32_t>((int32_t)st.cols.size());
+        for (size_t a = 0; a < st.cols.size(); a++) {
+            w.put<uint8_t>(st.has_nul[a] ? 1 : 0);
+            w.dev(st.cols[a], (size_t)st.rows * type_width(h->stream_types[s][a]));
+            w.dev(st.nuls[a], st.has_nul[a] ? (size_t)st.rows : 0);
+        }
+    }
+    if (h->mode == 0) {
+        w.put(h->lay);
+        w.put(h->nkeys_alloc);
+        w.dev(h->d_kstate, (size_t)h->nkeys_alloc * h->lay.key_bytes);
+    } else {
+        w.put(*h->T);
+        w.raw(h->caps, sizeof(h->caps));
+        w.put(h->n_nkeys);
+        w.put<int32_t>(h->klist_cur);
+        const size_t nk = (size_t)h->n_nkeys;
+        w.dev(h->n_kstate, nk * h->T->key_words * 8);
+        w.dev(h->n_armed, nk);
+        w.dev(h->n_klist[0], nk ? nk * 4 : 0);
+        w.dev(h->n_klist[1], nk ? nk * 4 : 0);
+        w.dev(h->n_arm_log, nk ? nk * 4 : 0);
+        w.dev(h->n_klist_n, h->n_klist_n.p ? 16 : 0);
+        w.dev(h->n_arm_ctr, h->n_arm_ctr.p ? 8 : 0);
+        w.put<uint8_t>(h->sm_on ? 1 : 0);
+        if (h->sm_on) {
+            w.vec(h->sm.chars);
+            w.vec(h->sm.off);
+            w.vec(h->sm.len);
+            w.vec(h->sm.hash);
+            w.vec(h->sm.used);
+            for (int s : h->sm.used) {
+                put_jmap(w, h->sm.maps[s]);
+                w.dev(h->n_rank[s], nk * 8);
+            }
+        }
+    }
+    if (w.bad) return fail(h, SH_E_HIP, "snapshot: device read-back failed");
+    return SH_OK;
+}
+
+extern "C" {
+
+int sh_snapshot(sh_handle* h, void* buf, int64_t cap, int64_t* size) {
+    if (!h || !size || (cap > 0 && !buf)) return SH_E_INVALID_ARG;
+    SnapW w;
+    const int rc = snapshot_image(h, w);
+    if (rc) return rc;
+    *size = (int64_t)w.b.size();
+    if (!buf || cap < *size) return SH_E_MORE;
+    memcpy(buf, w.b.data(), w.b.size());
+    return SH_OK;
+}
+
+int sh_restore(sh_handle* h, const void* buf, int64_t size) {
+    if (!h || !buf || size <= 0) return SH_E_INVALID_ARG;
+    if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
+    SnapR r{(const uint8_t*)buf, (size_t)size};
+    if (r.get<uint32_t>() != kSnapMagic || r.get<uint32_t>() != kSnapVersion)
+        return fail(h, SH_E_INVALID_ARG, "restore: not a matcher snapshot image of this version");
+    if (r.get<int32_t>() != h->mode || r.get<uint64_t>() != h->fp)
+        return fail(h, SH_E_INVALID_ARG, "restore: the image was taken from a different app");
+    for (auto& st : h->stores)
+        if (st.rows) return fail(h, SH_E_INVALID_ARG, "restore: the handle has processed events already");
+    hipStreamSynchronize(h->stream);
+    h->seq_next = r.get<uint64_t>();
+    h->seq_staged0 = r.get<uint64_t>();
+    h->max_key = r.get<int32_t>();
+    h->clock = r.get<int64_t>();
+    h->tick = r.get<uint64_t>();
+    h->started = r.get<uint8_t>() != 0;
+    h->batch_id = r.get<uint32_t>();
+    r.vec(h->o_query);
+    r.vec(h->o_seq);
+    r.vec(h->o_ts);
+    r.vec(h->o_vals);
+    r.vec(h->o_nulls);
+    h->o_read = r.get<int64_t>();
+    h->st_ts.clear();
+    h->st_stream.clear();
+    h->st_row.clear();
+    h->st_key.clear();
+    if (r.get<int32_t>() != (int32_t)h->stores.size()) r.bad = true;
+    for (size_t s = 0; s < h->stores.size() && !r.bad; s++) {
+        auto& st = h->stores[s];
+        st.rows = r.get<int64_t>();
+        if (r.get<int32_t>() != (int32_t)st.cols.size()) r.bad = true;
+        for (size_t a = 0; a < st.cols.size() && !r.bad; a++) {
+            st.has_nul[a] = r.get<uint8_t>() != 0;
+            r.dev(st.cols[a]);
+            r.dev(st.nuls[a]);
+        }
+    }
+    if (h->mode == 0 && !r.bad) {
+        h->lay = r.get<shp_layout>();
+        h->nkeys_alloc = r.get<int32_t>();
+        r.dev(h->d_kstate);
+    } else if (!r.bad) {
+        *h->T = r.get<nf_table>();
+        r.raw(h->caps, sizeof(h->caps));
+        h->n_nkeys = r.get<int32_t>();
+        h->klist_cur = r.get<int32_t>();
+        r.dev(h->n_kstate);
+        r.dev(h->n_armed);
+        r.dev(h->n_klist[0]);
+        r.dev(h->n_klist[1]);
+        r.dev(h->n_arm_log);
+        r.dev(h->n_klist_n);
+        r.dev(h->n_arm_ctr);
+        const bool sm_on = r.get<uint8_t>() != 0;
+        if (sm_on != h->sm_on) r.bad = true;
+        if (sm_on && !r.bad) {
+            r.vec(h->sm.chars);
+            r.vec(h->sm.off);
+            r.vec(h->sm.len);
+            r.vec(h->sm.hash);
+            std::vector<int> used;
+            r.vec(used);
+            if (used != h->sm.used) r.bad = true;
+            for (int s : used) {
+                if (r.bad) break;
+                get_jmap(r, h->sm.maps[s]);
+                r.dev(h->n_rank[s]);
+            }
+        }
+        if (!r.bad && nf_upload_table(h)) r.bad = true;
+    }
+    if (r.bad || r.at != r.n) return fail(h, SH_E_INVALID_ARG, "restore: truncated or inconsistent image");
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return fail(h, SH_E_HIP, "restore upload");
     return SH_OK;
 }
 

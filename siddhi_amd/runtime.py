@@ -19,6 +19,7 @@ Thread.sleep are deterministic ("time").
 """
 from __future__ import annotations
 
+import json
 import struct
 from typing import Callable, Dict, List, Optional
 
@@ -31,7 +32,8 @@ from .compiler import (BOOL, DOUBLE, FLOAT, INT, LONG, OBJECT, STRING, CompiledA
                        SiddhiAppValidationException, SiddhiParserException, UnsupportedQuery)
 
 __all__ = ["SiddhiManager", "SiddhiAppRuntime", "InputHandler", "StreamCallback", "QueryCallback",
-           "Event", "SiddhiAppCreationException", "SiddhiAppRuntimeException"]
+           "Event", "SiddhiAppCreationException", "SiddhiAppRuntimeException", "InMemoryPersistenceStore",
+           "NoPersistenceStoreException"]
 
 
 class SiddhiAppCreationException(Exception):
@@ -209,6 +211,8 @@ class SiddhiAppRuntime:
         self._query_by_name = {q.query.name: i for i, q in enumerate(compiled.queries)
                                if q.query.name}
         self._engine = engine_factory(compiled)
+        self._manager_store = None  # () -> the SiddhiManager's PersistenceStore
+        self._revision = 0
         self._started = False
         self._seq = 0
         self._range_ev: Dict[str, RangeEvaluator] = {}
@@ -247,6 +251,73 @@ class SiddhiAppRuntime:
         if self._engine is not None:
             self._engine.close()
             self._engine = None
+
+    # -- persistence (core/SiddhiAppRuntimeImpl.java snapshot / restore / persist /
+    # restoreLastRevision; core/util/snapshot/SnapshotService.java)
+    _SNAP_MAGIC = b"SHAP1\0"
+
+    def snapshot(self) -> bytes:
+        """byte[] snapshot(): the matcher image (sh_snapshot) plus the host state the
+        device ids refer to (string and partition-key dictionaries, clock, sequence)."""
+        if self._engine is None or not hasattr(self._engine, "snapshot"):
+            raise SiddhiAppRuntimeException("snapshot: the engine keeps no restorable state")
+        image = self._engine.snapshot()
+        host = json.dumps({"strings": list(self.strings._strs), "keys": list(self.keys.text),
+                           "clock": int(self.clock), "seq": int(self._seq)}).encode()
+        return self._SNAP_MAGIC + struct.pack("<Q", len(host)) + host + image
+
+    def restore(self, snapshot: bytes):
+        """restore(byte[]): into a started runtime of the same app that has not
+        received events (the reference restores into a fresh runtime after start)"""
+        m = self._SNAP_MAGIC
+        if not snapshot.startswith(m):
+            raise SiddhiAppRuntimeException("restore: not a snapshot of this engine")
+        (n,) = struct.unpack_from("<Q", snapshot, len(m))
+        host = json.loads(snapshot[len(m) + 8: len(m) + 8 + n].decode())
+        image = snapshot[len(m) + 8 + n:]
+        strs = host["strings"]
+        if strs[: len(self.strings)] != self.strings._strs:
+            raise SiddhiAppRuntimeException("restore: the snapshot was taken from another app")
+        for v in strs[len(self.strings):]:
+            self.strings.id(v)
+        if self.keys.text and self.keys.text != host["keys"][: len(self.keys.text)]:
+            raise SiddhiAppRuntimeException("restore: the runtime has seen other partition keys")
+        for t in host["keys"][len(self.keys.text):]:
+            self.keys.ids[t] = len(self.keys.text)
+            self.keys.text.append(t)
+        self.keys.registered = len(self.keys.text)  # the image carries the engine's key strings
+        self._engine.restore(image)
+        self.clock = max(self.clock, host["clock"])
+        self._seq = max(self._seq, host["seq"])
+        self._deliver()
+
+    def persist(self):
+        """persist(): snapshot into the manager's persistence store; returns the revision"""
+        store = self._manager_store() if self._manager_store else None
+        if store is None:
+            raise NoPersistenceStoreException("no persistence store assigned")
+        self._revision += 1
+        rev = f"{self._revision}_{self.name or 'SiddhiApp'}"
+        store.save(self.name or "SiddhiApp", rev, self.snapshot())
+        return rev
+
+    def restoreRevision(self, revision: str):
+        store = self._manager_store() if self._manager_store else None
+        if store is None:
+            raise NoPersistenceStoreException("no persistence store assigned")
+        data = store.load(self.name or "SiddhiApp", revision)
+        if data is None:
+            raise SiddhiAppRuntimeException(f"no revision {revision}")
+        self.restore(data)
+
+    def restoreLastRevision(self):
+        store = self._manager_store() if self._manager_store else None
+        if store is None:
+            raise NoPersistenceStoreException("no persistence store assigned")
+        rev = store.getLastRevision(self.name or "SiddhiApp")
+        if rev is not None:
+            self.restoreRevision(rev)
+        return rev
 
     def sleep(self, ms: int):
         """Thread.sleep stand-in: advances the virtual clock (and fires due timers)."""
@@ -363,6 +434,33 @@ class SiddhiAppRuntime:
             i = j
 
 
+class NoPersistenceStoreException(Exception):
+    pass
+
+
+class InMemoryPersistenceStore:
+    """core/util/persistence/InMemoryPersistenceStore.java: revisions per app, in order"""
+
+    def __init__(self):
+        self._revs: Dict[str, List[tuple]] = {}
+
+    def save(self, app: str, revision: str, snapshot: bytes):
+        self._revs.setdefault(app, []).append((revision, bytes(snapshot)))
+
+    def load(self, app: str, revision: str):
+        for r, b in self._revs.get(app, []):
+            if r == revision:
+                return b
+        return None
+
+    def getLastRevision(self, app: str):
+        revs = self._revs.get(app)
+        return revs[-1][0] if revs else None
+
+    def clearAllRevisions(self, app: str):
+        self._revs.pop(app, None)
+
+
 class SiddhiManager:
     """core/SiddhiManager.java"""
 
@@ -372,6 +470,10 @@ class SiddhiManager:
             engine_factory = HipEngine
         self._engine_factory = engine_factory
         self._runtimes = []
+        self._store = None
+
+    def setPersistenceStore(self, store):
+        self._store = store
 
     def createSiddhiAppRuntime(self, app: str) -> SiddhiAppRuntime:
         try:
@@ -379,6 +481,7 @@ class SiddhiManager:
         except (SiddhiParserException, SiddhiAppValidationException, UnsupportedQuery) as e:
             raise SiddhiAppCreationException(str(e)) from e
         rt = SiddhiAppRuntime(compiled, self._engine_factory)
+        rt._manager_store = lambda: self._store
         self._runtimes.append(rt)
         return rt
 
