@@ -34,7 +34,7 @@
 
 #define BK_TPB 512
 #define BK_ITEMS (SHB_TILE / BK_TPB)
-#define BK_ROWMAP 2048  // rows per 1,024-event block written row-parallel
+#define BK_ROWMAP 2048  // rows per 512-event block written row-parallel
 
 static_assert(BK_ITEMS == 16, "tile / threads");
 
@@ -312,8 +312,8 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
     __shared__ uint32_t S[SHB_TILE];
     __shared__ int32_t o_kind[SHB_MAX_OUT], o_type[SHB_MAX_OUT];
     __shared__ const void* o_src[SHB_MAX_OUT];
-    __shared__ uint16_t evmap[BK_ROWMAP];
-    __shared__ uint32_t blk_mpos[BK_TPB];
+    __shared__ uint16_t evmap[2 * BK_ROWMAP];
+    __shared__ uint32_t blk_mpos[2 * BK_TPB];
     __shared__ uint32_t s_tot;
     const int T = bk_tile(P.nt);
     if (T < 0) return;
@@ -408,21 +408,27 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
         }
     }
     __syncthreads();
+    // two 512-event blocks at a time: their events enter their rows into the row
+    // -> event map, then thread t writes rows r0 + t, r0 + t + 512, ...
+    // (consecutive lanes, consecutive rows: coalesced)
 #pragma unroll
-    for (int j = 0; j < BK_ITEMS; j++) {
+    for (int j = 0; j < BK_ITEMS; j += 2) {
         const int lb = j * BK_TPB;
         if (lb >= tile_n) break;  // uniform
-        const int l = lb + threadIdx.x;
         const uint32_t r0 = S[lb];
-        const uint32_t r1 = lb + BK_TPB < tile_n ? S[lb + BK_TPB] : s_tot;
+        const uint32_t r1 = lb + 2 * BK_TPB < tile_n ? S[lb + 2 * BK_TPB] : s_tot;
         const uint32_t R = r1 - r0;
-        const uint32_t c = pk[j] == ~0u ? 0u : (pk[j] >> 8) & 0xFFu;
-        if (R <= BK_ROWMAP) {
-            if (c) {
-                const uint32_t at = S[l] - r0;
-                for (uint32_t k = 0; k < c; k++) evmap[at + k] = (uint16_t)threadIdx.x;
+        if (R <= 2 * BK_ROWMAP) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int l = lb + h * BK_TPB + threadIdx.x;
+                const uint32_t c = (l < tile_n && pk[j + h] != ~0u) ? (pk[j + h] >> 8) & 0xFFu : 0u;
+                if (c) {
+                    const uint32_t at = S[l] - r0;
+                    for (uint32_t k = 0; k < c; k++) evmap[at + k] = (uint16_t)(h * BK_TPB + threadIdx.x);
+                }
+                blk_mpos[h * BK_TPB + threadIdx.x] = mpos[j + h];
             }
-            blk_mpos[threadIdx.x] = mpos[j];
             __syncthreads();
             for (uint32_t t = threadIdx.x; t < R; t += BK_TPB) {
                 const int e = evmap[t];
@@ -464,21 +470,26 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
             __syncthreads();
             continue;
         }
-        // a dense block (more rows than the map holds): event-parallel writes
-        if (!c) continue;
-        const int64_t i = b0 + l;
-        const int64_t row0 = (int64_t)tb + S[l];
-        if (row0 + c > out_cap) continue;
-        if (out_seq)
-            for (uint32_t k = 0; k < c; k++) out_seq[row0 + k] = seq_base + (uint64_t)i;
-        if (!out_vals && !COLS) continue;
-        for (int o = 0; o < no; o++) {
-            const void* src = o_src[o];
-            const int ty = o_type[o];
-            for (uint32_t k = 0; k < c; k++) {
-                const int64_t v = bk_raw(src, o_kind[o] == 1 ? i : (int64_t)mpos[j] + k, ty);
-                if (COLS) bk_put(OC.cols[o], OC.colw[o], row0 + k, v);
-                else out_vals[(row0 + k) * no + o] = v;
+        // a dense pair of blocks (more rows than the map holds): event-parallel writes
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int l = lb + h * BK_TPB + threadIdx.x;
+            const uint32_t c = (l < tile_n && pk[j + h] != ~0u) ? (pk[j + h] >> 8) & 0xFFu : 0u;
+            if (!c) continue;
+            const int64_t i = b0 + l;
+            const int64_t row0 = (int64_t)tb + S[l];
+            if (row0 + c > out_cap) continue;
+            if (out_seq)
+                for (uint32_t k = 0; k < c; k++) out_seq[row0 + k] = seq_base + (uint64_t)i;
+            if (!out_vals && !COLS) continue;
+            for (int o = 0; o < no; o++) {
+                const void* src = o_src[o];
+                const int ty = o_type[o];
+                for (uint32_t k = 0; k < c; k++) {
+                    const int64_t v = bk_raw(src, o_kind[o] == 1 ? i : (int64_t)mpos[j + h] + k, ty);
+                    if (COLS) bk_put(OC.cols[o], OC.colw[o], row0 + k, v);
+                    else out_vals[(row0 + k) * no + o] = v;
+                }
             }
         }
     }
