@@ -2218,8 +2218,8 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     B.flag = h->bk_flag.as<int32_t>();
     static const bool prof = getenv("SH_BK_PROFILE") != nullptr;
     if (prof) {
-        if (h->bk_prof.ensure_fresh(64)) return fail(h, SH_E_OOM, "profile");
-        hipMemsetAsync(h->bk_prof.p, 0, 64, h->stream);
+        if (h->bk_prof.ensure_fresh(128)) return fail(h, SH_E_OOM, "profile");
+        hipMemsetAsync(h->bk_prof.p, 0, 128, h->stream);
         B.prof = h->bk_prof.as<unsigned long long>();
     }
     // packed timestamps: ts - tbase in 32 - kb bits, centred on the first event
@@ -2247,8 +2247,8 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     const int32_t flag = *h->bk_rd.as<int32_t>(0);
     const int64_t total = *h->bk_rd.as<uint32_t>(8);
     if (B.prof) {
-        unsigned long long pr[8];
-        hipMemcpy(pr, B.prof, 64, hipMemcpyDeviceToHost);
+        unsigned long long pr[16];
+        hipMemcpy(pr, B.prof, 128, hipMemcpyDeviceToHost);
         fprintf(stderr, "[shb_match clock ticks, sum over workgroups] load %llu rank %llu walk %llu scan+psum %llu emit %llu\n",
                 pr[0], pr[1], pr[2], pr[3], pr[4]);
     }
