@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SH_DESC_VERSION 1
+#define SH_DESC_VERSION 2
 
 /* Attribute.Type (api/definition/Attribute.java) */
 enum sh_type {
@@ -82,7 +82,9 @@ enum sh_op {
     SH_OP_IS_NULL = 16,        /* IsNullConditionExpressionExecutor      */
     SH_OP_IS_NULL_STREAM = 17, /* IsNullStreamConditionExpressionExecutor (e1 is null) */
     SH_OP_IF_THEN_ELSE = 18,   /* function/IfThenElseFunctionExecutor (cond=lhs, a=rhs, b=third) */
-    SH_OP_BOOL_VAR = 19        /* BoolConditionExpressionExecutor wrapping a BOOL expr */
+    SH_OP_BOOL_VAR = 19,       /* BoolConditionExpressionExecutor wrapping a BOOL expr */
+    SH_OP_OUTPUT = 20          /* having: output attribute `attr` of the selected event
+                                  (HAVING_STATE variables, ExpressionParser.java:1308-1318) */
 };
 
 /* select-clause aggregators (query/selector/attribute/aggregator/) */
@@ -151,6 +153,9 @@ typedef struct sh_query_desc {
     const sh_state_elem* elems;
     const sh_expr* exprs;
     const sh_output_attr* outputs;
+    int32_t having;              /* having condition root (QuerySelector havingConditionExecutor,
+                                    SelectorParser.java:248-260), -1 if none */
+    int32_t pad;
 } sh_query_desc;
 
 typedef struct sh_app_desc {

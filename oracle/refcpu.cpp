@@ -492,6 +492,7 @@ struct Selector : Proc {
     }
     void process(Chunk<StateEvent>& c) override;
     void populate(StateEvent* se);
+    bool having(StateEvent* se);
     void sendToCallBacks(Chunk<StateEvent>& c);
 };
 
@@ -1059,6 +1060,11 @@ Val QueryRT::eval(int e, StateEvent* se) {
         case SH_OP_BOOL_VAR: {
             Val l = eval(x.lhs, se);
             return mkBool(!l.null && l.b);
+        }
+        case SH_OP_OUTPUT: {
+            // HAVING_STATE variable: the selected event's output data (outputData)
+            if (x.attr < 0 || x.attr >= (int)se->out.size()) return mkNull(x.type);
+            return se->out[x.attr];
         }
         case SH_OP_EQ:
         case SH_OP_NE:
@@ -2065,9 +2071,16 @@ void Selector::populate(StateEvent* se) {
         se->out[i] = r;
     }
 }
+// havingConditionExecutor.execute (a ConditionExpressionExecutor: null is false)
+bool Selector::having(StateEvent* se) {
+    if (q->d.having < 0) return true;
+    const Val v = q->eval(q->d.having, se);
+    return !v.null && v.b;
+}
 void Selector::process(Chunk<StateEvent>& c) {
     if (containsAggregator) {
-        // processInBatchNoGroupBy, QuerySelector.java:271-313
+        // processInBatchNoGroupBy, QuerySelector.java:271-313: the last event that
+        // passes `having` is the chunk's output
         c.reset();
         SE lastEv;
         while (c.hasNext()) {
@@ -2075,7 +2088,7 @@ void Selector::process(Chunk<StateEvent>& c) {
             if (ev->type == CURRENT || ev->type == EXPIRED) {
                 populate(ev.get());
                 ev->sel_seq = q->app->curSeq;
-                if (ev->type == CURRENT) {
+                if (having(ev.get()) && ev->type == CURRENT) {
                     c.remove();
                     lastEv = ev;
                 }
@@ -2097,7 +2110,8 @@ void Selector::process(Chunk<StateEvent>& c) {
             case EXPIRED:
                 populate(ev.get());
                 ev->sel_seq = q->app->curSeq;
-                if (ev->type != CURRENT) c.remove();  // currentOn only (insert into)
+                // currentOn only (insert into); events failing `having` leave the chunk
+                if (ev->type != CURRENT || !having(ev.get())) c.remove();
                 break;
             case TIMER:
                 c.remove();

@@ -1,7 +1,7 @@
 """ctypes mirror of include/sh_query.h and include/siddhi_hip.h (the C-ABI boundary)."""
 import ctypes as C
 
-SH_DESC_VERSION = 1
+SH_DESC_VERSION = 2
 
 SH_OK = 0
 SH_E_INVALID_ARG = -1
@@ -42,7 +42,7 @@ class sh_query_desc(C.Structure):
                 ("n_exprs", C.c_int32), ("n_outputs", C.c_int32), ("n_slots", C.c_int32),
                 ("partition", C.c_int32), ("output_stream", C.c_int32), ("within_ms", C.c_int64),
                 ("elems", C.POINTER(sh_state_elem)), ("exprs", C.POINTER(sh_expr)),
-                ("outputs", C.POINTER(sh_output_attr))]
+                ("outputs", C.POINTER(sh_output_attr)), ("having", C.c_int32), ("pad", C.c_int32)]
 
 
 class sh_app_desc(C.Structure):

@@ -34,6 +34,7 @@ TYPE_STR = {v: k.upper() for k, v in TYPE_NAMES.items()}
 CURRENT = -1   # SiddhiConstants.CURRENT
 LAST = -2      # SiddhiConstants.LAST
 UNKNOWN_STATE = -1
+HAVING_STATE = -2  # SiddhiConstants.HAVING_STATE
 
 
 class SiddhiParserException(Exception):
@@ -186,6 +187,7 @@ class Query:
     select_star: bool
     output: str
     partition: int = -1
+    having: object = None        # Selector.having (QuerySelector havingConditionExecutor)
 
 
 @dataclass
@@ -419,7 +421,7 @@ class Parser:
         if self.kw("within"):
             self.next()
             within = self.time_value()
-        sel, star = [], False
+        sel, star, having = [], False, None
         if self.kw("select"):
             self.next()
             if self.op("*"):
@@ -440,7 +442,12 @@ class Parser:
                         self.next()
                         continue
                     break
-            for w in ("group", "having", "order", "limit", "offset"):
+            if self.kw("group"):
+                raise UnsupportedQuery("`group by` is out of scope (SURVEY.md 8f next)")
+            if self.kw("having"):
+                self.next()
+                having = self.expr()
+            for w in ("order", "limit", "offset"):
                 if self.kw(w):
                     raise UnsupportedQuery(f"`{w}` is out of scope (SURVEY.md 8f next)")
         else:
@@ -459,7 +466,7 @@ class Parser:
         if self.op("#"):
             raise UnsupportedQuery("inner-stream outputs (#Stream) are out of scope")
         out = self.ident()
-        return Query(name, st, root, within, sel, star, out)
+        return Query(name, st, root, within, sel, star, out, having=having)
 
     def detect_state_type(self):
         depth = 0
@@ -770,6 +777,13 @@ class Lowerer:
             raise UnsupportedQuery("select * on patterns")
         for oa in q.select:
             outs.append(self.out_attr(oa))
+        self.having = -1
+        if q.having is not None:
+            # HAVING_STATE (ExpressionParser.java:1308-1318): a bare name is first an
+            # output attribute of the selected event, else a state-event attribute
+            self.out_alias = {oa.name: (o, outs[o]["type"]) for o, oa in enumerate(q.select)}
+            self.having = self.expr(q.having, HAVING_STATE, 0)
+            self._want_bool(self.having)
         return root, outs
 
     def elem(self, s, multi):
@@ -900,6 +914,11 @@ class Lowerer:
             t = e.type
             return self._e(op=0, type=t, is_null=1 if e.is_null else 0, cval=self.const_bits(e))
         if isinstance(e, EVar):
+            if current == HAVING_STATE:
+                if e.stream is None and e.index is None and e.name in self.out_alias:
+                    o, t = self.out_alias[e.name]
+                    return self._e(op=20, type=t, attr=o)
+                current = UNKNOWN_STATE
             slot, chain, attr, typ = self.resolve_var(e, current, default_index)
             return self._e(op=1, type=typ, slot=slot, chain=chain, attr=attr)
         if isinstance(e, EStreamRef):
@@ -945,6 +964,15 @@ class Lowerer:
                 if self.etype(a) != self.etype(b):
                     raise SiddhiAppValidationException("ifThenElse branches must have one type")
                 return self._e(op=18, type=self.etype(a), lhs=c, rhs=a, third=b)
+            inst = {"instanceoffloat": FLOAT, "instanceofinteger": INT, "instanceoflong": LONG,
+                    "instanceofdouble": DOUBLE, "instanceofstring": STRING, "instanceofboolean": BOOL}
+            if n in inst and len(e.args) == 1:
+                # function/InstanceOf*FunctionExecutor: `value instanceof T` -- with static
+                # types, true iff the argument has type T and is not null
+                a = self.expr(e.args[0], current, default_index)
+                if self.etype(a) != inst[n]:
+                    return self._e(op=0, type=BOOL, cval=0)
+                return self._e(op=4, type=BOOL, lhs=self._e(op=16, type=BOOL, lhs=a))
             raise UnsupportedQuery(f"function {e.name}() is out of scope")
         raise UnsupportedQuery(f"expression {e!r}")
 
@@ -1033,6 +1061,7 @@ class CompiledQuery:
     out_names: List[str]
     out_types: List[int]
     output_stream: int
+    having: int = -1
 
 
 @dataclass
@@ -1081,6 +1110,7 @@ class CompiledApp:
             q.partition = cq.query.partition
             q.output_stream = cq.output_stream
             q.within_ms = cq.query.within_ms
+            q.having = cq.having
             q.elems = el
             q.exprs = ex
             q.outputs = ou
@@ -1136,7 +1166,7 @@ def compile_app(text: str, strings: Optional[StringDict] = None) -> CompiledApp:
             query=q, elems=low.elems, exprs=low.exprs, outs=outs, root=root,
             n_slots=len(low.slots), slot_streams=[sd.name for sd, _, _ in low.slots],
             out_names=[o.name for o in q.select], out_types=[o["type"] for o in outs],
-            output_stream=out_streams.index(q.output)))
+            output_stream=out_streams.index(q.output), having=low.having))
     # a stream may be keyed by at most one partition (one key array per batch)
     owner = {}
     for p, spec in enumerate(app.partitions):

@@ -132,6 +132,7 @@ struct nf_query {
     nf_proc proc[NF_MAX_PROC];
     nf_receiver recv[NF_MAX_STREAMS];
     int32_t out_pc[NF_MAX_OUT], out_len[NF_MAX_OUT], out_agg[NF_MAX_OUT], out_type[NF_MAX_OUT];
+    int32_t having_pc, having_len;  // QuerySelector havingConditionExecutor (-1: none)
     nf_layout lay;
     int64_t q_off;          // word offset of this query's block inside a key block
     // rise-and-fall sequence `every e1=S, e2=S[f2(e2, e1)]+, e3=S[f3(e3, e2[last])]`
@@ -825,6 +826,15 @@ struct NfLane {
                     break;
                 }
                 case OPC_CAST: st[sp - 1].t = in.b; break;
+                case OPC_OUTPUT: {
+                    // HAVING_STATE variable: the selected event's output data
+                    NfVal v;
+                    v.t = in.c;
+                    v.b = (int64_t)se_out(s)[in.b];
+                    v.null = (uint8_t)((se(s)[3] >> in.b) & 1u);
+                    st[sp++] = v;
+                    break;
+                }
             }
         }
         return st[sp - 1];
@@ -1439,8 +1449,16 @@ struct NfLane {
         se(s)[3] = mask;
     }
     NF_HD void set_sel_seq(uint32_t s) { se(s)[1] = cur_seq; }
+    // havingConditionExecutor.execute (ConditionExpressionExecutor: null is false)
+    NF_HD bool having_ok(uint32_t s) const {
+        if (Q->having_pc < 0) return true;
+        const NfVal v = eval(Q->having_pc, Q->having_len, s);
+        return !v.null && v.b;
+    }
     NF_HD void selector_process(uint32_t* c) {
         if (Q->contains_agg) {
+            // processInBatchNoGroupBy (QuerySelector.java:271-313): the last event
+            // that passes `having` is the chunk's output
             ch_reset(c);
             uint32_t last = 0;
             while (ch_has_next(c)) {
@@ -1449,7 +1467,7 @@ struct NfLane {
                 if (ty == NF_CURRENT || ty == NF_EXPIRED) {
                     populate(ev);
                     set_sel_seq(ev);
-                    if (ty == NF_CURRENT) {
+                    if (having_ok(ev) && ty == NF_CURRENT) {
                         ch_remove(c);
                         last = ev;
                     }
@@ -1469,7 +1487,8 @@ struct NfLane {
             if (ty == NF_CURRENT || ty == NF_EXPIRED) {
                 populate(ev);
                 set_sel_seq(ev);
-                if (ty != NF_CURRENT) ch_remove(c);  // insert into: current events only
+                // insert into: current events only; events failing `having` leave the chunk
+                if (ty != NF_CURRENT || !having_ok(ev)) ch_remove(c);
             } else if (ty == NF_TIMER) {
                 ch_remove(c);
             }

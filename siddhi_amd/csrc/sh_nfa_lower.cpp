@@ -379,6 +379,12 @@ struct QueryLowering {
             case SH_OP_IF_THEN_ELSE:
                 return gen(x.lhs, depth + 1) && gen(x.rhs, depth + 2) && gen(x.third, depth + 3) &&
                        emit(OPC_SELECT, 0, 0, 0, 0) && emit(OPC_CAST, 0, (uint8_t)x.type, 0, 0);
+            case SH_OP_OUTPUT:
+                if (x.attr < 0 || x.attr >= q->n_outputs) {
+                    err = "having: output attribute out of range";
+                    return false;
+                }
+                return emit(OPC_OUTPUT, 0, (uint8_t)x.attr, (uint8_t)x.type, 0);
         }
         err = "unsupported expression operator";
         return false;
@@ -584,7 +590,7 @@ struct QueryLowering {
             err = "device engine: at most 16 output attributes";
             return false;
         }
-        detect_seq3();
+        if (q->having < 0) detect_seq3();  // k_seq3 emits without a selector pass
         Q->n_out = q->n_outputs;
         for (int o = 0; o < q->n_outputs; o++) {
             const sh_output_attr& oa = q->outputs[o];
@@ -599,6 +605,13 @@ struct QueryLowering {
                 Q->out_pc[o] = -1;
                 Q->out_len[o] = 0;
             }
+        }
+        Q->having_pc = -1;
+        Q->having_len = 0;
+        if (q->having >= 0) {
+            Q->having_pc = T->n_code;
+            if (!gen(q->having, 0)) return false;
+            Q->having_len = T->n_code - Q->having_pc;
         }
         return true;
     }

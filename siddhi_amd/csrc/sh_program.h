@@ -33,7 +33,8 @@ enum shp_opcode {
     OPC_ISNULL = 8,
     OPC_ISNULL_STREAM = 9,  // a = slot, x = chain index
     OPC_SELECT = 10,    // if-then-else: pops else, then, cond
-    OPC_CAST = 11       // b = target type (retag only)
+    OPC_CAST = 11,      // b = target type (retag only)
+    OPC_OUTPUT = 12     // having: b = output attribute, c = its type
 };
 
 struct shp_instr {
