@@ -272,8 +272,10 @@ def main_sharded(args, torch, dist, world, rank, dev):
     compiled = compiler.compile_app(synth.C2_QUERY)
     runner = DeviceRunner(compiled, device=str(dev))
     stream = torch.cuda.current_stream(dev)
+    comm = shard.BounceComm(world) if os.environ.get("SH_BENCH_SHARE_GPU") else None
     step = shard.KeyShardedStep(world, rank, shard.HipShardOps(str(dev)),
-                                lambda t, k, c, nk: runner.run(t, k, c, nk, stream=stream), n_out=4)
+                                lambda t, k, c, nk: runner.run(t, k, c, nk, stream=stream), n_out=4, comm=comm)
+    rdev = "cpu" if comm is not None else dev  # device of the timing / count reductions
 
     def one():
         return step.run(d_ts, d_k, [d_k, d_p, d_v], lo, K, key_attr=0)
@@ -291,10 +293,10 @@ def main_sharded(args, torch, dist, world, rank, dev):
     dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=rdev)
     dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
-    m_t = torch.tensor([int(seq.numel())], dtype=torch.int64, device=dev)
+    m_t = torch.tensor([int(seq.numel())], dtype=torch.int64, device=rdev)
     dist.all_reduce(m_t)
     m = int(m_t.item())
     verified = None
@@ -332,9 +334,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SH_BENCH_SHARE_GPU"):
+        # rehearsal of the N-rank path on a one-GPU box: every rank on device 0
+        local = 0
+    share = bool(os.environ.get("SH_BENCH_SHARE_GPU"))
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # rehearsal on one GPU: gloo through host memory (RCCL refuses duplicate devices)
+        dist.init_process_group("gloo" if share else "nccl")
     dev = torch.device(f"cuda:{local}")
     if args.config == "c4":
         return main_c4(args, torch, dist, world, rank, dev)

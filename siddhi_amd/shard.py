@@ -177,6 +177,17 @@ class TorchComm:
         return recv
 
 
+class BounceComm(TorchComm):
+    """rehearsal of the exchanges over gloo through host memory (several ranks on one
+    GPU, where RCCL refuses duplicate devices); same split semantics as TorchComm"""
+
+    def counts(self, counts, device):
+        return super().counts(counts, "cpu")
+
+    def exchange(self, send, send_counts, recv_counts, per):
+        return super().exchange(send.cpu(), send_counts, recv_counts, per).to(send.device)
+
+
 class KeyShardedStep:
     """One sharded pass on this rank (see the module docstring).
 
