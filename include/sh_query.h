@@ -34,7 +34,8 @@
 extern "C" {
 #endif
 
-#define SH_DESC_VERSION 2
+#define SH_DESC_VERSION 3
+#define SH_MAX_ORDER 4
 
 /* Attribute.Type (api/definition/Attribute.java) */
 enum sh_type {
@@ -155,7 +156,13 @@ typedef struct sh_query_desc {
     const sh_output_attr* outputs;
     int32_t having;              /* having condition root (QuerySelector havingConditionExecutor,
                                     SelectorParser.java:248-260), -1 if none */
+    int32_t n_order;             /* `order by` attributes (OrderByEventComparator, SelectorParser.java:110-114), 0 if none */
+    int32_t order_expr[SH_MAX_ORDER]; /* variable expression per order-by attribute (HAVING_STATE resolution);
+                                    INT / LONG / FLOAT / DOUBLE / BOOL (string order needs the text) */
+    int32_t order_desc;          /* bit i: attribute i is DESC                  */
     int32_t pad;
+    int64_t limit;               /* QuerySelector.limit, -1 if none (SelectorParser.java:115-123) */
+    int64_t offset;              /* QuerySelector.offset, -1 if none (:124-132)  */
 } sh_query_desc;
 
 typedef struct sh_app_desc {

@@ -493,6 +493,10 @@ struct Selector : Proc {
     void process(Chunk<StateEvent>& c) override;
     void populate(StateEvent* se);
     bool having(StateEvent* se);
+    int orderCompare(StateEvent* a, StateEvent* b);
+    void orderChunk(Chunk<StateEvent>& c);
+    void offsetChunk(Chunk<StateEvent>& c);
+    void limitChunk(Chunk<StateEvent>& c);
     void sendToCallBacks(Chunk<StateEvent>& c);
 };
 
@@ -2077,6 +2081,107 @@ bool Selector::having(StateEvent* se) {
     const Val v = q->eval(q->d.having, se);
     return !v.null && v.b;
 }
+// Integer/Long/Float/Double/Boolean.compareTo (OrderByEventComparator.java:73-99);
+// Float.compare / Double.compare order by the canonical bits when not < or >
+static int javaCompare(const Val& x, const Val& y) {
+    switch (x.t) {
+        case SH_T_FLOAT: {
+            const float a = f32(x.b), b = f32(y.b);
+            if (a < b) return -1;
+            if (a > b) return 1;
+            const int32_t ia = std::isnan(a) ? 0x7fc00000 : (int32_t)(uint32_t)bf32(a);
+            const int32_t ib = std::isnan(b) ? 0x7fc00000 : (int32_t)(uint32_t)bf32(b);
+            return ia == ib ? 0 : (ia < ib ? -1 : 1);
+        }
+        case SH_T_DOUBLE: {
+            const double a = f64(x.b), b = f64(y.b);
+            if (a < b) return -1;
+            if (a > b) return 1;
+            const int64_t ia = std::isnan(a) ? 0x7ff8000000000000ll : bf64(a);
+            const int64_t ib = std::isnan(b) ? 0x7ff8000000000000ll : bf64(b);
+            return ia == ib ? 0 : (ia < ib ? -1 : 1);
+        }
+        case SH_T_BOOL: return (int)(x.b != 0) - (int)(y.b != 0);
+        case SH_T_INT: {
+            const int32_t a = (int32_t)x.b, b = (int32_t)y.b;
+            return a < b ? -1 : (a > b ? 1 : 0);
+        }
+        default: return x.b < y.b ? -1 : (x.b > y.b ? 1 : 0);
+    }
+}
+// OrderByEventComparator.compare, OrderByEventComparator.java:62-116
+int Selector::orderCompare(StateEvent* a, StateEvent* b) {
+    for (int i = 0; i < q->d.n_order; i++) {
+        const Val x = q->eval(q->d.order_expr[i], a);
+        const Val y = q->eval(q->d.order_expr[i], b);
+        if (!x.null && !y.null) {
+            int r = javaCompare(x, y);
+            if ((q->d.order_desc >> i) & 1) r = -r;
+            if (r != 0) return r;
+        } else if (!x.null) {
+            return -1;
+        } else if (!y.null) {
+            return 1;
+        }
+    }
+    return 0;
+}
+// QuerySelector.orderEventChunk, QuerySelector.java:452-483
+void Selector::orderChunk(Chunk<StateEvent>& c) {
+    Chunk<StateEvent> ordering;
+    std::vector<SE> list;
+    auto flush = [&]() {
+        std::stable_sort(list.begin(), list.end(),
+                         [&](const SE& a, const SE& b) { return orderCompare(a.get(), b.get()) < 0; });
+        for (auto& e : list) ordering.add(e);
+        list.clear();
+    };
+    c.reset();
+    if (!c.first) return;
+    EvType cur = c.first->type;
+    while (c.hasNext()) {
+        SE ev = c.next();
+        c.remove();
+        if (ev->type != cur) {
+            cur = ev->type;
+            flush();
+        }
+        list.push_back(ev);
+    }
+    flush();
+    c.clear();
+    c.add(ordering.first);
+}
+// QuerySelector.offsetEventChunk, QuerySelector.java:502-519 (insert into: currentOn only)
+void Selector::offsetChunk(Chunk<StateEvent>& c) {
+    c.reset();
+    int64_t n = 0;
+    while (c.hasNext()) {
+        SE ev = c.next();
+        if (ev->type == CURRENT || ev->type == EXPIRED) {
+            if (q->d.offset > n) {
+                if (ev->type == CURRENT) n++;
+                c.remove();
+            } else {
+                break;
+            }
+        }
+    }
+}
+// QuerySelector.limitEventChunk, QuerySelector.java:485-500
+void Selector::limitChunk(Chunk<StateEvent>& c) {
+    c.reset();
+    int64_t n = 0;
+    while (c.hasNext()) {
+        SE ev = c.next();
+        if (ev->type == CURRENT || ev->type == EXPIRED) {
+            if (q->d.limit > n && ev->type == CURRENT)
+                n++;
+            else
+                c.remove();
+        }
+    }
+}
 void Selector::process(Chunk<StateEvent>& c) {
     if (containsAggregator) {
         // processInBatchNoGroupBy, QuerySelector.java:271-313: the last event that
@@ -2120,6 +2225,9 @@ void Selector::process(Chunk<StateEvent>& c) {
                 break;
         }
     }
+    if (q->d.n_order > 0) orderChunk(c);
+    if (q->d.offset >= 0) offsetChunk(c);
+    if (q->d.limit >= 0) limitChunk(c);
     c.reset();
     if (c.hasNext()) sendToCallBacks(c);
 }
@@ -2516,6 +2624,23 @@ ref_app* ref_create(const sh_app_desc* d, char* err, int errlen) {
             std::string m = q->err;
             delete ra;
             return fail("query " + std::to_string(qi) + ": " + m);
+        }
+        std::string serr;
+        if (qd.n_order < 0 || qd.n_order > SH_MAX_ORDER) serr = "order by: 0..4 attributes";
+        for (int i = 0; i < qd.n_order && serr.empty(); i++) {
+            const int e = qd.order_expr[i];
+            if (e < 0 || e >= qd.n_exprs)
+                serr = "order by: expression out of range";
+            else if (qd.exprs[e].type == SH_T_STRING || qd.exprs[e].type == SH_T_OBJECT)
+                serr = "order by: string / object attributes are outside the restatement";
+        }
+        bool agg = false;
+        for (int o = 0; o < qd.n_outputs; o++) agg |= qd.outputs[o].agg != SH_AGG_NONE;
+        // processInBatchNoGroupBy would pass an empty chunk on (QuerySelector.java:304-311)
+        if (agg && (qd.offset > 0 || qd.limit == 0)) serr = "aggregating selector with offset > 0 or limit 0";
+        if (!serr.empty()) {
+            delete ra;
+            return fail("query " + std::to_string(qi) + ": " + serr);
         }
         if (qd.partition >= 0) a.partitions[qd.partition].queries.push_back(q);
         for (auto& kv : q->receivers) {

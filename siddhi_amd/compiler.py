@@ -188,6 +188,9 @@ class Query:
     output: str
     partition: int = -1
     having: object = None        # Selector.having (QuerySelector havingConditionExecutor)
+    order_by: list = field(default_factory=list)   # [(EVar, desc)] (Selector.orderByList)
+    limit: object = None         # Selector.limit / offset expressions (constants)
+    offset: object = None
 
 
 @dataclass
@@ -422,6 +425,7 @@ class Parser:
             self.next()
             within = self.time_value()
         sel, star, having = [], False, None
+        order, limit, offset = [], None, None
         if self.kw("select"):
             self.next()
             if self.op("*"):
@@ -447,9 +451,28 @@ class Parser:
             if self.kw("having"):
                 self.next()
                 having = self.expr()
-            for w in ("order", "limit", "offset"):
-                if self.kw(w):
-                    raise UnsupportedQuery(f"`{w}` is out of scope (SURVEY.md 8f next)")
+            if self.kw("order"):
+                # order_by: ORDER BY attribute_reference (ASC|DESC)? (, ...)* (SiddhiQL.g4:375-385)
+                self.next()
+                self.expect_kw("by")
+                while True:
+                    v = self.primary()
+                    if not isinstance(v, EVar):
+                        self.err("order by takes attribute references")
+                    desc = False
+                    if self.kw("asc") or self.kw("desc"):
+                        desc = self.next().text.lower() == "desc"
+                    order.append((v, desc))
+                    if self.op(","):
+                        self.next()
+                        continue
+                    break
+            if self.kw("limit"):
+                self.next()
+                limit = self.expr()
+            if self.kw("offset"):
+                self.next()
+                offset = self.expr()
         else:
             star = True
         if self.kw("output"):
@@ -466,7 +489,8 @@ class Parser:
         if self.op("#"):
             raise UnsupportedQuery("inner-stream outputs (#Stream) are out of scope")
         out = self.ident()
-        return Query(name, st, root, within, sel, star, out, having=having)
+        return Query(name, st, root, within, sel, star, out, having=having, order_by=order,
+                     limit=limit, offset=offset)
 
     def detect_state_type(self):
         depth = 0
@@ -778,13 +802,38 @@ class Lowerer:
         for oa in q.select:
             outs.append(self.out_attr(oa))
         self.having = -1
+        # HAVING_STATE (ExpressionParser.java:1308-1318): a bare name is first an
+        # output attribute of the selected event, else a state-event attribute
+        self.out_alias = {oa.name: (o, outs[o]["type"]) for o, oa in enumerate(q.select)}
         if q.having is not None:
-            # HAVING_STATE (ExpressionParser.java:1308-1318): a bare name is first an
-            # output attribute of the selected event, else a state-event attribute
-            self.out_alias = {oa.name: (o, outs[o]["type"]) for o, oa in enumerate(q.select)}
             self.having = self.expr(q.having, HAVING_STATE, 0)
             self._want_bool(self.having)
+        # OrderByEventComparator parses each attribute at HAVING_STATE (SelectorParser.java:110-114)
+        self.order = []
+        if len(q.order_by) > abi.SH_MAX_ORDER:
+            raise UnsupportedQuery(f"order by: at most {abi.SH_MAX_ORDER} attributes")
+        for v, desc in q.order_by:
+            i = self.expr(v, HAVING_STATE, 0)
+            if self.etype(i) in (STRING, OBJECT):
+                raise UnsupportedQuery("order by a string attribute needs the text (host-side order)")
+            self.order.append((i, desc))
+        self.limit = self._count_const(q.limit, "limit")
+        self.offset = self._count_const(q.offset, "offset")
+        if any(o["agg"] != 0 for o in outs) and (self.offset > 0 or self.limit == 0):
+            raise UnsupportedQuery("an aggregating selector with offset > 0 or limit 0 never emits")
         return root, outs
+
+    @staticmethod
+    def _count_const(e, what):
+        """QuerySelector.setLimit / setOffset (:436-450): a constant, read as Number.longValue()."""
+        if e is None:
+            return -1
+        if not isinstance(e, EConst) or e.type not in (INT, LONG, FLOAT, DOUBLE) or e.value is None:
+            raise SiddhiAppValidationException(f"'{what}' must be a numeric constant")
+        v = int(e.value)  # longValue(): truncation toward zero
+        if v < 0:
+            raise SiddhiAppValidationException(f"'{what}' cannot have negative value, but found '{v}'")
+        return v
 
     def elem(self, s, multi):
         if isinstance(s, SStream):
@@ -1062,6 +1111,9 @@ class CompiledQuery:
     out_types: List[int]
     output_stream: int
     having: int = -1
+    order: list = field(default_factory=list)   # [(expr index, desc)]
+    limit: int = -1
+    offset: int = -1
 
 
 @dataclass
@@ -1111,6 +1163,13 @@ class CompiledApp:
             q.output_stream = cq.output_stream
             q.within_ms = cq.query.within_ms
             q.having = cq.having
+            q.n_order = len(cq.order)
+            q.order_desc = 0
+            for i, (ei, desc) in enumerate(cq.order):
+                q.order_expr[i] = ei
+                q.order_desc |= (1 << i) if desc else 0
+            q.limit = cq.limit
+            q.offset = cq.offset
             q.elems = el
             q.exprs = ex
             q.outputs = ou
@@ -1166,7 +1225,8 @@ def compile_app(text: str, strings: Optional[StringDict] = None) -> CompiledApp:
             query=q, elems=low.elems, exprs=low.exprs, outs=outs, root=root,
             n_slots=len(low.slots), slot_streams=[sd.name for sd, _, _ in low.slots],
             out_names=[o.name for o in q.select], out_types=[o["type"] for o in outs],
-            output_stream=out_streams.index(q.output), having=low.having))
+            output_stream=out_streams.index(q.output), having=low.having,
+            order=low.order, limit=low.limit, offset=low.offset))
     # a stream may be keyed by at most one partition (one key array per batch)
     owner = {}
     for p, spec in enumerate(app.partitions):

@@ -569,15 +569,19 @@ static int lower_chain(sh_handle* h, const sh_app_desc* app, int qi, shp_program
     return SH_OK;
 }
 
-static bool has_having(const sh_app_desc* app) {
-    for (int32_t q = 0; q < app->n_queries; q++)
-        if (app->queries[q].having >= 0) return true;
+// having / order by / limit / offset need the selector pass of the general engine
+static bool has_selector_extras(const sh_app_desc* app) {
+    for (int32_t q = 0; q < app->n_queries; q++) {
+        const sh_query_desc& d = app->queries[q];
+        if (d.having >= 0 || d.n_order > 0 || d.limit >= 0 || d.offset >= 0) return true;
+    }
     return false;
 }
 
 static int compile_chain(sh_handle* h, const sh_app_desc* app) {
     if (app->n_queries != 1) return fail(h, SH_E_UNSUPPORTED, "chain engine: one query per app");
-    if (has_having(app)) return fail(h, SH_E_UNSUPPORTED, "chain engine: `having` runs on the general engine");
+    if (has_selector_extras(app))
+        return fail(h, SH_E_UNSUPPORTED, "chain engine: having / order by / limit run on the general engine");
     shp_program P;
     int rc = lower_chain(h, app, 0, P);
     if (rc) return rc;
@@ -614,7 +618,8 @@ static int64_t ix_const_key(int type, int64_t c) {
 static int compile_rules(sh_handle* h, const sh_app_desc* app) {
     if (app->n_queries < 2 || app->n_streams != 1)
         return fail(h, SH_E_UNSUPPORTED, "rule engine: two or more queries over one stream");
-    if (has_having(app)) return fail(h, SH_E_UNSUPPORTED, "rule engine: `having` runs on the general engine");
+    if (has_selector_extras(app))
+        return fail(h, SH_E_UNSUPPORTED, "rule engine: having / order by / limit run on the general engine");
     const int part = app->queries[0].partition;
     std::vector<shr_rule> rules(app->n_queries);
     std::unique_ptr<sh_handle> tmp(new sh_handle());

@@ -133,6 +133,9 @@ struct nf_query {
     nf_receiver recv[NF_MAX_STREAMS];
     int32_t out_pc[NF_MAX_OUT], out_len[NF_MAX_OUT], out_agg[NF_MAX_OUT], out_type[NF_MAX_OUT];
     int32_t having_pc, having_len;  // QuerySelector havingConditionExecutor (-1: none)
+    int32_t n_order, order_desc;    // OrderByEventComparator: attributes, DESC bit per attribute
+    int32_t order_pc[SH_MAX_ORDER], order_len[SH_MAX_ORDER];
+    int64_t limit, offset;          // QuerySelector limit / offset (-1: none)
     nf_layout lay;
     int64_t q_off;          // word offset of this query's block inside a key block
     // rise-and-fall sequence `every e1=S, e2=S[f2(e2, e1)]+, e3=S[f3(e3, e2[last])]`
@@ -284,6 +287,33 @@ NF_INL double nf_to_f64(const NfVal& v) {
         case SH_T_LONG: return (double)v.b;
         case SH_T_FLOAT: return (double)nf_f32(v.b);
         default: return nf_f64(v.b);
+    }
+}
+// Integer/Long/Float/Double/Boolean.compareTo for OrderByEventComparator (operands share
+// the executor's return type): Float.compare orders -0.0 before 0.0 and NaN last
+NF_INL int nf_java_compare(const NfVal& x, const NfVal& y) {
+    switch (x.t) {
+        case SH_T_FLOAT: {
+            const float a = nf_f32(x.b), c = nf_f32(y.b);
+            if (a < c) return -1;
+            if (a > c) return 1;
+            const int32_t ia = a != a ? 0x7fc00000 : (int32_t)nf_bf32(a);
+            const int32_t ic = c != c ? 0x7fc00000 : (int32_t)nf_bf32(c);
+            return ia == ic ? 0 : (ia < ic ? -1 : 1);
+        }
+        case SH_T_DOUBLE: {
+            const double a = nf_f64(x.b), c = nf_f64(y.b);
+            if (a < c) return -1;
+            if (a > c) return 1;
+            const int64_t ia = a != a ? 0x7ff8000000000000ll : nf_bf64(a);
+            const int64_t ic = c != c ? 0x7ff8000000000000ll : nf_bf64(c);
+            return ia == ic ? 0 : (ia < ic ? -1 : 1);
+        }
+        case SH_T_BOOL: return (int)(x.b != 0) - (int)(y.b != 0);
+        default: {
+            const int64_t a = nf_to_i64(x), c = nf_to_i64(y);
+            return a < c ? -1 : (a > c ? 1 : 0);
+        }
     }
 }
 template <typename T>
@@ -1455,6 +1485,88 @@ struct NfLane {
         const NfVal v = eval(Q->having_pc, Q->having_len, s);
         return !v.null && v.b;
     }
+    // OrderByEventComparator.compare (OrderByEventComparator.java:62-116): nulls after
+    // values whatever the direction
+    NF_HD int order_compare(uint32_t a, uint32_t b) const {
+        for (int i = 0; i < Q->n_order; i++) {
+            const NfVal x = eval(Q->order_pc[i], Q->order_len[i], a);
+            const NfVal y = eval(Q->order_pc[i], Q->order_len[i], b);
+            if (!x.null && !y.null) {
+                int r = nf_java_compare(x, y);
+                if ((Q->order_desc >> i) & 1) r = -r;
+                if (r) return r;
+            } else if (!x.null) {
+                return -1;
+            } else if (!y.null) {
+                return 1;
+            }
+        }
+        return 0;
+    }
+    // QuerySelector.orderEventChunk (:452-483): each run of one event type is sorted
+    // with List.sort (stable); here a stable insertion sort of the linked chunk
+    NF_HD void order_chunk(uint32_t* c) {
+        uint32_t head = 0, tail = 0, run_prev = 0;  // run_prev: node before the current run
+        int run_type = -1;
+        uint32_t ev = c[0];
+        while (ev) {
+            const uint32_t nx = se_next(ev);
+            se_set_next(ev, 0);
+            const int ty = se_type(ev);
+            if (ty != run_type) {
+                run_type = ty;
+                run_prev = tail;
+            }
+            // first node of the run that orders strictly after ev
+            uint32_t prev = run_prev, cur = run_prev ? se_next(run_prev) : head;
+            while (cur && order_compare(cur, ev) <= 0) {
+                prev = cur;
+                cur = se_next(cur);
+            }
+            se_set_next(ev, cur);
+            if (prev)
+                se_set_next(prev, ev);
+            else
+                head = ev;
+            if (!cur) tail = ev;
+            ev = nx;
+        }
+        c[0] = head;
+        c[1] = tail;
+        c[2] = c[3] = 0;
+    }
+    // QuerySelector.offsetEventChunk (:502-519), insert into: currentOn only
+    NF_HD void offset_chunk(uint32_t* c) {
+        ch_reset(c);
+        int64_t n = 0;
+        while (ch_has_next(c)) {
+            const uint32_t ev = ch_next(c);
+            const int ty = se_type(ev);
+            if (ty == NF_CURRENT || ty == NF_EXPIRED) {
+                if (Q->offset > n) {
+                    if (ty == NF_CURRENT) n++;
+                    ch_remove(c);
+                } else {
+                    break;
+                }
+            }
+        }
+    }
+    // QuerySelector.limitEventChunk (:485-500), insert into: currentOn only
+    NF_HD void limit_chunk(uint32_t* c) {
+        ch_reset(c);
+        int64_t n = 0;
+        while (ch_has_next(c)) {
+            const uint32_t ev = ch_next(c);
+            const int ty = se_type(ev);
+            if (ty == NF_CURRENT || ty == NF_EXPIRED) {
+                if (Q->limit > n && ty == NF_CURRENT)
+                    n++;
+                else
+                    ch_remove(c);
+            }
+        }
+    }
     NF_HD void selector_process(uint32_t* c) {
         if (Q->contains_agg) {
             // processInBatchNoGroupBy (QuerySelector.java:271-313): the last event
@@ -1493,6 +1605,9 @@ struct NfLane {
                 ch_remove(c);
             }
         }
+        if (Q->n_order > 0) order_chunk(c);
+        if (Q->offset >= 0) offset_chunk(c);
+        if (Q->limit >= 0) limit_chunk(c);
         ch_reset(c);
         if (ch_has_next(c)) send_to_callbacks(c);
     }

@@ -590,7 +590,8 @@ struct QueryLowering {
             err = "device engine: at most 16 output attributes";
             return false;
         }
-        if (q->having < 0) detect_seq3();  // k_seq3 emits without a selector pass
+        // k_seq3 emits without a selector pass
+        if (q->having < 0 && q->n_order == 0 && q->limit < 0 && q->offset < 0) detect_seq3();
         Q->n_out = q->n_outputs;
         for (int o = 0; o < q->n_outputs; o++) {
             const sh_output_attr& oa = q->outputs[o];
@@ -612,6 +613,34 @@ struct QueryLowering {
             Q->having_pc = T->n_code;
             if (!gen(q->having, 0)) return false;
             Q->having_len = T->n_code - Q->having_pc;
+        }
+        if (q->n_order < 0 || q->n_order > SH_MAX_ORDER) {
+            err = "order by: 0..4 attributes";
+            return false;
+        }
+        Q->n_order = q->n_order;
+        Q->order_desc = q->order_desc;
+        for (int i = 0; i < q->n_order; i++) {
+            const int e = q->order_expr[i];
+            if (e < 0 || e >= q->n_exprs) {
+                err = "order by: expression out of range";
+                return false;
+            }
+            const int t = q->exprs[e].type;
+            if (t == SH_T_STRING || t == SH_T_OBJECT) {
+                err = "order by: string / object attributes need the host's values";
+                return false;
+            }
+            Q->order_pc[i] = T->n_code;
+            if (!gen(q->order_expr[i], 0)) return false;
+            Q->order_len[i] = T->n_code - Q->order_pc[i];
+        }
+        Q->limit = q->limit;
+        Q->offset = q->offset;
+        if (Q->contains_agg && (q->offset > 0 || q->limit == 0)) {
+            // processInBatchNoGroupBy would hand an empty chunk to the rate limiter
+            err = "aggregating selector with offset > 0 or limit 0 never emits";
+            return false;
         }
         return true;
     }
