@@ -359,7 +359,8 @@ struct sh_handle {
     uint64_t seq_staged0 = 0;
     // workspaces
     DevBuf w_ts, w_stream, w_row, w_key, w_keys_a, w_keys_b, w_idx_a, w_idx_b, w_hist, w_scan, w_seg;
-    DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls, w_oq;
+    DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls, w_oq, w_inv;
+    bool dev_want_query = false;  // sh_run_device asked for d_out_query
     DevBuf v_sts, v_mpos, v_flag, v_cnts, v_mid_ts, v_dir;
     DevBuf v_scol[32], v_mid[32];
     int64_t tmp_cap = 0;
@@ -859,7 +860,7 @@ void sh_destroy(sh_handle* h) {
         DevBuf* bufs[] = {&h->d_prog, &h->d_cols_desc, &h->d_kstate, &h->d_err, &h->w_ts, &h->w_stream, &h->w_row,
                           &h->w_key, &h->w_keys_a, &h->w_keys_b, &h->w_idx_a, &h->w_idx_b, &h->w_hist, &h->w_scan,
                           &h->w_seg, &h->w_cnt, &h->w_off, &h->w_tmp, &h->w_ctr, &h->w_oseq, &h->w_ots,
-                          &h->w_ovals, &h->w_onulls};
+                          &h->w_ovals, &h->w_onulls, &h->w_inv};
         for (DevBuf* b : bufs) b->release();
         DevBuf* nbufs[] = {&h->d_T, &h->d_T_old, &h->d_ncols, &h->n_kstate, &h->n_kstate2, &h->n_save, &h->n_recs,
                            &h->n_ctr, &h->n_err, &h->n_cand, &h->n_sel, &h->n_bid, &h->w_oq,
@@ -1366,20 +1367,21 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
     if (total == 0) return SH_OK;
     const int stride = NF_REC_HDR + std::max(1, h->n_out);
     const int no = std::max(1, h->n_out);
-    if (d_seq) {  // device-resident output (sh_run_device)
+    if (h->w_inv.ensure_fresh(total * 4)) return fail(h, SH_E_OOM, "placement index");
+    if (d_seq) {  // device-resident output (sh_run_device): seq, values and, when asked, the query
         if (total > cap) return SH_E_MORE;
-        if (h->w_onulls.ensure_fresh(total * no) || h->w_ots.ensure_fresh(total * 8) ||
-            h->w_oq.ensure_fresh(total * 4))
-            return fail(h, SH_E_OOM, "output buffers");
-        nfd_place(h->n_recs.as<uint64_t>(), (int64_t)nrec, stride, h->w_off.as<uint32_t>(), no, h->w_oq.as<int32_t>(),
-                  d_seq, h->w_ots.as<int64_t>(), d_vals, h->w_onulls.as<uint8_t>(), st);
+        if (h->dev_want_query && h->w_oq.ensure_fresh(total * 4)) return fail(h, SH_E_OOM, "output buffers");
+        nfd_place(h->n_recs.as<uint64_t>(), (int64_t)nrec, stride, h->w_off.as<uint32_t>(), no,
+                  h->dev_want_query ? h->w_oq.as<int32_t>() : nullptr, d_seq, nullptr, d_vals, nullptr,
+                  h->w_inv.as<uint32_t>(), total, st);
         return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "placement");
     }
     if (h->w_oseq.ensure_fresh(total * 8) || h->w_ots.ensure_fresh(total * 8) || h->w_ovals.ensure_fresh(total * no * 8) ||
         h->w_onulls.ensure_fresh(total * no) || h->w_oq.ensure_fresh(total * 4))
         return fail(h, SH_E_OOM, "output buffers");
     nfd_place(h->n_recs.as<uint64_t>(), (int64_t)nrec, stride, h->w_off.as<uint32_t>(), no, h->w_oq.as<int32_t>(),
-              h->w_oseq.as<uint64_t>(), h->w_ots.as<int64_t>(), h->w_ovals.as<int64_t>(), h->w_onulls.as<uint8_t>(), st);
+              h->w_oseq.as<uint64_t>(), h->w_ots.as<int64_t>(), h->w_ovals.as<int64_t>(), h->w_onulls.as<uint8_t>(),
+              h->w_inv.as<uint32_t>(), total, st);
     const size_t base = h->o_seq.size();
     h->o_query.resize(base + total);
     h->o_seq.resize(base + total);
@@ -2326,6 +2328,7 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
         B.n = run->n;
         int64_t rows = 0;
         h->times = sh_kernel_times{};
+        h->dev_want_query = run->d_out_query != nullptr;
         rc = nf_process(h, B, nkeys, cols, run->d_out_seq, run->d_out_values, run->out_capacity, &rows, true,
                         run->batch_events, getenv("SH_NFA_GATHER") ? nullptr : run);
         run->out_count = rows;

@@ -171,44 +171,36 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
                                                        int shift, const uint32_t* __restrict__ offs, int64_t ntiles,
                                                        uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out,
                                                        shd_payload PL, int sub_shift) {
-    __shared__ uint32_t running[256];
+    // every wave owns a contiguous quarter of the tile (items j*64 + lane), so ranking in
+    // (j, lane) order inside a wave and then across waves is arrival order: a running
+    // count per (wave, digit) bumped by each peer group's leader (returning LDS atomic)
+    // replaces a block barrier per item
+    constexpr int WAVE_ITEMS = RADIX_TILE / (TPB / 64);
+    __shared__ uint32_t wcnt[TPB / 64][256];
     __shared__ uint32_t tstart[256];
     __shared__ uint32_t gbase[256];
-    __shared__ uint32_t wcnt[TPB / 64][256];
     __shared__ uint8_t dig[RADIX_TILE];
     __shared__ uint64_t stage[RADIX_TILE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t base = (int64_t)blockIdx.x * RADIX_TILE;
+    const int64_t wbase = base + (int64_t)w * WAVE_ITEMS + lane;  // element j: wbase + j * 64
     const int64_t tile_n = (n - base) < RADIX_TILE ? (n - base) : RADIX_TILE;
-    // tile histogram -> tile-local digit starts
-    running[threadIdx.x] = 0;
+#pragma unroll
+    for (int q = 0; q < TPB / 64; q++) wcnt[q][threadIdx.x] = 0;
     gbase[threadIdx.x] = offs[hist_idx(threadIdx.x, blockIdx.x, ntiles, sub_shift)];
-    __syncthreads();
     uint32_t key[RADIX_ITEMS];
 #pragma unroll
     for (int j = 0; j < RADIX_ITEMS; j++) {
-        const int64_t i = base + j * TPB + threadIdx.x;
+        const int64_t i = wbase + j * 64;
         key[j] = (i < n) ? load_key(keys_in, raw, sentinel, i) : 0u;
-        if (i < n) atomicAdd(&running[(key[j] >> shift) & 0xFF], 1u);
     }
     __syncthreads();
-    {
-        uint32_t tot;
-        const uint32_t c = running[threadIdx.x];
-        const uint32_t ex = block_excl_scan(c, &tot);
-        tstart[threadIdx.x] = ex;
-        running[threadIdx.x] = 0;
-    }
-    __syncthreads();
-    // stable rank of every element inside its digit (arrival order)
+    // wave-local stable rank inside the digit
     uint32_t lp[RADIX_ITEMS];
-    for (int j = 0; j < RADIX_ITEMS; j++) {
 #pragma unroll
-        for (int q = 0; q < TPB / 64; q++) wcnt[q][threadIdx.x] = 0;
-        __syncthreads();
-        const int64_t i = base + j * TPB + threadIdx.x;
-        const bool valid = i < n;
+    for (int j = 0; j < RADIX_ITEMS; j++) {
+        const bool valid = wbase + j * 64 < n;
         const uint32_t d = (key[j] >> shift) & 0xFF;
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -217,27 +209,41 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
             const uint64_t m = __ballot(valid && bit);
             peers &= bit ? m : ~m;
         }
+        uint32_t old = 0;
         const uint32_t rank = __popcll(peers & lt_mask);
-        if (valid && rank == 0) wcnt[w][d] = __popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t pre = 0;
-            for (int q = 0; q < w; q++) pre += wcnt[q][d];
-            lp[j] = tstart[d] + running[d] + pre + rank;
+        if (valid && rank == 0) old = atomicAdd(&wcnt[w][d], (uint32_t)__popcll(peers));
+        const int leader = valid ? __ffsll((unsigned long long)peers) - 1 : lane;
+        old = __shfl(old, leader);
+        lp[j] = old + rank;
+    }
+    __syncthreads();
+    {
+        // per digit: exclusive prefix over the waves, then the tile-local digit starts
+        uint32_t c[TPB / 64], tot = 0;
+#pragma unroll
+        for (int q = 0; q < TPB / 64; q++) {
+            c[q] = wcnt[q][threadIdx.x];
+            wcnt[q][threadIdx.x] = tot;
+            tot += c[q];
+        }
+        uint32_t all;
+        tstart[threadIdx.x] = block_excl_scan(tot, &all);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RADIX_ITEMS; j++) {
+        if (wbase + j * 64 < n) {
+            const uint32_t d = (key[j] >> shift) & 0xFF;
+            lp[j] += tstart[d] + wcnt[w][d];
             dig[lp[j]] = (uint8_t)d;
         }
-        __syncthreads();
-        uint32_t add = 0;
-#pragma unroll
-        for (int q = 0; q < TPB / 64; q++) add += wcnt[q][threadIdx.x];
-        running[threadIdx.x] += add;
-        __syncthreads();
     }
+    __syncthreads();
     // write-out through LDS: contiguous runs per digit
 #define SH_STAGE_OUT(T, SRCEXPR, DST)                                                           \
     {                                                                                           \
         for (int j = 0; j < RADIX_ITEMS; j++) {                                                 \
-            const int64_t i = base + j * TPB + threadIdx.x;                                     \
+            const int64_t i = wbase + j * 64;                                                   \
             if (i < n) stage[lp[j]] = (uint64_t)(SRCEXPR);                                      \
         }                                                                                       \
         __syncthreads();                                                                        \

@@ -6,13 +6,15 @@
 //                and writes emission records through a chunked sink
 //   k_nfa_due    scheduler scan: keys whose FIFO head is due (Scheduler.onTimeChange)
 //   k_nfa_timer  one lane per selected key: sendTimerEvents
-//   k_nfa_place  ordered placement of emission records (exclusive scan of counts)
+//   k_nfa_inv / k_nfa_gather  ordered placement of emission records (exclusive scan of
+//                counts; row -> record index, then a row-ordered gather)
 //   k_nfa_save / k_nfa_load   copy the touched keys' blocks (replay after growth)
 //   k_nfa_relayout            re-lays every key block into grown capacities
 //
 // Latency-bound by design: the parallelism is the number of keys present in a
 // flush (C3: 1M keys, C4: 10M keys); per-key work is pointer chasing in the key's
 // own arena, which stays L2-resident while its lane runs.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -156,7 +158,7 @@ __device__ __forceinline__ NfVal s3_val(const nf_cols* C, int a, int t, uint32_t
     return v;
 }
 
-#define S3_U 8
+template <int S3_U>
 __global__ void __launch_bounds__(NF_TPB) k_seq3(const nf_table* __restrict__ T, const nf_cols* __restrict__ C,
                                                  DevEvents E, int64_t n, const uint32_t* __restrict__ seg_list,
                                                  const uint32_t* __restrict__ nseg,
@@ -184,6 +186,7 @@ __global__ void __launch_bounds__(NF_TPB) k_seq3(const nf_table* __restrict__ T,
     const nf_query& Q = T->q[0];
     const bool same2 = Q.s3_e1a == Q.s3_a2 && Q.s3_e1t == Q.s3_t2;  // e1's operand is x's f2 operand
     const bool same3 = Q.s3_la == Q.s3_a3 && Q.s3_lt == Q.s3_t3;
+    const bool same23 = Q.s3_a2 == Q.s3_a3 && Q.s3_t2 == Q.s3_t3;  // f2 and f3 read one attribute of x
     DevSink sink;
     sink.buf = EM.recs;
     sink.ctr = EM.ctr;
@@ -207,7 +210,7 @@ __global__ void __launch_bounds__(NF_TPB) k_seq3(const nf_table* __restrict__ T,
             const int64_t k = k0 + u < end ? k0 + u : end - 1;
             const uint32_t row = ev.row(k);
             x2v[u] = s3_val(C, Q.s3_a2, Q.s3_t2, row);
-            x3v[u] = s3_val(C, Q.s3_a3, Q.s3_t3, row);
+            x3v[u] = same23 ? x2v[u] : s3_val(C, Q.s3_a3, Q.s3_t3, row);
         }
 #pragma unroll
         for (int u = 0; u < S3_U; u++) {
@@ -421,25 +424,37 @@ __global__ void __launch_bounds__(NF_TPB) k_nfa_timer(const nf_table* __restrict
     if (L.err) atomicOr(EM.err, L.err);
 }
 
-__global__ void __launch_bounds__(256) k_nfa_place(const uint64_t* __restrict__ recs, int64_t nrec, int stride,
-                                                   const uint32_t* __restrict__ offsets, int n_out,
-                                                   int32_t* __restrict__ out_query, uint64_t* __restrict__ out_seq,
-                                                   int64_t* __restrict__ out_ts, int64_t* __restrict__ out_vals,
-                                                   uint8_t* __restrict__ out_nulls) {
+// ordered placement in two passes: the records (grouped by key) scatter only their
+// index to the row they own (inv, 4 B per row: the random writes stay small and sit in
+// the memory-side cache), then one thread per output row gathers its record and writes
+// every output array in row order (coalesced). Unused outputs are NULL.
+__global__ void __launch_bounds__(256) k_nfa_inv(const uint64_t* __restrict__ recs, int64_t nrec, int stride,
+                                                 const uint32_t* __restrict__ offsets, uint32_t* __restrict__ inv) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nrec) return;
-    const uint64_t* r = recs + i * stride;
-    const uint64_t tag = r[0];
+    const uint64_t tag = recs[i * stride];
     if (tag == ~0ull) return;
-    const int64_t dst = (int64_t)offsets[(uint32_t)tag] + (int64_t)(tag >> 32);
-    const int q = (int)(r[2] >> 32);
-    out_query[dst] = q;
-    out_seq[dst] = r[3];
-    out_ts[dst] = (int64_t)r[1];
+    inv[(int64_t)offsets[(uint32_t)tag] + (int64_t)(tag >> 32)] = (uint32_t)i;
+}
+
+__global__ void __launch_bounds__(256) k_nfa_gather(const uint64_t* __restrict__ recs, const uint32_t* __restrict__ inv,
+                                                    int64_t total, int64_t nrec, int stride, int n_out,
+                                                    int32_t* __restrict__ out_query, uint64_t* __restrict__ out_seq,
+                                                    int64_t* __restrict__ out_ts, int64_t* __restrict__ out_vals,
+                                                    uint8_t* __restrict__ out_nulls) {
+    const int64_t dst = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (dst >= total) return;
+    const uint32_t ix = inv[dst];
+    if ((int64_t)ix >= nrec) return;  // no record (an emission overflow, reported through err)
+    const uint64_t* r = recs + (int64_t)ix * stride;
+    const uint64_t h2 = r[2];
+    if (out_query) out_query[dst] = (int)(h2 >> 32);
+    if (out_seq) out_seq[dst] = r[3];
+    if (out_ts) out_ts[dst] = (int64_t)r[1];
     for (int c = 0; c < n_out; c++) {
         const bool has = c < stride - NF_REC_HDR;
-        out_vals[dst * n_out + c] = has ? (int64_t)r[NF_REC_HDR + c] : 0;
-        out_nulls[dst * n_out + c] = has ? (uint8_t)((r[2] >> c) & 1) : 1;
+        if (out_vals) out_vals[dst * n_out + c] = has ? (int64_t)r[NF_REC_HDR + c] : 0;
+        if (out_nulls) out_nulls[dst * n_out + c] = has ? (uint8_t)((h2 >> c) & 1) : 1;
     }
 }
 
@@ -547,8 +562,19 @@ extern "C" int nfd_seq3(const nf_table* dT, const nf_cols* dC, const nfd_events*
     E.sts = ev->sts;
     E.sorted_rows = ev->sorted_rows;
     if (max_segments < 1) max_segments = 1;
-    hipLaunchKernelGGL(k_seq3, dim3(nf_blocks(max_segments, NF_TPB)), dim3(NF_TPB), 0, (hipStream_t)stream, dT, dC, E,
-                       n, seg_list, nseg, skeys, nkeys, *em);
+    // events per lane per load block (SH_S3_U: 4 / 8 / 16; measured)
+    static const int u = [] {
+        const char* e = getenv("SH_S3_U");
+        const int v = e ? atoi(e) : 8;
+        return v == 4 || v == 16 ? v : 8;
+    }();
+    const dim3 g(nf_blocks(max_segments, NF_TPB)), b(NF_TPB);
+    if (u == 4)
+        hipLaunchKernelGGL(k_seq3<4>, g, b, 0, (hipStream_t)stream, dT, dC, E, n, seg_list, nseg, skeys, nkeys, *em);
+    else if (u == 16)
+        hipLaunchKernelGGL(k_seq3<16>, g, b, 0, (hipStream_t)stream, dT, dC, E, n, seg_list, nseg, skeys, nkeys, *em);
+    else
+        hipLaunchKernelGGL(k_seq3<8>, g, b, 0, (hipStream_t)stream, dT, dC, E, n, seg_list, nseg, skeys, nkeys, *em);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -620,10 +646,13 @@ extern "C" int nfd_timer(const nf_table* dT, const nf_cols* dC, uint64_t* kstate
 
 extern "C" int nfd_place(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets, int n_out,
                          int32_t* out_query, uint64_t* out_seq, int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls,
-                         void* stream) {
-    if (nrec <= 0) return 0;
-    hipLaunchKernelGGL(k_nfa_place, dim3(nf_blocks(nrec, 256)), dim3(256), 0, (hipStream_t)stream, recs, nrec, stride,
-                       offsets, n_out, out_query, out_seq, out_ts, out_vals, out_nulls);
+                         uint32_t* inv, int64_t total, void* stream) {
+    if (nrec <= 0 || total <= 0) return 0;
+    hipMemsetAsync(inv, 0xFF, (size_t)total * 4, (hipStream_t)stream);
+    hipLaunchKernelGGL(k_nfa_inv, dim3(nf_blocks(nrec, 256)), dim3(256), 0, (hipStream_t)stream, recs, nrec, stride,
+                       offsets, inv);
+    hipLaunchKernelGGL(k_nfa_gather, dim3(nf_blocks(total, 256)), dim3(256), 0, (hipStream_t)stream, recs,
+                       (const uint32_t*)inv, total, nrec, stride, n_out, out_query, out_seq, out_ts, out_vals, out_nulls);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
