@@ -22,3 +22,9 @@ grep '^{' gpurun_out/bench_c2.log | cut -c1-300
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
     python bench.py --steps 3 --warmup 1 --cpu-sample 0 --no-verify > gpurun_out/prof/bench_prof.log 2>&1
 echo "prof rc=$?"
+$S 300 gpurun_out/bench_c3.log python -u bench.py --config c3 --steps 5 --warmup 1 || exit $?
+grep '^{' gpurun_out/bench_c3.log | cut -c1-300
+mkdir -p gpurun_out/prof3
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof3 -o run -- \
+    python bench.py --config c3 --steps 3 --warmup 1 --cpu-sample 0 --no-verify > gpurun_out/prof3/bench_prof.log 2>&1
+echo "prof3 rc=$?"

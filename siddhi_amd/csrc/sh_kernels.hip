@@ -170,7 +170,16 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
                                                        uint32_t sentinel, const uint32_t* __restrict__ idx_in, int64_t n,
                                                        int shift, const uint32_t* __restrict__ offs, int64_t ntiles,
                                                        uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out,
-                                                       shd_payload PL, int sub_shift) {
+                                                       shd_payload PL, int sub_shift, int xcd) {
+    // xcd: consecutive tiles go to one XCD (blocks are dealt round-robin over the 8
+    // XCDs), so the short per-digit runs neighbouring tiles write into the same digit
+    // region meet in one L2 and leave it as whole lines
+    int64_t tile = blockIdx.x;
+    if (xcd) {
+        const int64_t per = (ntiles + 7) >> 3;
+        tile = (int64_t)(blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+        if (tile >= ntiles) return;
+    }
     // every wave owns a contiguous quarter of the tile (items j*64 + lane), so ranking in
     // (j, lane) order inside a wave and then across waves is arrival order: a running
     // count per (wave, digit) bumped by each peer group's leader (returning LDS atomic)
@@ -183,12 +192,12 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
     __shared__ uint64_t stage[RADIX_TILE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int64_t base = (int64_t)blockIdx.x * RADIX_TILE;
+    const int64_t base = tile * RADIX_TILE;
     const int64_t wbase = base + (int64_t)w * WAVE_ITEMS + lane;  // element j: wbase + j * 64
     const int64_t tile_n = (n - base) < RADIX_TILE ? (n - base) : RADIX_TILE;
 #pragma unroll
     for (int q = 0; q < TPB / 64; q++) wcnt[q][threadIdx.x] = 0;
-    gbase[threadIdx.x] = offs[hist_idx(threadIdx.x, blockIdx.x, ntiles, sub_shift)];
+    gbase[threadIdx.x] = offs[hist_idx(threadIdx.x, (uint32_t)tile, ntiles, sub_shift)];
     uint32_t key[RADIX_ITEMS];
 #pragma unroll
     for (int j = 0; j < RADIX_ITEMS; j++) {
@@ -647,6 +656,15 @@ __global__ void k_place(const uint64_t* __restrict__ tmp, int64_t nrec, int rec_
 }
 
 // ------------------------------------------------------------------ host entry points
+// XCD-ordered scatter tiles (SH_RADIX_XCD=0 turns it off for A/B runs)
+static int radix_xcd() {
+    static const int on = [] {
+        const char* e = getenv("SH_RADIX_XCD");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    return on;
+}
+static unsigned scatter_grid(int64_t ntiles) { return radix_xcd() ? 8u * (unsigned)((ntiles + 7) >> 3) : (unsigned)ntiles; }
 static uint32_t g_bits_for(uint32_t maxkey) {
     uint32_t b = 0;
     while (b < 32 && (maxkey >> b)) b++;
@@ -690,8 +708,8 @@ extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segmen
                 PL.dst[c] = last ? carry->dst[c] : (to_mid ? mid[c] : carry->dst[c]);
             }
         }
-        hipLaunchKernelGGL(k_digit_scatter, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, b->keys, sentinel, iin, n,
-                           shift, (const uint32_t*)ws->hist, ntiles, kout, iout, PL, sub_shift);
+        hipLaunchKernelGGL(k_digit_scatter, dim3(scatter_grid(ntiles)), dim3(TPB), 0, st, kin, b->keys, sentinel, iin,
+                           n, shift, (const uint32_t*)ws->hist, ntiles, kout, iout, PL, sub_shift, radix_xcd());
         kin = kout;
         iin = iout;
         kout = (kout == ws->keys_a) ? ws->keys_b : ws->keys_a;
@@ -732,9 +750,9 @@ extern "C" int shd_sort_pairs(const uint32_t* keys, const uint32_t* vals, int64_
                            0xFFFFFFFFu, n, shift, hist, ntiles, -1);
         int rc = shd_exclusive_scan(hist, hist, 256 * ntiles, scan_tmp, stream);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_digit_scatter, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
+        hipLaunchKernelGGL(k_digit_scatter, dim3(scatter_grid(ntiles)), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
                            0xFFFFFFFFu, vin, n, shift, (const uint32_t*)hist, ntiles, kbuf[ps & 1], vbuf[ps & 1], PL,
-                           -1);
+                           -1, radix_xcd());
         kin = kbuf[ps & 1];
         vin = vbuf[ps & 1];
     }
