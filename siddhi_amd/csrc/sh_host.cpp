@@ -998,8 +998,9 @@ static int ensure_ws(sh_handle* h, int64_t n) {
     rc |= h->w_keys_b.ensure_fresh(n * 4);
     rc |= h->w_idx_a.ensure_fresh(n * 4);
     rc |= h->w_idx_b.ensure_fresh(n * 4);
-    rc |= h->w_hist.ensure_fresh(256 * tiles * 4 + 64);
-    size_t sw = std::max(shd_scan_tmp_words(256 * tiles), shd_scan_tmp_words(n));
+    // digit histograms: up to 1024 digits per radix block (10-bit passes)
+    rc |= h->w_hist.ensure_fresh(1024 * tiles * 4 + 64);
+    size_t sw = std::max(shd_scan_tmp_words(1024 * tiles), shd_scan_tmp_words(n));
     rc |= h->w_scan.ensure_fresh(sw * 4 + 64);
     rc |= h->w_seg.ensure_fresh((3 * n + 4) * 4);
     rc |= h->w_cnt.ensure_fresh(n * 4 + 4);

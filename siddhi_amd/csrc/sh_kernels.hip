@@ -23,6 +23,7 @@
 #include "sh_device.h"
 
 #include <string.h>
+#include <type_traits>
 
 #define TPB 256
 #define RADIX_ITEMS 16
@@ -125,17 +126,21 @@ extern "C" int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, 
 // (sub_shift >= 0, 2^sub_shift blocks per arrival tile): hist[(tile, d, blk in
 // tile)], so the scan keeps every arrival tile in its own region and sorts each
 // tile by key: the stable LSD passes then produce (tile, key, arrival) order.
+template <int B>
 __device__ __forceinline__ int64_t hist_idx(uint32_t d, uint32_t blk, int64_t ntiles, int sub_shift) {
     if (sub_shift < 0) return (int64_t)d * ntiles + blk;
-    return ((((int64_t)(blk >> sub_shift)) * 256 + d) << sub_shift) + (blk & ((1u << sub_shift) - 1u));
+    return ((((int64_t)(blk >> sub_shift)) * (1 << B) + d) << sub_shift) + (blk & ((1u << sub_shift) - 1u));
 }
 
-// digit histogram per block (layout: hist_idx)
+// digit histogram per block (layout: hist_idx); B-bit digits (8, or 10 for two
+// passes over 17..20-bit key ranges)
+template <int B>
 __global__ void __launch_bounds__(TPB) k_digit_hist(const uint32_t* __restrict__ keys, const int32_t* __restrict__ raw,
                                                     uint32_t sentinel, int64_t n, int shift,
                                                     uint32_t* __restrict__ hist, int64_t ntiles, int sub_shift) {
-    __shared__ uint32_t h[256];
-    h[threadIdx.x] = 0;
+    constexpr int ND = 1 << B;
+    __shared__ uint32_t h[ND];
+    for (int d = threadIdx.x; d < ND; d += TPB) h[d] = 0;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * RADIX_TILE;
 #pragma unroll 4
@@ -149,11 +154,11 @@ __global__ void __launch_bounds__(TPB) k_digit_hist(const uint32_t* __restrict__
                 int32_t r = raw ? raw[i] : 0;
                 k = r < 0 ? sentinel : (uint32_t)r;
             }
-            atomicAdd(&h[(k >> shift) & 0xFF], 1u);
+            atomicAdd(&h[(k >> shift) & (ND - 1)], 1u);
         }
     }
     __syncthreads();
-    hist[hist_idx(threadIdx.x, blockIdx.x, ntiles, sub_shift)] = h[threadIdx.x];
+    for (int d = threadIdx.x; d < ND; d += TPB) hist[hist_idx<B>(d, blockIdx.x, ntiles, sub_shift)] = h[d];
 }
 
 // stable scatter: elements of a tile are ranked in arrival order within their
@@ -166,6 +171,7 @@ __device__ __forceinline__ uint32_t load_key(const uint32_t* __restrict__ keys_i
     return r < 0 ? sentinel : (uint32_t)r;
 }
 
+template <int B>
 __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ raw,
                                                        uint32_t sentinel, const uint32_t* __restrict__ idx_in, int64_t n,
                                                        int shift, const uint32_t* __restrict__ offs, int64_t ntiles,
@@ -184,20 +190,24 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
     // (j, lane) order inside a wave and then across waves is arrival order: a running
     // count per (wave, digit) bumped by each peer group's leader (returning LDS atomic)
     // replaces a block barrier per item
+    constexpr int ND = 1 << B, DPT = ND / TPB;  // digits per thread in the prefix
     constexpr int WAVE_ITEMS = RADIX_TILE / (TPB / 64);
-    __shared__ uint32_t wcnt[TPB / 64][256];
-    __shared__ uint32_t tstart[256];
-    __shared__ uint32_t gbase[256];
-    __shared__ uint8_t dig[RADIX_TILE];
+    using dig_t = typename std::conditional<(B <= 8), uint8_t, uint16_t>::type;
+    __shared__ uint32_t wcnt[TPB / 64][ND];
+    __shared__ uint32_t tstart[ND];
+    __shared__ uint32_t gbase[ND];
+    __shared__ dig_t dig[RADIX_TILE];
     __shared__ uint64_t stage[RADIX_TILE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t base = tile * RADIX_TILE;
     const int64_t wbase = base + (int64_t)w * WAVE_ITEMS + lane;  // element j: wbase + j * 64
     const int64_t tile_n = (n - base) < RADIX_TILE ? (n - base) : RADIX_TILE;
+    for (int d = threadIdx.x; d < ND; d += TPB) {
 #pragma unroll
-    for (int q = 0; q < TPB / 64; q++) wcnt[q][threadIdx.x] = 0;
-    gbase[threadIdx.x] = offs[hist_idx(threadIdx.x, (uint32_t)tile, ntiles, sub_shift)];
+        for (int q = 0; q < TPB / 64; q++) wcnt[q][d] = 0;
+        gbase[d] = offs[hist_idx<B>(d, (uint32_t)tile, ntiles, sub_shift)];
+    }
     uint32_t key[RADIX_ITEMS];
 #pragma unroll
     for (int j = 0; j < RADIX_ITEMS; j++) {
@@ -210,10 +220,10 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
 #pragma unroll
     for (int j = 0; j < RADIX_ITEMS; j++) {
         const bool valid = wbase + j * 64 < n;
-        const uint32_t d = (key[j] >> shift) & 0xFF;
+        const uint32_t d = (key[j] >> shift) & (ND - 1);
         uint64_t peers = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; b++) {
+        for (int b = 0; b < B; b++) {
             const bool bit = (d >> b) & 1u;
             const uint64_t m = __ballot(valid && bit);
             peers &= bit ? m : ~m;
@@ -228,23 +238,33 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
     __syncthreads();
     {
         // per digit: exclusive prefix over the waves, then the tile-local digit starts
-        uint32_t c[TPB / 64], tot = 0;
+        // (thread t owns digits t*DPT .. t*DPT+DPT-1)
+        uint32_t loc[DPT], sum = 0;
 #pragma unroll
-        for (int q = 0; q < TPB / 64; q++) {
-            c[q] = wcnt[q][threadIdx.x];
-            wcnt[q][threadIdx.x] = tot;
-            tot += c[q];
+        for (int i = 0; i < DPT; i++) {
+            const int d = threadIdx.x * DPT + i;
+            uint32_t tot = 0;
+#pragma unroll
+            for (int q = 0; q < TPB / 64; q++) {
+                const uint32_t c = wcnt[q][d];
+                wcnt[q][d] = tot;
+                tot += c;
+            }
+            loc[i] = sum;
+            sum += tot;
         }
         uint32_t all;
-        tstart[threadIdx.x] = block_excl_scan(tot, &all);
+        const uint32_t ex = block_excl_scan(sum, &all);
+#pragma unroll
+        for (int i = 0; i < DPT; i++) tstart[threadIdx.x * DPT + i] = ex + loc[i];
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < RADIX_ITEMS; j++) {
         if (wbase + j * 64 < n) {
-            const uint32_t d = (key[j] >> shift) & 0xFF;
+            const uint32_t d = (key[j] >> shift) & (ND - 1);
             lp[j] += tstart[d] + wcnt[w][d];
-            dig[lp[j]] = (uint8_t)d;
+            dig[lp[j]] = (dig_t)d;
         }
     }
     __syncthreads();
@@ -664,6 +684,16 @@ static int radix_xcd() {
     }();
     return on;
 }
+// 10-bit digits for 17..20-bit key ranges: opt-in (SH_RADIX10=1). Measured on C3 / C5
+// (1M keys): two 10-bit passes 6.9 ms vs three 8-bit passes 6.35 ms for the segment
+// phase; a 1024-digit tile needs 64 KB of LDS (2 blocks per CU) and writes runs of ~4
+static int radix10() {
+    static const int on = [] {
+        const char* e = getenv("SH_RADIX10");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    return on;
+}
 static unsigned scatter_grid(int64_t ntiles) { return radix_xcd() ? 8u * (unsigned)((ntiles + 7) >> 3) : (unsigned)ntiles; }
 static uint32_t g_bits_for(uint32_t maxkey) {
     uint32_t b = 0;
@@ -682,16 +712,22 @@ extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segmen
     int64_t ntiles = ceil_div(n, RADIX_TILE);
     if (sub_shift >= 0) ntiles = ceil_div(ntiles, (int64_t)1 << sub_shift) << sub_shift;
     const uint32_t bits = g_bits_for(sentinel);
-    const int passes = b->keys ? (int)((bits + 7) / 8) : 0;
+    // 17..20-bit key ranges: two passes of 10-bit digits instead of three of 8 (opt-in)
+    const int db = (bits > 16 && bits <= 20 && radix10()) ? 10 : 8;
+    const int passes = b->keys ? (int)((bits + db - 1) / db) : 0;
     const uint32_t* kin = nullptr;
     const uint32_t* iin = nullptr;
     uint32_t* kout = ws->keys_a;
     uint32_t* iout = ws->idx_a;
     for (int ps = 0; ps < passes; ps++) {
-        const int shift = ps * 8;
-        hipLaunchKernelGGL(k_digit_hist, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, b->keys, sentinel, n, shift,
-                           ws->hist, ntiles, sub_shift);
-        int rc = shd_exclusive_scan(ws->hist, ws->hist, 256 * ntiles, ws->scan_tmp, stream);
+        const int shift = ps * db;
+        if (db == 10)
+            hipLaunchKernelGGL(k_digit_hist<10>, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, b->keys, sentinel, n,
+                               shift, ws->hist, ntiles, sub_shift);
+        else
+            hipLaunchKernelGGL(k_digit_hist<8>, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, b->keys, sentinel, n,
+                               shift, ws->hist, ntiles, sub_shift);
+        int rc = shd_exclusive_scan(ws->hist, ws->hist, ((int64_t)1 << db) * ntiles, ws->scan_tmp, stream);
         if (rc) return rc;
         // payload ping-pong: pass ps reads the previous pass's output (or the
         // original columns) and writes `mid` (odd distance to the last pass) or
@@ -708,8 +744,12 @@ extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segmen
                 PL.dst[c] = last ? carry->dst[c] : (to_mid ? mid[c] : carry->dst[c]);
             }
         }
-        hipLaunchKernelGGL(k_digit_scatter, dim3(scatter_grid(ntiles)), dim3(TPB), 0, st, kin, b->keys, sentinel, iin,
-                           n, shift, (const uint32_t*)ws->hist, ntiles, kout, iout, PL, sub_shift, radix_xcd());
+        if (db == 10)
+            hipLaunchKernelGGL(k_digit_scatter<10>, dim3(scatter_grid(ntiles)), dim3(TPB), 0, st, kin, b->keys, sentinel,
+                               iin, n, shift, (const uint32_t*)ws->hist, ntiles, kout, iout, PL, sub_shift, radix_xcd());
+        else
+            hipLaunchKernelGGL(k_digit_scatter<8>, dim3(scatter_grid(ntiles)), dim3(TPB), 0, st, kin, b->keys, sentinel,
+                               iin, n, shift, (const uint32_t*)ws->hist, ntiles, kout, iout, PL, sub_shift, radix_xcd());
         kin = kout;
         iin = iout;
         kout = (kout == ws->keys_a) ? ws->keys_b : ws->keys_a;
@@ -746,11 +786,11 @@ extern "C" int shd_sort_pairs(const uint32_t* keys, const uint32_t* vals, int64_
     memset(&PL, 0, sizeof(PL));
     for (int ps = 0; ps < passes && n > 0; ps++) {
         const int shift = ps * 8;
-        hipLaunchKernelGGL(k_digit_hist, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
+        hipLaunchKernelGGL(k_digit_hist<8>, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
                            0xFFFFFFFFu, n, shift, hist, ntiles, -1);
         int rc = shd_exclusive_scan(hist, hist, 256 * ntiles, scan_tmp, stream);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_digit_scatter, dim3(scatter_grid(ntiles)), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
+        hipLaunchKernelGGL(k_digit_scatter<8>, dim3(scatter_grid(ntiles)), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
                            0xFFFFFFFFu, vin, n, shift, (const uint32_t*)hist, ntiles, kbuf[ps & 1], vbuf[ps & 1], PL,
                            -1, radix_xcd());
         kin = kbuf[ps & 1];

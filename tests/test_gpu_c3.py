@@ -74,3 +74,19 @@ def test_mixed_attribute_shape_vs_oracle():
     assert st == 1
     assert len(gseq) == len(seq) > 0
     assert np.array_equal(gseq, seq.astype(np.int64)) and np.array_equal(gvals, vals)
+
+
+@pytest.mark.parametrize("engine", ["seq3", "general"])
+def test_c3_18bit_keys_vs_restatement(engine, monkeypatch):
+    """200k keys (18 bits) on the rise-and-fall and the general engine: three 8-bit
+    radix passes by default, two 10-bit passes when the process runs with SH_RADIX10=1
+    (scripts/gpu_radix10.sh ran this file both ways)"""
+    if engine == "general":
+        monkeypatch.setenv("SH_NO_SEQ3", "1")
+    n, nk = 4_000_000, 200_000
+    ts, k, p, v = synth.stock_stream(n, nk, 1000, config_index=3)
+    gseq, gvals, st = _gpu(synth.C3_QUERY, ts, [k, p, v], k, nk)
+    assert st == (1 if engine == "seq3" else 0)
+    eseq, evals = c3_expected(ts, k, p)
+    assert len(gseq) == len(eseq) > 0
+    assert np.array_equal(gseq, eseq) and np.array_equal(gvals, evals)
