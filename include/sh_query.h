@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SH_DESC_VERSION 3
+#define SH_DESC_VERSION 4
 #define SH_MAX_ORDER 4
 
 /* Attribute.Type (api/definition/Attribute.java) */
@@ -160,10 +160,16 @@ typedef struct sh_query_desc {
     int32_t order_expr[SH_MAX_ORDER]; /* variable expression per order-by attribute (HAVING_STATE resolution);
                                     INT / LONG / FLOAT / DOUBLE / BOOL (string order needs the text) */
     int32_t order_desc;          /* bit i: attribute i is DESC                  */
-    int32_t pad;
+    int32_t rate_kind;           /* enum sh_rate: the query's OutputRateLimiter (OutputParser.constructOutputRateLimiter) */
     int64_t limit;               /* QuerySelector.limit, -1 if none (SelectorParser.java:115-123) */
     int64_t offset;              /* QuerySelector.offset, -1 if none (:124-132)  */
+    int32_t rate_value;          /* events per period for SH_RATE_FIRST_EVENTS  */
+    int32_t pad;
 } sh_query_desc;
+
+/* output rate limiting (query/output/ratelimit/): PassThroughOutputRateLimiter, or
+   `output first every N events` (FirstPerEventOutputRateLimiter.java:47-72) */
+enum sh_rate { SH_RATE_NONE = 0, SH_RATE_FIRST_EVENTS = 1 };
 
 typedef struct sh_app_desc {
     int32_t version;             /* SH_DESC_VERSION                            */

@@ -497,6 +497,8 @@ struct Selector : Proc {
     void orderChunk(Chunk<StateEvent>& c);
     void offsetChunk(Chunk<StateEvent>& c);
     void limitChunk(Chunk<StateEvent>& c);
+    void rateProcess(Chunk<StateEvent>& c);
+    std::unordered_map<int64_t, int32_t> rateCounter;  // RateLimiterState per partition flow
     void sendToCallBacks(Chunk<StateEvent>& c);
 };
 
@@ -2182,6 +2184,30 @@ void Selector::limitChunk(Chunk<StateEvent>& c) {
         }
     }
 }
+// the query's OutputRateLimiter.process: PassThroughOutputRateLimiter, or
+// FirstPerEventOutputRateLimiter.process (FirstPerEventOutputRateLimiter.java:47-72) with
+// its counter in a per-partition state (int arithmetic: with N == 1 it never resets)
+void Selector::rateProcess(Chunk<StateEvent>& c) {
+    if (q->d.rate_kind != SH_RATE_FIRST_EVENTS) {
+        sendToCallBacks(c);
+        return;
+    }
+    Chunk<StateEvent> out;
+    int32_t& counter = rateCounter[q->app->flow.key];
+    c.reset();
+    while (c.hasNext()) {
+        SE ev = c.next();
+        c.remove();
+        counter = (int32_t)((uint32_t)counter + 1u);
+        if (counter == 1) {
+            out.add(ev);
+        } else if (counter == q->d.rate_value) {
+            counter = 0;
+        }
+    }
+    out.reset();
+    if (out.hasNext()) sendToCallBacks(out);
+}
 void Selector::process(Chunk<StateEvent>& c) {
     if (containsAggregator) {
         // processInBatchNoGroupBy, QuerySelector.java:271-313: the last event that
@@ -2202,7 +2228,7 @@ void Selector::process(Chunk<StateEvent>& c) {
         if (lastEv) {
             c.clear();
             c.add(lastEv);
-            sendToCallBacks(c);
+            rateProcess(c);
         }
         return;
     }
@@ -2229,7 +2255,7 @@ void Selector::process(Chunk<StateEvent>& c) {
     if (q->d.offset >= 0) offsetChunk(c);
     if (q->d.limit >= 0) limitChunk(c);
     c.reset();
-    if (c.hasNext()) sendToCallBacks(c);
+    if (c.hasNext()) rateProcess(c);
 }
 // OutputRateLimiter.sendToCallBacks, OutputRateLimiter.java:63-106
 void Selector::sendToCallBacks(Chunk<StateEvent>& c) {
@@ -2638,6 +2664,8 @@ ref_app* ref_create(const sh_app_desc* d, char* err, int errlen) {
         for (int o = 0; o < qd.n_outputs; o++) agg |= qd.outputs[o].agg != SH_AGG_NONE;
         // processInBatchNoGroupBy would pass an empty chunk on (QuerySelector.java:304-311)
         if (agg && (qd.offset > 0 || qd.limit == 0)) serr = "aggregating selector with offset > 0 or limit 0";
+        if (qd.rate_kind != SH_RATE_NONE && (qd.rate_kind != SH_RATE_FIRST_EVENTS || qd.rate_value < 1))
+            serr = "output rate limiting: `output first every N events` only";
         if (!serr.empty()) {
             delete ra;
             return fail("query " + std::to_string(qi) + ": " + serr);

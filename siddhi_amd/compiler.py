@@ -191,6 +191,7 @@ class Query:
     order_by: list = field(default_factory=list)   # [(EVar, desc)] (Selector.orderByList)
     limit: object = None         # Selector.limit / offset expressions (constants)
     offset: object = None
+    rate_first_events: Optional[int] = None   # `output first every N events`
 
 
 @dataclass
@@ -475,8 +476,25 @@ class Parser:
                 offset = self.expr()
         else:
             star = True
+        rate = None
         if self.kw("output"):
-            raise UnsupportedQuery("output rate limiting is out of scope")
+            # output_rate: OUTPUT (ALL|LAST|FIRST)? EVERY (INT EVENTS | time) | OUTPUT SNAPSHOT EVERY time
+            # (SiddhiQL.g4 output_rate); the device runs `output first every N events`
+            self.next()
+            kind = None
+            for w in ("all", "last", "first", "snapshot"):
+                if self.kw(w):
+                    kind = self.next().text.lower()
+                    break
+            self.expect_kw("every")
+            tk = self.peek()
+            if kind != "first" or tk.kind != "num" or not self.peek(1).text.lower() == "events":
+                raise UnsupportedQuery("output rate limiting: only `output first every N events` runs on the device")
+            n = int(self.next().text)
+            self.next()  # events
+            if n < 1:
+                raise UnsupportedQuery("output first every 0 events")
+            rate = n
         self.expect_kw("insert")
         if self.kw("current"):
             self.next()
@@ -490,7 +508,7 @@ class Parser:
             raise UnsupportedQuery("inner-stream outputs (#Stream) are out of scope")
         out = self.ident()
         return Query(name, st, root, within, sel, star, out, having=having, order_by=order,
-                     limit=limit, offset=offset)
+                     limit=limit, offset=offset, rate_first_events=rate)
 
     def detect_state_type(self):
         depth = 0
@@ -1170,6 +1188,9 @@ class CompiledApp:
                 q.order_desc |= (1 << i) if desc else 0
             q.limit = cq.limit
             q.offset = cq.offset
+            if cq.query.rate_first_events:
+                q.rate_kind = 1  # SH_RATE_FIRST_EVENTS
+                q.rate_value = cq.query.rate_first_events
             q.elems = el
             q.exprs = ex
             q.outputs = ou

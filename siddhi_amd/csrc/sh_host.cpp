@@ -570,11 +570,13 @@ static int lower_chain(sh_handle* h, const sh_app_desc* app, int qi, shp_program
     return SH_OK;
 }
 
-// having / order by / limit / offset need the selector pass of the general engine
+// having / order by / limit / offset / output rate limiting need the selector pass of
+// the general engine
 static bool has_selector_extras(const sh_app_desc* app) {
     for (int32_t q = 0; q < app->n_queries; q++) {
         const sh_query_desc& d = app->queries[q];
-        if (d.having >= 0 || d.n_order > 0 || d.limit >= 0 || d.offset >= 0) return true;
+        if (d.having >= 0 || d.n_order > 0 || d.limit >= 0 || d.offset >= 0 || d.rate_kind != SH_RATE_NONE)
+            return true;
     }
     return false;
 }

@@ -136,6 +136,7 @@ struct nf_query {
     int32_t n_order, order_desc;    // OrderByEventComparator: attributes, DESC bit per attribute
     int32_t order_pc[SH_MAX_ORDER], order_len[SH_MAX_ORDER];
     int64_t limit, offset;          // QuerySelector limit / offset (-1: none)
+    int32_t rate_kind, rate_value;  // OutputRateLimiter (enum sh_rate); its counter: qb[3] >> 32
     nf_layout lay;
     int64_t q_off;          // word offset of this query's block inside a key block
     // rise-and-fall sequence `every e1=S, e2=S[f2(e2, e1)]+, e3=S[f3(e3, e2[last])]`
@@ -1567,6 +1568,27 @@ struct NfLane {
             }
         }
     }
+    // the query's OutputRateLimiter.process: PassThrough, or FirstPerEventOutputRateLimiter
+    // (FirstPerEventOutputRateLimiter.java:47-72): per partition a counter; an event is
+    // kept when the counter reaches 1 and the counter resets when it reaches N (with N = 1
+    // it never resets, as in the reference: only the first event ever passes)
+    NF_HD void rate_send(uint32_t* c) {
+        if (Q->rate_kind == SH_RATE_FIRST_EVENTS) {
+            uint32_t cnt = (uint32_t)(qb[3] >> 32);
+            ch_reset(c);
+            while (ch_has_next(c)) {
+                ch_next(c);
+                cnt++;
+                if (cnt == 1u) continue;
+                if (cnt == (uint32_t)Q->rate_value) cnt = 0;
+                ch_remove(c);
+            }
+            qb[3] = (qb[3] & 0xFFFFFFFFull) | ((uint64_t)cnt << 32);
+            ch_reset(c);
+            if (!ch_has_next(c)) return;
+        }
+        send_to_callbacks(c);
+    }
     NF_HD void selector_process(uint32_t* c) {
         if (Q->contains_agg) {
             // processInBatchNoGroupBy (QuerySelector.java:271-313): the last event
@@ -1588,7 +1610,7 @@ struct NfLane {
             if (last) {
                 ch_clear(c);
                 ch_add(c, last);
-                send_to_callbacks(c);
+                rate_send(c);
             }
             return;
         }
@@ -1609,7 +1631,7 @@ struct NfLane {
         if (Q->offset >= 0) offset_chunk(c);
         if (Q->limit >= 0) limit_chunk(c);
         ch_reset(c);
-        if (ch_has_next(c)) send_to_callbacks(c);
+        if (ch_has_next(c)) rate_send(c);
     }
     // OutputRateLimiter.sendToCallBacks (OutputRateLimiter.java:63-106)
     NF_HD void send_to_callbacks(uint32_t* c) {

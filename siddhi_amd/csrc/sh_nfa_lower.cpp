@@ -591,7 +591,8 @@ struct QueryLowering {
             return false;
         }
         // k_seq3 emits without a selector pass
-        if (q->having < 0 && q->n_order == 0 && q->limit < 0 && q->offset < 0) detect_seq3();
+        if (q->having < 0 && q->n_order == 0 && q->limit < 0 && q->offset < 0 && q->rate_kind == SH_RATE_NONE)
+            detect_seq3();
         Q->n_out = q->n_outputs;
         for (int o = 0; o < q->n_outputs; o++) {
             const sh_output_attr& oa = q->outputs[o];
@@ -637,6 +638,12 @@ struct QueryLowering {
         }
         Q->limit = q->limit;
         Q->offset = q->offset;
+        Q->rate_kind = q->rate_kind;
+        Q->rate_value = q->rate_value;
+        if (q->rate_kind != SH_RATE_NONE && (q->rate_kind != SH_RATE_FIRST_EVENTS || q->rate_value < 1)) {
+            err = "output rate limiting: `output first every N events` (N >= 1) only";
+            return false;
+        }
         if (Q->contains_agg && (q->offset > 0 || q->limit == 0)) {
             // processInBatchNoGroupBy would hand an empty chunk to the rate limiter
             err = "aggregating selector with offset > 0 or limit 0 never emits";

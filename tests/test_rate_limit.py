@@ -1,0 +1,158 @@
+"""`output first every N events` on pattern / sequence queries (SURVEY.md 8(f) row 3,
+output rate limiting). FirstPerEventOutputRateLimiter.process
+(FirstPerEventOutputRateLimiter.java:47-72): a counter per partition (RateLimiterState
+through the query's state holder); an event passes when the counter reaches 1, the
+counter resets when it reaches N, so with N = 1 only the first event ever passes.
+Pinned by the counts of the reference's EventOutputRateLimitTestCase (5 events, N = 2
+-> 3 outputs; N = 3 -> 2 outputs), transcribed onto a one-state pattern that emits once
+per event; randomized apps hold the general engine's kernel logic and the device to the
+oracle. Other rate limiters (all / last per events, time, snapshot) stay on the Java
+side (UnsupportedQuery)."""
+import random
+import re
+
+import pytest
+
+from fixture_runner import Unsupported
+from nfa_cases import nfa_case, run_case, same_rows
+from nfa_host_engine import NfaHostEngine, NfaUnsupported
+from oracle_engine import OracleEngine
+from siddhi_amd import SiddhiAppCreationException, compiler
+
+LOGIN = ("define stream LoginEvents (timestamp long, ip string); "
+         "@info(name = 'query1') from every e1=LoginEvents select e1.ip as ip "
+         "output first every {n} events insert into Out;")
+IPS = ["192.10.1.5", "192.10.1.3", "192.10.1.9", "192.10.1.4", "192.10.1.3"]
+
+BASE = ("define stream A (sym string, price float, n int); define stream B (sym string, price float, n int); "
+        "@info(name = 'query1') from every e1=A -> e2=B[price > e1.price] "
+        "select e1.price as p1, e2.price as p2 {tail} insert into Out;")
+ACTS = [("send", "A", [(1, ["x", 10.0, 2])]), ("send", "A", [(2, ["x", 30.0, 1])]),
+        ("send", "A", [(3, ["x", 20.0, 2])]), ("send", "B", [(4, ["x", 40.0, 0])]),
+        ("send", "A", [(5, ["x", 1.0, 2])]), ("send", "B", [(6, ["x", 2.0, 0])]),
+        ("send", "A", [(7, ["x", 1.0, 2])]), ("send", "B", [(8, ["x", 3.0, 0])])]
+# the five matches in emission order: (10,40) (30,40) (20,40) (1,2) (1,3)
+KNOWN = [
+    ("", [[10.0, 40.0], [30.0, 40.0], [20.0, 40.0], [1.0, 2.0], [1.0, 3.0]]),
+    ("output first every 2 events", [[10.0, 40.0], [20.0, 40.0], [1.0, 3.0]]),
+    ("output first every 3 events", [[10.0, 40.0], [1.0, 2.0]]),
+    ("output first every 1 events", [[10.0, 40.0]]),
+    ("output first every 9 events", [[10.0, 40.0]]),
+]
+PART = ("define stream A (sym string, price float, n int); partition with (sym of A) begin "
+        "@info(name = 'query1') from every e1=A select e1.sym as s, e1.n as n "
+        "output first every 2 events insert into Out; end;")
+
+
+def _hip_factory():
+    from siddhi_amd._native import HipEngine, HipError
+
+    def hip(c):
+        try:
+            return HipEngine(c)
+        except HipError as e:
+            if e.code == -4:
+                raise Unsupported(str(e))
+            raise
+    return hip
+
+
+def _login(factory, n):
+    acts = [("send", "LoginEvents", [(1000 + i, [1000 + i, ip])]) for i, ip in enumerate(IPS)]
+    return run_case(factory, LOGIN.format(n=n), acts)
+
+
+ENGINES = [("oracle", lambda: OracleEngine), ("kernel_logic", lambda: NfaHostEngine)]
+
+
+@pytest.mark.parametrize("name,factory", ENGINES)
+@pytest.mark.parametrize("n,count", [(2, 3), (3, 2)])
+def test_reference_counts(name, factory, n, count):
+    """EventOutputRateLimitTestCase: 5 events, first every 2 -> 3; first every 3 -> 2"""
+    got = _login(factory(), n)
+    assert len(got) == count
+    assert [r[2][0] for r in got] == [IPS[i] for i in range(0, len(IPS), n)]
+
+
+@pytest.mark.parametrize("name,factory", ENGINES)
+@pytest.mark.parametrize("tail,want", KNOWN)
+def test_known_answers(name, factory, tail, want):
+    assert [r[2] for r in run_case(factory(), BASE.format(tail=tail), ACTS)] == want
+
+
+@pytest.mark.parametrize("name,factory", ENGINES)
+def test_per_partition_counter(name, factory):
+    """one RateLimiterState per partition key: each key's 1st, 3rd, ... event passes"""
+    ev = [("K0", 1), ("K1", 2), ("K0", 3), ("K0", 4), ("K1", 5), ("K1", 6), ("K0", 7), ("K0", 8)]
+    acts = [("send", "A", [(10 + i, [k, 1.0, n])]) for i, (k, n) in enumerate(ev)]
+    got = [r[2] for r in run_case(factory(), PART, acts)]
+    assert got == [["K0", 1], ["K1", 2], ["K0", 4], ["K1", 6], ["K0", 8]]
+
+
+def test_parse():
+    c = compiler.compile_app(BASE.format(tail="output first every 4 events"))
+    d = c.descriptor().queries[0]
+    assert d.rate_kind == 1 and d.rate_value == 4
+    assert compiler.compile_app(BASE.format(tail="")).descriptor().queries[0].rate_kind == 0
+    for tail in ("output last every 2 events", "output all every 2 events", "output every 2 events",
+                 "output first every 1 sec", "output snapshot every 1 sec"):
+        with pytest.raises(compiler.UnsupportedQuery):
+            compiler.compile_app(BASE.format(tail=tail))
+
+
+def rate_case(seed):
+    rng = random.Random(5100 + seed)
+    app, actions = nfa_case(rng)
+    if " select " not in app:
+        return None
+    app = re.sub(r" insert into Out;", lambda m: f" output first every {rng.choice([1, 2, 2, 3, 5])} events"
+                 " insert into Out;", app)
+    return app, actions
+
+
+def _apps(n):
+    return [(s, c) for s in range(n) for c in [rate_case(s)] if c is not None]
+
+
+@pytest.mark.parametrize("seed,case", _apps(100), ids=lambda x: str(x) if isinstance(x, int) else "")
+def test_rate_kernel_logic_vs_oracle(seed, case):
+    app, actions = case
+    try:
+        ref = run_case(OracleEngine, app, actions)
+    except (SiddhiAppCreationException, Unsupported, RuntimeError) as e:
+        pytest.skip(f"outside the subset: {e}")
+    try:
+        got = run_case(NfaHostEngine, app, actions)
+    except NfaUnsupported as e:
+        pytest.skip(f"not lowered: {e}")
+    assert same_rows(got, ref), app
+
+
+@pytest.mark.gpu
+def test_known_and_reference_counts_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    hip = _hip_factory()
+    for n, count in [(2, 3), (3, 2)]:
+        assert len(_login(hip, n)) == count
+    for tail, want in KNOWN:
+        assert [r[2] for r in run_case(hip, BASE.format(tail=tail), ACTS)] == want, tail
+    ev = [("K0", 1), ("K1", 2), ("K0", 3), ("K0", 4), ("K1", 5), ("K1", 6), ("K0", 7), ("K0", 8)]
+    acts = [("send", "A", [(10 + i, [k, 1.0, n])]) for i, (k, n) in enumerate(ev)]
+    assert [r[2] for r in run_case(hip, PART, acts)] == [["K0", 1], ["K1", 2], ["K0", 4], ["K1", 6], ["K0", 8]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,case", _apps(50), ids=lambda x: str(x) if isinstance(x, int) else "")
+def test_rate_gpu_vs_oracle(seed, case):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    app, actions = case
+    try:
+        ref = run_case(OracleEngine, app, actions)
+        got = run_case(_hip_factory(), app, actions)
+    except (SiddhiAppCreationException, Unsupported, RuntimeError) as e:
+        pytest.skip(f"outside the subset: {e}")
+    assert same_rows(got, ref), app
