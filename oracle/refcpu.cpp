@@ -2184,11 +2184,13 @@ void Selector::limitChunk(Chunk<StateEvent>& c) {
         }
     }
 }
-// the query's OutputRateLimiter.process: PassThroughOutputRateLimiter, or
-// FirstPerEventOutputRateLimiter.process (FirstPerEventOutputRateLimiter.java:47-72) with
-// its counter in a per-partition state (int arithmetic: with N == 1 it never resets)
+// the query's OutputRateLimiter.process: PassThroughOutputRateLimiter,
+// FirstPerEventOutputRateLimiter.process (FirstPerEventOutputRateLimiter.java:47-72) or
+// LastPerEventOutputRateLimiter.process (LastPerEventOutputRateLimiter.java:45-68), each
+// with its counter in a per-partition state (int arithmetic: FIRST with N == 1 never resets)
 void Selector::rateProcess(Chunk<StateEvent>& c) {
-    if (q->d.rate_kind != SH_RATE_FIRST_EVENTS) {
+    const int kind = q->d.rate_kind;
+    if (kind != SH_RATE_FIRST_EVENTS && kind != SH_RATE_LAST_EVENTS) {
         sendToCallBacks(c);
         return;
     }
@@ -2197,12 +2199,21 @@ void Selector::rateProcess(Chunk<StateEvent>& c) {
     c.reset();
     while (c.hasNext()) {
         SE ev = c.next();
-        c.remove();
-        counter = (int32_t)((uint32_t)counter + 1u);
-        if (counter == 1) {
-            out.add(ev);
-        } else if (counter == q->d.rate_value) {
-            counter = 0;
+        if (kind == SH_RATE_FIRST_EVENTS) {
+            c.remove();
+            counter = (int32_t)((uint32_t)counter + 1u);
+            if (counter == 1) {
+                out.add(ev);
+            } else if (counter == q->d.rate_value) {
+                counter = 0;
+            }
+        } else if (ev->type == CURRENT || ev->type == EXPIRED) {
+            counter = (int32_t)((uint32_t)counter + 1u);
+            if (counter == q->d.rate_value) {
+                c.remove();
+                out.add(ev);
+                counter = 0;
+            }
         }
     }
     out.reset();
@@ -2664,8 +2675,9 @@ ref_app* ref_create(const sh_app_desc* d, char* err, int errlen) {
         for (int o = 0; o < qd.n_outputs; o++) agg |= qd.outputs[o].agg != SH_AGG_NONE;
         // processInBatchNoGroupBy would pass an empty chunk on (QuerySelector.java:304-311)
         if (agg && (qd.offset > 0 || qd.limit == 0)) serr = "aggregating selector with offset > 0 or limit 0";
-        if (qd.rate_kind != SH_RATE_NONE && (qd.rate_kind != SH_RATE_FIRST_EVENTS || qd.rate_value < 1))
-            serr = "output rate limiting: `output first every N events` only";
+        if (qd.rate_kind != SH_RATE_NONE &&
+            ((qd.rate_kind != SH_RATE_FIRST_EVENTS && qd.rate_kind != SH_RATE_LAST_EVENTS) || qd.rate_value < 1))
+            serr = "output rate limiting: `output first|last every N events` only";
         if (!serr.empty()) {
             delete ra;
             return fail("query " + std::to_string(qi) + ": " + serr);

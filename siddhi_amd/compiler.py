@@ -191,7 +191,7 @@ class Query:
     order_by: list = field(default_factory=list)   # [(EVar, desc)] (Selector.orderByList)
     limit: object = None         # Selector.limit / offset expressions (constants)
     offset: object = None
-    rate_first_events: Optional[int] = None   # `output first every N events`
+    rate: Optional[Tuple[int, int]] = None   # (enum sh_rate, N): `output first|last every N events`
 
 
 @dataclass
@@ -488,13 +488,13 @@ class Parser:
                     break
             self.expect_kw("every")
             tk = self.peek()
-            if kind != "first" or tk.kind != "num" or not self.peek(1).text.lower() == "events":
-                raise UnsupportedQuery("output rate limiting: only `output first every N events` runs on the device")
+            if kind not in ("first", "last") or tk.kind != "num" or not self.peek(1).text.lower() == "events":
+                raise UnsupportedQuery("output rate limiting: only `output first|last every N events` runs on the device")
             n = int(self.next().text)
             self.next()  # events
             if n < 1:
-                raise UnsupportedQuery("output first every 0 events")
-            rate = n
+                raise UnsupportedQuery(f"output {kind} every 0 events")
+            rate = (1 if kind == "first" else 2, n)
         self.expect_kw("insert")
         if self.kw("current"):
             self.next()
@@ -508,7 +508,7 @@ class Parser:
             raise UnsupportedQuery("inner-stream outputs (#Stream) are out of scope")
         out = self.ident()
         return Query(name, st, root, within, sel, star, out, having=having, order_by=order,
-                     limit=limit, offset=offset, rate_first_events=rate)
+                     limit=limit, offset=offset, rate=rate)
 
     def detect_state_type(self):
         depth = 0
@@ -1188,9 +1188,8 @@ class CompiledApp:
                 q.order_desc |= (1 << i) if desc else 0
             q.limit = cq.limit
             q.offset = cq.offset
-            if cq.query.rate_first_events:
-                q.rate_kind = 1  # SH_RATE_FIRST_EVENTS
-                q.rate_value = cq.query.rate_first_events
+            if cq.query.rate:
+                q.rate_kind, q.rate_value = cq.query.rate
             q.elems = el
             q.exprs = ex
             q.outputs = ou

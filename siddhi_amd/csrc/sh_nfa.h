@@ -1568,19 +1568,29 @@ struct NfLane {
             }
         }
     }
-    // the query's OutputRateLimiter.process: PassThrough, or FirstPerEventOutputRateLimiter
-    // (FirstPerEventOutputRateLimiter.java:47-72): per partition a counter; an event is
-    // kept when the counter reaches 1 and the counter resets when it reaches N (with N = 1
-    // it never resets, as in the reference: only the first event ever passes)
+    // the query's OutputRateLimiter.process with its counter per partition:
+    // FirstPerEventOutputRateLimiter (FirstPerEventOutputRateLimiter.java:47-72) keeps an
+    // event when the counter reaches 1 and resets at N (with N = 1 it never resets, as in
+    // the reference: only the first event ever passes); LastPerEventOutputRateLimiter
+    // (LastPerEventOutputRateLimiter.java:45-68) keeps every N-th current event
     NF_HD void rate_send(uint32_t* c) {
-        if (Q->rate_kind == SH_RATE_FIRST_EVENTS) {
+        if (Q->rate_kind == SH_RATE_FIRST_EVENTS || Q->rate_kind == SH_RATE_LAST_EVENTS) {
+            const bool first = Q->rate_kind == SH_RATE_FIRST_EVENTS;
             uint32_t cnt = (uint32_t)(qb[3] >> 32);
             ch_reset(c);
             while (ch_has_next(c)) {
-                ch_next(c);
-                cnt++;
-                if (cnt == 1u) continue;
-                if (cnt == (uint32_t)Q->rate_value) cnt = 0;
+                const uint32_t ev = ch_next(c);
+                if (first) {
+                    cnt++;
+                    if (cnt == 1u) continue;
+                    if (cnt == (uint32_t)Q->rate_value) cnt = 0;
+                } else {
+                    const int ty = se_type(ev);
+                    if ((ty == NF_CURRENT || ty == NF_EXPIRED) && ++cnt == (uint32_t)Q->rate_value) {
+                        cnt = 0;
+                        continue;
+                    }
+                }
                 ch_remove(c);
             }
             qb[3] = (qb[3] & 0xFFFFFFFFull) | ((uint64_t)cnt << 32);

@@ -1,13 +1,15 @@
-"""`output first every N events` on pattern / sequence queries (SURVEY.md 8(f) row 3,
+"""`output first|last every N events` on pattern / sequence queries (SURVEY.md 8(f) row 3,
 output rate limiting). FirstPerEventOutputRateLimiter.process
 (FirstPerEventOutputRateLimiter.java:47-72): a counter per partition (RateLimiterState
 through the query's state holder); an event passes when the counter reaches 1, the
-counter resets when it reaches N, so with N = 1 only the first event ever passes.
-Pinned by the counts of the reference's EventOutputRateLimitTestCase (5 events, N = 2
--> 3 outputs; N = 3 -> 2 outputs), transcribed onto a one-state pattern that emits once
+counter resets when it reaches N, so with N = 1 only the first event ever passes;
+LastPerEventOutputRateLimiter.process (LastPerEventOutputRateLimiter.java:45-68) passes
+every N-th current event. Pinned by the counts of the reference's
+EventOutputRateLimitTestCase (5 events: first every 2 -> 3, first every 3 -> 2, last
+every 2 -> 2, last every 4 -> 1), transcribed onto a one-state pattern that emits once
 per event; randomized apps hold the general engine's kernel logic and the device to the
-oracle. Other rate limiters (all / last per events, time, snapshot) stay on the Java
-side (UnsupportedQuery)."""
+oracle. The other rate limiters (all per events, time, snapshot) stay on the Java side
+(UnsupportedQuery)."""
 import random
 import re
 
@@ -21,7 +23,7 @@ from siddhi_amd import SiddhiAppCreationException, compiler
 
 LOGIN = ("define stream LoginEvents (timestamp long, ip string); "
          "@info(name = 'query1') from every e1=LoginEvents select e1.ip as ip "
-         "output first every {n} events insert into Out;")
+         "output {kind} every {n} events insert into Out;")
 IPS = ["192.10.1.5", "192.10.1.3", "192.10.1.9", "192.10.1.4", "192.10.1.3"]
 
 BASE = ("define stream A (sym string, price float, n int); define stream B (sym string, price float, n int); "
@@ -38,6 +40,10 @@ KNOWN = [
     ("output first every 3 events", [[10.0, 40.0], [1.0, 2.0]]),
     ("output first every 1 events", [[10.0, 40.0]]),
     ("output first every 9 events", [[10.0, 40.0]]),
+    ("output last every 2 events", [[30.0, 40.0], [1.0, 2.0]]),
+    ("output last every 3 events", [[20.0, 40.0]]),
+    ("output last every 1 events", [[10.0, 40.0], [30.0, 40.0], [20.0, 40.0], [1.0, 2.0], [1.0, 3.0]]),
+    ("output last every 9 events", []),
 ]
 PART = ("define stream A (sym string, price float, n int); partition with (sym of A) begin "
         "@info(name = 'query1') from every e1=A select e1.sym as s, e1.n as n "
@@ -57,21 +63,26 @@ def _hip_factory():
     return hip
 
 
-def _login(factory, n):
+def _login(factory, n, kind="first"):
     acts = [("send", "LoginEvents", [(1000 + i, [1000 + i, ip])]) for i, ip in enumerate(IPS)]
-    return run_case(factory, LOGIN.format(n=n), acts)
+    return run_case(factory, LOGIN.format(n=n, kind=kind), acts)
 
 
 ENGINES = [("oracle", lambda: OracleEngine), ("kernel_logic", lambda: NfaHostEngine)]
 
 
+REF_COUNTS = [("first", 2, 3), ("first", 3, 2), ("last", 2, 2), ("last", 4, 1)]
+
+
 @pytest.mark.parametrize("name,factory", ENGINES)
-@pytest.mark.parametrize("n,count", [(2, 3), (3, 2)])
-def test_reference_counts(name, factory, n, count):
-    """EventOutputRateLimitTestCase: 5 events, first every 2 -> 3; first every 3 -> 2"""
-    got = _login(factory(), n)
+@pytest.mark.parametrize("kind,n,count", REF_COUNTS)
+def test_reference_counts(name, factory, kind, n, count):
+    """EventOutputRateLimitTestCase: 5 events; first every 2 -> 3, first every 3 -> 2,
+    last every 2 -> 2, last every 4 -> 1"""
+    got = _login(factory(), n, kind)
     assert len(got) == count
-    assert [r[2][0] for r in got] == [IPS[i] for i in range(0, len(IPS), n)]
+    start = 0 if kind == "first" else n - 1
+    assert [r[2][0] for r in got] == [IPS[i] for i in range(start, len(IPS), n)]
 
 
 @pytest.mark.parametrize("name,factory", ENGINES)
@@ -93,8 +104,10 @@ def test_parse():
     c = compiler.compile_app(BASE.format(tail="output first every 4 events"))
     d = c.descriptor().queries[0]
     assert d.rate_kind == 1 and d.rate_value == 4
+    d = compiler.compile_app(BASE.format(tail="output last every 3 events")).descriptor().queries[0]
+    assert d.rate_kind == 2 and d.rate_value == 3
     assert compiler.compile_app(BASE.format(tail="")).descriptor().queries[0].rate_kind == 0
-    for tail in ("output last every 2 events", "output all every 2 events", "output every 2 events",
+    for tail in ("output all every 2 events", "output every 2 events",
                  "output first every 1 sec", "output snapshot every 1 sec"):
         with pytest.raises(compiler.UnsupportedQuery):
             compiler.compile_app(BASE.format(tail=tail))
@@ -105,8 +118,8 @@ def rate_case(seed):
     app, actions = nfa_case(rng)
     if " select " not in app:
         return None
-    app = re.sub(r" insert into Out;", lambda m: f" output first every {rng.choice([1, 2, 2, 3, 5])} events"
-                 " insert into Out;", app)
+    app = re.sub(r" insert into Out;", lambda m: f" output {rng.choice(['first', 'last'])} every "
+                 f"{rng.choice([1, 2, 2, 3, 5])} events insert into Out;", app)
     return app, actions
 
 
@@ -134,8 +147,8 @@ def test_known_and_reference_counts_gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     hip = _hip_factory()
-    for n, count in [(2, 3), (3, 2)]:
-        assert len(_login(hip, n)) == count
+    for kind, n, count in REF_COUNTS:
+        assert len(_login(hip, n, kind)) == count
     for tail, want in KNOWN:
         assert [r[2] for r in run_case(hip, BASE.format(tail=tail), ACTS)] == want, tail
     ev = [("K0", 1), ("K1", 2), ("K0", 3), ("K0", 4), ("K1", 5), ("K1", 6), ("K0", 7), ("K0", 8)]
