@@ -153,6 +153,24 @@ def test_random_apps_continue_exactly_after_restore(seed):
         assert same_rows(got, ref), (app, cut)
 
 
+@pytest.mark.parametrize("seed", range(16))
+def test_rate_limited_apps_continue_exactly_after_restore(seed):
+    """the output rate limiter's per-partition counter (FirstPer / LastPerEventOutputRateLimiter
+    RateLimiterState.snapshot) travels in the key blocks of the image"""
+    import re
+    rng = random.Random(4600 + seed)
+    app, actions = nfa_case(rng)
+    app = re.sub(r" insert into Out;", lambda m: f" output {rng.choice(['first', 'last'])} every "
+                 f"{rng.choice([2, 3, 4])} events insert into Out;", app)
+    try:
+        ref = _full(app, actions)
+    except (Unsupported, SiddhiAppCreationException):
+        pytest.skip("invalid app or a shape not lowered to the device")
+    for cut in sorted({1, len(actions) // 3, len(actions) // 2, (2 * len(actions)) // 3}):
+        got = _run_split(app, actions, cut)
+        assert same_rows(got, ref), (app, cut)
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_window_apps_continue_exactly_after_restore(seed):
     """streaming chain / window engine (mode 0): partial lists in the key blocks"""
