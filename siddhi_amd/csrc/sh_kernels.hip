@@ -287,16 +287,19 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
     }
     SH_STAGE_OUT(uint32_t, key[j], keys_out);
     SH_STAGE_OUT(uint32_t, (idx_in ? idx_in[i] : (uint32_t)i), idx_out);
+    // PL.pad: the columns are in arrival order and gathered through idx_in (payload
+    // carried by the last pass only)
+    const bool gather = PL.pad && idx_in;
     for (int c = 0; c < PL.n; c++) {
         if (PL.width[c] == 8) {
             const uint64_t* src = (const uint64_t*)PL.src[c];
-            SH_STAGE_OUT(uint64_t, src[i], PL.dst[c]);
+            SH_STAGE_OUT(uint64_t, src[gather ? idx_in[i] : i], PL.dst[c]);
         } else if (PL.width[c] == 4) {
             const uint32_t* src = (const uint32_t*)PL.src[c];
-            SH_STAGE_OUT(uint32_t, src[i], PL.dst[c]);
+            SH_STAGE_OUT(uint32_t, src[gather ? idx_in[i] : i], PL.dst[c]);
         } else {
             const uint8_t* src = (const uint8_t*)PL.src[c];
-            SH_STAGE_OUT(uint8_t, src[i], PL.dst[c]);
+            SH_STAGE_OUT(uint8_t, src[gather ? idx_in[i] : i], PL.dst[c]);
         }
     }
 #undef SH_STAGE_OUT
@@ -734,8 +737,19 @@ extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segmen
         // the final arrays
         shd_payload PL;
         memset(&PL, 0, sizeof(PL));
-        if (carry) {
+        static const bool last_carry = [] {
+            const char* e = getenv("SH_SEG_LASTCARRY");
+            return e && e[0] == '1';
+        }();
+        if (carry && last_carry) {
+            // the columns travel once, in the last pass, gathered by arrival index
+            if (ps == passes - 1) {
+                PL = *carry;
+                PL.pad = 1;
+            }
+        } else if (carry) {
             PL = *carry;
+            PL.pad = 0;
             const bool last = ps == passes - 1;
             const bool to_mid = ((passes - 1 - ps) & 1) != 0;
             for (int c = 0; c < carry->n; c++) {
