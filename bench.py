@@ -12,14 +12,17 @@ A step = one full pass of the matcher over the 100M events from fresh per-key
 state (radix segment -> per-key NFA advance -> ordered match placement), with
 the ordered match stream written to HBM.
 
-Multi-GPU (torchrun, C2): one process per GPU, strong scaling over ONE
-100M-event stream. Every rank ingests an arrival-contiguous slice; a step
-routes the slice's events to the ranks owning their symbols (mix32(key) %
-world, one RCCL all-to-all of packed records), runs the matcher on the owned
-events, sends every match row back to the rank holding its trigger event (a
-second all-to-all) and k-way merges the runs by trigger sequence
+Multi-GPU (torchrun; C2, C3, C5): one process per GPU, strong scaling over
+ONE stream. Every rank ingests an arrival-contiguous slice (cut at send() call
+boundaries); a step routes the slice's events to the ranks owning their keys
+(mix32(key) % world, one RCCL all-to-all of packed records), runs the matcher on
+the owned events, sends every match row back to the rank holding its trigger
+event (a second all-to-all) and k-way merges the runs by trigger sequence (C5:
+by the trigger's PartitionStreamReceiver run, whose rows stay query-major)
 (siddhi_amd/shard.py, include/siddhi_shard.h). value = the stream's events /
-the max-over-ranks step time. Other configs at N > 1: independent replicas.
+the max-over-ranks step time; the roofline is per GPU (all ranks' algorithmic
+matcher bytes / world / the slowest rank's matcher kernel time). C1 (no
+partition) runs replicas; C4 runs its streaming path per rank (main_c4).
 """
 import argparse
 import json
@@ -79,23 +82,22 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def workload(args, rank):
-    """Synthetic stream, compiled app, columns, bytes and checks of one config."""
+def workload(args):
+    """Synthetic stream, compiled app, columns, bytes and checks of one config
+    (one stream: at N > 1 the ranks split it by key, or replicate it for C1)."""
     from siddhi_amd import compiler, synth
     n, K = args.events, args.keys
     if args.config == "c5":
-        ts, card, amount, merchant = synth.txn_stream(n, K, args.rate, seed=synth.SEED + 5 + 7919 * rank)
+        ts, card, amount, merchant = synth.txn_stream(n, K, args.rate, seed=synth.SEED + 5)
         rules = synth.c5_rules(args.rules)
         text = synth.c5_query(rules)
         strings = compiler.StringDict()
         compiled = compiler.compile_app(text, strings)
 
-        def verify(oseq, ovals, oq):
+        def expected():
             sys.path.insert(0, os.path.join(HERE, "tests"))
             from c5_check import c5_expected
-            eseq, erule, evals = c5_expected(ts, card, amount, merchant, rules)
-            return bool(np.array_equal(oseq, eseq) and np.array_equal(oq, erule)
-                        and np.array_equal(ovals[:, :2], evals))
+            return c5_expected(ts, card, amount, merchant, rules)
 
         def cpu(s, idx=None):
             sys.path.insert(0, os.path.join(HERE, "tests"))
@@ -104,43 +106,42 @@ def workload(args, rank):
             run_columns_oracle(compiled, ts[ix], [card[ix], amount[ix], merchant[ix]], card[ix], batch=4096)
 
         return dict(
-            ts=ts, keys=card, cols=[card, amount, merchant], compiled=compiled, verify=verify, cpu=cpu,
+            ts=ts, keys=card, cols=[card, amount, merchant], compiled=compiled, expected=expected, cpu=cpu,
+            with_query=True, runs=True,
             b_event=20, b_match=20, cpu_sample=min(args.cpu_sample, 1_000_000), cpu_split=True,
             desc=f"C5: {args.rules} fraud rules `every e1=Txn[amount > A and merchant == M] -> "
                  f"e2=Txn[card == e1.card and amount > e1.amount * F] within W sec`, one partition (card of Txn)",
             key_name="cards_per_gpu", bytes_note="event: ts 8 + card 4 + amount 4 + merchant 4 = 20 B; "
             "match: seq 8 + query 4 + card 4 + amount 4 = 20 B")
     if args.config == "c1":
-        ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=1, seed=synth.SEED + 1 + 7919 * rank)
+        ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=1, seed=synth.SEED + 1)
         compiled = compiler.compile_app(synth.C1_QUERY)
 
-        def verify(oseq, ovals, oq):
+        def expected():
             sys.path.insert(0, os.path.join(HERE, "tests"))
             from c2_check import c2_expected
-            eseq, evals = c2_expected(ts, keys, price, vol)
-            return bool(len(oseq) == len(eseq) and np.array_equal(oseq, eseq) and np.array_equal(ovals, evals))
+            return c2_expected(ts, keys, price, vol) + (None,)
 
         def cpu(s):
             sys.path.insert(0, os.path.join(HERE, "tests"))
             from oracle_engine import run_columns_oracle
             run_columns_oracle(compiled, ts[:s], [keys[:s], price[:s], vol[:s]], None, batch=4096)
 
-        return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, verify=verify, cpu=cpu,
+        return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, expected=expected, cpu=cpu,
                     run_keys=np.zeros(n, np.int32), n_keys=1, b_event=24, b_match=28, cpu_sample=args.cpu_sample,
                     desc="C1: every e1[price>20] -> e2[symbol==e1.symbol and price>e1.price] within 1 sec, "
                          "no partition (BASELINE.json configs[0])", key_name="symbols_per_gpu",
                     bytes_note="event: ts 8 + symbol 4 + price 4 + volume 8 = 24 B; "
                                "match: seq 8 + symbol 4 + p1 4 + p2 4 + v2 8 = 28 B")
     ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=3 if args.config == "c3" else 2,
-                                              seed=synth.SEED + (3 if args.config == "c3" else 2) + 7919 * rank)
+                                              seed=synth.SEED + (3 if args.config == "c3" else 2))
     if args.config == "c3":
         compiled = compiler.compile_app(synth.C3_QUERY)
 
-        def verify(oseq, ovals, oq):
+        def expected():
             sys.path.insert(0, os.path.join(HERE, "tests"))
             from c3_check import c3_expected
-            eseq, evals = c3_expected(ts, keys, price)
-            return bool(len(oseq) == len(eseq) and np.array_equal(oseq, eseq) and np.array_equal(ovals, evals))
+            return c3_expected(ts, keys, price) + (None,)
 
         def cpu(s, idx=None):
             sys.path.insert(0, os.path.join(HERE, "tests"))
@@ -148,18 +149,17 @@ def workload(args, rank):
             ix = np.arange(s) if idx is None else idx
             run_stock_oracle(compiled, ts[ix], keys[ix], price[ix], vol[ix], batch=4096)
 
-        return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, verify=verify, cpu=cpu,
+        return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, expected=expected, cpu=cpu,
                     b_event=16, b_match=20, cpu_sample=args.cpu_sample, cpu_split=True,
                     desc="C3: every e1=S, e2=S[price>e1.price]+, e3=S[price<e2[last].price], "
                          "partition with (symbol of S)", key_name="keys_per_gpu",
                     bytes_note="event: ts 8 + symbol 4 + price 4 = 16 B; match: seq 8 + 3 x price 4 = 20 B")
     compiled = compiler.compile_app(synth.C2_QUERY)
 
-    def verify(oseq, ovals, oq):
+    def expected():
         sys.path.insert(0, os.path.join(HERE, "tests"))
         from c2_check import c2_expected
-        eseq, evals = c2_expected(ts, keys, price, vol)
-        return bool(len(oseq) == len(eseq) and np.array_equal(oseq, eseq) and np.array_equal(ovals, evals))
+        return c2_expected(ts, keys, price, vol) + (None,)
 
     def cpu(s, idx=None):
         sys.path.insert(0, os.path.join(HERE, "tests"))
@@ -167,7 +167,7 @@ def workload(args, rank):
         ix = np.arange(s) if idx is None else idx
         run_stock_oracle(compiled, ts[ix], keys[ix], price[ix], vol[ix], batch=4096)
 
-    return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, verify=verify, cpu=cpu,
+    return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, expected=expected, cpu=cpu,
                 b_event=24, b_match=28, cpu_sample=args.cpu_sample, cpu_split=True,
                 desc="C2: every e1[price>20] -> e2[symbol==e1.symbol and price>e1.price] within 1 sec, "
                      "partition with (symbol of StockStream)", key_name="symbols_per_gpu",
@@ -256,29 +256,89 @@ def main_c4(args, torch, dist, world, rank, dev):
         dist.destroy_process_group()
 
 
+def check_rows(W, oseq, ovals, oq, sel_range=None):
+    """the device's ordered rows == the vectorised restatement's (optionally only
+    the rows whose trigger events lie in [lo, hi): one rank's slice)"""
+    eseq, evals, eq = W["expected"]()
+    if sel_range is not None:
+        sel = (eseq >= sel_range[0]) & (eseq < sel_range[1])
+        eseq, evals = eseq[sel], evals[sel]
+        eq = eq[sel] if eq is not None else None
+    ok = len(oseq) == len(eseq) and np.array_equal(oseq, eseq) and np.array_equal(ovals[:, :evals.shape[1]], evals)
+    if eq is not None:
+        ok = ok and oq is not None and np.array_equal(oq, eq)
+    return bool(ok)
+
+
+def cpu_baseline(args, W, n):
+    """the oracle (C++ restatement of siddhi-core's processors) on a bounded sample
+    of the same stream, on this host's cores"""
+    if args.cpu_sample <= 0:
+        return None
+    s = min(W["cpu_sample"], n)
+    threads = args.cpu_threads or (min(16, os.cpu_count() or 1) if args.config == "c5" else 1)
+    if not W.get("cpu_split"):
+        threads = 1
+    log(f"CPU baseline on {s} events, {threads} thread(s)")
+    t1 = time.perf_counter()
+    if threads == 1:
+        W["cpu"](s)
+    else:
+        # partitions are independent (no timers): the sample's events split by
+        # key over threads, each with its own oracle instance (ctypes releases
+        # the GIL inside the restatement)
+        from concurrent.futures import ThreadPoolExecutor
+        part = W["keys"][:s] % threads
+        idxs = [np.flatnonzero(part == t) for t in range(threads)]
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(lambda ix: W["cpu"](s, ix), idxs))
+    cdt = time.perf_counter() - t1
+    return {"value": s / cdt, "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"first {s} events of the same {args.config.upper()} stream, send(Event[]) batches of "
+                      f"4096, C++ restatement of siddhi-core's processors (oracle/), {threads} thread(s)"
+                      + (" over key-disjoint sub-streams" if threads > 1 else "")}
+
+
+BATCH = 4096  # events per send(Event[]) call (SURVEY.md 8d)
+
+
 def main_sharded(args, torch, dist, world, rank, dev):
-    """C2 over `world` GPUs: one stream, key-sharded step (module docstring)."""
-    from siddhi_amd import compiler, shard, synth
+    """C2 / C3 / C5 over `world` GPUs: one stream, key-sharded step (module docstring)."""
+    from siddhi_amd import shard
     from siddhi_amd.device_run import DeviceRunner
-    n, K = args.events, args.keys
-    log(f"rank {rank}: generating the C2 stream ({n} events, {K} symbols), slice {rank}/{world}")
-    ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=2, seed=synth.SEED + 2)
-    b = shard.slice_bounds(n, world)
+    log(f"rank {rank}: generating the {args.config} stream, slice {rank}/{world}")
+    W = workload(args)
+    n = len(W["ts"])
+    K = W.get("n_keys", args.keys)
+    b = shard.slice_bounds(n, world, align=BATCH)
     lo, hi = b[rank], b[rank + 1]
-    d_ts = torch.from_numpy(ts[lo:hi].copy()).to(dev)
-    d_k = torch.from_numpy(keys[lo:hi].copy()).to(dev)
-    d_p = torch.from_numpy(price[lo:hi].copy()).to(dev)
-    d_v = torch.from_numpy(vol[lo:hi].copy()).to(dev)
-    compiled = compiler.compile_app(synth.C2_QUERY)
-    runner = DeviceRunner(compiled, device=str(dev))
+    d_ts = torch.from_numpy(W["ts"][lo:hi].copy()).to(dev)
+    d_cols = [torch.from_numpy(c[lo:hi].copy()).to(dev) for c in W["cols"]]
+    d_run = None
+    if W.get("runs"):
+        # PartitionStreamReceiver runs of the whole stream (a property of its
+        # send() calls), computed at ingest
+        d_run = torch.from_numpy(shard.stream_run_ids(W["keys"], BATCH)[lo:hi].copy()).to(dev)
+    runner = DeviceRunner(W["compiled"], device=str(dev))
     stream = torch.cuda.current_stream(dev)
+    wq = bool(W.get("with_query"))
+    kt_acc = {"ms": 0.0}
+
+    def matcher(t, k, c, nk, run=None):
+        r = runner.run(t, k, c, nk, stream=stream, with_query=wq, run_ids=run)
+        kt_acc["ms"] += runner.kernel_times()["total_ms"]
+        if not wq:
+            return r
+        m, s_, v, q = r
+        return m, s_, torch.cat([v, q[:m].to(torch.int64).view(-1, 1)], 1)
+
     comm = shard.BounceComm(world) if os.environ.get("SH_BENCH_SHARE_GPU") else None
-    step = shard.KeyShardedStep(world, rank, shard.HipShardOps(str(dev)),
-                                lambda t, k, c, nk: runner.run(t, k, c, nk, stream=stream), n_out=4, comm=comm)
+    step = shard.KeyShardedStep(world, rank, shard.HipShardOps(str(dev)), matcher,
+                                n_out=runner.n_out + (1 if wq else 0), comm=comm)
     rdev = "cpu" if comm is not None else dev  # device of the timing / count reductions
 
     def one():
-        return step.run(d_ts, d_k, [d_k, d_p, d_v], lo, K, key_attr=0)
+        return step.run(d_ts, d_cols[0], d_cols, lo, K, key_attr=0, run_ids=d_run)
 
     log("warmup")
     for _ in range(args.warmup):
@@ -286,6 +346,7 @@ def main_sharded(args, torch, dist, world, rank, dev):
     torch.cuda.synchronize(dev)
     dist.barrier()
     torch.cuda.synchronize(dev)
+    kt_acc["ms"] = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         seq, vals = one()
@@ -296,17 +357,27 @@ def main_sharded(args, torch, dist, world, rank, dev):
     dt_t = torch.tensor([dt], dtype=torch.float64, device=rdev)
     dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
-    m_t = torch.tensor([int(seq.numel())], dtype=torch.int64, device=rdev)
-    dist.all_reduce(m_t)
-    m = int(m_t.item())
+    # per rank: matches triggered by its slice, matches made here, events received,
+    # matcher kernel time per step
+    mine = torch.tensor([[float(seq.numel()), float(step.last["matches_here"]), float(sum(step.last["received"])),
+                          kt_acc["ms"] / args.steps]], dtype=torch.float64, device=rdev)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    allr = torch.cat(allr).cpu().numpy()
+    m = int(allr[:, 0].sum())
+    # roofline per GPU: the algorithmic bytes of every rank's matcher (events it
+    # received + matches it made) over the slowest rank's matcher kernel time
+    b_alg = W["b_event"] * allr[:, 2] + W["b_match"] * allr[:, 1]
+    kmax = float(allr[:, 3].max())
+    achieved = float(b_alg.sum()) / world / (kmax / 1000.0)
+    peak = 8.0e12
     verified = None
     if not args.no_verify and rank == 0:
         log("verifying rank 0's ordered rows against the vectorised restatement")
-        sys.path.insert(0, os.path.join(HERE, "tests"))
-        from c2_check import c2_expected
-        eseq, evals = c2_expected(ts, keys, price, vol)
-        sel = (eseq >= lo) & (eseq < hi)
-        verified = bool(np.array_equal(seq.cpu().numpy(), eseq[sel]) and np.array_equal(vals.cpu().numpy(), evals[sel]))
+        v = vals.cpu().numpy()
+        oq = v[:, -1].astype(np.int32) if wq else None
+        verified = check_rows(W, seq.cpu().numpy(), v[:, :-1] if wq else v, oq, (lo, hi))
+    cpu = cpu_baseline(args, W, n) if rank == 0 else None
     if rank == 0:
         print(json.dumps({
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
@@ -314,13 +385,17 @@ def main_sharded(args, torch, dist, world, rank, dev):
             "warmup": args.warmup, "ms_per_step": dt * 1000.0 / args.steps, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic",
             "nproc": os.cpu_count(),
-            "config": {"workload": "C2: every e1[price>20] -> e2[symbol==e1.symbol and price>e1.price] within 1 "
-                                   "sec, partition with (symbol of StockStream); one stream split by symbol",
-                       "events_total": n, "symbols": K, "rate_ev_per_ms": args.rate, "matches_total": m,
+            "config": {"workload": W["desc"] + "; one stream split by key", "events_total": n,
+                       W["key_name"].replace("_per_gpu", ""): args.keys, "rate_ev_per_ms": args.rate,
+                       "matches_total": m,
                        "parallelism": f"key-sharded x{world}: RCCL all-to-all route + return, k-way merge",
-                       "rank0_slice": [lo, hi], "rank0_step": step.last},
-            "roofline": None,
-            "cpu_baseline": None,
+                       "rank0_slice": [lo, hi], "rank0_step": step.last, "bytes": W["bytes_note"]},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",
+                         "frac": achieved / peak, "traffic": None,
+                         "kernel": "matcher step per GPU (every matcher kernel; HIP events on the launch stream): "
+                                   "algorithmic bytes of all ranks / world / slowest rank's matcher time",
+                         "kernels_ms_per_step_max": kmax, "algorithmic_bytes_per_rank": b_alg.tolist()},
+            "cpu_baseline": cpu,
             "verified_vs_restatement": verified}))
     runner.close()
     dist.destroy_process_group()
@@ -345,14 +420,14 @@ def main():
     dev = torch.device(f"cuda:{local}")
     if args.config == "c4":
         return main_c4(args, torch, dist, world, rank, dev)
-    if args.config == "c2" and world > 1:
+    if args.config in ("c2", "c3", "c5") and world > 1:
         return main_sharded(args, torch, dist, world, rank, dev)
 
     from siddhi_amd.device_run import DeviceRunner
 
     n, K = args.events, args.keys
     log(f"generating {args.config} workload: {n} events, {K} keys")
-    W = workload(args, rank)   # each rank: its own stream over its own key range (weak scaling)
+    W = workload(args)   # C1 at N > 1: every rank a replica of the one stream
     runner = DeviceRunner(W["compiled"], device=str(dev))
     # host -> device ingest of the input columns (outside the timed region:
     # the timed step starts from HBM-resident events)
@@ -366,7 +441,7 @@ def main():
     ingest_bytes = W["ts"].nbytes + sum(c.nbytes for c in W["cols"])
     K = W.get("n_keys", K)
     stream = torch.cuda.current_stream(dev)
-    with_q = args.config == "c5"
+    with_q = bool(W.get("with_query"))
 
     # --columns: the match stream as typed columns (sh_device_run.d_out_cols: seq 8
     # + symbol 4 + p1 4 + p2 4 + v2 8 bytes per match) instead of raw 8-byte rows;
@@ -427,7 +502,7 @@ def main():
             ovals_np = columns_to_raw([c.cpu().numpy() for c in ovals], runner.out_types)
         else:
             ovals_np = ovals.cpu().numpy()
-        verified = W["verify"](oseq.cpu().numpy(), ovals_np, oq.cpu().numpy() if oq is not None else None)
+        verified = check_rows(W, oseq.cpu().numpy(), ovals_np, oq.cpu().numpy() if oq is not None else None)
 
     # HBM bytes per step from the committed rocprofv3 PMC passes of this
     # workload (scripts/pmc_traffic.py), when they match the configuration
@@ -441,38 +516,16 @@ def main():
         except Exception:
             traffic = None
 
-    cpu = None
-    if rank == 0 and args.cpu_sample > 0:
-        s = min(W["cpu_sample"], n)
-        threads = args.cpu_threads or (min(16, os.cpu_count() or 1) if args.config == "c5" else 1)
-        if not W.get("cpu_split"):
-            threads = 1
-        log(f"CPU baseline on {s} events, {threads} thread(s)")
-        t1 = time.perf_counter()
-        if threads == 1:
-            W["cpu"](s)
-        else:
-            # partitions are independent (no timers): the sample's events split by
-            # key over threads, each with its own oracle instance (ctypes releases
-            # the GIL inside the restatement)
-            from concurrent.futures import ThreadPoolExecutor
-            part = W["keys"][:s] % threads
-            idxs = [np.flatnonzero(part == t) for t in range(threads)]
-            with ThreadPoolExecutor(threads) as ex:
-                list(ex.map(lambda ix: W["cpu"](s, ix), idxs))
-        cdt = time.perf_counter() - t1
-        cpu = {"value": s / cdt, "unit": "events/s", "cores": threads, "kind": "port",
-               "sample": f"first {s} events of the same {args.config.upper()} stream, send(Event[]) batches of "
-                         f"4096, C++ restatement of siddhi-core's processors (oracle/), {threads} thread(s)"
-                         + (" over key-disjoint sub-streams" if threads > 1 else "")}
+    cpu = cpu_baseline(args, W, n) if rank == 0 else None
 
     if rank == 0:
         line = {
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
-            # C2 at N > 1 splits the same 100M stream (main_sharded): strong
-            "scaling": "strong" if args.config in ("c1", "c2") else "weak",
+            # N = 1 here (C2 / C3 / C5 at N > 1 split the one stream: main_sharded);
+            # C1 at N > 1 runs replicas of its unpartitioned stream
+            "scaling": "weak" if args.config == "c1" and world > 1 else "strong",
             "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic",
             "nproc": os.cpu_count(),
             "ingest": {"bytes": ingest_bytes, "ms": ingest_s * 1000.0, "GBps": ingest_bytes / ingest_s / 1e9,

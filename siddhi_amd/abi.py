@@ -74,7 +74,11 @@ class sh_device_run(C.Structure):
                 ("n_keys", C.c_int32), ("batch_events", C.c_int32), ("d_cols", C.POINTER(C.c_void_p)),
                 ("out_capacity", C.c_int64), ("d_out_seq", C.c_void_p),
                 ("d_out_values", C.c_void_p), ("out_count", C.c_int64), ("stream", C.c_void_p),
-                ("d_out_query", C.c_void_p), ("d_out_cols", C.POINTER(C.c_void_p))]
+                ("d_out_query", C.c_void_p), ("version", C.c_int32), ("pad", C.c_int32),
+                ("d_out_cols", C.POINTER(C.c_void_p)), ("d_run", C.c_void_p)]
+
+
+SH_DEVICE_RUN_V2 = 2
 
 
 class sh_kernel_times(C.Structure):

@@ -361,6 +361,7 @@ struct sh_handle {
     DevBuf w_ts, w_stream, w_row, w_key, w_keys_a, w_keys_b, w_idx_a, w_idx_b, w_hist, w_scan, w_seg;
     DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls, w_oq, w_inv;
     bool dev_want_query = false;  // sh_run_device asked for d_out_query
+    const uint32_t* dev_run_ids = nullptr;  // sh_run_device's d_run while it runs the general engine
     DevBuf v_sts, v_mpos, v_flag, v_cnts, v_mid_ts, v_dir;
     DevBuf v_scol[32], v_mid[32];
     int64_t tmp_cap = 0;
@@ -1475,6 +1476,8 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     E.batch_events = batch_events;
     E.sts = sorted_cols ? h->v_sts.as<int64_t>() : nullptr;
     E.sorted_rows = sorted_cols ? 1 : 0;
+    E.pad = 0;
+    E.run = fresh ? h->dev_run_ids : nullptr;
     for (int attempt = 0; attempt < 64; attempt++) {
         const size_t kw = (size_t)h->T->key_words;
         if (!fresh) {
@@ -2077,7 +2080,7 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
         if (sorted) {
             if (h->r_run.ensure_fresh((size_t)n * 12)) return fail(h, SH_E_OOM, "run ids");
             uint32_t* f = h->r_run.as<uint32_t>();
-            if (shr_run_ids(run->d_keys, n, batch, f, f + n, f + 2 * n, h->w_scan.as<uint32_t>(), st))
+            if (shr_run_ids(run->d_keys, run->d_run, n, batch, f, f + n, f + 2 * n, h->w_scan.as<uint32_t>(), st))
                 return fail(h, SH_E_HIP, "run id launch failed");
             flags = f;
             rid = f + n;
@@ -2332,8 +2335,10 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
         int64_t rows = 0;
         h->times = sh_kernel_times{};
         h->dev_want_query = run->d_out_query != nullptr;
+        h->dev_run_ids = run->d_run;
         rc = nf_process(h, B, nkeys, cols, run->d_out_seq, run->d_out_values, run->out_capacity, &rows, true,
                         run->batch_events, getenv("SH_NFA_GATHER") ? nullptr : run);
+        h->dev_run_ids = nullptr;
         run->out_count = rows;
         if (rc == SH_OK && run->d_out_query && rows > 0) {
             hipMemcpyAsync(run->d_out_query, h->w_oq.p, rows * 4, hipMemcpyDeviceToDevice, h->stream);
@@ -2451,8 +2456,22 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
     return rc;
 }
 
-int sh_run_device(sh_handle* h, sh_device_run* run) {
-    if (!h || !run) return SH_E_INVALID_ARG;
+static int run_device_cols(sh_handle* h, sh_device_run* run);
+
+int sh_run_device(sh_handle* h, sh_device_run* user) {
+    if (!h || !user) return SH_E_INVALID_ARG;
+    // the V2 fields are read only from a struct that says it has them
+    sh_device_run r = *user;
+    if (r.version != SH_DEVICE_RUN_V2) {
+        r.d_out_cols = nullptr;
+        r.d_run = nullptr;
+    }
+    const int rc = run_device_cols(h, &r);
+    user->out_count = r.out_count;
+    return rc;
+}
+
+static int run_device_cols(sh_handle* h, sh_device_run* run) {
     if (!run->d_out_cols) return run_device_impl(h, run);
     // typed columns: one output type per select position across the app's queries
     int32_t w[SHB_MAX_OUT];

@@ -2199,7 +2199,8 @@ struct NfLane {
 
 // ------------------------------------------------------------------ segment driver
 // Events interface (key-segment position k): ts(k), row(k), seq(k), stream(k),
-// local(k) = arrival index inside the flushed batch set, batch(k) = send() call id.
+// local(k) = arrival index inside the flushed batch set, batch(k) = send() call id,
+// joins(e, k) = position e continues the same-key run started at k.
 //
 // PartitionStreamReceiver.receive(Event[]) (core/partition/PartitionStreamReceiver.java:176-272)
 // splits a send() call into consecutive same-key runs, lazily inits the key's
@@ -2215,7 +2216,7 @@ NF_HD void nf_process_segment(NfLane<Sink>& L, const Events& ev, int64_t beg, in
     int64_t k = beg;
     while (k < end && !L.err) {
         int64_t e = k + 1;
-        while (e < end && ev.local(e) == ev.local(e - 1) + 1 && ev.batch(e) == ev.batch(k)) e++;
+        while (e < end && ev.joins(e, k)) e++;
         L.tag_index = ev.local(k);
         L.ordinal = 0;
         if (T->partitioned && !(L.kb[0] & 1ull)) {

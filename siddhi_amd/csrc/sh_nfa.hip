@@ -59,6 +59,7 @@ struct DevEvents {
     int64_t batch_events;
     const int64_t* sts;
     int32_t sorted_rows;
+    const uint32_t* run;    // caller's run ids by arrival index (NULL: from adjacency and the send() call)
     __device__ uint32_t at(int64_t k) const { return perm ? perm[k] : (uint32_t)k; }
 };
 // the Events interface of nf_process_segment / NfLane::receive
@@ -76,6 +77,11 @@ struct DevEv {
     __device__ uint32_t local(int64_t k) const { return E->at(k); }
     __device__ uint32_t batch(int64_t k) const {
         return E->bid ? E->bid[E->at(k)] : (E->batch_events ? (uint32_t)(E->at(k) / E->batch_events) : 0u);
+    }
+    // key-segment position e continues the run that starts at k (e - 1 does)
+    __device__ bool joins(int64_t e, int64_t k) const {
+        if (E->run) return E->run[E->at(e)] == E->run[E->at(k)];
+        return local(e) == local(e - 1) + 1 && batch(e) == batch(k);
     }
 };
 
@@ -540,6 +546,7 @@ extern "C" int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, 
     E.perm = ev->perm;
     E.seq_base = ev->seq_base;
     E.batch_events = ev->batch_events;
+    E.run = ev->run;
     E.sts = ev->sts;
     E.sorted_rows = ev->sorted_rows;
     if (max_segments < 1) max_segments = 1;
@@ -559,6 +566,7 @@ extern "C" int nfd_seq3(const nf_table* dT, const nf_cols* dC, const nfd_events*
     E.perm = ev->perm;
     E.seq_base = ev->seq_base;
     E.batch_events = ev->batch_events;
+    E.run = ev->run;
     E.sts = ev->sts;
     E.sorted_rows = ev->sorted_rows;
     if (max_segments < 1) max_segments = 1;

@@ -28,6 +28,7 @@ struct nfd_events {
     const int64_t* sts;            // timestamps in key-segment order (NULL: gather ts through perm)
     int32_t sorted_rows;           // 1: column rows are key-segment positions (columns carried by the segment)
     int32_t pad;
+    const uint32_t* run;           // caller's PartitionStreamReceiver run per arrival index (sh_device_run.d_run), NULL: none
 };
 
 struct nfd_cand {

@@ -42,9 +42,10 @@ int shr_write(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, in
               const shd_cols* dC, const uint32_t* cnt, const uint32_t* off, uint32_t* rec_p, uint32_t* rec_q,
               uint32_t* rec_r, void* stream);
 // PartitionStreamReceiver runs of an arrival-order key array: flags[i] (run
-// start), rid[i] (exclusive scan of flags), rfirst[run] (first arrival index)
-int shr_run_ids(const int32_t* akeys, int64_t n, int64_t batch, uint32_t* flags, uint32_t* rid, uint32_t* rfirst,
-                uint32_t* scan_tmp, void* stream);
+// start), rid[i] (exclusive scan of flags), rfirst[run] (first arrival index);
+// run_ids (may be NULL): the caller's run of every event (sh_device_run.d_run)
+int shr_run_ids(const int32_t* akeys, const uint32_t* run_ids, int64_t n, int64_t batch, uint32_t* flags,
+                uint32_t* rid, uint32_t* rfirst, uint32_t* scan_tmp, void* stream);
 // order keys of the records: packed -> k0 = rule << qbits | offset in run,
 // k1 = run; else k0 = offset in run, k1 = rule, k2 = run
 int shr_keys(const uint32_t* rec_q, const uint32_t* rec_r, int64_t m, const uint32_t* perm, const uint32_t* flags,

@@ -147,11 +147,17 @@ __global__ void __launch_bounds__(RTPB) k_rules_scan(const shr_table* __restrict
 
 // start of a PartitionStreamReceiver run: the first keyed event of a send() call,
 // or a keyed event whose key differs from the previous keyed event of the call
-__global__ void k_run_flags(const int32_t* __restrict__ akeys, int64_t n, int64_t batch, uint32_t* __restrict__ flags) {
+// (run_ids: the caller's runs, a new id starts a run)
+__global__ void k_run_flags(const int32_t* __restrict__ akeys, const uint32_t* __restrict__ run_ids, int64_t n,
+                            int64_t batch, uint32_t* __restrict__ flags) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t k = akeys[i];
         uint32_t f = 0;
-        if (k >= 0) {
+        if (k >= 0 && run_ids) {
+            int64_t j = i - 1;
+            while (j >= 0 && akeys[j] < 0) j--;
+            f = (j < 0 || run_ids[j] != run_ids[i]) ? 1u : 0u;
+        } else if (k >= 0) {
             const int64_t b0 = batch > 0 ? i - i % batch : 0;
             int64_t j = i - 1;
             while (j >= b0 && akeys[j] < 0) j--;
@@ -249,10 +255,10 @@ extern "C" int shr_write(const shr_table* dT, const int64_t* sts, const uint32_t
     return rules_ok();
 }
 
-extern "C" int shr_run_ids(const int32_t* akeys, int64_t n, int64_t batch, uint32_t* flags, uint32_t* rid,
-                           uint32_t* rfirst, uint32_t* scan_tmp, void* stream) {
+extern "C" int shr_run_ids(const int32_t* akeys, const uint32_t* run_ids, int64_t n, int64_t batch, uint32_t* flags,
+                           uint32_t* rid, uint32_t* rfirst, uint32_t* scan_tmp, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_run_flags, dim3(rgrid(n)), dim3(RTPB), 0, st, akeys, n, batch, flags);
+    hipLaunchKernelGGL(k_run_flags, dim3(rgrid(n)), dim3(RTPB), 0, st, akeys, run_ids, n, batch, flags);
     int rc = shd_exclusive_scan(flags, rid, n, scan_tmp, stream);
     if (rc) return rc;
     hipLaunchKernelGGL(k_run_first, dim3(rgrid(n)), dim3(RTPB), 0, st, (const uint32_t*)flags, (const uint32_t*)rid,

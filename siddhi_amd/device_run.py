@@ -42,9 +42,11 @@ class DeviceRunner:
         self._col_cap = 0
 
     def run(self, ts, keys, cols, n_keys, out_capacity=None, stream=None, batch_events=4096, with_query=False,
-            columns=False):
+            columns=False, run_ids=None):
         """ts/keys/cols: device tensors (int64 / int32 / stream attribute order);
         the events arrive as send(Event[]) calls of `batch_events`.
+        run_ids (optional int32/uint32 device tensor): the PartitionStreamReceiver
+        run of every event (sh_device_run.d_run), for a key shard of a stream.
         Returns (n_matches, out_seq[n], out_values[n, n_out]) as device tensors,
         plus out_query[n] (emitting query index) when `with_query`. With
         `columns`, out_values is a list of typed columns (sh_device_run.d_out_cols:
@@ -66,6 +68,8 @@ class DeviceRunner:
                 self.out_vals = torch.empty(self._out_cap * self.n_out, dtype=torch.int64, device=self.device)
             cp = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
             r = abi.sh_device_run()
+            r.version = abi.SH_DEVICE_RUN_V2
+            r.d_run = run_ids.data_ptr() if run_ids is not None else None
             r.n = n
             r.d_ts = ts.data_ptr()
             r.d_keys = keys.data_ptr()

@@ -51,9 +51,29 @@ def split(keys, world):
     return [np.nonzero(s == r)[0] for r in range(world)]
 
 
-def slice_bounds(n_total, world):
-    """arrival-contiguous ingest slices: rank r holds [b[r], b[r+1])"""
-    return [n_total * r // world for r in range(world + 1)]
+def slice_bounds(n_total, world, align=1):
+    """arrival-contiguous ingest slices: rank r holds [b[r], b[r+1]); align: cut
+    only at multiples of it (the send() call size, so no call spans two slices)"""
+    units = (n_total + align - 1) // align
+    return [min(n_total, (units * r // world) * align) for r in range(world + 1)]
+
+
+def stream_run_ids(keys, batch):
+    """PartitionStreamReceiver runs of an arrival-ordered stream sent as
+    send(Event[]) calls of `batch` events (core/partition/PartitionStreamReceiver.java:176-216:
+    a run is the consecutive same-key events of one call): per event, the arrival
+    index of its run's first event (uint32, non-decreasing). A key shard of the
+    stream keeps these ids, so its matcher sees the runs the whole stream had
+    (sh_device_run.d_run)."""
+    keys = np.asarray(keys)
+    n = len(keys)
+    start = np.ones(n, bool)
+    if n > 1:
+        start[1:] = keys[1:] != keys[:-1]
+    if batch > 0:
+        start[::batch] = True
+    idx = np.where(start, np.arange(n, dtype=np.int64), 0)
+    return np.maximum.accumulate(idx).astype(np.uint32).view(np.int32)
 
 
 def _width(t):
@@ -202,44 +222,65 @@ class KeyShardedStep:
         self.comm = comm if comm is not None else TorchComm(world)
         self.last = {}
 
-    def run(self, ts, keys, cols, seq0, n_keys, key_attr=None):
+    def run(self, ts, keys, cols, seq0, n_keys, key_attr=None, run_ids=None):
         """ts / keys / cols: this rank's ingest slice (arrival order), seq0 its
         first global sequence number; key_attr: index of the attribute column
-        that holds the partition key ids (then `keys` travels once). Returns
-        (seq[m], values[m, n_out]) of the rows triggered by the slice's events,
-        in the reference's order."""
+        that holds the partition key ids (then `keys` travels once); run_ids
+        (optional, stream_run_ids of the slice): travel with the events and reach
+        the matcher as `run=` (apps whose output order depends on the
+        PartitionStreamReceiver runs, e.g. several queries in one partition).
+        Returns (seq[m], values[m, n_out]) of the rows triggered by the slice's
+        events, in the reference's order."""
         dev = ts.device
         world = self.world
-        # 1. route + pack (columns: ts, [keys,] then the attribute columns)
+        # 1. route + pack (columns: ts, [keys,] then the attribute columns[, run ids])
         pos, send_counts = self.ops.route(keys, world)
-        allc = [ts] + ([] if key_attr is not None else [keys]) + list(cols)
+        allc = [ts] + ([] if key_attr is not None else [keys]) + list(cols) + ([run_ids] if run_ids is not None else [])
         rec, stride = self.ops.pack(pos, allc, seq0)
         # 2. shuffle
         recv_counts = self.comm.counts(send_counts, dev)
         rrec = self.comm.exchange(rec, send_counts, recv_counts, stride)
         n_recv = sum(recv_counts)
         ucols, gseq = self.ops.unpack(rrec, n_recv, allc)
+        r_run = None
+        if run_ids is not None:
+            r_run, ucols = ucols[-1], ucols[:-1]
         if key_attr is not None:
             r_ts, r_cols = ucols[0], ucols[1:]
             r_keys = r_cols[key_attr]
         else:
             r_ts, r_keys, r_cols = ucols[0], ucols[1], ucols[2:]
         # 3. match on the owned keys' events
-        m, oseq, ovals = self.matcher(r_ts, r_keys, r_cols, n_keys)
+        if r_run is None:
+            m, oseq, ovals = self.matcher(r_ts, r_keys, r_cols, n_keys)
+        else:
+            m, oseq, ovals = self.matcher(r_ts, r_keys, r_cols, n_keys, run=r_run)
         # 4. rows back to the ranks holding their trigger events
         src_off = [0]
         for c in recv_counts:
             src_off.append(src_off[-1] + c)
         oseq = oseq[:m].contiguous()
         ovals = ovals[:m].contiguous().view(-1)
+        # merge key: the trigger sequence, or with run ids the trigger's run (rows of
+        # one run stay in the matcher's order, e.g. query-major inside the run, and
+        # a run lives on one owner; its rows are grouped by source rank as long as
+        # the ingest slices cut the stream at send() call boundaries)
+        mkey = r_run[oseq].to(oseq.dtype) if r_run is not None else None
         row_counts = self.ops.rows_home(oseq, m, 0, gseq, src_off, world)
         back_counts = self.comm.counts(row_counts, dev)
+        n_val = self.n_out
+        if mkey is not None:
+            import torch
+            ovals = torch.cat([oseq.view(m, 1), ovals.view(m, self.n_out)], 1).contiguous().view(-1)
+            oseq, n_val = mkey.contiguous(), self.n_out + 1
         hseq = self.comm.exchange(oseq, row_counts, back_counts, 1)
-        hvals = self.comm.exchange(ovals, row_counts, back_counts, self.n_out)
-        # 5. k-way merge of the owners' runs by trigger sequence
+        hvals = self.comm.exchange(ovals, row_counts, back_counts, n_val)
+        # 5. k-way merge of the owners' runs by trigger sequence (or run)
         run_off = [0]
         for c in back_counts:
             run_off.append(run_off[-1] + c)
-        seq, vals = self.ops.merge(hseq, hvals, self.n_out, run_off)
+        seq, vals = self.ops.merge(hseq, hvals, n_val, run_off)
+        if mkey is not None:
+            seq, vals = vals[:, 0].contiguous(), vals[:, 1:].contiguous()
         self.last = dict(sent=send_counts, received=recv_counts, matches_here=m, rows_home=run_off[-1])
         return seq, vals

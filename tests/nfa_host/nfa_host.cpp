@@ -45,6 +45,7 @@ struct SegEvents {
     int stream(int64_t k) const { return (*v)[k].stream; }
     uint32_t local(int64_t k) const { return (*v)[k].local; }
     uint32_t batch(int64_t k) const { return (*v)[k].batch; }
+    bool joins(int64_t e, int64_t k) const { return local(e) == local(e - 1) + 1 && batch(e) == batch(k); }
 };
 
 struct OutRow {

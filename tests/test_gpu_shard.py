@@ -117,29 +117,57 @@ class _ThreadComm:
         return V()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_step_virtual_ranks_equal_single_stream(world):
-    import torch
+def _shard_case(config):
+    """(compiled, ts, keys, cols, n_keys, expected(), with_query, runs) per config"""
+    from siddhi_amd import compiler, synth
+    if config == "c5":
+        from c5_check import c5_expected
+        ts, card, amount, merchant = synth.txn_stream(2_000_000, 20_000, 100)
+        rules = synth.c5_rules(200)
+        return (compiler.compile_app(synth.c5_query(rules)), ts, card, [card, amount, merchant], 20_000,
+                lambda: c5_expected(ts, card, amount, merchant, rules), True, True)
+    ts, k, p, v = synth.stock_stream(2_000_000, 100_000 if config == "c3" else 10_000,
+                                     1000 if config == "c3" else 100)
+    if config == "c3":
+        from c3_check import c3_expected
+        return (compiler.compile_app(synth.C3_QUERY), ts, k, [k, p, v], 100_000,
+                lambda: c3_expected(ts, k, p) + (None,), False, False)
     from c2_check import c2_expected
-    from siddhi_amd import compiler, shard, synth
+    return (compiler.compile_app(synth.C2_QUERY), ts, k, [k, p, v], 10_000,
+            lambda: c2_expected(ts, k, p, v) + (None,), False, False)
+
+
+@pytest.mark.parametrize("config", ["c2", "c3", "c5"])
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_step_virtual_ranks_equal_single_stream(world, config):
+    import torch
+    from siddhi_amd import shard
     from siddhi_amd.device_run import DeviceRunner
-    n, K = 2_000_000, 10_000
-    ts, k, p, v = synth.stock_stream(n, K, 100)
-    b = shard.slice_bounds(n, world)
+    ca, ts, k, cols, K, expected, wq, runs = _shard_case(config)
+    n = len(ts)
+    b = shard.slice_bounds(n, world, align=4096)
+    rid = shard.stream_run_ids(k, 4096) if runs else None
     comm = _ThreadComm(world)
-    ca = compiler.compile_app(synth.C2_QUERY)
     out = [None] * world
     errs = []
 
     def rank_main(r):
         try:
             runner = DeviceRunner(ca)
-            step = shard.KeyShardedStep(world, r, _ops(),
-                                        lambda t, kk, cc, nk: runner.run(t, kk, cc, nk), n_out=4,
+
+            def matcher(t, kk, cc, nk, run=None):
+                res = runner.run(t, kk, cc, nk, with_query=wq, run_ids=run)
+                if not wq:
+                    return res
+                m, s_, v, q = res
+                return m, s_, torch.cat([v, q[:m].to(torch.int64).view(-1, 1)], 1)
+
+            step = shard.KeyShardedStep(world, r, _ops(), matcher, n_out=runner.n_out + (1 if wq else 0),
                                         comm=comm.view(r))
             lo, hi = b[r], b[r + 1]
-            dev = [torch.from_numpy(a[lo:hi].copy()).cuda() for a in (ts, k, p, v)]
-            seq, vals = step.run(dev[0], dev[1], [dev[1], dev[2], dev[3]], lo, K, key_attr=0)
+            dev = [torch.from_numpy(a[lo:hi].copy()).cuda() for a in [ts] + cols]
+            d_run = torch.from_numpy(rid[lo:hi].copy()).cuda() if rid is not None else None
+            seq, vals = step.run(dev[0], dev[1], dev[1:], lo, K, key_attr=0, run_ids=d_run)
             torch.cuda.synchronize()
             out[r] = (seq.cpu().numpy(), vals.cpu().numpy(), step.last)
             runner.close()
@@ -153,10 +181,13 @@ def test_sharded_step_virtual_ranks_equal_single_stream(world):
     for t in th:
         t.join(timeout=300)
     assert not errs, errs
-    eseq, evals = c2_expected(ts, k, p, v)
+    eseq, evals, eq = expected()
     mseq = np.concatenate([o[0] for o in out])
     mvals = np.concatenate([o[1] for o in out])
     assert all(o[2]["matches_here"] > 0 for o in out)
     assert len(mseq) == len(eseq) > 0
     assert np.array_equal(mseq, eseq)
-    assert np.array_equal(mvals, evals)
+    if wq:
+        assert np.array_equal(mvals[:, -1], eq)
+        mvals = mvals[:, :-1]
+    assert np.array_equal(mvals[:, :evals.shape[1]], evals)

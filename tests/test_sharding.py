@@ -71,35 +71,68 @@ class CpuShardOps:
         return torch.from_numpy(s[order].copy()), torch.from_numpy(v[order].copy())
 
 
-def _oracle_matcher(compiled):
+def _oracle_matcher(compiled, with_query=False):
+    """the CPU oracle on the received events: send() calls cut at the run ids when
+    given (each PartitionStreamReceiver run of the whole stream its own call, which
+    keeps the reference's (run, query, event) order), else calls of 4096"""
     sys.path.insert(0, HERE)
-    from oracle_engine import run_stock_oracle
+    from oracle_engine import OracleEngine
 
-    def match(ts, keys, cols, n_keys):
-        seq, _, vals, _ = run_stock_oracle(compiled, ts.numpy(), keys.numpy(), cols[0].numpy(), cols[1].numpy())
-        return len(seq), torch.from_numpy(seq.astype(np.int64)), torch.from_numpy(vals)
+    def match(ts, keys, cols, n_keys, run=None):
+        ts, keys = ts.numpy(), keys.numpy()
+        cols = [c.numpy() for c in cols]
+        n = len(ts)
+        if run is not None:
+            r = run.numpy()
+            cuts = np.concatenate([[0], np.flatnonzero(r[1:] != r[:-1]) + 1, [n]])
+        else:
+            cuts = np.concatenate([np.arange(0, n, 4096), [n]])
+        eng = OracleEngine(compiled)
+        eng.start()
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            if b > a:
+                eng.send(0, ts[a:b], [np.ascontiguousarray(c[a:b]) for c in cols], [None] * len(cols),
+                         np.ascontiguousarray(keys[a:b]), int(a))
+        out = eng.drain()
+        eng.close()
+        vals = out["values"]
+        if with_query:
+            vals = np.concatenate([vals, out["query"].astype(np.int64)[:, None]], 1)
+        return len(out["seq"]), torch.from_numpy(out["seq"].astype(np.int64)), torch.from_numpy(vals)
     return match
 
 
-def _stream():
-    from siddhi_amd import synth
-    return synth.stock_stream(60_000, 300, 20)
+C5_TEST_RULES = 40
 
 
-def _worker(rank, world, port, result_q):
+def _case(config):
+    """(compiled, ts, keys, cols, n_keys, n_out, with_query, run ids?) of a small stream"""
+    from siddhi_amd import compiler, synth
+    if config == "c5":
+        ts, card, amount, merchant = synth.txn_stream(60_000, 300, 20, n_merchants=20)
+        rules = synth.c5_rules(C5_TEST_RULES, merchants=20, within=(1, 3), amount=(20.0, 200.0))
+        ca = compiler.compile_app(synth.c5_query(rules))
+        return ca, ts, card, [card, amount, merchant], 300, 2, True, True
+    ts, k, p, v = synth.stock_stream(60_000, 300, 20)
+    ca = compiler.compile_app(synth.C3_QUERY if config == "c3" else synth.C2_QUERY)
+    return ca, ts, k, [k, p, v], 300, 3 if config == "c3" else 4, False, False
+
+
+def _worker(rank, world, port, config, result_q):
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from siddhi_amd import compiler, shard, synth
-    ts, k, p, v = _stream()
-    b = shard.slice_bounds(len(ts), world)
+    from siddhi_amd import shard
+    ca, ts, k, cols, K, n_out, wq, runs = _case(config)
+    b = shard.slice_bounds(len(ts), world, align=4096)
     lo, hi = b[rank], b[rank + 1]
-    ca = compiler.compile_app(synth.C2_QUERY)
-    step = shard.KeyShardedStep(world, rank, CpuShardOps(), _oracle_matcher(ca), n_out=4)
-    seq, vals = step.run(torch.from_numpy(ts[lo:hi].copy()), torch.from_numpy(k[lo:hi].copy()),
-                         [torch.from_numpy(p[lo:hi].copy()), torch.from_numpy(v[lo:hi].copy())], lo, 300)
+    rid = shard.stream_run_ids(k, 4096) if runs else None
+    step = shard.KeyShardedStep(world, rank, CpuShardOps(), _oracle_matcher(ca, wq), n_out=n_out + (1 if wq else 0))
+    t = lambda a: torch.from_numpy(a[lo:hi].copy())  # noqa: E731
+    seq, vals = step.run(t(ts), t(k), [t(c) for c in cols], lo, K, key_attr=0,
+                         run_ids=t(rid) if rid is not None else None)
     parts = [None] * world
     dist.all_gather_object(parts, (seq.numpy(), vals.numpy(), step.last))
     if rank == 0:
@@ -108,28 +141,53 @@ def _worker(rank, world, port, result_q):
     dist.destroy_process_group()
 
 
-def test_sharded_step_world2_equals_single_process():
-    from oracle_engine import run_stock_oracle
-    from siddhi_amd import compiler, synth
+@pytest.mark.parametrize("config", ["c2", "c3", "c5"])
+def test_sharded_step_world2_equals_single_process(config):
+    """C2, C3 and C5 (1 stream, world 2): the ranks' outputs concatenated equal the
+    single-process oracle's ordered match stream (C5 with its query column; its
+    rows leave each run query-major, so the step carries the run ids)."""
+    from oracle_engine import OracleEngine
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 1000
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    port = 29500 + (os.getpid() + hash(config)) % 1000
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, config, q)) for r in range(2)]
     for pr in procs:
         pr.start()
     parts = q.get(timeout=300)
     for pr in procs:
         pr.join(timeout=120)
         assert pr.exitcode == 0
-    ts, k, p, v = _stream()
-    seq, _, vals, _ = run_stock_oracle(compiler.compile_app(synth.C2_QUERY), ts, k, p, v)
+    ca, ts, k, cols, K, n_out, wq, runs = _case(config)
+    eng = OracleEngine(ca)
+    eng.start()
+    for b0 in range(0, len(ts), 4096):
+        b1 = min(len(ts), b0 + 4096)
+        eng.send(0, ts[b0:b1], [np.ascontiguousarray(c[b0:b1]) for c in cols], [None] * len(cols),
+                 np.ascontiguousarray(k[b0:b1]), b0)
+    ref = eng.drain()
+    eng.close()
+    want = ref["values"]
+    if wq:
+        want = np.concatenate([want, ref["query"].astype(np.int64)[:, None]], 1)
     mseq = np.concatenate([x[0] for x in parts])
     mvals = np.concatenate([x[1] for x in parts])
     # both ranks shuffled events both ways and matched
     assert all(min(x[2]["sent"]) > 0 and x[2]["matches_here"] > 0 for x in parts)
-    assert len(mseq) == len(seq) > 0
-    assert np.array_equal(mseq, seq.astype(np.int64))
-    assert np.array_equal(mvals, vals)
+    assert len(mseq) == len(ref["seq"]) > 0
+    assert np.array_equal(mseq, ref["seq"].astype(np.int64))
+    assert np.array_equal(mvals, want)
+    if config == "c5":
+        # the stream has same-card runs longer than one event, and the order inside
+        # them is not the trigger order (what the run-keyed merge must keep)
+        assert not np.all(np.diff(ref["seq"].astype(np.int64)) >= 0)
+
+
+def test_stream_run_ids():
+    from siddhi_amd import shard
+    k = np.array([5, 5, 7, 7, 7, 5, 5, 5, 9], np.int32)
+    assert shard.stream_run_ids(k, 4).tolist() == [0, 0, 2, 2, 4, 5, 5, 5, 8]
+    assert shard.stream_run_ids(k, 0).tolist() == [0, 0, 2, 2, 2, 5, 5, 5, 8]
+    assert shard.slice_bounds(10_000, 3, align=4096) == [0, 4096, 8192, 10_000]
 
 
 @pytest.mark.parametrize("world", [1, 3])
