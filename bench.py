@@ -97,7 +97,8 @@ def workload(args):
         def expected():
             sys.path.insert(0, os.path.join(HERE, "tests"))
             from c5_check import c5_expected
-            return c5_expected(ts, card, amount, merchant, rules)
+            eseq, erule, evals = c5_expected(ts, card, amount, merchant, rules)
+            return eseq, evals, erule
 
         def cpu(s, idx=None):
             sys.path.insert(0, os.path.join(HERE, "tests"))

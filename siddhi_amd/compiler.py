@@ -52,11 +52,17 @@ class UnsupportedQuery(Exception):
 # ----------------------------------------------------------------- lexer
 _TOKEN_RE = re.compile(r"""
     (?P<ws>\s+|--[^\n]*|/\*.*?\*/)
-  | (?P<str>'(?:[^'\\]|\\.)*'|"(?:[^"\\]|\\.)*")
+  | (?P<str>"{3}.*?"{3}|'[^'"\x00-\x1f]*'|"[^"\x00-\x1f]*")
   | (?P<num>(?:\d+\.\d*|\.\d+|\d+)(?:[eE][-+]?\d+)?[lLfFdD]?)
   | (?P<id>[A-Za-z_][A-Za-z0-9_]*)
   | (?P<op>->|==|!=|>=|<=|[-+*/%<>=(),;\[\].@:#!?{}])
 """, re.VERBOSE | re.DOTALL)
+
+
+def _str_text(lit: str) -> str:
+    """STRING_LITERAL text (SiddhiQL.g4:854-860): the characters between the quotes,
+    verbatim -- the grammar has no escape sequences"""
+    return lit[3:-3] if lit.startswith('"""') else lit[1:-1]
 
 
 @dataclass
@@ -372,7 +378,7 @@ class Parser:
                     if tk.kind != "str":
                         self.err("expected a range label string")
                     self.next()
-                    ranges.append((e, bytes(tk.text[1:-1], "utf-8").decode("unicode_escape")))
+                    ranges.append((e, _str_text(tk.text)))
                     if self.kw("or"):
                         self.next()
                         e = self.expr()
@@ -739,7 +745,7 @@ class Parser:
             return self.number(tk.text)
         if tk.kind == "str":
             self.next()
-            return EConst(STRING, bytes(tk.text[1:-1], "utf-8").decode("unicode_escape"))
+            return EConst(STRING, _str_text(tk.text))
         if tk.kind == "id":
             low = tk.text.lower()
             if low in ("true", "false"):
@@ -1254,5 +1260,15 @@ def compile_app(text: str, strings: Optional[StringDict] = None) -> CompiledApp:
             if s in owner and owner[s] != p:
                 raise UnsupportedQuery(f"stream {s} partitioned twice")
             owner[s] = p
+    # a range partition hands each query inside it the expanded stream (one copy of
+    # an event per range that holds, none when no range does), while a query outside
+    # it reads the original stream (PartitionStreamReceiver feeds only the
+    # partition's own junction): one batch cannot serve both, so such apps stay on
+    # the Java runtime
+    for cq in cqs:
+        for sname in set(cq.slot_streams):
+            p = owner.get(sname)
+            if p is not None and isinstance(app.partitions[p][sname], RangeSpec) and cq.query.partition != p:
+                raise UnsupportedQuery(f"stream {sname} is range-partitioned and also read outside the partition")
     app.output_streams = out_streams
     return CompiledApp(app, cqs, strings, out_streams)

@@ -362,6 +362,7 @@ struct sh_handle {
     DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls, w_oq, w_inv;
     bool dev_want_query = false;  // sh_run_device asked for d_out_query
     const uint32_t* dev_run_ids = nullptr;  // sh_run_device's d_run while it runs the general engine
+    bool poisoned = false;  // a failed restore could not put the handle back: every call is refused
     DevBuf v_sts, v_mpos, v_flag, v_cnts, v_mid_ts, v_dir;
     DevBuf v_scol[32], v_mid[32];
     int64_t tmp_cap = 0;
@@ -888,6 +889,7 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall = false);
 static int nf_next_due(sh_handle* h, int64_t* out);
 
 int sh_push_batch(sh_handle* h, const sh_batch* b) {
+    if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !b) return SH_E_INVALID_ARG;
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
     if (b->stream < 0 || b->stream >= h->app.n_streams) return fail(h, SH_E_INVALID_ARG, "bad stream index");
@@ -949,6 +951,7 @@ int sh_set_partition_keys(sh_handle* h, int32_t first_key, int32_t n, const uint
 }
 
 int sh_advance_time(sh_handle* h, int64_t now_ms) {
+    if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h) return SH_E_INVALID_ARG;
     if (h->mode != 1) return SH_OK;  // the chain / window engines have no timer states
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
@@ -976,6 +979,7 @@ int sh_advance_time(sh_handle* h, int64_t now_ms) {
 }
 
 int sh_start(sh_handle* h) {
+    if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h) return SH_E_INVALID_ARG;
     if (h->mode != 1) return SH_OK;
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
@@ -1913,6 +1917,7 @@ int64_t sh_pending(sh_handle* h) {
 }
 
 int sh_drain(sh_handle* h, sh_match_buf* out) {
+    if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !out) return SH_E_INVALID_ARG;
     int rc = flush(h);
     if (rc) return rc;
@@ -2459,6 +2464,7 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
 static int run_device_cols(sh_handle* h, sh_device_run* run);
 
 int sh_run_device(sh_handle* h, sh_device_run* user) {
+    if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !user) return SH_E_INVALID_ARG;
     // the V2 fields are read only from a struct that says it has them
     sh_device_run r = *user;
@@ -2763,6 +2769,7 @@ static int snapshot_image(sh_handle* h, SnapW& w) {
 extern "C" {
 
 int sh_snapshot(sh_handle* h, void* buf, int64_t cap, int64_t* size) {
+    if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !size || (cap > 0 && !buf)) return SH_E_INVALID_ARG;
     SnapW w;
     const int rc = snapshot_image(h, w);
@@ -2773,9 +2780,33 @@ int sh_snapshot(sh_handle* h, void* buf, int64_t cap, int64_t* size) {
     return SH_OK;
 }
 
+static int restore_image(sh_handle* h, const void* buf, int64_t size);
+
 int sh_restore(sh_handle* h, const void* buf, int64_t size) {
     if (!h || !buf || size <= 0) return SH_E_INVALID_ARG;
+    if (h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
+    for (auto& st : h->stores)
+        if (st.rows) return fail(h, SH_E_INVALID_ARG, "restore: the handle has processed events already");
+    // the image is applied as it is parsed: keep the handle's own (fresh) image
+    // and put it back when the new one turns out damaged, so a failed restore
+    // leaves the handle as it was
+    SnapW w0;
+    int rc = snapshot_image(h, w0);
+    if (rc) return rc;
+    rc = restore_image(h, buf, size);
+    if (rc != SH_OK) {
+        const std::string why = h->err;
+        if (restore_image(h, w0.b.data(), (int64_t)w0.b.size()) != SH_OK) {
+            h->poisoned = true;
+            return fail(h, rc, why + " (and the handle could not be reset: " + h->err + "; it refuses further calls)");
+        }
+        return fail(h, rc, why);
+    }
+    return SH_OK;
+}
+
+static int restore_image(sh_handle* h, const void* buf, int64_t size) {
     SnapR r{(const uint8_t*)buf, (size_t)size};
     if (r.get<uint32_t>() != kSnapMagic || r.get<uint32_t>() != kSnapVersion)
         return fail(h, SH_E_INVALID_ARG, "restore: not a matcher snapshot image of this version");

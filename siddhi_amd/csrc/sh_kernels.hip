@@ -21,6 +21,7 @@
 
 #include "../../include/sh_query.h"
 #include "sh_device.h"
+#include "sh_wave.h"
 
 #include <string.h>
 #include <type_traits>
@@ -32,15 +33,8 @@
 #define SCAN_TILE (TPB * SCAN_ITEMS)
 
 // ------------------------------------------------------------------ scan
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
+// wave scans: the DPP row-shift / row-broadcast form of sh_wave.h
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) { return shw_incl_scan(v); }
 
 // block-wide exclusive scan of one value per thread; returns block total in *total
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total) {

@@ -395,8 +395,20 @@ class SiddhiAppRuntime:
     def _send(self, stream_id: int, ts, rows):
         if not self._started:
             raise SiddhiAppRuntimeException("SiddhiAppRuntime not started")
+        last_in = None
+        if rows and self.app.playback:
+            last_in = self.clock if ts[-1] is None else int(ts[-1])
         ts, rows, labels = self._range_expand(stream_id, ts, rows)
         self._labels = labels
+        if last_in is not None and labels is not None:
+            # InputHandler.send moves the playback clock to the batch's last event
+            # before any partition routing (InputHandler.java:85-96), even when no
+            # range keeps that event: one time change to it here; the engine's own
+            # advance to an earlier kept timestamp then notifies nobody
+            # (TimestampGeneratorImpl.setCurrentTimestamp: only ts >= current)
+            kept = None if not rows else (self.clock if ts[-1] is None else int(ts[-1]))
+            if (kept is None or kept < last_in) and last_in >= self.clock:
+                self.advance_time(last_in)
         if not rows:
             return
         tsa, cols, nulls, keys = self._pack(stream_id, ts, rows)

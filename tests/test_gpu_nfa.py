@@ -38,10 +38,13 @@ class _Unlowered(Exception):
 def _check(seed):
     rng = random.Random(seed)
     app, actions = nfa_case(rng)
+    from siddhi_amd.runtime import SiddhiAppCreationException
     try:
         ref = run_case(OracleEngine, app, actions)
-    except Exception as e:
-        pytest.skip(str(e)[:100])
+    except SiddhiAppCreationException as e:
+        # only a creation-time refusal (a shape outside the subset) skips; any
+        # other oracle failure fails the test
+        pytest.skip(f"not created: {str(e)[:100]}")
     try:
         got = run_case(hip_factory, app, actions)
     except _Unlowered as e:

@@ -125,7 +125,7 @@ def _shard_case(config):
         ts, card, amount, merchant = synth.txn_stream(2_000_000, 20_000, 100)
         rules = synth.c5_rules(200)
         return (compiler.compile_app(synth.c5_query(rules)), ts, card, [card, amount, merchant], 20_000,
-                lambda: c5_expected(ts, card, amount, merchant, rules), True, True)
+                lambda: (lambda r: (r[0], r[2], r[1]))(c5_expected(ts, card, amount, merchant, rules)), True, True)
     ts, k, p, v = synth.stock_stream(2_000_000, 100_000 if config == "c3" else 10_000,
                                      1000 if config == "c3" else 100)
     if config == "c3":

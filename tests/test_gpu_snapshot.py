@@ -244,8 +244,37 @@ def test_restore_refuses_another_app_and_used_handles():
     ea2.start()
     with pytest.raises(HipError):
         ea2.restore(image[: len(image) // 2])
+    # a failed restore leaves the handle as it was: the good image still restores
+    ea2.restore(image)
     ea3 = HipEngine(a)
     ea3.start()
     ea3.restore(image)
     for e in (ea, eb, ea2, ea3):
         e.close()
+
+
+def test_failed_restore_leaves_the_handle_usable():
+    """a damaged image is refused after part of it was applied; the handle keeps
+    working from its own state (the C4 stream then matches the oracle's)"""
+    from c4_cases import register_users, run_c4, same_output
+    from siddhi_amd._native import HipEngine, HipError
+    from oracle_engine import OracleEngine
+    c = compiler.compile_app(synth.C4_QUERY)
+    blocks = synth.c4_stream(3_000, seconds=20, seed=11)
+    src = HipEngine(c)
+    register_users(src, blocks)
+    src.start()
+    seq = 0
+    for st, ts, cols, keys in blocks[: len(blocks) // 2]:
+        src.send(st, ts, cols, [None] * len(cols), keys, seq)
+        seq += len(ts)
+    image = src.snapshot()
+    src.close()
+    eng = HipEngine(c)
+    with pytest.raises(HipError) as ei:
+        eng.restore(image[: len(image) - 16])  # parsed almost to the end before it fails
+    assert "could not be reset" not in str(ei.value), str(ei.value)
+    got = run_c4(eng, blocks)
+    ref = run_c4(OracleEngine(c), blocks)
+    eng.close()
+    assert len(ref["seq"]) > 0 and same_output(got, ref)

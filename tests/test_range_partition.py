@@ -176,3 +176,70 @@ def test_range_partition_gpu_vs_oracle(app, seed):
 
     ts, rows = _stream(200 + seed, 600)
     assert run_app(app, ts, rows, hip) == run_app(app, ts, rows, OracleEngine)
+
+
+def test_range_stream_read_outside_the_partition_is_refused():
+    """a query outside a range partition reads the original stream, one inside it
+    the expanded one: such apps stay on the Java runtime"""
+    from siddhi_amd.runtime import SiddhiAppCreationException
+    app = RANGE_APP.replace("end;", "end;\n@info(name = 'g') from every e1=S -> e2=S[price > e1.price] "
+                                    "select e1.price as p1, e2.price as p2 insert into G;")
+    with pytest.raises(SiddhiAppCreationException):
+        SiddhiManager(engine_factory=OracleEngine).createSiddhiAppRuntime(app)
+
+
+ABSENT_RANGE_APP = """
+@app:playback
+define stream S (symbol string, price float, volume long);
+partition with (price >= 100 as 'large' of S)
+begin
+  @info(name = 'q')
+  from e1=S[price >= 100] -> not S[price > e1.price] for 1 sec
+  select e1.price as p
+  insert into Out;
+end;
+"""
+
+
+def _absent_range(factory):
+    steps = []
+    for second in ([[1500, 2500], [["A", 120.0, 1], ["A", 10.0, 1]]],   # the last event is in no range
+                   [[2500], [["A", 10.0, 1]]]):                        # no event is in a range
+        mgr = SiddhiManager(engine_factory=factory)
+        rt = mgr.createSiddhiAppRuntime(ABSENT_RANGE_APP)
+        got = []
+        rt.addCallback("Out", lambda evs: got.extend((e.timestamp, tuple(e.data)) for e in evs))
+        rt.start()
+        h = rt.getInputHandler("S")
+        h.send_batch([1000], [["A", 150.0, 1]])
+        # the clock moves to the batch's last event (2500) before the batch
+        # (InputHandler.java:85-96), so the timer due at 2000 fires first
+        h.send_batch(*second)
+        steps.append(list(got))
+        rt.shutdown()
+    return steps
+
+
+def test_playback_clock_moves_on_events_no_range_keeps():
+    assert _absent_range(OracleEngine) == [[(2000, (150.0,))], [(2000, (150.0,))]]
+
+
+@pytest.mark.gpu
+def test_playback_clock_no_range_gpu_vs_oracle():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from siddhi_amd._native import HipEngine
+    assert _absent_range(HipEngine) == _absent_range(OracleEngine)
+
+
+def test_labels_and_string_literals_are_verbatim():
+    """STRING_LITERAL has no escapes (SiddhiQL.g4:854-860): non-ASCII labels and
+    backslashes reach the partition key text unchanged (its String.hashCode
+    orders the scheduler's map)"""
+    app = compiler.parse("define stream S (s string, p float); partition with (p >= 1 as 'größer' or "
+                         "p < 1 as \"a\\tb\" of S) begin from every e1=S -> e2=S[s == 'x\\y'] "
+                         "select e1.p as p insert into O; end;")
+    assert [lb for _, lb in app.partitions[0]["S"].ranges] == ["größer", "a\\tb"]
+    got = run_app(app_text := RANGE_APP.replace("'large'", "'größer'"), *_stream(3), OracleEngine)
+    assert got == run_app(RANGE_APP, *_stream(3), OracleEngine) and app_text
