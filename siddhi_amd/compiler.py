@@ -822,7 +822,18 @@ class Lowerer:
             self.elems[eidx]["filter"] = self.expr(flt, slot, CURRENT)
         outs = []
         if q.select_star:
-            raise UnsupportedQuery("select * on patterns")
+            # SelectorParser.java:180-205: every attribute of every state's stream, in
+            # slot order, each as a bare variable; a name two streams share is a
+            # DuplicateAttributeException
+            sel, seen = [], set()
+            for sd, _, _ in self.slots:
+                for name, _ in sd.attrs:
+                    if name in seen:
+                        raise SiddhiAppValidationException(
+                            f"Duplicate attribute exist in streams: '{name}' (select *)")
+                    seen.add(name)
+                    sel.append(OutAttr(EVar(None, name), name))
+            q.select, q.select_star = sel, False
         for oa in q.select:
             outs.append(self.out_attr(oa))
         self.having = -1

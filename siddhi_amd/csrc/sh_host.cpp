@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/siddhi_hip.h"
+#include "sh_agg.h"
 #include "sh_device.h"
 #include "sh_jit.h"
 #include "sh_jmap.h"
@@ -374,7 +375,7 @@ struct sh_handle {
     std::vector<uint8_t> o_nulls;
     int64_t o_read = 0;
     sh_kernel_times times{};
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // [4, 5]: aggregate post-pass
     // hipRTC-specialised window kernels (sh_jit.cpp): 0 untried, 1 loaded, <0 unavailable
     int jit_state = 0;
     shj_window jit{};
@@ -393,6 +394,7 @@ struct sh_handle {
     DevBuf n_klist[2], n_klist_n, n_arm_log, n_arm_ctr;
     int klist_cur = 0;
     int seq3_last = 0;                  // the last general-engine run took k_seq3
+    bool no_seq3 = false;               // rerun without k_seq3 (aggregates not exact in parallel)
     // scheduler maps' iteration order (sh_jmap.h): host models fed by the
     // launches' getState history, per-key ranks uploaded for the due-key pick
     bool sm_on = false;
@@ -414,6 +416,10 @@ struct sh_handle {
     bool r_partitioned = false;
     int32_t r_nout = 0;
     std::vector<shr_rule> r_rules;
+    bool r_aggp = false;                 // every rule aggregates (sh_agg.hip post-pass)
+    int32_t r_agg[SHP_MAX_OUT] = {0}, r_argt[SHP_MAX_OUT] = {0};
+    DevBuf a_q;                          // query per row when the caller wants none
+    bool skip_rules = false;             // rerun on the general engine (aggregates not exact in parallel)
     std::vector<int64_t> r_ixval;
     std::vector<uint32_t> r_ixstart, r_ixrule, r_free;
     shr_table r_tab{};
@@ -431,6 +437,10 @@ struct sh_handle {
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
     DevBuf w_colrows;
     bool cols_rows = false;
+    // aggregators behind the fast engines (sh_agg.hip): scratch, trigger sequence
+    // numbers when the caller wants none, and the last run's path
+    DevBuf a_scratch, a_seq;
+    int agg_last = 0;  // 1: post-pass done, 2: post-pass not exact -> sequential engine
     std::vector<int32_t> out_types;  // per select position over the queries (-2: types differ)
     uint64_t fp = 0;                 // compiled-program fingerprint (snapshot images)
 };
@@ -527,15 +537,24 @@ static int lower_chain(sh_handle* h, const sh_app_desc* app, int qi, shp_program
     if (q.n_outputs > SHP_MAX_OUT) return fail(h, SH_E_UNSUPPORTED, "device engine: at most 16 output attributes");
     P.n_out = q.n_outputs;
     P.out_fast = getenv("SH_DISABLE_FAST_FILTER") ? 0 : 1;
+    P.agg_post = 0;
     for (int o = 0; o < q.n_outputs; o++) {
         const sh_output_attr& oa = q.outputs[o];
-        if (oa.agg != SH_AGG_NONE || oa.expr < 0 || !Lowering::is_var(q.exprs[oa.expr])) {
+        const bool postable = oa.agg == SH_AGG_SUM || oa.agg == SH_AGG_AVG || oa.agg == SH_AGG_COUNT;
+        if (oa.agg == SH_AGG_COUNT && oa.expr < 0) {
+            // count(): the row carries any value; the post-pass counts rows
+            P.out_slot[o] = 1;
+            P.out_attr[o] = 0;
+            P.agg_post = 1;
+        } else if ((oa.agg != SH_AGG_NONE && !postable) || oa.expr < 0 || !Lowering::is_var(q.exprs[oa.expr])) {
             P.out_fast = 0;
         } else {
             P.out_slot[o] = q.exprs[oa.expr].slot;
             P.out_attr[o] = q.exprs[oa.expr].attr;
+            if (oa.agg != SH_AGG_NONE) P.agg_post = 1;
         }
     }
+    if (!P.out_fast || getenv("SH_NO_AGG_POST")) P.agg_post = 0;
     for (int o = 0; o < q.n_outputs; o++) {
         const sh_output_attr& oa = q.outputs[o];
         P.out_agg[o] = oa.agg;
@@ -555,7 +574,7 @@ static int lower_chain(sh_handle* h, const sh_app_desc* app, int qi, shp_program
     {
         bool agg = false;
         for (int o = 0; o < P.n_out; o++) agg |= P.out_agg[o] != SH_AGG_NONE;
-        P.window_ok = (P.n_states == 2 && P.every_start && P.within_ms >= 0 && !agg &&
+        P.window_ok = (P.n_states == 2 && P.every_start && P.within_ms >= 0 && (!agg || P.agg_post) &&
                        P.state_stream[0] == P.state_stream[1] && app->n_streams == 1)
                           ? 1
                           : 0;
@@ -649,6 +668,22 @@ static int compile_rules(sh_handle* h, const sh_app_desc* app) {
         for (int o = 0; o < P->n_out; o++) {
             R.out_slot[o] = (int8_t)P->out_slot[o];
             R.out_attr[o] = (int8_t)P->out_attr[o];
+        }
+        // aggregators: one layout for the whole set (the post-pass runs per column
+        // over every rule's rows, keyed by (rule, partition key))
+        if (qi == 0) {
+            h->r_aggp = P->agg_post != 0;
+            for (int o = 0; o < SHP_MAX_OUT; o++) {
+                h->r_agg[o] = o < P->n_out ? P->out_agg[o] : SH_AGG_NONE;
+                h->r_argt[o] = o < P->n_out ? P->out_arg_type[o] : 0;
+            }
+        } else {
+            bool same = (P->agg_post != 0) == h->r_aggp;
+            for (int o = 0; o < P->n_out && same; o++)
+                same = P->out_agg[o] == h->r_agg[o] && (P->out_agg[o] == SH_AGG_NONE || P->out_arg_type[o] == h->r_argt[o]);
+            for (int o = P->n_out; o < SHP_MAX_OUT && same; o++) same = h->r_agg[o] == SH_AGG_NONE;
+            if (!same)
+                return fail(h, SH_E_UNSUPPORTED, "rule engine: the queries aggregate different select positions");
         }
     }
     // predicate index: the slot-0 attribute most start filters compare for
@@ -1507,7 +1542,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
         }
         nfd_emit em = nf_emit(h);
         // the rise-and-fall sequence engine: fresh single-query runs of that shape
-        const bool seq3 = fresh && h->T->n_queries == 1 && h->T->q[0].s3 && !getenv("SH_NO_SEQ3");
+        const bool seq3 = fresh && h->T->n_queries == 1 && h->T->q[0].s3 && !h->no_seq3 && !getenv("SH_NO_SEQ3");
         h->seq3_last = seq3 ? 1 : 0;
         if (seq3) {
             if (nfd_seq3(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), &E, n, seg_list, nseg, skeys, nkeys, max_seg,
@@ -2014,6 +2049,9 @@ static int tile_shift_for(int64_t n, int32_t nkeys) {
 }
 
 // batch-compiled rule sets (sh_rules.hip) over HBM-resident columns
+static int agg_post(sh_handle* h, sh_device_run* run, int32_t nkeys, const int32_t* d_query, int n_query,
+                    const int32_t* agg_kind, const int32_t* arg_type, int n_out);
+
 static int run_rules(sh_handle* h, sh_device_run* run) {
     hipStream_t st = h->stream;
     const int64_t n = run->n;
@@ -2134,6 +2172,16 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
             order = vo;
         }
         hipEventRecord(h->ev[2], st);
+        if (h->r_aggp) {
+            if (!run->d_out_query) {
+                if (h->a_q.ensure((size_t)m * 4)) return fail(h, SH_E_OOM, "aggregate query ids");
+                run->d_out_query = h->a_q.as<int32_t>();
+            }
+            if (!run->d_out_seq) {
+                if (h->a_seq.ensure((size_t)m * 8)) return fail(h, SH_E_OOM, "aggregate sequence numbers");
+                run->d_out_seq = h->a_seq.as<uint64_t>();
+            }
+        }
         if (shr_place(dT, order, m, rec_p, rec_q, rec_r, perm, sts, dC, 0, std::max(1, h->n_out), run->d_out_seq,
                       run->d_out_query, nullptr, run->d_out_values, st))
             return fail(h, SH_E_HIP, "rule placement launch failed");
@@ -2147,6 +2195,12 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
     hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
     hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
     h->times.advance_launches = 1;
+    if (h->r_aggp && m > 0) {
+        const int arc = agg_post(h, run, nkeys, run->d_out_query, (int)h->r_rules.size(), h->r_agg, h->r_argt,
+                                 std::max(1, h->n_out));
+        if (arc < 0) return arc;
+        if (arc == 1) return 1;  // not exact in parallel: the caller runs the general engine
+    }
     return SH_OK;
 }
 
@@ -2226,7 +2280,7 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
         if (O.kind[o] == 0) O.src[o] = B.ms[(int)(intptr_t)O.src[o]];
     shb_cols OC;
     memset(&OC, 0, sizeof(OC));
-    if (run->d_out_cols) {
+    if (run->d_out_cols && !P.agg_post) {
         OC.use = 1;
         for (int o = 0; o < O.n_out; o++) {
             OC.cols[o] = run->d_out_cols[o];
@@ -2304,6 +2358,38 @@ static int rows_for_cols(sh_handle* h, sh_device_run* run) {
     return SH_OK;
 }
 
+// the running aggregates of the fast engines' ordered rows (sh_agg.hip): SH_OK,
+// 1 = the double additions would round (the caller reruns sequentially), < 0 error
+static int agg_post(sh_handle* h, sh_device_run* run, int32_t nkeys, const int32_t* d_query, int n_query,
+                    const int32_t* agg_kind, const int32_t* arg_type, int n_out) {
+    const int64_t m = run->out_count;
+    if (m <= 0) return SH_OK;
+    sha_desc D;
+    memset(&D, 0, sizeof(D));
+    for (int o = 0; o < n_out && D.n_cols < SHA_MAX_COLS; o++)
+        if (agg_kind[o] != SH_AGG_NONE) {
+            D.c[D.n_cols].col = o;
+            D.c[D.n_cols].kind = agg_kind[o];
+            D.c[D.n_cols].arg_type = arg_type[o];
+            D.n_cols++;
+        }
+    if (D.n_cols == 0) return SH_OK;
+    if (h->a_scratch.ensure((size_t)sha_scratch_bytes(m))) return fail(h, SH_E_OOM, "aggregate scratch");
+    hipEventRecord(h->ev[4], h->stream);
+    const int rc = sha_running(run->d_out_seq, run->d_out_values, n_out, m, d_query, n_query,
+                               h->partitioned ? run->d_keys : nullptr, h->partitioned ? nkeys : 1, 0, &D,
+                               h->a_scratch.p, h->stream);
+    if (rc < 0) return fail(h, SH_E_HIP, "aggregate post-pass failed");
+    hipEventRecord(h->ev[5], h->stream);
+    hipEventSynchronize(h->ev[5]);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, h->ev[4], h->ev[5]);
+    h->times.emit_ms += ms;
+    h->times.total_ms += ms;
+    h->agg_last = rc == 0 ? 1 : 2;
+    return rc;
+}
+
 static int run_device_impl(sh_handle* h, sh_device_run* run) {
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device");
     if (h->app.n_streams != 1) return fail(h, SH_E_UNSUPPORTED, "sh_run_device: single-stream apps only");
@@ -2311,7 +2397,17 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
     h->stream = run->stream ? (hipStream_t)run->stream : h->own_stream;
     if (h->has_rules && (h->mode == 2 || !getenv("SH_DISABLE_RULES"))) {
         const int crc = rows_for_cols(h, run);
-        return crc ? crc : run_rules(h, run);
+        if (crc) return crc;
+        int32_t* user_q = run->d_out_query;
+        uint64_t* user_seq = run->d_out_seq;
+        int rrc = run_rules(h, run);
+        if (rrc != 1) return rrc;
+        // the aggregates would round in parallel: the general engine adds in sequence
+        run->d_out_query = user_q;
+        run->d_out_seq = user_seq;
+        if (h->mode == 2)
+            return fail(h, SH_E_UNSUPPORTED, "rule set aggregates are not exact in parallel and the set is "
+                                             "beyond the general engine's query table");
     }
     if (h->mode == 1) {
         const int crc = rows_for_cols(h, run);
@@ -2321,30 +2417,52 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
         if (h->T->has_absent) return fail(h, SH_E_UNSUPPORTED, "sh_run_device: absent states need sh_push_batch");
         const int32_t nkeys = h->partitioned ? std::max(1, run->n_keys) : 1;
         if (nf_ensure_keys(h, nkeys)) return fail(h, SH_E_OOM, "key state");
-        hipMemsetAsync(h->n_kstate.p, 0, (size_t)nkeys * h->T->key_words * 8, h->stream);
-        h->started = false;
-        int rc = nf_start(h);
-        if (rc) return rc;
-        nf_cols cols;
-        memset(&cols, 0, sizeof(cols));
-        for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = run->d_cols[a];
-        shd_batch B;
-        B.ts = run->d_ts;
-        B.stream = nullptr;
-        B.row = nullptr;
-        B.keys = h->partitioned ? run->d_keys : nullptr;
-        B.row_base = 0;
-        B.pad = 0;
-        B.seq_base = 0;
-        B.n = run->n;
+        const nf_query& Q0 = h->T->q[0];
+        const bool aggp = h->T->n_queries == 1 && Q0.s3 && Q0.contains_agg;
+        if (aggp && !run->d_out_seq) {
+            if (h->a_seq.ensure((size_t)std::max<int64_t>(1, run->out_capacity) * 8))
+                return fail(h, SH_E_OOM, "aggregate sequence numbers");
+            run->d_out_seq = h->a_seq.as<uint64_t>();
+        }
+        int rc = SH_OK;
         int64_t rows = 0;
-        h->times = sh_kernel_times{};
-        h->dev_want_query = run->d_out_query != nullptr;
-        h->dev_run_ids = run->d_run;
-        rc = nf_process(h, B, nkeys, cols, run->d_out_seq, run->d_out_values, run->out_capacity, &rows, true,
-                        run->batch_events, getenv("SH_NFA_GATHER") ? nullptr : run);
-        h->dev_run_ids = nullptr;
-        run->out_count = rows;
+        h->agg_last = 0;
+        h->no_seq3 = false;
+        for (int pass = 0; pass < 2; pass++) {
+            hipMemsetAsync(h->n_kstate.p, 0, (size_t)nkeys * h->T->key_words * 8, h->stream);
+            h->started = false;
+            rc = nf_start(h);
+            if (rc) return rc;
+            nf_cols cols;
+            memset(&cols, 0, sizeof(cols));
+            for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = run->d_cols[a];
+            shd_batch B;
+            B.ts = run->d_ts;
+            B.stream = nullptr;
+            B.row = nullptr;
+            B.keys = h->partitioned ? run->d_keys : nullptr;
+            B.row_base = 0;
+            B.pad = 0;
+            B.seq_base = 0;
+            B.n = run->n;
+            rows = 0;
+            h->times = sh_kernel_times{};
+            h->dev_want_query = run->d_out_query != nullptr;
+            h->dev_run_ids = run->d_run;
+            rc = nf_process(h, B, nkeys, cols, run->d_out_seq, run->d_out_values, run->out_capacity, &rows, true,
+                            run->batch_events, getenv("SH_NFA_GATHER") ? nullptr : run);
+            h->dev_run_ids = nullptr;
+            run->out_count = rows;
+            if (rc != SH_OK || !aggp || !h->seq3_last) break;
+            // k_seq3 wrote the aggregators' arguments: the running values
+            int32_t arg_type[NF_MAX_OUT];
+            for (int o = 0; o < Q0.n_out; o++) arg_type[o] = Q0.s3_out_type[o];
+            const int arc = agg_post(h, run, nkeys, nullptr, 1, Q0.out_agg, arg_type, Q0.n_out);
+            if (arc < 0) return arc;
+            if (arc == 0) break;
+            h->no_seq3 = true;  // not exact: the general engine adds in sequence
+        }
+        h->no_seq3 = false;
         if (rc == SH_OK && run->d_out_query && rows > 0) {
             hipMemcpyAsync(run->d_out_query, h->w_oq.p, rows * 4, hipMemcpyDeviceToDevice, h->stream);
             hipStreamSynchronize(h->stream);
@@ -2368,15 +2486,39 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
     for (size_t a = 0; a < h->stream_types[0].size(); a++) cols.col[0][a] = run->d_cols[a];
     int64_t nm = 0;
     h->times = sh_kernel_times{};
+    h->agg_last = 0;
+    // aggregators: the fast engines write raw rows with the arguments, the
+    // post-pass turns them into running values (or asks for the sequential engine)
+    const bool aggp = h->prog.agg_post != 0;
+    bool sequential = false;
+    if (aggp) {
+        const int crc = rows_for_cols(h, run);
+        if (crc) return crc;
+        if (!run->d_out_seq) {
+            if (h->a_seq.ensure((size_t)std::max<int64_t>(1, run->out_capacity) * 8))
+                return fail(h, SH_E_OOM, "aggregate sequence numbers");
+            run->d_out_seq = h->a_seq.as<uint64_t>();
+        }
+    }
+    auto finish_agg = [&](int32_t nk) {
+        const int arc = agg_post(h, run, nk, nullptr, 1, h->prog.out_agg, h->prog.out_arg_type, h->prog.n_out);
+        if (arc == 1) sequential = true;
+        return arc;
+    };
     if (h->prog.window_ok) {
         const int brc = run_bucket(h, run, nkeys);
-        if (brc != 1) return brc;
+        if (brc == SH_OK && aggp) {
+            const int arc = finish_agg(nkeys);
+            if (arc <= 0) return arc;
+        } else if (brc != 1) {
+            return brc;
+        }
     }
     {
         const int crc = rows_for_cols(h, run);
         if (crc) return crc;
     }
-    if (h->prog.window_ok && h->stream_types[0].size() <= 7) {
+    if (!sequential && h->prog.window_ok && h->stream_types[0].size() <= 7) {
         const int64_t n = run->n;
         hipStream_t st = h->stream;
         if (ensure_ws(h, n)) return fail(h, SH_E_OOM, "workspace");
@@ -2447,7 +2589,9 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
             hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
             hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
             h->times.advance_launches = 1;
-            return SH_OK;
+            if (!aggp) return SH_OK;
+            const int arc = finish_agg(nkeys);
+            if (arc <= 0) return arc;
         }
         // wrc == 1: timestamps decrease inside a key -> sequential per-key engine
     }
@@ -2529,6 +2673,9 @@ int shx_bucket_status(sh_handle* h) {
 
 // 1: the last general-engine sh_run_device took the rise-and-fall sequence engine
 int shx_seq3_status(sh_handle* h) { return h ? h->seq3_last : 0; }
+// aggregators of the last sh_run_device: 0 none on a fast engine, 1 the post-pass
+// (sh_agg.hip) formed them, 2 it was not exact and a sequential engine ran
+int shx_agg_status(sh_handle* h) { return h ? h->agg_last : 0; }
 // 1: the compiled app has the rise-and-fall sequence shape (no device needed)
 int shx_seq3_shape(sh_handle* h) { return h && h->T && h->T->n_queries == 1 && h->T->q[0].s3 ? 1 : 0; }
 
@@ -2812,8 +2959,6 @@ static int restore_image(sh_handle* h, const void* buf, int64_t size) {
         return fail(h, SH_E_INVALID_ARG, "restore: not a matcher snapshot image of this version");
     if (r.get<int32_t>() != h->mode || r.get<uint64_t>() != h->fp)
         return fail(h, SH_E_INVALID_ARG, "restore: the image was taken from a different app");
-    for (auto& st : h->stores)
-        if (st.rows) return fail(h, SH_E_INVALID_ARG, "restore: the handle has processed events already");
     hipStreamSynchronize(h->stream);
     h->seq_next = r.get<uint64_t>();
     h->seq_staged0 = r.get<uint64_t>();

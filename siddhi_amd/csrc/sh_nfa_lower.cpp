@@ -464,7 +464,16 @@ struct QueryLowering {
         if (q->n_outputs > NF_MAX_OUT) return;
         for (int o = 0; o < q->n_outputs; o++) {
             const sh_output_attr& oa = q->outputs[o];
-            if (oa.agg != SH_AGG_NONE || oa.expr < 0) return;
+            // sum / avg / count of a plain attribute: the engine writes the argument,
+            // the post-pass over the ordered rows forms the running value (sh_agg.hip)
+            if (oa.agg == SH_AGG_COUNT && oa.expr < 0) {
+                Q->s3_out_slot[o] = 2;
+                Q->s3_out_attr[o] = 0;
+                Q->s3_out_type[o] = (int8_t)app->streams[c3.stream].attr_types[0];
+                continue;
+            }
+            if (oa.agg != SH_AGG_NONE && oa.agg != SH_AGG_SUM && oa.agg != SH_AGG_AVG && oa.agg != SH_AGG_COUNT) return;
+            if (oa.expr < 0) return;
             const sh_expr& x = q->exprs[oa.expr];
             int at, ty;
             if (x.op != SH_OP_VAR || x.slot < 0 || x.slot > 2) return;

@@ -76,6 +76,10 @@ struct shp_program {
     int32_t out_fast;
     int32_t out_slot[SHP_MAX_OUT];
     int32_t out_attr[SHP_MAX_OUT];
+    // aggregators (sum / avg / count of a plain attribute) on the fast engines:
+    // (out_slot, out_attr) is the argument, turned into the running value per
+    // partition key by the post-pass over the ordered rows (sh_agg.hip)
+    int32_t agg_post;
     // per stream: which states update (stabilizeStates) and the processing order
     // (eventSequence: reverse of setup order), PatternSingle/MultiProcessStreamReceiver
     int32_t upd_count[SHP_MAX_STREAMS];

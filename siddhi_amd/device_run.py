@@ -115,6 +115,11 @@ class DeviceRunner:
         """1: the last run took the rise-and-fall sequence engine (k_seq3)."""
         return lib().shx_seq3_status(self.handle.h)
 
+    def agg_status(self):
+        """aggregators of the last run: 1 post-pass over a fast engine's rows
+        (sh_agg.hip), 2 not exact in parallel (a sequential engine ran), 0 none."""
+        return lib().shx_agg_status(self.handle.h)
+
     def last_error(self):
         return lib().sh_last_error(self.handle.h).decode()
 

@@ -1,0 +1,146 @@
+"""Select-clause aggregators on the fast engines (sh_agg.hip post-pass): the
+bucketed / window engines (C2 / C1 shapes), the rise-and-fall sequence engine
+(C3) and the rule set (C5) write the aggregators' arguments and the post-pass
+forms the running sum / avg / count per (query, partition key) in match order,
+after proving the double additions exact. Bit-exact against the oracle
+(QuerySelector + Sum/Avg aggregators restated), and at full size against the
+vectorised restatement (tests/agg_check.py). A stream whose additions round
+takes the sequential engines (agg_status 2) and still matches the oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+C2_AGG = ("define stream StockStream (symbol string, price float, volume long); "
+          "partition with (symbol of StockStream) begin @info(name = 'query1') "
+          "from every e1=StockStream[price>20] -> e2=StockStream[symbol==e1.symbol and price>e1.price] "
+          "within 1 sec select e1.symbol as symbol, sum(e2.price) as total, avg(e1.price) as a1, "
+          "count() as n, sum(e2.volume) as vol insert into Out; end;")
+C1_AGG = C2_AGG.replace("partition with (symbol of StockStream) begin ", "").replace(" end;", "")
+C3_AGG = ("define stream S (symbol string, price float, volume long); "
+          "partition with (symbol of S) begin @info(name = 'query1') "
+          "from every e1=S, e2=S[price>e1.price]+, e3=S[price<e2[last].price] "
+          "select e1.price as p1, sum(e3.price) as s3, avg(e2[last].price) as apeak, count() as n "
+          "insert into Out; end;")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _run(text, ts, k, cols, nkeys, with_query=False):
+    import torch
+    from siddhi_amd import compiler
+    from siddhi_amd.device_run import DeviceRunner
+    r = DeviceRunner(compiler.compile_app(text))
+    dev = torch.device("cuda:0")
+    tk = torch.from_numpy(k).to(dev)
+    res = r.run(torch.from_numpy(ts).to(dev), tk, [torch.from_numpy(c).to(dev) for c in cols], nkeys,
+                with_query=with_query)
+    torch.cuda.synchronize()
+    out = [res[0]] + [x.cpu().numpy() for x in res[1:]]
+    st = dict(agg=r.agg_status(), bucket=r.bucket_status(), seq3=r.seq3_status())
+    r.close()
+    return out, st
+
+
+def _oracle(text, ts, cols, keys):
+    from oracle_engine import OracleEngine
+    from siddhi_amd import compiler
+    eng = OracleEngine(compiler.compile_app(text))
+    eng.start()
+    for b0 in range(0, len(ts), 4096):
+        b1 = min(len(ts), b0 + 4096)
+        eng.send(0, ts[b0:b1], [np.ascontiguousarray(c[b0:b1]) for c in cols], [None] * len(cols),
+                 None if keys is None else np.ascontiguousarray(keys[b0:b1]), b0)
+    out = eng.drain()
+    eng.close()
+    return out
+
+
+@pytest.mark.parametrize("n,K", [(400_000, 2_000), (300_000, 20_000)])
+def test_c2_aggregates_bucketed_vs_oracle(n, K):
+    from siddhi_amd import synth
+    ts, k, p, v = synth.stock_stream(n, K, 100)
+    (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], K)
+    ref = _oracle(C2_AGG, ts, [k, p, v], k)
+    assert st["bucket"] == 1 and st["agg"] == 1, st
+    assert m == len(ref["seq"]) > 0
+    assert np.array_equal(seq, ref["seq"].astype(np.int64))
+    assert np.array_equal(vals, ref["values"])
+
+
+def test_c1_aggregates_unpartitioned_window_vs_oracle():
+    from siddhi_amd import synth
+    ts, k, p, v = synth.stock_stream(100_000, 100, 1, config_index=1)
+    (m, seq, vals), st = _run(C1_AGG, ts, np.zeros(len(ts), np.int32), [k, p, v], 1)
+    ref = _oracle(C1_AGG, ts, [k, p, v], None)
+    assert st["agg"] == 1, st
+    assert m == len(ref["seq"]) > 0
+    assert np.array_equal(seq, ref["seq"].astype(np.int64))
+    assert np.array_equal(vals, ref["values"])
+
+
+def test_c3_aggregates_seq3_vs_oracle():
+    from siddhi_amd import synth
+    ts, k, p, v = synth.stock_stream(300_000, 3_000, 1000, config_index=3)
+    (m, seq, vals), st = _run(C3_AGG, ts, k, [k, p, v], 3_000)
+    ref = _oracle(C3_AGG, ts, [k, p, v], k)
+    assert st["seq3"] == 1 and st["agg"] == 1, st
+    assert m == len(ref["seq"]) > 0
+    assert np.array_equal(seq, ref["seq"].astype(np.int64))
+    assert np.array_equal(vals, ref["values"])
+
+
+def test_c5_aggregates_rule_set_vs_oracle():
+    from siddhi_amd import synth
+    rules = synth.c5_rules(100)
+    text = synth.c5_query(rules).replace("e2.amount as amount", "sum(e2.amount) as total, avg(e1.amount) as a1")
+    ts, card, amount, merchant = synth.txn_stream(200_000, 5_000, 100)
+    (m, seq, vals, q), st = _run(text, ts, card, [card, amount, merchant], 5_000, with_query=True)
+    ref = _oracle(text, ts, [card, amount, merchant], card)
+    assert st["agg"] == 1, st
+    assert m == len(ref["seq"]) > 0
+    assert np.array_equal(seq, ref["seq"].astype(np.int64))
+    assert np.array_equal(q, ref["query"])
+    assert np.array_equal(vals, ref["values"])
+
+
+def test_rounding_additions_take_the_sequential_engine():
+    """prices spanning 2^-60 .. 2^60: the double additions round, so the post-pass
+    refuses and the sequential engine's sums (== the oracle's) are returned"""
+    from siddhi_amd import synth
+    ts, k, p, v = synth.stock_stream(200_000, 2_000, 100)
+    p = p.copy()
+    p[::7] *= np.float32(2.0 ** 60)
+    p[3::11] *= np.float32(2.0 ** -60)
+    (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], 2_000)
+    ref = _oracle(C2_AGG, ts, [k, p, v], k)
+    assert st["agg"] == 2, st
+    assert m == len(ref["seq"]) > 0
+    assert np.array_equal(seq, ref["seq"].astype(np.int64))
+    assert np.array_equal(vals, ref["values"])
+
+
+def test_c2_aggregates_full_size_vs_restatement():
+    """BASELINE size (100M ticks, 10k symbols): the running sums of every key over
+    the whole match stream equal per-key left-to-right double additions"""
+    from agg_check import raw_bits, running
+    from c2_check import c2_expected
+    from siddhi_amd import synth
+    ts, k, p, v = synth.stock_stream(100_000_000, 10_000, 100)
+    (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], 10_000)
+    assert st["bucket"] == 1 and st["agg"] == 1, st
+    eseq, ev = c2_expected(ts, k, p, v)
+    assert np.array_equal(seq, eseq)
+    grp = k[eseq].astype(np.int64)
+    p2 = ev[:, 2].astype(np.uint32).view(np.float32).astype(np.float64)
+    p1 = ev[:, 1].astype(np.uint32).view(np.float32).astype(np.float64)
+    assert np.array_equal(vals[:, 0], ev[:, 0])
+    assert np.array_equal(vals[:, 1], raw_bits(running(grp, p2, "sum")))
+    assert np.array_equal(vals[:, 2], raw_bits(running(grp, p1, "avg")))
+    assert np.array_equal(vals[:, 3], running(grp, None, "count"))
+    assert np.array_equal(vals[:, 4], running(grp, ev[:, 3], "sum"))
