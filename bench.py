@@ -48,12 +48,14 @@ def parse():
                     help="CPU baseline threads for partitioned configs without timers (events split by key; "
                          "0 = 1 thread, except C5: min(16, nproc))")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--agg", action="store_true",
+                    help="c2 / c3: SURVEY.md 8d select variant (ii), the projection + sum / avg aggregators")
     ap.add_argument("--columns", action="store_true",
                     help="c2: typed output columns (d_out_cols) instead of the raw 8-byte rows (d_out_values)")
     ap.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default, BASELINE.json configs[1]); c1 / c3 / c4 / c5 measure the other configs")
-    ap.add_argument("--seconds", type=int, default=100, help="c4: stream duration (playback seconds)")
     ap.add_argument("--c4-calls", type=int, default=0, help="c4: send only the first N calls (profiling; 0 = all)")
+    ap.add_argument("--c4-every", action="store_true", help="c4: the `every (e1=Login and e2=Txn) -> ...` variant")
     ap.add_argument("--rules", type=int, default=1000, help="c5: rule count")
     args = ap.parse_args()
     if args.config == "c1":
@@ -137,12 +139,15 @@ def workload(args):
     ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=3 if args.config == "c3" else 2,
                                               seed=synth.SEED + (3 if args.config == "c3" else 2))
     if args.config == "c3":
-        compiled = compiler.compile_app(synth.C3_QUERY)
+        compiled = compiler.compile_app(synth.C3_AGG_QUERY if args.agg else synth.C3_QUERY)
 
         def expected():
             sys.path.insert(0, os.path.join(HERE, "tests"))
             from c3_check import c3_expected
-            return c3_expected(ts, keys, price) + (None,)
+            eseq, ev = c3_expected(ts, keys, price)
+            if args.agg:
+                ev = with_aggregates(keys[eseq], ev, [("sum", ev[:, 2]), ("avg", ev[:, 1])])
+            return eseq, ev, None
 
         def cpu(s, idx=None):
             sys.path.insert(0, os.path.join(HERE, "tests"))
@@ -151,16 +156,20 @@ def workload(args):
             run_stock_oracle(compiled, ts[ix], keys[ix], price[ix], vol[ix], batch=4096)
 
         return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, expected=expected, cpu=cpu,
-                    b_event=16, b_match=20, cpu_sample=args.cpu_sample, cpu_split=True,
+                    b_event=16, b_match=20 + (16 if args.agg else 0), cpu_sample=args.cpu_sample, cpu_split=True,
                     desc="C3: every e1=S, e2=S[price>e1.price]+, e3=S[price<e2[last].price], "
-                         "partition with (symbol of S)", key_name="keys_per_gpu",
-                    bytes_note="event: ts 8 + symbol 4 + price 4 = 16 B; match: seq 8 + 3 x price 4 = 20 B")
-    compiled = compiler.compile_app(synth.C2_QUERY)
+                         "partition with (symbol of S)" + AGG_NOTE[args.agg], key_name="keys_per_gpu",
+                    bytes_note="event: ts 8 + symbol 4 + price 4 = 16 B; match: seq 8 + 3 x price 4 = 20 B"
+                               + (" + sum 8 + avg 8 = 36 B" if args.agg else ""))
+    compiled = compiler.compile_app(synth.C2_AGG_QUERY if args.agg else synth.C2_QUERY)
 
     def expected():
         sys.path.insert(0, os.path.join(HERE, "tests"))
         from c2_check import c2_expected
-        return c2_expected(ts, keys, price, vol) + (None,)
+        eseq, ev = c2_expected(ts, keys, price, vol)
+        if args.agg:
+            ev = with_aggregates(keys[eseq], ev, [("sum", ev[:, 2]), ("avg", ev[:, 1])])
+        return eseq, ev, None
 
     def cpu(s, idx=None):
         sys.path.insert(0, os.path.join(HERE, "tests"))
@@ -169,11 +178,26 @@ def workload(args):
         run_stock_oracle(compiled, ts[ix], keys[ix], price[ix], vol[ix], batch=4096)
 
     return dict(ts=ts, keys=keys, cols=[keys, price, vol], compiled=compiled, expected=expected, cpu=cpu,
-                b_event=24, b_match=28, cpu_sample=args.cpu_sample, cpu_split=True,
+                b_event=24, b_match=28 + (16 if args.agg else 0), cpu_sample=args.cpu_sample, cpu_split=True,
                 desc="C2: every e1[price>20] -> e2[symbol==e1.symbol and price>e1.price] within 1 sec, "
-                     "partition with (symbol of StockStream)", key_name="symbols_per_gpu",
+                     "partition with (symbol of StockStream)" + AGG_NOTE[args.agg], key_name="symbols_per_gpu",
                 bytes_note="event: ts 8 + symbol 4 + price 4 + volume 8 = 24 B; "
-                           "match: seq 8 + symbol 4 + p1 4 + p2 4 + v2 8 = 28 B")
+                           "match: seq 8 + symbol 4 + p1 4 + p2 4 + v2 8 = 28 B"
+                           + (" + sum 8 + avg 8 = 44 B" if args.agg else ""))
+
+
+AGG_NOTE = {False: "", True: "; select variant (ii): + sum / avg running per partition key"}
+
+
+def with_aggregates(group, ev, aggs):
+    """the restatement's rows + the running aggregates (tests/agg_check.py): each
+    (kind, raw float column) adds one double-valued column"""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    from agg_check import raw_bits, running
+    g = group.astype(np.int64)
+    extra = [raw_bits(running(g, col.astype(np.uint32).view(np.float32).astype(np.float64), kind))
+             for kind, col in aggs]
+    return np.concatenate([ev] + [e.reshape(-1, 1) for e in extra], 1)
 
 
 import numpy as np  # noqa: E402
@@ -181,28 +205,52 @@ import numpy as np  # noqa: E402
 
 def main_c4(args, torch, dist, world, rank, dev):
     """C4 (BASELINE.json configs[3]): `(e1=Login and e2=Txn) -> not Logout for 5 sec`
-    partitioned by user, playback time. Absent states need the playback scheduler,
-    so this config runs through the streaming C-ABI (sh_push_batch per send(Event[])
-    batch, sh_advance_time, sh_drain): host buffers cross PCIe inside the timed
-    region, unlike C2's HBM-resident sh_run_device. A step = one fresh engine
-    start + the whole stream + the drain of every match."""
+    (or the `every (...)` variant, --c4-every) partitioned by user, playback time,
+    on the SURVEY 8d workload: --events (100M) over Login 20% / Txn 60% / Logout 20%,
+    --keys (10M) users, R = --rate (100) ev/ms, send(Event[]) calls of 4,096 events
+    per stream (synth.c4_spec_stream). Absent states need the playback scheduler,
+    so this config runs through the streaming C-ABI (sh_push_batch per call,
+    sh_advance_time, sh_drain): host buffers cross PCIe inside the timed region.
+    At N > 1 the users are key-sharded (siddhi_amd/shard_stream.py): every rank sees
+    every call and pushes its users' events (sh_push_batch_part); the one state per
+    due time Scheduler.onTimeChange fires and the state map's HashMap order are
+    agreed over gloo (candidate gather + history exchange). A step = one fresh
+    engine start + the whole stream + the drain of every match."""
     sys.path.insert(0, os.path.join(HERE, "tests"))
-    from c4_cases import run_c4
+    from c4_cases import register_users
     from siddhi_amd import compiler, synth
     from siddhi_amd._native import HipEngine
-    log(f"generating c4 workload: {args.keys} users over {args.seconds} s")
-    blocks = synth.c4_stream(args.keys, seconds=args.seconds, seed=synth.SEED + 4 + 7919 * rank)
+    log(f"generating c4 workload: {args.events} events, {args.keys} users, R = {args.rate} ev/ms")
+    blocks = synth.c4_spec_stream(args.events, args.keys, rate_per_ms=args.rate, batch=BATCH)
     if args.c4_calls:
         blocks = blocks[:args.c4_calls]
     n = sum(len(b[1]) for b in blocks)
-    c = compiler.compile_app(synth.C4_QUERY)
+    text = synth.C4_EVERY_QUERY if args.c4_every else synth.C4_QUERY
+    c = compiler.compile_app(text)
+    end = synth.c4_end_time(blocks)
+    group = dist.new_group(backend="gloo") if world > 1 else None
 
     def step():
-        eng = HipEngine(c)
+        base = HipEngine(c)
+        eng = base
+        if world > 1:
+            from siddhi_amd.shard_stream import ShardedStreamEngine, TorchGroupComm
+            eng = ShardedStreamEngine(base, TorchGroupComm(group))
+        register_users(eng, blocks)
         t = time.perf_counter()
-        out = run_c4(eng, blocks, progress=log)
+        eng.start()
+        t_log = time.monotonic()
+        for i, (st, ts, cols, keys) in enumerate(blocks):
+            if time.monotonic() - t_log > 20:
+                t_log = time.monotonic()
+                log(f"{i}/{len(blocks)} send calls")
+            eng.send(st, ts, cols, [None] * len(cols), keys, 0)
+        eng.advance_time(end)
+        out = eng.drain()
         dt = time.perf_counter() - t
-        eng.close()
+        if world > 1:
+            eng.check()
+        base.close()
         return len(out["seq"]), dt
 
     for i in range(args.warmup):
@@ -215,17 +263,25 @@ def main_c4(args, torch, dist, world, rank, dev):
         m, dt = step()
         tot += dt
         log(f"step {i}: {dt * 1000:.0f} ms, {m} matches")
-    dt_t = torch.tensor([tot], dtype=torch.float64, device=dev)
+    dt_t = torch.tensor([tot, float(m)], dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    tot = float(dt_t.item())
-    value = n * world * args.steps / tot
+        dist.all_reduce(dt_t[:1], op=dist.ReduceOp.MAX, group=group)
+        dist.all_reduce(dt_t[1:], op=dist.ReduceOp.SUM, group=group)
+    tot, m = float(dt_t[0].item()), int(dt_t[1].item())
+    value = n * args.steps / tot   # the one stream, all ranks
+    # algorithmic bytes: Login / Logout 12 B, Txn 16 B, + 1 B stream
+    # tag per event; per alert seq 8 + user 4 + ip 4 + amount 4 = 20 B
+    n_txn = sum(len(b[1]) for b in blocks if b[0] == 1)
+    b_alg = 13 * n + 4 * n_txn + 20 * m
+    achieved = b_alg / (tot / args.steps)
     cpu = None
     if rank == 0 and args.cpu_sample > 0:
         from oracle_engine import OracleEngine
+        from c4_cases import run_c4
         acc, sub = 0, []
+        want = max(1_000_000, min(args.cpu_sample, 2_000_000))
         for b in blocks:
-            if acc >= args.cpu_sample:
+            if acc >= want:
                 break
             sub.append(b)
             acc += len(b[1])
@@ -234,25 +290,34 @@ def main_c4(args, torch, dist, world, rank, dev):
         run_c4(OracleEngine(c), sub)
         cdt = time.perf_counter() - t1
         cpu = {"value": acc / cdt, "unit": "events/s", "cores": 1, "kind": "port",
-               "sample": f"first {acc} events of the same C4 stream (its own send(Event[]) batches), C++ "
+               "sample": f"first {acc} events ({len(sub)} send(Event[]) calls) of the same C4 stream, C++ "
                          f"restatement of siddhi-core's processors (oracle/), 1 thread"}
     if rank == 0:
         print(json.dumps({
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": tot * 1000.0 / args.steps, "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": tot * 1000.0 / args.steps, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic", "nproc": os.cpu_count(),
             "ingest": {"path": "host buffers of every send(Event[]) call cross PCIe inside the timed step"},
-            "config": {"workload": "C4: (e1=Login and e2=Txn) -> not Logout for 5 sec, partition with (user of "
-                                   "Login, user of Txn, user of Logout), @app:playback",
-                       "events_per_gpu": n, "users_per_gpu": args.keys, "seconds": args.seconds,
-                       "send_calls": len(blocks), "matches_per_gpu": int(m),
+            "config": {"workload": ("C4: " + ("every " if args.c4_every else "") + "(e1=Login and e2=Txn) -> not "
+                                    "Logout for 5 sec, partition with (user of Login, user of Txn, user of "
+                                    "Logout), @app:playback; Login 20% / Txn 60% / Logout 20%, calls of 4,096 "
+                                    "per stream"),
+                       "events_total": n, "users": args.keys, "rate_ev_per_ms": args.rate,
+                       "send_calls": len(blocks), "matches_total": int(m),
                        "path": "streaming C-ABI from host buffers (PCIe-inclusive)",
-                       "parallelism": f"key-sharded x{world}"},
-            "roofline": None,
+                       "parallelism": (f"key-sharded x{world}: events routed per call by user, due-timer "
+                                       "candidates and scheduler-map history exchanged per time step (gloo)")
+                       if world > 1 else "one GPU"},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": 8000.0, "unit": "GB/s",
+                         "frac": achieved / 8.0e12, "traffic": None,
+                         "kernel": "whole streaming step (wall clock, PCIe and per-call launches included): "
+                                   "algorithmic bytes / step time",
+                         "algorithmic_bytes": b_alg},
             "cpu_baseline": cpu,
             "verified_vs_restatement": None,
-            "parity": "tests/test_gpu_c4.py (whole streams up to 400k users vs the oracle)"}))
+            "parity": "tests/test_gpu_c4.py, tests/test_gpu_shard_stream.py (whole streams vs the oracle, "
+                      "1M users on one GPU, 2 / 4 key-sharded virtual ranks)"}))
     if world > 1:
         dist.destroy_process_group()
 

@@ -11,7 +11,8 @@
  * Threading: calls on one handle are serialised by the caller (the reference
  * serialises a query under patternSyncObject, MultiProcessStreamReceiver.java:158).
  * Independent handles may run concurrently, each on its own HIP stream.
- * Results come back through sh_drain; the library never calls back.
+ * Results come back through sh_drain; the library never calls back, except
+ * through the coordinator a key-sharded handle is given (sh_set_coordinator).
  */
 #ifndef SIDDHI_HIP_H
 #define SIDDHI_HIP_H
@@ -172,6 +173,53 @@ int sh_snapshot(sh_handle* h, void* buf, int64_t cap, int64_t* size);
    SnapshotService.java:333-430). SH_E_INVALID_ARG: another app's image or a
    damaged one. */
 int sh_restore(sh_handle* h, const void* buf, int64_t size);
+
+/* ---- key-sharded streaming: apps with scheduler (absent) states on several GPUs
+   One process per GPU, each with a handle compiled from the same app. Every rank
+   sees every InputHandler.send(Event[]) call and pushes only the events of the
+   partition keys it owns (PartitionStreamReceiver.receive routes per key,
+   core/partition/PartitionStreamReceiver.java:176-272), keeping the call's
+   playback clock step (InputHandler.java:85-96) and global sequence numbers.
+   Keys couple only through Scheduler.onTimeChange (core/util/Scheduler.java:74-99):
+   (1) one state per distinct due time fires -- the first in the scheduler's state
+       map iteration order over ALL keys (TreeMultimap with a zero value comparator);
+   (2) that order is PartitionStateHolder's HashMap<String, ...>
+       (util/snapshot/state/PartitionStateHolder.java:36,131-162), shaped by every
+       rank's getState / returnAllStates history.
+   The handle reaches the other ranks through three callbacks, invoked at the same
+   points of the call sequence on every rank (collectives; any transport). */
+typedef struct sh_due_cand {
+    int64_t t;                   /* head notify time (the TreeMultimap key)          */
+    uint64_t order;              /* the key's position in the state map's iteration order */
+    int32_t key;                 /* partition key id                                 */
+    int32_t pad;
+} sh_due_cand;
+typedef struct sh_coordinator {
+    void* user;
+    /* one launch's scheduler-map history: this rank's records in (2 words each:
+       processing stamp, key | scheduler << 32 | kind << 48), every rank's records
+       of the launch out (*all stays valid until the next callback) */
+    int (*history)(void* user, const uint64_t* local, int64_t n_local, const uint64_t** all, int64_t* n_all);
+    /* the pick: this rank's due candidates in; out: pos[i] = position of candidate
+       i in the firing order over all ranks (-1: not fired) and *n_fire = states
+       fired over all ranks. Playback (wall == 0): the earliest `order` per distinct
+       t, fired in t order; wall clock (wall == 1): every candidate, by (t, order). */
+    int (*select)(void* user, int32_t wall, const sh_due_cand* local, int64_t n_local, int64_t* pos, int64_t* n_fire);
+    /* the minimum over the ranks of a time (wall-clock stepping through notify times) */
+    int (*min_time)(void* user, int64_t local, int64_t* global);
+} sh_coordinator;
+/* Turns the handle into one rank of a key-sharded group (before sh_start). */
+int sh_set_coordinator(sh_handle* h, const sh_coordinator* c);
+/* One send(Event[]) call of `call_n` events of which this rank owns `batch->n`
+   (may be 0): index[i] is event i's position in the call (ascending), call_last_ts
+   the call's last timestamp (the playback clock step). Trigger sequence numbers
+   and processing order are the whole call's. */
+int sh_push_batch_part(sh_handle* h, const sh_batch* batch, const uint32_t* index, int64_t call_n,
+                       int64_t call_last_ts);
+/* sh_drain plus, per row, its position in the global processing order
+   (launch << 32 | position inside the launch): the ranks' drained rows merged by
+   it (a stable sort) are the single-process output. */
+int sh_drain_ordered(sh_handle* h, sh_match_buf* out, uint64_t* order);
 
 /* library / device info */
 const char* sh_version(void);

@@ -94,6 +94,31 @@ class HipEngine:
         b.nulls = npp if any(m is not None for m in nulls) else None
         check(self.h, _lib.sh_push_batch(self.h, C.byref(b)))
 
+    def set_coordinator(self, coord):
+        """make this handle one rank of a key-sharded group (shard_stream.Coordinator)"""
+        self._coord = coord  # the callbacks must outlive the handle's use of them
+        check(self.h, _lib.sh_set_coordinator(self.h, C.byref(coord.struct())))
+
+    def send_part(self, stream, tsa, cols, nulls, keys, index, call_n, call_last):
+        """this rank's events of one send() call: index = their positions in the
+        call (uint32, ascending), call_n its size, call_last its last timestamp"""
+        tsa = np.ascontiguousarray(tsa, dtype=np.int64)
+        index = np.ascontiguousarray(index, dtype=np.uint32)
+        cols = [np.ascontiguousarray(c) for c in cols]
+        cp = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
+        npp = (C.c_void_p * max(1, len(cols)))(*[(m.ctypes.data if m is not None else None) for m in nulls])
+        b = abi.sh_batch()
+        b.stream = stream
+        b.on_device = 0
+        b.n = len(tsa)
+        b.ts = tsa.ctypes.data if len(tsa) else None
+        ka = np.ascontiguousarray(keys, dtype=np.int32) if keys is not None else None
+        b.keys = ka.ctypes.data if ka is not None and len(tsa) else None
+        b.cols = cp
+        b.nulls = npp if any(m is not None for m in nulls) else None
+        check(self.h, _lib.sh_push_batch_part(self.h, C.byref(b), index.ctypes.data if len(index) else None,
+                                              int(call_n), int(call_last)))
+
     def set_partition_keys(self, first, strings=None, utf16=None, offsets=None):
         """attr.toString() of key ids first.. (a list of str, or packed UTF-16 + offsets)"""
         from .javastr import pack_utf16
@@ -119,7 +144,9 @@ class HipEngine:
         """load an image taken from an engine of the same app (sh_restore)"""
         check(self.h, _lib.sh_restore(self.h, image, len(image)))
 
-    def drain(self):
+    def drain(self, ordered=False):
+        """ordered: also each row's position in the global processing order
+        (key-sharded handles; sh_drain_ordered)"""
         n = _lib.sh_pending(self.h)
         if n < 0:
             check(self.h, int(n))
@@ -128,6 +155,7 @@ class HipEngine:
         ts = np.zeros(n, np.int64)
         vals = np.zeros((n, self.n_out), np.int64)
         nls = np.zeros((n, self.n_out), np.uint8)
+        order = np.zeros(n, np.uint64)
         if n:
             mb = abi.sh_match_buf()
             mb.capacity = n
@@ -137,11 +165,17 @@ class HipEngine:
             mb.values = vals.ctypes.data_as(C.POINTER(C.c_int64))
             mb.nulls = nls.ctypes.data_as(C.POINTER(C.c_uint8))
             mb.n_out = self.n_out
-            check(self.h, _lib.sh_drain(self.h, C.byref(mb)))
+            if ordered:
+                check(self.h, _lib.sh_drain_ordered(self.h, C.byref(mb), order.ctypes.data))
+            else:
+                check(self.h, _lib.sh_drain(self.h, C.byref(mb)))
         # one callback chunk per (send, query): the device path keeps arrival
         # order; chunking of callbacks is cosmetic
         grp = np.zeros(n, np.int32)
-        return dict(query=q, seq=seq, ts=ts, values=vals, nulls=nls, group=grp)
+        out = dict(query=q, seq=seq, ts=ts, values=vals, nulls=nls, group=grp)
+        if ordered:
+            out["order"] = order
+        return out
 
     def close(self):
         self.handle.close()

@@ -81,6 +81,22 @@ class sh_device_run(C.Structure):
 SH_DEVICE_RUN_V2 = 2
 
 
+class sh_due_cand(C.Structure):
+    _fields_ = [("t", C.c_int64), ("order", C.c_uint64), ("key", C.c_int32), ("pad", C.c_int32)]
+
+
+# sh_coordinator callbacks (include/siddhi_hip.h, key-sharded streaming)
+HISTORY_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_int64,
+                         C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.c_int64))
+SELECT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.POINTER(sh_due_cand), C.c_int64,
+                        C.POINTER(C.c_int64), C.POINTER(C.c_int64))
+MIN_TIME_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.POINTER(C.c_int64))
+
+
+class sh_coordinator(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("history", HISTORY_FN), ("select", SELECT_FN), ("min_time", MIN_TIME_FN)]
+
+
 class sh_kernel_times(C.Structure):
     _fields_ = [("segment_ms", C.c_float), ("advance_ms", C.c_float), ("emit_ms", C.c_float),
                 ("total_ms", C.c_float), ("advance_launches", C.c_int64)]
@@ -89,7 +105,8 @@ class sh_kernel_times(C.Structure):
 # every symbol include/siddhi_hip.h declares (checked by tests/test_abi.py)
 EXPORTED = ["sh_start", "sh_compile", "sh_push_batch", "sh_advance_time", "sh_drain", "sh_pending",
             "sh_destroy", "sh_last_error", "sh_run_device", "sh_last_kernel_times",
-            "sh_version", "sh_device_count", "sh_set_partition_keys", "sh_snapshot", "sh_restore"]
+            "sh_version", "sh_device_count", "sh_set_partition_keys", "sh_snapshot", "sh_restore",
+            "sh_set_coordinator", "sh_push_batch_part", "sh_drain_ordered"]
 
 
 def bind_product(lib):
@@ -119,6 +136,12 @@ def bind_product(lib):
     lib.sh_snapshot.restype = C.c_int
     lib.sh_restore.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     lib.sh_restore.restype = C.c_int
+    lib.sh_set_coordinator.argtypes = [C.c_void_p, C.POINTER(sh_coordinator)]
+    lib.sh_set_coordinator.restype = C.c_int
+    lib.sh_push_batch_part.argtypes = [C.c_void_p, C.POINTER(sh_batch), C.c_void_p, C.c_int64, C.c_int64]
+    lib.sh_push_batch_part.restype = C.c_int
+    lib.sh_drain_ordered.argtypes = [C.c_void_p, C.POINTER(sh_match_buf), C.c_void_p]
+    lib.sh_drain_ordered.restype = C.c_int
     lib.sh_version.argtypes = []
     lib.sh_version.restype = C.c_char_p
     lib.sh_device_count.argtypes = []

@@ -373,7 +373,12 @@ struct sh_handle {
     std::vector<int64_t> o_ts;
     std::vector<int64_t> o_vals;
     std::vector<uint8_t> o_nulls;
+    std::vector<uint64_t> o_order;  // key-sharded: per row, launch << 32 | position in the launch
     int64_t o_read = 0;
+    // ---- key-sharded streaming (sh_set_coordinator): the other ranks
+    bool coord_on = false;
+    sh_coordinator coord{};
+    DevBuf w_gidx, n_gpos;
     sh_kernel_times times{};
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // [4, 5]: aggregate post-pass
     // hipRTC-specialised window kernels (sh_jit.cpp): 0 untried, 1 loaded, <0 unavailable
@@ -918,12 +923,13 @@ void sh_destroy(sh_handle* h) {
     delete h;
 }
 
-static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0);
+static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0, const uint32_t* index = nullptr, int64_t call_n = 0,
+                   int64_t call_last = 0);
 static int nf_start(sh_handle* h);
 static int nf_timers(sh_handle* h, int64_t now, bool wall = false);
 static int nf_next_due(sh_handle* h, int64_t* out);
 
-int sh_push_batch(sh_handle* h, const sh_batch* b) {
+static int push_impl(sh_handle* h, const sh_batch* b, const uint32_t* index, int64_t call_n, int64_t call_last) {
     if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !b) return SH_E_INVALID_ARG;
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
@@ -932,6 +938,17 @@ int sh_push_batch(sh_handle* h, const sh_batch* b) {
     if (h->mode == 2)
         return fail(h, SH_E_UNSUPPORTED, "rule sets larger than the general engine's query table run through "
                                          "sh_run_device only");
+    if (h->coord_on && !index)
+        return fail(h, SH_E_INVALID_ARG, "a key-sharded handle takes its events through sh_push_batch_part");
+    if (index) {
+        if (!h->coord_on) return fail(h, SH_E_INVALID_ARG, "sh_push_batch_part needs sh_set_coordinator first");
+        if (call_n <= 0 || b->n < 0 || b->n > call_n || call_n > 0xFFFFFFFFll)
+            return fail(h, SH_E_INVALID_ARG, "bad key-sharded call size");
+        for (int64_t i = 0; i < b->n; i++)
+            if ((int64_t)index[i] >= call_n || (i && index[i] <= index[i - 1]))
+                return fail(h, SH_E_INVALID_ARG, "call positions must ascend below call_n");
+        if (b->n == 0) return nf_push(h, b, h->stores[b->stream].rows, index, call_n, call_last);
+    }
     if (b->n <= 0) return SH_OK;
     auto& st = h->stores[b->stream];
     const auto& types = h->stream_types[b->stream];
@@ -966,7 +983,7 @@ int sh_push_batch(sh_handle* h, const sh_batch* b) {
     // the async copies above read caller memory: complete them before returning
     hipStreamSynchronize(h->stream);
     st.rows += b->n;
-    if (h->mode == 1) return nf_push(h, b, r0);
+    if (h->mode == 1) return nf_push(h, b, r0, index, call_n, call_last);
     for (int64_t i = 0; i < b->n; i++) {
         h->st_ts.push_back(b->ts[i]);
         h->st_stream.push_back((uint8_t)b->stream);
@@ -976,6 +993,25 @@ int sh_push_batch(sh_handle* h, const sh_batch* b) {
         if (k + 1 > h->max_key) h->max_key = k + 1;
     }
     h->seq_next += b->n;
+    return SH_OK;
+}
+
+int sh_push_batch(sh_handle* h, const sh_batch* b) { return push_impl(h, b, nullptr, 0, 0); }
+
+int sh_push_batch_part(sh_handle* h, const sh_batch* b, const uint32_t* index, int64_t call_n, int64_t call_last_ts) {
+    if (!h || !b || (b->n > 0 && !index)) return SH_E_INVALID_ARG;
+    static const uint32_t none = 0;
+    return push_impl(h, b, index ? index : &none, call_n, call_last_ts);
+}
+
+int sh_set_coordinator(sh_handle* h, const sh_coordinator* c) {
+    if (!h || !c || !c->history || !c->select || !c->min_time) return SH_E_INVALID_ARG;
+    if (h->mode != 1)
+        return fail(h, SH_E_UNSUPPORTED, "key-sharded streaming coordinates the general engine's schedulers only");
+    if (!h->partitioned) return fail(h, SH_E_UNSUPPORTED, "an unpartitioned app does not shard by key");
+    if (h->started || h->tick != 1) return fail(h, SH_E_INVALID_ARG, "set the coordinator before sh_start");
+    h->coord = *c;
+    h->coord_on = true;
     return SH_OK;
 }
 
@@ -1264,12 +1300,25 @@ static int nf_sev_apply(sh_handle* h) {
     if (h->pin_sev.ensure(64)) return fail(h, SH_E_OOM, "pinned staging");
     hipMemcpyAsync(h->pin_sev.p, h->n_sev_ctr.p, 8, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
-    const int64_t n = (int64_t)*h->pin_sev.as<unsigned long long>();
-    if (n == 0) return SH_OK;
-    if (h->pin_sev.ensure((size_t)n * 16)) return fail(h, SH_E_OOM, "pinned staging");
-    hipMemcpyAsync(h->pin_sev.p, h->n_sev.p, (size_t)n * 16, hipMemcpyDeviceToHost, st);
+    int64_t n = (int64_t)*h->pin_sev.as<unsigned long long>();
+    if (n == 0 && !h->coord_on) return SH_OK;
+    if (h->pin_sev.ensure((size_t)std::max<int64_t>(n, 1) * 16)) return fail(h, SH_E_OOM, "pinned staging");
+    if (n) hipMemcpyAsync(h->pin_sev.p, h->n_sev.p, (size_t)n * 16, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
-    if (!h->sm.apply(h->pin_sev.as<uint64_t>(), (size_t)n))
+    const uint64_t* recs = h->pin_sev.as<uint64_t>();
+    if (h->coord_on) {
+        // the launch's history of every rank: the maps model the one state map
+        // all keys share (the same launch ticks on every rank keep the stamps
+        // comparable)
+        const uint64_t* all = nullptr;
+        int64_t n_all = 0;
+        if (h->coord.history(h->coord.user, recs, n, &all, &n_all) || n_all < 0 || (n_all && !all))
+            return fail(h, SH_E_INVALID_ARG, "coordinator: history exchange failed");
+        recs = all;
+        n = n_all;
+        if (n == 0) return SH_OK;
+    }
+    if (!h->sm.apply(recs, (size_t)n))
         return fail(h, SH_E_UNSUPPORTED, "more than 2^26 scheduler map bins (keys waiting on one absent state)");
     // ranks: whole array after a resize, else the touched keys
     std::vector<int32_t> ks;
@@ -1394,7 +1443,9 @@ static void nf_put_cols(sh_handle* h, const nf_cols& cols) {
 
 // scan the per-index counts, place the records, append them to the host queue
 // (or to the caller's device buffers); returns the number of rows
-static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_seq, int64_t* d_vals, int64_t cap) {
+// (launch: the launch's tick, for the key-sharded rows' order tags)
+static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_seq, int64_t* d_vals, int64_t cap,
+                    uint64_t launch) {
     hipStream_t st = h->stream;
     if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
     hipMemcpyAsync(h->pin_rd.as<void>(PR_NREC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
@@ -1408,6 +1459,17 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
     const int64_t total = (int64_t)last_off + last_cnt;
     *rows_out = total;
     if (total == 0) return SH_OK;
+    if (h->coord_on && !d_seq) {
+        // rows are placed by (position in the launch, ordinal): each row's tag is
+        // the position whose count range holds it
+        std::vector<uint32_t> cnt((size_t)n_idx);
+        hipMemcpy(cnt.data(), h->w_cnt.p, (size_t)n_idx * 4, hipMemcpyDeviceToHost);
+        const size_t base = h->o_order.size();
+        h->o_order.reserve(base + (size_t)total);
+        for (int64_t t = 0; t < n_idx; t++)
+            for (uint32_t c = 0; c < cnt[t]; c++) h->o_order.push_back((launch << 32) | (uint64_t)t);
+        if ((int64_t)(h->o_order.size() - base) != total) return fail(h, SH_E_HIP, "order tags");
+    }
     const int stride = NF_REC_HDR + std::max(1, h->n_out);
     const int no = std::max(1, h->n_out);
     if (h->w_inv.ensure_fresh(total * 4)) return fail(h, SH_E_OOM, "placement index");
@@ -1460,12 +1522,15 @@ static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carr
 
 // `carry` (sh_run_device, single stream): ts and the stream-0 columns are moved
 // into key-segment order by the segment, so each lane streams its own events
+// gidx / n_idx (key-sharded push): each event's position in the whole send()
+// call of n_idx events (match counts and order tags are indexed by it)
 static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& cols_in, uint64_t* d_seq,
                       int64_t* d_vals, int64_t cap, int64_t* n_rows, bool fresh = false, int64_t batch_events = 0,
-                      const sh_device_run* carry_run = nullptr) {
+                      const sh_device_run* carry_run = nullptr, const uint32_t* gidx = nullptr, int64_t n_idx = 0) {
     hipStream_t st = h->stream;
     const int64_t n = B.n;
-    if (ensure_ws(h, n)) return fail(h, SH_E_OOM, "workspace");
+    if (!gidx) n_idx = n;
+    if (ensure_ws(h, std::max(n, n_idx))) return fail(h, SH_E_OOM, "workspace");
     if (nf_ensure_keys(h, nkeys)) return fail(h, SH_E_OOM, "key state");
     if (nf_ensure_recs(h, std::max<int64_t>(h->rec_cap, n + 4096))) return fail(h, SH_E_OOM, "emission buffer");
     nf_cols cols = cols_in;
@@ -1517,6 +1582,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     E.sorted_rows = sorted_cols ? 1 : 0;
     E.pad = 0;
     E.run = fresh ? h->dev_run_ids : nullptr;
+    E.gidx = gidx;
     for (int attempt = 0; attempt < 64; attempt++) {
         const size_t kw = (size_t)h->T->key_words;
         if (!fresh) {
@@ -1524,7 +1590,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
             nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, seg_list, nseg, skeys, max_seg, h->n_save.as<uint64_t>(),
                      0, st);
         }
-        hipMemsetAsync(h->w_cnt.p, 0, n * 4, st);
+        hipMemsetAsync(h->w_cnt.p, 0, n_idx * 4, st);
         hipMemsetAsync(h->n_ctr.p, 0, 8, st);
         hipMemsetAsync(h->n_err.p, 0, 4, st);
         if (h->sm_on) {
@@ -1559,7 +1625,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
             h->tick++;
             int src = nf_sev_apply(h);
             if (src) return src;
-            int rc = nf_place(h, n, n_rows, d_seq, d_vals, cap);
+            int rc = nf_place(h, n_idx, n_rows, d_seq, d_vals, cap, h->tick - 1);
             hipEventRecord(h->ev[3], st);
             hipStreamSynchronize(st);
             hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
@@ -1600,8 +1666,9 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
 }
 
-// earliest queued notify time over every scheduler and key (INT64_MAX: none)
-static int nf_next_due(sh_handle* h, int64_t* out) {
+// earliest queued notify time over every scheduler and key (INT64_MAX: none;
+// key-sharded: over every rank)
+static int nf_next_due_local(sh_handle* h, int64_t* out) {
     *out = INT64_MAX;
     if (!h->T->has_absent || h->n_nkeys == 0) return SH_OK;
     hipStream_t st = h->stream;
@@ -1628,11 +1695,24 @@ static int nf_next_due(sh_handle* h, int64_t* out) {
     return SH_OK;
 }
 
+static int nf_next_due(sh_handle* h, int64_t* out) {
+    int rc = nf_next_due_local(h, out);
+    if (rc || !h->coord_on) return rc;
+    int64_t g = INT64_MAX;
+    if (h->coord.min_time(h->coord.user, *out, &g)) return fail(h, SH_E_INVALID_ARG, "coordinator: min_time failed");
+    *out = g;
+    return SH_OK;
+}
+
 // Scheduler.onTimeChange(now) for every scheduler (absent pre-state) in creation
 // order. wall: the EventCaller form outside playback (Scheduler.java:285-300) --
 // every due key fires on its own, no collapse of equal due times.
+// Key-sharded (coord_on): every rank takes every step (the coordinator calls are
+// collectives); the pick runs over all ranks' candidates and the firing order
+// positions are global, so registration stamps and row order match one process.
 static int nf_timers(sh_handle* h, int64_t now, bool wall) {
-    if (!h->T->has_absent || h->n_nkeys == 0) return SH_OK;
+    if (!h->T->has_absent) return SH_OK;
+    if (h->n_nkeys == 0 && !h->coord_on) return SH_OK;
     hipStream_t st = h->stream;
     if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
     nf_put_cols(h, nf_store_cols(h));
@@ -1645,44 +1725,73 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
         for (int si = 0; si < h->T->q[q].n_sched; si++) {
             const int p = h->T->q[q].sched_seq[si];
             const int32_t nkeys = h->n_nkeys;
-            // due keys
-            if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");
-            hipMemsetAsync(h->n_ctr.p, 0, 8, st);
-            const uint64_t* rank = h->sm_on ? h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>() : nullptr;
-            if (armed_flags(h) && h->n_arm_log.p) {
-                // the armed-key list (+ the keys armed since the last pass on the
-                // first scheduler's pass, which also rebuilds the list)
-                unsigned long long* ln = h->n_klist_n.as<unsigned long long>();
-                const int c = h->klist_cur;
-                if (first_pass) {
-                    hipMemsetAsync(ln + (c ^ 1), 0, 8, st);
-                    nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
-                                 ln + c, h->n_arm_log.as<int32_t>(), h->n_arm_ctr.as<unsigned long long>(), now,
-                                 h->n_cand.as<nfd_cand>(), h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h),
-                                 n_absent == 1 ? 1 : 0, rank, h->n_klist[c ^ 1].as<int32_t>(), ln + (c ^ 1),
-                                 (int64_t)nkeys, st);
-                    hipMemsetAsync(h->n_arm_ctr.p, 0, 8, st);
-                    h->klist_cur ^= 1;
-                    first_pass = false;
+            unsigned long long nc = 0;
+            if (nkeys > 0) {
+                // due keys
+                if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");
+                hipMemsetAsync(h->n_ctr.p, 0, 8, st);
+                const uint64_t* rank = h->sm_on ? h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>() : nullptr;
+                if (armed_flags(h) && h->n_arm_log.p) {
+                    // the armed-key list (+ the keys armed since the last pass on the
+                    // first scheduler's pass, which also rebuilds the list)
+                    unsigned long long* ln = h->n_klist_n.as<unsigned long long>();
+                    const int c = h->klist_cur;
+                    if (first_pass) {
+                        hipMemsetAsync(ln + (c ^ 1), 0, 8, st);
+                        nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
+                                     ln + c, h->n_arm_log.as<int32_t>(), h->n_arm_ctr.as<unsigned long long>(), now,
+                                     h->n_cand.as<nfd_cand>(), h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h),
+                                     n_absent == 1 ? 1 : 0, rank, h->n_klist[c ^ 1].as<int32_t>(), ln + (c ^ 1),
+                                     (int64_t)nkeys, st);
+                        hipMemsetAsync(h->n_arm_ctr.p, 0, 8, st);
+                        h->klist_cur ^= 1;
+                        first_pass = false;
+                    } else {
+                        nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
+                                     ln + c, nullptr, nullptr, now, h->n_cand.as<nfd_cand>(),
+                                     h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), 0, rank, nullptr, nullptr,
+                                     (int64_t)nkeys, st);
+                    }
                 } else {
-                    nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
-                                 ln + c, nullptr, nullptr, now, h->n_cand.as<nfd_cand>(),
-                                 h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), 0, rank, nullptr, nullptr,
-                                 (int64_t)nkeys, st);
+                    nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, now, h->n_cand.as<nfd_cand>(),
+                            h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0, rank, st);
                 }
-            } else {
-                nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, now, h->n_cand.as<nfd_cand>(),
-                        h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0, rank, st);
+                hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
+                if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
+                nc = *h->pin_rd.as<unsigned long long>(PR_NC);
             }
-            hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
-            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
-            const unsigned long long nc = *h->pin_rd.as<unsigned long long>(PR_NC);
-            if (nc == 0) continue;
+            if (nc == 0 && !h->coord_on) continue;
             // TreeMultimap<Long, SchedulerState> with a zero comparator: one key per
             // distinct due time, the first in keyOrder (earliest registration)
             std::vector<int32_t> sel;
+            std::vector<uint32_t> gpos;  // key-sharded: firing positions over all ranks
+            int64_t n_idx = 0;           // positions in the launch (match counts)
             bool picked = false;
-            if ((int64_t)nc >= kDeviceTieBreak && !wall) {
+            if (h->coord_on) {
+                std::vector<nfd_cand> cs(nc);
+                if (nc) hipMemcpy(cs.data(), h->n_cand.p, nc * sizeof(nfd_cand), hipMemcpyDeviceToHost);
+                std::vector<int64_t> pos(nc, -1);
+                int64_t n_fire = 0;
+                static_assert(sizeof(nfd_cand) == sizeof(sh_due_cand), "candidate layout");
+                if (h->coord.select(h->coord.user, wall ? 1 : 0, (const sh_due_cand*)cs.data(), (int64_t)nc, pos.data(),
+                                    &n_fire))
+                    return fail(h, SH_E_INVALID_ARG, "coordinator: select failed");
+                if (n_fire == 0) continue;  // every rank skips this launch
+                std::vector<std::pair<int64_t, int32_t>> mine;
+                for (size_t i = 0; i < cs.size(); i++)
+                    if (pos[i] >= 0) {
+                        if (pos[i] >= n_fire) return fail(h, SH_E_INVALID_ARG, "coordinator: position out of range");
+                        mine.emplace_back(pos[i], cs[i].key);
+                    }
+                std::sort(mine.begin(), mine.end());
+                for (auto& m : mine) {
+                    sel.push_back(m.second);
+                    gpos.push_back((uint32_t)m.first);
+                }
+                n_idx = n_fire;
+                picked = true;
+            }
+            if (!picked && (int64_t)nc >= kDeviceTieBreak && !wall) {
                 // large backlog of due keys: pick on the device (slot per due time)
                 if (h->n_tmin.ensure_fresh(8)) return fail(h, SH_E_OOM, "timer tie-break");
                 nfd_cand_tmin(h->n_cand.as<nfd_cand>(), (int64_t)nc, h->n_tmin.as<unsigned long long>(), st);
@@ -1715,20 +1824,27 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
                     if (wall || i == 0 || cs[i].t != cs[i - 1].t) sel.push_back(cs[i].key);
             }
             const int32_t ns = (int32_t)sel.size();
-            if (h->n_sel.ensure_fresh((size_t)ns * 4) || h->n_save.ensure_fresh((size_t)ns * h->T->key_words * 8))
+            if (!h->coord_on) n_idx = ns;
+            if (h->n_sel.ensure_fresh((size_t)std::max(ns, 1) * 4) ||
+                h->n_save.ensure_fresh((size_t)std::max(ns, 1) * h->T->key_words * 8) ||
+                h->n_gpos.ensure_fresh((size_t)std::max(ns, 1) * 4))
                 return fail(h, SH_E_OOM, "timer keys");
-            if (h->pin_out.ensure((size_t)ns * 4)) return fail(h, SH_E_OOM, "pinned staging");
-            memcpy(h->pin_out.p, sel.data(), (size_t)ns * 4);  // read by the copy before the loop's sync
-            hipMemcpyAsync(h->n_sel.p, h->pin_out.p, (size_t)ns * 4, hipMemcpyHostToDevice, st);
-            if (ensure_ws(h, ns)) return fail(h, SH_E_OOM, "workspace");
+            if (h->pin_out.ensure((size_t)std::max(ns, 1) * 8)) return fail(h, SH_E_OOM, "pinned staging");
+            if (ns) {
+                memcpy(h->pin_out.p, sel.data(), (size_t)ns * 4);  // read by the copies before the loop's sync
+                hipMemcpyAsync(h->n_sel.p, h->pin_out.p, (size_t)ns * 4, hipMemcpyHostToDevice, st);
+                if (h->coord_on) {
+                    memcpy(h->pin_out.as<uint8_t>((size_t)ns * 4), gpos.data(), (size_t)ns * 4);
+                    hipMemcpyAsync(h->n_gpos.p, h->pin_out.as<uint8_t>((size_t)ns * 4), (size_t)ns * 4,
+                                   hipMemcpyHostToDevice, st);
+                }
+            }
+            if (ensure_ws(h, std::max<int64_t>(n_idx, 1))) return fail(h, SH_E_OOM, "workspace");
             if (nf_ensure_recs(h, std::max<int64_t>(h->rec_cap, ns + 4096))) return fail(h, SH_E_OOM, "emission");
             for (int attempt = 0;; attempt++) {
                 if (attempt > 64) return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
                 const size_t kw = (size_t)h->T->key_words;
-                if (h->n_save.ensure_fresh((size_t)ns * kw * 8)) return fail(h, SH_E_OOM, "save area");
-                nfd_save_keys(h->n_kstate.as<uint64_t>(), (int64_t)kw, h->n_sel.as<int32_t>(), ns,
-                              h->n_save.as<uint64_t>(), 0, st);
-                hipMemsetAsync(h->w_cnt.p, 0, (size_t)ns * 4, st);
+                hipMemsetAsync(h->w_cnt.p, 0, (size_t)n_idx * 4, st);
                 hipMemsetAsync(h->n_ctr.p, 0, 8, st);
                 hipMemsetAsync(h->n_err.p, 0, 4, st);
                 if (h->sm_on) {
@@ -1737,9 +1853,14 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
                     if (nf_sev_ready(h, ns)) return fail(h, SH_E_OOM, "scheduler history");
                     if (sev0 != h->n_sev.p || cap0 != h->sev_cap || attempt > 0) nf_put_cols(h, nf_store_cols(h));
                 }
+                if (ns == 0) break;  // key-sharded: another rank fires this launch
+                if (h->n_save.ensure_fresh((size_t)ns * kw * 8)) return fail(h, SH_E_OOM, "save area");
+                nfd_save_keys(h->n_kstate.as<uint64_t>(), (int64_t)kw, h->n_sel.as<int32_t>(), ns,
+                              h->n_save.as<uint64_t>(), 0, st);
                 nfd_emit em = nf_emit(h);
                 nfd_timer(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), q, p,
-                          h->n_sel.as<int32_t>(), ns, now, h->tick, h->clock, h->seq_next, &em, st);
+                          h->n_sel.as<int32_t>(), ns, now, h->tick, h->clock, h->seq_next, &em, st,
+                          h->coord_on ? h->n_gpos.as<uint32_t>() : nullptr);
                 hipMemcpyAsync(h->pin_rd.as<void>(PR_ERR), h->n_err.p, 4, hipMemcpyDeviceToHost, st);
                 if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_timer");
                 unsigned err = *h->pin_rd.as<unsigned>(PR_ERR);
@@ -1765,7 +1886,7 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
                 if (src) return src;
             }
             int64_t rows = 0;
-            int rc = nf_place(h, ns, &rows, nullptr, nullptr, 0);
+            int rc = nf_place(h, n_idx, &rows, nullptr, nullptr, 0, h->tick - 1);
             if (rc) return rc;
         }
     }
@@ -1792,14 +1913,18 @@ static int nf_start(sh_handle* h) {
 }
 
 // InputHandler.send(Event[]) on the general engine: playback clock + due timers
-// first (InputHandler.java:85-96), then the batch
-static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0) {
+// first (InputHandler.java:85-96), then the batch. index (key-sharded): the
+// positions of this rank's events in the whole call of call_n events, whose last
+// timestamp is call_last; the rank takes every step of the call even when it owns
+// none of its events (the coordinator's exchanges are collectives).
+static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0, const uint32_t* index, int64_t call_n,
+                   int64_t call_last) {
     if (!h->started) {
         int rc = nf_start(h);
         if (rc) return rc;
     }
     if (h->app.playback) {
-        const int64_t last = b->ts[b->n - 1];
+        const int64_t last = index ? call_last : b->ts[b->n - 1];
         if (last >= h->clock) {
             h->clock = last;
             int rc = nf_timers(h, last);
@@ -1808,6 +1933,16 @@ static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0) {
     }
     const int64_t n = b->n;
     hipStream_t st = h->stream;
+    if (index && n == 0) {
+        // none of the call's events is ours: the launch still ticks and its
+        // (empty) scheduler history joins the others'
+        if (h->sm_on && nf_sev_ready(h, 0)) return fail(h, SH_E_OOM, "scheduler history");
+        h->tick++;
+        int rc = nf_sev_apply(h);
+        h->seq_next += call_n;
+        h->seq_staged0 = h->seq_next;
+        return rc;
+    }
     // staged in pinned memory (pin_in; the column copies of this call are complete)
     const size_t o_ts = 0, o_rows = (size_t)n * 8, o_keys = o_rows + (size_t)n * 4, o_sv = o_keys + (size_t)n * 4;
     if (h->pin_in.ensure(o_sv + (size_t)n)) return fail(h, SH_E_OOM, "pinned staging");
@@ -1843,8 +1978,14 @@ static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0) {
     B.seq_base = h->seq_next;
     B.n = n;
     int64_t nrows = 0;
-    int rc = nf_process(h, B, nk, nf_store_cols(h), nullptr, nullptr, 0, &nrows);
-    h->seq_next += n;
+    const uint32_t* gidx = nullptr;
+    if (index) {
+        if (h->w_gidx.ensure_fresh((size_t)n * 4)) return fail(h, SH_E_OOM, "staging");
+        hipMemcpyAsync(h->w_gidx.p, index, (size_t)n * 4, hipMemcpyHostToDevice, st);
+        gidx = h->w_gidx.as<uint32_t>();
+    }
+    int rc = nf_process(h, B, nk, nf_store_cols(h), nullptr, nullptr, 0, &nrows, false, 0, nullptr, gidx, call_n);
+    h->seq_next += index ? call_n : n;
     h->seq_staged0 = h->seq_next;
     return rc;
 }
@@ -1951,7 +2092,7 @@ int64_t sh_pending(sh_handle* h) {
     return (int64_t)h->o_seq.size() - h->o_read;
 }
 
-int sh_drain(sh_handle* h, sh_match_buf* out) {
+static int drain_impl(sh_handle* h, sh_match_buf* out, uint64_t* order) {
     if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !out) return SH_E_INVALID_ARG;
     int rc = flush(h);
@@ -1959,8 +2100,11 @@ int sh_drain(sh_handle* h, sh_match_buf* out) {
     const int64_t avail = (int64_t)h->o_seq.size() - h->o_read;
     const int64_t k = std::min(avail, out->capacity);
     const int no = out->n_out;
+    if (order && h->o_order.size() != h->o_seq.size())
+        return fail(h, SH_E_INVALID_ARG, "order tags exist on key-sharded handles only");
     for (int64_t i = 0; i < k; i++) {
         const int64_t r = h->o_read + i;
+        if (order) order[i] = h->o_order[r];
         if (out->query) out->query[i] = h->o_query[r];
         if (out->trigger_seq) out->trigger_seq[i] = h->o_seq[r];
         if (out->ts) out->ts[i] = h->o_ts[r];
@@ -1978,10 +2122,14 @@ int sh_drain(sh_handle* h, sh_match_buf* out) {
         h->o_ts.clear();
         h->o_vals.clear();
         h->o_nulls.clear();
+        h->o_order.clear();
         h->o_read = 0;
     }
     return avail > k ? SH_E_MORE : SH_OK;
 }
+
+int sh_drain(sh_handle* h, sh_match_buf* out) { return drain_impl(h, out, nullptr); }
+int sh_drain_ordered(sh_handle* h, sh_match_buf* out, uint64_t* order) { return drain_impl(h, out, order); }
 
 static int bits_for(uint64_t v) {
     int b = 0;
@@ -2916,6 +3064,7 @@ static int snapshot_image(sh_handle* h, SnapW& w) {
 extern "C" {
 
 int sh_snapshot(sh_handle* h, void* buf, int64_t cap, int64_t* size) {
+    if (h && h->coord_on) return fail(h, SH_E_UNSUPPORTED, "snapshots of key-sharded handles are not supported");
     if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !size || (cap > 0 && !buf)) return SH_E_INVALID_ARG;
     SnapW w;

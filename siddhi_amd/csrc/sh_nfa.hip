@@ -60,7 +60,9 @@ struct DevEvents {
     const int64_t* sts;
     int32_t sorted_rows;
     const uint32_t* run;    // caller's run ids by arrival index (NULL: from adjacency and the send() call)
+    const uint32_t* gidx;   // key-sharded push: position of each event in the whole send() call
     __device__ uint32_t at(int64_t k) const { return perm ? perm[k] : (uint32_t)k; }
+    __device__ uint32_t pos(int64_t k) const { return gidx ? gidx[at(k)] : at(k); }
 };
 // the Events interface of nf_process_segment / NfLane::receive
 struct DevEv {
@@ -72,9 +74,9 @@ struct DevEv {
         if (E->sorted_rows) return (uint32_t)k;
         return E->row ? E->row[E->at(k)] : E->at(k);
     }
-    __device__ uint64_t seq(int64_t k) const { return E->seq_base + E->at(k); }
+    __device__ uint64_t seq(int64_t k) const { return E->seq_base + E->pos(k); }
     __device__ int stream(int64_t k) const { return E->stream ? E->stream[E->at(k)] : 0; }
-    __device__ uint32_t local(int64_t k) const { return E->at(k); }
+    __device__ uint32_t local(int64_t k) const { return E->pos(k); }
     __device__ uint32_t batch(int64_t k) const {
         return E->bid ? E->bid[E->at(k)] : (E->batch_events ? (uint32_t)(E->at(k) / E->batch_events) : 0u);
     }
@@ -406,9 +408,11 @@ __global__ void __launch_bounds__(256) k_cand_pick(const nfd_cand* __restrict__ 
 __global__ void __launch_bounds__(NF_TPB) k_nfa_timer(const nf_table* __restrict__ T, const nf_cols* __restrict__ C,
                                                       uint64_t* __restrict__ kstate, int q, int p,
                                                       const int32_t* __restrict__ keys, int32_t nsel, int64_t now,
-                                                      uint64_t tick, int64_t clock, uint64_t seq, nfd_emit EM) {
-    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nsel) return;
+                                                      uint64_t tick, int64_t clock, uint64_t seq, nfd_emit EM,
+                                                      const uint32_t* __restrict__ gpos) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nsel) return;
+    const uint32_t r = gpos ? gpos[i] : (uint32_t)i;  // position in the firing order
     DevSink sink;
     sink.buf = EM.recs;
     sink.ctr = EM.ctr;
@@ -417,7 +421,7 @@ __global__ void __launch_bounds__(NF_TPB) k_nfa_timer(const nf_table* __restrict
     sink.chunk = nullptr;
     sink.used = sink.n = 0;
     NfLane<DevSink> L;
-    lane_init(L, T, C, kstate + (int64_t)keys[r] * T->key_words, &sink, clock, keys[r]);
+    lane_init(L, T, C, kstate + (int64_t)keys[i] * T->key_words, &sink, clock, keys[i]);
     L.Q = &T->q[q];
     L.qb = L.kb + L.Q->q_off;
     L.qi = q;
@@ -547,6 +551,7 @@ extern "C" int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, 
     E.seq_base = ev->seq_base;
     E.batch_events = ev->batch_events;
     E.run = ev->run;
+    E.gidx = ev->gidx;
     E.sts = ev->sts;
     E.sorted_rows = ev->sorted_rows;
     if (max_segments < 1) max_segments = 1;
@@ -567,6 +572,7 @@ extern "C" int nfd_seq3(const nf_table* dT, const nf_cols* dC, const nfd_events*
     E.seq_base = ev->seq_base;
     E.batch_events = ev->batch_events;
     E.run = ev->run;
+    E.gidx = ev->gidx;
     E.sts = ev->sts;
     E.sorted_rows = ev->sorted_rows;
     if (max_segments < 1) max_segments = 1;
@@ -645,10 +651,10 @@ extern "C" int nfd_cand_select(const nfd_cand* cand, int64_t nc, int64_t tmin, i
 
 extern "C" int nfd_timer(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, int q, int p, const int32_t* keys,
                          int32_t nsel, int64_t now, uint64_t tick, int64_t clock, uint64_t seq, const nfd_emit* em,
-                         void* stream) {
+                         void* stream, const uint32_t* gpos) {
     if (nsel <= 0) return 0;
     hipLaunchKernelGGL(k_nfa_timer, dim3(nf_blocks(nsel, NF_TPB)), dim3(NF_TPB), 0, (hipStream_t)stream, dT, dC,
-                       kstate, q, p, keys, nsel, now, tick, clock, seq, *em);
+                       kstate, q, p, keys, nsel, now, tick, clock, seq, *em, gpos);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

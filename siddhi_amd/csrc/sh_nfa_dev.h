@@ -29,6 +29,7 @@ struct nfd_events {
     int32_t sorted_rows;           // 1: column rows are key-segment positions (columns carried by the segment)
     int32_t pad;
     const uint32_t* run;           // caller's PartitionStreamReceiver run per arrival index (sh_device_run.d_run), NULL: none
+    const uint32_t* gidx;          // key-sharded push: arrival index -> position in the whole send() call, NULL: identity
 };
 
 struct nfd_cand {
@@ -73,9 +74,12 @@ int nfd_rank_scatter(const int32_t* keys, const uint64_t* ranks, int64_t n, uint
 int nfd_cand_tmin(const nfd_cand* cand, int64_t nc, unsigned long long* tmin, void* stream);
 int nfd_cand_select(const nfd_cand* cand, int64_t nc, int64_t tmin, int64_t range, unsigned long long* slot_stamp,
                     int32_t* slot_key, void* stream);
-// seq: trigger sequence number of the rows the timers emit (the next input event's)
+// seq: trigger sequence number of the rows the timers emit (the next input event's);
+// gpos (may be NULL): per selected key its position in the firing order over all
+// ranks (key-sharded), which orders its rows and registration stamps
 int nfd_timer(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, int q, int p, const int32_t* keys, int32_t nsel,
-              int64_t now, uint64_t tick, int64_t clock, uint64_t seq, const nfd_emit* em, void* stream);
+              int64_t now, uint64_t tick, int64_t clock, uint64_t seq, const nfd_emit* em, void* stream,
+              const uint32_t* gpos = nullptr);
 int nfd_place(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets, int n_out, int32_t* out_query,
               uint64_t* out_seq, int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, uint32_t* inv, int64_t total,
               void* stream);

@@ -14,22 +14,28 @@ import numpy as np
 def running(group, x, kind):
     """group: per row the (query, key) segment; x: per row the addend (float64,
     or int64 for long sums); kind: 'sum' | 'avg' | 'count'. Returns the running
-    values (float64, or int64 for count and long sums) in row order."""
+    values (float64, or int64 for count and long sums) in row order. The groups
+    are laid out as the rows of a padded 2-D array and accumulated along its
+    columns: each group is still a left-to-right chain of additions."""
     n = len(group)
+    out_t = np.int64 if (kind == "count" or (x is not None and x.dtype == np.int64)) else np.float64
+    if n == 0:
+        return np.zeros(0, out_t)
     order = np.argsort(group, kind="stable")
     g = group[order]
-    starts = np.flatnonzero(np.r_[True, g[1:] != g[:-1]]) if n else np.zeros(0, np.int64)
-    ends = np.r_[starts[1:], n] if n else np.zeros(0, np.int64)
-    out = np.empty(n, np.int64 if (kind == "count" or x.dtype == np.int64) else np.float64)
-    xs = x[order] if x is not None else None
-    for a, b in zip(starts, ends):
-        if kind == "count":
-            r = np.arange(1, b - a + 1, dtype=np.int64)
-        elif kind == "avg":
-            r = np.add.accumulate(xs[a:b]) / np.arange(1, b - a + 1, dtype=np.float64)
-        else:
-            r = np.add.accumulate(xs[a:b])
-        out[order[a:b]] = r
+    starts = np.flatnonzero(np.r_[True, g[1:] != g[:-1]])
+    lens = np.diff(np.r_[starts, n])
+    gi = np.repeat(np.arange(len(starts)), lens)            # group index per sorted row
+    col = np.arange(n) - np.repeat(starts, lens)             # position inside its group
+    ordinal = (col + 1).astype(np.int64)
+    out = np.empty(n, out_t)
+    if kind == "count":
+        out[order] = ordinal
+        return out
+    grid = np.zeros((len(starts), int(lens.max())), x.dtype)
+    grid[gi, col] = x[order]
+    acc = np.add.accumulate(grid, axis=1)[gi, col]
+    out[order] = acc / ordinal.astype(np.float64) if kind == "avg" else acc
     return out
 
 

@@ -78,6 +78,10 @@ struct nfh {
     std::vector<uint64_t> sev;
     unsigned long long sev_n = 0;
     uint64_t next_seq = 0;  // sequence number of the next input event
+    // key-sharded streaming (sh_coordinator, as sh_host.cpp drives it)
+    bool coord_on = false;
+    sh_coordinator coord{};
+    std::vector<uint64_t> order;  // per output row: launch << 32 | position in the launch
 };
 
 static int width(int t) {
@@ -107,10 +111,24 @@ static nf_cols host_cols(nfh* h) {
     return c;
 }
 
-// a launch's getState history -> the order models
+// a launch's getState history -> the order models (key-sharded: every rank's)
 static int apply_history(nfh* h) {
-    if (!h->sm_on || h->sev_n == 0) return 0;
-    if (!h->sm.apply(h->sev.data(), (size_t)h->sev_n)) {
+    if (!h->sm_on) return 0;
+    const uint64_t* recs = h->sev.data();
+    int64_t n = (int64_t)h->sev_n;
+    if (h->coord_on) {
+        const uint64_t* all = nullptr;
+        int64_t n_all = 0;
+        if (h->coord.history(h->coord.user, recs, n, &all, &n_all)) {
+            h->err = "coordinator: history exchange failed";
+            return -1;
+        }
+        recs = all;
+        n = n_all;
+    }
+    h->sev_n = 0;
+    if (n == 0) return 0;
+    if (!h->sm.apply(recs, (size_t)n)) {
         h->err = "scheduler map beyond the rank encoding";
         return -4;
     }
@@ -118,7 +136,6 @@ static int apply_history(nfh* h) {
         h->sm.maps[s].dirty.clear();
         h->sm.maps[s].rerank_all = false;
     }
-    h->sev_n = 0;
     return 0;
 }
 
@@ -178,7 +195,7 @@ static bool grow(nfh* h, uint32_t err) {
     return true;
 }
 
-static void take_records(nfh* h, HostSink& sink, int32_t nq) {
+static void take_records(nfh* h, HostSink& sink, int32_t nq, uint64_t launch) {
     // records are appended per lane; order them by (tag index, ordinal)
     struct R {
         uint64_t tag;
@@ -212,6 +229,7 @@ static void take_records(nfh* h, HostSink& sink, int32_t nq) {
             o.nul.push_back((uint8_t)((r[2] >> c) & 1));
         }
         h->out.push_back(std::move(o));
+        if (h->coord_on) h->order.push_back((launch << 32) | (uint32_t)x.tag);
     }
 }
 
@@ -233,23 +251,20 @@ static NfLane<HostSink> make_lane(nfh* h, const nf_cols* C, HostSink* sink, int3
 // collapse of equal due times
 static int timers(nfh* h, int64_t now, bool wall = false) {
     if (!h->T.has_absent) return 0;
-    for (int attempt = 0; attempt < 40; attempt++) {
-        std::vector<uint64_t> backup = h->kstate;
-        const size_t out0 = h->out.size();
-        uint32_t err = 0;
-        nf_cols C = host_cols(h);
-        for (int q = 0; q < h->T.n_queries && !err; q++) {
-            const nf_query& Q = h->T.q[q];
-            for (int si = 0; si < Q.n_sched && !err; si++) {
-                const int p = Q.sched_seq[si];
-                // due keys: head <= now; one key per distinct due time (TreeMultimap
-                // with a zero comparator), the earliest-registered wins
-                struct Cand {
-                    int64_t t;
-                    uint64_t stamp;
-                    int32_t key;
-                };
-                std::vector<Cand> cs;
+    for (int q = 0; q < h->T.n_queries; q++) {
+        const nf_query& Q = h->T.q[q];
+        for (int si = 0; si < Q.n_sched; si++) {
+            const int p = Q.sched_seq[si];
+            // due keys: head <= now; one key per distinct due time (TreeMultimap
+            // with a zero comparator), the earliest-registered wins
+            struct Cand {
+                int64_t t;
+                uint64_t stamp;
+                int32_t key;
+            };
+            std::vector<Cand> cs;
+            {
+                nf_cols C = host_cols(h);
                 for (int32_t k = 0; k < h->nkeys; k++) {
                     NfLane<HostSink> L = make_lane(h, &C, nullptr, k);
                     L.Q = &Q;
@@ -262,41 +277,70 @@ static int timers(nfh* h, int64_t now, bool wall = false) {
                                                                      : (L.sched(p)[1] & ~(1ull << 63));
                     if (L.sched_head(p, &t) && t <= now) cs.push_back({t, rank, k});
                 }
+            }
+            // the fired keys with their positions in the firing order
+            std::vector<std::pair<uint32_t, int32_t>> fire;
+            if (h->coord_on) {
+                std::vector<sh_due_cand> dc(cs.size());
+                for (size_t i = 0; i < cs.size(); i++) dc[i] = {cs[i].t, cs[i].stamp, cs[i].key, 0};
+                std::vector<int64_t> pos(cs.size(), -1);
+                int64_t n_fire = 0;
+                if (h->coord.select(h->coord.user, wall ? 1 : 0, dc.data(), (int64_t)dc.size(), pos.data(), &n_fire)) {
+                    h->err = "coordinator: select failed";
+                    return -1;
+                }
+                if (n_fire == 0) continue;
+                for (size_t i = 0; i < cs.size(); i++)
+                    if (pos[i] >= 0) fire.emplace_back((uint32_t)pos[i], cs[i].key);
+                std::sort(fire.begin(), fire.end());
+            } else {
+                if (cs.empty()) continue;
                 std::sort(cs.begin(), cs.end(), [](const Cand& a, const Cand& b) {
                     if (a.t != b.t) return a.t < b.t;
                     return a.stamp < b.stamp;
                 });
-                HostSink sink;
                 uint32_t rank = 0;
                 for (size_t i = 0; i < cs.size(); i++) {
                     if (i && cs[i].t == cs[i - 1].t && !wall) continue;
-                    NfLane<HostSink> L = make_lane(h, &C, &sink, cs[i].key);
+                    fire.emplace_back(rank++, cs[i].key);
+                }
+            }
+            // sendTimerEvents per fired key (state growth: restore, grow, replay)
+            HostSink sink;
+            for (int attempt = 0;; attempt++) {
+                if (attempt >= 40) {
+                    h->err = "state overflow in timers";
+                    return -5;
+                }
+                std::vector<uint64_t> backup = h->kstate;
+                nf_cols C = host_cols(h);
+                sink = HostSink();
+                uint32_t err = 0;
+                for (auto& f : fire) {
+                    NfLane<HostSink> L = make_lane(h, &C, &sink, f.second);
                     L.Q = &Q;
                     L.qb = L.kb + Q.q_off;
                     L.qi = q;
-                    L.tag_index = rank++;
+                    L.tag_index = f.first;
                     L.cur_seq = h->next_seq;
                     L.stamp = (h->tick << 32) | L.tag_index;
                     L.send_timer_events(p, now);
                     err |= L.err;
                 }
-                h->tick++;
-                if (!err) {
-                    take_records(h, sink, h->T.n_queries);
-                    const int rc = apply_history(h);
-                    if (rc) return rc;
+                if (!err) break;
+                h->kstate.swap(backup);
+                if ((err & (NF_E_UNSUP | NF_E_EMIT | NF_E_KEY)) || !grow(h, err)) {
+                    h->err = "state overflow / unsupported in timers";
+                    return -5;
                 }
             }
-        }
-        if (!err) return 0;
-        h->kstate.swap(backup);
-        h->out.resize(out0);
-        if ((err & (NF_E_UNSUP | NF_E_EMIT | NF_E_KEY)) || !grow(h, err)) {
-            h->err = "state overflow / unsupported in timers";
-            return -5;
+            h->tick++;
+            take_records(h, sink, h->T.n_queries, h->tick - 1);
+            const int rc = apply_history(h);
+            if (rc) return rc;
         }
     }
-    return -5;
+    return 0;
 }
 
 extern "C" {
@@ -377,12 +421,19 @@ static int64_t next_due(nfh* h) {
     return tmin;
 }
 
+static int64_t next_due_all(nfh* h) {
+    int64_t t = next_due(h), g = t;
+    if (h->coord_on && h->coord.min_time(h->coord.user, t, &g)) return INT64_MIN;
+    return g;
+}
+
 int nfh_advance_time(nfh* h, int64_t now) {
     if (now < h->clock) return 0;
     if (!h->T.playback) {
         // wall clock: step through every queued notify time
         for (;;) {
-            const int64_t t = next_due(h);
+            const int64_t t = next_due_all(h);
+            if (t == INT64_MIN) return -1;
             if (t > now) break;
             h->clock = std::max(h->clock, t);
             const int rc = timers(h, h->clock, true);
@@ -395,8 +446,11 @@ int nfh_advance_time(nfh* h, int64_t now) {
     return timers(h, now);
 }
 
-int nfh_send(nfh* h, const sh_batch* b, uint64_t first_seq) {
-    if (b->n <= 0) return 0;
+// index (key-sharded): positions of this rank's events in the whole call of
+// call_n events whose last timestamp is call_last (the rank takes every step)
+static int send_impl(nfh* h, const sh_batch* b, uint64_t first_seq, const uint32_t* index, int64_t call_n,
+                     int64_t call_last) {
+    if (b->n <= 0 && !index) return 0;
     const int s = b->stream;
     const int64_t r0 = h->rows[s];
     for (int a = 0; a < h->T.stream_nattr[s]; a++) {
@@ -416,10 +470,10 @@ int nfh_send(nfh* h, const sh_batch* b, uint64_t first_seq) {
     // InputHandler.send in playback: clock -> last timestamp, due timers first
     h->next_seq = first_seq;
     if (h->T.playback) {
-        int rc = nfh_advance_time(h, b->ts[b->n - 1]);
+        int rc = nfh_advance_time(h, index ? call_last : b->ts[b->n - 1]);
         if (rc) return rc;
     }
-    h->next_seq = first_seq + (uint64_t)b->n;
+    h->next_seq = first_seq + (uint64_t)(index ? call_n : b->n);
     // stable segment by key (null keys dropped)
     std::vector<Ev> evs;
     int32_t maxk = 0;
@@ -433,7 +487,8 @@ int nfh_send(nfh* h, const sh_batch* b, uint64_t first_seq) {
     for (int64_t i = 0; i < b->n; i++) {
         int32_t k = h->T.partitioned ? (b->keys ? b->keys[i] : 0) : 0;
         if (k < 0) continue;
-        byKey[k].push_back({b->ts[i], (uint32_t)(r0 + i), first_seq + i, s, (uint32_t)i, 0});
+        const uint32_t at = index ? index[i] : (uint32_t)i;  // position in the call
+        byKey[k].push_back({b->ts[i], (uint32_t)(r0 + i), first_seq + at, s, at, 0});
     }
     for (int attempt = 0; attempt < 40; attempt++) {
         std::vector<uint64_t> backup = h->kstate;
@@ -449,7 +504,7 @@ int nfh_send(nfh* h, const sh_batch* b, uint64_t first_seq) {
         }
         if (!err) {
             h->tick++;
-            take_records(h, sink, h->T.n_queries);
+            take_records(h, sink, h->T.n_queries, h->tick - 1);
             return apply_history(h);
         }
         h->kstate.swap(backup);
@@ -459,6 +514,28 @@ int nfh_send(nfh* h, const sh_batch* b, uint64_t first_seq) {
         }
     }
     return -5;
+}
+
+int nfh_send(nfh* h, const sh_batch* b, uint64_t first_seq) { return send_impl(h, b, first_seq, nullptr, 0, 0); }
+
+int nfh_send_part(nfh* h, const sh_batch* b, uint64_t first_seq, const uint32_t* index, int64_t call_n,
+                  int64_t call_last) {
+    static const uint32_t none = 0;
+    if (!h->coord_on || call_n <= 0) return -1;
+    return send_impl(h, b, first_seq, index ? index : &none, call_n, call_last);
+}
+
+int nfh_set_coordinator(nfh* h, const sh_coordinator* c) {
+    if (!c || !c->history || !c->select || !c->min_time || !h->T.partitioned || h->started) return -1;
+    h->coord = *c;
+    h->coord_on = true;
+    return 0;
+}
+
+int nfh_out_order(nfh* h, int64_t start, int64_t count, uint64_t* order) {
+    if (!h->coord_on || start < 0 || start + count > (int64_t)h->order.size()) return -1;
+    memcpy(order, h->order.data() + start, (size_t)count * 8);
+    return 0;
 }
 
 int64_t nfh_out_count(nfh* h) { return (int64_t)h->out.size(); }

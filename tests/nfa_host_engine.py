@@ -44,6 +44,13 @@ def load():
         lib.nfh_last_error.restype = C.c_char_p
         lib.nfh_set_partition_keys.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         lib.nfh_set_partition_keys.restype = C.c_int
+        lib.nfh_send_part.argtypes = [C.c_void_p, C.POINTER(abi.sh_batch), C.c_uint64, C.c_void_p, C.c_int64,
+                                      C.c_int64]
+        lib.nfh_send_part.restype = C.c_int
+        lib.nfh_set_coordinator.argtypes = [C.c_void_p, C.POINTER(abi.sh_coordinator)]
+        lib.nfh_set_coordinator.restype = C.c_int
+        lib.nfh_out_order.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
+        lib.nfh_out_order.restype = C.c_int
         lib.nfh_destroy.argtypes = [C.c_void_p]
         lib.nfh_destroy.restype = None
         _lib = lib
@@ -65,6 +72,7 @@ class NfaHostEngine:
             raise NfaUnsupported(err.value.decode())
         self.n_out = max([len(q.outs) for q in compiled.queries] + [1])
         self.read = 0
+        self.seq = 0  # next input sequence number (send_part)
 
     def start(self):
         self._check(self.lib.nfh_start(self.h))
@@ -78,6 +86,20 @@ class NfaHostEngine:
         b, keep = make_batch(stream, tsa, cols, nulls, keys)
         self._check(self.lib.nfh_send(self.h, C.byref(b), first_seq))
 
+    def set_coordinator(self, coord):
+        self._coord = coord
+        self._check(self.lib.nfh_set_coordinator(self.h, C.byref(coord.struct())))
+
+    def send_part(self, stream, tsa, cols, nulls, keys, index, call_n, call_last, first_seq=None):
+        tsa = np.ascontiguousarray(tsa, dtype=np.int64)
+        index = np.ascontiguousarray(index, dtype=np.uint32)
+        cs = [np.ascontiguousarray(c) for c in cols]
+        ka = None if keys is None else np.ascontiguousarray(keys, dtype=np.int32)
+        b, keep = make_batch(stream, tsa, cs, nulls, ka)
+        self._check(self.lib.nfh_send_part(self.h, C.byref(b), self.seq if first_seq is None else first_seq,
+                                           index.ctypes.data if len(index) else None, int(call_n), int(call_last)))
+        self.seq += int(call_n)
+
     def set_partition_keys(self, first, strings=None, utf16=None, offsets=None):
         from siddhi_amd.javastr import pack_utf16
         if utf16 is None:
@@ -88,7 +110,7 @@ class NfaHostEngine:
     def advance_time(self, now):
         self._check(self.lib.nfh_advance_time(self.h, int(now)))
 
-    def drain(self):
+    def drain(self, ordered=False):
         total = self.lib.nfh_out_count(self.h)
         n = total - self.read
         q = np.zeros(n, np.int32)
@@ -99,8 +121,14 @@ class NfaHostEngine:
         if n:
             self.lib.nfh_out_read(self.h, self.read, n, q.ctypes.data, seq.ctypes.data, ts.ctypes.data,
                                   vals.ctypes.data, nls.ctypes.data, self.n_out)
+        out = dict(query=q, seq=seq, ts=ts, values=vals, nulls=nls, group=np.zeros(n, np.int32))
+        if ordered:
+            order = np.zeros(n, np.uint64)
+            if n:
+                self._check(self.lib.nfh_out_order(self.h, self.read, n, order.ctypes.data))
+            out["order"] = order
         self.read = total
-        return dict(query=q, seq=seq, ts=ts, values=vals, nulls=nls, group=np.zeros(n, np.int32))
+        return out
 
     def close(self):
         if self.h:
