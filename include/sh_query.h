@@ -84,8 +84,15 @@ enum sh_op {
     SH_OP_IS_NULL_STREAM = 17, /* IsNullStreamConditionExpressionExecutor (e1 is null) */
     SH_OP_IF_THEN_ELSE = 18,   /* function/IfThenElseFunctionExecutor (cond=lhs, a=rhs, b=third) */
     SH_OP_BOOL_VAR = 19,       /* BoolConditionExpressionExecutor wrapping a BOOL expr */
-    SH_OP_OUTPUT = 20          /* having: output attribute `attr` of the selected event
+    SH_OP_OUTPUT = 20,         /* having: output attribute `attr` of the selected event
                                   (HAVING_STATE variables, ExpressionParser.java:1308-1318) */
+    SH_OP_MULTI_VAR = 21       /* select of a count state's attribute without an index:
+                                  MultiValueVariableFunctionExecutor (core/executor/
+                                  MultiValueVariableFunctionExecutor.java:39-70, chosen at
+                                  ExpressionParser.java:1385-1437) -- attribute `attr` of every
+                                  event of slot `slot`'s chain from index `chain` on, as a List;
+                                  type OBJECT, ltype = the attribute's type. Output rows carry
+                                  a list handle (sh_list_get). */
 };
 
 /* select-clause aggregators (query/selector/attribute/aggregator/) */

@@ -103,6 +103,14 @@ int sh_advance_time(sh_handle* h, int64_t now_ms);
    (core/query/output/ratelimit/OutputRateLimiter.java:63-106): ordered matches. */
 int sh_drain(sh_handle* h, sh_match_buf* out);
 
+/* A List value -- the select of a count state's attribute without an index,
+   MultiValueVariableFunctionExecutor (core/executor/MultiValueVariableFunctionExecutor.java:39-70):
+   an SH_T_OBJECT output column holds a list handle. Copies up to cap elements
+   (raw 8-byte values of the attribute's type, null flags) and returns the list's
+   length (SH_E_INVALID_ARG: no such list). A row's handles stay valid until the
+   next sh_drain call. */
+int64_t sh_list_get(sh_handle* h, int64_t list, int64_t cap, int64_t* values, uint8_t* nulls);
+
 /* Number of rows sh_drain would return right now (forces pending device work). */
 int64_t sh_pending(sh_handle* h);
 

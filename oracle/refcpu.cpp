@@ -678,6 +678,9 @@ struct App {
     int32_t cbGroup = 0;
     int64_t clock = 0;  // TimestampGeneratorImpl current time (playback)
     std::vector<OutRow> out;
+    // List values of SH_OP_MULTI_VAR outputs (a row holds the list's index)
+    std::vector<std::vector<int64_t>> listV;
+    std::vector<std::vector<uint8_t>> listN;
     std::vector<StateBase*> zombies;  // destroyed states still referenced in-frame
     std::vector<Scheduler*> schedulers;
     std::string err;
@@ -1042,6 +1045,23 @@ Val QueryRT::eval(int e, StateEvent* se) {
             v.t = (int8_t)x.type;
             v.b = s->row->v[x.attr];
             v.null = s->row->nul[x.attr] != 0;
+            return v;
+        }
+        case SH_OP_MULTI_VAR: {
+            // MultiValueVariableFunctionExecutor.execute (MultiValueVariableFunctionExecutor.java:62-70):
+            // getStreamEvent(position), then the attribute of it and every later event of the chain
+            std::vector<int64_t> lv;
+            std::vector<uint8_t> ln;
+            for (StreamEvent* s = chainAt(se, x.slot, x.chain); s; s = s->next.get()) {
+                lv.push_back(s->row->v[x.attr]);
+                ln.push_back(s->row->nul[x.attr] != 0);
+            }
+            Val v;
+            v.t = SH_T_OBJECT;
+            v.null = false;
+            v.b = (int64_t)app->listV.size();
+            app->listV.push_back(std::move(lv));
+            app->listN.push_back(std::move(ln));
             return v;
         }
         case SH_OP_AND: {
@@ -2843,6 +2863,18 @@ int ref_out_read(ref_app* ra, int64_t start, int64_t count, int32_t* query, uint
 }
 
 void ref_out_clear(ref_app* ra) { ra->a.out.clear(); }
+
+int64_t ref_list_get(ref_app* ra, int64_t list, int64_t cap, int64_t* values, uint8_t* nulls) {
+    App& a = ra->a;
+    if (list < 0 || list >= (int64_t)a.listV.size()) return -1;
+    const auto& v = a.listV[list];
+    const auto& nl = a.listN[list];
+    for (int64_t i = 0; i < (int64_t)v.size() && i < cap; i++) {
+        if (values) values[i] = v[i];
+        if (nulls) nulls[i] = nl[i];
+    }
+    return (int64_t)v.size();
+}
 
 void ref_destroy(ref_app* ra) { delete ra; }
 

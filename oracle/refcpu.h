@@ -40,6 +40,8 @@ int64_t ref_out_count(ref_app* a);
 int ref_out_read(ref_app* a, int64_t start, int64_t count, int32_t* query, uint64_t* seq,
                  int64_t* ts, int64_t* values, uint8_t* nulls, int32_t n_out, int32_t* cb_group);
 void ref_out_clear(ref_app* a);
+/* a List output value (SH_OP_MULTI_VAR): copies up to cap elements, returns the length (-1: no such list) */
+int64_t ref_list_get(ref_app* a, int64_t list, int64_t cap, int64_t* values, uint8_t* nulls);
 void ref_destroy(ref_app* a);
 const char* ref_last_error(ref_app* a);
 

@@ -75,6 +75,7 @@ class HipEngine:
         self.handle = CompiledHandle(compiled)
         self.h = self.handle.h
         self.n_out = max([len(q.outs) for q in compiled.queries] + [1])
+        self.obj_cols = abi.object_columns(compiled)
 
     def start(self):
         check(self.h, _lib.sh_start(self.h))
@@ -175,7 +176,8 @@ class HipEngine:
         out = dict(query=q, seq=seq, ts=ts, values=vals, nulls=nls, group=grp)
         if ordered:
             out["order"] = order
-        return out
+        # List values (multi-value selects) are read before the next drain
+        return abi.resolve_lists(out, self.obj_cols, abi.list_getter(_lib.sh_list_get, self.h))
 
     def close(self):
         self.handle.close()

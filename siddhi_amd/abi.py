@@ -106,7 +106,7 @@ class sh_kernel_times(C.Structure):
 EXPORTED = ["sh_start", "sh_compile", "sh_push_batch", "sh_advance_time", "sh_drain", "sh_pending",
             "sh_destroy", "sh_last_error", "sh_run_device", "sh_last_kernel_times",
             "sh_version", "sh_device_count", "sh_set_partition_keys", "sh_snapshot", "sh_restore",
-            "sh_set_coordinator", "sh_push_batch_part", "sh_drain_ordered"]
+            "sh_set_coordinator", "sh_push_batch_part", "sh_drain_ordered", "sh_list_get"]
 
 
 def bind_product(lib):
@@ -142,6 +142,8 @@ def bind_product(lib):
     lib.sh_push_batch_part.restype = C.c_int
     lib.sh_drain_ordered.argtypes = [C.c_void_p, C.POINTER(sh_match_buf), C.c_void_p]
     lib.sh_drain_ordered.restype = C.c_int
+    lib.sh_list_get.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
+    lib.sh_list_get.restype = C.c_int64
     lib.sh_version.argtypes = []
     lib.sh_version.restype = C.c_char_p
     lib.sh_device_count.argtypes = []
@@ -184,6 +186,47 @@ def bind_oracle(lib):
     lib.ref_out_read.restype = C.c_int
     lib.ref_out_clear.argtypes = [C.c_void_p]
     lib.ref_out_clear.restype = None
+    lib.ref_list_get.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
+    lib.ref_list_get.restype = C.c_int64
     lib.ref_destroy.argtypes = [C.c_void_p]
     lib.ref_destroy.restype = None
     return lib
+
+
+def object_columns(compiled):
+    """per query, the select positions of type OBJECT (List values of
+    SH_OP_MULTI_VAR outputs, MultiValueVariableFunctionExecutor)"""
+    return [[k for k, t in enumerate(q.out_types) if t == 6] for q in compiled.queries]
+
+
+def resolve_lists(out, obj_cols, get):
+    """out: a drain dict; obj_cols: object_columns(compiled); get(handle) ->
+    (values int64[], nulls uint8[]) while the handles are valid. Adds
+    out["lists"] = {(row, col): (values, nulls)} for every List value."""
+    import numpy as np
+    lists = {}
+    if any(obj_cols):
+        q = out["query"]
+        for r in range(len(q)):
+            cols = obj_cols[int(q[r])] if 0 <= int(q[r]) < len(obj_cols) else []
+            for c in cols:
+                if not out["nulls"][r, c]:
+                    v, nl = get(int(out["values"][r, c]))
+                    lists[(r, c)] = (np.asarray(v, np.int64), np.asarray(nl, np.uint8))
+    out["lists"] = lists
+    return out
+
+
+def list_getter(fn, h):
+    """get(handle) over a C function fn(h, handle, cap, values, nulls) -> length"""
+    import numpy as np
+
+    def get(handle):
+        n = int(fn(h, handle, 0, None, None))
+        if n < 0:
+            raise RuntimeError(f"no list {handle}")
+        v = np.zeros(max(n, 1), np.int64)
+        nl = np.zeros(max(n, 1), np.uint8)
+        fn(h, handle, n, v.ctypes.data, nl.ctypes.data)
+        return v[:n], nl[:n]
+    return get

@@ -806,6 +806,8 @@ class Lowerer:
     expression types / variable positions like ExpressionParser."""
 
     def __init__(self, app: App, strings: "StringDict"):
+        self.multi_ok = False   # expr(): a multi-value variable is allowed here
+        self.last_multi = False
         self.app = app
         self.strings = strings
         self.stream_ids = {n: i for i, n in enumerate(app.stream_order)}
@@ -988,8 +990,7 @@ class Lowerer:
         if slot < 0:
             raise SiddhiAppValidationException(
                 f"no matching stream reference for attribute '{v.name}'")
-        if multi:
-            raise UnsupportedQuery("multi-value (List) select of a count state")
+        self.last_multi = bool(multi)
         sd = self.slots[slot][0]
         return slot, chain, sd.index(v.name), typ
 
@@ -1004,6 +1005,12 @@ class Lowerer:
                     return self._e(op=20, type=t, attr=o)
                 current = UNKNOWN_STATE
             slot, chain, attr, typ = self.resolve_var(e, current, default_index)
+            if self.last_multi:
+                # MultiValueVariableFunctionExecutor: a List of the chain's values
+                # (ExpressionParser.java:1385-1437); only a select output may hold it
+                if not self.multi_ok:
+                    raise UnsupportedQuery("multi-value (List) attribute inside an expression")
+                return self._e(op=21, type=OBJECT, slot=slot, chain=chain, attr=attr, ltype=typ)
             return self._e(op=1, type=typ, slot=slot, chain=chain, attr=attr)
         if isinstance(e, EStreamRef):
             raise UnsupportedQuery("bare stream reference outside `is null`")
@@ -1104,7 +1111,12 @@ class Lowerer:
             if n == "avg":
                 return dict(expr=a, agg=2, type=DOUBLE)
             return dict(expr=a, agg=4 if n == "max" else 5, type=at)
-        x = self.expr(e, UNKNOWN_STATE, 0)
+        # a bare count-state attribute may select a List (MultiValueVariableFunctionExecutor)
+        self.multi_ok = isinstance(e, EVar)
+        try:
+            x = self.expr(e, UNKNOWN_STATE, 0)
+        finally:
+            self.multi_ok = False
         return dict(expr=x, agg=0, type=self.etype(x))
 
 
@@ -1149,6 +1161,7 @@ class CompiledQuery:
     order: list = field(default_factory=list)   # [(expr index, desc)]
     limit: int = -1
     offset: int = -1
+    out_elem_types: List[int] = field(default_factory=list)  # OBJECT (List) outputs: element type, else -1
 
 
 @dataclass
@@ -1263,7 +1276,9 @@ def compile_app(text: str, strings: Optional[StringDict] = None) -> CompiledApp:
             n_slots=len(low.slots), slot_streams=[sd.name for sd, _, _ in low.slots],
             out_names=[o.name for o in q.select], out_types=[o["type"] for o in outs],
             output_stream=out_streams.index(q.output), having=low.having,
-            order=low.order, limit=low.limit, offset=low.offset))
+            order=low.order, limit=low.limit, offset=low.offset,
+            out_elem_types=[low.exprs[o["expr"]]["ltype"] if o["expr"] >= 0 and o["agg"] == 0
+                            and low.exprs[o["expr"]]["op"] == 21 else -1 for o in outs]))
     # a stream may be keyed by at most one partition (one key array per batch)
     owner = {}
     for p, spec in enumerate(app.partitions):

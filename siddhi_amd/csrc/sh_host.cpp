@@ -379,6 +379,15 @@ struct sh_handle {
     bool coord_on = false;
     sh_coordinator coord{};
     DevBuf w_gidx, n_gpos;
+    // ---- List outputs (SH_OP_MULTI_VAR): the launch's device buffer (nf_cols.lst)
+    // and the host lists rows hand out (ids l_base ..; valid until the next drain)
+    bool has_lists = false;
+    DevBuf n_lst, n_lst_ctr;
+    int64_t lst_cap = 0;
+    std::vector<int64_t> l_vals;
+    std::vector<uint8_t> l_nuls;
+    std::vector<int64_t> l_start;  // per live list: offset into l_vals (plus one end entry)
+    int64_t l_base = 0;            // id of the first live list
     sh_kernel_times times{};
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // [4, 5]: aggregate post-pass
     // hipRTC-specialised window kernels (sh_jit.cpp): 0 untried, 1 loaded, <0 unavailable
@@ -603,6 +612,10 @@ static bool has_selector_extras(const sh_app_desc* app) {
         const sh_query_desc& d = app->queries[q];
         if (d.having >= 0 || d.n_order > 0 || d.limit >= 0 || d.offset >= 0 || d.rate_kind != SH_RATE_NONE)
             return true;
+        // a List output (SH_OP_MULTI_VAR) is built by the general engine's selector
+        for (int32_t o = 0; o < d.n_outputs; o++)
+            if (d.outputs[o].expr >= 0 && d.outputs[o].expr < d.n_exprs && d.exprs[d.outputs[o].expr].op == SH_OP_MULTI_VAR)
+                return true;
     }
     return false;
 }
@@ -787,6 +800,9 @@ static int compile_nfa(sh_handle* h, const sh_app_desc* app) {
     for (int q = 0; q < T->n_queries; q++) nout = std::max(nout, T->q[q].n_out);
     h->n_out = nout;
     h->partitioned = T->partitioned;
+    for (int q = 0; q < T->n_queries; q++)
+        for (int o = 0; o < T->q[q].n_out; o++)
+            if (T->q[q].out_pc[o] == NF_PC_LIST) h->has_lists = true;
     if (T->partitioned && T->has_absent && !getenv("SH_NO_MAP_ORDER")) {
         std::vector<int> ids;
         for (int q = 0; q < T->n_queries; q++)
@@ -1252,7 +1268,28 @@ static nf_cols nf_store_cols(sh_handle* h) {
         c.sev_ctr = h->n_sev_ctr.as<unsigned long long>();
         c.sev_cap = (uint64_t)h->sev_cap;
     }
+    if (h->has_lists && h->n_lst.p) {
+        c.lst = h->n_lst.as<uint64_t>();
+        c.lst_ctr = h->n_lst_ctr.as<unsigned long long>();
+        c.lst_cap = (uint64_t)h->lst_cap;
+    }
     return c;
+}
+
+// the List buffer of a launch: allocated once (grown on NF_E_LST), counter zeroed
+static int nf_lst_ready(sh_handle* h) {
+    if (!h->has_lists) return 0;
+    if (!h->n_lst.p) {
+        h->lst_cap = 1 << 16;
+        if (h->n_lst.ensure_fresh((size_t)h->lst_cap * 8) || h->n_lst_ctr.ensure_fresh(64)) return SH_E_OOM;
+    }
+    return hipMemsetAsync(h->n_lst_ctr.p, 0, 8, h->stream) == hipSuccess ? 0 : SH_E_HIP;
+}
+static int nf_lst_grow(sh_handle* h) {
+    hipStreamSynchronize(h->stream);
+    if (h->n_lst.ensure_fresh((size_t)h->lst_cap * 4 * 8)) return SH_E_OOM;
+    h->lst_cap *= 4;
+    return 0;
 }
 
 static int nf_ensure_keys(sh_handle* h, int32_t nkeys) {
@@ -1513,6 +1550,30 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
         memcpy(h->o_vals.data() + base * h->n_out, h->pin_out.as<void>(b_v), total * no * 8);
         memcpy(h->o_nulls.data() + base * h->n_out, h->pin_out.as<void>(b_n), total * no);
     }
+    if (h->has_lists && vals) {
+        // List outputs: the launch's buffer offsets become host list ids
+        unsigned long long nw = 0;
+        hipMemcpy(&nw, h->n_lst_ctr.p, 8, hipMemcpyDeviceToHost);
+        std::vector<uint64_t> L(nw);
+        if (nw) hipMemcpy(L.data(), h->n_lst.p, nw * 8, hipMemcpyDeviceToHost);
+        if (h->l_start.empty()) h->l_start.push_back(0);
+        for (int64_t r = base; r < base + total; r++) {
+            const nf_query& Q = h->T->q[h->o_query[r]];
+            for (int c = 0; c < Q.n_out; c++) {
+                if (Q.out_pc[c] != NF_PC_LIST || h->o_nulls[r * h->n_out + c]) continue;
+                const uint64_t off = (uint64_t)h->o_vals[r * h->n_out + c];
+                if (off >= nw) return fail(h, SH_E_HIP, "list value out of range");
+                const uint64_t len = L[off];
+                if (off + 1 + len + (len + 63) / 64 > nw) return fail(h, SH_E_HIP, "list value out of range");
+                for (uint64_t i = 0; i < len; i++) {
+                    h->l_vals.push_back((int64_t)L[off + 1 + i]);
+                    h->l_nuls.push_back((uint8_t)((L[off + 1 + len + i / 64] >> (i % 64)) & 1));
+                }
+                h->o_vals[r * h->n_out + c] = h->l_base + (int64_t)h->l_start.size() - 1;
+                h->l_start.push_back((int64_t)h->l_vals.size());
+            }
+        }
+    }
     return SH_OK;
 }
 
@@ -1593,6 +1654,13 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
         hipMemsetAsync(h->w_cnt.p, 0, n_idx * 4, st);
         hipMemsetAsync(h->n_ctr.p, 0, 8, st);
         hipMemsetAsync(h->n_err.p, 0, 4, st);
+        if (nf_lst_ready(h)) return fail(h, SH_E_OOM, "list values");
+        if (h->has_lists && (cols.lst != h->n_lst.as<uint64_t>() || cols.lst_cap != (uint64_t)h->lst_cap)) {
+            cols.lst = h->n_lst.as<uint64_t>();
+            cols.lst_ctr = h->n_lst_ctr.as<unsigned long long>();
+            cols.lst_cap = (uint64_t)h->lst_cap;
+            nf_put_cols(h, cols);
+        }
         if (h->sm_on) {
             if (nf_sev_ready(h, n)) return fail(h, SH_E_OOM, "scheduler history");
             if (cols.sev != h->n_sev.as<uint64_t>() || cols.sev_cap != (uint64_t)h->sev_cap) {
@@ -1650,7 +1718,8 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
             if (h->n_sev.ensure_fresh((size_t)h->sev_cap * 4 * 16)) return fail(h, SH_E_OOM, "scheduler history");
             h->sev_cap *= 4;
         }
-        if (err & ~(unsigned)(NF_E_EMIT | NF_E_SEV)) {
+        if ((err & NF_E_LST) && nf_lst_grow(h)) return fail(h, SH_E_OOM, "list values");
+        if (err & ~(unsigned)(NF_E_EMIT | NF_E_SEV | NF_E_LST)) {
             int rc = nf_grow(h, err);
             if (rc) return rc;
         }
@@ -1847,11 +1916,18 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
                 hipMemsetAsync(h->w_cnt.p, 0, (size_t)n_idx * 4, st);
                 hipMemsetAsync(h->n_ctr.p, 0, 8, st);
                 hipMemsetAsync(h->n_err.p, 0, 4, st);
+                {
+                    const void* lst0 = h->n_lst.p;
+                    if (nf_lst_ready(h)) return fail(h, SH_E_OOM, "list values");
+                    if (lst0 != h->n_lst.p) nf_put_cols(h, nf_store_cols(h));
+                }
                 if (h->sm_on) {
                     const void* sev0 = h->n_sev.p;
                     const int64_t cap0 = h->sev_cap;
                     if (nf_sev_ready(h, ns)) return fail(h, SH_E_OOM, "scheduler history");
                     if (sev0 != h->n_sev.p || cap0 != h->sev_cap || attempt > 0) nf_put_cols(h, nf_store_cols(h));
+                } else if (attempt > 0) {
+                    nf_put_cols(h, nf_store_cols(h));
                 }
                 if (ns == 0) break;  // key-sharded: another rank fires this launch
                 if (h->n_save.ensure_fresh((size_t)ns * kw * 8)) return fail(h, SH_E_OOM, "save area");
@@ -1874,6 +1950,10 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
                     if (h->n_sev.ensure_fresh((size_t)h->sev_cap * 4 * 16)) return fail(h, SH_E_OOM, "history");
                     h->sev_cap *= 4;
                     err &= ~(unsigned)NF_E_SEV;
+                }
+                if (err & NF_E_LST) {
+                    if (nf_lst_grow(h)) return fail(h, SH_E_OOM, "list values");
+                    err &= ~(unsigned)NF_E_LST;
                 }
                 if (err & ~(unsigned)NF_E_EMIT) {
                     int rc = nf_grow(h, err);
@@ -2102,6 +2182,27 @@ static int drain_impl(sh_handle* h, sh_match_buf* out, uint64_t* order) {
     const int no = out->n_out;
     if (order && h->o_order.size() != h->o_seq.size())
         return fail(h, SH_E_INVALID_ARG, "order tags exist on key-sharded handles only");
+    if (h->has_lists && h->l_start.size() > 1) {
+        // the lists of rows returned by earlier drains are released now (a
+        // handle stays valid until the next drain): keep from the first list the
+        // undelivered rows hold
+        int64_t keep = h->l_base + (int64_t)h->l_start.size() - 1;
+        for (int64_t r = h->o_read; r < (int64_t)h->o_seq.size() && keep > h->l_base; r++) {
+            const nf_query& Q = h->T->q[h->o_query[r]];
+            for (int c = 0; c < Q.n_out; c++)
+                if (Q.out_pc[c] == NF_PC_LIST && !h->o_nulls[r * h->n_out + c])
+                    keep = std::min(keep, h->o_vals[r * h->n_out + c]);
+        }
+        const int64_t drop = keep - h->l_base;
+        if (drop > 0) {
+            const int64_t cut = h->l_start[drop];
+            h->l_vals.erase(h->l_vals.begin(), h->l_vals.begin() + cut);
+            h->l_nuls.erase(h->l_nuls.begin(), h->l_nuls.begin() + cut);
+            h->l_start.erase(h->l_start.begin(), h->l_start.begin() + drop);
+            for (auto& x : h->l_start) x -= cut;
+            h->l_base = keep;
+        }
+    }
     for (int64_t i = 0; i < k; i++) {
         const int64_t r = h->o_read + i;
         if (order) order[i] = h->o_order[r];
@@ -2129,6 +2230,17 @@ static int drain_impl(sh_handle* h, sh_match_buf* out, uint64_t* order) {
 }
 
 int sh_drain(sh_handle* h, sh_match_buf* out) { return drain_impl(h, out, nullptr); }
+
+int64_t sh_list_get(sh_handle* h, int64_t list, int64_t cap, int64_t* values, uint8_t* nulls) {
+    if (!h || list < h->l_base || list >= h->l_base + (int64_t)h->l_start.size() - 1) return SH_E_INVALID_ARG;
+    const int64_t i = list - h->l_base;
+    const int64_t a = h->l_start[i], n = h->l_start[i + 1] - a;
+    for (int64_t k = 0; k < n && k < cap; k++) {
+        if (values) values[k] = h->l_vals[a + k];
+        if (nulls) nulls[k] = h->l_nuls[a + k];
+    }
+    return n;
+}
 int sh_drain_ordered(sh_handle* h, sh_match_buf* out, uint64_t* order) { return drain_impl(h, out, order); }
 
 static int bits_for(uint64_t v) {
@@ -2759,6 +2871,7 @@ int sh_run_device(sh_handle* h, sh_device_run* user) {
     if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !user) return SH_E_INVALID_ARG;
     // the V2 fields are read only from a struct that says it has them
+    if (h->has_lists) return fail(h, SH_E_UNSUPPORTED, "List (multi-value) outputs come back through sh_drain");
     sh_device_run r = *user;
     if (r.version != SH_DEVICE_RUN_V2) {
         r.d_out_cols = nullptr;
@@ -2879,7 +2992,7 @@ int sh_last_kernel_times(sh_handle* h, sh_kernel_times* t) {
 
 namespace {
 const uint32_t kSnapMagic = 0x31534853u;  // "SHS1"
-const uint32_t kSnapVersion = 1;
+const uint32_t kSnapVersion = 2;  // 2: List values of undelivered rows
 
 struct SnapW {
     std::vector<uint8_t> b;
@@ -3016,6 +3129,11 @@ static int snapshot_image(sh_handle* h, SnapW& w) {
     w.vec(h->o_vals);
     w.vec(h->o_nulls);
     w.put(h->o_read);
+    // the List values undelivered rows hold
+    w.vec(h->l_vals);
+    w.vec(h->l_nuls);
+    w.vec(h->l_start);
+    w.put(h->l_base);
     w.put<int32_t>((int32_t)h->stores.size());
     for (size_t s = 0; s < h->stores.size(); s++) {
         const auto& st = h->stores[s];
@@ -3122,6 +3240,10 @@ static int restore_image(sh_handle* h, const void* buf, int64_t size) {
     r.vec(h->o_vals);
     r.vec(h->o_nulls);
     h->o_read = r.get<int64_t>();
+    r.vec(h->l_vals);
+    r.vec(h->l_nuls);
+    r.vec(h->l_start);
+    h->l_base = r.get<int64_t>();
     h->st_ts.clear();
     h->st_stream.clear();
     h->st_row.clear();

@@ -132,6 +132,8 @@ struct nf_query {
     nf_proc proc[NF_MAX_PROC];
     nf_receiver recv[NF_MAX_STREAMS];
     int32_t out_pc[NF_MAX_OUT], out_len[NF_MAX_OUT], out_agg[NF_MAX_OUT], out_type[NF_MAX_OUT];
+    // List outputs (out_pc == NF_PC_LIST, SH_OP_MULTI_VAR): slot, chain index, attribute, element type
+    int32_t out_mv_slot[NF_MAX_OUT], out_mv_chain[NF_MAX_OUT], out_mv_attr[NF_MAX_OUT], out_mv_type[NF_MAX_OUT];
     int32_t having_pc, having_len;  // QuerySelector havingConditionExecutor (-1: none)
     int32_t n_order, order_desc;    // OrderByEventComparator: attributes, DESC bit per attribute
     int32_t order_pc[SH_MAX_ORDER], order_len[SH_MAX_ORDER];
@@ -186,7 +188,14 @@ struct nf_cols {
     uint64_t* sev;
     unsigned long long* sev_ctr;
     uint64_t sev_cap;
+    // this launch's List values (SH_OP_MULTI_VAR outputs): per list, word 0 the
+    // length n, then n raw values, then ceil(n / 64) null-bit words; an output
+    // holds the list's word offset. NULL: the app has no List output
+    uint64_t* lst;
+    unsigned long long* lst_ctr;
+    uint64_t lst_cap;
 };
+#define NF_PC_LIST (-2)  // out_pc of a List output
 #define NF_SEV_INSERT 0  // getState added the key (computeIfAbsent)
 #define NF_SEV_CALL 1    // getState of a present key (lazy resize only)
 #define NF_SEV_REMOVE 2  // queue drained: returnAllStates removes the state
@@ -441,7 +450,8 @@ enum nf_err {
     NF_E_EMIT = 32,   // emission buffer full
     NF_E_UNSUP = 64,  // a reference behaviour outside the lowered subset (recursion)
     NF_E_KEY = 128,   // key id out of range
-    NF_E_SEV = 256    // scheduler-history buffer full
+    NF_E_SEV = 256,   // scheduler-history buffer full
+    NF_E_LST = 512    // List-value buffer full
 };
 
 // ------------------------------------------------------------------ the lane
@@ -1384,11 +1394,54 @@ struct NfLane {
     // ---------------------------------------------------------- selector
     // QuerySelector.processNoGroupBy / processInBatchNoGroupBy (:161-205, :271-313)
     // with the Sum/Avg/Count/Max/Min aggregators (per partition key)
+    // MultiValueVariableFunctionExecutor.execute (MultiValueVariableFunctionExecutor.java:62-70):
+    // the attribute of getStreamEvent(position) and of every later event of its
+    // chain, into this launch's List buffer; returns the list's word offset
+    NF_HD uint64_t collect_list(uint32_t s, int o) {
+        const int slot = Q->out_mv_slot[o], a = Q->out_mv_attr[o], ty = Q->out_mv_type[o];
+        const uint32_t first = chain_at(s, slot, Q->out_mv_chain[o]);
+        uint64_t n = 0;
+        for (uint32_t x = first; x; x = nd_next(x)) n++;
+        const uint64_t words = 1 + n + (n + 63) / 64;
+        if (!C || !C->lst) {
+            err |= NF_E_UNSUP;
+            return 0;
+        }
+#if defined(__HIP_DEVICE_COMPILE__)
+        const unsigned long long at = atomicAdd(C->lst_ctr, (unsigned long long)words);
+#else
+        const unsigned long long at = *C->lst_ctr;
+        *C->lst_ctr += words;
+#endif
+        if (at + words > C->lst_cap) {
+            err |= NF_E_LST;
+            return 0;
+        }
+        uint64_t* L = C->lst + at;
+        L[0] = n;
+        for (uint64_t w = 0; w < (n + 63) / 64; w++) L[1 + n + w] = 0;
+        const int strm = Q->slot_stream[slot];
+        uint64_t i = 0;
+        for (uint32_t x = first; x; x = nd_next(x), i++) {
+            const uint32_t row = nd_row(x);
+            const uint8_t* nm = C->nul[strm][a];
+            const bool nul = row == NF_ROW_NULL || (nm && nm[row]);
+            L[1 + i] = nul ? 0 : (uint64_t)load_attr(strm, a, ty, row);
+            if (nul) L[1 + n + i / 64] |= 1ull << (i % 64);
+        }
+        return (uint64_t)at;
+    }
+
     NF_HD void populate(uint32_t s) {
         uint64_t* agg = qb + Q->lay.off_agg;
         uint64_t* out = se_out(s);
         uint64_t mask = se(s)[3];
         for (int o = 0; o < Q->n_out; o++) {
+            if (Q->out_pc[o] == NF_PC_LIST) {
+                out[o] = collect_list(s, o);
+                mask &= ~(1ull << o);
+                continue;
+            }
             const int ak = Q->out_agg[o];
             if (ak == SH_AGG_NONE) {
                 NfVal v = eval(Q->out_pc[o], Q->out_len[o], s);

@@ -608,6 +608,21 @@ struct QueryLowering {
             Q->out_agg[o] = oa.agg;
             Q->out_type[o] = oa.type;
             if (oa.agg != SH_AGG_NONE) Q->contains_agg = 1;
+            if (oa.expr >= 0 && oa.expr < q->n_exprs && oa.agg == SH_AGG_NONE && q->exprs[oa.expr].op == SH_OP_MULTI_VAR) {
+                // a List of the chain's values (MultiValueVariableFunctionExecutor)
+                const sh_expr& x = q->exprs[oa.expr];
+                if (x.slot < 0 || x.slot >= q->n_slots || x.attr < 0 || x.attr >= NF_MAX_ATTRS) {
+                    err = "device engine: bad multi-value variable";
+                    return false;
+                }
+                Q->out_pc[o] = NF_PC_LIST;
+                Q->out_len[o] = 0;
+                Q->out_mv_slot[o] = x.slot;
+                Q->out_mv_chain[o] = x.chain;
+                Q->out_mv_attr[o] = x.attr;
+                Q->out_mv_type[o] = x.ltype;
+                continue;
+            }
             if (oa.expr >= 0) {
                 Q->out_pc[o] = T->n_code;
                 if (!gen(oa.expr, 0)) return false;
@@ -709,7 +724,9 @@ int nf_lower(const sh_app_desc* app, nf_table* T, std::string* err) {
                 slot_stream[qd.elems[e].slot] = qd.elems[e].stream;
         for (int x = 0; x < qd.n_exprs; x++) {
             const sh_expr& ex = qd.exprs[x];
-            if (ex.op != SH_OP_VAR || ex.slot < 0 || ex.slot >= qd.n_slots || ex.attr < 0 || ex.attr >= 32) continue;
+            if ((ex.op != SH_OP_VAR && ex.op != SH_OP_MULTI_VAR) || ex.slot < 0 || ex.slot >= qd.n_slots || ex.attr < 0 ||
+                ex.attr >= 32)
+                continue;
             const int st = slot_stream[ex.slot];
             if (st >= 0 && st < NF_MAX_STREAMS) T->attr_used[st] |= 1u << ex.attr;
         }

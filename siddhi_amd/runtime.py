@@ -435,9 +435,20 @@ class SiddhiAppRuntime:
             q = int(qs[i])
             cq = self.compiled.queries[q]
             evs = []
+            lists = res.get("lists") or {}
             for k in range(i, j):
-                data = [None if nls[k, c] else decode_value(int(vals[k, c]), cq.out_types[c], self.strings)
-                        for c in range(len(cq.out_types))]
+                data = []
+                for c in range(len(cq.out_types)):
+                    if nls[k, c]:
+                        data.append(None)
+                    elif cq.out_types[c] == OBJECT and (k, c) in lists:
+                        # a List (MultiValueVariableFunctionExecutor) of the element type
+                        lv, ln = lists[(k, c)]
+                        et = cq.out_elem_types[c]
+                        data.append([None if ln[x] else decode_value(int(lv[x]), et, self.strings)
+                                     for x in range(len(lv))])
+                    else:
+                        data.append(decode_value(int(vals[k, c]), cq.out_types[c], self.strings))
                 evs.append(Event(int(tss[k]), data))
             for cb in self._query_cbs.get(q, []):
                 cb.receive(evs[-1].timestamp, evs, None)

@@ -31,6 +31,9 @@ def py_value(v):
 
 
 def same(expected, got) -> bool:
+    if isinstance(expected, list):
+        # a List value (multi-value select), compared as Arrays.deepToString does
+        return isinstance(got, list) and len(expected) == len(got) and all(same(e, g) for e, g in zip(expected, got))
     if isinstance(expected, dict):
         if "f" in expected:
             if not isinstance(got, float):

@@ -124,7 +124,11 @@ def parse_object_array(toks, i):
         if toks[j][1] == "(":
             raise Skip("expression inside Object[]")
         if toks[j][1] == "new":
-            raise Skip("nested object in Object[]")
+            # a nested Object[] (the List value of a multi-value select, compared
+            # through Arrays.deepToString)
+            inner, j = parse_object_array(toks, j)
+            vals.append(inner)
+            continue
         if toks[j + 1][1] not in (",", "}"):
             raise Skip("expression inside Object[]")
         vals.append(value(toks[j]))
@@ -363,6 +367,14 @@ def interpret(body):
                                      "first_of_callback": False})
                     i = j
                     continue
+            if t.endswith("assertEquals") and toks[i + 1][1] == "(" and toks[i + 2][1] == "Arrays.deepToString" \
+                    and toks[i + 4][1] == "new":
+                # assertEquals(Arrays.deepToString(new Object[]{new Object[]{..}, ..}),
+                #              Arrays.deepToString(event.getData()))
+                vals, j = parse_object_array(toks, i + 4)
+                rows.append({"guard": guard, "row": vals, "first_of_callback": False})
+                i = j
+                continue
             if t.endswith("assertArrayEquals") and toks[i + 1][1] == "(":
                 vals, j = parse_object_array(toks, i + 2)
                 # which event: inEvents[0] / events[0] / event

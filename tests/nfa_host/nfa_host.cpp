@@ -82,6 +82,12 @@ struct nfh {
     bool coord_on = false;
     sh_coordinator coord{};
     std::vector<uint64_t> order;  // per output row: launch << 32 | position in the launch
+    // List values: this launch's buffer (nf_cols.lst) and the lists handed out
+    bool has_lists = false;
+    std::vector<uint64_t> lst;
+    unsigned long long lst_n = 0;
+    std::vector<std::vector<int64_t>> listV;
+    std::vector<std::vector<uint8_t>> listN;
 };
 
 static int width(int t) {
@@ -107,6 +113,13 @@ static nf_cols host_cols(nfh* h) {
         c.sev = h->sev.data();
         c.sev_ctr = &h->sev_n;
         c.sev_cap = h->sev.size() / 2;
+    }
+    if (h->has_lists) {
+        if (h->lst.size() < 4096) h->lst.resize(4096);
+        h->lst_n = 0;
+        c.lst = h->lst.data();
+        c.lst_ctr = &h->lst_n;
+        c.lst_cap = h->lst.size();
     }
     return c;
 }
@@ -147,6 +160,11 @@ static void ensure_keys(nfh* h, int32_t n) {
 
 // grow every capacity named by the error bits; re-lay every key block
 static bool grow(nfh* h, uint32_t err) {
+    if (err & NF_E_LST) {
+        h->lst.resize(h->lst.size() * 4);
+        err &= ~(uint32_t)NF_E_LST;
+        if (!err) return true;
+    }
     int c[5];
     memcpy(c, h->caps, sizeof(c));
     if (err & NF_E_LIST) c[0] *= 2;
@@ -223,9 +241,25 @@ static void take_records(nfh* h, HostSink& sink, int32_t nq, uint64_t launch) {
         o.query = (int32_t)(r[2] >> 32);
         o.ts = (int64_t)r[1];
         o.seq = r[3];
-        const int n = h->T.q[o.query].n_out;
+        const nf_query& Q = h->T.q[o.query];
+        const int n = Q.n_out;
         for (int c = 0; c < n; c++) {
-            o.v.push_back((int64_t)r[NF_REC_HDR + c]);
+            int64_t v = (int64_t)r[NF_REC_HDR + c];
+            if (Q.out_pc[c] == NF_PC_LIST) {
+                // this launch's List buffer -> a list handed out with the row
+                const uint64_t* L = h->lst.data() + v;
+                const uint64_t len = L[0];
+                std::vector<int64_t> lv(len);
+                std::vector<uint8_t> ln(len);
+                for (uint64_t i = 0; i < len; i++) {
+                    lv[i] = (int64_t)L[1 + i];
+                    ln[i] = (uint8_t)((L[1 + len + i / 64] >> (i % 64)) & 1);
+                }
+                v = (int64_t)h->listV.size();
+                h->listV.push_back(std::move(lv));
+                h->listN.push_back(std::move(ln));
+            }
+            o.v.push_back(v);
             o.nul.push_back((uint8_t)((r[2] >> c) & 1));
         }
         h->out.push_back(std::move(o));
@@ -363,6 +397,9 @@ nfh* nfh_create(const sh_app_desc* d, char* err, int errlen) {
         h->has_nul[s].assign(d->streams[s].n_attrs, false);
     }
     nf_set_caps(&h->T, h->caps[0], h->caps[1], h->caps[2], h->caps[3], h->caps[4]);
+    for (int q = 0; q < h->T.n_queries; q++)
+        for (int o = 0; o < h->T.q[q].n_out; o++)
+            if (h->T.q[q].out_pc[o] == NF_PC_LIST) h->has_lists = true;
     if (h->T.partitioned && h->T.has_absent) {
         std::vector<int> ids;
         for (int q = 0; q < h->T.n_queries; q++)
@@ -530,6 +567,16 @@ int nfh_set_coordinator(nfh* h, const sh_coordinator* c) {
     h->coord = *c;
     h->coord_on = true;
     return 0;
+}
+
+int64_t nfh_list_get(nfh* h, int64_t list, int64_t cap, int64_t* values, uint8_t* nulls) {
+    if (list < 0 || list >= (int64_t)h->listV.size()) return -1;
+    const auto& v = h->listV[list];
+    for (int64_t i = 0; i < (int64_t)v.size() && i < cap; i++) {
+        if (values) values[i] = v[i];
+        if (nulls) nulls[i] = h->listN[list][i];
+    }
+    return (int64_t)v.size();
 }
 
 int nfh_out_order(nfh* h, int64_t start, int64_t count, uint64_t* order) {

@@ -49,6 +49,8 @@ def load():
         lib.nfh_send_part.restype = C.c_int
         lib.nfh_set_coordinator.argtypes = [C.c_void_p, C.POINTER(abi.sh_coordinator)]
         lib.nfh_set_coordinator.restype = C.c_int
+        lib.nfh_list_get.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
+        lib.nfh_list_get.restype = C.c_int64
         lib.nfh_out_order.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
         lib.nfh_out_order.restype = C.c_int
         lib.nfh_destroy.argtypes = [C.c_void_p]
@@ -128,7 +130,7 @@ class NfaHostEngine:
                 self._check(self.lib.nfh_out_order(self.h, self.read, n, order.ctypes.data))
             out["order"] = order
         self.read = total
-        return out
+        return abi.resolve_lists(out, abi.object_columns(self.compiled), abi.list_getter(self.lib.nfh_list_get, self.h))
 
     def close(self):
         if self.h:

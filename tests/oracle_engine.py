@@ -95,7 +95,8 @@ class OracleEngine:
             self.lib.ref_out_read(self.h, self.read, n, q.ctypes.data, seq.ctypes.data, ts.ctypes.data,
                                   vals.ctypes.data, nls.ctypes.data, self.n_out, grp.ctypes.data)
         self.read = total
-        return dict(query=q, seq=seq, ts=ts, values=vals, nulls=nls, group=grp)
+        out = dict(query=q, seq=seq, ts=ts, values=vals, nulls=nls, group=grp)
+        return abi.resolve_lists(out, abi.object_columns(self.compiled), abi.list_getter(self.lib.ref_list_get, self.h))
 
     def close(self):
         if self.h:
