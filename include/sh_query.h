@@ -170,14 +170,15 @@ typedef struct sh_query_desc {
     int32_t rate_kind;           /* enum sh_rate: the query's OutputRateLimiter (OutputParser.constructOutputRateLimiter) */
     int64_t limit;               /* QuerySelector.limit, -1 if none (SelectorParser.java:115-123) */
     int64_t offset;              /* QuerySelector.offset, -1 if none (:124-132)  */
-    int32_t rate_value;          /* events per period (SH_RATE_FIRST_EVENTS / SH_RATE_LAST_EVENTS) */
+    int32_t rate_value;          /* events per period (SH_RATE_FIRST_EVENTS / _LAST_EVENTS / _ALL_EVENTS) */
     int32_t pad;
 } sh_query_desc;
 
 /* output rate limiting (query/output/ratelimit/): PassThroughOutputRateLimiter,
    `output first every N events` (FirstPerEventOutputRateLimiter.java:47-72) or
    `output last every N events` (LastPerEventOutputRateLimiter.java:45-68) */
-enum sh_rate { SH_RATE_NONE = 0, SH_RATE_FIRST_EVENTS = 1, SH_RATE_LAST_EVENTS = 2 };
+enum sh_rate { SH_RATE_NONE = 0, SH_RATE_FIRST_EVENTS = 1, SH_RATE_LAST_EVENTS = 2,
+               SH_RATE_ALL_EVENTS = 3 /* `output [all] every N events`: AllPerEventOutputRateLimiter */ };
 
 typedef struct sh_app_desc {
     int32_t version;             /* SH_DESC_VERSION                            */

@@ -499,6 +499,7 @@ struct Selector : Proc {
     void limitChunk(Chunk<StateEvent>& c);
     void rateProcess(Chunk<StateEvent>& c);
     std::unordered_map<int64_t, int32_t> rateCounter;  // RateLimiterState per partition flow
+    std::unordered_map<int64_t, Chunk<StateEvent>> rateHeld;  // AllPerEvent: allComplexEventChunk per partition flow
     void sendToCallBacks(Chunk<StateEvent>& c);
 };
 
@@ -2210,7 +2211,7 @@ void Selector::limitChunk(Chunk<StateEvent>& c) {
 // with its counter in a per-partition state (int arithmetic: FIRST with N == 1 never resets)
 void Selector::rateProcess(Chunk<StateEvent>& c) {
     const int kind = q->d.rate_kind;
-    if (kind != SH_RATE_FIRST_EVENTS && kind != SH_RATE_LAST_EVENTS) {
+    if (kind != SH_RATE_FIRST_EVENTS && kind != SH_RATE_LAST_EVENTS && kind != SH_RATE_ALL_EVENTS) {
         sendToCallBacks(c);
         return;
     }
@@ -2219,7 +2220,21 @@ void Selector::rateProcess(Chunk<StateEvent>& c) {
     c.reset();
     while (c.hasNext()) {
         SE ev = c.next();
-        if (kind == SH_RATE_FIRST_EVENTS) {
+        if (kind == SH_RATE_ALL_EVENTS) {
+            // AllPerEventOutputRateLimiter.process (AllPerEventOutputRateLimiter.java:48-75): every
+            // current / expired event is held; the N-th releases the held chunk
+            if (ev->type == CURRENT || ev->type == EXPIRED) {
+                c.remove();
+                Chunk<StateEvent>& held = rateHeld[q->app->flow.key];
+                held.add(ev);
+                counter = (int32_t)((uint32_t)counter + 1u);
+                if (counter == q->d.rate_value) {
+                    out.add(held.first);
+                    held.clear();
+                    counter = 0;
+                }
+            }
+        } else if (kind == SH_RATE_FIRST_EVENTS) {
             c.remove();
             counter = (int32_t)((uint32_t)counter + 1u);
             if (counter == 1) {
@@ -2696,7 +2711,8 @@ ref_app* ref_create(const sh_app_desc* d, char* err, int errlen) {
         // processInBatchNoGroupBy would pass an empty chunk on (QuerySelector.java:304-311)
         if (agg && (qd.offset > 0 || qd.limit == 0)) serr = "aggregating selector with offset > 0 or limit 0";
         if (qd.rate_kind != SH_RATE_NONE &&
-            ((qd.rate_kind != SH_RATE_FIRST_EVENTS && qd.rate_kind != SH_RATE_LAST_EVENTS) || qd.rate_value < 1))
+            ((qd.rate_kind != SH_RATE_FIRST_EVENTS && qd.rate_kind != SH_RATE_LAST_EVENTS &&
+              qd.rate_kind != SH_RATE_ALL_EVENTS) || qd.rate_value < 1))
             serr = "output rate limiting: `output first|last every N events` only";
         if (!serr.empty()) {
             delete ra;

@@ -230,3 +230,17 @@ def list_getter(fn, h):
         fn(h, handle, n, v.ctypes.data, nl.ctypes.data)
         return v[:n], nl[:n]
     return get
+
+
+def concat_drains(parts):
+    """drain dicts of consecutive drains as one (List values re-keyed by row)"""
+    import numpy as np
+    keys = [k for k in parts[-1] if k != "lists"]
+    out = {k: np.concatenate([p[k] for p in parts]) for k in keys}
+    lists, base = {}, 0
+    for p in parts:
+        for (r, c), v in (p.get("lists") or {}).items():
+            lists[(r + base, c)] = v
+        base += len(p["query"])
+    out["lists"] = lists
+    return out

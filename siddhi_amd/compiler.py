@@ -494,13 +494,15 @@ class Parser:
                     break
             self.expect_kw("every")
             tk = self.peek()
-            if kind not in ("first", "last") or tk.kind != "num" or not self.peek(1).text.lower() == "events":
-                raise UnsupportedQuery("output rate limiting: only `output first|last every N events` runs on the device")
+            if kind == "snapshot" or tk.kind != "num" or not self.peek(1).text.lower() == "events":
+                raise UnsupportedQuery("output rate limiting: only `output [first|last|all] every N events` runs "
+                                       "on the device")
             n = int(self.next().text)
             self.next()  # events
             if n < 1:
                 raise UnsupportedQuery(f"output {kind} every 0 events")
-            rate = (1 if kind == "first" else 2, n)
+            # OutputParser.constructOutputRateLimiter: no keyword is ALL
+            rate = ({"first": 1, "last": 2}.get(kind, 3), n)
         self.expect_kw("insert")
         if self.kw("current"):
             self.next()

@@ -214,6 +214,10 @@ struct nf_cols {
 #define NF_QH_WORDS 4
 
 NF_INL int64_t nf_round_words(int64_t bytes) { return (bytes + 7) / 8; }
+// the aggregator words (5 per output) + the AllPerEvent limiter's held chunk (first, last)
+NF_INL int64_t nf_agg_words(const nf_query& q) {
+    return (int64_t)q.n_out * 5 + (q.rate_kind == SH_RATE_ALL_EVENTS ? 2 : 0);
+}
 
 // computes `lay` for query q with the given capacities (host side)
 NF_INL void nf_set_layout(nf_query& q, int32_t n_slots, int32_t list_cap, int32_t se_cap, int32_t node_cap,
@@ -231,7 +235,7 @@ NF_INL void nf_set_layout(nf_query& q, int32_t n_slots, int32_t list_cap, int32_
     L.off_lists = w;
     w += nf_round_words((int64_t)q.n_proc * 2 * list_cap * 4);
     L.off_agg = w;
-    w += (int64_t)q.n_out * 5;
+    w += nf_agg_words(q);
     L.off_hold = w;
     w += 3 + (int64_t)hold_cap;
     L.off_sched = w;
@@ -1627,6 +1631,34 @@ struct NfLane {
     // the reference: only the first event ever passes); LastPerEventOutputRateLimiter
     // (LastPerEventOutputRateLimiter.java:45-68) keeps every N-th current event
     NF_HD void rate_send(uint32_t* c) {
+        if (Q->rate_kind == SH_RATE_ALL_EVENTS) {
+            // AllPerEventOutputRateLimiter.process (AllPerEventOutputRateLimiter.java:48-75): every
+            // current / expired event joins the held chunk (key block, after the
+            // aggregators); the N-th releases it as one chunk
+            uint64_t* hw = qb + Q->lay.off_agg + (int64_t)Q->n_out * 5;
+            uint32_t held[4] = {(uint32_t)hw[0], (uint32_t)hw[1], 0, 0};
+            uint32_t out[4] = {0, 0, 0, 0};
+            uint32_t cnt = (uint32_t)(qb[3] >> 32);
+            ch_reset(c);
+            while (ch_has_next(c)) {
+                const uint32_t ev = ch_next(c);
+                const int ty = se_type(ev);
+                if (ty != NF_CURRENT && ty != NF_EXPIRED) continue;
+                ch_remove(c);
+                ch_add(held, ev);
+                if (++cnt == (uint32_t)Q->rate_value) {
+                    ch_add(out, held[0]);
+                    ch_clear(held);
+                    cnt = 0;
+                }
+            }
+            hw[0] = held[0];
+            hw[1] = held[1];
+            qb[3] = (qb[3] & 0xFFFFFFFFull) | ((uint64_t)cnt << 32);
+            ch_reset(out);
+            if (ch_has_next(out)) send_to_callbacks(out);
+            return;
+        }
         if (Q->rate_kind == SH_RATE_FIRST_EVENTS || Q->rate_kind == SH_RATE_LAST_EVENTS) {
             const bool first = Q->rate_kind == SH_RATE_FIRST_EVENTS;
             uint32_t cnt = (uint32_t)(qb[3] >> 32);
@@ -2207,6 +2239,7 @@ struct NfLane {
         for (int i = 0; i < 4; i++) gc_mark(rc[i]);
         const uint32_t nh = n_holders();
         for (uint32_t i = 0; i < 2 * nh; i++) gc_mark(holders()[i]);
+        if (Q->rate_kind == SH_RATE_ALL_EVENTS) gc_mark((uint32_t)qb[Q->lay.off_agg + (int64_t)Q->n_out * 5]);
         if (in_holder) {
             gc_mark(h_first);
             gc_mark(h_last);

@@ -520,7 +520,7 @@ __global__ void k_nfa_relayout(const nf_table* __restrict__ A, const nf_table* _
             const int64_t pl = i / QA.lay.list_cap, e = i % QA.lay.list_cap;
             ((uint32_t*)(d + QB.lay.off_lists))[pl * QB.lay.list_cap + e] = ((const uint32_t*)(s + QA.lay.off_lists))[i];
         }
-        for (int w = t; w < QA.n_out * 5; w += nt) d[QB.lay.off_agg + w] = s[QA.lay.off_agg + w];
+        for (int w = t; w < nf_agg_words(QA); w += nt) d[QB.lay.off_agg + w] = s[QA.lay.off_agg + w];
         for (int w = t; w < 3 + QA.lay.hold_cap; w += nt) d[QB.lay.off_hold + w] = s[QA.lay.off_hold + w];
         for (int p = 0; p < QA.n_proc; p++) {
             const uint64_t* sq = s + QA.lay.off_sched + (int64_t)p * (2 + QA.lay.sched_cap);

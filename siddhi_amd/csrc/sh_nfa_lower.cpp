@@ -665,7 +665,8 @@ struct QueryLowering {
         Q->rate_kind = q->rate_kind;
         Q->rate_value = q->rate_value;
         if (q->rate_kind != SH_RATE_NONE &&
-            ((q->rate_kind != SH_RATE_FIRST_EVENTS && q->rate_kind != SH_RATE_LAST_EVENTS) || q->rate_value < 1)) {
+            ((q->rate_kind != SH_RATE_FIRST_EVENTS && q->rate_kind != SH_RATE_LAST_EVENTS &&
+              q->rate_kind != SH_RATE_ALL_EVENTS) || q->rate_value < 1)) {
             err = "output rate limiting: `output first|last every N events` (N >= 1) only";
             return false;
         }

@@ -241,7 +241,11 @@ def merge_ordered(outs):
     """the ranks' drained rows (dicts with 'order') merged into the single-process
     order: a stable sort by the processing-order tag (rows sharing a tag come
     from one key, hence one rank, already in order)"""
-    keys = ("query", "seq", "ts", "values", "nulls", "group")
-    cat = {k: np.concatenate([o[k] for o in outs]) for k in keys + ("order",)}
+    from .abi import concat_drains
+    cat = concat_drains(list(outs))
     o = np.argsort(cat["order"], kind="stable")
-    return {k: cat[k][o] for k in keys + ("order",)}
+    res = {k: v[o] for k, v in cat.items() if k != "lists"}
+    pos = np.empty(len(o), np.int64)
+    pos[o] = np.arange(len(o))
+    res["lists"] = {(int(pos[r]), c): v for (r, c), v in cat["lists"].items()}
+    return res

@@ -193,7 +193,7 @@ static bool grow(nfh* h, uint32_t err) {
                     uint32_t* dl = (uint32_t*)(d + B.lay.off_lists) + ((int64_t)p * 2 + wh) * B.lay.list_cap;
                     for (int i = 0; i < A.lay.list_cap; i++) dl[i] = sl[i];
                 }
-            for (int w = 0; w < A.n_out * 5; w++) d[B.lay.off_agg + w] = s[A.lay.off_agg + w];
+            for (int w = 0; w < nf_agg_words(A); w++) d[B.lay.off_agg + w] = s[A.lay.off_agg + w];
             for (int w = 0; w < 3; w++) d[B.lay.off_hold + w] = s[A.lay.off_hold + w];
             for (int w = 0; w < A.lay.hold_cap; w++) d[B.lay.off_hold + 3 + w] = s[A.lay.off_hold + 3 + w];
             for (int p = 0; p < A.n_proc; p++) {

@@ -8,8 +8,10 @@ every N-th current event. Pinned by the counts of the reference's
 EventOutputRateLimitTestCase (5 events: first every 2 -> 3, first every 3 -> 2, last
 every 2 -> 2, last every 4 -> 1), transcribed onto a one-state pattern that emits once
 per event; randomized apps hold the general engine's kernel logic and the device to the
-oracle. The other rate limiters (all per events, time, snapshot) stay on the Java side
-(UnsupportedQuery)."""
+oracle. `output [all] every N events` (AllPerEventOutputRateLimiter.process,
+AllPerEventOutputRateLimiter.java:48-75) holds every event per partition and releases the
+held chunk with the N-th (EventOutputRateLimitTestCase: all every 2 -> 4, every 2 -> 4,
+every 5 -> 5 of 5). The time and snapshot limiters stay on the Java side (UnsupportedQuery)."""
 import random
 import re
 
@@ -44,6 +46,11 @@ KNOWN = [
     ("output last every 3 events", [[20.0, 40.0]]),
     ("output last every 1 events", [[10.0, 40.0], [30.0, 40.0], [20.0, 40.0], [1.0, 2.0], [1.0, 3.0]]),
     ("output last every 9 events", []),
+    # AllPerEventOutputRateLimiter: the N-th match releases the held ones, the rest stay held
+    ("output all every 2 events", [[10.0, 40.0], [30.0, 40.0], [20.0, 40.0], [1.0, 2.0]]),
+    ("output every 3 events", [[10.0, 40.0], [30.0, 40.0], [20.0, 40.0]]),
+    ("output all every 1 events", [[10.0, 40.0], [30.0, 40.0], [20.0, 40.0], [1.0, 2.0], [1.0, 3.0]]),
+    ("output all every 6 events", []),
 ]
 PART = ("define stream A (sym string, price float, n int); partition with (sym of A) begin "
         "@info(name = 'query1') from every e1=A select e1.sym as s, e1.n as n "
@@ -65,24 +72,28 @@ def _hip_factory():
 
 def _login(factory, n, kind="first"):
     acts = [("send", "LoginEvents", [(1000 + i, [1000 + i, ip])]) for i, ip in enumerate(IPS)]
-    return run_case(factory, LOGIN.format(n=n, kind=kind), acts)
+    return run_case(factory, LOGIN.format(n=n, kind=kind).replace("output  every", "output every"), acts)
 
 
 ENGINES = [("oracle", lambda: OracleEngine), ("kernel_logic", lambda: NfaHostEngine)]
 
 
-REF_COUNTS = [("first", 2, 3), ("first", 3, 2), ("last", 2, 2), ("last", 4, 1)]
+REF_COUNTS = [("first", 2, 3), ("first", 3, 2), ("last", 2, 2), ("last", 4, 1), ("all", 2, 4), ("", 2, 4),
+              ("", 5, 5)]
 
 
 @pytest.mark.parametrize("name,factory", ENGINES)
 @pytest.mark.parametrize("kind,n,count", REF_COUNTS)
 def test_reference_counts(name, factory, kind, n, count):
     """EventOutputRateLimitTestCase: 5 events; first every 2 -> 3, first every 3 -> 2,
-    last every 2 -> 2, last every 4 -> 1"""
+    last every 2 -> 2, last every 4 -> 1, all every 2 -> 4, every 2 -> 4, every 5 -> 5"""
     got = _login(factory(), n, kind)
     assert len(got) == count
-    start = 0 if kind == "first" else n - 1
-    assert [r[2][0] for r in got] == [IPS[i] for i in range(start, len(IPS), n)]
+    if kind in ("first", "last"):
+        start = 0 if kind == "first" else n - 1
+        assert [r[2][0] for r in got] == [IPS[i] for i in range(start, len(IPS), n)]
+    else:  # all: every complete group of n, in arrival order
+        assert [r[2][0] for r in got] == IPS[:len(IPS) // n * n]
 
 
 @pytest.mark.parametrize("name,factory", ENGINES)
@@ -107,8 +118,9 @@ def test_parse():
     d = compiler.compile_app(BASE.format(tail="output last every 3 events")).descriptor().queries[0]
     assert d.rate_kind == 2 and d.rate_value == 3
     assert compiler.compile_app(BASE.format(tail="")).descriptor().queries[0].rate_kind == 0
-    for tail in ("output all every 2 events", "output every 2 events",
-                 "output first every 1 sec", "output snapshot every 1 sec"):
+    assert compiler.compile_app(BASE.format(tail="output all every 2 events")).descriptor().queries[0].rate_kind == 3
+    assert compiler.compile_app(BASE.format(tail="output every 7 events")).descriptor().queries[0].rate_value == 7
+    for tail in ("output first every 1 sec", "output every 2 sec", "output snapshot every 1 sec"):
         with pytest.raises(compiler.UnsupportedQuery):
             compiler.compile_app(BASE.format(tail=tail))
 
@@ -118,7 +130,7 @@ def rate_case(seed):
     app, actions = nfa_case(rng)
     if " select " not in app:
         return None
-    app = re.sub(r" insert into Out;", lambda m: f" output {rng.choice(['first', 'last'])} every "
+    app = re.sub(r" insert into Out;", lambda m: f" output {rng.choice(['first', 'last', 'all', ''])} every "
                  f"{rng.choice([1, 2, 2, 3, 5])} events insert into Out;", app)
     return app, actions
 
