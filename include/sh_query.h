@@ -34,8 +34,9 @@
 extern "C" {
 #endif
 
-#define SH_DESC_VERSION 4
+#define SH_DESC_VERSION 5
 #define SH_MAX_ORDER 4
+#define SH_MAX_GROUP 4
 
 /* Attribute.Type (api/definition/Attribute.java) */
 enum sh_type {
@@ -171,7 +172,9 @@ typedef struct sh_query_desc {
     int64_t limit;               /* QuerySelector.limit, -1 if none (SelectorParser.java:115-123) */
     int64_t offset;              /* QuerySelector.offset, -1 if none (:124-132)  */
     int32_t rate_value;          /* events per period (SH_RATE_FIRST_EVENTS / _LAST_EVENTS / _ALL_EVENTS) */
-    int32_t pad;
+    int32_t n_group;             /* `group by` attributes (GroupByKeyGenerator, SelectorParser.java:102-108), 0 if none */
+    int32_t group_expr[SH_MAX_GROUP]; /* variable expression per group-by attribute (UNKNOWN_STATE, default index 0):
+                                    the aggregators keep one state per (partition key, group key) */
 } sh_query_desc;
 
 /* output rate limiting (query/output/ratelimit/): PassThroughOutputRateLimiter,

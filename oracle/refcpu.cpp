@@ -487,10 +487,15 @@ struct Selector : Proc {
     QueryRT* q = nullptr;
     bool containsAggregator = false;
     std::unordered_map<int64_t, AggState*> agg;  // per partition flow key
+    // with `group by`: per (partition flow key, group key) -- SiddhiAppContext.startGroupByFlow
+    // (QuerySelector.java:315-340) keys the aggregators' state holders by the group key
+    std::map<std::pair<int64_t, std::vector<int64_t>>, AggState*> aggG;
     ~Selector() {
         for (auto& kv : agg) delete kv.second;
+        for (auto& kv : aggG) delete kv.second;
     }
     void process(Chunk<StateEvent>& c) override;
+    std::vector<int64_t> groupKey(StateEvent* se);
     void populate(StateEvent* se);
     bool having(StateEvent* se);
     int orderCompare(StateEvent* a, StateEvent* b);
@@ -2018,11 +2023,27 @@ void Scheduler::onTimeChange(int64_t now) {
 
 // ------------------------------------------------------------ selector
 // QuerySelector.java:161-313 + aggregators
+// GroupByKeyGenerator.constructEventKey (GroupByKeyGenerator.java:60-71): the group-by
+// values' toString() joined by KEY_DELIMITER; equal strings <=> equal (value, null)
+// pairs with every NaN of a type alike (Float/Double.toString prints "NaN")
+std::vector<int64_t> Selector::groupKey(StateEvent* se) {
+    std::vector<int64_t> k;
+    for (int i = 0; i < q->d.n_group; i++) {
+        Val v = q->eval(q->d.group_expr[i], se);
+        int64_t b = v.null ? 0 : v.b;
+        if (!v.null && v.t == SH_T_FLOAT && (b & 0x7F800000ll) == 0x7F800000ll && (b & 0x7FFFFFll)) b = 0x7FC00000ll;
+        if (!v.null && v.t == SH_T_DOUBLE && std::isnan(asD(v))) b = 0x7FF8000000000000ll;
+        k.push_back(b);
+        k.push_back(v.null ? 1 : 0);
+    }
+    return k;
+}
+
 void Selector::populate(StateEvent* se) {
     int64_t key = q->app->flow.key;
     AggState* as = nullptr;
     if (containsAggregator) {
-        AggState*& a = agg[key];
+        AggState*& a = q->d.n_group > 0 ? aggG[std::make_pair(key, groupKey(se))] : agg[key];
         if (!a) {
             a = new AggState();
             size_t n = q->outs.size();

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_nfa.py tests/test_gpu_snapshot.py tests/test_abi.py tests/test_gpu_shard_stream.py -x -v -rs --timeout 300 --timeout-method thread > gpurun_out/r3h_tests.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests/test_gpu_snapshot.py tests/test_rate_limit.py tests/test_gpu_parity.py tests/test_gpu_nfa.py tests/test_abi.py -x -v -rs --timeout 300 --timeout-method thread > gpurun_out/r3h_tests.log 2>&1; rc=$?
 grep -E "passed|failed" gpurun_out/r3h_tests.log | tail -2
 [ $rc -ne 0 ] && { grep -E "FAIL|Error" gpurun_out/r3h_tests.log | head -20; tail -40 gpurun_out/r3h_tests.log; exit 1; }
 timeout -k 10 500 python -u scripts/c5_shard_probe2.py > gpurun_out/r3h_c5probe2.log 2>&1; echo "probe2 rc=$?"; grep -v amdgpu.ids gpurun_out/r3h_c5probe2.log | tail -12

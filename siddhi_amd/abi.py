@@ -1,8 +1,9 @@
 """ctypes mirror of include/sh_query.h and include/siddhi_hip.h (the C-ABI boundary)."""
 import ctypes as C
 
-SH_DESC_VERSION = 4
+SH_DESC_VERSION = 5
 SH_MAX_ORDER = 4
+SH_MAX_GROUP = 4
 
 SH_OK = 0
 SH_E_INVALID_ARG = -1
@@ -45,7 +46,8 @@ class sh_query_desc(C.Structure):
                 ("elems", C.POINTER(sh_state_elem)), ("exprs", C.POINTER(sh_expr)),
                 ("outputs", C.POINTER(sh_output_attr)), ("having", C.c_int32), ("n_order", C.c_int32),
                 ("order_expr", C.c_int32 * SH_MAX_ORDER), ("order_desc", C.c_int32), ("rate_kind", C.c_int32),
-                ("limit", C.c_int64), ("offset", C.c_int64), ("rate_value", C.c_int32), ("pad", C.c_int32)]
+                ("limit", C.c_int64), ("offset", C.c_int64), ("rate_value", C.c_int32), ("n_group", C.c_int32),
+                ("group_expr", C.c_int32 * SH_MAX_GROUP)]
 
 
 class sh_app_desc(C.Structure):

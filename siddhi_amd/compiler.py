@@ -195,6 +195,7 @@ class Query:
     partition: int = -1
     having: object = None        # Selector.having (QuerySelector havingConditionExecutor)
     order_by: list = field(default_factory=list)   # [(EVar, desc)] (Selector.orderByList)
+    group_by: list = field(default_factory=list)   # [EVar] (Selector.groupByList)
     limit: object = None         # Selector.limit / offset expressions (constants)
     offset: object = None
     rate: Optional[Tuple[int, int]] = None   # (enum sh_rate, N): `output first|last every N events`
@@ -432,7 +433,7 @@ class Parser:
             self.next()
             within = self.time_value()
         sel, star, having = [], False, None
-        order, limit, offset = [], None, None
+        order, limit, offset, group = [], None, None, []
         if self.kw("select"):
             self.next()
             if self.op("*"):
@@ -454,7 +455,18 @@ class Parser:
                         continue
                     break
             if self.kw("group"):
-                raise UnsupportedQuery("`group by` is out of scope (SURVEY.md 8f next)")
+                # group_by: GROUP BY attribute_reference (, attribute_reference)* (SiddhiQL.g4)
+                self.next()
+                self.expect_kw("by")
+                while True:
+                    v = self.primary()
+                    if not isinstance(v, EVar):
+                        self.err("group by takes attribute references")
+                    group.append(v)
+                    if self.op(","):
+                        self.next()
+                        continue
+                    break
             if self.kw("having"):
                 self.next()
                 having = self.expr()
@@ -515,7 +527,7 @@ class Parser:
         if self.op("#"):
             raise UnsupportedQuery("inner-stream outputs (#Stream) are out of scope")
         out = self.ident()
-        return Query(name, st, root, within, sel, star, out, having=having, order_by=order,
+        return Query(name, st, root, within, sel, star, out, having=having, order_by=order, group_by=group,
                      limit=limit, offset=offset, rate=rate)
 
     def detect_state_type(self):
@@ -848,6 +860,15 @@ class Lowerer:
             self.having = self.expr(q.having, HAVING_STATE, 0)
             self._want_bool(self.having)
         # OrderByEventComparator parses each attribute at HAVING_STATE (SelectorParser.java:110-114)
+        # GroupByKeyGenerator (SelectorParser.java:102-108): UNKNOWN_STATE, default index 0
+        self.group = []
+        if len(q.group_by) > abi.SH_MAX_GROUP:
+            raise UnsupportedQuery(f"group by: at most {abi.SH_MAX_GROUP} attributes")
+        for v in q.group_by:
+            self.group.append(self.expr(v, UNKNOWN_STATE, 0))
+        if q.group_by and q.rate and q.rate[0] in (1, 2):
+            # OutputParser picks the GroupBy first / last limiters (one counter per group)
+            raise UnsupportedQuery("group by with `output first|last every N events` (per-group limiters)")
         self.order = []
         if len(q.order_by) > abi.SH_MAX_ORDER:
             raise UnsupportedQuery(f"order by: at most {abi.SH_MAX_ORDER} attributes")
@@ -1164,6 +1185,7 @@ class CompiledQuery:
     limit: int = -1
     offset: int = -1
     out_elem_types: List[int] = field(default_factory=list)  # OBJECT (List) outputs: element type, else -1
+    group: List[int] = field(default_factory=list)           # group-by expression roots
 
 
 @dataclass
@@ -1222,6 +1244,9 @@ class CompiledApp:
             q.offset = cq.offset
             if cq.query.rate:
                 q.rate_kind, q.rate_value = cq.query.rate
+            q.n_group = len(cq.group)
+            for i, ei in enumerate(cq.group):
+                q.group_expr[i] = ei
             q.elems = el
             q.exprs = ex
             q.outputs = ou
@@ -1278,7 +1303,7 @@ def compile_app(text: str, strings: Optional[StringDict] = None) -> CompiledApp:
             n_slots=len(low.slots), slot_streams=[sd.name for sd, _, _ in low.slots],
             out_names=[o.name for o in q.select], out_types=[o["type"] for o in outs],
             output_stream=out_streams.index(q.output), having=low.having,
-            order=low.order, limit=low.limit, offset=low.offset,
+            order=low.order, limit=low.limit, offset=low.offset, group=low.group,
             out_elem_types=[low.exprs[o["expr"]]["ltype"] if o["expr"] >= 0 and o["agg"] == 0
                             and low.exprs[o["expr"]]["op"] == 21 else -1 for o in outs]))
     # a stream may be keyed by at most one partition (one key array per batch)

@@ -417,7 +417,7 @@ struct sh_handle {
     std::vector<DevBuf> n_rank;         // by scheduler id, [n_nkeys] u64
     PinBuf pin_sev, pin_rk;
     int64_t sev_cap = 0;
-    int caps[5] = {16, 32, 64, 32, 8};
+    int caps[6] = {16, 32, 64, 32, 8, 4};  // list, se, node, hold, sched, group
     int32_t n_nkeys = 0;          // key blocks allocated
     int64_t rec_cap = 0;
     int64_t clock = 0;            // TimestampGeneratorImpl current time
@@ -792,8 +792,9 @@ static int compile_nfa(sh_handle* h, const sh_app_desc* app) {
         return fail(h, SH_E_UNSUPPORTED, err);
     }
     const char* capenv = getenv("SH_NFA_CAPS");  // list,se,node,hold,sched (tests: force growth)
-    if (capenv) sscanf(capenv, "%d,%d,%d,%d,%d", &h->caps[0], &h->caps[1], &h->caps[2], &h->caps[3], &h->caps[4]);
-    nf_set_caps(T, h->caps[0], h->caps[1], h->caps[2], h->caps[3], h->caps[4]);
+    if (capenv) sscanf(capenv, "%d,%d,%d,%d,%d,%d", &h->caps[0], &h->caps[1], &h->caps[2], &h->caps[3], &h->caps[4],
+                       &h->caps[5]);
+    nf_set_caps(T, h->caps[0], h->caps[1], h->caps[2], h->caps[3], h->caps[4], h->caps[5]);
     h->T = T;
     h->mode = 1;
     int nout = 0;
@@ -1406,17 +1407,19 @@ static int nf_upload_table(sh_handle* h) {
 
 // grow the capacities named by `err` and re-lay every key block
 static int nf_grow(sh_handle* h, uint32_t err) {
-    int c[5];
+    int c[6];
     memcpy(c, h->caps, sizeof(c));
+    if (err & NF_E_GRP) c[5] *= 2;
     if (err & NF_E_LIST) c[0] *= 2;
     if (err & NF_E_SE) c[1] *= 2;
     if (err & NF_E_NODE) c[2] *= 2;
     if (err & NF_E_HOLD) c[3] *= 2;
     if (err & NF_E_SCHED) c[4] *= 2;
-    if (c[0] > 60000 || c[1] > (1 << 22) || c[2] > (1 << 24) || c[3] > (1 << 22) || c[4] > (1 << 20))
+    if (c[0] > 60000 || c[1] > (1 << 22) || c[2] > (1 << 24) || c[3] > (1 << 22) || c[4] > (1 << 20) ||
+        c[5] > (1 << 16))
         return fail(h, SH_E_STATE_OVERFLOW, "partial-match state overflow");
     std::unique_ptr<nf_table> old(new nf_table(*h->T));
-    nf_set_caps(h->T, c[0], c[1], c[2], c[3], c[4]);
+    nf_set_caps(h->T, c[0], c[1], c[2], c[3], c[4], c[5]);
     memcpy(h->caps, c, sizeof(c));
     hipStream_t st = h->stream;
     if (h->d_T_old.ensure(sizeof(nf_table))) return fail(h, SH_E_OOM, "table");

@@ -102,6 +102,7 @@ struct nf_layout {
     int32_t hold_cap;       // ReturnEventHolder chunks per run
     int32_t se_words;       // words per StateEvent
     int32_t sched_cap;      // Scheduler toNotify queue capacity
+    int32_t group_cap;      // `group by`: aggregator groups per key
     int64_t off_pstate;     // NF_PS_WORDS per proc
     int64_t off_lists;      // per proc: pending[list_cap] then nae[list_cap] (u32 ids)
     int64_t off_agg;        // 5 words per output
@@ -139,6 +140,8 @@ struct nf_query {
     int32_t order_pc[SH_MAX_ORDER], order_len[SH_MAX_ORDER];
     int64_t limit, offset;          // QuerySelector limit / offset (-1: none)
     int32_t rate_kind, rate_value;  // OutputRateLimiter (enum sh_rate); its counter: qb[3] >> 32
+    int32_t n_group;                // `group by` attributes (aggregator state per group)
+    int32_t group_pc[SH_MAX_GROUP], group_len[SH_MAX_GROUP];
     nf_layout lay;
     int64_t q_off;          // word offset of this query's block inside a key block
     // rise-and-fall sequence `every e1=S, e2=S[f2(e2, e1)]+, e3=S[f3(e3, e2[last])]`
@@ -214,15 +217,22 @@ struct nf_cols {
 #define NF_QH_WORDS 4
 
 NF_INL int64_t nf_round_words(int64_t bytes) { return (bytes + 7) / 8; }
-// the aggregator words (5 per output) + the AllPerEvent limiter's held chunk (first, last)
-NF_INL int64_t nf_agg_words(const nf_query& q) {
-    return (int64_t)q.n_out * 5 + (q.rate_kind == SH_RATE_ALL_EVENTS ? 2 : 0);
+// the aggregator region of a query block: the AllPerEvent limiter's held chunk
+// (first, last: 2 words), then the aggregators -- 5 words per output, or with
+// `group by` a table: a count word + group_cap entries of (value, null) per
+// group-by attribute followed by the group's 5 words per output
+NF_INL int64_t nf_held_words(const nf_query& q) { return q.rate_kind == SH_RATE_ALL_EVENTS ? 2 : 0; }
+NF_INL int64_t nf_group_entry_words(const nf_query& q) { return 2 * (int64_t)q.n_group + (int64_t)q.n_out * 5; }
+NF_INL int64_t nf_agg_words_cap(const nf_query& q, int32_t group_cap) {
+    return nf_held_words(q) + (q.n_group ? 1 + (int64_t)group_cap * nf_group_entry_words(q) : (int64_t)q.n_out * 5);
 }
+NF_INL int64_t nf_agg_words(const nf_query& q) { return nf_agg_words_cap(q, q.lay.group_cap); }
 
 // computes `lay` for query q with the given capacities (host side)
 NF_INL void nf_set_layout(nf_query& q, int32_t n_slots, int32_t list_cap, int32_t se_cap, int32_t node_cap,
-                          int32_t hold_cap, int32_t sched_cap) {
+                          int32_t hold_cap, int32_t sched_cap, int32_t group_cap) {
     nf_layout& L = q.lay;
+    L.group_cap = group_cap;
     L.list_cap = list_cap;
     L.se_cap = se_cap;
     L.node_cap = node_cap;
@@ -455,7 +465,8 @@ enum nf_err {
     NF_E_UNSUP = 64,  // a reference behaviour outside the lowered subset (recursion)
     NF_E_KEY = 128,   // key id out of range
     NF_E_SEV = 256,   // scheduler-history buffer full
-    NF_E_LST = 512    // List-value buffer full
+    NF_E_LST = 512,   // List-value buffer full
+    NF_E_GRP = 1024   // group-by aggregator table of a key full
 };
 
 // ------------------------------------------------------------------ the lane
@@ -1436,8 +1447,48 @@ struct NfLane {
         return (uint64_t)at;
     }
 
+    // the aggregator words of the state event's group (`group by`): GroupByKeyGenerator's
+    // key (the group-by values' toString(), GroupByKeyGenerator.java:60-71) compared as
+    // (value, null) pairs with every NaN of a type alike; a new group takes a fresh entry
+    NF_HD uint64_t* group_aggs(uint32_t s) {
+        uint64_t* tab = qb + Q->lay.off_agg + nf_held_words(*Q);
+        const int ng = Q->n_group;
+        uint64_t g[2 * SH_MAX_GROUP];
+        for (int i = 0; i < ng; i++) {
+            const NfVal v = eval(Q->group_pc[i], Q->group_len[i], s);
+            uint64_t b = v.null ? 0ull : (uint64_t)v.b;
+            if (!v.null && v.t == SH_T_FLOAT && (b & 0x7F800000ull) == 0x7F800000ull && (b & 0x7FFFFFull)) b = 0x7FC00000ull;
+            if (!v.null && v.t == SH_T_DOUBLE && (b & 0x7FF0000000000000ull) == 0x7FF0000000000000ull &&
+                (b & 0xFFFFFFFFFFFFFull))
+                b = 0x7FF8000000000000ull;
+            g[2 * i] = b;
+            g[2 * i + 1] = v.null ? 1ull : 0ull;
+        }
+        const int64_t E = nf_group_entry_words(*Q);
+        const uint64_t n = tab[0];
+        for (uint64_t e = 0; e < n; e++) {
+            uint64_t* ent = tab + 1 + e * E;
+            bool same = true;
+            for (int i = 0; i < 2 * ng && same; i++) same = ent[i] == g[i];
+            if (same) return ent + 2 * ng;
+        }
+        if (n >= (uint64_t)Q->lay.group_cap) {
+            err |= NF_E_GRP;
+            return nullptr;
+        }
+        uint64_t* ent = tab + 1 + n * E;
+        for (int i = 0; i < 2 * ng; i++) ent[i] = g[i];
+        for (int64_t w = 2 * ng; w < E; w++) ent[w] = 0;
+        tab[0] = n + 1;
+        return ent + 2 * ng;
+    }
+
     NF_HD void populate(uint32_t s) {
-        uint64_t* agg = qb + Q->lay.off_agg;
+        uint64_t* agg = qb + Q->lay.off_agg + nf_held_words(*Q);
+        if (Q->n_group && Q->contains_agg) {
+            agg = group_aggs(s);
+            if (!agg) return;
+        }
         uint64_t* out = se_out(s);
         uint64_t mask = se(s)[3];
         for (int o = 0; o < Q->n_out; o++) {
@@ -1635,7 +1686,7 @@ struct NfLane {
             // AllPerEventOutputRateLimiter.process (AllPerEventOutputRateLimiter.java:48-75): every
             // current / expired event joins the held chunk (key block, after the
             // aggregators); the N-th releases it as one chunk
-            uint64_t* hw = qb + Q->lay.off_agg + (int64_t)Q->n_out * 5;
+            uint64_t* hw = qb + Q->lay.off_agg;
             uint32_t held[4] = {(uint32_t)hw[0], (uint32_t)hw[1], 0, 0};
             uint32_t out[4] = {0, 0, 0, 0};
             uint32_t cnt = (uint32_t)(qb[3] >> 32);
@@ -2239,7 +2290,7 @@ struct NfLane {
         for (int i = 0; i < 4; i++) gc_mark(rc[i]);
         const uint32_t nh = n_holders();
         for (uint32_t i = 0; i < 2 * nh; i++) gc_mark(holders()[i]);
-        if (Q->rate_kind == SH_RATE_ALL_EVENTS) gc_mark((uint32_t)qb[Q->lay.off_agg + (int64_t)Q->n_out * 5]);
+        if (Q->rate_kind == SH_RATE_ALL_EVENTS) gc_mark((uint32_t)qb[Q->lay.off_agg]);
         if (in_holder) {
             gc_mark(h_first);
             gc_mark(h_last);

@@ -632,6 +632,22 @@ struct QueryLowering {
                 Q->out_len[o] = 0;
             }
         }
+        // GroupByKeyGenerator's executors (the group key of the aggregators' state)
+        if (q->n_group < 0 || q->n_group > SH_MAX_GROUP) {
+            err = "device engine: at most 4 group-by attributes";
+            return false;
+        }
+        Q->n_group = q->n_group;
+        for (int i = 0; i < q->n_group; i++) {
+            const int e = q->group_expr[i];
+            if (e < 0 || e >= q->n_exprs || q->exprs[e].type == SH_T_OBJECT) {
+                err = "device engine: bad group-by attribute";
+                return false;
+            }
+            Q->group_pc[i] = T->n_code;
+            if (!gen(e, 0)) return false;
+            Q->group_len[i] = T->n_code - Q->group_pc[i];
+        }
         Q->having_pc = -1;
         Q->having_len = 0;
         if (q->having >= 0) {
@@ -770,11 +786,11 @@ int nf_lower(const sh_app_desc* app, nf_table* T, std::string* err) {
     return 0;
 }
 
-void nf_set_caps(nf_table* T, int list_cap, int se_cap, int node_cap, int hold_cap, int sched_cap) {
+void nf_set_caps(nf_table* T, int list_cap, int se_cap, int node_cap, int hold_cap, int sched_cap, int group_cap) {
     int64_t w = 1;  // key header word: bit 0 = partition seen (initPartition done)
     for (int i = 0; i < T->n_queries; i++) {
         nf_query& Q = T->q[i];
-        nf_set_layout(Q, Q.n_proc, list_cap, se_cap, node_cap, hold_cap, sched_cap);
+        nf_set_layout(Q, Q.n_proc, list_cap, se_cap, node_cap, hold_cap, sched_cap, group_cap);
         Q.q_off = w;
         w += Q.lay.words;
     }

@@ -71,7 +71,7 @@ struct nfh {
     uint64_t tick = 1;
     bool started = false;
     std::vector<OutRow> out;
-    int caps[5] = {16, 32, 64, 32, 8};
+    int caps[6] = {16, 32, 64, 32, 8, 4};
     // scheduler-map order models (as sh_host.cpp keeps them)
     bool sm_on = false;
     ShSchedModels sm;
@@ -165,16 +165,19 @@ static bool grow(nfh* h, uint32_t err) {
         err &= ~(uint32_t)NF_E_LST;
         if (!err) return true;
     }
-    int c[5];
+    int c[6];
     memcpy(c, h->caps, sizeof(c));
+    if (err & NF_E_GRP) c[5] *= 2;
     if (err & NF_E_LIST) c[0] *= 2;
     if (err & NF_E_SE) c[1] *= 2;
     if (err & NF_E_NODE) c[2] *= 2;
     if (err & NF_E_HOLD) c[3] *= 2;
     if (err & NF_E_SCHED) c[4] *= 2;
-    if (c[0] > 60000 || c[1] > (1 << 22) || c[2] > (1 << 24) || c[3] > (1 << 22) || c[4] > (1 << 20)) return false;
+    if (c[0] > 60000 || c[1] > (1 << 22) || c[2] > (1 << 24) || c[3] > (1 << 22) || c[4] > (1 << 20) ||
+        c[5] > (1 << 16))
+        return false;
     nf_table old = h->T;
-    nf_set_caps(&h->T, c[0], c[1], c[2], c[3], c[4]);
+    nf_set_caps(&h->T, c[0], c[1], c[2], c[3], c[4], c[5]);
     std::vector<uint64_t> ns((size_t)h->nkeys * h->T.key_words, 0);
     for (int32_t k = 0; k < h->nkeys; k++) {
         const uint64_t* src = h->kstate.data() + (size_t)k * old.key_words;
@@ -396,7 +399,7 @@ nfh* nfh_create(const sh_app_desc* d, char* err, int errlen) {
         h->nuls[s].resize(d->streams[s].n_attrs);
         h->has_nul[s].assign(d->streams[s].n_attrs, false);
     }
-    nf_set_caps(&h->T, h->caps[0], h->caps[1], h->caps[2], h->caps[3], h->caps[4]);
+    nf_set_caps(&h->T, h->caps[0], h->caps[1], h->caps[2], h->caps[3], h->caps[4], h->caps[5]);
     for (int q = 0; q < h->T.n_queries; q++)
         for (int o = 0; o < h->T.q[q].n_out; o++)
             if (h->T.q[q].out_pc[o] == NF_PC_LIST) h->has_lists = true;

@@ -58,8 +58,8 @@ def test_parse_and_lower_having():
     assert 20 in ops  # output-attribute variables (HAVING_STATE)
     d = c.descriptor()
     assert d.queries[0].having == q.having
-    with pytest.raises(compiler.UnsupportedQuery):
-        compiler.compile_app(app.replace("having", "group by e1.sym having"))
+    # group by + having lowers too (tests/test_group_by.py)
+    assert compiler.compile_app(app.replace("having", "group by e1.sym having")).descriptor().queries[0].n_group == 1
 
 
 @pytest.mark.parametrize("seed,case", _apps(120), ids=lambda x: str(x) if isinstance(x, int) else "")
