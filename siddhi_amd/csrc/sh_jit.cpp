@@ -62,6 +62,9 @@ const int kHalo = env_int("SH_JIT_HALO", 256, 0, 1024);
 // predecessors the bucketed matcher's walk loads and evaluates per block
 // (measured on C2: 4 -> 2.04 ms, 8 -> 2.13 ms, 12 -> 2.42 ms per matcher pass)
 const int kWalkBlock = env_int("SH_BK_WALK", 4, 2, 16);
+// the count walk hands consumers out per lane (SH_BK_DYN=0: every lane of a wave
+// walks its consumer to the wave's longest walk)
+const int kWalkDyn = env_int("SH_BK_DYN", 1, 0, 1);
 
 const char* col_ctype(int t) {
     switch (t) {
@@ -912,6 +915,84 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
              "if (roff && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n";
         return s;
     };
+    // the same float-domain count walk with work handed out per lane: a wave owns a
+    // contiguous range of the chunk's consumers; a lane whose walk ended stores its
+    // result and takes the next consumer of the range (ballot rank), so a block of
+    // SHB_D steps runs for busy lanes only instead of every lane waiting for the
+    // wave's longest walk (C2: mean walk 3.4 steps, p90 9, wave max ~15)
+    auto walk_count_f_dyn = [&]() {
+        const bool mx = F.op == SH_OP_GT || F.op == SH_OP_GE;
+        const std::string opn = std::to_string(F.op);
+        const std::string ext = F.dom == DOM_F32 ? (mx ? "__builtin_fmaxf" : "__builtin_fminf")
+                                                 : (mx ? "__builtin_fmax" : "__builtin_fmin");
+        const std::string nan = F.dom == DOM_F32 ? "__builtin_nanf(\"\")" : "__builtin_nan(\"\")";
+        std::string cand_f = "bool ok = true;\n" + unguard(gq.terms(F.f1, "ok")) + unguard(gq.terms(F.ionly, "ok")) +
+                             "{\n" + unguard(gq.yval(F, "y")) + "ok = ok && cmp_op<" + DT + ">(" + opn +
+                             ", xq, y) && !cmp_op<" + DT + ">(" + opn + ", Mx, y);\n}\n";
+        std::string mid_f = "bool mk = true;\n" + unguard(gi.terms(F.qonly, "mk")) + "{\n" + unguard(gi.xval(F, "xr")) +
+                            "Mx = (act && mk) ? " + ext + "(Mx, xr) : Mx;\n}\n";
+        std::string s =
+            "{\n"
+            "const int dl_ = (int)(threadIdx.x & 63u), dw_ = (int)(threadIdx.x >> 6);\n"
+            "const int per_ = (nc + (SHB_TPB / 64) - 1) / (SHB_TPB / 64);\n"
+            "const int c0_ = dw_ * per_ < nc ? dw_ * per_ : nc, c1_ = c0_ + per_ < nc ? c0_ + per_ : nc;\n"
+            "const uint64_t dlt_ = dl_ ? (~0ull >> (64 - dl_)) : 0ull;\n"
+            "int next_ = c0_, ci = -1, sp = 0, i = 0, base = 0;\n"
+            "uint32_t wq = 0u, tlo = 0u, mask = 0u, cext = 0u, roff = 0u, live = 0u;\n" +
+            DT + " xq = 0;\n" + DT + " Mx = " + nan + ";\n"
+            "for (;;) {\n"
+            "    if (ci >= 0 && !live) {\n"
+            "        const uint32_t c_ = (uint32_t)__popc(mask & ~SHB_MOVF) + cext;\n"
+            "        if (roff && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n"
+            "        if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);\n"
+            "        s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);\n"
+            "        s_msk[i - hl] = (uint16_t)mask;\n"
+            "        ci = -1;\n"
+            "    }\n"
+            "    const uint64_t im_ = __ballot(ci < 0);\n"
+            "    const int r_ = (int)__popcll(im_ & dlt_);\n"
+            "    if (ci < 0 && next_ + r_ < c1_) {\n"
+            "        ci = next_ + r_;\n"
+            "        const uint32_t cw = s_cons[ci];\n"
+            "        sp = (int)(cw & 0xFFFFu);\n"
+            "        i = hl + (int)(cw >> 16);\n"
+            "        wq = s_ws[sp];\n"
+            "        const uint32_t tq32 = wq >> kb;\n"
+            "        tlo = tq32 > SHB_WLIM ? tq32 - SHB_WLIM : 0u;\n" +
+            decl_attrs(need_q, 1) + loads(need_q, "x1_", "sp") + "xq = 0;\n" + qhead +
+            "        Mx = " + nan + ";\n"
+            "        mask = 0u; cext = 0u; roff = 0u; base = 0;\n"
+            "        live = (qok && xq == xq) ? 1u : 0u;\n"
+            "        if (live && sp >= 1) {\n"
+            "            const uint32_t wp = s_ws[sp - 1];\n"
+            "            if (((wp ^ wq) & kmask) == 0u && (wp >> kb) > tq32) atomicOr(P.flag, SHB_F_MONO);\n"
+            "        }\n"
+            "    }\n"
+            "    next_ += (int)__popcll(im_);\n"
+            "    if (__ballot(ci >= 0) == 0ull) break;\n"
+            "    uint32_t wv[SHB_D];\n";
+        for (int a : need_r)
+            s += std::string(col_ctype(P.attr_type[0][a])) + " av" + std::to_string(a) + "[SHB_D];\n";
+        s += "#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n    const int o0 = sp - 1 - base - u;\n"
+             "    const int o = o0 < 0 ? 0 : o0;\n    wv[u] = s_ws[o];\n";
+        for (int a : need_r) s += "    av" + std::to_string(a) + "[u] = " + lds(a) + "[o];\n";
+        s += "}\n" + decl_attrs(need_r, 0) +
+             "#pragma unroll\nfor (int u = 0; u < SHB_D; u++) {\n"
+             "    const int step = base + u;\n"
+             "    const uint32_t same = (u < sp - base && ((wv[u] ^ wq) & kmask) == 0u) ? 1u : 0u;\n"
+             "    roff |= live & (same ^ 1u);\n"
+             "    const uint32_t act = live & same & ((wv[u] >> kb) >= tlo ? 1u : 0u);\n";
+        for (int a : need_r)
+            s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
+        s += "    {\n" + cand_f +
+             "    const uint32_t cons = act & (ok ? 1u : 0u);\n"
+             "    if (step < SHB_MSTEPS) mask |= cons << step;\n"
+             "    else { cext += cons; mask |= cons ? SHB_MOVF : 0u; }\n    }\n";
+        s += "    {\n" + mid_f + "    }\n    live = act & (cmp_op<" + DT + ">(" + (mx ? std::to_string(SH_OP_GE)
+                                                                                  : std::to_string(SH_OP_LE)) +
+             ", Mx, xq) ? 0u : 1u);\n}\nbase += SHB_D;\n}\n}\n";
+        return s;
+    };
     auto walk = [&](bool count, const std::string& on_consumed) {
         return head() + slow(count, on_consumed, "sp - 1");
     };
@@ -1052,18 +1133,25 @@ for (int k = 0; k < SHB_NR; k++) {
     src += R"(}
 __syncthreads();
 SHB_PROF(1)
-// consumers (chunk events) in sorted order: partials taken per event
+)";
+    if (fdom && kWalkDyn) {
+        // consumers (chunk events): per-lane work hand-out over each wave's range
+        src += "// consumers (chunk events): partials taken per event\n" + walk_count_f_dyn() + "__syncthreads();\n";
+    } else {
+        src += R"(// consumers (chunk events) in sorted order: partials taken per event
 for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {
 const uint32_t cw = s_cons[ci];
 const int sp = (int)(cw & 0xFFFFu), i = hl + (int)(cw >> 16);
 uint32_t c_ = 0;
 )";
-    src += fdom ? walk_count_f() : walk_count();
-    src += R"(if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);
+        src += fdom ? walk_count_f() : walk_count();
+        src += R"(if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);
 s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);
 s_msk[i - hl] = (uint16_t)mask;
 }
-__syncthreads();
+__syncthreads();)";
+    }
+    src += R"(
 SHB_PROF(2)
 // exclusive prefix of the counts over the chunk (arrival order inside the
 // bucket); the counts go out as bytes, 8 per thread
