@@ -610,7 +610,8 @@ static int lower_chain(sh_handle* h, const sh_app_desc* app, int qi, shp_program
 static bool has_selector_extras(const sh_app_desc* app) {
     for (int32_t q = 0; q < app->n_queries; q++) {
         const sh_query_desc& d = app->queries[q];
-        if (d.having >= 0 || d.n_order > 0 || d.limit >= 0 || d.offset >= 0 || d.rate_kind != SH_RATE_NONE)
+        if (d.having >= 0 || d.n_order > 0 || d.limit >= 0 || d.offset >= 0 || d.rate_kind != SH_RATE_NONE ||
+            d.n_group > 0)
             return true;
         // a List output (SH_OP_MULTI_VAR) is built by the general engine's selector
         for (int32_t o = 0; o < d.n_outputs; o++)
