@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "../../include/sh_query.h"
 #include "sh_agg.h"
 #include "sh_device.h"
@@ -113,40 +115,66 @@ __global__ void __launch_bounds__(SHA_TPB) k_sha_prep(const uint64_t* __restrict
                                                       const int32_t* __restrict__ keys, int32_t nkeys,
                                                       uint64_t seq_base, sha_desc D, uint32_t* __restrict__ seg,
                                                       uint32_t* __restrict__ idx, int32_t* __restrict__ range) {
-    const int64_t r = (int64_t)blockIdx.x * SHA_TPB + threadIdx.x;
-    if (r < m) {
+    // grid-stride over the rows with the exponent range per column in registers,
+    // then one reduction per workgroup: the range words are a handful of
+    // addresses, so per-wave atomics would serialise on them
+    int lo[SHA_MAX_COLS], hi[SHA_MAX_COLS], bad[SHA_MAX_COLS];
+#pragma unroll
+    for (int k = 0; k < SHA_MAX_COLS; k++) {
+        lo[k] = 1 << 30;
+        hi[k] = -(1 << 30);
+        bad[k] = 0;
+    }
+    for (int64_t r = (int64_t)blockIdx.x * SHA_TPB + threadIdx.x; r < m; r += (int64_t)gridDim.x * SHA_TPB) {
         const int64_t key = keys ? keys[seq[r] - seq_base] : 0;
         const int64_t q = query ? query[r] : 0;
         seg[r] = (uint32_t)(q * nkeys + key);
         idx[r] = (uint32_t)r;
-    }
-    for (int k = 0; k < D.n_cols; k++) {
-        const sha_col c = D.c[k];
-        if (!sha_fp(c)) continue;
-        int lo = 1 << 30, hi = -(1 << 30), bad = 0;
-        if (r < m) {
+#pragma unroll
+        for (int k = 0; k < SHA_MAX_COLS; k++) {
+            const sha_col c = D.c[k];
+            if (k >= D.n_cols || !sha_fp(c)) continue;
             const double d = sha_as_double(vals[r * n_out + c.col], c.arg_type);
             if (!isfinite(d)) {
-                bad = 1;
+                bad[k] = 1;
             } else if (d != 0.0) {
                 uint64_t mm;
                 int e, ng;
                 sha_split(d, &mm, &e, &ng);
-                lo = e;
-                hi = e + 63 - __builtin_clzll(mm);
+                lo[k] = min(lo[k], e);
+                hi[k] = max(hi[k], e + 63 - __builtin_clzll(mm));
             }
         }
-        // wave reductions, then one atomic per wave
+    }
+    __shared__ int s_r[SHA_TPB / 64][SHA_MAX_COLS][3];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < SHA_MAX_COLS; k++) {
+        if (k >= D.n_cols) continue;
+        int l = lo[k], h = hi[k], b = bad[k];
         for (int o = 32; o > 0; o >>= 1) {
-            lo = min(lo, __shfl_xor(lo, o));
-            hi = max(hi, __shfl_xor(hi, o));
-            bad |= __shfl_xor(bad, o);
+            l = min(l, __shfl_xor(l, o));
+            h = max(h, __shfl_xor(h, o));
+            b |= __shfl_xor(b, o);
         }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(&range[3 * k], lo);
-            atomicMax(&range[3 * k + 1], hi);
-            if (bad) atomicOr(&range[3 * k + 2], 1);
+        if (lane == 0) {
+            s_r[wave][k][0] = l;
+            s_r[wave][k][1] = h;
+            s_r[wave][k][2] = b;
         }
+    }
+    __syncthreads();
+    const int k = threadIdx.x;
+    if (k < D.n_cols && sha_fp(D.c[k])) {
+        int l = s_r[0][k][0], h = s_r[0][k][1], b = s_r[0][k][2];
+        for (int w = 1; w < SHA_TPB / 64; w++) {
+            l = min(l, s_r[w][k][0]);
+            h = max(h, s_r[w][k][1]);
+            b |= s_r[w][k][2];
+        }
+        atomicMin(&range[3 * k], l);
+        atomicMax(&range[3 * k + 1], h);
+        if (b) atomicOr(&range[3 * k + 2], 1);
     }
 }
 
@@ -433,7 +461,7 @@ extern "C" int sha_running(const uint64_t* d_seq, int64_t* d_vals, int32_t n_out
     hipMemcpyAsync(range, h_range, sizeof(h_range), hipMemcpyHostToDevice, st);
     hipMemsetAsync(range + 3 * SHA_MAX_COLS, 0, 4, st);
     const unsigned g = (unsigned)((m + SHA_TPB - 1) / SHA_TPB);
-    hipLaunchKernelGGL(k_sha_prep, dim3(g), dim3(SHA_TPB), 0, st, d_seq, (const int64_t*)d_vals, n_out, m, d_query,
+    hipLaunchKernelGGL(k_sha_prep, dim3((unsigned)std::min<int64_t>(g, 2048)), dim3(SHA_TPB), 0, st, d_seq, (const int64_t*)d_vals, n_out, m, d_query,
                        d_keys, n_keys, seq_base, *D, seg, idx, range);
     if (sha_ok()) return -3;
     int bits = 0;

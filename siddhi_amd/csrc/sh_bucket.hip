@@ -303,7 +303,9 @@ __global__ void __launch_bounds__(256) k_bk_ttot(shb_plan P) {
 // ---------------------------------------------------------------- emitter
 // per event (registers): bucket d | count << 8 | rank << 16, and its
 // match-stream position; the select list lives in LDS (uniform per output)
-template <bool COLS>  // COLS: typed output columns (OC.cols), else raw 8-byte rows
+// COLS: typed output columns (OC.cols), else raw 8-byte rows; NO: the select width
+// (1..8: unrolled, the descriptors in scalar registers; 0: any width, a loop)
+template <bool COLS, int NO>
 __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ keys, shb_plan P, shb_out O,
                                                     shb_cols OC, uint64_t seq_base, uint64_t* __restrict__ out_seq,
                                                     int64_t* __restrict__ out_vals, int64_t out_cap) {
@@ -441,24 +443,26 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(const int32_t* __restrict__ 
                 if (!out_vals && !COLS) continue;
                 // output descriptors straight from the kernel arguments (scalar
                 // registers: uniform branches)
-                if (no == 4) {
+                if (NO > 0) {
                     const int64_t mp = (int64_t)blk_mpos[e] + k;
-                    const int64_t v0 = bk_raw(O.src[0], O.kind[0] == 1 ? i : mp, O.type[0]);
-                    const int64_t v1 = bk_raw(O.src[1], O.kind[1] == 1 ? i : mp, O.type[1]);
-                    const int64_t v2 = bk_raw(O.src[2], O.kind[2] == 1 ? i : mp, O.type[2]);
-                    const int64_t v3 = bk_raw(O.src[3], O.kind[3] == 1 ? i : mp, O.type[3]);
+                    int64_t v[NO > 0 ? NO : 1];
+#pragma unroll
+                    for (int o = 0; o < NO; o++) v[o] = bk_raw(O.src[o], O.kind[o] == 1 ? i : mp, O.type[o]);
                     if (COLS) {
                         // typed columns: consecutive lanes, consecutive elements of each column
-                        bk_put(OC.cols[0], OC.colw[0], row, v0);
-                        bk_put(OC.cols[1], OC.colw[1], row, v1);
-                        bk_put(OC.cols[2], OC.colw[2], row, v2);
-                        bk_put(OC.cols[3], OC.colw[3], row, v3);
+#pragma unroll
+                        for (int o = 0; o < NO; o++) bk_put(OC.cols[o], OC.colw[o], row, v[o]);
                         continue;
                     }
-                    // a 32-byte row as two 16-byte stores: consecutive lanes fill whole lines
-                    longlong2* dst = (longlong2*)(out_vals + row * 4);
-                    dst[0] = make_longlong2(v0, v1);
-                    dst[1] = make_longlong2(v2, v3);
+                    if (NO % 2 == 0) {
+                        // a row of NO words as 16-byte stores: consecutive lanes fill whole lines
+                        longlong2* dst = (longlong2*)(out_vals + row * NO);
+#pragma unroll
+                        for (int o = 0; o < NO; o += 2) dst[o / 2] = make_longlong2(v[o], v[o + 1]);
+                    } else {
+#pragma unroll
+                        for (int o = 0; o < NO; o++) out_vals[row * NO + o] = v[o];
+                    }
                     continue;
                 }
                 for (int o = 0; o < no; o++) {
@@ -525,14 +529,35 @@ extern "C" int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream) {
     return shd_exclusive_scan(P->ttot, P->ttot, (int64_t)P->nt + 1, scan_tmp, stream);
 }
 
+template <bool COLS, int NO>
+static void bk_emit_launch(const int32_t* keys, const shb_plan* P, const shb_out* O, const shb_cols& OC,
+                           uint64_t seq_base, uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
+    hipLaunchKernelGGL((k_bk_emit<COLS, NO>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O,
+                       OC, seq_base, out_seq, out_vals, out_cap);
+}
+
+template <bool COLS>
+static void bk_emit_width(const int32_t* keys, const shb_plan* P, const shb_out* O, const shb_cols& OC,
+                          uint64_t seq_base, uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
+    switch (O->n_out) {
+        case 1: bk_emit_launch<COLS, 1>(keys, P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 2: bk_emit_launch<COLS, 2>(keys, P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 3: bk_emit_launch<COLS, 3>(keys, P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 4: bk_emit_launch<COLS, 4>(keys, P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 5: bk_emit_launch<COLS, 5>(keys, P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 6: bk_emit_launch<COLS, 6>(keys, P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 7: bk_emit_launch<COLS, 7>(keys, P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 8: bk_emit_launch<COLS, 8>(keys, P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        default: bk_emit_launch<COLS, 0>(keys, P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+    }
+}
+
 extern "C" int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, const shb_cols* OC,
                         uint64_t seq_base, uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
     if (OC && OC->use)
-        hipLaunchKernelGGL(k_bk_emit<true>, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O,
-                           *OC, seq_base, out_seq, out_vals, out_cap);
+        bk_emit_width<true>(keys, P, O, *OC, seq_base, out_seq, out_vals, out_cap, stream);
     else
-        hipLaunchKernelGGL(k_bk_emit<false>, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, keys, *P, *O,
-                           shb_cols{}, seq_base, out_seq, out_vals, out_cap);
+        bk_emit_width<false>(keys, P, O, shb_cols{}, seq_base, out_seq, out_vals, out_cap, stream);
     return bk_ok();
 }
 

@@ -2658,7 +2658,10 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device");
     if (h->app.n_streams != 1) return fail(h, SH_E_UNSUPPORTED, "sh_run_device: single-stream apps only");
     if (run->n <= 0 || run->n > 0x7FFFFFFFll) return fail(h, SH_E_INVALID_ARG, "sh_run_device: 1 <= n < 2^31");
-    h->stream = run->stream ? (hipStream_t)run->stream : h->own_stream;
+    // NULL = the default (null) stream, as the header says: the caller's buffers
+    // were written there (the handle's own stream is non-blocking and would not
+    // wait for them)
+    h->stream = (hipStream_t)run->stream;
     if (h->has_rules && (h->mode == 2 || !getenv("SH_DISABLE_RULES"))) {
         const int crc = rows_for_cols(h, run);
         if (crc) return crc;
