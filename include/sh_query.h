@@ -171,7 +171,8 @@ typedef struct sh_query_desc {
     int32_t rate_kind;           /* enum sh_rate: the query's OutputRateLimiter (OutputParser.constructOutputRateLimiter) */
     int64_t limit;               /* QuerySelector.limit, -1 if none (SelectorParser.java:115-123) */
     int64_t offset;              /* QuerySelector.offset, -1 if none (:124-132)  */
-    int32_t rate_value;          /* events per period (SH_RATE_FIRST_EVENTS / _LAST_EVENTS / _ALL_EVENTS) */
+    int32_t rate_value;          /* events per period (SH_RATE_FIRST_EVENTS / _LAST_EVENTS / _ALL_EVENTS),
+                                    or the period in ms (SH_RATE_FIRST_TIME) */
     int32_t n_group;             /* `group by` attributes (GroupByKeyGenerator, SelectorParser.java:102-108), 0 if none */
     int32_t group_expr[SH_MAX_GROUP]; /* variable expression per group-by attribute (UNKNOWN_STATE, default index 0):
                                     the aggregators keep one state per (partition key, group key) */
@@ -181,7 +182,9 @@ typedef struct sh_query_desc {
    `output first every N events` (FirstPerEventOutputRateLimiter.java:47-72) or
    `output last every N events` (LastPerEventOutputRateLimiter.java:45-68) */
 enum sh_rate { SH_RATE_NONE = 0, SH_RATE_FIRST_EVENTS = 1, SH_RATE_LAST_EVENTS = 2,
-               SH_RATE_ALL_EVENTS = 3 /* `output [all] every N events`: AllPerEventOutputRateLimiter */ };
+               SH_RATE_ALL_EVENTS = 3, /* `output [all] every N events`: AllPerEventOutputRateLimiter */
+               SH_RATE_FIRST_TIME = 4  /* `output first every T` (rate_value = T in ms), playback apps:
+                                          FirstPerTimeOutputRateLimiter.java:53-75 against the playback clock */ };
 
 typedef struct sh_app_desc {
     int32_t version;             /* SH_DESC_VERSION                            */

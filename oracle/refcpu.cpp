@@ -505,6 +505,7 @@ struct Selector : Proc {
     void rateProcess(Chunk<StateEvent>& c);
     std::unordered_map<int64_t, int32_t> rateCounter;  // RateLimiterState per partition flow
     std::unordered_map<int64_t, Chunk<StateEvent>> rateHeld;  // AllPerEvent: allComplexEventChunk per partition flow
+    std::unordered_map<int64_t, int64_t> rateOutTime;         // FirstPerTime: RateLimiterState.outputTime (absent: null)
     void sendToCallBacks(Chunk<StateEvent>& c);
 };
 
@@ -2232,6 +2233,25 @@ void Selector::limitChunk(Chunk<StateEvent>& c) {
 // with its counter in a per-partition state (int arithmetic: FIRST with N == 1 never resets)
 void Selector::rateProcess(Chunk<StateEvent>& c) {
     const int kind = q->d.rate_kind;
+    if (kind == SH_RATE_FIRST_TIME) {
+        // FirstPerTimeOutputRateLimiter.process (FirstPerTimeOutputRateLimiter.java:53-75): the
+        // chunk's first event passes when the partition's outputTime is null or
+        // outputTime + value <= the timestamp generator's current time (playback: the
+        // clock InputHandler.send moved), which becomes the new outputTime
+        const int64_t now = q->app->clock;
+        auto it = rateOutTime.find(q->app->flow.key);
+        if (it == rateOutTime.end() || (int64_t)((uint64_t)it->second + (uint64_t)q->d.rate_value) <= now) {
+            rateOutTime[q->app->flow.key] = now;
+            c.reset();
+            SE ev = c.next();
+            c.remove();
+            Chunk<StateEvent> out;
+            out.add(ev);
+            out.reset();
+            sendToCallBacks(out);
+        }
+        return;
+    }
     if (kind != SH_RATE_FIRST_EVENTS && kind != SH_RATE_LAST_EVENTS && kind != SH_RATE_ALL_EVENTS) {
         sendToCallBacks(c);
         return;
@@ -2733,8 +2753,11 @@ ref_app* ref_create(const sh_app_desc* d, char* err, int errlen) {
         if (agg && (qd.offset > 0 || qd.limit == 0)) serr = "aggregating selector with offset > 0 or limit 0";
         if (qd.rate_kind != SH_RATE_NONE &&
             ((qd.rate_kind != SH_RATE_FIRST_EVENTS && qd.rate_kind != SH_RATE_LAST_EVENTS &&
-              qd.rate_kind != SH_RATE_ALL_EVENTS) || qd.rate_value < 1))
-            serr = "output rate limiting: `output first|last every N events` only";
+              qd.rate_kind != SH_RATE_ALL_EVENTS && qd.rate_kind != SH_RATE_FIRST_TIME) ||
+             qd.rate_value < (qd.rate_kind == SH_RATE_FIRST_TIME ? 0 : 1)))
+            serr = "output rate limiting: `output [first|last|all] every N events` or `output first every T`";
+        if (qd.rate_kind == SH_RATE_FIRST_TIME && !d->playback)
+            serr = "output first every T: the limiter reads the wall clock outside @app:playback";
         if (!serr.empty()) {
             delete ra;
             return fail("query " + std::to_string(qi) + ": " + serr);

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 600 python -u -m pytest tests/test_gpu_c3.py tests/test_gpu_agg.py tests/test_gpu_nfa.py -x -v -rs --timeout 300 --timeout-method thread > gpurun_out/r3k_tests.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_c3.py tests/test_gpu_agg.py tests/test_gpu_nfa.py tests/test_rate_limit.py tests/test_gpu_rules.py -x -v -rs --timeout 300 --timeout-method thread > gpurun_out/r3k_tests.log 2>&1; rc=$?
 grep -E "passed|failed" gpurun_out/r3k_tests.log | tail -2
 [ $rc -ne 0 ] && { grep -E "FAIL|Error" gpurun_out/r3k_tests.log | head -20; tail -40 gpurun_out/r3k_tests.log; exit 1; }
 timeout -k 10 400 python -u bench.py --config c3 --steps 10 --warmup 3 > gpurun_out/r3k_c3.json 2> gpurun_out/r3k_c3.err || { tail -20 gpurun_out/r3k_c3.err; exit 1; }

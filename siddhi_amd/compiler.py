@@ -506,15 +506,27 @@ class Parser:
                     break
             self.expect_kw("every")
             tk = self.peek()
-            if kind == "snapshot" or tk.kind != "num" or not self.peek(1).text.lower() == "events":
-                raise UnsupportedQuery("output rate limiting: only `output [first|last|all] every N events` runs "
-                                       "on the device")
-            n = int(self.next().text)
-            self.next()  # events
-            if n < 1:
-                raise UnsupportedQuery(f"output {kind} every 0 events")
-            # OutputParser.constructOutputRateLimiter: no keyword is ALL
-            rate = ({"first": 1, "last": 2}.get(kind, 3), n)
+            if kind == "first" and tk.kind == "num" and self.peek(1).kind == "id" and \
+                    self.peek(1).text.lower() in _TIME_UNITS:
+                # FirstPerTimeOutputRateLimiter against the timestamp generator's clock
+                # (playback apps only: checked when the query is lowered)
+                ms = self.time_value()
+                if ms >= 1 << 31:
+                    raise UnsupportedQuery("output first every T: T >= 2^31 ms")
+                rate = (4, ms)
+            elif kind == "snapshot" or tk.kind != "num" or not self.peek(1).text.lower() == "events":
+                # LastPerTime / AllPerTime schedule from System.currentTimeMillis() when a
+                # partition is created (AllPerTimeOutputRateLimiter.java:97-108), even in
+                # playback, and the snapshot limiters run on such a timer: no replayable answer
+                raise UnsupportedQuery("output rate limiting: `output [first|last|all] every N events` and "
+                                       "`output first every T` (@app:playback) run on the device")
+            else:
+                n = int(self.next().text)
+                self.next()  # events
+                if n < 1:
+                    raise UnsupportedQuery(f"output {kind} every 0 events")
+                # OutputParser.constructOutputRateLimiter: no keyword is ALL
+                rate = ({"first": 1, "last": 2}.get(kind, 3), n)
         self.expect_kw("insert")
         if self.kw("current"):
             self.next()
@@ -866,9 +878,12 @@ class Lowerer:
             raise UnsupportedQuery(f"group by: at most {abi.SH_MAX_GROUP} attributes")
         for v in q.group_by:
             self.group.append(self.expr(v, UNKNOWN_STATE, 0))
-        if q.group_by and q.rate and q.rate[0] in (1, 2):
+        if q.group_by and q.rate and q.rate[0] in (1, 2, 4):
             # OutputParser picks the GroupBy first / last limiters (one counter per group)
-            raise UnsupportedQuery("group by with `output first|last every N events` (per-group limiters)")
+            raise UnsupportedQuery("group by with `output first|last every ...` (per-group limiters)")
+        if q.rate and q.rate[0] == 4 and not self.app.playback:
+            # TimestampGeneratorImpl.currentTime is System.currentTimeMillis() outside playback
+            raise UnsupportedQuery("output first every T outside @app:playback reads the wall clock")
         self.order = []
         if len(q.order_by) > abi.SH_MAX_ORDER:
             raise UnsupportedQuery(f"order by: at most {abi.SH_MAX_ORDER} attributes")

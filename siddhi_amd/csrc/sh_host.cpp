@@ -1583,7 +1583,7 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
 
 // one or more send() calls resident on the device, processed by k_nfa_run
 static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid, int* alias,
-                       bool used_only = false);
+                       bool used_only = false, bool with_ts = true);
 
 // `carry` (sh_run_device, single stream): ts and the stream-0 columns are moved
 // into key-segment order by the segment, so each lane streams its own events
@@ -1609,8 +1609,12 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     void* mid[8] = {nullptr};
     int alias = -1;
     const bool sorted_cols = carry_run && B.keys && h->stream_types[0].size() <= 7;
+    // the rise-and-fall sequence engine: fresh single-query runs of that shape; its
+    // device-resident rows carry no timestamps, so the segment leaves them behind
+    const bool s3_shape = fresh && h->T->n_queries == 1 && h->T->q[0].s3 && !h->no_seq3 && !getenv("SH_NO_SEQ3");
+    const bool sorted_ts = !(s3_shape && d_seq);
     if (sorted_cols) {
-        if (carry_setup(h, carry_run, &carry, mid, &alias, true)) return fail(h, SH_E_OOM, "sorted columns");
+        if (carry_setup(h, carry_run, &carry, mid, &alias, true, sorted_ts)) return fail(h, SH_E_OOM, "sorted columns");
         for (size_t a = 0; a < h->stream_types[0].size(); a++)
             if (a >= 32 || ((h->T->attr_used[0] >> a) & 1u)) cols.col[0][a] = h->v_scol[a].p;
     }
@@ -1643,7 +1647,19 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     E.perm = perm;
     E.seq_base = B.seq_base;
     E.batch_events = batch_events;
-    E.sts = sorted_cols ? h->v_sts.as<int64_t>() : nullptr;
+    E.sts = sorted_cols && sorted_ts ? h->v_sts.as<int64_t>() : nullptr;
+    // k_seq3's LDS-staged form: every operand and output of the one attribute A
+    // (4 bytes, no null mask), read from its key-ordered copy
+    const void* s3_col = nullptr;
+    if (s3_shape && sorted_cols) {
+        const nf_query& Q = h->T->q[0];
+        const int A = Q.s3_a2, ty = Q.s3_t2;
+        bool ok = (ty == SH_T_FLOAT || ty == SH_T_INT) && A >= 0 && A < (int)h->stream_types[0].size() &&
+                  type_width(h->stream_types[0][A]) == 4 && Q.s3_a3 == A && Q.s3_e1a == A && Q.s3_la == A &&
+                  Q.s3_t3 == ty && Q.s3_e1t == ty && Q.s3_lt == ty && !cols.nul[0][A];
+        for (int o = 0; o < Q.n_out && ok; o++) ok = Q.s3_out_attr[o] == A && Q.s3_out_type[o] == ty;
+        if (ok) s3_col = alias == A ? (const void*)skeys : (const void*)cols.col[0][A];
+    }
     E.sorted_rows = sorted_cols ? 1 : 0;
     E.pad = 0;
     E.run = fresh ? h->dev_run_ids : nullptr;
@@ -1680,11 +1696,11 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
         }
         nfd_emit em = nf_emit(h);
         // the rise-and-fall sequence engine: fresh single-query runs of that shape
-        const bool seq3 = fresh && h->T->n_queries == 1 && h->T->q[0].s3 && !h->no_seq3 && !getenv("SH_NO_SEQ3");
+        const bool seq3 = s3_shape;
         h->seq3_last = seq3 ? 1 : 0;
         if (seq3) {
             if (nfd_seq3(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), &E, n, seg_list, nseg, skeys, nkeys, max_seg,
-                         &em, st))
+                         &em, st, s3_col))
                 return fail(h, SH_E_HIP, "k_seq3 launch failed");
         } else if (nfd_run(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), &E, n,
                            seg_list, nseg, skeys, nkeys, max_seg, h->tick, h->clock, &em, st))
@@ -2272,17 +2288,19 @@ static shd_segment_ws seg_ws(sh_handle* h, int64_t n) {
 // sorted key array (*alias = that attribute, -1 if none). Null-key events
 // (sorted to the sentinel bucket) are never read.
 static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid, int* alias,
-                       bool used_only) {
+                       bool used_only, bool with_ts) {
     const int64_t n = run->n;
     const int na = (int)h->stream_types[0].size();
     memset(carry, 0, sizeof(*carry));
     *alias = -1;
-    if (h->v_sts.ensure_fresh(n * 8) || h->v_mid_ts.ensure_fresh(n * 8)) return SH_E_OOM;
     int c = 0;
-    carry->src[c] = run->d_ts;
-    carry->dst[c] = h->v_sts.p;
-    carry->width[c] = 8;
-    mid[c++] = h->v_mid_ts.p;
+    if (with_ts) {
+        if (h->v_sts.ensure_fresh(n * 8) || h->v_mid_ts.ensure_fresh(n * 8)) return SH_E_OOM;
+        carry->src[c] = run->d_ts;
+        carry->dst[c] = h->v_sts.p;
+        carry->width[c] = 8;
+        mid[c++] = h->v_mid_ts.p;
+    }
     for (int a = 0; a < na; a++) {
         const int w = type_width(h->stream_types[0][a]);
         if (used_only && h->T && a < 32 && !((h->T->attr_used[0] >> a) & 1u)) continue;  // no expression reads it

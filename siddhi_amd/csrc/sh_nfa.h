@@ -221,7 +221,10 @@ NF_INL int64_t nf_round_words(int64_t bytes) { return (bytes + 7) / 8; }
 // (first, last: 2 words), then the aggregators -- 5 words per output, or with
 // `group by` a table: a count word + group_cap entries of (value, null) per
 // group-by attribute followed by the group's 5 words per output
-NF_INL int64_t nf_held_words(const nf_query& q) { return q.rate_kind == SH_RATE_ALL_EVENTS ? 2 : 0; }
+// (the FirstPerTime limiter's RateLimiterState: outputTime set, outputTime: 2 words)
+NF_INL int64_t nf_held_words(const nf_query& q) {
+    return q.rate_kind == SH_RATE_ALL_EVENTS || q.rate_kind == SH_RATE_FIRST_TIME ? 2 : 0;
+}
 NF_INL int64_t nf_group_entry_words(const nf_query& q) { return 2 * (int64_t)q.n_group + (int64_t)q.n_out * 5; }
 NF_INL int64_t nf_agg_words_cap(const nf_query& q, int32_t group_cap) {
     return nf_held_words(q) + (q.n_group ? 1 + (int64_t)group_cap * nf_group_entry_words(q) : (int64_t)q.n_out * 5);
@@ -1682,6 +1685,23 @@ struct NfLane {
     // the reference: only the first event ever passes); LastPerEventOutputRateLimiter
     // (LastPerEventOutputRateLimiter.java:45-68) keeps every N-th current event
     NF_HD void rate_send(uint32_t* c) {
+        if (Q->rate_kind == SH_RATE_FIRST_TIME) {
+            // FirstPerTimeOutputRateLimiter.process (FirstPerTimeOutputRateLimiter.java:53-75):
+            // the chunk's first event passes when the partition's outputTime is unset or
+            // outputTime + T <= the playback clock, which becomes the new outputTime
+            uint64_t* hw = qb + Q->lay.off_agg;
+            if (hw[0] != 0 && (int64_t)(hw[1] + (uint64_t)(int64_t)Q->rate_value) > clock) return;
+            hw[0] = 1;
+            hw[1] = (uint64_t)clock;
+            ch_reset(c);
+            const uint32_t ev = ch_next(c);
+            ch_remove(c);
+            uint32_t out[4] = {0, 0, 0, 0};
+            ch_add(out, ev);
+            ch_reset(out);
+            send_to_callbacks(out);
+            return;
+        }
         if (Q->rate_kind == SH_RATE_ALL_EVENTS) {
             // AllPerEventOutputRateLimiter.process (AllPerEventOutputRateLimiter.java:48-75): every
             // current / expired event joins the held chunk (key block, after the

@@ -263,6 +263,116 @@ __global__ void __launch_bounds__(NF_TPB) k_seq3(const nf_table* __restrict__ T,
     if (fail) atomicOr(EM.err, (unsigned)NF_E_EMIT);
 }
 
+// The same sequence, LDS-staged: when every operand and output reads one 4-byte
+// attribute without a null mask (C3), a workgroup owns 256 consecutive key
+// segments, one per lane, and sweeps their key-ordered events in chunks the
+// whole workgroup loads coalesced into LDS (value + arrival index); each lane
+// walks its own key's events of the chunk from LDS. k_seq3's lane-strided loads
+// touch one line per lane per load and lose most lines before the lane returns.
+#define S3S_TPB 256
+#define S3S_CH 4096
+__device__ __forceinline__ NfVal s3_bits(uint32_t b, int t) {
+    NfVal v;
+    v.t = (uint8_t)t;
+    v.null = 0;
+    v.b = t == SH_T_INT ? (int64_t)(int32_t)b : (int64_t)b;
+    return v;
+}
+
+__global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ T, const uint32_t* __restrict__ col,
+                                                   const uint32_t* __restrict__ perm, uint64_t seq_base, int64_t n,
+                                                   const uint32_t* __restrict__ seg_list,
+                                                   const uint32_t* __restrict__ nseg,
+                                                   const uint32_t* __restrict__ skeys, int32_t nkeys, nfd_emit EM) {
+    __shared__ uint32_t sv[S3S_CH], sp[S3S_CH];
+    __shared__ int64_t s_end;
+    const uint32_t ns = *nseg;
+    const uint32_t s0 = blockIdx.x * S3S_TPB;
+    if (s0 >= ns) return;  // uniform per workgroup
+    const uint32_t sl = min(s0 + (uint32_t)S3S_TPB, ns) - 1u;  // the workgroup's last segment
+    if (threadIdx.x == 0) {
+        // segments are listed in order; only the last one may be followed by the
+        // null-key run
+        int64_t e;
+        if (sl + 1u < ns) {
+            e = seg_list[sl + 1u];
+        } else if (!skeys) {
+            e = n;
+        } else {
+            const uint32_t k = skeys[seg_list[sl]];
+            e = (int64_t)seg_list[sl] + 1;
+            while (e < n && skeys[e] == k) e++;
+        }
+        s_end = e;
+    }
+    __syncthreads();
+    const int64_t P0 = seg_list[s0], P1 = s_end;
+    const uint32_t sidx = s0 + threadIdx.x;
+    int64_t b = P1, e = P1;  // lanes past the last segment: empty
+    if (sidx <= sl) {
+        b = seg_list[sidx];
+        e = sidx < sl ? (int64_t)seg_list[sidx + 1u] : P1;
+        if ((skeys ? skeys[b] : 0u) >= (uint32_t)nkeys) {
+            atomicOr(EM.err, (unsigned)NF_E_KEY);
+            b = e = P1;
+        }
+    }
+    const nf_query& Q = T->q[0];
+    const int t = Q.s3_t2;  // the one attribute's type (checked on the host)
+    const int op2 = Q.s3_op2, dom2 = Q.s3_dom2, op3 = Q.s3_op3, dom3 = Q.s3_dom3, no = Q.n_out;
+    DevSink sink;
+    sink.buf = EM.recs;
+    sink.ctr = EM.ctr;
+    sink.cap = EM.cap;
+    sink.stride = EM.stride;
+    sink.chunk = nullptr;
+    sink.used = sink.n = 0;
+    bool has_last = false, has_e1 = false, fail = false;
+    uint32_t e1b = 0, lastb = 0;
+    for (int64_t c0 = P0; c0 < P1; c0 += S3S_CH) {
+        const int cn = (int)(P1 - c0 < S3S_CH ? P1 - c0 : S3S_CH);
+        __syncthreads();  // the previous chunk is consumed
+        for (int i = threadIdx.x; i < cn; i += S3S_TPB) {
+            sv[i] = col[c0 + i];
+            sp[i] = perm ? perm[c0 + i] : (uint32_t)(c0 + i);
+        }
+        __syncthreads();
+        const int64_t kb = b > c0 ? b : c0, ke = e < c0 + cn ? e : c0 + cn;
+        for (int64_t k = kb; k < ke && !fail; k++) {
+            const uint32_t xb = sv[k - c0];
+            const NfVal x = s3_bits(xb, t);
+            const bool hit = has_last && nf_cmp(op3, dom3, x, s3_bits(lastb, t));
+            if (hit) {
+                uint64_t* r = sink.slot(0);
+                if (!r) {
+                    fail = true;
+                    break;
+                }
+                const uint32_t loc = sp[k - c0];
+                r[0] = (uint64_t)loc;
+                r[1] = 0;  // the device path places no timestamps
+                r[2] = 0;  // no nulls, query 0
+                r[3] = seq_base + loc;
+                for (int o = 0; o < no; o++) {
+                    const int s = Q.s3_out_slot[o];
+                    r[NF_REC_HDR + o] = (uint64_t)s3_bits(s == 0 ? e1b : s == 1 ? lastb : xb, t).b;
+                }
+                EM.match_cnt[loc] = 1;
+            }
+            if (!hit && has_e1 && nf_cmp(op2, dom2, x, s3_bits(e1b, t))) {
+                has_last = true;
+                lastb = xb;
+            } else {
+                has_last = false;
+                has_e1 = true;
+                e1b = xb;
+            }
+        }
+    }
+    if (sink.chunk) sink.finish();
+    if (fail) atomicOr(EM.err, (unsigned)NF_E_EMIT);
+}
+
 // unpartitioned apps: StateStreamRuntime.initPartition at SiddhiAppRuntime.start
 __global__ void k_nfa_start(const nf_table* __restrict__ T, const nf_cols* __restrict__ C, uint64_t* __restrict__ kstate,
                             uint64_t tick, int64_t clock, nfd_emit EM) {
@@ -562,7 +672,19 @@ extern "C" int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, 
 
 extern "C" int nfd_seq3(const nf_table* dT, const nf_cols* dC, const nfd_events* ev, int64_t n,
                         const uint32_t* seg_list, const uint32_t* nseg, const uint32_t* skeys, int32_t nkeys,
-                        int64_t max_segments, const nfd_emit* em, void* stream) {
+                        int64_t max_segments, const nfd_emit* em, void* stream, const void* s3_col) {
+    if (s3_col && !ev->gidx) {
+        // LDS-staged (the host checked the shape: one 4-byte attribute, no nulls,
+        // key-ordered copy in s3_col)
+        static const bool off = getenv("SH_S3_STAGED") && getenv("SH_S3_STAGED")[0] == '0';
+        if (!off) {
+            if (max_segments < 1) max_segments = 1;
+            hipLaunchKernelGGL(k_seq3s, dim3(nf_blocks(max_segments, S3S_TPB)), dim3(S3S_TPB), 0, (hipStream_t)stream,
+                               dT, (const uint32_t*)s3_col, ev->perm, ev->seq_base, n, seg_list, nseg, skeys, nkeys,
+                               *em);
+            return hipGetLastError() == hipSuccess ? 0 : -3;
+        }
+    }
     DevEvents E;
     E.ts = ev->ts;
     E.stream = ev->stream;

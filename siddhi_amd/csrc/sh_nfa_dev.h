@@ -48,7 +48,7 @@ int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, const nfd_e
 // the rise-and-fall sequence engine (nf_query.s3) over the key segments, fresh state
 int nfd_seq3(const nf_table* dT, const nf_cols* dC, const nfd_events* ev, int64_t n, const uint32_t* seg_list,
              const uint32_t* nseg, const uint32_t* skeys, int32_t nkeys, int64_t max_segments, const nfd_emit* em,
-             void* stream);
+             void* stream, const void* s3_col = nullptr);
 int nfd_start(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, uint64_t tick, int64_t clock,
               const nfd_emit* em, void* stream);
 // armed (may be NULL): per-key maybe-registered flags (nf_cols.sched_armed);

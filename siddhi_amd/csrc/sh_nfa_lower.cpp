@@ -682,8 +682,15 @@ struct QueryLowering {
         Q->rate_value = q->rate_value;
         if (q->rate_kind != SH_RATE_NONE &&
             ((q->rate_kind != SH_RATE_FIRST_EVENTS && q->rate_kind != SH_RATE_LAST_EVENTS &&
-              q->rate_kind != SH_RATE_ALL_EVENTS) || q->rate_value < 1)) {
-            err = "output rate limiting: `output first|last every N events` (N >= 1) only";
+              q->rate_kind != SH_RATE_ALL_EVENTS && q->rate_kind != SH_RATE_FIRST_TIME) ||
+             q->rate_value < (q->rate_kind == SH_RATE_FIRST_TIME ? 0 : 1))) {
+            err = "output rate limiting: `output [first|last|all] every N events` (N >= 1) or `output first every T`";
+            return false;
+        }
+        if (q->rate_kind == SH_RATE_FIRST_TIME && (!app->playback || q->n_group > 0)) {
+            // outside playback the limiter reads System.currentTimeMillis(); with group by
+            // OutputParser picks FirstGroupByPerTimeOutputRateLimiter
+            err = "output first every T: @app:playback apps without group by only";
             return false;
         }
         if (Q->contains_agg && (q->offset > 0 || q->limit == 0)) {

@@ -34,6 +34,7 @@
 #include "sh_vm.h"
 
 #define RTPB 256
+#define SHR_LDS_IX 2048  // index groups staged in LDS (24 KB)
 
 static unsigned rgrid(int64_t n) {
     int64_t g = (n + RTPB - 1) / RTPB;
@@ -95,6 +96,17 @@ __global__ void __launch_bounds__(RTPB) k_rules_scan(const shr_table* __restrict
     const int ix_attr = RT->ix_attr;
     const int n_ix = RT->n_ix;
     const uint32_t n_free = (uint32_t)RT->n_free;
+    // the predicate index in LDS (a lane's binary search is a chain of dependent
+    // loads: from LDS instead of L2); the grid is sized so each workgroup stages
+    // it once for many events
+    __shared__ int64_t s_ixv[SHR_LDS_IX];
+    __shared__ uint32_t s_ixs[SHR_LDS_IX + 1];
+    const bool lds_ix = ix_attr >= 0 && n_ix <= SHR_LDS_IX;
+    if (lds_ix) {
+        for (int i = threadIdx.x; i < n_ix; i += blockDim.x) s_ixv[i] = RT->ix_val[i];
+        for (int i = threadIdx.x; i <= n_ix; i += blockDim.x) s_ixs[i] = RT->ix_start[i];
+    }
+    __syncthreads();
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
         if (WRITE && cnt[p] == 0) continue;
         const uint32_t key = skeys ? skeys[p] : 0u;
@@ -106,16 +118,30 @@ __global__ void __launch_bounds__(RTPB) k_rules_scan(const shr_table* __restrict
             const int ty = RT->attr_type[ix_attr];
             const int64_t x = rule_ix_key(ty, load_attr(C, 0, ix_attr, ty, (uint32_t)p));
             int a = 0, b = n_ix;
-            while (a < b) {
-                const int m = (a + b) >> 1;
-                if (RT->ix_val[m] < x)
-                    a = m + 1;
-                else
-                    b = m;
-            }
-            if (a < n_ix && RT->ix_val[a] == x) {
-                lo = RT->ix_start[a];
-                hi = RT->ix_start[a + 1];
+            if (lds_ix) {
+                while (a < b) {
+                    const int m = (a + b) >> 1;
+                    if (s_ixv[m] < x)
+                        a = m + 1;
+                    else
+                        b = m;
+                }
+                if (a < n_ix && s_ixv[a] == x) {
+                    lo = s_ixs[a];
+                    hi = s_ixs[a + 1];
+                }
+            } else {
+                while (a < b) {
+                    const int m = (a + b) >> 1;
+                    if (RT->ix_val[m] < x)
+                        a = m + 1;
+                    else
+                        b = m;
+                }
+                if (a < n_ix && RT->ix_val[a] == x) {
+                    lo = RT->ix_start[a];
+                    hi = RT->ix_start[a + 1];
+                }
             }
         }
         const uint32_t nsel = hi - lo, total = nsel + n_free;
@@ -239,9 +265,16 @@ __global__ void k_rules_place(const shr_table* __restrict__ RT, const uint32_t* 
 
 static int rules_ok() { return hipGetLastError() == hipSuccess ? 0 : -3; }
 
+// the scans' grid: a few workgroups per CU, each striding over many events (the
+// LDS index is staged once per workgroup)
+static unsigned sgrid(int64_t n) {
+    const unsigned g = rgrid(n);
+    return g < 1536u ? g : 1536u;  // 6 per CU (LDS)
+}
+
 extern "C" int shr_count(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
                          const shd_cols* dC, uint32_t* cnt, int32_t* flag, void* stream) {
-    hipLaunchKernelGGL(k_rules_scan<0>, dim3(rgrid(n)), dim3(RTPB), 0, (hipStream_t)stream, dT, sts, skeys, n,
+    hipLaunchKernelGGL(k_rules_scan<0>, dim3(sgrid(n)), dim3(RTPB), 0, (hipStream_t)stream, dT, sts, skeys, n,
                        sentinel, dC, cnt, (const uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
                        (uint32_t*)nullptr, flag);
     return rules_ok();
@@ -250,7 +283,7 @@ extern "C" int shr_count(const shr_table* dT, const int64_t* sts, const uint32_t
 extern "C" int shr_write(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
                          const shd_cols* dC, const uint32_t* cnt, const uint32_t* off, uint32_t* rec_p,
                          uint32_t* rec_q, uint32_t* rec_r, void* stream) {
-    hipLaunchKernelGGL(k_rules_scan<1>, dim3(rgrid(n)), dim3(RTPB), 0, (hipStream_t)stream, dT, sts, skeys, n,
+    hipLaunchKernelGGL(k_rules_scan<1>, dim3(sgrid(n)), dim3(RTPB), 0, (hipStream_t)stream, dT, sts, skeys, n,
                        sentinel, dC, (uint32_t*)cnt, off, rec_p, rec_q, rec_r, (int32_t*)nullptr);
     return rules_ok();
 }

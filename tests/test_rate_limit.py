@@ -11,7 +11,15 @@ per event; randomized apps hold the general engine's kernel logic and the device
 oracle. `output [all] every N events` (AllPerEventOutputRateLimiter.process,
 AllPerEventOutputRateLimiter.java:48-75) holds every event per partition and releases the
 held chunk with the N-th (EventOutputRateLimitTestCase: all every 2 -> 4, every 2 -> 4,
-every 5 -> 5 of 5). The time and snapshot limiters stay on the Java side (UnsupportedQuery)."""
+every 5 -> 5 of 5). `output first every T` in a playback app (FirstPerTimeOutputRateLimiter.process,
+FirstPerTimeOutputRateLimiter.java:53-75) passes a chunk's first event when the partition's
+outputTime is unset or outputTime + T <= the timestamp generator's current time (the clock
+InputHandler.send moves to the call's last timestamp, InputHandler.java:85-96); the reference
+pins it only with wall-clock tests (TimeOutputRateLimitTestCase), so its answers below are worked
+by hand from that code. Outside playback that clock is System.currentTimeMillis(), and the
+last / all per-time limiters schedule from the wall clock when a partition is created
+(AllPerTimeOutputRateLimiter.java:97-108), as the snapshot limiters do: those stay on the Java
+side (UnsupportedQuery)."""
 import random
 import re
 
@@ -125,11 +133,56 @@ def test_parse():
             compiler.compile_app(BASE.format(tail=tail))
 
 
+FT_APP = ("@app:playback define stream LoginEvents (timestamp long, ip string); {part}"
+          "@info(name = 'query1') from every e1=LoginEvents select e1.ip as ip "
+          "output first every 2 sec insert into Out;{end}")
+FT_TS = [1000, 1500, 2999, 3000, 3500, 5200, 5200, 7199, 7200]
+
+
+def _first_time(factory, batched=False, part=False):
+    ips = [f"10.0.0.{i % 2 if part else i}" for i in range(len(FT_TS))]
+    rows = [(t, [t, ip]) for t, ip in zip(FT_TS, ips)]
+    acts = [("send", "LoginEvents", rows[:3]), ("send", "LoginEvents", rows[3:])] if batched else \
+        [("send", "LoginEvents", [r]) for r in rows]
+    text = FT_APP.format(part="partition with (ip of LoginEvents) begin " if part else "",
+                         end=" end;" if part else "")
+    return [r[2][0] for r in run_case(factory, text, acts)]
+
+
+# one event per call: outputTime 1000 -> 3000 (3000 <= 3000) -> 5200 -> 7200;
+# two calls (clock 2999, then 7200): each call's first event only;
+# partitioned by ip (keys .0 .1 in turn): each key's first event, then >= 2 s later
+FT_KNOWN = [(False, False, ["10.0.0.0", "10.0.0.3", "10.0.0.5", "10.0.0.8"]),
+            (True, False, ["10.0.0.0", "10.0.0.3"]),
+            (False, True, ["10.0.0.0", "10.0.0.1", "10.0.0.0", "10.0.0.1", "10.0.0.0"])]
+
+
+@pytest.mark.parametrize("name,factory", ENGINES)
+@pytest.mark.parametrize("batched,part,want", FT_KNOWN)
+def test_first_per_time(name, factory, batched, part, want):
+    assert _first_time(factory(), batched, part) == want
+
+
+def test_first_per_time_parse_and_refusals():
+    d = compiler.compile_app(FT_APP.format(part="", end="")).descriptor().queries[0]
+    assert d.rate_kind == 4 and d.rate_value == 2000
+    for text in (FT_APP.format(part="", end="").replace("@app:playback ", ""),
+                 FT_APP.format(part="", end="").replace("first every 2 sec", "last every 2 sec"),
+                 FT_APP.format(part="", end="").replace("first every 2 sec", "every 2 sec"),
+                 FT_APP.format(part="", end="").replace("select e1.ip as ip", "select e1.ip as ip group by e1.ip")):
+        with pytest.raises(compiler.UnsupportedQuery):
+            compiler.compile_app(text)
+
+
 def rate_case(seed):
     rng = random.Random(5100 + seed)
     app, actions = nfa_case(rng)
     if " select " not in app:
         return None
+    if app.startswith("@app:playback") and rng.random() < 0.3:
+        app = re.sub(r" insert into Out;", lambda m: f" output first every {rng.choice([1, 5, 20, 60])} ms "
+                     "insert into Out;", app)
+        return app, actions
     app = re.sub(r" insert into Out;", lambda m: f" output {rng.choice(['first', 'last', 'all', ''])} every "
                  f"{rng.choice([1, 2, 2, 3, 5])} events insert into Out;", app)
     return app, actions
@@ -163,6 +216,8 @@ def test_known_and_reference_counts_gpu():
         assert len(_login(hip, n, kind)) == count
     for tail, want in KNOWN:
         assert [r[2] for r in run_case(hip, BASE.format(tail=tail), ACTS)] == want, tail
+    for batched, part, want in FT_KNOWN:
+        assert _first_time(hip, batched, part) == want
     ev = [("K0", 1), ("K1", 2), ("K0", 3), ("K0", 4), ("K1", 5), ("K1", 6), ("K0", 7), ("K0", 8)]
     acts = [("send", "A", [(10 + i, [k, 1.0, n])]) for i, (k, n) in enumerate(ev)]
     assert [r[2] for r in run_case(hip, PART, acts)] == [["K0", 1], ["K1", 2], ["K0", 4], ["K1", 6], ["K0", 8]]
