@@ -346,18 +346,19 @@ def cpu_baseline(args, W, n):
     if not W.get("cpu_split"):
         threads = 1
     log(f"CPU baseline on {s} events, {threads} thread(s)")
+    from concurrent.futures import ThreadPoolExecutor, wait
     t1 = time.perf_counter()
-    if threads == 1:
-        W["cpu"](s)
-    else:
-        # partitions are independent (no timers): the sample's events split by
-        # key over threads, each with its own oracle instance (ctypes releases
-        # the GIL inside the restatement)
-        from concurrent.futures import ThreadPoolExecutor
-        part = W["keys"][:s] % threads
-        idxs = [np.flatnonzero(part == t) for t in range(threads)]
-        with ThreadPoolExecutor(threads) as ex:
-            list(ex.map(lambda ix: W["cpu"](s, ix), idxs))
+    # partitions are independent (no timers): with several threads the sample's
+    # events split by key, each thread with its own oracle instance (ctypes releases
+    # the GIL inside the restatement); the main thread logs while they run
+    part = W["keys"][:s] % threads if threads > 1 else None
+    jobs = [None] if threads == 1 else [np.flatnonzero(part == t) for t in range(threads)]
+    with ThreadPoolExecutor(threads) as ex:
+        futs = [ex.submit((lambda: W["cpu"](s)) if ix is None else (lambda ix=ix: W["cpu"](s, ix))) for ix in jobs]
+        while wait(futs, timeout=30).not_done:
+            log(f"CPU baseline: {time.perf_counter() - t1:.0f} s")
+        for f in futs:
+            f.result()
     cdt = time.perf_counter() - t1
     return {"value": s / cdt, "unit": "events/s", "cores": threads, "kind": "port",
             "sample": f"first {s} events of the same {args.config.upper()} stream, send(Event[]) batches of "

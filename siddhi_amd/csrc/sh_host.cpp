@@ -408,6 +408,9 @@ struct sh_handle {
     DevBuf n_klist[2], n_klist_n, n_arm_log, n_arm_ctr;
     int klist_cur = 0;
     int seq3_last = 0;                  // the last general-engine run took k_seq3
+    bool s3_compact = false;            // ... with k_seq3s's compact records (nfd_place_s3 places them)
+    int s3_type = 0;                    // their values' type (one 4-byte attribute)
+    uint64_t s3_seq_base = 0;           // and the run's first trigger sequence number
     bool no_seq3 = false;               // rerun without k_seq3 (aggregates not exact in parallel)
     // scheduler maps' iteration order (sh_jmap.h): host models fed by the
     // launches' getState history, per-key ranks uploaded for the due-key pick
@@ -1517,6 +1520,12 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
     if (d_seq) {  // device-resident output (sh_run_device): seq, values and, when asked, the query
         if (total > cap) return SH_E_MORE;
         if (h->dev_want_query && h->w_oq.ensure_fresh(total * 4)) return fail(h, SH_E_OOM, "output buffers");
+        if (h->s3_compact) {
+            nfd_place_s3(h->n_recs.as<uint64_t>(), h->rec_cap, (int64_t)nrec, no, h->s3_type, h->s3_seq_base,
+                         h->w_off.as<uint32_t>(), h->dev_want_query ? h->w_oq.as<int32_t>() : nullptr, d_seq, d_vals,
+                         h->w_inv.as<uint32_t>(), total, st);
+            return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "placement");
+        }
         nfd_place(h->n_recs.as<uint64_t>(), (int64_t)nrec, stride, h->w_off.as<uint32_t>(), no,
                   h->dev_want_query ? h->w_oq.as<int32_t>() : nullptr, d_seq, nullptr, d_vals, nullptr,
                   h->w_inv.as<uint32_t>(), total, st);
@@ -1658,8 +1667,14 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
                   type_width(h->stream_types[0][A]) == 4 && Q.s3_a3 == A && Q.s3_e1a == A && Q.s3_la == A &&
                   Q.s3_t3 == ty && Q.s3_e1t == ty && Q.s3_lt == ty && !cols.nul[0][A];
         for (int o = 0; o < Q.n_out && ok; o++) ok = Q.s3_out_attr[o] == A && Q.s3_out_type[o] == ty;
-        if (ok) s3_col = alias == A ? (const void*)skeys : (const void*)cols.col[0][A];
+        static const bool staged = !(getenv("SH_S3_STAGED") && getenv("SH_S3_STAGED")[0] == '0');
+        if (ok && staged) s3_col = alias == A ? (const void*)skeys : (const void*)cols.col[0][A];
     }
+    // its records in the compact form (SH_S3_COMPACT=0: the generic records, for A/B)
+    static const bool s3_compact_on = !(getenv("SH_S3_COMPACT") && getenv("SH_S3_COMPACT")[0] == '0');
+    h->s3_compact = s3_col && d_seq && s3_compact_on;
+    h->s3_type = h->T->q[0].s3_t2;
+    h->s3_seq_base = B.seq_base;
     E.sorted_rows = sorted_cols ? 1 : 0;
     E.pad = 0;
     E.run = fresh ? h->dev_run_ids : nullptr;
@@ -1700,7 +1715,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
         h->seq3_last = seq3 ? 1 : 0;
         if (seq3) {
             if (nfd_seq3(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), &E, n, seg_list, nseg, skeys, nkeys, max_seg,
-                         &em, st, s3_col))
+                         &em, st, s3_col, h->s3_compact ? 1 : 0))
                 return fail(h, SH_E_HIP, "k_seq3 launch failed");
         } else if (nfd_run(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), &E, n,
                            seg_list, nseg, skeys, nkeys, max_seg, h->tick, h->clock, &em, st))

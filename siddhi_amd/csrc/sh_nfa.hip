@@ -265,12 +265,14 @@ __global__ void __launch_bounds__(NF_TPB) k_seq3(const nf_table* __restrict__ T,
 
 // The same sequence, LDS-staged: when every operand and output reads one 4-byte
 // attribute without a null mask (C3), a workgroup owns 256 consecutive key
-// segments, one per lane, and sweeps their key-ordered events in chunks the
-// whole workgroup loads coalesced into LDS (value + arrival index); each lane
-// walks its own key's events of the chunk from LDS. k_seq3's lane-strided loads
-// touch one line per lane per load and lose most lines before the lane returns.
+// segments, one per lane, and walks them in rounds: each round the workgroup
+// loads the next S3S_E events of EVERY lane's segment into LDS (value + arrival
+// index; 16 threads per 64-byte run) and each lane then steps through its own
+// window from LDS. k_seq3's lane-strided loads touch one line per lane per load
+// and lose most lines before the lane comes back for the rest.
 #define S3S_TPB 256
-#define S3S_CH 4096
+#define S3S_E 16
+#define S3S_LD (S3S_E + 1)  // padded lane stride: the lanes' LDS reads hit distinct banks
 __device__ __forceinline__ NfVal s3_bits(uint32_t b, int t) {
     NfVal v;
     v.t = (uint8_t)t;
@@ -279,12 +281,17 @@ __device__ __forceinline__ NfVal s3_bits(uint32_t b, int t) {
     return v;
 }
 
+// COMPACT: the records are SoA over the emission buffer -- loc[cap] (arrival index, ~0u:
+// unused slot), then the raw 4-byte select values [cap][n_out] -- and k_s3_inv /
+// k_s3_gather place them (16 bytes per C3 record instead of a 56-byte generic one)
+template <bool COMPACT>
 __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ T, const uint32_t* __restrict__ col,
                                                    const uint32_t* __restrict__ perm, uint64_t seq_base, int64_t n,
                                                    const uint32_t* __restrict__ seg_list,
                                                    const uint32_t* __restrict__ nseg,
                                                    const uint32_t* __restrict__ skeys, int32_t nkeys, nfd_emit EM) {
-    __shared__ uint32_t sv[S3S_CH], sp[S3S_CH];
+    __shared__ uint32_t sv[S3S_TPB * S3S_LD], sp[S3S_TPB * S3S_LD];
+    __shared__ uint32_t s_b[S3S_TPB], s_e[S3S_TPB];
     __shared__ int64_t s_end;
     const uint32_t ns = *nseg;
     const uint32_t s0 = blockIdx.x * S3S_TPB;
@@ -306,17 +313,19 @@ __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ 
         s_end = e;
     }
     __syncthreads();
-    const int64_t P0 = seg_list[s0], P1 = s_end;
+    const uint32_t P1 = (uint32_t)s_end;
     const uint32_t sidx = s0 + threadIdx.x;
-    int64_t b = P1, e = P1;  // lanes past the last segment: empty
+    uint32_t b = P1, e = P1;  // lanes past the last segment: empty
     if (sidx <= sl) {
         b = seg_list[sidx];
-        e = sidx < sl ? (int64_t)seg_list[sidx + 1u] : P1;
+        e = sidx < sl ? seg_list[sidx + 1u] : P1;
         if ((skeys ? skeys[b] : 0u) >= (uint32_t)nkeys) {
             atomicOr(EM.err, (unsigned)NF_E_KEY);
             b = e = P1;
         }
     }
+    s_b[threadIdx.x] = b;
+    s_e[threadIdx.x] = e;
     const nf_query& Q = T->q[0];
     const int t = Q.s3_t2;  // the one attribute's type (checked on the host)
     const int op2 = Q.s3_op2, dom2 = Q.s3_dom2, op3 = Q.s3_op3, dom3 = Q.s3_dom3, no = Q.n_out;
@@ -327,28 +336,55 @@ __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ 
     sink.stride = EM.stride;
     sink.chunk = nullptr;
     sink.used = sink.n = 0;
+    uint32_t* const rl = (uint32_t*)EM.recs;  // COMPACT: loc per record, then the values
+    uint32_t* const rv = rl + EM.cap;
+    int64_t cbase = -1;
+    int cused = NF_SINK_CHUNK;
     bool has_last = false, has_e1 = false, fail = false;
     uint32_t e1b = 0, lastb = 0;
-    for (int64_t c0 = P0; c0 < P1; c0 += S3S_CH) {
-        const int cn = (int)(P1 - c0 < S3S_CH ? P1 - c0 : S3S_CH);
-        __syncthreads();  // the previous chunk is consumed
-        for (int i = threadIdx.x; i < cn; i += S3S_TPB) {
-            sv[i] = col[c0 + i];
-            sp[i] = perm ? perm[c0 + i] : (uint32_t)(c0 + i);
+    __syncthreads();
+    for (uint32_t r0 = 0;; r0 += S3S_E) {
+        // every lane's next window, loaded by the whole workgroup
+        for (int idx = threadIdx.x; idx < S3S_TPB * S3S_E; idx += S3S_TPB) {
+            const int l = idx / S3S_E, j = idx % S3S_E;
+            const uint32_t p = s_b[l] + r0 + (uint32_t)j;
+            if (p < s_e[l]) {
+                sv[l * S3S_LD + j] = col[p];
+                sp[l * S3S_LD + j] = perm ? perm[p] : p;
+            }
         }
         __syncthreads();
-        const int64_t kb = b > c0 ? b : c0, ke = e < c0 + cn ? e : c0 + cn;
-        for (int64_t k = kb; k < ke && !fail; k++) {
-            const uint32_t xb = sv[k - c0];
+        const uint32_t w0 = b + r0;
+        const int cnt = w0 >= e ? 0 : (e - w0 < (uint32_t)S3S_E ? (int)(e - w0) : S3S_E);
+        for (int j = 0; j < cnt && !fail; j++) {
+            const uint32_t xb = sv[threadIdx.x * S3S_LD + j];
             const NfVal x = s3_bits(xb, t);
             const bool hit = has_last && nf_cmp(op3, dom3, x, s3_bits(lastb, t));
-            if (hit) {
+            if (hit && COMPACT) {
+                if (cused == NF_SINK_CHUNK) {
+                    const unsigned long long at = atomicAdd(EM.ctr, (unsigned long long)NF_SINK_CHUNK);
+                    if ((int64_t)at + NF_SINK_CHUNK > EM.cap) {
+                        fail = true;
+                        break;
+                    }
+                    cbase = (int64_t)at;
+                    cused = 0;
+                }
+                const int64_t ri = cbase + cused++;
+                const uint32_t loc = sp[threadIdx.x * S3S_LD + j];
+                rl[ri] = loc;
+                for (int o = 0; o < no; o++) {
+                    const int s = Q.s3_out_slot[o];
+                    rv[ri * no + o] = s == 0 ? e1b : s == 1 ? lastb : xb;
+                }
+                EM.match_cnt[loc] = 1;
+            } else if (hit) {
                 uint64_t* r = sink.slot(0);
                 if (!r) {
                     fail = true;
                     break;
                 }
-                const uint32_t loc = sp[k - c0];
+                const uint32_t loc = sp[threadIdx.x * S3S_LD + j];
                 r[0] = (uint64_t)loc;
                 r[1] = 0;  // the device path places no timestamps
                 r[2] = 0;  // no nulls, query 0
@@ -368,9 +404,52 @@ __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ 
                 e1b = xb;
             }
         }
+        // (a barrier too: the next round's loads wait for every lane's walk)
+        if (!__syncthreads_or(w0 + S3S_E < e)) break;
     }
-    if (sink.chunk) sink.finish();
+    if (COMPACT && cbase >= 0)
+        for (int i = cused; i < NF_SINK_CHUNK; i++) rl[cbase + i] = ~0u;
+    if (!COMPACT && sink.chunk) sink.finish();
     if (fail) atomicOr(EM.err, (unsigned)NF_E_EMIT);
+}
+
+// ordered placement of the compact records (k_nfa_inv / k_nfa_gather for k_seq3s)
+__global__ void __launch_bounds__(256) k_s3_inv(const uint32_t* __restrict__ rl, int64_t nrec,
+                                                const uint32_t* __restrict__ offsets, uint32_t* __restrict__ inv) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrec) return;
+    const uint32_t loc = rl[i];
+    if (loc == ~0u) return;
+    inv[offsets[loc]] = (uint32_t)i;  // at most one row per event
+}
+
+__global__ void __launch_bounds__(256) k_s3_gather(const uint32_t* __restrict__ rl, const uint32_t* __restrict__ rv,
+                                                   const uint32_t* __restrict__ inv, int64_t total, int64_t nrec,
+                                                   int n_out, int type, uint64_t seq_base,
+                                                   int32_t* __restrict__ out_query, uint64_t* __restrict__ out_seq,
+                                                   int64_t* __restrict__ out_vals) {
+    const int64_t dst = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (dst >= total) return;
+    const uint32_t ix = inv[dst];
+    if ((int64_t)ix >= nrec) return;  // no record (an emission overflow, reported through err)
+    if (out_query) out_query[dst] = 0;
+    if (out_seq) out_seq[dst] = seq_base + rl[ix];
+    if (out_vals)
+        for (int o = 0; o < n_out; o++) out_vals[dst * n_out + o] = s3_bits(rv[(int64_t)ix * n_out + o], type).b;
+}
+
+extern "C" int nfd_place_s3(const uint64_t* recs, int64_t cap, int64_t nrec, int n_out, int type, uint64_t seq_base,
+                            const uint32_t* offsets, int32_t* out_query, uint64_t* out_seq, int64_t* out_vals,
+                            uint32_t* inv, int64_t total, void* stream) {
+    if (nrec <= 0 || total <= 0) return 0;
+    const uint32_t* rl = (const uint32_t*)recs;
+    hipMemsetAsync(inv, 0xFF, (size_t)total * 4, (hipStream_t)stream);
+    hipLaunchKernelGGL(k_s3_inv, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rl, nrec,
+                       offsets, inv);
+    hipLaunchKernelGGL(k_s3_gather, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rl,
+                       rl + cap, (const uint32_t*)inv, total, nrec, n_out, type, seq_base, out_query, out_seq,
+                       out_vals);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 // unpartitioned apps: StateStreamRuntime.initPartition at SiddhiAppRuntime.start
@@ -672,18 +751,19 @@ extern "C" int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, 
 
 extern "C" int nfd_seq3(const nf_table* dT, const nf_cols* dC, const nfd_events* ev, int64_t n,
                         const uint32_t* seg_list, const uint32_t* nseg, const uint32_t* skeys, int32_t nkeys,
-                        int64_t max_segments, const nfd_emit* em, void* stream, const void* s3_col) {
+                        int64_t max_segments, const nfd_emit* em, void* stream, const void* s3_col, int compact) {
     if (s3_col && !ev->gidx) {
         // LDS-staged (the host checked the shape: one 4-byte attribute, no nulls,
         // key-ordered copy in s3_col)
-        static const bool off = getenv("SH_S3_STAGED") && getenv("SH_S3_STAGED")[0] == '0';
-        if (!off) {
-            if (max_segments < 1) max_segments = 1;
-            hipLaunchKernelGGL(k_seq3s, dim3(nf_blocks(max_segments, S3S_TPB)), dim3(S3S_TPB), 0, (hipStream_t)stream,
-                               dT, (const uint32_t*)s3_col, ev->perm, ev->seq_base, n, seg_list, nseg, skeys, nkeys,
-                               *em);
-            return hipGetLastError() == hipSuccess ? 0 : -3;
-        }
+        if (max_segments < 1) max_segments = 1;
+        const dim3 g(nf_blocks(max_segments, S3S_TPB)), b(S3S_TPB);
+        if (compact)
+            hipLaunchKernelGGL(k_seq3s<true>, g, b, 0, (hipStream_t)stream, dT, (const uint32_t*)s3_col, ev->perm,
+                               ev->seq_base, n, seg_list, nseg, skeys, nkeys, *em);
+        else
+            hipLaunchKernelGGL(k_seq3s<false>, g, b, 0, (hipStream_t)stream, dT, (const uint32_t*)s3_col, ev->perm,
+                               ev->seq_base, n, seg_list, nseg, skeys, nkeys, *em);
+        return hipGetLastError() == hipSuccess ? 0 : -3;
     }
     DevEvents E;
     E.ts = ev->ts;
