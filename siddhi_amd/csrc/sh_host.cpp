@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -407,6 +408,8 @@ struct sh_handle {
     // in n_klist_n[0..1]) and the log of keys armed since the last pass
     DevBuf n_klist[2], n_klist_n, n_arm_log, n_arm_ctr;
     int klist_cur = 0;
+    double hp_ms[6] = {0, 0, 0, 0, 0, 0};  // SH_HOST_PROF: wall time per host phase (printed by sh_destroy)
+    int64_t hp_n[6] = {0, 0, 0, 0, 0, 0};
     int seq3_last = 0;                  // the last general-engine run took k_seq3
     bool s3_compact = false;            // ... with k_seq3s's compact records (nfd_place_s3 places them)
     int s3_type = 0;                    // their values' type (one 4-byte attribute)
@@ -460,6 +463,21 @@ struct sh_handle {
     int agg_last = 0;  // 1: post-pass done, 2: post-pass not exact -> sequential engine
     std::vector<int32_t> out_types;  // per select position over the queries (-2: types differ)
     uint64_t fp = 0;                 // compiled-program fingerprint (snapshot images)
+};
+
+// SH_HOST_PROF: a phase's wall time into h->hp_ms[i] (scope lifetime)
+struct HpScope {
+    sh_handle* h;
+    int i;
+    std::chrono::steady_clock::time_point t0;
+    HpScope(sh_handle* hh, int ii) : h(getenv("SH_HOST_PROF") ? hh : nullptr), i(ii) {
+        if (h) t0 = std::chrono::steady_clock::now();
+    }
+    ~HpScope() {
+        if (!h) return;
+        h->hp_ms[i] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        h->hp_n[i]++;
+    }
 };
 
 static void set_layout(shp_layout& Y, const shp_program& P, int32_t cap) {
@@ -900,6 +918,12 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
 
 void sh_destroy(sh_handle* h) {
     if (!h) return;
+    if (getenv("SH_HOST_PROF") && h->hp_n[0]) {
+        static const char* names[6] = {"push", "timers", "process", "history", "place", "drain"};
+        fprintf(stderr, "[sh host profile]");
+        for (int i = 0; i < 6; i++) fprintf(stderr, " %s %.1f ms / %lld", names[i], h->hp_ms[i], (long long)h->hp_n[i]);
+        fprintf(stderr, "\n");
+    }
     if (h->has_device) {
         hipStreamSynchronize(h->stream);
         h->pin_in.release();
@@ -951,6 +975,7 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall = false);
 static int nf_next_due(sh_handle* h, int64_t* out);
 
 static int push_impl(sh_handle* h, const sh_batch* b, const uint32_t* index, int64_t call_n, int64_t call_last) {
+    HpScope hp_(h, 0);
     if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !b) return SH_E_INVALID_ARG;
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device: the matcher has no CPU fallback");
@@ -1337,6 +1362,7 @@ static int nf_sev_ready(sh_handle* h, int64_t events) {
 // replay the launch's getState history on the host models and upload the
 // changed ranks (before the next due scan, on the same stream)
 static int nf_sev_apply(sh_handle* h) {
+    HpScope hp_(h, 3);
     if (!h->sm_on) return SH_OK;
     hipStream_t st = h->stream;
     if (h->pin_sev.ensure(64)) return fail(h, SH_E_OOM, "pinned staging");
@@ -1490,6 +1516,7 @@ static void nf_put_cols(sh_handle* h, const nf_cols& cols) {
 // (launch: the launch's tick, for the key-sharded rows' order tags)
 static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_seq, int64_t* d_vals, int64_t cap,
                     uint64_t launch) {
+    HpScope hp_(h, 4);
     hipStream_t st = h->stream;
     if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
     hipMemcpyAsync(h->pin_rd.as<void>(PR_NREC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
@@ -1521,7 +1548,8 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
         if (total > cap) return SH_E_MORE;
         if (h->dev_want_query && h->w_oq.ensure_fresh(total * 4)) return fail(h, SH_E_OOM, "output buffers");
         if (h->s3_compact) {
-            nfd_place_s3(h->n_recs.as<uint64_t>(), h->rec_cap, (int64_t)nrec, no, h->s3_type, h->s3_seq_base,
+            // one record slot per key-ordered position of the run (n_idx events)
+            nfd_place_s3(h->n_recs.as<uint64_t>(), h->rec_cap, n_idx, no, h->s3_type, h->s3_seq_base,
                          h->w_off.as<uint32_t>(), h->dev_want_query ? h->w_oq.as<int32_t>() : nullptr, d_seq, d_vals,
                          h->w_inv.as<uint32_t>(), total, st);
             return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "placement");
@@ -1601,6 +1629,7 @@ static int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carr
 static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& cols_in, uint64_t* d_seq,
                       int64_t* d_vals, int64_t cap, int64_t* n_rows, bool fresh = false, int64_t batch_events = 0,
                       const sh_device_run* carry_run = nullptr, const uint32_t* gidx = nullptr, int64_t n_idx = 0) {
+    HpScope hp_(h, 2);
     hipStream_t st = h->stream;
     const int64_t n = B.n;
     if (!gidx) n_idx = n;
@@ -1815,6 +1844,7 @@ static int nf_next_due(sh_handle* h, int64_t* out) {
 // collectives); the pick runs over all ranks' candidates and the firing order
 // positions are global, so registration stamps and row order match one process.
 static int nf_timers(sh_handle* h, int64_t now, bool wall) {
+    HpScope hp_(h, 1);
     if (!h->T->has_absent) return SH_OK;
     if (h->n_nkeys == 0 && !h->coord_on) return SH_OK;
     hipStream_t st = h->stream;
@@ -2208,6 +2238,7 @@ int64_t sh_pending(sh_handle* h) {
 }
 
 static int drain_impl(sh_handle* h, sh_match_buf* out, uint64_t* order) {
+    HpScope hp_(h, 5);
     if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !out) return SH_E_INVALID_ARG;
     int rc = flush(h);

@@ -281,9 +281,12 @@ __device__ __forceinline__ NfVal s3_bits(uint32_t b, int t) {
     return v;
 }
 
-// COMPACT: the records are SoA over the emission buffer -- loc[cap] (arrival index, ~0u:
-// unused slot), then the raw 4-byte select values [cap][n_out] -- and k_s3_inv /
-// k_s3_gather place them (16 bytes per C3 record instead of a 56-byte generic one)
+// COMPACT: one record slot per key-ordered position (each event triggers at most one
+// match), SoA over the emission buffer -- loc[cap] (the trigger's arrival index, ~0u:
+// no match; written for every position, coalesced from LDS), then the raw 4-byte
+// select values [cap][n_out] of the positions that matched -- placed by k_s3_inv /
+// k_s3_gather. No record counter: the generic sink's chunk claims are one atomic on
+// a single word per 16 records, which serialises at the L2 (C3: 1.5M claims).
 template <bool COMPACT>
 __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ T, const uint32_t* __restrict__ col,
                                                    const uint32_t* __restrict__ perm, uint64_t seq_base, int64_t n,
@@ -295,7 +298,12 @@ __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ 
     __shared__ int64_t s_end;
     const uint32_t ns = *nseg;
     const uint32_t s0 = blockIdx.x * S3S_TPB;
-    if (s0 >= ns) return;  // uniform per workgroup
+    if (s0 >= ns) {  // uniform per workgroup
+        // COMPACT, no keyed event at all: every slot is empty
+        if (COMPACT && ns == 0 && blockIdx.x == 0)
+            for (int64_t p = threadIdx.x; p < n; p += S3S_TPB) ((uint32_t*)EM.recs)[p] = ~0u;
+        return;
+    }
     const uint32_t sl = min(s0 + (uint32_t)S3S_TPB, ns) - 1u;  // the workgroup's last segment
     if (threadIdx.x == 0) {
         // segments are listed in order; only the last one may be followed by the
@@ -338,8 +346,6 @@ __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ 
     sink.used = sink.n = 0;
     uint32_t* const rl = (uint32_t*)EM.recs;  // COMPACT: loc per record, then the values
     uint32_t* const rv = rl + EM.cap;
-    int64_t cbase = -1;
-    int cused = NF_SINK_CHUNK;
     bool has_last = false, has_e1 = false, fail = false;
     uint32_t e1b = 0, lastb = 0;
     __syncthreads();
@@ -360,24 +366,18 @@ __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ 
             const uint32_t xb = sv[threadIdx.x * S3S_LD + j];
             const NfVal x = s3_bits(xb, t);
             const bool hit = has_last && nf_cmp(op3, dom3, x, s3_bits(lastb, t));
-            if (hit && COMPACT) {
-                if (cused == NF_SINK_CHUNK) {
-                    const unsigned long long at = atomicAdd(EM.ctr, (unsigned long long)NF_SINK_CHUNK);
-                    if ((int64_t)at + NF_SINK_CHUNK > EM.cap) {
-                        fail = true;
-                        break;
-                    }
-                    cbase = (int64_t)at;
-                    cused = 0;
-                }
-                const int64_t ri = cbase + cused++;
+            if (COMPACT) {
+                // the slot's record: the trigger's arrival index or ~0u, written back below
                 const uint32_t loc = sp[threadIdx.x * S3S_LD + j];
-                rl[ri] = loc;
-                for (int o = 0; o < no; o++) {
-                    const int s = Q.s3_out_slot[o];
-                    rv[ri * no + o] = s == 0 ? e1b : s == 1 ? lastb : xb;
+                sv[threadIdx.x * S3S_LD + j] = hit ? loc : ~0u;
+                if (hit) {
+                    const int64_t ri = (int64_t)(w0 + (uint32_t)j);
+                    for (int o = 0; o < no; o++) {
+                        const int s = Q.s3_out_slot[o];
+                        rv[ri * no + o] = s == 0 ? e1b : s == 1 ? lastb : xb;
+                    }
+                    EM.match_cnt[loc] = 1;
                 }
-                EM.match_cnt[loc] = 1;
             } else if (hit) {
                 uint64_t* r = sink.slot(0);
                 if (!r) {
@@ -404,11 +404,21 @@ __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ 
                 e1b = xb;
             }
         }
-        // (a barrier too: the next round's loads wait for every lane's walk)
-        if (!__syncthreads_or(w0 + S3S_E < e)) break;
+        // (a barrier too: the write-back and the next round's loads wait for every walk)
+        const bool more = __syncthreads_or(w0 + S3S_E < e);
+        if (COMPACT) {
+            for (int idx = threadIdx.x; idx < S3S_TPB * S3S_E; idx += S3S_TPB) {
+                const int l = idx / S3S_E, j = idx % S3S_E;
+                const uint32_t p = s_b[l] + r0 + (uint32_t)j;
+                if (p < s_e[l]) rl[p] = sv[l * S3S_LD + j];
+            }
+            __syncthreads();
+        }
+        if (!more) break;
     }
-    if (COMPACT && cbase >= 0)
-        for (int i = cused; i < NF_SINK_CHUNK; i++) rl[cbase + i] = ~0u;
+    // COMPACT: the null-key run after the last segment has no records
+    if (COMPACT && sl + 1u == ns)
+        for (int64_t p = (int64_t)P1 + threadIdx.x; p < n; p += S3S_TPB) rl[p] = ~0u;
     if (!COMPACT && sink.chunk) sink.finish();
     if (fail) atomicOr(EM.err, (unsigned)NF_E_EMIT);
 }
