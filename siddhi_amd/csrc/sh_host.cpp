@@ -412,6 +412,7 @@ struct sh_handle {
     int64_t hp_n[6] = {0, 0, 0, 0, 0, 0};
     int seq3_last = 0;                  // the last general-engine run took k_seq3
     bool s3_compact = false;            // ... with k_seq3s's compact records (nfd_place_s3 places them)
+    bool kstate_stale = false;          // key blocks not reset after a k_seq3 run (reset before the next use)
     int s3_type = 0;                    // their values' type (one 4-byte attribute)
     uint64_t s3_seq_base = 0;           // and the run's first trigger sequence number
     bool no_seq3 = false;               // rerun without k_seq3 (aggregates not exact in parallel)
@@ -2064,6 +2065,11 @@ static int nf_start(sh_handle* h) {
 // none of its events (the coordinator's exchanges are collectives).
 static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0, const uint32_t* index, int64_t call_n,
                    int64_t call_last) {
+    if (h->kstate_stale) {
+        hipMemsetAsync(h->n_kstate.p, 0, (size_t)h->n_nkeys * h->T->key_words * 8, h->stream);
+        h->kstate_stale = false;
+        h->started = false;
+    }
     if (!h->started) {
         int rc = nf_start(h);
         if (rc) return rc;
@@ -2760,7 +2766,15 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
         h->agg_last = 0;
         h->no_seq3 = false;
         for (int pass = 0; pass < 2; pass++) {
-            hipMemsetAsync(h->n_kstate.p, 0, (size_t)nkeys * h->T->key_words * 8, h->stream);
+            // the rise-and-fall engine keeps no key blocks: their reset waits for a
+            // later user (kstate_stale)
+            const bool s3_run = h->T->n_queries == 1 && Q0.s3 && !h->no_seq3 && !getenv("SH_NO_SEQ3");
+            if (s3_run) {
+                h->kstate_stale = true;
+            } else {
+                hipMemsetAsync(h->n_kstate.p, 0, (size_t)nkeys * h->T->key_words * 8, h->stream);
+                h->kstate_stale = false;
+            }
             h->started = false;
             rc = nf_start(h);
             if (rc) return rc;
@@ -3256,6 +3270,11 @@ int sh_snapshot(sh_handle* h, void* buf, int64_t cap, int64_t* size) {
     if (h && h->coord_on) return fail(h, SH_E_UNSUPPORTED, "snapshots of key-sharded handles are not supported");
     if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !size || (cap > 0 && !buf)) return SH_E_INVALID_ARG;
+    if (h->kstate_stale && h->n_kstate.p) {
+        hipMemsetAsync(h->n_kstate.p, 0, (size_t)h->n_nkeys * h->T->key_words * 8, h->stream);
+        hipStreamSynchronize(h->stream);
+        h->kstate_stale = false;
+    }
     SnapW w;
     const int rc = snapshot_image(h, w);
     if (rc) return rc;

@@ -282,10 +282,10 @@ __device__ __forceinline__ NfVal s3_bits(uint32_t b, int t) {
 }
 
 // COMPACT: one record slot per key-ordered position (each event triggers at most one
-// match), SoA over the emission buffer -- loc[cap] (the trigger's arrival index, ~0u:
-// no match; written for every position, coalesced from LDS), then the raw 4-byte
-// select values [cap][n_out] of the positions that matched -- placed by k_s3_inv /
-// k_s3_gather. No record counter: the generic sink's chunk claims are one atomic on
+// match) over the emission buffer -- loc[cap] (the trigger's arrival index, ~0u: no
+// match; written for every position, coalesced from LDS), then [cap][1 + n_out] words
+// (loc again and the raw 4-byte select values) for the positions that matched --
+// placed by k_s3_inv / k_s3_gather. No record counter: the generic sink's chunk claims are one atomic on
 // a single word per 16 records, which serialises at the L2 (C3: 1.5M claims).
 template <bool COMPACT>
 __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ T, const uint32_t* __restrict__ col,
@@ -371,10 +371,12 @@ __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ 
                 const uint32_t loc = sp[threadIdx.x * S3S_LD + j];
                 sv[threadIdx.x * S3S_LD + j] = hit ? loc : ~0u;
                 if (hit) {
-                    const int64_t ri = (int64_t)(w0 + (uint32_t)j);
+                    // [loc, values]: the gather reads one record in one line
+                    uint32_t* r = rv + (int64_t)(w0 + (uint32_t)j) * (no + 1);
+                    r[0] = loc;
                     for (int o = 0; o < no; o++) {
                         const int s = Q.s3_out_slot[o];
-                        rv[ri * no + o] = s == 0 ? e1b : s == 1 ? lastb : xb;
+                        r[1 + o] = s == 0 ? e1b : s == 1 ? lastb : xb;
                     }
                     EM.match_cnt[loc] = 1;
                 }
@@ -442,10 +444,11 @@ __global__ void __launch_bounds__(256) k_s3_gather(const uint32_t* __restrict__ 
     if (dst >= total) return;
     const uint32_t ix = inv[dst];
     if ((int64_t)ix >= nrec) return;  // no record (an emission overflow, reported through err)
+    const uint32_t* r = rv + (int64_t)ix * (n_out + 1);
     if (out_query) out_query[dst] = 0;
-    if (out_seq) out_seq[dst] = seq_base + rl[ix];
+    if (out_seq) out_seq[dst] = seq_base + r[0];
     if (out_vals)
-        for (int o = 0; o < n_out; o++) out_vals[dst * n_out + o] = s3_bits(rv[(int64_t)ix * n_out + o], type).b;
+        for (int o = 0; o < n_out; o++) out_vals[dst * n_out + o] = s3_bits(r[1 + o], type).b;
 }
 
 extern "C" int nfd_place_s3(const uint64_t* recs, int64_t cap, int64_t nrec, int n_out, int type, uint64_t seq_base,
