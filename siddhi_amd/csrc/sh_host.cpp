@@ -84,7 +84,10 @@ struct PinBuf {
         return 0;
     }
     void release() {
-        if (p) hipHostFree(p);
+        if (p) {
+            hipDeviceSynchronize();  // an async copy may still read it
+            hipHostFree(p);
+        }
         p = nullptr;
         bytes = 0;
     }
@@ -402,6 +405,7 @@ struct sh_handle {
     // pinned staging of the streaming path: pin_in = one send() call's uploads,
     // pin_rd = small read-backs + the nf_cols image, pin_out = placed rows
     PinBuf pin_in, pin_rd, pin_out;
+    PinBuf pin_stage;  // the general engine's per-call event staging (nf_push)
     DevBuf n_tmin, n_slot_s, n_slot_k;  // device tie-break of due keys
     DevBuf n_armed;                     // per key: may hold a scheduler entry (nf_cols.sched_armed)
     // the armed-key list of the due pass (two buffers, swapped per pass; counts
@@ -928,6 +932,7 @@ void sh_destroy(sh_handle* h) {
     if (h->has_device) {
         hipStreamSynchronize(h->stream);
         h->pin_in.release();
+        h->pin_stage.release();
         h->pin_rd.release();
         h->pin_out.release();
         h->n_tmin.release();
@@ -1004,6 +1009,7 @@ static int push_impl(sh_handle* h, const sh_batch* b, const uint32_t* index, int
     for (size_t a = 0; a < types.size(); a++) pin_need += (size_t)b->n * type_width(types[a]);
     if (h->pin_in.ensure(pin_need)) return fail(h, SH_E_OOM, "pinned staging");
     size_t pin_off = 0;
+    bool caller_copy = false;  // a copy reads the caller's memory directly (null masks)
     for (size_t a = 0; a < types.size(); a++) {
         const int w = type_width(types[a]);
         if (st.cols[a].ensure((size_t)(r0 + b->n) * w)) return fail(h, SH_E_OOM, "column store");
@@ -1021,15 +1027,19 @@ static int push_impl(sh_handle* h, const sh_batch* b, const uint32_t* index, int
             } else if (st.nuls[a].ensure((size_t)(r0 + b->n))) {
                 return fail(h, SH_E_OOM, "null mask");
             }
-            if (nm)
+            if (nm) {
                 hipMemcpyAsync((uint8_t*)st.nuls[a].p + r0, nm, b->n, hipMemcpyHostToDevice, h->stream);
+                caller_copy = true;
+            }
             else
                 hipMemsetAsync((uint8_t*)st.nuls[a].p + r0, 0, b->n, h->stream);
         }
     }
-    // the async copies above read caller memory: complete them before returning
-    hipStreamSynchronize(h->stream);
     st.rows += b->n;
+    // the copies read pin_in, which the general engine's push does not touch (it
+    // stages through pin_stage) and which is next written after its syncs; the
+    // staged engines reuse pin_in on the next call: complete the copies first
+    if (caller_copy || h->mode != 1) hipStreamSynchronize(h->stream);
     if (h->mode == 1) return nf_push(h, b, r0, index, call_n, call_last);
     for (int64_t i = 0; i < b->n; i++) {
         h->st_ts.push_back(b->ts[i]);
@@ -1362,13 +1372,22 @@ static int nf_sev_ready(sh_handle* h, int64_t events) {
 
 // replay the launch's getState history on the host models and upload the
 // changed ranks (before the next due scan, on the same stream)
-static int nf_sev_apply(sh_handle* h) {
+// the launch's history count into pin_sev[0], read back with the caller's next sync
+static void nf_sev_count_async(sh_handle* h) {
+    if (h->sm_on && !h->pin_sev.ensure(64))
+        hipMemcpyAsync(h->pin_sev.p, h->n_sev_ctr.p, 8, hipMemcpyDeviceToHost, h->stream);
+}
+
+// counted: nf_sev_count_async ran before the caller's last sync
+static int nf_sev_apply(sh_handle* h, bool counted = false) {
     HpScope hp_(h, 3);
     if (!h->sm_on) return SH_OK;
     hipStream_t st = h->stream;
     if (h->pin_sev.ensure(64)) return fail(h, SH_E_OOM, "pinned staging");
-    hipMemcpyAsync(h->pin_sev.p, h->n_sev_ctr.p, 8, hipMemcpyDeviceToHost, st);
-    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+    if (!counted) {
+        hipMemcpyAsync(h->pin_sev.p, h->n_sev_ctr.p, 8, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+    }
     int64_t n = (int64_t)*h->pin_sev.as<unsigned long long>();
     if (n == 0 && !h->coord_on) return SH_OK;
     if (h->pin_sev.ensure((size_t)std::max<int64_t>(n, 1) * 16)) return fail(h, SH_E_OOM, "pinned staging");
@@ -1400,7 +1419,7 @@ static int nf_sev_apply(sh_handle* h) {
             uint64_t* r = h->pin_rk.as<uint64_t>();
             for (int32_t k = 0; k < nk; k++) r[k] = M.present(k) ? M.rank(k) : ~0ull;
             hipMemcpyAsync(h->n_rank[s].p, r, (size_t)nk * 8, hipMemcpyHostToDevice, st);
-            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "rank upload");
+            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "rank upload");  // (rare: after a resize)
         } else if (!M.dirty.empty()) {
             ks.clear();
             vs.clear();
@@ -1421,7 +1440,8 @@ static int nf_sev_apply(sh_handle* h) {
                 hipMemcpyAsync(h->n_rk_keys.p, h->pin_rk.as<uint8_t>(m * 8), m * 4, hipMemcpyHostToDevice, st);
                 nfd_rank_scatter(h->n_rk_keys.as<int32_t>(), h->n_rk_vals.as<uint64_t>(), (int64_t)m,
                                  h->n_rank[s].as<uint64_t>(), st);
-                if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "rank upload");
+                // no sync: the next launch follows on this stream, and pin_rk is next
+                // written after that launch's error read-back has synchronised
             }
         }
         M.rerank_all = false;
@@ -1752,11 +1772,12 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
             return fail(h, SH_E_HIP, "k_nfa_run launch failed");
         hipEventRecord(h->ev[2], st);
         hipMemcpyAsync(h->pin_rd.as<void>(PR_ERR), h->n_err.p, 4, hipMemcpyDeviceToHost, st);
+        nf_sev_count_async(h);
         if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_run");
         const unsigned err = *h->pin_rd.as<unsigned>(PR_ERR);
         if (!err) {
             h->tick++;
-            int src = nf_sev_apply(h);
+            int src = nf_sev_apply(h, true);
             if (src) return src;
             int rc = nf_place(h, n_idx, n_rows, d_seq, d_vals, cap, h->tick - 1);
             hipEventRecord(h->ev[3], st);
@@ -1976,6 +1997,7 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
             }
             if (ensure_ws(h, std::max<int64_t>(n_idx, 1))) return fail(h, SH_E_OOM, "workspace");
             if (nf_ensure_recs(h, std::max<int64_t>(h->rec_cap, ns + 4096))) return fail(h, SH_E_OOM, "emission");
+            bool counted = false;  // the history count came back with the last error read-back
             for (int attempt = 0;; attempt++) {
                 if (attempt > 64) return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
                 const size_t kw = (size_t)h->T->key_words;
@@ -2004,9 +2026,13 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
                           h->n_sel.as<int32_t>(), ns, now, h->tick, h->clock, h->seq_next, &em, st,
                           h->coord_on ? h->n_gpos.as<uint32_t>() : nullptr);
                 hipMemcpyAsync(h->pin_rd.as<void>(PR_ERR), h->n_err.p, 4, hipMemcpyDeviceToHost, st);
+                nf_sev_count_async(h);
                 if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_timer");
                 unsigned err = *h->pin_rd.as<unsigned>(PR_ERR);
-                if (!err) break;
+                if (!err) {
+                    counted = true;
+                    break;
+                }
                 if (err & NF_E_UNSUP) return fail(h, SH_E_UNSUPPORTED, "startStateReset recursion");
                 nfd_save_keys(h->n_kstate.as<uint64_t>(), (int64_t)kw, h->n_sel.as<int32_t>(), ns,
                               h->n_save.as<uint64_t>(), 1, st);
@@ -2028,7 +2054,7 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
             }
             h->tick++;
             {
-                int src = nf_sev_apply(h);
+                int src = nf_sev_apply(h, counted);
                 if (src) return src;
             }
             int64_t rows = 0;
@@ -2096,12 +2122,12 @@ static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0, const uint32_t* 
     }
     // staged in pinned memory (pin_in; the column copies of this call are complete)
     const size_t o_ts = 0, o_rows = (size_t)n * 8, o_keys = o_rows + (size_t)n * 4, o_sv = o_keys + (size_t)n * 4;
-    if (h->pin_in.ensure(o_sv + (size_t)n)) return fail(h, SH_E_OOM, "pinned staging");
-    uint8_t* sv = h->pin_in.as<uint8_t>(o_sv);
-    uint32_t* rows = h->pin_in.as<uint32_t>(o_rows);
-    int32_t* keys = h->pin_in.as<int32_t>(o_keys);
+    if (h->pin_stage.ensure(o_sv + (size_t)n)) return fail(h, SH_E_OOM, "pinned staging");
+    uint8_t* sv = h->pin_stage.as<uint8_t>(o_sv);
+    uint32_t* rows = h->pin_stage.as<uint32_t>(o_rows);
+    int32_t* keys = h->pin_stage.as<int32_t>(o_keys);
     memset(sv, (uint8_t)b->stream, (size_t)n);
-    memcpy(h->pin_in.as<int64_t>(o_ts), b->ts, (size_t)n * 8);
+    memcpy(h->pin_stage.as<int64_t>(o_ts), b->ts, (size_t)n * 8);
     int32_t nk = 1;
     for (int64_t i = 0; i < n; i++) {
         rows[i] = (uint32_t)(r0 + i);
@@ -2114,7 +2140,7 @@ static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0, const uint32_t* 
     if (h->w_ts.ensure_fresh(n * 8) || h->w_stream.ensure_fresh(n) || h->w_row.ensure_fresh(n * 4) ||
         h->w_key.ensure_fresh(n * 4) || h->n_bid.ensure_fresh(n * 4))
         return fail(h, SH_E_OOM, "staging");
-    hipMemcpyAsync(h->w_ts.p, h->pin_in.as<int64_t>(o_ts), n * 8, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(h->w_ts.p, h->pin_stage.as<int64_t>(o_ts), n * 8, hipMemcpyHostToDevice, st);
     hipMemcpyAsync(h->w_stream.p, sv, n, hipMemcpyHostToDevice, st);
     hipMemcpyAsync(h->w_row.p, rows, n * 4, hipMemcpyHostToDevice, st);
     hipMemcpyAsync(h->w_key.p, keys, n * 4, hipMemcpyHostToDevice, st);
