@@ -449,6 +449,8 @@ struct sh_handle {
     std::vector<uint32_t> r_ixstart, r_ixrule, r_free;
     shr_table r_tab{};
     DevBuf rd_rules, rd_ixval, rd_ixstart, rd_ixrule, rd_free, rd_tab;
+    DevBuf rd_img;   // the rule set's LDS image (shr_img), when it fits
+    shr_img r_img{};
     DevBuf r_rec, r_keys, r_g, r_sk, r_sv, r_hist, r_scan, r_run;
     // ---- bucketed window engine (sh_bucket.hip + shb_match): 0 untried, 1 loaded, <0 unavailable
     int bk_state = 0;
@@ -800,6 +802,55 @@ static int upload_rules(sh_handle* h) {
     if (!h->r_ixrule.empty())
         hipMemcpy(h->rd_ixrule.p, h->r_ixrule.data(), 4 * h->r_ixrule.size(), hipMemcpyHostToDevice);
     if (!h->r_free.empty()) hipMemcpy(h->rd_free.p, h->r_free.data(), 4 * h->r_free.size(), hipMemcpyHostToDevice);
+    // the LDS image: index values / starts, rule ids, per-rule window + term range, terms
+    {
+        memset(&h->r_img, 0, sizeof(h->r_img));
+        std::vector<uint8_t> img;
+        auto sect = [&](size_t bytes) {
+            const size_t at = (img.size() + 15) & ~(size_t)15;
+            img.resize(at + bytes);
+            return at;
+        };
+        size_t nterms = 0;
+        for (const shr_rule& r : h->r_rules) nterms += (size_t)r.nt[0] + r.nt[1];
+        const size_t o_ixv = sect(8 * h->r_ixval.size());
+        const size_t o_ixs = sect(4 * h->r_ixstart.size());
+        const size_t o_ixr = sect(4 * h->r_ixrule.size());
+        const size_t o_fr = sect(4 * h->r_free.size());
+        const size_t o_meta = sect(sizeof(shr_meta) * nr);
+        const size_t o_terms = sect(sizeof(shp_term) * nterms);
+        img.resize((img.size() + 15) & ~(size_t)15);
+        static const bool img_on = !(getenv("SH_RULES_IMG") && getenv("SH_RULES_IMG")[0] == '0');
+        if (img_on && img.size() <= SHR_IMG_MAX && nterms < 65536) {
+            if (!h->r_ixval.empty()) memcpy(&img[o_ixv], h->r_ixval.data(), 8 * h->r_ixval.size());
+            memcpy(&img[o_ixs], h->r_ixstart.data(), 4 * h->r_ixstart.size());
+            if (!h->r_ixrule.empty()) memcpy(&img[o_ixr], h->r_ixrule.data(), 4 * h->r_ixrule.size());
+            if (!h->r_free.empty()) memcpy(&img[o_fr], h->r_free.data(), 4 * h->r_free.size());
+            size_t tk = 0;
+            for (size_t i = 0; i < nr; i++) {
+                const shr_rule& r = h->r_rules[i];
+                shr_meta m;
+                memset(&m, 0, sizeof(m));
+                m.within = r.within;
+                m.toff = (uint16_t)tk;
+                m.nt0 = (uint8_t)r.nt[0];
+                m.nt1 = (uint8_t)r.nt[1];
+                memcpy(&img[o_meta + i * sizeof(shr_meta)], &m, sizeof(m));
+                for (int k = 0; k < 2; k++)
+                    for (int t = 0; t < r.nt[k]; t++, tk++)
+                        memcpy(&img[o_terms + tk * sizeof(shp_term)], &r.t[k][t], sizeof(shp_term));
+            }
+            if (h->rd_img.ensure(img.size())) return fail(h, SH_E_OOM, "hipMalloc failed");
+            hipMemcpy(h->rd_img.p, img.data(), img.size(), hipMemcpyHostToDevice);
+            h->r_img.bytes = (int32_t)img.size();
+            h->r_img.off_ixv = (int32_t)o_ixv;
+            h->r_img.off_ixs = (int32_t)o_ixs;
+            h->r_img.off_ixr = (int32_t)o_ixr;
+            h->r_img.off_free = (int32_t)o_fr;
+            h->r_img.off_meta = (int32_t)o_meta;
+            h->r_img.off_terms = (int32_t)o_terms;
+        }
+    }
     shr_table t = h->r_tab;
     t.rules = h->rd_rules.as<shr_rule>();
     t.ix_val = h->rd_ixval.as<int64_t>();
@@ -959,7 +1010,7 @@ void sh_destroy(sh_handle* h) {
         for (DevBuf* b : bufs) b->release();
         DevBuf* nbufs[] = {&h->d_T, &h->d_T_old, &h->d_ncols, &h->n_kstate, &h->n_kstate2, &h->n_save, &h->n_recs,
                            &h->n_ctr, &h->n_err, &h->n_cand, &h->n_sel, &h->n_bid, &h->w_oq,
-                           &h->rd_rules, &h->rd_ixval, &h->rd_ixstart, &h->rd_ixrule, &h->rd_free, &h->rd_tab,
+                           &h->rd_rules, &h->rd_ixval, &h->rd_ixstart, &h->rd_ixrule, &h->rd_free, &h->rd_tab, &h->rd_img,
                            &h->r_rec, &h->r_keys, &h->r_g, &h->r_sk, &h->r_sv, &h->r_hist, &h->r_scan, &h->r_run};
         for (DevBuf* b : nbufs) b->release();
         for (auto& st : h->stores) {
@@ -2449,7 +2500,8 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
     uint32_t* cnt = h->w_cnt.as<uint32_t>();
     uint32_t* off = h->w_off.as<uint32_t>();
     hipMemsetAsync(h->v_flag.p, 0, 4, st);
-    if (shr_count(dT, sts, skeys, n, sentinel, dC, cnt, h->v_flag.as<int32_t>(), st) ||
+    if (shr_count(dT, sts, skeys, n, sentinel, dC, cnt, h->v_flag.as<int32_t>(), st,
+                  h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr, &h->r_img) ||
         shd_exclusive_scan(cnt, off, n, h->w_scan.as<uint32_t>(), st))
         return fail(h, SH_E_HIP, "rule scan launch failed");
     uint32_t lo = 0, lc = 0;
@@ -2473,7 +2525,8 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
         uint32_t* rec_p = h->r_rec.as<uint32_t>();
         uint32_t* rec_q = rec_p + m;
         uint32_t* rec_r = rec_q + m;
-        if (shr_write(dT, sts, skeys, n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, st))
+        if (shr_write(dT, sts, skeys, n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, st,
+                      h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr, &h->r_img))
             return fail(h, SH_E_HIP, "rule write launch failed");
         // PartitionStreamReceiver runs inside each send() call
         const int64_t batch = run->batch_events > 0 ? run->batch_events : 0;

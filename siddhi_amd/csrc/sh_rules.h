@@ -30,17 +30,33 @@ struct shr_table {
     const uint32_t* free_rule;          // device [n_free], ascending
 };
 
+// the rule set as one image the scan kernel copies into LDS (built by the host when
+// it fits): the predicate index, the rule ids per group and without the indexed
+// conjunct, per rule its window and term range, and every term
+struct shr_meta {
+    int64_t within;
+    uint16_t toff;                      // first term (f1's, then f2's)
+    uint8_t nt0, nt1;
+    uint32_t pad;
+};
+struct shr_img {
+    int32_t bytes;                      // image size (multiple of 16), 0: no image
+    int32_t off_ixv, off_ixs, off_ixr, off_free, off_meta, off_terms, pad;
+};
+#define SHR_IMG_MAX (144 * 1024)
+
 #ifdef __cplusplus
 extern "C" {
 #endif
 // matches opened at every key-segment position (cnt[p]); flag := 1 when a key's
 // timestamps decrease (the window reduction does not hold)
 int shr_count(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
-              const shd_cols* dC, uint32_t* cnt, int32_t* flag, void* stream);
+              const shd_cols* dC, uint32_t* cnt, int32_t* flag, void* stream, const uint8_t* img = nullptr,
+              const shr_img* I = nullptr);
 // the same scan, writing (opening, consuming, rule) records at off[p]
 int shr_write(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
               const shd_cols* dC, const uint32_t* cnt, const uint32_t* off, uint32_t* rec_p, uint32_t* rec_q,
-              uint32_t* rec_r, void* stream);
+              uint32_t* rec_r, void* stream, const uint8_t* img = nullptr, const shr_img* I = nullptr);
 // PartitionStreamReceiver runs of an arrival-order key array: flags[i] (run
 // start), rid[i] (exclusive scan of flags), rfirst[run] (first arrival index);
 // run_ids (may be NULL): the caller's run of every event (sh_device_run.d_run)

@@ -171,6 +171,150 @@ __global__ void __launch_bounds__(RTPB) k_rules_scan(const shr_table* __restrict
     }
 }
 
+// the same scan over the rule set's LDS image (shr_img): the index search, the rule
+// ids, every term and the stream's column pointers come from LDS, so a lane's chain
+// of dependent reads (group -> rule -> terms -> column) stays on chip; one 1024-thread
+// workgroup per CU strides over the events
+#define RTPB_IMG 1024
+__device__ __forceinline__ int64_t rule_attr(const void* const* cols, int a, int type, uint32_t row) {
+    const void* p = cols[a];
+    switch (type) {
+        case SH_T_LONG:
+        case SH_T_DOUBLE: return ((const int64_t*)p)[row];
+        case SH_T_FLOAT: return (int64_t)(uint32_t)((const uint32_t*)p)[row];
+        case SH_T_BOOL: return ((const uint8_t*)p)[row] ? 1 : 0;
+        default: return (int64_t)((const int32_t*)p)[row];
+    }
+}
+
+__device__ __forceinline__ bool rule_terms_img(const shp_term* T, int nt, uint32_t r0, uint32_t r1,
+                                               const void* const* cols) {
+    for (int t = 0; t < nt; t++) {
+        const shp_term X = T[t];
+        const uint32_t lr = X.lslot ? r1 : r0;
+        if (lr == SHD_NULL_ROW) return false;
+        VmVal l, r;
+        l.t = X.ltype;
+        l.null = 0;
+        l.b = rule_attr(cols, X.lattr, X.ltype, lr);
+        if (X.rkind == 1) {
+            r.t = X.ctype;
+            r.null = 0;
+            r.b = X.c;
+        } else {
+            const uint32_t rr = X.rslot ? r1 : r0;
+            if (rr == SHD_NULL_ROW) return false;
+            r.t = X.rtype;
+            r.null = 0;
+            r.b = rule_attr(cols, X.rattr, X.rtype, rr);
+            if (X.rkind == 2) {
+                VmVal c;
+                c.t = X.ctype;
+                c.null = 0;
+                c.b = X.c;
+                r = vm_arith(X.aop, X.atype, r, c);
+                if (r.null) return false;
+            }
+        }
+        if (!vm_cmp(X.op, X.dom, l, r)) return false;
+    }
+    return true;
+}
+
+template <int WRITE>
+__global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
+    const shr_table* __restrict__ RT, const int64_t* __restrict__ sts, const uint32_t* __restrict__ skeys, int64_t n,
+    uint32_t sentinel, const shd_cols* __restrict__ C, uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
+    uint32_t* __restrict__ rec_p, uint32_t* __restrict__ rec_q, uint32_t* __restrict__ rec_r, int32_t* __restrict__ flag,
+    const uint8_t* __restrict__ img, shr_img I) {
+    extern __shared__ uint4 s_img[];
+    __shared__ const void* s_col[32];
+    for (int i = threadIdx.x; i < I.bytes / 16; i += blockDim.x) s_img[i] = ((const uint4*)img)[i];
+    if (threadIdx.x < 32) s_col[threadIdx.x] = C->col[0][threadIdx.x];
+    __syncthreads();
+    const uint8_t* L = (const uint8_t*)s_img;
+    const int64_t* ixv = (const int64_t*)(L + I.off_ixv);
+    const uint32_t* ixs = (const uint32_t*)(L + I.off_ixs);
+    const uint32_t* ixr = (const uint32_t*)(L + I.off_ixr);
+    const uint32_t* fr = (const uint32_t*)(L + I.off_free);
+    const shr_meta* meta = (const shr_meta*)(L + I.off_meta);
+    const shp_term* terms = (const shp_term*)(L + I.off_terms);
+    const int ix_attr = RT->ix_attr;
+    const int n_ix = RT->n_ix;
+    const uint32_t n_free = (uint32_t)RT->n_free;
+    const int ix_ty = ix_attr >= 0 ? RT->attr_type[ix_attr] : 0;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        if (WRITE && cnt[p] == 0) continue;
+        const uint32_t key = skeys ? skeys[p] : 0u;
+        if (key == sentinel) continue;
+        const int64_t t0 = sts[p];
+        if (!WRITE && p > 0 && (!skeys || skeys[p - 1] == key) && t0 < sts[p - 1]) atomicExch(flag, 1);
+        uint32_t lo = 0, hi = 0;
+        if (ix_attr >= 0) {
+            const int64_t x = rule_ix_key(ix_ty, rule_attr(s_col, ix_attr, ix_ty, (uint32_t)p));
+            int a = 0, b = n_ix;
+            while (a < b) {
+                const int m = (a + b) >> 1;
+                if (ixv[m] < x)
+                    a = m + 1;
+                else
+                    b = m;
+            }
+            if (a < n_ix && ixv[a] == x) {
+                lo = ixs[a];
+                hi = ixs[a + 1];
+            }
+        }
+        const uint32_t nsel = hi - lo, total = nsel + n_free;
+        uint32_t c = 0;
+        const uint32_t o = WRITE ? off[p] : 0u;
+        for (uint32_t k = 0; k < total; k++) {
+            const uint32_t r = k < nsel ? ixr[lo + k] : fr[k - nsel];
+            const shr_meta M = meta[r];
+            const shp_term* T0 = terms + M.toff;
+            if (!rule_terms_img(T0, M.nt0, (uint32_t)p, SHD_NULL_ROW, s_col)) continue;
+            const shp_term* T1 = T0 + M.nt0;
+            const int64_t W = M.within;
+            for (int64_t q = p + 1; q < n; q++) {
+                if (skeys && skeys[q] != key) break;
+                const int64_t d = sts[q] - t0;
+                if (W >= 0 && (d < 0 ? -d : d) > W) break;  // expired before event q is matched
+                if (rule_terms_img(T1, M.nt1, (uint32_t)p, (uint32_t)q, s_col)) {
+                    if (WRITE) {
+                        rec_p[o + c] = (uint32_t)p;
+                        rec_q[o + c] = (uint32_t)q;
+                        rec_r[o + c] = r;
+                    }
+                    c++;
+                    break;
+                }
+            }
+        }
+        if (!WRITE) cnt[p] = c;
+    }
+}
+
+template <int WRITE>
+static int rules_scan_img(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
+                          const shd_cols* dC, uint32_t* cnt, const uint32_t* off, uint32_t* rec_p, uint32_t* rec_q,
+                          uint32_t* rec_r, int32_t* flag, const uint8_t* img, const shr_img& I, hipStream_t st) {
+    static int attr_set = 0;  // the dynamic LDS limit, raised once per instantiation
+    if (!attr_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rules_scan_img<WRITE>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, SHR_IMG_MAX) != hipSuccess)
+            return -3;
+        attr_set = 1;
+    }
+    int64_t g = (n + RTPB_IMG - 1) / RTPB_IMG;
+    const int per_cu = (160 * 1024) / (I.bytes + 1024);
+    const int64_t gmax = 256LL * (per_cu < 1 ? 1 : per_cu);
+    if (g > gmax) g = gmax;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(k_rules_scan_img<WRITE>, dim3((unsigned)g), dim3(RTPB_IMG), (size_t)I.bytes, st, dT, sts, skeys,
+                       n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, flag, img, I);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 // start of a PartitionStreamReceiver run: the first keyed event of a send() call,
 // or a keyed event whose key differs from the previous keyed event of the call
 // (run_ids: the caller's runs, a new id starts a run)
@@ -273,7 +417,11 @@ static unsigned sgrid(int64_t n) {
 }
 
 extern "C" int shr_count(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
-                         const shd_cols* dC, uint32_t* cnt, int32_t* flag, void* stream) {
+                         const shd_cols* dC, uint32_t* cnt, int32_t* flag, void* stream, const uint8_t* img,
+                         const shr_img* I) {
+    if (img && I && I->bytes > 0)
+        return rules_scan_img<0>(dT, sts, skeys, n, sentinel, dC, cnt, nullptr, nullptr, nullptr, nullptr, flag, img, *I,
+                                 (hipStream_t)stream);
     hipLaunchKernelGGL(k_rules_scan<0>, dim3(sgrid(n)), dim3(RTPB), 0, (hipStream_t)stream, dT, sts, skeys, n,
                        sentinel, dC, cnt, (const uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
                        (uint32_t*)nullptr, flag);
@@ -282,7 +430,10 @@ extern "C" int shr_count(const shr_table* dT, const int64_t* sts, const uint32_t
 
 extern "C" int shr_write(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
                          const shd_cols* dC, const uint32_t* cnt, const uint32_t* off, uint32_t* rec_p,
-                         uint32_t* rec_q, uint32_t* rec_r, void* stream) {
+                         uint32_t* rec_q, uint32_t* rec_r, void* stream, const uint8_t* img, const shr_img* I) {
+    if (img && I && I->bytes > 0)
+        return rules_scan_img<1>(dT, sts, skeys, n, sentinel, dC, (uint32_t*)cnt, off, rec_p, rec_q, rec_r, nullptr,
+                                 img, *I, (hipStream_t)stream);
     hipLaunchKernelGGL(k_rules_scan<1>, dim3(sgrid(n)), dim3(RTPB), 0, (hipStream_t)stream, dT, sts, skeys, n,
                        sentinel, dC, (uint32_t*)cnt, off, rec_p, rec_q, rec_r, (int32_t*)nullptr);
     return rules_ok();
