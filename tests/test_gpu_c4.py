@@ -63,3 +63,20 @@ def test_c4_colliding_names_on_gpu():
     eng.close()
     assert len(ref["seq"]) > 500
     assert same_output(got, ref)
+
+
+@pytest.mark.parametrize("every", [False, True])
+def test_c4_spec_workload_1M_users(every):
+    """the SURVEY 8d workload shape (Login 20% / Txn 60% / Logout 20%, R = 100 ev/ms,
+    calls of 4,096 per stream, synth.c4_spec_stream) over 1M users, whole stream vs the
+    oracle, for the query and its `every (...)` variant"""
+    from siddhi_amd import compiler, synth
+    from siddhi_amd._native import HipEngine
+    c = compiler.compile_app(synth.C4_EVERY_QUERY if every else synth.C4_QUERY)
+    blocks = synth.c4_spec_stream(3_000_000, 1_000_000, rate_per_ms=100, batch=4096)
+    ref = run_c4(OracleEngine(c), blocks)
+    eng = HipEngine(c)
+    got = run_c4(eng, blocks)
+    eng.close()
+    assert len(ref["seq"]) > 10_000
+    assert same_output(got, ref), (len(got["seq"]), len(ref["seq"]))
