@@ -416,6 +416,9 @@ struct sh_handle {
     int64_t hp_n[6] = {0, 0, 0, 0, 0, 0};
     int seq3_last = 0;                  // the last general-engine run took k_seq3
     bool s3_compact = false;            // ... with k_seq3s's compact records (nfd_place_s3 places them)
+    bool s3_agg = false;                // ... whose aggregates ran in the kernel (no post-pass)
+    int s3_rw = 0;                      // record words
+    uint32_t s3_wide = 0;               // outputs held as 2-word running values
     bool kstate_stale = false;          // key blocks not reset after a k_seq3 run (reset before the next use)
     int s3_type = 0;                    // their values' type (one 4-byte attribute)
     uint64_t s3_seq_base = 0;           // and the run's first trigger sequence number
@@ -467,7 +470,7 @@ struct sh_handle {
     // aggregators behind the fast engines (sh_agg.hip): scratch, trigger sequence
     // numbers when the caller wants none, and the last run's path
     DevBuf a_scratch, a_seq;
-    int agg_last = 0;  // 1: post-pass done, 2: post-pass not exact -> sequential engine
+    int agg_last = 0;  // 1: post-pass done, 2: post-pass not exact -> sequential engine, 3: in the k_seq3s lanes
     std::vector<int32_t> out_types;  // per select position over the queries (-2: types differ)
     uint64_t fp = 0;                 // compiled-program fingerprint (snapshot images)
 };
@@ -1623,7 +1626,7 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
             // one record slot per key-ordered position of the run (n_idx events)
             nfd_place_s3(h->n_recs.as<uint64_t>(), h->rec_cap, n_idx, no, h->s3_type, h->s3_seq_base,
                          h->w_off.as<uint32_t>(), h->dev_want_query ? h->w_oq.as<int32_t>() : nullptr, d_seq, d_vals,
-                         h->w_inv.as<uint32_t>(), total, st);
+                         h->w_inv.as<uint32_t>(), total, st, h->s3_rw, h->s3_wide);
             return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "placement");
         }
         nfd_place(h->n_recs.as<uint64_t>(), (int64_t)nrec, stride, h->w_off.as<uint32_t>(), no,
@@ -1776,6 +1779,24 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     h->s3_compact = s3_col && d_seq && s3_compact_on;
     h->s3_type = h->T->q[0].s3_t2;
     h->s3_seq_base = B.seq_base;
+    // sum / avg / count in the kernel's lanes (each key's matches in trigger order: the
+    // reference's own additions), when every aggregate is one of those and the record fits
+    {
+        const nf_query& Q = h->T->q[0];
+        bool agg = h->s3_compact && Q.contains_agg && Q.n_out <= 6 && !getenv("SH_S3_AGG_POST");
+        int rw = 1;
+        uint32_t wide = 0;
+        for (int o = 0; o < Q.n_out; o++) {
+            const int ak = Q.out_agg[o];
+            if (ak != SH_AGG_NONE && ak != SH_AGG_SUM && ak != SH_AGG_AVG && ak != SH_AGG_COUNT) agg = false;
+            const bool w = ak != SH_AGG_NONE;
+            rw += w ? 2 : 1;
+            if (w) wide |= 1u << o;
+        }
+        h->s3_agg = agg;
+        h->s3_rw = agg ? rw : 1 + std::max(1, Q.n_out);
+        h->s3_wide = agg ? wide : 0u;
+    }
     E.sorted_rows = sorted_cols ? 1 : 0;
     E.pad = 0;
     E.run = fresh ? h->dev_run_ids : nullptr;
@@ -1816,7 +1837,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
         h->seq3_last = seq3 ? 1 : 0;
         if (seq3) {
             if (nfd_seq3(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), &E, n, seg_list, nseg, skeys, nkeys, max_seg,
-                         &em, st, s3_col, h->s3_compact ? 1 : 0))
+                         &em, st, s3_col, h->s3_compact ? 1 : 0, h->s3_agg ? 1 : 0, h->s3_rw))
                 return fail(h, SH_E_HIP, "k_seq3 launch failed");
         } else if (nfd_run(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), &E, n,
                            seg_list, nseg, skeys, nkeys, max_seg, h->tick, h->clock, &em, st))
@@ -2877,7 +2898,8 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
                             run->batch_events, getenv("SH_NFA_GATHER") ? nullptr : run);
             h->dev_run_ids = nullptr;
             run->out_count = rows;
-            if (rc != SH_OK || !aggp || !h->seq3_last) break;
+            if (rc == SH_OK && aggp && h->seq3_last && h->s3_agg) h->agg_last = 3;
+            if (rc != SH_OK || !aggp || !h->seq3_last || h->s3_agg) break;
             // k_seq3 wrote the aggregators' arguments: the running values
             int32_t arg_type[NF_MAX_OUT];
             for (int o = 0; o < Q0.n_out; o++) arg_type[o] = Q0.s3_out_type[o];

@@ -287,12 +287,18 @@ __device__ __forceinline__ NfVal s3_bits(uint32_t b, int t) {
 // (loc again and the raw 4-byte select values) for the positions that matched --
 // placed by k_s3_inv / k_s3_gather. No record counter: the generic sink's chunk claims are one atomic on
 // a single word per 16 records, which serialises at the L2 (C3: 1.5M claims).
-template <bool COMPACT>
+// AGG (COMPACT only): the selector's sum / avg / count run in the lane -- one key's
+// matches in trigger order, the reference's own sequence of double additions
+// (AttributeAggregatorExecutor state per partition key) -- and the record holds the
+// running value (2 words) instead of the argument; rw = record words
+#define S3S_MAXO 6
+template <bool COMPACT, bool AGG>
 __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ T, const uint32_t* __restrict__ col,
                                                    const uint32_t* __restrict__ perm, uint64_t seq_base, int64_t n,
                                                    const uint32_t* __restrict__ seg_list,
                                                    const uint32_t* __restrict__ nseg,
-                                                   const uint32_t* __restrict__ skeys, int32_t nkeys, nfd_emit EM) {
+                                                   const uint32_t* __restrict__ skeys, int32_t nkeys, nfd_emit EM,
+                                                   int rw) {
     __shared__ uint32_t sv[S3S_TPB * S3S_LD], sp[S3S_TPB * S3S_LD];
     __shared__ uint32_t s_b[S3S_TPB], s_e[S3S_TPB];
     __shared__ int64_t s_end;
@@ -348,6 +354,9 @@ __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ 
     uint32_t* const rv = rl + EM.cap;
     bool has_last = false, has_e1 = false, fail = false;
     uint32_t e1b = 0, lastb = 0;
+    int64_t acc[S3S_MAXO], acnt[S3S_MAXO];  // AGG: running sum (long or double bits) and count per output
+#pragma unroll
+    for (int o = 0; o < S3S_MAXO; o++) acc[o] = acnt[o] = 0;
     __syncthreads();
     for (uint32_t r0 = 0;; r0 += S3S_E) {
         // every lane's next window, loaded by the whole workgroup
@@ -370,13 +379,47 @@ __global__ void __launch_bounds__(S3S_TPB) k_seq3s(const nf_table* __restrict__ 
                 // the slot's record: the trigger's arrival index or ~0u, written back below
                 const uint32_t loc = sp[threadIdx.x * S3S_LD + j];
                 sv[threadIdx.x * S3S_LD + j] = hit ? loc : ~0u;
-                if (hit) {
+                if (hit && !AGG) {
                     // [loc, values]: the gather reads one record in one line
-                    uint32_t* r = rv + (int64_t)(w0 + (uint32_t)j) * (no + 1);
+                    uint32_t* r = rv + (int64_t)(w0 + (uint32_t)j) * rw;
                     r[0] = loc;
                     for (int o = 0; o < no; o++) {
                         const int s = Q.s3_out_slot[o];
                         r[1 + o] = s == 0 ? e1b : s == 1 ? lastb : xb;
+                    }
+                    EM.match_cnt[loc] = 1;
+                } else if (hit) {
+                    uint32_t* r = rv + (int64_t)(w0 + (uint32_t)j) * rw;
+                    r[0] = loc;
+                    int wi = 1;
+#pragma unroll
+                    for (int o = 0; o < S3S_MAXO; o++) {
+                        const int ak = o < no ? Q.out_agg[o] : -1;
+                        if (ak < 0) continue;
+                        const int s = Q.s3_out_slot[o];
+                        const uint32_t vb = s == 0 ? e1b : s == 1 ? lastb : xb;
+                        if (ak == SH_AGG_NONE) {
+                            r[wi++] = vb;
+                            continue;
+                        }
+                        // SumAttributeAggregatorExecutor / AvgAttributeAggregatorExecutor /
+                        // CountAttributeAggregatorExecutor on a current event (no nulls here)
+                        acnt[o]++;
+                        uint64_t ov;
+                        if (ak == SH_AGG_COUNT) {
+                            ov = (uint64_t)acnt[o];
+                        } else if (ak == SH_AGG_SUM && t == SH_T_INT) {
+                            acc[o] = (int64_t)((uint64_t)acc[o] + (uint64_t)(int64_t)(int32_t)vb);
+                            ov = (uint64_t)acc[o];
+                        } else {
+                            const double x = t == SH_T_INT ? (double)(int32_t)vb : (double)__uint_as_float(vb);
+                            const double d = __longlong_as_double(acc[o]) + x;
+                            acc[o] = __double_as_longlong(d);
+                            ov = (uint64_t)__double_as_longlong(ak == SH_AGG_AVG ? d / (double)acnt[o] : d);
+                        }
+                        r[wi] = (uint32_t)ov;
+                        r[wi + 1] = (uint32_t)(ov >> 32);
+                        wi += 2;
                     }
                     EM.match_cnt[loc] = 1;
                 }
@@ -439,21 +482,31 @@ __global__ void __launch_bounds__(256) k_s3_gather(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ inv, int64_t total, int64_t nrec,
                                                    int n_out, int type, uint64_t seq_base,
                                                    int32_t* __restrict__ out_query, uint64_t* __restrict__ out_seq,
-                                                   int64_t* __restrict__ out_vals) {
+                                                   int64_t* __restrict__ out_vals, int rw, uint32_t wide) {
     const int64_t dst = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (dst >= total) return;
     const uint32_t ix = inv[dst];
     if ((int64_t)ix >= nrec) return;  // no record (an emission overflow, reported through err)
-    const uint32_t* r = rv + (int64_t)ix * (n_out + 1);
+    const uint32_t* r = rv + (int64_t)ix * rw;
     if (out_query) out_query[dst] = 0;
     if (out_seq) out_seq[dst] = seq_base + r[0];
-    if (out_vals)
-        for (int o = 0; o < n_out; o++) out_vals[dst * n_out + o] = s3_bits(r[1 + o], type).b;
+    if (out_vals) {
+        // wide bit o: output o is a running aggregate (two words)
+        int wi = 1;
+        for (int o = 0; o < n_out; o++) {
+            if ((wide >> o) & 1u) {
+                out_vals[dst * n_out + o] = (int64_t)((uint64_t)r[wi] | ((uint64_t)r[wi + 1] << 32));
+                wi += 2;
+            } else {
+                out_vals[dst * n_out + o] = s3_bits(r[wi++], type).b;
+            }
+        }
+    }
 }
 
 extern "C" int nfd_place_s3(const uint64_t* recs, int64_t cap, int64_t nrec, int n_out, int type, uint64_t seq_base,
                             const uint32_t* offsets, int32_t* out_query, uint64_t* out_seq, int64_t* out_vals,
-                            uint32_t* inv, int64_t total, void* stream) {
+                            uint32_t* inv, int64_t total, void* stream, int rw, uint32_t wide) {
     if (nrec <= 0 || total <= 0) return 0;
     const uint32_t* rl = (const uint32_t*)recs;
     hipMemsetAsync(inv, 0xFF, (size_t)total * 4, (hipStream_t)stream);
@@ -461,7 +514,7 @@ extern "C" int nfd_place_s3(const uint64_t* recs, int64_t cap, int64_t nrec, int
                        offsets, inv);
     hipLaunchKernelGGL(k_s3_gather, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rl,
                        rl + cap, (const uint32_t*)inv, total, nrec, n_out, type, seq_base, out_query, out_seq,
-                       out_vals);
+                       out_vals, rw, wide);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -764,18 +817,22 @@ extern "C" int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, 
 
 extern "C" int nfd_seq3(const nf_table* dT, const nf_cols* dC, const nfd_events* ev, int64_t n,
                         const uint32_t* seg_list, const uint32_t* nseg, const uint32_t* skeys, int32_t nkeys,
-                        int64_t max_segments, const nfd_emit* em, void* stream, const void* s3_col, int compact) {
+                        int64_t max_segments, const nfd_emit* em, void* stream, const void* s3_col, int compact,
+                        int agg, int rw) {
     if (s3_col && !ev->gidx) {
         // LDS-staged (the host checked the shape: one 4-byte attribute, no nulls,
         // key-ordered copy in s3_col)
         if (max_segments < 1) max_segments = 1;
         const dim3 g(nf_blocks(max_segments, S3S_TPB)), b(S3S_TPB);
-        if (compact)
-            hipLaunchKernelGGL(k_seq3s<true>, g, b, 0, (hipStream_t)stream, dT, (const uint32_t*)s3_col, ev->perm,
-                               ev->seq_base, n, seg_list, nseg, skeys, nkeys, *em);
+        if (compact && agg)
+            hipLaunchKernelGGL((k_seq3s<true, true>), g, b, 0, (hipStream_t)stream, dT, (const uint32_t*)s3_col,
+                               ev->perm, ev->seq_base, n, seg_list, nseg, skeys, nkeys, *em, rw);
+        else if (compact)
+            hipLaunchKernelGGL((k_seq3s<true, false>), g, b, 0, (hipStream_t)stream, dT, (const uint32_t*)s3_col,
+                               ev->perm, ev->seq_base, n, seg_list, nseg, skeys, nkeys, *em, rw);
         else
-            hipLaunchKernelGGL(k_seq3s<false>, g, b, 0, (hipStream_t)stream, dT, (const uint32_t*)s3_col, ev->perm,
-                               ev->seq_base, n, seg_list, nseg, skeys, nkeys, *em);
+            hipLaunchKernelGGL((k_seq3s<false, false>), g, b, 0, (hipStream_t)stream, dT, (const uint32_t*)s3_col,
+                               ev->perm, ev->seq_base, n, seg_list, nseg, skeys, nkeys, *em, rw);
         return hipGetLastError() == hipSuccess ? 0 : -3;
     }
     DevEvents E;

@@ -48,11 +48,12 @@ int nfd_run(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, const nfd_e
 // the rise-and-fall sequence engine (nf_query.s3) over the key segments, fresh state
 int nfd_seq3(const nf_table* dT, const nf_cols* dC, const nfd_events* ev, int64_t n, const uint32_t* seg_list,
              const uint32_t* nseg, const uint32_t* skeys, int32_t nkeys, int64_t max_segments, const nfd_emit* em,
-             void* stream, const void* s3_col = nullptr, int compact = 0);
-// placement of k_seq3s's compact records (loc[cap], then values[cap][n_out] over recs)
+             void* stream, const void* s3_col = nullptr, int compact = 0, int agg = 0, int rw = 0);
+// placement of k_seq3s's compact records (loc[cap], then [cap][rw] words over recs;
+// wide bit o: output o is a 2-word running aggregate)
 int nfd_place_s3(const uint64_t* recs, int64_t cap, int64_t nrec, int n_out, int type, uint64_t seq_base,
                  const uint32_t* offsets, int32_t* out_query, uint64_t* out_seq, int64_t* out_vals, uint32_t* inv,
-                 int64_t total, void* stream);
+                 int64_t total, void* stream, int rw, uint32_t wide);
 int nfd_start(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, uint64_t tick, int64_t clock,
               const nfd_emit* em, void* stream);
 // armed (may be NULL): per-key maybe-registered flags (nf_cols.sched_armed);

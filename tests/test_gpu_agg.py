@@ -84,12 +84,17 @@ def test_c1_aggregates_unpartitioned_window_vs_oracle():
     assert np.array_equal(vals, ref["values"])
 
 
-def test_c3_aggregates_seq3_vs_oracle():
+@pytest.mark.parametrize("post", [False, True])
+def test_c3_aggregates_seq3_vs_oracle(post, monkeypatch):
+    """sum / avg in the rise-and-fall kernel's lanes (agg status 3), or as the
+    post-pass over the rows (SH_S3_AGG_POST, status 1)"""
     from siddhi_amd import synth
+    if post:
+        monkeypatch.setenv("SH_S3_AGG_POST", "1")
     ts, k, p, v = synth.stock_stream(300_000, 3_000, 1000, config_index=3)
     (m, seq, vals), st = _run(C3_AGG, ts, k, [k, p, v], 3_000)
     ref = _oracle(C3_AGG, ts, [k, p, v], k)
-    assert st["seq3"] == 1 and st["agg"] == 1, st
+    assert st["seq3"] == 1 and st["agg"] == (1 if post else 3), st
     assert m == len(ref["seq"]) > 0
     assert np.array_equal(seq, ref["seq"].astype(np.int64))
     assert np.array_equal(vals, ref["values"])
