@@ -33,8 +33,15 @@ namespace {
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool view = false;  // points into another buffer (set_view): never reallocated or freed here
+    void set_view(void* at, size_t n) {
+        p = at;
+        bytes = n;
+        view = true;
+    }
     int ensure(size_t need) {
         if (need <= bytes) return 0;
+        if (view) return SH_E_OOM;
         size_t nb = std::max(need, bytes * 2);
         void* q = nullptr;
         if (hipMalloc(&q, nb) != hipSuccess) return SH_E_OOM;
@@ -48,6 +55,7 @@ struct DevBuf {
     }
     int ensure_fresh(size_t need) {  // no content preservation
         if (need <= bytes) return 0;
+        if (view) return SH_E_OOM;
         if (p) hipFree(p);
         p = nullptr;
         bytes = 0;
@@ -57,9 +65,10 @@ struct DevBuf {
         return 0;
     }
     void release() {
-        if (p) hipFree(p);
+        if (p && !view) hipFree(p);
         p = nullptr;
         bytes = 0;
+        view = false;
     }
     template <class T>
     T* as() const {
@@ -428,6 +437,11 @@ struct sh_handle {
     bool sm_on = false;
     ShSchedModels sm;
     DevBuf n_sev, n_sev_ctr, n_rk_keys, n_rk_vals;
+    // the general engine's per-launch counters in one block (one fill, one read-back):
+    // record counter n_ctr at 0, error word n_err at 8, history counter n_sev_ctr at 16
+    DevBuf n_ctl;
+    nf_cols cols_last;          // the column image last uploaded to d_ncols (nf_put_cols)
+    bool cols_cached = false;
     std::vector<DevBuf> n_rank;         // by scheduler id, [n_nkeys] u64
     PinBuf pin_sev, pin_rk;
     int64_t sev_cap = 0;
@@ -960,9 +974,12 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
         return fail(h, SH_E_OOM, "hipMalloc failed");
     hipMemcpy(h->d_prog.p, &h->prog, sizeof(shp_program), hipMemcpyHostToDevice);
     if (h->mode == 1) {
-        if (h->d_T.ensure(sizeof(nf_table)) || h->d_ncols.ensure(sizeof(nf_cols)) || h->n_err.ensure(64) ||
-            h->n_ctr.ensure(64))
+        if (h->d_T.ensure(sizeof(nf_table)) || h->d_ncols.ensure(sizeof(nf_cols)) || h->n_ctl.ensure(256))
             return fail(h, SH_E_OOM, "hipMalloc failed");
+        hipMemset(h->n_ctl.p, 0, 256);
+        h->n_ctr.set_view(h->n_ctl.as<uint8_t>(), 8);
+        h->n_err.set_view(h->n_ctl.as<uint8_t>() + 8, 8);
+        h->n_sev_ctr.set_view(h->n_ctl.as<uint8_t>() + 16, 64);
         hipMemcpy(h->d_T.p, h->T, sizeof(nf_table), hipMemcpyHostToDevice);
     }
     if (h->has_rules && upload_rules(h)) return SH_E_OOM;
@@ -1014,6 +1031,7 @@ void sh_destroy(sh_handle* h) {
         DevBuf* nbufs[] = {&h->d_T, &h->d_T_old, &h->d_ncols, &h->n_kstate, &h->n_kstate2, &h->n_save, &h->n_recs,
                            &h->n_ctr, &h->n_err, &h->n_cand, &h->n_sel, &h->n_bid, &h->w_oq,
                            &h->rd_rules, &h->rd_ixval, &h->rd_ixstart, &h->rd_ixrule, &h->rd_free, &h->rd_tab, &h->rd_img,
+                           &h->n_ctl,
                            &h->r_rec, &h->r_keys, &h->r_g, &h->r_sk, &h->r_sv, &h->r_hist, &h->r_scan, &h->r_run};
         for (DevBuf* b : nbufs) b->release();
         for (auto& st : h->stores) {
@@ -1413,7 +1431,8 @@ static int nf_ensure_keys(sh_handle* h, int32_t nkeys) {
 }
 
 // scheduler-history buffer for a launch processing `events` events / keys
-static int nf_sev_ready(sh_handle* h, int64_t events) {
+// (zero: clear the counter here; the launch paths clear the whole counter block)
+static int nf_sev_ready(sh_handle* h, int64_t events, bool zero = true) {
     if (!h->sm_on) return 0;
     const int64_t need = std::max<int64_t>(4096, 2 * (events + 64) * (int64_t)h->sm.used.size());
     if (need > h->sev_cap) {
@@ -1421,28 +1440,40 @@ static int nf_sev_ready(sh_handle* h, int64_t events) {
         if (h->n_sev.ensure_fresh((size_t)need * 16) || h->n_sev_ctr.ensure_fresh(64)) return SH_E_OOM;
         h->sev_cap = need;
     }
+    if (!zero) return 0;
     return hipMemsetAsync(h->n_sev_ctr.p, 0, 8, h->stream) == hipSuccess ? 0 : SH_E_HIP;
 }
 
+// the counter block's record counter, error word and history counter, zeroed at once
+static void nf_ctl_zero(sh_handle* h) { hipMemsetAsync(h->n_ctl.p, 0, 24, h->stream); }
+
 // replay the launch's getState history on the host models and upload the
 // changed ranks (before the next due scan, on the same stream)
-// the launch's history count into pin_sev[0], read back with the caller's next sync
-static void nf_sev_count_async(sh_handle* h) {
-    if (h->sm_on && !h->pin_sev.ensure(64))
-        hipMemcpyAsync(h->pin_sev.p, h->n_sev_ctr.p, 8, hipMemcpyDeviceToHost, h->stream);
+// pin_rd slots of the counter block read back after a launch (nf_ctl_read)
+enum { PR_CTL = 40 };
+// the launch's counter block (records, error, history count) into pin_rd[PR_CTL..+24),
+// read with the caller's next sync
+static void nf_ctl_read(sh_handle* h) {
+    hipMemcpyAsync(h->pin_rd.as<uint8_t>() + PR_CTL, h->n_ctl.p, 24, hipMemcpyDeviceToHost, h->stream);
 }
+static unsigned nf_ctl_err(sh_handle* h) { return *(const unsigned*)(h->pin_rd.as<uint8_t>() + PR_CTL + 8); }
+static int64_t nf_ctl_nrec(sh_handle* h) { return *(const int64_t*)(h->pin_rd.as<uint8_t>() + PR_CTL); }
+static int64_t nf_ctl_nsev(sh_handle* h) { return *(const int64_t*)(h->pin_rd.as<uint8_t>() + PR_CTL + 16); }
 
-// counted: nf_sev_count_async ran before the caller's last sync
+// counted: nf_ctl_read ran before the caller's last sync (the history count is in pin_rd)
 static int nf_sev_apply(sh_handle* h, bool counted = false) {
     HpScope hp_(h, 3);
     if (!h->sm_on) return SH_OK;
     hipStream_t st = h->stream;
     if (h->pin_sev.ensure(64)) return fail(h, SH_E_OOM, "pinned staging");
-    if (!counted) {
+    int64_t n;
+    if (counted) {
+        n = nf_ctl_nsev(h);
+    } else {
         hipMemcpyAsync(h->pin_sev.p, h->n_sev_ctr.p, 8, hipMemcpyDeviceToHost, st);
         if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+        n = (int64_t)*h->pin_sev.as<unsigned long long>();
     }
-    int64_t n = (int64_t)*h->pin_sev.as<unsigned long long>();
     if (n == 0 && !h->coord_on) return SH_OK;
     if (h->pin_sev.ensure((size_t)std::max<int64_t>(n, 1) * 16)) return fail(h, SH_E_OOM, "pinned staging");
     if (n) hipMemcpyAsync(h->pin_sev.p, h->n_sev.p, (size_t)n * 16, hipMemcpyDeviceToHost, st);
@@ -1582,25 +1613,31 @@ static int pin_rd_ready(sh_handle* h) { return h->pin_rd.ensure(PR_COLS + sizeof
 // upload the nf_cols image through pinned memory (the caller synchronises the
 // stream before the slot is written again)
 static void nf_put_cols(sh_handle* h, const nf_cols& cols) {
+    // unchanged since the last upload (the common case per call): nothing to copy
+    if (h->cols_cached && !memcmp(&h->cols_last, &cols, sizeof(nf_cols))) return;
     memcpy(h->pin_rd.as<nf_cols>(PR_COLS), &cols, sizeof(nf_cols));
     hipMemcpyAsync(h->d_ncols.p, h->pin_rd.as<nf_cols>(PR_COLS), sizeof(nf_cols), hipMemcpyHostToDevice, h->stream);
+    h->cols_last = cols;
+    h->cols_cached = true;
 }
 
 // scan the per-index counts, place the records, append them to the host queue
 // (or to the caller's device buffers); returns the number of rows
 // (launch: the launch's tick, for the key-sharded rows' order tags)
+// nrec_known >= 0: the launch's record count, read back with its error word
 static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_seq, int64_t* d_vals, int64_t cap,
-                    uint64_t launch) {
+                    uint64_t launch, int64_t nrec_known) {
     HpScope hp_(h, 4);
     hipStream_t st = h->stream;
     if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
-    hipMemcpyAsync(h->pin_rd.as<void>(PR_NREC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
+    if (nrec_known < 0) hipMemcpyAsync(h->pin_rd.as<void>(PR_NREC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
     if (shd_exclusive_scan(h->w_cnt.as<uint32_t>(), h->w_off.as<uint32_t>(), n_idx, h->w_scan.as<uint32_t>(), st))
         return fail(h, SH_E_HIP, "scan");
     hipMemcpyAsync(h->pin_rd.as<void>(PR_LOFF), h->w_off.as<uint32_t>() + (n_idx - 1), 4, hipMemcpyDeviceToHost, st);
     hipMemcpyAsync(h->pin_rd.as<void>(PR_LCNT), h->w_cnt.as<uint32_t>() + (n_idx - 1), 4, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error before placement");
-    const unsigned long long nrec = *h->pin_rd.as<unsigned long long>(PR_NREC);
+    const unsigned long long nrec =
+        nrec_known >= 0 ? (unsigned long long)nrec_known : *h->pin_rd.as<unsigned long long>(PR_NREC);
     const uint32_t last_off = *h->pin_rd.as<uint32_t>(PR_LOFF), last_cnt = *h->pin_rd.as<uint32_t>(PR_LCNT);
     const int64_t total = (int64_t)last_off + last_cnt;
     *rows_out = total;
@@ -1809,8 +1846,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
                      0, st);
         }
         hipMemsetAsync(h->w_cnt.p, 0, n_idx * 4, st);
-        hipMemsetAsync(h->n_ctr.p, 0, 8, st);
-        hipMemsetAsync(h->n_err.p, 0, 4, st);
+        nf_ctl_zero(h);
         if (nf_lst_ready(h)) return fail(h, SH_E_OOM, "list values");
         if (h->has_lists && (cols.lst != h->n_lst.as<uint64_t>() || cols.lst_cap != (uint64_t)h->lst_cap)) {
             cols.lst = h->n_lst.as<uint64_t>();
@@ -1819,7 +1855,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
             nf_put_cols(h, cols);
         }
         if (h->sm_on) {
-            if (nf_sev_ready(h, n)) return fail(h, SH_E_OOM, "scheduler history");
+            if (nf_sev_ready(h, n, false)) return fail(h, SH_E_OOM, "scheduler history");
             if (cols.sev != h->n_sev.as<uint64_t>() || cols.sev_cap != (uint64_t)h->sev_cap) {
                 // the buffer moved: refresh the column image
                 cols = nf_store_cols(h);
@@ -1843,15 +1879,15 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
                            seg_list, nseg, skeys, nkeys, max_seg, h->tick, h->clock, &em, st))
             return fail(h, SH_E_HIP, "k_nfa_run launch failed");
         hipEventRecord(h->ev[2], st);
-        hipMemcpyAsync(h->pin_rd.as<void>(PR_ERR), h->n_err.p, 4, hipMemcpyDeviceToHost, st);
-        nf_sev_count_async(h);
+        nf_ctl_read(h);
         if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_run");
-        const unsigned err = *h->pin_rd.as<unsigned>(PR_ERR);
+        const unsigned err = nf_ctl_err(h);
         if (!err) {
             h->tick++;
+            const int64_t nrec = nf_ctl_nrec(h);
             int src = nf_sev_apply(h, true);
             if (src) return src;
-            int rc = nf_place(h, n_idx, n_rows, d_seq, d_vals, cap, h->tick - 1);
+            int rc = nf_place(h, n_idx, n_rows, d_seq, d_vals, cap, h->tick - 1, nrec);
             hipEventRecord(h->ev[3], st);
             hipStreamSynchronize(st);
             hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
@@ -2074,8 +2110,7 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
                 if (attempt > 64) return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
                 const size_t kw = (size_t)h->T->key_words;
                 hipMemsetAsync(h->w_cnt.p, 0, (size_t)n_idx * 4, st);
-                hipMemsetAsync(h->n_ctr.p, 0, 8, st);
-                hipMemsetAsync(h->n_err.p, 0, 4, st);
+                nf_ctl_zero(h);
                 {
                     const void* lst0 = h->n_lst.p;
                     if (nf_lst_ready(h)) return fail(h, SH_E_OOM, "list values");
@@ -2084,7 +2119,7 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
                 if (h->sm_on) {
                     const void* sev0 = h->n_sev.p;
                     const int64_t cap0 = h->sev_cap;
-                    if (nf_sev_ready(h, ns)) return fail(h, SH_E_OOM, "scheduler history");
+                    if (nf_sev_ready(h, ns, false)) return fail(h, SH_E_OOM, "scheduler history");
                     if (sev0 != h->n_sev.p || cap0 != h->sev_cap || attempt > 0) nf_put_cols(h, nf_store_cols(h));
                 } else if (attempt > 0) {
                     nf_put_cols(h, nf_store_cols(h));
@@ -2097,10 +2132,9 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
                 nfd_timer(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), q, p,
                           h->n_sel.as<int32_t>(), ns, now, h->tick, h->clock, h->seq_next, &em, st,
                           h->coord_on ? h->n_gpos.as<uint32_t>() : nullptr);
-                hipMemcpyAsync(h->pin_rd.as<void>(PR_ERR), h->n_err.p, 4, hipMemcpyDeviceToHost, st);
-                nf_sev_count_async(h);
+                nf_ctl_read(h);
                 if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_timer");
-                unsigned err = *h->pin_rd.as<unsigned>(PR_ERR);
+                unsigned err = nf_ctl_err(h);
                 if (!err) {
                     counted = true;
                     break;
@@ -2130,7 +2164,7 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
                 if (src) return src;
             }
             int64_t rows = 0;
-            int rc = nf_place(h, n_idx, &rows, nullptr, nullptr, 0, h->tick - 1);
+            int rc = nf_place(h, n_idx, &rows, nullptr, nullptr, 0, h->tick - 1, counted ? nf_ctl_nrec(h) : -1);
             if (rc) return rc;
         }
     }
@@ -2144,6 +2178,7 @@ static int nf_start(sh_handle* h) {
     if (nf_ensure_keys(h, 1)) return fail(h, SH_E_OOM, "key state");
     const nf_cols cols = nf_store_cols(h);
     hipMemcpyAsync(h->d_ncols.p, &cols, sizeof(nf_cols), hipMemcpyHostToDevice, h->stream);
+    h->cols_cached = false;
     hipMemsetAsync(h->n_err.p, 0, 4, h->stream);
     if (nf_ensure_recs(h, 4096)) return fail(h, SH_E_OOM, "emission");
     nfd_emit em = nf_emit(h);
