@@ -1808,11 +1808,11 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
                   type_width(h->stream_types[0][A]) == 4 && Q.s3_a3 == A && Q.s3_e1a == A && Q.s3_la == A &&
                   Q.s3_t3 == ty && Q.s3_e1t == ty && Q.s3_lt == ty && !cols.nul[0][A];
         for (int o = 0; o < Q.n_out && ok; o++) ok = Q.s3_out_attr[o] == A && Q.s3_out_type[o] == ty;
-        static const bool staged = !(getenv("SH_S3_STAGED") && getenv("SH_S3_STAGED")[0] == '0');
+        const bool staged = !(getenv("SH_S3_STAGED") && getenv("SH_S3_STAGED")[0] == '0');
         if (ok && staged) s3_col = alias == A ? (const void*)skeys : (const void*)cols.col[0][A];
     }
     // its records in the compact form (SH_S3_COMPACT=0: the generic records, for A/B)
-    static const bool s3_compact_on = !(getenv("SH_S3_COMPACT") && getenv("SH_S3_COMPACT")[0] == '0');
+    const bool s3_compact_on = !(getenv("SH_S3_COMPACT") && getenv("SH_S3_COMPACT")[0] == '0');
     h->s3_compact = s3_col && d_seq && s3_compact_on;
     h->s3_type = h->T->q[0].s3_t2;
     h->s3_seq_base = B.seq_base;

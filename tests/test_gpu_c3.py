@@ -90,3 +90,31 @@ def test_c3_18bit_keys_vs_restatement(engine, monkeypatch):
     eseq, evals = c3_expected(ts, k, p)
     assert len(gseq) == len(eseq) > 0
     assert np.array_equal(gseq, eseq) and np.array_equal(gvals, evals)
+
+
+@pytest.mark.parametrize("variant", ["null_keys", "all_null", "hot_key", "generic_records", "unstaged"])
+def test_c3_seq3_edge_cases_vs_oracle(variant, monkeypatch):
+    """k_seq3s's edges: null-key events (the run after the last segment has no
+    records), no keyed event at all, one hot key walked over many rounds while its
+    workgroup's other lanes idle; and the A/B forms (generic records, the one-lane-
+    per-key k_seq3)"""
+    n, nk = 200_000, 2_000
+    ts, k, p, v = synth.stock_stream(n, nk, 1000, config_index=3)
+    k = k.copy()
+    rng = np.random.default_rng(11)
+    if variant == "null_keys":
+        k[rng.random(n) < 0.1] = -1
+    elif variant == "all_null":
+        k[:] = -1
+    elif variant == "hot_key":
+        k[rng.random(n) < 0.3] = 7
+    elif variant == "generic_records":
+        monkeypatch.setenv("SH_S3_COMPACT", "0")
+    else:
+        monkeypatch.setenv("SH_S3_STAGED", "0")
+    seq, _, vals, _ = run_columns_oracle(compiler.compile_app(synth.C3_QUERY), ts, [k, p, v], k)
+    gseq, gvals, st = _gpu(synth.C3_QUERY, ts, [k, p, v], k, nk)
+    assert st == 1
+    assert len(gseq) == len(seq)
+    assert (len(seq) == 0) == (variant == "all_null")
+    assert np.array_equal(gseq, seq.astype(np.int64)) and np.array_equal(gvals, vals)
