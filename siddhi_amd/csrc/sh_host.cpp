@@ -1807,7 +1807,9 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
         bool ok = (ty == SH_T_FLOAT || ty == SH_T_INT) && A >= 0 && A < (int)h->stream_types[0].size() &&
                   type_width(h->stream_types[0][A]) == 4 && Q.s3_a3 == A && Q.s3_e1a == A && Q.s3_la == A &&
                   Q.s3_t3 == ty && Q.s3_e1t == ty && Q.s3_lt == ty && !cols.nul[0][A];
-        for (int o = 0; o < Q.n_out && ok; o++) ok = Q.s3_out_attr[o] == A && Q.s3_out_type[o] == ty;
+        // (count() reads no attribute)
+        for (int o = 0; o < Q.n_out && ok; o++)
+            ok = Q.out_agg[o] == SH_AGG_COUNT || (Q.s3_out_attr[o] == A && Q.s3_out_type[o] == ty);
         const bool staged = !(getenv("SH_S3_STAGED") && getenv("SH_S3_STAGED")[0] == '0');
         if (ok && staged) s3_col = alias == A ? (const void*)skeys : (const void*)cols.col[0][A];
     }
