@@ -21,7 +21,7 @@ struct sha_desc {
 #ifdef __cplusplus
 extern "C" {
 #endif
-int64_t sha_scratch_bytes(int64_t m);
+int64_t sha_scratch_bytes(int64_t m, int n_cols);
 // d_vals [m x n_out] raw rows in output order (d_seq the trigger sequence numbers,
 // d_query the emitting query or NULL): each listed column's argument values
 // become the running aggregate per (query, partition key of the trigger event

@@ -179,14 +179,14 @@ __global__ void __launch_bounds__(SHA_TPB) k_sha_prep(const uint64_t* __restrict
 }
 
 // ---------------------------------------------------------------- scans
-// the addend of sorted position p for column c (fixed point at 2^q for doubles)
-__device__ __forceinline__ sha_el sha_load(const int64_t* __restrict__ vals, int n_out, const uint32_t* __restrict__ idx,
-                                           int64_t p, const sha_col& c, int q) {
+// the addend of sorted position p for column c (fixed point at 2^q for doubles), from
+// the column's copy in sorted order (sv[p])
+__device__ __forceinline__ sha_el sha_load(const int64_t* __restrict__ sv, int64_t p, const sha_col& c, int q) {
     sha_el x;
     x.f = 0;
     x.c = 1;
     x.v = sha_zero();
-    const int64_t raw = vals[(int64_t)idx[p] * n_out + c.col];
+    const int64_t raw = sv[p];
     if (c.kind == SH_AGG_COUNT) return x;
     if (!sha_fp(c)) {
         // long arithmetic (sum of int / long): the low 64 bits wrap like Java's long
@@ -252,9 +252,8 @@ __device__ __forceinline__ sha_el sha_block_scan(sha_el x, sha_el* wsum) {
 
 // per tile: inclusive segmented scan (sorted order) into out[], the tile's
 // aggregate and the tile offset of its first segment start (SHA_TILE: none)
-__global__ void __launch_bounds__(SHA_TPB) k_sha_tile(const int64_t* __restrict__ vals, int n_out,
-                                                      const uint32_t* __restrict__ sseg,
-                                                      const uint32_t* __restrict__ idx, int64_t m, sha_col c, int q,
+__global__ void __launch_bounds__(SHA_TPB) k_sha_tile(const int64_t* __restrict__ scol,
+                                                      const uint32_t* __restrict__ sseg, int64_t m, sha_col c, int q,
                                                       sha_i128* __restrict__ out_v, int64_t* __restrict__ out_c,
                                                       sha_el* __restrict__ tiles, uint32_t* __restrict__ first_head) {
     __shared__ sha_el wsum[SHA_TPB / 64];
@@ -274,7 +273,7 @@ __global__ void __launch_bounds__(SHA_TPB) k_sha_tile(const int64_t* __restrict_
         const int64_t p = p0 + j;
         sha_el x;
         if (p < m) {
-            x = sha_load(vals, n_out, idx, p, c, q);
+            x = sha_load(scol, p, c, q);
             x.f = (p == 0 || sseg[p] != sseg[p - 1]) ? 1u : 0u;
             if (x.f && myfh == SHA_TILE) myfh = (uint32_t)(p - t0);
         } else {
@@ -357,8 +356,7 @@ __global__ void __launch_bounds__(SHA_CARRY_TPB) k_sha_carry(sha_el* __restrict_
 }
 
 // carry-in, exactness, conversion, write into the row
-__global__ void __launch_bounds__(SHA_TPB) k_sha_out(int64_t* __restrict__ vals, int n_out,
-                                                     const uint32_t* __restrict__ idx, int64_t m, sha_col c, int q,
+__global__ void __launch_bounds__(SHA_TPB) k_sha_out(int64_t* __restrict__ scol, int64_t m, sha_col c, int q,
                                                      const sha_i128* __restrict__ in_v, const int64_t* __restrict__ in_c,
                                                      const sha_el* __restrict__ tiles,
                                                      const uint32_t* __restrict__ first_head, int32_t* __restrict__ flag) {
@@ -408,17 +406,37 @@ __global__ void __launch_bounds__(SHA_TPB) k_sha_out(int64_t* __restrict__ vals,
         }
         out = c.kind == SH_AGG_AVG ? __double_as_longlong(d / (double)cnt) : __double_as_longlong(d);
     }
-    vals[(int64_t)idx[p] * n_out + c.col] = out;
+    scol[p] = out;
+}
+
+// the aggregate columns into sorted order, one row read for all of them (SoA: column k
+// at sc + k * m), and back into the rows once every column is done
+__global__ void __launch_bounds__(SHA_TPB) k_sha_gather(const int64_t* __restrict__ vals, int n_out,
+                                                        const uint32_t* __restrict__ idx, int64_t m, sha_desc D,
+                                                        int64_t* __restrict__ sc) {
+    const int64_t p = (int64_t)blockIdx.x * SHA_TPB + threadIdx.x;
+    if (p >= m) return;
+    const int64_t* row = vals + (int64_t)idx[p] * n_out;
+    for (int k = 0; k < D.n_cols; k++) sc[(int64_t)k * m + p] = row[D.c[k].col];
+}
+
+__global__ void __launch_bounds__(SHA_TPB) k_sha_scatter(int64_t* __restrict__ vals, int n_out,
+                                                         const uint32_t* __restrict__ idx, int64_t m, sha_desc D,
+                                                         const int64_t* __restrict__ sc) {
+    const int64_t p = (int64_t)blockIdx.x * SHA_TPB + threadIdx.x;
+    if (p >= m) return;
+    int64_t* row = vals + (int64_t)idx[p] * n_out;
+    for (int k = 0; k < D.n_cols; k++) row[D.c[k].col] = sc[(int64_t)k * m + p];
 }
 
 // ---------------------------------------------------------------- host
-extern "C" int64_t sha_scratch_bytes(int64_t m) {
+extern "C" int64_t sha_scratch_bytes(int64_t m, int n_cols) {
     const int64_t nt = (m + SHA_TILE - 1) / SHA_TILE;
     const int64_t rt = (m + 4095) / 4096;
     // seg, idx, 2 x 2 sort buffers, 128-bit values, counts, tiles, first heads,
-    // sort histogram, scan temporaries, exponent ranges
+    // sort histogram, scan temporaries, exponent ranges, the sorted column copies
     return m * 4 * 6 + m * 16 + m * 8 + nt * (int64_t)sizeof(sha_el) + nt * 4 + 256 * rt * 4 +
-           (int64_t)shd_scan_tmp_words(256 * rt) * 4 + 4096;
+           (int64_t)shd_scan_tmp_words(256 * rt) * 4 + 4096 + (int64_t)(n_cols < 1 ? 1 : n_cols) * m * 8 + 256;
 }
 
 static int sha_ok() { return hipGetLastError() == hipSuccess ? 0 : -3; }
@@ -452,6 +470,7 @@ extern "C" int sha_running(const uint64_t* d_seq, int64_t* d_vals, int32_t n_out
     uint32_t* hist = (uint32_t*)take(256 * rt * 4);
     uint32_t* stmp = (uint32_t*)take((int64_t)shd_scan_tmp_words(256 * rt) * 4);
     int32_t* range = (int32_t*)take(4 * 3 * SHA_MAX_COLS + 64);
+    int64_t* scol = (int64_t*)take((int64_t)D->n_cols * m * 8);
     int32_t h_range[3 * SHA_MAX_COLS];
     for (int k = 0; k < SHA_MAX_COLS; k++) {
         h_range[3 * k] = 1 << 30;
@@ -471,6 +490,7 @@ extern "C" int sha_running(const uint64_t* d_seq, int64_t* d_vals, int32_t n_out
     uint32_t* kbuf[2] = {kb0, kb1};
     uint32_t* vbuf[2] = {vb0, vb1};
     if (bits > 0 && shd_sort_pairs(seg, idx, m, bits, kbuf, vbuf, hist, stmp, stream, &sseg, &sidx)) return -3;
+    hipLaunchKernelGGL(k_sha_gather, dim3(g), dim3(SHA_TPB), 0, st, (const int64_t*)d_vals, n_out, sidx, m, *D, scol);
     hipMemcpyAsync(h_range, range, sizeof(h_range), hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return -3;
     for (int k = 0; k < D->n_cols; k++) {
@@ -485,14 +505,17 @@ extern "C" int sha_running(const uint64_t* d_seq, int64_t* d_vals, int32_t n_out
                 q = lo;
             }
         }
-        hipLaunchKernelGGL(k_sha_tile, dim3((unsigned)nt), dim3(SHA_TPB), 0, st, (const int64_t*)d_vals, n_out, sseg,
-                           sidx, m, c, q, sv, sc, tiles, fh);
+        int64_t* colk = scol + (int64_t)k * m;
+        hipLaunchKernelGGL(k_sha_tile, dim3((unsigned)nt), dim3(SHA_TPB), 0, st, (const int64_t*)colk, sseg, m, c, q,
+                           sv, sc, tiles, fh);
         hipLaunchKernelGGL(k_sha_carry, dim3(1), dim3(SHA_CARRY_TPB), 0, st, tiles, nt);
-        hipLaunchKernelGGL(k_sha_out, dim3(g), dim3(SHA_TPB), 0, st, d_vals, n_out, sidx, m, c, q,
-                           (const sha_i128*)sv, (const int64_t*)sc, (const sha_el*)tiles, (const uint32_t*)fh,
-                           range + 3 * SHA_MAX_COLS);
+        hipLaunchKernelGGL(k_sha_out, dim3(g), dim3(SHA_TPB), 0, st, colk, m, c, q, (const sha_i128*)sv,
+                           (const int64_t*)sc, (const sha_el*)tiles, (const uint32_t*)fh, range + 3 * SHA_MAX_COLS);
         if (sha_ok()) return -3;
     }
+    hipLaunchKernelGGL(k_sha_scatter, dim3(g), dim3(SHA_TPB), 0, st, d_vals, n_out, sidx, m, *D,
+                       (const int64_t*)scol);
+    if (sha_ok()) return -3;
     int32_t inexact = 0;
     hipMemcpyAsync(&inexact, range + 3 * SHA_MAX_COLS, 4, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return -3;

@@ -2845,7 +2845,7 @@ static int agg_post(sh_handle* h, sh_device_run* run, int32_t nkeys, const int32
             D.n_cols++;
         }
     if (D.n_cols == 0) return SH_OK;
-    if (h->a_scratch.ensure((size_t)sha_scratch_bytes(m))) return fail(h, SH_E_OOM, "aggregate scratch");
+    if (h->a_scratch.ensure((size_t)sha_scratch_bytes(m, D.n_cols))) return fail(h, SH_E_OOM, "aggregate scratch");
     hipEventRecord(h->ev[4], h->stream);
     const int rc = sha_running(run->d_out_seq, run->d_out_values, n_out, m, d_query, n_query,
                                h->partitioned ? run->d_keys : nullptr, h->partitioned ? nkeys : 1, 0, &D,
