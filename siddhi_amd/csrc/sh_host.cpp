@@ -467,6 +467,7 @@ struct sh_handle {
     shr_table r_tab{};
     DevBuf rd_rules, rd_ixval, rd_ixstart, rd_ixrule, rd_free, rd_tab;
     DevBuf rd_img;   // the rule set's LDS image (shr_img), when it fits
+    DevBuf r_tsr, v_ts32, v_sts32, v_mid_ts32;  // 32-bit timestamp offsets of a rule run (range, arrival, sorted, mid)
     shr_img r_img{};
     DevBuf r_rec, r_keys, r_g, r_sk, r_sv, r_hist, r_scan, r_run;
     // ---- bucketed window engine (sh_bucket.hip + shb_match): 0 untried, 1 loaded, <0 unavailable
@@ -1031,6 +1032,7 @@ void sh_destroy(sh_handle* h) {
         DevBuf* nbufs[] = {&h->d_T, &h->d_T_old, &h->d_ncols, &h->n_kstate, &h->n_kstate2, &h->n_save, &h->n_recs,
                            &h->n_ctr, &h->n_err, &h->n_cand, &h->n_sel, &h->n_bid, &h->w_oq,
                            &h->rd_rules, &h->rd_ixval, &h->rd_ixstart, &h->rd_ixrule, &h->rd_free, &h->rd_tab, &h->rd_img,
+                           &h->r_tsr, &h->v_ts32, &h->v_sts32, &h->v_mid_ts32,
                            &h->n_ctl,
                            &h->r_rec, &h->r_keys, &h->r_g, &h->r_sk, &h->r_sv, &h->r_hist, &h->r_scan, &h->r_run};
         for (DevBuf* b : nbufs) b->release();
@@ -2538,15 +2540,36 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
     shd_payload carry;
     void* mid[8] = {nullptr};
     int alias = -1;
-    if (sorted && carry_setup(h, run, &carry, mid, &alias)) return fail(h, SH_E_OOM, "rule workspace");
     hipEventRecord(h->ev[0], st);
+    // timestamps travel through the segment as 32-bit offsets from the run's first
+    // time when its range fits (4 bytes fewer per event and pass); SH_RULES_TS64=1: int64
+    int64_t tlo = 0, thi = 0;
+    bool ts32 = false;
+    if (sorted && !getenv("SH_RULES_TS64")) {
+        if (h->r_tsr.ensure_fresh(64)) return fail(h, SH_E_OOM, "rule workspace");
+        if (shr_ts_range(run->d_ts, n, &tlo, &thi, h->r_tsr.p, st)) return fail(h, SH_E_HIP, "timestamp range");
+        ts32 = thi >= tlo && (uint64_t)(thi - tlo) <= 0xFFFFFFFFull;
+    }
+    if (sorted && carry_setup(h, run, &carry, mid, &alias, false, !ts32)) return fail(h, SH_E_OOM, "rule workspace");
+    if (ts32) {
+        if (h->v_ts32.ensure_fresh((size_t)n * 4) || h->v_sts32.ensure_fresh((size_t)n * 4) ||
+            h->v_mid_ts32.ensure_fresh((size_t)n * 4))
+            return fail(h, SH_E_OOM, "rule workspace");
+        if (shr_ts_to32(run->d_ts, n, tlo, h->v_ts32.as<uint32_t>(), st)) return fail(h, SH_E_HIP, "timestamps");
+        carry.src[carry.n] = h->v_ts32.p;
+        carry.dst[carry.n] = h->v_sts32.p;
+        carry.width[carry.n] = 4;
+        mid[carry.n] = h->v_mid_ts32.p;
+        carry.n++;
+    }
+    const uint32_t* sts32 = ts32 ? h->v_sts32.as<uint32_t>() : nullptr;
     shd_segment_ws ws = seg_ws(h, n);
     const uint32_t* perm = nullptr;
     const uint32_t* skeys = nullptr;
     if (shd_segment_payload(&B, nkeys, &ws, st, &perm, &skeys, sorted ? &carry : nullptr, mid, 0, 0))
         return fail(h, SH_E_HIP, "segment launch failed");
     hipEventRecord(h->ev[1], st);
-    const int64_t* sts = sorted ? h->v_sts.as<int64_t>() : run->d_ts;
+    const int64_t* sts = ts32 ? nullptr : (sorted ? h->v_sts.as<int64_t>() : run->d_ts);
     shd_cols sc;
     memset(&sc, 0, sizeof(sc));
     for (int a = 0; a < na; a++) sc.col[0][a] = sorted ? (const void*)h->v_scol[a].p : run->d_cols[a];
@@ -2559,7 +2582,7 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
     uint32_t* off = h->w_off.as<uint32_t>();
     hipMemsetAsync(h->v_flag.p, 0, 4, st);
     if (shr_count(dT, sts, skeys, n, sentinel, dC, cnt, h->v_flag.as<int32_t>(), st,
-                  h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr, &h->r_img) ||
+                  h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr, &h->r_img, sts32, tlo) ||
         shd_exclusive_scan(cnt, off, n, h->w_scan.as<uint32_t>(), st))
         return fail(h, SH_E_HIP, "rule scan launch failed");
     uint32_t lo = 0, lc = 0;
@@ -2584,7 +2607,7 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
         uint32_t* rec_q = rec_p + m;
         uint32_t* rec_r = rec_q + m;
         if (shr_write(dT, sts, skeys, n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, st,
-                      h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr, &h->r_img))
+                      h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr, &h->r_img, sts32, tlo))
             return fail(h, SH_E_HIP, "rule write launch failed");
         // PartitionStreamReceiver runs inside each send() call
         const int64_t batch = run->batch_events > 0 ? run->batch_events : 0;
@@ -2654,7 +2677,7 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
             }
         }
         if (shr_place(dT, order, m, rec_p, rec_q, rec_r, perm, sts, dC, 0, std::max(1, h->n_out), run->d_out_seq,
-                      run->d_out_query, nullptr, run->d_out_values, st))
+                      run->d_out_query, nullptr, run->d_out_values, st, sts32, tlo))
             return fail(h, SH_E_HIP, "rule placement launch failed");
     } else {
         hipEventRecord(h->ev[2], st);

@@ -50,13 +50,15 @@ extern "C" {
 #endif
 // matches opened at every key-segment position (cnt[p]); flag := 1 when a key's
 // timestamps decrease (the window reduction does not hold)
+// sts32 (optional): the sorted timestamps as 32-bit offsets from tbase (sts unused)
 int shr_count(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
               const shd_cols* dC, uint32_t* cnt, int32_t* flag, void* stream, const uint8_t* img = nullptr,
-              const shr_img* I = nullptr);
+              const shr_img* I = nullptr, const uint32_t* sts32 = nullptr, int64_t tbase = 0);
 // the same scan, writing (opening, consuming, rule) records at off[p]
 int shr_write(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
               const shd_cols* dC, const uint32_t* cnt, const uint32_t* off, uint32_t* rec_p, uint32_t* rec_q,
-              uint32_t* rec_r, void* stream, const uint8_t* img = nullptr, const shr_img* I = nullptr);
+              uint32_t* rec_r, void* stream, const uint8_t* img = nullptr, const shr_img* I = nullptr,
+              const uint32_t* sts32 = nullptr, int64_t tbase = 0);
 // PartitionStreamReceiver runs of an arrival-order key array: flags[i] (run
 // start), rid[i] (exclusive scan of flags), rfirst[run] (first arrival index);
 // run_ids (may be NULL): the caller's run of every event (sh_device_run.d_run)
@@ -72,7 +74,11 @@ int shr_gather(const uint32_t* key, const uint32_t* order, int64_t m, uint32_t* 
 // ordered output rows from the sorted record order
 int shr_place(const shr_table* dT, const uint32_t* order, int64_t m, const uint32_t* rec_p, const uint32_t* rec_q,
               const uint32_t* rec_r, const uint32_t* perm, const int64_t* sts, const shd_cols* dC, uint64_t seq_base,
-              int n_out, uint64_t* out_seq, int32_t* out_query, int64_t* out_ts, int64_t* out_vals, void* stream);
+              int n_out, uint64_t* out_seq, int32_t* out_query, int64_t* out_ts, int64_t* out_vals, void* stream,
+              const uint32_t* sts32 = nullptr, int64_t tbase = 0);
+// the run's timestamp range (one read-back), and the 32-bit offsets from `base`
+int shr_ts_range(const int64_t* ts, int64_t n, int64_t* lo, int64_t* hi, void* scratch16, void* stream);
+int shr_ts_to32(const int64_t* ts, int64_t n, int64_t base, uint32_t* t32, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -28,12 +28,17 @@
 // sort of the records by (run, query, consuming event) -> k_rules_place.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdint>
+
 #include "../../include/sh_query.h"
 #include "sh_device.h"
 #include "sh_rules.h"
 #include "sh_vm.h"
 
 #define RTPB 256
+// a sorted timestamp: 32-bit offsets from tb when the run's range fits (s32), else int64
+#define SHR_TS(i) (s32 ? tb + (int64_t)s32[(i)] : sts[(i)])
 #define SHR_LDS_IX 2048  // index groups staged in LDS (24 KB)
 
 static unsigned rgrid(int64_t n) {
@@ -92,7 +97,8 @@ __global__ void __launch_bounds__(RTPB) k_rules_scan(const shr_table* __restrict
                                                      const shd_cols* __restrict__ C, uint32_t* __restrict__ cnt,
                                                      const uint32_t* __restrict__ off, uint32_t* __restrict__ rec_p,
                                                      uint32_t* __restrict__ rec_q, uint32_t* __restrict__ rec_r,
-                                                     int32_t* __restrict__ flag) {
+                                                     int32_t* __restrict__ flag, const uint32_t* __restrict__ s32,
+                                                     int64_t tb) {
     const int ix_attr = RT->ix_attr;
     const int n_ix = RT->n_ix;
     const uint32_t n_free = (uint32_t)RT->n_free;
@@ -111,8 +117,8 @@ __global__ void __launch_bounds__(RTPB) k_rules_scan(const shr_table* __restrict
         if (WRITE && cnt[p] == 0) continue;
         const uint32_t key = skeys ? skeys[p] : 0u;
         if (key == sentinel) continue;
-        const int64_t t0 = sts[p];
-        if (!WRITE && p > 0 && (!skeys || skeys[p - 1] == key) && t0 < sts[p - 1]) atomicExch(flag, 1);
+        const int64_t t0 = SHR_TS(p);
+        if (!WRITE && p > 0 && (!skeys || skeys[p - 1] == key) && t0 < SHR_TS(p - 1)) atomicExch(flag, 1);
         uint32_t lo = 0, hi = 0;
         if (ix_attr >= 0) {
             const int ty = RT->attr_type[ix_attr];
@@ -154,7 +160,7 @@ __global__ void __launch_bounds__(RTPB) k_rules_scan(const shr_table* __restrict
             const int64_t W = R->within;
             for (int64_t q = p + 1; q < n; q++) {
                 if (skeys && skeys[q] != key) break;
-                const int64_t d = sts[q] - t0;
+                const int64_t d = SHR_TS(q) - t0;
                 if (W >= 0 && (d < 0 ? -d : d) > W) break;  // expired before event q is matched
                 if (rule_terms(R->t[1], R->nt[1], (uint32_t)p, (uint32_t)q, C)) {
                     if (WRITE) {
@@ -226,7 +232,7 @@ __global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
     const shr_table* __restrict__ RT, const int64_t* __restrict__ sts, const uint32_t* __restrict__ skeys, int64_t n,
     uint32_t sentinel, const shd_cols* __restrict__ C, uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
     uint32_t* __restrict__ rec_p, uint32_t* __restrict__ rec_q, uint32_t* __restrict__ rec_r, int32_t* __restrict__ flag,
-    const uint8_t* __restrict__ img, shr_img I) {
+    const uint8_t* __restrict__ img, shr_img I, const uint32_t* __restrict__ s32, int64_t tb) {
     extern __shared__ uint4 s_img[];
     __shared__ const void* s_col[32];
     for (int i = threadIdx.x; i < I.bytes / 16; i += blockDim.x) s_img[i] = ((const uint4*)img)[i];
@@ -247,8 +253,8 @@ __global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
         if (WRITE && cnt[p] == 0) continue;
         const uint32_t key = skeys ? skeys[p] : 0u;
         if (key == sentinel) continue;
-        const int64_t t0 = sts[p];
-        if (!WRITE && p > 0 && (!skeys || skeys[p - 1] == key) && t0 < sts[p - 1]) atomicExch(flag, 1);
+        const int64_t t0 = SHR_TS(p);
+        if (!WRITE && p > 0 && (!skeys || skeys[p - 1] == key) && t0 < SHR_TS(p - 1)) atomicExch(flag, 1);
         uint32_t lo = 0, hi = 0;
         if (ix_attr >= 0) {
             const int64_t x = rule_ix_key(ix_ty, rule_attr(s_col, ix_attr, ix_ty, (uint32_t)p));
@@ -277,7 +283,7 @@ __global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
             const int64_t W = M.within;
             for (int64_t q = p + 1; q < n; q++) {
                 if (skeys && skeys[q] != key) break;
-                const int64_t d = sts[q] - t0;
+                const int64_t d = SHR_TS(q) - t0;
                 if (W >= 0 && (d < 0 ? -d : d) > W) break;  // expired before event q is matched
                 if (rule_terms_img(T1, M.nt1, (uint32_t)p, (uint32_t)q, s_col)) {
                     if (WRITE) {
@@ -297,7 +303,8 @@ __global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
 template <int WRITE>
 static int rules_scan_img(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
                           const shd_cols* dC, uint32_t* cnt, const uint32_t* off, uint32_t* rec_p, uint32_t* rec_q,
-                          uint32_t* rec_r, int32_t* flag, const uint8_t* img, const shr_img& I, hipStream_t st) {
+                          uint32_t* rec_r, int32_t* flag, const uint8_t* img, const shr_img& I, hipStream_t st,
+                          const uint32_t* s32, int64_t tb) {
     static int attr_set = 0;  // the dynamic LDS limit, raised once per instantiation
     if (!attr_set) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rules_scan_img<WRITE>),
@@ -311,7 +318,7 @@ static int rules_scan_img(const shr_table* dT, const int64_t* sts, const uint32_
     if (g > gmax) g = gmax;
     if (g < 1) g = 1;
     hipLaunchKernelGGL(k_rules_scan_img<WRITE>, dim3((unsigned)g), dim3(RTPB_IMG), (size_t)I.bytes, st, dT, sts, skeys,
-                       n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, flag, img, I);
+                       n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, flag, img, I, s32, tb);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -387,14 +394,15 @@ __global__ void k_rules_place(const shr_table* __restrict__ RT, const uint32_t* 
                               const uint32_t* __restrict__ rec_r, const uint32_t* __restrict__ perm,
                               const int64_t* __restrict__ sts, const shd_cols* __restrict__ C, uint64_t seq_base,
                               int n_out, uint64_t* __restrict__ out_seq, int32_t* __restrict__ out_query,
-                              int64_t* __restrict__ out_ts, int64_t* __restrict__ out_vals) {
+                              int64_t* __restrict__ out_ts, int64_t* __restrict__ out_vals,
+                              const uint32_t* __restrict__ s32, int64_t tb) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t id = order ? order[i] : (uint32_t)i;
         const uint32_t p = rec_p[id], q = rec_q[id];
         const shr_rule* R = RT->rules + rec_r[id];
         if (out_seq) out_seq[i] = seq_base + (perm ? perm[q] : q);
         if (out_query) out_query[i] = R->query;
-        if (out_ts) out_ts[i] = sts[q];
+        if (out_ts) out_ts[i] = SHR_TS(q);
         if (out_vals)
             for (int o = 0; o < n_out; o++) {
                 int64_t v = 0;
@@ -418,24 +426,25 @@ static unsigned sgrid(int64_t n) {
 
 extern "C" int shr_count(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
                          const shd_cols* dC, uint32_t* cnt, int32_t* flag, void* stream, const uint8_t* img,
-                         const shr_img* I) {
+                         const shr_img* I, const uint32_t* s32, int64_t tb) {
     if (img && I && I->bytes > 0)
         return rules_scan_img<0>(dT, sts, skeys, n, sentinel, dC, cnt, nullptr, nullptr, nullptr, nullptr, flag, img, *I,
-                                 (hipStream_t)stream);
+                                 (hipStream_t)stream, s32, tb);
     hipLaunchKernelGGL(k_rules_scan<0>, dim3(sgrid(n)), dim3(RTPB), 0, (hipStream_t)stream, dT, sts, skeys, n,
                        sentinel, dC, cnt, (const uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                       (uint32_t*)nullptr, flag);
+                       (uint32_t*)nullptr, flag, s32, tb);
     return rules_ok();
 }
 
 extern "C" int shr_write(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, int64_t n, uint32_t sentinel,
                          const shd_cols* dC, const uint32_t* cnt, const uint32_t* off, uint32_t* rec_p,
-                         uint32_t* rec_q, uint32_t* rec_r, void* stream, const uint8_t* img, const shr_img* I) {
+                         uint32_t* rec_q, uint32_t* rec_r, void* stream, const uint8_t* img, const shr_img* I,
+                         const uint32_t* s32, int64_t tb) {
     if (img && I && I->bytes > 0)
         return rules_scan_img<1>(dT, sts, skeys, n, sentinel, dC, (uint32_t*)cnt, off, rec_p, rec_q, rec_r, nullptr,
-                                 img, *I, (hipStream_t)stream);
+                                 img, *I, (hipStream_t)stream, s32, tb);
     hipLaunchKernelGGL(k_rules_scan<1>, dim3(sgrid(n)), dim3(RTPB), 0, (hipStream_t)stream, dT, sts, skeys, n,
-                       sentinel, dC, (uint32_t*)cnt, off, rec_p, rec_q, rec_r, (int32_t*)nullptr);
+                       sentinel, dC, (uint32_t*)cnt, off, rec_p, rec_q, rec_r, (int32_t*)nullptr, s32, tb);
     return rules_ok();
 }
 
@@ -467,8 +476,56 @@ extern "C" int shr_gather(const uint32_t* key, const uint32_t* order, int64_t m,
 extern "C" int shr_place(const shr_table* dT, const uint32_t* order, int64_t m, const uint32_t* rec_p,
                          const uint32_t* rec_q, const uint32_t* rec_r, const uint32_t* perm, const int64_t* sts,
                          const shd_cols* dC, uint64_t seq_base, int n_out, uint64_t* out_seq, int32_t* out_query,
-                         int64_t* out_ts, int64_t* out_vals, void* stream) {
+                         int64_t* out_ts, int64_t* out_vals, void* stream, const uint32_t* s32, int64_t tb) {
     hipLaunchKernelGGL(k_rules_place, dim3(rgrid(m)), dim3(RTPB), 0, (hipStream_t)stream, dT, order, m, rec_p, rec_q,
-                       rec_r, perm, sts, dC, seq_base, n_out, out_seq, out_query, out_ts, out_vals);
+                       rec_r, perm, sts, dC, seq_base, n_out, out_seq, out_query, out_ts, out_vals, s32, tb);
+    return rules_ok();
+}
+
+// the timestamps' range (min, max) of a run, for the 32-bit offsets
+__global__ void __launch_bounds__(256) k_ts_range(const int64_t* __restrict__ ts, int64_t n,
+                                                  unsigned long long* __restrict__ mm) {
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = ts[i];
+        lo = t < lo ? t : lo;
+        hi = t > hi ? t : hi;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t l2 = __shfl_xor(lo, o), h2 = __shfl_xor(hi, o);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    // order-preserving unsigned form of the signed values
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&mm[0], (unsigned long long)lo ^ 0x8000000000000000ull);
+        atomicMax(&mm[1], (unsigned long long)hi ^ 0x8000000000000000ull);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ts_to32(const int64_t* __restrict__ ts, int64_t n, int64_t base,
+                                                 uint32_t* __restrict__ t32) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        t32[i] = (uint32_t)(ts[i] - base);
+}
+
+extern "C" int shr_ts_range(const int64_t* ts, int64_t n, int64_t* lo, int64_t* hi, void* scratch, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    unsigned long long init[2] = {~0ull, 0ull};
+    hipMemcpyAsync(scratch, init, 16, hipMemcpyHostToDevice, st);
+    const unsigned g = n > 0 ? (unsigned)std::min<int64_t>((n + 255) / 256, 4096) : 1u;
+    hipLaunchKernelGGL(k_ts_range, dim3(g), dim3(256), 0, st, ts, n, (unsigned long long*)scratch);
+    unsigned long long out[2];
+    hipMemcpyAsync(out, scratch, 16, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return -3;
+    *lo = (int64_t)(out[0] ^ 0x8000000000000000ull);
+    *hi = (int64_t)(out[1] ^ 0x8000000000000000ull);
+    return 0;
+}
+
+extern "C" int shr_ts_to32(const int64_t* ts, int64_t n, int64_t base, uint32_t* t32, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_ts_to32, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 65536)), dim3(256), 0,
+                       (hipStream_t)stream, ts, n, base, t32);
     return rules_ok();
 }
