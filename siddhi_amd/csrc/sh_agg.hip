@@ -27,10 +27,11 @@
 //
 // Pipeline: k_sha_prep (segment id = query * nkeys + key of the trigger event,
 // exponent range per column) -> stable radix sort of (segment, row) ->
-// per column: k_sha_tile (segmented inclusive scan of 2,048-row tiles in
+// k_sha_gather (every aggregate column of a row into sorted order, one row read)
+// -> per column: k_sha_tile (segmented inclusive scan of 2,048-row tiles in
 // registers + LDS) -> k_sha_carry (one workgroup: segmented scan of the tile
-// aggregates) -> k_sha_out (carry-in, exactness check, double conversion,
-// write into the row).
+// aggregates) -> k_sha_out (carry-in, exactness check, double conversion)
+// -> k_sha_scatter (every column back into its row, one row write).
 #include <hip/hip_runtime.h>
 #include <string.h>
 
