@@ -2541,11 +2541,13 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
     void* mid[8] = {nullptr};
     int alias = -1;
     hipEventRecord(h->ev[0], st);
-    // timestamps travel through the segment as 32-bit offsets from the run's first
-    // time when its range fits (4 bytes fewer per event and pass); SH_RULES_TS64=1: int64
+    // SH_RULES_TS32=1: timestamps travel through the segment as 32-bit offsets from
+    // the run's first time when its range fits (4 bytes fewer per event and pass).
+    // Off by default: on C5 the three passes gained 0.35 ms, the range and
+    // conversion passes cost 0.66 ms (profiles/r3_c5_ts32_ab.txt)
     int64_t tlo = 0, thi = 0;
     bool ts32 = false;
-    if (sorted && !getenv("SH_RULES_TS64")) {
+    if (sorted && getenv("SH_RULES_TS32") && getenv("SH_RULES_TS32")[0] == '1') {
         if (h->r_tsr.ensure_fresh(64)) return fail(h, SH_E_OOM, "rule workspace");
         if (shr_ts_range(run->d_ts, n, &tlo, &thi, h->r_tsr.p, st)) return fail(h, SH_E_HIP, "timestamp range");
         ts32 = thi >= tlo && (uint64_t)(thi - tlo) <= 0xFFFFFFFFull;
