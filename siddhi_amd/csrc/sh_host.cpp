@@ -829,44 +829,53 @@ static int upload_rules(sh_handle* h) {
             img.resize(at + bytes);
             return at;
         };
-        size_t nterms = 0;
-        for (const shr_rule& r : h->r_rules) nterms += (size_t)r.nt[0] + r.nt[1];
+        size_t nt0 = 0, nt1 = 0;
+        for (const shr_rule& r : h->r_rules) {
+            nt0 += (size_t)r.nt[0];
+            nt1 += (size_t)r.nt[1];
+        }
         const size_t o_ixv = sect(8 * h->r_ixval.size());
         const size_t o_ixs = sect(4 * h->r_ixstart.size());
         const size_t o_ixr = sect(4 * h->r_ixrule.size());
         const size_t o_fr = sect(4 * h->r_free.size());
         const size_t o_meta = sect(sizeof(shr_meta) * nr);
-        const size_t o_terms = sect(sizeof(shp_term) * nterms);
+        const size_t o_t1 = sect(sizeof(shp_term) * nt1);
+        const size_t lds = (img.size() + 15) & ~(size_t)15;
+        const size_t o_t0 = sect(sizeof(shp_term) * nt0);
         img.resize((img.size() + 15) & ~(size_t)15);
         static const bool img_on = !(getenv("SH_RULES_IMG") && getenv("SH_RULES_IMG")[0] == '0');
-        if (img_on && img.size() <= SHR_IMG_MAX && nterms < 65536) {
+        if (img_on && lds <= SHR_IMG_MAX && nt0 < 65536 && nt1 < 65536) {
             if (!h->r_ixval.empty()) memcpy(&img[o_ixv], h->r_ixval.data(), 8 * h->r_ixval.size());
             memcpy(&img[o_ixs], h->r_ixstart.data(), 4 * h->r_ixstart.size());
             if (!h->r_ixrule.empty()) memcpy(&img[o_ixr], h->r_ixrule.data(), 4 * h->r_ixrule.size());
             if (!h->r_free.empty()) memcpy(&img[o_fr], h->r_free.data(), 4 * h->r_free.size());
-            size_t tk = 0;
+            size_t k0 = 0, k1 = 0;
             for (size_t i = 0; i < nr; i++) {
                 const shr_rule& r = h->r_rules[i];
                 shr_meta m;
                 memset(&m, 0, sizeof(m));
                 m.within = r.within;
-                m.toff = (uint16_t)tk;
+                m.toff0 = (uint16_t)k0;
+                m.toff1 = (uint16_t)k1;
                 m.nt0 = (uint8_t)r.nt[0];
                 m.nt1 = (uint8_t)r.nt[1];
                 memcpy(&img[o_meta + i * sizeof(shr_meta)], &m, sizeof(m));
-                for (int k = 0; k < 2; k++)
-                    for (int t = 0; t < r.nt[k]; t++, tk++)
-                        memcpy(&img[o_terms + tk * sizeof(shp_term)], &r.t[k][t], sizeof(shp_term));
+                for (int t = 0; t < r.nt[0]; t++, k0++)
+                    memcpy(&img[o_t0 + k0 * sizeof(shp_term)], &r.t[0][t], sizeof(shp_term));
+                for (int t = 0; t < r.nt[1]; t++, k1++)
+                    memcpy(&img[o_t1 + k1 * sizeof(shp_term)], &r.t[1][t], sizeof(shp_term));
             }
             if (h->rd_img.ensure(img.size())) return fail(h, SH_E_OOM, "hipMalloc failed");
             hipMemcpy(h->rd_img.p, img.data(), img.size(), hipMemcpyHostToDevice);
             h->r_img.bytes = (int32_t)img.size();
+            h->r_img.lds = (int32_t)lds;
             h->r_img.off_ixv = (int32_t)o_ixv;
             h->r_img.off_ixs = (int32_t)o_ixs;
             h->r_img.off_ixr = (int32_t)o_ixr;
             h->r_img.off_free = (int32_t)o_fr;
             h->r_img.off_meta = (int32_t)o_meta;
-            h->r_img.off_terms = (int32_t)o_terms;
+            h->r_img.off_terms1 = (int32_t)o_t1;
+            h->r_img.off_terms0 = (int32_t)o_t0;
         }
     }
     shr_table t = h->r_tab;

@@ -35,13 +35,17 @@ struct shr_table {
 // conjunct, per rule its window and term range, and every term
 struct shr_meta {
     int64_t within;
-    uint16_t toff;                      // first term (f1's, then f2's)
+    uint16_t toff0, toff1;              // first term of f1 (global part), of f2 (LDS part)
     uint8_t nt0, nt1;
-    uint32_t pad;
+    uint16_t pad;
 };
+// the image's first `lds` bytes (index, rule ids, metas, f2's terms: read per walk
+// step) go to LDS; f1's terms (read once per candidate rule) stay in global memory,
+// so two 1024-thread workgroups fit a CU
 struct shr_img {
     int32_t bytes;                      // image size (multiple of 16), 0: no image
-    int32_t off_ixv, off_ixs, off_ixr, off_free, off_meta, off_terms, pad;
+    int32_t lds;                        // bytes staged in LDS (multiple of 16)
+    int32_t off_ixv, off_ixs, off_ixr, off_free, off_meta, off_terms1, off_terms0, pad;
 };
 #define SHR_IMG_MAX (144 * 1024)
 

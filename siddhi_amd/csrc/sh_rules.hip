@@ -235,7 +235,7 @@ __global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
     const uint8_t* __restrict__ img, shr_img I, const uint32_t* __restrict__ s32, int64_t tb) {
     extern __shared__ uint4 s_img[];
     __shared__ const void* s_col[32];
-    for (int i = threadIdx.x; i < I.bytes / 16; i += blockDim.x) s_img[i] = ((const uint4*)img)[i];
+    for (int i = threadIdx.x; i < I.lds / 16; i += blockDim.x) s_img[i] = ((const uint4*)img)[i];
     if (threadIdx.x < 32) s_col[threadIdx.x] = C->col[0][threadIdx.x];
     __syncthreads();
     const uint8_t* L = (const uint8_t*)s_img;
@@ -244,7 +244,8 @@ __global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
     const uint32_t* ixr = (const uint32_t*)(L + I.off_ixr);
     const uint32_t* fr = (const uint32_t*)(L + I.off_free);
     const shr_meta* meta = (const shr_meta*)(L + I.off_meta);
-    const shp_term* terms = (const shp_term*)(L + I.off_terms);
+    const shp_term* terms1 = (const shp_term*)(L + I.off_terms1);           // LDS
+    const shp_term* terms0 = (const shp_term*)(img + I.off_terms0);         // global
     const int ix_attr = RT->ix_attr;
     const int n_ix = RT->n_ix;
     const uint32_t n_free = (uint32_t)RT->n_free;
@@ -277,9 +278,8 @@ __global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
         for (uint32_t k = 0; k < total; k++) {
             const uint32_t r = k < nsel ? ixr[lo + k] : fr[k - nsel];
             const shr_meta M = meta[r];
-            const shp_term* T0 = terms + M.toff;
-            if (!rule_terms_img(T0, M.nt0, (uint32_t)p, SHD_NULL_ROW, s_col)) continue;
-            const shp_term* T1 = T0 + M.nt0;
+            if (!rule_terms_img(terms0 + M.toff0, M.nt0, (uint32_t)p, SHD_NULL_ROW, s_col)) continue;
+            const shp_term* T1 = terms1 + M.toff1;
             const int64_t W = M.within;
             for (int64_t q = p + 1; q < n; q++) {
                 if (skeys && skeys[q] != key) break;
@@ -313,11 +313,11 @@ static int rules_scan_img(const shr_table* dT, const int64_t* sts, const uint32_
         attr_set = 1;
     }
     int64_t g = (n + RTPB_IMG - 1) / RTPB_IMG;
-    const int per_cu = (160 * 1024) / (I.bytes + 1024);
+    const int per_cu = (160 * 1024) / (I.lds + 1024);
     const int64_t gmax = 256LL * (per_cu < 1 ? 1 : per_cu);
     if (g > gmax) g = gmax;
     if (g < 1) g = 1;
-    hipLaunchKernelGGL(k_rules_scan_img<WRITE>, dim3((unsigned)g), dim3(RTPB_IMG), (size_t)I.bytes, st, dT, sts, skeys,
+    hipLaunchKernelGGL(k_rules_scan_img<WRITE>, dim3((unsigned)g), dim3(RTPB_IMG), (size_t)I.lds, st, dT, sts, skeys,
                        n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, flag, img, I, s32, tb);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
