@@ -23,6 +23,7 @@
 #include "sh_device.h"
 #include "sh_wave.h"
 
+#include <stdlib.h>
 #include <string.h>
 #include <type_traits>
 
@@ -698,6 +699,94 @@ static uint32_t g_bits_for(uint32_t maxkey) {
     return b;
 }
 
+// Small batches (a send() call of the streaming path, n <= SEG1_MAXN, no carried
+// columns): the whole segment in ONE workgroup -- stable LSD passes of 8-bit digits
+// in LDS (shw_rank8 ranks each round in element order), then the segment starts --
+// instead of ~15 launches (histogram, scans and scatter per pass, flags, scan,
+// compaction) that each cost more than the work of a 4,096-event call.
+#define SEG1_NT 512
+#define SEG1_MAXN 4096
+#define SEG1_R (SEG1_MAXN / SEG1_NT)
+__global__ void __launch_bounds__(SEG1_NT) k_segment_small(const int32_t* __restrict__ raw, int64_t n, uint32_t sentinel,
+                                                           int passes, uint32_t* __restrict__ keys_out,
+                                                           uint32_t* __restrict__ idx_out, uint32_t* __restrict__ seg_list,
+                                                           uint32_t* __restrict__ nseg) {
+    __shared__ uint32_t kA[SEG1_MAXN], kB[SEG1_MAXN];
+    __shared__ uint16_t iA[SEG1_MAXN], iB[SEG1_MAXN];
+    __shared__ uint32_t wcnt[SEG1_NT / 64][256];
+    __shared__ uint32_t run[256], ws[SEG1_NT / 64];
+    const int nn = (int)n;
+    for (int i = threadIdx.x; i < nn; i += SEG1_NT) {
+        const int32_t r = raw[i];
+        kA[i] = r < 0 ? sentinel : (uint32_t)r;
+        iA[i] = (uint16_t)i;
+    }
+    uint32_t* kin = kA;
+    uint32_t* kout = kB;
+    uint16_t* iin = iA;
+    uint16_t* iout = iB;
+    for (int ps = 0; ps < passes; ps++) {
+        const int shift = 8 * ps;
+        if (threadIdx.x < 256) run[threadIdx.x] = 0u;
+        __syncthreads();
+        uint32_t rk[SEG1_R], dg[SEG1_R];
+#pragma unroll
+        for (int r = 0; r < SEG1_R; r++) {
+            const int i = r * SEG1_NT + threadIdx.x;
+            const bool valid = i < nn;
+            dg[r] = valid ? (kin[i] >> shift) & 0xFFu : 0u;
+            rk[r] = shw_rank8<SEG1_NT>(dg[r], valid, wcnt, run);
+        }
+        // digit starts: exclusive scan of the digits' totals
+        {
+            uint32_t tot;
+            const uint32_t c = threadIdx.x < 256 ? run[threadIdx.x] : 0u;
+            const uint32_t ex = shw_block_excl<SEG1_NT>(c, ws, &tot);
+            __syncthreads();
+            if (threadIdx.x < 256) run[threadIdx.x] = ex;
+            __syncthreads();
+        }
+#pragma unroll
+        for (int r = 0; r < SEG1_R; r++) {
+            const int i = r * SEG1_NT + threadIdx.x;
+            if (i < nn) {
+                const uint32_t pos = run[dg[r]] + rk[r];
+                kout[pos] = kin[i];
+                iout[pos] = iin[i];
+            }
+        }
+        __syncthreads();
+        uint32_t* tk = kin;
+        kin = kout;
+        kout = tk;
+        uint16_t* ti = iin;
+        iin = iout;
+        iout = ti;
+    }
+    // sorted keys and permutation out; segment starts (a key change, the null-key
+    // sentinel excluded) into kout as 0/1 flags, scanned in place
+    for (int i = threadIdx.x; i < nn; i += SEG1_NT) {
+        const uint32_t k = kin[i];
+        keys_out[i] = k;
+        idx_out[i] = (uint32_t)iin[i];
+        kout[i] = ((i == 0 || kin[i - 1] != k) && k != sentinel) ? 1u : 0u;
+    }
+    __syncthreads();
+    uint32_t flag[SEG1_R];
+#pragma unroll
+    for (int r = 0; r < SEG1_R; r++) {
+        const int i = threadIdx.x * SEG1_R + r;
+        flag[r] = i < nn ? kout[i] : 0u;
+    }
+    const uint32_t total = shw_lds_excl_scan<SEG1_NT, SEG1_R>(kout, nn, ws);
+#pragma unroll
+    for (int r = 0; r < SEG1_R; r++) {
+        const int i = threadIdx.x * SEG1_R + r;
+        if (i < nn && flag[r]) seg_list[kout[i]] = (uint32_t)i;
+    }
+    if (threadIdx.x == 0) *nseg = total;
+}
+
 extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segment_ws* ws, void* stream,
                                    const uint32_t** perm_out, const uint32_t** skeys_out, const shd_payload* carry,
                                    void* const* mid, int tile_shift, int want_segments) {
@@ -709,6 +798,17 @@ extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segmen
     int64_t ntiles = ceil_div(n, RADIX_TILE);
     if (sub_shift >= 0) ntiles = ceil_div(ntiles, (int64_t)1 << sub_shift) << sub_shift;
     const uint32_t bits = g_bits_for(sentinel);
+    static const bool small_on = !(getenv("SH_SEG_SMALL") && getenv("SH_SEG_SMALL")[0] == '0');
+    if (small_on && b->keys && n <= SEG1_MAXN && n > 0 && !carry && want_segments && sub_shift < 0 && bits <= 32) {
+        // the whole segment in one workgroup (small send() calls)
+        const int passes8 = (int)((bits + 7) / 8);
+        uint32_t* seg_list = ws->seg_off + 2 * n;
+        hipLaunchKernelGGL(k_segment_small, dim3(1), dim3(SEG1_NT), 0, st, b->keys, n, sentinel, passes8, ws->keys_a,
+                           ws->idx_a, seg_list, seg_list + n);
+        *perm_out = ws->idx_a;
+        *skeys_out = ws->keys_a;
+        return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
     // 17..20-bit key ranges: two passes of 10-bit digits instead of three of 8 (opt-in)
     const int db = (bits > 16 && bits <= 20 && radix10()) ? 10 : 8;
     const int passes = b->keys ? (int)((bits + db - 1) / db) : 0;
