@@ -840,9 +840,11 @@ static int upload_rules(sh_handle* h) {
         const size_t o_fr = sect(4 * h->r_free.size());
         const size_t o_meta = sect(sizeof(shr_meta) * nr);
         const size_t o_t1 = sect(sizeof(shp_term) * nt1);
-        const size_t lds = (img.size() + 15) & ~(size_t)15;
+        const size_t lds_split = (img.size() + 15) & ~(size_t)15;
         const size_t o_t0 = sect(sizeof(shp_term) * nt0);
         img.resize((img.size() + 15) & ~(size_t)15);
+        const bool split = getenv("SH_RULES_IMG_SPLIT") && getenv("SH_RULES_IMG_SPLIT")[0] == '1';
+        const size_t lds = split ? lds_split : img.size();
         static const bool img_on = !(getenv("SH_RULES_IMG") && getenv("SH_RULES_IMG")[0] == '0');
         if (img_on && lds <= SHR_IMG_MAX && nt0 < 65536 && nt1 < 65536) {
             if (!h->r_ixval.empty()) memcpy(&img[o_ixv], h->r_ixval.data(), 8 * h->r_ixval.size());

@@ -39,9 +39,10 @@ struct shr_meta {
     uint8_t nt0, nt1;
     uint16_t pad;
 };
-// the image's first `lds` bytes (index, rule ids, metas, f2's terms: read per walk
-// step) go to LDS; f1's terms (read once per candidate rule) stay in global memory,
-// so two 1024-thread workgroups fit a CU
+// the image's first `lds` bytes go to LDS: all of it (one 1024-thread workgroup per CU),
+// or with SH_RULES_IMG_SPLIT=1 everything but f1's terms (read once per candidate rule),
+// so two workgroups fit a CU -- measured slower on C5 (14.5 vs 14.0 ms): the L2 reads
+// of f1's terms cost more than the extra occupancy gained
 struct shr_img {
     int32_t bytes;                      // image size (multiple of 16), 0: no image
     int32_t lds;                        // bytes staged in LDS (multiple of 16)

@@ -245,7 +245,8 @@ __global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
     const uint32_t* fr = (const uint32_t*)(L + I.off_free);
     const shr_meta* meta = (const shr_meta*)(L + I.off_meta);
     const shp_term* terms1 = (const shp_term*)(L + I.off_terms1);           // LDS
-    const shp_term* terms0 = (const shp_term*)(img + I.off_terms0);         // global
+    // f1's terms: in LDS when staged, else from the global image (I.lds stops before them)
+    const shp_term* terms0 = (const shp_term*)((I.off_terms0 < I.lds ? L : img) + I.off_terms0);
     const int ix_attr = RT->ix_attr;
     const int n_ix = RT->n_ix;
     const uint32_t n_free = (uint32_t)RT->n_free;
