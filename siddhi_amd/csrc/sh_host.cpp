@@ -373,6 +373,7 @@ struct sh_handle {
     uint64_t seq_staged0 = 0;
     // workspaces
     DevBuf w_ts, w_stream, w_row, w_key, w_keys_a, w_keys_b, w_idx_a, w_idx_b, w_hist, w_scan, w_seg;
+    DevBuf w_pstage;  // the general engine's per-call staging (nf_push), one block
     DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls, w_oq, w_inv;
     bool dev_want_query = false;  // sh_run_device asked for d_out_query
     const uint32_t* dev_run_ids = nullptr;  // sh_run_device's d_run while it runs the general engine
@@ -1036,6 +1037,7 @@ void sh_destroy(sh_handle* h) {
         for (auto& b : h->v_scol) b.release();
         for (auto& b : h->v_mid) b.release();
         DevBuf* bufs[] = {&h->d_prog, &h->d_cols_desc, &h->d_kstate, &h->d_err, &h->w_ts, &h->w_stream, &h->w_row,
+                          &h->w_pstage,
                           &h->w_key, &h->w_keys_a, &h->w_keys_b, &h->w_idx_a, &h->w_idx_b, &h->w_hist, &h->w_scan,
                           &h->w_seg, &h->w_cnt, &h->w_off, &h->w_tmp, &h->w_ctr, &h->w_oseq, &h->w_ots,
                           &h->w_ovals, &h->w_onulls, &h->w_inv};
@@ -1806,7 +1808,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
     E.ts = B.ts;
     E.stream = B.stream;
     E.row = B.row;
-    E.bid = fresh ? nullptr : h->n_bid.as<uint32_t>();
+    E.bid = nullptr;  // one send() call per launch (batch 0), or fresh runs' batch_events
     E.perm = perm;
     E.seq_base = B.seq_base;
     E.batch_events = batch_events;
@@ -2259,19 +2261,14 @@ static int nf_push(sh_handle* h, const sh_batch* b, int64_t r0, const uint32_t* 
             nk = std::max(nk, keys[i] + 1);
         }
     }
-    if (h->w_ts.ensure_fresh(n * 8) || h->w_stream.ensure_fresh(n) || h->w_row.ensure_fresh(n * 4) ||
-        h->w_key.ensure_fresh(n * 4) || h->n_bid.ensure_fresh(n * 4))
-        return fail(h, SH_E_OOM, "staging");
-    hipMemcpyAsync(h->w_ts.p, h->pin_stage.as<int64_t>(o_ts), n * 8, hipMemcpyHostToDevice, st);
-    hipMemcpyAsync(h->w_stream.p, sv, n, hipMemcpyHostToDevice, st);
-    hipMemcpyAsync(h->w_row.p, rows, n * 4, hipMemcpyHostToDevice, st);
-    hipMemcpyAsync(h->w_key.p, keys, n * 4, hipMemcpyHostToDevice, st);
-    hipMemsetAsync(h->n_bid.p, 0, n * 4, st);
+    // one copy: the device staging mirrors pin_stage's layout (ts | rows | keys | stream)
+    if (h->w_pstage.ensure_fresh(o_sv + (size_t)n)) return fail(h, SH_E_OOM, "staging");
+    hipMemcpyAsync(h->w_pstage.p, h->pin_stage.p, o_sv + (size_t)n, hipMemcpyHostToDevice, st);
     shd_batch B;
-    B.ts = h->w_ts.as<int64_t>();
-    B.stream = h->w_stream.as<uint8_t>();
-    B.row = h->w_row.as<uint32_t>();
-    B.keys = h->partitioned ? h->w_key.as<int32_t>() : nullptr;
+    B.ts = h->w_pstage.as<int64_t>();
+    B.stream = h->w_pstage.as<uint8_t>() + o_sv;
+    B.row = (const uint32_t*)(h->w_pstage.as<uint8_t>() + o_rows);
+    B.keys = h->partitioned ? (const int32_t*)(h->w_pstage.as<uint8_t>() + o_keys) : nullptr;
     B.row_base = 0;
     B.pad = 0;
     B.seq_base = h->seq_next;
