@@ -374,6 +374,7 @@ struct sh_handle {
     // workspaces
     DevBuf w_ts, w_stream, w_row, w_key, w_keys_a, w_keys_b, w_idx_a, w_idx_b, w_hist, w_scan, w_seg;
     DevBuf w_pstage;  // the general engine's per-call staging (nf_push), one block
+    DevBuf w_orows;   // placed rows of a streaming launch, one block (query | seq | ts | values | nulls)
     DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls, w_oq, w_inv;
     bool dev_want_query = false;  // sh_run_device asked for d_out_query
     const uint32_t* dev_run_ids = nullptr;  // sh_run_device's d_run while it runs the general engine
@@ -1037,7 +1038,7 @@ void sh_destroy(sh_handle* h) {
         for (auto& b : h->v_scol) b.release();
         for (auto& b : h->v_mid) b.release();
         DevBuf* bufs[] = {&h->d_prog, &h->d_cols_desc, &h->d_kstate, &h->d_err, &h->w_ts, &h->w_stream, &h->w_row,
-                          &h->w_pstage,
+                          &h->w_pstage, &h->w_orows,
                           &h->w_key, &h->w_keys_a, &h->w_keys_b, &h->w_idx_a, &h->w_idx_b, &h->w_hist, &h->w_scan,
                           &h->w_seg, &h->w_cnt, &h->w_off, &h->w_tmp, &h->w_ctr, &h->w_oseq, &h->w_ots,
                           &h->w_ovals, &h->w_onulls, &h->w_inv};
@@ -1686,30 +1687,24 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
                   h->w_inv.as<uint32_t>(), total, st);
         return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "placement");
     }
-    if (h->w_oseq.ensure_fresh(total * 8) || h->w_ots.ensure_fresh(total * 8) || h->w_ovals.ensure_fresh(total * no * 8) ||
-        h->w_onulls.ensure_fresh(total * no) || h->w_oq.ensure_fresh(total * 4))
-        return fail(h, SH_E_OOM, "output buffers");
-    nfd_place(h->n_recs.as<uint64_t>(), (int64_t)nrec, stride, h->w_off.as<uint32_t>(), no, h->w_oq.as<int32_t>(),
-              h->w_oseq.as<uint64_t>(), h->w_ots.as<int64_t>(), h->w_ovals.as<int64_t>(), h->w_onulls.as<uint8_t>(),
-              h->w_inv.as<uint32_t>(), total, st);
+    // the rows are placed into one device block laid out like the pinned staging
+    // (query | seq | ts | values | nulls) and come back in one copy, then into the host queue
+    const size_t b_q = 0, b_seq = b_q + ((size_t)total * 4 + 7) / 8 * 8, b_ts = b_seq + (size_t)total * 8,
+                 b_v = b_ts + (size_t)total * 8, b_n = b_v + (size_t)total * no * 8, b_end = b_n + (size_t)total * no;
+    if (h->w_orows.ensure_fresh(b_end)) return fail(h, SH_E_OOM, "output buffers");
+    uint8_t* ob = h->w_orows.as<uint8_t>();
+    nfd_place(h->n_recs.as<uint64_t>(), (int64_t)nrec, stride, h->w_off.as<uint32_t>(), no, (int32_t*)(ob + b_q),
+              (uint64_t*)(ob + b_seq), (int64_t*)(ob + b_ts), (int64_t*)(ob + b_v), ob + b_n, h->w_inv.as<uint32_t>(),
+              total, st);
     const size_t base = h->o_seq.size();
     h->o_query.resize(base + total);
     h->o_seq.resize(base + total);
     h->o_ts.resize(base + total);
     h->o_vals.resize((base + total) * h->n_out);
     h->o_nulls.resize((base + total) * h->n_out);
-    // rows come back through pinned staging, then into the host queue
-    const size_t b_q = 0, b_seq = b_q + ((size_t)total * 4 + 7) / 8 * 8, b_ts = b_seq + (size_t)total * 8,
-                 b_v = b_ts + (size_t)total * 8, b_n = b_v + (size_t)total * no * 8, b_end = b_n + (size_t)total * no;
     if (h->pin_out.ensure(b_end)) return fail(h, SH_E_OOM, "pinned staging");
-    hipMemcpyAsync(h->pin_out.as<void>(b_q), h->w_oq.p, total * 4, hipMemcpyDeviceToHost, st);
-    hipMemcpyAsync(h->pin_out.as<void>(b_seq), h->w_oseq.p, total * 8, hipMemcpyDeviceToHost, st);
-    hipMemcpyAsync(h->pin_out.as<void>(b_ts), h->w_ots.p, total * 8, hipMemcpyDeviceToHost, st);
     const bool vals = h->n_out && no == h->n_out;
-    if (vals) {
-        hipMemcpyAsync(h->pin_out.as<void>(b_v), h->w_ovals.p, total * no * 8, hipMemcpyDeviceToHost, st);
-        hipMemcpyAsync(h->pin_out.as<void>(b_n), h->w_onulls.p, total * no, hipMemcpyDeviceToHost, st);
-    }
+    hipMemcpyAsync(h->pin_out.p, ob, vals ? b_end : b_v, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "output copy");
     memcpy(h->o_query.data() + base, h->pin_out.as<void>(b_q), total * 4);
     memcpy(h->o_seq.data() + base, h->pin_out.as<void>(b_seq), total * 8);
