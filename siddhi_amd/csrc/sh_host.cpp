@@ -841,6 +841,14 @@ static int upload_rules(sh_handle* h) {
         const size_t o_ixr = sect(4 * h->r_ixrule.size());
         const size_t o_fr = sect(4 * h->r_free.size());
         const size_t o_meta = sect(sizeof(shr_meta) * nr);
+        // dense index over a small key range (SH_RULES_DENSE=0: the binary search)
+        int64_t dmin = 0, drange = 0;
+        if (!h->r_ixval.empty() && !(getenv("SH_RULES_DENSE") && getenv("SH_RULES_DENSE")[0] == '0')) {
+            dmin = h->r_ixval.front();
+            const int64_t r = h->r_ixval.back() - dmin + 1;
+            if (r > 0 && r <= 16384) drange = r;
+        }
+        const size_t o_dense = sect(8 * (size_t)drange);
         const size_t o_t1 = sect(sizeof(shp_term) * nt1);
         const size_t lds_split = (img.size() + 15) & ~(size_t)15;
         const size_t o_t0 = sect(sizeof(shp_term) * nt0);
@@ -853,6 +861,10 @@ static int upload_rules(sh_handle* h) {
             memcpy(&img[o_ixs], h->r_ixstart.data(), 4 * h->r_ixstart.size());
             if (!h->r_ixrule.empty()) memcpy(&img[o_ixr], h->r_ixrule.data(), 4 * h->r_ixrule.size());
             if (!h->r_free.empty()) memcpy(&img[o_fr], h->r_free.data(), 4 * h->r_free.size());
+            for (size_t g = 0; drange && g < h->r_ixval.size(); g++) {
+                const uint32_t e[2] = {h->r_ixstart[g], h->r_ixstart[g + 1]};
+                memcpy(&img[o_dense + 8 * (size_t)(h->r_ixval[g] - dmin)], e, 8);
+            }
             size_t k0 = 0, k1 = 0;
             for (size_t i = 0; i < nr; i++) {
                 const shr_rule& r = h->r_rules[i];
@@ -880,6 +892,9 @@ static int upload_rules(sh_handle* h) {
             h->r_img.off_meta = (int32_t)o_meta;
             h->r_img.off_terms1 = (int32_t)o_t1;
             h->r_img.off_terms0 = (int32_t)o_t0;
+            h->r_img.dense_min = dmin;
+            h->r_img.dense_n = (int32_t)drange;
+            h->r_img.off_dense = (int32_t)o_dense;
         }
     }
     shr_table t = h->r_tab;

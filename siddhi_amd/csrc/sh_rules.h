@@ -47,6 +47,10 @@ struct shr_img {
     int32_t bytes;                      // image size (multiple of 16), 0: no image
     int32_t lds;                        // bytes staged in LDS (multiple of 16)
     int32_t off_ixv, off_ixs, off_ixr, off_free, off_meta, off_terms1, off_terms0, pad;
+    // dense index: (group start, end) per key value in [dense_min, dense_min + dense_n)
+    // when the indexed constants span a small range (one LDS read instead of a search)
+    int64_t dense_min;
+    int32_t dense_n, off_dense;
 };
 #define SHR_IMG_MAX (144 * 1024)
 

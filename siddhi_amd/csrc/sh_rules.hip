@@ -260,17 +260,26 @@ __global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
         uint32_t lo = 0, hi = 0;
         if (ix_attr >= 0) {
             const int64_t x = rule_ix_key(ix_ty, rule_attr(s_col, ix_attr, ix_ty, (uint32_t)p));
-            int a = 0, b = n_ix;
-            while (a < b) {
-                const int m = (a + b) >> 1;
-                if (ixv[m] < x)
-                    a = m + 1;
-                else
-                    b = m;
-            }
-            if (a < n_ix && ixv[a] == x) {
-                lo = ixs[a];
-                hi = ixs[a + 1];
+            if (I.dense_n) {
+                const int64_t dv = x - I.dense_min;
+                if (dv >= 0 && dv < I.dense_n) {
+                    const uint2 e = ((const uint2*)(L + I.off_dense))[dv];
+                    lo = e.x;
+                    hi = e.y;
+                }
+            } else {
+                int a = 0, b = n_ix;
+                while (a < b) {
+                    const int m = (a + b) >> 1;
+                    if (ixv[m] < x)
+                        a = m + 1;
+                    else
+                        b = m;
+                }
+                if (a < n_ix && ixv[a] == x) {
+                    lo = ixs[a];
+                    hi = ixs[a + 1];
+                }
             }
         }
         const uint32_t nsel = hi - lo, total = nsel + n_free;
