@@ -2634,15 +2634,9 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
         const uint32_t* flags = nullptr;
         const uint32_t* rid = nullptr;
         const uint32_t* rfirst = nullptr;
-        if (sorted) {
-            if (h->r_run.ensure_fresh((size_t)n * 12)) return fail(h, SH_E_OOM, "run ids");
-            uint32_t* f = h->r_run.as<uint32_t>();
-            if (shr_run_ids(run->d_keys, run->d_run, n, batch, f, f + n, f + 2 * n, h->w_scan.as<uint32_t>(), st))
-                return fail(h, SH_E_HIP, "run id launch failed");
-            flags = f;
-            rid = f + n;
-            rfirst = f + 2 * n;
-        }
+        // the runs of the consuming events only, walked back from each record's event
+        // (SH_RULES_RUNSCAN=1: flags, scan and first index over every event)
+        const bool walk_runs = sorted && !getenv("SH_RULES_RUNSCAN");
         // order key (run, query, consuming event), least significant first; the
         // records are in (opening event, rule) order, which the stable sort keeps
         // among equal keys (creation order of the partials a consumer takes)
@@ -2654,7 +2648,29 @@ static int run_rules(sh_handle* h, sh_device_run* run) {
         uint32_t* k0 = h->r_keys.as<uint32_t>();
         uint32_t* k1 = k0 + m;
         uint32_t* k2 = k1 + m;
-        if (shr_keys(rec_q, rec_r, m, perm, flags, rid, rfirst, batch, qbits, packed ? 1 : 0, k0, k1, k2, st))
+        bool scan_runs = sorted && !walk_runs;
+        if (walk_runs) {
+            int32_t* long_run = h->v_flag.as<int32_t>() + 1;
+            int32_t lr = 0;
+            hipMemsetAsync(long_run, 0, 4, st);
+            if (shr_keys(rec_q, rec_r, m, perm, nullptr, nullptr, nullptr, batch, qbits, packed ? 1 : 0, k0, k1, k2,
+                         st, run->d_keys, run->d_run, long_run))
+                return fail(h, SH_E_HIP, "rule key launch failed");
+            hipMemcpyAsync(&lr, long_run, 4, hipMemcpyDeviceToHost, st);
+            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the rule keys");
+            scan_runs = lr != 0;
+        }
+        if (scan_runs) {
+            if (h->r_run.ensure_fresh((size_t)n * 12)) return fail(h, SH_E_OOM, "run ids");
+            uint32_t* f = h->r_run.as<uint32_t>();
+            if (shr_run_ids(run->d_keys, run->d_run, n, batch, f, f + n, f + 2 * n, h->w_scan.as<uint32_t>(), st))
+                return fail(h, SH_E_HIP, "run id launch failed");
+            flags = f;
+            rid = f + n;
+            rfirst = f + 2 * n;
+        }
+        if ((scan_runs || !walk_runs) &&
+            shr_keys(rec_q, rec_r, m, perm, flags, rid, rfirst, batch, qbits, packed ? 1 : 0, k0, k1, k2, st))
             return fail(h, SH_E_HIP, "rule key launch failed");
         const uint32_t* stage_key[3];
         int stage_bits[3];

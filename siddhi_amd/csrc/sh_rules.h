@@ -74,10 +74,15 @@ int shr_write(const shr_table* dT, const int64_t* sts, const uint32_t* skeys, in
 int shr_run_ids(const int32_t* akeys, const uint32_t* run_ids, int64_t n, int64_t batch, uint32_t* flags,
                 uint32_t* rid, uint32_t* rfirst, uint32_t* scan_tmp, void* stream);
 // order keys of the records: packed -> k0 = rule << qbits | offset in run,
-// k1 = run; else k0 = offset in run, k1 = rule, k2 = run
+// k1 = run; else k0 = offset in run, k1 = rule, k2 = run. akeys (the arrival-order
+// keys): each run found by walking back from its consuming event, keyed by its first
+// arrival index (flags / rid / rfirst unused); a walk longer than 512 events sets
+// *long_run and leaves the keys unusable
 int shr_keys(const uint32_t* rec_q, const uint32_t* rec_r, int64_t m, const uint32_t* perm, const uint32_t* flags,
              const uint32_t* rid, const uint32_t* rfirst, int64_t batch, int qbits, int packed, uint32_t* k0,
-             uint32_t* k1, uint32_t* k2, void* stream);
+             uint32_t* k1, uint32_t* k2, void* stream,
+             const int32_t* akeys = nullptr, const uint32_t* run_ids = nullptr,
+             int32_t* long_run = nullptr);
 // gk[i] = key[order[i]], gv[i] = order[i] (order NULL: identity)
 int shr_gather(const uint32_t* key, const uint32_t* order, int64_t m, uint32_t* gk, uint32_t* gv, void* stream);
 // ordered output rows from the sorted record order

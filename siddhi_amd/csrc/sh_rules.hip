@@ -360,16 +360,42 @@ __global__ void k_run_first(const uint32_t* __restrict__ flags, const uint32_t* 
         if (flags[i]) rfirst[rid[i]] = (uint32_t)i;
 }
 
+#define SHR_WALK_MAX 512
+
 __global__ void k_rules_keys(const uint32_t* __restrict__ rec_q, const uint32_t* __restrict__ rec_r, int64_t m,
                              const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
                              const uint32_t* __restrict__ rid, const uint32_t* __restrict__ rfirst, int64_t batch,
                              int qbits, int packed, uint32_t* __restrict__ k0, uint32_t* __restrict__ k1,
-                             uint32_t* __restrict__ k2) {
+                             uint32_t* __restrict__ k2, const int32_t* __restrict__ akeys,
+                             const uint32_t* __restrict__ run_ids, int32_t* __restrict__ long_run) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t q = rec_q[i];
         const uint32_t qa = perm ? perm[q] : q;
         uint32_t run, qoff;
-        if (flags) {
+        if (akeys) {
+            // the consuming event's PartitionStreamReceiver run, found by walking back
+            // from it (the run's first arrival index orders the runs like their ordinal):
+            // a keyed event continues the run of the previous keyed event of its call
+            // with the same key (or the same caller run id)
+            const int32_t key = akeys[qa];
+            const int64_t lb = run_ids ? 0 : (batch > 0 ? (int64_t)qa - (int64_t)qa % batch : 0);
+            // bounded: a run longer than SHR_WALK_MAX events reports itself and the host
+            // redoes the keys from the per-event run scan (no quadratic hot-key walk)
+            int64_t first = qa;
+            for (;;) {
+                int64_t j = first - 1;
+                while (j >= lb && akeys[j] < 0 && (int64_t)qa - j <= SHR_WALK_MAX) j--;
+                if (j < lb) break;
+                if ((int64_t)qa - j > SHR_WALK_MAX) {
+                    *long_run = 1;
+                    break;
+                }
+                if (run_ids ? run_ids[j] != run_ids[qa] : akeys[j] != key) break;
+                first = j;
+            }
+            run = (uint32_t)first;
+            qoff = qa - (uint32_t)first;
+        } else if (flags) {
             run = rid[qa] + flags[qa] - 1u;
             qoff = qa - rfirst[run];
         } else if (batch > 0) {
@@ -471,9 +497,11 @@ extern "C" int shr_run_ids(const int32_t* akeys, const uint32_t* run_ids, int64_
 
 extern "C" int shr_keys(const uint32_t* rec_q, const uint32_t* rec_r, int64_t m, const uint32_t* perm,
                         const uint32_t* flags, const uint32_t* rid, const uint32_t* rfirst, int64_t batch, int qbits,
-                        int packed, uint32_t* k0, uint32_t* k1, uint32_t* k2, void* stream) {
+                        int packed, uint32_t* k0, uint32_t* k1, uint32_t* k2, void* stream, const int32_t* akeys,
+                        const uint32_t* run_ids, int32_t* long_run) {
+    if (akeys && !long_run) return 1;
     hipLaunchKernelGGL(k_rules_keys, dim3(rgrid(m)), dim3(RTPB), 0, (hipStream_t)stream, rec_q, rec_r, m, perm, flags,
-                       rid, rfirst, batch, qbits, packed, k0, k1, k2);
+                       rid, rfirst, batch, qbits, packed, k0, k1, k2, akeys, run_ids, long_run);
     return rules_ok();
 }
 

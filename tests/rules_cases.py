@@ -38,6 +38,7 @@ CASES = [
     (30000, 2000, 300, 1, 4096, 40, True, (), 16),
     (20000, 200, 64, 4, 997, 12, True, (3, 7, 9), 17),
     (10000, 10, 2, 1, 4096, 5, True, (), 18),
+    (10000, 1, 6, 2, 4096, 4, True, (), 19),         # one card, 4096-event runs (beyond the keys kernel's walk)
 ]
 
 
