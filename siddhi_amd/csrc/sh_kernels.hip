@@ -167,7 +167,7 @@ __device__ __forceinline__ uint32_t load_key(const uint32_t* __restrict__ keys_i
 }
 
 template <int B>
-__global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ raw,
+__global__ void __launch_bounds__(TPB, (B <= 8 ? 4 : 3)) k_digit_scatter(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ raw,
                                                        uint32_t sentinel, const uint32_t* __restrict__ idx_in, int64_t n,
                                                        int shift, const uint32_t* __restrict__ offs, int64_t ntiles,
                                                        uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out,
@@ -192,7 +192,10 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
     __shared__ uint32_t tstart[ND];
     __shared__ uint32_t gbase[ND];
     __shared__ dig_t dig[RADIX_TILE];
-    __shared__ uint64_t stage[RADIX_TILE];
+    // 16 KB: 4-byte staging of a whole tile; 8-byte columns go through it as two
+    // halves of the tile (values held in registers), so the scatter fits ~26 KB of
+    // LDS and five to six workgroups per CU instead of three
+    __shared__ __align__(16) uint32_t stage[RADIX_TILE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t base = tile * RADIX_TILE;
@@ -268,7 +271,7 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
     {                                                                                           \
         for (int j = 0; j < RADIX_ITEMS; j++) {                                                 \
             const int64_t i = wbase + j * 64;                                                   \
-            if (i < n) stage[lp[j]] = (uint64_t)(SRCEXPR);                                      \
+            if (i < n) stage[lp[j]] = (uint32_t)(SRCEXPR);                                      \
         }                                                                                       \
         __syncthreads();                                                                        \
         for (int m = 0; m < RADIX_ITEMS; m++) {                                                 \
@@ -288,7 +291,30 @@ __global__ void __launch_bounds__(TPB) k_digit_scatter(const uint32_t* __restric
     for (int c = 0; c < PL.n; c++) {
         if (PL.width[c] == 8) {
             const uint64_t* src = (const uint64_t*)PL.src[c];
-            SH_STAGE_OUT(uint64_t, src[gather ? idx_in[i] : i], PL.dst[c]);
+            uint64_t* dst = (uint64_t*)PL.dst[c];
+            uint64_t v[RADIX_ITEMS];
+#pragma unroll
+            for (int j = 0; j < RADIX_ITEMS; j++) {
+                const int64_t i = wbase + j * 64;
+                v[j] = (i < n) ? src[gather ? idx_in[i] : i] : 0ull;
+            }
+            uint64_t* st64 = (uint64_t*)stage;
+            constexpr uint32_t HALF = RADIX_TILE / 2;
+            for (uint32_t lo = 0; lo < (uint32_t)tile_n; lo += HALF) {  // uniform
+#pragma unroll
+                for (int j = 0; j < RADIX_ITEMS; j++)
+                    if (wbase + j * 64 < n && lp[j] - lo < HALF) st64[lp[j] - lo] = v[j];
+                __syncthreads();
+#pragma unroll
+                for (int m = 0; m < RADIX_ITEMS / 2; m++) {
+                    const uint32_t l = lo + m * TPB + threadIdx.x;
+                    if (l < (uint32_t)tile_n) {
+                        const uint32_t d = dig[l];
+                        dst[gbase[d] + l - tstart[d]] = st64[l - lo];
+                    }
+                }
+                __syncthreads();
+            }
         } else if (PL.width[c] == 4) {
             const uint32_t* src = (const uint32_t*)PL.src[c];
             SH_STAGE_OUT(uint32_t, src[gather ? idx_in[i] : i], PL.dst[c]);
