@@ -466,6 +466,7 @@ struct sh_handle {
     bool skip_rules = false;             // rerun on the general engine (aggregates not exact in parallel)
     std::vector<int64_t> r_ixval;
     std::vector<uint32_t> r_ixstart, r_ixrule, r_free;
+    std::vector<int8_t> r_ixterm;  // per rule: the f1 term its index group implies (-1: none)
     shr_table r_tab{};
     DevBuf rd_rules, rd_ixval, rd_ixstart, rd_ixrule, rd_free, rd_tab;
     DevBuf rd_img;   // the rule set's LDS image (shr_img), when it fits
@@ -772,6 +773,7 @@ static int compile_rules(sh_handle* h, const sh_app_desc* app) {
         if (votes[a] > 0 && (ix < 0 || votes[a] > votes[ix])) ix = a;
     std::vector<std::pair<int64_t, uint32_t>> ent;
     h->r_free.clear();
+    h->r_ixterm.assign(rules.size(), (int8_t)-1);
     for (uint32_t r = 0; r < (uint32_t)rules.size(); r++) {
         int t = -1;
         for (int k = 0; ix >= 0 && k < rules[r].nt[0]; k++)
@@ -779,6 +781,7 @@ static int compile_rules(sh_handle* h, const sh_app_desc* app) {
                 t = k;
                 break;
             }
+        h->r_ixterm[r] = (int8_t)t;
         if (t < 0)
             h->r_free.push_back(r);
         else
@@ -831,23 +834,30 @@ static int upload_rules(sh_handle* h) {
             img.resize(at + bytes);
             return at;
         };
+        // an indexed rule's equality term on the index attribute holds for every event
+        // its group is looked up for (the lookup matched the constant's key exactly),
+        // so the image leaves it out (SH_RULES_IXTERM=1 keeps it)
+        const bool drop_ix = !(getenv("SH_RULES_IXTERM") && getenv("SH_RULES_IXTERM")[0] == '1');
+        auto implied = [&](size_t i) { return drop_ix && i < h->r_ixterm.size() ? (int)h->r_ixterm[i] : -1; };
         size_t nt0 = 0, nt1 = 0;
-        for (const shr_rule& r : h->r_rules) {
-            nt0 += (size_t)r.nt[0];
+        for (size_t i = 0; i < nr; i++) {
+            const shr_rule& r = h->r_rules[i];
+            nt0 += (size_t)r.nt[0] - (implied(i) >= 0 ? 1 : 0);
             nt1 += (size_t)r.nt[1];
         }
-        const size_t o_ixv = sect(8 * h->r_ixval.size());
-        const size_t o_ixs = sect(4 * h->r_ixstart.size());
-        const size_t o_ixr = sect(4 * h->r_ixrule.size());
-        const size_t o_fr = sect(4 * h->r_free.size());
-        const size_t o_meta = sect(sizeof(shr_meta) * nr);
-        // dense index over a small key range (SH_RULES_DENSE=0: the binary search)
+        // dense index over a small key range (SH_RULES_DENSE=0: the binary search,
+        // whose values and starts are then the only copy of the groups)
         int64_t dmin = 0, drange = 0;
         if (!h->r_ixval.empty() && !(getenv("SH_RULES_DENSE") && getenv("SH_RULES_DENSE")[0] == '0')) {
             dmin = h->r_ixval.front();
             const int64_t r = h->r_ixval.back() - dmin + 1;
             if (r > 0 && r <= 16384) drange = r;
         }
+        const size_t o_ixv = sect(drange ? 0 : 8 * h->r_ixval.size());
+        const size_t o_ixs = sect(drange ? 0 : 4 * h->r_ixstart.size());
+        const size_t o_ixr = sect(4 * h->r_ixrule.size());
+        const size_t o_fr = sect(4 * h->r_free.size());
+        const size_t o_meta = sect(sizeof(shr_meta) * nr);
         const size_t o_dense = sect(8 * (size_t)drange);
         const size_t o_t1 = sect(sizeof(shp_term) * nt1);
         const size_t lds_split = (img.size() + 15) & ~(size_t)15;
@@ -857,8 +867,10 @@ static int upload_rules(sh_handle* h) {
         const size_t lds = split ? lds_split : img.size();
         static const bool img_on = !(getenv("SH_RULES_IMG") && getenv("SH_RULES_IMG")[0] == '0');
         if (img_on && lds <= SHR_IMG_MAX && nt0 < 65536 && nt1 < 65536) {
-            if (!h->r_ixval.empty()) memcpy(&img[o_ixv], h->r_ixval.data(), 8 * h->r_ixval.size());
-            memcpy(&img[o_ixs], h->r_ixstart.data(), 4 * h->r_ixstart.size());
+            if (!drange) {
+                if (!h->r_ixval.empty()) memcpy(&img[o_ixv], h->r_ixval.data(), 8 * h->r_ixval.size());
+                memcpy(&img[o_ixs], h->r_ixstart.data(), 4 * h->r_ixstart.size());
+            }
             if (!h->r_ixrule.empty()) memcpy(&img[o_ixr], h->r_ixrule.data(), 4 * h->r_ixrule.size());
             if (!h->r_free.empty()) memcpy(&img[o_fr], h->r_free.data(), 4 * h->r_free.size());
             for (size_t g = 0; drange && g < h->r_ixval.size(); g++) {
@@ -873,11 +885,15 @@ static int upload_rules(sh_handle* h) {
                 m.within = r.within;
                 m.toff0 = (uint16_t)k0;
                 m.toff1 = (uint16_t)k1;
-                m.nt0 = (uint8_t)r.nt[0];
+                const int skip = implied(i);
+                m.nt0 = (uint8_t)(r.nt[0] - (skip >= 0 ? 1 : 0));
                 m.nt1 = (uint8_t)r.nt[1];
                 memcpy(&img[o_meta + i * sizeof(shr_meta)], &m, sizeof(m));
-                for (int t = 0; t < r.nt[0]; t++, k0++)
+                for (int t = 0; t < r.nt[0]; t++) {
+                    if (t == skip) continue;
                     memcpy(&img[o_t0 + k0 * sizeof(shp_term)], &r.t[0][t], sizeof(shp_term));
+                    k0++;
+                }
                 for (int t = 0; t < r.nt[1]; t++, k1++)
                     memcpy(&img[o_t1 + k1 * sizeof(shp_term)], &r.t[1][t], sizeof(shp_term));
             }

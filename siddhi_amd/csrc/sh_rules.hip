@@ -227,8 +227,9 @@ __device__ __forceinline__ bool rule_terms_img(const shp_term* T, int nt, uint32
     return true;
 }
 
-template <int WRITE>
-__global__ void __launch_bounds__(RTPB_IMG) k_rules_scan_img(
+// OCC2: the image fits two workgroups per CU, registers capped for 8 waves per SIMD
+template <int WRITE, int OCC2>
+__global__ void __launch_bounds__(RTPB_IMG) __attribute__((amdgpu_waves_per_eu(OCC2 ? 8 : 1))) k_rules_scan_img(
     const shr_table* __restrict__ RT, const int64_t* __restrict__ sts, const uint32_t* __restrict__ skeys, int64_t n,
     uint32_t sentinel, const shd_cols* __restrict__ C, uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
     uint32_t* __restrict__ rec_p, uint32_t* __restrict__ rec_q, uint32_t* __restrict__ rec_r, int32_t* __restrict__ flag,
@@ -317,7 +318,9 @@ static int rules_scan_img(const shr_table* dT, const int64_t* sts, const uint32_
                           const uint32_t* s32, int64_t tb) {
     static int attr_set = 0;  // the dynamic LDS limit, raised once per instantiation
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rules_scan_img<WRITE>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rules_scan_img<WRITE, 0>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, SHR_IMG_MAX) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rules_scan_img<WRITE, 1>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, SHR_IMG_MAX) != hipSuccess)
             return -3;
         attr_set = 1;
@@ -327,8 +330,13 @@ static int rules_scan_img(const shr_table* dT, const int64_t* sts, const uint32_
     const int64_t gmax = 256LL * (per_cu < 1 ? 1 : per_cu);
     if (g > gmax) g = gmax;
     if (g < 1) g = 1;
-    hipLaunchKernelGGL(k_rules_scan_img<WRITE>, dim3((unsigned)g), dim3(RTPB_IMG), (size_t)I.lds, st, dT, sts, skeys,
-                       n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, flag, img, I, s32, tb);
+    static const bool occ_on = !(getenv("SH_RULES_OCC2") && getenv("SH_RULES_OCC2")[0] == '0');
+    if (per_cu >= 2 && occ_on)
+        hipLaunchKernelGGL((k_rules_scan_img<WRITE, 1>), dim3((unsigned)g), dim3(RTPB_IMG), (size_t)I.lds, st, dT, sts,
+                           skeys, n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, flag, img, I, s32, tb);
+    else
+        hipLaunchKernelGGL((k_rules_scan_img<WRITE, 0>), dim3((unsigned)g), dim3(RTPB_IMG), (size_t)I.lds, st, dT, sts,
+                           skeys, n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, flag, img, I, s32, tb);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
