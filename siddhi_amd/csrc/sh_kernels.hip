@@ -300,7 +300,9 @@ __global__ void __launch_bounds__(TPB, (B <= 8 ? 4 : 3)) k_digit_scatter(const u
             }
             uint64_t* st64 = (uint64_t*)stage;
             constexpr uint32_t HALF = RADIX_TILE / 2;
-            for (uint32_t lo = 0; lo < (uint32_t)tile_n; lo += HALF) {  // uniform
+            // tile_n <= 0 for the padding tiles of arrival-tile-major order: no rounds
+            const uint32_t tn = tile_n > 0 ? (uint32_t)tile_n : 0u;
+            for (uint32_t lo = 0; lo < tn; lo += HALF) {  // uniform
 #pragma unroll
                 for (int j = 0; j < RADIX_ITEMS; j++)
                     if (wbase + j * 64 < n && lp[j] - lo < HALF) st64[lp[j] - lo] = v[j];
@@ -308,7 +310,7 @@ __global__ void __launch_bounds__(TPB, (B <= 8 ? 4 : 3)) k_digit_scatter(const u
 #pragma unroll
                 for (int m = 0; m < RADIX_ITEMS / 2; m++) {
                     const uint32_t l = lo + m * TPB + threadIdx.x;
-                    if (l < (uint32_t)tile_n) {
+                    if (l < tn) {
                         const uint32_t d = dig[l];
                         dst[gbase[d] + l - tstart[d]] = st64[l - lo];
                     }
