@@ -65,6 +65,9 @@ const int kWalkBlock = env_int("SH_BK_WALK", 4, 2, 16);
 // the count walk hands consumers out per lane (SH_BK_DYN=0: every lane of a wave
 // walks its consumer to the wave's longest walk)
 const int kWalkDyn = env_int("SH_BK_DYN", 1, 0, 1);
+// the bucketed matcher's launch bound: minimum workgroups per CU the register
+// allocation is sized for (its LDS holds two 512-thread workgroups per CU)
+const int kMatchMinBlocks = env_int("SH_BK_MINB", 4, 1, 8);
 
 const char* col_ctype(int t) {
     switch (t) {
@@ -1009,9 +1012,10 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     src += "\n#define SHJ_W " + lit64(P.within_ms) + "\n#define SHB_WLIM " + std::to_string(wlim) +
            "u\n#define SHB_TPB 512\n#define SHB_D " + std::to_string(kWalkBlock) +
            "\n#define SHB_MOVF 0x8000u\n#define SHB_MSTEPS 15\n"
+           "#define SHB_MINB " + std::to_string(kMatchMinBlocks) + "\n"
            "#define SHB_NR (SHB_SPAN / SHB_TPB)\nstatic_assert(SHB_SPAN % SHB_TPB == 0 && SHB_NR * SHB_TPB == SHB_SPAN, \"span\");\n";
     src += R"(
-extern "C" __global__ void __launch_bounds__(SHB_TPB, 4) shb_match(shb_plan P) {
+extern "C" __global__ void __launch_bounds__(SHB_TPB, SHB_MINB) shb_match(shb_plan P) {
 __shared__ uint32_t s_ws[SHB_SPAN];
 // the chunk's consumers in sorted order: sorted position | (arrival - hl) << 16
 __shared__ uint32_t s_cons[SHB_CH];
