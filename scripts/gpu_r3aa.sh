@@ -14,3 +14,5 @@ run minb2 SH_BK_MINB=2
 run minb3 SH_BK_MINB=3
 run minb2_w6 SH_BK_MINB=2 SH_BK_WALK=6
 run minb2_w8 SH_BK_MINB=2 SH_BK_WALK=8
+SH_BK_MINB=2 timeout -k 10 600 python -u -m pytest tests/test_gpu_bucket.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r3aa_bucket_minb2.log 2>&1 || { tail -30 gpurun_out/r3aa_bucket_minb2.log; exit 1; }
+tail -1 gpurun_out/r3aa_bucket_minb2.log
