@@ -405,7 +405,7 @@ def main_sharded(args, torch, dist, world, rank, dev):
     rdev = "cpu" if comm is not None else dev  # device of the timing / count reductions
 
     def one():
-        return step.run(d_ts, d_cols[0], d_cols, lo, K, key_attr=0, run_ids=d_run)
+        return step.run(d_ts, d_cols[0], d_cols, lo, K, key_attr=0, run_ids=d_run, batch=BATCH)
 
     log("warmup")
     for _ in range(args.warmup):

@@ -136,15 +136,16 @@ typedef struct sh_device_run {
     int64_t out_count;           /* out: matches produced                           */
     void* stream;                /* hipStream_t to run on (NULL = default)          */
     int32_t* d_out_query;        /* out (optional): query index per match (ordered) */
-    /* SH_DEVICE_RUN_V2 to have the fields below read. Zero-initialise the struct:
-       any other value (an older caller's struct) leaves them unread. */
-    int32_t version;
-    int32_t pad;
     /* out (optional): the select values as typed columns, one device pointer per
        output attribute in its natural width (long/double 8 B, int/float/string id
        4 B, bool 1 B), ordered like d_out_seq. When set, d_out_values may be NULL
        and is not written; the row-major raw layout stays the default. */
     void* const* d_out_cols;
+    /* ---- end of the V1 struct (96 bytes): sh_run_device reads only the fields
+       above. The fields below are read by sh_run_device_v2 alone, which requires
+       version == SH_DEVICE_RUN_V2. */
+    int32_t version;
+    int32_t pad;
     /* optional: the PartitionStreamReceiver run of every event (one run = the
        consecutive same-key events of one send() call,
        core/partition/PartitionStreamReceiver.java:176-216), as a non-decreasing
@@ -154,8 +155,12 @@ typedef struct sh_device_run {
     const uint32_t* d_run;
 } sh_device_run;
 #define SH_DEVICE_RUN_V2 2
+#define SH_DEVICE_RUN_V1_BYTES 96
 
+/* reads the V1 prefix of *run (SH_DEVICE_RUN_V1_BYTES) and writes out_count */
 int sh_run_device(sh_handle* h, sh_device_run* run);
+/* the whole struct; SH_E_INVALID_ARG unless run->version == SH_DEVICE_RUN_V2 */
+int sh_run_device_v2(sh_handle* h, sh_device_run* run);
 
 /* kernel timing of the last sh_run_device call (HIP events on run->stream) */
 typedef struct sh_kernel_times {

@@ -78,16 +78,20 @@ struct shd_window_ws {
 };
 
 // ---- bucketed window engine (sh_bucket.hip + the hipRTC matcher shb_match)
-// Partitioned `every e1=S[f1] -> e2=S[f2] within W`: events are moved once into
-// SHB_NB key buckets (bucket = key & (SHB_NB-1), arrival order kept inside a
-// bucket), the matcher walks each consumer's key back through an LDS-resident
-// chunk of its bucket, and the emitter restores arrival order per arrival tile.
+// Partitioned `every e1=S[f1] -> e2=S[f2] within W`: each arrival tile of
+// SHB_TILE events is stably reordered by key bucket (bucket = key & (SHB_NB-1))
+// in its own region (the tile's bucket order: tile-local, no global pass), the
+// matcher gathers one bucket's segments of a run of tiles (plus halo tiles that
+// cover the window) into LDS and walks each consumer's key back, and the
+// emitter restores arrival order per tile.
 #define SHB_NB 256
 #define SHB_TILE_SHIFT 13
 #define SHB_TILE (1 << SHB_TILE_SHIFT)
-#define SHB_CH 4096
-#define SHB_HALO 1024
-#define SHB_SPAN (SHB_CH + SHB_HALO)
+#define SHB_CH 4096       // chunk (consumer) events of one matcher pass, at most
+#define SHB_SPAN 5120     // chunk + halo events staged in LDS, at most
+#define SHB_TOFF 264      // u16 stride of a tile's bucket-start row (257 used)
+#define SHB_HMAX 64       // halo tiles before a chunk, at most
+#define SHB_CT_MAX 160    // tiles per matcher chunk, at most
 #define SHB_MAX_STAGED 4
 #define SHB_MAX_MS 4
 #define SHB_MAX_OUT 16
@@ -97,30 +101,33 @@ struct shd_window_ws {
 #define SHB_F_MONO 4      // timestamps decrease inside a key
 #define SHB_F_COUNT 8     // one consumer takes > 255 partials
 #define SHB_F_HALO 16     // a walk reached the halo start
+#define SHB_F_SPAN 32     // one tile's bucket segment exceeds a chunk
 
 struct shb_plan {
     int64_t n;
     int64_t tbase;            // packed ts = ts - tbase in the high (32 - kb) bits of w0
     int32_t nt;               // arrival tiles of SHB_TILE events
     int32_t kb;               // local key bits: w0 low bits = key >> log2(SHB_NB)
-    int32_t grid_g;           // matcher grid = SHB_NB * grid_g; a workgroup takes chunks c, c + grid_g, ...
-    int64_t n_gch;            // matcher chunk ids: chunk c of bucket b = bs / SHB_CH + c + b
+    int32_t ct;               // arrival tiles per matcher chunk (<= SHB_CT_MAX)
+    int32_t n_chunks;         // matcher grid = SHB_NB * n_chunks
     int32_t n_staged;
     int32_t pad;
     const void* st_src[SHB_MAX_STAGED];  // arrival-order columns moved into bucket order
     void* st_dst[SHB_MAX_STAGED];
     int32_t st_width[SHB_MAX_STAGED];
     int32_t n_ms;             // match-stream columns (e1-side select values)
-    void* ms[SHB_MAX_MS];     // [n_gch * SHB_SPAN] each, natural width
+    void* ms[SHB_MAX_MS];     // [n] each, natural width; regions taken per matcher pass
     int32_t ms_width[SHB_MAX_MS];
-    uint32_t* w0;             // bucket order: packed ts | local key
-    uint16_t* rk;             // arrival order: rank of the event inside its (tile, bucket) segment
-    uint32_t* base;           // [SHB_NB * nt + 1]: (bucket, tile) counts -> exclusive scan
-    uint8_t* cnt;             // bucket order: partials consumed per event
-    uint32_t* psum;           // [SHB_NB * nt]: within-chunk prefix at each (bucket, tile) segment start
-    uint32_t* ctot;           // [n_gch + 1]: matches per matcher chunk -> exclusive scan
-    uint32_t* cum;            // [SHB_NB * (nt + 1)]: matches of a bucket before each segment
+    const int64_t* ts;        // arrival-order timestamps (tile first timestamps: the halo)
+    const int32_t* keys;      // arrival-order partition keys
+    uint32_t* w0;             // tiles' bucket order: packed ts | local key
+    uint16_t* sp;             // arrival order: the event's slot in its tile's bucket order
+    uint16_t* toff;           // [nt][SHB_TOFF]: bucket starts in the tile's bucket order ([256]: valid events)
+    uint8_t* cnt;             // tiles' bucket order: partials consumed per event
+    uint32_t* mstart;         // [nt][SHB_NB]: match-stream position of each (tile, bucket) segment's first match
     uint32_t* ttot;           // [nt + 1]: matches per arrival tile -> exclusive scan
+    uint32_t* ms_ctr;         // match-stream region allocator
+    int64_t* tpre;            // [nt]: latest timestamp of each tile -> of all tiles before it
     int32_t* flag;
     unsigned long long* prof; // diagnostics (SH_BK_PROFILE): clock ticks per matcher phase, NULL off
 };
@@ -183,11 +190,10 @@ int shd_sort_pairs(const uint32_t* keys, const uint32_t* vals, int64_t n, int bi
                    const uint32_t** keys_out, const uint32_t** vals_out);
 int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, void* stream);
 // bucketed window engine launch steps (sh_bucket.hip), all async on `stream`
-int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_plan* P, uint32_t* scan_tmp,
-                  void* stream);
+int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_plan* P, void* stream);
 int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream);
-int shb_emit(const int32_t* keys, const shb_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base,
-             uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream);
+int shb_emit(const shb_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base, uint64_t* out_seq,
+             int64_t* out_vals, int64_t out_cap, void* stream);
 // raw 8-byte rows [m x n_out] -> typed columns of widths w[o] (8, 4 or 1 bytes)
 int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, void* const* cols, const int32_t* w, void* stream);
 #ifdef __cplusplus

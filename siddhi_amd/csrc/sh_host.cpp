@@ -479,7 +479,7 @@ struct sh_handle {
     int bk_last = 0;          // 1: the last sh_run_device ran on the bucketed engine
     shj_bucket bk{};
     std::string bk_err;
-    DevBuf bk_w0, bk_rk, bk_base, bk_cnt, bk_psum, bk_ctot, bk_cum, bk_ttot, bk_flag, bk_prof;
+    DevBuf bk_w0, bk_sp, bk_toff, bk_cnt, bk_mstart, bk_tpre, bk_ttot, bk_flag, bk_prof;
     DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS];
     PinBuf bk_rd;
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
@@ -2795,30 +2795,36 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     hipStream_t st = h->stream;
     shb_plan B;
     memset(&B, 0, sizeof(B));
+    if (n >= ((int64_t)1 << 32) - SHB_TILE) return 1;  // event indices are 32-bit on this engine
     B.n = n;
     B.nt = (int32_t)((n + SHB_TILE - 1) / SHB_TILE);
     B.kb = kb;
-    B.n_gch = n / SHB_CH + SHB_NB + 2;
-    B.grid_g = (int32_t)((n / SHB_NB + SHB_CH - 1) / SHB_CH) + 2;
-    const int64_t cells = (int64_t)SHB_NB * B.nt;
-    if (ensure_ws(h, std::max<int64_t>(n, cells + 1)) || h->bk_w0.ensure_fresh(n * 4) || h->bk_rk.ensure_fresh(n * 2) ||
-        h->bk_base.ensure_fresh((cells + 1) * 4) || h->bk_cnt.ensure_fresh(n) || h->bk_psum.ensure_fresh(cells * 4) ||
-        h->bk_ctot.ensure_fresh((B.n_gch + 1) * 4) || h->bk_cum.ensure_fresh((cells + SHB_NB) * 4) ||
-        h->bk_ttot.ensure_fresh((B.nt + 1) * 4) || h->bk_flag.ensure_fresh(64) || h->bk_rd.ensure(64))
+    // tiles per matcher chunk: 3,584 events of a bucket at uniform keys (32 per
+    // tile), so a chunk and its halo fit the LDS span; denser buckets split
+    static const int ct_env = getenv("SH_BK_CT") ? atoi(getenv("SH_BK_CT")) : 0;
+    B.ct = ct_env > 0 ? std::min(ct_env, SHB_CT_MAX) : 112;
+    B.n_chunks = (B.nt + B.ct - 1) / B.ct;
+    const int64_t slots = (int64_t)B.nt * SHB_TILE;  // the tiles' bucket order
+    if (ensure_ws(h, std::max<int64_t>(n, (int64_t)B.nt + 1)) || h->bk_w0.ensure_fresh(slots * 4) ||
+        h->bk_sp.ensure_fresh(n * 2) || h->bk_toff.ensure_fresh((int64_t)B.nt * SHB_TOFF * 2) ||
+        h->bk_cnt.ensure_fresh(slots) || h->bk_mstart.ensure_fresh((int64_t)B.nt * SHB_NB * 4) ||
+        h->bk_tpre.ensure_fresh((int64_t)B.nt * 8) || h->bk_ttot.ensure_fresh(((int64_t)B.nt + 1) * 4) ||
+        h->bk_flag.ensure_fresh(64) || h->bk_rd.ensure(64))
         return fail(h, SH_E_OOM, "bucket workspace");
     B.n_staged = h->bk.n_staged;
     for (int k = 0; k < B.n_staged; k++) {
         const int a = h->bk.staged_attr[k];
         const int w = type_width(P.attr_type[0][a]);
-        if (h->bk_st[k].ensure_fresh(n * w)) return fail(h, SH_E_OOM, "bucket workspace");
+        if (h->bk_st[k].ensure_fresh(slots * w)) return fail(h, SH_E_OOM, "bucket workspace");
         B.st_src[k] = run->d_cols[a];
         B.st_dst[k] = h->bk_st[k].p;
         B.st_width[k] = w;
     }
+    // match stream: every partial is consumed at most once, so n values suffice
     B.n_ms = n_ms;
     for (int m = 0; m < n_ms; m++) {
         const int w = type_width(P.attr_type[0][ms[m]]);
-        if (h->bk_ms[m].ensure_fresh(B.n_gch * SHB_SPAN * w)) return fail(h, SH_E_OOM, "match stream");
+        if (h->bk_ms[m].ensure_fresh(n * w)) return fail(h, SH_E_OOM, "match stream");
         B.ms[m] = h->bk_ms[m].p;
         B.ms_width[m] = w;
     }
@@ -2833,15 +2839,17 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
             OC.colw[o] = type_width(O.type[o]);
         }
     }
+    B.ts = run->d_ts;
+    B.keys = run->d_keys;
     B.w0 = h->bk_w0.as<uint32_t>();
-    B.rk = h->bk_rk.as<uint16_t>();
-    B.base = h->bk_base.as<uint32_t>();
+    B.sp = h->bk_sp.as<uint16_t>();
+    B.toff = h->bk_toff.as<uint16_t>();
     B.cnt = h->bk_cnt.as<uint8_t>();
-    B.psum = h->bk_psum.as<uint32_t>();
-    B.ctot = h->bk_ctot.as<uint32_t>();
-    B.cum = h->bk_cum.as<uint32_t>();
+    B.mstart = h->bk_mstart.as<uint32_t>();
+    B.tpre = h->bk_tpre.as<int64_t>();
     B.ttot = h->bk_ttot.as<uint32_t>();
     B.flag = h->bk_flag.as<int32_t>();
+    B.ms_ctr = h->bk_flag.as<uint32_t>() + 4;
     static const bool prof = getenv("SH_BK_PROFILE") != nullptr;
     if (prof) {
         if (h->bk_prof.ensure_fresh(128)) return fail(h, SH_E_OOM, "profile");
@@ -2853,18 +2861,17 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "bucket: timestamp read");
     B.tbase = *h->bk_rd.as<int64_t>() - ((int64_t)1 << (31 - kb));
     hipEventRecord(h->ev[0], st);
-    hipMemsetAsync(B.flag, 0, 4, st);
-    hipMemsetAsync(B.ctot, 0, (B.n_gch + 1) * 4, st);
-    if (shb_partition(run->d_keys, run->d_ts, nkeys, &B, h->w_scan.as<uint32_t>(), st))
-        return fail(h, SH_E_HIP, "bucket partition launch failed");
+    hipMemsetAsync(B.flag, 0, 32, st);  // flag word + match-stream allocator
+    hipMemsetAsync(B.ttot, 0, ((int64_t)B.nt + 1) * 4, st);
+    if (shb_partition(run->d_keys, run->d_ts, nkeys, &B, st)) return fail(h, SH_E_HIP, "bucket partition launch failed");
     hipEventRecord(h->ev[1], st);
     void* args[] = {&B};
-    if (hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.grid_g), 1, 1, 512, 1, 1, 0, st,
+    if (hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.n_chunks), 1, 1, 512, 1, 1, 0, st,
                               args, nullptr) != hipSuccess)
         return fail(h, SH_E_HIP, "shb_match launch failed");
     if (shb_finish(&B, h->w_scan.as<uint32_t>(), st)) return fail(h, SH_E_HIP, "bucket scan launch failed");
     hipEventRecord(h->ev[2], st);
-    if (shb_emit(run->d_keys, &B, &O, &OC, 0, run->d_out_seq, run->d_out_values, run->out_capacity, st))
+    if (shb_emit(&B, &O, &OC, 0, run->d_out_seq, run->d_out_values, run->out_capacity, st))
         return fail(h, SH_E_HIP, "bucket emit launch failed");
     hipEventRecord(h->ev[3], st);
     hipMemcpyAsync(h->bk_rd.as<void>(0), B.flag, 4, hipMemcpyDeviceToHost, st);
@@ -3165,20 +3172,34 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
 
 static int run_device_cols(sh_handle* h, sh_device_run* run);
 
-int sh_run_device(sh_handle* h, sh_device_run* user) {
+static_assert(offsetof(sh_device_run, version) == SH_DEVICE_RUN_V1_BYTES, "V1 prefix of sh_device_run");
+
+static int run_device_entry(sh_handle* h, sh_device_run* user, bool v2) {
     if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !user) return SH_E_INVALID_ARG;
-    // the V2 fields are read only from a struct that says it has them
     if (h->has_lists) return fail(h, SH_E_UNSUPPORTED, "List (multi-value) outputs come back through sh_drain");
-    sh_device_run r = *user;
-    if (r.version != SH_DEVICE_RUN_V2) {
-        r.d_out_cols = nullptr;
-        r.d_run = nullptr;
+    // a V1 caller's struct ends before `version`: only its prefix is read
+    // the run borrows the caller's stream; the handle's own stream is back for
+    // every later call (push, advance, drain), whatever path this one leaves by
+    struct StreamGuard {
+        sh_handle* h;
+        ~StreamGuard() { h->stream = h->own_stream; }
+    } guard{h};
+    sh_device_run r;
+    memset(&r, 0, sizeof(r));
+    if (v2) {
+        if (user->version != SH_DEVICE_RUN_V2) return fail(h, SH_E_INVALID_ARG, "sh_run_device_v2: version");
+        r = *user;
+    } else {
+        memcpy(&r, user, SH_DEVICE_RUN_V1_BYTES);
     }
     const int rc = run_device_cols(h, &r);
     user->out_count = r.out_count;
     return rc;
 }
+
+int sh_run_device(sh_handle* h, sh_device_run* user) { return run_device_entry(h, user, false); }
+int sh_run_device_v2(sh_handle* h, sh_device_run* user) { return run_device_entry(h, user, true); }
 
 static int run_device_cols(sh_handle* h, sh_device_run* run) {
     if (!run->d_out_cols) return run_device_impl(h, run);

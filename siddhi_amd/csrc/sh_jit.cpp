@@ -865,7 +865,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
         s += "    {\n" + mid_fast + "    }\n    {\n    const uint32_t st = (act && (" + stop_cond +
              ")) ? 1u : 0u;\n    stopped |= st;\n    live = act & (st ^ 1u);\n    }\n}\n}\n"
              "if (mono) atomicOr(P.flag, SHB_F_MONO);\n";
-        s += "if (!stopped && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n";
+        s += "if (!stopped && SHB_OFF(tq)) atomicOr(P.flag, SHB_F_HALO);\n";
         return s;
     };
     // the count walk for a floating-point ordering term: ext starts as NaN (no
@@ -915,7 +915,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
                                                                                   : std::to_string(SH_OP_LE)) +
              ", Mx, xq) ? 0u : 1u);\n}\n}\n"
              "c_ = (uint32_t)__popc(mask & ~SHB_MOVF) + cext;\n"
-             "if (roff && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n";
+             "if (roff && SHB_OFF(tq32)) atomicOr(P.flag, SHB_F_HALO);\n";
         return s;
     };
     // the same float-domain count walk with work handed out per lane: a wave owns a
@@ -946,7 +946,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
             "for (;;) {\n"
             "    if (ci >= 0 && !live) {\n"
             "        const uint32_t c_ = (uint32_t)__popc(mask & ~SHB_MOVF) + cext;\n"
-            "        if (roff && hs > 0) atomicOr(P.flag, SHB_F_HALO);\n"
+            "        if (roff && SHB_OFF(wq >> kb)) atomicOr(P.flag, SHB_F_HALO);\n"
             "        if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);\n"
             "        s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);\n"
             "        s_msk[i - hl] = (uint16_t)mask;\n"
@@ -1013,7 +1013,9 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
            "u\n#define SHB_TPB 512\n#define SHB_D " + std::to_string(kWalkBlock) +
            "\n#define SHB_MOVF 0x8000u\n#define SHB_MSTEPS 15\n"
            "#define SHB_MINB " + std::to_string(kMatchMinBlocks) + "\n"
-           "#define SHB_NR (SHB_SPAN / SHB_TPB)\nstatic_assert(SHB_SPAN % SHB_TPB == 0 && SHB_NR * SHB_TPB == SHB_SPAN, \"span\");\n";
+           "#define SHB_NSEG (SHB_CT_MAX + SHB_HMAX)\n"
+           "#define SHB_NR (SHB_SPAN / SHB_TPB)\nstatic_assert(SHB_SPAN % SHB_TPB == 0 && SHB_NR * SHB_TPB == SHB_SPAN, \"span\");\n"
+           "static_assert(SHB_NSEG < 256 && SHB_NSEG < SHB_TPB, \"segments\");\n";
     src += R"(
 extern "C" __global__ void __launch_bounds__(SHB_TPB, SHB_MINB) shb_match(shb_plan P) {
 __shared__ uint32_t s_ws[SHB_SPAN];
@@ -1026,6 +1028,13 @@ uint16_t* const s_msk = (uint16_t*)u_buf;
 static_assert((SHB_TPB / 64) * 256 * 4 >= SHB_CH * 2, "masks fit u_buf");
 // run: halo events per local key, then their inclusive prefix over the keys
 __shared__ uint32_t run[256], tstart[256], ws[SHB_TPB / 64];
+// the pass's segments, one per tile from the first halo tile: start in span
+// order (exclusive prefix of the lengths, from the table's first tile) and the
+// global index of the first event; seg_of[j]: segment of span event 32 j
+__shared__ uint32_t seg_p[SHB_NSEG + 1];
+__shared__ uint32_t seg_g[SHB_NSEG];
+__shared__ uint8_t seg_of[SHB_SPAN / 32];
+__shared__ int s_i[2];
 )";
     for (int a : staged_out)
         src += "__shared__ " + std::string(col_ctype(P.attr_type[0][a])) + " " + lds(a) + "[SHB_SPAN];\n";
@@ -1036,26 +1045,98 @@ __shared__ uint32_t run[256], tstart[256], ws[SHB_TPB / 64];
                std::to_string(k) + "];\n";
     }
     src += R"(
-const int b = (int)(blockIdx.x % SHB_NB);
-const uint32_t bs = P.base[(int64_t)b * P.nt];
-const int64_t nb = (int64_t)P.base[(int64_t)(b + 1) * P.nt] - bs;
+// consecutive buckets on one XCD (blocks are dealt round-robin to the 8 XCDs):
+// neighbouring segments of a tile share cache lines
+const int b = (int)((blockIdx.x & 7u) * (SHB_NB / 8) + ((blockIdx.x >> 3) & (SHB_NB / 8 - 1)));
+const int A = (int)(blockIdx.x / SHB_NB) * P.ct;
+const int E = A + P.ct < P.nt ? A + P.ct : P.nt;
 const int kb = P.kb;
 const uint32_t kmask = (1u << kb) - 1u;
-const uint32_t* __restrict__ row = P.base + (int64_t)b * P.nt;
-for (int64_t c = blockIdx.x / SHB_NB; c * SHB_CH < nb; c += P.grid_g) {
-const int64_t cs = c * SHB_CH;
-const int64_t hs = cs > SHB_HALO ? cs - SHB_HALO : 0;
-const int64_t he = (cs + SHB_CH < nb) ? cs + SHB_CH : nb;
-const int L = (int)(he - hs), hl = (int)(cs - hs), nc = L - hl;
-__syncthreads();
-if (threadIdx.x < 256) run[threadIdx.x] = 0u;
+const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
+for (int a = A; a < E;) {
 __syncthreads();
 unsigned long long t_prev = wall_clock64();
 #define SHB_PROF(ph) if (P.prof && threadIdx.x == 0) { const unsigned long long t_now = wall_clock64(); atomicAdd(&P.prof[ph], t_now - t_prev); t_prev = t_now; }
-// the chunk and its halo into registers (all loads in flight together): wave v
-// owns the contiguous events [v * SHB_NR * 64, (v + 1) * SHB_NR * 64)
-const uint32_t* __restrict__ gw = P.w0 + (int64_t)bs + hs;
-const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
+// halo: tile a - 1, and before it every tile whose successor starts within W
+// of tile a's first event (for streams in time order: every tile that can
+// hold an event the window reaches); a walk that needs more raises SHB_F_HALO
+if (threadIdx.x < 64) {
+    const int t = (int)threadIdx.x;
+    bool ok = false;
+    if (t >= 1 && a - t >= 0) {
+        const int64_t ta_ = P.ts[(int64_t)a << SHB_TILE_SHIFT];
+        const int64_t tlim = ta_ < INT64_MIN + SHJ_W ? INT64_MIN : ta_ - SHJ_W;
+        ok = P.ts[(int64_t)(a - t) << SHB_TILE_SHIFT] >= tlim;
+    }
+    const uint64_t m = __ballot(ok);
+    if (t == 0) {
+        int h = 1 + (int)__builtin_ctzll(~(m >> 1));
+        if (h > a) h = a;
+        if (h > SHB_HMAX) h = SHB_HMAX;
+        s_i[0] = a - h;
+    }
+}
+__syncthreads();
+const int h0 = s_i[0];  // first tile of the segment table
+const int nseg = E - h0;
+{
+    uint32_t len = 0u, g = 0u;
+    if ((int)threadIdx.x < nseg) {
+        const int T = h0 + (int)threadIdx.x;
+        const uint16_t* r = P.toff + (int64_t)T * SHB_TOFF + b;
+        const uint32_t lo = r[0], hi = r[1];
+        len = hi - lo;
+        g = ((uint32_t)T << SHB_TILE_SHIFT) + lo;
+    }
+    uint32_t tot;
+    const uint32_t pre = shw_block_excl<SHB_TPB>(len, ws, &tot);
+    if ((int)threadIdx.x < nseg) {
+        seg_p[threadIdx.x] = pre;
+        seg_g[threadIdx.x] = g;
+    }
+    if ((int)threadIdx.x == nseg) seg_p[nseg] = tot;
+}
+__syncthreads();
+// this pass: consumers from tiles [a, a + ne), at most SHB_CH events; the halo
+// from segment sb on (trimmed at the front when it and tile a overflow the span)
+const int ta = a - h0;
+const uint32_t pa = seg_p[ta];
+const int sb = __syncthreads_count((int)threadIdx.x < ta && seg_p[ta + 1] - seg_p[threadIdx.x] > SHB_SPAN);
+const uint32_t sbase = seg_p[sb];
+const int ne = __syncthreads_count((int)threadIdx.x >= ta && (int)threadIdx.x < nseg &&
+                                   seg_p[threadIdx.x + 1] - pa <= SHB_CH &&
+                                   seg_p[threadIdx.x + 1] - sbase <= SHB_SPAN);
+if (ne == 0) {
+    // tile a's segment alone exceeds a chunk
+    if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_SPAN);
+    a++;
+    continue;
+}
+const int se = ta + ne;      // one past the pass's last segment
+const int hs = h0 + sb;      // the span's first tile (> 0: earlier events exist)
+const int L = (int)(seg_p[se] - sbase), hl = (int)(pa - sbase), nc = L - hl;
+// a walk that leaves its key's run in the span while still in the window could
+// have missed earlier events of the key only if some event before the span is
+// as late as the window's start (tpre: the latest timestamp before each tile)
+const int64_t tmx_ = hs > 0 ? P.tpre[hs] - P.tbase : INT64_MIN;
+#define SHB_OFF(t32) ((int64_t)(t32) - SHJ_W <= tmx_)
+for (int j = (int)threadIdx.x; j * 32 < L; j += SHB_TPB) {
+    const uint32_t e = sbase + (uint32_t)j * 32u;
+    int lo = sb, hi = se - 1;  // the last segment starting at or before e
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (seg_p[mid] <= e) lo = mid;
+        else hi = mid - 1;
+    }
+    seg_of[j] = (uint8_t)lo;
+}
+__syncthreads();
+// global index of span event i (segments in span order)
+#define SHB_GIDX(i, out) { int sg_ = seg_of[(i) >> 5]; while (seg_p[sg_ + 1] - sbase <= (uint32_t)(i)) sg_++; \
+    out = seg_g[sg_] + ((uint32_t)(i) - (seg_p[sg_] - sbase)); }
+if (threadIdx.x < 256) run[threadIdx.x] = 0u;
+// the span into registers (all loads in flight together): wave v owns the
+// contiguous span events [v * SHB_NR * 64, (v + 1) * SHB_NR * 64)
 uint32_t wr[SHB_NR];
 )";
     for (int a : staged_out)
@@ -1063,10 +1144,12 @@ uint32_t wr[SHB_NR];
     src += R"(#pragma unroll
 for (int k = 0; k < SHB_NR; k++) {
     const int i = (wv * SHB_NR + k) * 64 + lane;
-    wr[k] = i < L ? gw[i] : 0u;
+    uint32_t gi = 0u;
+    if (i < L) SHB_GIDX(i, gi)
+    wr[k] = i < L ? P.w0[gi] : 0u;
 )";
     for (int a : staged_out)
-        src += "    vr" + std::to_string(a) + "[k] = i < L ? g_a" + std::to_string(a) + "[(int64_t)bs + hs + i] : 0;\n";
+        src += "    vr" + std::to_string(a) + "[k] = i < L ? g_a" + std::to_string(a) + "[gi] : 0;\n";
     src += R"(}
 for (int c = (int)threadIdx.x; c < (SHB_TPB / 64) * 256; c += SHB_TPB) (&wcnt[0][0])[c] = 0u;
 __syncthreads();
@@ -1157,58 +1240,45 @@ __syncthreads();)";
     }
     src += R"(
 SHB_PROF(2)
-// exclusive prefix of the counts over the chunk (arrival order inside the
-// bucket); the counts go out as bytes, 8 per thread
+// the counts to the events' slots; their exclusive prefix over the chunk
+// (arrival order inside the bucket)
 uint32_t total;
 {
     const int p0 = (int)threadIdx.x * (SHB_CH / SHB_TPB);
     uint32_t v[SHB_CH / SHB_TPB];
     uint32_t sum = 0;
-    uint64_t packed = 0;
 #pragma unroll
     for (int q = 0; q < SHB_CH / SHB_TPB; q++) {
         v[q] = (p0 + q < nc) ? (uint32_t)s_pre[p0 + q] : 0u;
         sum += v[q];
-        packed |= (uint64_t)v[q] << (8 * q);
     }
     uint32_t off = shw_block_excl<SHB_TPB>(sum, ws, &total);
-    if (p0 + (SHB_CH / SHB_TPB) <= nc && (((int64_t)bs + cs + p0) & 7) == 0) {
-        *(uint64_t*)(P.cnt + (int64_t)bs + cs + p0) = packed;
-    } else {
-        for (int q = 0; q < SHB_CH / SHB_TPB; q++)
-            if (p0 + q < nc) P.cnt[(int64_t)bs + cs + p0 + q] = (uint8_t)v[q];
-    }
 #pragma unroll
     for (int q = 0; q < SHB_CH / SHB_TPB; q++) {
-        if (p0 + q < nc) s_pre[p0 + q] = (uint16_t)off;
+        if (p0 + q < nc) {
+            uint32_t gi;
+            SHB_GIDX(hl + p0 + q, gi)
+            P.cnt[gi] = (uint8_t)v[q];
+            s_pre[p0 + q] = (uint16_t)off;
+        }
         off += v[q];
     }
 }
+// the pass's match-stream region
+if (threadIdx.x == 0) s_i[1] = total ? (int)atomicAdd(P.ms_ctr, total) : 0;
 __syncthreads();
-const int64_t gch = (int64_t)(bs / SHB_CH) + c + b;
-if (threadIdx.x == 0) P.ctot[gch] = total;
-// prefix at every (bucket, tile) segment start inside the chunk: first tile
-// whose segment starts at or after cs (two parallel search rounds)
-{
-    const int stride = (P.nt + SHB_TPB - 1) / SHB_TPB;
-    const int tc = (int)threadIdx.x * stride;
-    const int n1 = __syncthreads_count(tc < P.nt && (int64_t)(row[tc] - bs) < cs);
-    int t0 = 0;
-    if (n1 > 0) {
-        const int lo = (n1 - 1) * stride;
-        const int tf = lo + 1 + (int)threadIdx.x;
-        const int n2 = __syncthreads_count((int)threadIdx.x < stride && tf < P.nt && (int64_t)(row[tf] - bs) < cs);
-        t0 = lo + 1 + n2;
-    }
-    for (int T = t0 + (int)threadIdx.x; T < P.nt; T += SHB_TPB) {
-        const int64_t x = (int64_t)(row[T] - bs);
-        if (x >= he) break;
-        P.psum[(int64_t)b * P.nt + T] = s_pre[x - cs];
-    }
+const int64_t rbase = (int64_t)(uint32_t)s_i[1];
+// per chunk tile: the first match position of its segment, its matches
+for (int t = ta + (int)threadIdx.x; t < se; t += SHB_TPB) {
+    const uint32_t x0 = seg_p[t] - pa, x1 = seg_p[t + 1] - pa;
+    const uint32_t q0 = x0 < (uint32_t)nc ? (uint32_t)s_pre[x0] : total;
+    const uint32_t q1 = x1 < (uint32_t)nc ? (uint32_t)s_pre[x1] : total;
+    const int T = h0 + t;
+    P.mstart[(int64_t)T * SHB_NB + b] = (uint32_t)rbase + q0;
+    if (q1 > q0) atomicAdd(&P.ttot[T], q1 - q0);
 }
 SHB_PROF(3)
-// the partials again, their e1-side select values into the chunk's region
-const int64_t rbase = gch * SHB_SPAN;
+// the partials again, their e1-side select values into the region
 for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {
 const uint32_t cw = s_cons[ci];
 const int sp = (int)(cw & 0xFFFFu), i = hl + (int)(cw >> 16);
@@ -1223,8 +1293,7 @@ uint32_t k = 0;
            "    while (m) {\n        const int o = sp - __ffs(m);\n        m &= m - 1u;\n"
            "        const int64_t dst = rbase + (int64_t)off + (int64_t)(cn - 1u - k);\n        k++;\n" +
            ms_put + "    }\n} else {\n" + walk(false, put) + "}\n";
-    src += "}\n__syncthreads();\n";
-    src += "SHB_PROF(4)\n}\n}\n";
+    src += "}\nSHB_PROF(4)\na += ne;\n}\n}\n";
     return true;
 }
 

@@ -84,7 +84,7 @@ class DeviceRunner:
                 r.d_out_cols = ocp
             r.stream = stream.cuda_stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
             r.d_out_query = self.out_q.data_ptr() if with_query else None
-            rc = lib().sh_run_device(self.handle.h, C.byref(r))
+            rc = lib().sh_run_device_v2(self.handle.h, C.byref(r))
             if rc == abi.SH_E_MORE and attempt == 0 and int(r.out_count) > self._out_cap:
                 # more matches than events: grow the output to the reported count and rerun
                 cap = int(r.out_count)

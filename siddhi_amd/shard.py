@@ -222,7 +222,7 @@ class KeyShardedStep:
         self.comm = comm if comm is not None else TorchComm(world)
         self.last = {}
 
-    def run(self, ts, keys, cols, seq0, n_keys, key_attr=None, run_ids=None):
+    def run(self, ts, keys, cols, seq0, n_keys, key_attr=None, run_ids=None, batch=None):
         """ts / keys / cols: this rank's ingest slice (arrival order), seq0 its
         first global sequence number; key_attr: index of the attribute column
         that holds the partition key ids (then `keys` travels once); run_ids
@@ -230,7 +230,11 @@ class KeyShardedStep:
         the matcher as `run=` (apps whose output order depends on the
         PartitionStreamReceiver runs, e.g. several queries in one partition).
         Returns (seq[m], values[m, n_out]) of the rows triggered by the slice's
-        events, in the reference's order."""
+        events, in the reference's order. batch: events per send() call; with
+        run_ids the slice must start at a call boundary (a run never spans two
+        ranks' slices), which is checked when batch is given."""
+        if run_ids is not None and batch:
+            assert seq0 % batch == 0, "run ids need ingest slices cut at send() call boundaries"
         dev = ts.device
         world = self.world
         # 1. route + pack (columns: ts, [keys,] then the attribute columns[, run ids])
@@ -265,7 +269,9 @@ class KeyShardedStep:
         # one run stay in the matcher's order, e.g. query-major inside the run, and
         # a run lives on one owner; its rows are grouped by source rank as long as
         # the ingest slices cut the stream at send() call boundaries)
-        mkey = r_run[oseq].to(oseq.dtype) if r_run is not None else None
+        # (run ids are uint32 carried in int32 lanes: zero-extended, so slices past
+        # 2^31 events keep their order)
+        mkey = (r_run[oseq].to(oseq.dtype) & 0xFFFFFFFF) if r_run is not None else None
         row_counts = self.ops.rows_home(oseq, m, 0, gseq, src_off, world)
         back_counts = self.comm.counts(row_counts, dev)
         n_val = self.n_out

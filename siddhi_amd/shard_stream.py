@@ -81,6 +81,11 @@ class ThreadComm:
     def view(self, rank):
         return _ThreadView(self, rank)
 
+    def abort(self):
+        """a failed rank breaks the barrier: every other rank's pending or next
+        all_gather raises BrokenBarrierError (its call fails) instead of waiting"""
+        self.bar.abort()
+
 
 class _ThreadView:
     def __init__(self, comm, rank):
@@ -93,6 +98,9 @@ class _ThreadView:
         out = [s.copy() for s in c.slots]
         c.bar.wait()  # every rank has read before the slots are reused
         return out
+
+    def abort(self):
+        self.c.abort()
 
 
 _CAND = np.dtype([("t", np.int64), ("order", np.uint64), ("key", np.int32), ("pad", np.int32)])
@@ -124,7 +132,17 @@ def pick(parts, wall):
 
 class Coordinator:
     """The sh_coordinator callbacks of one rank over `comm` (all_gather of int64
-    arrays). Exceptions inside a callback are kept and reported as a failed call."""
+    arrays). Exceptions inside a callback are kept and reported as a failed call;
+    the comm is aborted too (ThreadComm: the barrier breaks, so the other ranks'
+    calls fail instead of waiting; gloo: the peers' collectives fail at the
+    process group's timeout, `init_process_group(timeout=...)`)."""
+
+    def _fail(self, e):
+        self.error = e
+        abort = getattr(self.comm, "abort", None)
+        if abort is not None:
+            abort()
+        return 1
 
     def __init__(self, comm):
         self.comm = comm
@@ -150,8 +168,7 @@ class Coordinator:
             self.exchanges += 1
             return 0
         except Exception as e:  # noqa: BLE001 (reported to the handle as a failure)
-            self.error = e
-            return 1
+            return self._fail(e)
 
     def _select(self, user, wall, cand, n_local, pos_p, n_fire_p):
         try:
@@ -169,8 +186,7 @@ class Coordinator:
             self.exchanges += 1
             return 0
         except Exception as e:  # noqa: BLE001
-            self.error = e
-            return 1
+            return self._fail(e)
 
     def _min_time(self, user, local, out_p):
         try:
@@ -178,8 +194,7 @@ class Coordinator:
             out_p[0] = int(min(int(p[0]) for p in parts))
             return 0
         except Exception as e:  # noqa: BLE001
-            self.error = e
-            return 1
+            return self._fail(e)
 
 
 class ShardedStreamEngine:
@@ -215,7 +230,10 @@ class ShardedStreamEngine:
         n = len(ts)
         if n == 0:
             return
-        idx = np.flatnonzero(self.owner(keys) == self.rank) if keys is not None else np.arange(n)
+        if keys is not None:
+            idx = np.flatnonzero(self.owner(keys) == self.rank)
+        else:  # a stream without a key: null-key events, owned like keys < 0
+            idx = np.arange(n) if self.rank == self.null_key_rank else np.zeros(0, np.int64)
         self.eng.send_part(stream, ts[idx], [c[idx] for c in cols],
                            [None if m is None else m[idx] for m in nulls],
                            None if keys is None else keys[idx], idx.astype(np.uint32), n, int(ts[-1]))

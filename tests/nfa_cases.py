@@ -18,13 +18,18 @@ def _filter(rng, k, aliases):
     refs = [a for a in aliases if a[0] < k]
     if refs:
         a, cnt = rng.choice(refs)[1:]
-        idx = rng.choice(["", "[0]", "[last]"]) if cnt else ""
+        # a count state's attribute always indexed: without an index it is a List
+        # (MultiValueVariableFunctionExecutor), which no filter expression takes
+        idx = rng.choice(["[0]", "[last]"]) if cnt else ""
         opts += [f"price > {a}{idx}.price", f"x < {a}{idx}.x + {{c}}", f"price * 2 > {a}{idx}.price + x",
                  f"{a}{idx}.price - price < {{c}}.0", f"volume >= {a}{idx}.volume"]
     return rng.choice(opts).format(c=rng.randint(1, 20))
 
 
-def nfa_query(rng, streams, qname, allow_absent):
+def nfa_query(rng, streams, qname, allow_absent, partitioned=False):
+    """partitioned: the last state is never a count with min 0 (the device leaves
+    that shape -- CountPostStateProcessor.isEventReturned, one field shared by every
+    key -- to the reference runtime)"""
     seq = rng.random() < 0.4
     sep = ", " if seq else " -> "
     n = rng.randint(2, 4)
@@ -62,7 +67,10 @@ def nfa_query(rng, streams, qname, allow_absent):
         f = _filter(rng, k + 1 if kind == "count" else k, aliases + ([(k, a, True)] if kind == "count" else []))
         src = f"{a}={s}[{f}]"
         if kind == "count":
-            counts = ["<1:3>", "<2:4>", "<0:2>", "<2>", "<1:>"] + (["+", "*", "?"] * 2 if seq else [])
+            min0 = ["<0:2>"] + (["*", "?"] * 2 if seq else [])
+            counts = ["<1:3>", "<2:4>", "<2>", "<1:>"] + (["+"] * 2 if seq else [])
+            if not (partitioned and i == n - 1):
+                counts += min0
             src += rng.choice(counts)
         parts.append(src)
         aliases.append((k, a, kind == "count"))
@@ -78,7 +86,7 @@ def nfa_query(rng, streams, qname, allow_absent):
     if not sel:
         sel = ["1 as c0"]
     if rng.random() < 0.25 and aliases:
-        sel.append(f"sum({aliases[-1][1]}.price) as s")
+        sel.append(f"sum({aliases[-1][1]}{'[last]' if aliases[-1][2] else ''}.price) as s")
     if rng.random() < 0.15 and aliases:
         sel.append(f"count() as n")
     q = f"@info(name = '{qname}') from {body} select {', '.join(sel)} insert into Out;"
@@ -94,7 +102,7 @@ def nfa_case(rng, multi_query=None):
     partitioned = rng.random() < 0.6 or nq > 1
     qs, used = [], set()
     for i in range(nq):
-        q, u = nfa_query(rng, streams, f"query{i + 1}", allow_absent=playback)
+        q, u = nfa_query(rng, streams, f"query{i + 1}", allow_absent=playback, partitioned=partitioned)
         qs.append(q)
         used |= u
     body = " ".join(qs)

@@ -41,11 +41,22 @@ def test_shard_owner_matches_python_hash(lib):
 
 def test_header_declares_exactly_the_exported_symbols(lib):
     hdr = open(os.path.join(ROOT, "include", "siddhi_hip.h")).read()
-    declared = set(re.findall(r"\b(sh_[a-z_]+)\s*\(", hdr))
+    declared = set(re.findall(r"\b(sh_[a-z0-9_]+)\s*\(", hdr))
     assert declared == set(abi.EXPORTED)
     out = subprocess.run(["nm", "-D", "--defined-only", build.OUT], capture_output=True, text=True).stdout
-    exported = set(re.findall(r" T (sh_[a-z_]+)", out))
+    exported = set(re.findall(r" T (sh_[a-z0-9_]+)", out))
     assert declared <= exported
+
+
+def test_device_run_struct_keeps_the_v1_layout():
+    """sh_device_run: the V1 struct (round 2 callers) is the first 96 bytes with
+    d_out_cols at 88; the V2 fields follow it (sh_run_device reads the prefix only,
+    sh_run_device_v2 the whole struct)"""
+    R = abi.sh_device_run
+    assert R.d_out_query.offset == 80 and R.d_out_cols.offset == 88
+    assert R.version.offset == 96 and R.d_run.offset == 104 and C.sizeof(R) == 112
+    hdr = open(os.path.join(ROOT, "include", "siddhi_hip.h")).read()
+    assert "#define SH_DEVICE_RUN_V1_BYTES 96" in hdr
 
 
 def _compile(lib, text):

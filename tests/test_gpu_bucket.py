@@ -60,13 +60,14 @@ def test_c2_bucket_vs_oracle():
 
 
 @pytest.mark.parametrize("n,nk,bucketed,columns", [(10_000_000, 10_000, 1, False), (100_000_000, 10_000, 1, False),
-                                                   (100_000_000, 10_000, 1, True), (3_000_000, 60_000, 0, False),
-                                                   (3_000_000, 60_000, 0, True)])
+                                                   (100_000_000, 10_000, 1, True), (3_000_000, 60_000, 1, False),
+                                                   (3_000_000, 60_000, 1, True)])
 def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed, columns):
-    """60k symbols at 100 ev/ms: a key's previous event is often beyond the
-    matcher's halo (SHB_HALO bucket events), so the run falls back -- exactly.
-    `columns`: typed output columns (the bucketed engine writes them itself, the
-    fallback's rows are narrowed)"""
+    """60k symbols at 100 ev/ms: a key's previous event is often more than a
+    window back, so many walks leave their key's run in the span; the halo covers
+    the window in time and the check against the latest timestamp before the
+    span (tpre) proves those walks complete, so the run stays bucketed.
+    `columns`: typed output columns (the bucketed engine writes them itself)"""
     ts, k, p, v = synth.stock_stream(n, nk, 100)
     (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk, columns)
     assert status == bucketed, err

@@ -73,7 +73,7 @@ def group_case(seed):
     if not refs:
         return None
     g = ", ".join(f"{rng.choice(refs)}.{rng.choice(['x', 'sym', 'price'])}" for _ in range(rng.choice([1, 1, 2])))
-    aggs = "" if " as s" in app else f", sum({refs[-1]}.price) as s"
+    aggs = "" if " as s" in m.group(1) else f", sum({refs[-1]}.price) as s"
     tail = rng.choice(["", "", " having s > 10.0", " output every 2 events"])
     app = app.replace(" insert into Out;", f"{aggs}, count() as gn group by {g}{tail} insert into Out;", 1)
     return app, actions

@@ -10,6 +10,7 @@ testQuery26 (tests/golden/fixtures.json, run by test_oracle_golden /
 test_nfa_engine_cpu / test_gpu_parity); here randomized apps hold the general engine's
 kernel logic (compiled for the CPU) and the device to the oracle."""
 import random
+import re
 
 import pytest
 
@@ -19,22 +20,50 @@ from nfa_host_engine import NfaHostEngine, NfaUnsupported
 from oracle_engine import OracleEngine
 from siddhi_amd import SiddhiAppCreationException, compiler
 
-HAVING = ["c0 is null", "not (c0 is null)", "c1 != 'K0'", "s > 20.0", "n > 1", "c0 > 3 or c1 == 'K1'",
-          "not (n > 2)", "s is null", "instanceOfLong(c2)", "instanceOfFloat(c2) or n == 1"]
+_ATTR_T = {"price": "f", "x": "i", "sym": "s", "volume": "i"}
+
+
+def _outputs(select):
+    """output attribute -> 'f' / 'i' / 's' (float-like, int-like, string) of a
+    generated select list (c0.., s = sum(...) double, n = count() long)"""
+    outs = {}
+    for expr, name in re.findall(r"([^,]+?) as (\w+)", select):
+        expr = expr.strip()
+        if name == "s":
+            outs[name] = "f"
+        elif name == "n":
+            outs[name] = "i"
+        else:
+            a = expr.rsplit(".", 1)[-1]
+            outs[name] = _ATTR_T.get(a, "i")
+    return outs
+
+
+def _cond(rng, outs):
+    c = rng.choice(sorted(outs))
+    t = outs[c]
+    forms = [f"{c} is null", f"not ({c} is null)", f"instanceOfLong({c})", f"instanceOfFloat({c})"]
+    forms += {"f": [f"{c} > 20.0", f"{c} < 15.5", f"not ({c} >= 12.0)"],
+              "i": [f"{c} > 3", f"{c} != 2", f"not ({c} > 1)"],
+              "s": [f"{c} != 'K0'", f"{c} == 'K1'"]}[t]
+    return rng.choice(forms)
 
 
 def having_case(seed):
+    """a random app of tests/nfa_cases.py with a `having` over the outputs its
+    first query's select list defines, each compared with a constant of its type"""
     rng = random.Random(9000 + seed)
     app, actions = nfa_case(rng)
-    if " select " not in app:
+    m = re.search(r" select (.*?) insert into Out;", app)
+    if m is None:
         return None
-    h = rng.choice(HAVING)
-    # every generated select list starts with c0, c1, c2 and may add s / n (aggregators)
-    if ("s" in h.split() or "s " in h) and " as s" not in app:
-        h = "c0 is null"
-    if ("n" in h.split()) and " as n" not in app:
-        h = "not (c0 is null)"
-    app = app.replace(" insert into Out;", f" having {h} insert into Out;")
+    outs = _outputs(m.group(1))
+    if not outs:
+        return None
+    h = _cond(rng, outs)
+    if rng.random() < 0.4:
+        h = f"{h} {rng.choice(['and', 'or'])} {_cond(rng, outs)}"
+    app = app.replace(" insert into Out;", f" having {h} insert into Out;", 1)
     return app, actions
 
 

@@ -159,3 +159,61 @@ def test_c4_gloo_world2_equals_single_process():
     ref = _oracle(c, synth.c4_stream(3000, seconds=5))
     assert len(ref["seq"]) > 1000
     assert same_output(got, ref)
+
+
+class _RecEngine:
+    """records what ShardedStreamEngine pushes (no device)"""
+
+    def __init__(self):
+        self.parts = []
+
+    def set_coordinator(self, coord):
+        pass
+
+    def send_part(self, stream, ts, cols, nulls, keys, index, call_n, call_last):
+        self.parts.append((len(ts), None if keys is None else keys.copy(), index.copy(), call_n))
+
+
+def test_keyless_stream_goes_to_the_null_key_rank_only():
+    """a stream without a partition key (null keys) is pushed by the rank that
+    owns null keys, as owner() routes keys < 0 -- never by every rank"""
+    from siddhi_amd.shard_stream import ShardedStreamEngine, ThreadComm
+    comm = ThreadComm(3)
+    engs = [_RecEngine() for _ in range(3)]
+    shards = [ShardedStreamEngine(e, comm.view(r), null_key_rank=1) for r, e in enumerate(engs)]
+    ts = np.arange(10, dtype=np.int64)
+    for s in shards:
+        s.send(0, ts, [np.arange(10, dtype=np.int32)], [None], None)
+    assert [e.parts[0][0] for e in engs] == [0, 10, 0]
+    assert all(e.parts[0][3] == 10 for e in engs)  # every rank still takes the call's steps
+    keys = np.array([-1, 3, -1, 7, 5], np.int32)
+    for s in shards:
+        s.send(0, ts[:5], [keys], [None], keys)
+    pushed = sorted(int(i) for e in engs for i in e.parts[1][2])
+    assert pushed == list(range(5))
+    assert set(engs[1].parts[1][2]) >= {0, 2}
+
+
+def test_thread_comm_failure_breaks_the_group():
+    """one rank's failing coordinator callback aborts the barrier: the other
+    ranks' all_gather fails promptly instead of waiting forever"""
+    import threading
+    from siddhi_amd.shard_stream import Coordinator, ThreadComm
+    comm = ThreadComm(3)
+    c0 = Coordinator(comm.view(0))
+    errors = []
+
+    def peer(r):
+        try:
+            comm.view(r).all_gather(np.zeros(1, np.int64))
+        except threading.BrokenBarrierError as e:
+            errors.append(e)
+
+    th = [threading.Thread(target=peer, args=(r,)) for r in (1, 2)]
+    for t in th:
+        t.start()
+    assert c0._fail(RuntimeError("rank 0 failed")) == 1
+    for t in th:
+        t.join(timeout=10)
+    assert not any(t.is_alive() for t in th)
+    assert len(errors) == 2 and isinstance(c0.error, RuntimeError)
