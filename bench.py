@@ -251,7 +251,10 @@ def main_c4(args, torch, dist, world, rank, dev):
         if world > 1:
             eng.check()
         base.close()
+        last["out"] = out
         return len(out["seq"]), dt
+
+    last = {}
 
     for i in range(args.warmup):
         log(f"warmup {i}")
@@ -269,6 +272,18 @@ def main_c4(args, torch, dist, world, rank, dev):
         dist.all_reduce(dt_t[1:], op=dist.ReduceOp.SUM, group=group)
     tot, m = float(dt_t[0].item()), int(dt_t[1].item())
     value = n * args.steps / tot   # the one stream, all ranks
+    # the ordered output vs the oracle's digest on the same stream (tests/golden/
+    # c4_digest.json, tests/golden/make_c4_digest.py), when it holds this workload
+    verified = None
+    if world == 1 and not args.c4_calls:
+        try:
+            from c4_cases import c4_digest
+            key = ("every" if args.c4_every else "default") + f"_{args.events}_{args.keys}"
+            want = json.load(open(os.path.join(HERE, "tests", "golden", "c4_digest.json"))).get(key)
+            if want is not None:
+                verified = c4_digest(last["out"]) == {"rows": want["rows"], "sha256": want["sha256"]}
+        except (OSError, ValueError):
+            verified = None
     # algorithmic bytes: Login / Logout 12 B, Txn 16 B, + 1 B stream
     # tag per event; per alert seq 8 + user 4 + ip 4 + amount 4 = 20 B
     n_txn = sum(len(b[1]) for b in blocks if b[0] == 1)
@@ -315,9 +330,10 @@ def main_c4(args, torch, dist, world, rank, dev):
                                    "algorithmic bytes / step time",
                          "algorithmic_bytes": b_alg},
             "cpu_baseline": cpu,
-            "verified_vs_restatement": None,
-            "parity": "tests/test_gpu_c4.py, tests/test_gpu_shard_stream.py (whole streams vs the oracle, "
-                      "1M users on one GPU, 2 / 4 key-sharded virtual ranks)"}))
+            "verified_vs_restatement": verified,
+            "verified_against": "digest of the oracle's ordered output on this stream (tests/golden/c4_digest.json)",
+            "parity": "tests/test_gpu_c4.py (whole streams vs the oracle up to 1M users; the 10M-user stream vs "
+                      "the oracle's digest), tests/test_gpu_shard_stream.py (2 / 4 key-sharded virtual ranks)"}))
     if world > 1:
         dist.destroy_process_group()
 
@@ -334,6 +350,12 @@ def check_rows(W, oseq, ovals, oq, sel_range=None):
     if eq is not None:
         ok = ok and oq is not None and np.array_equal(oq, eq)
     return bool(ok)
+
+
+def engine_tag():
+    """identifies the device pipeline a PMC profile was taken on (bumped when a
+    pipeline's kernels change what they move)"""
+    return "r4-tile-local"
 
 
 def cpu_baseline(args, W, n):
@@ -445,6 +467,7 @@ def main_sharded(args, torch, dist, world, rank, dev):
         oq = v[:, -1].astype(np.int32) if wq else None
         verified = check_rows(W, seq.cpu().numpy(), v[:, :-1] if wq else v, oq, (lo, hi))
     cpu = cpu_baseline(args, W, n) if rank == 0 else None
+    phases = step.phase_ms()
     if rank == 0:
         print(json.dumps({
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
@@ -457,6 +480,7 @@ def main_sharded(args, torch, dist, world, rank, dev):
                        "matches_total": m,
                        "parallelism": f"key-sharded x{world}: RCCL all-to-all route + return, k-way merge",
                        "rank0_slice": [lo, hi], "rank0_step": step.last, "bytes": W["bytes_note"]},
+            "phase_ms_rank0_last_step": phases,
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": None,
                          "kernel": "matcher step per GPU (every matcher kernel; HIP events on the launch stream): "
@@ -571,15 +595,19 @@ def main():
             ovals_np = ovals.cpu().numpy()
         verified = check_rows(W, oseq.cpu().numpy(), ovals_np, oq.cpu().numpy() if oq is not None else None)
 
-    # HBM bytes per step from the committed rocprofv3 PMC passes of this
-    # workload (scripts/pmc_traffic.py), when they match the configuration
-    traffic = None
-    prof = os.path.join(HERE, "profiles", f"pmc_{args.config}.json")
+    # HBM bytes per step from the committed rocprofv3 PMC passes of this exact
+    # workload and variant (scripts/pmc_traffic.py): config, events, keys, --agg,
+    # --columns and the engine build must all match, else null
+    traffic, traffic_src = None, None
+    variant = args.config + ("_agg" if args.agg else "") + ("_cols" if use_cols else "")
+    prof = os.path.join(HERE, "profiles", f"pmc_{variant}.json")
     if os.path.exists(prof):
         try:
             pj = json.load(open(prof))
-            if pj.get("events") == n and pj.get("keys") == K:
+            if (pj.get("events") == n and pj.get("keys") == K and bool(pj.get("agg")) == bool(args.agg)
+                    and bool(pj.get("columns")) == bool(use_cols) and pj.get("engine") == engine_tag()):
                 traffic = pj.get("hbm_bytes_per_step")
+                traffic_src = os.path.relpath(prof, HERE)
         except Exception:
             traffic = None
 
@@ -603,7 +631,7 @@ def main():
                        "matches_per_gpu": int(m), "parallelism": f"key-sharded x{world}",
                        "bytes": W["bytes_note"]},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",
-                         "frac": achieved / peak, "traffic": traffic,
+                         "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "matcher step (every kernel of one pass, HIP events on the launch stream)",
                          "kernels_ms_per_step": step_kernels_ms, "algorithmic_bytes": b_alg,
                          "match_kernel_only_GBps": match_only / 1e9},

@@ -52,6 +52,22 @@ int shs_pack(const uint32_t* d_pos, int64_t n, int32_t n_cols, const void* const
 int shs_unpack(const uint32_t* d_rec, int64_t n, int32_t n_cols, void* const* d_cols, const int32_t* widths,
                uint64_t* d_seq, void* stream);
 
+/* Compact records (C2: 24 bytes instead of 32): a column of width code
+   SHS_W_OFF is an 8-byte column (timestamps) carried as a 32-bit offset from
+   h_base[c] (the caller checks the slice's range fits), and the sequence number
+   is carried as the 32-bit index into the source slice. */
+#define SHS_W_OFF 5
+int32_t shs_record_words_compact(int32_t n_cols, const int32_t* widths);
+/* rec[d_pos[i]] = cols (SHS_W_OFF: v - h_base[c]) ++ (uint32)i */
+int shs_pack_compact(const uint32_t* d_pos, int64_t n, int32_t n_cols, const void* const* d_cols,
+                     const int32_t* widths, const int64_t* h_base, uint32_t* d_rec, void* stream);
+/* the inverse over the records received from each source rank r (records
+   [h_src_off[r], h_src_off[r+1])): SHS_W_OFF columns + h_src_base[r * n_cols + c],
+   sequence numbers h_src_seq0[r] + index */
+int shs_unpack_compact(const uint32_t* d_rec, int32_t n_cols, void* const* d_cols, const int32_t* widths,
+                       const int64_t* h_src_off, int32_t world, const int64_t* h_src_base, const uint64_t* h_src_seq0,
+                       uint64_t* d_seq, void* stream);
+
 /* owner side of the return route: d_oseq (m matcher rows, values seq_base +
    local event index, ascending) -> global sequence numbers d_gseq[local]; and
    h_counts[r] = rows whose event came from rank r (received events are laid

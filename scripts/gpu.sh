@@ -24,7 +24,8 @@ prof)
     export TMPDIR=/tmp
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/$name -o run -- python3 -u bench.py "$@" \
         > gpurun_out/$name.out 2> gpurun_out/$name.err || { tail -30 gpurun_out/$name.err; exit 1; }
-    find gpurun_out/$name -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/$name.kernel_stats.csv
+    db=$(find gpurun_out/$name -name "*.db" | head -1)
+    python scripts/prof_db.py "$db" gpurun_out/$name.kernel_stats.csv
     head -12 gpurun_out/$name.kernel_stats.csv | cut -c1-160
     ;;
 pmc)

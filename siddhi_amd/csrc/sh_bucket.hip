@@ -32,6 +32,7 @@
 
 #include "../../include/sh_query.h"
 #include "sh_device.h"
+#include "sh_nfa.h"
 #include "sh_wave.h"
 
 #define BK_TPB 512
@@ -123,9 +124,9 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
         for (int j = 0; j < BK_ITEMS; j++) {
             const int64_t dt = tv[j] - P.tbase;
             if (key[j] >= nkeys) badk = true;
-            if (key[j] >= 0 && (dt < 0 || dt >= lim)) bad = true;
+            if (key[j] >= 0 && !P.no_ts && (dt < 0 || dt >= lim)) bad = true;
             if (key[j] >= 0 && tv[j] > tmx) tmx = tv[j];
-            wp[j] = ((uint32_t)dt << P.kb) | ((uint32_t)key[j] >> 8);
+            wp[j] = P.no_ts ? ((uint32_t)key[j] >> 8) : (((uint32_t)dt << P.kb) | ((uint32_t)key[j] >> 8));
             rw[j] = key[j] >= 0 ? ((uint32_t)key[j] & (SHB_NB - 1)) << 16 : ~0u;
         }
         if (bad) atomicOr(P.flag, SHB_F_TS);
@@ -137,6 +138,7 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
             tmx = y > tmx ? y : tmx;
         }
         if (lane == 0) s_tmx[w] = tmx;
+        if (threadIdx.x == 0) P.tfirst[T] = tv[0];
     }
     // each wave ranks its own contiguous 1,024 events (16 rounds of 64): the
     // rank of an event among the wave's same-bucket events before it, from 8
@@ -304,8 +306,36 @@ __device__ __forceinline__ void bk_row(const shb_out& O, const shb_cols& OC, con
     }
 }
 
+// the select values of a row (NO > 0: unrolled, the descriptors in scalar registers)
+template <int NO>
+__device__ __forceinline__ void bk_vals(const shb_out& O, int64_t i, int64_t mp, int64_t* v) {
+#pragma unroll
+    for (int o = 0; o < NO; o++) v[o] = BK_VAL(o, i, mp);
+}
+
 template <bool COLS, int NO>
-__global__ void __launch_bounds__(BK_TPB) k_bk_emit(shb_plan P, shb_out O, shb_cols OC, uint64_t seq_base,
+__device__ __forceinline__ void bk_store(const shb_cols& OC, int64_t row, const int64_t* v, uint64_t seq,
+                                         uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_vals) {
+    if (out_seq) out_seq[row] = seq;
+    if (COLS) {
+#pragma unroll
+        for (int o = 0; o < NO; o++) bk_put(OC.cols[o], OC.colw[o], row, v[o]);
+    } else if (out_vals) {
+        if (NO % 2 == 0) {
+            longlong2* dst = (longlong2*)(out_vals + row * NO);
+#pragma unroll
+            for (int o = 0; o < NO; o += 2) dst[o / 2] = make_longlong2(v[o], v[o + 1]);
+        } else {
+#pragma unroll
+            for (int o = 0; o < NO; o++) out_vals[row * NO + o] = v[o];
+        }
+    }
+}
+
+#define BK_RU 4  // rows per lane whose loads are issued before their stores
+
+template <bool COLS, int NO>
+__global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, shb_cols OC, uint64_t seq_base,
                                                     uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_vals,
                                                     int64_t out_cap) {
     __shared__ uint32_t pfx[SHB_TILE + 1];
@@ -318,6 +348,7 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(shb_plan P, shb_out O, shb_c
     __shared__ int32_t o_kind[SHB_MAX_OUT], o_type[SHB_MAX_OUT];
     __shared__ const void* o_src[SHB_MAX_OUT];
     __shared__ uint32_t s_tb;
+    constexpr int NV = NO > 0 ? NO : 1;
     const int T = bk_tile(P.nt);
     if (T < 0) return;
     const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
@@ -423,15 +454,41 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(shb_plan P, shb_out O, shb_c
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (R <= BK_EROWS) {
-            // row-parallel: lane t writes rows t, t + 64, ...
-            for (uint32_t t = lane; t < R; t += 64) {
-                const int e = rmap[w][t];
-                const uint32_t k = t - ero[w][e];
-                const int64_t i = ib + e;
-                const int64_t row = (int64_t)rb + t;
-                if (row >= out_cap) continue;  // the host reports SH_E_MORE
-                bk_row<COLS, NO>(O, OC, o_kind, o_type, o_src, row, i, (int64_t)emp[w][e] + k, seq_base + (uint64_t)i,
-                                 out_seq, out_vals);
+            // row-parallel: lane t writes rows t, t + 64, ... (consecutive lanes,
+            // consecutive rows); BK_RU rows' loads go out before their stores
+            if (NO > 0) {
+                for (uint32_t t0 = 0; t0 < R; t0 += 64 * BK_RU) {
+                    int64_t v[BK_RU][NV];
+                    int64_t ii[BK_RU];
+                    bool ok[BK_RU];
+#pragma unroll
+                    for (int u = 0; u < BK_RU; u++) {
+                        const uint32_t t = t0 + u * 64 + lane;
+                        ok[u] = t < R && (int64_t)rb + t < out_cap;  // (past out_cap: the host reports SH_E_MORE)
+                        ii[u] = ib;
+                        if (ok[u]) {
+                            const int e = rmap[w][t];
+                            const uint32_t k = t - ero[w][e];
+                            ii[u] = ib + e;
+                            bk_vals<NV>(O, ii[u], (int64_t)emp[w][e] + k, v[u]);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < BK_RU; u++)
+                        if (ok[u])
+                            bk_store<COLS, NV>(OC, (int64_t)rb + t0 + u * 64 + lane, v[u],
+                                                           seq_base + (uint64_t)ii[u], out_seq, out_vals);
+                }
+            } else {
+                for (uint32_t t = lane; t < R; t += 64) {
+                    const int e = rmap[w][t];
+                    const uint32_t k = t - ero[w][e];
+                    const int64_t i = ib + e;
+                    const int64_t row = (int64_t)rb + t;
+                    if (row >= out_cap) continue;  // the host reports SH_E_MORE
+                    bk_row<COLS, NO>(O, OC, o_kind, o_type, o_src, row, i, (int64_t)emp[w][e] + k,
+                                     seq_base + (uint64_t)i, out_seq, out_vals);
+                }
             }
         } else {
             // a dense half (more rows than the map holds): each event writes its rows
@@ -457,8 +514,25 @@ __global__ void __launch_bounds__(BK_TPB) k_bk_emit(shb_plan P, shb_out O, shb_c
 }
 
 // ---------------------------------------------------------------- halo bound
+// hstart[T] <- the first halo tile of a matcher pass whose chunk starts at tile
+// T: tile T - 1, and before it every tile whose successor starts within W of
+// tile T's first event (for streams in time order, every tile that can hold an
+// event the window reaches), at most SHB_HMAX. One thread per tile.
+__global__ void __launch_bounds__(256) k_bk_halo(const int64_t* __restrict__ tfirst, int32_t* __restrict__ hstart,
+                                                 int32_t nt, int64_t within) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= nt) return;
+    const int64_t ta = tfirst[t];
+    const int64_t tlim = ta < INT64_MIN + within ? INT64_MIN : ta - within;
+    int h = t > 0 ? 1 : 0;
+    while (h < t && h < SHB_HMAX && tfirst[t - h] >= tlim) h++;
+    hstart[t] = t - h;
+}
+
 // tpre[T] <- the latest timestamp of the tiles before T (exclusive prefix max,
-// INT64_MIN for tile 0); one workgroup, each thread a contiguous run of tiles
+// INT64_MIN for tile 0): the matcher's proof that a walk leaving its key's run
+// saw every event of the key inside the window. One workgroup, each thread a
+// contiguous run of tiles (independent loads), one LDS scan.
 __global__ void __launch_bounds__(1024) k_bk_tpre(int64_t* __restrict__ tpre, int32_t nt) {
     __shared__ int64_t s[1024];
     const int per = (nt + 1023) / 1024;
@@ -481,6 +555,239 @@ __global__ void __launch_bounds__(1024) k_bk_tpre(int64_t* __restrict__ tpre, in
     }
 }
 
+// ---------------------------------------------------------------- sequence carry
+// The rise-and-fall sequence `every e1=S, e2=S[f2(x, e1)]+, e3=S[f3(x, e2[last])]`
+// (nf_query.s3; SEQUENCE semantics make each key's state ONE partial: k_seq3s in
+// sh_nfa.hip states the per-event step, CountPreStateProcessor.java:52-193,
+// StreamPreStateProcessor.java:325-403). Per event x of a key:
+//   hit = (a last e2 exists) && f3(x, last)   -> one match (e1, last, x)
+//   else if (an e1 exists) && f2(x, e1)       -> last = x (the e2 run grows)
+//   else                                      -> e1 = x, no last (every: a new start)
+// The sequence has no window, so a key's state runs over the whole stream. One
+// workgroup per key bucket walks the bucket's segments of every tile in order,
+// in chunks of at most S3B_CH events, with the state of each of its keys in LDS:
+// a chunk is sorted stably by local key (two 6-bit passes of wave ballots), the
+// first event of each key run steps through the run, and the chunk's matches go
+// out in arrival order: count 0/1 at the event's slot, the e1 / last values in
+// the slot range of the event's (tile, bucket) segment (at most one match per
+// event, so the segment's slots hold its matches), the segment's first match
+// position and the tile's matches. k_bk_emit then writes the ordered rows.
+#define S3B_TPB 1024
+#define S3B_CH 4096
+#define S3B_NR (S3B_CH / S3B_TPB)
+#define S3B_NK 4096  // local keys per bucket (kb <= 12)
+#define S3B_W (S3B_TPB / 64)
+
+__device__ __forceinline__ NfVal s3b_val(uint32_t b, int t) {
+    NfVal v;
+    v.t = (uint8_t)t;
+    v.null = 0;
+    v.b = t == SH_T_INT ? (int64_t)(int32_t)b : (int64_t)b;
+    return v;
+}
+
+// one stable multisplit pass over 6 bits of the local key: the chunk positions
+// in `in` order (identity when in == nullptr) -> `out`
+__device__ __forceinline__ void s3b_sort_pass(const uint32_t* __restrict__ c_key, const uint16_t* in,
+                                              uint16_t* out, int L, int sh, uint32_t (*wc)[64], uint32_t* ws) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int c = threadIdx.x; c < S3B_W * 64; c += S3B_TPB) (&wc[0][0])[c] = 0u;
+    __syncthreads();
+    uint32_t rk[S3B_NR], dg[S3B_NR], ix[S3B_NR];
+#pragma unroll
+    for (int r = 0; r < S3B_NR; r++) {
+        const int pos = (w * S3B_NR + r) * 64 + lane;  // wave w owns positions [w * 256, w * 256 + 256)
+        const bool valid = pos < L;
+        ix[r] = valid ? (in ? (uint32_t)in[pos] : (uint32_t)pos) : 0u;
+        const uint32_t d = valid ? (c_key[ix[r]] >> sh) & 63u : 0u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bb = 0; bb < 6; bb++) {
+            const bool bit = (d >> bb) & 1u;
+            const uint64_t m = __ballot(valid && bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t r_ = (uint32_t)__popcll(peers & lt);
+        const uint32_t base = valid ? wc[w][d] : 0u;
+        if (valid && r_ == 0) wc[w][d] = base + (uint32_t)__popcll(peers);
+        rk[r] = valid ? base + r_ : ~0u;
+        dg[r] = d;
+    }
+    __syncthreads();
+    // (digit, wave) exclusive offsets: thread t = digit * 16 + wave
+    {
+        const int d = threadIdx.x >> 4, q = threadIdx.x & 15;
+        uint32_t tot;
+        const uint32_t ex = shw_block_excl<S3B_TPB>(wc[q][d], ws, &tot);
+        __syncthreads();
+        wc[q][d] = ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < S3B_NR; r++)
+        if (rk[r] != ~0u) out[wc[w][dg[r]] + rk[r]] = (uint16_t)ix[r];
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(S3B_TPB) k_s3b(shb_plan P, shb_s3 S) {
+    __shared__ uint32_t st_e1[S3B_NK], st_last[S3B_NK];
+    __shared__ uint8_t st_f[S3B_NK];  // bit 0: an e1, bit 1: a last e2
+    __shared__ uint32_t c_key[S3B_CH], c_val[S3B_CH];
+    __shared__ uint16_t o_a[S3B_CH], o_b[S3B_CH];
+    __shared__ uint32_t m_v0[S3B_CH], m_v1[S3B_CH];
+    __shared__ uint16_t m_pre[S3B_CH];  // 0/1 per event, then its exclusive prefix over the chunk
+    __shared__ uint32_t wc[S3B_W][64];
+    __shared__ uint32_t ws[S3B_W];
+    __shared__ uint32_t seg_p[SHB_CT_MAX + 1], seg_g[SHB_CT_MAX];
+    __shared__ uint8_t seg_of[S3B_CH / 32];
+    const int b = blockIdx.x;
+    const int kb = P.kb;
+    const uint32_t kmask = (1u << kb) - 1u;
+    const int t = S.type;
+    for (int k = threadIdx.x; k < S3B_NK; k += S3B_TPB) st_f[k] = 0;
+    const uint32_t* __restrict__ gcol = (const uint32_t*)P.st_dst[0];
+    for (int a = 0; a < P.nt;) {
+        __syncthreads();
+        // the bucket's segments of tiles [a, a + SHB_CT_MAX), their prefix
+        const int nseg = P.nt - a < SHB_CT_MAX ? P.nt - a : SHB_CT_MAX;
+        uint32_t len = 0u, g = 0u;
+        if ((int)threadIdx.x < nseg) {
+            const int T = a + (int)threadIdx.x;
+            const uint16_t* r = P.toff + (int64_t)T * SHB_TOFF + b;
+            const uint32_t lo = r[0], hi = r[1];
+            len = hi - lo;
+            g = ((uint32_t)T << SHB_TILE_SHIFT) + lo;
+        }
+        {
+            uint32_t tot;
+            const uint32_t pre = shw_block_excl<S3B_TPB>(len, ws, &tot);
+            if ((int)threadIdx.x < nseg) {
+                seg_p[threadIdx.x] = pre;
+                seg_g[threadIdx.x] = g;
+            }
+            if ((int)threadIdx.x == nseg) seg_p[nseg] = tot;
+        }
+        __syncthreads();
+        // this chunk: tiles [a, a + ne), at most S3B_CH events
+        const int ne = __syncthreads_count((int)threadIdx.x < nseg && seg_p[threadIdx.x + 1] <= S3B_CH);
+        if (ne == 0) {
+            if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_SPAN);
+            return;  // (uniform) the host reruns on the general engine
+        }
+        const int L = (int)seg_p[ne];
+        for (int j = (int)threadIdx.x; j * 32 < L; j += S3B_TPB) {
+            const uint32_t e = (uint32_t)j * 32u;
+            int lo = 0, hi = ne - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (seg_p[mid] <= e) lo = mid;
+                else hi = mid - 1;
+            }
+            seg_of[j] = (uint8_t)lo;
+        }
+        __syncthreads();
+#define S3B_GIDX(i, out) { int sg_ = seg_of[(i) >> 5]; while (seg_p[sg_ + 1] <= (uint32_t)(i)) sg_++; \
+    out = seg_g[sg_] + ((uint32_t)(i) - seg_p[sg_]); }
+        // the chunk's events (arrival order inside the bucket)
+#pragma unroll
+        for (int k = 0; k < S3B_NR; k++) {
+            const int i = k * S3B_TPB + (int)threadIdx.x;
+            if (i < L) {
+                uint32_t gi;
+                S3B_GIDX(i, gi)
+                c_key[i] = P.w0[gi] & kmask;
+                c_val[i] = gcol[gi];
+            }
+        }
+        __syncthreads();
+        // stable sort by local key
+        const uint16_t* srt;
+        if (kb <= 6) {
+            s3b_sort_pass(c_key, nullptr, o_a, L, 0, wc, ws);
+            srt = o_a;
+        } else {
+            s3b_sort_pass(c_key, nullptr, o_a, L, 0, wc, ws);
+            s3b_sort_pass(c_key, o_a, o_b, L, 6, wc, ws);
+            srt = o_b;
+        }
+        // the first event of each key run steps through the run
+        for (int q = threadIdx.x; q < L; q += S3B_TPB) {
+            const uint32_t ci = srt[q];
+            const uint32_t key = c_key[ci];
+            if (q > 0 && c_key[srt[q - 1]] == key) continue;
+            uint32_t f = st_f[key], e1b = st_e1[key], lastb = st_last[key];
+            for (int r = q; r < L; r++) {
+                const uint32_t cr = r == q ? ci : srt[r];
+                if (r > q && c_key[cr] != key) break;
+                const uint32_t xb = c_val[cr];
+                const NfVal x = s3b_val(xb, t);
+                const bool hit = (f & 2u) && nf_cmp(S.op3, S.dom3, x, s3b_val(lastb, t));
+                m_pre[cr] = hit ? 1 : 0;
+                m_v0[cr] = e1b;
+                m_v1[cr] = lastb;
+                if (!hit && (f & 1u) && nf_cmp(S.op2, S.dom2, x, s3b_val(e1b, t))) {
+                    f |= 2u;
+                    lastb = xb;
+                } else {
+                    f = 1u;
+                    e1b = xb;
+                }
+            }
+            st_f[key] = (uint8_t)f;
+            st_e1[key] = e1b;
+            st_last[key] = lastb;
+        }
+        __syncthreads();
+        // matches: exclusive prefix over the chunk in arrival order (4 per thread)
+        uint32_t total;
+        {
+            const int p0 = (int)threadIdx.x * S3B_NR;
+            uint32_t v[S3B_NR], sum = 0;
+#pragma unroll
+            for (int q = 0; q < S3B_NR; q++) {
+                v[q] = p0 + q < L ? (uint32_t)m_pre[p0 + q] : 0u;
+                sum += v[q];
+            }
+            uint32_t off = shw_block_excl<S3B_TPB>(sum, ws, &total);
+#pragma unroll
+            for (int q = 0; q < S3B_NR; q++) {
+                if (p0 + q < L) {
+                    uint32_t gi;
+                    S3B_GIDX(p0 + q, gi)
+                    P.cnt[gi] = (uint8_t)v[q];
+                    m_pre[p0 + q] = (uint16_t)off;
+                }
+                off += v[q];
+            }
+        }
+        __syncthreads();
+        // per tile: its segment's matches start at the segment's first slot
+        for (int sg = threadIdx.x; sg < ne; sg += S3B_TPB) {
+            const uint32_t x0 = seg_p[sg], x1 = seg_p[sg + 1];
+            const uint32_t q0 = x0 < (uint32_t)L ? (uint32_t)m_pre[x0] : total;
+            const uint32_t q1 = x1 < (uint32_t)L ? (uint32_t)m_pre[x1] : total;
+            const int T = a + sg;
+            P.mstart[(int64_t)T * SHB_NB + b] = seg_g[sg];
+            if (q1 > q0) atomicAdd(&P.ttot[T], q1 - q0);
+        }
+        // the matches' e1 / last values, compact inside their segment's slots
+        for (int i = threadIdx.x; i < L; i += S3B_TPB) {
+            const uint32_t pre = m_pre[i];
+            const uint32_t nxt = i + 1 < L ? (uint32_t)m_pre[i + 1] : total;
+            if (nxt == pre) continue;
+            int sg = seg_of[i >> 5];
+            while (seg_p[sg + 1] <= (uint32_t)i) sg++;
+            const uint32_t s0 = seg_p[sg];
+            const uint32_t q0 = s0 < (uint32_t)L ? (uint32_t)m_pre[s0] : total;
+            const int64_t dst = (int64_t)seg_g[sg] + (pre - q0);
+            for (int m = 0; m < S.n_ms; m++) ((uint32_t*)P.ms[m])[dst] = S.ms_slot[m] == 0 ? m_v0[i] : m_v1[i];
+        }
+#undef S3B_GIDX
+        a += ne;
+    }
+}
+
 // ---------------------------------------------------------------- launches
 static int bk_ok() { return hipGetLastError() == hipSuccess ? 0 : -3; }
 
@@ -494,7 +801,11 @@ extern "C" int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nke
     else
         hipLaunchKernelGGL(k_bk_scatter<4>, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, nkeys, *P);
     if (bk_ok()) return -3;
-    hipLaunchKernelGGL(k_bk_tpre, dim3(1), dim3(1024), 0, st, P->tpre, P->nt);
+    if (!P->no_ts) {
+        hipLaunchKernelGGL(k_bk_halo, dim3((P->nt + 255) / 256), dim3(256), 0, st, P->tfirst, P->hstart, P->nt,
+                           P->within);
+        hipLaunchKernelGGL(k_bk_tpre, dim3(1), dim3(1024), 0, st, P->tpre, P->nt);
+    }
     return bk_ok();
 }
 
@@ -502,6 +813,12 @@ extern "C" int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nke
 // ttot[nt] = the total
 extern "C" int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream) {
     return shd_exclusive_scan(P->ttot, P->ttot, (int64_t)P->nt + 1, scan_tmp, stream);
+}
+
+extern "C" int shb_s3_carry(const shb_plan* P, const shb_s3* S, void* stream) {
+    if (P->kb > 12 || P->n_staged < 1 || P->st_width[0] != 4) return -1;
+    hipLaunchKernelGGL(k_s3b, dim3(SHB_NB), dim3(S3B_TPB), 0, (hipStream_t)stream, *P, *S);
+    return bk_ok();
 }
 
 template <bool COLS, int NO>

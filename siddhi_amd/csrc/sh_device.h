@@ -111,7 +111,7 @@ struct shb_plan {
     int32_t ct;               // arrival tiles per matcher chunk (<= SHB_CT_MAX)
     int32_t n_chunks;         // matcher grid = SHB_NB * n_chunks
     int32_t n_staged;
-    int32_t pad;
+    int32_t no_ts;            // 1: w0 = the local key alone (no timestamps: the sequence engine)
     const void* st_src[SHB_MAX_STAGED];  // arrival-order columns moved into bucket order
     void* st_dst[SHB_MAX_STAGED];
     int32_t st_width[SHB_MAX_STAGED];
@@ -128,6 +128,9 @@ struct shb_plan {
     uint32_t* ttot;           // [nt + 1]: matches per arrival tile -> exclusive scan
     uint32_t* ms_ctr;         // match-stream region allocator
     int64_t* tpre;            // [nt]: latest timestamp of each tile -> of all tiles before it
+    int64_t* tfirst;          // [nt]: timestamp of each tile's first event
+    int32_t* hstart;          // [nt]: first halo tile of a matcher pass starting at each tile
+    int64_t within;           // the window W (ms): halo tiles
     int32_t* flag;
     unsigned long long* prof; // diagnostics (SH_BK_PROFILE): clock ticks per matcher phase, NULL off
 };
@@ -140,6 +143,17 @@ struct shb_out {
     int32_t kind[SHB_MAX_OUT];
     int32_t type[SHB_MAX_OUT];    // sh_type: raw-value conversion
     const void* src[SHB_MAX_OUT]; // kind 0: match-stream column, kind 1: consumer column
+};
+
+// the rise-and-fall sequence (nf_query.s3) for the bucket-carry engine: every
+// operand of f2 / f3 and every e1 / e2[last] select value is one 4-byte attribute
+// (staged column 0) of type `type`; ms_slot[m]: match-stream column m holds e1's
+// value (slot 0) or the last e2's (slot 1)
+struct shb_s3 {
+    int32_t type;                 // SH_T_INT or SH_T_FLOAT
+    int32_t op2, dom2, op3, dom3;
+    int32_t n_ms;
+    int32_t ms_slot[2];
 };
 
 // typed output columns (sh_device_run.d_out_cols) instead of raw 8-byte rows
@@ -192,6 +206,9 @@ int shd_exclusive_scan(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* t
 // bucketed window engine launch steps (sh_bucket.hip), all async on `stream`
 int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_plan* P, void* stream);
 int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream);
+// the rise-and-fall sequence: one workgroup per key bucket carries its keys' state
+// across the tiles (after shb_partition with no_ts; before shb_finish)
+int shb_s3_carry(const shb_plan* P, const shb_s3* S, void* stream);
 int shb_emit(const shb_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base, uint64_t* out_seq,
              int64_t* out_vals, int64_t out_cap, void* stream);
 // raw 8-byte rows [m x n_out] -> typed columns of widths w[o] (8, 4 or 1 bytes)

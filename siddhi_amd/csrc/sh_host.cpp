@@ -423,8 +423,8 @@ struct sh_handle {
     // in n_klist_n[0..1]) and the log of keys armed since the last pass
     DevBuf n_klist[2], n_klist_n, n_arm_log, n_arm_ctr;
     int klist_cur = 0;
-    double hp_ms[6] = {0, 0, 0, 0, 0, 0};  // SH_HOST_PROF: wall time per host phase (printed by sh_destroy)
-    int64_t hp_n[6] = {0, 0, 0, 0, 0, 0};
+    double hp_ms[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // SH_HOST_PROF: wall time per host phase (printed by sh_destroy)
+    int64_t hp_n[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     int seq3_last = 0;                  // the last general-engine run took k_seq3
     bool s3_compact = false;            // ... with k_seq3s's compact records (nfd_place_s3 places them)
     bool s3_agg = false;                // ... whose aggregates ran in the kernel (no post-pass)
@@ -445,6 +445,12 @@ struct sh_handle {
     nf_cols cols_last;          // the column image last uploaded to d_ncols (nf_put_cols)
     bool cols_cached = false;
     std::vector<DevBuf> n_rank;         // by scheduler id, [n_nkeys] u64
+    // deferred scheduler history (single process): launches whose records were
+    // copied to pin_hist but not yet replayed on the models (nf_sev_flush replays
+    // them, in launch order, before the next use of the ranks)
+    PinBuf pin_hist;
+    int64_t hist_used = 0;                        // records in pin_hist
+    std::vector<std::pair<int64_t, int64_t>> sev_pend;  // (first record, records) per launch
     PinBuf pin_sev, pin_rk;
     int64_t sev_cap = 0;
     int caps[6] = {16, 32, 64, 32, 8, 4};  // list, se, node, hold, sched, group
@@ -477,9 +483,10 @@ struct sh_handle {
     int bk_state = 0;
     int32_t part_attr0 = -1;  // stream-0 attribute keying query 0's partition
     int bk_last = 0;          // 1: the last sh_run_device ran on the bucketed engine
+    int s3b_last = 0;         // 1: ... on the sequence bucket-carry engine (k_s3b)
     shj_bucket bk{};
     std::string bk_err;
-    DevBuf bk_w0, bk_sp, bk_toff, bk_cnt, bk_mstart, bk_tpre, bk_ttot, bk_flag, bk_prof;
+    DevBuf bk_w0, bk_sp, bk_toff, bk_cnt, bk_mstart, bk_tpre, bk_tfirst, bk_hstart, bk_ttot, bk_flag, bk_prof;
     DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS];
     PinBuf bk_rd;
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
@@ -1040,9 +1047,11 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
 void sh_destroy(sh_handle* h) {
     if (!h) return;
     if (getenv("SH_HOST_PROF") && h->hp_n[0]) {
-        static const char* names[6] = {"push", "timers", "process", "history", "place", "drain"};
+        static const char* names[10] = {"push", "timers", "process", "history", "place", "drain",
+                                        "hist_copy", "hist_apply", "hist_rank", "hist_records"};
         fprintf(stderr, "[sh host profile]");
-        for (int i = 0; i < 6; i++) fprintf(stderr, " %s %.1f ms / %lld", names[i], h->hp_ms[i], (long long)h->hp_n[i]);
+        for (int i = 0; i < 9; i++) fprintf(stderr, " %s %.1f ms / %lld", names[i], h->hp_ms[i], (long long)h->hp_n[i]);
+        fprintf(stderr, " %s %lld", names[9], (long long)h->hp_n[9]);
         fprintf(stderr, "\n");
     }
     if (h->has_device) {
@@ -1051,6 +1060,7 @@ void sh_destroy(sh_handle* h) {
         h->pin_stage.release();
         h->pin_rd.release();
         h->pin_out.release();
+        h->pin_hist.release();
         h->n_tmin.release();
         h->n_armed.release();
         h->n_klist[0].release();
@@ -1507,40 +1517,10 @@ static unsigned nf_ctl_err(sh_handle* h) { return *(const unsigned*)(h->pin_rd.a
 static int64_t nf_ctl_nrec(sh_handle* h) { return *(const int64_t*)(h->pin_rd.as<uint8_t>() + PR_CTL); }
 static int64_t nf_ctl_nsev(sh_handle* h) { return *(const int64_t*)(h->pin_rd.as<uint8_t>() + PR_CTL + 16); }
 
-// counted: nf_ctl_read ran before the caller's last sync (the history count is in pin_rd)
-static int nf_sev_apply(sh_handle* h, bool counted = false) {
-    HpScope hp_(h, 3);
-    if (!h->sm_on) return SH_OK;
+// the models' ranks after a replay: whole array after a resize, else the touched
+// keys (uploaded on the stream, ahead of the next due pass)
+static int nf_rank_upload(sh_handle* h) {
     hipStream_t st = h->stream;
-    if (h->pin_sev.ensure(64)) return fail(h, SH_E_OOM, "pinned staging");
-    int64_t n;
-    if (counted) {
-        n = nf_ctl_nsev(h);
-    } else {
-        hipMemcpyAsync(h->pin_sev.p, h->n_sev_ctr.p, 8, hipMemcpyDeviceToHost, st);
-        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
-        n = (int64_t)*h->pin_sev.as<unsigned long long>();
-    }
-    if (n == 0 && !h->coord_on) return SH_OK;
-    if (h->pin_sev.ensure((size_t)std::max<int64_t>(n, 1) * 16)) return fail(h, SH_E_OOM, "pinned staging");
-    if (n) hipMemcpyAsync(h->pin_sev.p, h->n_sev.p, (size_t)n * 16, hipMemcpyDeviceToHost, st);
-    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
-    const uint64_t* recs = h->pin_sev.as<uint64_t>();
-    if (h->coord_on) {
-        // the launch's history of every rank: the maps model the one state map
-        // all keys share (the same launch ticks on every rank keep the stamps
-        // comparable)
-        const uint64_t* all = nullptr;
-        int64_t n_all = 0;
-        if (h->coord.history(h->coord.user, recs, n, &all, &n_all) || n_all < 0 || (n_all && !all))
-            return fail(h, SH_E_INVALID_ARG, "coordinator: history exchange failed");
-        recs = all;
-        n = n_all;
-        if (n == 0) return SH_OK;
-    }
-    if (!h->sm.apply(recs, (size_t)n))
-        return fail(h, SH_E_UNSUPPORTED, "more than 2^26 scheduler map bins (keys waiting on one absent state)");
-    // ranks: whole array after a resize, else the touched keys
     std::vector<int32_t> ks;
     std::vector<uint64_t> vs;
     for (int s : h->sm.used) {
@@ -1580,6 +1560,87 @@ static int nf_sev_apply(sh_handle* h, bool counted = false) {
         M.dirty.clear();
     }
     return SH_OK;
+}
+
+// replay the deferred launches' history (in launch order: a timer launch's
+// removals follow its own getState calls, so each launch is one apply) and
+// upload the changed ranks; before every use of the ranks or the models
+static int nf_sev_flush(sh_handle* h) {
+    if (h->sev_pend.empty()) return SH_OK;
+    HpScope hp_(h, 3);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+    {
+        HpScope ha_(h, 7);
+        for (const auto& pr : h->sev_pend)
+            if (!h->sm.apply(h->pin_hist.as<uint64_t>((size_t)pr.first * 16), (size_t)pr.second))
+                return fail(h, SH_E_UNSUPPORTED, "more than 2^26 scheduler map bins (keys waiting on one absent state)");
+    }
+    h->sev_pend.clear();
+    h->hist_used = 0;
+    HpScope hr_(h, 8);
+    return nf_rank_upload(h);
+}
+
+// after a launch: its scheduler history. Single process: copied behind the
+// launch (no synchronisation) and replayed by nf_sev_flush before the ranks are
+// next needed. Key-sharded: exchanged now (the coordinator's history call is a
+// collective every rank makes per launch), replayed and uploaded.
+// counted: nf_ctl_read ran before the caller's last sync (the history count is in pin_rd)
+static int nf_sev_apply(sh_handle* h, bool counted = false) {
+    if (!h->sm_on) return SH_OK;
+    hipStream_t st = h->stream;
+    if (h->pin_sev.ensure(64)) return fail(h, SH_E_OOM, "pinned staging");
+    int64_t n;
+    {
+        HpScope hc_(h, 6);
+        if (counted) {
+            n = nf_ctl_nsev(h);
+        } else {
+            hipMemcpyAsync(h->pin_sev.p, h->n_sev_ctr.p, 8, hipMemcpyDeviceToHost, st);
+            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+            n = (int64_t)*h->pin_sev.as<unsigned long long>();
+        }
+        h->hp_n[9] += n;
+        if (!h->coord_on) {
+            if (n == 0) return SH_OK;
+            const size_t need = (size_t)(h->hist_used + n) * 16;
+            if (need > h->pin_hist.bytes) {
+                // grow, keeping the records already copied (their copies must land first)
+                if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+                PinBuf nb;
+                if (nb.ensure(need)) return fail(h, SH_E_OOM, "pinned staging");
+                if (h->hist_used) memcpy(nb.p, h->pin_hist.p, (size_t)h->hist_used * 16);
+                h->pin_hist.release();
+                h->pin_hist = nb;
+                nb.p = nullptr;
+                nb.bytes = 0;
+            }
+            hipMemcpyAsync(h->pin_hist.as<uint8_t>((size_t)h->hist_used * 16), h->n_sev.p, (size_t)n * 16,
+                           hipMemcpyDeviceToHost, st);
+            h->sev_pend.emplace_back(h->hist_used, n);
+            h->hist_used += n;
+            return SH_OK;
+        }
+        if (h->pin_sev.ensure((size_t)std::max<int64_t>(n, 1) * 16)) return fail(h, SH_E_OOM, "pinned staging");
+        if (n) hipMemcpyAsync(h->pin_sev.p, h->n_sev.p, (size_t)n * 16, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+    }
+    HpScope hp_(h, 3);
+    const uint64_t* recs = h->pin_sev.as<uint64_t>();
+    // the launch's history of every rank: the maps model the one state map all
+    // keys share (the same launch ticks on every rank keep the stamps comparable)
+    const uint64_t* all = nullptr;
+    int64_t n_all = 0;
+    if (h->coord.history(h->coord.user, recs, n, &all, &n_all) || n_all < 0 || (n_all && !all))
+        return fail(h, SH_E_INVALID_ARG, "coordinator: history exchange failed");
+    if (n_all == 0) return SH_OK;
+    {
+        HpScope ha_(h, 7);
+        if (!h->sm.apply(all, (size_t)n_all))
+            return fail(h, SH_E_UNSUPPORTED, "more than 2^26 scheduler map bins (keys waiting on one absent state)");
+    }
+    HpScope hr_(h, 8);
+    return nf_rank_upload(h);
 }
 
 static int nf_upload_table(sh_handle* h) {
@@ -1977,6 +2038,7 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
 static int nf_next_due_local(sh_handle* h, int64_t* out) {
     *out = INT64_MAX;
     if (!h->T->has_absent || h->n_nkeys == 0) return SH_OK;
+    if (nf_sev_flush(h)) return SH_E_HIP;
     hipStream_t st = h->stream;
     if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
     const int32_t nkeys = h->n_nkeys;
@@ -2031,6 +2093,10 @@ static int nf_timers(sh_handle* h, int64_t now, bool wall) {
         // Scheduler creation order (the TimestampGenerator's listener order)
         for (int si = 0; si < h->T->q[q].n_sched; si++) {
             const int p = h->T->q[q].sched_seq[si];
+            {
+                const int frc = nf_sev_flush(h);  // the ranks the due pass reads
+                if (frc) return frc;
+            }
             const int32_t nkeys = h->n_nkeys;
             unsigned long long nc = 0;
             if (nkeys > 0) {
@@ -2808,7 +2874,8 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     if (ensure_ws(h, std::max<int64_t>(n, (int64_t)B.nt + 1)) || h->bk_w0.ensure_fresh(slots * 4) ||
         h->bk_sp.ensure_fresh(n * 2) || h->bk_toff.ensure_fresh((int64_t)B.nt * SHB_TOFF * 2) ||
         h->bk_cnt.ensure_fresh(slots) || h->bk_mstart.ensure_fresh((int64_t)B.nt * SHB_NB * 4) ||
-        h->bk_tpre.ensure_fresh((int64_t)B.nt * 8) || h->bk_ttot.ensure_fresh(((int64_t)B.nt + 1) * 4) ||
+        h->bk_tpre.ensure_fresh((int64_t)B.nt * 8) || h->bk_tfirst.ensure_fresh((int64_t)B.nt * 8) ||
+        h->bk_hstart.ensure_fresh((int64_t)B.nt * 4) || h->bk_ttot.ensure_fresh(((int64_t)B.nt + 1) * 4) ||
         h->bk_flag.ensure_fresh(64) || h->bk_rd.ensure(64))
         return fail(h, SH_E_OOM, "bucket workspace");
     B.n_staged = h->bk.n_staged;
@@ -2820,11 +2887,14 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
         B.st_dst[k] = h->bk_st[k].p;
         B.st_width[k] = w;
     }
-    // match stream: every partial is consumed at most once, so n values suffice
+    // match stream: one region of SHB_SPAN values per matcher workgroup (its first
+    // pass), then a shared tail for further passes; every partial is consumed at
+    // most once, so n values suffice for the tail
     B.n_ms = n_ms;
+    const int64_t ms_vals = (int64_t)SHB_NB * B.n_chunks * SHB_SPAN + n;
     for (int m = 0; m < n_ms; m++) {
         const int w = type_width(P.attr_type[0][ms[m]]);
-        if (h->bk_ms[m].ensure_fresh(n * w)) return fail(h, SH_E_OOM, "match stream");
+        if (h->bk_ms[m].ensure_fresh(ms_vals * w)) return fail(h, SH_E_OOM, "match stream");
         B.ms[m] = h->bk_ms[m].p;
         B.ms_width[m] = w;
     }
@@ -2847,6 +2917,9 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     B.cnt = h->bk_cnt.as<uint8_t>();
     B.mstart = h->bk_mstart.as<uint32_t>();
     B.tpre = h->bk_tpre.as<int64_t>();
+    B.tfirst = h->bk_tfirst.as<int64_t>();
+    B.hstart = h->bk_hstart.as<int32_t>();
+    B.within = std::max<int64_t>(0, P.within_ms);
     B.ttot = h->bk_ttot.as<uint32_t>();
     B.flag = h->bk_flag.as<int32_t>();
     B.ms_ctr = h->bk_flag.as<uint32_t>() + 4;
@@ -2897,6 +2970,129 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     h->times.advance_launches = 1;
     h->bk_last = 1;
     return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "bucket engine");
+}
+
+// the rise-and-fall sequence on the bucket-carry engine (sh_bucket.hip k_s3b):
+// the tile-local bucket partition, one workgroup per bucket carrying its keys'
+// state across the stream, the ordered rows by k_bk_emit. 0 ok, 1 = not
+// applicable or refused on the device (the caller runs k_seq3s), <0 error
+static int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
+    const bool off = getenv("SH_DISABLE_S3B") != nullptr || getenv("SH_NO_SEQ3") != nullptr;  // (per call: tests A/B it)
+    h->s3b_last = 0;
+    if (off || !h->partitioned || h->T->n_queries != 1 || !h->T->q[0].s3 || nkeys < 1024 || run->n < SHB_TILE)
+        return 1;
+    const nf_query& Q = h->T->q[0];
+    const int kb = std::max(0, bits_for((uint64_t)(nkeys - 1)) - 8);
+    if (kb > 12 || Q.contains_agg) return 1;
+    // every operand and select value: one 4-byte attribute A (no null masks on this path)
+    const int A = Q.s3_a2, ty = Q.s3_t2;
+    if (!(ty == SH_T_FLOAT || ty == SH_T_INT) || A < 0 || A >= (int)h->stream_types[0].size() ||
+        type_width(h->stream_types[0][A]) != 4 || Q.s3_a3 != A || Q.s3_e1a != A || Q.s3_la != A || Q.s3_t3 != ty ||
+        Q.s3_e1t != ty || Q.s3_lt != ty)
+        return 1;
+    shb_out O;
+    memset(&O, 0, sizeof(O));
+    O.n_out = Q.n_out;
+    shb_s3 S;
+    memset(&S, 0, sizeof(S));
+    S.type = ty;
+    S.op2 = Q.s3_op2;
+    S.dom2 = Q.s3_dom2;
+    S.op3 = Q.s3_op3;
+    S.dom3 = Q.s3_dom3;
+    for (int o = 0; o < Q.n_out; o++) {
+        if (Q.s3_out_attr[o] != A || Q.s3_out_type[o] != ty) return 1;
+        O.type[o] = ty;
+        const int sl = Q.s3_out_slot[o];
+        if (sl == 2) {
+            O.kind[o] = 1;
+            O.src[o] = run->d_cols[A];
+            continue;
+        }
+        int m = 0;
+        while (m < S.n_ms && S.ms_slot[m] != sl) m++;
+        if (m == S.n_ms) S.ms_slot[S.n_ms++] = sl;
+        O.kind[o] = 0;
+        O.src[o] = (const void*)(intptr_t)m;  // resolved below
+    }
+    hipStream_t st = h->stream;
+    shb_plan B;
+    memset(&B, 0, sizeof(B));
+    B.n = run->n;
+    B.nt = (int32_t)((run->n + SHB_TILE - 1) / SHB_TILE);
+    B.kb = kb;
+    B.no_ts = 1;
+    const int64_t slots = (int64_t)B.nt * SHB_TILE;
+    if (ensure_ws(h, (int64_t)B.nt + 1) || h->bk_w0.ensure_fresh(slots * 4) || h->bk_sp.ensure_fresh(run->n * 2) ||
+        h->bk_toff.ensure_fresh((int64_t)B.nt * SHB_TOFF * 2) || h->bk_cnt.ensure_fresh(slots) ||
+        h->bk_mstart.ensure_fresh((int64_t)B.nt * SHB_NB * 4) || h->bk_tpre.ensure_fresh((int64_t)B.nt * 8) ||
+        h->bk_tfirst.ensure_fresh((int64_t)B.nt * 8) || h->bk_hstart.ensure_fresh((int64_t)B.nt * 4) ||
+        h->bk_ttot.ensure_fresh(((int64_t)B.nt + 1) * 4) || h->bk_flag.ensure_fresh(64) || h->bk_rd.ensure(64) ||
+        h->bk_st[0].ensure_fresh(slots * 4))
+        return fail(h, SH_E_OOM, "sequence workspace");
+    B.n_staged = 1;
+    B.st_src[0] = run->d_cols[A];
+    B.st_dst[0] = h->bk_st[0].p;
+    B.st_width[0] = 4;
+    // match stream: at most one match per event, in its segment's slots
+    B.n_ms = S.n_ms;
+    for (int m = 0; m < S.n_ms; m++) {
+        if (h->bk_ms[m].ensure_fresh(slots * 4)) return fail(h, SH_E_OOM, "match stream");
+        B.ms[m] = h->bk_ms[m].p;
+        B.ms_width[m] = 4;
+    }
+    for (int o = 0; o < O.n_out; o++)
+        if (O.kind[o] == 0) O.src[o] = B.ms[(int)(intptr_t)O.src[o]];
+    shb_cols OC;
+    memset(&OC, 0, sizeof(OC));
+    if (run->d_out_cols) {
+        OC.use = 1;
+        for (int o = 0; o < O.n_out; o++) {
+            OC.cols[o] = run->d_out_cols[o];
+            OC.colw[o] = 4;
+        }
+    }
+    B.ts = run->d_ts;
+    B.keys = run->d_keys;
+    B.w0 = h->bk_w0.as<uint32_t>();
+    B.sp = h->bk_sp.as<uint16_t>();
+    B.toff = h->bk_toff.as<uint16_t>();
+    B.cnt = h->bk_cnt.as<uint8_t>();
+    B.mstart = h->bk_mstart.as<uint32_t>();
+    B.tpre = h->bk_tpre.as<int64_t>();
+    B.tfirst = h->bk_tfirst.as<int64_t>();
+    B.hstart = h->bk_hstart.as<int32_t>();
+    B.ttot = h->bk_ttot.as<uint32_t>();
+    B.flag = h->bk_flag.as<int32_t>();
+    B.ms_ctr = h->bk_flag.as<uint32_t>() + 4;
+    hipEventRecord(h->ev[0], st);
+    hipMemsetAsync(B.flag, 0, 32, st);
+    hipMemsetAsync(B.ttot, 0, ((int64_t)B.nt + 1) * 4, st);
+    if (shb_partition(run->d_keys, run->d_ts, nkeys, &B, st)) return fail(h, SH_E_HIP, "sequence partition failed");
+    hipEventRecord(h->ev[1], st);
+    if (shb_s3_carry(&B, &S, st)) return fail(h, SH_E_HIP, "sequence carry launch failed");
+    if (shb_finish(&B, h->w_scan.as<uint32_t>(), st)) return fail(h, SH_E_HIP, "sequence scan failed");
+    hipEventRecord(h->ev[2], st);
+    if (shb_emit(&B, &O, &OC, 0, run->d_out_seq, run->d_out_values, run->out_capacity, st))
+        return fail(h, SH_E_HIP, "sequence emit failed");
+    hipEventRecord(h->ev[3], st);
+    hipMemcpyAsync(h->bk_rd.as<void>(0), B.flag, 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(h->bk_rd.as<void>(8), B.ttot + B.nt, 4, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the sequence engine");
+    const int32_t flag = *h->bk_rd.as<int32_t>(0);
+    const int64_t total = *h->bk_rd.as<uint32_t>(8);
+    if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
+    if (flag) return 1;
+    run->out_count = total;
+    if (total > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
+    if (run->d_out_query && total > 0) hipMemsetAsync(run->d_out_query, 0, total * 4, st);
+    hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
+    hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
+    hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
+    hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
+    h->times.advance_launches = 1;
+    h->s3b_last = 1;
+    return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "sequence engine");
 }
 
 // typed output columns requested: engines that write raw rows write them into a
@@ -2979,6 +3175,13 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
             if (h->a_seq.ensure((size_t)std::max<int64_t>(1, run->out_capacity) * 8))
                 return fail(h, SH_E_OOM, "aggregate sequence numbers");
             run->d_out_seq = h->a_seq.as<uint64_t>();
+        }
+        {
+            const int src = run_s3b(h, run, nkeys);
+            if (src != 1) {
+                if (src == SH_OK) h->kstate_stale = true;  // (no key blocks used: reset for a later user)
+                return src;
+            }
         }
         int rc = SH_OK;
         int64_t rows = 0;
@@ -3252,7 +3455,7 @@ int shx_bucket_status(sh_handle* h) {
 }
 
 // 1: the last general-engine sh_run_device took the rise-and-fall sequence engine
-int shx_seq3_status(sh_handle* h) { return h ? h->seq3_last : 0; }
+int shx_seq3_status(sh_handle* h) { return h ? (h->s3b_last ? 2 : h->seq3_last) : 0; }
 // aggregators of the last sh_run_device: 0 none on a fast engine, 1 the post-pass
 // (sh_agg.hip) formed them, 2 it was not exact and a sequential engine ran
 int shx_agg_status(sh_handle* h) { return h ? h->agg_last : 0; }
@@ -3508,6 +3711,10 @@ int sh_snapshot(sh_handle* h, void* buf, int64_t cap, int64_t* size) {
         hipMemsetAsync(h->n_kstate.p, 0, (size_t)h->n_nkeys * h->T->key_words * 8, h->stream);
         hipStreamSynchronize(h->stream);
         h->kstate_stale = false;
+    }
+    if (h->has_device) {
+        const int frc = nf_sev_flush(h);  // the models and ranks the image holds
+        if (frc) return frc;
     }
     SnapW w;
     const int rc = snapshot_image(h, w);

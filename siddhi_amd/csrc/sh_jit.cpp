@@ -69,6 +69,8 @@ const int kWalkDyn = env_int("SH_BK_DYN", 1, 0, 1);
 // allocation is sized for (its LDS holds two 512-thread workgroups per CU)
 const int kMatchMinBlocks = env_int("SH_BK_MINB", 4, 1, 8);
 
+int type_width_of(int t) { return t == SH_T_LONG || t == SH_T_DOUBLE ? 8 : (t == SH_T_BOOL ? 1 : 4); }
+
 const char* col_ctype(int t) {
     switch (t) {
         case SH_T_LONG:
@@ -1057,44 +1059,29 @@ for (int a = A; a < E;) {
 __syncthreads();
 unsigned long long t_prev = wall_clock64();
 #define SHB_PROF(ph) if (P.prof && threadIdx.x == 0) { const unsigned long long t_now = wall_clock64(); atomicAdd(&P.prof[ph], t_now - t_prev); t_prev = t_now; }
-// halo: tile a - 1, and before it every tile whose successor starts within W
-// of tile a's first event (for streams in time order: every tile that can
-// hold an event the window reaches); a walk that needs more raises SHB_F_HALO
-if (threadIdx.x < 64) {
-    const int t = (int)threadIdx.x;
-    bool ok = false;
-    if (t >= 1 && a - t >= 0) {
-        const int64_t ta_ = P.ts[(int64_t)a << SHB_TILE_SHIFT];
-        const int64_t tlim = ta_ < INT64_MIN + SHJ_W ? INT64_MIN : ta_ - SHJ_W;
-        ok = P.ts[(int64_t)(a - t) << SHB_TILE_SHIFT] >= tlim;
-    }
-    const uint64_t m = __ballot(ok);
-    if (t == 0) {
-        int h = 1 + (int)__builtin_ctzll(~(m >> 1));
-        if (h > a) h = a;
-        if (h > SHB_HMAX) h = SHB_HMAX;
-        s_i[0] = a - h;
-    }
+// the halo start (k_bk_tpre: tile a - 1 and the tiles before it that the window
+// can reach) and the bucket starts of tiles [a - SHB_HMAX, E), loaded together
+if (threadIdx.x == 0) s_i[0] = P.hstart[a];
+const int Tm = a - SHB_HMAX + (int)threadIdx.x;
+uint32_t len = 0u, g = 0u;
+if (Tm >= 0 && Tm < E) {
+    const uint16_t* r = P.toff + (int64_t)Tm * SHB_TOFF + b;
+    const uint32_t lo = r[0], hi = r[1];
+    len = hi - lo;
+    g = ((uint32_t)Tm << SHB_TILE_SHIFT) + lo;
 }
 __syncthreads();
 const int h0 = s_i[0];  // first tile of the segment table
 const int nseg = E - h0;
 {
-    uint32_t len = 0u, g = 0u;
-    if ((int)threadIdx.x < nseg) {
-        const int T = h0 + (int)threadIdx.x;
-        const uint16_t* r = P.toff + (int64_t)T * SHB_TOFF + b;
-        const uint32_t lo = r[0], hi = r[1];
-        len = hi - lo;
-        g = ((uint32_t)T << SHB_TILE_SHIFT) + lo;
-    }
+    if (Tm < h0) len = 0u;
     uint32_t tot;
     const uint32_t pre = shw_block_excl<SHB_TPB>(len, ws, &tot);
-    if ((int)threadIdx.x < nseg) {
-        seg_p[threadIdx.x] = pre;
-        seg_g[threadIdx.x] = g;
+    if (Tm >= h0 && Tm < E) {
+        seg_p[Tm - h0] = pre;
+        seg_g[Tm - h0] = g;
     }
-    if ((int)threadIdx.x == nseg) seg_p[nseg] = tot;
+    if (Tm == E) seg_p[nseg] = tot;
 }
 __syncthreads();
 // this pass: consumers from tiles [a, a + ne), at most SHB_CH events; the halo
@@ -1264,10 +1251,12 @@ uint32_t total;
         off += v[q];
     }
 }
-// the pass's match-stream region
-if (threadIdx.x == 0) s_i[1] = total ? (int)atomicAdd(P.ms_ctr, total) : 0;
+// the pass's match-stream region: the workgroup's own for its first pass (a
+// pass takes at most SHB_SPAN), taken from the shared tail for any further one
+if (a != A && threadIdx.x == 0) s_i[1] = total ? (int)atomicAdd(P.ms_ctr, total) : 0;
 __syncthreads();
-const int64_t rbase = (int64_t)(uint32_t)s_i[1];
+const int64_t rbase = a == A ? (int64_t)blockIdx.x * SHB_SPAN
+                             : (int64_t)gridDim.x * SHB_SPAN + (int64_t)(uint32_t)s_i[1];
 // per chunk tile: the first match position of its segment, its matches
 for (int t = ta + (int)threadIdx.x; t < se; t += SHB_TPB) {
     const uint32_t x0 = seg_p[t] - pa, x1 = seg_p[t + 1] - pa;
@@ -1278,7 +1267,34 @@ for (int t = ta + (int)threadIdx.x; t < se; t += SHB_TPB) {
     if (q1 > q0) atomicAdd(&P.ttot[T], q1 - q0);
 }
 SHB_PROF(3)
-// the partials again, their e1-side select values into the region
+)";
+    // one 4-byte match-stream column (C2's e1.price): when no consumer needs the
+    // slow walk (which reads s_ws), the values are staged in s_ws in region order
+    // and the region goes out as one coalesced run
+    const bool stage1 = ms_attrs.size() == 1 && type_width_of(P.attr_type[0][ms_attrs[0]]) == 4;
+    if (stage1) {
+        const std::string a0 = lds(ms_attrs[0]);
+        src += "int slow_ = 0;\nfor (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {\n"
+               "    const int i = hl + (int)(s_cons[ci] >> 16);\n"
+               "    if (s_msk[i - hl] & SHB_MOVF) slow_ = 1;\n}\n"
+               "if (!__syncthreads_or(slow_)) {\n"
+               "for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {\n"
+               "    const uint32_t cw = s_cons[ci];\n"
+               "    const int sp = (int)(cw & 0xFFFFu), i = hl + (int)(cw >> 16);\n"
+               "    const uint32_t off = s_pre[i - hl];\n"
+               "    const uint32_t cn = ((i + 1 < L) ? (uint32_t)s_pre[i + 1 - hl] : total) - off;\n"
+               "    uint32_t m = s_msk[i - hl], k = 0;\n"
+               "    while (m) {\n"
+               "        const int o = sp - __ffs(m);\n"
+               "        m &= m - 1u;\n"
+               "        s_ws[off + (cn - 1u - k)] = (uint32_t)" + a0 + "[o];\n"
+               "        k++;\n"
+               "    }\n}\n"
+               "__syncthreads();\n"
+               "for (int q = threadIdx.x; q < (int)total; q += SHB_TPB) ((uint32_t*)P.ms[0])[rbase + q] = s_ws[q];\n"
+               "} else {\n";
+    }
+    src += R"(// the partials again, their e1-side select values into the region
 for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {
 const uint32_t cw = s_cons[ci];
 const int sp = (int)(cw & 0xFFFFu), i = hl + (int)(cw >> 16);
@@ -1293,7 +1309,9 @@ uint32_t k = 0;
            "    while (m) {\n        const int o = sp - __ffs(m);\n        m &= m - 1u;\n"
            "        const int64_t dst = rbase + (int64_t)off + (int64_t)(cn - 1u - k);\n        k++;\n" +
            ms_put + "    }\n} else {\n" + walk(false, put) + "}\n";
-    src += "}\nSHB_PROF(4)\na += ne;\n}\n}\n";
+    src += "}\n";
+    if (stage1) src += "}\n";
+    src += "SHB_PROF(4)\na += ne;\n}\n}\n";
     return true;
 }
 

@@ -32,9 +32,12 @@ __host__ __device__ __forceinline__ uint32_t shs_mix32(uint32_t x) {
 struct shs_cols {
     const void* src[SHS_MAX_COLS];
     void* dst[SHS_MAX_COLS];
+    int64_t base[SHS_MAX_COLS];  // SHS_W_OFF columns: the offsets' base
     int32_t width[SHS_MAX_COLS];
     int32_t n;
-    int32_t stride;  // record words
+    int32_t stride;   // record words
+    int32_t compact;  // 1: the sequence number is a 32-bit index into the source slice
+    int32_t pad;
 };
 
 struct shs_offs {
@@ -94,18 +97,25 @@ __global__ void k_shs_pack(const uint32_t* __restrict__ pos, int64_t n, shs_cols
             r[w] = (uint32_t)v;
             r[w + 1] = (uint32_t)(v >> 32);
             w += 2;
+        } else if (wd == SHS_W_OFF) {
+            r[w++] = (uint32_t)(((const uint64_t*)C.src[c])[i] - (uint64_t)C.base[c]);
         } else if (wd == 4) {
             r[w++] = ((const uint32_t*)C.src[c])[i];
         } else {
             r[w++] = ((const uint8_t*)C.src[c])[i];
         }
     }
+    if (C.compact) {
+        r[w] = (uint32_t)i;
+        return;
+    }
     const uint64_t s = seq0 + (uint64_t)i;
     r[w] = (uint32_t)s;
     r[w + 1] = (uint32_t)(s >> 32);
 }
 
-__global__ void k_shs_unpack(const uint32_t* __restrict__ rec, int64_t n, shs_cols C, uint64_t* __restrict__ seq) {
+__global__ void k_shs_unpack(const uint32_t* __restrict__ rec, int64_t n, shs_cols C, uint64_t seq0,
+                             uint64_t* __restrict__ seq) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t* r = rec + i * C.stride;
@@ -117,13 +127,15 @@ __global__ void k_shs_unpack(const uint32_t* __restrict__ rec, int64_t n, shs_co
         if (wd == 8) {
             ((uint64_t*)C.dst[c])[i] = (uint64_t)r[w] | ((uint64_t)r[w + 1] << 32);
             w += 2;
+        } else if (wd == SHS_W_OFF) {
+            ((uint64_t*)C.dst[c])[i] = (uint64_t)C.base[c] + (uint64_t)r[w++];
         } else if (wd == 4) {
             ((uint32_t*)C.dst[c])[i] = r[w++];
         } else {
             ((uint8_t*)C.dst[c])[i] = (uint8_t)r[w++];
         }
     }
-    if (seq) seq[i] = (uint64_t)r[w] | ((uint64_t)r[w + 1] << 32);
+    if (seq) seq[i] = C.compact ? seq0 + (uint64_t)r[w] : ((uint64_t)r[w] | ((uint64_t)r[w + 1] << 32));
 }
 
 // first index j in [0, m) with a[j] >= v (a ascending)
@@ -210,17 +222,19 @@ extern "C" int shs_route(const int32_t* d_keys, int64_t n, int32_t world, uint32
     return SH_OK;
 }
 
-static int shs_fill(shs_cols* C, int32_t n_cols, const int32_t* widths) {
+static int shs_fill(shs_cols* C, int32_t n_cols, const int32_t* widths, bool compact = false) {
     if (n_cols < 0 || n_cols > SHS_MAX_COLS || (n_cols && !widths)) return SH_E_INVALID_ARG;
     memset(C, 0, sizeof(*C));
     C->n = n_cols;
+    C->compact = compact ? 1 : 0;
     int w = 0;
     for (int c = 0; c < n_cols; c++) {
-        if (widths[c] != 1 && widths[c] != 4 && widths[c] != 8) return SH_E_INVALID_ARG;
+        if (widths[c] != 1 && widths[c] != 4 && widths[c] != 8 && !(compact && widths[c] == SHS_W_OFF))
+            return SH_E_INVALID_ARG;
         C->width[c] = widths[c];
         w += widths[c] == 8 ? 2 : 1;
     }
-    C->stride = w + 2;
+    C->stride = w + (compact ? 1 : 2);
     return SH_OK;
 }
 
@@ -253,8 +267,53 @@ extern "C" int shs_unpack(const uint32_t* d_rec, int64_t n, int32_t n_cols, void
     }
     if (n == 0) return SH_OK;
     hipLaunchKernelGGL(k_shs_unpack, dim3(shs_blocks(n, 256)), dim3(256), 0, (hipStream_t)stream, d_rec, n, C,
-                       d_seq);
+                       (uint64_t)0, d_seq);
     return shs_ok();
+}
+
+extern "C" int32_t shs_record_words_compact(int32_t n_cols, const int32_t* widths) {
+    shs_cols C;
+    return shs_fill(&C, n_cols, widths, true) == SH_OK ? C.stride : -1;
+}
+
+extern "C" int shs_pack_compact(const uint32_t* d_pos, int64_t n, int32_t n_cols, const void* const* d_cols,
+                                const int32_t* widths, const int64_t* h_base, uint32_t* d_rec, void* stream) {
+    shs_cols C;
+    if (shs_fill(&C, n_cols, widths, true) || n < 0 || n >= ((int64_t)1 << 32) || (n && (!d_pos || !d_rec)))
+        return SH_E_INVALID_ARG;
+    for (int c = 0; c < n_cols; c++) {
+        if (!d_cols[c] || (widths[c] == SHS_W_OFF && !h_base)) return SH_E_INVALID_ARG;
+        C.src[c] = d_cols[c];
+        C.base[c] = widths[c] == SHS_W_OFF ? h_base[c] : 0;
+    }
+    if (n == 0) return SH_OK;
+    hipLaunchKernelGGL(k_shs_pack, dim3(shs_blocks(n, 256)), dim3(256), 0, (hipStream_t)stream, d_pos, n, C,
+                       (uint64_t)0, d_rec);
+    return shs_ok();
+}
+
+extern "C" int shs_unpack_compact(const uint32_t* d_rec, int32_t n_cols, void* const* d_cols, const int32_t* widths,
+                                  const int64_t* h_src_off, int32_t world, const int64_t* h_src_base,
+                                  const uint64_t* h_src_seq0, uint64_t* d_seq, void* stream) {
+    shs_cols C;
+    if (shs_fill(&C, n_cols, widths, true) || world < 1 || world > SHS_MAX_WORLD || !h_src_off || !h_src_seq0)
+        return SH_E_INVALID_ARG;
+    // one launch per source rank: its records' bases and first sequence number
+    for (int r = 0; r < world; r++) {
+        const int64_t a = h_src_off[r], m = h_src_off[r + 1] - a;
+        if (m < 0) return SH_E_INVALID_ARG;
+        if (m == 0) continue;
+        for (int c = 0; c < n_cols; c++) {
+            if (!d_cols[c] || (widths[c] == SHS_W_OFF && !h_src_base)) return SH_E_INVALID_ARG;
+            const int w = widths[c] == SHS_W_OFF ? 8 : widths[c];
+            C.dst[c] = (uint8_t*)d_cols[c] + a * w;
+            C.base[c] = widths[c] == SHS_W_OFF ? h_src_base[(int64_t)r * n_cols + c] : 0;
+        }
+        hipLaunchKernelGGL(k_shs_unpack, dim3(shs_blocks(m, 256)), dim3(256), 0, (hipStream_t)stream,
+                           d_rec + a * C.stride, m, C, h_src_seq0[r], d_seq ? d_seq + a : nullptr);
+        if (shs_ok()) return SH_E_HIP;
+    }
+    return SH_OK;
 }
 
 extern "C" int shs_rows_home(uint64_t* d_oseq, int64_t m, uint64_t seq_base, const uint64_t* d_gseq,

@@ -101,6 +101,14 @@ class HipShardOps:
         L.shs_pack.restype = C.c_int
         L.shs_unpack.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.shs_unpack.restype = C.c_int
+        L.shs_record_words_compact.argtypes = [C.c_int32, C.c_void_p]
+        L.shs_record_words_compact.restype = C.c_int32
+        L.shs_pack_compact.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p]
+        L.shs_pack_compact.restype = C.c_int
+        L.shs_unpack_compact.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.shs_unpack_compact.restype = C.c_int
         L.shs_rows_home.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
                                     C.c_void_p]
         L.shs_rows_home.restype = C.c_int
@@ -155,6 +163,40 @@ class HipShardOps:
                     "shs_unpack")
         return cols, seq
 
+    # compact records: column 0 (timestamps) as a 32-bit offset from the slice's
+    # base, the sequence number as a 32-bit index into the source slice
+    compact = True
+
+    def pack_compact(self, pos, cols, tbase):
+        torch = self.torch
+        n = cols[0].numel()
+        widths = [SHS_W_OFF] + [_width(c) for c in cols[1:]]
+        w = (C.c_int32 * len(widths))(*widths)
+        stride = int(self.lib.shs_record_words_compact(len(widths), w))
+        rec = torch.empty(max(n * stride, 1), dtype=torch.int32, device=self.device)
+        cp = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
+        base = (C.c_int64 * len(cols))(*([tbase] + [0] * (len(cols) - 1)))
+        self._check(self.lib.shs_pack_compact(pos.data_ptr(), n, len(cols), cp, w, base, rec.data_ptr(),
+                                              self._stream()), "shs_pack_compact")
+        return rec[: n * stride], stride
+
+    def unpack_compact(self, rec, like, src_off, src_tbase, src_seq0):
+        torch = self.torch
+        n = src_off[-1]
+        world = len(src_off) - 1
+        cols = [torch.empty(max(n, 1), dtype=c.dtype, device=self.device)[:n] for c in like]
+        seq = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)[:n]
+        widths = [SHS_W_OFF] + [_width(c) for c in like[1:]]
+        nc = len(like)
+        cp = (C.c_void_p * nc)(*[c.data_ptr() for c in cols])
+        w = (C.c_int32 * nc)(*widths)
+        offs = (C.c_int64 * (world + 1))(*src_off)
+        base = (C.c_int64 * (world * nc))(*[src_tbase[r] if c == 0 else 0 for r in range(world) for c in range(nc)])
+        s0 = (C.c_uint64 * world)(*src_seq0)
+        self._check(self.lib.shs_unpack_compact(rec.data_ptr(), nc, cp, w, offs, world, base, s0, seq.data_ptr(),
+                                                self._stream()), "shs_unpack_compact")
+        return cols, seq
+
     def rows_home(self, oseq, m, seq_base, gseq, src_off, world):
         offs = (C.c_int64 * (world + 1))(*src_off)
         counts = (C.c_int64 * world)()
@@ -173,6 +215,9 @@ class HipShardOps:
         return seq_out[:m], vals_out[: m * n_out].view(m, n_out)
 
 
+SHS_W_OFF = 5  # include/siddhi_shard.h: an 8-byte column carried as a 32-bit offset
+
+
 class TorchComm:
     """the step's two exchanges over torch.distributed (RCCL "nccl" on GPUs, gloo
     on CPU): all_to_all_single with per-rank split sizes"""
@@ -180,6 +225,14 @@ class TorchComm:
     def __init__(self, world, group=None):
         import torch.distributed as dist
         self.dist, self.world, self.group = dist, world, group
+
+    def meta(self, vals, device):
+        """every rank's small int64 vector (all_gather): list per rank"""
+        import torch
+        mine = torch.tensor(vals, dtype=torch.int64, device=device)
+        out = [torch.empty_like(mine) for _ in range(self.world)]
+        self.dist.all_gather(out, mine, group=self.group)
+        return [[int(x) for x in o.cpu().tolist()] for o in out]
 
     def counts(self, counts, device):
         import torch
@@ -203,6 +256,9 @@ class BounceComm(TorchComm):
 
     def counts(self, counts, device):
         return super().counts(counts, "cpu")
+
+    def meta(self, vals, device):
+        return super().meta(vals, "cpu")
 
     def exchange(self, send, send_counts, recv_counts, per):
         return super().exchange(send.cpu(), send_counts, recv_counts, per).to(send.device)
@@ -237,15 +293,39 @@ class KeyShardedStep:
             assert seq0 % batch == 0, "run ids need ingest slices cut at send() call boundaries"
         dev = ts.device
         world = self.world
+        ev = self._events(dev)
+        self._mark(ev, 0)
+        # compact records when every rank's slice fits 32-bit timestamp offsets:
+        # every rank's first sequence number and timestamp base travel once
+        compact = False
+        if getattr(self.ops, "compact", False) and hasattr(self.comm, "meta") and ts.numel() > 0:
+            import torch
+            lo_hi = torch.stack([ts.min(), ts.max()]).cpu().tolist()
+            meta = self.comm.meta([seq0, lo_hi[0], int(lo_hi[1] - lo_hi[0] < (1 << 32) - 1)], dev)
+            compact = all(m[2] for m in meta)
+        elif getattr(self.ops, "compact", False) and hasattr(self.comm, "meta"):
+            meta = self.comm.meta([seq0, 0, 1], dev)
+            compact = all(m[2] for m in meta)
         # 1. route + pack (columns: ts, [keys,] then the attribute columns[, run ids])
         pos, send_counts = self.ops.route(keys, world)
         allc = [ts] + ([] if key_attr is not None else [keys]) + list(cols) + ([run_ids] if run_ids is not None else [])
-        rec, stride = self.ops.pack(pos, allc, seq0)
+        if compact:
+            rec, stride = self.ops.pack_compact(pos, allc, meta[self.rank][1])
+        else:
+            rec, stride = self.ops.pack(pos, allc, seq0)
+        self._mark(ev, 1)
         # 2. shuffle
         recv_counts = self.comm.counts(send_counts, dev)
         rrec = self.comm.exchange(rec, send_counts, recv_counts, stride)
         n_recv = sum(recv_counts)
-        ucols, gseq = self.ops.unpack(rrec, n_recv, allc)
+        self._mark(ev, 2)
+        if compact:
+            off = [0]
+            for c in recv_counts:
+                off.append(off[-1] + c)
+            ucols, gseq = self.ops.unpack_compact(rrec, allc, off, [m[1] for m in meta], [m[0] for m in meta])
+        else:
+            ucols, gseq = self.ops.unpack(rrec, n_recv, allc)
         r_run = None
         if run_ids is not None:
             r_run, ucols = ucols[-1], ucols[:-1]
@@ -259,6 +339,7 @@ class KeyShardedStep:
             m, oseq, ovals = self.matcher(r_ts, r_keys, r_cols, n_keys)
         else:
             m, oseq, ovals = self.matcher(r_ts, r_keys, r_cols, n_keys, run=r_run)
+        self._mark(ev, 3)
         # 4. rows back to the ranks holding their trigger events
         src_off = [0]
         for c in recv_counts:
@@ -281,6 +362,7 @@ class KeyShardedStep:
             oseq, n_val = mkey.contiguous(), self.n_out + 1
         hseq = self.comm.exchange(oseq, row_counts, back_counts, 1)
         hvals = self.comm.exchange(ovals, row_counts, back_counts, n_val)
+        self._mark(ev, 4)
         # 5. k-way merge of the owners' runs by trigger sequence (or run)
         run_off = [0]
         for c in back_counts:
@@ -288,5 +370,31 @@ class KeyShardedStep:
         seq, vals = self.ops.merge(hseq, hvals, n_val, run_off)
         if mkey is not None:
             seq, vals = vals[:, 0].contiguous(), vals[:, 1:].contiguous()
-        self.last = dict(sent=send_counts, received=recv_counts, matches_here=m, rows_home=run_off[-1])
+        self._mark(ev, 5)
+        self.last = dict(sent=send_counts, received=recv_counts, matches_here=m, rows_home=run_off[-1],
+                         record_bytes=4 * stride, compact=compact)
+        self._ev = ev
         return seq, vals
+
+    PHASES = ("route_pack", "exchange_out", "unpack_match", "exchange_back", "merge")
+
+    def _events(self, dev):
+        """timing marks on the launch stream (device GPUs only)"""
+        if getattr(dev, "type", "cpu") != "cuda":
+            return None
+        import torch
+        return [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+
+    @staticmethod
+    def _mark(ev, i):
+        if ev is not None:
+            ev[i].record()
+
+    def phase_ms(self):
+        """the last step's phases in ms (route + pack, exchange out, unpack +
+        match, row return, merge), from events on the launch stream"""
+        ev = getattr(self, "_ev", None)
+        if ev is None:
+            return None
+        ev[5].synchronize()
+        return {k: ev[i].elapsed_time(ev[i + 1]) for i, k in enumerate(self.PHASES)}

@@ -74,3 +74,18 @@ class CollidingNames:
 
     def __getattr__(self, name):
         return getattr(self.eng, name)
+
+
+def c4_digest(out):
+    """count and SHA-256 of a drained output's rows in order: per row the trigger
+    sequence (int64), query (int32), output timestamp (int64), raw values (int64)
+    and null flags (the fields same_output compares)"""
+    import hashlib
+    m = len(out["seq"])
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(np.asarray(out["seq"], np.int64)).tobytes())
+    h.update(np.ascontiguousarray(np.asarray(out["query"], np.int32)).tobytes())
+    h.update(np.ascontiguousarray(np.asarray(out["ts"], np.int64)).tobytes())
+    h.update(np.ascontiguousarray(np.asarray(out["values"], np.int64)).tobytes())
+    h.update(np.ascontiguousarray(np.asarray(out["nulls"]).astype(np.uint8)).tobytes())
+    return {"rows": int(m), "sha256": h.hexdigest()}

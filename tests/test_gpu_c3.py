@@ -1,9 +1,10 @@
-"""C3 (BASELINE.json configs[2]) on the rise-and-fall sequence engine (k_seq3,
-sh_nfa.hip) through sh_run_device: bit-exact against the oracle at 300k events
-(with price ties), against the vectorised restatement tests/c3_check.py
-(pinned to the oracle in tests/test_c3_checker.py) at the full 100M events /
-1M keys, and the general engine on the same input (SH_NO_SEQ3) for the shape's
-near relatives."""
+"""C3 (BASELINE.json configs[2]) through sh_run_device on its three device forms:
+the bucket-carry engine (k_s3b, sh_bucket.hip: the default, seq3 status 2), the
+rise-and-fall key-segment engine (k_seq3s / k_seq3, sh_nfa.hip, status 1;
+SH_DISABLE_S3B=1) and the general engine (SH_NO_SEQ3=1, status 0): bit-exact
+against the oracle at 300k events (with price ties), against the vectorised
+restatement tests/c3_check.py (pinned to the oracle in tests/test_c3_checker.py)
+at the full 100M events / 1M keys, and the shape's near relatives."""
 import os
 
 import numpy as np
@@ -36,26 +37,39 @@ def _gpu(text, ts, cols, keys, nk):
     return r
 
 
-@pytest.mark.parametrize("ties,engine", [(False, "seq3"), (True, "seq3"), (False, "general")])
-def test_c3_vs_oracle(ties, engine, monkeypatch):
+ENGINE = {"s3b": 2, "seq3": 1, "general": 0}
+
+
+def _engine(engine, monkeypatch):
     if engine == "general":
         monkeypatch.setenv("SH_NO_SEQ3", "1")
+    elif engine == "seq3":
+        monkeypatch.setenv("SH_DISABLE_S3B", "1")
+    return ENGINE[engine]
+
+
+@pytest.mark.parametrize("ties,engine", [(False, "s3b"), (True, "s3b"), (False, "seq3"), (True, "seq3"),
+                                         (False, "general")])
+def test_c3_vs_oracle(ties, engine, monkeypatch):
+    want = _engine(engine, monkeypatch)
     n, nk = 300_000, 5_000
     ts, k, p, v = synth.stock_stream(n, nk, 1000, config_index=3)
     if ties:
         p = np.random.default_rng(3).integers(0, 5, n).astype(np.float32)
     seq, _, vals, _ = run_stock_oracle(compiler.compile_app(synth.C3_QUERY), ts, k, p, v)
     gseq, gvals, st = _gpu(synth.C3_QUERY, ts, [k, p, v], k, nk)
-    assert st == (1 if engine == "seq3" else 0)
+    assert st == want
     assert len(gseq) == len(seq) > 0
     assert np.array_equal(gseq, seq.astype(np.int64)) and np.array_equal(gvals, vals)
 
 
-def test_c3_full_size_vs_restatement():
+@pytest.mark.parametrize("engine", ["s3b", "seq3"])
+def test_c3_full_size_vs_restatement(engine, monkeypatch):
+    want = _engine(engine, monkeypatch)
     n, nk = 100_000_000, 1_000_000
     ts, k, p, v = synth.stock_stream(n, nk, 1000, config_index=3)
     gseq, gvals, st = _gpu(synth.C3_QUERY, ts, [k, p, v], k, nk)
-    assert st == 1
+    assert st == want
     eseq, evals = c3_expected(ts, k, p)
     assert len(gseq) == len(eseq) > 0
     assert np.array_equal(gseq, eseq) and np.array_equal(gvals, evals)
@@ -76,29 +90,35 @@ def test_mixed_attribute_shape_vs_oracle():
     assert np.array_equal(gseq, seq.astype(np.int64)) and np.array_equal(gvals, vals)
 
 
-@pytest.mark.parametrize("engine", ["seq3", "general"])
+@pytest.mark.parametrize("engine", ["s3b", "seq3", "general"])
 def test_c3_18bit_keys_vs_restatement(engine, monkeypatch):
-    """200k keys (18 bits) on the rise-and-fall and the general engine: three 8-bit
-    radix passes by default, two 10-bit passes when the process runs with SH_RADIX10=1
-    (scripts/gpu_radix10.sh ran this file both ways)"""
-    if engine == "general":
-        monkeypatch.setenv("SH_NO_SEQ3", "1")
+    """200k keys (18 bits): 10 local key bits per bucket on the carry engine (two
+    6-bit sort passes per chunk); three 8-bit radix passes on the key-segment ones"""
+    want = _engine(engine, monkeypatch)
     n, nk = 4_000_000, 200_000
     ts, k, p, v = synth.stock_stream(n, nk, 1000, config_index=3)
     gseq, gvals, st = _gpu(synth.C3_QUERY, ts, [k, p, v], k, nk)
-    assert st == (1 if engine == "seq3" else 0)
+    assert st == want
     eseq, evals = c3_expected(ts, k, p)
     assert len(gseq) == len(eseq) > 0
     assert np.array_equal(gseq, eseq) and np.array_equal(gvals, evals)
 
 
-@pytest.mark.parametrize("variant", ["null_keys", "all_null", "hot_key", "generic_records", "unstaged"])
-def test_c3_seq3_edge_cases_vs_oracle(variant, monkeypatch):
-    """k_seq3s's edges: null-key events (the run after the last segment has no
-    records), no keyed event at all, one hot key walked over many rounds while its
-    workgroup's other lanes idle; and the A/B forms (generic records, the one-lane-
+@pytest.mark.parametrize("engine", ["s3b", "seq3"])
+@pytest.mark.parametrize("variant", ["null_keys", "all_null", "hot_key", "generic_records", "unstaged",
+                                     "few_keys"])
+def test_c3_seq3_edge_cases_vs_oracle(variant, engine, monkeypatch):
+    """edges: null-key events (no bucket on the carry engine; the run after the
+    last segment on k_seq3s), no keyed event at all, one hot key (30% of the events:
+    one tile per carry chunk; many rounds of one lane on k_seq3s), 64 local keys
+    (kb = 6: one sort pass); and k_seq3s's A/B forms (generic records, the one-lane-
     per-key k_seq3)"""
+    if engine == "s3b" and variant in ("generic_records", "unstaged"):
+        pytest.skip("k_seq3s forms")
+    want = _engine(engine, monkeypatch)
     n, nk = 200_000, 2_000
+    if variant == "few_keys":
+        nk = 16_384
     ts, k, p, v = synth.stock_stream(n, nk, 1000, config_index=3)
     k = k.copy()
     rng = np.random.default_rng(11)
@@ -114,7 +134,7 @@ def test_c3_seq3_edge_cases_vs_oracle(variant, monkeypatch):
         monkeypatch.setenv("SH_S3_STAGED", "0")
     seq, _, vals, _ = run_columns_oracle(compiler.compile_app(synth.C3_QUERY), ts, [k, p, v], k)
     gseq, gvals, st = _gpu(synth.C3_QUERY, ts, [k, p, v], k, nk)
-    assert st == 1
+    assert st == want
     assert len(gseq) == len(seq)
     assert (len(seq) == 0) == (variant == "all_null")
     assert np.array_equal(gseq, seq.astype(np.int64)) and np.array_equal(gvals, vals)

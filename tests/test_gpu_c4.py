@@ -80,3 +80,23 @@ def test_c4_spec_workload_1M_users(every):
     eng.close()
     assert len(ref["seq"]) > 10_000
     assert same_output(got, ref), (len(got["seq"]), len(ref["seq"]))
+
+
+def test_c4_spec_workload_10M_users_digest():
+    """the full SURVEY 8d C4 stream -- 100M events over 10M users -- against the
+    digest of the oracle's ordered output on the same stream (tests/golden/
+    c4_digest.json, tests/golden/make_c4_digest.py): at 10M keys the scheduler's
+    HashMap resizes through tables no smaller test reaches (Scheduler.java:74-99,
+    PartitionStateHolder.java:36)"""
+    import json
+    import os
+    from c4_cases import c4_digest
+    from siddhi_amd import compiler, synth
+    from siddhi_amd._native import HipEngine
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c4_digest.json")
+    want = json.load(open(path))["default_100000000_10000000"]
+    blocks = synth.c4_spec_stream(100_000_000, 10_000_000, rate_per_ms=100, batch=4096)
+    eng = HipEngine(compiler.compile_app(synth.C4_QUERY))
+    got = run_c4(eng, blocks)
+    eng.close()
+    assert c4_digest(got) == {"rows": want["rows"], "sha256": want["sha256"]}

@@ -52,9 +52,10 @@ def test_rule_sets_vs_oracle(ci, general, monkeypatch):
     assert np.array_equal(vals[:, :2], ref["values"][:, :2])
 
 
-def test_c5_large_vs_vectorised_restatement():
-    """1,000 rules (BASELINE distributions), 20M card transactions, 200k cards."""
-    n, cards = 20_000_000, 200_000
+@pytest.mark.parametrize("n,cards", [(20_000_000, 200_000), (100_000_000, 1_000_000)])
+def test_c5_large_vs_vectorised_restatement(n, cards):
+    """1,000 rules (BASELINE distributions): 20M card transactions over 200k cards,
+    and the full SURVEY 8d size, 100M transactions over 1M cards."""
     ts, card, amount, merchant = synth.txn_stream(n, cards, 100)
     rules = synth.c5_rules()
     text = synth.c5_query(rules)

@@ -56,6 +56,41 @@ def test_route_pack_unpack_match_contract(world):
     assert np.array_equal(seq.cpu().numpy(), 77 + order)
 
 
+def test_compact_pack_unpack_match_contract():
+    """shs_pack_compact / shs_unpack_compact against the numpy contract: two
+    sources with their own timestamp bases and first sequence numbers"""
+    import torch
+    from test_sharding import CpuShardOps
+    rng = np.random.default_rng(71)
+    hip, cpu = _ops(), CpuShardOps()
+    recs_d, recs_c, want, s0s, tbs = [], [], [], [], []
+    s0 = 0
+    for n, tb in ((200_003, 1_700_000_000_000), (150_001, 1_700_003_000_000)):
+        keys = rng.integers(0, 10_000, n).astype(np.int32)
+        ts = tb + np.cumsum(rng.integers(0, 3, n)).astype(np.int64)
+        f = rng.random(n).astype(np.float32)
+        v = rng.integers(-5, 5, n).astype(np.int64)
+        host = [torch.from_numpy(a) for a in (ts, keys, f, v)]
+        pos_c, _ = cpu.route(host[1], 3)
+        pos_d = pos_c.to(torch.int32).cuda()
+        rd, sd = hip.pack_compact(pos_d, [t.cuda() for t in host], int(ts.min()))
+        rc, sc = cpu.pack_compact(pos_c, host, int(ts.min()))
+        assert sd == sc == 6  # ts 1 + key 1 + price 1 + volume 2 + index 1 words (24 B)
+        assert np.array_equal(rd.cpu().numpy(), rc.numpy())
+        order = np.argsort(pos_c.numpy())
+        recs_d.append(rd)
+        want.append((ts[order], keys[order], f[order], v[order], s0 + order))
+        s0s.append(s0)
+        tbs.append(int(ts.min()))
+        s0 += n
+    like = [torch.zeros(1, dtype=t, device="cuda:0") for t in (torch.int64, torch.int32, torch.float32, torch.int64)]
+    off = [0, 200_003, 350_004, 350_004]
+    cols, seq = hip.unpack_compact(torch.cat(recs_d), like, off, tbs + [0], s0s + [0])
+    for i, c in enumerate(cols):
+        assert np.array_equal(c.cpu().numpy(), np.concatenate([w[i] for w in want]))
+    assert np.array_equal(seq.cpu().numpy(), np.concatenate([w[4] for w in want]))
+
+
 def test_rows_home_and_merge():
     import torch
     rng = np.random.default_rng(5)
@@ -93,6 +128,13 @@ class _ThreadComm:
         comm = self
 
         class V:
+            def meta(self, vals, device):
+                comm.box[("meta", rank)] = list(vals)
+                comm.bar.wait()
+                got = [list(comm.box[("meta", s)]) for s in range(comm.world)]
+                comm.bar.wait()
+                return got
+
             def counts(self, counts, device):
                 for d in range(comm.world):
                     comm.box[(rank, d)] = counts[d]
@@ -185,6 +227,7 @@ def test_sharded_step_virtual_ranks_equal_single_stream(world, config):
     mseq = np.concatenate([o[0] for o in out])
     mvals = np.concatenate([o[1] for o in out])
     assert all(o[2]["matches_here"] > 0 for o in out)
+    assert all(o[2]["compact"] for o in out)
     assert len(mseq) == len(eseq) > 0
     assert np.array_equal(mseq, eseq)
     if wq:

@@ -58,6 +58,37 @@ class CpuShardOps:
         seq = torch.from_numpy(rows[:, w:w + 2].copy().view(np.int64).reshape(n))
         return cols, seq
 
+    # the compact record contract (shs_pack_compact / shs_unpack_compact): column 0
+    # as a 32-bit offset from the slice's timestamp base, the sequence number as a
+    # 32-bit index into the source slice
+    compact = True
+
+    def pack_compact(self, pos, cols, tbase):
+        n = cols[0].numel()
+        words = [(cols[0].numpy().astype(np.int64) - tbase).astype(np.uint32).reshape(n, 1)]
+        for c in cols[1:]:
+            a = c.numpy()
+            words.append(a.view(np.uint32).reshape(n, 2 if a.dtype.itemsize == 8 else 1))
+        idx = np.arange(n, dtype=np.uint32).reshape(n, 1)
+        rows = np.concatenate(words + [idx], axis=1)
+        out = np.empty_like(rows)
+        out[pos.numpy()] = rows
+        return torch.from_numpy(out.view(np.int32).reshape(-1).copy()), rows.shape[1]
+
+    def unpack_compact(self, rec, like, src_off, src_tbase, src_seq0):
+        n = src_off[-1]
+        stride = 1 + sum(2 if c.element_size() == 8 else 1 for c in like[1:]) + 1
+        rows = rec.numpy().view(np.uint32).reshape(n, stride)
+        src = np.searchsorted(np.asarray(src_off[1:]), np.arange(n), side="right")
+        cols = [torch.from_numpy((rows[:, 0].astype(np.int64) + np.asarray(src_tbase, np.int64)[src]))]
+        w = 1
+        for c in like[1:]:
+            k = 2 if c.element_size() == 8 else 1
+            cols.append(torch.from_numpy(rows[:, w:w + k].copy().view(c.numpy().dtype).reshape(n)))
+            w += k
+        seq = np.asarray(src_seq0, np.int64)[src] + rows[:, w].astype(np.int64)
+        return cols, torch.from_numpy(seq)
+
     def rows_home(self, oseq, m, seq_base, gseq, src_off, world):
         local = oseq.numpy()[:m] - seq_base
         b = np.searchsorted(local, np.asarray(src_off), side="left")
@@ -171,8 +202,11 @@ def test_sharded_step_world2_equals_single_process(config):
         want = np.concatenate([want, ref["query"].astype(np.int64)[:, None]], 1)
     mseq = np.concatenate([x[0] for x in parts])
     mvals = np.concatenate([x[1] for x in parts])
-    # both ranks shuffled events both ways and matched
+    # both ranks shuffled events both ways and matched, in compact records
     assert all(min(x[2]["sent"]) > 0 and x[2]["matches_here"] > 0 for x in parts)
+    assert all(x[2]["compact"] for x in parts)
+    if config == "c2":  # ts offset 4 + symbol 4 + price 4 + volume 8 + slice index 4
+        assert all(x[2]["record_bytes"] == 24 for x in parts)
     assert len(mseq) == len(ref["seq"]) > 0
     assert np.array_equal(mseq, ref["seq"].astype(np.int64))
     assert np.array_equal(mvals, want)
@@ -209,3 +243,27 @@ def test_cpu_ops_route_pack_roundtrip(world):
     order = np.argsort(own, kind="stable")
     assert np.array_equal(cols[0].numpy(), ts[order]) and np.array_equal(cols[1].numpy(), keys[order])
     assert np.array_equal(cols[2].numpy(), f[order]) and np.array_equal(seq.numpy(), 1000 + order)
+
+
+def test_cpu_ops_compact_roundtrip():
+    """compact records: timestamps rebuilt from each source's base, sequence
+    numbers from each source's first one"""
+    rng = np.random.default_rng(5)
+    ops = CpuShardOps()
+    parts = []
+    for src, (n, tb, s0) in enumerate([(700, 1_700_000_000_000, 0), (500, 1_700_000_900_000, 700)]):
+        keys = rng.integers(0, 99, n).astype(np.int32)
+        ts = tb + np.sort(rng.integers(0, 1 << 31, n)).astype(np.int64)
+        v = rng.integers(-5, 5, n).astype(np.int64)
+        pos = torch.from_numpy(np.arange(n))
+        rec, stride = ops.pack_compact(pos, [torch.from_numpy(ts), torch.from_numpy(keys), torch.from_numpy(v)],
+                                       int(ts.min()))
+        assert stride == 5  # 1 + 1 + 2 + 1 words
+        parts.append((rec, ts, keys, v, int(ts.min()), s0))
+    rec = torch.cat([p[0] for p in parts])
+    like = [torch.zeros(1, dtype=torch.int64), torch.zeros(1, dtype=torch.int32), torch.zeros(1, dtype=torch.int64)]
+    cols, seq = ops.unpack_compact(rec, like, [0, 700, 1200], [p[4] for p in parts], [p[5] for p in parts])
+    assert np.array_equal(cols[0].numpy(), np.concatenate([p[1] for p in parts]))
+    assert np.array_equal(cols[1].numpy(), np.concatenate([p[2] for p in parts]))
+    assert np.array_equal(cols[2].numpy(), np.concatenate([p[3] for p in parts]))
+    assert np.array_equal(seq.numpy(), np.arange(1200))
