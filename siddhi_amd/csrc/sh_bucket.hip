@@ -378,13 +378,13 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
             sl[j] = l < tile_n ? (uint32_t)P.sp[b0 + l] : 0u;
         }
     }
-    // 1. counts in the tile's bucket order -> pfx
+    // 1. counts in the tile's bucket order -> pfx (loaded with the events; the
+    // slots past the tile's valid events are masked below)
     {
+        const int s0 = threadIdx.x * 16;
+        const uint4 q = *(const uint4*)(P.cnt + b0 + s0);
         __syncthreads();
         const int nv = to[SHB_NB];
-        const int s0 = threadIdx.x * 16;
-        uint4 q = make_uint4(0u, 0u, 0u, 0u);
-        if (s0 < nv) q = *(const uint4*)(P.cnt + b0 + s0);
         uint32_t c[16];
         const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
         uint32_t sum = 0;
@@ -647,6 +647,13 @@ __global__ void __launch_bounds__(S3B_TPB) k_s3b(shb_plan P, shb_s3 S) {
     const int t = S.type;
     for (int k = threadIdx.x; k < S3B_NK; k += S3B_TPB) st_f[k] = 0;
     const uint32_t* __restrict__ gcol = (const uint32_t*)P.st_dst[0];
+    unsigned long long t_prev = wall_clock64();
+#define S3B_PROF(ph)                                                                 \
+    if (P.prof && threadIdx.x == 0) {                                                \
+        const unsigned long long t_now = wall_clock64();                             \
+        atomicAdd(&P.prof[ph], t_now - t_prev);                                      \
+        t_prev = t_now;                                                              \
+    }
     for (int a = 0; a < P.nt;) {
         __syncthreads();
         // the bucket's segments of tiles [a, a + SHB_CT_MAX), their prefix
@@ -701,6 +708,7 @@ __global__ void __launch_bounds__(S3B_TPB) k_s3b(shb_plan P, shb_s3 S) {
             }
         }
         __syncthreads();
+        S3B_PROF(0)
         // stable sort by local key
         const uint16_t* srt;
         if (kb <= 6) {
@@ -711,6 +719,7 @@ __global__ void __launch_bounds__(S3B_TPB) k_s3b(shb_plan P, shb_s3 S) {
             s3b_sort_pass(c_key, o_a, o_b, L, 6, wc, ws);
             srt = o_b;
         }
+        S3B_PROF(1)
         // the first event of each key run steps through the run
         for (int q = threadIdx.x; q < L; q += S3B_TPB) {
             const uint32_t ci = srt[q];
@@ -739,6 +748,7 @@ __global__ void __launch_bounds__(S3B_TPB) k_s3b(shb_plan P, shb_s3 S) {
             st_last[key] = lastb;
         }
         __syncthreads();
+        S3B_PROF(2)
         // matches: exclusive prefix over the chunk in arrival order (4 per thread)
         uint32_t total;
         {
@@ -784,6 +794,219 @@ __global__ void __launch_bounds__(S3B_TPB) k_s3b(shb_plan P, shb_s3 S) {
             for (int m = 0; m < S.n_ms; m++) ((uint32_t*)P.ms[m])[dst] = S.ms_slot[m] == 0 ? m_v0[i] : m_v1[i];
         }
 #undef S3B_GIDX
+        S3B_PROF(3)
+        a += ne;
+    }
+#undef S3B_PROF
+}
+
+// ---------------------------------------------------------------- aggregate carry
+// Select-clause aggregators of the bucketed window engine (C2 select variant ii):
+// one running value per partition key and output, added in the reference's order
+// -- the key's matches in trigger order, each consumer's matches in partial
+// creation order (AttributeAggregatorExecutor state per partition key;
+// SumAttributeAggregatorExecutor.java:167-185: sum(int|long) -> long with Java
+// wrap-around, sum(float|double) -> double, value += (double) x;
+// AvgAttributeAggregatorExecutor.java:145-155: the double sum / count;
+// count() -> long). One workgroup per key bucket walks the bucket's segments of
+// every tile in order (chunks of at most AGC_CH events), with every local key's
+// running values in LDS: per chunk the events' counts (cnt, at their slots) give
+// each consumer its rows -- a prefix over the chunk, and the match-stream position
+// mstart[T][b] + the prefix inside its (tile, bucket) segment; the e1-side
+// arguments of the chunk's rows are gathered into LDS; a stable sort by local key
+// puts each key's consumers together in arrival order and the first consumer of
+// each key run adds them all in sequence, writing the running values by match-
+// stream position (k_bk_emit writes them into the rows). No exactness proof is
+// needed: the additions are the reference's own sequence.
+#define AGC_TPB 1024
+#define AGC_CH 4096
+#define AGC_NR (AGC_CH / AGC_TPB)
+#define AGC_ROWS 8192  // rows of a chunk whose e1-side arguments fit LDS (more: SHB_F_AGG)
+
+__device__ __forceinline__ int64_t agc_load(const void* p, int64_t i, int type) {
+    return (type == SH_T_LONG || type == SH_T_DOUBLE) ? ((const int64_t*)p)[i] : (int64_t)((const uint32_t*)p)[i];
+}
+
+// one running value: sum(int|long) in long, the rest in double (bits)
+__device__ __forceinline__ void agc_add(int kind, int type, int64_t& acc, int64_t x) {
+    if (kind == SH_AGG_SUM && (type == SH_T_INT || type == SH_T_LONG)) {
+        const int64_t v = type == SH_T_INT ? (int64_t)(int32_t)x : x;
+        acc = (int64_t)((uint64_t)acc + (uint64_t)v);
+        return;
+    }
+    double d;
+    switch (type) {
+        case SH_T_INT: d = (double)(int32_t)x; break;
+        case SH_T_LONG: d = (double)x; break;
+        case SH_T_FLOAT: d = (double)__uint_as_float((uint32_t)x); break;
+        default: d = __longlong_as_double(x);
+    }
+    acc = __double_as_longlong(__longlong_as_double(acc) + d);
+}
+
+__global__ void __launch_bounds__(AGC_TPB) k_bk_aggc(shb_plan P, shb_aggc A) {
+    __shared__ int64_t st_acc[SHB_MAX_AGG][256];
+    __shared__ int64_t st_cnt[256];
+    __shared__ uint32_t c_key[AGC_CH];   // local key | count << 16
+    __shared__ uint16_t c_pre[AGC_CH];   // the consumer's first row in the chunk
+    __shared__ uint32_t c_mp[AGC_CH];    // ... and its match-stream position
+    __shared__ int64_t c_e2w[AGC_CH];    // e2-side argument, column 0 (any width)
+    __shared__ uint32_t c_e2n[AGC_CH];   // e2-side argument, column 1 (4-byte)
+    __shared__ uint32_t r_e1[AGC_ROWS];  // e1-side argument per row of the chunk
+    __shared__ uint16_t o_a[AGC_CH], o_b[AGC_CH];
+    __shared__ uint32_t wc[AGC_TPB / 64][64];
+    __shared__ uint32_t ws[AGC_TPB / 64];
+    __shared__ uint32_t seg_p[SHB_CT_MAX + 1], seg_g[SHB_CT_MAX];
+    __shared__ uint8_t seg_of[AGC_CH / 32];
+    const int b = blockIdx.x;
+    const int kb = P.kb;
+    const uint32_t kmask = (1u << kb) - 1u;
+    for (int k = threadIdx.x; k < 256; k += AGC_TPB) {
+        st_cnt[k] = 0;
+        for (int o = 0; o < SHB_MAX_AGG; o++) st_acc[o][k] = 0;  // 0 == long 0 == double +0.0
+    }
+    const void* e1src = A.e1_col >= 0 ? P.ms[A.e1_col] : nullptr;
+    const void* e2src = A.e2_col[0] >= 0 ? P.st_dst[A.e2_col[0]] : nullptr;
+    const void* e2srn = A.e2_col[1] >= 0 ? P.st_dst[A.e2_col[1]] : nullptr;
+    for (int a = 0; a < P.nt;) {
+        __syncthreads();
+        const int nseg = P.nt - a < SHB_CT_MAX ? P.nt - a : SHB_CT_MAX;
+        uint32_t len = 0u, g = 0u;
+        if ((int)threadIdx.x < nseg) {
+            const int T = a + (int)threadIdx.x;
+            const uint16_t* r = P.toff + (int64_t)T * SHB_TOFF + b;
+            const uint32_t lo = r[0], hi = r[1];
+            len = hi - lo;
+            g = ((uint32_t)T << SHB_TILE_SHIFT) + lo;
+        }
+        {
+            uint32_t tot;
+            const uint32_t pre = shw_block_excl<AGC_TPB>(len, ws, &tot);
+            if ((int)threadIdx.x < nseg) {
+                seg_p[threadIdx.x] = pre;
+                seg_g[threadIdx.x] = g;
+            }
+            if ((int)threadIdx.x == nseg) seg_p[nseg] = tot;
+        }
+        __syncthreads();
+        const int ne = __syncthreads_count((int)threadIdx.x < nseg && seg_p[threadIdx.x + 1] <= AGC_CH);
+        if (ne == 0) {
+            if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_AGG);
+            return;  // (uniform) the host runs the post-pass instead
+        }
+        const int L = (int)seg_p[ne];
+        for (int j = (int)threadIdx.x; j * 32 < L; j += AGC_TPB) {
+            const uint32_t e = (uint32_t)j * 32u;
+            int lo = 0, hi = ne - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (seg_p[mid] <= e) lo = mid;
+                else hi = mid - 1;
+            }
+            seg_of[j] = (uint8_t)lo;
+        }
+        __syncthreads();
+        // the chunk's consumers (arrival order inside the bucket): key, count, e2 argument
+        uint32_t cc[AGC_NR];
+        int sgi[AGC_NR];
+#pragma unroll
+        for (int k = 0; k < AGC_NR; k++) {
+            const int i = (int)threadIdx.x * AGC_NR + k;  // 4 consecutive events per thread
+            cc[k] = 0u;
+            sgi[k] = 0;
+            if (i < L) {
+                int sg = seg_of[i >> 5];
+                while (seg_p[sg + 1] <= (uint32_t)i) sg++;
+                sgi[k] = sg;
+                const uint32_t gi = seg_g[sg] + ((uint32_t)i - seg_p[sg]);
+                cc[k] = P.cnt[gi];
+                c_key[i] = (P.w0[gi] & kmask) | (cc[k] << 16);
+                if (e2src) c_e2w[i] = agc_load(e2src, gi, A.e2_type[0]);
+                if (e2srn) c_e2n[i] = ((const uint32_t*)e2srn)[gi];
+            }
+        }
+        // rows: exclusive prefix over the chunk
+        uint32_t total;
+        {
+            uint32_t sum = 0;
+#pragma unroll
+            for (int k = 0; k < AGC_NR; k++) sum += cc[k];
+            uint32_t off = shw_block_excl<AGC_TPB>(sum, ws, &total);
+#pragma unroll
+            for (int k = 0; k < AGC_NR; k++) {
+                const int i = (int)threadIdx.x * AGC_NR + k;
+                if (i < L) c_pre[i] = (uint16_t)off;
+                off += cc[k];
+            }
+        }
+        if (total > AGC_ROWS) {
+            if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_AGG);
+            return;  // (uniform: total is the block sum)
+        }
+        __syncthreads();
+        // match-stream positions (the segment's first match + the prefix inside it)
+        // and the e1-side arguments of the rows
+#pragma unroll
+        for (int k = 0; k < AGC_NR; k++) {
+            const int i = (int)threadIdx.x * AGC_NR + k;
+            if (i >= L) continue;
+            const int sg = sgi[k];
+            const uint32_t mp = P.mstart[(int64_t)(a + sg) * SHB_NB + b] + c_pre[i] - c_pre[seg_p[sg]];
+            c_mp[i] = mp;
+            if (e1src)
+                for (uint32_t q = 0; q < cc[k]; q++) r_e1[c_pre[i] + q] = (uint32_t)((const uint32_t*)e1src)[mp + q];
+        }
+        __syncthreads();
+        // stable sort by local key (kb <= 8: 6 bits, then the high bits)
+        const uint16_t* srt = o_a;
+        s3b_sort_pass(c_key, nullptr, o_a, L, 0, wc, ws);  // (digits of the low 12 bits: the key)
+        if (kb > 6) {
+            s3b_sort_pass(c_key, o_a, o_b, L, 6, wc, ws);
+            srt = o_b;
+        }
+        // the first consumer of each key run adds the run's rows in sequence
+        for (int q = threadIdx.x; q < L; q += AGC_TPB) {
+            const uint32_t ci = srt[q];
+            const uint32_t key = c_key[ci] & 0xFFFFu;
+            if (q > 0 && (c_key[srt[q - 1]] & 0xFFFFu) == key) continue;
+            int64_t acc[SHB_MAX_AGG];
+#pragma unroll
+            for (int o = 0; o < SHB_MAX_AGG; o++) acc[o] = st_acc[o][key];
+            int64_t n = st_cnt[key];
+            for (int r = q; r < L; r++) {
+                const uint32_t cr = r == q ? ci : srt[r];
+                const uint32_t kw = c_key[cr];
+                if (r > q && (kw & 0xFFFFu) != key) break;
+                const uint32_t c = kw >> 16;
+                const uint32_t r0 = c_pre[cr], mp = c_mp[cr];
+                const int64_t x2 = e2src ? c_e2w[cr] : 0;
+                const int64_t x3 = e2srn ? (int64_t)c_e2n[cr] : 0;
+                for (uint32_t m = 0; m < c; m++) {
+                    n++;
+                    const int64_t x1 = e1src ? (int64_t)r_e1[r0 + m] : 0;
+#pragma unroll
+                    for (int o = 0; o < SHB_MAX_AGG; o++) {
+                        if (o >= A.n) break;
+                        const int kind = A.kind[o];
+                        int64_t v;
+                        if (kind == SH_AGG_COUNT) {
+                            v = n;
+                        } else {
+                            const int sd = A.side[o];
+                            agc_add(kind, sd == 0 ? A.e1_type : A.e2_type[sd - 1], acc[o],
+                                    sd == 0 ? x1 : (sd == 1 ? x2 : x3));
+                            v = kind == SH_AGG_AVG
+                                    ? __double_as_longlong(__longlong_as_double(acc[o]) / (double)n)
+                                    : acc[o];
+                        }
+                        ((int64_t*)A.out[o])[(int64_t)mp + m] = v;
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 0; o < SHB_MAX_AGG; o++) st_acc[o][key] = acc[o];
+            st_cnt[key] = n;
+        }
         a += ne;
     }
 }
@@ -818,6 +1041,13 @@ extern "C" int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream) {
 extern "C" int shb_s3_carry(const shb_plan* P, const shb_s3* S, void* stream) {
     if (P->kb > 12 || P->n_staged < 1 || P->st_width[0] != 4) return -1;
     hipLaunchKernelGGL(k_s3b, dim3(SHB_NB), dim3(S3B_TPB), 0, (hipStream_t)stream, *P, *S);
+    return bk_ok();
+}
+
+extern "C" int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream) {
+    static_assert(AGC_TPB == S3B_TPB && AGC_CH == S3B_CH, "the sort pass shape");
+    if (P->kb > 8 || A->n < 1 || A->n > SHB_MAX_AGG) return -1;
+    hipLaunchKernelGGL(k_bk_aggc, dim3(SHB_NB), dim3(AGC_TPB), 0, (hipStream_t)stream, *P, *A);
     return bk_ok();
 }
 

@@ -156,6 +156,21 @@ struct shb_s3 {
     int32_t ms_slot[2];
 };
 
+// select-clause aggregators carried per key by the bucketed engine (k_bk_aggc):
+// output o's running value (8-byte raw: long sum / count, double sum / avg) by
+// match-stream position, from addends on the e1 side (match-stream column e1_col)
+// or the e2 side (staged column e2_col, at the consumer's slot) or none (count())
+#define SHB_MAX_AGG 4
+#define SHB_F_AGG 64      // a carry chunk's rows overflow its LDS: the post-pass runs
+struct shb_aggc {
+    int32_t n;
+    int32_t e1_col, e1_type;      // match-stream column of the e1-side argument (-1: none; 4-byte)
+    int32_t e2_col[2], e2_type[2];  // staged columns of e2-side arguments (-1: none; [1]: 4-byte)
+    int32_t kind[SHB_MAX_AGG];    // SH_AGG_SUM / AVG / COUNT
+    int32_t side[SHB_MAX_AGG];    // 0: e1, 1: e2 column 0, 2: e2 column 1, 3: none
+    void* out[SHB_MAX_AGG];       // [match-stream positions] int64 / double bits
+};
+
 // typed output columns (sh_device_run.d_out_cols) instead of raw 8-byte rows
 struct shb_cols {
     void* cols[SHB_MAX_OUT];      // natural width per select value
@@ -209,6 +224,9 @@ int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream);
 // the rise-and-fall sequence: one workgroup per key bucket carries its keys' state
 // across the tiles (after shb_partition with no_ts; before shb_finish)
 int shb_s3_carry(const shb_plan* P, const shb_s3* S, void* stream);
+// running aggregates per key: one workgroup per key bucket in arrival order (after
+// the matcher, before shb_finish / shb_emit)
+int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream);
 int shb_emit(const shb_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base, uint64_t* out_seq,
              int64_t* out_vals, int64_t out_cap, void* stream);
 // raw 8-byte rows [m x n_out] -> typed columns of widths w[o] (8, 4 or 1 bytes)

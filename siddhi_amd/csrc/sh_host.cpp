@@ -389,6 +389,14 @@ struct sh_handle {
     std::vector<int64_t> o_vals;
     std::vector<uint8_t> o_nulls;
     std::vector<uint64_t> o_order;  // key-sharded: per row, launch << 32 | position in the launch
+    // deferred rows of streaming launches (single process, no List outputs): each
+    // launch's placed rows are appended on the device after the *df_ctr rows already
+    // there; they join the host queue above at the next flush (drain / pending /
+    // snapshot), so a send() costs no placement round trip. df_ub: an upper bound of
+    // the rows held (the launches' record counts), df_stream: the stream they are on.
+    DevBuf df_q, df_seq, df_ts, df_vals, df_nulls, df_ctr;
+    int64_t df_cap = 0, df_ub = 0;
+    hipStream_t df_stream = nullptr;
     int64_t o_read = 0;
     // ---- key-sharded streaming (sh_set_coordinator): the other ranks
     bool coord_on = false;
@@ -487,7 +495,8 @@ struct sh_handle {
     shj_bucket bk{};
     std::string bk_err;
     DevBuf bk_w0, bk_sp, bk_toff, bk_cnt, bk_mstart, bk_tpre, bk_tfirst, bk_hstart, bk_ttot, bk_flag, bk_prof;
-    DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS];
+    DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS], bk_agg[SHB_MAX_AGG];
+    bool bk_agg_carried = false;  // the last bucketed run carried its aggregates (k_bk_aggc)
     PinBuf bk_rd;
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
     DevBuf w_colrows;
@@ -495,7 +504,8 @@ struct sh_handle {
     // aggregators behind the fast engines (sh_agg.hip): scratch, trigger sequence
     // numbers when the caller wants none, and the last run's path
     DevBuf a_scratch, a_seq;
-    int agg_last = 0;  // 1: post-pass done, 2: post-pass not exact -> sequential engine, 3: in the k_seq3s lanes
+    int agg_last = 0;  // 1: post-pass done, 2: post-pass not exact -> sequential engine, 3: in the k_seq3s lanes,
+                       // 4: carried per key by the bucketed engine (k_bk_aggc)
     std::vector<int32_t> out_types;  // per select position over the queries (-2: types differ)
     uint64_t fp = 0;                 // compiled-program fingerprint (snapshot images)
 };
@@ -1729,6 +1739,83 @@ static void nf_put_cols(sh_handle* h, const nf_cols& cols) {
     h->cols_cached = true;
 }
 
+// the deferred rows into the host queue (one sync + one copy per array)
+static int nf_app_pull(sh_handle* h) {
+    if (h->df_ub == 0) return SH_OK;
+    hipStream_t st = h->df_stream;
+    unsigned long long n = 0;
+    if (hipMemcpyAsync(&n, h->df_ctr.p, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return fail(h, SH_E_HIP, "deferred rows");
+    if ((int64_t)n > h->df_ub) return fail(h, SH_E_HIP, "deferred row count");
+    const int no = std::max(1, h->n_out);
+    const size_t base = h->o_seq.size();
+    h->o_query.resize(base + n);
+    h->o_seq.resize(base + n);
+    h->o_ts.resize(base + n);
+    h->o_vals.resize((base + n) * h->n_out);
+    h->o_nulls.resize((base + n) * h->n_out);
+    if (n) {
+        const size_t b_q = 0, b_seq = ((size_t)n * 4 + 7) / 8 * 8, b_ts = b_seq + (size_t)n * 8,
+                     b_v = b_ts + (size_t)n * 8, b_n = b_v + (size_t)n * no * 8, b_end = b_n + (size_t)n * no;
+        if (h->pin_out.ensure(b_end)) return fail(h, SH_E_OOM, "pinned staging");
+        uint8_t* pb = h->pin_out.as<uint8_t>();
+        hipMemcpyAsync(pb + b_q, h->df_q.p, (size_t)n * 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(pb + b_seq, h->df_seq.p, (size_t)n * 8, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(pb + b_ts, h->df_ts.p, (size_t)n * 8, hipMemcpyDeviceToHost, st);
+        if (h->n_out) {
+            hipMemcpyAsync(pb + b_v, h->df_vals.p, (size_t)n * no * 8, hipMemcpyDeviceToHost, st);
+            hipMemcpyAsync(pb + b_n, h->df_nulls.p, (size_t)n * no, hipMemcpyDeviceToHost, st);
+        }
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "deferred rows copy");
+        memcpy(h->o_query.data() + base, pb + b_q, n * 4);
+        memcpy(h->o_seq.data() + base, pb + b_seq, n * 8);
+        memcpy(h->o_ts.data() + base, pb + b_ts, n * 8);
+        if (h->n_out) {
+            memcpy(h->o_vals.data() + base * h->n_out, pb + b_v, n * no * 8);
+            memcpy(h->o_nulls.data() + base * h->n_out, pb + b_n, n * no);
+        }
+    }
+    hipMemsetAsync(h->df_ctr.p, 0, 8, st);
+    h->df_ub = 0;
+    return SH_OK;
+}
+
+// a streaming launch's rows appended to the deferred device rows (no sync): the
+// scan, the placement and the count stay on the stream; nrec bounds the rows
+static int nf_place_deferred(sh_handle* h, int64_t n_idx, int64_t nrec) {
+    hipStream_t st = h->stream;
+    if (h->df_ub && st != h->df_stream) {
+        int rc = nf_app_pull(h);
+        if (rc) return rc;
+    }
+    const int no = std::max(1, h->n_out);
+    if (h->df_ub + nrec > h->df_cap) {
+        int rc = nf_app_pull(h);
+        if (rc) return rc;
+        if (nrec > h->df_cap) {
+            const int64_t cap = std::max<int64_t>(nrec, (int64_t)1 << 20);
+            if (h->df_q.ensure_fresh(cap * 4) || h->df_seq.ensure_fresh(cap * 8) || h->df_ts.ensure_fresh(cap * 8) ||
+                h->df_vals.ensure_fresh(cap * no * 8) || h->df_nulls.ensure_fresh(cap * no) ||
+                h->df_ctr.ensure_fresh(8))
+                return fail(h, SH_E_OOM, "deferred rows");
+            h->df_cap = cap;
+        }
+    }
+    if (h->df_ub == 0) hipMemsetAsync(h->df_ctr.p, 0, 8, st);
+    if (shd_exclusive_scan(h->w_cnt.as<uint32_t>(), h->w_off.as<uint32_t>(), n_idx, h->w_scan.as<uint32_t>(), st))
+        return fail(h, SH_E_HIP, "scan");
+    if (h->w_inv.ensure_fresh(nrec * 4)) return fail(h, SH_E_OOM, "placement index");
+    if (nfd_place_app(h->n_recs.as<uint64_t>(), nrec, NF_REC_HDR + no, h->w_off.as<uint32_t>(),
+                      h->w_cnt.as<uint32_t>(), n_idx, no, h->df_ctr.as<unsigned long long>(), h->df_q.as<int32_t>(),
+                      h->df_seq.as<uint64_t>(), h->df_ts.as<int64_t>(), h->df_vals.as<int64_t>(), h->df_nulls.as<uint8_t>(),
+                      h->w_inv.as<uint32_t>(), st))
+        return fail(h, SH_E_HIP, "placement");
+    h->df_ub += nrec;
+    h->df_stream = st;
+    return SH_OK;
+}
+
 // scan the per-index counts, place the records, append them to the host queue
 // (or to the caller's device buffers); returns the number of rows
 // (launch: the launch's tick, for the key-sharded rows' order tags)
@@ -1737,6 +1824,14 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
                     uint64_t launch, int64_t nrec_known) {
     HpScope hp_(h, 4);
     hipStream_t st = h->stream;
+    if (!d_seq && !h->coord_on && !h->has_lists && nrec_known >= 0 && !getenv("SH_NO_DEFER_ROWS")) {
+        *rows_out = -1;  // not known on the host (the rows are counted on the device)
+        return nrec_known ? nf_place_deferred(h, n_idx, nrec_known) : SH_OK;
+    }
+    if (!d_seq) {
+        int rc = nf_app_pull(h);  // host rows go after the deferred ones
+        if (rc) return rc;
+    }
     if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
     if (nrec_known < 0) hipMemcpyAsync(h->pin_rd.as<void>(PR_NREC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
     if (shd_exclusive_scan(h->w_cnt.as<uint32_t>(), h->w_off.as<uint32_t>(), n_idx, h->w_scan.as<uint32_t>(), st))
@@ -1992,12 +2087,17 @@ static int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_
             int src = nf_sev_apply(h, true);
             if (src) return src;
             int rc = nf_place(h, n_idx, n_rows, d_seq, d_vals, cap, h->tick - 1, nrec);
-            hipEventRecord(h->ev[3], st);
-            hipStreamSynchronize(st);
             hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
             hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
-            hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
-            hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
+            if (*n_rows >= 0) {
+                hipEventRecord(h->ev[3], st);
+                hipStreamSynchronize(st);
+                hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
+                hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
+            } else {  // deferred rows: the placement is still on the stream
+                h->times.emit_ms = 0.0f;
+                hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[2]);
+            }
             h->times.advance_launches = attempt + 1;
             return rc;
         }
@@ -2391,7 +2491,7 @@ static shd_cols store_cols(sh_handle* h) {
 
 // process every staged event
 static int flush(sh_handle* h) {
-    if (h->mode == 1) return SH_OK;  // the general engine processes each send() at once
+    if (h->mode == 1) return nf_app_pull(h);  // the general engine processes each send() at once
     const int64_t n = (int64_t)h->st_ts.size();
     if (n == 0) return SH_OK;
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device");
@@ -2898,11 +2998,97 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
         B.ms[m] = h->bk_ms[m].p;
         B.ms_width[m] = w;
     }
-    for (int o = 0; o < O.n_out; o++)
-        if (O.kind[o] == 0) O.src[o] = B.ms[(int)(intptr_t)O.src[o]];
+    int ms_of[SHB_MAX_OUT];
+    for (int o = 0; o < O.n_out; o++) {
+        ms_of[o] = O.kind[o] == 0 ? (int)(intptr_t)O.src[o] : -1;
+        if (O.kind[o] == 0) O.src[o] = B.ms[ms_of[o]];
+    }
+    // aggregators carried per key in arrival order (k_bk_aggc: the reference's own
+    // additions, no exactness proof): e1-side arguments from one 4-byte match-stream
+    // column, e2-side ones from up to two staged columns (one of them 4-byte), count()
+    // without one; anything else takes the post-pass (sh_agg.hip)
+    shb_aggc AG;
+    memset(&AG, 0, sizeof(AG));
+    AG.e1_col = AG.e2_col[0] = AG.e2_col[1] = -1;
+    bool carry = P.agg_post && !getenv("SH_BK_AGG_POST");
+    int agg_of[SHB_MAX_OUT];
+    for (int o = 0; o < P.n_out; o++) agg_of[o] = -1;
+    for (int o = 0; o < P.n_out && carry; o++) {
+        const int ak = P.out_agg[o];
+        if (ak == SH_AGG_NONE) continue;
+        if (AG.n == SHB_MAX_AGG || (ak != SH_AGG_SUM && ak != SH_AGG_AVG && ak != SH_AGG_COUNT)) {
+            carry = false;
+            break;
+        }
+        const int i = AG.n++;
+        AG.kind[i] = ak;
+        agg_of[o] = i;
+        if (ak == SH_AGG_COUNT) {
+            AG.side[i] = 3;
+            continue;
+        }
+        const int a = P.out_attr[o], t = P.attr_type[0][a];
+        if (t != SH_T_INT && t != SH_T_FLOAT && t != SH_T_LONG && t != SH_T_DOUBLE) {
+            carry = false;
+            break;
+        }
+        const int w = type_width(t);
+        if (P.out_slot[o] == 0 && ms_of[o] >= 0 && w == 4 && (AG.e1_col < 0 || AG.e1_col == ms_of[o])) {
+            AG.e1_col = ms_of[o];
+            AG.e1_type = t;
+            AG.side[i] = 0;
+        } else if (P.out_slot[o] == 1) {
+            // the consumer's column at its slot: staged by the partition (the matcher's
+            // own staged columns first, then the carry's)
+            int k = 0;
+            while (k < B.n_staged && (B.st_src[k] != run->d_cols[a])) k++;
+            if (k == B.n_staged) {
+                if (B.n_staged == SHB_MAX_STAGED || h->bk_st[k].ensure_fresh(slots * w))
+                    return B.n_staged == SHB_MAX_STAGED ? 1 : fail(h, SH_E_OOM, "bucket workspace");
+                B.st_src[k] = run->d_cols[a];
+                B.st_dst[k] = h->bk_st[k].p;
+                B.st_width[k] = w;
+                B.n_staged++;
+            }
+            int c = (AG.e2_col[0] == k) ? 0 : (AG.e2_col[1] == k ? 1 : -1);
+            if (c < 0) {
+                if (AG.e2_col[0] < 0) c = 0;
+                else if (AG.e2_col[1] < 0 && w == 4) c = 1;
+                else if (AG.e2_col[1] < 0 && type_width(AG.e2_type[0]) == 4) {
+                    // keep the 8-byte column in slot 0
+                    AG.e2_col[1] = AG.e2_col[0];
+                    AG.e2_type[1] = AG.e2_type[0];
+                    for (int j = 0; j < i; j++)
+                        if (AG.side[j] == 1) AG.side[j] = 2;
+                    c = 0;
+                } else {
+                    carry = false;
+                    break;
+                }
+                AG.e2_col[c] = k;
+                AG.e2_type[c] = t;
+            }
+            AG.side[i] = 1 + c;
+        } else {
+            carry = false;
+        }
+    }
+    if (carry) {
+        for (int i = 0; i < AG.n; i++) {
+            if (h->bk_agg[i].ensure_fresh(ms_vals * 8)) return fail(h, SH_E_OOM, "aggregate columns");
+            AG.out[i] = h->bk_agg[i].p;
+        }
+        for (int o = 0; o < O.n_out; o++)
+            if (agg_of[o] >= 0) {
+                O.kind[o] = 0;
+                O.src[o] = AG.out[agg_of[o]];
+                O.type[o] = P.out_type[o];
+            }
+    }
+    h->bk_agg_carried = false;
     shb_cols OC;
     memset(&OC, 0, sizeof(OC));
-    if (run->d_out_cols && !P.agg_post) {
+    if (run->d_out_cols && !h->cols_rows && (!P.agg_post || carry)) {
         OC.use = 1;
         for (int o = 0; o < O.n_out; o++) {
             OC.cols[o] = run->d_out_cols[o];
@@ -2942,6 +3128,7 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     if (hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.n_chunks), 1, 1, 512, 1, 1, 0, st,
                               args, nullptr) != hipSuccess)
         return fail(h, SH_E_HIP, "shb_match launch failed");
+    if (carry && shb_agg_carry(&B, &AG, st)) return fail(h, SH_E_HIP, "aggregate carry launch failed");
     if (shb_finish(&B, h->w_scan.as<uint32_t>(), st)) return fail(h, SH_E_HIP, "bucket scan launch failed");
     hipEventRecord(h->ev[2], st);
     if (shb_emit(&B, &O, &OC, 0, run->d_out_seq, run->d_out_values, run->out_capacity, st))
@@ -2969,6 +3156,8 @@ static int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
     h->times.advance_launches = 1;
     h->bk_last = 1;
+    h->bk_agg_carried = carry;
+    if (carry) h->agg_last = 4;
     return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "bucket engine");
 }
 
@@ -3065,6 +3254,12 @@ static int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     B.ttot = h->bk_ttot.as<uint32_t>();
     B.flag = h->bk_flag.as<int32_t>();
     B.ms_ctr = h->bk_flag.as<uint32_t>() + 4;
+    static const bool prof = getenv("SH_BK_PROFILE") != nullptr;
+    if (prof) {
+        if (h->bk_prof.ensure_fresh(128)) return fail(h, SH_E_OOM, "profile");
+        hipMemsetAsync(h->bk_prof.p, 0, 128, st);
+        B.prof = h->bk_prof.as<unsigned long long>();
+    }
     hipEventRecord(h->ev[0], st);
     hipMemsetAsync(B.flag, 0, 32, st);
     hipMemsetAsync(B.ttot, 0, ((int64_t)B.nt + 1) * 4, st);
@@ -3081,6 +3276,12 @@ static int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the sequence engine");
     const int32_t flag = *h->bk_rd.as<int32_t>(0);
     const int64_t total = *h->bk_rd.as<uint32_t>(8);
+    if (B.prof) {
+        unsigned long long pr[16];
+        hipMemcpy(pr, B.prof, 128, hipMemcpyDeviceToHost);
+        fprintf(stderr, "[k_s3b clock ticks, sum over workgroups] tables+load %llu sort %llu carry %llu out %llu\n",
+                pr[0], pr[1], pr[2], pr[3]);
+    }
     if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
     if (flag) return 1;
     run->out_count = total;
@@ -3275,7 +3476,7 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
     };
     if (h->prog.window_ok) {
         const int brc = run_bucket(h, run, nkeys);
-        if (brc == SH_OK && aggp) {
+        if (brc == SH_OK && aggp && !h->bk_agg_carried) {
             const int arc = finish_agg(nkeys);
             if (arc <= 0) return arc;
         } else if (brc != 1) {

@@ -942,6 +942,55 @@ extern "C" int nfd_place(const uint64_t* recs, int64_t nrec, int stride, const u
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// the same placement appended to device-resident output arrays: the launch's rows
+// (their count off[n-1] + cnt[n-1] read on the device) go after the *base rows
+// already there, then *base grows by them -- no host round trip per launch
+__global__ void __launch_bounds__(256) k_nfa_gather_app(const uint64_t* __restrict__ recs,
+                                                        const uint32_t* __restrict__ inv, int64_t nrec, int stride,
+                                                        int n_out, const uint32_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ cnt, int64_t n_idx,
+                                                        const unsigned long long* __restrict__ base,
+                                                        int32_t* __restrict__ out_query, uint64_t* __restrict__ out_seq,
+                                                        int64_t* __restrict__ out_ts, int64_t* __restrict__ out_vals,
+                                                        uint8_t* __restrict__ out_nulls) {
+    const int64_t dst = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)off[n_idx - 1] + cnt[n_idx - 1];
+    if (dst >= total) return;
+    const uint32_t ix = inv[dst];
+    if ((int64_t)ix >= nrec) return;
+    const int64_t o = (int64_t)*base + dst;
+    const uint64_t* r = recs + (int64_t)ix * stride;
+    const uint64_t h2 = r[2];
+    out_query[o] = (int)(h2 >> 32);
+    out_seq[o] = r[3];
+    out_ts[o] = (int64_t)r[1];
+    for (int c = 0; c < n_out; c++) {
+        const bool has = c < stride - NF_REC_HDR;
+        out_vals[o * n_out + c] = has ? (int64_t)r[NF_REC_HDR + c] : 0;
+        out_nulls[o * n_out + c] = has ? (uint8_t)((h2 >> c) & 1) : 1;
+    }
+}
+
+__global__ void k_nfa_app_bump(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt, int64_t n_idx,
+                               unsigned long long* __restrict__ base) {
+    *base += (unsigned long long)off[n_idx - 1] + cnt[n_idx - 1];
+}
+
+extern "C" int nfd_place_app(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets,
+                             const uint32_t* counts, int64_t n_idx, int n_out, unsigned long long* base,
+                             int32_t* out_query, uint64_t* out_seq, int64_t* out_ts, int64_t* out_vals,
+                             uint8_t* out_nulls, uint32_t* inv, void* stream) {
+    if (nrec <= 0 || n_idx <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    hipMemsetAsync(inv, 0xFF, (size_t)nrec * 4, st);
+    hipLaunchKernelGGL(k_nfa_inv, dim3(nf_blocks(nrec, 256)), dim3(256), 0, st, recs, nrec, stride, offsets, inv);
+    hipLaunchKernelGGL(k_nfa_gather_app, dim3(nf_blocks(nrec, 256)), dim3(256), 0, st, recs, (const uint32_t*)inv, nrec,
+                       stride, n_out, offsets, counts, n_idx, (const unsigned long long*)base, out_query, out_seq,
+                       out_ts, out_vals, out_nulls);
+    hipLaunchKernelGGL(k_nfa_app_bump, dim3(1), dim3(1), 0, st, offsets, counts, n_idx, base);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 extern "C" int nfd_save(uint64_t* kstate, int64_t key_words, const uint32_t* seg_list, const uint32_t* nseg,
                         const uint32_t* skeys, int64_t max_segments, uint64_t* save, int dir, void* stream) {
     if (max_segments < 1) return 0;

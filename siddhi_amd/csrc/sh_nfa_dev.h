@@ -88,6 +88,10 @@ int nfd_timer(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, int q, in
 int nfd_place(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets, int n_out, int32_t* out_query,
               uint64_t* out_seq, int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, uint32_t* inv, int64_t total,
               void* stream);
+// nfd_place appended to device-resident output arrays after *base rows (count on the device)
+int nfd_place_app(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets, const uint32_t* counts,
+                  int64_t n_idx, int n_out, unsigned long long* base, int32_t* out_query, uint64_t* out_seq,
+                  int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, uint32_t* inv, void* stream);
 int nfd_save(uint64_t* kstate, int64_t key_words, const uint32_t* seg_list, const uint32_t* nseg, const uint32_t* skeys,
              int64_t max_segments, uint64_t* save, int dir, void* stream);
 int nfd_save_keys(uint64_t* kstate, int64_t key_words, const int32_t* keys, int32_t nkeys, uint64_t* save, int dir,

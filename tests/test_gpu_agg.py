@@ -1,11 +1,14 @@
-"""Select-clause aggregators on the fast engines (sh_agg.hip post-pass): the
-bucketed / window engines (C2 / C1 shapes), the rise-and-fall sequence engine
-(C3) and the rule set (C5) write the aggregators' arguments and the post-pass
-forms the running sum / avg / count per (query, partition key) in match order,
-after proving the double additions exact. Bit-exact against the oracle
-(QuerySelector + Sum/Avg aggregators restated), and at full size against the
-vectorised restatement (tests/agg_check.py). A stream whose additions round
-takes the sequential engines (agg_status 2) and still matches the oracle."""
+"""Select-clause aggregators on the fast engines. The bucketed engine (C2 shape)
+carries every key's running sum / avg / count across its buckets in arrival
+order (k_bk_aggc, agg_status 4: the reference's own sequence of additions); the
+window engine (C1), the rise-and-fall key-segment engine (C3) and the rule set
+(C5) write the aggregators' arguments and the sh_agg.hip post-pass forms the
+running values per (query, partition key) in match order after proving the
+double additions exact (agg_status 1; SH_BK_AGG_POST=1 sends the bucketed engine
+there too). Bit-exact against the oracle (QuerySelector + Sum/Avg aggregators
+restated), and at full size against the vectorised restatement
+(tests/agg_check.py). A stream whose additions round takes the sequential
+engines from the post-pass (agg_status 2) and still matches the oracle."""
 import numpy as np
 import pytest
 
@@ -61,13 +64,16 @@ def _oracle(text, ts, cols, keys):
     return out
 
 
+@pytest.mark.parametrize("post", [False, True])
 @pytest.mark.parametrize("n,K", [(400_000, 2_000), (300_000, 20_000)])
-def test_c2_aggregates_bucketed_vs_oracle(n, K):
+def test_c2_aggregates_bucketed_vs_oracle(n, K, post, monkeypatch):
     from siddhi_amd import synth
+    if post:
+        monkeypatch.setenv("SH_BK_AGG_POST", "1")
     ts, k, p, v = synth.stock_stream(n, K, 100)
     (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], K)
     ref = _oracle(C2_AGG, ts, [k, p, v], k)
-    assert st["bucket"] == 1 and st["agg"] == 1, st
+    assert st["bucket"] == 1 and st["agg"] == (1 if post else 4), st
     assert m == len(ref["seq"]) > 0
     assert np.array_equal(seq, ref["seq"].astype(np.int64))
     assert np.array_equal(vals, ref["values"])
@@ -114,17 +120,21 @@ def test_c5_aggregates_rule_set_vs_oracle():
     assert np.array_equal(vals, ref["values"])
 
 
-def test_rounding_additions_take_the_sequential_engine():
-    """prices spanning 2^-60 .. 2^60: the double additions round, so the post-pass
-    refuses and the sequential engine's sums (== the oracle's) are returned"""
+@pytest.mark.parametrize("post", [False, True])
+def test_rounding_additions_stay_exact(post, monkeypatch):
+    """prices spanning 2^-60 .. 2^60: the double additions round. The carry adds in
+    the reference's sequence anyway (agg_status 4); the post-pass refuses and the
+    sequential engine's sums are returned (agg_status 2); both == the oracle's"""
     from siddhi_amd import synth
+    if post:
+        monkeypatch.setenv("SH_BK_AGG_POST", "1")
     ts, k, p, v = synth.stock_stream(200_000, 2_000, 100)
     p = p.copy()
     p[::7] *= np.float32(2.0 ** 60)
     p[3::11] *= np.float32(2.0 ** -60)
     (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], 2_000)
     ref = _oracle(C2_AGG, ts, [k, p, v], k)
-    assert st["agg"] == 2, st
+    assert st["agg"] == (2 if post else 4), st
     assert m == len(ref["seq"]) > 0
     assert np.array_equal(seq, ref["seq"].astype(np.int64))
     assert np.array_equal(vals, ref["values"])
@@ -138,7 +148,7 @@ def test_c2_aggregates_full_size_vs_restatement():
     from siddhi_amd import synth
     ts, k, p, v = synth.stock_stream(100_000_000, 10_000, 100)
     (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], 10_000)
-    assert st["bucket"] == 1 and st["agg"] == 1, st
+    assert st["bucket"] == 1 and st["agg"] == 4, st
     eseq, ev = c2_expected(ts, k, p, v)
     assert np.array_equal(seq, eseq)
     grp = k[eseq].astype(np.int64)
