@@ -181,7 +181,7 @@ struct nf_cols {
     // (NULL: every key is scanned)
     uint8_t* sched_armed;
     // keys whose flag went 0 -> 1 since the last due pass (the device due list
-    // takes them in, sh_host.cpp nf_timers); NULL: off
+    // takes them in, sh_host_nfa.cpp nf_timers); NULL: off
     int32_t* arm_log;
     unsigned long long* arm_ctr;
     uint64_t arm_cap;

@@ -1,5 +1,5 @@
 // sh_nfa_dev.h — host <-> kernel interface of the general engine (sh_nfa.hip),
-// called from sh_host.cpp.
+// called from sh_host_nfa.cpp.
 #pragma once
 #include <stdint.h>
 

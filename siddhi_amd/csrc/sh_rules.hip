@@ -22,7 +22,7 @@
 // plus the rules without such a conjunct. Every conjunct is still evaluated, so
 // the index only prunes.
 //
-// Pipeline (sh_host.cpp run_rules): segment (sh_kernels.hip) -> k_rules_scan<0>
+// Pipeline (sh_host_fast.cpp run_rules): segment (sh_kernels.hip) -> k_rules_scan<0>
 // (matches per opening event) -> exclusive scan -> k_rules_scan<1> (records in
 // (opening event, rule) order) -> run ids -> k_rules_keys -> stable LSD radix
 // sort of the records by (run, query, consuming event) -> k_rules_place.
