@@ -1620,6 +1620,8 @@ int shx_seq3_status(sh_handle* h) { return h ? (h->s3b_last ? 2 : h->seq3_last) 
 // aggregators of the last sh_run_device: 0 none on a fast engine, 1 the post-pass
 // (sh_agg.hip) formed them, 2 it was not exact and a sequential engine ran
 int shx_agg_status(sh_handle* h) { return h ? h->agg_last : 0; }
+
+int shx_rules_status(sh_handle* h) { return h ? h->rs_last : 0; }
 // 1: the compiled app has the rise-and-fall sequence shape (no device needed)
 int shx_seq3_shape(sh_handle* h) { return h && h->T && h->T->n_queries == 1 && h->T->q[0].s3 ? 1 : 0; }
 

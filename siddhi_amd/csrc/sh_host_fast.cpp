@@ -73,6 +73,210 @@ int tile_shift_for(int64_t n, int32_t nkeys) {
 
 // batch-compiled rule sets (sh_rules.hip) over HBM-resident columns
 
+// the records' output order -- (run, query, consuming event), stable over the
+// records' (opening event, rule) order; by_p: the records are in any order, so
+// the first sort stage restores that order -- and the placed rows
+static int rules_order_place(sh_handle* h, sh_device_run* run, int64_t m, const uint32_t* rec_p, const uint32_t* rec_q,
+                             const uint32_t* rec_r, const uint32_t* perm, const int64_t* sts, const shd_cols* dC,
+                             const uint32_t* sts32, int64_t tlo, bool sorted, bool by_p) {
+    hipStream_t st = h->stream;
+    const int64_t n = run->n;
+    const shr_table* dT = h->rd_tab.as<shr_table>();
+    const int64_t mt = (m + 4095) / 4096;
+    const size_t sw = std::max(shd_scan_tmp_words(256 * mt), (size_t)16);
+    if (h->r_keys.ensure_fresh((size_t)m * 12) || h->r_g.ensure_fresh((size_t)m * 8) ||
+        h->r_sk.ensure_fresh((size_t)m * 8) || h->r_sv.ensure_fresh((size_t)m * 8) ||
+        h->r_hist.ensure_fresh((size_t)256 * mt * 4 + 64) || h->r_scan.ensure_fresh(sw * 4 + 64))
+        return fail(h, SH_E_OOM, "match records");
+    // PartitionStreamReceiver runs inside each send() call
+    const int64_t batch = run->batch_events > 0 ? run->batch_events : 0;
+    const uint32_t* flags = nullptr;
+    const uint32_t* rid = nullptr;
+    const uint32_t* rfirst = nullptr;
+    // the runs of the consuming events only, walked back from each record's event
+    // (SH_RULES_RUNSCAN=1: flags, scan and first index over every event)
+    const bool walk_runs = sorted && !getenv("SH_RULES_RUNSCAN");
+    // order key (run, query, consuming event), least significant first; the
+    // records are in (opening event, rule) order, which the stable sort keeps
+    // among equal keys (creation order of the partials a consumer takes)
+    const int64_t runlen = batch > 0 ? std::min(batch, n) : n;
+    const int qbits = bits_for((uint64_t)(runlen - 1));
+    const int rbits = bits_for((uint64_t)(h->r_rules.size() - 1));
+    const int nbits = bits_for((uint64_t)(n - 1));
+    const bool packed = qbits + rbits <= 32;
+    uint32_t* k0 = h->r_keys.as<uint32_t>();
+    uint32_t* k1 = k0 + m;
+    uint32_t* k2 = k1 + m;
+    bool scan_runs = sorted && !walk_runs;
+    if (walk_runs) {
+        int32_t* long_run = h->v_flag.as<int32_t>() + 1;
+        int32_t lr = 0;
+        hipMemsetAsync(long_run, 0, 4, st);
+        if (shr_keys(rec_q, rec_r, m, perm, nullptr, nullptr, nullptr, batch, qbits, packed ? 1 : 0, k0, k1, k2,
+                     st, run->d_keys, run->d_run, long_run))
+            return fail(h, SH_E_HIP, "rule key launch failed");
+        hipMemcpyAsync(&lr, long_run, 4, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the rule keys");
+        scan_runs = lr != 0;
+    }
+    if (scan_runs) {
+        if (h->r_run.ensure_fresh((size_t)n * 12)) return fail(h, SH_E_OOM, "run ids");
+        uint32_t* f = h->r_run.as<uint32_t>();
+        if (shr_run_ids(run->d_keys, run->d_run, n, batch, f, f + n, f + 2 * n, h->w_scan.as<uint32_t>(), st))
+            return fail(h, SH_E_HIP, "run id launch failed");
+        flags = f;
+        rid = f + n;
+        rfirst = f + 2 * n;
+    }
+    if ((scan_runs || !walk_runs) &&
+        shr_keys(rec_q, rec_r, m, perm, flags, rid, rfirst, batch, qbits, packed ? 1 : 0, k0, k1, k2, st))
+        return fail(h, SH_E_HIP, "rule key launch failed");
+    const uint32_t* stage_key[4];
+    int stage_bits[4];
+    int ns = 0;
+    if (by_p) {
+        stage_key[ns] = rec_p;
+        stage_bits[ns++] = nbits;
+    }
+    if (packed) {
+        stage_key[ns] = k0;
+        stage_bits[ns++] = qbits + rbits;
+    } else {
+        stage_key[ns] = k0;
+        stage_bits[ns++] = qbits;
+        stage_key[ns] = k1;
+        stage_bits[ns++] = rbits;
+    }
+    stage_key[ns] = packed ? k1 : k2;
+    stage_bits[ns++] = nbits;
+    const uint32_t* order = nullptr;
+    uint32_t* gk = h->r_g.as<uint32_t>();
+    uint32_t* gv = gk + m;
+    uint32_t* kb[2] = {h->r_sk.as<uint32_t>(), h->r_sk.as<uint32_t>() + m};
+    uint32_t* vb[2] = {h->r_sv.as<uint32_t>(), h->r_sv.as<uint32_t>() + m};
+    for (int s = 0; s < ns; s++) {
+        if (stage_bits[s] == 0) continue;
+        const uint32_t* ko = nullptr;
+        const uint32_t* vo = nullptr;
+        if (shr_gather(stage_key[s], order, m, gk, gv, st) ||
+            shd_sort_pairs(gk, gv, m, stage_bits[s], kb, vb, h->r_hist.as<uint32_t>(), h->r_scan.as<uint32_t>(),
+                           st, &ko, &vo))
+            return fail(h, SH_E_HIP, "rule sort launch failed");
+        order = vo;
+    }
+    hipEventRecord(h->ev[2], st);
+    if (h->r_aggp) {
+        if (!run->d_out_query) {
+            if (h->a_q.ensure((size_t)m * 4)) return fail(h, SH_E_OOM, "aggregate query ids");
+            run->d_out_query = h->a_q.as<int32_t>();
+        }
+        if (!run->d_out_seq) {
+            if (h->a_seq.ensure((size_t)m * 8)) return fail(h, SH_E_OOM, "aggregate sequence numbers");
+            run->d_out_seq = h->a_seq.as<uint64_t>();
+        }
+    }
+    if (shr_place(dT, order, m, rec_p, rec_q, rec_r, perm, sts, dC, 0, std::max(1, h->n_out), run->d_out_seq,
+                  run->d_out_query, nullptr, run->d_out_values, st, sts32, tlo))
+        return fail(h, SH_E_HIP, "rule placement launch failed");
+    return SH_OK;
+}
+
+// the end of a rule run: kernel times, the aggregate post-pass
+static int rules_finish(sh_handle* h, sh_device_run* run, int64_t m, int32_t nkeys) {
+    hipStream_t st = h->stream;
+    hipEventRecord(h->ev[3], st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the rule engine");
+    hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
+    hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
+    hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
+    hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
+    h->times.advance_launches = 1;
+    if (h->r_aggp && m > 0) {
+        const int arc = agg_post(h, run, nkeys, run->d_out_query, (int)h->r_rules.size(), h->r_agg, h->r_argt,
+                                 std::max(1, h->n_out));
+        if (arc < 0) return arc;
+        if (arc == 1) return 1;  // not exact in parallel: the caller runs the general engine
+    }
+    return SH_OK;
+}
+
+// partitioned rule sets whose start filters open few partials: no key segment
+// (sh_rules.hip, "sparse partials"); 1 = not taken (decreasing timestamps, keys
+// out of range, more partials than n / 8): the caller runs the key-segment path.
+// Phases: segment = the partials and their lists, advance = the consuming events
+// and the records' order, emit = placement.
+static int run_rules_sparse(sh_handle* h, sh_device_run* run, int32_t nkeys) {
+    h->rs_last = 0;
+    if (const char* e = getenv("SH_RULES_SPARSE"))
+        if (e[0] == '0') return 1;
+    hipStream_t st = h->stream;
+    const int64_t n = run->n;
+    if (n <= 1 || n >= (int64_t)0xFFFFFFFFll || !run->d_keys) return 1;
+    const int64_t cap = std::max<int64_t>(65536, n / 8);
+    const size_t nk1 = (size_t)nkeys + 1;
+    if (h->rs_pr.ensure_fresh((size_t)cap * 16) || h->rs_key.ensure_fresh(nk1 * 8) ||
+        h->rs_list.ensure_fresh((size_t)cap * 20) || h->rs_ctl.ensure_fresh(64) || ensure_ws(h, (int64_t)nk1))
+        return fail(h, SH_E_OOM, "rule workspace");
+    uint32_t* pr = h->rs_pr.as<uint32_t>();
+    uint32_t* key_cnt = h->rs_key.as<uint32_t>();
+    uint32_t* key_off = key_cnt + nk1;
+    unsigned long long* ctl = h->rs_ctl.as<unsigned long long>();  // [0] partials, [1] records, [2] flag
+    shd_cols sc;
+    memset(&sc, 0, sizeof(sc));
+    const int na = (int)h->stream_types[0].size();
+    for (int a = 0; a < na; a++) sc.col[0][a] = run->d_cols[a];
+    hipEventRecord(h->ev[0], st);
+    hipMemcpyAsync(h->d_cols_desc.p, &sc, sizeof(sc), hipMemcpyHostToDevice, st);
+    const shd_cols* dC = h->d_cols_desc.as<shd_cols>();
+    const shr_table* dT = h->rd_tab.as<shr_table>();
+    hipMemsetAsync(key_cnt, 0, nk1 * 4, st);
+    hipMemsetAsync(ctl, 0, 24, st);
+    if (shr_sparse_open(dT, run->d_ts, run->d_keys, n, nkeys, dC, h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr,
+                        &h->r_img, pr, pr + cap, pr + 2 * cap, pr + 3 * cap, key_cnt, ctl, cap, (int32_t*)(ctl + 2),
+                        st))
+        return fail(h, SH_E_HIP, "sparse partial launch failed");
+    unsigned long long rd[3] = {0, 0, 0};
+    hipMemcpyAsync(rd, ctl, 24, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the sparse partials");
+    const int64_t np = (int64_t)rd[0];
+    if (rd[2] || np > cap) return 1;
+    if (shd_exclusive_scan(key_cnt, key_off, (int64_t)nk1, h->w_scan.as<uint32_t>(), st))
+        return fail(h, SH_E_HIP, "scan");
+    hipEventRecord(h->ev[1], st);
+    uint32_t* l_p = h->rs_list.as<uint32_t>();
+    uint32_t* l_r = l_p + cap;
+    uint32_t* l_q = l_r + cap;
+    int64_t* l_te = (int64_t*)(l_q + cap);
+    const int64_t rcap = std::max<int64_t>(np, 1);
+    if (h->r_rec.ensure_fresh((size_t)rcap * 12)) return fail(h, SH_E_OOM, "match records");
+    uint32_t* rec_p = h->r_rec.as<uint32_t>();
+    uint32_t* rec_q = rec_p + rcap;
+    uint32_t* rec_r = rec_q + rcap;
+    if (np > 0 &&
+        shr_sparse_match(dT, run->d_ts, run->d_keys, n, dC, pr, pr + cap, pr + 2 * cap, pr + 3 * cap, ctl, np, key_off,
+                         l_p, l_r, l_te, l_q, rec_p, rec_q, rec_r, ctl + 1, rcap, st))
+        return fail(h, SH_E_HIP, "sparse match launch failed");
+    hipMemcpyAsync(rd, ctl, 16, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the sparse match");
+    const int64_t m = (int64_t)rd[1];
+    h->rs_last = 1;
+    run->out_count = m;
+    if (m > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
+    if (m > 0) {
+        // the records' arrays hold rcap entries each: compact them for the order stages
+        if (m < rcap) {
+            hipMemcpyAsync(rec_p + m, rec_q, (size_t)m * 4, hipMemcpyDeviceToDevice, st);
+            hipMemcpyAsync(rec_p + 2 * m, rec_r, (size_t)m * 4, hipMemcpyDeviceToDevice, st);
+        }
+        int prc = rules_order_place(h, run, m, rec_p, rec_p + m, rec_p + 2 * m, nullptr, run->d_ts, dC, nullptr, 0,
+                                    true, true);
+        if (prc) return prc;
+    } else {
+        hipEventRecord(h->ev[2], st);
+    }
+    return rules_finish(h, run, m, nkeys);
+}
+
 int run_rules(sh_handle* h, sh_device_run* run) {
     hipStream_t st = h->stream;
     const int64_t n = run->n;
@@ -82,6 +286,10 @@ int run_rules(sh_handle* h, sh_device_run* run) {
     const int32_t nkeys = sorted ? std::max(1, run->n_keys) : 1;
     if (ensure_ws(h, n) || h->v_flag.ensure_fresh(64)) return fail(h, SH_E_OOM, "workspace");
     h->times = sh_kernel_times{};
+    if (sorted) {
+        const int src = run_rules_sparse(h, run, nkeys);
+        if (src != 1) return src;
+    }
     shd_batch B;
     memset(&B, 0, sizeof(B));
     B.ts = run->d_ts;
@@ -148,122 +356,19 @@ int run_rules(sh_handle* h, sh_device_run* run) {
     run->out_count = m;
     if (m > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
     if (m > 0) {
-        const int64_t mt = (m + 4095) / 4096;
-        const size_t sw = std::max(shd_scan_tmp_words(256 * mt), (size_t)16);
-        if (h->r_rec.ensure_fresh((size_t)m * 12) || h->r_keys.ensure_fresh((size_t)m * 12) ||
-            h->r_g.ensure_fresh((size_t)m * 8) || h->r_sk.ensure_fresh((size_t)m * 8) ||
-            h->r_sv.ensure_fresh((size_t)m * 8) || h->r_hist.ensure_fresh((size_t)256 * mt * 4 + 64) ||
-            h->r_scan.ensure_fresh(sw * 4 + 64))
-            return fail(h, SH_E_OOM, "match records");
+        if (h->r_rec.ensure_fresh((size_t)m * 12)) return fail(h, SH_E_OOM, "match records");
         uint32_t* rec_p = h->r_rec.as<uint32_t>();
         uint32_t* rec_q = rec_p + m;
         uint32_t* rec_r = rec_q + m;
         if (shr_write(dT, sts, skeys, n, sentinel, dC, cnt, off, rec_p, rec_q, rec_r, st,
                       h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr, &h->r_img, sts32, tlo))
             return fail(h, SH_E_HIP, "rule write launch failed");
-        // PartitionStreamReceiver runs inside each send() call
-        const int64_t batch = run->batch_events > 0 ? run->batch_events : 0;
-        const uint32_t* flags = nullptr;
-        const uint32_t* rid = nullptr;
-        const uint32_t* rfirst = nullptr;
-        // the runs of the consuming events only, walked back from each record's event
-        // (SH_RULES_RUNSCAN=1: flags, scan and first index over every event)
-        const bool walk_runs = sorted && !getenv("SH_RULES_RUNSCAN");
-        // order key (run, query, consuming event), least significant first; the
-        // records are in (opening event, rule) order, which the stable sort keeps
-        // among equal keys (creation order of the partials a consumer takes)
-        const int64_t runlen = batch > 0 ? std::min(batch, n) : n;
-        const int qbits = bits_for((uint64_t)(runlen - 1));
-        const int rbits = bits_for((uint64_t)(h->r_rules.size() - 1));
-        const int nbits = bits_for((uint64_t)(n - 1));
-        const bool packed = qbits + rbits <= 32;
-        uint32_t* k0 = h->r_keys.as<uint32_t>();
-        uint32_t* k1 = k0 + m;
-        uint32_t* k2 = k1 + m;
-        bool scan_runs = sorted && !walk_runs;
-        if (walk_runs) {
-            int32_t* long_run = h->v_flag.as<int32_t>() + 1;
-            int32_t lr = 0;
-            hipMemsetAsync(long_run, 0, 4, st);
-            if (shr_keys(rec_q, rec_r, m, perm, nullptr, nullptr, nullptr, batch, qbits, packed ? 1 : 0, k0, k1, k2,
-                         st, run->d_keys, run->d_run, long_run))
-                return fail(h, SH_E_HIP, "rule key launch failed");
-            hipMemcpyAsync(&lr, long_run, 4, hipMemcpyDeviceToHost, st);
-            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the rule keys");
-            scan_runs = lr != 0;
-        }
-        if (scan_runs) {
-            if (h->r_run.ensure_fresh((size_t)n * 12)) return fail(h, SH_E_OOM, "run ids");
-            uint32_t* f = h->r_run.as<uint32_t>();
-            if (shr_run_ids(run->d_keys, run->d_run, n, batch, f, f + n, f + 2 * n, h->w_scan.as<uint32_t>(), st))
-                return fail(h, SH_E_HIP, "run id launch failed");
-            flags = f;
-            rid = f + n;
-            rfirst = f + 2 * n;
-        }
-        if ((scan_runs || !walk_runs) &&
-            shr_keys(rec_q, rec_r, m, perm, flags, rid, rfirst, batch, qbits, packed ? 1 : 0, k0, k1, k2, st))
-            return fail(h, SH_E_HIP, "rule key launch failed");
-        const uint32_t* stage_key[3];
-        int stage_bits[3];
-        int ns = 0;
-        if (packed) {
-            stage_key[ns] = k0;
-            stage_bits[ns++] = qbits + rbits;
-        } else {
-            stage_key[ns] = k0;
-            stage_bits[ns++] = qbits;
-            stage_key[ns] = k1;
-            stage_bits[ns++] = rbits;
-        }
-        stage_key[ns] = packed ? k1 : k2;
-        stage_bits[ns++] = nbits;
-        const uint32_t* order = nullptr;
-        uint32_t* gk = h->r_g.as<uint32_t>();
-        uint32_t* gv = gk + m;
-        uint32_t* kb[2] = {h->r_sk.as<uint32_t>(), h->r_sk.as<uint32_t>() + m};
-        uint32_t* vb[2] = {h->r_sv.as<uint32_t>(), h->r_sv.as<uint32_t>() + m};
-        for (int s = 0; s < ns; s++) {
-            if (stage_bits[s] == 0) continue;
-            const uint32_t* ko = nullptr;
-            const uint32_t* vo = nullptr;
-            if (shr_gather(stage_key[s], order, m, gk, gv, st) ||
-                shd_sort_pairs(gk, gv, m, stage_bits[s], kb, vb, h->r_hist.as<uint32_t>(), h->r_scan.as<uint32_t>(),
-                               st, &ko, &vo))
-                return fail(h, SH_E_HIP, "rule sort launch failed");
-            order = vo;
-        }
-        hipEventRecord(h->ev[2], st);
-        if (h->r_aggp) {
-            if (!run->d_out_query) {
-                if (h->a_q.ensure((size_t)m * 4)) return fail(h, SH_E_OOM, "aggregate query ids");
-                run->d_out_query = h->a_q.as<int32_t>();
-            }
-            if (!run->d_out_seq) {
-                if (h->a_seq.ensure((size_t)m * 8)) return fail(h, SH_E_OOM, "aggregate sequence numbers");
-                run->d_out_seq = h->a_seq.as<uint64_t>();
-            }
-        }
-        if (shr_place(dT, order, m, rec_p, rec_q, rec_r, perm, sts, dC, 0, std::max(1, h->n_out), run->d_out_seq,
-                      run->d_out_query, nullptr, run->d_out_values, st, sts32, tlo))
-            return fail(h, SH_E_HIP, "rule placement launch failed");
+        int prc = rules_order_place(h, run, m, rec_p, rec_q, rec_r, perm, sts, dC, sts32, tlo, sorted, false);
+        if (prc) return prc;
     } else {
         hipEventRecord(h->ev[2], st);
     }
-    hipEventRecord(h->ev[3], st);
-    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the rule engine");
-    hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
-    hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
-    hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
-    hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
-    h->times.advance_launches = 1;
-    if (h->r_aggp && m > 0) {
-        const int arc = agg_post(h, run, nkeys, run->d_out_query, (int)h->r_rules.size(), h->r_agg, h->r_argt,
-                                 std::max(1, h->n_out));
-        if (arc < 0) return arc;
-        if (arc == 1) return 1;  // not exact in parallel: the caller runs the general engine
-    }
-    return SH_OK;
+    return rules_finish(h, run, m, nkeys);
 }
 
 // bucketed window engine (sh_bucket.hip): partitioned window programs with a

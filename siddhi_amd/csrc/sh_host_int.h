@@ -262,6 +262,10 @@ struct sh_handle {
     DevBuf r_tsr, v_ts32, v_sts32, v_mid_ts32;  // 32-bit timestamp offsets of a rule run (range, arrival, sorted, mid)
     shr_img r_img{};
     DevBuf r_rec, r_keys, r_g, r_sk, r_sv, r_hist, r_scan, r_run;
+    // sparse partials (shr_sparse_*): the partials, per key counts and list starts,
+    // the keys' lists (opening event, rule, consuming event, expiry), counters
+    DevBuf rs_pr, rs_key, rs_list, rs_ctl;
+    int rs_last = 0;  // 1: the last rule run took the sparse-partial path
     // ---- bucketed window engine (sh_bucket.hip + shb_match): 0 untried, 1 loaded, <0 unavailable
     int bk_state = 0;
     int32_t part_attr0 = -1;  // stream-0 attribute keying query 0's partition
@@ -338,6 +342,7 @@ int shx_jit_compile(sh_handle* h);
 int shx_bucket_status(sh_handle* h);
 int shx_seq3_status(sh_handle* h);
 int shx_agg_status(sh_handle* h);
+int shx_rules_status(sh_handle* h);
 int shx_seq3_shape(sh_handle* h);
 int shx_bucket_compile(sh_handle* h, char* buf, int64_t len);
 int64_t shx_jit_source(sh_handle* h, char* buf, int64_t len);

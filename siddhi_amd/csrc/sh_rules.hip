@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 
 #include "../../include/sh_query.h"
 #include "sh_device.h"
@@ -573,5 +574,248 @@ extern "C" int shr_ts_to32(const int64_t* ts, int64_t n, int64_t base, uint32_t*
     if (n <= 0) return 0;
     hipLaunchKernelGGL(k_ts_to32, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 65536)), dim3(256), 0,
                        (hipStream_t)stream, ts, n, base, t32);
+    return rules_ok();
+}
+
+// ---------------------------------------------------------------- sparse partials
+// The same matches without a key segment, for partitioned rule sets whose start
+// filters open few partials (C5: `amount > A and merchant == M` holds for ~2% of
+// the events). Every partial (p, r) is independent -- it is consumed by the first
+// later event q of its key with |ts_q - ts_p| <= W_r and f2_r(p, q) -- so with
+// non-decreasing timestamps (checked over the whole run) the consuming event is
+// the least such q:
+//   k_sparse_open: per event (arrival order) the index lookup and f1 of its
+//     candidate rules -> the partials (p, r), appended through an LDS buffer per
+//     workgroup, and per key a count (the partial's slot in its key's list);
+//   scan of the per-key counts -> each key's list;
+//   k_sparse_place: the partials into their keys' lists, with their expiry time;
+//   k_sparse_take: per event q, its key's partials opened before it that are not
+//     expired at ts_q and whose f2 holds -> atomicMin of q into the partial;
+//   k_sparse_rec: the taken partials -> (p, q, r) records (any order: the host
+//     sorts them by p first, which restores the (opening event, rule) order the
+//     record sort's stability relies on).
+// A run whose timestamps decrease, whose keys leave [0, nkeys), or whose partials
+// overflow the buffers (the host reads the count) sets a flag: the host runs the
+// key-segment path instead.
+#define SPA_TPB 1024
+#define SPA_BUF 4096
+#define SPA_F_TS 1
+#define SPA_F_KEY 2
+
+__device__ __forceinline__ void spa_lookup(const shr_table* __restrict__ RT, const shd_cols* __restrict__ C,
+                                           const int64_t* s_ixv, const uint32_t* s_ixs, bool lds_ix,
+                                           const uint8_t* __restrict__ img, const shr_img& I, uint32_t p,
+                                           uint32_t* lo, uint32_t* hi) {
+    *lo = *hi = 0;
+    const int ix_attr = RT->ix_attr;
+    if (ix_attr < 0) return;
+    const int ty = RT->attr_type[ix_attr];
+    const int64_t x = rule_ix_key(ty, load_attr(C, 0, ix_attr, ty, p));
+    if (img && I.dense_n) {
+        const int64_t dv = x - I.dense_min;
+        if (dv >= 0 && dv < I.dense_n) {
+            const uint2 e = ((const uint2*)(img + I.off_dense))[dv];
+            *lo = e.x;
+            *hi = e.y;
+        }
+        return;
+    }
+    const int n_ix = RT->n_ix;
+    int a = 0, b = n_ix;
+    while (a < b) {
+        const int m = (a + b) >> 1;
+        if ((lds_ix ? s_ixv[m] : RT->ix_val[m]) < x)
+            a = m + 1;
+        else
+            b = m;
+    }
+    if (a < n_ix && (lds_ix ? s_ixv[a] : RT->ix_val[a]) == x) {
+        *lo = lds_ix ? s_ixs[a] : RT->ix_start[a];
+        *hi = lds_ix ? s_ixs[a + 1] : RT->ix_start[a + 1];
+    }
+}
+
+__global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __restrict__ RT,
+                                                         const int64_t* __restrict__ ts,
+                                                         const int32_t* __restrict__ akeys, int64_t n, int32_t nkeys,
+                                                         const shd_cols* __restrict__ C,
+                                                         const uint8_t* __restrict__ img, shr_img I,
+                                                         uint32_t* __restrict__ pr_p, uint32_t* __restrict__ pr_r,
+                                                         uint32_t* __restrict__ pr_key, uint32_t* __restrict__ pr_slot,
+                                                         uint32_t* __restrict__ key_cnt,
+                                                         unsigned long long* __restrict__ ctr, int64_t cap,
+                                                         int32_t* __restrict__ flag) {
+    __shared__ int64_t s_ixv[SHR_LDS_IX];
+    __shared__ uint32_t s_ixs[SHR_LDS_IX + 1];
+    __shared__ uint32_t b_p[SPA_BUF], b_r[SPA_BUF], b_k[SPA_BUF], b_s[SPA_BUF];
+    __shared__ uint32_t s_fill;
+    __shared__ unsigned long long s_base;
+    const int n_ix = RT->n_ix;
+    const bool lds_ix = RT->ix_attr >= 0 && n_ix <= SHR_LDS_IX && !(img && I.dense_n);
+    if (lds_ix) {
+        for (int i = threadIdx.x; i < n_ix; i += blockDim.x) s_ixv[i] = RT->ix_val[i];
+        for (int i = threadIdx.x; i <= n_ix; i += blockDim.x) s_ixs[i] = RT->ix_start[i];
+    }
+    if (threadIdx.x == 0) s_fill = 0u;
+    const uint32_t n_free = (uint32_t)RT->n_free;
+    int32_t fl = 0;
+    __syncthreads();
+    for (int64_t base = (int64_t)blockIdx.x * SPA_TPB; base < n; base += (int64_t)gridDim.x * SPA_TPB) {
+        const int64_t p = base + threadIdx.x;
+        if (p < n) {
+            if (p > 0 && ts[p] < ts[p - 1]) fl |= SPA_F_TS;
+            const int32_t key = akeys[p];
+            if (key >= nkeys) fl |= SPA_F_KEY;
+            if (key >= 0 && key < nkeys) {
+                uint32_t lo, hi;
+                spa_lookup(RT, C, s_ixv, s_ixs, lds_ix, img, I, (uint32_t)p, &lo, &hi);
+                const uint32_t nsel = hi - lo, total = nsel + n_free;
+                for (uint32_t k = 0; k < total; k++) {
+                    const uint32_t r = k < nsel ? RT->ix_rule[lo + k] : RT->free_rule[k - nsel];
+                    const shr_rule* R = RT->rules + r;
+                    if (!rule_terms(R->t[0], R->nt[0], (uint32_t)p, SHD_NULL_ROW, C)) continue;
+                    const uint32_t slot = atomicAdd(&key_cnt[key], 1u);
+                    const uint32_t at = atomicAdd(&s_fill, 1u);
+                    if (at < SPA_BUF) {
+                        b_p[at] = (uint32_t)p;
+                        b_r[at] = r;
+                        b_k[at] = (uint32_t)key;
+                        b_s[at] = slot;
+                    } else {
+                        // (a chunk with more than the buffer: straight to global)
+                        const unsigned long long g = atomicAdd(ctr, 1ull);
+                        if ((int64_t)g < cap) {
+                            pr_p[g] = (uint32_t)p;
+                            pr_r[g] = r;
+                            pr_key[g] = (uint32_t)key;
+                            pr_slot[g] = slot;
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t fill = s_fill < SPA_BUF ? s_fill : SPA_BUF;
+        const bool last = base + (int64_t)gridDim.x * SPA_TPB >= n;
+        if (fill >= SPA_BUF / 2 || (last && fill)) {
+            if (threadIdx.x == 0) s_base = atomicAdd(ctr, (unsigned long long)fill);
+            __syncthreads();
+            const int64_t g0 = (int64_t)s_base;
+            for (uint32_t i = threadIdx.x; i < fill; i += SPA_TPB) {
+                const int64_t g = g0 + i;
+                if (g < cap) {
+                    pr_p[g] = b_p[i];
+                    pr_r[g] = b_r[i];
+                    pr_key[g] = b_k[i];
+                    pr_slot[g] = b_s[i];
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) s_fill = 0u;
+        }
+        __syncthreads();
+    }
+    if (fl) atomicOr(flag, fl);
+}
+
+__global__ void k_sparse_place(const uint32_t* __restrict__ pr_p, const uint32_t* __restrict__ pr_r,
+                               const uint32_t* __restrict__ pr_key, const uint32_t* __restrict__ pr_slot,
+                               const unsigned long long* __restrict__ ctr, const uint32_t* __restrict__ key_off,
+                               const shr_table* __restrict__ RT, const int64_t* __restrict__ ts,
+                               uint32_t* __restrict__ l_p, uint32_t* __restrict__ l_r, int64_t* __restrict__ l_te,
+                               uint32_t* __restrict__ l_q) {
+    const int64_t np = (int64_t)*ctr;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < np; s += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = pr_p[s], r = pr_r[s];  // (np <= the buffers: the host checked the count)
+        const uint32_t pos = key_off[pr_key[s]] + pr_slot[s];
+        const int64_t W = RT->rules[r].within;
+        const int64_t t = ts[p];
+        l_p[pos] = p;
+        l_r[pos] = r;
+        l_te[pos] = (W < 0 || t > INT64_MAX - W) ? INT64_MAX : t + W;
+        l_q[pos] = 0xFFFFFFFFu;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sparse_take(const shr_table* __restrict__ RT, const int64_t* __restrict__ ts,
+                                                     const int32_t* __restrict__ akeys, int64_t n,
+                                                     const shd_cols* __restrict__ C,
+                                                     const uint32_t* __restrict__ key_off,
+                                                     const uint32_t* __restrict__ l_p, const uint32_t* __restrict__ l_r,
+                                                     const int64_t* __restrict__ l_te, uint32_t* __restrict__ l_q) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t key = akeys[q];
+        if (key < 0) continue;
+        const uint32_t lo = key_off[key], hi = key_off[key + 1];
+        if (lo == hi) continue;
+        const int64_t tq = ts[q];
+        for (uint32_t pos = lo; pos < hi; pos++) {
+            const uint32_t p = l_p[pos];
+            if ((int64_t)p >= q || tq > l_te[pos]) continue;
+            const shr_rule* R = RT->rules + l_r[pos];
+            if (rule_terms(R->t[1], R->nt[1], p, (uint32_t)q, C)) atomicMin(&l_q[pos], (uint32_t)q);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sparse_rec(const uint32_t* __restrict__ l_p,
+                                                    const uint32_t* __restrict__ l_r,
+                                                    const uint32_t* __restrict__ l_q,
+                                                    const unsigned long long* __restrict__ ctr,
+                                                    uint32_t* __restrict__ rec_p, uint32_t* __restrict__ rec_q,
+                                                    uint32_t* __restrict__ rec_r, unsigned long long* __restrict__ rctr,
+                                                    int64_t rcap) {
+    const int64_t np = (int64_t)*ctr;
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < np; s0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = s0 + threadIdx.x;
+        const bool hit = s < np && l_q[s] != 0xFFFFFFFFu;
+        const uint64_t m = __ballot(hit);
+        if (m == 0ull) continue;
+        unsigned long long b = 0;
+        if (lane == __ffsll((unsigned long long)m) - 1) b = atomicAdd(rctr, (unsigned long long)__popcll(m));
+        b = __shfl(b, __ffsll((unsigned long long)m) - 1);
+        if (hit) {
+            const int64_t o = (int64_t)b + __popcll(m & lt);
+            if (o < rcap) {
+                rec_p[o] = l_p[s];
+                rec_q[o] = l_q[s];
+                rec_r[o] = l_r[s];
+            }
+        }
+    }
+}
+
+extern "C" int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int32_t* akeys, int64_t n, int32_t nkeys,
+                               const shd_cols* dC, const uint8_t* img, const shr_img* I, uint32_t* pr_p,
+                               uint32_t* pr_r, uint32_t* pr_key, uint32_t* pr_slot, uint32_t* key_cnt,
+                               unsigned long long* ctr, int64_t cap, int32_t* flag, void* stream) {
+    shr_img none;
+    memset(&none, 0, sizeof(none));
+    const bool use_img = img && I && I->bytes > 0;
+    int64_t g = (n + SPA_TPB - 1) / SPA_TPB;
+    if (g > 1024) g = 1024;  // 4 per CU, each striding over many tiles (few buffer flushes)
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(k_sparse_open, dim3((unsigned)g), dim3(SPA_TPB), 0, (hipStream_t)stream, dT, ts, akeys, n, nkeys,
+                       dC, use_img ? img : (const uint8_t*)nullptr, use_img ? *I : none, pr_p, pr_r, pr_key, pr_slot,
+                       key_cnt, ctr, cap, flag);
+    return rules_ok();
+}
+
+extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const int32_t* akeys, int64_t n,
+                                const shd_cols* dC, const uint32_t* pr_p, const uint32_t* pr_r,
+                                const uint32_t* pr_key, const uint32_t* pr_slot, const unsigned long long* ctr,
+                                int64_t n_pairs_max, const uint32_t* key_off, uint32_t* l_p, uint32_t* l_r,
+                                int64_t* l_te, uint32_t* l_q, uint32_t* rec_p, uint32_t* rec_q, uint32_t* rec_r,
+                                unsigned long long* rctr, int64_t rcap, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned gp = rgrid(n_pairs_max);
+    hipLaunchKernelGGL(k_sparse_place, dim3(gp), dim3(RTPB), 0, st, pr_p, pr_r, pr_key, pr_slot, ctr, key_off, dT, ts,
+                       l_p, l_r, l_te, l_q);
+    hipLaunchKernelGGL(k_sparse_take, dim3(rgrid(n) < 8192u ? rgrid(n) : 8192u), dim3(256), 0, st, dT, ts, akeys, n, dC,
+                       key_off, (const uint32_t*)l_p, (const uint32_t*)l_r, (const int64_t*)l_te, l_q);
+    hipLaunchKernelGGL(k_sparse_rec, dim3(gp), dim3(256), 0, st, (const uint32_t*)l_p, (const uint32_t*)l_r,
+                       (const uint32_t*)l_q, ctr, rec_p, rec_q, rec_r, rctr, rcap);
     return rules_ok();
 }

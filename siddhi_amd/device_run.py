@@ -115,6 +115,11 @@ class DeviceRunner:
         """1: the last run took the rise-and-fall sequence engine (k_seq3)."""
         return lib().shx_seq3_status(self.handle.h)
 
+    def rules_status(self):
+        """1: the last rule-set run took the sparse-partial path (no key segment),
+        0: the key-segment path (or not a rule set)."""
+        return lib().shx_rules_status(self.handle.h)
+
     def agg_status(self):
         """aggregators of the last run: 1 post-pass over a fast engine's rows
         (sh_agg.hip), 2 not exact in parallel (a sequential engine ran), 0 none."""

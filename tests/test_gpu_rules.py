@@ -20,7 +20,7 @@ def _device():
         pytest.skip("no GPU")
 
 
-def _device_run(text, n_cards, ts, card, amount, merchant, batch, partitioned=True):
+def _device_run(text, n_cards, ts, card, amount, merchant, batch, partitioned=True, status=None):
     import torch
     from siddhi_amd.device_run import DeviceRunner
     runner = DeviceRunner(compiler.compile_app(text, card_strings(n_cards)))
@@ -30,38 +30,72 @@ def _device_run(text, n_cards, ts, card, amount, merchant, batch, partitioned=Tr
                                  batch_events=batch, with_query=True)
     torch.cuda.synchronize()
     res = (seq.cpu().numpy(), vals.cpu().numpy(), q.cpu().numpy())
+    if status is not None:
+        status.append(runner.rules_status())
     runner.close()
     return res
 
 
-@pytest.mark.parametrize("general", [False, True], ids=["rules", "general"])
+@pytest.mark.parametrize("engine", ["sparse", "segment", "general"])
 @pytest.mark.parametrize("ci", range(len(CASES)))
-def test_rule_sets_vs_oracle(ci, general, monkeypatch):
+def test_rule_sets_vs_oracle(ci, engine, monkeypatch):
+    """sparse: the partials found in arrival order (partitioned sets; small runs
+    always fit its buffers), segment: the key-segment scan (SH_RULES_SPARSE=0),
+    general: the general NFA engine"""
     case = CASES[ci]
     n, cards, nr, rate, batch, merchants, partitioned, free, seed = case
-    if general:
+    if engine == "general":
         if nr > 16:
             pytest.skip("the general engine's query table holds 16 queries")
         monkeypatch.setenv("SH_DISABLE_RULES", "1")
+    if engine == "segment":
+        monkeypatch.setenv("SH_RULES_SPARSE", "0")
     text, rules, (ts, card, amount, merchant) = case_data(case)
     ref = oracle_run(text, cards, ts, card, amount, merchant, batch, partitioned)
-    seq, vals, q = _device_run(text, cards, ts, card, amount, merchant, batch, partitioned)
+    st = []
+    seq, vals, q = _device_run(text, cards, ts, card, amount, merchant, batch, partitioned, status=st)
+    if engine != "general":
+        assert st == [1 if (engine == "sparse" and partitioned) else 0]
     assert len(seq) == len(ref["seq"]) > 0
     assert np.array_equal(seq, ref["seq"].astype(np.int64))
     assert np.array_equal(q, ref["query"])
     assert np.array_equal(vals[:, :2], ref["values"][:, :2])
 
 
-@pytest.mark.parametrize("n,cards", [(20_000_000, 200_000), (100_000_000, 1_000_000)])
-def test_c5_large_vs_vectorised_restatement(n, cards):
-    """1,000 rules (BASELINE distributions): 20M card transactions over 200k cards,
-    and the full SURVEY 8d size, 100M transactions over 1M cards."""
+@pytest.mark.parametrize("n,cards,sparse", [(20_000_000, 200_000, "1"), (20_000_000, 200_000, "0"),
+                                            (100_000_000, 1_000_000, "1")], ids=["20M", "20M-segment", "100M"])
+def test_c5_large_vs_vectorised_restatement(n, cards, sparse, monkeypatch):
+    """1,000 rules (BASELINE distributions): 20M card transactions over 200k cards
+    (sparse-partial and key-segment paths), and the full SURVEY 8d size, 100M
+    transactions over 1M cards."""
+    monkeypatch.setenv("SH_RULES_SPARSE", sparse)
     ts, card, amount, merchant = synth.txn_stream(n, cards, 100)
     rules = synth.c5_rules()
     text = synth.c5_query(rules)
-    seq, vals, q = _device_run(text, cards, ts, card, amount, merchant, 4096)
+    st = []
+    seq, vals, q = _device_run(text, cards, ts, card, amount, merchant, 4096, status=st)
+    assert st == [int(sparse)]
     eseq, erule, evals = c5_expected(ts, card, amount, merchant, rules)
     assert len(seq) == len(eseq) > 0
     assert np.array_equal(seq, eseq)
     assert np.array_equal(q, erule)
     assert np.array_equal(vals[:, :2], evals)
+
+
+def test_sparse_falls_back_on_decreasing_timestamps():
+    """a run whose timestamps decrease somewhere (but not inside a key) leaves the
+    sparse path; the key-segment scan gives the oracle's rows"""
+    case = CASES[0]
+    n, cards, nr, rate, batch, merchants, partitioned, free, seed = case
+    text, rules, (ts, card, amount, merchant) = case_data(case)
+    # swap two adjacent events of different cards whose times differ
+    i = next(k for k in range(1, n) if card[k] != card[k - 1] and ts[k] > ts[k - 1])
+    for a in (ts, card, amount, merchant):
+        a[[i - 1, i]] = a[[i, i - 1]]
+    ref = oracle_run(text, cards, ts, card, amount, merchant, batch, partitioned)
+    st = []
+    seq, vals, q = _device_run(text, cards, ts, card, amount, merchant, batch, partitioned, status=st)
+    assert st == [0]
+    assert np.array_equal(seq, ref["seq"].astype(np.int64))
+    assert np.array_equal(q, ref["query"])
+    assert np.array_equal(vals[:, :2], ref["values"][:, :2])
