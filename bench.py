@@ -637,9 +637,10 @@ def main():
                          "match_kernel_only_GBps": match_only / 1e9},
             "phase_ms": {"segment": seg_ms, "advance": adv_ms, "emit": emt_ms},
             # which device engine ran (DeviceRunner status: bucketed 1, sequence carry
-            # seq3 2 / key-segment seq3 1, aggregates carried 4 / post-pass 1 / in lanes 3)
+            # seq3 2 / key-segment seq3 1, aggregates carried 4 / post-pass 1 / in lanes 3,
+            # rule sets: sparse partials 1 / key-segment scan 0)
             "engine": {"bucket": runner.bucket_status(), "seq3": runner.seq3_status(),
-                       "agg": runner.agg_status()},
+                       "agg": runner.agg_status(), "rules_sparse": runner.rules_status()},
             "cpu_baseline": cpu,
             "verified_vs_restatement": verified,
         }
