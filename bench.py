@@ -230,12 +230,18 @@ def main_c4(args, torch, dist, world, rank, dev):
     end = synth.c4_end_time(blocks)
     group = dist.new_group(backend="gloo") if world > 1 else None
 
+    # phase clocks of the streaming path (sh_host_nfa.cpp HpScope; a few clock reads
+    # per call): host work vs time blocked on the device and copies
+    os.environ["SH_HOST_PROF"] = "1"
+
     def step():
         base = HipEngine(c)
         eng = base
+        comm = None
         if world > 1:
             from siddhi_amd.shard_stream import ShardedStreamEngine, TorchGroupComm
-            eng = ShardedStreamEngine(base, TorchGroupComm(group))
+            comm = TorchGroupComm(group)
+            eng = ShardedStreamEngine(base, comm)
         register_users(eng, blocks)
         t = time.perf_counter()
         eng.start()
@@ -250,8 +256,11 @@ def main_c4(args, torch, dist, world, rank, dev):
         dt = time.perf_counter() - t
         if world > 1:
             eng.check()
+        last["prof"] = base.host_profile()
+        last["comm"] = (comm.seconds, comm.calls) if comm is not None else None
         base.close()
         last["out"] = out
+        last["dt"] = dt
         return len(out["seq"]), dt
 
     last = {}
@@ -307,10 +316,22 @@ def main_c4(args, torch, dist, world, rank, dev):
         cpu = {"value": acc / cdt, "unit": "events/s", "cores": 1, "kind": "port",
                "sample": f"first {acc} events ({len(sub)} send(Event[]) calls) of the same C4 stream, C++ "
                          f"restatement of siddhi-core's processors (oracle/), 1 thread"}
+    # the last step's split (rank 0): wall = host work + time blocked in stream syncs
+    # (kernels and copies the host waits for) + coordination (N > 1: all_gathers)
+    hp = last.get("prof") or {}
+    wall_ms = last.get("dt", 0.0) * 1000.0
+    wait_ms = hp.get("sync_wait", (0.0, 0))[0]
+    comm_ms = last["comm"][0] * 1000.0 if last.get("comm") else 0.0
+    split = {"wall_ms": wall_ms, "blocked_on_device_ms": wait_ms, "syncs": hp.get("sync_wait", (0.0, 0))[1],
+             "coordination_ms": comm_ms, "coordination_calls": last["comm"][1] if last.get("comm") else 0,
+             "host_ms": wall_ms - wait_ms - comm_ms,
+             "phases_ms": {k: round(v[0], 1) for k, v in hp.items() if k not in ("hist_records", "sync_wait")},
+             "calls": len(blocks)}
     if rank == 0:
         print(json.dumps({
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "split_last_step": split,
             "ms_per_step": tot * 1000.0 / args.steps, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic", "nproc": os.cpu_count(),
             "ingest": {"path": "host buffers of every send(Event[]) call cross PCIe inside the timed step"},

@@ -131,6 +131,18 @@ class HipEngine:
     def advance_time(self, now):
         check(self.h, _lib.sh_advance_time(self.h, int(now)))
 
+    HOST_PHASES = ("push", "timers", "process", "history", "place", "drain", "hist_copy", "hist_apply",
+                   "hist_rank", "hist_records", "sync_wait", "pull")
+
+    def host_profile(self):
+        """SH_HOST_PROF phase clocks of this handle: {phase: (ms, count)} (zeros
+        unless SH_HOST_PROF was set when the calls ran)"""
+        k = len(self.HOST_PHASES)
+        ms = (C.c_double * k)()
+        cnt = (C.c_int64 * k)()
+        _lib.shx_host_profile(self.h, ms, cnt, k)
+        return {name: (float(ms[i]), int(cnt[i])) for i, name in enumerate(self.HOST_PHASES)}
+
     def snapshot(self) -> bytes:
         """the matcher state image (sh_snapshot)"""
         size = C.c_int64(0)

@@ -170,6 +170,8 @@ def bind_product(lib):
     lib.shx_agg_status.restype = C.c_int
     lib.shx_rules_status.argtypes = [C.c_void_p]
     lib.shx_rules_status.restype = C.c_int
+    lib.shx_host_profile.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    lib.shx_host_profile.restype = C.c_int
     lib.shx_seq3_shape.argtypes = [C.c_void_p]
     lib.shx_seq3_shape.restype = C.c_int
     return lib

@@ -770,11 +770,16 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
 void sh_destroy(sh_handle* h) {
     if (!h) return;
     if (getenv("SH_HOST_PROF") && h->hp_n[0]) {
-        static const char* names[10] = {"push", "timers", "process", "history", "place", "drain",
-                                        "hist_copy", "hist_apply", "hist_rank", "hist_records"};
+        static const char* names[SH_HP_N] = {"push",      "timers",     "process",   "history",
+                                             "place",     "drain",      "hist_copy", "hist_apply",
+                                             "hist_rank", "hist_records", "sync_wait", "pull"};
         fprintf(stderr, "[sh host profile]");
-        for (int i = 0; i < 9; i++) fprintf(stderr, " %s %.1f ms / %lld", names[i], h->hp_ms[i], (long long)h->hp_n[i]);
-        fprintf(stderr, " %s %lld", names[9], (long long)h->hp_n[9]);
+        for (int i = 0; i < SH_HP_N; i++) {
+            if (i == 9)
+                fprintf(stderr, " %s %lld", names[i], (long long)h->hp_n[i]);
+            else
+                fprintf(stderr, " %s %.1f ms / %lld", names[i], h->hp_ms[i], (long long)h->hp_n[i]);
+        }
         fprintf(stderr, "\n");
     }
     if (h->has_device) {
@@ -1622,6 +1627,17 @@ int shx_seq3_status(sh_handle* h) { return h ? (h->s3b_last ? 2 : h->seq3_last) 
 int shx_agg_status(sh_handle* h) { return h ? h->agg_last : 0; }
 
 int shx_rules_status(sh_handle* h) { return h ? h->rs_last : 0; }
+
+// SH_HOST_PROF phase clocks of a streaming handle (ms and counts, SH_HP_N phases)
+int shx_host_profile(sh_handle* h, double* ms, int64_t* n, int cap) {
+    if (!h) return 0;
+    const int k = cap < SH_HP_N ? cap : SH_HP_N;
+    for (int i = 0; i < k; i++) {
+        if (ms) ms[i] = h->hp_ms[i];
+        if (n) n[i] = h->hp_n[i];
+    }
+    return SH_HP_N;
+}
 // 1: the compiled app has the rise-and-fall sequence shape (no device needed)
 int shx_seq3_shape(sh_handle* h) { return h && h->T && h->T->n_queries == 1 && h->T->q[0].s3 ? 1 : 0; }
 

@@ -118,6 +118,7 @@ using shh::DevBuf;
 using shh::PinBuf;
 using shh::type_width;
 
+#define SH_HP_N 12
 struct sh_handle {
     std::string err;
     bool has_device = false;
@@ -206,8 +207,11 @@ struct sh_handle {
     // in n_klist_n[0..1]) and the log of keys armed since the last pass
     DevBuf n_klist[2], n_klist_n, n_arm_log, n_arm_ctr;
     int klist_cur = 0;
-    double hp_ms[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // SH_HOST_PROF: wall time per host phase (printed by sh_destroy)
-    int64_t hp_n[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // SH_HOST_PROF: wall time per host phase (shx_host_profile; printed by sh_destroy)
+    // 0 push, 1 timers, 2 process, 3 history, 4 place, 5 drain, 6 hist_copy, 7 hist_apply,
+    // 8 hist_rank, 9 history records (count), 10 blocked in stream syncs, 11 deferred-row pulls
+    double hp_ms[SH_HP_N] = {};
+    int64_t hp_n[SH_HP_N] = {};
     int seq3_last = 0;                  // the last general-engine run took k_seq3
     bool s3_compact = false;            // ... with k_seq3s's compact records (nfd_place_s3 places them)
     bool s3_agg = false;                // ... whose aggregates ran in the kernel (no post-pass)
@@ -304,6 +308,12 @@ struct HpScope {
     }
 };
 
+// a stream sync of the streaming path (its wait counted as phase 10)
+inline hipError_t nf_sync(sh_handle* h, hipStream_t st) {
+    HpScope w_(h, 10);
+    return hipStreamSynchronize(st);
+}
+
 // ---- shared host functions (definitions in the .cpp named in the comment)
 // sh_host.cpp
 int ensure_ws(sh_handle* h, int64_t n);
@@ -343,6 +353,7 @@ int shx_bucket_status(sh_handle* h);
 int shx_seq3_status(sh_handle* h);
 int shx_agg_status(sh_handle* h);
 int shx_rules_status(sh_handle* h);
+int shx_host_profile(sh_handle* h, double* ms, int64_t* n, int cap);
 int shx_seq3_shape(sh_handle* h);
 int shx_bucket_compile(sh_handle* h, char* buf, int64_t len);
 int64_t shx_jit_source(sh_handle* h, char* buf, int64_t len);

@@ -51,7 +51,7 @@ static int nf_lst_ready(sh_handle* h) {
     return hipMemsetAsync(h->n_lst_ctr.p, 0, 8, h->stream) == hipSuccess ? 0 : SH_E_HIP;
 }
 static int nf_lst_grow(sh_handle* h) {
-    hipStreamSynchronize(h->stream);
+    nf_sync(h, h->stream);
     if (h->n_lst.ensure_fresh((size_t)h->lst_cap * 4 * 8)) return SH_E_OOM;
     h->lst_cap *= 4;
     return 0;
@@ -62,7 +62,7 @@ int nf_ensure_keys(sh_handle* h, int32_t nkeys) {
     const int32_t nk = std::max(nkeys, h->n_nkeys * 2);
     const size_t kb = (size_t)h->T->key_words * 8;
     const size_t old = (size_t)h->n_nkeys * kb, need = (size_t)nk * kb;
-    hipStreamSynchronize(h->stream);
+    nf_sync(h, h->stream);
     if (h->n_kstate.ensure(need)) return SH_E_OOM;
     hipMemsetAsync((uint8_t*)h->n_kstate.p + old, 0, need - old, h->stream);
     if (h->n_armed.ensure((size_t)nk)) return SH_E_OOM;
@@ -88,7 +88,7 @@ static int nf_sev_ready(sh_handle* h, int64_t events, bool zero = true) {
     if (!h->sm_on) return 0;
     const int64_t need = std::max<int64_t>(4096, 2 * (events + 64) * (int64_t)h->sm.used.size());
     if (need > h->sev_cap) {
-        hipStreamSynchronize(h->stream);
+        nf_sync(h, h->stream);
         if (h->n_sev.ensure_fresh((size_t)need * 16) || h->n_sev_ctr.ensure_fresh(64)) return SH_E_OOM;
         h->sev_cap = need;
     }
@@ -126,7 +126,7 @@ static int nf_rank_upload(sh_handle* h) {
             uint64_t* r = h->pin_rk.as<uint64_t>();
             for (int32_t k = 0; k < nk; k++) r[k] = M.present(k) ? M.rank(k) : ~0ull;
             hipMemcpyAsync(h->n_rank[s].p, r, (size_t)nk * 8, hipMemcpyHostToDevice, st);
-            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "rank upload");  // (rare: after a resize)
+            if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "rank upload");  // (rare: after a resize)
         } else if (!M.dirty.empty()) {
             ks.clear();
             vs.clear();
@@ -163,7 +163,7 @@ static int nf_rank_upload(sh_handle* h) {
 int nf_sev_flush(sh_handle* h) {
     if (h->sev_pend.empty()) return SH_OK;
     HpScope hp_(h, 3);
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+    if (nf_sync(h, h->stream) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
     {
         HpScope ha_(h, 7);
         for (const auto& pr : h->sev_pend)
@@ -192,7 +192,7 @@ static int nf_sev_apply(sh_handle* h, bool counted = false) {
             n = nf_ctl_nsev(h);
         } else {
             hipMemcpyAsync(h->pin_sev.p, h->n_sev_ctr.p, 8, hipMemcpyDeviceToHost, st);
-            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+            if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
             n = (int64_t)*h->pin_sev.as<unsigned long long>();
         }
         h->hp_n[9] += n;
@@ -201,7 +201,7 @@ static int nf_sev_apply(sh_handle* h, bool counted = false) {
             const size_t need = (size_t)(h->hist_used + n) * 16;
             if (need > h->pin_hist.bytes) {
                 // grow, keeping the records already copied (their copies must land first)
-                if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+                if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
                 PinBuf nb;
                 if (nb.ensure(need)) return fail(h, SH_E_OOM, "pinned staging");
                 if (h->hist_used) memcpy(nb.p, h->pin_hist.p, (size_t)h->hist_used * 16);
@@ -218,7 +218,7 @@ static int nf_sev_apply(sh_handle* h, bool counted = false) {
         }
         if (h->pin_sev.ensure((size_t)std::max<int64_t>(n, 1) * 16)) return fail(h, SH_E_OOM, "pinned staging");
         if (n) hipMemcpyAsync(h->pin_sev.p, h->n_sev.p, (size_t)n * 16, hipMemcpyDeviceToHost, st);
-        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
+        if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
     }
     HpScope hp_(h, 3);
     const uint64_t* recs = h->pin_sev.as<uint64_t>();
@@ -269,13 +269,13 @@ static int nf_grow(sh_handle* h, uint32_t err) {
         if (fresh.ensure_fresh((size_t)h->n_nkeys * h->T->key_words * 8)) return fail(h, SH_E_OOM, "state growth");
         nfd_relayout(h->d_T_old.as<nf_table>(), h->d_T.as<nf_table>(), h->n_kstate.as<uint64_t>(),
                      fresh.as<uint64_t>(), h->n_nkeys, st);
-        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "relayout");
+        if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "relayout");
         h->n_kstate.release();
         h->n_kstate = fresh;
         fresh.p = nullptr;
         fresh.bytes = 0;
     } else {
-        hipStreamSynchronize(st);
+        nf_sync(h, st);
     }
     return SH_OK;
 }
@@ -283,7 +283,7 @@ static int nf_grow(sh_handle* h, uint32_t err) {
 static int nf_ensure_recs(sh_handle* h, int64_t cap) {
     const int stride = NF_REC_HDR + std::max(1, h->n_out);
     if (cap <= h->rec_cap) return 0;
-    hipStreamSynchronize(h->stream);
+    nf_sync(h, h->stream);
     if (h->n_recs.ensure_fresh((size_t)cap * stride * 8)) return SH_E_OOM;
     h->rec_cap = cap;
     return 0;
@@ -327,10 +327,11 @@ static void nf_put_cols(sh_handle* h, const nf_cols& cols) {
 // the deferred rows into the host queue (one sync + one copy per array)
 int nf_app_pull(sh_handle* h) {
     if (h->df_ub == 0) return SH_OK;
+    HpScope hp_(h, 11);
     hipStream_t st = h->df_stream;
     unsigned long long n = 0;
     if (hipMemcpyAsync(&n, h->df_ctr.p, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
+        nf_sync(h, st) != hipSuccess)
         return fail(h, SH_E_HIP, "deferred rows");
     if ((int64_t)n > h->df_ub) return fail(h, SH_E_HIP, "deferred row count");
     const int no = std::max(1, h->n_out);
@@ -352,7 +353,7 @@ int nf_app_pull(sh_handle* h) {
             hipMemcpyAsync(pb + b_v, h->df_vals.p, (size_t)n * no * 8, hipMemcpyDeviceToHost, st);
             hipMemcpyAsync(pb + b_n, h->df_nulls.p, (size_t)n * no, hipMemcpyDeviceToHost, st);
         }
-        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "deferred rows copy");
+        if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "deferred rows copy");
         memcpy(h->o_query.data() + base, pb + b_q, n * 4);
         memcpy(h->o_seq.data() + base, pb + b_seq, n * 8);
         memcpy(h->o_ts.data() + base, pb + b_ts, n * 8);
@@ -423,7 +424,7 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
         return fail(h, SH_E_HIP, "scan");
     hipMemcpyAsync(h->pin_rd.as<void>(PR_LOFF), h->w_off.as<uint32_t>() + (n_idx - 1), 4, hipMemcpyDeviceToHost, st);
     hipMemcpyAsync(h->pin_rd.as<void>(PR_LCNT), h->w_cnt.as<uint32_t>() + (n_idx - 1), 4, hipMemcpyDeviceToHost, st);
-    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error before placement");
+    if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "device error before placement");
     const unsigned long long nrec =
         nrec_known >= 0 ? (unsigned long long)nrec_known : *h->pin_rd.as<unsigned long long>(PR_NREC);
     const uint32_t last_off = *h->pin_rd.as<uint32_t>(PR_LOFF), last_cnt = *h->pin_rd.as<uint32_t>(PR_LCNT);
@@ -452,12 +453,12 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
             nfd_place_s3(h->n_recs.as<uint64_t>(), h->rec_cap, n_idx, no, h->s3_type, h->s3_seq_base,
                          h->w_off.as<uint32_t>(), h->dev_want_query ? h->w_oq.as<int32_t>() : nullptr, d_seq, d_vals,
                          h->w_inv.as<uint32_t>(), total, st, h->s3_rw, h->s3_wide);
-            return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "placement");
+            return nf_sync(h, st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "placement");
         }
         nfd_place(h->n_recs.as<uint64_t>(), (int64_t)nrec, stride, h->w_off.as<uint32_t>(), no,
                   h->dev_want_query ? h->w_oq.as<int32_t>() : nullptr, d_seq, nullptr, d_vals, nullptr,
                   h->w_inv.as<uint32_t>(), total, st);
-        return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "placement");
+        return nf_sync(h, st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "placement");
     }
     // the rows are placed into one device block laid out like the pinned staging
     // (query | seq | ts | values | nulls) and come back in one copy, then into the host queue
@@ -477,7 +478,7 @@ static int nf_place(sh_handle* h, int64_t n_idx, int64_t* rows_out, uint64_t* d_
     if (h->pin_out.ensure(b_end)) return fail(h, SH_E_OOM, "pinned staging");
     const bool vals = h->n_out && no == h->n_out;
     hipMemcpyAsync(h->pin_out.p, ob, vals ? b_end : b_v, hipMemcpyDeviceToHost, st);
-    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "output copy");
+    if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "output copy");
     memcpy(h->o_query.data() + base, h->pin_out.as<void>(b_q), total * 4);
     memcpy(h->o_seq.data() + base, h->pin_out.as<void>(b_seq), total * 8);
     memcpy(h->o_ts.data() + base, h->pin_out.as<void>(b_ts), total * 8);
@@ -662,7 +663,7 @@ int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& c
             return fail(h, SH_E_HIP, "k_nfa_run launch failed");
         hipEventRecord(h->ev[2], st);
         nf_ctl_read(h);
-        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_run");
+        if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_run");
         const unsigned err = nf_ctl_err(h);
         if (!err) {
             h->tick++;
@@ -674,7 +675,7 @@ int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& c
             hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
             if (*n_rows >= 0) {
                 hipEventRecord(h->ev[3], st);
-                hipStreamSynchronize(st);
+                nf_sync(h, st);
                 hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
                 hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
             } else {  // deferred rows: the placement is still on the stream
@@ -695,7 +696,7 @@ int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& c
             if (nf_ensure_recs(h, h->rec_cap * 4)) return fail(h, SH_E_OOM, "emission buffer");
         }
         if (err & NF_E_SEV) {
-            hipStreamSynchronize(st);
+            nf_sync(h, st);
             if (h->n_sev.ensure_fresh((size_t)h->sev_cap * 4 * 16)) return fail(h, SH_E_OOM, "scheduler history");
             h->sev_cap *= 4;
         }
@@ -734,12 +735,12 @@ static int nf_next_due_local(sh_handle* h, int64_t* out) {
             nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, INT64_MAX,
                     h->n_cand.as<nfd_cand>(), h->n_ctr.as<unsigned long long>(), nkeys, nullptr, 0, nullptr, st);
             hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
-            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
+            if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
             const int64_t nc = (int64_t)*h->pin_rd.as<unsigned long long>(PR_NC);
             if (nc == 0) continue;
             nfd_cand_tmin(h->n_cand.as<nfd_cand>(), nc, h->n_tmin.as<unsigned long long>(), st);
             hipMemcpyAsync(h->pin_rd.as<void>(PR_TMIN), h->n_tmin.p, 8, hipMemcpyDeviceToHost, st);
-            if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_cand_tmin");
+            if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "k_cand_tmin");
             *out = std::min(*out, (int64_t)*h->pin_rd.as<unsigned long long>(PR_TMIN));
         }
     }
@@ -813,7 +814,7 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
                             h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0, rank, st);
                 }
                 hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
-                if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
+                if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
                 nc = *h->pin_rd.as<unsigned long long>(PR_NC);
             }
             if (nc == 0 && !h->coord_on) continue;
@@ -852,7 +853,7 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
                 if (h->n_tmin.ensure_fresh(8)) return fail(h, SH_E_OOM, "timer tie-break");
                 nfd_cand_tmin(h->n_cand.as<nfd_cand>(), (int64_t)nc, h->n_tmin.as<unsigned long long>(), st);
                 hipMemcpyAsync(h->pin_rd.as<void>(PR_TMIN), h->n_tmin.p, 8, hipMemcpyDeviceToHost, st);
-                if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_cand_tmin");
+                if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "k_cand_tmin");
                 const int64_t tmin = (int64_t)*h->pin_rd.as<unsigned long long>(PR_TMIN);
                 const int64_t range = now - tmin + 1;
                 if (tmin >= 0 && range > 0 && range <= kTieBreakSlots) {
@@ -862,7 +863,7 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
                     nfd_cand_select(h->n_cand.as<nfd_cand>(), (int64_t)nc, tmin, range,
                                     h->n_slot_s.as<unsigned long long>(), h->n_slot_k.as<int32_t>(), st);
                     hipMemcpyAsync(h->pin_out.p, h->n_slot_k.p, (size_t)range * 4, hipMemcpyDeviceToHost, st);
-                    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "k_cand_select");
+                    if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "k_cand_select");
                     const int32_t* sk = h->pin_out.as<int32_t>();
                     for (int64_t r = 0; r < range; r++)
                         if (sk[r] >= 0) sel.push_back(sk[r]);
@@ -925,7 +926,7 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
                           h->n_sel.as<int32_t>(), ns, now, h->tick, h->clock, h->seq_next, &em, st,
                           h->coord_on ? h->n_gpos.as<uint32_t>() : nullptr);
                 nf_ctl_read(h);
-                if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_timer");
+                if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_timer");
                 unsigned err = nf_ctl_err(h);
                 if (!err) {
                     counted = true;
@@ -936,7 +937,7 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
                               h->n_save.as<uint64_t>(), 1, st);
                 if (err & NF_E_EMIT && nf_ensure_recs(h, h->rec_cap * 4)) return fail(h, SH_E_OOM, "emission");
                 if (err & NF_E_SEV) {
-                    hipStreamSynchronize(st);
+                    nf_sync(h, st);
                     if (h->n_sev.ensure_fresh((size_t)h->sev_cap * 4 * 16)) return fail(h, SH_E_OOM, "history");
                     h->sev_cap *= 4;
                     err &= ~(unsigned)NF_E_SEV;
@@ -978,7 +979,7 @@ int nf_start(sh_handle* h) {
               h->stream);
     unsigned err = 0;
     hipMemcpyAsync(&err, h->n_err.p, 4, hipMemcpyDeviceToHost, h->stream);
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_start");
+    if (nf_sync(h, h->stream) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_start");
     h->tick++;
     return err ? fail(h, SH_E_STATE_OVERFLOW, "start state overflow") : SH_OK;
 }

@@ -51,8 +51,19 @@ class TorchGroupComm:
         self.dist, self.group = dist, group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.seconds = 0.0   # wall time inside all_gather (the coordination cost)
+        self.calls = 0
 
     def all_gather(self, arr):
+        import time
+        t0 = time.perf_counter()
+        try:
+            return self._all_gather(arr)
+        finally:
+            self.seconds += time.perf_counter() - t0
+            self.calls += 1
+
+    def _all_gather(self, arr):
         import torch
         arr = np.ascontiguousarray(arr, dtype=np.int64)
         n = torch.tensor([arr.size], dtype=torch.int64)
