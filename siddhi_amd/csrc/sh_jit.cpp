@@ -68,6 +68,17 @@ const int kWalkDyn = env_int("SH_BK_DYN", 1, 0, 1);
 // the bucketed matcher's launch bound: minimum workgroups per CU the register
 // allocation is sized for (its LDS holds two 512-thread workgroups per CU)
 const int kMatchMinBlocks = env_int("SH_BK_MINB", 4, 1, 8);
+// a matcher pass's LDS span and consumer limit (events; multiples of its 512
+// threads, at most SHB_SPAN / SHB_CH): smaller passes take less LDS, so more
+// workgroups share a CU, at the price of more halo events per consumer
+const int kSpan = [] {
+    const int v = env_int("SH_BK_SPAN", SHB_SPAN, 1024, SHB_SPAN);
+    return v % 512 ? SHB_SPAN : v;
+}();
+const int kChunk = [] {
+    const int v = env_int("SH_BK_CH", SHB_CH, 512, SHB_CH);
+    return (v % 512 || v > kSpan) ? (kSpan < SHB_CH ? kSpan : SHB_CH) : v;
+}();
 
 int type_width_of(int t) { return t == SH_T_LONG || t == SH_T_DOUBLE ? 8 : (t == SH_T_BOOL ? 1 : 4); }
 
@@ -1016,18 +1027,19 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
            "\n#define SHB_MOVF 0x8000u\n#define SHB_MSTEPS 15\n"
            "#define SHB_MINB " + std::to_string(kMatchMinBlocks) + "\n"
            "#define SHB_NSEG (SHB_CT_MAX + SHB_HMAX)\n"
-           "#define SHB_NR (SHB_SPAN / SHB_TPB)\nstatic_assert(SHB_SPAN % SHB_TPB == 0 && SHB_NR * SHB_TPB == SHB_SPAN, \"span\");\n"
+           "#define SHB_SPANJ " + std::to_string(kSpan) + "\n#define SHB_CHJ " + std::to_string(kChunk) + "\n"
+           "#define SHB_NR (SHB_SPANJ / SHB_TPB)\nstatic_assert(SHB_SPANJ % SHB_TPB == 0 && SHB_NR * SHB_TPB == SHB_SPANJ && SHB_SPANJ <= SHB_SPAN && SHB_CHJ <= SHB_CH && SHB_CHJ % SHB_TPB == 0, \"span\");\n"
            "static_assert(SHB_NSEG < 256 && SHB_NSEG < SHB_TPB, \"segments\");\n";
     src += R"(
 extern "C" __global__ void __launch_bounds__(SHB_TPB, SHB_MINB) shb_match(shb_plan P) {
-__shared__ uint32_t s_ws[SHB_SPAN];
+__shared__ uint32_t s_ws[SHB_SPANJ];
 // the chunk's consumers in sorted order: sorted position | (arrival - hl) << 16
-__shared__ uint32_t s_cons[SHB_CH];
-__shared__ uint16_t s_pre[SHB_CH];
+__shared__ uint32_t s_cons[SHB_CHJ];
+__shared__ uint16_t s_pre[SHB_CHJ];
 __shared__ uint32_t u_buf[(SHB_TPB / 64) * 256];  // rank phase: per-wave key counts; then the u16 consumed masks
 uint32_t (*const wcnt)[256] = (uint32_t(*)[256])u_buf;
 uint16_t* const s_msk = (uint16_t*)u_buf;
-static_assert((SHB_TPB / 64) * 256 * 4 >= SHB_CH * 2, "masks fit u_buf");
+static_assert((SHB_TPB / 64) * 256 * 4 >= SHB_CHJ * 2, "masks fit u_buf");
 // run: halo events per local key, then their inclusive prefix over the keys
 __shared__ uint32_t run[256], tstart[256], ws[SHB_TPB / 64];
 // the pass's segments, one per tile from the first halo tile: start in span
@@ -1035,11 +1047,11 @@ __shared__ uint32_t run[256], tstart[256], ws[SHB_TPB / 64];
 // global index of the first event; seg_of[j]: segment of span event 32 j
 __shared__ uint32_t seg_p[SHB_NSEG + 1];
 __shared__ uint32_t seg_g[SHB_NSEG];
-__shared__ uint8_t seg_of[SHB_SPAN / 32];
+__shared__ uint8_t seg_of[SHB_SPANJ / 32];
 __shared__ int s_i[2];
 )";
     for (int a : staged_out)
-        src += "__shared__ " + std::string(col_ctype(P.attr_type[0][a])) + " " + lds(a) + "[SHB_SPAN];\n";
+        src += "__shared__ " + std::string(col_ctype(P.attr_type[0][a])) + " " + lds(a) + "[SHB_SPANJ];\n";
     for (size_t k = 0; k < staged_out.size(); k++) {
         const int a = staged_out[k];
         const std::string ct = col_ctype(P.attr_type[0][a]);
@@ -1084,15 +1096,15 @@ const int nseg = E - h0;
     if (Tm == E) seg_p[nseg] = tot;
 }
 __syncthreads();
-// this pass: consumers from tiles [a, a + ne), at most SHB_CH events; the halo
+// this pass: consumers from tiles [a, a + ne), at most SHB_CHJ events; the halo
 // from segment sb on (trimmed at the front when it and tile a overflow the span)
 const int ta = a - h0;
 const uint32_t pa = seg_p[ta];
-const int sb = __syncthreads_count((int)threadIdx.x < ta && seg_p[ta + 1] - seg_p[threadIdx.x] > SHB_SPAN);
+const int sb = __syncthreads_count((int)threadIdx.x < ta && seg_p[ta + 1] - seg_p[threadIdx.x] > SHB_SPANJ);
 const uint32_t sbase = seg_p[sb];
 const int ne = __syncthreads_count((int)threadIdx.x >= ta && (int)threadIdx.x < nseg &&
-                                   seg_p[threadIdx.x + 1] - pa <= SHB_CH &&
-                                   seg_p[threadIdx.x + 1] - sbase <= SHB_SPAN);
+                                   seg_p[threadIdx.x + 1] - pa <= SHB_CHJ &&
+                                   seg_p[threadIdx.x + 1] - sbase <= SHB_SPANJ);
 if (ne == 0) {
     // tile a's segment alone exceeds a chunk
     if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_SPAN);
@@ -1231,17 +1243,17 @@ SHB_PROF(2)
 // (arrival order inside the bucket)
 uint32_t total;
 {
-    const int p0 = (int)threadIdx.x * (SHB_CH / SHB_TPB);
-    uint32_t v[SHB_CH / SHB_TPB];
+    const int p0 = (int)threadIdx.x * (SHB_CHJ / SHB_TPB);
+    uint32_t v[SHB_CHJ / SHB_TPB];
     uint32_t sum = 0;
 #pragma unroll
-    for (int q = 0; q < SHB_CH / SHB_TPB; q++) {
+    for (int q = 0; q < SHB_CHJ / SHB_TPB; q++) {
         v[q] = (p0 + q < nc) ? (uint32_t)s_pre[p0 + q] : 0u;
         sum += v[q];
     }
     uint32_t off = shw_block_excl<SHB_TPB>(sum, ws, &total);
 #pragma unroll
-    for (int q = 0; q < SHB_CH / SHB_TPB; q++) {
+    for (int q = 0; q < SHB_CHJ / SHB_TPB; q++) {
         if (p0 + q < nc) {
             uint32_t gi;
             SHB_GIDX(hl + p0 + q, gi)
@@ -1252,7 +1264,7 @@ uint32_t total;
     }
 }
 // the pass's match-stream region: the workgroup's own for its first pass (a
-// pass takes at most SHB_SPAN), taken from the shared tail for any further one
+// pass takes at most SHB_SPANJ), taken from the shared tail for any further one
 if (a != A && threadIdx.x == 0) s_i[1] = total ? (int)atomicAdd(P.ms_ctr, total) : 0;
 __syncthreads();
 const int64_t rbase = a == A ? (int64_t)blockIdx.x * SHB_SPAN

@@ -65,7 +65,7 @@ def test_c2_bucket_matcher_compiles(lib):
     rc = lib.shx_bucket_compile(h, buf, 1 << 20)
     src = buf.value.decode()
     assert rc == abi.SH_OK, (lib.sh_last_error(h), src[-3000:])
-    assert "s_a1[SHB_SPAN]" in src and "s_a0[" not in src and "s_a2[" not in src
+    assert "s_a1[SHB_SPANJ]" in src and "s_a0[" not in src and "s_a2[" not in src
     assert "P.ms[0])[dst] = s_a1[o]" in src
     lib.sh_destroy(h)
 
