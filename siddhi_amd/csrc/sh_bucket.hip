@@ -661,8 +661,7 @@ __global__ void __launch_bounds__(S3B_TPB) k_s3b(shb_plan P, shb_s3 S) {
         uint32_t len = 0u, g = 0u;
         if ((int)threadIdx.x < nseg) {
             const int T = a + (int)threadIdx.x;
-            const uint16_t* r = P.toff + (int64_t)T * SHB_TOFF + b;
-            const uint32_t lo = r[0], hi = r[1];
+            const uint32_t lo = P.tofft[(int64_t)b * P.tstride + T], hi = P.tofft[(int64_t)(b + 1) * P.tstride + T];
             len = hi - lo;
             g = ((uint32_t)T << SHB_TILE_SHIFT) + lo;
         }
@@ -874,8 +873,7 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggc(shb_plan P, shb_aggc A) {
         uint32_t len = 0u, g = 0u;
         if ((int)threadIdx.x < nseg) {
             const int T = a + (int)threadIdx.x;
-            const uint16_t* r = P.toff + (int64_t)T * SHB_TOFF + b;
-            const uint32_t lo = r[0], hi = r[1];
+            const uint32_t lo = P.tofft[(int64_t)b * P.tstride + T], hi = P.tofft[(int64_t)(b + 1) * P.tstride + T];
             len = hi - lo;
             g = ((uint32_t)T << SHB_TILE_SHIFT) + lo;
         }
@@ -1014,6 +1012,25 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggc(shb_plan P, shb_aggc A) {
 // ---------------------------------------------------------------- launches
 static int bk_ok() { return hipGetLastError() == hipSuccess ? 0 : -3; }
 
+// the tiles' bucket starts transposed (bucket-major): a matcher workgroup reads its
+// bucket's starts over ~180 tiles as one contiguous run instead of one cache line
+// per tile (64 tiles per workgroup, staged in LDS)
+#define TT_T 64
+__global__ void __launch_bounds__(256) k_bk_toff_t(const uint16_t* __restrict__ toff, int nt,
+                                                   uint16_t* __restrict__ tofft, int stride) {
+    __shared__ uint16_t s[TT_T][SHB_NB + 2];
+    const int T0 = (int)blockIdx.x * TT_T;
+    for (int i = threadIdx.x; i < TT_T * (SHB_NB + 1); i += 256) {
+        const int t = i / (SHB_NB + 1), b = i - t * (SHB_NB + 1);
+        s[t][b] = T0 + t < nt ? toff[(int64_t)(T0 + t) * SHB_TOFF + b] : (uint16_t)0;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (SHB_NB + 1) * TT_T; i += 256) {
+        const int b = i / TT_T, t = i - b * TT_T;
+        if (T0 + t < nt) tofft[(int64_t)b * stride + T0 + t] = s[t][b];
+    }
+}
+
 extern "C" int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_plan* P, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     // SH_BK_SCAT=1: no occupancy bound on the scatter (more registers, one
@@ -1024,6 +1041,9 @@ extern "C" int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nke
     else
         hipLaunchKernelGGL(k_bk_scatter<4>, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, nkeys, *P);
     if (bk_ok()) return -3;
+    if (P->tstride < P->nt) return -1;
+    hipLaunchKernelGGL(k_bk_toff_t, dim3((P->nt + TT_T - 1) / TT_T), dim3(256), 0, st, (const uint16_t*)P->toff, P->nt,
+                       P->tofft, P->tstride);
     if (!P->no_ts) {
         hipLaunchKernelGGL(k_bk_halo, dim3((P->nt + 255) / 256), dim3(256), 0, st, P->tfirst, P->hstart, P->nt,
                            P->within);

@@ -123,6 +123,9 @@ struct shb_plan {
     uint32_t* w0;             // tiles' bucket order: packed ts | local key
     uint16_t* sp;             // arrival order: the event's slot in its tile's bucket order
     uint16_t* toff;           // [nt][SHB_TOFF]: bucket starts in the tile's bucket order ([256]: valid events)
+    uint16_t* tofft;          // the same transposed, [SHB_NB + 1][tstride]: a bucket's starts over the tiles
+    int32_t tstride;          // (contiguous for the matchers, which read one bucket over many tiles)
+    int32_t pad_t;
     uint8_t* cnt;             // tiles' bucket order: partials consumed per event
     uint32_t* mstart;         // [nt][SHB_NB]: match-stream position of each (tile, bucket) segment's first match
     uint32_t* ttot;           // [nt + 1]: matches per arrival tile -> exclusive scan

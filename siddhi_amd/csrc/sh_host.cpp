@@ -769,6 +769,7 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
 
 void sh_destroy(sh_handle* h) {
     if (!h) return;
+    nf_hist_stop(h);
     if (getenv("SH_HOST_PROF") && h->hp_n[0]) {
         static const char* names[SH_HP_N] = {"push",      "timers",     "process",   "history",
                                              "place",     "drain",      "hist_copy", "hist_apply",
@@ -789,6 +790,9 @@ void sh_destroy(sh_handle* h) {
         h->pin_rd.release();
         h->pin_out.release();
         h->pin_hist.release();
+        h->pin_sev.release();
+        h->pin_rk.release();
+        h->pin_cand.release();
         h->n_tmin.release();
         h->n_armed.release();
         h->n_klist[0].release();
@@ -926,6 +930,10 @@ int sh_set_coordinator(sh_handle* h, const sh_coordinator* c) {
 
 int sh_set_partition_keys(sh_handle* h, int32_t first_key, int32_t n, const uint16_t* utf16, const int64_t* offsets) {
     if (!h || first_key < 0 || n < 0 || (n && (!utf16 || !offsets))) return SH_E_INVALID_ARG;
+    if (h->mode == 1) {
+        const int frc = nf_sev_flush(h);  // (the replay thread reads the key strings)
+        if (frc) return frc;
+    }
     h->sm.set_keys(first_key, n, utf16, offsets);
     return SH_OK;
 }
@@ -1440,10 +1448,17 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
         return arc;
     };
     if (h->prog.window_ok) {
-        const int brc = run_bucket(h, run, nkeys);
+        int brc = run_bucket(h, run, nkeys);
         if (brc == SH_OK && aggp && !h->bk_agg_carried) {
             const int arc = finish_agg(nkeys);
             if (arc <= 0) return arc;
+            if (!getenv("SH_BK_AGG_POST")) {
+                // the post-pass's additions are not exact in parallel: the bucketed
+                // engine again, its carry adding in the reference's sequence
+                brc = run_bucket(h, run, nkeys, true);
+                if (brc == SH_OK && h->bk_agg_carried) return SH_OK;
+                if (brc != SH_OK && brc != 1) return brc;
+            }
         } else if (brc != 1) {
             return brc;
         }

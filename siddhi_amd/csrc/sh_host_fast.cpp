@@ -375,7 +375,7 @@ int run_rules(sh_handle* h, sh_device_run* run) {
 // consumer-side form and a null-free projection; 0 ok, 1 = not applicable or a
 // premise failed on the device (the caller runs the general window path),
 // SH_E_MORE = output capacity too small (out_count = matches), <0 error
-int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
+int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry) {
     static const bool off = getenv("SH_DISABLE_BUCKET") != nullptr;
     h->bk_last = 0;
     const shp_program& P = h->prog;
@@ -465,7 +465,10 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     shb_aggc AG;
     memset(&AG, 0, sizeof(AG));
     AG.e1_col = AG.e2_col[0] = AG.e2_col[1] = -1;
-    bool carry = P.agg_post && !getenv("SH_BK_AGG_POST");
+    // (k_bk_aggc walks every key of a bucket in one workgroup: C2's 40 keys per bucket
+    // leave most lanes idle -- 28 ms against the post-pass's 8.7 -- so it runs when the
+    // post-pass refuses (its double additions are not exact in parallel) or SH_BK_AGGC=1)
+    bool carry = P.agg_post && !getenv("SH_BK_AGG_POST") && (force_carry || getenv("SH_BK_AGGC"));
     int agg_of[SHB_MAX_OUT];
     for (int o = 0; o < P.n_out; o++) agg_of[o] = -1;
     for (int o = 0; o < P.n_out && carry; o++) {
@@ -555,6 +558,9 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     B.w0 = h->bk_w0.as<uint32_t>();
     B.sp = h->bk_sp.as<uint16_t>();
     B.toff = h->bk_toff.as<uint16_t>();
+    B.tstride = (B.nt + 63) & ~63;
+    if (h->bk_tofft.ensure_fresh((int64_t)(SHB_NB + 1) * B.tstride * 2)) return fail(h, SH_E_OOM, "bucket workspace");
+    B.tofft = h->bk_tofft.as<uint16_t>();
     B.cnt = h->bk_cnt.as<uint8_t>();
     B.mstart = h->bk_mstart.as<uint32_t>();
     B.tpre = h->bk_tpre.as<int64_t>();
@@ -701,6 +707,9 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     B.w0 = h->bk_w0.as<uint32_t>();
     B.sp = h->bk_sp.as<uint16_t>();
     B.toff = h->bk_toff.as<uint16_t>();
+    B.tstride = (B.nt + 63) & ~63;
+    if (h->bk_tofft.ensure_fresh((int64_t)(SHB_NB + 1) * B.tstride * 2)) return fail(h, SH_E_OOM, "bucket workspace");
+    B.tofft = h->bk_tofft.as<uint16_t>();
     B.cnt = h->bk_cnt.as<uint8_t>();
     B.mstart = h->bk_mstart.as<uint32_t>();
     B.tpre = h->bk_tpre.as<int64_t>();

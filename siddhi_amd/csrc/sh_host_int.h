@@ -9,11 +9,15 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/siddhi_hip.h"
@@ -237,8 +241,23 @@ struct sh_handle {
     // them, in launch order, before the next use of the ranks)
     PinBuf pin_hist;
     int64_t hist_used = 0;                        // records in pin_hist
-    std::vector<std::pair<int64_t, int64_t>> sev_pend;  // (first record, records) per launch
-    PinBuf pin_sev, pin_rk;
+    // the replay runs on a host thread (hw_*): a launch's records are queued with
+    // an event recorded behind their copy; the thread waits for it and applies the
+    // launches in order while this thread goes on (stages and launches the next
+    // call); every use of the models joins it first (nf_sev_flush)
+    struct HistJob {
+        int64_t first, n;
+        hipEvent_t ev;
+    };
+    std::thread hw_thread;
+    std::mutex hw_mu;
+    std::condition_variable hw_cv, hw_idle;
+    std::deque<HistJob> hw_q;
+    bool hw_busy = false, hw_stop = false, hw_fail = false;
+    hipEvent_t hw_ev[16] = {};
+    int hw_ev_next = 0;
+    double hw_ms = 0.0;  // the thread's replay time (phase 7 when profiled)
+    PinBuf pin_sev, pin_rk, pin_cand;
     int64_t sev_cap = 0;
     int caps[6] = {16, 32, 64, 32, 8, 4};  // list, se, node, hold, sched, group
     int32_t n_nkeys = 0;          // key blocks allocated
@@ -277,7 +296,7 @@ struct sh_handle {
     int s3b_last = 0;         // 1: ... on the sequence bucket-carry engine (k_s3b)
     shj_bucket bk{};
     std::string bk_err;
-    DevBuf bk_w0, bk_sp, bk_toff, bk_cnt, bk_mstart, bk_tpre, bk_tfirst, bk_hstart, bk_ttot, bk_flag, bk_prof;
+    DevBuf bk_w0, bk_sp, bk_toff, bk_tofft, bk_cnt, bk_mstart, bk_tpre, bk_tfirst, bk_hstart, bk_ttot, bk_flag, bk_prof;
     DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS], bk_agg[SHB_MAX_AGG];
     bool bk_agg_carried = false;  // the last bucketed run carried its aggregates (k_bk_aggc)
     PinBuf bk_rd;
@@ -307,6 +326,9 @@ struct HpScope {
         h->hp_n[i]++;
     }
 };
+
+// the scheduler-history replay thread: stop it (sh_destroy)
+void nf_hist_stop(sh_handle* h);
 
 // a stream sync of the streaming path (its wait counted as phase 10)
 inline hipError_t nf_sync(sh_handle* h, hipStream_t st) {
@@ -339,7 +361,7 @@ int bits_for(uint64_t v);
 int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid, int* alias,
                 bool used_only = false, bool with_ts = true);
 int rows_for_cols(sh_handle* h, sh_device_run* run);
-int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys);
+int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry = false);
 int run_rules(sh_handle* h, sh_device_run* run);
 int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys);
 shd_segment_ws seg_ws(sh_handle* h, int64_t n);

@@ -157,21 +157,94 @@ static int nf_rank_upload(sh_handle* h) {
     return SH_OK;
 }
 
-// replay the deferred launches' history (in launch order: a timer launch's
-// removals follow its own getState calls, so each launch is one apply) and
-// upload the changed ranks; before every use of the ranks or the models
-int nf_sev_flush(sh_handle* h) {
-    if (h->sev_pend.empty()) return SH_OK;
-    HpScope hp_(h, 3);
-    if (nf_sync(h, h->stream) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
-    {
-        HpScope ha_(h, 7);
-        for (const auto& pr : h->sev_pend)
-            if (!h->sm.apply(h->pin_hist.as<uint64_t>((size_t)pr.first * 16), (size_t)pr.second))
-                return fail(h, SH_E_UNSUPPORTED, "more than 2^26 scheduler map bins (keys waiting on one absent state)");
+// the replay thread: applies queued launches in order, each after its copy's event
+static void hw_loop(sh_handle* h) {
+    for (;;) {
+        sh_handle::HistJob j;
+        {
+            std::unique_lock<std::mutex> lk(h->hw_mu);
+            h->hw_cv.wait(lk, [h] { return h->hw_stop || !h->hw_q.empty(); });
+            if (h->hw_q.empty()) return;  // (stop)
+            j = h->hw_q.front();
+            h->hw_busy = true;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        bool ok = hipEventSynchronize(j.ev) == hipSuccess;
+        ok = ok && h->sm.apply(h->pin_hist.as<uint64_t>((size_t)j.first * 16), (size_t)j.n);
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        {
+            std::lock_guard<std::mutex> lk(h->hw_mu);
+            h->hw_q.pop_front();
+            h->hw_busy = false;
+            h->hw_ms += ms;
+            if (!ok) h->hw_fail = true;
+        }
+        h->hw_idle.notify_all();
     }
-    h->sev_pend.clear();
+}
+
+// queue a launch's records [first, first + n) of pin_hist (their copy is on h->stream)
+static int hw_submit(sh_handle* h, int64_t first, int64_t n) {
+    if (!h->hw_thread.joinable()) {
+        for (auto& e : h->hw_ev)
+            if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+                return fail(h, SH_E_HIP, "history events");
+        h->hw_stop = false;
+        h->hw_thread = std::thread(hw_loop, h);
+    }
+    {
+        std::unique_lock<std::mutex> lk(h->hw_mu);
+        // (an event is reused only after its job is done: at most 15 queued)
+        h->hw_idle.wait(lk, [h] { return h->hw_q.size() < 15; });
+    }
+    hipEvent_t ev = h->hw_ev[h->hw_ev_next];
+    h->hw_ev_next = (h->hw_ev_next + 1) % 16;
+    if (hipEventRecord(ev, h->stream) != hipSuccess) return fail(h, SH_E_HIP, "history event");
+    {
+        std::lock_guard<std::mutex> lk(h->hw_mu);
+        h->hw_q.push_back({first, n, ev});
+    }
+    h->hw_cv.notify_one();
+    return SH_OK;
+}
+
+void nf_hist_stop(sh_handle* h) {
+    if (!h->hw_thread.joinable()) return;
+    {
+        std::lock_guard<std::mutex> lk(h->hw_mu);
+        h->hw_stop = true;
+    }
+    h->hw_cv.notify_all();
+    h->hw_thread.join();
+    for (auto& e : h->hw_ev)
+        if (e) {
+            hipEventDestroy(e);
+            e = nullptr;
+        }
+}
+
+// wait for the replay thread to apply every queued launch; before every use of
+// the models (a due pick, a rank upload, a snapshot, new key strings)
+int nf_sev_flush(sh_handle* h) {
+    if (!h->hw_thread.joinable()) return SH_OK;
+    HpScope hp_(h, 3);
+    bool bad;
+    {
+        std::unique_lock<std::mutex> lk(h->hw_mu);
+        h->hw_idle.wait(lk, [h] { return h->hw_q.empty() && !h->hw_busy; });
+        bad = h->hw_fail;
+        h->hw_fail = false;
+        h->hp_ms[7] = h->hw_ms;
+    }
     h->hist_used = 0;
+    if (bad) return fail(h, SH_E_UNSUPPORTED, "more than 2^26 scheduler map bins (keys waiting on one absent state)");
+    return SH_OK;
+}
+
+// the models' ranks on the device (the device pick of a large due backlog)
+static int nf_rank_sync(sh_handle* h) {
+    int rc = nf_sev_flush(h);
+    if (rc) return rc;
     HpScope hr_(h, 8);
     return nf_rank_upload(h);
 }
@@ -198,21 +271,16 @@ static int nf_sev_apply(sh_handle* h, bool counted = false) {
         h->hp_n[9] += n;
         if (!h->coord_on) {
             if (n == 0) return SH_OK;
-            const size_t need = (size_t)(h->hist_used + n) * 16;
-            if (need > h->pin_hist.bytes) {
-                // grow, keeping the records already copied (their copies must land first)
-                if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "scheduler history");
-                PinBuf nb;
-                if (nb.ensure(need)) return fail(h, SH_E_OOM, "pinned staging");
-                if (h->hist_used) memcpy(nb.p, h->pin_hist.p, (size_t)h->hist_used * 16);
-                h->pin_hist.release();
-                h->pin_hist = nb;
-                nb.p = nullptr;
-                nb.bytes = 0;
+            if ((size_t)(h->hist_used + n) * 16 > h->pin_hist.bytes) {
+                // grow: once the thread has applied the queued launches, the buffer restarts
+                int frc = nf_sev_flush(h);
+                if (frc) return frc;
+                if (h->pin_hist.ensure((size_t)n * 16)) return fail(h, SH_E_OOM, "pinned staging");
             }
             hipMemcpyAsync(h->pin_hist.as<uint8_t>((size_t)h->hist_used * 16), h->n_sev.p, (size_t)n * 16,
                            hipMemcpyDeviceToHost, st);
-            h->sev_pend.emplace_back(h->hist_used, n);
+            int qrc = hw_submit(h, h->hist_used, n);
+            if (qrc) return qrc;
             h->hist_used += n;
             return SH_OK;
         }
@@ -311,6 +379,8 @@ static const int64_t kDeviceTieBreak = [] {
     return e ? (int64_t)atoll(e) : (int64_t)4096;
 }();
 static const int64_t kTieBreakSlots = (int64_t)1 << 22;
+// due candidates copied back with their count (a larger backlog takes a second copy)
+static const int64_t kCandSpec = 2048;
 static int pin_rd_ready(sh_handle* h) { return h->pin_rd.ensure(PR_COLS + sizeof(nf_cols)); }
 
 // upload the nf_cols image through pinned memory (the caller synchronises the
@@ -777,8 +847,13 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
         // Scheduler creation order (the TimestampGenerator's listener order)
         for (int si = 0; si < h->T->q[q].n_sched; si++) {
             const int p = h->T->q[q].sched_seq[si];
-            {
-                const int frc = nf_sev_flush(h);  // the ranks the due pass reads
+            // single process: the due pass runs while the replay thread applies the
+            // last launches' history; the candidates' stamps (the scheduler map's
+            // order) come from the models once it is done (host_stamps). Key-sharded:
+            // the ranks are current on the device (applied at each exchange)
+            const bool host_stamps = h->sm_on && !h->coord_on;
+            if (!host_stamps) {
+                const int frc = nf_sev_flush(h);
                 if (frc) return frc;
             }
             const int32_t nkeys = h->n_nkeys;
@@ -787,7 +862,8 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
                 // due keys
                 if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");
                 hipMemsetAsync(h->n_ctr.p, 0, 8, st);
-                const uint64_t* rank = h->sm_on ? h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>() : nullptr;
+                const uint64_t* rank =
+                    h->sm_on && !host_stamps ? h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>() : nullptr;
                 if (armed_flags(h) && h->n_arm_log.p) {
                     // the armed-key list (+ the keys armed since the last pass on the
                     // first scheduler's pass, which also rebuilds the list)
@@ -814,6 +890,10 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
                             h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0, rank, st);
                 }
                 hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
+                // the first candidates come back with the count (most passes need no second copy)
+                if (h->pin_cand.ensure((size_t)kCandSpec * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "pinned staging");
+                hipMemcpyAsync(h->pin_cand.p, h->n_cand.p, (size_t)std::min<int64_t>(nkeys, kCandSpec) * sizeof(nfd_cand),
+                               hipMemcpyDeviceToHost, st);
                 if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
                 nc = *h->pin_rd.as<unsigned long long>(PR_NC);
             }
@@ -850,6 +930,12 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
             }
             if (!picked && (int64_t)nc >= kDeviceTieBreak && !wall) {
                 // large backlog of due keys: pick on the device (slot per due time)
+                if (host_stamps) {
+                    const int rrc = nf_rank_sync(h);
+                    if (rrc) return rrc;
+                    nfd_cand_restamp(h->n_cand.as<nfd_cand>(), (int64_t)nc, h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>(),
+                                     st);
+                }
                 if (h->n_tmin.ensure_fresh(8)) return fail(h, SH_E_OOM, "timer tie-break");
                 nfd_cand_tmin(h->n_cand.as<nfd_cand>(), (int64_t)nc, h->n_tmin.as<unsigned long long>(), st);
                 hipMemcpyAsync(h->pin_rd.as<void>(PR_TMIN), h->n_tmin.p, 8, hipMemcpyDeviceToHost, st);
@@ -872,7 +958,16 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
             }
             if (!picked) {
                 std::vector<nfd_cand> cs(nc);
-                hipMemcpy(cs.data(), h->n_cand.p, nc * sizeof(nfd_cand), hipMemcpyDeviceToHost);
+                if ((int64_t)nc <= kCandSpec)
+                    memcpy(cs.data(), h->pin_cand.p, nc * sizeof(nfd_cand));
+                else
+                    hipMemcpy(cs.data(), h->n_cand.p, nc * sizeof(nfd_cand), hipMemcpyDeviceToHost);
+                if (host_stamps) {
+                    const int frc = nf_sev_flush(h);
+                    if (frc) return frc;
+                    const ShJMap& M = h->sm.maps[q * NF_MAX_PROC + p];
+                    for (auto& c : cs) c.stamp = M.present(c.key) ? M.rank(c.key) : ~0ull;
+                }
                 std::sort(cs.begin(), cs.end(), [](const nfd_cand& a, const nfd_cand& b) {
                     if (a.t != b.t) return a.t < b.t;
                     return a.stamp < b.stamp;

@@ -1077,8 +1077,7 @@ if (threadIdx.x == 0) s_i[0] = P.hstart[a];
 const int Tm = a - SHB_HMAX + (int)threadIdx.x;
 uint32_t len = 0u, g = 0u;
 if (Tm >= 0 && Tm < E) {
-    const uint16_t* r = P.toff + (int64_t)Tm * SHB_TOFF + b;
-    const uint32_t lo = r[0], hi = r[1];
+    const uint32_t lo = P.tofft[(int64_t)b * P.tstride + Tm], hi = P.tofft[(int64_t)(b + 1) * P.tstride + Tm];
     len = hi - lo;
     g = ((uint32_t)Tm << SHB_TILE_SHIFT) + lo;
 }

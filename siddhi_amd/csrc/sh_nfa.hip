@@ -890,6 +890,18 @@ extern "C" int nfd_due_list(const nf_table* dT, int q, int p, const uint64_t* ks
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// the candidates' stamps from the scheduler map's ranks (host-modelled order)
+__global__ void k_cand_restamp(nfd_cand* __restrict__ cand, int64_t nc, const uint64_t* __restrict__ rank) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nc) cand[i].stamp = rank[cand[i].key];
+}
+
+extern "C" int nfd_cand_restamp(nfd_cand* cand, int64_t nc, const uint64_t* rank, void* stream) {
+    if (nc <= 0) return 0;
+    hipLaunchKernelGGL(k_cand_restamp, dim3(nf_blocks(nc, 256)), dim3(256), 0, (hipStream_t)stream, cand, nc, rank);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 extern "C" int nfd_cand_tmin(const nfd_cand* cand, int64_t nc, unsigned long long* tmin, void* stream) {
     if (nc <= 0) return 0;
     hipMemsetAsync(tmin, 0xFF, 8, (hipStream_t)stream);

@@ -76,6 +76,8 @@ int nfd_due_list(const nf_table* dT, int q, int p, const uint64_t* kstate, const
 int nfd_rank_scatter(const int32_t* keys, const uint64_t* ranks, int64_t n, uint64_t* dst, void* stream);
 // device tie-break of a due-key backlog: tmin of the candidates, then per due
 // time t (slot t - tmin of `range`) the key with the earliest stamp (-1: none)
+// cand[i].stamp = rank[cand[i].key]
+int nfd_cand_restamp(nfd_cand* cand, int64_t nc, const uint64_t* rank, void* stream);
 int nfd_cand_tmin(const nfd_cand* cand, int64_t nc, unsigned long long* tmin, void* stream);
 int nfd_cand_select(const nfd_cand* cand, int64_t nc, int64_t tmin, int64_t range, unsigned long long* slot_stamp,
                     int32_t* slot_key, void* stream);
