@@ -31,7 +31,7 @@ prof)
 pmc)
     ctr=$1; shift
     export TMPDIR=/tmp
-    timeout -s KILL 300 rocprofv3 --pmc $ctr -d gpurun_out/$name -o run -- python3 -u bench.py "$@" \
+    timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/$name -o run -- python3 -u bench.py "$@" \
         > gpurun_out/$name.out 2> gpurun_out/$name.err || { tail -30 gpurun_out/$name.err; exit 1; }
     echo "pmc $name $ctr done"
     ;;
