@@ -202,7 +202,8 @@ static int rules_finish(sh_handle* h, sh_device_run* run, int64_t m, int32_t nke
 
 // partitioned rule sets whose start filters open few partials: no key segment
 // (sh_rules.hip, "sparse partials"); 1 = not taken (decreasing timestamps, keys
-// out of range, more partials than n / 8): the caller runs the key-segment path.
+// out of range, more partials than max(65536, n / 8) or than 64 per key): the
+// caller runs the key-segment path.
 // Phases: segment = the partials and their lists, advance = the consuming events
 // and the records' order, emit = placement.
 static int run_rules_sparse(sh_handle* h, sh_device_run* run, int32_t nkeys) {
@@ -239,7 +240,9 @@ static int run_rules_sparse(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     hipMemcpyAsync(rd, ctl, 24, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the sparse partials");
     const int64_t np = (int64_t)rd[0];
-    if (rd[2] || np > cap) return 1;
+    // a key's events each test all of its key's partials: dense partials per key take
+    // the key-segment path (whose walk stops at each partial's window)
+    if (rd[2] || np > cap || np > (int64_t)64 * nkeys) return 1;
     if (shd_exclusive_scan(key_cnt, key_off, (int64_t)nk1, h->w_scan.as<uint32_t>(), st))
         return fail(h, SH_E_HIP, "scan");
     hipEventRecord(h->ev[1], st);

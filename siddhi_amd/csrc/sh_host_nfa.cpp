@@ -169,7 +169,11 @@ static void hw_loop(sh_handle* h) {
             h->hw_busy = true;
         }
         const auto t0 = std::chrono::steady_clock::now();
-        bool ok = hipEventSynchronize(j.ev) == hipSuccess;
+        // polled (a blocking wait would hold the runtime's locks against the
+        // launching thread's calls)
+        hipError_t q;
+        while ((q = hipEventQuery(j.ev)) == hipErrorNotReady) std::this_thread::yield();
+        bool ok = q == hipSuccess;
         ok = ok && h->sm.apply(h->pin_hist.as<uint64_t>((size_t)j.first * 16), (size_t)j.n);
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         {

@@ -54,8 +54,33 @@ def test_rule_sets_vs_oracle(ci, engine, monkeypatch):
     ref = oracle_run(text, cards, ts, card, amount, merchant, batch, partitioned)
     st = []
     seq, vals, q = _device_run(text, cards, ts, card, amount, merchant, batch, partitioned, status=st)
-    if engine != "general":
-        assert st == [1 if (engine == "sparse" and partitioned) else 0]
+    if engine == "segment" or (engine == "sparse" and not partitioned):
+        assert st == [0]
+    assert len(seq) == len(ref["seq"]) > 0
+    assert np.array_equal(seq, ref["seq"].astype(np.int64))
+    assert np.array_equal(q, ref["query"])
+    assert np.array_equal(vals[:, :2], ref["values"][:, :2])
+
+
+# selective start filters (the C5 distributions at small size): the sparse path
+SPARSE_CASES = [
+    # n, cards, rules, rate, batch, merchants, free, seed, amount range of the rules
+    (60_000, 300, 100, 2, 4096, 50, (), 31, (100.0, 400.0)),
+    (40_000, 2000, 40, 1, 997, 8, (0, 3), 32, (150.0, 600.0)),   # free rules (no merchant conjunct)
+    (30_000, 20, 30, 5, 64, 6, (), 33, (400.0, 1500.0)),         # 20 cards: long same-card runs
+]
+
+
+@pytest.mark.parametrize("ci", range(len(SPARSE_CASES)))
+def test_sparse_partials_vs_oracle(ci):
+    n, cards, nr, rate, batch, merchants, free, seed, amt = SPARSE_CASES[ci]
+    ts, card, amount, merchant = synth.txn_stream(n, cards, rate, n_merchants=merchants, seed=seed)
+    rules = synth.c5_rules(nr, seed=seed, amount=amt, merchants=merchants, factor=(1.05, 1.8), within=(1, 40))
+    text = synth.c5_query(rules, unit="milliseconds", free=free)
+    ref = oracle_run(text, cards, ts, card, amount, merchant, batch, True)
+    st = []
+    seq, vals, q = _device_run(text, cards, ts, card, amount, merchant, batch, True, status=st)
+    assert st == [1]
     assert len(seq) == len(ref["seq"]) > 0
     assert np.array_equal(seq, ref["seq"].astype(np.int64))
     assert np.array_equal(q, ref["query"])
