@@ -606,8 +606,9 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     if (B.prof) {
         unsigned long long pr[16];
         hipMemcpy(pr, B.prof, 128, hipMemcpyDeviceToHost);
-        fprintf(stderr, "[shb_match clock ticks, sum over workgroups] load %llu rank %llu walk %llu scan+psum %llu emit %llu\n",
-                pr[0], pr[1], pr[2], pr[3], pr[4]);
+        fprintf(stderr, "[shb_match clock ticks, sum over workgroups] table %llu load %llu rank %llu walk %llu "
+                        "scan+psum %llu emit %llu\n",
+                pr[5], pr[0], pr[1], pr[2], pr[3], pr[4]);
     }
     if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
     if (flag) return 1;

@@ -1129,6 +1129,7 @@ for (int j = (int)threadIdx.x; j * 32 < L; j += SHB_TPB) {
     seg_of[j] = (uint8_t)lo;
 }
 __syncthreads();
+SHB_PROF(5)
 // global index of span event i (segments in span order)
 #define SHB_GIDX(i, out) { int sg_ = seg_of[(i) >> 5]; while (seg_p[sg_ + 1] - sbase <= (uint32_t)(i)) sg_++; \
     out = seg_g[sg_] + ((uint32_t)(i) - (seg_p[sg_] - sbase)); }
