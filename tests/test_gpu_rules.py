@@ -64,18 +64,18 @@ def test_rule_sets_vs_oracle(ci, engine, monkeypatch):
 
 # selective start filters (the C5 distributions at small size): the sparse path
 SPARSE_CASES = [
-    # n, cards, rules, rate, batch, merchants, free, seed, amount range of the rules
-    (60_000, 300, 100, 2, 4096, 50, (), 31, (100.0, 400.0)),
-    (40_000, 2000, 40, 1, 997, 8, (0, 3), 32, (150.0, 600.0)),   # free rules (no merchant conjunct)
-    (30_000, 20, 30, 5, 64, 6, (), 33, (400.0, 1500.0)),         # 20 cards: long same-card runs
+    # n, cards, rules, rate, batch, merchants, free, seed, amount range, factor range of the rules
+    (60_000, 300, 100, 2, 4096, 50, (), 31, (100.0, 400.0), (1.05, 1.8)),
+    (40_000, 2000, 40, 50, 997, 8, (0, 3), 32, (150.0, 600.0), (1.05, 1.8)),  # free rules (no merchant conjunct)
+    (30_000, 20, 30, 5, 64, 6, (), 33, (400.0, 1500.0), (0.3, 1.0)),          # 20 cards: long same-card runs
 ]
 
 
 @pytest.mark.parametrize("ci", range(len(SPARSE_CASES)))
 def test_sparse_partials_vs_oracle(ci):
-    n, cards, nr, rate, batch, merchants, free, seed, amt = SPARSE_CASES[ci]
+    n, cards, nr, rate, batch, merchants, free, seed, amt, fac = SPARSE_CASES[ci]
     ts, card, amount, merchant = synth.txn_stream(n, cards, rate, n_merchants=merchants, seed=seed)
-    rules = synth.c5_rules(nr, seed=seed, amount=amt, merchants=merchants, factor=(1.05, 1.8), within=(1, 40))
+    rules = synth.c5_rules(nr, seed=seed, amount=amt, merchants=merchants, factor=fac, within=(1, 40))
     text = synth.c5_query(rules, unit="milliseconds", free=free)
     ref = oracle_run(text, cards, ts, card, amount, merchant, batch, True)
     st = []
