@@ -867,6 +867,13 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggc(shb_plan P, shb_aggc A) {
     const void* e1src = A.e1_col >= 0 ? P.ms[A.e1_col] : nullptr;
     const void* e2src = A.e2_col[0] >= 0 ? P.st_dst[A.e2_col[0]] : nullptr;
     const void* e2srn = A.e2_col[1] >= 0 ? P.st_dst[A.e2_col[1]] : nullptr;
+    unsigned long long t_prev = wall_clock64();
+#define AGC_PROF(ph)                                                                 \
+    if (P.prof && threadIdx.x == 0) {                                                \
+        const unsigned long long t_now = wall_clock64();                             \
+        atomicAdd(&P.prof[8 + (ph)], t_now - t_prev);                                \
+        t_prev = t_now;                                                              \
+    }
     for (int a = 0; a < P.nt;) {
         __syncthreads();
         const int nseg = P.nt - a < SHB_CT_MAX ? P.nt - a : SHB_CT_MAX;
@@ -904,6 +911,7 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggc(shb_plan P, shb_aggc A) {
             seg_of[j] = (uint8_t)lo;
         }
         __syncthreads();
+        AGC_PROF(0)
         // the chunk's consumers (arrival order inside the bucket): key, count, e2 argument
         uint32_t cc[AGC_NR];
         int sgi[AGC_NR];
@@ -942,6 +950,7 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggc(shb_plan P, shb_aggc A) {
             return;  // (uniform: total is the block sum)
         }
         __syncthreads();
+        AGC_PROF(1)
         // match-stream positions (the segment's first match + the prefix inside it)
         // and the e1-side arguments of the rows
 #pragma unroll
@@ -955,6 +964,7 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggc(shb_plan P, shb_aggc A) {
                 for (uint32_t q = 0; q < cc[k]; q++) r_e1[c_pre[i] + q] = (uint32_t)((const uint32_t*)e1src)[mp + q];
         }
         __syncthreads();
+        AGC_PROF(2)
         // stable sort by local key (kb <= 8: 6 bits, then the high bits)
         const uint16_t* srt = o_a;
         s3b_sort_pass(c_key, nullptr, o_a, L, 0, wc, ws);  // (digits of the low 12 bits: the key)
@@ -962,6 +972,7 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggc(shb_plan P, shb_aggc A) {
             s3b_sort_pass(c_key, o_a, o_b, L, 6, wc, ws);
             srt = o_b;
         }
+        AGC_PROF(3)
         // the first consumer of each key run adds the run's rows in sequence
         for (int q = threadIdx.x; q < L; q += AGC_TPB) {
             const uint32_t ci = srt[q];
@@ -1005,8 +1016,11 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggc(shb_plan P, shb_aggc A) {
             for (int o = 0; o < SHB_MAX_AGG; o++) st_acc[o][key] = acc[o];
             st_cnt[key] = n;
         }
+        __syncthreads();
+        AGC_PROF(4)
         a += ne;
     }
+#undef AGC_PROF
 }
 
 // ---------------------------------------------------------------- launches

@@ -609,6 +609,10 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
         fprintf(stderr, "[shb_match clock ticks, sum over workgroups] table %llu load %llu rank %llu walk %llu "
                         "scan+psum %llu emit %llu\n",
                 pr[5], pr[0], pr[1], pr[2], pr[3], pr[4]);
+        if (carry)
+            fprintf(stderr, "[k_bk_aggc clock ticks, sum over workgroups] table %llu load+prefix %llu e1 %llu "
+                            "sort %llu walk %llu\n",
+                    pr[8], pr[9], pr[10], pr[11], pr[12]);
     }
     if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
     if (flag) return 1;
