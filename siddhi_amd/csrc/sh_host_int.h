@@ -257,6 +257,8 @@ struct sh_handle {
     hipEvent_t hw_ev[16] = {};
     int hw_ev_next = 0;
     double hw_ms = 0.0;  // the thread's replay time (phase 7 when profiled)
+    bool hist_spec = false;  // the last launch's first history records came back with its counters
+    std::vector<nfd_cand> pick_slots;  // host pick of the due keys: one slot per due millisecond
     PinBuf pin_sev, pin_rk, pin_cand;
     int64_t sev_cap = 0;
     int caps[6] = {16, 32, 64, 32, 8, 4};  // list, se, node, hold, sched, group

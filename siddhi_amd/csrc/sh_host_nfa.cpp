@@ -103,10 +103,24 @@ static void nf_ctl_zero(sh_handle* h) { hipMemsetAsync(h->n_ctl.p, 0, 24, h->str
 // changed ranks (before the next due scan, on the same stream)
 // pin_rd slots of the counter block read back after a launch (nf_ctl_read)
 enum { PR_CTL = 40 };
+// scheduler-history records copied back speculatively with a launch's counters
+// (a launch with more takes a second, event-tracked copy)
+static const int64_t kHistSpec = 4096;
+
 // the launch's counter block (records, error, history count) into pin_rd[PR_CTL..+24),
-// read with the caller's next sync
+// read with the caller's next sync; single process with scheduler maps: the first
+// kHistSpec history records come back in the same sync (h->hist_spec)
 static void nf_ctl_read(sh_handle* h) {
     hipMemcpyAsync(h->pin_rd.as<uint8_t>() + PR_CTL, h->n_ctl.p, 24, hipMemcpyDeviceToHost, h->stream);
+    h->hist_spec = false;
+    if (!h->sm_on || h->coord_on || h->sev_cap < kHistSpec) return;
+    if ((size_t)(h->hist_used + kHistSpec) * 16 > h->pin_hist.bytes) {
+        if (nf_sev_flush(h)) return;  // (the buffer restarts once the thread is idle)
+        if (h->pin_hist.ensure((size_t)kHistSpec * 16 * 4)) return;
+    }
+    hipMemcpyAsync(h->pin_hist.as<uint8_t>((size_t)h->hist_used * 16), h->n_sev.p, (size_t)kHistSpec * 16,
+                   hipMemcpyDeviceToHost, h->stream);
+    h->hist_spec = true;
 }
 static unsigned nf_ctl_err(sh_handle* h) { return *(const unsigned*)(h->pin_rd.as<uint8_t>() + PR_CTL + 8); }
 static int64_t nf_ctl_nrec(sh_handle* h) { return *(const int64_t*)(h->pin_rd.as<uint8_t>() + PR_CTL); }
@@ -171,8 +185,9 @@ static void hw_loop(sh_handle* h) {
         const auto t0 = std::chrono::steady_clock::now();
         // polled (a blocking wait would hold the runtime's locks against the
         // launching thread's calls)
-        hipError_t q;
-        while ((q = hipEventQuery(j.ev)) == hipErrorNotReady) std::this_thread::yield();
+        hipError_t q = hipSuccess;
+        if (j.ev)
+            while ((q = hipEventQuery(j.ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(5));
         bool ok = q == hipSuccess;
         ok = ok && h->sm.apply(h->pin_hist.as<uint64_t>((size_t)j.first * 16), (size_t)j.n);
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -188,7 +203,7 @@ static void hw_loop(sh_handle* h) {
 }
 
 // queue a launch's records [first, first + n) of pin_hist (their copy is on h->stream)
-static int hw_submit(sh_handle* h, int64_t first, int64_t n) {
+static int hw_submit(sh_handle* h, int64_t first, int64_t n, bool tracked) {
     if (!h->hw_thread.joinable()) {
         for (auto& e : h->hw_ev)
             if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
@@ -201,9 +216,12 @@ static int hw_submit(sh_handle* h, int64_t first, int64_t n) {
         // (an event is reused only after its job is done: at most 15 queued)
         h->hw_idle.wait(lk, [h] { return h->hw_q.size() < 15; });
     }
-    hipEvent_t ev = h->hw_ev[h->hw_ev_next];
-    h->hw_ev_next = (h->hw_ev_next + 1) % 16;
-    if (hipEventRecord(ev, h->stream) != hipSuccess) return fail(h, SH_E_HIP, "history event");
+    hipEvent_t ev = nullptr;  // (untracked: the records are on the host already)
+    if (tracked) {
+        ev = h->hw_ev[h->hw_ev_next];
+        h->hw_ev_next = (h->hw_ev_next + 1) % 16;
+        if (hipEventRecord(ev, h->stream) != hipSuccess) return fail(h, SH_E_HIP, "history event");
+    }
     {
         std::lock_guard<std::mutex> lk(h->hw_mu);
         h->hw_q.push_back({first, n, ev});
@@ -274,7 +292,16 @@ static int nf_sev_apply(sh_handle* h, bool counted = false) {
         }
         h->hp_n[9] += n;
         if (!h->coord_on) {
+            const bool spec = counted && h->hist_spec;
+            h->hist_spec = false;
             if (n == 0) return SH_OK;
+            if (spec && n <= kHistSpec) {
+                // already on the host (the counters' sync): the thread starts at once
+                int qrc = hw_submit(h, h->hist_used, n, false);
+                if (qrc) return qrc;
+                h->hist_used += n;
+                return SH_OK;
+            }
             if ((size_t)(h->hist_used + n) * 16 > h->pin_hist.bytes) {
                 // grow: once the thread has applied the queued launches, the buffer restarts
                 int frc = nf_sev_flush(h);
@@ -283,7 +310,7 @@ static int nf_sev_apply(sh_handle* h, bool counted = false) {
             }
             hipMemcpyAsync(h->pin_hist.as<uint8_t>((size_t)h->hist_used * 16), h->n_sev.p, (size_t)n * 16,
                            hipMemcpyDeviceToHost, st);
-            int qrc = hw_submit(h, h->hist_used, n);
+            int qrc = hw_submit(h, h->hist_used, n, true);
             if (qrc) return qrc;
             h->hist_used += n;
             return SH_OK;
@@ -380,11 +407,12 @@ enum { PR_NREC = 0, PR_LOFF = 8, PR_LCNT = 12, PR_ERR = 16, PR_NC = 24, PR_TMIN 
 // due times span at most kTieBreakSlots milliseconds (SH_TIEBREAK_MIN overrides)
 static const int64_t kDeviceTieBreak = [] {
     const char* e = getenv("SH_TIEBREAK_MIN");
-    return e ? (int64_t)atoll(e) : (int64_t)4096;
+    return e ? (int64_t)atoll(e) : (int64_t)65536;
 }();
 static const int64_t kTieBreakSlots = (int64_t)1 << 22;
 // due candidates copied back with their count (a larger backlog takes a second copy)
-static const int64_t kCandSpec = 2048;
+static const int64_t kCandSpec = 4096;
+
 static int pin_rd_ready(sh_handle* h) { return h->pin_rd.ensure(PR_COLS + sizeof(nf_cols)); }
 
 // upload the nf_cols image through pinned memory (the caller synchronises the
@@ -972,12 +1000,31 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
                     const ShJMap& M = h->sm.maps[q * NF_MAX_PROC + p];
                     for (auto& c : cs) c.stamp = M.present(c.key) ? M.rank(c.key) : ~0ull;
                 }
-                std::sort(cs.begin(), cs.end(), [](const nfd_cand& a, const nfd_cand& b) {
-                    if (a.t != b.t) return a.t < b.t;
-                    return a.stamp < b.stamp;
-                });
-                for (size_t i = 0; i < cs.size(); i++)
-                    if (wall || i == 0 || cs[i].t != cs[i - 1].t) sel.push_back(cs[i].key);
+                int64_t tlo = INT64_MAX, thi = INT64_MIN;
+                for (const auto& c : cs) {
+                    tlo = std::min(tlo, c.t);
+                    thi = std::max(thi, c.t);
+                }
+                const int64_t range = cs.empty() ? 0 : thi - tlo + 1;
+                if (!wall && range > 0 && range <= std::max<int64_t>(4 * (int64_t)nc, 65536)) {
+                    // one slot per due millisecond: the least (stamp) candidate of each
+                    // (TreeMultimap with a zero comparator keeps the first per time)
+                    auto& sl = h->pick_slots;
+                    sl.assign((size_t)range, nfd_cand{0, ~0ull, -1, 0});
+                    for (const auto& c : cs) {
+                        nfd_cand& o = sl[(size_t)(c.t - tlo)];
+                        if (o.key < 0 || c.stamp < o.stamp) o = c;
+                    }
+                    for (const auto& o : sl)
+                        if (o.key >= 0) sel.push_back(o.key);
+                } else {
+                    std::sort(cs.begin(), cs.end(), [](const nfd_cand& a, const nfd_cand& b) {
+                        if (a.t != b.t) return a.t < b.t;
+                        return a.stamp < b.stamp;
+                    });
+                    for (size_t i = 0; i < cs.size(); i++)
+                        if (wall || i == 0 || cs[i].t != cs[i - 1].t) sel.push_back(cs[i].key);
+                }
             }
             const int32_t ns = (int32_t)sel.size();
             if (!h->coord_on) n_idx = ns;
