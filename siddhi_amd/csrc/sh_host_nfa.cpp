@@ -113,7 +113,8 @@ static const int64_t kHistSpec = 4096;
 static void nf_ctl_read(sh_handle* h) {
     hipMemcpyAsync(h->pin_rd.as<uint8_t>() + PR_CTL, h->n_ctl.p, 24, hipMemcpyDeviceToHost, h->stream);
     h->hist_spec = false;
-    if (!h->sm_on || h->coord_on || h->sev_cap < kHistSpec) return;
+    static const bool spec_off = getenv("SH_HIST_SPEC") && getenv("SH_HIST_SPEC")[0] == '0';
+    if (spec_off || !h->sm_on || h->coord_on || h->sev_cap < kHistSpec) return;
     if ((size_t)(h->hist_used + kHistSpec) * 16 > h->pin_hist.bytes) {
         if (nf_sev_flush(h)) return;  // (the buffer restarts once the thread is idle)
         if (h->pin_hist.ensure((size_t)kHistSpec * 16 * 4)) return;
@@ -1006,7 +1007,8 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
                     thi = std::max(thi, c.t);
                 }
                 const int64_t range = cs.empty() ? 0 : thi - tlo + 1;
-                if (!wall && range > 0 && range <= std::max<int64_t>(4 * (int64_t)nc, 65536)) {
+                static const bool slots_off = getenv("SH_HOST_SLOTS") && getenv("SH_HOST_SLOTS")[0] == '0';
+                if (!slots_off && !wall && range > 0 && range <= std::max<int64_t>(4 * (int64_t)nc, 65536)) {
                     // one slot per due millisecond: the least (stamp) candidate of each
                     // (TreeMultimap with a zero comparator keeps the first per time)
                     auto& sl = h->pick_slots;
