@@ -602,15 +602,10 @@ extern "C" int shr_ts_to32(const int64_t* ts, int64_t n, int64_t base, uint32_t*
 #define SPA_F_TS 1
 #define SPA_F_KEY 2
 
-__device__ __forceinline__ void spa_lookup(const shr_table* __restrict__ RT, const shd_cols* __restrict__ C,
-                                           const int64_t* s_ixv, const uint32_t* s_ixs, bool lds_ix,
-                                           const uint8_t* __restrict__ img, const shr_img& I, uint32_t p,
-                                           uint32_t* lo, uint32_t* hi) {
+// the predicate-index group of value x of the indexed attribute: [lo, hi) of ix_rule
+__device__ __forceinline__ void spa_group(const shr_table* __restrict__ RT, const uint8_t* __restrict__ img,
+                                          const shr_img& I, int64_t x, uint32_t* lo, uint32_t* hi) {
     *lo = *hi = 0;
-    const int ix_attr = RT->ix_attr;
-    if (ix_attr < 0) return;
-    const int ty = RT->attr_type[ix_attr];
-    const int64_t x = rule_ix_key(ty, load_attr(C, 0, ix_attr, ty, p));
     if (img && I.dense_n) {
         const int64_t dv = x - I.dense_min;
         if (dv >= 0 && dv < I.dense_n) {
@@ -624,16 +619,18 @@ __device__ __forceinline__ void spa_lookup(const shr_table* __restrict__ RT, con
     int a = 0, b = n_ix;
     while (a < b) {
         const int m = (a + b) >> 1;
-        if ((lds_ix ? s_ixv[m] : RT->ix_val[m]) < x)
+        if (RT->ix_val[m] < x)
             a = m + 1;
         else
             b = m;
     }
-    if (a < n_ix && (lds_ix ? s_ixv[a] : RT->ix_val[a]) == x) {
-        *lo = lds_ix ? s_ixs[a] : RT->ix_start[a];
-        *hi = lds_ix ? s_ixs[a + 1] : RT->ix_start[a + 1];
+    if (a < n_ix && RT->ix_val[a] == x) {
+        *lo = RT->ix_start[a];
+        *hi = RT->ix_start[a + 1];
     }
 }
+
+#define SPA_U 4  // events per thread and round, their loads issued together
 
 __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __restrict__ RT,
                                                          const int64_t* __restrict__ ts,
@@ -645,58 +642,70 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
                                                          uint32_t* __restrict__ key_cnt,
                                                          unsigned long long* __restrict__ ctr, int64_t cap,
                                                          int32_t* __restrict__ flag) {
-    __shared__ int64_t s_ixv[SHR_LDS_IX];
-    __shared__ uint32_t s_ixs[SHR_LDS_IX + 1];
     __shared__ uint32_t b_p[SPA_BUF], b_r[SPA_BUF], b_k[SPA_BUF], b_s[SPA_BUF];
     __shared__ uint32_t s_fill;
     __shared__ unsigned long long s_base;
-    const int n_ix = RT->n_ix;
-    const bool lds_ix = RT->ix_attr >= 0 && n_ix <= SHR_LDS_IX && !(img && I.dense_n);
-    if (lds_ix) {
-        for (int i = threadIdx.x; i < n_ix; i += blockDim.x) s_ixv[i] = RT->ix_val[i];
-        for (int i = threadIdx.x; i <= n_ix; i += blockDim.x) s_ixs[i] = RT->ix_start[i];
-    }
     if (threadIdx.x == 0) s_fill = 0u;
     const uint32_t n_free = (uint32_t)RT->n_free;
+    const int ix_attr = RT->ix_attr;
+    const int ix_ty = ix_attr >= 0 ? RT->attr_type[ix_attr] : 0;
+    const void* ix_col = ix_attr >= 0 ? C->col[0][ix_attr] : nullptr;
     int32_t fl = 0;
     __syncthreads();
-    for (int64_t base = (int64_t)blockIdx.x * SPA_TPB; base < n; base += (int64_t)gridDim.x * SPA_TPB) {
-        const int64_t p = base + threadIdx.x;
-        if (p < n) {
-            if (p > 0 && ts[p] < ts[p - 1]) fl |= SPA_F_TS;
-            const int32_t key = akeys[p];
-            if (key >= nkeys) fl |= SPA_F_KEY;
-            if (key >= 0 && key < nkeys) {
-                uint32_t lo, hi;
-                spa_lookup(RT, C, s_ixv, s_ixs, lds_ix, img, I, (uint32_t)p, &lo, &hi);
-                const uint32_t nsel = hi - lo, total = nsel + n_free;
-                for (uint32_t k = 0; k < total; k++) {
-                    const uint32_t r = k < nsel ? RT->ix_rule[lo + k] : RT->free_rule[k - nsel];
-                    const shr_rule* R = RT->rules + r;
-                    if (!rule_terms(R->t[0], R->nt[0], (uint32_t)p, SHD_NULL_ROW, C)) continue;
-                    const uint32_t slot = atomicAdd(&key_cnt[key], 1u);
-                    const uint32_t at = atomicAdd(&s_fill, 1u);
-                    if (at < SPA_BUF) {
-                        b_p[at] = (uint32_t)p;
-                        b_r[at] = r;
-                        b_k[at] = (uint32_t)key;
-                        b_s[at] = slot;
-                    } else {
-                        // (a chunk with more than the buffer: straight to global)
-                        const unsigned long long g = atomicAdd(ctr, 1ull);
-                        if ((int64_t)g < cap) {
-                            pr_p[g] = (uint32_t)p;
-                            pr_r[g] = r;
-                            pr_key[g] = (uint32_t)key;
-                            pr_slot[g] = slot;
-                        }
+    const int64_t round = (int64_t)SPA_TPB * SPA_U;
+    for (int64_t base = (int64_t)blockIdx.x * round; base < n; base += (int64_t)gridDim.x * round) {
+        // SPA_U consecutive runs of the workgroup's events: ts, key, index value
+        int64_t tv[SPA_U], tp[SPA_U];
+        int32_t key[SPA_U];
+        int64_t xv[SPA_U];
+#pragma unroll
+        for (int u = 0; u < SPA_U; u++) {
+            const int64_t p = base + (int64_t)u * SPA_TPB + threadIdx.x;
+            const bool in = p < n;
+            tv[u] = in ? ts[p] : 0;
+            tp[u] = in && p > 0 ? ts[p - 1] : INT64_MIN;
+            key[u] = in ? akeys[p] : -1;
+            xv[u] = (in && ix_col) ? rule_ix_key(ix_ty, rule_attr(&ix_col, 0, ix_ty, (uint32_t)p)) : 0;
+        }
+        uint32_t lo[SPA_U], hi[SPA_U];
+#pragma unroll
+        for (int u = 0; u < SPA_U; u++) {
+            if (tv[u] < tp[u]) fl |= SPA_F_TS;
+            if (key[u] >= nkeys) fl |= SPA_F_KEY;
+            lo[u] = hi[u] = 0;
+            if (ix_col && key[u] >= 0 && key[u] < nkeys) spa_group(RT, img, I, xv[u], &lo[u], &hi[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < SPA_U; u++) {
+            const int64_t p = base + (int64_t)u * SPA_TPB + threadIdx.x;
+            if (key[u] < 0 || key[u] >= nkeys) continue;
+            const uint32_t nsel = hi[u] - lo[u], total = nsel + n_free;
+            for (uint32_t k = 0; k < total; k++) {
+                const uint32_t r = k < nsel ? RT->ix_rule[lo[u] + k] : RT->free_rule[k - nsel];
+                const shr_rule* R = RT->rules + r;
+                if (!rule_terms(R->t[0], R->nt[0], (uint32_t)p, SHD_NULL_ROW, C)) continue;
+                const uint32_t slot = atomicAdd(&key_cnt[key[u]], 1u);
+                const uint32_t at = atomicAdd(&s_fill, 1u);
+                if (at < SPA_BUF) {
+                    b_p[at] = (uint32_t)p;
+                    b_r[at] = r;
+                    b_k[at] = (uint32_t)key[u];
+                    b_s[at] = slot;
+                } else {
+                    // (a round with more than the buffer: straight to global)
+                    const unsigned long long g = atomicAdd(ctr, 1ull);
+                    if ((int64_t)g < cap) {
+                        pr_p[g] = (uint32_t)p;
+                        pr_r[g] = r;
+                        pr_key[g] = (uint32_t)key[u];
+                        pr_slot[g] = slot;
                     }
                 }
             }
         }
         __syncthreads();
         const uint32_t fill = s_fill < SPA_BUF ? s_fill : SPA_BUF;
-        const bool last = base + (int64_t)gridDim.x * SPA_TPB >= n;
+        const bool last = base + (int64_t)gridDim.x * round >= n;
         if (fill >= SPA_BUF / 2 || (last && fill)) {
             if (threadIdx.x == 0) s_base = atomicAdd(ctr, (unsigned long long)fill);
             __syncthreads();
@@ -743,17 +752,36 @@ __global__ void __launch_bounds__(256) k_sparse_take(const shr_table* __restrict
                                                      const uint32_t* __restrict__ key_off,
                                                      const uint32_t* __restrict__ l_p, const uint32_t* __restrict__ l_r,
                                                      const int64_t* __restrict__ l_te, uint32_t* __restrict__ l_q) {
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t key = akeys[q];
-        if (key < 0) continue;
-        const uint32_t lo = key_off[key], hi = key_off[key + 1];
-        if (lo == hi) continue;
-        const int64_t tq = ts[q];
-        for (uint32_t pos = lo; pos < hi; pos++) {
-            const uint32_t p = l_p[pos];
-            if ((int64_t)p >= q || tq > l_te[pos]) continue;
-            const shr_rule* R = RT->rules + l_r[pos];
-            if (rule_terms(R->t[1], R->nt[1], p, (uint32_t)q, C)) atomicMin(&l_q[pos], (uint32_t)q);
+    // SPA_U events per thread and round: their key, list bounds and first list
+    // entry are loaded together (three dependent random reads per event otherwise)
+    const int64_t round = (int64_t)blockDim.x * SPA_U;
+    for (int64_t base = (int64_t)blockIdx.x * round; base < n; base += (int64_t)gridDim.x * round) {
+        int32_t key[SPA_U];
+#pragma unroll
+        for (int u = 0; u < SPA_U; u++) {
+            const int64_t q = base + (int64_t)u * blockDim.x + threadIdx.x;
+            key[u] = q < n ? akeys[q] : -1;
+        }
+        uint32_t lo[SPA_U], hi[SPA_U];
+#pragma unroll
+        for (int u = 0; u < SPA_U; u++) {
+            lo[u] = hi[u] = 0;
+            if (key[u] >= 0) {
+                lo[u] = key_off[key[u]];
+                hi[u] = key_off[key[u] + 1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < SPA_U; u++) {
+            if (lo[u] == hi[u]) continue;
+            const int64_t q = base + (int64_t)u * blockDim.x + threadIdx.x;
+            const int64_t tq = ts[q];
+            for (uint32_t pos = lo[u]; pos < hi[u]; pos++) {
+                const uint32_t p = l_p[pos];
+                if ((int64_t)p >= q || tq > l_te[pos]) continue;
+                const shr_rule* R = RT->rules + l_r[pos];
+                if (rule_terms(R->t[1], R->nt[1], p, (uint32_t)q, C)) atomicMin(&l_q[pos], (uint32_t)q);
+            }
         }
     }
 }
@@ -794,8 +822,8 @@ extern "C" int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int
     shr_img none;
     memset(&none, 0, sizeof(none));
     const bool use_img = img && I && I->bytes > 0;
-    int64_t g = (n + SPA_TPB - 1) / SPA_TPB;
-    if (g > 1024) g = 1024;  // 4 per CU, each striding over many tiles (few buffer flushes)
+    int64_t g = (n + SPA_TPB * SPA_U - 1) / (SPA_TPB * SPA_U);
+    if (g > 512) g = 512;  // 2 per CU (64 KB of LDS each), striding over the run (few buffer flushes)
     if (g < 1) g = 1;
     hipLaunchKernelGGL(k_sparse_open, dim3((unsigned)g), dim3(SPA_TPB), 0, (hipStream_t)stream, dT, ts, akeys, n, nkeys,
                        dC, use_img ? img : (const uint8_t*)nullptr, use_img ? *I : none, pr_p, pr_r, pr_key, pr_slot,
@@ -813,7 +841,9 @@ extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const in
     const unsigned gp = rgrid(n_pairs_max);
     hipLaunchKernelGGL(k_sparse_place, dim3(gp), dim3(RTPB), 0, st, pr_p, pr_r, pr_key, pr_slot, ctr, key_off, dT, ts,
                        l_p, l_r, l_te, l_q);
-    hipLaunchKernelGGL(k_sparse_take, dim3(rgrid(n) < 8192u ? rgrid(n) : 8192u), dim3(256), 0, st, dT, ts, akeys, n, dC,
+    const int64_t tg = (n + 256 * SPA_U - 1) / (256 * SPA_U);
+    hipLaunchKernelGGL(k_sparse_take, dim3((unsigned)(tg < 4096 ? (tg < 1 ? 1 : tg) : 4096)), dim3(256), 0, st, dT, ts,
+                       akeys, n, dC,
                        key_off, (const uint32_t*)l_p, (const uint32_t*)l_r, (const int64_t*)l_te, l_q);
     hipLaunchKernelGGL(k_sparse_rec, dim3(gp), dim3(256), 0, st, (const uint32_t*)l_p, (const uint32_t*)l_r,
                        (const uint32_t*)l_q, ctr, rec_p, rec_q, rec_r, rctr, rcap);

@@ -10,7 +10,13 @@ tests/test_gpu_c4.py holds the device to this digest: the scheduler's HashMap
 (PartitionStateHolder / Scheduler.onTimeChange order) only resizes through the
 tables of a 10M-key run at that size. Runtime ~10 min on one core.
 
-usage: python tests/golden/make_c4_digest.py [--events N --users U --every]"""
+The smaller streams of tests/test_gpu_c4.py are digested the same way
+(--kind stream: synth.c4_stream(users, seconds); --kind spec --events 3000000
+--users 1000000 [--every]), so the GPU suite compares against them instead of
+running the oracle on the GPU box.
+
+usage: python tests/golden/make_c4_digest.py [--kind spec|stream] [--events N --users U
+       --seconds S --every]"""
 import argparse
 import json
 import os
@@ -27,22 +33,32 @@ def main():
     ap.add_argument("--events", type=int, default=100_000_000)
     ap.add_argument("--users", type=int, default=10_000_000)
     ap.add_argument("--every", action="store_true")
+    ap.add_argument("--kind", choices=["spec", "stream"], default="spec")
+    ap.add_argument("--seconds", type=int, default=60)
     ap.add_argument("--out", default=os.path.join(HERE, "c4_digest.json"))
     a = ap.parse_args()
     from c4_cases import c4_digest, run_c4
     from oracle_engine import OracleEngine
     from siddhi_amd import compiler, synth
     t0 = time.time()
-    blocks = synth.c4_spec_stream(a.events, a.users, rate_per_ms=100, batch=4096)
+    if a.kind == "spec":
+        blocks = synth.c4_spec_stream(a.events, a.users, rate_per_ms=100, batch=4096)
+    else:
+        blocks = synth.c4_stream(a.users, seconds=a.seconds)
     print(f"stream: {len(blocks)} calls in {time.time() - t0:.0f} s", flush=True)
     c = compiler.compile_app(synth.C4_EVERY_QUERY if a.every else synth.C4_QUERY)
     t1 = time.time()
     out = run_c4(OracleEngine(c), blocks, progress=lambda m: print(m, flush=True))
     d = c4_digest(out)
-    d.update({"events": a.events, "users": a.users, "rate_ev_per_ms": 100, "batch": 4096,
-              "query": "every" if a.every else "default", "oracle_seconds": round(time.time() - t1, 1),
-              "generator": "tests/golden/make_c4_digest.py (synth.c4_spec_stream, oracle/refcpu.cpp)"})
-    key = ("every" if a.every else "default") + f"_{a.events}_{a.users}"
+    if a.kind == "spec":
+        d.update({"events": a.events, "users": a.users, "rate_ev_per_ms": 100, "batch": 4096,
+                  "generator": "tests/golden/make_c4_digest.py (synth.c4_spec_stream, oracle/refcpu.cpp)"})
+        key = ("every" if a.every else "default") + f"_{a.events}_{a.users}"
+    else:
+        d.update({"users": a.users, "seconds": a.seconds,
+                  "generator": "tests/golden/make_c4_digest.py --kind stream (synth.c4_stream, oracle/refcpu.cpp)"})
+        key = ("every" if a.every else "default") + f"_stream_{a.users}_{a.seconds}"
+    d.update({"query": "every" if a.every else "default", "oracle_seconds": round(time.time() - t1, 1)})
     res = json.load(open(a.out)) if os.path.exists(a.out) else {}
     res[key] = d
     json.dump(res, open(a.out, "w"), indent=1, sort_keys=True)
