@@ -102,7 +102,7 @@ int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int32_t* akeys
 // consuming event of each (least later event of its key in the window with f2),
 // and the (p, q, r) records of the consumed ones (count in *rctr, any order)
 int shr_sparse_match(const shr_table* dT, const int64_t* ts, const int32_t* akeys, int64_t n, const shd_cols* dC,
-                     const uint32_t* pr_p, const uint32_t* pr_r, const uint32_t* pr_key, const uint32_t* pr_slot,
+                     const uint8_t* img, const shr_img* I, const uint32_t* pr_p, const uint32_t* pr_r, const uint32_t* pr_key, const uint32_t* pr_slot,
                      const unsigned long long* ctr, int64_t n_pairs_max, const uint32_t* key_off, uint32_t* l_p,
                      uint32_t* l_r, int64_t* l_te, uint32_t* l_q, uint32_t* rec_p, uint32_t* rec_q, uint32_t* rec_r,
                      unsigned long long* rctr, int64_t rcap, void* stream);

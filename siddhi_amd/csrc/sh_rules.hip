@@ -598,7 +598,7 @@ extern "C" int shr_ts_to32(const int64_t* ts, int64_t n, int64_t base, uint32_t*
 // overflow the buffers (the host reads the count) sets a flag: the host runs the
 // key-segment path instead.
 #define SPA_TPB 1024
-#define SPA_BUF 4096
+#define SPA_BUF 1024
 #define SPA_F_TS 1
 #define SPA_F_KEY 2
 
@@ -632,6 +632,93 @@ __device__ __forceinline__ void spa_group(const shr_table* __restrict__ RT, cons
 
 #define SPA_U 4  // events per thread and round, their loads issued together
 
+// the rule set as the sparse kernels read it: the LDS image (IMG, shr_img: the
+// index, rule ids, windows and terms on chip, like k_rules_scan_img) or the table
+// in global memory
+struct SpaRules {
+    const uint8_t* L;          // LDS image
+    const uint8_t* G;          // the whole image (global): f1's terms past I.lds
+    const void* const* cols;   // stream-0 column pointers (LDS)
+};
+
+template <bool IMG>
+__device__ __forceinline__ void spa_stage(const uint8_t* __restrict__ img, const shr_img& I,
+                                          const shd_cols* __restrict__ C, uint4* s_img, const void** s_col) {
+    if (IMG)
+        for (int i = threadIdx.x; i < I.lds / 16; i += blockDim.x) s_img[i] = ((const uint4*)img)[i];
+    if (threadIdx.x < 32) s_col[threadIdx.x] = C->col[0][threadIdx.x];
+}
+
+// candidate rule group of an index value: [lo, hi) of the rule ids
+template <bool IMG>
+__device__ __forceinline__ void spa_candidates(const shr_table* __restrict__ RT, const shr_img& I, const SpaRules& S,
+                                               const uint8_t* __restrict__ img, int64_t x, uint32_t* lo,
+                                               uint32_t* hi) {
+    if (!IMG) {
+        spa_group(RT, img, I, x, lo, hi);
+        return;
+    }
+    *lo = *hi = 0;
+    if (I.dense_n) {
+        const int64_t dv = x - I.dense_min;
+        if (dv >= 0 && dv < I.dense_n) {
+            const uint2 e = ((const uint2*)(S.L + I.off_dense))[dv];
+            *lo = e.x;
+            *hi = e.y;
+        }
+        return;
+    }
+    const int64_t* ixv = (const int64_t*)(S.L + I.off_ixv);
+    const uint32_t* ixs = (const uint32_t*)(S.L + I.off_ixs);
+    const int n_ix = RT->n_ix;
+    int a = 0, b = n_ix;
+    while (a < b) {
+        const int m = (a + b) >> 1;
+        if (ixv[m] < x)
+            a = m + 1;
+        else
+            b = m;
+    }
+    if (a < n_ix && ixv[a] == x) {
+        *lo = ixs[a];
+        *hi = ixs[a + 1];
+    }
+}
+
+template <bool IMG>
+__device__ __forceinline__ uint32_t spa_rule_id(const shr_table* __restrict__ RT, const shr_img& I, const SpaRules& S,
+                                                uint32_t lo, uint32_t k, uint32_t nsel) {
+    if (IMG)
+        return k < nsel ? ((const uint32_t*)(S.L + I.off_ixr))[lo + k] : ((const uint32_t*)(S.L + I.off_free))[k - nsel];
+    return k < nsel ? RT->ix_rule[lo + k] : RT->free_rule[k - nsel];
+}
+
+// f1 of rule r on row p
+template <bool IMG>
+__device__ __forceinline__ bool spa_f1(const shr_table* __restrict__ RT, const shr_img& I, const SpaRules& S,
+                                       const shd_cols* __restrict__ C, uint32_t r, uint32_t p) {
+    if (IMG) {
+        const shr_meta M = ((const shr_meta*)(S.L + I.off_meta))[r];
+        const shp_term* T0 = (const shp_term*)((I.off_terms0 < I.lds ? S.L : S.G) + I.off_terms0) + M.toff0;
+        return rule_terms_img(T0, M.nt0, p, SHD_NULL_ROW, S.cols);
+    }
+    const shr_rule* R = RT->rules + r;
+    return rule_terms(R->t[0], R->nt[0], p, SHD_NULL_ROW, C);
+}
+
+// f2 of rule r on (p, q)
+template <bool IMG>
+__device__ __forceinline__ bool spa_f2(const shr_table* __restrict__ RT, const shr_img& I, const SpaRules& S,
+                                       const shd_cols* __restrict__ C, uint32_t r, uint32_t p, uint32_t q) {
+    if (IMG) {
+        const shr_meta M = ((const shr_meta*)(S.L + I.off_meta))[r];
+        return rule_terms_img((const shp_term*)(S.L + I.off_terms1) + M.toff1, M.nt1, p, q, S.cols);
+    }
+    const shr_rule* R = RT->rules + r;
+    return rule_terms(R->t[1], R->nt[1], p, q, C);
+}
+
+template <bool IMG>
 __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __restrict__ RT,
                                                          const int64_t* __restrict__ ts,
                                                          const int32_t* __restrict__ akeys, int64_t n, int32_t nkeys,
@@ -642,19 +729,23 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
                                                          uint32_t* __restrict__ key_cnt,
                                                          unsigned long long* __restrict__ ctr, int64_t cap,
                                                          int32_t* __restrict__ flag) {
+    extern __shared__ uint4 s_img[];
+    __shared__ const void* s_col[32];
     __shared__ uint32_t b_p[SPA_BUF], b_r[SPA_BUF], b_k[SPA_BUF], b_s[SPA_BUF];
     __shared__ uint32_t s_fill;
     __shared__ unsigned long long s_base;
+    spa_stage<IMG>(img, I, C, s_img, s_col);
     if (threadIdx.x == 0) s_fill = 0u;
+    const SpaRules S{(const uint8_t*)s_img, img, s_col};
     const uint32_t n_free = (uint32_t)RT->n_free;
     const int ix_attr = RT->ix_attr;
     const int ix_ty = ix_attr >= 0 ? RT->attr_type[ix_attr] : 0;
-    const void* ix_col = ix_attr >= 0 ? C->col[0][ix_attr] : nullptr;
     int32_t fl = 0;
     __syncthreads();
+    const void* ix_col = ix_attr >= 0 ? s_col[ix_attr] : nullptr;
     const int64_t round = (int64_t)SPA_TPB * SPA_U;
     for (int64_t base = (int64_t)blockIdx.x * round; base < n; base += (int64_t)gridDim.x * round) {
-        // SPA_U consecutive runs of the workgroup's events: ts, key, index value
+        // SPA_U runs of the workgroup's events: ts, key, index value
         int64_t tv[SPA_U], tp[SPA_U];
         int32_t key[SPA_U];
         int64_t xv[SPA_U];
@@ -673,7 +764,7 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
             if (tv[u] < tp[u]) fl |= SPA_F_TS;
             if (key[u] >= nkeys) fl |= SPA_F_KEY;
             lo[u] = hi[u] = 0;
-            if (ix_col && key[u] >= 0 && key[u] < nkeys) spa_group(RT, img, I, xv[u], &lo[u], &hi[u]);
+            if (ix_col && key[u] >= 0 && key[u] < nkeys) spa_candidates<IMG>(RT, I, S, img, xv[u], &lo[u], &hi[u]);
         }
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
@@ -681,9 +772,8 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
             if (key[u] < 0 || key[u] >= nkeys) continue;
             const uint32_t nsel = hi[u] - lo[u], total = nsel + n_free;
             for (uint32_t k = 0; k < total; k++) {
-                const uint32_t r = k < nsel ? RT->ix_rule[lo[u] + k] : RT->free_rule[k - nsel];
-                const shr_rule* R = RT->rules + r;
-                if (!rule_terms(R->t[0], R->nt[0], (uint32_t)p, SHD_NULL_ROW, C)) continue;
+                const uint32_t r = spa_rule_id<IMG>(RT, I, S, lo[u], k, nsel);
+                if (!spa_f1<IMG>(RT, I, S, C, r, (uint32_t)p)) continue;
                 const uint32_t slot = atomicAdd(&key_cnt[key[u]], 1u);
                 const uint32_t at = atomicAdd(&s_fill, 1u);
                 if (at < SPA_BUF) {
@@ -746,20 +836,29 @@ __global__ void k_sparse_place(const uint32_t* __restrict__ pr_p, const uint32_t
     }
 }
 
-__global__ void __launch_bounds__(256) k_sparse_take(const shr_table* __restrict__ RT, const int64_t* __restrict__ ts,
-                                                     const int32_t* __restrict__ akeys, int64_t n,
-                                                     const shd_cols* __restrict__ C,
-                                                     const uint32_t* __restrict__ key_off,
-                                                     const uint32_t* __restrict__ l_p, const uint32_t* __restrict__ l_r,
-                                                     const int64_t* __restrict__ l_te, uint32_t* __restrict__ l_q) {
+template <bool IMG>
+__global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __restrict__ RT,
+                                                         const int64_t* __restrict__ ts,
+                                                         const int32_t* __restrict__ akeys, int64_t n,
+                                                         const shd_cols* __restrict__ C,
+                                                         const uint8_t* __restrict__ img, shr_img I,
+                                                         const uint32_t* __restrict__ key_off,
+                                                         const uint32_t* __restrict__ l_p,
+                                                         const uint32_t* __restrict__ l_r,
+                                                         const int64_t* __restrict__ l_te, uint32_t* __restrict__ l_q) {
+    extern __shared__ uint4 s_img[];
+    __shared__ const void* s_col[32];
+    spa_stage<IMG>(img, I, C, s_img, s_col);
+    __syncthreads();
+    const SpaRules S{(const uint8_t*)s_img, img, s_col};
     // SPA_U events per thread and round: their key, list bounds and first list
     // entry are loaded together (three dependent random reads per event otherwise)
-    const int64_t round = (int64_t)blockDim.x * SPA_U;
+    const int64_t round = (int64_t)SPA_TPB * SPA_U;
     for (int64_t base = (int64_t)blockIdx.x * round; base < n; base += (int64_t)gridDim.x * round) {
         int32_t key[SPA_U];
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
-            const int64_t q = base + (int64_t)u * blockDim.x + threadIdx.x;
+            const int64_t q = base + (int64_t)u * SPA_TPB + threadIdx.x;
             key[u] = q < n ? akeys[q] : -1;
         }
         uint32_t lo[SPA_U], hi[SPA_U];
@@ -774,13 +873,12 @@ __global__ void __launch_bounds__(256) k_sparse_take(const shr_table* __restrict
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
             if (lo[u] == hi[u]) continue;
-            const int64_t q = base + (int64_t)u * blockDim.x + threadIdx.x;
+            const int64_t q = base + (int64_t)u * SPA_TPB + threadIdx.x;
             const int64_t tq = ts[q];
             for (uint32_t pos = lo[u]; pos < hi[u]; pos++) {
                 const uint32_t p = l_p[pos];
                 if ((int64_t)p >= q || tq > l_te[pos]) continue;
-                const shr_rule* R = RT->rules + l_r[pos];
-                if (rule_terms(R->t[1], R->nt[1], p, (uint32_t)q, C)) atomicMin(&l_q[pos], (uint32_t)q);
+                if (spa_f2<IMG>(RT, I, S, C, l_r[pos], p, (uint32_t)q)) atomicMin(&l_q[pos], (uint32_t)q);
             }
         }
     }
@@ -815,24 +913,46 @@ __global__ void __launch_bounds__(256) k_sparse_rec(const uint32_t* __restrict__
     }
 }
 
+// a sparse kernel with the rule image in LDS: its dynamic LDS limit raised once
+template <typename K>
+static bool spa_img_attr(K* kern, int extra) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               SHR_IMG_MAX) == hipSuccess &&
+           extra >= 0;
+}
+
+// the rule image fits LDS beside `static_lds` bytes of a kernel's own arrays
+static bool spa_img_fits(const uint8_t* img, const shr_img* I, int static_lds) {
+    return img && I && I->bytes > 0 && I->lds + static_lds + 256 <= 160 * 1024;
+}
+
 extern "C" int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int32_t* akeys, int64_t n, int32_t nkeys,
                                const shd_cols* dC, const uint8_t* img, const shr_img* I, uint32_t* pr_p,
                                uint32_t* pr_r, uint32_t* pr_key, uint32_t* pr_slot, uint32_t* key_cnt,
                                unsigned long long* ctr, int64_t cap, int32_t* flag, void* stream) {
     shr_img none;
     memset(&none, 0, sizeof(none));
-    const bool use_img = img && I && I->bytes > 0;
+    const int buf = 4 * SPA_BUF * 4 + 512;
+    const bool use_img = spa_img_fits(img, I, buf) && !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0');
+    static const bool attr = spa_img_attr(&k_sparse_open<true>, 0);
     int64_t g = (n + SPA_TPB * SPA_U - 1) / (SPA_TPB * SPA_U);
-    if (g > 512) g = 512;  // 2 per CU (64 KB of LDS each), striding over the run (few buffer flushes)
+    const int per_cu = use_img ? (160 * 1024) / (I->lds + buf) : (160 * 1024) / buf;
+    const int64_t gmax = 256LL * std::max(1, std::min(per_cu, 2));
+    if (g > gmax) g = gmax;  // each workgroup strides over the run (the image staged once, few buffer flushes)
     if (g < 1) g = 1;
-    hipLaunchKernelGGL(k_sparse_open, dim3((unsigned)g), dim3(SPA_TPB), 0, (hipStream_t)stream, dT, ts, akeys, n, nkeys,
-                       dC, use_img ? img : (const uint8_t*)nullptr, use_img ? *I : none, pr_p, pr_r, pr_key, pr_slot,
-                       key_cnt, ctr, cap, flag);
+    if (use_img && attr)
+        hipLaunchKernelGGL(k_sparse_open<true>, dim3((unsigned)g), dim3(SPA_TPB), (size_t)I->lds, (hipStream_t)stream, dT,
+                           ts, akeys, n, nkeys, dC, img, *I, pr_p, pr_r, pr_key, pr_slot, key_cnt, ctr, cap, flag);
+    else
+        hipLaunchKernelGGL(k_sparse_open<false>, dim3((unsigned)g), dim3(SPA_TPB), 0, (hipStream_t)stream, dT, ts, akeys,
+                           n, nkeys, dC, img && I && I->bytes > 0 ? img : (const uint8_t*)nullptr,
+                           img && I && I->bytes > 0 ? *I : none, pr_p, pr_r, pr_key, pr_slot, key_cnt, ctr, cap,
+                           flag);
     return rules_ok();
 }
 
 extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const int32_t* akeys, int64_t n,
-                                const shd_cols* dC, const uint32_t* pr_p, const uint32_t* pr_r,
+                                const shd_cols* dC, const uint8_t* img, const shr_img* I, const uint32_t* pr_p, const uint32_t* pr_r,
                                 const uint32_t* pr_key, const uint32_t* pr_slot, const unsigned long long* ctr,
                                 int64_t n_pairs_max, const uint32_t* key_off, uint32_t* l_p, uint32_t* l_r,
                                 int64_t* l_te, uint32_t* l_q, uint32_t* rec_p, uint32_t* rec_q, uint32_t* rec_r,
@@ -841,10 +961,25 @@ extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const in
     const unsigned gp = rgrid(n_pairs_max);
     hipLaunchKernelGGL(k_sparse_place, dim3(gp), dim3(RTPB), 0, st, pr_p, pr_r, pr_key, pr_slot, ctr, key_off, dT, ts,
                        l_p, l_r, l_te, l_q);
-    const int64_t tg = (n + 256 * SPA_U - 1) / (256 * SPA_U);
-    hipLaunchKernelGGL(k_sparse_take, dim3((unsigned)(tg < 4096 ? (tg < 1 ? 1 : tg) : 4096)), dim3(256), 0, st, dT, ts,
-                       akeys, n, dC,
-                       key_off, (const uint32_t*)l_p, (const uint32_t*)l_r, (const int64_t*)l_te, l_q);
+    {
+        shr_img none;
+        memset(&none, 0, sizeof(none));
+        const bool use_img = spa_img_fits(img, I, 512) && !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0');
+        static const bool attr = spa_img_attr(&k_sparse_take<true>, 0);
+        int64_t tg = (n + SPA_TPB * SPA_U - 1) / (SPA_TPB * SPA_U);
+        const int per_cu = use_img ? (160 * 1024) / (I->lds + 512) : 2;
+        const int64_t gmax = 256LL * std::max(1, std::min(per_cu, 2));
+        if (tg > gmax) tg = gmax;
+        if (tg < 1) tg = 1;
+        if (use_img && attr)
+            hipLaunchKernelGGL(k_sparse_take<true>, dim3((unsigned)tg), dim3(SPA_TPB), (size_t)I->lds, st, dT, ts, akeys,
+                               n, dC, img, *I, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
+                               (const int64_t*)l_te, l_q);
+        else
+            hipLaunchKernelGGL(k_sparse_take<false>, dim3((unsigned)tg), dim3(SPA_TPB), 0, st, dT, ts, akeys, n, dC,
+                               (const uint8_t*)nullptr, none, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
+                               (const int64_t*)l_te, l_q);
+    }
     hipLaunchKernelGGL(k_sparse_rec, dim3(gp), dim3(256), 0, st, (const uint32_t*)l_p, (const uint32_t*)l_r,
                        (const uint32_t*)l_q, ctr, rec_p, rec_q, rec_r, rctr, rcap);
     return rules_ok();
