@@ -96,9 +96,6 @@ static int nf_sev_ready(sh_handle* h, int64_t events, bool zero = true) {
     return hipMemsetAsync(h->n_sev_ctr.p, 0, 8, h->stream) == hipSuccess ? 0 : SH_E_HIP;
 }
 
-// the counter block's record counter, error word and history counter, zeroed at once
-static void nf_ctl_zero(sh_handle* h) { hipMemsetAsync(h->n_ctl.p, 0, 24, h->stream); }
-
 // replay the launch's getState history on the host models and upload the
 // changed ranks (before the next due scan, on the same stream)
 // pin_rd slots of the counter block read back after a launch (nf_ctl_read)
@@ -492,6 +489,17 @@ static int nf_place_deferred(sh_handle* h, int64_t n_idx, int64_t nrec) {
         }
     }
     if (h->df_ub == 0) hipMemsetAsync(h->df_ctr.p, 0, 8, st);
+    static const bool multi = getenv("SH_PLACE_MULTI") != nullptr;
+    if (nrec <= 8192 && n_idx <= 8192 && !multi) {
+        // one workgroup: scan, map, gather and the row count in one launch
+        if (nfd_place_app_small(h->n_recs.as<uint64_t>(), nrec, NF_REC_HDR + no, h->w_cnt.as<uint32_t>(), n_idx, no,
+                                h->df_ctr.as<unsigned long long>(), h->df_q.as<int32_t>(), h->df_seq.as<uint64_t>(),
+                                h->df_ts.as<int64_t>(), h->df_vals.as<int64_t>(), h->df_nulls.as<uint8_t>(), st))
+            return fail(h, SH_E_HIP, "placement");
+        h->df_ub += nrec;
+        h->df_stream = st;
+        return SH_OK;
+    }
     if (shd_exclusive_scan(h->w_cnt.as<uint32_t>(), h->w_off.as<uint32_t>(), n_idx, h->w_scan.as<uint32_t>(), st))
         return fail(h, SH_E_HIP, "scan");
     if (h->w_inv.ensure_fresh(nrec * 4)) return fail(h, SH_E_OOM, "placement index");
@@ -731,8 +739,7 @@ int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& c
             nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, seg_list, nseg, skeys, max_seg, h->n_save.as<uint64_t>(),
                      0, st);
         }
-        hipMemsetAsync(h->w_cnt.p, 0, n_idx * 4, st);
-        nf_ctl_zero(h);
+        nfd_zero2(h->w_cnt.p, n_idx * 4, h->n_ctl.p, 24, st);  // match counts + counter block
         if (nf_lst_ready(h)) return fail(h, SH_E_OOM, "list values");
         if (h->has_lists && (cols.lst != h->n_lst.as<uint64_t>() || cols.lst_cap != (uint64_t)h->lst_cap)) {
             cols.lst = h->n_lst.as<uint64_t>();
@@ -894,16 +901,17 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
             if (nkeys > 0) {
                 // due keys
                 if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");
-                hipMemsetAsync(h->n_ctr.p, 0, 8, st);
                 const uint64_t* rank =
                     h->sm_on && !host_stamps ? h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>() : nullptr;
-                if (armed_flags(h) && h->n_arm_log.p) {
+                const bool list_pass = armed_flags(h) && h->n_arm_log.p;
+                if (!(list_pass && first_pass)) hipMemsetAsync(h->n_ctr.p, 0, 8, st);
+                if (list_pass) {
                     // the armed-key list (+ the keys armed since the last pass on the
                     // first scheduler's pass, which also rebuilds the list)
                     unsigned long long* ln = h->n_klist_n.as<unsigned long long>();
                     const int c = h->klist_cur;
                     if (first_pass) {
-                        hipMemsetAsync(ln + (c ^ 1), 0, 8, st);
+                        nfd_zero2(h->n_ctr.p, 8, ln + (c ^ 1), 8, st);  // candidates + the next list's count
                         nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
                                      ln + c, h->n_arm_log.as<int32_t>(), h->n_arm_ctr.as<unsigned long long>(), now,
                                      h->n_cand.as<nfd_cand>(), h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h),
@@ -1050,8 +1058,7 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
             for (int attempt = 0;; attempt++) {
                 if (attempt > 64) return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
                 const size_t kw = (size_t)h->T->key_words;
-                hipMemsetAsync(h->w_cnt.p, 0, (size_t)n_idx * 4, st);
-                nf_ctl_zero(h);
+                nfd_zero2(h->w_cnt.p, (int64_t)n_idx * 4, h->n_ctl.p, 24, st);  // match counts + counter block
                 {
                     const void* lst0 = h->n_lst.p;
                     if (nf_lst_ready(h)) return fail(h, SH_E_OOM, "list values");

@@ -21,6 +21,7 @@
 
 #include "sh_nfa.h"
 #include "sh_nfa_dev.h"
+#include "sh_wave.h"
 
 #define NF_TPB 128
 #define NF_SINK_CHUNK 16
@@ -986,6 +987,95 @@ __global__ void __launch_bounds__(256) k_nfa_gather_app(const uint64_t* __restri
 __global__ void k_nfa_app_bump(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt, int64_t n_idx,
                                unsigned long long* __restrict__ base) {
     *base += (unsigned long long)off[n_idx - 1] + cnt[n_idx - 1];
+}
+
+// two device ranges zeroed in one launch (4-byte multiples): a launch's match
+// counts and counter block, or the due pass's counters
+__global__ void k_zero2(uint32_t* __restrict__ a, int64_t na, uint32_t* __restrict__ b, int64_t nb) {
+    const int64_t n = na > nb ? na : nb;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i < na) a[i] = 0u;
+        if (i < nb) b[i] = 0u;
+    }
+}
+
+extern "C" int nfd_zero2(void* a, int64_t abytes, void* b, int64_t bbytes, void* stream) {
+    const int64_t na = abytes / 4, nb = bbytes / 4, n = na > nb ? na : nb;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_zero2, dim3(nf_blocks(n, 256) < 1024 ? nf_blocks(n, 256) : 1024), dim3(256), 0,
+                       (hipStream_t)stream, (uint32_t*)a, na, (uint32_t*)b, nb);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// the same appended placement for a small launch in ONE workgroup: the counts'
+// scan, the row -> record map and the gather in LDS, the row counter bumped at the
+// end (one launch instead of scan, fill, map, gather and bump)
+#define NF_PS_TPB 1024
+#define NF_PS_MAX 8192
+__global__ void __launch_bounds__(NF_PS_TPB) k_nfa_place_small(const uint64_t* __restrict__ recs, int nrec,
+                                                              int stride, const uint32_t* __restrict__ counts,
+                                                              int n_idx, int n_out, unsigned long long* __restrict__ base,
+                                                              int32_t* __restrict__ out_query,
+                                                              uint64_t* __restrict__ out_seq,
+                                                              int64_t* __restrict__ out_ts,
+                                                              int64_t* __restrict__ out_vals,
+                                                              uint8_t* __restrict__ out_nulls) {
+    __shared__ uint32_t off[NF_PS_MAX];
+    __shared__ uint32_t inv[NF_PS_MAX];
+    __shared__ uint32_t ws[NF_PS_TPB / 64];
+    constexpr int PER = NF_PS_MAX / NF_PS_TPB;
+    const int i0 = (int)threadIdx.x * PER;
+    uint32_t c[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        c[k] = i0 + k < n_idx ? counts[i0 + k] : 0u;
+        sum += c[k];
+    }
+    uint32_t total;
+    uint32_t o = shw_block_excl<NF_PS_TPB>(sum, ws, &total);
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        off[i0 + k] = o;
+        o += c[k];
+    }
+    for (uint32_t d = threadIdx.x; d < total; d += NF_PS_TPB) inv[d] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nrec; i += NF_PS_TPB) {
+        const uint64_t tag = recs[(int64_t)i * stride];
+        if (tag == ~0ull) continue;
+        const uint32_t d = off[(uint32_t)tag] + (uint32_t)(tag >> 32);
+        if (d < total) inv[d] = (uint32_t)i;
+    }
+    __syncthreads();
+    const int64_t b0 = (int64_t)*base;
+    for (uint32_t d = threadIdx.x; d < total; d += NF_PS_TPB) {
+        const uint32_t ix = inv[d];
+        if (ix >= (uint32_t)nrec) continue;
+        const int64_t o2 = b0 + d;
+        const uint64_t* r = recs + (int64_t)ix * stride;
+        const uint64_t h2 = r[2];
+        out_query[o2] = (int)(h2 >> 32);
+        out_seq[o2] = r[3];
+        out_ts[o2] = (int64_t)r[1];
+        for (int cc = 0; cc < n_out; cc++) {
+            const bool has = cc < stride - NF_REC_HDR;
+            out_vals[o2 * n_out + cc] = has ? (int64_t)r[NF_REC_HDR + cc] : 0;
+            out_nulls[o2 * n_out + cc] = has ? (uint8_t)((h2 >> cc) & 1) : 1;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *base = (unsigned long long)(b0 + total);
+}
+
+extern "C" int nfd_place_app_small(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* counts,
+                                   int64_t n_idx, int n_out, unsigned long long* base, int32_t* out_query,
+                                   uint64_t* out_seq, int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls,
+                                   void* stream) {
+    if (nrec > NF_PS_MAX || n_idx > NF_PS_MAX) return -1;
+    if (nrec <= 0 || n_idx <= 0) return 0;
+    hipLaunchKernelGGL(k_nfa_place_small, dim3(1), dim3(NF_PS_TPB), 0, (hipStream_t)stream, recs, (int)nrec, stride,
+                       counts, (int)n_idx, n_out, base, out_query, out_seq, out_ts, out_vals, out_nulls);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 extern "C" int nfd_place_app(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets,

@@ -90,6 +90,13 @@ int nfd_timer(const nf_table* dT, const nf_cols* dC, uint64_t* kstate, int q, in
 int nfd_place(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets, int n_out, int32_t* out_query,
               uint64_t* out_seq, int64_t* out_ts, int64_t* out_vals, uint8_t* out_nulls, uint32_t* inv, int64_t total,
               void* stream);
+// [a, a + abytes) and [b, b + bbytes) zeroed in one launch (4-byte multiples)
+int nfd_zero2(void* a, int64_t abytes, void* b, int64_t bbytes, void* stream);
+// the same for a launch of at most 8,192 records and events, in one workgroup
+// (-1: too large, use nfd_place_app)
+int nfd_place_app_small(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* counts, int64_t n_idx,
+                        int n_out, unsigned long long* base, int32_t* out_query, uint64_t* out_seq, int64_t* out_ts,
+                        int64_t* out_vals, uint8_t* out_nulls, void* stream);
 // nfd_place appended to device-resident output arrays after *base rows (count on the device)
 int nfd_place_app(const uint64_t* recs, int64_t nrec, int stride, const uint32_t* offsets, const uint32_t* counts,
                   int64_t n_idx, int n_out, unsigned long long* base, int32_t* out_query, uint64_t* out_seq,
