@@ -913,12 +913,23 @@ __global__ void __launch_bounds__(256) k_sparse_rec(const uint32_t* __restrict__
     }
 }
 
-// a sparse kernel with the rule image in LDS: its dynamic LDS limit raised once
+// a sparse kernel with the rule image in LDS: its dynamic LDS limit raised once, to
+// what its static arrays leave of the CU's 160 KB (a failed call is cleared, so it
+// does not surface as the next launch's error)
 template <typename K>
-static bool spa_img_attr(K* kern, int extra) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               SHR_IMG_MAX) == hipSuccess &&
-           extra >= 0;
+static int spa_img_attr(K* kern) {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern)) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    const int lim = std::min<int>(SHR_IMG_MAX, 160 * 1024 - (int)fa.sharedSizeBytes);
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lim) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return lim;
 }
 
 // the rule image fits LDS beside `static_lds` bytes of a kernel's own arrays
@@ -933,14 +944,15 @@ extern "C" int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int
     shr_img none;
     memset(&none, 0, sizeof(none));
     const int buf = 4 * SPA_BUF * 4 + 512;
-    const bool use_img = spa_img_fits(img, I, buf) && !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0');
-    static const bool attr = spa_img_attr(&k_sparse_open<true>, 0);
+    static const int lim = spa_img_attr(&k_sparse_open<true>);
+    const bool use_img = spa_img_fits(img, I, buf) && I->lds <= lim &&
+                         !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0');
     int64_t g = (n + SPA_TPB * SPA_U - 1) / (SPA_TPB * SPA_U);
     const int per_cu = use_img ? (160 * 1024) / (I->lds + buf) : (160 * 1024) / buf;
     const int64_t gmax = 256LL * std::max(1, std::min(per_cu, 2));
     if (g > gmax) g = gmax;  // each workgroup strides over the run (the image staged once, few buffer flushes)
     if (g < 1) g = 1;
-    if (use_img && attr)
+    if (use_img)
         hipLaunchKernelGGL(k_sparse_open<true>, dim3((unsigned)g), dim3(SPA_TPB), (size_t)I->lds, (hipStream_t)stream, dT,
                            ts, akeys, n, nkeys, dC, img, *I, pr_p, pr_r, pr_key, pr_slot, key_cnt, ctr, cap, flag);
     else
@@ -964,14 +976,15 @@ extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const in
     {
         shr_img none;
         memset(&none, 0, sizeof(none));
-        const bool use_img = spa_img_fits(img, I, 512) && !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0');
-        static const bool attr = spa_img_attr(&k_sparse_take<true>, 0);
+        static const int lim = spa_img_attr(&k_sparse_take<true>);
+        const bool use_img = spa_img_fits(img, I, 512) && I->lds <= lim &&
+                             !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0');
         int64_t tg = (n + SPA_TPB * SPA_U - 1) / (SPA_TPB * SPA_U);
         const int per_cu = use_img ? (160 * 1024) / (I->lds + 512) : 2;
         const int64_t gmax = 256LL * std::max(1, std::min(per_cu, 2));
         if (tg > gmax) tg = gmax;
         if (tg < 1) tg = 1;
-        if (use_img && attr)
+        if (use_img)
             hipLaunchKernelGGL(k_sparse_take<true>, dim3((unsigned)tg), dim3(SPA_TPB), (size_t)I->lds, st, dT, ts, akeys,
                                n, dC, img, *I, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
                                (const int64_t*)l_te, l_q);
