@@ -265,9 +265,8 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
 //     t + 64, ... (consecutive lanes, consecutive rows: coalesced stores); the
 //     consumer-side values are read by arrival index, the e1-side values from
 //     the match stream
-#define BK_EHALF 256   // events of one row-map pass of a wave (4 of its 64-event rounds)
-#define BK_EROWS 512   // rows the wave's map holds per pass (more: event-parallel writes)
-#define BK_EJ (BK_EHALF / 64)
+#define BK_EHALF 512   // events of one row-map pass of a wave
+#define BK_EROWS 1024  // rows the wave's map holds per pass (more: event-parallel writes)
 
 // select value o of a row (raw 8-byte form)
 #define BK_VAL(o, i, mp) bk_raw(O.src[o], O.kind[o] == 1 ? (i) : (mp), O.type[o])
@@ -333,16 +332,13 @@ __device__ __forceinline__ void bk_store(const shb_cols& OC, int64_t row, const 
     }
 }
 
-#define BK_RU 2  // rows per lane whose loads are issued before their stores
+#define BK_RU 4  // rows per lane whose loads are issued before their stores
 
 template <bool COLS, int NO>
-__global__ void __launch_bounds__(BK_TPB, 6) k_bk_emit(shb_plan P, shb_out O, shb_cols OC, uint64_t seq_base,
+__global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, shb_cols OC, uint64_t seq_base,
                                                     uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_vals,
                                                     int64_t out_cap) {
-    // the counts' prefix in the tile's bucket order, mod 2^16: exact for the two uses,
-    // a count (< 256) and the rows of a (tile, bucket) segment before an event (a
-    // segment belongs to one matcher pass, whose matches are <= SHB_SPAN)
-    __shared__ uint16_t pfx[SHB_TILE + 1];
+    __shared__ uint32_t pfx[SHB_TILE + 1];
     __shared__ uint32_t ms0[SHB_NB];
     __shared__ uint16_t to[SHB_NB + 1];
     __shared__ uint32_t wtot[BK_TPB / 64], ws[BK_TPB / 64];
@@ -401,10 +397,10 @@ __global__ void __launch_bounds__(BK_TPB, 6) k_bk_emit(shb_plan P, shb_out O, sh
         uint32_t off = shw_block_excl<BK_TPB>(sum, ws, &tot);
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-            pfx[s0 + k] = (uint16_t)off;
+            pfx[s0 + k] = off;
             off += c[k];
         }
-        if (threadIdx.x == 0) pfx[SHB_TILE] = (uint16_t)tot;
+        if (threadIdx.x == 0) pfx[SHB_TILE] = tot;
         __syncthreads();
     }
     // 2. counts (4 packed per register) and match-stream positions of the wave's events
@@ -419,8 +415,8 @@ __global__ void __launch_bounds__(BK_TPB, 6) k_bk_emit(shb_plan P, shb_out O, sh
             const uint32_t d = (uint32_t)kk[j] & (SHB_NB - 1);
             const uint32_t s = sl[j];
             const uint32_t ps = pfx[s];
-            c = (uint32_t)(uint16_t)(pfx[s + 1] - ps);
-            mp[j] = ms0[d] + (uint32_t)(uint16_t)(ps - pfx[to[d]]);
+            c = pfx[s + 1] - ps;
+            mp[j] = ms0[d] + ps - pfx[to[d]];
         }
         if ((j & 3) == 0) cp[j >> 2] = 0u;
         cp[j >> 2] |= c << (8 * (j & 3));
@@ -433,14 +429,14 @@ __global__ void __launch_bounds__(BK_TPB, 6) k_bk_emit(shb_plan P, shb_out O, sh
     __syncthreads();
     uint64_t rb = s_tb;  // this wave's first row
     for (int q = 0; q < w; q++) rb += wtot[q];
-    // 3. rows, BK_EHALF events at a time
+    // 3. rows, one half (512 events) at a time
 #pragma unroll
-    for (int hf = 0; hf < BK_ITEMS / BK_EJ; hf++) {
+    for (int hf = 0; hf < BK_ITEMS / 8; hf++) {
         uint32_t carry = 0;
-        uint32_t ro8[BK_EJ];
+        uint32_t ro8[8];
 #pragma unroll
-        for (int jj = 0; jj < BK_EJ; jj++) {
-            const int j = hf * BK_EJ + jj;
+        for (int jj = 0; jj < 8; jj++) {
+            const int j = hf * 8 + jj;
             const uint32_t c = (cp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
             const uint32_t incl = shw_incl_scan(c);
             const uint32_t ro = carry + incl - c;
@@ -497,8 +493,8 @@ __global__ void __launch_bounds__(BK_TPB, 6) k_bk_emit(shb_plan P, shb_out O, sh
         } else {
             // a dense half (more rows than the map holds): each event writes its rows
 #pragma unroll
-            for (int jj = 0; jj < BK_EJ; jj++) {
-                const int j = hf * BK_EJ + jj;
+            for (int jj = 0; jj < 8; jj++) {
+                const int j = hf * 8 + jj;
                 const uint32_t c = (cp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
                 const int64_t i = ib + jj * 64 + lane;
                 for (uint32_t k = 0; k < c; k++) {
