@@ -769,6 +769,7 @@ int sh_compile(const sh_app_desc* app, sh_handle** out) {
 
 void sh_destroy(sh_handle* h) {
     if (!h) return;
+    if (h->mode == 1 && h->pend.on) nf_settle(h);
     nf_hist_stop(h);
     if (getenv("SH_HOST_PROF") && h->hp_n[0]) {
         static const char* names[SH_HP_N] = {"push",      "timers",     "process",   "history",
@@ -868,6 +869,10 @@ static int push_impl(sh_handle* h, const sh_batch* b, const uint32_t* index, int
     bool caller_copy = false;  // a copy reads the caller's memory directly (null masks)
     for (size_t a = 0; a < types.size(); a++) {
         const int w = type_width(types[a]);
+        if ((size_t)(r0 + b->n) * w > st.cols[a].bytes && h->mode == 1) {
+            const int src = nf_settle(h);  // (the store moves: a pending launch reads it)
+            if (src) return src;
+        }
         if (st.cols[a].ensure((size_t)(r0 + b->n) * w)) return fail(h, SH_E_OOM, "column store");
         // through pinned staging (the sync below completes the copy before reuse)
         memcpy(h->pin_in.as<void>(pin_off), b->cols[a], (size_t)b->n * w);
@@ -877,7 +882,11 @@ static int push_impl(sh_handle* h, const sh_batch* b, const uint32_t* index, int
         const uint8_t* nm = b->nulls ? b->nulls[a] : nullptr;
         if (nm || st.has_nul[a]) {
             if (!st.has_nul[a]) {
-                if (st.nuls[a].ensure((size_t)(r0 + b->n))) return fail(h, SH_E_OOM, "null mask");
+                if ((size_t)(r0 + b->n) > st.nuls[a].bytes && h->mode == 1) {
+                const int src = nf_settle(h);
+                if (src) return src;
+            }
+            if (st.nuls[a].ensure((size_t)(r0 + b->n))) return fail(h, SH_E_OOM, "null mask");
                 hipMemsetAsync(st.nuls[a].p, 0, r0, h->stream);
                 st.has_nul[a] = true;
             } else if (st.nuls[a].ensure((size_t)(r0 + b->n))) {
@@ -931,7 +940,8 @@ int sh_set_coordinator(sh_handle* h, const sh_coordinator* c) {
 int sh_set_partition_keys(sh_handle* h, int32_t first_key, int32_t n, const uint16_t* utf16, const int64_t* offsets) {
     if (!h || first_key < 0 || n < 0 || (n && (!utf16 || !offsets))) return SH_E_INVALID_ARG;
     if (h->mode == 1) {
-        const int frc = nf_sev_flush(h);  // (the replay thread reads the key strings)
+        int frc = nf_settle(h);
+        if (!frc) frc = nf_sev_flush(h);  // (the replay thread reads the key strings)
         if (frc) return frc;
     }
     h->sm.set_keys(first_key, n, utf16, offsets);
@@ -1152,7 +1162,10 @@ static shd_cols store_cols(sh_handle* h) {
 
 // process every staged event
 int flush(sh_handle* h) {
-    if (h->mode == 1) return nf_app_pull(h);  // the general engine processes each send() at once
+    if (h->mode == 1) {  // the general engine processes each send() at once
+        const int src = nf_settle(h);  // (a push's launch may still be pending)
+        return src ? src : nf_app_pull(h);
+    }
     const int64_t n = (int64_t)h->st_ts.size();
     if (n == 0) return SH_OK;
     if (!h->has_device) return fail(h, SH_E_NO_DEVICE, "no HIP device");
@@ -1562,6 +1575,10 @@ static int run_device_entry(sh_handle* h, sh_device_run* user, bool v2) {
     if (h && h->poisoned) return fail(h, SH_E_INVALID_ARG, "handle unusable after a failed restore");
     if (!h || !user) return SH_E_INVALID_ARG;
     if (h->has_lists) return fail(h, SH_E_UNSUPPORTED, "List (multi-value) outputs come back through sh_drain");
+    if (h->mode == 1) {
+        const int src = nf_settle(h);  // a streaming push's launch, on the handle's own stream
+        if (src) return src;
+    }
     // a V1 caller's struct ends before `version`: only its prefix is read
     // the run borrows the caller's stream; the handle's own stream is back for
     // every later call (push, advance, drain), whatever path this one leaves by

@@ -123,6 +123,27 @@ using shh::PinBuf;
 using shh::type_width;
 
 #define SH_HP_N 12
+// one k_nfa_run launch of the general engine: what its completion and any replay
+// need (sh_host_nfa.cpp nf_launch / nf_complete); a streaming push leaves it
+// pending (on) until the next call into the handle settles it
+struct NfLaunch {
+    bool on = false;
+    shd_batch B{};
+    nfd_events E{};
+    nf_cols cols{};
+    int64_t n = 0, n_idx = 0, max_seg = 0, cap = 0;
+    int32_t nkeys = 0;
+    const uint32_t* seg_list = nullptr;
+    const uint32_t* nseg = nullptr;
+    const uint32_t* skeys = nullptr;
+    bool fresh = false, sorted_cols = false, s3_shape = false;
+    int alias = -1;
+    const void* s3_col = nullptr;
+    uint64_t* d_seq = nullptr;
+    int64_t* d_vals = nullptr;
+    int attempt = 0;
+};
+
 struct sh_handle {
     std::string err;
     bool has_device = false;
@@ -153,7 +174,9 @@ struct sh_handle {
     uint64_t seq_staged0 = 0;
     // workspaces
     DevBuf w_ts, w_stream, w_row, w_key, w_keys_a, w_keys_b, w_idx_a, w_idx_b, w_hist, w_scan, w_seg;
-    DevBuf w_pstage;  // the general engine's per-call staging (nf_push), one block
+    DevBuf w_pstage, w_pstage2;  // the general engine's per-call staging (nf_push), one block; two
+    int pst = 0;                 // alternate per call (a call's launch may still read the last one)
+    NfLaunch pend;               // a streaming push's launch not yet completed (nf_settle)
     DevBuf w_orows;   // placed rows of a streaming launch, one block (query | seq | ts | values | nulls)
     DevBuf w_cnt, w_off, w_tmp, w_ctr, w_oseq, w_ots, w_ovals, w_onulls, w_oq, w_inv;
     bool dev_want_query = false;  // sh_run_device asked for d_out_query
@@ -204,7 +227,7 @@ struct sh_handle {
     // pinned staging of the streaming path: pin_in = one send() call's uploads,
     // pin_rd = small read-backs + the nf_cols image, pin_out = placed rows
     PinBuf pin_in, pin_rd, pin_out;
-    PinBuf pin_stage;  // the general engine's per-call event staging (nf_push)
+    PinBuf pin_stage, pin_stage2;  // the general engine's per-call event staging (nf_push), alternating
     DevBuf n_tmin, n_slot_s, n_slot_k;  // device tie-break of due keys
     DevBuf n_armed;                     // per key: may hold a scheduler entry (nf_cols.sched_armed)
     // the armed-key list of the due pass (two buffers, swapped per pass; counts
@@ -319,7 +342,11 @@ struct HpScope {
     sh_handle* h;
     int i;
     std::chrono::steady_clock::time_point t0;
-    HpScope(sh_handle* hh, int ii) : h(getenv("SH_HOST_PROF") ? hh : nullptr), i(ii) {
+    static bool on() {
+        static const bool v = getenv("SH_HOST_PROF") != nullptr;  // (read once per process)
+        return v;
+    }
+    HpScope(sh_handle* hh, int ii) : h(on() ? hh : nullptr), i(ii) {
         if (h) t0 = std::chrono::steady_clock::now();
     }
     ~HpScope() {
@@ -344,6 +371,9 @@ int ensure_ws(sh_handle* h, int64_t n);
 int fail(sh_handle* h, int code, const std::string& m);
 int flush(sh_handle* h);
 // sh_host_nfa.cpp
+int nf_launch(sh_handle* h, NfLaunch& L);
+int nf_complete(sh_handle* h, NfLaunch& L, int64_t* n_rows);
+int nf_settle(sh_handle* h);
 int nf_app_pull(sh_handle* h);
 int nf_ensure_keys(sh_handle* h, int32_t nkeys);
 int nf_next_due(sh_handle* h, int64_t* out);

@@ -732,47 +732,95 @@ int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& c
     E.pad = 0;
     E.run = fresh ? h->dev_run_ids : nullptr;
     E.gidx = gidx;
-    for (int attempt = 0; attempt < 64; attempt++) {
-        const size_t kw = (size_t)h->T->key_words;
-        if (!fresh) {
-            if (h->n_save.ensure_fresh((size_t)max_seg * kw * 8)) return fail(h, SH_E_OOM, "save area");
-            nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, seg_list, nseg, skeys, max_seg, h->n_save.as<uint64_t>(),
-                     0, st);
-        }
-        nfd_zero2(h->w_cnt.p, n_idx * 4, h->n_ctl.p, 24, st);  // match counts + counter block
-        if (nf_lst_ready(h)) return fail(h, SH_E_OOM, "list values");
-        if (h->has_lists && (cols.lst != h->n_lst.as<uint64_t>() || cols.lst_cap != (uint64_t)h->lst_cap)) {
-            cols.lst = h->n_lst.as<uint64_t>();
-            cols.lst_ctr = h->n_lst_ctr.as<unsigned long long>();
-            cols.lst_cap = (uint64_t)h->lst_cap;
+    NfLaunch& L = h->pend;
+    L = NfLaunch{};
+    L.B = B;
+    L.E = E;
+    L.cols = cols;
+    L.n = n;
+    L.n_idx = n_idx;
+    L.nkeys = nkeys;
+    L.max_seg = max_seg;
+    L.seg_list = seg_list;
+    L.nseg = nseg;
+    L.skeys = skeys;
+    L.fresh = fresh;
+    L.sorted_cols = sorted_cols;
+    L.alias = alias;
+    L.s3_shape = s3_shape;
+    L.s3_col = s3_col;
+    L.d_seq = d_seq;
+    L.d_vals = d_vals;
+    L.cap = cap;
+    // a streaming push (single process, host rows) leaves the launch's completion --
+    // its error word, history and placement -- to the next call into the handle
+    // (nf_settle), so the caller prepares the next send() while this one runs
+    static const bool no_defer = getenv("SH_NO_DEFER_LAUNCH") != nullptr;
+    const bool defer = !no_defer && !d_seq && !fresh && !h->coord_on && !h->has_lists && !sorted_cols;
+    int rc = nf_launch(h, L);
+    if (rc) return rc;
+    if (defer) {
+        L.on = true;
+        *n_rows = -1;
+        return SH_OK;
+    }
+    return nf_complete(h, L, n_rows);
+}
+
+// one attempt of a k_nfa_run launch: save the touched keys, clear the counters, the
+// kernel, and the counter block (+ the first history records) read back behind it
+int nf_launch(sh_handle* h, NfLaunch& L) {
+    hipStream_t st = h->stream;
+    const size_t kw = (size_t)h->T->key_words;
+    if (!L.fresh) {
+        if (h->n_save.ensure_fresh((size_t)L.max_seg * kw * 8)) return fail(h, SH_E_OOM, "save area");
+        nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, L.seg_list, L.nseg, L.skeys, L.max_seg,
+                 h->n_save.as<uint64_t>(), 0, st);
+    }
+    nfd_zero2(h->w_cnt.p, L.n_idx * 4, h->n_ctl.p, 24, st);  // match counts + counter block
+    if (nf_lst_ready(h)) return fail(h, SH_E_OOM, "list values");
+    nf_cols& cols = L.cols;
+    if (h->has_lists && (cols.lst != h->n_lst.as<uint64_t>() || cols.lst_cap != (uint64_t)h->lst_cap)) {
+        cols.lst = h->n_lst.as<uint64_t>();
+        cols.lst_ctr = h->n_lst_ctr.as<unsigned long long>();
+        cols.lst_cap = (uint64_t)h->lst_cap;
+        nf_put_cols(h, cols);
+    }
+    if (h->sm_on) {
+        if (nf_sev_ready(h, L.n, false)) return fail(h, SH_E_OOM, "scheduler history");
+        if (cols.sev != h->n_sev.as<uint64_t>() || cols.sev_cap != (uint64_t)h->sev_cap) {
+            // the buffer moved: refresh the column image
+            const nf_cols keep = cols;
+            cols = nf_store_cols(h);
+            if (L.sorted_cols) {
+                for (size_t a = 0; a < h->stream_types[0].size(); a++)
+                    if (a >= 32 || ((h->T->attr_used[0] >> a) & 1u)) cols.col[0][a] = keep.col[0][a];
+            }
             nf_put_cols(h, cols);
         }
-        if (h->sm_on) {
-            if (nf_sev_ready(h, n, false)) return fail(h, SH_E_OOM, "scheduler history");
-            if (cols.sev != h->n_sev.as<uint64_t>() || cols.sev_cap != (uint64_t)h->sev_cap) {
-                // the buffer moved: refresh the column image
-                cols = nf_store_cols(h);
-                if (sorted_cols) {
-                    for (size_t a = 0; a < h->stream_types[0].size(); a++)
-                        if (a >= 32 || ((h->T->attr_used[0] >> a) & 1u)) cols.col[0][a] = h->v_scol[a].p;
-                    if (alias >= 0) cols.col[0][alias] = skeys;
-                }
-                nf_put_cols(h, cols);
-            }
-        }
-        nfd_emit em = nf_emit(h);
-        // the rise-and-fall sequence engine: fresh single-query runs of that shape
-        const bool seq3 = s3_shape;
-        h->seq3_last = seq3 ? 1 : 0;
-        if (seq3) {
-            if (nfd_seq3(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), &E, n, seg_list, nseg, skeys, nkeys, max_seg,
-                         &em, st, s3_col, h->s3_compact ? 1 : 0, h->s3_agg ? 1 : 0, h->s3_rw))
-                return fail(h, SH_E_HIP, "k_seq3 launch failed");
-        } else if (nfd_run(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), &E, n,
-                           seg_list, nseg, skeys, nkeys, max_seg, h->tick, h->clock, &em, st))
-            return fail(h, SH_E_HIP, "k_nfa_run launch failed");
-        hipEventRecord(h->ev[2], st);
-        nf_ctl_read(h);
+    }
+    nfd_emit em = nf_emit(h);
+    // the rise-and-fall sequence engine: fresh single-query runs of that shape
+    h->seq3_last = L.s3_shape ? 1 : 0;
+    if (L.s3_shape) {
+        if (nfd_seq3(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), &L.E, L.n, L.seg_list, L.nseg, L.skeys,
+                     L.nkeys, L.max_seg, &em, st, L.s3_col, h->s3_compact ? 1 : 0, h->s3_agg ? 1 : 0, h->s3_rw))
+            return fail(h, SH_E_HIP, "k_seq3 launch failed");
+    } else if (nfd_run(h->d_T.as<nf_table>(), h->d_ncols.as<nf_cols>(), h->n_kstate.as<uint64_t>(), &L.E, L.n,
+                       L.seg_list, L.nseg, L.skeys, L.nkeys, L.max_seg, h->tick, h->clock, &em, st))
+        return fail(h, SH_E_HIP, "k_nfa_run launch failed");
+    hipEventRecord(h->ev[2], st);
+    nf_ctl_read(h);
+    L.attempt++;
+    return SH_OK;
+}
+
+// wait for a launched attempt; on success its history and rows, else restore the
+// touched keys (or the fresh state), grow what overflowed, and launch again
+int nf_complete(sh_handle* h, NfLaunch& L, int64_t* n_rows) {
+    hipStream_t st = h->stream;
+    L.on = false;
+    for (;;) {
         if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_run");
         const unsigned err = nf_ctl_err(h);
         if (!err) {
@@ -780,10 +828,12 @@ int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& c
             const int64_t nrec = nf_ctl_nrec(h);
             int src = nf_sev_apply(h, true);
             if (src) return src;
-            int rc = nf_place(h, n_idx, n_rows, d_seq, d_vals, cap, h->tick - 1, nrec);
+            int64_t rows = 0;
+            int rc = nf_place(h, L.n_idx, &rows, L.d_seq, L.d_vals, L.cap, h->tick - 1, nrec);
+            if (n_rows) *n_rows = rows;
             hipEventElapsedTime(&h->times.segment_ms, h->ev[0], h->ev[1]);
             hipEventElapsedTime(&h->times.advance_ms, h->ev[1], h->ev[2]);
-            if (*n_rows >= 0) {
+            if (rows >= 0) {
                 hipEventRecord(h->ev[3], st);
                 nf_sync(h, st);
                 hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
@@ -792,15 +842,16 @@ int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& c
                 h->times.emit_ms = 0.0f;
                 hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[2]);
             }
-            h->times.advance_launches = attempt + 1;
+            h->times.advance_launches = L.attempt;
             return rc;
         }
         if (err & NF_E_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
         if (err & NF_E_UNSUP)
             return fail(h, SH_E_UNSUPPORTED, "CountPreStateProcessor.startStateReset recursion (reference overflows)");
-        // restore the touched keys (or the fresh state), grow, replay
-        if (!fresh)
-            nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, seg_list, nseg, skeys, max_seg,
+        if (L.attempt >= 64) return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
+        const size_t kw = (size_t)h->T->key_words;
+        if (!L.fresh)
+            nfd_save(h->n_kstate.as<uint64_t>(), (int64_t)kw, L.seg_list, L.nseg, L.skeys, L.max_seg,
                      h->n_save.as<uint64_t>(), 1, st);
         if (err & NF_E_EMIT) {
             if (nf_ensure_recs(h, h->rec_cap * 4)) return fail(h, SH_E_OOM, "emission buffer");
@@ -815,22 +866,34 @@ int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& c
             int rc = nf_grow(h, err);
             if (rc) return rc;
         }
-        if (fresh) {
-            hipMemsetAsync(h->n_kstate.p, 0, (size_t)nkeys * h->T->key_words * 8, st);
+        if (L.fresh) {
+            hipMemsetAsync(h->n_kstate.p, 0, (size_t)L.nkeys * h->T->key_words * 8, st);
             if (!h->T->partitioned) {
                 h->started = false;
                 int rc = nf_start(h);
                 if (rc) return rc;
             }
         }
+        int lrc = nf_launch(h, L);
+        if (lrc) return lrc;
     }
-    return fail(h, SH_E_STATE_OVERFLOW, "replay limit");
+}
+
+// complete a streaming push's launch left pending (see nf_process); before every
+// other use of the handle's device state
+int nf_settle(sh_handle* h) {
+    if (!h->pend.on) return SH_OK;
+    return nf_complete(h, h->pend, nullptr);
 }
 
 // earliest queued notify time over every scheduler and key (INT64_MAX: none;
 // key-sharded: over every rank)
 static int nf_next_due_local(sh_handle* h, int64_t* out) {
     *out = INT64_MAX;
+    {
+        int src = nf_settle(h);
+        if (src) return src;
+    }
     if (!h->T->has_absent || h->n_nkeys == 0) return SH_OK;
     if (nf_sev_flush(h)) return SH_E_HIP;
     hipStream_t st = h->stream;
@@ -874,6 +937,10 @@ int nf_next_due(sh_handle* h, int64_t* out) {
 // positions are global, so registration stamps and row order match one process.
 int nf_timers(sh_handle* h, int64_t now, bool wall) {
     HpScope hp_(h, 1);
+    {
+        int src = nf_settle(h);
+        if (src) return src;
+    }
     if (!h->T->has_absent) return SH_OK;
     if (h->n_nkeys == 0 && !h->coord_on) return SH_OK;
     hipStream_t st = h->stream;
@@ -1155,17 +1222,17 @@ int nf_push(sh_handle* h, const sh_batch* b, int64_t r0, const uint32_t* index, 
         int rc = nf_start(h);
         if (rc) return rc;
     }
-    if (h->app.playback) {
-        const int64_t last = index ? call_last : b->ts[b->n - 1];
-        if (last >= h->clock) {
-            h->clock = last;
-            int rc = nf_timers(h, last);
-            if (rc) return rc;
-        }
-    }
     const int64_t n = b->n;
     hipStream_t st = h->stream;
     if (index && n == 0) {
+        if (h->app.playback) {
+            const int64_t last = index ? call_last : b->ts[b->n - 1];
+            if (last >= h->clock) {
+                h->clock = last;
+                int rc = nf_timers(h, last);
+                if (rc) return rc;
+            }
+        }
         // none of the call's events is ours: the launch still ticks and its
         // (empty) scheduler history joins the others'
         if (h->sm_on && nf_sev_ready(h, 0)) return fail(h, SH_E_OOM, "scheduler history");
@@ -1175,14 +1242,23 @@ int nf_push(sh_handle* h, const sh_batch* b, int64_t r0, const uint32_t* index, 
         h->seq_staged0 = h->seq_next;
         return rc;
     }
-    // staged in pinned memory (pin_in; the column copies of this call are complete)
+    // the events are staged first (host copies and one upload), so this work overlaps
+    // the last call's launch, which the timer pass below settles
+    // staged in pinned memory (pin_in; the column copies of this call are complete);
+    // the staging buffers alternate per call: the last call's launch may still read its own
+    PinBuf& ps = h->pst ? h->pin_stage2 : h->pin_stage;
+    DevBuf& ds = h->pst ? h->w_pstage2 : h->w_pstage;
     const size_t o_ts = 0, o_rows = (size_t)n * 8, o_keys = o_rows + (size_t)n * 4, o_sv = o_keys + (size_t)n * 4;
-    if (h->pin_stage.ensure(o_sv + (size_t)n)) return fail(h, SH_E_OOM, "pinned staging");
-    uint8_t* sv = h->pin_stage.as<uint8_t>(o_sv);
-    uint32_t* rows = h->pin_stage.as<uint32_t>(o_rows);
-    int32_t* keys = h->pin_stage.as<int32_t>(o_keys);
+    if ((size_t)(o_sv + n) > ps.bytes || (size_t)(o_sv + n) > ds.bytes) {
+        int src = nf_settle(h);  // (a reallocation waits for the device)
+        if (src) return src;
+    }
+    if (ps.ensure(o_sv + (size_t)n)) return fail(h, SH_E_OOM, "pinned staging");
+    uint8_t* sv = ps.as<uint8_t>(o_sv);
+    uint32_t* rows = ps.as<uint32_t>(o_rows);
+    int32_t* keys = ps.as<int32_t>(o_keys);
     memset(sv, (uint8_t)b->stream, (size_t)n);
-    memcpy(h->pin_stage.as<int64_t>(o_ts), b->ts, (size_t)n * 8);
+    memcpy(ps.as<int64_t>(o_ts), b->ts, (size_t)n * 8);
     int32_t nk = 1;
     for (int64_t i = 0; i < n; i++) {
         rows[i] = (uint32_t)(r0 + i);
@@ -1193,13 +1269,13 @@ int nf_push(sh_handle* h, const sh_batch* b, int64_t r0, const uint32_t* index, 
         }
     }
     // one copy: the device staging mirrors pin_stage's layout (ts | rows | keys | stream)
-    if (h->w_pstage.ensure_fresh(o_sv + (size_t)n)) return fail(h, SH_E_OOM, "staging");
-    hipMemcpyAsync(h->w_pstage.p, h->pin_stage.p, o_sv + (size_t)n, hipMemcpyHostToDevice, st);
+    if (ds.ensure_fresh(o_sv + (size_t)n)) return fail(h, SH_E_OOM, "staging");
+    hipMemcpyAsync(ds.p, ps.p, o_sv + (size_t)n, hipMemcpyHostToDevice, st);
     shd_batch B;
-    B.ts = h->w_pstage.as<int64_t>();
-    B.stream = h->w_pstage.as<uint8_t>() + o_sv;
-    B.row = (const uint32_t*)(h->w_pstage.as<uint8_t>() + o_rows);
-    B.keys = h->partitioned ? (const int32_t*)(h->w_pstage.as<uint8_t>() + o_keys) : nullptr;
+    B.ts = ds.as<int64_t>();
+    B.stream = ds.as<uint8_t>() + o_sv;
+    B.row = (const uint32_t*)(ds.as<uint8_t>() + o_rows);
+    B.keys = h->partitioned ? (const int32_t*)(ds.as<uint8_t>() + o_keys) : nullptr;
     B.row_base = 0;
     B.pad = 0;
     B.seq_base = h->seq_next;
@@ -1211,7 +1287,20 @@ int nf_push(sh_handle* h, const sh_batch* b, int64_t r0, const uint32_t* index, 
         hipMemcpyAsync(h->w_gidx.p, index, (size_t)n * 4, hipMemcpyHostToDevice, st);
         gidx = h->w_gidx.as<uint32_t>();
     }
+    if (h->app.playback) {
+        const int64_t last = index ? call_last : b->ts[b->n - 1];
+        if (last >= h->clock) {
+            h->clock = last;
+            int rc = nf_timers(h, last);
+            if (rc) return rc;
+        }
+    }
+    {
+        int src = nf_settle(h);  // the last call's launch completes (its work overlapped this staging)
+        if (src) return src;
+    }
     int rc = nf_process(h, B, nk, nf_store_cols(h), nullptr, nullptr, 0, &nrows, false, 0, nullptr, gidx, call_n);
+    if (h->pend.on) h->pst ^= 1;
     h->seq_next += index ? call_n : n;
     h->seq_staged0 = h->seq_next;
     return rc;

@@ -753,32 +753,55 @@ __global__ void __launch_bounds__(SEG1_NT) k_segment_small(const int32_t* __rest
     uint32_t* kout = kB;
     uint16_t* iin = iA;
     uint16_t* iout = iB;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     for (int ps = 0; ps < passes; ps++) {
         const int shift = 8 * ps;
-        if (threadIdx.x < 256) run[threadIdx.x] = 0u;
+        for (int i = threadIdx.x; i < (SEG1_NT / 64) * 256; i += SEG1_NT) (&wcnt[0][0])[i] = 0u;
         __syncthreads();
+        // each wave ranks its own contiguous SEG1_R rounds of 64 events in order,
+        // keeping its running per-digit counts (no block barrier per round)
         uint32_t rk[SEG1_R], dg[SEG1_R];
 #pragma unroll
         for (int r = 0; r < SEG1_R; r++) {
-            const int i = r * SEG1_NT + threadIdx.x;
+            const int i = (wv * SEG1_R + r) * 64 + lane;
             const bool valid = i < nn;
-            dg[r] = valid ? (kin[i] >> shift) & 0xFFu : 0u;
-            rk[r] = shw_rank8<SEG1_NT>(dg[r], valid, wcnt, run);
+            const uint32_t d = valid ? (kin[i] >> shift) & 0xFFu : 0u;
+            uint64_t peers = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t m = __ballot(valid && bit);
+                peers &= bit ? m : ~m;
+            }
+            const uint32_t rr = (uint32_t)__popcll(peers & lt);
+            const uint32_t base = valid ? wcnt[wv][d] : 0u;
+            if (valid && rr == 0) wcnt[wv][d] = base + (uint32_t)__popcll(peers);
+            rk[r] = base + rr;
+            dg[r] = valid ? d : 0x100u;
         }
-        // digit starts: exclusive scan of the digits' totals
+        __syncthreads();
+        // (digit, wave) starts: digits in order, waves in order inside a digit
         {
+            uint32_t tot_d = 0;
+            if (threadIdx.x < 256) {
+#pragma unroll
+                for (int q = 0; q < SEG1_NT / 64; q++) {
+                    const uint32_t c = wcnt[q][threadIdx.x];
+                    wcnt[q][threadIdx.x] = tot_d;
+                    tot_d += c;
+                }
+            }
             uint32_t tot;
-            const uint32_t c = threadIdx.x < 256 ? run[threadIdx.x] : 0u;
-            const uint32_t ex = shw_block_excl<SEG1_NT>(c, ws, &tot);
-            __syncthreads();
+            const uint32_t ex = shw_block_excl<SEG1_NT>(threadIdx.x < 256 ? tot_d : 0u, ws, &tot);
             if (threadIdx.x < 256) run[threadIdx.x] = ex;
             __syncthreads();
         }
 #pragma unroll
         for (int r = 0; r < SEG1_R; r++) {
-            const int i = r * SEG1_NT + threadIdx.x;
-            if (i < nn) {
-                const uint32_t pos = run[dg[r]] + rk[r];
+            const int i = (wv * SEG1_R + r) * 64 + lane;
+            if (dg[r] < 0x100u) {
+                const uint32_t pos = run[dg[r]] + wcnt[wv][dg[r]] + rk[r];
                 kout[pos] = kin[i];
                 iout[pos] = iin[i];
             }
