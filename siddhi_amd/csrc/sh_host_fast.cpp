@@ -215,12 +215,13 @@ static int run_rules_sparse(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     if (n <= 1 || n >= (int64_t)0xFFFFFFFFll || !run->d_keys) return 1;
     const int64_t cap = std::max<int64_t>(65536, n / 8);
     const size_t nk1 = (size_t)nkeys + 1;
-    if (h->rs_pr.ensure_fresh((size_t)cap * 16) || h->rs_key.ensure_fresh(nk1 * 8) ||
+    if (h->rs_pr.ensure_fresh((size_t)cap * 16) || h->rs_key.ensure_fresh(nk1 * 12) ||
         h->rs_list.ensure_fresh((size_t)cap * 20) || h->rs_ctl.ensure_fresh(64) || ensure_ws(h, (int64_t)nk1))
         return fail(h, SH_E_OOM, "rule workspace");
     uint32_t* pr = h->rs_pr.as<uint32_t>();
     uint32_t* key_cnt = h->rs_key.as<uint32_t>();
     uint32_t* key_off = key_cnt + nk1;
+    uint32_t* key_fill = key_off + nk1;
     unsigned long long* ctl = h->rs_ctl.as<unsigned long long>();  // [0] partials, [1] records, [2] flag
     shd_cols sc;
     memset(&sc, 0, sizeof(sc));
@@ -231,9 +232,10 @@ static int run_rules_sparse(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     const shd_cols* dC = h->d_cols_desc.as<shd_cols>();
     const shr_table* dT = h->rd_tab.as<shr_table>();
     hipMemsetAsync(key_cnt, 0, nk1 * 4, st);
+    hipMemsetAsync(key_fill, 0, nk1 * 4, st);
     hipMemsetAsync(ctl, 0, 24, st);
     if (shr_sparse_open(dT, run->d_ts, run->d_keys, n, nkeys, dC, h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr,
-                        &h->r_img, pr, pr + cap, pr + 2 * cap, pr + 3 * cap, key_cnt, ctl, cap, (int32_t*)(ctl + 2),
+                        &h->r_img, pr, pr + cap, pr + 2 * cap, key_cnt, ctl, cap, (int32_t*)(ctl + 2),
                         st))
         return fail(h, SH_E_HIP, "sparse partial launch failed");
     unsigned long long rd[3] = {0, 0, 0};
@@ -257,7 +259,7 @@ static int run_rules_sparse(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     uint32_t* rec_r = rec_q + rcap;
     if (np > 0 &&
         shr_sparse_match(dT, run->d_ts, run->d_keys, n, dC, h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr,
-                         &h->r_img, pr, pr + cap, pr + 2 * cap, pr + 3 * cap, ctl, np, key_off,
+                         &h->r_img, pr, pr + cap, pr + 2 * cap, key_fill, ctl, np, key_off,
                          l_p, l_r, l_te, l_q, rec_p, rec_q, rec_r, ctl + 1, rcap, st))
         return fail(h, SH_E_HIP, "sparse match launch failed");
     hipMemcpyAsync(rd, ctl, 16, hipMemcpyDeviceToHost, st);

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -142,6 +143,9 @@ struct NfLaunch {
     uint64_t* d_seq = nullptr;
     int64_t* d_vals = nullptr;
     int attempt = 0;
+    bool defer = false;     // may be left pending (streaming push, single process)
+    bool early = false;     // this attempt's history job was queued at launch (its counter block: ctl)
+    const uint8_t* ctl = nullptr;
 };
 
 struct sh_handle {
@@ -271,12 +275,16 @@ struct sh_handle {
     struct HistJob {
         int64_t first, n;
         hipEvent_t ev;
+        const uint8_t* ctl;  // (a launch queued before its completion: its counter block, n from it)
     };
     std::thread hw_thread;
     std::mutex hw_mu;
-    std::condition_variable hw_cv, hw_idle;
     std::deque<HistJob> hw_q;
-    bool hw_busy = false, hw_stop = false, hw_fail = false;
+    std::atomic<int> hw_pending{0};      // queued or running jobs (the thread and the joins spin on it)
+    std::atomic<bool> hw_stop{false};
+    bool hw_fail = false;
+    PinBuf pin_ctl2;                     // counter blocks of launches whose history jobs were queued at launch
+                                         // (one 32-byte slot per history event, hw_ev)
     hipEvent_t hw_ev[16] = {};
     int hw_ev_next = 0;
     double hw_ms = 0.0;  // the thread's replay time (phase 7 when profiled)

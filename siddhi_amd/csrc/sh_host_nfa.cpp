@@ -120,9 +120,10 @@ static void nf_ctl_read(sh_handle* h) {
                    hipMemcpyDeviceToHost, h->stream);
     h->hist_spec = true;
 }
-static unsigned nf_ctl_err(sh_handle* h) { return *(const unsigned*)(h->pin_rd.as<uint8_t>() + PR_CTL + 8); }
-static int64_t nf_ctl_nrec(sh_handle* h) { return *(const int64_t*)(h->pin_rd.as<uint8_t>() + PR_CTL); }
-static int64_t nf_ctl_nsev(sh_handle* h) { return *(const int64_t*)(h->pin_rd.as<uint8_t>() + PR_CTL + 16); }
+static const uint8_t* nf_ctl(sh_handle* h) { return h->pin_rd.as<uint8_t>() + PR_CTL; }
+static unsigned nf_ctl_err(sh_handle* h) { return *(const unsigned*)(nf_ctl(h) + 8); }
+static int64_t nf_ctl_nrec(sh_handle* h) { return *(const int64_t*)nf_ctl(h); }
+static int64_t nf_ctl_nsev(sh_handle* h) { return *(const int64_t*)(nf_ctl(h) + 16); }
 
 // the models' ranks after a replay: whole array after a resize, else the touched
 // keys (uploaded on the stream, ahead of the next due pass)
@@ -169,50 +170,71 @@ static int nf_rank_upload(sh_handle* h) {
     return SH_OK;
 }
 
-// the replay thread: applies queued launches in order, each after its copy's event
+// the replay thread: applies queued launches in order, each after its copy's event.
+// It spins on the pending count (a condition variable's wake-up cost the launching
+// thread ~20 us per launch); a job queued before its launch completed reads its
+// record count from the launch's counter block and skips a failed launch (the
+// replay queues its own job) or one with more records than came back (the
+// completion applies those itself)
+static inline void hw_relax(int& spins) {
+    if (++spins < 256)
+        __builtin_ia32_pause();
+    else
+        std::this_thread::yield();
+}
+
 static void hw_loop(sh_handle* h) {
     for (;;) {
+        int spins = 0;
+        while (h->hw_pending.load(std::memory_order_acquire) == 0) {
+            if (h->hw_stop.load(std::memory_order_acquire)) return;
+            hw_relax(spins);
+        }
         sh_handle::HistJob j;
         {
-            std::unique_lock<std::mutex> lk(h->hw_mu);
-            h->hw_cv.wait(lk, [h] { return h->hw_stop || !h->hw_q.empty(); });
-            if (h->hw_q.empty()) return;  // (stop)
+            std::lock_guard<std::mutex> lk(h->hw_mu);
             j = h->hw_q.front();
-            h->hw_busy = true;
         }
         const auto t0 = std::chrono::steady_clock::now();
         // polled (a blocking wait would hold the runtime's locks against the
         // launching thread's calls)
         hipError_t q = hipSuccess;
+        spins = 0;
         if (j.ev)
-            while ((q = hipEventQuery(j.ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(5));
+            while ((q = hipEventQuery(j.ev)) == hipErrorNotReady) hw_relax(spins);
         bool ok = q == hipSuccess;
-        ok = ok && h->sm.apply(h->pin_hist.as<uint64_t>((size_t)j.first * 16), (size_t)j.n);
+        int64_t n = j.n;
+        if (ok && j.ctl) {
+            const unsigned err = *(const unsigned*)(j.ctl + 8);
+            const int64_t ns = *(const int64_t*)(j.ctl + 16);
+            n = (err || ns > kHistSpec) ? 0 : ns;
+        }
+        if (ok && n > 0) ok = h->sm.apply(h->pin_hist.as<uint64_t>((size_t)j.first * 16), (size_t)n);
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         {
             std::lock_guard<std::mutex> lk(h->hw_mu);
             h->hw_q.pop_front();
-            h->hw_busy = false;
             h->hw_ms += ms;
             if (!ok) h->hw_fail = true;
         }
-        h->hw_idle.notify_all();
+        h->hw_pending.fetch_sub(1, std::memory_order_release);
     }
 }
 
-// queue a launch's records [first, first + n) of pin_hist (their copy is on h->stream)
-static int hw_submit(sh_handle* h, int64_t first, int64_t n, bool tracked) {
+// queue a launch's records [first, first + n) of pin_hist (tracked: their copy is
+// on h->stream; ctl: n comes from this counter block once the copy has landed)
+static int hw_submit(sh_handle* h, int64_t first, int64_t n, bool tracked, const uint8_t* ctl = nullptr) {
     if (!h->hw_thread.joinable()) {
         for (auto& e : h->hw_ev)
             if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
                 return fail(h, SH_E_HIP, "history events");
-        h->hw_stop = false;
+        h->hw_stop.store(false);
         h->hw_thread = std::thread(hw_loop, h);
     }
     {
-        std::unique_lock<std::mutex> lk(h->hw_mu);
         // (an event is reused only after its job is done: at most 15 queued)
-        h->hw_idle.wait(lk, [h] { return h->hw_q.size() < 15; });
+        int spins = 0;
+        while (h->hw_pending.load(std::memory_order_acquire) >= 15) hw_relax(spins);
     }
     hipEvent_t ev = nullptr;  // (untracked: the records are on the host already)
     if (tracked) {
@@ -222,20 +244,18 @@ static int hw_submit(sh_handle* h, int64_t first, int64_t n, bool tracked) {
     }
     {
         std::lock_guard<std::mutex> lk(h->hw_mu);
-        h->hw_q.push_back({first, n, ev});
+        h->hw_q.push_back({first, n, ev, ctl});
     }
-    h->hw_cv.notify_one();
+    h->hw_pending.fetch_add(1, std::memory_order_release);
     return SH_OK;
 }
 
 void nf_hist_stop(sh_handle* h) {
     if (!h->hw_thread.joinable()) return;
-    {
-        std::lock_guard<std::mutex> lk(h->hw_mu);
-        h->hw_stop = true;
-    }
-    h->hw_cv.notify_all();
+    h->hw_stop.store(true, std::memory_order_release);
     h->hw_thread.join();
+    h->hw_pending.store(0);
+    h->hw_q.clear();
     for (auto& e : h->hw_ev)
         if (e) {
             hipEventDestroy(e);
@@ -248,10 +268,11 @@ void nf_hist_stop(sh_handle* h) {
 int nf_sev_flush(sh_handle* h) {
     if (!h->hw_thread.joinable()) return SH_OK;
     HpScope hp_(h, 3);
+    int spins = 0;
+    while (h->hw_pending.load(std::memory_order_acquire) != 0) hw_relax(spins);
     bool bad;
     {
-        std::unique_lock<std::mutex> lk(h->hw_mu);
-        h->hw_idle.wait(lk, [h] { return h->hw_q.empty() && !h->hw_busy; });
+        std::lock_guard<std::mutex> lk(h->hw_mu);
         bad = h->hw_fail;
         h->hw_fail = false;
         h->hp_ms[7] = h->hw_ms;
@@ -757,6 +778,7 @@ int nf_process(sh_handle* h, const shd_batch& B, int32_t nkeys, const nf_cols& c
     // (nf_settle), so the caller prepares the next send() while this one runs
     static const bool no_defer = getenv("SH_NO_DEFER_LAUNCH") != nullptr;
     const bool defer = !no_defer && !d_seq && !fresh && !h->coord_on && !h->has_lists && !sorted_cols;
+    L.defer = defer;
     int rc = nf_launch(h, L);
     if (rc) return rc;
     if (defer) {
@@ -810,7 +832,30 @@ int nf_launch(sh_handle* h, NfLaunch& L) {
                        L.seg_list, L.nseg, L.skeys, L.nkeys, L.max_seg, h->tick, h->clock, &em, st))
         return fail(h, SH_E_HIP, "k_nfa_run launch failed");
     hipEventRecord(h->ev[2], st);
-    nf_ctl_read(h);
+    L.early = false;
+    static const bool early_off = getenv("SH_HIST_EARLY") && getenv("SH_HIST_EARLY")[0] == '0';
+    if (L.defer && L.attempt == 0 && h->sm_on && !h->coord_on && h->sev_cap >= kHistSpec && !early_off) {
+        // its history job is queued now: the replay thread applies the records as
+        // soon as they land, while the caller prepares the next call
+        if (h->pin_ctl2.ensure(16 * 32)) return fail(h, SH_E_OOM, "pinned staging");
+        if ((size_t)(h->hist_used + kHistSpec) * 16 > h->pin_hist.bytes) {
+            const int frc = nf_sev_flush(h);
+            if (frc) return frc;
+            if (h->pin_hist.ensure((size_t)kHistSpec * 16 * 4)) return fail(h, SH_E_OOM, "pinned staging");
+        }
+        uint8_t* slot = h->pin_ctl2.as<uint8_t>((size_t)h->hw_ev_next * 32);  // (the job's event index)
+        hipMemcpyAsync(slot, h->n_ctl.p, 24, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(h->pin_hist.as<uint8_t>((size_t)h->hist_used * 16), h->n_sev.p, (size_t)kHistSpec * 16,
+                       hipMemcpyDeviceToHost, st);
+        const int qrc = hw_submit(h, h->hist_used, -1, true, slot);
+        if (qrc) return qrc;
+        h->hist_used += kHistSpec;
+        h->hist_spec = false;
+        L.early = true;
+        L.ctl = slot;
+    } else {
+        nf_ctl_read(h);
+    }
     L.attempt++;
     return SH_OK;
 }
@@ -822,12 +867,29 @@ int nf_complete(sh_handle* h, NfLaunch& L, int64_t* n_rows) {
     L.on = false;
     for (;;) {
         if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "device error in k_nfa_run");
-        const unsigned err = nf_ctl_err(h);
+        const uint8_t* ctl = L.early ? L.ctl : nf_ctl(h);
+        const unsigned err = *(const unsigned*)(ctl + 8);
         if (!err) {
             h->tick++;
-            const int64_t nrec = nf_ctl_nrec(h);
-            int src = nf_sev_apply(h, true);
-            if (src) return src;
+            const int64_t nrec = *(const int64_t*)ctl;
+            if (L.early) {
+                // its job is queued; more records than came back: the thread skips
+                // them, so they are applied here, in order, once it is idle
+                const int64_t ns = *(const int64_t*)(ctl + 16);
+                h->hp_n[9] += ns;
+                if (ns > kHistSpec) {
+                    int frc = nf_sev_flush(h);
+                    if (frc) return frc;
+                    if (h->pin_hist.ensure((size_t)ns * 16)) return fail(h, SH_E_OOM, "pinned staging");
+                    hipMemcpyAsync(h->pin_hist.p, h->n_sev.p, (size_t)ns * 16, hipMemcpyDeviceToHost, st);
+                    const int qrc = hw_submit(h, 0, ns, true);
+                    if (qrc) return qrc;
+                    h->hist_used = ns;
+                }
+            } else {
+                int src = nf_sev_apply(h, true);
+                if (src) return src;
+            }
             int64_t rows = 0;
             int rc = nf_place(h, L.n_idx, &rows, L.d_seq, L.d_vals, L.cap, h->tick - 1, nrec);
             if (n_rows) *n_rows = rows;

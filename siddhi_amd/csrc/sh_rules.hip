@@ -718,6 +718,8 @@ __device__ __forceinline__ bool spa_f2(const shr_table* __restrict__ RT, const s
     return rule_terms(R->t[1], R->nt[1], p, q, C);
 }
 
+#define SPA_WBUF 256  // partials a wave holds before it appends them (one global atomic per flush)
+
 template <bool IMG>
 __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __restrict__ RT,
                                                          const int64_t* __restrict__ ts,
@@ -725,17 +727,19 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
                                                          const shd_cols* __restrict__ C,
                                                          const uint8_t* __restrict__ img, shr_img I,
                                                          uint32_t* __restrict__ pr_p, uint32_t* __restrict__ pr_r,
-                                                         uint32_t* __restrict__ pr_key, uint32_t* __restrict__ pr_slot,
-                                                         uint32_t* __restrict__ key_cnt,
+                                                         uint32_t* __restrict__ pr_key, uint32_t* __restrict__ key_cnt,
                                                          unsigned long long* __restrict__ ctr, int64_t cap,
                                                          int32_t* __restrict__ flag) {
     extern __shared__ uint4 s_img[];
     __shared__ const void* s_col[32];
-    __shared__ uint32_t b_p[SPA_BUF], b_r[SPA_BUF], b_k[SPA_BUF], b_s[SPA_BUF];
-    __shared__ uint32_t s_fill;
-    __shared__ unsigned long long s_base;
+    // per wave: its pending partials (opening event, rule, key) and their count --
+    // waves run independently, no block barrier after the image is staged
+    __shared__ uint32_t w_p[SPA_TPB / 64][SPA_WBUF], w_r[SPA_TPB / 64][SPA_WBUF], w_k[SPA_TPB / 64][SPA_WBUF];
+    __shared__ uint32_t w_fill[SPA_TPB / 64];
     spa_stage<IMG>(img, I, C, s_img, s_col);
-    if (threadIdx.x == 0) s_fill = 0u;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    if (lane == 0) w_fill[wv] = 0u;
     const SpaRules S{(const uint8_t*)s_img, img, s_col};
     const uint32_t n_free = (uint32_t)RT->n_free;
     const int ix_attr = RT->ix_attr;
@@ -743,6 +747,20 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
     int32_t fl = 0;
     __syncthreads();
     const void* ix_col = ix_attr >= 0 ? s_col[ix_attr] : nullptr;
+    // a wave's partials to global: one atomic for the run, then coalesced stores
+    auto flush = [&](uint32_t fill) {
+        unsigned long long g0 = 0;
+        if (lane == 0) g0 = atomicAdd(ctr, (unsigned long long)fill);
+        g0 = __shfl(g0, 0);
+        for (uint32_t i = lane; i < fill; i += 64) {
+            const int64_t g = (int64_t)g0 + i;
+            if (g < cap) {
+                pr_p[g] = w_p[wv][i];
+                pr_r[g] = w_r[wv][i];
+                pr_key[g] = w_k[wv][i];
+            }
+        }
+    };
     const int64_t round = (int64_t)SPA_TPB * SPA_U;
     for (int64_t base = (int64_t)blockIdx.x * round; base < n; base += (int64_t)gridDim.x * round) {
         // SPA_U runs of the workgroup's events: ts, key, index value
@@ -756,7 +774,7 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
             tv[u] = in ? ts[p] : 0;
             tp[u] = in && p > 0 ? ts[p - 1] : INT64_MIN;
             key[u] = in ? akeys[p] : -1;
-            xv[u] = (in && ix_col) ? rule_ix_key(ix_ty, rule_attr(&ix_col, 0, ix_ty, (uint32_t)p)) : 0;
+            xv[u] = (in && ix_col) ? rule_ix_key(ix_ty, rule_attr(s_col, ix_attr, ix_ty, (uint32_t)p)) : 0;
         }
         uint32_t lo[SPA_U], hi[SPA_U];
 #pragma unroll
@@ -769,64 +787,65 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
             const int64_t p = base + (int64_t)u * SPA_TPB + threadIdx.x;
-            if (key[u] < 0 || key[u] >= nkeys) continue;
-            const uint32_t nsel = hi[u] - lo[u], total = nsel + n_free;
-            for (uint32_t k = 0; k < total; k++) {
-                const uint32_t r = spa_rule_id<IMG>(RT, I, S, lo[u], k, nsel);
-                if (!spa_f1<IMG>(RT, I, S, C, r, (uint32_t)p)) continue;
-                const uint32_t slot = atomicAdd(&key_cnt[key[u]], 1u);
-                const uint32_t at = atomicAdd(&s_fill, 1u);
-                if (at < SPA_BUF) {
-                    b_p[at] = (uint32_t)p;
-                    b_r[at] = r;
-                    b_k[at] = (uint32_t)key[u];
-                    b_s[at] = slot;
-                } else {
-                    // (a round with more than the buffer: straight to global)
-                    const unsigned long long g = atomicAdd(ctr, 1ull);
-                    if ((int64_t)g < cap) {
-                        pr_p[g] = (uint32_t)p;
-                        pr_r[g] = r;
-                        pr_key[g] = (uint32_t)key[u];
-                        pr_slot[g] = slot;
+            const bool live = key[u] >= 0 && key[u] < nkeys;
+            const uint32_t total = live ? hi[u] - lo[u] + n_free : 0u;
+            const uint32_t nsel = hi[u] - lo[u];
+            // every lane of the wave takes the same number of steps (the wave's most
+            // candidate rules), so each step's partials are ranked by one ballot
+            uint32_t steps = total;
+            for (int o = 32; o > 0; o >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, o));
+            for (uint32_t k = 0; k < steps; k++) {
+                uint32_t r = 0u;
+                bool ok = false;
+                if (k < total) {
+                    r = spa_rule_id<IMG>(RT, I, S, lo[u], k, nsel);
+                    ok = spa_f1<IMG>(RT, I, S, C, r, (uint32_t)p);
+                }
+                const uint64_t m = __ballot(ok);
+                if (m == 0ull) continue;
+                const uint32_t fill = w_fill[wv];
+                const uint32_t at = fill + (uint32_t)__popcll(m & lt);
+                if (ok) {
+                    atomicAdd(&key_cnt[key[u]], 1u);  // (no return: the slot is taken at placement)
+                    if (at < SPA_WBUF) {
+                        w_p[wv][at] = (uint32_t)p;
+                        w_r[wv][at] = r;
+                        w_k[wv][at] = (uint32_t)key[u];
+                    } else {
+                        const unsigned long long g = atomicAdd(ctr, 1ull);  // (buffer full: straight out)
+                        if ((int64_t)g < cap) {
+                            pr_p[g] = (uint32_t)p;
+                            pr_r[g] = r;
+                            pr_key[g] = (uint32_t)key[u];
+                        }
                     }
                 }
-            }
-        }
-        __syncthreads();
-        const uint32_t fill = s_fill < SPA_BUF ? s_fill : SPA_BUF;
-        const bool last = base + (int64_t)gridDim.x * round >= n;
-        if (fill >= SPA_BUF / 2 || (last && fill)) {
-            if (threadIdx.x == 0) s_base = atomicAdd(ctr, (unsigned long long)fill);
-            __syncthreads();
-            const int64_t g0 = (int64_t)s_base;
-            for (uint32_t i = threadIdx.x; i < fill; i += SPA_TPB) {
-                const int64_t g = g0 + i;
-                if (g < cap) {
-                    pr_p[g] = b_p[i];
-                    pr_r[g] = b_r[i];
-                    pr_key[g] = b_k[i];
-                    pr_slot[g] = b_s[i];
+                const uint32_t nf = min(fill + (uint32_t)__popcll(m), (uint32_t)SPA_WBUF);
+                if (lane == 0) w_fill[wv] = nf;
+                if (nf > SPA_WBUF - 64) {
+                    flush(nf);
+                    if (lane == 0) w_fill[wv] = 0u;
                 }
             }
-            __syncthreads();
-            if (threadIdx.x == 0) s_fill = 0u;
         }
-        __syncthreads();
+    }
+    {
+        const uint32_t fill = w_fill[wv];
+        if (fill) flush(fill);
     }
     if (fl) atomicOr(flag, fl);
 }
 
 __global__ void k_sparse_place(const uint32_t* __restrict__ pr_p, const uint32_t* __restrict__ pr_r,
-                               const uint32_t* __restrict__ pr_key, const uint32_t* __restrict__ pr_slot,
+                               const uint32_t* __restrict__ pr_key, uint32_t* __restrict__ key_fill,
                                const unsigned long long* __restrict__ ctr, const uint32_t* __restrict__ key_off,
                                const shr_table* __restrict__ RT, const int64_t* __restrict__ ts,
                                uint32_t* __restrict__ l_p, uint32_t* __restrict__ l_r, int64_t* __restrict__ l_te,
                                uint32_t* __restrict__ l_q) {
     const int64_t np = (int64_t)*ctr;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < np; s += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t p = pr_p[s], r = pr_r[s];  // (np <= the buffers: the host checked the count)
-        const uint32_t pos = key_off[pr_key[s]] + pr_slot[s];
+        const uint32_t p = pr_p[s], r = pr_r[s], key = pr_key[s];  // (np <= the buffers: the host checked the count)
+        const uint32_t pos = key_off[key] + atomicAdd(&key_fill[key], 1u);  // (any order inside a key's list)
         const int64_t W = RT->rules[r].within;
         const int64_t t = ts[p];
         l_p[pos] = p;
@@ -939,11 +958,11 @@ static bool spa_img_fits(const uint8_t* img, const shr_img* I, int static_lds) {
 
 extern "C" int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int32_t* akeys, int64_t n, int32_t nkeys,
                                const shd_cols* dC, const uint8_t* img, const shr_img* I, uint32_t* pr_p,
-                               uint32_t* pr_r, uint32_t* pr_key, uint32_t* pr_slot, uint32_t* key_cnt,
+                               uint32_t* pr_r, uint32_t* pr_key, uint32_t* key_cnt,
                                unsigned long long* ctr, int64_t cap, int32_t* flag, void* stream) {
     shr_img none;
     memset(&none, 0, sizeof(none));
-    const int buf = 4 * SPA_BUF * 4 + 512;
+    const int buf = 3 * (SPA_TPB / 64) * SPA_WBUF * 4 + 512;
     static const int lim = spa_img_attr(&k_sparse_open<true>);
     const bool use_img = spa_img_fits(img, I, buf) && I->lds <= lim &&
                          !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0');
@@ -954,24 +973,24 @@ extern "C" int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int
     if (g < 1) g = 1;
     if (use_img)
         hipLaunchKernelGGL(k_sparse_open<true>, dim3((unsigned)g), dim3(SPA_TPB), (size_t)I->lds, (hipStream_t)stream, dT,
-                           ts, akeys, n, nkeys, dC, img, *I, pr_p, pr_r, pr_key, pr_slot, key_cnt, ctr, cap, flag);
+                           ts, akeys, n, nkeys, dC, img, *I, pr_p, pr_r, pr_key, key_cnt, ctr, cap, flag);
     else
         hipLaunchKernelGGL(k_sparse_open<false>, dim3((unsigned)g), dim3(SPA_TPB), 0, (hipStream_t)stream, dT, ts, akeys,
                            n, nkeys, dC, img && I && I->bytes > 0 ? img : (const uint8_t*)nullptr,
-                           img && I && I->bytes > 0 ? *I : none, pr_p, pr_r, pr_key, pr_slot, key_cnt, ctr, cap,
+                           img && I && I->bytes > 0 ? *I : none, pr_p, pr_r, pr_key, key_cnt, ctr, cap,
                            flag);
     return rules_ok();
 }
 
 extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const int32_t* akeys, int64_t n,
                                 const shd_cols* dC, const uint8_t* img, const shr_img* I, const uint32_t* pr_p, const uint32_t* pr_r,
-                                const uint32_t* pr_key, const uint32_t* pr_slot, const unsigned long long* ctr,
+                                const uint32_t* pr_key, uint32_t* key_fill, const unsigned long long* ctr,
                                 int64_t n_pairs_max, const uint32_t* key_off, uint32_t* l_p, uint32_t* l_r,
                                 int64_t* l_te, uint32_t* l_q, uint32_t* rec_p, uint32_t* rec_q, uint32_t* rec_r,
                                 unsigned long long* rctr, int64_t rcap, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const unsigned gp = rgrid(n_pairs_max);
-    hipLaunchKernelGGL(k_sparse_place, dim3(gp), dim3(RTPB), 0, st, pr_p, pr_r, pr_key, pr_slot, ctr, key_off, dT, ts,
+    hipLaunchKernelGGL(k_sparse_place, dim3(gp), dim3(RTPB), 0, st, pr_p, pr_r, pr_key, key_fill, ctr, key_off, dT, ts,
                        l_p, l_r, l_te, l_q);
     {
         shr_img none;
