@@ -282,6 +282,8 @@ struct sh_handle {
     std::deque<HistJob> hw_q;
     std::atomic<int> hw_pending{0};      // queued or running jobs (the thread and the joins spin on it)
     std::atomic<bool> hw_stop{false};
+    std::condition_variable hw_cv;       // (SH_HIST_SPIN=0: the thread sleeps on it between jobs)
+    bool hw_spin = true;
     bool hw_fail = false;
     PinBuf pin_ctl2;                     // counter blocks of launches whose history jobs were queued at launch
                                          // (one 32-byte slot per history event, hw_ev)

@@ -186,9 +186,15 @@ static inline void hw_relax(int& spins) {
 static void hw_loop(sh_handle* h) {
     for (;;) {
         int spins = 0;
-        while (h->hw_pending.load(std::memory_order_acquire) == 0) {
-            if (h->hw_stop.load(std::memory_order_acquire)) return;
-            hw_relax(spins);
+        if (h->hw_spin) {
+            while (h->hw_pending.load(std::memory_order_acquire) == 0) {
+                if (h->hw_stop.load(std::memory_order_acquire)) return;
+                hw_relax(spins);
+            }
+        } else {
+            std::unique_lock<std::mutex> lk(h->hw_mu);
+            h->hw_cv.wait(lk, [h] { return h->hw_stop.load() || h->hw_pending.load() != 0; });
+            if (h->hw_pending.load() == 0) return;
         }
         sh_handle::HistJob j;
         {
@@ -201,7 +207,7 @@ static void hw_loop(sh_handle* h) {
         hipError_t q = hipSuccess;
         spins = 0;
         if (j.ev)
-            while ((q = hipEventQuery(j.ev)) == hipErrorNotReady) hw_relax(spins);
+            while ((q = hipEventQuery(j.ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(5));
         bool ok = q == hipSuccess;
         int64_t n = j.n;
         if (ok && j.ctl) {
@@ -229,6 +235,7 @@ static int hw_submit(sh_handle* h, int64_t first, int64_t n, bool tracked, const
             if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
                 return fail(h, SH_E_HIP, "history events");
         h->hw_stop.store(false);
+        h->hw_spin = !(getenv("SH_HIST_SPIN") && getenv("SH_HIST_SPIN")[0] == '0');
         h->hw_thread = std::thread(hw_loop, h);
     }
     {
@@ -243,16 +250,21 @@ static int hw_submit(sh_handle* h, int64_t first, int64_t n, bool tracked, const
         if (hipEventRecord(ev, h->stream) != hipSuccess) return fail(h, SH_E_HIP, "history event");
     }
     {
-        std::lock_guard<std::mutex> lk(h->hw_mu);
+        std::lock_guard<std::mutex> lk(h->hw_mu);  // (the count under the lock: no lost wake-up)
         h->hw_q.push_back({first, n, ev, ctl});
+        h->hw_pending.fetch_add(1, std::memory_order_release);
     }
-    h->hw_pending.fetch_add(1, std::memory_order_release);
+    if (!h->hw_spin) h->hw_cv.notify_one();
     return SH_OK;
 }
 
 void nf_hist_stop(sh_handle* h) {
     if (!h->hw_thread.joinable()) return;
-    h->hw_stop.store(true, std::memory_order_release);
+    {
+        std::lock_guard<std::mutex> lk(h->hw_mu);
+        h->hw_stop.store(true, std::memory_order_release);
+    }
+    h->hw_cv.notify_all();
     h->hw_thread.join();
     h->hw_pending.store(0);
     h->hw_q.clear();
