@@ -845,7 +845,9 @@ int nf_launch(sh_handle* h, NfLaunch& L) {
         return fail(h, SH_E_HIP, "k_nfa_run launch failed");
     hipEventRecord(h->ev[2], st);
     L.early = false;
-    static const bool early_off = getenv("SH_HIST_EARLY") && getenv("SH_HIST_EARLY")[0] == '0';
+    // early jobs are opt-in (SH_HIST_EARLY=1): on the 3,000-call A/B they measured no
+    // faster than queueing the job at settle (profiles/r4_c4_hist_ab.txt)
+    static const bool early_off = !(getenv("SH_HIST_EARLY") && getenv("SH_HIST_EARLY")[0] == '1');
     if (L.defer && L.attempt == 0 && h->sm_on && !h->coord_on && h->sev_cap >= kHistSpec && !early_off) {
         // its history job is queued now: the replay thread applies the records as
         // soon as they land, while the caller prepares the next call

@@ -85,15 +85,24 @@ struct SnapR {
     }
 };
 
+// the per-key records as the image's per-field arrays (the image layout predates them)
+template <class T, class F>
+static std::vector<T> jmap_field(const ShJMap& M, F get) {
+    std::vector<T> v(M.nd.size());
+    for (size_t i = 0; i < v.size(); i++) v[i] = get(M.nd[i]);
+    return v;
+}
+
 void put_jmap(SnapW& w, const ShJMap& M) {
-    w.vec(M.h);
-    w.vec(M.nx);
-    w.vec(M.pv);
-    w.vec(M.pa);
-    w.vec(M.lf);
-    w.vec(M.rt);
-    w.vec(M.fl);
-    w.vec(M.code);
+    using N = ShJMap::Node;
+    w.vec(jmap_field<int32_t>(M, [](const N& x) { return x.h; }));
+    w.vec(jmap_field<int32_t>(M, [](const N& x) { return x.nx; }));
+    w.vec(jmap_field<int32_t>(M, [](const N& x) { return x.pv; }));
+    w.vec(jmap_field<int32_t>(M, [](const N& x) { return x.pa; }));
+    w.vec(jmap_field<int32_t>(M, [](const N& x) { return x.lf; }));
+    w.vec(jmap_field<int32_t>(M, [](const N& x) { return x.rt; }));
+    w.vec(jmap_field<uint8_t>(M, [](const N& x) { return x.fl; }));
+    w.vec(jmap_field<uint64_t>(M, [](const N& x) { return x.code; }));
     w.vec(M.tab);
     w.put(M.size);
     w.put(M.threshold);
@@ -106,14 +115,29 @@ void put_jmap(SnapW& w, const ShJMap& M) {
 }
 
 void get_jmap(SnapR& r, ShJMap& M) {
-    r.vec(M.h);
-    r.vec(M.nx);
-    r.vec(M.pv);
-    r.vec(M.pa);
-    r.vec(M.lf);
-    r.vec(M.rt);
-    r.vec(M.fl);
-    r.vec(M.code);
+    std::vector<int32_t> h, nx, pv, pa, lf, rt;
+    std::vector<uint8_t> fl;
+    std::vector<uint64_t> code;
+    r.vec(h);
+    r.vec(nx);
+    r.vec(pv);
+    r.vec(pa);
+    r.vec(lf);
+    r.vec(rt);
+    r.vec(fl);
+    r.vec(code);
+    M.nd.assign(h.size(), ShJMap::Node{0, 0, -1, -1, -1, -1, -1, 0});
+    for (size_t i = 0; i < h.size(); i++) {
+        ShJMap::Node& x = M.nd[i];
+        x.h = h[i];
+        x.nx = i < nx.size() ? nx[i] : -1;
+        x.pv = i < pv.size() ? pv[i] : -1;
+        x.pa = i < pa.size() ? pa[i] : -1;
+        x.lf = i < lf.size() ? lf[i] : -1;
+        x.rt = i < rt.size() ? rt[i] : -1;
+        x.fl = i < fl.size() ? fl[i] : 0;
+        x.code = i < code.size() ? code[i] : 0;
+    }
     r.vec(M.tab);
     M.size = r.get<int32_t>();
     M.threshold = r.get<int32_t>();

@@ -35,10 +35,15 @@ struct ShJMap {
     static const int kRankBucketBits = 26;  // rank = bucket << 38 | code
 
     // per key (dense ids)
-    std::vector<int32_t> h;        // spread hash (registered once per key)
-    std::vector<int32_t> nx, pv, pa, lf, rt;
-    std::vector<uint8_t> fl;       // 1 present, 2 tree node, 4 red
-    std::vector<uint64_t> code;
+    // one record per key (a key's fields share a cache line: the replay's accesses
+    // are random over up to 10M keys)
+    struct Node {
+        uint64_t code;             // position code (rank = bucket << 38 | code)
+        int32_t h;                 // spread hash (registered once per key)
+        int32_t nx, pv, pa, lf, rt;
+        uint8_t fl;                // 1 present, 2 tree node, 4 red
+    };
+    std::vector<Node> nd;
     std::vector<int32_t> tab;      // bin heads, -1 empty
     int32_t size = 0, threshold = 0;
     uint64_t ord = 0;              // insert ordinal (plain-bin codes)
@@ -50,39 +55,32 @@ struct ShJMap {
     bool rerank_all = false;
 
     void ensure(int32_t k) {
-        if (k < (int32_t)h.size()) return;
-        const size_t n = std::max<size_t>((size_t)k + 1, h.size() * 2);
-        h.resize(n, 0);
-        nx.resize(n, -1);
-        pv.resize(n, -1);
-        pa.resize(n, -1);
-        lf.resize(n, -1);
-        rt.resize(n, -1);
-        fl.resize(n, 0);
-        code.resize(n, 0);
+        if (k < (int32_t)nd.size()) return;
+        const size_t n = std::max<size_t>((size_t)k + 1, nd.size() * 2);
+        nd.resize(n, Node{0, 0, -1, -1, -1, -1, -1, 0});
     }
     static int32_t spread(int32_t x) { return x ^ (int32_t)((uint32_t)x >> 16); }
     void set_hash(int32_t k, int32_t string_hash) {
         ensure(k);
-        h[k] = spread(string_hash);
+        nd[k].h = spread(string_hash);
     }
-    bool present(int32_t k) const { return k < (int32_t)fl.size() && (fl[k] & 1); }
-    bool is_tree(int32_t k) const { return (fl[k] & 2) != 0; }
-    bool red(int32_t k) const { return k >= 0 && (fl[k] & 4) != 0; }
+    bool present(int32_t k) const { return k < (int32_t)nd.size() && (nd[k].fl & 1); }
+    bool is_tree(int32_t k) const { return (nd[k].fl & 2) != 0; }
+    bool red(int32_t k) const { return k >= 0 && (nd[k].fl & 4) != 0; }
     void set_red(int32_t k, bool r) {
-        if (r) fl[k] |= 4;
-        else fl[k] &= (uint8_t)~4;
+        if (r) nd[k].fl |= 4;
+        else nd[k].fl &= (uint8_t)~4;
     }
     int cap() const { return (int)tab.size(); }
-    int bin_of(int32_t k) const { return (cap() - 1) & h[k]; }
-    uint64_t rank(int32_t k) const { return ((uint64_t)(uint32_t)bin_of(k) << 38) | code[k]; }
+    int bin_of(int32_t k) const { return (cap() - 1) & nd[k].h; }
+    uint64_t rank(int32_t k) const { return ((uint64_t)(uint32_t)bin_of(k) << 38) | nd[k].code; }
     bool rank_fits() const { return cap() <= (1 << kRankBucketBits); }
 
     // list positions of an irregular bin become its codes
     void recode_bin(int b) {
         uint64_t pos = 0;
-        for (int32_t e = tab[b]; e >= 0; e = nx[e]) {
-            code[e] = pos++;
+        for (int32_t e = tab[b]; e >= 0; e = nd[e].nx) {
+            nd[e].code = pos++;
             dirty.push_back(e);
         }
         if (tab[b] < 0) irregular.erase(b);
@@ -102,19 +100,19 @@ struct ShJMap {
         int bin_count = 0;
         const bool tree_bin = first >= 0 && is_tree(first);
         if (!tree_bin)
-            for (int32_t e = first; e >= 0; e = nx[e]) ++bin_count;
-        fl[k] = 1;
-        pa[k] = lf[k] = rt[k] = pv[k] = -1;
+            for (int32_t e = first; e >= 0; e = nd[e].nx) ++bin_count;
+        nd[k].fl = 1;
+        nd[k].pa = nd[k].lf = nd[k].rt = nd[k].pv = -1;
         if (tree_bin) {
             put_tree_val(first, k);
             irregular.insert(i);
             recode_bin(i);
         } else {
-            nx[k] = first;  // newNode(hash, key, value, first): the new head
+            nd[k].nx = first;  // newNode(hash, key, value, first): the new head
             tab[i] = k;
-            code[k] = kMaxCode - (ord++ & kMaxCode);
+            nd[k].code = kMaxCode - (ord++ & kMaxCode);
             dirty.push_back(k);
-            if (bin_count >= kTreeify - 1) treeify_bin(h[k]);
+            if (bin_count >= kTreeify - 1) treeify_bin(nd[k].h);
             touch_bin(bin_of(k));
         }
         ++size;
@@ -131,14 +129,14 @@ struct ShJMap {
         if (is_tree(k)) {
             remove_tree_node(k, movable);
         } else if (tab[idx] == k) {
-            tab[idx] = nx[k];
+            tab[idx] = nd[k].nx;
         } else {
             int32_t p = tab[idx];
-            while (nx[p] != k) p = nx[p];
-            nx[p] = nx[k];
+            while (nd[p].nx != k) p = nd[p].nx;
+            nd[p].nx = nd[k].nx;
         }
-        fl[k] = 0;
-        nx[k] = pv[k] = pa[k] = lf[k] = rt[k] = -1;
+        nd[k].fl = 0;
+        nd[k].nx = nd[k].pv = nd[k].pa = nd[k].lf = nd[k].rt = -1;
         --size;
         touch_bin(idx);
     }
@@ -149,9 +147,9 @@ struct ShJMap {
         for (int32_t k : ks) {
             uint64_t pos = 0;
             if (present(k) && irregular.count(bin_of(k))) {
-                for (int32_t e = tab[bin_of(k)]; e >= 0 && e != k; e = nx[e]) ++pos;
+                for (int32_t e = tab[bin_of(k)]; e >= 0 && e != k; e = nd[e].nx) ++pos;
             } else if (present(k)) {
-                pos = code[k];
+                pos = nd[k].code;
             }
             r.push_back({((uint64_t)(uint32_t)(present(k) ? bin_of(k) : 0) << 38) | pos, k});
         }
@@ -195,9 +193,9 @@ struct ShJMap {
             const int32_t e = old[j];
             if (e < 0) continue;
             const bool irr = old_irr.count(j) != 0;
-            if (nx[e] < 0) {
-                tab[h[e] & (new_cap - 1)] = e;
-                if (irr) mark_irregular(h[e] & (new_cap - 1));
+            if (nd[e].nx < 0) {
+                tab[nd[e].h & (new_cap - 1)] = e;
+                if (irr) mark_irregular(nd[e].h & (new_cap - 1));
             } else if (is_tree(e)) {
                 split(e, j, old_cap);
                 mark_irregular(j);
@@ -205,24 +203,24 @@ struct ShJMap {
             } else {
                 int32_t lo_h = -1, lo_t = -1, hi_h = -1, hi_t = -1;
                 for (int32_t x = e; x >= 0;) {
-                    const int32_t n = nx[x];
-                    if ((h[x] & old_cap) == 0) {
+                    const int32_t n = nd[x].nx;
+                    if ((nd[x].h & old_cap) == 0) {
                         if (lo_t < 0) lo_h = x;
-                        else nx[lo_t] = x;
+                        else nd[lo_t].nx = x;
                         lo_t = x;
                     } else {
                         if (hi_t < 0) hi_h = x;
-                        else nx[hi_t] = x;
+                        else nd[hi_t].nx = x;
                         hi_t = x;
                     }
                     x = n;
                 }
                 if (lo_t >= 0) {
-                    nx[lo_t] = -1;
+                    nd[lo_t].nx = -1;
                     tab[j] = lo_h;
                 }
                 if (hi_t >= 0) {
-                    nx[hi_t] = -1;
+                    nd[hi_t].nx = -1;
                     tab[j + old_cap] = hi_h;
                 }
                 if (irr) {
@@ -247,10 +245,10 @@ struct ShJMap {
         int32_t hd = tab[idx];
         if (hd < 0) return;
         int32_t tl = -1;
-        for (int32_t e = hd; e >= 0; e = nx[e]) {  // replacementTreeNode: same list order
-            fl[e] = (uint8_t)((fl[e] & 1) | 2);
-            pa[e] = lf[e] = rt[e] = -1;
-            pv[e] = tl;
+        for (int32_t e = hd; e >= 0; e = nd[e].nx) {  // replacementTreeNode: same list order
+            nd[e].fl = (uint8_t)((nd[e].fl & 1) | 2);
+            nd[e].pa = nd[e].lf = nd[e].rt = -1;
+            nd[e].pv = tl;
             tl = e;
         }
         treeify(hd);
@@ -258,22 +256,22 @@ struct ShJMap {
         recode_bin(idx);
     }
     int32_t root_of(int32_t r) const {
-        while (pa[r] >= 0) r = pa[r];
+        while (nd[r].pa >= 0) r = nd[r].pa;
         return r;
     }
     // String keys order by spread hash, then String.compareTo
     int dir_for(int32_t x, int32_t p) const {
-        if (h[p] > h[x]) return -1;
-        if (h[p] < h[x]) return 1;
+        if (nd[p].h > nd[x].h) return -1;
+        if (nd[p].h < nd[x].h) return 1;
         return cmp(x, p);
     }
     void treeify(int32_t head) {
         int32_t root = -1;
         for (int32_t x = head, n; x >= 0; x = n) {
-            n = nx[x];
-            lf[x] = rt[x] = -1;
+            n = nd[x].nx;
+            nd[x].lf = nd[x].rt = -1;
             if (root < 0) {
-                pa[x] = -1;
+                nd[x].pa = -1;
                 set_red(x, false);
                 root = x;
                 continue;
@@ -281,11 +279,11 @@ struct ShJMap {
             for (int32_t p = root;;) {
                 const int dir = dir_for(x, p);
                 const int32_t xp = p;
-                p = dir <= 0 ? lf[p] : rt[p];
+                p = dir <= 0 ? nd[p].lf : nd[p].rt;
                 if (p < 0) {
-                    pa[x] = xp;
-                    if (dir <= 0) lf[xp] = x;
-                    else rt[xp] = x;
+                    nd[x].pa = xp;
+                    if (dir <= 0) nd[xp].lf = x;
+                    else nd[xp].rt = x;
                     root = balance_insertion(root, x);
                     break;
                 }
@@ -294,27 +292,27 @@ struct ShJMap {
         move_root_to_front(root);
     }
     int32_t untreeify(int32_t head) {
-        for (int32_t q = head; q >= 0; q = nx[q]) {
-            fl[q] &= 1;
-            pa[q] = lf[q] = rt[q] = pv[q] = -1;
+        for (int32_t q = head; q >= 0; q = nd[q].nx) {
+            nd[q].fl &= 1;
+            nd[q].pa = nd[q].lf = nd[q].rt = nd[q].pv = -1;
         }
         return head;
     }
     void put_tree_val(int32_t first, int32_t x) {
-        const int32_t root = pa[first] >= 0 ? root_of(first) : first;
-        fl[x] = 1 | 2;
+        const int32_t root = nd[first].pa >= 0 ? root_of(first) : first;
+        nd[x].fl = 1 | 2;
         for (int32_t p = root;;) {
             const int dir = dir_for(x, p);
             const int32_t xp = p;
-            p = dir <= 0 ? lf[p] : rt[p];
+            p = dir <= 0 ? nd[p].lf : nd[p].rt;
             if (p < 0) {
-                const int32_t xpn = nx[xp];
-                nx[x] = xpn;  // linked right after its tree parent
-                if (dir <= 0) lf[xp] = x;
-                else rt[xp] = x;
-                nx[xp] = x;
-                pa[x] = pv[x] = xp;
-                if (xpn >= 0) pv[xpn] = x;
+                const int32_t xpn = nd[xp].nx;
+                nd[x].nx = xpn;  // linked right after its tree parent
+                if (dir <= 0) nd[xp].lf = x;
+                else nd[xp].rt = x;
+                nd[xp].nx = x;
+                nd[x].pa = nd[x].pv = xp;
+                if (xpn >= 0) nd[xpn].pv = x;
                 move_root_to_front(balance_insertion(root, x));
                 return;
             }
@@ -326,71 +324,71 @@ struct ShJMap {
         const int32_t first = tab[idx];
         if (root == first) return;
         tab[idx] = root;
-        const int32_t rp = pv[root], rn = nx[root];
-        if (rn >= 0) pv[rn] = rp;
-        if (rp >= 0) nx[rp] = rn;
-        if (first >= 0) pv[first] = root;
-        nx[root] = first;
-        pv[root] = -1;
+        const int32_t rp = nd[root].pv, rn = nd[root].nx;
+        if (rn >= 0) nd[rn].pv = rp;
+        if (rp >= 0) nd[rp].nx = rn;
+        if (first >= 0) nd[first].pv = root;
+        nd[root].nx = first;
+        nd[root].pv = -1;
     }
     int32_t rotate_left(int32_t root, int32_t p) {
         int32_t r, pp, rl;
-        if (p >= 0 && (r = rt[p]) >= 0) {
-            rl = rt[p] = lf[r];
-            if (rl >= 0) pa[rl] = p;
-            pp = pa[r] = pa[p];
+        if (p >= 0 && (r = nd[p].rt) >= 0) {
+            rl = nd[p].rt = nd[r].lf;
+            if (rl >= 0) nd[rl].pa = p;
+            pp = nd[r].pa = nd[p].pa;
             if (pp < 0) {
                 root = r;
                 set_red(r, false);
-            } else if (lf[pp] == p) {
-                lf[pp] = r;
+            } else if (nd[pp].lf == p) {
+                nd[pp].lf = r;
             } else {
-                rt[pp] = r;
+                nd[pp].rt = r;
             }
-            lf[r] = p;
-            pa[p] = r;
+            nd[r].lf = p;
+            nd[p].pa = r;
         }
         return root;
     }
     int32_t rotate_right(int32_t root, int32_t p) {
         int32_t l, pp, lr;
-        if (p >= 0 && (l = lf[p]) >= 0) {
-            lr = lf[p] = rt[l];
-            if (lr >= 0) pa[lr] = p;
-            pp = pa[l] = pa[p];
+        if (p >= 0 && (l = nd[p].lf) >= 0) {
+            lr = nd[p].lf = nd[l].rt;
+            if (lr >= 0) nd[lr].pa = p;
+            pp = nd[l].pa = nd[p].pa;
             if (pp < 0) {
                 root = l;
                 set_red(l, false);
-            } else if (rt[pp] == p) {
-                rt[pp] = l;
+            } else if (nd[pp].rt == p) {
+                nd[pp].rt = l;
             } else {
-                lf[pp] = l;
+                nd[pp].lf = l;
             }
-            rt[l] = p;
-            pa[p] = l;
+            nd[l].rt = p;
+            nd[p].pa = l;
         }
         return root;
     }
     int32_t balance_insertion(int32_t root, int32_t x) {
         set_red(x, true);
         for (;;) {
-            int32_t xp = pa[x], xpp, xppl, xppr;
+            int32_t xp = nd[x].pa, xpp, xppl, xppr;
             if (xp < 0) {
                 set_red(x, false);
                 return x;
             }
-            if (!red(xp) || (xpp = pa[xp]) < 0) return root;
-            if (xp == (xppl = lf[xpp])) {
-                if ((xppr = rt[xpp]) >= 0 && red(xppr)) {
+            if (!red(xp) || (xpp = nd[xp].pa) < 0) return root;
+            if (xp == (xppl = nd[xpp].lf)) {
+                if ((xppr = nd[xpp].rt) >= 0 && red(xppr)) {
                     set_red(xppr, false);
                     set_red(xp, false);
                     set_red(xpp, true);
                     x = xpp;
                 } else {
-                    if (x == rt[xp]) {
+                    if (x == nd[xp].rt) {
                         root = rotate_left(root, x = xp);
-                        xp = pa[x];
-                        xpp = xp < 0 ? -1 : pa[xp];
+                        xp = nd[x].pa;
+                        xpp = xp < 0 ? -1 : nd[xp].pa;
                     }
                     if (xp >= 0) {
                         set_red(xp, false);
@@ -407,10 +405,10 @@ struct ShJMap {
                     set_red(xpp, true);
                     x = xpp;
                 } else {
-                    if (x == lf[xp]) {
+                    if (x == nd[xp].lf) {
                         root = rotate_right(root, x = xp);
-                        xp = pa[x];
-                        xpp = xp < 0 ? -1 : pa[xp];
+                        xp = nd[x].pa;
+                        xpp = xp < 0 ? -1 : nd[xp].pa;
                     }
                     if (xp >= 0) {
                         set_red(xp, false);
@@ -427,7 +425,7 @@ struct ShJMap {
         for (;;) {
             int32_t xp, xpl, xpr;
             if (x < 0 || x == root) return root;
-            if ((xp = pa[x]) < 0) {
+            if ((xp = nd[x].pa) < 0) {
                 set_red(x, false);
                 return x;
             }
@@ -435,18 +433,18 @@ struct ShJMap {
                 set_red(x, false);
                 return root;
             }
-            if ((xpl = lf[xp]) == x) {
-                if ((xpr = rt[xp]) >= 0 && red(xpr)) {
+            if ((xpl = nd[xp].lf) == x) {
+                if ((xpr = nd[xp].rt) >= 0 && red(xpr)) {
                     set_red(xpr, false);
                     set_red(xp, true);
                     root = rotate_left(root, xp);
-                    xp = pa[x];
-                    xpr = xp < 0 ? -1 : rt[xp];
+                    xp = nd[x].pa;
+                    xpr = xp < 0 ? -1 : nd[xp].rt;
                 }
                 if (xpr < 0) {
                     x = xp;
                 } else {
-                    int32_t sl = lf[xpr], sr = rt[xpr];
+                    int32_t sl = nd[xpr].lf, sr = nd[xpr].rt;
                     if ((sr < 0 || !red(sr)) && (sl < 0 || !red(sl))) {
                         set_red(xpr, true);
                         x = xp;
@@ -455,12 +453,12 @@ struct ShJMap {
                             if (sl >= 0) set_red(sl, false);
                             set_red(xpr, true);
                             root = rotate_right(root, xpr);
-                            xp = pa[x];
-                            xpr = xp < 0 ? -1 : rt[xp];
+                            xp = nd[x].pa;
+                            xpr = xp < 0 ? -1 : nd[xp].rt;
                         }
                         if (xpr >= 0) {
                             set_red(xpr, xp >= 0 ? red(xp) : false);
-                            if ((sr = rt[xpr]) >= 0) set_red(sr, false);
+                            if ((sr = nd[xpr].rt) >= 0) set_red(sr, false);
                         }
                         if (xp >= 0) {
                             set_red(xp, false);
@@ -474,13 +472,13 @@ struct ShJMap {
                     set_red(xpl, false);
                     set_red(xp, true);
                     root = rotate_right(root, xp);
-                    xp = pa[x];
-                    xpl = xp < 0 ? -1 : lf[xp];
+                    xp = nd[x].pa;
+                    xpl = xp < 0 ? -1 : nd[xp].lf;
                 }
                 if (xpl < 0) {
                     x = xp;
                 } else {
-                    int32_t sl = lf[xpl], sr = rt[xpl];
+                    int32_t sl = nd[xpl].lf, sr = nd[xpl].rt;
                     if ((sl < 0 || !red(sl)) && (sr < 0 || !red(sr))) {
                         set_red(xpl, true);
                         x = xp;
@@ -489,12 +487,12 @@ struct ShJMap {
                             if (sr >= 0) set_red(sr, false);
                             set_red(xpl, true);
                             root = rotate_left(root, xpl);
-                            xp = pa[x];
-                            xpl = xp < 0 ? -1 : lf[xp];
+                            xp = nd[x].pa;
+                            xpl = xp < 0 ? -1 : nd[xp].lf;
                         }
                         if (xpl >= 0) {
                             set_red(xpl, xp >= 0 ? red(xp) : false);
-                            if ((sl = lf[xpl]) >= 0) set_red(sl, false);
+                            if ((sl = nd[xpl].lf) >= 0) set_red(sl, false);
                         }
                         if (xp >= 0) {
                             set_red(xp, false);
@@ -509,42 +507,42 @@ struct ShJMap {
     void remove_tree_node(int32_t self, bool movable) {
         const int idx = bin_of(self);
         int32_t first = tab[idx], root = first, rl;
-        const int32_t succ = nx[self], pred = pv[self];
+        const int32_t succ = nd[self].nx, pred = nd[self].pv;
         if (pred < 0) tab[idx] = first = succ;
-        else nx[pred] = succ;
-        if (succ >= 0) pv[succ] = pred;
+        else nd[pred].nx = succ;
+        if (succ >= 0) nd[succ].pv = pred;
         if (first < 0) return;
-        if (pa[root] >= 0) root = root_of(root);
-        if (root < 0 || (movable && (rt[root] < 0 || (rl = lf[root]) < 0 || lf[rl] < 0))) {
+        if (nd[root].pa >= 0) root = root_of(root);
+        if (root < 0 || (movable && (nd[root].rt < 0 || (rl = nd[root].lf) < 0 || nd[rl].lf < 0))) {
             tab[idx] = untreeify(first);  // too small
             return;
         }
-        int32_t p = self, pl = lf[self], pr = rt[self], replacement;
+        int32_t p = self, pl = nd[self].lf, pr = nd[self].rt, replacement;
         if (pl >= 0 && pr >= 0) {
             int32_t s = pr, sl;
-            while ((sl = lf[s]) >= 0) s = sl;  // successor
+            while ((sl = nd[s].lf) >= 0) s = sl;  // successor
             const bool c = red(s);
             set_red(s, red(p));
             set_red(p, c);
-            const int32_t sr = rt[s];
-            const int32_t pp = pa[p];
+            const int32_t sr = nd[s].rt;
+            const int32_t pp = nd[p].pa;
             if (s == pr) {
-                pa[p] = s;
-                rt[s] = p;
+                nd[p].pa = s;
+                nd[s].rt = p;
             } else {
-                const int32_t sp = pa[s];
-                if ((pa[p] = sp) >= 0) {
-                    if (s == lf[sp]) lf[sp] = p;
-                    else rt[sp] = p;
+                const int32_t sp = nd[s].pa;
+                if ((nd[p].pa = sp) >= 0) {
+                    if (s == nd[sp].lf) nd[sp].lf = p;
+                    else nd[sp].rt = p;
                 }
-                if ((rt[s] = pr) >= 0) pa[pr] = s;
+                if ((nd[s].rt = pr) >= 0) nd[pr].pa = s;
             }
-            lf[p] = -1;
-            if ((rt[p] = sr) >= 0) pa[sr] = p;
-            if ((lf[s] = pl) >= 0) pa[pl] = s;
-            if ((pa[s] = pp) < 0) root = s;
-            else if (p == lf[pp]) lf[pp] = s;
-            else rt[pp] = s;
+            nd[p].lf = -1;
+            if ((nd[p].rt = sr) >= 0) nd[sr].pa = p;
+            if ((nd[s].lf = pl) >= 0) nd[pl].pa = s;
+            if ((nd[s].pa = pp) < 0) root = s;
+            else if (p == nd[pp].lf) nd[pp].lf = s;
+            else nd[pp].rt = s;
             replacement = sr >= 0 ? sr : p;
         } else if (pl >= 0) {
             replacement = pl;
@@ -554,19 +552,19 @@ struct ShJMap {
             replacement = p;
         }
         if (replacement != p) {
-            const int32_t pp = pa[replacement] = pa[p];
+            const int32_t pp = nd[replacement].pa = nd[p].pa;
             if (pp < 0) root = replacement;
-            else if (p == lf[pp]) lf[pp] = replacement;
-            else rt[pp] = replacement;
-            lf[p] = rt[p] = pa[p] = -1;
+            else if (p == nd[pp].lf) nd[pp].lf = replacement;
+            else nd[pp].rt = replacement;
+            nd[p].lf = nd[p].rt = nd[p].pa = -1;
         }
         const int32_t r = red(p) ? root : balance_deletion(root, replacement);
         if (replacement == p) {  // detach
-            const int32_t pp = pa[p];
-            pa[p] = -1;
+            const int32_t pp = nd[p].pa;
+            nd[p].pa = -1;
             if (pp >= 0) {
-                if (p == lf[pp]) lf[pp] = -1;
-                else if (p == rt[pp]) rt[pp] = -1;
+                if (p == nd[pp].lf) nd[pp].lf = -1;
+                else if (p == nd[pp].rt) nd[pp].rt = -1;
             }
         }
         if (movable) move_root_to_front(r);
@@ -575,16 +573,16 @@ struct ShJMap {
         int32_t lo_h = -1, lo_t = -1, hi_h = -1, hi_t = -1;
         int lc = 0, hc = 0;
         for (int32_t e = b, n; e >= 0; e = n) {
-            n = nx[e];
-            nx[e] = -1;
-            if ((h[e] & bit) == 0) {
-                if ((pv[e] = lo_t) < 0) lo_h = e;
-                else nx[lo_t] = e;
+            n = nd[e].nx;
+            nd[e].nx = -1;
+            if ((nd[e].h & bit) == 0) {
+                if ((nd[e].pv = lo_t) < 0) lo_h = e;
+                else nd[lo_t].nx = e;
                 lo_t = e;
                 ++lc;
             } else {
-                if ((pv[e] = hi_t) < 0) hi_h = e;
-                else nx[hi_t] = e;
+                if ((nd[e].pv = hi_t) < 0) hi_h = e;
+                else nd[hi_t].nx = e;
                 hi_t = e;
                 ++hc;
             }
