@@ -51,7 +51,10 @@ def parse():
     ap.add_argument("--agg", action="store_true",
                     help="c2 / c3: SURVEY.md 8d select variant (ii), the projection + sum / avg aggregators")
     ap.add_argument("--columns", action="store_true",
-                    help="c2: typed output columns (d_out_cols) instead of the raw 8-byte rows (d_out_values)")
+                    help="c2: typed output columns (d_out_cols); same as --layout columns")
+    ap.add_argument("--layout", choices=["packed", "raw", "columns"], default=None,
+                    help="c2 output layout: packed (default: SH_OUT_PACKED rows, trigger_seq + natural-width "
+                         "values, 32 B per match), raw (trigger_seq + 8-byte words, 40 B), columns (d_out_cols)")
     ap.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default, BASELINE.json configs[1]); c1 / c3 / c4 / c5 measure the other configs")
     ap.add_argument("--c4-calls", type=int, default=0, help="c4: send only the first N calls (profiling; 0 = all)")
@@ -376,7 +379,7 @@ def check_rows(W, oseq, ovals, oq, sel_range=None):
 def engine_tag():
     """identifies the device pipeline a PMC profile was taken on (bumped when a
     pipeline's kernels change what they move)"""
-    return "r4-tile-local"
+    return "r4-packed"
 
 
 def cpu_baseline(args, W, n):
@@ -555,13 +558,20 @@ def main():
     stream = torch.cuda.current_stream(dev)
     with_q = bool(W.get("with_query"))
 
-    # --columns: the match stream as typed columns (sh_device_run.d_out_cols: seq 8
-    # + symbol 4 + p1 4 + p2 4 + v2 8 bytes per match) instead of raw 8-byte rows;
-    # fewer bytes but more store instructions (measured slower: 2.25 vs 1.83 ms emit)
-    use_cols = args.config == "c2" and args.columns
+    # c2's output layout: packed rows (SH_OUT_PACKED: seq 8 + symbol 4 + p1 4 + p2 4
+    # + pad 4 + v2 8 = 32 B per match, two 16-byte stores) by default; raw rows
+    # (seq 8 apart + four 8-byte words, 40 B) or typed columns (28 B in five
+    # arrays: more store instructions, measured slower) on request
+    layout = (args.layout or ("columns" if args.columns else "packed")) if args.config == "c2" else "raw"
+    use_cols = layout == "columns"
+    use_packed = layout == "packed"
 
     def step():
-        r = runner.run(t_ts, t_k, cols, K, stream=stream, with_query=with_q, columns=use_cols)
+        if use_packed:
+            r = runner.run(t_ts, t_k, cols, K, stream=stream, with_query=with_q, packed=True)
+            r = (r[0], None, r[1]) + ((r[2],) if with_q else ())
+        else:
+            r = runner.run(t_ts, t_k, cols, K, stream=stream, with_query=with_q, columns=use_cols)
         return r if with_q else r + (None,)
 
     log("warmup")
@@ -609,24 +619,34 @@ def main():
     verified = None
     if not args.no_verify and rank == 0:
         log("verifying the full output against the vectorised restatement")
-        if use_cols:
+        if use_packed:
+            import numpy as np
+            from siddhi_amd.device_run import packed_to_raw
+            offs, rb = runner.packed_layout()
+            oseq_np, ovals_np = packed_to_raw(ovals.cpu().numpy(), runner.out_types, offs, rb)
+            oseq_np = oseq_np.view(np.int64)
+        elif use_cols:
             from siddhi_amd.device_run import columns_to_raw
             ovals_np = columns_to_raw([c.cpu().numpy() for c in ovals], runner.out_types)
+            oseq_np = oseq.cpu().numpy()
         else:
             ovals_np = ovals.cpu().numpy()
-        verified = check_rows(W, oseq.cpu().numpy(), ovals_np, oq.cpu().numpy() if oq is not None else None)
+            oseq_np = oseq.cpu().numpy()
+        verified = check_rows(W, oseq_np, ovals_np, oq.cpu().numpy() if oq is not None else None)
 
     # HBM bytes per step from the committed rocprofv3 PMC passes of this exact
     # workload and variant (scripts/pmc_traffic.py): config, events, keys, --agg,
     # --columns and the engine build must all match, else null
     traffic, traffic_src = None, None
-    variant = args.config + ("_agg" if args.agg else "") + ("_cols" if use_cols else "")
+    variant = args.config + ("_agg" if args.agg else "") + {"packed": "", "raw": "_raw", "columns": "_cols"}[layout]
+    if args.config != "c2":
+        variant = args.config + ("_agg" if args.agg else "")
     prof = os.path.join(HERE, "profiles", f"pmc_{variant}.json")
     if os.path.exists(prof):
         try:
             pj = json.load(open(prof))
             if (pj.get("events") == n and pj.get("keys") == K and bool(pj.get("agg")) == bool(args.agg)
-                    and bool(pj.get("columns")) == bool(use_cols) and pj.get("engine") == engine_tag()):
+                    and pj.get("layout", "raw") == layout and pj.get("engine") == engine_tag()):
                 traffic = pj.get("hbm_bytes_per_step")
                 traffic_src = os.path.relpath(prof, HERE)
         except Exception:
@@ -648,7 +668,9 @@ def main():
                        "path": "pageable host numpy -> HBM (torch .to), before the timed steps"},
             "config": {"workload": W["desc"], "events_per_gpu": n, W["key_name"]: args.keys,
                        "rate_ev_per_ms": args.rate,
-                       "output": "typed columns (d_out_cols)" if use_cols else "raw 8-byte rows (d_out_values)",
+                       "output": {"packed": "packed rows (SH_OUT_PACKED, 32 B per match)",
+                                  "columns": "typed columns (d_out_cols)",
+                                  "raw": "raw 8-byte rows (d_out_values) + trigger_seq"}[layout],
                        "matches_per_gpu": int(m), "parallelism": f"key-sharded x{world}",
                        "bytes": W["bytes_note"]},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",

@@ -145,7 +145,13 @@ typedef struct sh_device_run {
        above. The fields below are read by sh_run_device_v2 alone, which requires
        version == SH_DEVICE_RUN_V2. */
     int32_t version;
-    int32_t pad;
+    /* SH_OUT_RAW (0): d_out_seq + d_out_values as above (or d_out_cols).
+       SH_OUT_PACKED (1): d_out_values holds out_capacity packed rows instead, one
+       per match: the trigger_seq (8 B), then each select value at its natural
+       width (as d_out_cols; bool in a 4-byte slot) aligned to that width, the row
+       padded to a multiple of 16 B -- sh_packed_row_layout gives the offsets.
+       d_out_seq is not written; d_out_cols must be NULL. */
+    int32_t out_layout;
     /* optional: the PartitionStreamReceiver run of every event (one run = the
        consecutive same-key events of one send() call,
        core/partition/PartitionStreamReceiver.java:176-216), as a non-decreasing
@@ -156,11 +162,21 @@ typedef struct sh_device_run {
 } sh_device_run;
 #define SH_DEVICE_RUN_V2 2
 #define SH_DEVICE_RUN_V1_BYTES 96
+#define SH_OUT_RAW 0
+#define SH_OUT_PACKED 1
 
 /* reads the V1 prefix of *run (SH_DEVICE_RUN_V1_BYTES) and writes out_count */
 int sh_run_device(sh_handle* h, sh_device_run* run);
 /* the whole struct; SH_E_INVALID_ARG unless run->version == SH_DEVICE_RUN_V2 */
 int sh_run_device_v2(sh_handle* h, sh_device_run* run);
+
+/* The SH_OUT_PACKED row of this app: byte offset of each select value
+   (offsets[0 .. *n_out - 1]; cap entries at most) and the row size. The same
+   Event the reference hands StreamCallback.receive (core/stream/output/
+   StreamCallback.java:44-60: timestamp-ordered data[] of the select), as one
+   fixed-size record. SH_E_UNSUPPORTED: queries select different types at one
+   position. */
+int sh_packed_row_layout(sh_handle* h, int32_t* offsets, int32_t cap, int32_t* n_out, int32_t* row_bytes);
 
 /* kernel timing of the last sh_run_device call (HIP events on run->stream) */
 typedef struct sh_kernel_times {

@@ -3,10 +3,10 @@
 
 usage: pmc_traffic.py <fetch_dir> <write_dir> <steps> <events> <keys> <out.json> [config]
                       [--calib <cal_fetch_dir> <cal_write_dir> <bytes_per_kernel>]
-                      [--agg] [--columns] [--engine TAG]
+                      [--agg] [--layout packed|raw|columns] [--engine TAG]
 
 steps = every matcher pass the profiled bench ran (its --warmup + --steps). The
-output records the variant (config, --agg, --columns, bench.engine_tag()) so
+output records the variant (config, --agg, --layout, bench.engine_tag()) so
 bench.py attaches it only to a line of that exact workload.
 
 FETCH_SIZE / WRITE_SIZE are in KB (rocprofv3 derived counters). MI355X_MICROARCH.md
@@ -62,13 +62,17 @@ def main():
         cal = calib(args[i + 1], args[i + 2], float(args[i + 3]))
         args = args[:i] + args[i + 4:]
     agg = "--agg" in args
-    cols = "--columns" in args
+    layout = "raw"
+    if "--layout" in args:
+        i = args.index("--layout")
+        layout = args[i + 1]
+        args = args[:i] + args[i + 2:]
     engine = None
     if "--engine" in args:
         i = args.index("--engine")
         engine = args[i + 1]
         args = args[:i] + args[i + 2:]
-    args = [a for a in args if a not in ("--agg", "--columns")]
+    args = [a for a in args if a != "--agg"]
     fdir, wdir, steps, events, keys, out = args[:6]
     config = args[6] if len(args) > 6 else "c2"
     steps = int(steps)
@@ -88,7 +92,7 @@ def main():
         wb = wfac * write.get(k, 0.0) * 1024.0 / steps
         kernels[k] = {"read_bytes": rb, "write_bytes": wb, "calls_per_step": fcalls.get(k, 0) / steps}
         tot += rb + wb
-    res = {"config": config, "events": int(events), "keys": int(keys), "steps": steps, "agg": agg, "columns": cols,
+    res = {"config": config, "events": int(events), "keys": int(keys), "steps": steps, "agg": agg, "layout": layout,
            "engine": engine,
            "hbm_bytes_per_step": tot, "kernels": kernels,
            "calibration": cal, "read_factor": rfac, "write_factor": wfac,

@@ -78,10 +78,12 @@ class sh_device_run(C.Structure):
                 ("d_out_values", C.c_void_p), ("out_count", C.c_int64), ("stream", C.c_void_p),
                 ("d_out_query", C.c_void_p), ("d_out_cols", C.POINTER(C.c_void_p)),
                 # end of the V1 struct (SH_DEVICE_RUN_V1_BYTES); read by sh_run_device_v2 only
-                ("version", C.c_int32), ("pad", C.c_int32), ("d_run", C.c_void_p)]
+                ("version", C.c_int32), ("out_layout", C.c_int32), ("d_run", C.c_void_p)]
 
 
 SH_DEVICE_RUN_V2 = 2
+SH_OUT_RAW = 0
+SH_OUT_PACKED = 1
 
 
 class sh_due_cand(C.Structure):
@@ -109,7 +111,8 @@ class sh_kernel_times(C.Structure):
 EXPORTED = ["sh_start", "sh_compile", "sh_push_batch", "sh_advance_time", "sh_drain", "sh_pending",
             "sh_destroy", "sh_last_error", "sh_run_device", "sh_run_device_v2", "sh_last_kernel_times",
             "sh_version", "sh_device_count", "sh_set_partition_keys", "sh_snapshot", "sh_restore",
-            "sh_set_coordinator", "sh_push_batch_part", "sh_drain_ordered", "sh_list_get"]
+            "sh_set_coordinator", "sh_push_batch_part", "sh_drain_ordered", "sh_list_get",
+            "sh_packed_row_layout"]
 
 
 def bind_product(lib):
@@ -137,6 +140,9 @@ def bind_product(lib):
     lib.sh_run_device_v2.restype = C.c_int
     lib.sh_last_kernel_times.argtypes = [C.c_void_p, C.POINTER(sh_kernel_times)]
     lib.sh_last_kernel_times.restype = C.c_int
+    lib.sh_packed_row_layout.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_int32)]
+    lib.sh_packed_row_layout.restype = C.c_int
     lib.sh_snapshot.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
     lib.sh_snapshot.restype = C.c_int
     lib.sh_restore.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]

@@ -266,44 +266,45 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
 //     consumer-side values are read by arrival index, the e1-side values from
 //     the match stream
 #define BK_EHALF 512   // events of one row-map pass of a wave
+#define BK_PFX_BITS 24  // pfx words: prefix in the low bits, the slot's bucket above
+#define BK_PFX_MASK ((1u << BK_PFX_BITS) - 1u)
+#define BK_NOSLOT 0xFFFFFFFFu
 #define BK_EROWS 1024  // rows the wave's map holds per pass (more: event-parallel writes)
 
 // select value o of a row (raw 8-byte form)
 #define BK_VAL(o, i, mp) bk_raw(O.src[o], O.kind[o] == 1 ? (i) : (mp), O.type[o])
 
-template <bool COLS, int NO>
-__device__ __forceinline__ void bk_row(const shb_out& O, const shb_cols& OC, const int32_t* o_kind,
-                                       const int32_t* o_type, const void* const* o_src, int64_t row, int64_t i,
-                                       int64_t mp, uint64_t seq, uint64_t* __restrict__ out_seq,
-                                       int64_t* __restrict__ out_vals) {
-    if (out_seq) out_seq[row] = seq;
-    if (!out_vals && !COLS) return;
-    if (NO > 0) {
-        int64_t v[NO > 0 ? NO : 1];
+// a packed row (SHB_OUT_PACKED): the trigger sequence number in words 0-1, then
+// each select value at its natural width in OC.woff[o] (8-byte values at even
+// words), OC.rw words per row (a multiple of 4: whole 16-byte stores). Value o
+// sits in words [2 + o, 2 + 2o] (every earlier value one word .. two), so only
+// those candidates are tested: the offsets are kernel arguments (scalar), the
+// row stays in registers.
+template <int NO>
+__device__ __forceinline__ void bk_pack(const shb_cols& OC, int64_t row, const int64_t* v, uint64_t seq) {
+    constexpr int RW = ((2 + 2 * NO) + 3) & ~3;
+    uint32_t wv[RW];
+    wv[0] = (uint32_t)seq;
+    wv[1] = (uint32_t)(seq >> 32);
 #pragma unroll
-        for (int o = 0; o < NO; o++) v[o] = BK_VAL(o, i, mp);
-        if (COLS) {
+    for (int k = 2; k < RW; k++) wv[k] = 0u;
 #pragma unroll
-            for (int o = 0; o < NO; o++) bk_put(OC.cols[o], OC.colw[o], row, v[o]);
-            return;
-        }
-        if (NO % 2 == 0) {
-            // a row of NO words as 16-byte stores: consecutive lanes fill whole lines
-            longlong2* dst = (longlong2*)(out_vals + row * NO);
+    for (int o = 0; o < NO; o++) {
+        const int wo = OC.woff[o];
+        const bool wide = OC.colw[o] == 8;
+        const uint32_t lo = OC.colw[o] == 1 ? (uint32_t)(uint8_t)v[o] : (uint32_t)v[o];
+        const uint32_t hi = (uint32_t)((uint64_t)v[o] >> 32);
 #pragma unroll
-            for (int o = 0; o < NO; o += 2) dst[o / 2] = make_longlong2(v[o], v[o + 1]);
-        } else {
+        for (int k = 2 + o; k <= 2 + 2 * o && k < RW; k++)
+            if (k == wo) wv[k] = lo;
 #pragma unroll
-            for (int o = 0; o < NO; o++) out_vals[row * NO + o] = v[o];
-        }
-        return;
+        for (int k = 3 + o; k <= 3 + 2 * o && k < RW; k++)
+            if (wide && k == wo + 1) wv[k] = hi;
     }
-    const int no = O.n_out;
-    for (int o = 0; o < no; o++) {
-        const int64_t v = bk_raw(o_src[o], o_kind[o] == 1 ? i : mp, o_type[o]);
-        if (COLS) bk_put(OC.cols[o], OC.colw[o], row, v);
-        else out_vals[row * no + o] = v;
-    }
+    uint4* dst = (uint4*)((uint32_t*)OC.rows + row * OC.rw);
+#pragma unroll
+    for (int q = 0; q < RW / 4; q++)
+        if (4 * q < OC.rw) dst[q] = make_uint4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
 }
 
 // the select values of a row (NO > 0: unrolled, the descriptors in scalar registers)
@@ -313,15 +314,22 @@ __device__ __forceinline__ void bk_vals(const shb_out& O, int64_t i, int64_t mp,
     for (int o = 0; o < NO; o++) v[o] = BK_VAL(o, i, mp);
 }
 
-template <bool COLS, int NO>
+// one row in the caller's layout (MODE: SHB_OUT_RAW 8-byte words + out_seq,
+// SHB_OUT_COLS natural-width columns + out_seq, SHB_OUT_PACKED rows)
+template <int MODE, int NO>
 __device__ __forceinline__ void bk_store(const shb_cols& OC, int64_t row, const int64_t* v, uint64_t seq,
                                          uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_vals) {
+    if (MODE == SHB_OUT_PACKED) {
+        bk_pack<NO>(OC, row, v, seq);
+        return;
+    }
     if (out_seq) out_seq[row] = seq;
-    if (COLS) {
+    if (MODE == SHB_OUT_COLS) {
 #pragma unroll
         for (int o = 0; o < NO; o++) bk_put(OC.cols[o], OC.colw[o], row, v[o]);
     } else if (out_vals) {
         if (NO % 2 == 0) {
+            // a row of NO words as 16-byte stores: consecutive lanes fill whole lines
             longlong2* dst = (longlong2*)(out_vals + row * NO);
 #pragma unroll
             for (int o = 0; o < NO; o += 2) dst[o / 2] = make_longlong2(v[o], v[o + 1]);
@@ -332,9 +340,44 @@ __device__ __forceinline__ void bk_store(const shb_cols& OC, int64_t row, const 
     }
 }
 
+template <int MODE, int NO>
+__device__ __forceinline__ void bk_row(const shb_out& O, const shb_cols& OC, const int32_t* o_kind,
+                                       const int32_t* o_type, const void* const* o_src, int64_t row, int64_t i,
+                                       int64_t mp, uint64_t seq, uint64_t* __restrict__ out_seq,
+                                       int64_t* __restrict__ out_vals) {
+    if (NO > 0) {
+        int64_t v[NO > 0 ? NO : 1];
+        bk_vals<NO>(O, i, mp, v);
+        bk_store<MODE, NO>(OC, row, v, seq, out_seq, out_vals);
+        return;
+    }
+    // any number of values: the descriptors from LDS, one value at a time
+    const int no = O.n_out;
+    if (MODE == SHB_OUT_PACKED) {
+        uint32_t* r = (uint32_t*)OC.rows + row * OC.rw;
+        r[0] = (uint32_t)seq;
+        r[1] = (uint32_t)(seq >> 32);
+        for (int k = 2; k < OC.rw; k++) r[k] = 0u;
+    } else if (out_seq) {
+        out_seq[row] = seq;
+    }
+    for (int o = 0; o < no; o++) {
+        const int64_t v = bk_raw(o_src[o], o_kind[o] == 1 ? i : mp, o_type[o]);
+        if (MODE == SHB_OUT_PACKED) {
+            uint32_t* r = (uint32_t*)OC.rows + row * OC.rw + OC.woff[o];
+            r[0] = OC.colw[o] == 1 ? (uint32_t)(uint8_t)v : (uint32_t)v;
+            if (OC.colw[o] == 8) r[1] = (uint32_t)((uint64_t)v >> 32);
+        } else if (MODE == SHB_OUT_COLS) {
+            bk_put(OC.cols[o], OC.colw[o], row, v);
+        } else if (out_vals) {
+            out_vals[row * no + o] = v;
+        }
+    }
+}
+
 #define BK_RU 4  // rows per lane whose loads are issued before their stores
 
-template <bool COLS, int NO>
+template <int MODE, int NO>
 __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, shb_cols OC, uint64_t seq_base,
                                                     uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_vals,
                                                     int64_t out_cap) {
@@ -366,20 +409,22 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
                 o_src[o] = O.src[o];
             }
     }
-    // the events of this wave (arrival order): key and slot, loaded up front
-    int32_t kk[BK_ITEMS];
+    // the events of this wave (arrival order): their slots, loaded up front (the
+    // bucket of a slot follows from the tile's bucket starts: no key read)
     uint32_t sl[BK_ITEMS];
     {
         const int l0 = w * (64 * BK_ITEMS) + lane;
 #pragma unroll
         for (int j = 0; j < BK_ITEMS; j++) {
             const int l = l0 + j * 64;
-            kk[j] = l < tile_n ? P.keys[b0 + l] : -1;
-            sl[j] = l < tile_n ? (uint32_t)P.sp[b0 + l] : 0u;
+            sl[j] = l < tile_n ? (uint32_t)P.sp[b0 + l] : BK_NOSLOT;
         }
     }
     // 1. counts in the tile's bucket order -> pfx (loaded with the events; the
-    // slots past the tile's valid events are masked below)
+    // slots past the tile's valid events are masked below). Each word holds the
+    // exclusive prefix (< 2^21: 8,192 counts of at most 255) and, in its top 8
+    // bits, the slot's bucket: a thread's 16 consecutive slots find theirs by one
+    // binary search over the bucket starts and a forward walk
     {
         const int s0 = threadIdx.x * 16;
         const uint4 q = *(const uint4*)(P.cnt + b0 + s0);
@@ -395,9 +440,20 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
         }
         uint32_t tot;
         uint32_t off = shw_block_excl<BK_TPB>(sum, ws, &tot);
+        int d = 0;  // the last bucket whose start is <= s0
+        {
+            int lo = 0, hi = SHB_NB - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if ((int)to[mid] <= s0) lo = mid;
+                else hi = mid - 1;
+            }
+            d = lo;
+        }
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-            pfx[s0 + k] = off;
+            while (d < SHB_NB - 1 && (int)to[d + 1] <= s0 + k) d++;
+            pfx[s0 + k] = off | ((uint32_t)d << BK_PFX_BITS);
             off += c[k];
         }
         if (threadIdx.x == 0) pfx[SHB_TILE] = tot;
@@ -411,12 +467,13 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
     for (int j = 0; j < BK_ITEMS; j++) {
         uint32_t c = 0;
         mp[j] = 0u;
-        if (kk[j] >= 0) {
-            const uint32_t d = (uint32_t)kk[j] & (SHB_NB - 1);
+        if (sl[j] != BK_NOSLOT) {
             const uint32_t s = sl[j];
-            const uint32_t ps = pfx[s];
-            c = pfx[s + 1] - ps;
-            mp[j] = ms0[d] + ps - pfx[to[d]];
+            const uint32_t pw = pfx[s];
+            const uint32_t d = pw >> BK_PFX_BITS;
+            const uint32_t ps = pw & BK_PFX_MASK;
+            c = (pfx[s + 1] & BK_PFX_MASK) - ps;
+            mp[j] = ms0[d] + ps - (pfx[to[d]] & BK_PFX_MASK);
         }
         if ((j & 3) == 0) cp[j >> 2] = 0u;
         cp[j >> 2] |= c << (8 * (j & 3));
@@ -476,7 +533,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
 #pragma unroll
                     for (int u = 0; u < BK_RU; u++)
                         if (ok[u])
-                            bk_store<COLS, NV>(OC, (int64_t)rb + t0 + u * 64 + lane, v[u],
+                            bk_store<MODE, NV>(OC, (int64_t)rb + t0 + u * 64 + lane, v[u],
                                                            seq_base + (uint64_t)ii[u], out_seq, out_vals);
                 }
             } else {
@@ -486,7 +543,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
                     const int64_t i = ib + e;
                     const int64_t row = (int64_t)rb + t;
                     if (row >= out_cap) continue;  // the host reports SH_E_MORE
-                    bk_row<COLS, NO>(O, OC, o_kind, o_type, o_src, row, i, (int64_t)emp[w][e] + k,
+                    bk_row<MODE, NO>(O, OC, o_kind, o_type, o_src, row, i, (int64_t)emp[w][e] + k,
                                      seq_base + (uint64_t)i, out_seq, out_vals);
                 }
             }
@@ -500,7 +557,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
                 for (uint32_t k = 0; k < c; k++) {
                     const int64_t row = (int64_t)rb + ro8[jj] + k;
                     if (row >= out_cap) break;
-                    bk_row<COLS, NO>(O, OC, o_kind, o_type, o_src, row, i, (int64_t)mp[j] + k,
+                    bk_row<MODE, NO>(O, OC, o_kind, o_type, o_src, row, i, (int64_t)mp[j] + k,
                                      seq_base + (uint64_t)i, out_seq, out_vals);
                 }
             }
@@ -1085,35 +1142,39 @@ extern "C" int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream)
     return bk_ok();
 }
 
-template <bool COLS, int NO>
+template <int MODE, int NO>
 static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& OC, uint64_t seq_base,
                            uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
-    hipLaunchKernelGGL((k_bk_emit<COLS, NO>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P, *O, OC,
+    hipLaunchKernelGGL((k_bk_emit<MODE, NO>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P, *O, OC,
                        seq_base, out_seq, out_vals, out_cap);
 }
 
-template <bool COLS>
+template <int MODE>
 static void bk_emit_width(const shb_plan* P, const shb_out* O, const shb_cols& OC, uint64_t seq_base,
                           uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
     switch (O->n_out) {
-        case 1: bk_emit_launch<COLS, 1>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
-        case 2: bk_emit_launch<COLS, 2>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
-        case 3: bk_emit_launch<COLS, 3>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
-        case 4: bk_emit_launch<COLS, 4>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
-        case 5: bk_emit_launch<COLS, 5>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
-        case 6: bk_emit_launch<COLS, 6>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
-        case 7: bk_emit_launch<COLS, 7>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
-        case 8: bk_emit_launch<COLS, 8>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
-        default: bk_emit_launch<COLS, 0>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 1: bk_emit_launch<MODE, 1>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 2: bk_emit_launch<MODE, 2>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 3: bk_emit_launch<MODE, 3>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 4: bk_emit_launch<MODE, 4>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 5: bk_emit_launch<MODE, 5>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 6: bk_emit_launch<MODE, 6>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 7: bk_emit_launch<MODE, 7>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        case 8: bk_emit_launch<MODE, 8>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
+        default: bk_emit_launch<MODE, 0>(P, O, OC, seq_base, out_seq, out_vals, out_cap, stream); break;
     }
 }
 
 extern "C" int shb_emit(const shb_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base,
                         uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
-    if (OC && OC->use)
-        bk_emit_width<true>(P, O, *OC, seq_base, out_seq, out_vals, out_cap, stream);
-    else
-        bk_emit_width<false>(P, O, shb_cols{}, seq_base, out_seq, out_vals, out_cap, stream);
+    if (OC && OC->use == SHB_OUT_PACKED) {
+        if (OC->rw % 4 || OC->rw > 2 + 2 * SHB_MAX_OUT + 2) return -1;
+        bk_emit_width<SHB_OUT_PACKED>(P, O, *OC, seq_base, out_seq, out_vals, out_cap, stream);
+    } else if (OC && OC->use == SHB_OUT_COLS) {
+        bk_emit_width<SHB_OUT_COLS>(P, O, *OC, seq_base, out_seq, out_vals, out_cap, stream);
+    } else {
+        bk_emit_width<SHB_OUT_RAW>(P, O, shb_cols{}, seq_base, out_seq, out_vals, out_cap, stream);
+    }
     return bk_ok();
 }
 
@@ -1138,5 +1199,40 @@ extern "C" int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, vo
     }
     hipLaunchKernelGGL(k_narrow_rows, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, vals, n_out,
                        m, OC);
+    return bk_ok();
+}
+
+// raw rows (the engines that write 8-byte words) -> the caller's packed rows
+__global__ void __launch_bounds__(256) k_pack_rows(const uint64_t* __restrict__ seq, const int64_t* __restrict__ vals,
+                                                   int32_t n_out, int64_t m, shb_cols OC) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= m) return;
+    uint32_t* row = (uint32_t*)OC.rows + r * OC.rw;
+    const uint64_t q = seq[r];
+    row[0] = (uint32_t)q;
+    row[1] = (uint32_t)(q >> 32);
+    for (int k = 2; k < OC.rw; k++) row[k] = 0u;
+    for (int o = 0; o < n_out; o++) {
+        const int64_t v = vals[r * n_out + o];
+        row[OC.woff[o]] = OC.colw[o] == 1 ? (uint32_t)(uint8_t)v : (uint32_t)v;
+        if (OC.colw[o] == 8) row[OC.woff[o] + 1] = (uint32_t)((uint64_t)v >> 32);
+    }
+}
+
+extern "C" int shd_pack_rows(const uint64_t* seq, const int64_t* vals, int32_t n_out, int64_t m, const int32_t* w,
+                             const int32_t* woff, int32_t rw, void* rows, void* stream) {
+    if (m <= 0) return 0;
+    if (n_out > SHB_MAX_OUT) return -1;
+    shb_cols OC;
+    memset(&OC, 0, sizeof(OC));
+    OC.use = SHB_OUT_PACKED;
+    OC.rw = rw;
+    OC.rows = rows;
+    for (int o = 0; o < n_out; o++) {
+        OC.colw[o] = w[o];
+        OC.woff[o] = woff[o];
+    }
+    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, seq, vals,
+                       n_out, m, OC);
     return bk_ok();
 }

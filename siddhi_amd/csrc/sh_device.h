@@ -175,11 +175,16 @@ struct shb_aggc {
 };
 
 // typed output columns (sh_device_run.d_out_cols) instead of raw 8-byte rows
+#define SHB_OUT_RAW 0      // rows of raw 8-byte words (+ the sequence numbers apart)
+#define SHB_OUT_COLS 1     // one natural-width column per select value (+ sequence numbers)
+#define SHB_OUT_PACKED 2   // packed rows: sequence number, then the values at natural width
 struct shb_cols {
     void* cols[SHB_MAX_OUT];      // natural width per select value
     int32_t colw[SHB_MAX_OUT];    // their widths: 8, 4 or 1 bytes
-    int32_t use;                  // 1: write the columns
-    int32_t pad;
+    int32_t use;                  // SHB_OUT_*
+    int32_t rw;                   // packed: 4-byte words per row (a multiple of 4)
+    int32_t woff[SHB_MAX_OUT];    // packed: word offset of each value in its row
+    void* rows;                   // packed: the rows
 };
 
 #ifdef __cplusplus
@@ -234,6 +239,9 @@ int shb_emit(const shb_plan* P, const shb_out* O, const shb_cols* OC, uint64_t s
              int64_t* out_vals, int64_t out_cap, void* stream);
 // raw 8-byte rows [m x n_out] -> typed columns of widths w[o] (8, 4 or 1 bytes)
 int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, void* const* cols, const int32_t* w, void* stream);
+// raw rows + sequence numbers -> packed rows (SHB_OUT_PACKED; woff / rw as in shb_cols)
+int shd_pack_rows(const uint64_t* seq, const int64_t* vals, int32_t n_out, int64_t m, const int32_t* w,
+                  const int32_t* woff, int32_t rw, void* rows, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -1349,8 +1349,6 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
                                              "beyond the general engine's query table");
     }
     if (h->mode == 1) {
-        const int crc = rows_for_cols(h, run);
-        if (crc) return crc;
         // general engine from fresh per-key state; the events arrive as send()
         // calls of run->batch_events
         if (h->T->has_absent) return fail(h, SH_E_UNSUPPORTED, "sh_run_device: absent states need sh_push_batch");
@@ -1364,11 +1362,16 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
             run->d_out_seq = h->a_seq.as<uint64_t>();
         }
         {
+            // (the sequence bucket-carry engine writes typed columns / packed rows itself)
             const int src = run_s3b(h, run, nkeys);
             if (src != 1) {
                 if (src == SH_OK) h->kstate_stale = true;  // (no key blocks used: reset for a later user)
                 return src;
             }
+        }
+        {
+            const int crc = rows_for_cols(h, run);
+            if (crc) return crc;
         }
         int rc = SH_OK;
         int64_t rows = 0;
@@ -1602,28 +1605,79 @@ static int run_device_entry(sh_handle* h, sh_device_run* user, bool v2) {
 int sh_run_device(sh_handle* h, sh_device_run* user) { return run_device_entry(h, user, false); }
 int sh_run_device_v2(sh_handle* h, sh_device_run* user) { return run_device_entry(h, user, true); }
 
-static int run_device_cols(sh_handle* h, sh_device_run* run) {
-    if (!run->d_out_cols) return run_device_impl(h, run);
-    // typed columns: one output type per select position across the app's queries
-    int32_t w[SHB_MAX_OUT];
-    if (h->n_out > SHB_MAX_OUT) return fail(h, SH_E_UNSUPPORTED, "typed columns: too many select values");
+// the natural width of every select position (typed columns / packed rows)
+static int out_widths(sh_handle* h, int32_t* w, const char* what) {
+    if (h->n_out > SHB_MAX_OUT) return fail(h, SH_E_UNSUPPORTED, std::string(what) + ": too many select values");
     for (int o = 0; o < h->n_out; o++) {
         const int t = o < (int)h->out_types.size() ? h->out_types[o] : SH_T_LONG;
-        if (t == -2) return fail(h, SH_E_UNSUPPORTED, "typed columns: queries select different types at one position");
+        if (t == -2) return fail(h, SH_E_UNSUPPORTED, std::string(what) + ": queries select different types at one position");
         w[o] = type_width(t);
     }
+    return SH_OK;
+}
+
+// packed rows: the sequence number in words 0-1, each value aligned to its width
+// (1-byte values in a 4-byte slot), the row a multiple of 4 words (16 B)
+static void packed_layout(const int32_t* w, int n_out, int32_t* woff, int32_t* rw) {
+    int pos = 2;
+    for (int o = 0; o < n_out; o++) {
+        const int wd = w[o] == 8 ? 2 : 1;
+        if (wd == 2 && (pos & 1)) pos++;
+        woff[o] = pos;
+        pos += wd;
+    }
+    *rw = (pos + 3) & ~3;
+}
+
+int sh_packed_row_layout(sh_handle* h, int32_t* offsets, int32_t cap, int32_t* n_out, int32_t* row_bytes) {
+    if (!h || !n_out || !row_bytes) return SH_E_INVALID_ARG;
+    int32_t w[SHB_MAX_OUT], woff[SHB_MAX_OUT], rw = 0;
+    const int rc = out_widths(h, w, "packed rows");
+    if (rc) return rc;
+    packed_layout(w, h->n_out, woff, &rw);
+    for (int o = 0; o < h->n_out && offsets && o < cap; o++) offsets[o] = woff[o] * 4;
+    *n_out = h->n_out;
+    *row_bytes = rw * 4;
+    return SH_OK;
+}
+
+static int run_device_cols(sh_handle* h, sh_device_run* run) {
+    if (run->out_layout != SH_OUT_RAW && run->out_layout != SH_OUT_PACKED)
+        return fail(h, SH_E_INVALID_ARG, "sh_device_run.out_layout");
+    const bool packed = run->out_layout == SH_OUT_PACKED;
+    if (packed && run->d_out_cols) return fail(h, SH_E_INVALID_ARG, "packed rows and typed columns together");
+    if (packed && !run->d_out_values) return fail(h, SH_E_INVALID_ARG, "packed rows: d_out_values is NULL");
+    if (!run->d_out_cols && !packed) return run_device_impl(h, run);
+    // one output type per select position across the app's queries
+    int32_t w[SHB_MAX_OUT];
+    {
+        const int wrc = out_widths(h, w, packed ? "packed rows" : "typed columns");
+        if (wrc) return wrc;
+    }
+    h->out_mode = packed ? SHB_OUT_PACKED : SHB_OUT_COLS;
+    if (packed) {
+        for (int o = 0; o < h->n_out; o++) h->pk_w[o] = w[o];
+        packed_layout(w, h->n_out, h->pk_woff, &h->pk_rw);
+    }
     int64_t* user_vals = run->d_out_values;
+    uint64_t* user_seq = run->d_out_seq;
     h->cols_rows = false;
     int rc = run_device_impl(h, run);
     if (h->cols_rows) {
         if (rc == SH_OK && run->out_count > 0) {
-            if (shd_narrow_rows(h->w_colrows.as<int64_t>(), h->n_out, run->out_count, run->d_out_cols, w, h->stream) ||
-                hipStreamSynchronize(h->stream) != hipSuccess)
-                rc = fail(h, SH_E_HIP, "typed-column narrowing failed");
+            const int64_t m = std::min(run->out_count, run->out_capacity);
+            const int crc = packed ? shd_pack_rows(h->w_packseq.as<uint64_t>(), h->w_colrows.as<int64_t>(), h->n_out, m,
+                                                   w, h->pk_woff, h->pk_rw, user_vals, h->stream)
+                                   : shd_narrow_rows(h->w_colrows.as<int64_t>(), h->n_out, m, run->d_out_cols, w,
+                                                     h->stream);
+            if (crc || hipStreamSynchronize(h->stream) != hipSuccess)
+                rc = fail(h, SH_E_HIP, packed ? "packed-row conversion failed" : "typed-column narrowing failed");
         }
         h->cols_rows = false;
     }
+    h->out_mode = SHB_OUT_RAW;
     run->d_out_values = user_vals;
+    run->d_out_seq = user_seq;
     return rc;
 }
 

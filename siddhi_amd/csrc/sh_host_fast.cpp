@@ -426,10 +426,11 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     B.n = n;
     B.nt = (int32_t)((n + SHB_TILE - 1) / SHB_TILE);
     B.kb = kb;
-    // tiles per matcher chunk: 3,584 events of a bucket at uniform keys (32 per
-    // tile), so a chunk and its halo fit the LDS span; denser buckets split
+    // tiles per matcher chunk: 7/8 of the pass's consumer limit in events of a
+    // bucket at uniform keys (32 per tile; 56 tiles at 2,048), so a chunk and its
+    // halo fit the LDS span; denser buckets split
     static const int ct_env = getenv("SH_BK_CT") ? atoi(getenv("SH_BK_CT")) : 0;
-    B.ct = ct_env > 0 ? std::min(ct_env, SHB_CT_MAX) : 112;
+    B.ct = ct_env > 0 ? std::min(ct_env, SHB_CT_MAX) : std::min(shj_bucket_chunk() * 7 / 256, SHB_CT_MAX);
     B.n_chunks = (B.nt + B.ct - 1) / B.ct;
     const int64_t slots = (int64_t)B.nt * SHB_TILE;  // the tiles' bucket order
     if (ensure_ws(h, std::max<int64_t>(n, (int64_t)B.nt + 1)) || h->bk_w0.ensure_fresh(slots * 4) ||
@@ -552,12 +553,10 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     h->bk_agg_carried = false;
     shb_cols OC;
     memset(&OC, 0, sizeof(OC));
-    if (run->d_out_cols && !h->cols_rows && (!P.agg_post || carry)) {
-        OC.use = 1;
-        for (int o = 0; o < O.n_out; o++) {
-            OC.cols[o] = run->d_out_cols[o];
-            OC.colw[o] = type_width(O.type[o]);
-        }
+    if (!P.agg_post || carry) {
+        int32_t wd[SHB_MAX_OUT];
+        for (int o = 0; o < O.n_out; o++) wd[o] = type_width(O.type[o]);
+        direct_layout(h, run, wd, O.n_out, &OC);
     }
     B.ts = run->d_ts;
     B.keys = run->d_keys;
@@ -706,12 +705,10 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
         if (O.kind[o] == 0) O.src[o] = B.ms[(int)(intptr_t)O.src[o]];
     shb_cols OC;
     memset(&OC, 0, sizeof(OC));
-    if (run->d_out_cols) {
-        OC.use = 1;
-        for (int o = 0; o < O.n_out; o++) {
-            OC.cols[o] = run->d_out_cols[o];
-            OC.colw[o] = 4;
-        }
+    {
+        int32_t wd[SHB_MAX_OUT];
+        for (int o = 0; o < O.n_out; o++) wd[o] = 4;
+        direct_layout(h, run, wd, O.n_out, &OC);
     }
     B.ts = run->d_ts;
     B.keys = run->d_keys;
@@ -775,12 +772,31 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
 // workspace that sh_run_device narrows afterwards (the bucketed engine writes
 // the columns itself)
 int rows_for_cols(sh_handle* h, sh_device_run* run) {
-    if (!run->d_out_cols || h->cols_rows) return SH_OK;
-    if (h->w_colrows.ensure((size_t)std::max<int64_t>(1, run->out_capacity) * std::max(1, h->n_out) * 8))
-        return fail(h, SH_E_OOM, "typed-column row workspace");
+    if (h->out_mode == SHB_OUT_RAW || h->cols_rows) return SH_OK;
+    const size_t cap = (size_t)std::max<int64_t>(1, run->out_capacity);
+    if (h->w_colrows.ensure(cap * std::max(1, h->n_out) * 8)) return fail(h, SH_E_OOM, "typed-column row workspace");
     run->d_out_values = h->w_colrows.as<int64_t>();
+    if (h->out_mode == SHB_OUT_PACKED) {
+        if (h->w_packseq.ensure(cap * 8)) return fail(h, SH_E_OOM, "packed-row workspace");
+        run->d_out_seq = h->w_packseq.as<uint64_t>();
+    }
     h->cols_rows = true;
     return SH_OK;
+}
+
+void direct_layout(sh_handle* h, sh_device_run* run, const int32_t* widths, int n_out, shb_cols* OC) {
+    memset(OC, 0, sizeof(*OC));
+    if (h->out_mode == SHB_OUT_RAW || h->cols_rows) return;
+    OC->use = h->out_mode;
+    for (int o = 0; o < n_out && o < SHB_MAX_OUT; o++) {
+        OC->colw[o] = h->out_mode == SHB_OUT_PACKED ? h->pk_w[o] : widths[o];
+        if (h->out_mode == SHB_OUT_COLS) OC->cols[o] = run->d_out_cols[o];
+        else OC->woff[o] = h->pk_woff[o];
+    }
+    if (h->out_mode == SHB_OUT_PACKED) {
+        OC->rw = h->pk_rw;
+        OC->rows = run->d_out_values;
+    }
 }
 
 // the running aggregates of the fast engines' ordered rows (sh_agg.hip): SH_OK,

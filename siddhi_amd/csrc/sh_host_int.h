@@ -338,6 +338,12 @@ struct sh_handle {
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
     DevBuf w_colrows;
     bool cols_rows = false;
+    // the caller's layout of this sh_run_device call (SHB_OUT_*): engines that
+    // write it themselves take it, the others write raw rows into w_colrows (and
+    // the sequence numbers into w_packseq) for a conversion afterwards
+    int out_mode = SHB_OUT_RAW;
+    int32_t pk_w[SHB_MAX_OUT], pk_woff[SHB_MAX_OUT], pk_rw = 0;
+    DevBuf w_packseq;
     // aggregators behind the fast engines (sh_agg.hip): scratch, trigger sequence
     // numbers when the caller wants none, and the last run's path
     DevBuf a_scratch, a_seq;
@@ -403,6 +409,9 @@ int bits_for(uint64_t v);
 int carry_setup(sh_handle* h, const sh_device_run* run, shd_payload* carry, void** mid, int* alias,
                 bool used_only = false, bool with_ts = true);
 int rows_for_cols(sh_handle* h, sh_device_run* run);
+// the caller's layout for an engine that writes it itself (typed columns /
+// packed rows, unless the rows were sent to the workspace): OC->use = SHB_OUT_RAW otherwise
+void direct_layout(sh_handle* h, sh_device_run* run, const int32_t* widths, int n_out, shb_cols* OC);
 int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry = false);
 int run_rules(sh_handle* h, sh_device_run* run);
 int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys);

@@ -66,18 +66,20 @@ const int kWalkBlock = env_int("SH_BK_WALK", 4, 2, 16);
 // walks its consumer to the wave's longest walk)
 const int kWalkDyn = env_int("SH_BK_DYN", 1, 0, 1);
 // the bucketed matcher's launch bound: minimum workgroups per CU the register
-// allocation is sized for (its LDS holds two 512-thread workgroups per CU)
-const int kMatchMinBlocks = env_int("SH_BK_MINB", 4, 1, 8);
+// allocation is sized for (the default 3-KB pass's LDS holds three 512-thread
+// workgroups per CU)
+const int kMatchMinBlocks = env_int("SH_BK_MINB", 6, 1, 8);
 // a matcher pass's LDS span and consumer limit (events; multiples of its 512
 // threads, at most SHB_SPAN / SHB_CH): smaller passes take less LDS, so more
-// workgroups share a CU, at the price of more halo events per consumer
+// workgroups share a CU, at the price of more halo events per consumer. 3,072 /
+// 2,048 measured 4.44 vs 4.63 ms for 5,120 / 4,096 on C2 (profiles/r4_c2_span_ab.txt)
 const int kSpan = [] {
-    const int v = env_int("SH_BK_SPAN", SHB_SPAN, 1024, SHB_SPAN);
-    return v % 512 ? SHB_SPAN : v;
+    const int v = env_int("SH_BK_SPAN", 3072, 1024, SHB_SPAN);
+    return v % 512 ? 3072 : v;
 }();
 const int kChunk = [] {
-    const int v = env_int("SH_BK_CH", SHB_CH, 512, SHB_CH);
-    return (v % 512 || v > kSpan) ? (kSpan < SHB_CH ? kSpan : SHB_CH) : v;
+    const int v = env_int("SH_BK_CH", 2048, 512, SHB_CH);
+    return (v % 512 || v > kSpan) ? (kSpan < 2048 ? kSpan : 2048) : v;
 }();
 
 int type_width_of(int t) { return t == SH_T_LONG || t == SH_T_DOUBLE ? 8 : (t == SH_T_BOOL ? 1 : 4); }
@@ -1481,5 +1483,7 @@ unsigned shj_tiles(int64_t n, uint32_t* tiles_per_xcd, uint32_t* ntiles) {
     *tiles_per_xcd = (uint32_t)((t + 7) / 8);
     return *tiles_per_xcd * 8u;
 }
+
+int shj_bucket_chunk(void) { return kChunk; }
 
 int shj_tile_size(void) { return kTile; }

@@ -25,6 +25,8 @@ int shj_window_load(const shp_program* hp, shj_window* out, std::string* err);
 // grid of the XCD-major tile mapping for n events; returns the workgroup count
 unsigned shj_tiles(int64_t n, uint32_t* tiles_per_xcd, uint32_t* ntiles);
 int shj_tile_size(void);
+// the bucketed matcher's consumer limit per pass (events; SH_BK_CH)
+int shj_bucket_chunk(void);
 
 // bucketed window engine matcher (shb_match); ms_attrs: stream attributes the
 // match stream carries (e1-side select values), in match-stream column order

@@ -73,6 +73,35 @@ def test_c2_query_lowers(lib):
     lib.sh_destroy(h)
 
 
+def test_packed_row_layout(lib):
+    """SH_OUT_PACKED: trigger_seq 8 B, then symbol (string id) 4, p1 4, p2 4, a pad to
+    align v2 (long) 8: one 32-byte row for the C2 select"""
+    rc, h, _ = _compile(lib, synth.C2_QUERY)
+    assert rc == abi.SH_OK, lib.sh_last_error(h)
+    offs = (C.c_int32 * 16)()
+    n, rb = C.c_int32(), C.c_int32()
+    assert lib.sh_packed_row_layout(h, offs, 16, C.byref(n), C.byref(rb)) == abi.SH_OK
+    assert (n.value, rb.value, list(offs[:4])) == (4, 32, [8, 12, 16, 24])
+    assert abi.sh_device_run.out_layout.offset == 100
+    lib.sh_destroy(h)
+
+
+def test_packed_rows_decode():
+    """packed_to_raw reads what the layout says (host-side decoder, no device)"""
+    import numpy as np
+    from siddhi_amd.device_run import packed_to_raw
+    rows = np.zeros((2, 32), np.uint8)
+    rows[:, 0:8] = np.array([7, 9], np.uint64).view(np.uint8).reshape(2, 8)
+    rows[:, 8:12] = np.array([3, -1], np.int32).view(np.uint8).reshape(2, 4)
+    rows[:, 12:16] = np.array([1.5, 2.5], np.float32).view(np.uint8).reshape(2, 4)
+    rows[:, 16:20] = np.array([0.25, -4.0], np.float32).view(np.uint8).reshape(2, 4)
+    rows[:, 24:32] = np.array([2**40, -5], np.int64).view(np.uint8).reshape(2, 8)
+    seq, raw = packed_to_raw(rows, [compiler.STRING, compiler.FLOAT, compiler.FLOAT, compiler.LONG], [8, 12, 16, 24], 32)
+    assert seq.tolist() == [7, 9]
+    assert raw[:, 0].tolist() == [3, -1] and raw[:, 3].tolist() == [2**40, -5]
+    assert raw[0, 1] == np.array([1.5], np.float32).view(np.uint32)[0]
+
+
 @pytest.mark.parametrize("text", [
     # C3 (sequence + Kleene count) and a logical pattern: the general engine
     "define stream S (a int); from every e1=S, e2=S[a>e1.a]+, e3=S select e1.a as a insert into O;",

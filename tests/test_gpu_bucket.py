@@ -25,15 +25,25 @@ def _device():
         pytest.skip("no GPU")
 
 
-def _run(app, strings, ts, cols, keys, nk, columns=False):
-    """columns: typed output columns (d_out_cols), returned as raw rows for comparison"""
+def _run(app, strings, ts, cols, keys, nk, columns=False, batch_events=4096):
+    """columns: typed output columns (d_out_cols), "packed": SH_OUT_PACKED rows;
+    both returned as raw rows for comparison"""
     import torch
-    from siddhi_amd.device_run import DeviceRunner, columns_to_raw
+    from siddhi_amd.device_run import DeviceRunner, columns_to_raw, packed_to_raw
     runner = DeviceRunner(compiler.compile_app(app, strings))
     dev = torch.device("cuda:0")
     tcols = [torch.from_numpy(c).to(dev) for c in cols]
+    if columns == "packed":
+        offs, rb = runner.packed_layout()
+        m, rows = runner.run(torch.from_numpy(ts).to(dev), torch.from_numpy(keys).to(dev), tcols, nk,
+                             packed=True, batch_events=batch_events)
+        torch.cuda.synchronize()
+        status, err = runner.bucket_status(), runner.last_error()
+        oseq, ovals = packed_to_raw(rows.cpu().numpy(), runner.out_types, offs, rb)
+        runner.close()
+        return (m, oseq.astype(np.int64), ovals), status, err
     m, oseq, ovals = runner.run(torch.from_numpy(ts).to(dev), torch.from_numpy(keys).to(dev), tcols, nk,
-                                columns=columns)
+                                columns=columns, batch_events=batch_events)
     torch.cuda.synchronize()
     status = runner.bucket_status()
     err = runner.last_error()
@@ -59,15 +69,16 @@ def test_c2_bucket_vs_oracle():
     assert np.array_equal(ovals, vals)
 
 
-@pytest.mark.parametrize("n,nk,bucketed,columns", [(10_000_000, 10_000, 1, False), (100_000_000, 10_000, 1, False),
+@pytest.mark.parametrize("n,nk,bucketed,columns", [(10_000_000, 10_000, 1, False), (100_000_000, 10_000, 1, "packed"),
                                                    (100_000_000, 10_000, 1, True), (3_000_000, 60_000, 1, False),
-                                                   (3_000_000, 60_000, 1, True)])
+                                                   (3_000_000, 60_000, 1, True), (3_000_000, 60_000, 1, "packed")])
 def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed, columns):
     """60k symbols at 100 ev/ms: a key's previous event is often more than a
     window back, so many walks leave their key's run in the span; the halo covers
     the window in time and the check against the latest timestamp before the
     span (tpre) proves those walks complete, so the run stays bucketed.
-    `columns`: typed output columns (the bucketed engine writes them itself)"""
+    `columns`: typed output columns or packed rows (the bucketed engine writes them
+    itself; "packed" at 100M is the bench's layout)"""
     ts, k, p, v = synth.stock_stream(n, nk, 100)
     (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk, columns)
     assert status == bucketed, err
@@ -105,7 +116,8 @@ def test_random_window_queries_bucket_vs_oracle(seed):
         strings.id(f"K{i}")
     ca = compiler.compile_app(app, strings)
     seq, _, vals, nulls = run_columns_oracle(ca, ts, [keys, price, vol, x], keys)
-    (m, oseq, ovals), status, err = _run(app, strings, ts, [keys, price, vol, x], keys, nk)
+    layout = [False, "packed", True][seed % 3]  # raw rows, packed rows, typed columns
+    (m, oseq, ovals), status, err = _run(app, strings, ts, [keys, price, vol, x], keys, nk, layout)
     assert status >= 0, err  # 1 bucketed, 0 another engine (not applicable / premise failed)
     assert m == len(seq), app
     assert np.array_equal(oseq, seq.astype(np.int64)), app
@@ -128,7 +140,7 @@ def test_decreasing_timestamps_fall_back_exactly():
         strings.id(f"K{i}")
     ca = compiler.compile_app(app, strings)
     seq, _, vals, _ = run_columns_oracle(ca, ts, [keys, price, vol, x], keys)
-    (m, oseq, ovals), status, err = _run(app, strings, ts, [keys, price, vol, x], keys, nk)
+    (m, oseq, ovals), status, err = _run(app, strings, ts, [keys, price, vol, x], keys, nk, "packed")
     assert status == 0, "the bucketed engine must not accept decreasing timestamps"
     assert m == len(seq) and np.array_equal(oseq, seq.astype(np.int64)) and np.array_equal(ovals, vals)
 
@@ -153,3 +165,18 @@ def test_long_window_counts_exact():
     (m, oseq, ovals), status, err = _run(app, strings, ts, [keys, price, vol, x], keys, nk)
     assert status >= 0, err
     assert m == len(seq) > 0 and np.array_equal(oseq, seq.astype(np.int64)) and np.array_equal(ovals, vals)
+
+
+@pytest.mark.parametrize("query,layout", [("c3", "packed"), ("c3", True), ("c1", "packed"), ("c2agg", "packed")])
+def test_layouts_on_other_engines(query, layout):
+    """packed rows / typed columns from the engines that write raw rows into the
+    workspace for a conversion (rise-and-fall sequence, the unpartitioned window
+    path, the aggregate post-pass): identical to the raw rows of the same run"""
+    app = {"c3": synth.C3_QUERY, "c1": synth.C1_QUERY, "c2agg": synth.C2_AGG_QUERY}[query]
+    n, nk = 300_000, 2_000
+    ts, k, p, v = synth.stock_stream(n, nk, 100)
+    (m0, seq0, vals0), _, err0 = _run(app, None, ts, [k, p, v], k, nk)
+    (m1, seq1, vals1), _, err1 = _run(app, None, ts, [k, p, v], k, nk, layout)
+    assert m0 == m1 > 0, (err0, err1)
+    assert np.array_equal(seq0, seq1)
+    assert np.array_equal(vals0, vals1)
