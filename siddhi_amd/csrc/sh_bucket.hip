@@ -1202,11 +1202,21 @@ extern "C" int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, vo
     return bk_ok();
 }
 
-// raw rows (the engines that write 8-byte words) -> the caller's packed rows
+// raw rows (the engines that write 8-byte words) -> the caller's packed rows:
+// one row per thread, built in registers and stored as whole 16-byte pieces
+// (bk_pack); NO == 0: any number of values, word by word
+template <int NO>
 __global__ void __launch_bounds__(256) k_pack_rows(const uint64_t* __restrict__ seq, const int64_t* __restrict__ vals,
                                                    int32_t n_out, int64_t m, shb_cols OC) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= m) return;
+    if (NO > 0) {
+        int64_t v[NO > 0 ? NO : 1];
+#pragma unroll
+        for (int o = 0; o < NO; o++) v[o] = vals[r * NO + o];
+        bk_pack<NO>(OC, r, v, seq[r]);
+        return;
+    }
     uint32_t* row = (uint32_t*)OC.rows + r * OC.rw;
     const uint64_t q = seq[r];
     row[0] = (uint32_t)q;
@@ -1232,7 +1242,18 @@ extern "C" int shd_pack_rows(const uint64_t* seq, const int64_t* vals, int32_t n
         OC.colw[o] = w[o];
         OC.woff[o] = woff[o];
     }
-    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, seq, vals,
-                       n_out, m, OC);
+    const dim3 g((unsigned)((m + 255) / 256));
+    hipStream_t st = (hipStream_t)stream;
+    switch (n_out) {
+        case 1: hipLaunchKernelGGL(k_pack_rows<1>, g, dim3(256), 0, st, seq, vals, n_out, m, OC); break;
+        case 2: hipLaunchKernelGGL(k_pack_rows<2>, g, dim3(256), 0, st, seq, vals, n_out, m, OC); break;
+        case 3: hipLaunchKernelGGL(k_pack_rows<3>, g, dim3(256), 0, st, seq, vals, n_out, m, OC); break;
+        case 4: hipLaunchKernelGGL(k_pack_rows<4>, g, dim3(256), 0, st, seq, vals, n_out, m, OC); break;
+        case 5: hipLaunchKernelGGL(k_pack_rows<5>, g, dim3(256), 0, st, seq, vals, n_out, m, OC); break;
+        case 6: hipLaunchKernelGGL(k_pack_rows<6>, g, dim3(256), 0, st, seq, vals, n_out, m, OC); break;
+        case 7: hipLaunchKernelGGL(k_pack_rows<7>, g, dim3(256), 0, st, seq, vals, n_out, m, OC); break;
+        case 8: hipLaunchKernelGGL(k_pack_rows<8>, g, dim3(256), 0, st, seq, vals, n_out, m, OC); break;
+        default: hipLaunchKernelGGL(k_pack_rows<0>, g, dim3(256), 0, st, seq, vals, n_out, m, OC); break;
+    }
     return bk_ok();
 }
