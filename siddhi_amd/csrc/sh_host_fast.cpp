@@ -260,7 +260,7 @@ static int run_rules_sparse(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     if (np > 0 &&
         shr_sparse_match(dT, run->d_ts, run->d_keys, n, dC, h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr,
                          &h->r_img, pr, pr + cap, pr + 2 * cap, key_fill, ctl, np, key_off,
-                         l_p, l_r, l_te, l_q, rec_p, rec_q, rec_r, ctl + 1, rcap, st))
+                         l_p, l_r, l_te, l_q, rec_p, rec_q, rec_r, ctl + 1, rcap, nkeys, st))
         return fail(h, SH_E_HIP, "sparse match launch failed");
     hipMemcpyAsync(rd, ctl, 16, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the sparse match");

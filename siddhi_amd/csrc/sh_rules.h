@@ -106,7 +106,7 @@ int shr_sparse_match(const shr_table* dT, const int64_t* ts, const int32_t* akey
                      const uint8_t* img, const shr_img* I, const uint32_t* pr_p, const uint32_t* pr_r, const uint32_t* pr_key, uint32_t* key_fill,
                      const unsigned long long* ctr, int64_t n_pairs_max, const uint32_t* key_off, uint32_t* l_p,
                      uint32_t* l_r, int64_t* l_te, uint32_t* l_q, uint32_t* rec_p, uint32_t* rec_q, uint32_t* rec_r,
-                     unsigned long long* rctr, int64_t rcap, void* stream);
+                     unsigned long long* rctr, int64_t rcap, int32_t nkeys, void* stream);
 // the run's timestamp range (one read-back), and the 32-bit offsets from `base`
 int shr_ts_range(const int64_t* ts, int64_t n, int64_t* lo, int64_t* hi, void* scratch16, void* stream);
 int shr_ts_to32(const int64_t* ts, int64_t n, int64_t base, uint32_t* t32, void* stream);

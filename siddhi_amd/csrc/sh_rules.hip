@@ -864,21 +864,35 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __rest
                                                          const uint32_t* __restrict__ key_off,
                                                          const uint32_t* __restrict__ l_p,
                                                          const uint32_t* __restrict__ l_r,
-                                                         const int64_t* __restrict__ l_te, uint32_t* __restrict__ l_q) {
+                                                         const int64_t* __restrict__ l_te, uint32_t* __restrict__ l_q,
+                                                         int xcd, float slice_scale) {
     extern __shared__ uint4 s_img[];
     __shared__ const void* s_col[32];
     spa_stage<IMG>(img, I, C, s_img, s_col);
     __syncthreads();
     const SpaRules S{(const uint8_t*)s_img, img, s_col};
+    // XCD-sliced keys (xcd = 1, a grid of a multiple of 8): workgroups are dealt
+    // round-robin to the 8 XCDs, so workgroup w takes only the events whose key lies
+    // in the w % 8-th contiguous eighth of the key space. Each XCD's L2 then holds
+    // one eighth of the list offsets and lists (random reads per event) at the
+    // price of reading every key eight times (sequential). Any placement is
+    // correct (every event belongs to exactly one slice); this one is for speed.
+    const int xs = xcd ? (int)(blockIdx.x & 7u) : 0;
+    const int64_t wb = xcd ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
+    const int64_t nw = xcd ? (int64_t)(gridDim.x >> 3) : (int64_t)gridDim.x;
     // SPA_U events per thread and round: their key, list bounds and first list
     // entry are loaded together (three dependent random reads per event otherwise)
     const int64_t round = (int64_t)SPA_TPB * SPA_U;
-    for (int64_t base = (int64_t)blockIdx.x * round; base < n; base += (int64_t)gridDim.x * round) {
+    for (int64_t base = wb * round; base < n; base += nw * round) {
         int32_t key[SPA_U];
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
             const int64_t q = base + (int64_t)u * SPA_TPB + threadIdx.x;
             key[u] = q < n ? akeys[q] : -1;
+            if (xcd && key[u] >= 0) {
+                const int sl = min(7, (int)((float)key[u] * slice_scale));
+                if (sl != xs) key[u] = -1;
+            }
         }
         uint32_t lo[SPA_U], hi[SPA_U];
 #pragma unroll
@@ -987,7 +1001,7 @@ extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const in
                                 const uint32_t* pr_key, uint32_t* key_fill, const unsigned long long* ctr,
                                 int64_t n_pairs_max, const uint32_t* key_off, uint32_t* l_p, uint32_t* l_r,
                                 int64_t* l_te, uint32_t* l_q, uint32_t* rec_p, uint32_t* rec_q, uint32_t* rec_r,
-                                unsigned long long* rctr, int64_t rcap, void* stream) {
+                                unsigned long long* rctr, int64_t rcap, int32_t nkeys, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const unsigned gp = rgrid(n_pairs_max);
     hipLaunchKernelGGL(k_sparse_place, dim3(gp), dim3(RTPB), 0, st, pr_p, pr_r, pr_key, key_fill, ctr, key_off, dT, ts,
@@ -1003,14 +1017,19 @@ extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const in
         const int64_t gmax = 256LL * std::max(1, std::min(per_cu, 2));
         if (tg > gmax) tg = gmax;
         if (tg < 1) tg = 1;
+        // XCD-sliced keys for large key spaces (SH_SPARSE_XCD=0/1 overrides)
+        static const int xenv = getenv("SH_SPARSE_XCD") ? atoi(getenv("SH_SPARSE_XCD")) : -1;
+        const int xcd = (xenv >= 0 ? xenv : (nkeys >= 65536 ? 1 : 0)) && tg >= 64 ? 1 : 0;
+        if (xcd) tg &= ~7LL;
+        const float scale = 8.0f / (float)std::max(1, nkeys);
         if (use_img)
             hipLaunchKernelGGL(k_sparse_take<true>, dim3((unsigned)tg), dim3(SPA_TPB), (size_t)I->lds, st, dT, ts, akeys,
                                n, dC, img, *I, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
-                               (const int64_t*)l_te, l_q);
+                               (const int64_t*)l_te, l_q, xcd, scale);
         else
             hipLaunchKernelGGL(k_sparse_take<false>, dim3((unsigned)tg), dim3(SPA_TPB), 0, st, dT, ts, akeys, n, dC,
                                (const uint8_t*)nullptr, none, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
-                               (const int64_t*)l_te, l_q);
+                               (const int64_t*)l_te, l_q, xcd, scale);
     }
     hipLaunchKernelGGL(k_sparse_rec, dim3(gp), dim3(256), 0, st, (const uint32_t*)l_p, (const uint32_t*)l_r,
                        (const uint32_t*)l_q, ctr, rec_p, rec_q, rec_r, rctr, rcap);
