@@ -375,9 +375,10 @@ __device__ __forceinline__ void bk_row(const shb_out& O, const shb_cols& OC, con
     }
 }
 
-#define BK_RU 4  // rows per lane whose loads are issued before their stores
+// rows per lane whose loads are issued before their stores (the template's RU:
+// 4 or 6; a half of 512 events has ~290 rows on C2, one round of 6 x 64 rows)
 
-template <int MODE, int NO>
+template <int MODE, int NO, int BK_RU>
 __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, shb_cols OC, uint64_t seq_base,
                                                     uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_vals,
                                                     int64_t out_cap) {
@@ -1145,8 +1146,13 @@ extern "C" int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream)
 template <int MODE, int NO>
 static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& OC, uint64_t seq_base,
                            uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
-    hipLaunchKernelGGL((k_bk_emit<MODE, NO>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P, *O, OC,
-                       seq_base, out_seq, out_vals, out_cap);
+    static const int ru = getenv("SH_BK_RU") && atoi(getenv("SH_BK_RU")) == 4 ? 4 : 6;
+    if (ru == 4 || NO == 0 || NO > 4)
+        hipLaunchKernelGGL((k_bk_emit<MODE, NO, 4>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P,
+                           *O, OC, seq_base, out_seq, out_vals, out_cap);
+    else
+        hipLaunchKernelGGL((k_bk_emit<MODE, NO, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P,
+                           *O, OC, seq_base, out_seq, out_vals, out_cap);
 }
 
 template <int MODE>
