@@ -77,40 +77,41 @@ __device__ __forceinline__ void bk_put(void* col, int w, int64_t row, int64_t v)
 // key >> 8 and the staged columns at T * TILE + slot, the slot of every event
 // (sp, arrival order: the emitter finds an event's count and match-stream
 // position through it) and the tile's bucket starts (toff).
-template <int MINW>
-__global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __restrict__ keys,
+template <int MINW, int TPB>
+__global__ void __launch_bounds__(TPB, MINW) k_bk_scatter(const int32_t* __restrict__ keys,
                                                           const int64_t* __restrict__ ts, int32_t nkeys, shb_plan P) {
-    __shared__ uint32_t wcnt[BK_TPB / 64][256];
+    constexpr int SC_ITEMS = SHB_TILE / TPB;  // events per lane
+    __shared__ uint32_t wcnt[TPB / 64][256];
     __shared__ uint32_t tstart[256];
-    __shared__ uint32_t ws[BK_TPB / 64];
+    __shared__ uint32_t ws[TPB / 64];
     __shared__ uint32_t stage[SHB_TILE];
-    __shared__ int64_t s_tmx[BK_TPB / 64];
+    __shared__ int64_t s_tmx[TPB / 64];
     const int T = bk_tile(P.nt);
     if (T < 0) return;
     const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int c = threadIdx.x; c < (BK_TPB / 64) * 256; c += BK_TPB) (&wcnt[0][0])[c] = 0u;
+    for (int c = threadIdx.x; c < (TPB / 64) * 256; c += TPB) (&wcnt[0][0])[c] = 0u;
     __syncthreads();
     // the keys and timestamps of the tile are loaded up front (one HBM round
     // trip); the packed word is formed in registers
-    int32_t key[BK_ITEMS];
-    uint32_t rw[BK_ITEMS], wp[BK_ITEMS];
+    int32_t key[SC_ITEMS];
+    uint32_t rw[SC_ITEMS], wp[SC_ITEMS];
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     {
-        int64_t tv[BK_ITEMS];
-        const int64_t e0 = b0 + (int64_t)w * (64 * BK_ITEMS) + lane;
+        int64_t tv[SC_ITEMS];
+        const int64_t e0 = b0 + (int64_t)w * (64 * SC_ITEMS) + lane;
         if (b0 + SHB_TILE <= P.n) {
             // a full tile: unpredicated loads at immediate offsets from two bases
             const int32_t* __restrict__ pk = keys + e0;
             const int64_t* __restrict__ pt = ts + e0;
 #pragma unroll
-            for (int j = 0; j < BK_ITEMS; j++) {
+            for (int j = 0; j < SC_ITEMS; j++) {
                 key[j] = pk[j * 64];
                 tv[j] = pt[j * 64];
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < BK_ITEMS; j++) {
+            for (int j = 0; j < SC_ITEMS; j++) {
                 const int64_t i = e0 + j * 64;
                 const bool in = i < P.n;
                 key[j] = in ? keys[i] : -1;
@@ -121,7 +122,7 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
         bool bad = false, badk = false;
         int64_t tmx = INT64_MIN;
 #pragma unroll
-        for (int j = 0; j < BK_ITEMS; j++) {
+        for (int j = 0; j < SC_ITEMS; j++) {
             const int64_t dt = tv[j] - P.tbase;
             if (key[j] >= nkeys) badk = true;
             if (key[j] >= 0 && !P.no_ts && (dt < 0 || dt >= lim)) bad = true;
@@ -146,9 +147,9 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
     // the wave's running count with a returning LDS atomic and the group reads
     // its base from the leader
     {
-        uint32_t old[BK_ITEMS];
+        uint32_t old[SC_ITEMS];
 #pragma unroll
-        for (int j = 0; j < BK_ITEMS; j++) {
+        for (int j = 0; j < SC_ITEMS; j++) {
             const bool valid = rw[j] != ~0u;
             const uint32_t d = (rw[j] >> 16) & (SHB_NB - 1);
             uint64_t peers = __ballot(valid);
@@ -165,7 +166,7 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
             rw[j] = valid ? (r | ((uint32_t)(__ffsll((unsigned long long)peers) - 1) << 8) | (d << 16)) : ~0u;
         }
 #pragma unroll
-        for (int j = 0; j < BK_ITEMS; j++) {
+        for (int j = 0; j < SC_ITEMS; j++) {
             const uint32_t ld = rw[j] == ~0u ? (uint32_t)lane : (rw[j] >> 8) & 63u;
             const uint32_t base = (uint32_t)__shfl((int)old[j], (int)ld);
             if (rw[j] != ~0u) rw[j] = ((base + (rw[j] & 0xFFu)) & 0xFFFFu) | (rw[j] & 0xFF0000u);  // wave rank | bucket << 16
@@ -178,13 +179,13 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
         uint32_t tot = 0;
         if (threadIdx.x < 256) {
 #pragma unroll
-            for (int q = 0; q < BK_TPB / 64; q++) {
+            for (int q = 0; q < TPB / 64; q++) {
                 const uint32_t c = wcnt[q][threadIdx.x];
                 wcnt[q][threadIdx.x] = tot;
                 tot += c;
             }
         }
-        const uint32_t ex = shw_block_excl<BK_TPB>(threadIdx.x < 256 ? tot : 0u, ws, &nvalid);
+        const uint32_t ex = shw_block_excl<TPB>(threadIdx.x < 256 ? tot : 0u, ws, &nvalid);
         if (threadIdx.x < 256) {
             tstart[threadIdx.x] = ex;
             P.toff[(int64_t)T * SHB_TOFF + threadIdx.x] = (uint16_t)ex;
@@ -193,17 +194,17 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
         if (threadIdx.x == 0) {
             int64_t m = s_tmx[0];
 #pragma unroll
-            for (int q = 1; q < BK_TPB / 64; q++) m = s_tmx[q] > m ? s_tmx[q] : m;
+            for (int q = 1; q < TPB / 64; q++) m = s_tmx[q] > m ? s_tmx[q] : m;
             P.tpre[T] = m;
         }
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < BK_ITEMS; j++) {
+    for (int j = 0; j < SC_ITEMS; j++) {
         const bool valid = rw[j] != ~0u;
         const uint32_t d = (rw[j] >> 16) & (SHB_NB - 1);
         rw[j] = valid ? tstart[d] + wcnt[w][d] + (rw[j] & 0xFFFFu) : ~0u;  // the event's slot
-        const int64_t i = b0 + (int64_t)w * (64 * BK_ITEMS) + j * 64 + lane;
+        const int64_t i = b0 + (int64_t)w * (64 * SC_ITEMS) + j * 64 + lane;
         if (i < P.n) P.sp[i] = (uint16_t)rw[j];
         if (valid) stage[rw[j]] = wp[j];
     }
@@ -211,8 +212,8 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
     const int64_t ob = (int64_t)T << SHB_TILE_SHIFT;
 #define BK_WRITE_OUT(TY, DST, EXPR)                                                  \
     {                                                                                \
-        _Pragma("unroll 4") for (int m = 0; m < BK_ITEMS; m++) {                     \
-            const uint32_t l = (uint32_t)(m * BK_TPB + threadIdx.x);                 \
+        _Pragma("unroll 4") for (int m = 0; m < SC_ITEMS; m++) {                     \
+            const uint32_t l = (uint32_t)(m * TPB + threadIdx.x);                 \
             if (l < nvalid) ((TY*)(DST))[EXPR(ob + l)] = (TY)stage[l];               \
         }                                                                            \
         __syncthreads();                                                             \
@@ -226,9 +227,9 @@ __global__ void __launch_bounds__(BK_TPB, MINW) k_bk_scatter(const int32_t* __re
         const int halves = wd == 8 ? 2 : 1;
         for (int hh = 0; hh < halves; hh++) {
 #pragma unroll
-            for (int j = 0; j < BK_ITEMS; j++) {
+            for (int j = 0; j < SC_ITEMS; j++) {
                 if (rw[j] == ~0u) continue;
-                const int64_t i = b0 + (int64_t)w * (64 * BK_ITEMS) + j * 64 + lane;
+                const int64_t i = b0 + (int64_t)w * (64 * SC_ITEMS) + j * 64 + lane;
                 uint32_t v;
                 if (wd == 8) v = ((const uint32_t*)P.st_src[c])[2 * i + hh];
                 else if (wd == 4) v = ((const uint32_t*)P.st_src[c])[i];
@@ -1105,13 +1106,15 @@ __global__ void __launch_bounds__(256) k_bk_toff_t(const uint16_t* __restrict__ 
 
 extern "C" int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_plan* P, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    // SH_BK_SCAT=1: no occupancy bound on the scatter (more registers, one
-    // workgroup per CU); default: 4 waves per SIMD (two workgroups per CU)
+    // SH_BK_SCAT: 4 (default) 512 threads, 16 events per lane, 4 waves per SIMD;
+    // 1 the same without an occupancy bound; 8: 1,024 threads, 8 events per lane
     static const int scat = getenv("SH_BK_SCAT") ? atoi(getenv("SH_BK_SCAT")) : 4;
     if (scat == 1)
-        hipLaunchKernelGGL(k_bk_scatter<1>, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, nkeys, *P);
+        hipLaunchKernelGGL((k_bk_scatter<1, BK_TPB>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, nkeys, *P);
+    else if (scat == 8)
+        hipLaunchKernelGGL((k_bk_scatter<2, 1024>), dim3(bk_grid(P->nt)), dim3(1024), 0, st, keys, ts, nkeys, *P);
     else
-        hipLaunchKernelGGL(k_bk_scatter<4>, dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, nkeys, *P);
+        hipLaunchKernelGGL((k_bk_scatter<4, BK_TPB>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, nkeys, *P);
     if (bk_ok()) return -3;
     if (P->tstride < P->nt) return -1;
     hipLaunchKernelGGL(k_bk_toff_t, dim3((P->nt + TT_T - 1) / TT_T), dim3(256), 0, st, (const uint16_t*)P->toff, P->nt,
