@@ -1106,9 +1106,11 @@ __global__ void __launch_bounds__(256) k_bk_toff_t(const uint16_t* __restrict__ 
 
 extern "C" int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_plan* P, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    // SH_BK_SCAT: 4 (default) 512 threads, 16 events per lane, 4 waves per SIMD;
-    // 1 the same without an occupancy bound; 8: 1,024 threads, 8 events per lane
-    static const int scat = getenv("SH_BK_SCAT") ? atoi(getenv("SH_BK_SCAT")) : 4;
+    // SH_BK_SCAT: 8 (default) 1,024 threads, 8 events per lane: 61 VGPRs, 8 waves
+    // per SIMD (0.64 vs 0.79 ms on C2 in one call, profiles/r4_c2_scatter_ab.txt);
+    // 4: 512 threads, 16 events per lane, 94 VGPRs, 4 waves per SIMD; 1: the same
+    // without an occupancy bound
+    static const int scat = getenv("SH_BK_SCAT") ? atoi(getenv("SH_BK_SCAT")) : 8;
     if (scat == 1)
         hipLaunchKernelGGL((k_bk_scatter<1, BK_TPB>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, nkeys, *P);
     else if (scat == 8)
