@@ -1108,12 +1108,9 @@ extern "C" int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nke
     hipStream_t st = (hipStream_t)stream;
     // SH_BK_SCAT: 8 (default) 1,024 threads, 8 events per lane: 61 VGPRs, 8 waves
     // per SIMD (0.64 vs 0.79 ms on C2 in one call, profiles/r4_c2_scatter_ab.txt);
-    // 4: 512 threads, 16 events per lane, 94 VGPRs, 4 waves per SIMD; 1: the same
-    // without an occupancy bound
+    // 4: 512 threads, 16 events per lane, 94 VGPRs, 4 waves per SIMD
     static const int scat = getenv("SH_BK_SCAT") ? atoi(getenv("SH_BK_SCAT")) : 8;
-    if (scat == 1)
-        hipLaunchKernelGGL((k_bk_scatter<1, BK_TPB>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, nkeys, *P);
-    else if (scat == 8)
+    if (scat == 8)
         hipLaunchKernelGGL((k_bk_scatter<2, 1024>), dim3(bk_grid(P->nt)), dim3(1024), 0, st, keys, ts, nkeys, *P);
     else
         hipLaunchKernelGGL((k_bk_scatter<4, BK_TPB>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, nkeys, *P);
@@ -1151,13 +1148,11 @@ extern "C" int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream)
 template <int MODE, int NO>
 static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& OC, uint64_t seq_base,
                            uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
-    static const int ru = getenv("SH_BK_RU") && atoi(getenv("SH_BK_RU")) == 4 ? 4 : 6;
-    if (ru == 4 || NO == 0 || NO > 4)
-        hipLaunchKernelGGL((k_bk_emit<MODE, NO, 4>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P,
-                           *O, OC, seq_base, out_seq, out_vals, out_cap);
-    else
-        hipLaunchKernelGGL((k_bk_emit<MODE, NO, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P,
-                           *O, OC, seq_base, out_seq, out_vals, out_cap);
+    // 6 rows per lane and round up to 4 values (1.505 vs 1.526 ms for 4 on C2,
+    // profiles/r4_c2_emit_ru_ab.txt), 4 beyond (registers)
+    constexpr int RU = (NO >= 1 && NO <= 4) ? 6 : 4;
+    hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P, *O,
+                       OC, seq_base, out_seq, out_vals, out_cap);
 }
 
 template <int MODE>
