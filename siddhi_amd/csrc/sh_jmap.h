@@ -22,6 +22,7 @@
 #pragma once
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <functional>
@@ -41,7 +42,7 @@ struct ShJMap {
         uint64_t code;             // position code (rank = bucket << 38 | code)
         int32_t h;                 // spread hash (registered once per key)
         int32_t nx, pv, pa, lf, rt;
-        uint8_t fl;                // 1 present, 2 tree node, 4 red
+        uint8_t fl;                // 1 present, 2 tree node, 4 red, 8 hash set (kept across removal)
     };
     std::vector<Node> nd;
     std::vector<int32_t> tab;      // bin heads, -1 empty
@@ -63,6 +64,16 @@ struct ShJMap {
     void set_hash(int32_t k, int32_t string_hash) {
         ensure(k);
         nd[k].h = spread(string_hash);
+        nd[k].fl |= 8;
+    }
+    bool hashed(int32_t k) const { return k < (int32_t)nd.size() && (nd[k].fl & 8); }
+    // the replay's look-ahead: a key's node, then (hash set) its bin head
+    void prefetch_node(int32_t k) const {
+        if (k >= 0 && k < (int32_t)nd.size()) __builtin_prefetch(&nd[k], 1);
+    }
+    void prefetch_bin(int32_t k) const {
+        if (k >= 0 && k < (int32_t)nd.size() && (nd[k].fl & 8) && !tab.empty())
+            __builtin_prefetch(&tab[(size_t)((cap() - 1) & nd[k].h)], 1);
     }
     bool present(int32_t k) const { return k < (int32_t)nd.size() && (nd[k].fl & 1); }
     bool is_tree(int32_t k) const { return (nd[k].fl & 2) != 0; }
@@ -101,7 +112,7 @@ struct ShJMap {
         const bool tree_bin = first >= 0 && is_tree(first);
         if (!tree_bin)
             for (int32_t e = first; e >= 0; e = nd[e].nx) ++bin_count;
-        nd[k].fl = 1;
+        nd[k].fl = (uint8_t)((nd[k].fl & 8) | 1);
         nd[k].pa = nd[k].lf = nd[k].rt = nd[k].pv = -1;
         if (tree_bin) {
             put_tree_val(first, k);
@@ -135,7 +146,7 @@ struct ShJMap {
             while (nd[p].nx != k) p = nd[p].nx;
             nd[p].nx = nd[k].nx;
         }
-        nd[k].fl = 0;
+        nd[k].fl &= 8;
         nd[k].nx = nd[k].pv = nd[k].pa = nd[k].lf = nd[k].rt = -1;
         --size;
         touch_bin(idx);
@@ -246,7 +257,7 @@ struct ShJMap {
         if (hd < 0) return;
         int32_t tl = -1;
         for (int32_t e = hd; e >= 0; e = nd[e].nx) {  // replacementTreeNode: same list order
-            nd[e].fl = (uint8_t)((nd[e].fl & 1) | 2);
+            nd[e].fl = (uint8_t)((nd[e].fl & 9) | 2);
             nd[e].pa = nd[e].lf = nd[e].rt = -1;
             nd[e].pv = tl;
             tl = e;
@@ -293,14 +304,14 @@ struct ShJMap {
     }
     int32_t untreeify(int32_t head) {
         for (int32_t q = head; q >= 0; q = nd[q].nx) {
-            nd[q].fl &= 1;
+            nd[q].fl &= 9;
             nd[q].pa = nd[q].lf = nd[q].rt = nd[q].pv = -1;
         }
         return head;
     }
     void put_tree_val(int32_t first, int32_t x) {
         const int32_t root = nd[first].pa >= 0 ? root_of(first) : first;
-        nd[x].fl = 1 | 2;
+        nd[x].fl = (uint8_t)((nd[x].fl & 8) | 1 | 2);
         for (int32_t p = root;;) {
             const int dir = dir_for(x, p);
             const int32_t xp = p;
@@ -681,7 +692,29 @@ struct ShSchedModels {
         for (size_t i = 0; i < n; i++) ix[i] = i;
         std::stable_sort(ix.begin(), ix.end(), [&](size_t a, size_t b) { return recs[2 * a] < recs[2 * b]; });
         std::vector<std::vector<int32_t>> rem(maps.size());
-        for (size_t i : ix) {
+        // the records touch random keys of up to 10M: look ahead in the (fixed)
+        // replay order -- the node kPfNode records ahead, its bin head (or its
+        // string hash, first sight of the key) kPfBin ahead
+        const size_t kPfNode = 16, kPfBin = 8;
+        auto pf = [&](size_t j, bool node) {
+            const uint64_t w = recs[2 * ix[j] + 1];
+            const int s = (int)((w >> 32) & 0xFFFF);
+            if ((w >> 48) != 0 || s >= (int)maps.size()) return;
+            const int32_t key = (int32_t)(uint32_t)w;
+            if (node) {
+                maps[s].prefetch_node(key);
+            } else if (maps[s].hashed(key)) {
+                maps[s].prefetch_bin(key);
+            } else if (key >= 0 && key < (int32_t)hash.size()) {
+                __builtin_prefetch(&hash[key]);
+                __builtin_prefetch(&len[key]);
+            }
+        };
+        static const bool pf_on = !(getenv("SH_HIST_PF") && getenv("SH_HIST_PF")[0] == '0');
+        for (size_t j = 0; j < n; j++) {
+            if (pf_on && j + kPfNode < n) pf(j + kPfNode, true);
+            if (pf_on && j + kPfBin < n) pf(j + kPfBin, false);
+            const size_t i = ix[j];
             const uint64_t w = recs[2 * i + 1];
             const int32_t key = (int32_t)(uint32_t)w;
             const int s = (int)((w >> 32) & 0xFFFF);
@@ -690,7 +723,7 @@ struct ShSchedModels {
             ShJMap& M = maps[s];
             if (kind == 0) {
                 M.ensure(key);
-                M.set_hash(key, hash_of(key));
+                if (!M.hashed(key)) M.set_hash(key, hash_of(key));
                 M.compute_if_absent(key);
             } else if (kind == 1) {
                 M.touch();
