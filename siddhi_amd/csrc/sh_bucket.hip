@@ -64,6 +64,11 @@ __device__ __forceinline__ int bk_tile(int nt) {
 static inline unsigned bk_grid(int nt) { return 8u * (unsigned)((nt + 7) >> 3); }
 
 // one typed output column element (sh_device_run.d_out_cols): natural width
+// natural width of a select value's column (bk_raw's reads)
+__device__ __forceinline__ int bk_width(int type) {
+    return (type == SH_T_LONG || type == SH_T_DOUBLE) ? 8 : (type == SH_T_BOOL ? 1 : 4);
+}
+
 __device__ __forceinline__ void bk_put(void* col, int w, int64_t row, int64_t v) {
     if (w == 8) ((int64_t*)col)[row] = v;
     else if (w == 4) ((uint32_t*)col)[row] = (uint32_t)v;
@@ -399,6 +404,24 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
     const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
     const int tile_n = (int)((P.n - b0) < SHB_TILE ? (P.n - b0) : SHB_TILE);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // L2 warming (O.warm = 1): one read per 128-byte line of this wave's consumer-side
+    // columns, issued ahead of the loads the kernel first waits on, so that phase 3's
+    // row loads (rows -> their events, by arrival index) hit L2 instead of HBM; the
+    // values only feed an empty asm at the end (no memory effect)
+    uint32_t warm = 0u;
+    if (NO > 0 && O.warm) {
+        const int64_t e0 = b0 + (int64_t)w * (64 * BK_ITEMS);
+        const int nw = tile_n - w * (64 * BK_ITEMS);
+#pragma unroll
+        for (int o = 0; o < NV; o++) {
+            if (O.kind[o] != 1) continue;
+            const int wd = bk_width(O.type[o]);
+            const int per = 128 / wd;
+            for (int e = lane * per; e < nw && e < 64 * BK_ITEMS; e += 64 * per)
+                warm ^= wd == 1 ? (uint32_t)((const uint8_t*)O.src[o])[e0 + e]
+                                : ((const uint32_t*)O.src[o])[(e0 + e) * (wd / 4)];
+        }
+    }
     if (threadIdx.x <= SHB_NB) to[threadIdx.x] = P.toff[(int64_t)T * SHB_TOFF + threadIdx.x];
     if (threadIdx.x < SHB_NB) ms0[threadIdx.x] = P.mstart[(int64_t)T * SHB_NB + threadIdx.x];
     if (threadIdx.x == 0) s_tb = P.ttot[T];
@@ -460,6 +483,25 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
         }
         if (threadIdx.x == 0) pfx[SHB_TILE] = tot;
         __syncthreads();
+    }
+    // L2 warming of the match stream: the first line (two when longer) of each of the
+    // tile's (tile, bucket) segments that has matches
+    if (NO > 0 && O.warm && threadIdx.x < SHB_NB) {
+        const int bb = threadIdx.x;
+        const uint32_t m0 = pfx[to[bb]] & BK_PFX_MASK, m1 = pfx[to[bb + 1]] & BK_PFX_MASK;
+        if (m1 > m0) {
+            const int64_t p0 = ms0[bb];
+#pragma unroll
+            for (int o = 0; o < NV; o++) {
+                if (O.kind[o] != 0) continue;
+                const int wd = bk_width(O.type[o]);
+                warm ^= wd == 1 ? (uint32_t)((const uint8_t*)O.src[o])[p0] : ((const uint32_t*)O.src[o])[p0 * (wd / 4)];
+                if ((int64_t)(m1 - m0) * wd > 128) {
+                    const int64_t p1 = p0 + 128 / wd;
+                    warm ^= wd == 1 ? (uint32_t)((const uint8_t*)O.src[o])[p1] : ((const uint32_t*)O.src[o])[p1 * (wd / 4)];
+                }
+            }
+        }
     }
     // 2. counts (4 packed per register) and match-stream positions of the wave's events
     uint32_t cp[BK_ITEMS / 4];
@@ -570,6 +612,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    if (NO > 0 && O.warm) asm volatile("" ::"v"(warm));
 }
 
 // ---------------------------------------------------------------- halo bound

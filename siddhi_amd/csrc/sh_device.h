@@ -142,7 +142,7 @@ struct shb_plan {
 // (kind 0) or from the consumer event's attribute idx[o] (kind 1)
 struct shb_out {
     int32_t n_out;
-    int32_t pad;
+    int32_t warm;                 // 1: the emitter warms L2 with its row sources first
     int32_t kind[SHB_MAX_OUT];
     int32_t type[SHB_MAX_OUT];    // sh_type: raw-value conversion
     const void* src[SHB_MAX_OUT]; // kind 0: match-stream column, kind 1: consumer column

@@ -394,6 +394,9 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     shb_out O;
     memset(&O, 0, sizeof(O));
     O.n_out = P.n_out;
+    // the emitter's L2 warming of its row sources (SH_BK_WARM=0: off)
+    static const bool warm_off = getenv("SH_BK_WARM") && getenv("SH_BK_WARM")[0] == '0';
+    O.warm = warm_off ? 0 : 1;
     int ms[SHB_MAX_MS], n_ms = 0;
     const int part_attr = h->part_attr0;
     for (int o = 0; o < P.n_out; o++) {
