@@ -656,6 +656,8 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     shb_out O;
     memset(&O, 0, sizeof(O));
     O.n_out = Q.n_out;
+    static const bool warm_off = getenv("SH_BK_WARM") && getenv("SH_BK_WARM")[0] == '0';
+    O.warm = warm_off ? 0 : 1;  // the emitter's L2 warming (as the window engine's)
     shb_s3 S;
     memset(&S, 0, sizeof(S));
     S.type = ty;
