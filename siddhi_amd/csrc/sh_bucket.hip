@@ -272,6 +272,9 @@ __global__ void __launch_bounds__(TPB, MINW) k_bk_scatter(const int32_t* __restr
 //     consumer-side values are read by arrival index, the e1-side values from
 //     the match stream
 #define BK_EHALF 512   // events of one row-map pass of a wave
+#ifndef BK_WARM_B
+#define BK_WARM_B 64   // bytes per warming read (one read per 64-byte sector)
+#endif
 #define BK_PFX_BITS 24  // pfx words: prefix in the low bits, the slot's bucket above
 #define BK_PFX_MASK ((1u << BK_PFX_BITS) - 1u)
 #define BK_NOSLOT 0xFFFFFFFFu
@@ -404,7 +407,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
     const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
     const int tile_n = (int)((P.n - b0) < SHB_TILE ? (P.n - b0) : SHB_TILE);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // L2 warming (O.warm = 1): one read per 128-byte line of this wave's consumer-side
+    // L2 warming (O.warm = 1): one read per 64-byte sector of this wave's consumer-side
     // columns, issued ahead of the loads the kernel first waits on, so that phase 3's
     // row loads (rows -> their events, by arrival index) hit L2 instead of HBM; the
     // values only feed an empty asm at the end (no memory effect)
@@ -416,7 +419,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
         for (int o = 0; o < NV; o++) {
             if (O.kind[o] != 1) continue;
             const int wd = bk_width(O.type[o]);
-            const int per = 128 / wd;
+            const int per = BK_WARM_B / wd;  // events per warming read
             for (int e = lane * per; e < nw && e < 64 * BK_ITEMS; e += 64 * per)
                 warm ^= wd == 1 ? (uint32_t)((const uint8_t*)O.src[o])[e0 + e]
                                 : ((const uint32_t*)O.src[o])[(e0 + e) * (wd / 4)];
@@ -484,7 +487,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
         if (threadIdx.x == 0) pfx[SHB_TILE] = tot;
         __syncthreads();
     }
-    // L2 warming of the match stream: the first line (two when longer) of each of the
+    // L2 warming of the match stream: the first sector (two when longer) of each of the
     // tile's (tile, bucket) segments that has matches
     if (NO > 0 && O.warm && threadIdx.x < SHB_NB) {
         const int bb = threadIdx.x;
@@ -495,11 +498,8 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
             for (int o = 0; o < NV; o++) {
                 if (O.kind[o] != 0) continue;
                 const int wd = bk_width(O.type[o]);
-                warm ^= wd == 1 ? (uint32_t)((const uint8_t*)O.src[o])[p0] : ((const uint32_t*)O.src[o])[p0 * (wd / 4)];
-                if ((int64_t)(m1 - m0) * wd > 128) {
-                    const int64_t p1 = p0 + 128 / wd;
+                for (int64_t p1 = p0; p1 < p0 + (int64_t)(m1 - m0) && p1 < p0 + 2 * (BK_WARM_B / wd); p1 += BK_WARM_B / wd)
                     warm ^= wd == 1 ? (uint32_t)((const uint8_t*)O.src[o])[p1] : ((const uint32_t*)O.src[o])[p1 * (wd / 4)];
-                }
             }
         }
     }

@@ -80,7 +80,8 @@ const int kSpan = [] {
 // L2 warming of each pass's span (SH_BK_MWARM=0: off): the first line(s) of every
 // consumer / near-halo tile's segment are read as soon as the bucket starts arrive,
 // so the span loads after the segment table's barriers hit L2
-const int kSpanWarm = env_int("SH_BK_MWARM", 1, 0, 1);
+// (off by default: 2.21 vs 2.08 ms on C2 in one call, profiles/r4_c2_emit_warm_ab.txt)
+const int kSpanWarm = env_int("SH_BK_MWARM", 0, 0, 1);
 const int kChunk = [] {
     const int v = env_int("SH_BK_CH", 2048, 512, SHB_CH);
     return (v % 512 || v > kSpan) ? (kSpan < 2048 ? kSpan : 2048) : v;
