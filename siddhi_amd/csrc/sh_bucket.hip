@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(TPB, MINW) k_bk_scatter(const int32_t* __restr
 //     the match stream
 #define BK_EHALF 512   // events of one row-map pass of a wave
 #ifndef BK_WARM_B
-#define BK_WARM_B 64   // bytes per warming read (one read per 64-byte sector)
+#define BK_WARM_B 128  // bytes per warming read (one per 128-byte line; 64 measured 1.43 vs 1.405 ms)
 #endif
 #define BK_PFX_BITS 24  // pfx words: prefix in the low bits, the slot's bucket above
 #define BK_PFX_MASK ((1u << BK_PFX_BITS) - 1u)
@@ -407,7 +407,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
     const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
     const int tile_n = (int)((P.n - b0) < SHB_TILE ? (P.n - b0) : SHB_TILE);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // L2 warming (O.warm = 1): one read per 64-byte sector of this wave's consumer-side
+    // L2 warming (O.warm = 1): one read per 128-byte line of this wave's consumer-side
     // columns, issued ahead of the loads the kernel first waits on, so that phase 3's
     // row loads (rows -> their events, by arrival index) hit L2 instead of HBM; the
     // values only feed an empty asm at the end (no memory effect)
@@ -487,7 +487,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
         if (threadIdx.x == 0) pfx[SHB_TILE] = tot;
         __syncthreads();
     }
-    // L2 warming of the match stream: the first sector (two when longer) of each of the
+    // L2 warming of the match stream: the first line (two when longer) of each of the
     // tile's (tile, bucket) segments that has matches
     if (NO > 0 && O.warm && threadIdx.x < SHB_NB) {
         const int bb = threadIdx.x;
