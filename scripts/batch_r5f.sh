@@ -1,9 +1,5 @@
-B="--config c2 --steps 20 --warmup 3 --cpu-sample 0 --no-verify"
-A="--steps 1 --warmup 0 --cpu-sample 0 --no-verify"
-scripts/gpu.sh bench r5i_w64 --config c2 --steps 20 --warmup 3 \
-&& SH_BK_WARM=0 scripts/gpu.sh bench r5i_w0 $B \
-&& scripts/gpu.sh bench r5i_w64b $B \
-&& SH_BK_WARM=0 scripts/gpu.sh bench r5i_w0b $B \
-&& scripts/gpu.sh pmc r5i_c2f FETCH_SIZE --config c2 $A \
-&& scripts/gpu.sh pmc r5i_c2w WRITE_SIZE --config c2 $A \
-&& scripts/gpu.sh test r5i_bucket tests/test_gpu_bucket.py tests/test_gpu_c3.py
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5j_smoke.log 2>&1 && tail -1 gpurun_out/r5j_smoke.log \
+&& scripts/gpu.sh bench r5j_c2 --config c2 --steps 20 --warmup 3 \
+&& scripts/gpu.sh bench r5j_c3 --config c3 --steps 10 --warmup 2 \
+&& scripts/gpu.sh prof r5j_c2prof --config c2 --steps 5 --warmup 1 --cpu-sample 0 --no-verify \
+&& scripts/gpu.sh test r5j_t tests/test_gpu_bucket.py tests/test_gpu_c3.py tests/test_gpu_agg.py tests/test_gpu_shard.py tests/test_gpu_parity.py
