@@ -157,6 +157,8 @@ struct shb_s3 {
     int32_t op2, dom2, op3, dom3;
     int32_t n_ms;
     int32_t ms_slot[2];
+    int32_t warm;                 // 1: each chunk warms L2 with the next chunk's segments
+    int32_t pad;
 };
 
 // select-clause aggregators carried per key by the bucketed engine (k_bk_aggc):

@@ -661,6 +661,7 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     shb_s3 S;
     memset(&S, 0, sizeof(S));
     S.type = ty;
+    S.warm = getenv("SH_S3B_WARM") && getenv("SH_S3B_WARM")[0] == '0' ? 0 : 1;
     S.op2 = Q.s3_op2;
     S.dom2 = Q.s3_dom2;
     S.op3 = Q.s3_op3;
