@@ -1463,6 +1463,11 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
         if (arc == 1) sequential = true;
         return arc;
     };
+    h->stk_last = 0;
+    if (h->prog.window_ok && !aggp) {
+        const int krc = run_stack(h, run, nkeys);
+        if (krc != 1) return krc;
+    }
     if (h->prog.window_ok) {
         int brc = run_bucket(h, run, nkeys);
         if (brc == SH_OK && aggp && !h->bk_agg_carried) {
@@ -1694,7 +1699,7 @@ int shx_jit_compile(sh_handle* h) {
     return SH_OK;
 }
 
-// 1: the last sh_run_device ran on the bucketed engine; 0: another engine;
+// 2: the last sh_run_device ran on the stack engine, 1: on the bucketed engine; 0: another engine;
 // -1: its matcher could not be built (message in sh_last_error)
 int shx_bucket_status(sh_handle* h) {
     if (!h) return 0;
@@ -1703,8 +1708,11 @@ int shx_bucket_status(sh_handle* h) {
         h->err = h->bk_err;
         return -1;
     }
-    return h->bk_last;
+    return h->stk_last ? 2 : h->bk_last;
 }
+
+// the device flags (SHB_F_* / SHK_F_*) that sent the last run off the stack engine
+int shx_stack_refused(sh_handle* h) { return h ? h->stk_refused : 0; }
 
 // 1: the last general-engine sh_run_device took the rise-and-fall sequence engine
 int shx_seq3_status(sh_handle* h) { return h ? (h->s3b_last ? 2 : h->seq3_last) : 0; }

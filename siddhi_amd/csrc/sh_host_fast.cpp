@@ -635,6 +635,136 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "bucket engine");
 }
 
+// arrival-order stack engine (sh_stack.hip): partitioned `every e1=S[f1] ->
+// e2=S[x.a op e1.a and ...] within W` with the ordering attribute a 4-byte float or
+// int and at most 8 * shk_max_keys() keys, the select list made of e2-side values,
+// e1's partition attribute and e1.a. 0 ok, 1 = not applicable or refused on the
+// device (the caller takes the bucketed engine), SH_E_MORE, <0 error
+int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys) {
+    h->stk_last = 0;
+    h->stk_refused = 0;
+    const char* dis = getenv("SH_DISABLE_STACK");  // (read per call: tests A/B the engines)
+    if (dis && dis[0] && dis[0] != '0') return 1;
+    const shp_program& P = h->prog;
+    const int64_t n = run->n;
+    if (!h->partitioned || !P.out_fast || P.agg_post || n < 4096 || nkeys < 1) return 1;
+    if (h->stk_state == 0) h->stk_state = shj_stack_form(&P, &h->stk) == 0 ? 1 : -1;
+    if (h->stk_state != 1) return 1;
+    if (P.within_ms < 0 || P.within_ms > 65535) return 1;
+    const int kmax = shk_max_keys();
+    int gshift = 1;  // at least two groups: 2,048-event sub-tiles, 64 events per owner wave
+    while (gshift <= 3 && ((int64_t)nkeys + (1 << gshift) - 1) >> gshift > kmax) gshift++;
+    if (gshift > 3) return 1;
+    const shj_stack& S = h->stk;
+    shb_out O;
+    memset(&O, 0, sizeof(O));
+    O.n_out = P.n_out;
+    const int part_attr = h->part_attr0;
+    for (int o = 0; o < P.n_out; o++) {
+        const int a = P.out_attr[o], t = P.attr_type[0][a];
+        O.type[o] = t;
+        const bool fold = a == part_attr && (t == SH_T_STRING || t == SH_T_INT || t == SH_T_LONG || t == SH_T_BOOL);
+        if (P.out_slot[o] == 1 || fold) {
+            O.kind[o] = 1;
+            O.src[o] = run->d_cols[a];
+        } else if (a == S.xattr) {
+            O.kind[o] = SHB_OUT_KIND_Y;
+        } else {
+            return 1;  // another e1-side value: the bucketed engine's match stream
+        }
+    }
+    hipStream_t st = h->stream;
+    shk_plan K;
+    memset(&K, 0, sizeof(K));
+    K.n = n;
+    K.ts = run->d_ts;
+    K.keys = run->d_keys;
+    K.xcol = run->d_cols[S.xattr];
+    K.dom = S.dom;
+    K.op = S.op;
+    K.nkeys = nkeys;
+    K.gshift = gshift;
+    K.kpw = (int32_t)(((int64_t)nkeys + (1 << gshift) - 1) >> gshift);
+    K.within = P.within_ms;
+    K.n_terms = S.n_terms;
+    for (int k = 0; k < S.n_terms; k++) {
+        K.terms[k] = S.terms[k];
+        K.tl[k] = run->d_cols[S.terms[k].lattr];
+        K.tr[k] = S.terms[k].rkind == 1 ? nullptr : run->d_cols[S.terms[k].rattr];
+    }
+    const int64_t sub = (int64_t)1024 << gshift;  // events per sub-tile (EPL = G)
+    K.nsub = (int32_t)((n + sub - 1) / sub);
+    // chunks: one workgroup per CU (256 >> gshift chunks), each at least four
+    // windows of events at the stream's mean rate (the halo replay <= 25%)
+    if (h->bk_rd.ensure(64)) return fail(h, SH_E_OOM, "stack engine");
+    hipMemcpyAsync(h->bk_rd.as<void>(0), run->d_ts, 8, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(h->bk_rd.as<void>(8), run->d_ts + (n - 1), 8, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "stack engine: timestamp read");
+    const int64_t span = *h->bk_rd.as<int64_t>(8) - *h->bk_rd.as<int64_t>(0);
+    if (span < 0) return 1;  // timestamps go back
+    const double rate = (double)n / (double)(span + 1);  // events per ms
+    const int64_t min_chunk = (int64_t)(4.0 * rate * (double)(P.within_ms + 1)) + sub;
+    int n_chunks = 256 >> gshift;
+    for (;;) {
+        int64_t chunk = (n + n_chunks - 1) / n_chunks;
+        if (chunk < min_chunk) chunk = min_chunk;
+        chunk = (chunk + sub - 1) / sub * sub;
+        K.chunk = chunk;
+        K.n_chunks = (int32_t)((n + chunk - 1) / chunk);
+        K.cpx = (K.n_chunks + 7) / 8;
+        const int64_t grid = (int64_t)8 * K.cpx << gshift;
+        if (h->k_cnt.ensure_fresh((size_t)n) || h->k_ttot.ensure_fresh(((size_t)K.nsub + 1) * 4) ||
+            h->k_hstart.ensure_fresh((size_t)K.n_chunks * 8) || h->k_flag.ensure_fresh(64) ||
+            h->k_spill.ensure_fresh((size_t)grid * K.kpw * 32 * 8) ||
+            h->k_scan.ensure_fresh(shd_scan_tmp_words((int64_t)K.nsub + 1) * 4 + 64))
+            return fail(h, SH_E_OOM, "stack engine workspace");
+        K.cnt = h->k_cnt.as<uint8_t>();
+        K.ttot = h->k_ttot.as<uint32_t>();
+        K.hstart = h->k_hstart.as<int64_t>();
+        K.spill = h->k_spill.as<uint64_t>();
+        K.flag = h->k_flag.as<int32_t>();
+        shb_cols OC;
+        int32_t wd[SHB_MAX_OUT];
+        for (int o = 0; o < O.n_out; o++) wd[o] = type_width(O.type[o]);
+        direct_layout(h, run, wd, O.n_out, &OC);
+        hipEventRecord(h->ev[0], st);
+        hipMemsetAsync(K.flag, 0, 4, st);
+        hipMemsetAsync(K.ttot, 0, ((size_t)K.nsub + 1) * 4, st);
+        if (shk_count(&K, st)) return fail(h, SH_E_HIP, "stack engine count launch failed");
+        hipEventRecord(h->ev[1], st);
+        if (shd_exclusive_scan(K.ttot, K.ttot, (int64_t)K.nsub + 1, h->k_scan.as<uint32_t>(), st))
+            return fail(h, SH_E_HIP, "stack engine scan failed");
+        hipEventRecord(h->ev[2], st);
+        if (shk_emit(&K, &O, &OC, 0, run->d_out_seq, run->d_out_values, run->out_capacity, st))
+            return fail(h, SH_E_HIP, "stack engine emit launch failed");
+        hipEventRecord(h->ev[3], st);
+        hipMemcpyAsync(h->bk_rd.as<void>(0), K.flag, 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(h->bk_rd.as<void>(8), K.ttot + K.nsub, 4, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the stack engine");
+        const int32_t flag = *h->bk_rd.as<int32_t>(0);
+        if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
+        if (flag == SHB_F_HALO && n_chunks > 1) {
+            n_chunks = std::max(1, n_chunks / 4);  // bursty timestamps: longer chunks
+            continue;
+        }
+        if (flag) {
+            h->stk_refused = flag;
+            return 1;
+        }
+        const int64_t total = *h->bk_rd.as<uint32_t>(8);
+        run->out_count = total;
+        if (total > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
+        if (run->d_out_query && total > 0) hipMemsetAsync(run->d_out_query, 0, total * 4, st);
+        h->times.segment_ms = 0.0f;
+        hipEventElapsedTime(&h->times.advance_ms, h->ev[0], h->ev[2]);
+        hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
+        hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
+        h->times.advance_launches = 1;
+        h->stk_last = 1;
+        return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "stack engine");
+    }
+}
+
 // the rise-and-fall sequence on the bucket-carry engine (sh_bucket.hip k_s3b):
 // the tile-local bucket partition, one workgroup per bucket carrying its keys'
 // state across the stream, the ordered rows by k_bk_emit. 0 ok, 1 = not

@@ -335,6 +335,12 @@ struct sh_handle {
     DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS], bk_agg[SHB_MAX_AGG];
     bool bk_agg_carried = false;  // the last bucketed run carried its aggregates (k_bk_aggc)
     PinBuf bk_rd;
+    // ---- arrival-order stack engine (sh_stack.hip): 0 untried, 1 applicable, -1 not
+    int stk_state = 0;
+    int stk_last = 0;             // 1: the last sh_run_device ran on the stack engine
+    int stk_refused = 0;          // the device flags of the last refused run (diagnostics)
+    shj_stack stk{};
+    DevBuf k_cnt, k_ttot, k_hstart, k_spill, k_flag, k_scan;
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
     DevBuf w_colrows;
     bool cols_rows = false;
@@ -413,6 +419,7 @@ int rows_for_cols(sh_handle* h, sh_device_run* run);
 // packed rows, unless the rows were sent to the workspace): OC->use = SHB_OUT_RAW otherwise
 void direct_layout(sh_handle* h, sh_device_run* run, const int32_t* widths, int n_out, shb_cols* OC);
 int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry = false);
+int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys);
 int run_rules(sh_handle* h, sh_device_run* run);
 int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys);
 shd_segment_ws seg_ws(sh_handle* h, int64_t n);
@@ -423,6 +430,7 @@ extern "C" {
 int shx_jit_status(sh_handle* h);
 int shx_jit_compile(sh_handle* h);
 int shx_bucket_status(sh_handle* h);
+int shx_stack_refused(sh_handle* h);
 int shx_seq3_status(sh_handle* h);
 int shx_agg_status(sh_handle* h);
 int shx_rules_status(sh_handle* h);

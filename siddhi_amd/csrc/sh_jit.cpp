@@ -1504,3 +1504,25 @@ unsigned shj_tiles(int64_t n, uint32_t* tiles_per_xcd, uint32_t* ntiles) {
 int shj_bucket_chunk(void) { return kChunk; }
 
 int shj_tile_size(void) { return kTile; }
+
+int shj_stack_form(const shp_program* hp, shj_stack* out) {
+    memset(out, 0, sizeof(*out));
+    ExtForm F;
+    if (!hp->window_ok || !ext_form(*hp, F)) return -1;
+    // every consumer must take part: an event that skipped the consumer step but
+    // opened a partial would break the stack's order
+    if (!F.cross || !F.qonly.empty()) return -1;
+    const shp_term& T = F.ct;
+    if (T.rkind != 0 || T.lattr != T.rattr || T.ltype != T.rtype) return -1;
+    if (!((T.ltype == SH_T_FLOAT && F.dom == DOM_F32) || (T.ltype == SH_T_INT && F.dom == DOM_I32))) return -1;
+    if (F.f1.size() + F.ionly.size() > 4) return -1;
+    out->op = F.op;
+    out->dom = F.dom;
+    out->xattr = T.lattr;
+    for (const shp_term& t : F.f1) out->terms[out->n_terms++] = t;
+    for (const shp_term& t : F.ionly) {
+        if (t.lslot != 0 || (t.rkind != 1 && t.rslot != 0)) return -1;
+        out->terms[out->n_terms++] = t;
+    }
+    return 0;
+}

@@ -5,6 +5,7 @@ trigger sequence numbers and raw select values. The engine's device premises
 (packed timestamp range, non-decreasing timestamps per key, halo coverage,
 <= 255 partials per consumer) send the run back to the general window path;
 those cases must stay exact too."""
+import os
 import random
 
 import numpy as np
@@ -25,9 +26,23 @@ def _device():
         pytest.skip("no GPU")
 
 
-def _run(app, strings, ts, cols, keys, nk, columns=False, batch_events=4096):
+def _run(app, strings, ts, cols, keys, nk, columns=False, batch_events=4096, engine=None):
     """columns: typed output columns (d_out_cols), "packed": SH_OUT_PACKED rows;
-    both returned as raw rows for comparison"""
+    both returned as raw rows for comparison. engine="bucket": the stack engine
+    (sh_stack.hip) is switched off for the call (SH_DISABLE_STACK)"""
+    old = os.environ.get("SH_DISABLE_STACK")
+    if engine == "bucket":
+        os.environ["SH_DISABLE_STACK"] = "1"
+    try:
+        return _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events)
+    finally:
+        if old is None:
+            os.environ.pop("SH_DISABLE_STACK", None)
+        else:
+            os.environ["SH_DISABLE_STACK"] = old
+
+
+def _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events):
     import torch
     from siddhi_amd.device_run import DeviceRunner, columns_to_raw, packed_to_raw
     runner = DeviceRunner(compiler.compile_app(app, strings))
@@ -57,22 +72,26 @@ def _run(app, strings, ts, cols, keys, nk, columns=False, batch_events=4096):
     return res, status, err
 
 
-def test_c2_bucket_vs_oracle():
+@pytest.mark.parametrize("engine,expect", [("bucket", 1), (None, 2)])
+def test_c2_bucket_vs_oracle(engine, expect):
+    """status 1: the bucketed engine (stack engine off), 2: the stack engine"""
     n, nk = 400_000, 2_000
     ts, k, p, v = synth.stock_stream(n, nk, 100)
     ca = compiler.compile_app(synth.C2_QUERY)
     seq, _, vals, _ = run_stock_oracle(ca, ts, k, p, v)
-    (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk)
-    assert status == 1, err
+    (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk, engine=engine)
+    assert status == expect, err
     assert m == len(seq) > 0
     assert np.array_equal(oseq, seq.astype(np.int64))
     assert np.array_equal(ovals, vals)
 
 
-@pytest.mark.parametrize("n,nk,bucketed,columns", [(10_000_000, 10_000, 1, False), (100_000_000, 10_000, 1, "packed"),
-                                                   (100_000_000, 10_000, 1, True), (3_000_000, 60_000, 1, False),
-                                                   (3_000_000, 60_000, 1, True), (3_000_000, 60_000, 1, "packed")])
-def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed, columns):
+@pytest.mark.parametrize("n,nk,bucketed,columns,engine", [
+    (10_000_000, 10_000, 1, False, "bucket"), (10_000_000, 10_000, 2, False, None),
+    (100_000_000, 10_000, 2, "packed", None), (100_000_000, 10_000, 1, "packed", "bucket"),
+    (100_000_000, 10_000, 2, True, None), (3_000_000, 60_000, 1, False, None),
+    (3_000_000, 60_000, 1, True, None), (3_000_000, 60_000, 1, "packed", None)])
+def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed, columns, engine):
     """60k symbols at 100 ev/ms: a key's previous event is often more than a
     window back, so many walks leave their key's run in the span; the halo covers
     the window in time and the check against the latest timestamp before the
@@ -80,7 +99,7 @@ def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed, columns):
     `columns`: typed output columns or packed rows (the bucketed engine writes them
     itself; "packed" at 100M is the bench's layout)"""
     ts, k, p, v = synth.stock_stream(n, nk, 100)
-    (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk, columns)
+    (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk, columns, engine=engine)
     assert status == bucketed, err
     eseq, evals = c2_expected(ts, k, p, v)
     assert m == len(eseq) > 0
@@ -141,7 +160,7 @@ def test_decreasing_timestamps_fall_back_exactly():
     ca = compiler.compile_app(app, strings)
     seq, _, vals, _ = run_columns_oracle(ca, ts, [keys, price, vol, x], keys)
     (m, oseq, ovals), status, err = _run(app, strings, ts, [keys, price, vol, x], keys, nk, "packed")
-    assert status == 0, "the bucketed engine must not accept decreasing timestamps"
+    assert status == 0, "the stack and bucketed engines must not accept decreasing timestamps"
     assert m == len(seq) and np.array_equal(oseq, seq.astype(np.int64)) and np.array_equal(ovals, vals)
 
 
