@@ -80,7 +80,12 @@ int sh_start(sh_handle* h);
 /* Replaces InputHandler.send(Event[]) -> StreamJunction.sendEvent ->
    [PartitionStreamReceiver.receive] -> Pattern/Sequence*ProcessStreamReceiver.receive
    (core/stream/input/InputHandler.java:85-96, core/partition/PartitionStreamReceiver.java:176-216,
-   core/query/input/MultiProcessStreamReceiver.java:155-183). */
+   core/query/input/MultiProcessStreamReceiver.java:155-183).
+   Streaming handles (general engine) launch a push's device work and return
+   before it completes: an error the device raises for that batch (state or replay
+   capacity, a key id out of range) is returned by the NEXT call into the handle --
+   sh_push_batch, sh_drain, sh_pending, sh_advance_time, sh_snapshot or
+   sh_run_device -- and the handle keeps the state from before the failed batch. */
 int sh_push_batch(sh_handle* h, const sh_batch* batch);
 
 /* Registers attr.toString() of partition key ids [first_key, first_key + n) as
@@ -165,7 +170,11 @@ typedef struct sh_device_run {
 #define SH_OUT_RAW 0
 #define SH_OUT_PACKED 1
 
-/* reads the V1 prefix of *run (SH_DEVICE_RUN_V1_BYTES) and writes out_count */
+/* reads the V1 prefix of *run (SH_DEVICE_RUN_V1_BYTES) and writes out_count.
+   Layout 2 (sh_version() "... layout 2"): the 0.1 header of round 3 had version /
+   pad at offset 88 and d_out_cols at 96; a caller still built against it leaves a
+   small integer in d_out_cols and gets SH_E_INVALID_ARG instead of a write
+   through it -- rebuild the binding against this header. */
 int sh_run_device(sh_handle* h, sh_device_run* run);
 /* the whole struct; SH_E_INVALID_ARG unless run->version == SH_DEVICE_RUN_V2 */
 int sh_run_device_v2(sh_handle* h, sh_device_run* run);

@@ -7,7 +7,7 @@
 // needs one returns SH_E_NO_DEVICE.
 #include "sh_host_int.h"
 
-#define SH_VERSION_STR "siddhi_hip 0.1 (gfx950)"
+#define SH_VERSION_STR "siddhi_hip 0.2 (gfx950; sh_device_run layout 2)"
 
 namespace {
 
@@ -881,12 +881,13 @@ static int push_impl(sh_handle* h, const sh_batch* b, const uint32_t* index, int
         pin_off += (size_t)b->n * w;
         const uint8_t* nm = b->nulls ? b->nulls[a] : nullptr;
         if (nm || st.has_nul[a]) {
-            if (!st.has_nul[a]) {
-                if ((size_t)(r0 + b->n) > st.nuls[a].bytes && h->mode == 1) {
+            // the mask moves when it grows: a pending launch reads it (settle first)
+            if ((size_t)(r0 + b->n) > st.nuls[a].bytes && h->mode == 1) {
                 const int src = nf_settle(h);
                 if (src) return src;
             }
-            if (st.nuls[a].ensure((size_t)(r0 + b->n))) return fail(h, SH_E_OOM, "null mask");
+            if (!st.has_nul[a]) {
+                if (st.nuls[a].ensure((size_t)(r0 + b->n))) return fail(h, SH_E_OOM, "null mask");
                 hipMemsetAsync(st.nuls[a].p, 0, r0, h->stream);
                 st.has_nul[a] = true;
             } else if (st.nuls[a].ensure((size_t)(r0 + b->n))) {
@@ -944,6 +945,10 @@ int sh_set_partition_keys(sh_handle* h, int32_t first_key, int32_t n, const uint
         if (!frc) frc = nf_sev_flush(h);  // (the replay thread reads the key strings)
         if (frc) return frc;
     }
+    if (!h->sm.keys_settable(first_key, n, utf16, offsets))
+        return fail(h, SH_E_INVALID_ARG,
+                    "sh_set_partition_keys: a key id was used before its string was registered (its scheduler "
+                    "map position follows the old string); register strings before the ids appear");
     h->sm.set_keys(first_key, n, utf16, offsets);
     return SH_OK;
 }
@@ -1602,6 +1607,13 @@ static int run_device_entry(sh_handle* h, sh_device_run* user, bool v2) {
     } else {
         memcpy(&r, user, SH_DEVICE_RUN_V1_BYTES);
     }
+    // a binding built against the 0.1 header (version / pad at offset 88, the
+    // typed columns at 96) leaves a small integer where d_out_cols now sits:
+    // refuse it rather than write through it
+    if (r.d_out_cols && (uintptr_t)r.d_out_cols < 65536)
+        return fail(h, SH_E_INVALID_ARG,
+                    "sh_run_device: d_out_cols holds a small integer (a caller built against the 0.1 "
+                    "sh_device_run layout, version at offset 88?) -- rebuild against this header");
     const int rc = run_device_cols(h, &r);
     user->out_count = r.out_count;
     return rc;

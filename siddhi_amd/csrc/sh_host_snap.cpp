@@ -233,7 +233,10 @@ int sh_snapshot(sh_handle* h, void* buf, int64_t cap, int64_t* size) {
         h->kstate_stale = false;
     }
     if (h->has_device) {
-        const int frc = nf_sev_flush(h);  // the models and ranks the image holds
+        // settle the pending launch first (it queues its scheduler history), then
+        // wait for the history thread: the image reads the models and ranks
+        int frc = h->mode == 2 ? SH_OK : flush(h);
+        if (!frc) frc = nf_sev_flush(h);
         if (frc) return frc;
     }
     SnapW w;

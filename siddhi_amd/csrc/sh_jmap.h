@@ -641,6 +641,20 @@ struct ShSchedModels {
         used = ids;
         for (int s : ids) maps[s].cmp = [this](int32_t a, int32_t b) { return compare(a, b); };
     }
+    // false: some id in [first, first + n) already sits in a map under the hash of
+    // another string (it was used before its string was registered; its bin -- and
+    // so the due-timer tie order -- would stay that of the old string)
+    bool keys_settable(int32_t first, int32_t n, const uint16_t* utf16, const int64_t* offsets) const {
+        for (int32_t i = 0; i < n; i++) {
+            const int32_t k = first + i;
+            bool used_k = false;
+            for (const ShJMap& M : maps) used_k = used_k || M.hashed(k);
+            if (!used_k) continue;
+            const int32_t nh = sh_java_string_hash(utf16 + offsets[i], offsets[i + 1] - offsets[i]);
+            if (nh != hash_of(k)) return false;
+        }
+        return true;
+    }
     void set_keys(int32_t first, int32_t n, const uint16_t* utf16, const int64_t* offsets) {
         const size_t need = (size_t)first + (size_t)n;
         if (off.size() < need) {

@@ -150,3 +150,18 @@ def test_no_cpu_fallback_without_device(lib):
 
 def test_version_string(lib):
     assert b"gfx950" in lib.sh_version()
+
+
+def test_round3_layout_caller_is_refused(lib):
+    """a binding built against the 0.1 header put version (2) at offset 88, where
+    d_out_cols now sits: sh_run_device refuses the struct instead of treating the
+    integer as a column-pointer array (checked before any device work)"""
+    rc, h, _ = _compile(lib, synth.C2_QUERY)
+    assert rc == abi.SH_OK
+    run = abi.sh_device_run()
+    run.n = 1
+    C.memmove(C.addressof(run) + 88, C.byref(C.c_int64(2)), 8)  # version = 2, pad = 0 at offset 88
+    assert lib.sh_run_device(h, C.byref(run)) == abi.SH_E_INVALID_ARG
+    assert b"0.1" in lib.sh_last_error(h)
+    lib.sh_destroy(h)
+    assert b"layout 2" in lib.sh_version()
