@@ -216,14 +216,28 @@ struct shk_plan {
     int64_t chunk;                // events per chunk (a multiple of the sub-tile)
     int64_t within;               // W (ms), 0..65535
     int32_t n_terms;              // opening filter: conjunction of terms on the event itself
-    int32_t pad;
+    int32_t spill_cap;            // spilled entries per (workgroup, key) at most (else SHK_F_SPILL)
+    int32_t pre[2];               // [0]: the term whose 4-byte left column the loader prefetches (-1: none)
+    // order keys: stack entries hold key(x) ^ kflip (key: IEEE bits -> unsigned order,
+    // or int ^ sign bit), so every operator becomes `consume if cx > cy (or ==, ge)`
+    // on unsigned keys; zk1 -> zk0 merges -0.0 into +0.0 before a compare
+    uint32_t kflip, zk0, zk1;
+    int32_t ge;
+    // opening filter, fast form (fast_open = 1): every term compares a 4-byte column
+    // (0: the ordering column, 1: the prefetched one) with a constant through order
+    // keys: result = lt & (v < c) | eq & (v == c) | gt & (v > c), nan_res for NaN
+    int32_t fast_open;
+    int32_t f_col[SHK_MAX_TERMS], f_f32[SHK_MAX_TERMS], f_nan[SHK_MAX_TERMS], f_lt[SHK_MAX_TERMS], f_eq[SHK_MAX_TERMS],
+        f_gt[SHK_MAX_TERMS];
+    uint32_t f_ckey[SHK_MAX_TERMS];
+    const uint64_t* omask;        // fast_open = 0: the opening filter, one bit per event (shk_open_bits)
     shp_term terms[SHK_MAX_TERMS];
     const void* tl[SHK_MAX_TERMS];  // column of each term's left attribute
     const void* tr[SHK_MAX_TERMS];  // column of its right attribute (rkind 0 / 2)
     uint8_t* cnt;                 // [n] partials consumed per event (pass 1 -> pass 2)
     uint32_t* ttot;               // [nsub + 1] matches per sub-tile -> exclusive scan
     int64_t* hstart;              // [n_chunks] first event of each chunk's halo
-    uint64_t* spill;              // [grid][kpw][SK_SPILL] stack entries below the LDS ring
+    uint64_t* spill;              // [grid][kpw][spill_cap] stack entries below the LDS ring
     int32_t* flag;
     unsigned long long* prof;     // diagnostics (SH_STK_PROFILE): clock ticks per phase, NULL off
 };
@@ -286,6 +300,8 @@ int shk_emit(const shk_plan* P, const shb_out* O, const shb_cols* OC, uint64_t s
              int64_t* out_vals, int64_t out_cap, void* stream);
 // the keys one stack-engine workgroup holds at most (LDS)
 int shk_max_keys(void);
+// the opening filter's general form as one bit per event (into P->omask), before shk_count
+int shk_open_bits(const shk_plan* P, void* stream);
 // raw 8-byte rows [m x n_out] -> typed columns of widths w[o] (8, 4 or 1 bytes)
 int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, void* const* cols, const int32_t* w, void* stream);
 // raw rows + sequence numbers -> packed rows (SHB_OUT_PACKED; woff / rw as in shb_cols)

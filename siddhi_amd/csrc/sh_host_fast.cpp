@@ -643,18 +643,24 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
 int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     h->stk_last = 0;
     h->stk_refused = 0;
+    static const bool dbg = getenv("SH_STK_DEBUG") != nullptr;
+#define STK_NO(why)                                                          \
+    do {                                                                     \
+        if (dbg) fprintf(stderr, "[stack engine] not applicable: %s\n", why); \
+        return 1;                                                            \
+    } while (0)
     const char* dis = getenv("SH_DISABLE_STACK");  // (read per call: tests A/B the engines)
     if (dis && dis[0] && dis[0] != '0') return 1;
     const shp_program& P = h->prog;
     const int64_t n = run->n;
-    if (!h->partitioned || !P.out_fast || P.agg_post || n < 4096 || nkeys < 1) return 1;
+    if (!h->partitioned || !P.out_fast || P.agg_post || n < 4096 || nkeys < 1) STK_NO("shape / size");
     if (h->stk_state == 0) h->stk_state = shj_stack_form(&P, &h->stk) == 0 ? 1 : -1;
-    if (h->stk_state != 1) return 1;
-    if (P.within_ms < 0 || P.within_ms > 65535) return 1;
+    if (h->stk_state != 1) STK_NO("no stack form of f2");
+    if (P.within_ms < 0 || P.within_ms > 65535) STK_NO("window");
     const int kmax = shk_max_keys();
     int gshift = 1;  // at least two groups: 2,048-event sub-tiles, 64 events per owner wave
     while (gshift <= 3 && ((int64_t)nkeys + (1 << gshift) - 1) >> gshift > kmax) gshift++;
-    if (gshift > 3) return 1;
+    if (gshift > 3) STK_NO("too many keys");
     const shj_stack& S = h->stk;
     shb_out O;
     memset(&O, 0, sizeof(O));
@@ -670,7 +676,7 @@ int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys) {
         } else if (a == S.xattr) {
             O.kind[o] = SHB_OUT_KIND_Y;
         } else {
-            return 1;  // another e1-side value: the bucketed engine's match stream
+            STK_NO("an e1-side value other than the ordering attribute");
         }
     }
     hipStream_t st = h->stream;
@@ -687,10 +693,73 @@ int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     K.kpw = (int32_t)(((int64_t)nkeys + (1 << gshift) - 1) >> gshift);
     K.within = P.within_ms;
     K.n_terms = S.n_terms;
+    K.pre[0] = K.pre[1] = -1;
     for (int k = 0; k < S.n_terms; k++) {
         K.terms[k] = S.terms[k];
         K.tl[k] = run->d_cols[S.terms[k].lattr];
         K.tr[k] = S.terms[k].rkind == 1 ? nullptr : run->d_cols[S.terms[k].rattr];
+        // the loader prefetches one 4-byte left operand off the ordering column
+        const int lt = S.terms[k].ltype;
+        if (K.tl[k] != K.xcol && K.pre[0] < 0 && (lt == SH_T_INT || lt == SH_T_FLOAT || lt == SH_T_STRING))
+            K.pre[0] = k;
+    }
+    // order keys: `consume if cx > cy` (GT / LT after a flip), `or equal` for GE / LE
+    const bool f32 = S.dom == DOM_F32;
+    const bool flip = S.op == SH_OP_LT || S.op == SH_OP_LE;
+    K.kflip = flip ? 0xFFFFFFFFu : 0u;
+    K.ge = (S.op == SH_OP_GE || S.op == SH_OP_LE) ? 1 : 0;
+    // -0.0 and +0.0 have adjacent keys (0x7FFFFFFF, 0x80000000 before the flip):
+    // the compares merge the first into the second; ints need no merge
+    K.zk1 = f32 ? (0x7FFFFFFFu ^ K.kflip) : 0u;
+    K.zk0 = f32 ? (0x80000000u ^ K.kflip) : 0u;
+    // the opening filter's fast form: 4-byte column (ordering or prefetched) vs a
+    // constant in the column's own domain; anything else runs the generic terms
+    K.fast_open = 1;
+    for (int k = 0; k < S.n_terms; k++) {
+        const shp_term& T = S.terms[k];
+        const bool fl = T.ltype == SH_T_FLOAT && T.dom == DOM_F32;
+        const bool in = T.ltype == SH_T_INT && T.dom == DOM_I32;
+        const int col = K.tl[k] == K.xcol ? 0 : (k == K.pre[0] ? 1 : -1);
+        if (T.rkind != 1 || !(fl || in) || col < 0 || T.op < SH_OP_EQ || T.op > SH_OP_LE) {
+            K.fast_open = 0;
+            break;
+        }
+        uint32_t cb;  // the constant in the compare domain (binary numeric promotion)
+        if (fl) {
+            float cf;
+            switch (T.ctype) {
+                case SH_T_INT: cf = (float)(int32_t)T.c; break;
+                case SH_T_LONG: cf = (float)T.c; break;
+                case SH_T_FLOAT: memcpy(&cf, &T.c, 4); break;
+                case SH_T_DOUBLE: {
+                    double d;
+                    memcpy(&d, &T.c, 8);
+                    cf = (float)d;
+                    break;
+                }
+                default: K.fast_open = 0; cf = 0.f;
+            }
+            if (cf != cf) K.fast_open = 0;  // a NaN constant: the generic terms
+            memcpy(&cb, &cf, 4);
+            cb = (cb & 0x80000000u) ? ~cb : (cb | 0x80000000u);
+            if (cb == 0x7FFFFFFFu) cb = 0x80000000u;
+        } else {
+            if (T.ctype != SH_T_INT) K.fast_open = 0;
+            cb = (uint32_t)(int32_t)T.c ^ 0x80000000u;
+        }
+        if (!K.fast_open) break;
+        K.f_col[k] = col;
+        K.f_f32[k] = fl ? 1 : 0;
+        K.f_ckey[k] = cb;
+        K.f_lt[k] = T.op == SH_OP_LT || T.op == SH_OP_LE || T.op == SH_OP_NE;
+        K.f_eq[k] = T.op == SH_OP_EQ || T.op == SH_OP_GE || T.op == SH_OP_LE;
+        K.f_gt[k] = T.op == SH_OP_GT || T.op == SH_OP_GE || T.op == SH_OP_NE;
+        K.f_nan[k] = T.op == SH_OP_NE;  // NaN: every compare false but !=
+    }
+    static const bool prof = getenv("SH_STK_PROFILE") != nullptr;
+    if (prof) {
+        if (h->bk_prof.ensure_fresh(128)) return fail(h, SH_E_OOM, "profile");
+        K.prof = h->bk_prof.as<unsigned long long>();
     }
     const int64_t sub = (int64_t)1024 << gshift;  // events per sub-tile (EPL = G)
     K.nsub = (int32_t)((n + sub - 1) / sub);
@@ -701,10 +770,13 @@ int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     hipMemcpyAsync(h->bk_rd.as<void>(8), run->d_ts + (n - 1), 8, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "stack engine: timestamp read");
     const int64_t span = *h->bk_rd.as<int64_t>(8) - *h->bk_rd.as<int64_t>(0);
-    if (span < 0) return 1;  // timestamps go back
+    if (span < 0) STK_NO("timestamps go back");
     const double rate = (double)n / (double)(span + 1);  // events per ms
     const int64_t min_chunk = (int64_t)(4.0 * rate * (double)(P.within_ms + 1)) + sub;
     int n_chunks = 256 >> gshift;
+    // spilled entries per key: a few windows' worth of a key's events at the mean
+    // rate (a deeper run raises SHK_F_SPILL and the host retries with more)
+    int spill_cap = (int)std::min<double>(511.0, std::max(32.0, 2.0 * rate * (double)(P.within_ms + 1) / nkeys));
     for (;;) {
         int64_t chunk = (n + n_chunks - 1) / n_chunks;
         if (chunk < min_chunk) chunk = min_chunk;
@@ -715,7 +787,7 @@ int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys) {
         const int64_t grid = (int64_t)8 * K.cpx << gshift;
         if (h->k_cnt.ensure_fresh((size_t)n) || h->k_ttot.ensure_fresh(((size_t)K.nsub + 1) * 4) ||
             h->k_hstart.ensure_fresh((size_t)K.n_chunks * 8) || h->k_flag.ensure_fresh(64) ||
-            h->k_spill.ensure_fresh((size_t)grid * K.kpw * 32 * 8) ||
+            h->k_spill.ensure_fresh((size_t)grid * K.kpw * spill_cap * 8) ||
             h->k_scan.ensure_fresh(shd_scan_tmp_words((int64_t)K.nsub + 1) * 4 + 64))
             return fail(h, SH_E_OOM, "stack engine workspace");
         K.cnt = h->k_cnt.as<uint8_t>();
@@ -723,13 +795,21 @@ int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys) {
         K.hstart = h->k_hstart.as<int64_t>();
         K.spill = h->k_spill.as<uint64_t>();
         K.flag = h->k_flag.as<int32_t>();
+        K.spill_cap = spill_cap;
         shb_cols OC;
         int32_t wd[SHB_MAX_OUT];
         for (int o = 0; o < O.n_out; o++) wd[o] = type_width(O.type[o]);
         direct_layout(h, run, wd, O.n_out, &OC);
+        if (K.prof) hipMemsetAsync(K.prof, 0, 128, st);
         hipEventRecord(h->ev[0], st);
         hipMemsetAsync(K.flag, 0, 4, st);
         hipMemsetAsync(K.ttot, 0, ((size_t)K.nsub + 1) * 4, st);
+        K.omask = nullptr;
+        if (!K.fast_open && K.n_terms > 0) {
+            if (h->k_omask.ensure_fresh(((size_t)n / 64 + 2) * 8)) return fail(h, SH_E_OOM, "stack engine workspace");
+            K.omask = h->k_omask.as<uint64_t>();
+            if (shk_open_bits(&K, st)) return fail(h, SH_E_HIP, "stack engine filter launch failed");
+        }
         if (shk_count(&K, st)) return fail(h, SH_E_HIP, "stack engine count launch failed");
         hipEventRecord(h->ev[1], st);
         if (shd_exclusive_scan(K.ttot, K.ttot, (int64_t)K.nsub + 1, h->k_scan.as<uint32_t>(), st))
@@ -742,13 +822,26 @@ int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys) {
         hipMemcpyAsync(h->bk_rd.as<void>(8), K.ttot + K.nsub, 4, hipMemcpyDeviceToHost, st);
         if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the stack engine");
         const int32_t flag = *h->bk_rd.as<int32_t>(0);
+        if (K.prof) {
+            unsigned long long pr[16];
+            hipMemcpy(pr, K.prof, 128, hipMemcpyDeviceToHost);
+            fprintf(stderr, "[stack engine clock ticks, both passes, summed over waves] producer %llu queue %llu "
+                            "process %llu; batches %llu rounds %llu queued events %llu; grid %d, chunk %lld, groups %d\n",
+                    pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], (int)(8 * K.cpx << K.gshift), (long long)K.chunk,
+                    1 << K.gshift);
+        }
         if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
         if (flag == SHB_F_HALO && n_chunks > 1) {
             n_chunks = std::max(1, n_chunks / 4);  // bursty timestamps: longer chunks
             continue;
         }
+        if (flag == SHK_F_SPILL && spill_cap < 511) {
+            spill_cap = std::min(511, spill_cap * 4);  // deeper stacks than the mean rate suggests
+            continue;
+        }
         if (flag) {
             h->stk_refused = flag;
+            if (dbg) fprintf(stderr, "[stack engine] refused on the device: flags 0x%x\n", flag);
             return 1;
         }
         const int64_t total = *h->bk_rd.as<uint32_t>(8);
@@ -764,6 +857,7 @@ int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys) {
         return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "stack engine");
     }
 }
+#undef STK_NO
 
 // the rise-and-fall sequence on the bucket-carry engine (sh_bucket.hip k_s3b):
 // the tile-local bucket partition, one workgroup per bucket carrying its keys'

@@ -340,7 +340,7 @@ struct sh_handle {
     int stk_last = 0;             // 1: the last sh_run_device ran on the stack engine
     int stk_refused = 0;          // the device flags of the last refused run (diagnostics)
     shj_stack stk{};
-    DevBuf k_cnt, k_ttot, k_hstart, k_spill, k_flag, k_scan;
+    DevBuf k_cnt, k_ttot, k_hstart, k_spill, k_flag, k_scan, k_omask;
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
     DevBuf w_colrows;
     bool cols_rows = false;

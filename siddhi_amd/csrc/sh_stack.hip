@@ -52,19 +52,18 @@
 #define SK_D 8               // ring entries per key in LDS
 #define SK_KPW 2500          // keys per workgroup at most
 #define SK_CAPW 160          // queue entries per owner wave and sub-tile (64 expected)
-#define SK_SPILL 32          // spilled entries per (workgroup, key) at most
 #define SK_OFF_BITS 13       // q2: event offset in the sub-tile | row offset << 13
 #define SK_ROWS_LIM (1u << (32 - SK_OFF_BITS))
 
 static_assert(SK_NW == 16, "16 owner waves");
 
 struct SkLds {
-    uint32_t y[SK_D][SK_KPW];         // ring entries: ordering value (raw 32 bits)
+    uint32_t y[SK_D][SK_KPW];         // ring entries: order key of the ordering value
     uint16_t t[SK_D][SK_KPW];         // ... timestamp - tb
-    uint16_t h[SK_KPW];               // bottom (3 bits) | count << 3 (4) | spilled << 7 (6)
+    uint16_t h[SK_KPW];               // bottom (3 bits) | count << 3 (4) | spilled << 7 (9)
     uint16_t spt[SK_KPW];             // timestamp of the newest spilled entry
-    uint32_t qx[SK_NW * SK_CAPW];     // queue: ordering value
-    uint32_t q1[SK_NW * SK_CAPW];     // ts - tb | wave-local key << 16 | open << 31
+    uint32_t qx[SK_NW * SK_CAPW];     // queue: order key of the ordering value
+    uint32_t q1[SK_NW * SK_CAPW];     // ts - tb | wave-local key << 16 | NaN << 30 | open << 31
     uint32_t q2[SK_NW * SK_CAPW];     // offset in the sub-tile | row offset << 13 (pass 2)
     uint32_t wcnt[SK_NW][SK_NW];      // [producer wave][owner wave]: queued events
     uint32_t wrow[SK_NW];             // pass 2: rows of each producer wave's events
@@ -73,13 +72,37 @@ struct SkLds {
 };
 static_assert(sizeof(SkLds) <= 163840, "LDS");
 
-__device__ __forceinline__ bool sk_cmp(int op, int dom, uint32_t x, uint32_t y) {
-    if (dom == DOM_F32) return cmp_op<float>(op, __uint_as_float(x), __uint_as_float(y));
-    return cmp_op<int32_t>(op, (int32_t)x, (int32_t)y);
+// order keys: a float's IEEE bits (or an int) as an unsigned integer of the same
+// order -- positive floats get the sign bit set, negative ones are inverted -- so
+// every comparison of the ordering term is one unsigned compare, branch-free
+__device__ __forceinline__ uint32_t sk_key(uint32_t bits, bool f32) {
+    return f32 ? ((bits & 0x80000000u) ? ~bits : (bits | 0x80000000u)) : (bits ^ 0x80000000u);
+}
+__device__ __forceinline__ uint32_t sk_unkey(uint32_t k, bool f32) {
+    return f32 ? ((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k) : (k ^ 0x80000000u);
 }
 
-// the opening filter (f1 and the e1-only terms of f2) on event e, as terms_pass
-__device__ __forceinline__ bool sk_open(const shk_plan& P, int64_t e) {
+// the opening filter's fast form: each term compares a 4-byte column (the ordering
+// one or the prefetched one) with a constant through order keys
+__device__ __forceinline__ bool sk_open_fast(const shk_plan& P, uint32_t x, uint32_t l0) {
+    bool ok = true;
+    for (int k = 0; k < P.n_terms; k++) {
+        const uint32_t v = P.f_col[k] ? l0 : x;
+        const bool f = P.f_f32[k] != 0;
+        const bool nan = f && (v & 0x7FFFFFFFu) > 0x7F800000u;
+        uint32_t kv = sk_key(v, f);
+        kv = (f && kv == 0x7FFFFFFFu) ? 0x80000000u : kv;  // -0.0 compares as +0.0
+        const uint32_t kc = P.f_ckey[k];
+        const bool r = (P.f_lt[k] && kv < kc) || (P.f_eq[k] && kv == kc) || (P.f_gt[k] && kv > kc);
+        ok = ok && (nan ? P.f_nan[k] != 0 : r);
+    }
+    return ok;
+}
+
+// the opening filter (f1 and the e1-only terms of f2) on event e, as terms_pass:
+// the general form, evaluated by k_stk_open into a bit per event when the terms
+// have no fast form (keeps the VM's code out of the matcher)
+__device__ __forceinline__ bool sk_open_gen(const shk_plan& P, int64_t e) {
     for (int k = 0; k < P.n_terms; k++) {
         const shp_term T = P.terms[k];
         VmVal l, r;
@@ -106,6 +129,24 @@ __device__ __forceinline__ bool sk_open(const shk_plan& P, int64_t e) {
         if (!vm_cmp(T.op, T.dom, l, r)) return false;
     }
     return true;
+}
+
+// one bit per event: the opening filter's general form (64 events per word)
+__global__ void __launch_bounds__(256) k_stk_open(shk_plan P) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool ok = e < P.n && sk_open_gen(P, e);
+    const uint64_t m = __ballot(ok);
+    if ((threadIdx.x & 63) == 0 && e < P.n) const_cast<uint64_t*>(P.omask)[e >> 6] = m;
+}
+
+// a key's spilled entries are written by one lane and read back by another lane of
+// the same wave in a later round: both sides go to L2 (agent-scope relaxed atomics
+// bypass the CU's L1, whose copy of a reused slot would otherwise be stale)
+__device__ __forceinline__ uint64_t sk_spill_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sk_spill_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // value of a select entry of a row: the consumed partial's ordering value (y) or
@@ -183,27 +224,41 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
     const int64_t tb = P.ts[hb];
     for (int i = threadIdx.x; i < P.kpw; i += SK_TPB) L.h[i] = 0;
     const uint32_t W = (uint32_t)P.within;
+    const bool f32 = P.dom == DOM_F32;
 
-    // the producer's events of sub-tile s0: row i holds s0 + w * 64 * EPL + 64 i + lane
+    // the producer's events of sub-tile s0: row i holds s0 + w * 64 * EPL + 64 i + lane,
+    // loaded one sub-tile ahead (with the predecessor of row 0, the prefetched
+    // filter operands and, pass 2, the sub-tile's first row)
     int32_t kk[EPL];
     uint32_t xx[EPL];
     int64_t tt[EPL];
     uint32_t cc[EPL];
+    uint32_t la[EPL];
+    uint64_t om[EPL];
+    int64_t tpr = INT64_MIN;
+    uint32_t rows_next = 0;
     auto load = [&](int64_t s0) {
+        const int64_t e0 = s0 + (int64_t)w * (64 * EPL) + lane;
+        tpr = (e0 > hb && e0 - 1 < ce) ? P.ts[e0 - 1] : INT64_MIN;
+        if (PASS == 2 && s0 >= cb) rows_next = P.ttot[s0 / SUB];
 #pragma unroll
         for (int i = 0; i < EPL; i++) {
-            const int64_t e = s0 + (int64_t)w * (64 * EPL) + 64 * i + lane;
+            const int64_t e = e0 + 64 * i;
             const bool v = e < ce;
             kk[i] = v ? P.keys[e] : -1;
             xx[i] = v ? ((const uint32_t*)P.xcol)[e] : 0u;
             tt[i] = v ? P.ts[e] : tb;
             cc[i] = (PASS == 2 && v && s0 >= cb) ? (uint32_t)P.cnt[e] : 0u;
+            la[i] = (P.pre[0] >= 0 && v) ? ((const uint32_t*)P.tl[P.pre[0]])[e] : 0u;
+            om[i] = (P.omask && v) ? P.omask[e >> 6] : 0ull;  // (rows are 64-aligned)
         }
     };
     load(hb);
+    unsigned long long pc_prod = 0, pc_queue = 0, pc_proc = 0, pc0 = 0, n_batch = 0, n_round = 0, n_ev = 0;
     int64_t prev_sub = -1;  // pass 1: the last sub-tile whose totals wait in wsum
     for (int64_t s0 = hb; s0 < ce; s0 += SUB) {
         const bool emit = s0 >= cb;
+        if (P.prof) pc0 = clock64();
         // ---- producer: own events, their owner wave and rank
         if (lane < SK_NW) L.wcnt[w][lane] = 0u;
         uint32_t rk[EPL], qa[EPL], qb[EPL], qc[EPL];
@@ -220,17 +275,25 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
             const bool own = v && k >= 0 && k < P.nkeys && (k & (G - 1)) == g;
             const int64_t dt = tt[i] - tb;
             if (v && (dt < 0 || dt > 65535)) flag |= SHB_F_TS;
-            if (v && e > hb && P.ts[e - 1] > tt[i]) flag |= SHB_F_MONO;
+            {
+                // timestamps never go back: the previous event is lane - 1, the last of
+                // the previous row, or (row 0, lane 0) the previous wave's last event
+                const int64_t up = __shfl(tt[i], lane > 0 ? lane - 1 : 0);
+                const int64_t pv = lane > 0 ? up : (i > 0 ? __shfl(tt[i > 0 ? i - 1 : 0], 63) : tpr);
+                if (v && pv > tt[i]) flag |= SHB_F_MONO;
+            }
             const uint32_t lk = own ? (uint32_t)k >> P.gshift : 0u;
             const int b = (int)(lk & 15u);
             bn[i] = own ? b : -1;
+            // a NaN consumer takes nothing and never opens a partial
+            const bool xnan = f32 && (xx[i] & 0x7FFFFFFFu) > 0x7F800000u;
             bool open = false;
-            if (own) {
-                open = P.dom == DOM_F32 ? (__uint_as_float(xx[i]) == __uint_as_float(xx[i])) : true;
-                if (open && P.n_terms) open = sk_open(P, e);
+            if (own && !xnan) {
+                if (P.fast_open) open = sk_open_fast(P, xx[i], la[i]);
+                else open = (om[i] >> lane) & 1ull;
             }
-            qa[i] = xx[i];
-            qb[i] = (uint32_t)dt | ((lk >> 4) << 16) | (open ? 0x80000000u : 0u);
+            qa[i] = sk_key(xx[i], f32) ^ P.kflip;
+            qb[i] = (uint32_t)dt | ((lk >> 4) << 16) | (xnan ? 0x40000000u : 0u) | (open ? 0x80000000u : 0u);
             qc[i] = (uint32_t)(e - s0);
             if (PASS == 1 && emit && v && !(k >= 0 && k < P.nkeys) && g == 0) P.cnt[e] = 0;
             // rank among this wave's earlier events of the same owner wave
@@ -256,6 +319,11 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
         }
         if (flag) atomicOr(P.flag, (int)flag);
         if (PASS == 2 && lane == 0) L.wrow[w] = rcarry;
+        if (P.prof) {
+            const unsigned long long t = clock64();
+            pc_prod += t - pc0;
+            pc0 = t;
+        }
         __syncthreads();  // A: queue counts and row totals of the sub-tile are in
         if (PASS == 1 && threadIdx.x == 0 && prev_sub >= 0) {
             uint32_t s = 0;
@@ -298,12 +366,17 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
         uint32_t nq = lane < SK_NW ? L.wcnt[lane][w] : 0u;
         nq = shw_last(shw_incl_scan(nq));
         if (nq > SK_CAPW) nq = SK_CAPW;
-        const int64_t sub = s0 / SUB;
-        const uint64_t rows0 = (PASS == 2 && emit) ? (uint64_t)P.ttot[sub] : 0ull;
+        const uint64_t rows0 = (PASS == 2 && emit) ? (uint64_t)rows_next : 0ull;
         __syncthreads();  // B: queues complete
+        if (P.prof) {
+            const unsigned long long t = clock64();
+            pc_queue += t - pc0;
+            pc0 = t;
+        }
         if (s0 + SUB < ce) load(s0 + SUB);  // next sub-tile in flight during the queue
         // ---- owner: the wave's queue in batches of 64, the k-th event of a key in round k
         uint32_t msum = 0;
+        n_ev += nq;
         for (uint32_t base = 0; base < nq; base += 64) {
             const uint32_t idx = base + (uint32_t)lane;
             const bool act = idx < nq;
@@ -328,12 +401,14 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
                 for (int o = 0; o < (NO > 0 ? NO : 1); o++) {
                     v1[o] = 0;
                     if (O.kind[o] != 1 || !act || !emit) continue;
-                    if (O.src[o] == P.xcol) v1[o] = sk_yraw(x, O.type[o]);
+                    if (O.src[o] == P.xcol) v1[o] = sk_yraw(sk_unkey(x ^ P.kflip, f32), O.type[o]);
                     else if (O.src[o] == (const void*)P.keys) v1[o] = (int64_t)key;
                     else v1[o] = bk_raw(O.src[o], j, O.type[o]);
                 }
             }
+            n_batch++;
             for (uint32_t rd = 0; __ballot(act && rank >= rd) != 0ull; rd++) {
+                n_round++;
                 if (!(act && rank == rd)) continue;
                 // the key's ring: all entries at once (one LDS latency)
                 const uint32_t hw = L.h[lk];
@@ -360,28 +435,35 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
                     live &= ~E;
                     sc = 0;  // spilled entries are older than an expired one
                 }
-                // the entries x beats: the top of the stack
+                // the entries x beats: the top of the stack (order keys; -0.0 as +0.0)
+                const uint32_t cx = x == P.zk1 ? P.zk0 : x;
+                if (a1 & 0x40000000u) live = 0;  // a NaN consumer
                 uint32_t K = 0;
 #pragma unroll
-                for (int s = 0; s < SK_D; s++)
-                    K |= (((live >> s) & 1u) && sk_cmp(P.op, P.dom, x, y[s])) ? (1u << s) : 0u;
+                for (int s = 0; s < SK_D; s++) {
+                    const uint32_t cy = y[s] == P.zk1 ? P.zk0 : y[s];
+                    K |= (((live >> s) & 1u) && (cx > cy || (P.ge && cx == cy))) ? (1u << s) : 0u;
+                }
                 const uint32_t k = (uint32_t)__popc(K);
                 n -= k;
                 // below an emptied ring: the spilled entries (HBM)
-                uint64_t* spl = P.spill + ((uint64_t)blockIdx.x * (uint64_t)P.kpw + lk) * SK_SPILL;
-                const uint32_t sc0 = sc;
-                if (n == 0 && sc > 0) {
+                uint64_t* spl = P.spill + ((uint64_t)blockIdx.x * (uint64_t)P.kpw + lk) * (uint64_t)P.spill_cap;
+                uint32_t ks = 0;  // spilled entries popped (rows); `sc` may also drop to 0 by expiry
+                uint32_t slo = sc;  // the popped spilled entries are slots [slo, slo + ks)
+                if (n == 0 && sc > 0 && !(a1 & 0x40000000u)) {
                     while (sc > 0) {
-                        const uint64_t ev = spl[sc - 1];
+                        const uint64_t ev = sk_spill_load(spl + sc - 1);
                         if (((now - (uint32_t)(ev >> 32)) & 0xFFFFu) > W) {
-                            sc = 0;
+                            sc = 0;  // this one and every older spilled entry expired
                             break;
                         }
-                        if (!sk_cmp(P.op, P.dom, x, (uint32_t)ev)) break;
+                        const uint32_t cy = (uint32_t)ev == P.zk1 ? P.zk0 : (uint32_t)ev;
+                        if (!(cx > cy || (P.ge && cx == cy))) break;
                         sc--;
+                        ks++;
+                        slo = sc;
                     }
                 }
-                const uint32_t ks = sc0 > sc ? sc0 - sc : 0u;
                 const uint32_t total = ks + k;
                 if (PASS == 1) {
                     if (emit) {
@@ -400,7 +482,8 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
                             int64_t v[NO > 0 ? NO : 1];
 #pragma unroll
                             for (int o = 0; o < (NO > 0 ? NO : 1); o++)
-                                v[o] = O.kind[o] == SHB_OUT_KIND_Y ? sk_yraw(yv, O.type[o]) : v1[o];
+                                v[o] = O.kind[o] == SHB_OUT_KIND_Y ? sk_yraw(sk_unkey(yv ^ P.kflip, f32), O.type[o])
+                                                                   : v1[o];
                             bk_store<MODE, NO>(OC, row, v, seq, out_seq, out_vals);
                         } else {
                             const int no = O.n_out;
@@ -414,8 +497,8 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
                             }
                             for (int o = 0; o < no; o++) {
                                 int64_t vv;
-                                if (O.kind[o] == SHB_OUT_KIND_Y) vv = sk_yraw(yv, O.type[o]);
-                                else if (O.src[o] == P.xcol) vv = sk_yraw(x, O.type[o]);
+                                if (O.kind[o] == SHB_OUT_KIND_Y) vv = sk_yraw(sk_unkey(yv ^ P.kflip, f32), O.type[o]);
+                                else if (O.src[o] == P.xcol) vv = sk_yraw(sk_unkey(x ^ P.kflip, f32), O.type[o]);
                                 else if (O.src[o] == (const void*)P.keys) vv = (int64_t)key;
                                 else vv = bk_raw(O.src[o], j, O.type[o]);
                                 if (MODE == SHB_OUT_PACKED) {
@@ -430,7 +513,7 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
                             }
                         }
                     };
-                    for (uint32_t q = 0; q < ks; q++) put(r0 + q, (uint32_t)spl[sc + q]);
+                    for (uint32_t q = 0; q < ks; q++) put(r0 + q, (uint32_t)sk_spill_load(spl + slo + q));
                     uint32_t Km = K;
                     while (Km) {
                         const uint32_t s = (uint32_t)__ffs(Km) - 1u;
@@ -447,7 +530,7 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
                 if (a1 >> 31) {
                     if (n == SK_D) {
                         if (sc > 0 && ((now - (uint32_t)L.spt[lk]) & 0xFFFFu) > W) sc = 0;
-                        if (sc >= SK_SPILL) {
+                        if (sc >= (uint32_t)P.spill_cap) {
                             atomicOr(P.flag, SHK_F_SPILL);
                         } else {
                             uint32_t yb = y[0], tbb = tv[0];
@@ -456,7 +539,7 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
                                 yb = b == (uint32_t)u ? y[u] : yb;
                                 tbb = b == (uint32_t)u ? tv[u] : tbb;
                             }
-                            spl[sc] = (uint64_t)yb | ((uint64_t)tbb << 32);
+                            sk_spill_store(spl + sc, (uint64_t)yb | ((uint64_t)tbb << 32));
                             sc++;
                             L.spt[lk] = (uint16_t)tbb;
                         }
@@ -475,6 +558,17 @@ __global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_co
             msum = shw_last(shw_incl_scan(msum));
             if (lane == 0) L.wsum[w] = emit ? msum : 0u;
         }
+        if (P.prof) pc_proc += clock64() - pc0;
+    }
+    if (P.prof && lane == 0) {
+        // clock ticks per phase summed over the waves: producer, queue hand-off
+        // (both barriers' waits included), owner processing
+        atomicAdd(P.prof + 0, pc_prod);
+        atomicAdd(P.prof + 1, pc_queue);
+        atomicAdd(P.prof + 2, pc_proc);
+        atomicAdd(P.prof + 3, n_batch);
+        atomicAdd(P.prof + 4, n_round);
+        atomicAdd(P.prof + 5, n_ev);
     }
     if (PASS == 1) {
         __syncthreads();
@@ -492,6 +586,12 @@ static int sk_ok() { return hipGetLastError() == hipSuccess ? 0 : -3; }
 static unsigned sk_grid(const shk_plan* P) { return 8u * (unsigned)P->cpx << P->gshift; }
 
 extern "C" int shk_max_keys(void) { return SK_KPW; }
+
+extern "C" int shk_open_bits(const shk_plan* P, void* stream) {
+    if (!P->omask) return -1;
+    hipLaunchKernelGGL(k_stk_open, dim3((unsigned)((P->n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *P);
+    return sk_ok();
+}
 
 extern "C" int shk_count(const shk_plan* P, void* stream) {
     hipStream_t st = (hipStream_t)stream;

@@ -53,7 +53,7 @@ def _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events):
         m, rows = runner.run(torch.from_numpy(ts).to(dev), torch.from_numpy(keys).to(dev), tcols, nk,
                              packed=True, batch_events=batch_events)
         torch.cuda.synchronize()
-        status, err = runner.bucket_status(), runner.last_error()
+        status, err = runner.bucket_status(), runner.last_error() + f" (stack refused: {runner.stack_refused()})"
         oseq, ovals = packed_to_raw(rows.cpu().numpy(), runner.out_types, offs, rb)
         runner.close()
         return (m, oseq.astype(np.int64), ovals), status, err
@@ -61,7 +61,7 @@ def _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events):
                                 columns=columns, batch_events=batch_events)
     torch.cuda.synchronize()
     status = runner.bucket_status()
-    err = runner.last_error()
+    err = runner.last_error() + f" (stack refused: {runner.stack_refused()})"
     if columns:
         assert [c.dtype for c in ovals] == [{0: torch.int32, 1: torch.int32, 2: torch.int64, 3: torch.float32,
                                              4: torch.float64, 5: torch.uint8}[t] for t in runner.out_types]
