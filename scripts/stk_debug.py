@@ -1,9 +1,10 @@
-"""One C2-shaped run on the GPU with the stack engine's diagnostics (SH_STK_DEBUG)."""
+"""One C2-shaped run on the GPU on the stack matcher (SH_STACK=1) with its diagnostics (SH_STK_DEBUG)."""
 import os
 import sys
 import time
 
 os.environ.setdefault("SH_STK_DEBUG", "1")
+os.environ.setdefault("SH_STACK", "1")
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, ROOT)

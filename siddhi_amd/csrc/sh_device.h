@@ -189,59 +189,32 @@ struct shb_cols {
     void* rows;                   // packed: the rows
 };
 
-// ---- arrival-order stack engine (sh_stack.hip) for partitioned
+// ---- stack matcher (sh_stack.hip k_bk_stk) of the bucketed engine for partitioned
 // `every e1=S[f1] -> e2=S[x.a op e1.a] within W`: every pending partial of a key
 // is consumed by the first later event of the key with x_q op y_i, so a key's
 // pending partials form a monotone stack (consumers pop its top, expiry drops its
-// bottom). Workgroup (chunk, key group) streams the chunk's events in arrival
-// order and keeps the stacks of its keys in LDS; pass 1 counts, pass 2 writes the
-// ordered rows at the positions the scan of pass 1's counts gives.
+// bottom). One wave per (bucket, run of tiles) replaces shb_match between
+// shb_partition and shb_finish; the staged column 0 is the ordering attribute.
 #define SHK_MAX_TERMS 4
 #define SHK_F_SPILL 128   // a key's spill stack overflowed
-#define SHK_F_QUEUE 256   // a sub-tile sent more events to one wave than its queue holds
-#define SHK_F_ROWS 512    // a sub-tile's rows exceed the 19-bit row offset
-struct shk_plan {
-    int64_t n;
-    const int64_t* ts;            // arrival order, non-decreasing (else SHB_F_MONO)
-    const int32_t* keys;          // partition key ids
-    const void* xcol;             // the ordering attribute a (4-byte column)
+struct shk_params {
     int32_t dom;                  // compare domain: DOM_F32 or DOM_I32
-    int32_t op;                   // consumed when cmp_op(op, x_consumer, y_partial)
-    int32_t nkeys;
-    int32_t gshift;               // 1 << gshift key groups: key & (G - 1), local key = key >> gshift
-    int32_t kpw;                  // keys per workgroup (<= SK_KPW)
-    int32_t n_chunks;             // arrival chunks; grid = 8 * cpx << gshift
-    int32_t cpx;                  // chunks per XCD
-    int32_t nsub;                 // sub-tiles of the stream (row scan granularity)
-    int64_t chunk;                // events per chunk (a multiple of the sub-tile)
-    int64_t within;               // W (ms), 0..65535
-    int32_t n_terms;              // opening filter: conjunction of terms on the event itself
-    int32_t spill_cap;            // spilled entries per (workgroup, key) at most (else SHK_F_SPILL)
-    int32_t pre[2];               // [0]: the term whose 4-byte left column the loader prefetches (-1: none)
+    int32_t run_tiles;            // arrival tiles per run (<= shk_max_run_tiles())
+    int32_t want_ms;              // 1: match-stream column 0 takes e1's ordering value
+    int32_t spill_cap;            // spilled entries per (wave, key) at most (else SHK_F_SPILL)
     // order keys: stack entries hold key(x) ^ kflip (key: IEEE bits -> unsigned order,
     // or int ^ sign bit), so every operator becomes `consume if cx > cy (or ==, ge)`
     // on unsigned keys; zk1 -> zk0 merges -0.0 into +0.0 before a compare
     uint32_t kflip, zk0, zk1;
     int32_t ge;
-    // opening filter, fast form (fast_open = 1): every term compares a 4-byte column
-    // (0: the ordering column, 1: the prefetched one) with a constant through order
-    // keys: result = lt & (v < c) | eq & (v == c) | gt & (v > c), nan_res for NaN
-    int32_t fast_open;
-    int32_t f_col[SHK_MAX_TERMS], f_f32[SHK_MAX_TERMS], f_nan[SHK_MAX_TERMS], f_lt[SHK_MAX_TERMS], f_eq[SHK_MAX_TERMS],
+    // opening filter: every term compares the ordering column with a constant through
+    // order keys: result = lt & (v < c) | eq & (v == c) | gt & (v > c), f_nan for NaN
+    int32_t n_terms;
+    int32_t f_f32[SHK_MAX_TERMS], f_nan[SHK_MAX_TERMS], f_lt[SHK_MAX_TERMS], f_eq[SHK_MAX_TERMS],
         f_gt[SHK_MAX_TERMS];
     uint32_t f_ckey[SHK_MAX_TERMS];
-    const uint64_t* omask;        // fast_open = 0: the opening filter, one bit per event (shk_open_bits)
-    shp_term terms[SHK_MAX_TERMS];
-    const void* tl[SHK_MAX_TERMS];  // column of each term's left attribute
-    const void* tr[SHK_MAX_TERMS];  // column of its right attribute (rkind 0 / 2)
-    uint8_t* cnt;                 // [n] partials consumed per event (pass 1 -> pass 2)
-    uint32_t* ttot;               // [nsub + 1] matches per sub-tile -> exclusive scan
-    int64_t* hstart;              // [n_chunks] first event of each chunk's halo
-    uint64_t* spill;              // [grid][kpw][spill_cap] stack entries below the LDS ring
-    int32_t* flag;
-    unsigned long long* prof;     // diagnostics (SH_STK_PROFILE): clock ticks per phase, NULL off
+    uint64_t* spill;              // [grid * 4 waves][64 keys][spill_cap] entries below the LDS rings
 };
-#define SHB_OUT_KIND_Y 2          // shb_out kind: the consumed partial's ordering value (stack engine)
 
 #ifdef __cplusplus
 extern "C" {
@@ -293,15 +266,11 @@ int shb_s3_carry(const shb_plan* P, const shb_s3* S, void* stream);
 int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream);
 int shb_emit(const shb_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base, uint64_t* out_seq,
              int64_t* out_vals, int64_t out_cap, void* stream);
-// stack engine (sh_stack.hip): pass 1 counts (cnt, ttot, hstart), pass 2 (after
-// shd_exclusive_scan of ttot) writes the ordered rows
-int shk_count(const shk_plan* P, void* stream);
-int shk_emit(const shk_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base, uint64_t* out_seq,
-             int64_t* out_vals, int64_t out_cap, void* stream);
-// the keys one stack-engine workgroup holds at most (LDS)
-int shk_max_keys(void);
-// the opening filter's general form as one bit per event (into P->omask), before shk_count
-int shk_open_bits(const shk_plan* P, void* stream);
+// stack matcher (sh_stack.hip): after shb_partition (ordering attribute staged as
+// column 0), before shb_finish; -1: a plan it does not take
+int shk_match(const shb_plan* P, const shk_params* K, void* stream);
+int shk_max_run_tiles(void);
+int shk_spill_keys(void);   // keys per workgroup (spill rows per workgroup)
 // raw 8-byte rows [m x n_out] -> typed columns of widths w[o] (8, 4 or 1 bytes)
 int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, void* const* cols, const int32_t* w, void* stream);
 // raw rows + sequence numbers -> packed rows (SHB_OUT_PACKED; woff / rw as in shb_cols)

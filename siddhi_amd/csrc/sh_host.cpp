@@ -1468,11 +1468,6 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
         if (arc == 1) sequential = true;
         return arc;
     };
-    h->stk_last = 0;
-    if (h->prog.window_ok && !aggp) {
-        const int krc = run_stack(h, run, nkeys);
-        if (krc != 1) return krc;
-    }
     if (h->prog.window_ok) {
         int brc = run_bucket(h, run, nkeys);
         if (brc == SH_OK && aggp && !h->bk_agg_carried) {

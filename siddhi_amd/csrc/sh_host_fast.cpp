@@ -381,6 +381,62 @@ int run_rules(sh_handle* h, sh_device_run* run) {
 // consumer-side form and a null-free projection; 0 ok, 1 = not applicable or a
 // premise failed on the device (the caller runs the general window path),
 // SH_E_MORE = output capacity too small (out_count = matches), <0 error
+// the stack matcher's parameters (sh_stack.hip) for a query of stack form: the
+// ordering term `e2.a op e1.a` (a 4-byte float or int) and an opening filter of
+// terms comparing a with constants; false: the sort-and-walk matcher instead
+static bool stack_params(const shj_stack& S, int64_t within, shk_params* K) {
+    memset(K, 0, sizeof(*K));
+    if (S.op != SH_OP_GT && S.op != SH_OP_GE && S.op != SH_OP_LT && S.op != SH_OP_LE) return false;
+    if (within < 0 || within > 0x7FFFFFFF) return false;
+    const bool f32 = S.dom == DOM_F32;
+    K->dom = S.dom;
+    // order keys: `consume if cx > cy` (GT / LT after a flip), `or equal` for GE / LE;
+    // -0.0 and +0.0 have adjacent keys (0x7FFFFFFF, 0x80000000 before the flip): the
+    // compares merge the first into the second; ints need no merge
+    K->kflip = (S.op == SH_OP_LT || S.op == SH_OP_LE) ? 0xFFFFFFFFu : 0u;
+    K->ge = (S.op == SH_OP_GE || S.op == SH_OP_LE) ? 1 : 0;
+    K->zk1 = f32 ? (0x7FFFFFFFu ^ K->kflip) : 0u;
+    K->zk0 = f32 ? (0x80000000u ^ K->kflip) : 0u;
+    K->n_terms = S.n_terms;
+    for (int k = 0; k < S.n_terms; k++) {
+        const shp_term& T = S.terms[k];
+        const bool fl = T.ltype == SH_T_FLOAT && T.dom == DOM_F32;
+        const bool in = T.ltype == SH_T_INT && T.dom == DOM_I32;
+        if (T.rkind != 1 || T.lattr != S.xattr || T.lslot != 0 || !(fl || in) || T.op < SH_OP_EQ || T.op > SH_OP_LE)
+            return false;
+        uint32_t cb;  // the constant in the compare domain (binary numeric promotion)
+        if (fl) {
+            float cf;
+            switch (T.ctype) {
+                case SH_T_INT: cf = (float)(int32_t)T.c; break;
+                case SH_T_LONG: cf = (float)T.c; break;
+                case SH_T_FLOAT: memcpy(&cf, &T.c, 4); break;
+                case SH_T_DOUBLE: {
+                    double d;
+                    memcpy(&d, &T.c, 8);
+                    cf = (float)d;
+                    break;
+                }
+                default: return false;
+            }
+            if (cf != cf) return false;  // a NaN constant
+            memcpy(&cb, &cf, 4);
+            cb = (cb & 0x80000000u) ? ~cb : (cb | 0x80000000u);
+            if (cb == 0x7FFFFFFFu) cb = 0x80000000u;
+        } else {
+            if (T.ctype != SH_T_INT) return false;
+            cb = (uint32_t)(int32_t)T.c ^ 0x80000000u;
+        }
+        K->f_f32[k] = fl ? 1 : 0;
+        K->f_ckey[k] = cb;
+        K->f_lt[k] = T.op == SH_OP_LT || T.op == SH_OP_LE || T.op == SH_OP_NE;
+        K->f_eq[k] = T.op == SH_OP_EQ || T.op == SH_OP_GE || T.op == SH_OP_LE;
+        K->f_gt[k] = T.op == SH_OP_GT || T.op == SH_OP_GE || T.op == SH_OP_NE;
+        K->f_nan[k] = T.op == SH_OP_NE;  // NaN: every compare false but !=
+    }
+    return true;
+}
+
 int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry) {
     static const bool off = getenv("SH_DISABLE_BUCKET") != nullptr;
     h->bk_last = 0;
@@ -389,6 +445,19 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     if (off || !h->partitioned || nkeys < 1024 || !P.out_fast || n < SHB_TILE) return 1;
     const int kb = std::max(0, bits_for((uint64_t)(nkeys - 1)) - 8);
     if (kb > 8) return 1;
+    // the stack matcher (sh_stack.hip) for queries of stack form when SH_STACK=1
+    // (read per call: tests A/B the matchers; on C2 it is the slower of the two,
+    // DESIGN.md "stack matcher"), the sort-and-walk one (shb_match, hipRTC)
+    // otherwise or when the stack matcher refuses on the device
+    h->stk_last = 0;
+    const char* on = getenv("SH_STACK");
+    bool stk = (on && on[0] && on[0] != '0') && !h->stk_skip && kb <= 6 && !P.agg_post && !force_carry;
+    h->stk_skip = false;
+    shk_params K;
+    if (stk) {
+        if (h->stk_state == 0) h->stk_state = shj_stack_form(&P, &h->stk) == 0 ? 1 : -1;
+        stk = h->stk_state == 1 && stack_params(h->stk, P.within_ms, &K);
+    }
     // select list: e2-side values (and e1's partition attribute, equal to e2's
     // for these types) from the consumer row; other e1-side values ride the match stream
     shb_out O;
@@ -417,11 +486,16 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
         O.kind[o] = 0;
         O.src[o] = (const void*)(intptr_t)m;  // resolved below
     }
-    if (h->bk_state == 0) {
-        const int lrc = shj_bucket_load(&P, ms, n_ms, &h->bk, &h->bk_err);
-        h->bk_state = lrc == 0 ? 1 : (lrc == -1 ? -2 : -1);  // -2: no consumer-side form (not applicable)
+    // (the stack matcher's only e1-side value is the ordering attribute, through
+    // match-stream column 0)
+    if (stk && !(n_ms == 0 || (n_ms == 1 && ms[0] == h->stk.xattr))) stk = false;
+    if (!stk) {
+        if (h->bk_state == 0) {
+            const int lrc = shj_bucket_load(&P, ms, n_ms, &h->bk, &h->bk_err);
+            h->bk_state = lrc == 0 ? 1 : (lrc == -1 ? -2 : -1);  // -2: no consumer-side form (not applicable)
+        }
+        if (h->bk_state != 1) return 1;
     }
-    if (h->bk_state != 1) return 1;
     hipStream_t st = h->stream;
     shb_plan B;
     memset(&B, 0, sizeof(B));
@@ -443,9 +517,9 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
         h->bk_hstart.ensure_fresh((int64_t)B.nt * 4) || h->bk_ttot.ensure_fresh(((int64_t)B.nt + 1) * 4) ||
         h->bk_flag.ensure_fresh(64) || h->bk_rd.ensure(64))
         return fail(h, SH_E_OOM, "bucket workspace");
-    B.n_staged = h->bk.n_staged;
+    B.n_staged = stk ? 1 : h->bk.n_staged;
     for (int k = 0; k < B.n_staged; k++) {
-        const int a = h->bk.staged_attr[k];
+        const int a = stk ? h->stk.xattr : h->bk.staged_attr[k];
         const int w = type_width(P.attr_type[0][a]);
         if (h->bk_st[k].ensure_fresh(slots * w)) return fail(h, SH_E_OOM, "bucket workspace");
         B.st_src[k] = run->d_cols[a];
@@ -456,7 +530,32 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     // pass), then a shared tail for further passes; every partial is consumed at
     // most once, so n values suffice for the tail
     B.n_ms = n_ms;
-    const int64_t ms_vals = (int64_t)SHB_NB * B.n_chunks * SHB_SPAN + n;
+    // the stack matcher's runs: a run and its halo (the window's tiles before it) in
+    // one pass of SHB_TILE-event tiles, each run at least SH_STK_RUN_H halo lengths
+    // (default 8) at the stream's mean rate, at least 24 runs (a few workgroups per
+    // CU slot); each run's region of the match stream bounds its halo by SHB_HMAX tiles
+    int run_tiles = 0;
+    if (stk) {
+        hipMemcpyAsync(h->bk_rd.p, run->d_ts, 8, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(h->bk_rd.as<void>(8), run->d_ts + (n - 1), 8, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "bucket: timestamp read");
+        const int64_t span = *h->bk_rd.as<int64_t>(8) - *h->bk_rd.as<int64_t>(0);
+        const double rate = (double)n / (double)(std::max<int64_t>(span, 0) + 1);  // events per ms
+        const int halo_t = (int)std::min(1e6, rate * (double)(P.within_ms + 1) / SHB_TILE) + 1;
+        static const int run_h = getenv("SH_STK_RUN_H") ? std::max(1, atoi(getenv("SH_STK_RUN_H"))) : 8;
+        static const int run_env = getenv("SH_STK_RUN") ? atoi(getenv("SH_STK_RUN")) : 0;
+        run_tiles = run_env > 0 ? run_env : (int)std::min<int64_t>((int64_t)run_h * halo_t, std::max(1, B.nt / 24));
+        run_tiles = std::max(1, std::min(run_tiles, shk_max_run_tiles()));
+        K.run_tiles = run_tiles;
+        K.want_ms = n_ms;
+        // spilled entries per key (below the LDS ring): twice a key's mean events per
+        // window, at least 8 (a deeper stack raises SHK_F_SPILL: the host retries)
+        if (h->stk_cap == 0)
+            h->stk_cap = (int)std::min(511.0, std::max(8.0, 2.0 * rate * (double)(P.within_ms + 1) / nkeys));
+        K.spill_cap = h->stk_cap;
+    }
+    const int64_t runs = stk ? (B.nt + run_tiles - 1) / run_tiles : 0;
+    const int64_t ms_vals = stk ? n + runs * SHB_HMAX * SHB_TILE : (int64_t)SHB_NB * B.n_chunks * SHB_SPAN + n;
     for (int m = 0; m < n_ms; m++) {
         const int w = type_width(P.attr_type[0][ms[m]]);
         if (h->bk_ms[m].ensure_fresh(ms_vals * w)) return fail(h, SH_E_OOM, "match stream");
@@ -588,15 +687,23 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     hipMemcpyAsync(h->bk_rd.p, run->d_ts, 8, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "bucket: timestamp read");
     B.tbase = *h->bk_rd.as<int64_t>() - ((int64_t)1 << (31 - kb));
+    if (stk) {
+        const size_t sb = (size_t)runs * (SHB_NB / 4) * shk_spill_keys() * K.spill_cap * 8;
+        if (h->k_spill.ensure(sb)) return fail(h, SH_E_OOM, "stack matcher spill");
+        K.spill = h->k_spill.as<uint64_t>();
+    }
     hipEventRecord(h->ev[0], st);
     hipMemsetAsync(B.flag, 0, 32, st);  // flag word + match-stream allocator
     hipMemsetAsync(B.ttot, 0, ((int64_t)B.nt + 1) * 4, st);
     if (shb_partition(run->d_keys, run->d_ts, nkeys, &B, st)) return fail(h, SH_E_HIP, "bucket partition launch failed");
     hipEventRecord(h->ev[1], st);
     void* args[] = {&B};
-    if (hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.n_chunks), 1, 1, 512, 1, 1, 0, st,
-                              args, nullptr) != hipSuccess)
+    if (stk) {
+        if (shk_match(&B, &K, st)) return fail(h, SH_E_HIP, "stack matcher launch failed");
+    } else if (hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.n_chunks), 1, 1, 512, 1, 1, 0,
+                                     st, args, nullptr) != hipSuccess) {
         return fail(h, SH_E_HIP, "shb_match launch failed");
+    }
     if (carry && shb_agg_carry(&B, &AG, st)) return fail(h, SH_E_HIP, "aggregate carry launch failed");
     if (shb_finish(&B, h->w_scan.as<uint32_t>(), st)) return fail(h, SH_E_HIP, "bucket scan launch failed");
     hipEventRecord(h->ev[2], st);
@@ -608,7 +715,13 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in bucket engine");
     const int32_t flag = *h->bk_rd.as<int32_t>(0);
     const int64_t total = *h->bk_rd.as<uint32_t>(8);
-    if (B.prof) {
+    if (B.prof && stk) {
+        unsigned long long pr[16];
+        hipMemcpy(pr, B.prof, 128, hipMemcpyDeviceToHost);
+        fprintf(stderr, "[k_bk_stk clock ticks, sum over waves] setup %llu issue %llu sort %llu - %llu owner steps %llu "
+                        "rows %llu; batches %llu owner steps %llu; runs %lld of %d tiles\n",
+                pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], (long long)runs, run_tiles);
+    } else if (B.prof) {
         unsigned long long pr[16];
         hipMemcpy(pr, B.prof, 128, hipMemcpyDeviceToHost);
         fprintf(stderr, "[shb_match clock ticks, sum over workgroups] table %llu load %llu rank %llu walk %llu "
@@ -620,6 +733,19 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
                     pr[8], pr[9], pr[10], pr[11], pr[12]);
     }
     if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
+    if (flag && stk) {
+        static const bool dbg = getenv("SH_STK_DEBUG") != nullptr;
+        if (dbg) fprintf(stderr, "[stack matcher] refused on the device: flags 0x%x\n", flag);
+        h->stk_refused = flag;
+        if (flag == SHK_F_SPILL && h->stk_cap < 511) {
+            h->stk_cap = std::min(511, h->stk_cap * 4);  // deeper stacks than the mean rate suggests
+        } else if (flag & (SHB_F_TS | SHB_F_MONO)) {
+            return 1;  // neither matcher takes the batch
+        } else {
+            h->stk_skip = true;  // the sort-and-walk matcher once
+        }
+        return run_bucket(h, run, nkeys, force_carry);
+    }
     if (flag) return 1;
     run->out_count = total;
     if (total > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
@@ -630,234 +756,11 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
     h->times.advance_launches = 1;
     h->bk_last = 1;
+    h->stk_last = stk ? 1 : 0;
     h->bk_agg_carried = carry;
     if (carry) h->agg_last = 4;
     return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "bucket engine");
 }
-
-// arrival-order stack engine (sh_stack.hip): partitioned `every e1=S[f1] ->
-// e2=S[x.a op e1.a and ...] within W` with the ordering attribute a 4-byte float or
-// int and at most 8 * shk_max_keys() keys, the select list made of e2-side values,
-// e1's partition attribute and e1.a. 0 ok, 1 = not applicable or refused on the
-// device (the caller takes the bucketed engine), SH_E_MORE, <0 error
-int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys) {
-    h->stk_last = 0;
-    h->stk_refused = 0;
-    static const bool dbg = getenv("SH_STK_DEBUG") != nullptr;
-#define STK_NO(why)                                                          \
-    do {                                                                     \
-        if (dbg) fprintf(stderr, "[stack engine] not applicable: %s\n", why); \
-        return 1;                                                            \
-    } while (0)
-    const char* dis = getenv("SH_DISABLE_STACK");  // (read per call: tests A/B the engines)
-    if (dis && dis[0] && dis[0] != '0') return 1;
-    const shp_program& P = h->prog;
-    const int64_t n = run->n;
-    if (!h->partitioned || !P.out_fast || P.agg_post || n < 4096 || nkeys < 1) STK_NO("shape / size");
-    if (h->stk_state == 0) h->stk_state = shj_stack_form(&P, &h->stk) == 0 ? 1 : -1;
-    if (h->stk_state != 1) STK_NO("no stack form of f2");
-    if (P.within_ms < 0 || P.within_ms > 65535) STK_NO("window");
-    const int kmax = shk_max_keys();
-    int gshift = 1;  // at least two groups: 2,048-event sub-tiles, 64 events per owner wave
-    while (gshift <= 3 && ((int64_t)nkeys + (1 << gshift) - 1) >> gshift > kmax) gshift++;
-    if (gshift > 3) STK_NO("too many keys");
-    const shj_stack& S = h->stk;
-    shb_out O;
-    memset(&O, 0, sizeof(O));
-    O.n_out = P.n_out;
-    const int part_attr = h->part_attr0;
-    for (int o = 0; o < P.n_out; o++) {
-        const int a = P.out_attr[o], t = P.attr_type[0][a];
-        O.type[o] = t;
-        const bool fold = a == part_attr && (t == SH_T_STRING || t == SH_T_INT || t == SH_T_LONG || t == SH_T_BOOL);
-        if (P.out_slot[o] == 1 || fold) {
-            O.kind[o] = 1;
-            O.src[o] = run->d_cols[a];
-        } else if (a == S.xattr) {
-            O.kind[o] = SHB_OUT_KIND_Y;
-        } else {
-            STK_NO("an e1-side value other than the ordering attribute");
-        }
-    }
-    hipStream_t st = h->stream;
-    shk_plan K;
-    memset(&K, 0, sizeof(K));
-    K.n = n;
-    K.ts = run->d_ts;
-    K.keys = run->d_keys;
-    K.xcol = run->d_cols[S.xattr];
-    K.dom = S.dom;
-    K.op = S.op;
-    K.nkeys = nkeys;
-    K.gshift = gshift;
-    K.kpw = (int32_t)(((int64_t)nkeys + (1 << gshift) - 1) >> gshift);
-    K.within = P.within_ms;
-    K.n_terms = S.n_terms;
-    K.pre[0] = K.pre[1] = -1;
-    for (int k = 0; k < S.n_terms; k++) {
-        K.terms[k] = S.terms[k];
-        K.tl[k] = run->d_cols[S.terms[k].lattr];
-        K.tr[k] = S.terms[k].rkind == 1 ? nullptr : run->d_cols[S.terms[k].rattr];
-        // the loader prefetches one 4-byte left operand off the ordering column
-        const int lt = S.terms[k].ltype;
-        if (K.tl[k] != K.xcol && K.pre[0] < 0 && (lt == SH_T_INT || lt == SH_T_FLOAT || lt == SH_T_STRING))
-            K.pre[0] = k;
-    }
-    // order keys: `consume if cx > cy` (GT / LT after a flip), `or equal` for GE / LE
-    const bool f32 = S.dom == DOM_F32;
-    const bool flip = S.op == SH_OP_LT || S.op == SH_OP_LE;
-    K.kflip = flip ? 0xFFFFFFFFu : 0u;
-    K.ge = (S.op == SH_OP_GE || S.op == SH_OP_LE) ? 1 : 0;
-    // -0.0 and +0.0 have adjacent keys (0x7FFFFFFF, 0x80000000 before the flip):
-    // the compares merge the first into the second; ints need no merge
-    K.zk1 = f32 ? (0x7FFFFFFFu ^ K.kflip) : 0u;
-    K.zk0 = f32 ? (0x80000000u ^ K.kflip) : 0u;
-    // the opening filter's fast form: 4-byte column (ordering or prefetched) vs a
-    // constant in the column's own domain; anything else runs the generic terms
-    K.fast_open = 1;
-    for (int k = 0; k < S.n_terms; k++) {
-        const shp_term& T = S.terms[k];
-        const bool fl = T.ltype == SH_T_FLOAT && T.dom == DOM_F32;
-        const bool in = T.ltype == SH_T_INT && T.dom == DOM_I32;
-        const int col = K.tl[k] == K.xcol ? 0 : (k == K.pre[0] ? 1 : -1);
-        if (T.rkind != 1 || !(fl || in) || col < 0 || T.op < SH_OP_EQ || T.op > SH_OP_LE) {
-            K.fast_open = 0;
-            break;
-        }
-        uint32_t cb;  // the constant in the compare domain (binary numeric promotion)
-        if (fl) {
-            float cf;
-            switch (T.ctype) {
-                case SH_T_INT: cf = (float)(int32_t)T.c; break;
-                case SH_T_LONG: cf = (float)T.c; break;
-                case SH_T_FLOAT: memcpy(&cf, &T.c, 4); break;
-                case SH_T_DOUBLE: {
-                    double d;
-                    memcpy(&d, &T.c, 8);
-                    cf = (float)d;
-                    break;
-                }
-                default: K.fast_open = 0; cf = 0.f;
-            }
-            if (cf != cf) K.fast_open = 0;  // a NaN constant: the generic terms
-            memcpy(&cb, &cf, 4);
-            cb = (cb & 0x80000000u) ? ~cb : (cb | 0x80000000u);
-            if (cb == 0x7FFFFFFFu) cb = 0x80000000u;
-        } else {
-            if (T.ctype != SH_T_INT) K.fast_open = 0;
-            cb = (uint32_t)(int32_t)T.c ^ 0x80000000u;
-        }
-        if (!K.fast_open) break;
-        K.f_col[k] = col;
-        K.f_f32[k] = fl ? 1 : 0;
-        K.f_ckey[k] = cb;
-        K.f_lt[k] = T.op == SH_OP_LT || T.op == SH_OP_LE || T.op == SH_OP_NE;
-        K.f_eq[k] = T.op == SH_OP_EQ || T.op == SH_OP_GE || T.op == SH_OP_LE;
-        K.f_gt[k] = T.op == SH_OP_GT || T.op == SH_OP_GE || T.op == SH_OP_NE;
-        K.f_nan[k] = T.op == SH_OP_NE;  // NaN: every compare false but !=
-    }
-    static const bool prof = getenv("SH_STK_PROFILE") != nullptr;
-    if (prof) {
-        if (h->bk_prof.ensure_fresh(128)) return fail(h, SH_E_OOM, "profile");
-        K.prof = h->bk_prof.as<unsigned long long>();
-    }
-    const int64_t sub = (int64_t)1024 << gshift;  // events per sub-tile (EPL = G)
-    K.nsub = (int32_t)((n + sub - 1) / sub);
-    // chunks: one workgroup per CU (256 >> gshift chunks), each at least four
-    // windows of events at the stream's mean rate (the halo replay <= 25%)
-    if (h->bk_rd.ensure(64)) return fail(h, SH_E_OOM, "stack engine");
-    hipMemcpyAsync(h->bk_rd.as<void>(0), run->d_ts, 8, hipMemcpyDeviceToHost, st);
-    hipMemcpyAsync(h->bk_rd.as<void>(8), run->d_ts + (n - 1), 8, hipMemcpyDeviceToHost, st);
-    if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "stack engine: timestamp read");
-    const int64_t span = *h->bk_rd.as<int64_t>(8) - *h->bk_rd.as<int64_t>(0);
-    if (span < 0) STK_NO("timestamps go back");
-    const double rate = (double)n / (double)(span + 1);  // events per ms
-    const int64_t min_chunk = (int64_t)(4.0 * rate * (double)(P.within_ms + 1)) + sub;
-    int n_chunks = 256 >> gshift;
-    // spilled entries per key: a few windows' worth of a key's events at the mean
-    // rate (a deeper run raises SHK_F_SPILL and the host retries with more)
-    int spill_cap = (int)std::min<double>(511.0, std::max(32.0, 2.0 * rate * (double)(P.within_ms + 1) / nkeys));
-    for (;;) {
-        int64_t chunk = (n + n_chunks - 1) / n_chunks;
-        if (chunk < min_chunk) chunk = min_chunk;
-        chunk = (chunk + sub - 1) / sub * sub;
-        K.chunk = chunk;
-        K.n_chunks = (int32_t)((n + chunk - 1) / chunk);
-        K.cpx = (K.n_chunks + 7) / 8;
-        const int64_t grid = (int64_t)8 * K.cpx << gshift;
-        if (h->k_cnt.ensure_fresh((size_t)n) || h->k_ttot.ensure_fresh(((size_t)K.nsub + 1) * 4) ||
-            h->k_hstart.ensure_fresh((size_t)K.n_chunks * 8) || h->k_flag.ensure_fresh(64) ||
-            h->k_spill.ensure_fresh((size_t)grid * K.kpw * spill_cap * 8) ||
-            h->k_scan.ensure_fresh(shd_scan_tmp_words((int64_t)K.nsub + 1) * 4 + 64))
-            return fail(h, SH_E_OOM, "stack engine workspace");
-        K.cnt = h->k_cnt.as<uint8_t>();
-        K.ttot = h->k_ttot.as<uint32_t>();
-        K.hstart = h->k_hstart.as<int64_t>();
-        K.spill = h->k_spill.as<uint64_t>();
-        K.flag = h->k_flag.as<int32_t>();
-        K.spill_cap = spill_cap;
-        shb_cols OC;
-        int32_t wd[SHB_MAX_OUT];
-        for (int o = 0; o < O.n_out; o++) wd[o] = type_width(O.type[o]);
-        direct_layout(h, run, wd, O.n_out, &OC);
-        if (K.prof) hipMemsetAsync(K.prof, 0, 128, st);
-        hipEventRecord(h->ev[0], st);
-        hipMemsetAsync(K.flag, 0, 4, st);
-        hipMemsetAsync(K.ttot, 0, ((size_t)K.nsub + 1) * 4, st);
-        K.omask = nullptr;
-        if (!K.fast_open && K.n_terms > 0) {
-            if (h->k_omask.ensure_fresh(((size_t)n / 64 + 2) * 8)) return fail(h, SH_E_OOM, "stack engine workspace");
-            K.omask = h->k_omask.as<uint64_t>();
-            if (shk_open_bits(&K, st)) return fail(h, SH_E_HIP, "stack engine filter launch failed");
-        }
-        if (shk_count(&K, st)) return fail(h, SH_E_HIP, "stack engine count launch failed");
-        hipEventRecord(h->ev[1], st);
-        if (shd_exclusive_scan(K.ttot, K.ttot, (int64_t)K.nsub + 1, h->k_scan.as<uint32_t>(), st))
-            return fail(h, SH_E_HIP, "stack engine scan failed");
-        hipEventRecord(h->ev[2], st);
-        if (shk_emit(&K, &O, &OC, 0, run->d_out_seq, run->d_out_values, run->out_capacity, st))
-            return fail(h, SH_E_HIP, "stack engine emit launch failed");
-        hipEventRecord(h->ev[3], st);
-        hipMemcpyAsync(h->bk_rd.as<void>(0), K.flag, 4, hipMemcpyDeviceToHost, st);
-        hipMemcpyAsync(h->bk_rd.as<void>(8), K.ttot + K.nsub, 4, hipMemcpyDeviceToHost, st);
-        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the stack engine");
-        const int32_t flag = *h->bk_rd.as<int32_t>(0);
-        if (K.prof) {
-            unsigned long long pr[16];
-            hipMemcpy(pr, K.prof, 128, hipMemcpyDeviceToHost);
-            fprintf(stderr, "[stack engine clock ticks, both passes, summed over waves] producer %llu queue %llu "
-                            "process %llu; batches %llu rounds %llu queued events %llu; grid %d, chunk %lld, groups %d\n",
-                    pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], (int)(8 * K.cpx << K.gshift), (long long)K.chunk,
-                    1 << K.gshift);
-        }
-        if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
-        if (flag == SHB_F_HALO && n_chunks > 1) {
-            n_chunks = std::max(1, n_chunks / 4);  // bursty timestamps: longer chunks
-            continue;
-        }
-        if (flag == SHK_F_SPILL && spill_cap < 511) {
-            spill_cap = std::min(511, spill_cap * 4);  // deeper stacks than the mean rate suggests
-            continue;
-        }
-        if (flag) {
-            h->stk_refused = flag;
-            if (dbg) fprintf(stderr, "[stack engine] refused on the device: flags 0x%x\n", flag);
-            return 1;
-        }
-        const int64_t total = *h->bk_rd.as<uint32_t>(8);
-        run->out_count = total;
-        if (total > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
-        if (run->d_out_query && total > 0) hipMemsetAsync(run->d_out_query, 0, total * 4, st);
-        h->times.segment_ms = 0.0f;
-        hipEventElapsedTime(&h->times.advance_ms, h->ev[0], h->ev[2]);
-        hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
-        hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
-        h->times.advance_launches = 1;
-        h->stk_last = 1;
-        return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "stack engine");
-    }
-}
-#undef STK_NO
 
 // the rise-and-fall sequence on the bucket-carry engine (sh_bucket.hip k_s3b):
 // the tile-local bucket partition, one workgroup per bucket carrying its keys'

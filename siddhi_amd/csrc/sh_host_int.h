@@ -335,12 +335,14 @@ struct sh_handle {
     DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS], bk_agg[SHB_MAX_AGG];
     bool bk_agg_carried = false;  // the last bucketed run carried its aggregates (k_bk_aggc)
     PinBuf bk_rd;
-    // ---- arrival-order stack engine (sh_stack.hip): 0 untried, 1 applicable, -1 not
+    // ---- the bucketed engine's stack matcher (sh_stack.hip): 0 untried, 1 applicable, -1 not
     int stk_state = 0;
-    int stk_last = 0;             // 1: the last sh_run_device ran on the stack engine
-    int stk_refused = 0;          // the device flags of the last refused run (diagnostics)
+    int stk_last = 0;             // 1: the last bucketed run matched on the stack matcher
+    int stk_refused = 0;          // the device flags of the last refused stack-matcher run (diagnostics)
     shj_stack stk{};
-    DevBuf k_cnt, k_ttot, k_hstart, k_spill, k_flag, k_scan, k_omask;
+    bool stk_skip = false;        // the next bucketed run takes the sort-and-walk matcher
+    int stk_cap = 0;              // spilled entries per key (0: from the first batch's rate)
+    DevBuf k_spill;
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
     DevBuf w_colrows;
     bool cols_rows = false;
@@ -419,7 +421,6 @@ int rows_for_cols(sh_handle* h, sh_device_run* run);
 // packed rows, unless the rows were sent to the workspace): OC->use = SHB_OUT_RAW otherwise
 void direct_layout(sh_handle* h, sh_device_run* run, const int32_t* widths, int n_out, shb_cols* OC);
 int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry = false);
-int run_stack(sh_handle* h, sh_device_run* run, int32_t nkeys);
 int run_rules(sh_handle* h, sh_device_run* run);
 int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys);
 shd_segment_ws seg_ws(sh_handle* h, int64_t n);

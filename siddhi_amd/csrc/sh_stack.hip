@@ -1,4 +1,4 @@
-// sh_stack.hip — arrival-order stack engine for partitioned
+// sh_stack.hip — the stack matcher of the bucketed window engine for partitioned
 //   every e1=S[f1] -> e2=S[x.a op e1.a] within W          (C2)
 //
 // StreamPreStateProcessor.java:325-403 (break-early expiry, then processAndReturn
@@ -7,141 +7,101 @@
 // first later event q of its key with x_q op y_i (y_i = the same attribute of i),
 // unless ts_q - ts_i > W expired it first. When the ordering term compares one
 // attribute with itself, a key's pending partials form a monotone stack: a
-// consumer pops exactly the entries it beats, which sit on top (for `>` the stack
-// is non-increasing from the bottom up: every survivor of q is >= x_q = y_q and q
-// is pushed on top of them), and expiry drops entries from the bottom (creation
-// order is time order). The rows of a consumer are its popped entries in creation
-// order. No key sort, no segment, no walk back.
+// consumer takes exactly the entries it beats, which sit on top (for `>` the stack
+// never increases upwards: every survivor of q is >= x_q and q goes on top), and
+// expiry drops entries from the bottom (creation order is time order). A
+// consumer's rows are its popped entries in creation order.
 //
-// Layout of the work (gfx950: 256 CUs in 8 XCDs, 160 KiB LDS per CU):
-//  * the stream is cut into n_chunks arrival chunks; the keys into G = 2, 4 or 8
-//    groups (key & (G - 1)); workgroup (chunk, group) runs on one CU with the
-//    stacks of its <= SK_KPW keys in LDS (a ring of SK_D entries per key: the
-//    ordering value and the timestamp as a 16-bit offset; deeper entries spill to
-//    a per-key stack in HBM, touched by ~0.04% of the events on C2). The G
-//    workgroups of a chunk sit on one XCD, so the chunk's columns come from HBM
-//    once and from that XCD's L2 for the other groups.
-//  * a chunk first replays its halo (the events within W before it, found by a
-//    parallel search of the timestamps) without output, so its stacks start
-//    exact: a partial older than the halo is expired for every event of the chunk.
-//  * per sub-tile of 1,024 * EPL arrival events: every wave loads its contiguous
-//    64 * EPL events (coalesced rows), keeps its group's events and sends each to
-//    the wave that owns its key (local key & 15) through a per-wave LDS queue, in
-//    arrival order (ranks from wave ballots and returning LDS atomics; two
-//    workgroup barriers per sub-tile). Each wave then processes its queue in
-//    batches of 64: the k-th event of a key within the batch runs in round k, so
-//    the events of one round touch distinct keys; an event loads its key's whole
-//    ring (16 LDS reads issued together), expires, pops and pushes in registers.
-//  * pass 1 writes each event's count (u8) and the sub-tile totals (ttot); an
-//    exclusive scan turns them into each sub-tile's first row; pass 2 replays the
-//    chunk and writes each consumer's rows at sub-tile base + the prefix of the
-//    counts before it (the producer waves scan the counts of their rows).
-// HBM bytes per event (C2): pass 1 reads ts 8 + key 4 + price 4 and writes the
-// count 1; pass 2 reads them again + the count + volume 8 and writes 32 B per row.
+// This matcher can replace the sort-and-walk one (shb_match, hipRTC) between the
+// two kernels of sh_bucket.hip (opt-in, SH_STACK=1: on C2 at 100M it takes 3.7 ms
+// where shb_match takes 2.1, DESIGN.md "stack matcher"): k_bk_scatter has put
+// every arrival tile in key-bucket order (b = key & 255; per event the packed word
+// (ts - tbase) << kb | key >> 8 and the staged ordering column), k_bk_emit writes
+// the ordered rows from what this kernel leaves: the counts (cnt, at the slots),
+// the e1 values (match stream ms[0]), each (tile, bucket) segment's first match
+// position (mstart) and the per-tile totals (ttot).
+//
+// One wave per (bucket, run of tiles), four buckets of one run per workgroup:
+//  * a wave reads its bucket's events of the run's tiles (after the halo tiles the
+//    window reaches, replayed without output) as one stream in arrival order, in
+//    batches of SK_B events (the next batch's loads in flight while the current
+//    one runs);
+//  * lane k owns local key k (a bucket holds <= 64 keys): its stack's head (ring
+//    bottom and count, top value, bottom timestamp, spilled count) in registers,
+//    its ring of SK_D entries in an LDS column no other lane touches, deeper
+//    entries spilled to a per-key stack in HBM. Six ballots per 64 events sort the
+//    batch by key in LDS (stable: each key's events stay in arrival order), and
+//    each owner then runs its events: expire the bottom, take the entries the
+//    event beats, stage their values, push the event if it opens. A batch costs as
+//    many steps as its busiest key has events; every step reads one LDS word pair
+//    whose address is known a step ahead, and the second entries from the top and
+//    the bottom are read speculatively with it;
+//  * then, lanes over events: the counts' prefix gives every event its first
+//    match-stream position, each tile's first event of the bucket records the
+//    segment's position (mstart), and lanes over the staged values write them out.
+// No segment table, no walk back, no workgroup barrier.
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
 
 #include "../../include/sh_query.h"
 #include "sh_device.h"
-#include "sh_rows.h"
-#include "sh_vm.h"
 #include "sh_wave.h"
 
-#define SK_TPB 1024
-#define SK_NW (SK_TPB / 64)  // waves: a key's owner wave is its local key & 15
-#define SK_D 8               // ring entries per key in LDS
-#define SK_KPW 2500          // keys per workgroup at most
-#define SK_CAPW 160          // queue entries per owner wave and sub-tile (64 expected)
-#define SK_OFF_BITS 13       // q2: event offset in the sub-tile | row offset << 13
-#define SK_ROWS_LIM (1u << (32 - SK_OFF_BITS))
+#define SK_WPB 4        // waves (buckets) per workgroup
+#define SK_D 8          // ring entries per key in LDS
+#define SK_KEYS 64      // local keys of a bucket, at most (kb <= 6)
+#define SK_B 256        // events of a batch
+#define SK_RUNT 256     // tiles of a run and its halo, at most
+#define SK_STG 384      // staged matches of a batch, at most (else SHB_F_COUNT)
 
-static_assert(SK_NW == 16, "16 owner waves");
-
-struct SkLds {
-    uint32_t y[SK_D][SK_KPW];         // ring entries: order key of the ordering value
-    uint16_t t[SK_D][SK_KPW];         // ... timestamp - tb
-    uint16_t h[SK_KPW];               // bottom (3 bits) | count << 3 (4) | spilled << 7 (9)
-    uint16_t spt[SK_KPW];             // timestamp of the newest spilled entry
-    uint32_t qx[SK_NW * SK_CAPW];     // queue: order key of the ordering value
-    uint32_t q1[SK_NW * SK_CAPW];     // ts - tb | wave-local key << 16 | NaN << 30 | open << 31
-    uint32_t q2[SK_NW * SK_CAPW];     // offset in the sub-tile | row offset << 13 (pass 2)
-    uint32_t wcnt[SK_NW][SK_NW];      // [producer wave][owner wave]: queued events
-    uint32_t wrow[SK_NW];             // pass 2: rows of each producer wave's events
-    uint32_t wsum[SK_NW];             // pass 1: matches of each owner wave's events
-    unsigned long long sa, sz;        // halo search bounds
+struct SkWave {
+    uint32_t y[SK_D][SK_KEYS];   // ring entries: order keys (column k: key k's ring)
+    uint32_t t[SK_D][SK_KEYS];   // ... packed timestamps (ts - tbase)
+    union {
+        uint2 sw[SK_B];          // the batch by key: packed word, order key (^ kflip)
+        uint32_t pre[SK_B];      // then each event's first match-stream position
+    } u;
+    uint32_t bg[SK_B];           // tile << 13 | slot of each event (arrival order)
+    uint32_t stv[SK_STG];        // staged values of the batch's matches (order keys)
+    uint16_t stt[SK_STG];        // their event (arrival index in the batch) | row << 8
+    uint16_t so[SK_B];           // each sorted entry: arrival index | opens << 8 | NaN << 9
+    uint8_t cntb[SK_B];          // each event's matches (<= 255, else SHB_F_COUNT)
+    uint32_t cum[SK_RUNT + 1];   // stream position of each tile's first event of the bucket
+    uint16_t lo[SK_RUNT];        // the bucket's start in each tile's bucket order
+    uint32_t sn;                 // staged values so far
 };
-static_assert(sizeof(SkLds) <= 163840, "LDS");
 
 // order keys: a float's IEEE bits (or an int) as an unsigned integer of the same
 // order -- positive floats get the sign bit set, negative ones are inverted -- so
-// every comparison of the ordering term is one unsigned compare, branch-free
-__device__ __forceinline__ uint32_t sk_key(uint32_t bits, bool f32) {
-    return f32 ? ((bits & 0x80000000u) ? ~bits : (bits | 0x80000000u)) : (bits ^ 0x80000000u);
+// every operator becomes one unsigned compare
+template <bool F32>
+__device__ __forceinline__ uint32_t sk_key(uint32_t bits) {
+    return F32 ? ((bits & 0x80000000u) ? ~bits : (bits | 0x80000000u)) : (bits ^ 0x80000000u);
 }
-__device__ __forceinline__ uint32_t sk_unkey(uint32_t k, bool f32) {
-    return f32 ? ((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k) : (k ^ 0x80000000u);
+template <bool F32>
+__device__ __forceinline__ uint32_t sk_unkey(uint32_t k) {
+    return F32 ? ((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k) : (k ^ 0x80000000u);
 }
 
-// the opening filter's fast form: each term compares a 4-byte column (the ordering
-// one or the prefetched one) with a constant through order keys
-__device__ __forceinline__ bool sk_open_fast(const shk_plan& P, uint32_t x, uint32_t l0) {
+// the opening filter: terms on the ordering column against constants, through
+// order keys (-0.0 as +0.0; NaN: every compare false but !=)
+__device__ __forceinline__ bool sk_open(const shk_params& K, uint32_t x) {
     bool ok = true;
-    for (int k = 0; k < P.n_terms; k++) {
-        const uint32_t v = P.f_col[k] ? l0 : x;
-        const bool f = P.f_f32[k] != 0;
-        const bool nan = f && (v & 0x7FFFFFFFu) > 0x7F800000u;
-        uint32_t kv = sk_key(v, f);
-        kv = (f && kv == 0x7FFFFFFFu) ? 0x80000000u : kv;  // -0.0 compares as +0.0
-        const uint32_t kc = P.f_ckey[k];
-        const bool r = (P.f_lt[k] && kv < kc) || (P.f_eq[k] && kv == kc) || (P.f_gt[k] && kv > kc);
-        ok = ok && (nan ? P.f_nan[k] != 0 : r);
+#pragma unroll
+    for (int k = 0; k < SHK_MAX_TERMS; k++) {
+        if (k >= K.n_terms) break;
+        const bool f = K.f_f32[k] != 0;
+        const bool nan = f && (x & 0x7FFFFFFFu) > 0x7F800000u;
+        uint32_t kv = f ? sk_key<true>(x) : sk_key<false>(x);
+        kv = (f && kv == 0x7FFFFFFFu) ? 0x80000000u : kv;
+        const uint32_t kc = K.f_ckey[k];
+        const bool r = (K.f_lt[k] && kv < kc) || (K.f_eq[k] && kv == kc) || (K.f_gt[k] && kv > kc);
+        ok = ok && (nan ? K.f_nan[k] != 0 : r);
     }
     return ok;
 }
 
-// the opening filter (f1 and the e1-only terms of f2) on event e, as terms_pass:
-// the general form, evaluated by k_stk_open into a bit per event when the terms
-// have no fast form (keeps the VM's code out of the matcher)
-__device__ __forceinline__ bool sk_open_gen(const shk_plan& P, int64_t e) {
-    for (int k = 0; k < P.n_terms; k++) {
-        const shp_term T = P.terms[k];
-        VmVal l, r;
-        l.t = T.ltype;
-        l.null = 0;
-        l.b = bk_raw(P.tl[k], e, T.ltype);
-        if (T.rkind == 1) {
-            r.t = T.ctype;
-            r.null = 0;
-            r.b = T.c;
-        } else {
-            r.t = T.rtype;
-            r.null = 0;
-            r.b = bk_raw(P.tr[k], e, T.rtype);
-            if (T.rkind == 2) {
-                VmVal c;
-                c.t = T.ctype;
-                c.null = 0;
-                c.b = T.c;
-                r = vm_arith(T.aop, T.atype, r, c);
-                if (r.null) return false;
-            }
-        }
-        if (!vm_cmp(T.op, T.dom, l, r)) return false;
-    }
-    return true;
-}
-
-// one bit per event: the opening filter's general form (64 events per word)
-__global__ void __launch_bounds__(256) k_stk_open(shk_plan P) {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool ok = e < P.n && sk_open_gen(P, e);
-    const uint64_t m = __ballot(ok);
-    if ((threadIdx.x & 63) == 0 && e < P.n) const_cast<uint64_t*>(P.omask)[e >> 6] = m;
-}
-
-// a key's spilled entries are written by one lane and read back by another lane of
-// the same wave in a later round: both sides go to L2 (agent-scope relaxed atomics
-// bypass the CU's L1, whose copy of a reused slot would otherwise be stale)
+// a key's spilled entries are written and read back by its owner lane: through L2
+// (agent-scope relaxed atomics skip the L1)
 __device__ __forceinline__ uint64_t sk_spill_load(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -149,498 +109,356 @@ __device__ __forceinline__ void sk_spill_store(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// value of a select entry of a row: the consumed partial's ordering value (y) or
-// the consumer's attribute (preloaded)
-__device__ __forceinline__ int64_t sk_yraw(uint32_t y, int type) {
-    return type == SH_T_FLOAT ? (int64_t)y : (int64_t)(int32_t)y;
+__device__ __forceinline__ void sk_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// XCD-aware (chunk, group) of this workgroup: workgroups are dealt round-robin
-// to the 8 XCDs, so the G groups of a chunk take consecutive slots of one XCD
-__device__ __forceinline__ void sk_place(const shk_plan& P, int* c, int* g) {
+template <bool F32>
+__global__ void __launch_bounds__(64 * SK_WPB, 2) k_bk_stk(shb_plan P, shk_params K) {
+    __shared__ SkWave Ls[SK_WPB];
+    const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
+    SkWave& L = Ls[wv];
+    // workgroups are dealt round-robin to the 8 XCDs: XCD x takes bucket groups
+    // [8x, 8x + 8) of each run (whose tiles' columns its L2 then holds)
     const int xcd = (int)(blockIdx.x & 7u), slot = (int)(blockIdx.x >> 3);
-    *c = xcd * P.cpx + (slot >> P.gshift);
-    *g = slot & ((1 << P.gshift) - 1);
-}
-
-// first event of the halo of a chunk starting at cb: the first index with
-// ts >= ts[cb] - W (timestamps are non-decreasing), at most one chunk back
-// (else SHB_F_HALO); a 1,024-ary search over the timestamps
-__device__ int64_t sk_halo(const shk_plan& P, SkLds& L, int64_t cb) {
-    if (cb == 0) return 0;
-    const int64_t T = P.ts[cb] - P.within;
-    int64_t a = cb - P.chunk < 0 ? 0 : cb - P.chunk;
-    if (P.ts[a] >= T) {
-        if (a > 0 && threadIdx.x == 0) atomicOr(P.flag, SHB_F_HALO);
-        return a;
-    }
-    int64_t z = cb;  // ts[a] < T <= ts[z]
-    while (z - a > 1) {
-        const int64_t step = (z - a + SK_TPB - 1) / SK_TPB;
-        if (threadIdx.x == 0) {
-            L.sa = (unsigned long long)a;
-            L.sz = (unsigned long long)z;
-        }
-        __syncthreads();
-        const int64_t p = a + step * (int64_t)(threadIdx.x + 1);
-        if (p < z) {
-            if (P.ts[p] >= T) atomicMin(&L.sz, (unsigned long long)p);
-            else atomicMax(&L.sa, (unsigned long long)p);
-        }
-        __syncthreads();
-        a = (int64_t)L.sa;
-        z = (int64_t)L.sz;
-        __syncthreads();
-    }
-    return z;
-}
-
-template <int PASS, int EPL, int MODE, int NO>
-__global__ void __launch_bounds__(SK_TPB, 1) k_stk(shk_plan P, shb_out O, shb_cols OC, uint64_t seq_base,
-                                                  uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_vals,
-                                                  int64_t out_cap) {
-    __shared__ SkLds L;
-    constexpr int SUB = SK_TPB * EPL;
-    static_assert(SUB <= (1 << SK_OFF_BITS), "offsets");
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    int c, g;
-    sk_place(P, &c, &g);
-    if (c >= P.n_chunks) return;
-    const int64_t cb = (int64_t)c * P.chunk;
-    const int64_t ce = cb + P.chunk < P.n ? cb + P.chunk : P.n;
-    if (cb >= ce) return;
-    if (PASS == 2 && __hip_atomic_load(P.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-        return;  // pass 1 refused the run: the host takes another engine
-    const int G = 1 << P.gshift;
-    int64_t h;
-    if (PASS == 1) {
-        h = sk_halo(P, L, cb);
-        if (g == 0 && threadIdx.x == 0) P.hstart[c] = h;
-    } else {
-        h = P.hstart[c];
-    }
-    const int64_t hb = (h / SUB) * SUB;
-    const int64_t tb = P.ts[hb];
-    for (int i = threadIdx.x; i < P.kpw; i += SK_TPB) L.h[i] = 0;
+    const int run = slot >> 3;
+    const int b = (((xcd << 3) | (slot & 7)) * SK_WPB) + wv;
+    const int A = run * K.run_tiles;
+    if (A >= P.nt) return;
+    const int E = A + K.run_tiles < P.nt ? A + K.run_tiles : P.nt;
+    const int kb = P.kb;
+    const uint32_t kmask = (1u << kb) - 1u;
     const uint32_t W = (uint32_t)P.within;
-    const bool f32 = P.dom == DOM_F32;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const bool owner = (lane >> kb) == 0;  // lane `lane` owns local key `lane`
+    const int h0 = P.hstart[A];
+    const int nt = E - h0;  // tiles of the pass
+    uint32_t flag = 0u;
+    // the halo is complete for a consumer at packed time `now` iff every event
+    // before it is older than the window: now > tpre[h0] - tbase + W (hlim <= now)
+    uint32_t hlim = 0u;
+    if (h0 > 0) {
+        const int64_t hl = P.tpre[h0] - P.tbase + P.within + 1;
+        hlim = hl <= 0 ? 0u : (hl >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)hl);
+    }
+    if (nt > SK_RUNT) {
+        if (lane == 0) atomicOr(P.flag, SHB_F_HALO);
+        return;
+    }
+    // the bucket's segment of every tile (transposed starts) -> stream positions
+    uint32_t carry = 0u;
+    for (int i0 = 0; i0 < nt; i0 += 64) {
+        const int i = i0 + lane;
+        uint32_t l0 = 0u, c = 0u;
+        if (i < nt) {
+            l0 = P.tofft[(int64_t)b * P.tstride + h0 + i];
+            c = (uint32_t)P.tofft[(int64_t)(b + 1) * P.tstride + h0 + i] - l0;
+            L.lo[i] = (uint16_t)l0;
+        }
+        const uint32_t inc = shw_incl_scan(c);
+        if (i < nt) L.cum[i] = carry + inc - c;
+        carry += shw_last(inc);
+    }
+    const uint32_t nev = carry;  // events of the pass
+    if (lane == 0) {
+        L.cum[nt] = nev;
+        L.sn = 0u;
+    }
+    // the run's region of the match stream: a partial is consumed once, and the
+    // partials the run's consumers take are events of the pass
+    uint32_t mpos = 0u;
+    if (K.want_ms) {
+        if (lane == 0) mpos = atomicAdd(P.ms_ctr, nev);
+        mpos = (uint32_t)__shfl((int)mpos, 0);
+    }
+    const uint32_t* __restrict__ xs = (const uint32_t*)P.st_dst[0];
+    uint32_t* __restrict__ ms = (uint32_t*)P.ms[0];
+    // key `lane`'s spill stack (HBM)
+    uint64_t* const spl = K.spill + (((uint64_t)blockIdx.x * SK_WPB + wv) * SK_KEYS + lane) * (uint64_t)K.spill_cap;
+    const uint32_t gA = (uint32_t)A << SHB_TILE_SHIFT;  // the first emitting slot index
+    sk_wave_sync();
+    const uint32_t fem = L.cum[A - h0];                  // ... and stream position
 
-    // the producer's events of sub-tile s0: row i holds s0 + w * 64 * EPL + 64 i + lane,
-    // loaded one sub-tile ahead (with the predecessor of row 0, the prefetched
-    // filter operands and, pass 2, the sub-tile's first row)
-    int32_t kk[EPL];
-    uint32_t xx[EPL];
-    int64_t tt[EPL];
-    uint32_t cc[EPL];
-    uint32_t la[EPL];
-    uint64_t om[EPL];
-    int64_t tpr = INT64_MIN;
-    uint32_t rows_next = 0;
-    auto load = [&](int64_t s0) {
-        const int64_t e0 = s0 + (int64_t)w * (64 * EPL) + lane;
-        tpr = (e0 > hb && e0 - 1 < ce) ? P.ts[e0 - 1] : INT64_MIN;
-        if (PASS == 2 && s0 >= cb) rows_next = P.ttot[s0 / SUB];
+    // a batch's loads: stream position -> tile (binary search of cum) -> slot
+    uint32_t rw[SK_B / 64], rx[SK_B / 64], rg[SK_B / 64];
+    auto issue = [&](uint32_t fb) {
 #pragma unroll
-        for (int i = 0; i < EPL; i++) {
-            const int64_t e = e0 + 64 * i;
-            const bool v = e < ce;
-            kk[i] = v ? P.keys[e] : -1;
-            xx[i] = v ? ((const uint32_t*)P.xcol)[e] : 0u;
-            tt[i] = v ? P.ts[e] : tb;
-            cc[i] = (PASS == 2 && v && s0 >= cb) ? (uint32_t)P.cnt[e] : 0u;
-            la[i] = (P.pre[0] >= 0 && v) ? ((const uint32_t*)P.tl[P.pre[0]])[e] : 0u;
-            om[i] = (P.omask && v) ? P.omask[e >> 6] : 0ull;  // (rows are 64-aligned)
+        for (int j = 0; j < SK_B / 64; j++) {
+            const uint32_t f = fb + (uint32_t)(j * 64 + lane);
+            rw[j] = rx[j] = rg[j] = 0u;
+            if (f < nev) {
+                int lo = 0, hi = nt - 1;  // the last tile whose start is <= f
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (L.cum[mid] <= f) lo = mid;
+                    else hi = mid - 1;
+                }
+                const uint32_t g = ((uint32_t)(h0 + lo) << SHB_TILE_SHIFT) + L.lo[lo] + (f - L.cum[lo]);
+                rg[j] = g;
+                rw[j] = P.w0[g];
+                rx[j] = xs[g];
+            }
         }
     };
-    load(hb);
-    unsigned long long pc_prod = 0, pc_queue = 0, pc_proc = 0, pc0 = 0, n_batch = 0, n_round = 0, n_ev = 0;
-    int64_t prev_sub = -1;  // pass 1: the last sub-tile whose totals wait in wsum
-    for (int64_t s0 = hb; s0 < ce; s0 += SUB) {
-        const bool emit = s0 >= cb;
-        if (P.prof) pc0 = clock64();
-        // ---- producer: own events, their owner wave and rank
-        if (lane < SK_NW) L.wcnt[w][lane] = 0u;
-        uint32_t rk[EPL], qa[EPL], qb[EPL], qc[EPL];
-        int bn[EPL];
-        uint32_t rr[EPL];
-        uint32_t flag = 0;
-        uint32_t rcarry = 0;
+    // key `lane`'s stack head: ring bottom and count, spilled entries, latest
+    // timestamp, top value, bottom timestamp, newest spilled timestamp
+    uint32_t o_bo = 0u, o_c = 0u, o_sc = 0u, o_last = 0u, o_ytop = 0u, o_tbot = 0u, o_spt = 0u;
+    // diagnostics (SH_BK_PROFILE): clock ticks per phase and counts, per wave
+    const bool prof = P.prof != nullptr;
+    unsigned long long pt = prof ? clock64() : 0ull, pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define SK_TICK(i)                                 \
+    if (prof) {                                    \
+        const unsigned long long t2_ = clock64();  \
+        pr[i] += t2_ - pt;                         \
+        pt = t2_;                                  \
+    }
+    SK_TICK(0);
+    issue(0u);
+    SK_TICK(1);
+    uint32_t prevT = 0xFFFFFFFFu;  // the last tile whose segment position is recorded
+    for (uint32_t fb = 0; fb < nev; fb += SK_B) {
+        const uint32_t fe = fb + SK_B < nev ? fb + SK_B : nev;
+        const uint32_t ethr = fem <= fb ? 0u : (fem - fb < SK_B ? fem - fb : SK_B);  // first emitting event
+        // the batch by key, stable: each owner's events [kst, kst + kn) in arrival order
+        uint64_t mk[SK_B / 64];
+        uint32_t kn = 0u;
 #pragma unroll
-        for (int i = 0; i < EPL; i++) {
-            const int64_t e = s0 + (int64_t)w * (64 * EPL) + 64 * i + lane;
-            const bool v = e < ce;
-            const int32_t k = kk[i];
-            if (v && k >= P.nkeys) flag |= SHB_F_KEY;
-            const bool own = v && k >= 0 && k < P.nkeys && (k & (G - 1)) == g;
-            const int64_t dt = tt[i] - tb;
-            if (v && (dt < 0 || dt > 65535)) flag |= SHB_F_TS;
+        for (int j = 0; j < SK_B / 64; j++) {
+            const bool act = fb + (uint32_t)(j * 64 + lane) < fe;
+            const uint32_t kk = rw[j] & kmask;
+            uint64_t m = __ballot(act);
+            for (int bb = 0; bb < kb; bb++) {
+                const uint64_t bm = __ballot(act && ((kk >> bb) & 1u));
+                m &= ((lane >> bb) & 1) ? bm : ~bm;
+            }
+            mk[j] = owner ? m : 0ull;
+            kn += (uint32_t)__popcll(mk[j]);
+        }
+        const uint32_t kst = shw_incl_scan(kn) - kn;
+        uint32_t krun = kst;  // the owner's next sorted position
+#pragma unroll
+        for (int j = 0; j < SK_B / 64; j++) {
+            const bool act = fb + (uint32_t)(j * 64 + lane) < fe;
+            const int kk = (int)(rw[j] & kmask);
+            const uint32_t base = (uint32_t)__shfl((int)krun, kk);
+            const uint32_t plo = (uint32_t)__shfl((int)(uint32_t)mk[j], kk);
+            const uint32_t phi = (uint32_t)__shfl((int)(uint32_t)(mk[j] >> 32), kk);
+            const uint64_t peers = ((uint64_t)phi << 32) | plo;
+            if (act) {
+                const uint32_t d = base + (uint32_t)__popcll(peers & lt);
+                const uint32_t xr = rx[j];
+                const bool nan = F32 && (xr & 0x7FFFFFFFu) > 0x7F800000u;
+                const bool open = !nan && sk_open(K, xr);
+                L.u.sw[d] = make_uint2(rw[j], sk_key<F32>(xr) ^ K.kflip);
+                L.so[d] = (uint16_t)((j * 64 + lane) | (open ? 0x100 : 0) | (nan ? 0x200 : 0));
+                L.bg[j * 64 + lane] = rg[j];
+            }
+            krun += (uint32_t)__popcll(mk[j]);
+        }
+        sk_wave_sync();
+        SK_TICK(2);
+        if (fb + SK_B < nev) issue(fb + SK_B);
+        SK_TICK(1);
+        // the owners run their events (the next entry's words read a step ahead),
+        // as many steps as the busiest key has events
+        uint32_t nmax = kn;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) nmax = max(nmax, (uint32_t)__shfl_xor((int)nmax, d));
+        const uint32_t kl = kn ? kst + kn - 1u : kst;  // the owner's last entry
+        uint2 vn = L.u.sw[kst < SK_B ? kst : SK_B - 1];
+        uint32_t on = L.so[kst < SK_B ? kst : SK_B - 1];
+        for (uint32_t s = 0; s < nmax; s++) {
+            const uint2 v = vn;
+            uint32_t o = on;
             {
-                // timestamps never go back: the previous event is lane - 1, the last of
-                // the previous row, or (row 0, lane 0) the previous wave's last event
-                const int64_t up = __shfl(tt[i], lane > 0 ? lane - 1 : 0);
-                const int64_t pv = lane > 0 ? up : (i > 0 ? __shfl(tt[i > 0 ? i - 1 : 0], 63) : tpr);
-                if (v && pv > tt[i]) flag |= SHB_F_MONO;
+                const uint32_t sx = kst + s + 1u < kl ? kst + s + 1u : kl;
+                vn = L.u.sw[sx];
+                on = L.so[sx];
             }
-            const uint32_t lk = own ? (uint32_t)k >> P.gshift : 0u;
-            const int b = (int)(lk & 15u);
-            bn[i] = own ? b : -1;
-            // a NaN consumer takes nothing and never opens a partial
-            const bool xnan = f32 && (xx[i] & 0x7FFFFFFFu) > 0x7F800000u;
-            bool open = false;
-            if (own && !xnan) {
-                if (P.fast_open) open = sk_open_fast(P, xx[i], la[i]);
-                else open = (om[i] >> lane) & 1ull;
-            }
-            qa[i] = sk_key(xx[i], f32) ^ P.kflip;
-            qb[i] = (uint32_t)dt | ((lk >> 4) << 16) | (xnan ? 0x40000000u : 0u) | (open ? 0x80000000u : 0u);
-            qc[i] = (uint32_t)(e - s0);
-            if (PASS == 1 && emit && v && !(k >= 0 && k < P.nkeys) && g == 0) P.cnt[e] = 0;
-            // rank among this wave's earlier events of the same owner wave
-            uint64_t peers = __ballot(own);
-#pragma unroll
-            for (int bb = 0; bb < 4; bb++) {
-                const bool bit = (b >> bb) & 1;
-                const uint64_t m = __ballot(own && bit);
-                peers &= bit ? m : ~m;
-            }
-            const uint32_t r = (uint32_t)__popcll(peers & lt);
-            uint32_t old = 0u;
-            if (own && r == 0) old = atomicAdd(&L.wcnt[w][b], (uint32_t)__popcll(peers));
-            const int ld = own ? (int)__ffsll((unsigned long long)peers) - 1 : lane;
-            rk[i] = (uint32_t)__shfl((int)old, ld) + r;
-            if (PASS == 2) {
-                // rows of the events before this one in the wave's run (arrival order)
-                const uint32_t ci = emit ? cc[i] : 0u;
-                const uint32_t inc = shw_incl_scan(ci);
-                rr[i] = rcarry + inc - ci;
-                rcarry += shw_last(inc);
-            }
-        }
-        if (flag) atomicOr(P.flag, (int)flag);
-        if (PASS == 2 && lane == 0) L.wrow[w] = rcarry;
-        if (P.prof) {
-            const unsigned long long t = clock64();
-            pc_prod += t - pc0;
-            pc0 = t;
-        }
-        __syncthreads();  // A: queue counts and row totals of the sub-tile are in
-        if (PASS == 1 && threadIdx.x == 0 && prev_sub >= 0) {
-            uint32_t s = 0;
-#pragma unroll
-            for (int q = 0; q < SK_NW; q++) s += L.wsum[q];
-            if (s) atomicAdd(&P.ttot[prev_sub], s);
-        }
-        prev_sub = emit ? s0 / SUB : -1;
-        // queue positions: owner b's region, after the earlier producer waves' events
-        {
-            uint32_t pb = 0;
-            if (lane < SK_NW)
-                for (int q = 0; q < w; q++) pb += L.wcnt[q][lane];
-            uint32_t rbase = 0;
-            if (PASS == 2)
-                for (int q = 0; q < w; q++) rbase += L.wrow[q];
-#pragma unroll
-            for (int i = 0; i < EPL; i++) {
-                const int b = bn[i];
-                const uint32_t pos = (uint32_t)__shfl((int)pb, b < 0 ? 0 : b) + rk[i];
-                if (b >= 0) {
-                    if (pos >= SK_CAPW) {
-                        atomicOr(P.flag, SHK_F_QUEUE);
-                    } else {
-                        const int qi = b * SK_CAPW + (int)pos;
-                        L.qx[qi] = qa[i];
-                        L.q1[qi] = qb[i];
-                        uint32_t q2 = qc[i];
-                        if (PASS == 2) {
-                            const uint32_t ro = rbase + rr[i];
-                            if (ro >= SK_ROWS_LIM) atomicOr(P.flag, SHK_F_ROWS);
-                            q2 |= ro << SK_OFF_BITS;
-                        }
-                        L.q2[qi] = q2;
-                    }
+            if (s < kn) {
+                // speculative: the second entries from the bottom and from the top
+                const uint32_t tsec = L.t[(o_bo + 1u) & (SK_D - 1)][lane];
+                const uint32_t ysec = L.y[(o_bo + o_c - 2u) & (SK_D - 1)][lane];
+                const uint32_t w = v.x, x = v.y;
+                const bool open = (o & 0x100u) != 0u, nan = (o & 0x200u) != 0u;
+                o &= 0xFFu;
+                const bool emit = o >= ethr;
+                const uint32_t now = w >> kb;
+                flag |= (emit && now < hlim) ? (uint32_t)SHB_F_HALO : 0u;
+                flag |= now < o_last ? (uint32_t)SHB_F_MONO : 0u;
+                o_last = now;
+                const uint32_t cx = x == K.zk1 ? K.zk0 : x;
+                // expiry from the bottom (spilled entries are older still): one entry
+                // by the speculative read, more (rare) by a walk
+                const bool ex1 = o_c > 0u && now - o_tbot > W;
+                o_sc = ex1 ? 0u : o_sc;
+                o_bo = ex1 ? ((o_bo + 1u) & (SK_D - 1)) : o_bo;
+                o_tbot = ex1 ? tsec : o_tbot;
+                o_c = ex1 ? o_c - 1u : o_c;
+                if (ex1 && o_c > 0u && now - o_tbot > W) {
+                    do {
+                        o_bo = (o_bo + 1u) & (SK_D - 1);
+                        o_tbot = L.t[o_bo][lane];
+                    } while (--o_c > 0u && now - o_tbot > W);
                 }
-            }
-        }
-        // this wave's queue length (sum over the producer waves)
-        uint32_t nq = lane < SK_NW ? L.wcnt[lane][w] : 0u;
-        nq = shw_last(shw_incl_scan(nq));
-        if (nq > SK_CAPW) nq = SK_CAPW;
-        const uint64_t rows0 = (PASS == 2 && emit) ? (uint64_t)rows_next : 0ull;
-        __syncthreads();  // B: queues complete
-        if (P.prof) {
-            const unsigned long long t = clock64();
-            pc_queue += t - pc0;
-            pc0 = t;
-        }
-        if (s0 + SUB < ce) load(s0 + SUB);  // next sub-tile in flight during the queue
-        // ---- owner: the wave's queue in batches of 64, the k-th event of a key in round k
-        uint32_t msum = 0;
-        n_ev += nq;
-        for (uint32_t base = 0; base < nq; base += 64) {
-            const uint32_t idx = base + (uint32_t)lane;
-            const bool act = idx < nq;
-            const int qi = w * SK_CAPW + (int)(act ? idx : 0u);
-            const uint32_t x = L.qx[qi], a1 = L.q1[qi], a2 = L.q2[qi];
-            const uint32_t wl = (a1 >> 16) & 0xFFu;
-            uint64_t peers = __ballot(act);
-#pragma unroll
-            for (int bb = 0; bb < 8; bb++) {
-                const bool bit = (wl >> bb) & 1u;
-                const uint64_t m = __ballot(act && bit);
-                peers &= bit ? m : ~m;
-            }
-            const uint32_t rank = (uint32_t)__popcll(peers & lt);
-            const int64_t j = s0 + (int64_t)(a2 & ((1u << SK_OFF_BITS) - 1u));
-            const uint32_t lk = (wl << 4) | (uint32_t)w;
-            // consumer-side select values, loaded before the rounds
-            int64_t v1[NO > 0 ? NO : 1];
-            if (PASS == 2 && NO > 0) {
-                const int32_t key = (int32_t)((lk << P.gshift) | (uint32_t)g);
-#pragma unroll
-                for (int o = 0; o < (NO > 0 ? NO : 1); o++) {
-                    v1[o] = 0;
-                    if (O.kind[o] != 1 || !act || !emit) continue;
-                    if (O.src[o] == P.xcol) v1[o] = sk_yraw(sk_unkey(x ^ P.kflip, f32), O.type[o]);
-                    else if (O.src[o] == (const void*)P.keys) v1[o] = (int64_t)key;
-                    else v1[o] = bk_raw(O.src[o], j, O.type[o]);
-                }
-            }
-            n_batch++;
-            for (uint32_t rd = 0; __ballot(act && rank >= rd) != 0ull; rd++) {
-                n_round++;
-                if (!(act && rank == rd)) continue;
-                // the key's ring: all entries at once (one LDS latency)
-                const uint32_t hw = L.h[lk];
-                uint32_t y[SK_D];
-                uint32_t tv[SK_D];
-#pragma unroll
-                for (int s = 0; s < SK_D; s++) {
-                    y[s] = L.y[s][lk];
-                    tv[s] = L.t[s][lk];
-                }
-                uint32_t b = hw & 7u, n = (hw >> 3) & 15u, sc = hw >> 7;
-                const uint32_t now = a1 & 0xFFFFu;
-                const uint32_t full = n ? ((1u << n) - 1u) : 0u;
-                uint32_t live = ((full << b) | (full >> (SK_D - b))) & 0xFFu;
-                // expiry from the bottom (creation order is time order)
-                uint32_t E = 0;
-#pragma unroll
-                for (int s = 0; s < SK_D; s++)
-                    E |= (((live >> s) & 1u) && ((now - tv[s]) & 0xFFFFu) > W) ? (1u << s) : 0u;
-                if (E) {
-                    const uint32_t ne = (uint32_t)__popc(E);
-                    b = (b + ne) & 7u;
-                    n -= ne;
-                    live &= ~E;
-                    sc = 0;  // spilled entries are older than an expired one
-                }
-                // the entries x beats: the top of the stack (order keys; -0.0 as +0.0)
-                const uint32_t cx = x == P.zk1 ? P.zk0 : x;
-                if (a1 & 0x40000000u) live = 0;  // a NaN consumer
-                uint32_t K = 0;
-#pragma unroll
-                for (int s = 0; s < SK_D; s++) {
-                    const uint32_t cy = y[s] == P.zk1 ? P.zk0 : y[s];
-                    K |= (((live >> s) & 1u) && (cx > cy || (P.ge && cx == cy))) ? (1u << s) : 0u;
-                }
-                const uint32_t k = (uint32_t)__popc(K);
-                n -= k;
-                // below an emptied ring: the spilled entries (HBM)
-                uint64_t* spl = P.spill + ((uint64_t)blockIdx.x * (uint64_t)P.kpw + lk) * (uint64_t)P.spill_cap;
-                uint32_t ks = 0;  // spilled entries popped (rows); `sc` may also drop to 0 by expiry
-                uint32_t slo = sc;  // the popped spilled entries are slots [slo, slo + ks)
-                if (n == 0 && sc > 0 && !(a1 & 0x40000000u)) {
-                    while (sc > 0) {
-                        const uint64_t ev = sk_spill_load(spl + sc - 1);
-                        if (((now - (uint32_t)(ev >> 32)) & 0xFFFFu) > W) {
-                            sc = 0;  // this one and every older spilled entry expired
+                // the entries x beats: the top of the stack (top and second in registers)
+                const uint32_t ytop = o_ytop;
+                const uint32_t c0 = ytop == K.zk1 ? K.zk0 : ytop;
+                const uint32_t c1 = ysec == K.zk1 ? K.zk0 : ysec;
+                const bool b0 = !nan && o_c > 0u && (cx > c0 || (K.ge && cx == c0));
+                const bool b1 = b0 && o_c > 1u && (cx > c1 || (K.ge && cx == c1));
+                uint32_t kp = (b0 ? 1u : 0u) + (b1 ? 1u : 0u);
+                o_ytop = (b0 && !b1 && o_c > 1u) ? ysec : o_ytop;
+                if (b1 && o_c > 2u) {
+                    for (;;) {
+                        const uint32_t yv = L.y[(o_bo + o_c - 1u - kp) & (SK_D - 1)][lane];
+                        const uint32_t cy = yv == K.zk1 ? K.zk0 : yv;
+                        if (!(cx > cy || (K.ge && cx == cy))) {
+                            o_ytop = yv;  // the new top
                             break;
                         }
-                        const uint32_t cy = (uint32_t)ev == P.zk1 ? P.zk0 : (uint32_t)ev;
-                        if (!(cx > cy || (P.ge && cx == cy))) break;
-                        sc--;
+                        if (++kp == o_c) break;
+                    }
+                }
+                // below an emptied ring: the spilled entries
+                uint32_t ks = 0u, slo = o_sc;
+                if (kp == o_c && o_sc > 0u && !nan) {
+                    while (o_sc > 0u) {
+                        const uint64_t ev = sk_spill_load(spl + o_sc - 1u);
+                        if (now - (uint32_t)(ev >> 32) > W) {
+                            o_sc = 0u;  // it and every older spilled entry expired
+                            break;
+                        }
+                        const uint32_t cy = (uint32_t)ev == K.zk1 ? K.zk0 : (uint32_t)ev;
+                        if (!(cx > cy || (K.ge && cx == cy))) break;
+                        o_sc--;
                         ks++;
-                        slo = sc;
+                        slo = o_sc;
                     }
                 }
-                const uint32_t total = ks + k;
-                if (PASS == 1) {
-                    if (emit) {
-                        if (total > 255u) atomicOr(P.flag, SHB_F_COUNT);
-                        P.cnt[j] = (uint8_t)(total > 255u ? 255u : total);
-                        msum += total;
-                    }
-                } else if (emit && total) {
-                    // rows in creation order: the spilled entries, then the ring's
-                    const int64_t r0 = (int64_t)rows0 + (int64_t)(a2 >> SK_OFF_BITS);
-                    const uint64_t seq = seq_base + (uint64_t)j;
-                    const int32_t key = (int32_t)((lk << P.gshift) | (uint32_t)g);
-                    auto put = [&](int64_t row, uint32_t yv) {
-                        if (row >= out_cap) return;  // the host reports SH_E_MORE
-                        if (NO > 0) {
-                            int64_t v[NO > 0 ? NO : 1];
-#pragma unroll
-                            for (int o = 0; o < (NO > 0 ? NO : 1); o++)
-                                v[o] = O.kind[o] == SHB_OUT_KIND_Y ? sk_yraw(sk_unkey(yv ^ P.kflip, f32), O.type[o])
-                                                                   : v1[o];
-                            bk_store<MODE, NO>(OC, row, v, seq, out_seq, out_vals);
-                        } else {
-                            const int no = O.n_out;
-                            if (MODE == SHB_OUT_PACKED) {
-                                uint32_t* rp = (uint32_t*)OC.rows + row * OC.rw;
-                                rp[0] = (uint32_t)seq;
-                                rp[1] = (uint32_t)(seq >> 32);
-                                for (int q = 2; q < OC.rw; q++) rp[q] = 0u;
-                            } else if (out_seq) {
-                                out_seq[row] = seq;
+                const uint32_t tot = emit ? ks + kp : 0u;
+                flag |= tot > 255u ? (uint32_t)SHB_F_COUNT : 0u;
+                L.cntb[o] = (uint8_t)(tot > 255u ? 255u : tot);
+                // stage the values in creation order: spilled ones, then the ring's
+                if (K.want_ms && tot > 0u) {
+                    const uint32_t sb =
+                        __hip_atomic_fetch_add(&L.sn, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    if (sb + tot > SK_STG) {
+                        flag |= SHB_F_COUNT;
+                    } else {
+                        const uint32_t r0 = sb + ks;
+                        if (kp) {
+                            L.stv[r0 + kp - 1u] = ytop;
+                            L.stt[r0 + kp - 1u] = (uint16_t)(o | ((ks + kp - 1u) << 8));
+                        }
+                        if (kp >= 2u) {
+                            L.stv[r0 + kp - 2u] = ysec;
+                            L.stt[r0 + kp - 2u] = (uint16_t)(o | ((ks + kp - 2u) << 8));
+                        }
+                        if (kp >= 3u || ks) {
+                            for (uint32_t q = 0; q < ks; q++) {
+                                L.stv[sb + q] = (uint32_t)sk_spill_load(spl + slo + q);
+                                L.stt[sb + q] = (uint16_t)(o | (q << 8));
                             }
-                            for (int o = 0; o < no; o++) {
-                                int64_t vv;
-                                if (O.kind[o] == SHB_OUT_KIND_Y) vv = sk_yraw(sk_unkey(yv ^ P.kflip, f32), O.type[o]);
-                                else if (O.src[o] == P.xcol) vv = sk_yraw(sk_unkey(x ^ P.kflip, f32), O.type[o]);
-                                else if (O.src[o] == (const void*)P.keys) vv = (int64_t)key;
-                                else vv = bk_raw(O.src[o], j, O.type[o]);
-                                if (MODE == SHB_OUT_PACKED) {
-                                    uint32_t* rp = (uint32_t*)OC.rows + row * OC.rw + OC.woff[o];
-                                    rp[0] = OC.colw[o] == 1 ? (uint32_t)(uint8_t)vv : (uint32_t)vv;
-                                    if (OC.colw[o] == 8) rp[1] = (uint32_t)((uint64_t)vv >> 32);
-                                } else if (MODE == SHB_OUT_COLS) {
-                                    bk_put(OC.cols[o], OC.colw[o], row, vv);
-                                } else if (out_vals) {
-                                    out_vals[row * no + o] = vv;
-                                }
+                            for (uint32_t q = 0; q + 2u < kp; q++) {
+                                L.stv[r0 + q] = L.y[(o_bo + o_c - kp + q) & (SK_D - 1)][lane];
+                                L.stt[r0 + q] = (uint16_t)(o | ((ks + q) << 8));
                             }
                         }
-                    };
-                    for (uint32_t q = 0; q < ks; q++) put(r0 + q, (uint32_t)sk_spill_load(spl + slo + q));
-                    uint32_t Km = K;
-                    while (Km) {
-                        const uint32_t s = (uint32_t)__ffs(Km) - 1u;
-                        Km &= Km - 1u;
-                        uint32_t yv = y[0];
-#pragma unroll
-                        for (int u = 1; u < SK_D; u++) yv = s == (uint32_t)u ? y[u] : yv;
-                        // logical index above the new top
-                        const uint32_t li = (s - b) & 7u;
-                        put(r0 + (int64_t)ks + (int64_t)(li - n), yv);
                     }
                 }
+                o_c -= kp;
                 // push: a full ring spills its bottom entry first
-                if (a1 >> 31) {
-                    if (n == SK_D) {
-                        if (sc > 0 && ((now - (uint32_t)L.spt[lk]) & 0xFFFFu) > W) sc = 0;
-                        if (sc >= (uint32_t)P.spill_cap) {
-                            atomicOr(P.flag, SHK_F_SPILL);
+                if (open) {
+                    if (o_c == SK_D) {
+                        if (o_sc > 0u && now - o_spt > W) o_sc = 0u;
+                        if (o_sc >= (uint32_t)K.spill_cap) {
+                            flag |= SHK_F_SPILL;
                         } else {
-                            uint32_t yb = y[0], tbb = tv[0];
-#pragma unroll
-                            for (int u = 1; u < SK_D; u++) {
-                                yb = b == (uint32_t)u ? y[u] : yb;
-                                tbb = b == (uint32_t)u ? tv[u] : tbb;
-                            }
-                            sk_spill_store(spl + sc, (uint64_t)yb | ((uint64_t)tbb << 32));
-                            sc++;
-                            L.spt[lk] = (uint16_t)tbb;
+                            sk_spill_store(spl + o_sc, (uint64_t)L.y[o_bo][lane] | ((uint64_t)o_tbot << 32));
+                            o_spt = o_tbot;
+                            o_sc++;
                         }
-                        b = (b + 1u) & 7u;
-                        n = SK_D - 1;
+                        o_bo = (o_bo + 1u) & (SK_D - 1);
+                        o_c = SK_D - 1;
+                        o_tbot = L.t[o_bo][lane];
                     }
-                    const uint32_t s = (b + n) & 7u;
-                    L.y[s][lk] = x;
-                    L.t[s][lk] = (uint16_t)now;
-                    n++;
+                    const uint32_t sl = (o_bo + o_c) & (SK_D - 1);
+                    L.y[sl][lane] = x;
+                    L.t[sl][lane] = now;
+                    o_tbot = o_c == 0u ? now : o_tbot;
+                    o_c++;
+                    o_ytop = x;
                 }
-                L.h[lk] = (uint16_t)(b | (n << 3) | (sc << 7));
             }
         }
-        if (PASS == 1) {
-            msum = shw_last(shw_incl_scan(msum));
-            if (lane == 0) L.wsum[w] = emit ? msum : 0u;
-        }
-        if (P.prof) pc_proc += clock64() - pc0;
-    }
-    if (P.prof && lane == 0) {
-        // clock ticks per phase summed over the waves: producer, queue hand-off
-        // (both barriers' waits included), owner processing
-        atomicAdd(P.prof + 0, pc_prod);
-        atomicAdd(P.prof + 1, pc_queue);
-        atomicAdd(P.prof + 2, pc_proc);
-        atomicAdd(P.prof + 3, n_batch);
-        atomicAdd(P.prof + 4, n_round);
-        atomicAdd(P.prof + 5, n_ev);
-    }
-    if (PASS == 1) {
-        __syncthreads();
-        if (threadIdx.x == 0 && prev_sub >= 0) {
-            uint32_t s = 0;
+        if (prof) pr[7] += nmax;
+        sk_wave_sync();
+        SK_TICK(4);
+        if (prof) pr[6]++;
+        // lanes over events: counts, positions, each tile's segment
 #pragma unroll
-            for (int q = 0; q < SK_NW; q++) s += L.wsum[q];
-            if (s) atomicAdd(&P.ttot[prev_sub], s);
+        for (int j = 0; j < SK_B / 64; j++) {
+            const uint32_t e = (uint32_t)(j * 64 + lane);
+            const bool act = fb + e < fe;
+            const uint32_t tot = act ? (uint32_t)L.cntb[e] : 0u;
+            const uint32_t g = act ? L.bg[e] : 0u;
+            const bool emit = act && e >= ethr;
+            const uint32_t incm = shw_incl_scan(tot);
+            const uint32_t excl = incm - tot;
+            L.u.pre[e] = mpos + excl;
+            if (emit) P.cnt[g] = (uint8_t)tot;
+            // per tile of the block: its first lane records the segment's position
+            // (the tile's first event of the bucket) and adds the segment's matches
+            const uint32_t T = g >> SHB_TILE_SHIFT;
+            const uint32_t Tp = (uint32_t)__shfl((int)T, lane > 0 ? lane - 1 : 0);
+            const bool seg = emit && (lane == 0 || T != Tp);
+            const uint64_t fm = __ballot(seg);
+            const uint64_t after = lane == 63 ? 0ull : fm & ~((2ull << lane) - 1ull);
+            const int lastl = after ? (int)__builtin_ctzll(after) - 1 : 63;
+            const uint32_t tend = (uint32_t)__shfl((int)incm, lastl);
+            if (seg) {
+                if (lane != 0 || T != prevT) P.mstart[(int64_t)T * SHB_NB + b] = mpos + excl;
+                if (tend > excl) atomicAdd(&P.ttot[T], tend - excl);
+            }
+            if (fm) prevT = (uint32_t)__shfl((int)T, 63 - __builtin_clzll(fm));
+            mpos += shw_last(incm);
         }
+        sk_wave_sync();
+        // lanes over the staged values: into the match stream
+        if (K.want_ms) {
+            const uint32_t nst = L.sn < SK_STG ? L.sn : SK_STG;
+            for (uint32_t s = (uint32_t)lane; s < nst; s += 64) {
+                const uint32_t tg = L.stt[s];
+                ms[L.u.pre[tg & 0xFFu] + (tg >> 8)] = sk_unkey<F32>(L.stv[s] ^ K.kflip);
+            }
+        }
+        sk_wave_sync();
+        if (lane == 0) L.sn = 0u;
+        SK_TICK(5);
     }
+#undef SK_TICK
+    if (prof && lane == 0)
+        for (int i = 0; i < 8; i++) atomicAdd(P.prof + i, pr[i]);
+    if (flag) atomicOr(P.flag, (int)flag);
 }
 
-static int sk_ok() { return hipGetLastError() == hipSuccess ? 0 : -3; }
-
-static unsigned sk_grid(const shk_plan* P) { return 8u * (unsigned)P->cpx << P->gshift; }
-
-extern "C" int shk_max_keys(void) { return SK_KPW; }
-
-extern "C" int shk_open_bits(const shk_plan* P, void* stream) {
-    if (!P->omask) return -1;
-    hipLaunchKernelGGL(k_stk_open, dim3((unsigned)((P->n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *P);
-    return sk_ok();
+extern "C" int shk_match(const shb_plan* P, const shk_params* K, void* stream) {
+    if (P->kb > 6 || P->n_staged < 1 || P->st_width[0] != 4 || K->run_tiles < 1 ||
+        K->run_tiles > SK_RUNT - SHB_HMAX || K->n_terms < 0 || K->n_terms > SHK_MAX_TERMS || K->spill_cap < 1 ||
+        (K->want_ms && P->ms_width[0] != 4))
+        return -1;
+    const int runs = (P->nt + K->run_tiles - 1) / K->run_tiles;
+    // 64 workgroups of 4 buckets per run: XCD x holds bucket groups 8x .. 8x + 7
+    const unsigned grid = (unsigned)runs * (SHB_NB / SK_WPB);
+    if (K->dom == DOM_F32)
+        hipLaunchKernelGGL(k_bk_stk<true>, dim3(grid), dim3(64 * SK_WPB), 0, (hipStream_t)stream, *P, *K);
+    else
+        hipLaunchKernelGGL(k_bk_stk<false>, dim3(grid), dim3(64 * SK_WPB), 0, (hipStream_t)stream, *P, *K);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-extern "C" int shk_count(const shk_plan* P, void* stream) {
-    hipStream_t st = (hipStream_t)stream;
-    if (P->kpw > SK_KPW || P->gshift < 1 || P->gshift > 3) return -1;
-    const shb_out O{};
-    const shb_cols OC{};
-    switch (P->gshift) {
-        case 1: hipLaunchKernelGGL((k_stk<1, 2, SHB_OUT_RAW, 0>), dim3(sk_grid(P)), dim3(SK_TPB), 0, st, *P, O, OC, 0ull,
-                                   nullptr, nullptr, 0ll); break;
-        case 2: hipLaunchKernelGGL((k_stk<1, 4, SHB_OUT_RAW, 0>), dim3(sk_grid(P)), dim3(SK_TPB), 0, st, *P, O, OC, 0ull,
-                                   nullptr, nullptr, 0ll); break;
-        default: hipLaunchKernelGGL((k_stk<1, 8, SHB_OUT_RAW, 0>), dim3(sk_grid(P)), dim3(SK_TPB), 0, st, *P, O, OC,
-                                    0ull, nullptr, nullptr, 0ll); break;
-    }
-    return sk_ok();
-}
-
-template <int EPL, int MODE, int NO>
-static void sk_emit_launch(const shk_plan* P, const shb_out* O, const shb_cols& OC, uint64_t seq_base,
-                           uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, hipStream_t st) {
-    hipLaunchKernelGGL((k_stk<2, EPL, MODE, NO>), dim3(sk_grid(P)), dim3(SK_TPB), 0, st, *P, *O, OC, seq_base, out_seq,
-                       out_vals, out_cap);
-}
-
-template <int EPL>
-static void sk_emit_mode(const shk_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base,
-                         uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, hipStream_t st) {
-    // the packed four-value row of C2 unrolled; every other layout by descriptors
-    if (OC && OC->use == SHB_OUT_PACKED) {
-        if (O->n_out == 4) sk_emit_launch<EPL, SHB_OUT_PACKED, 4>(P, O, *OC, seq_base, out_seq, out_vals, out_cap, st);
-        else sk_emit_launch<EPL, SHB_OUT_PACKED, 0>(P, O, *OC, seq_base, out_seq, out_vals, out_cap, st);
-    } else if (OC && OC->use == SHB_OUT_COLS) {
-        sk_emit_launch<EPL, SHB_OUT_COLS, 0>(P, O, *OC, seq_base, out_seq, out_vals, out_cap, st);
-    } else if (O->n_out == 4) {
-        sk_emit_launch<EPL, SHB_OUT_RAW, 4>(P, O, shb_cols{}, seq_base, out_seq, out_vals, out_cap, st);
-    } else {
-        sk_emit_launch<EPL, SHB_OUT_RAW, 0>(P, O, shb_cols{}, seq_base, out_seq, out_vals, out_cap, st);
-    }
-}
-
-extern "C" int shk_emit(const shk_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base,
-                        uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
-    hipStream_t st = (hipStream_t)stream;
-    if (P->kpw > SK_KPW || P->gshift < 1 || P->gshift > 3) return -1;
-    if (OC && OC->use == SHB_OUT_PACKED && (OC->rw % 4 || OC->rw > 2 + 2 * SHB_MAX_OUT + 2)) return -1;
-    switch (P->gshift) {
-        case 1: sk_emit_mode<2>(P, O, OC, seq_base, out_seq, out_vals, out_cap, st); break;
-        case 2: sk_emit_mode<4>(P, O, OC, seq_base, out_seq, out_vals, out_cap, st); break;
-        default: sk_emit_mode<8>(P, O, OC, seq_base, out_seq, out_vals, out_cap, st); break;
-    }
-    return sk_ok();
-}
+extern "C" int shk_max_run_tiles(void) { return SK_RUNT - SHB_HMAX; }
+extern "C" int shk_spill_keys(void) { return SK_KEYS * SK_WPB; }

@@ -28,18 +28,21 @@ def _device():
 
 def _run(app, strings, ts, cols, keys, nk, columns=False, batch_events=4096, engine=None):
     """columns: typed output columns (d_out_cols), "packed": SH_OUT_PACKED rows;
-    both returned as raw rows for comparison. engine="bucket": the stack engine
-    (sh_stack.hip) is switched off for the call (SH_DISABLE_STACK)"""
-    old = os.environ.get("SH_DISABLE_STACK")
-    if engine == "bucket":
-        os.environ["SH_DISABLE_STACK"] = "1"
+    both returned as raw rows for comparison. engine="stack": the bucketed
+    engine's stack matcher (sh_stack.hip) for the call (SH_STACK=1), else the
+    default sort-and-walk matcher"""
+    old = os.environ.get("SH_STACK")
+    if engine == "stack":
+        os.environ["SH_STACK"] = "1"
+    else:
+        os.environ.pop("SH_STACK", None)
     try:
         return _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events)
     finally:
         if old is None:
-            os.environ.pop("SH_DISABLE_STACK", None)
+            os.environ.pop("SH_STACK", None)
         else:
-            os.environ["SH_DISABLE_STACK"] = old
+            os.environ["SH_STACK"] = old
 
 
 def _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events):
@@ -72,9 +75,9 @@ def _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events):
     return res, status, err
 
 
-@pytest.mark.parametrize("engine,expect", [("bucket", 1), (None, 2)])
+@pytest.mark.parametrize("engine,expect", [(None, 1), ("stack", 2)])
 def test_c2_bucket_vs_oracle(engine, expect):
-    """status 1: the bucketed engine (stack engine off), 2: the stack engine"""
+    """status 1: the sort-and-walk matcher (default), 2: the stack matcher"""
     n, nk = 400_000, 2_000
     ts, k, p, v = synth.stock_stream(n, nk, 100)
     ca = compiler.compile_app(synth.C2_QUERY)
@@ -87,9 +90,9 @@ def test_c2_bucket_vs_oracle(engine, expect):
 
 
 @pytest.mark.parametrize("n,nk,bucketed,columns,engine", [
-    (10_000_000, 10_000, 1, False, "bucket"), (10_000_000, 10_000, 2, False, None),
-    (100_000_000, 10_000, 2, "packed", None), (100_000_000, 10_000, 1, "packed", "bucket"),
-    (100_000_000, 10_000, 2, True, None), (3_000_000, 60_000, 1, False, None),
+    (10_000_000, 10_000, 1, False, None), (10_000_000, 10_000, 2, False, "stack"),
+    (100_000_000, 10_000, 2, "packed", "stack"), (100_000_000, 10_000, 1, "packed", None),
+    (100_000_000, 10_000, 1, True, None), (3_000_000, 60_000, 1, False, "stack"),
     (3_000_000, 60_000, 1, True, None), (3_000_000, 60_000, 1, "packed", None)])
 def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed, columns, engine):
     """60k symbols at 100 ev/ms: a key's previous event is often more than a
