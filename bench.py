@@ -60,7 +60,13 @@ def parse():
     ap.add_argument("--c4-calls", type=int, default=0, help="c4: send only the first N calls (profiling; 0 = all)")
     ap.add_argument("--c4-every", action="store_true", help="c4: the `every (e1=Login and e2=Txn) -> ...` variant")
     ap.add_argument("--rules", type=int, default=1000, help="c5: rule count")
+    ap.add_argument("--strong", action="store_true",
+                    help="N > 1: ONE stream over all ranks (c2 / c3 / c5: key-routed RCCL all-to-all + row return "
+                         "+ k-way merge; c4: key-sharded streaming with gloo coordination). Default: every GPU "
+                         "matches its own partition of the key space (its own stream over its own keys, no "
+                         "data-path collective; rank 0's stream is the canonical one), 'scaling': 'weak'")
     args = ap.parse_args()
+    args.seed_offset = 0  # (rank r of a weak-scaling run: its own partition's stream)
     if args.config == "c1":
         # BASELINE.json configs[0]: 10M ticks, 100 symbols, R = 1 ev/ms, no partition
         if args.events == 100_000_000:
@@ -92,8 +98,9 @@ def workload(args):
     (one stream: at N > 1 the ranks split it by key, or replicate it for C1)."""
     from siddhi_amd import compiler, synth
     n, K = args.events, args.keys
+    so = args.seed_offset
     if args.config == "c5":
-        ts, card, amount, merchant = synth.txn_stream(n, K, args.rate, seed=synth.SEED + 5)
+        ts, card, amount, merchant = synth.txn_stream(n, K, args.rate, seed=synth.SEED + 5 + so)
         rules = synth.c5_rules(args.rules)
         text = synth.c5_query(rules)
         strings = compiler.StringDict()
@@ -120,7 +127,7 @@ def workload(args):
             key_name="cards_per_gpu", bytes_note="event: ts 8 + card 4 + amount 4 + merchant 4 = 20 B; "
             "match: seq 8 + query 4 + card 4 + amount 4 = 20 B")
     if args.config == "c1":
-        ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=1, seed=synth.SEED + 1)
+        ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=1, seed=synth.SEED + 1 + so)
         compiled = compiler.compile_app(synth.C1_QUERY)
 
         def expected():
@@ -140,7 +147,7 @@ def workload(args):
                     bytes_note="event: ts 8 + symbol 4 + price 4 + volume 8 = 24 B; "
                                "match: seq 8 + symbol 4 + p1 4 + p2 4 + v2 8 = 28 B")
     ts, keys, price, vol = synth.stock_stream(n, K, args.rate, config_index=3 if args.config == "c3" else 2,
-                                              seed=synth.SEED + (3 if args.config == "c3" else 2))
+                                              seed=synth.SEED + (3 if args.config == "c3" else 2) + so)
     if args.config == "c3":
         compiled = compiler.compile_app(synth.C3_AGG_QUERY if args.agg else synth.C3_QUERY)
 
@@ -224,7 +231,11 @@ def main_c4(args, torch, dist, world, rank, dev):
     from siddhi_amd import compiler, synth
     from siddhi_amd._native import HipEngine
     log(f"generating c4 workload: {args.events} events, {args.keys} users, R = {args.rate} ev/ms")
-    blocks = synth.c4_spec_stream(args.events, args.keys, rate_per_ms=args.rate, batch=BATCH)
+    strong = world > 1 and args.strong
+    # weak scaling (default at N > 1): rank r streams its own partition of the users
+    # (its own stream, seed offset; rank 0's is the canonical one), no coordination
+    blocks = synth.c4_spec_stream(args.events, args.keys, rate_per_ms=args.rate, batch=BATCH,
+                                  seed=synth.SEED + 40 + (0 if strong else args.seed_offset))
     if args.c4_calls:
         blocks = blocks[:args.c4_calls]
     n = sum(len(b[1]) for b in blocks)
@@ -241,7 +252,7 @@ def main_c4(args, torch, dist, world, rank, dev):
         base = HipEngine(c)
         eng = base
         comm = None
-        if world > 1:
+        if strong:
             from siddhi_amd.shard_stream import ShardedStreamEngine, TorchGroupComm
             comm = TorchGroupComm(group)
             eng = ShardedStreamEngine(base, comm)
@@ -257,7 +268,7 @@ def main_c4(args, torch, dist, world, rank, dev):
         eng.advance_time(end)
         out = eng.drain()
         dt = time.perf_counter() - t
-        if world > 1:
+        if strong:
             eng.check()
         last["prof"] = base.host_profile()
         last["comm"] = (comm.seconds, comm.calls) if comm is not None else None
@@ -283,11 +294,12 @@ def main_c4(args, torch, dist, world, rank, dev):
         dist.all_reduce(dt_t[:1], op=dist.ReduceOp.MAX, group=group)
         dist.all_reduce(dt_t[1:], op=dist.ReduceOp.SUM, group=group)
     tot, m = float(dt_t[0].item()), int(dt_t[1].item())
-    value = n * args.steps / tot   # the one stream, all ranks
+    # strong: the one stream over all ranks; weak: every rank's own stream
+    value = (n if strong else n * world) * args.steps / tot
     # the ordered output vs the oracle's digest on the same stream (tests/golden/
     # c4_digest.json, tests/golden/make_c4_digest.py), when it holds this workload
     verified = None
-    if world == 1 and not args.c4_calls:
+    if (world == 1 or not strong) and not args.c4_calls:
         try:
             from c4_cases import c4_digest
             key = ("every" if args.c4_every else "default") + f"_{args.events}_{args.keys}"
@@ -335,19 +347,22 @@ def main_c4(args, torch, dist, world, rank, dev):
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "split_last_step": split,
-            "ms_per_step": tot * 1000.0 / args.steps, "higher_is_better": True, "scaling": "strong",
+            "ms_per_step": tot * 1000.0 / args.steps, "higher_is_better": True,
+            "scaling": "weak" if world > 1 and not strong else "strong",
             "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic", "nproc": os.cpu_count(),
             "ingest": {"path": "host buffers of every send(Event[]) call cross PCIe inside the timed step"},
             "config": {"workload": ("C4: " + ("every " if args.c4_every else "") + "(e1=Login and e2=Txn) -> not "
                                     "Logout for 5 sec, partition with (user of Login, user of Txn, user of "
                                     "Logout), @app:playback; Login 20% / Txn 60% / Logout 20%, calls of 4,096 "
                                     "per stream"),
-                       "events_total": n, "users": args.keys, "rate_ev_per_ms": args.rate,
+                       "events_total": n if strong else n * world, "events_per_gpu": n if not strong else None,
+                       "users": args.keys, "rate_ev_per_ms": args.rate,
                        "send_calls": len(blocks), "matches_total": int(m),
                        "path": "streaming C-ABI from host buffers (PCIe-inclusive)",
                        "parallelism": (f"key-sharded x{world}: events routed per call by user, due-timer "
                                        "candidates and scheduler-map history exchanged per time step (gloo)")
-                       if world > 1 else "one GPU"},
+                       if strong else (f"dp{world}: every GPU its own partition of the users (own stream), "
+                                       "no data-path collective" if world > 1 else "one GPU")},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8.0e12, "traffic": None,
                          "kernel": "whole streaming step (wall clock, PCIe and per-call launches included): "
@@ -439,7 +454,9 @@ def main_sharded(args, torch, dist, world, rank, dev):
 
     def matcher(t, k, c, nk, run=None):
         r = runner.run(t, k, c, nk, stream=stream, with_query=wq, run_ids=run)
-        kt_acc["ms"] += runner.kernel_times()["total_ms"]
+        kt = runner.kernel_times()
+        kt_acc["ms"] += kt["total_ms"]
+        kt_acc["last"] = kt
         if not wq:
             return r
         m, s_, v, q = r
@@ -491,7 +508,12 @@ def main_sharded(args, torch, dist, world, rank, dev):
         oq = v[:, -1].astype(np.int32) if wq else None
         verified = check_rows(W, seq.cpu().numpy(), v[:, :-1] if wq else v, oq, (lo, hi))
     cpu = cpu_baseline(args, W, n) if rank == 0 else None
-    phases = step.phase_ms()
+    # the same phase names as the one-GPU line (shard.KeyShardedStep.PHASES): the step's phases on
+    # rank 0's launch stream, the matcher's own split inside unpack_match
+    phases = dict(step.phase_ms() or {})
+    last = kt_acc.get("last") or {}
+    phases.update({"segment": last.get("segment_ms"), "advance": last.get("advance_ms"),
+                   "emit": last.get("emit_ms")})
     if rank == 0:
         print(json.dumps({
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
@@ -504,7 +526,8 @@ def main_sharded(args, torch, dist, world, rank, dev):
                        "matches_total": m,
                        "parallelism": f"key-sharded x{world}: RCCL all-to-all route + return, k-way merge",
                        "rank0_slice": [lo, hi], "rank0_step": step.last, "bytes": W["bytes_note"]},
-            "phase_ms_rank0_last_step": phases,
+            "phase_ms": phases,
+            "phase_ms_scope": "rank 0, last timed step",
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": None,
                          "kernel": "matcher step per GPU (every matcher kernel; HIP events on the launch stream): "
@@ -533,16 +556,20 @@ def main():
         # rehearsal on one GPU: gloo through host memory (RCCL refuses duplicate devices)
         dist.init_process_group("gloo" if share else "nccl")
     dev = torch.device(f"cuda:{local}")
+    if world > 1 and not args.strong:
+        # every rank matches its own partition of the key space (its own stream over
+        # its own keys; rank 0's is the canonical one, verified)
+        args.seed_offset = 7919 * rank
     if args.config == "c4":
         return main_c4(args, torch, dist, world, rank, dev)
-    if args.config in ("c2", "c3", "c5") and world > 1:
+    if args.config in ("c2", "c3", "c5") and world > 1 and args.strong:
         return main_sharded(args, torch, dist, world, rank, dev)
 
     from siddhi_amd.device_run import DeviceRunner
 
     n, K = args.events, args.keys
     log(f"generating {args.config} workload: {n} events, {K} keys")
-    W = workload(args)   # C1 at N > 1: every rank a replica of the one stream
+    W = workload(args)
     runner = DeviceRunner(W["compiled"], device=str(dev))
     # host -> device ingest of the input columns (outside the timed region:
     # the timed step starts from HBM-resident events)
@@ -597,7 +624,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    # (max over ranks; a one-GPU rehearsal's gloo group reduces host tensors)
+    dt_t = torch.tensor([dt], dtype=torch.float64, device="cpu" if os.environ.get("SH_BENCH_SHARE_GPU") else dev)
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
@@ -662,9 +690,8 @@ def main():
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
-            # N = 1 here (C2 / C3 / C5 at N > 1 split the one stream: main_sharded);
-            # C1 at N > 1 runs replicas of its unpartitioned stream
-            "scaling": "weak" if args.config == "c1" and world > 1 else "strong",
+            # N > 1 here: every GPU its own key partition (main_sharded: --strong)
+            "scaling": "weak" if world > 1 else "strong",
             "vs_baseline": None, "dtype": "f32+i64", "data": "synthetic",
             "nproc": os.cpu_count(),
             "ingest": {"bytes": ingest_bytes, "ms": ingest_s * 1000.0, "GBps": ingest_bytes / ingest_s / 1e9,
@@ -674,14 +701,22 @@ def main():
                        "output": {"packed": "packed rows (SH_OUT_PACKED, 32 B per match)",
                                   "columns": "typed columns (d_out_cols)",
                                   "raw": "raw 8-byte rows (d_out_values) + trigger_seq"}[layout],
-                       "matches_per_gpu": int(m), "parallelism": f"key-sharded x{world}",
+                       "matches_per_gpu": int(m),
+                       "parallelism": (f"dp{world}: every GPU matches its own partition of the key space (own "
+                                       "stream, own keys), no data-path collective; rank 0's stream verified")
+                       if world > 1 else "one GPU",
                        "bytes": W["bytes_note"]},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "matcher step (every kernel of one pass, HIP events on the launch stream)",
                          "kernels_ms_per_step": step_kernels_ms, "algorithmic_bytes": b_alg,
                          "match_kernel_only_GBps": match_only / 1e9},
-            "phase_ms": {"segment": seg_ms, "advance": adv_ms, "emit": emt_ms},
+            # the sharded step's phase names (main_sharded), so that a SCALE line reads
+            # against this one: at N = 1 the whole step is the matcher
+            "phase_ms": {"route_pack": 0.0, "exchange_out": 0.0, "unpack_match": step_kernels_ms,
+                         "exchange_back": 0.0, "merge": 0.0, "segment": seg_ms, "advance": adv_ms,
+                         "emit": emt_ms},
+            "phase_ms_scope": "mean over the timed steps",
             # which device engine ran (DeviceRunner status: bucketed 1, sequence carry
             # seq3 2 / key-segment seq3 1, aggregates carried 4 / post-pass 1 / in lanes 3,
             # rule sets: sparse partials 1 / key-segment scan 0)

@@ -234,12 +234,42 @@ static int run_rules_sparse(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     hipMemsetAsync(key_cnt, 0, nk1 * 4, st);
     hipMemsetAsync(key_fill, 0, nk1 * 4, st);
     hipMemsetAsync(ctl, 0, 24, st);
+    // the attributes the rules' terms read most on the opening event's row (f1) and on
+    // the consumer's row (f2): loaded once per event by the sparse kernels
+    int32_t pre_open[2] = {-1, -1}, pre_take[2] = {-1, -1};
+    {
+        int cnt0[32] = {0}, cnt1[32] = {0};
+        for (const shr_rule& R : h->r_rules) {
+            for (int t = 0; t < R.nt[0]; t++) {
+                const shp_term& T = R.t[0][t];
+                if (T.lslot == 0 && T.lattr >= 0 && T.lattr < 32) cnt0[T.lattr]++;
+                if (T.rkind != 1 && T.rslot == 0 && T.rattr >= 0 && T.rattr < 32) cnt0[T.rattr]++;
+            }
+            for (int t = 0; t < R.nt[1]; t++) {
+                const shp_term& T = R.t[1][t];
+                if (T.lslot == 1 && T.lattr >= 0 && T.lattr < 32) cnt1[T.lattr]++;
+                if (T.rkind != 1 && T.rslot == 1 && T.rattr >= 0 && T.rattr < 32) cnt1[T.rattr]++;
+            }
+        }
+        auto top2 = [](const int* c, int32_t* out) {
+            for (int k = 0; k < 2; k++) {
+                int best = -1;
+                for (int a = 0; a < 32; a++)
+                    if (c[a] > 0 && a != out[0] && (best < 0 || c[a] > c[best])) best = a;
+                out[k] = best;
+            }
+        };
+        top2(cnt0, pre_open);
+        top2(cnt1, pre_take);
+    }
     if (shr_sparse_open(dT, run->d_ts, run->d_keys, n, nkeys, dC, h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr,
-                        &h->r_img, pr, pr + cap, pr + 2 * cap, key_cnt, ctl, cap, (int32_t*)(ctl + 2),
+                        &h->r_img, pr, pr + cap, pr + 2 * cap, key_cnt, ctl, cap, (int32_t*)(ctl + 2), pre_open,
                         st))
         return fail(h, SH_E_HIP, "sparse partial launch failed");
-    unsigned long long rd[3] = {0, 0, 0};
+    unsigned long long rd[5] = {0, 0, 0, 0, 0};
     hipMemcpyAsync(rd, ctl, 24, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(rd + 3, run->d_ts, 8, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(rd + 4, run->d_ts + (n - 1), 8, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the sparse partials");
     const int64_t np = (int64_t)rd[0];
     // a key's events each test all of its key's partials: dense partials per key take
@@ -254,13 +284,34 @@ static int run_rules_sparse(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     int64_t* l_te = (int64_t*)(l_q + cap);
     const int64_t rcap = std::max<int64_t>(np, 1);
     if (h->r_rec.ensure_fresh((size_t)rcap * 12)) return fail(h, SH_E_OOM, "match records");
+    // the live-partial bitmap (shr_live): the run's time span in <= SH_SPARSE_SLICES
+    // (default 256) power-of-two slices, one bit per key and slice (SH_SPARSE_LIVE=0: off)
+    shr_live LV;
+    memset(&LV, 0, sizeof(LV));
+    {
+        static const bool live_off = getenv("SH_SPARSE_LIVE") && getenv("SH_SPARSE_LIVE")[0] == '0';
+        static const int max_sl = getenv("SH_SPARSE_SLICES") ? std::max(1, atoi(getenv("SH_SPARSE_SLICES"))) : 256;
+        const int64_t tmin = (int64_t)rd[3], span = (int64_t)rd[4] - tmin + 1;
+        if (!live_off && span > 0) {
+            int shift = 0;
+            while (shift < 62 && ((span - 1) >> shift) + 1 > max_sl) shift++;
+            LV.tmin = tmin;
+            LV.shift = shift;
+            LV.nslices = (int32_t)(((span - 1) >> shift) + 1);
+            LV.wps = (nkeys + 31) / 32;
+            const size_t bytes = (size_t)LV.nslices * LV.wps * 4;
+            if (h->rs_live.ensure(bytes)) return fail(h, SH_E_OOM, "live bitmap");
+            LV.bits = h->rs_live.as<uint32_t>();
+            hipMemsetAsync(LV.bits, 0, bytes, st);
+        }
+    }
     uint32_t* rec_p = h->r_rec.as<uint32_t>();
     uint32_t* rec_q = rec_p + rcap;
     uint32_t* rec_r = rec_q + rcap;
     if (np > 0 &&
         shr_sparse_match(dT, run->d_ts, run->d_keys, n, dC, h->r_img.bytes ? h->rd_img.as<uint8_t>() : nullptr,
                          &h->r_img, pr, pr + cap, pr + 2 * cap, key_fill, ctl, np, key_off,
-                         l_p, l_r, l_te, l_q, rec_p, rec_q, rec_r, ctl + 1, rcap, nkeys, st))
+                         l_p, l_r, l_te, l_q, rec_p, rec_q, rec_r, ctl + 1, rcap, nkeys, &LV, pre_take, st))
         return fail(h, SH_E_HIP, "sparse match launch failed");
     hipMemcpyAsync(rd, ctl, 16, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in the sparse match");

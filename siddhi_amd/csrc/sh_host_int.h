@@ -322,7 +322,7 @@ struct sh_handle {
     DevBuf r_rec, r_keys, r_g, r_sk, r_sv, r_hist, r_scan, r_run;
     // sparse partials (shr_sparse_*): the partials, per key counts and list starts,
     // the keys' lists (opening event, rule, consuming event, expiry), counters
-    DevBuf rs_pr, rs_key, rs_list, rs_ctl;
+    DevBuf rs_pr, rs_key, rs_list, rs_ctl, rs_live;
     int rs_last = 0;  // 1: the last rule run took the sparse-partial path
     // ---- bucketed window engine (sh_bucket.hip + shb_match): 0 untried, 1 loaded, <0 unavailable
     int bk_state = 0;

@@ -90,23 +90,35 @@ int shr_place(const shr_table* dT, const uint32_t* order, int64_t m, const uint3
               const uint32_t* rec_r, const uint32_t* perm, const int64_t* sts, const shd_cols* dC, uint64_t seq_base,
               int n_out, uint64_t* out_seq, int32_t* out_query, int64_t* out_ts, int64_t* out_vals, void* stream,
               const uint32_t* sts32 = nullptr, int64_t tbase = 0);
-// sparse partials over arrival order (no key segment; sh_rules.hip): the partials
+// sparse partials over arrival order (no key segment; sh_rules.hip): pre[2] (or
+// NULL) the attributes f1 reads most on the event's row, loaded with the event; the partials
 // (p, r, key) of every event into pr_* (count in *ctr, at most cap written), and
 // their count per key (key_cnt[key]++); *flag |= 1 when the run's timestamps
 // decrease, 2 when a key is >= nkeys
 int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int32_t* akeys, int64_t n, int32_t nkeys,
                     const shd_cols* dC, const uint8_t* img, const shr_img* I, uint32_t* pr_p, uint32_t* pr_r,
                     uint32_t* pr_key, uint32_t* key_cnt, unsigned long long* ctr, int64_t cap,
-                    int32_t* flag, void* stream);
+                    int32_t* flag, const int32_t* pre, void* stream);
+// live-partial bitmap of the sparse path: bit (s, key) set when a partial of `key`
+// may be consumed by an event of time slice s ([tmin + s << shift, ...)), i.e. it
+// opens before the slice ends and expires after it starts. Zeroed by the caller;
+// bits == NULL: no bitmap (every event reads its key's list bounds)
+struct shr_live {
+    uint32_t* bits;   // [nslices][wps]
+    int64_t tmin;
+    int32_t shift, nslices, wps, pad;
+};
 // the partials into their keys' lists (key_off: exclusive scan of key_cnt; key_fill:
-// zeroed per-key slot counters), the
+// zeroed per-key slot counters) and the live bitmap; pre[2] (or NULL) the attributes
+// f2 reads most on the consumer's row; the
 // consuming event of each (least later event of its key in the window with f2),
 // and the (p, q, r) records of the consumed ones (count in *rctr, any order)
 int shr_sparse_match(const shr_table* dT, const int64_t* ts, const int32_t* akeys, int64_t n, const shd_cols* dC,
                      const uint8_t* img, const shr_img* I, const uint32_t* pr_p, const uint32_t* pr_r, const uint32_t* pr_key, uint32_t* key_fill,
                      const unsigned long long* ctr, int64_t n_pairs_max, const uint32_t* key_off, uint32_t* l_p,
                      uint32_t* l_r, int64_t* l_te, uint32_t* l_q, uint32_t* rec_p, uint32_t* rec_q, uint32_t* rec_r,
-                     unsigned long long* rctr, int64_t rcap, int32_t nkeys, void* stream);
+                     unsigned long long* rctr, int64_t rcap, int32_t nkeys, const shr_live* live,
+                     const int32_t* pre, void* stream);
 // the run's timestamp range (one read-back), and the 32-bit offsets from `base`
 int shr_ts_range(const int64_t* ts, int64_t n, int64_t* lo, int64_t* hi, void* scratch16, void* stream);
 int shr_ts_to32(const int64_t* ts, int64_t n, int64_t base, uint32_t* t32, void* stream);

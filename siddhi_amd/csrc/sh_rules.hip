@@ -194,6 +194,57 @@ __device__ __forceinline__ int64_t rule_attr(const void* const* cols, int a, int
     }
 }
 
+// the row's attributes a rule set's terms read most, loaded once per event: row
+// `slot` (0: the opening event, 1: the consumer) of attribute a[0] / a[1] (-1: none)
+struct RowPre {
+    int slot;
+    int a[2];
+    int64_t v[2];
+};
+__device__ __forceinline__ int64_t rule_attr_pre(const void* const* cols, int a, int type, uint32_t row, int slot,
+                                                 const RowPre& R) {
+    if (slot == R.slot) {
+        if (a == R.a[0]) return R.v[0];
+        if (a == R.a[1]) return R.v[1];
+    }
+    return rule_attr(cols, a, type, row);
+}
+
+// terms as rule_terms_img, the preloaded attributes of one row from registers
+__device__ __forceinline__ bool rule_terms_pre(const shp_term* T, int nt, uint32_t r0, uint32_t r1,
+                                               const void* const* cols, const RowPre& R) {
+    for (int t = 0; t < nt; t++) {
+        const shp_term X = T[t];
+        const uint32_t lr = X.lslot ? r1 : r0;
+        if (lr == SHD_NULL_ROW) return false;
+        VmVal l, r;
+        l.t = X.ltype;
+        l.null = 0;
+        l.b = rule_attr_pre(cols, X.lattr, X.ltype, lr, X.lslot, R);
+        if (X.rkind == 1) {
+            r.t = X.ctype;
+            r.null = 0;
+            r.b = X.c;
+        } else {
+            const uint32_t rr = X.rslot ? r1 : r0;
+            if (rr == SHD_NULL_ROW) return false;
+            r.t = X.rtype;
+            r.null = 0;
+            r.b = rule_attr_pre(cols, X.rattr, X.rtype, rr, X.rslot, R);
+            if (X.rkind == 2) {
+                VmVal c;
+                c.t = X.ctype;
+                c.null = 0;
+                c.b = X.c;
+                r = vm_arith(X.aop, X.atype, r, c);
+                if (r.null) return false;
+            }
+        }
+        if (!vm_cmp(X.op, X.dom, l, r)) return false;
+    }
+    return true;
+}
+
 __device__ __forceinline__ bool rule_terms_img(const shp_term* T, int nt, uint32_t r0, uint32_t r1,
                                                const void* const* cols) {
     for (int t = 0; t < nt; t++) {
@@ -696,11 +747,11 @@ __device__ __forceinline__ uint32_t spa_rule_id(const shr_table* __restrict__ RT
 // f1 of rule r on row p
 template <bool IMG>
 __device__ __forceinline__ bool spa_f1(const shr_table* __restrict__ RT, const shr_img& I, const SpaRules& S,
-                                       const shd_cols* __restrict__ C, uint32_t r, uint32_t p) {
+                                       const shd_cols* __restrict__ C, uint32_t r, uint32_t p, const RowPre& RP) {
     if (IMG) {
         const shr_meta M = ((const shr_meta*)(S.L + I.off_meta))[r];
         const shp_term* T0 = (const shp_term*)((I.off_terms0 < I.lds ? S.L : S.G) + I.off_terms0) + M.toff0;
-        return rule_terms_img(T0, M.nt0, p, SHD_NULL_ROW, S.cols);
+        return rule_terms_pre(T0, M.nt0, p, SHD_NULL_ROW, S.cols, RP);
     }
     const shr_rule* R = RT->rules + r;
     return rule_terms(R->t[0], R->nt[0], p, SHD_NULL_ROW, C);
@@ -709,10 +760,11 @@ __device__ __forceinline__ bool spa_f1(const shr_table* __restrict__ RT, const s
 // f2 of rule r on (p, q)
 template <bool IMG>
 __device__ __forceinline__ bool spa_f2(const shr_table* __restrict__ RT, const shr_img& I, const SpaRules& S,
-                                       const shd_cols* __restrict__ C, uint32_t r, uint32_t p, uint32_t q) {
+                                       const shd_cols* __restrict__ C, uint32_t r, uint32_t p, uint32_t q,
+                                       const RowPre& RP) {
     if (IMG) {
         const shr_meta M = ((const shr_meta*)(S.L + I.off_meta))[r];
-        return rule_terms_img((const shp_term*)(S.L + I.off_terms1) + M.toff1, M.nt1, p, q, S.cols);
+        return rule_terms_pre((const shp_term*)(S.L + I.off_terms1) + M.toff1, M.nt1, p, q, S.cols, RP);
     }
     const shr_rule* R = RT->rules + r;
     return rule_terms(R->t[1], R->nt[1], p, q, C);
@@ -729,7 +781,7 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
                                                          uint32_t* __restrict__ pr_p, uint32_t* __restrict__ pr_r,
                                                          uint32_t* __restrict__ pr_key, uint32_t* __restrict__ key_cnt,
                                                          unsigned long long* __restrict__ ctr, int64_t cap,
-                                                         int32_t* __restrict__ flag) {
+                                                         int32_t* __restrict__ flag, int pa0, int pa1) {
     extern __shared__ uint4 s_img[];
     __shared__ const void* s_col[32];
     // per wave: its pending partials (opening event, rule, key) and their count --
@@ -776,6 +828,18 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
             key[u] = in ? akeys[p] : -1;
             xv[u] = (in && ix_col) ? rule_ix_key(ix_ty, rule_attr(s_col, ix_attr, ix_ty, (uint32_t)p)) : 0;
         }
+        // f1's most read attributes of the event, loaded with it (IMG: the terms
+        // come from LDS, so these are the chain's only global reads)
+        RowPre rp[SPA_U];
+#pragma unroll
+        for (int u = 0; u < SPA_U; u++) {
+            const int64_t p = base + (int64_t)u * SPA_TPB + threadIdx.x;
+            rp[u].slot = 0;
+            rp[u].a[0] = pa0;
+            rp[u].a[1] = pa1;
+            rp[u].v[0] = (pa0 >= 0 && p < n) ? rule_attr(s_col, pa0, RT->attr_type[pa0], (uint32_t)p) : 0;
+            rp[u].v[1] = (pa1 >= 0 && p < n) ? rule_attr(s_col, pa1, RT->attr_type[pa1], (uint32_t)p) : 0;
+        }
         uint32_t lo[SPA_U], hi[SPA_U];
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
@@ -799,7 +863,7 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
                 bool ok = false;
                 if (k < total) {
                     r = spa_rule_id<IMG>(RT, I, S, lo[u], k, nsel);
-                    ok = spa_f1<IMG>(RT, I, S, C, r, (uint32_t)p);
+                    ok = spa_f1<IMG>(RT, I, S, C, r, (uint32_t)p, rp[u]);
                 }
                 const uint64_t m = __ballot(ok);
                 if (m == 0ull) continue;
@@ -841,17 +905,27 @@ __global__ void k_sparse_place(const uint32_t* __restrict__ pr_p, const uint32_t
                                const unsigned long long* __restrict__ ctr, const uint32_t* __restrict__ key_off,
                                const shr_table* __restrict__ RT, const int64_t* __restrict__ ts,
                                uint32_t* __restrict__ l_p, uint32_t* __restrict__ l_r, int64_t* __restrict__ l_te,
-                               uint32_t* __restrict__ l_q) {
+                               uint32_t* __restrict__ l_q, shr_live LV) {
     const int64_t np = (int64_t)*ctr;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < np; s += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t p = pr_p[s], r = pr_r[s], key = pr_key[s];  // (np <= the buffers: the host checked the count)
         const uint32_t pos = key_off[key] + atomicAdd(&key_fill[key], 1u);  // (any order inside a key's list)
         const int64_t W = RT->rules[r].within;
         const int64_t t = ts[p];
+        const int64_t te = (W < 0 || t > INT64_MAX - W) ? INT64_MAX : t + W;
         l_p[pos] = p;
         l_r[pos] = r;
-        l_te[pos] = (W < 0 || t > INT64_MAX - W) ? INT64_MAX : t + W;
+        l_te[pos] = te;
         l_q[pos] = 0xFFFFFFFFu;
+        if (LV.bits) {
+            // the slices in which an event can consume it: from its own to its expiry's
+            // (the run's timestamps lie in [tmin, tmin + nslices << shift))
+            const int64_t s0 = (t - LV.tmin) >> LV.shift;
+            const int64_t tend = LV.tmin + ((int64_t)LV.nslices << LV.shift);  // (no overflow: te may be INT64_MAX)
+            const int64_t s1 = te >= tend ? LV.nslices - 1 : (te - LV.tmin) >> LV.shift;
+            for (int64_t sl = s0; sl <= s1; sl++)
+                atomicOr(&LV.bits[sl * LV.wps + (key >> 5)], 1u << (key & 31u));
+        }
     }
 }
 
@@ -865,7 +939,8 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __rest
                                                          const uint32_t* __restrict__ l_p,
                                                          const uint32_t* __restrict__ l_r,
                                                          const int64_t* __restrict__ l_te, uint32_t* __restrict__ l_q,
-                                                         int xcd, float slice_scale) {
+                                                         int xcd, float slice_scale, shr_live LV, int pa0,
+                                                         int pa1) {
     extern __shared__ uint4 s_img[];
     __shared__ const void* s_col[32];
     spa_stage<IMG>(img, I, C, s_img, s_col);
@@ -885,14 +960,32 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __rest
     const int64_t round = (int64_t)SPA_TPB * SPA_U;
     for (int64_t base = wb * round; base < n; base += nw * round) {
         int32_t key[SPA_U];
+        int64_t tq[SPA_U];
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
             const int64_t q = base + (int64_t)u * SPA_TPB + threadIdx.x;
             key[u] = q < n ? akeys[q] : -1;
+            tq[u] = q < n ? ts[q] : 0;
             if (xcd && key[u] >= 0) {
                 const int sl = min(7, (int)((float)key[u] * slice_scale));
                 if (sl != xs) key[u] = -1;
             }
+        }
+        // the live bitmap: an event whose key has no partial that can be consumed in
+        // its time slice reads nothing else (a 128 KB slice of bits per 1M keys, in L2)
+        if (LV.bits) {
+            uint32_t wbits[SPA_U];
+#pragma unroll
+            for (int u = 0; u < SPA_U; u++) {
+                wbits[u] = 0u;
+                if (key[u] >= 0) {
+                    const int64_t sl = (tq[u] - LV.tmin) >> LV.shift;
+                    wbits[u] = LV.bits[sl * LV.wps + ((uint32_t)key[u] >> 5)];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < SPA_U; u++)
+                if (key[u] >= 0 && !((wbits[u] >> ((uint32_t)key[u] & 31u)) & 1u)) key[u] = -1;
         }
         uint32_t lo[SPA_U], hi[SPA_U];
 #pragma unroll
@@ -907,11 +1000,17 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __rest
         for (int u = 0; u < SPA_U; u++) {
             if (lo[u] == hi[u]) continue;
             const int64_t q = base + (int64_t)u * SPA_TPB + threadIdx.x;
-            const int64_t tq = ts[q];
+            // f2's most read attributes of the consumer, loaded once for its list
+            RowPre rp;
+            rp.slot = 1;
+            rp.a[0] = pa0;
+            rp.a[1] = pa1;
+            rp.v[0] = pa0 >= 0 ? rule_attr(S.cols, pa0, RT->attr_type[pa0], (uint32_t)q) : 0;
+            rp.v[1] = pa1 >= 0 ? rule_attr(S.cols, pa1, RT->attr_type[pa1], (uint32_t)q) : 0;
             for (uint32_t pos = lo[u]; pos < hi[u]; pos++) {
                 const uint32_t p = l_p[pos];
-                if ((int64_t)p >= q || tq > l_te[pos]) continue;
-                if (spa_f2<IMG>(RT, I, S, C, l_r[pos], p, (uint32_t)q)) atomicMin(&l_q[pos], (uint32_t)q);
+                if ((int64_t)p >= q || tq[u] > l_te[pos]) continue;
+                if (spa_f2<IMG>(RT, I, S, C, l_r[pos], p, (uint32_t)q, rp)) atomicMin(&l_q[pos], (uint32_t)q);
             }
         }
     }
@@ -973,7 +1072,9 @@ static bool spa_img_fits(const uint8_t* img, const shr_img* I, int static_lds) {
 extern "C" int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int32_t* akeys, int64_t n, int32_t nkeys,
                                const shd_cols* dC, const uint8_t* img, const shr_img* I, uint32_t* pr_p,
                                uint32_t* pr_r, uint32_t* pr_key, uint32_t* key_cnt,
-                               unsigned long long* ctr, int64_t cap, int32_t* flag, void* stream) {
+                               unsigned long long* ctr, int64_t cap, int32_t* flag, const int32_t* pre,
+                               void* stream) {
+    const int pa0 = pre ? pre[0] : -1, pa1 = pre ? pre[1] : -1;
     shr_img none;
     memset(&none, 0, sizeof(none));
     const int buf = 3 * (SPA_TPB / 64) * SPA_WBUF * 4 + 512;
@@ -987,12 +1088,12 @@ extern "C" int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int
     if (g < 1) g = 1;
     if (use_img)
         hipLaunchKernelGGL(k_sparse_open<true>, dim3((unsigned)g), dim3(SPA_TPB), (size_t)I->lds, (hipStream_t)stream, dT,
-                           ts, akeys, n, nkeys, dC, img, *I, pr_p, pr_r, pr_key, key_cnt, ctr, cap, flag);
+                           ts, akeys, n, nkeys, dC, img, *I, pr_p, pr_r, pr_key, key_cnt, ctr, cap, flag, pa0, pa1);
     else
         hipLaunchKernelGGL(k_sparse_open<false>, dim3((unsigned)g), dim3(SPA_TPB), 0, (hipStream_t)stream, dT, ts, akeys,
                            n, nkeys, dC, img && I && I->bytes > 0 ? img : (const uint8_t*)nullptr,
                            img && I && I->bytes > 0 ? *I : none, pr_p, pr_r, pr_key, key_cnt, ctr, cap,
-                           flag);
+                           flag, pa0, pa1);
     return rules_ok();
 }
 
@@ -1001,11 +1102,16 @@ extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const in
                                 const uint32_t* pr_key, uint32_t* key_fill, const unsigned long long* ctr,
                                 int64_t n_pairs_max, const uint32_t* key_off, uint32_t* l_p, uint32_t* l_r,
                                 int64_t* l_te, uint32_t* l_q, uint32_t* rec_p, uint32_t* rec_q, uint32_t* rec_r,
-                                unsigned long long* rctr, int64_t rcap, int32_t nkeys, void* stream) {
+                                unsigned long long* rctr, int64_t rcap, int32_t nkeys, const shr_live* live,
+                                const int32_t* pre, void* stream) {
+    const int pa0 = pre ? pre[0] : -1, pa1 = pre ? pre[1] : -1;
     hipStream_t st = (hipStream_t)stream;
     const unsigned gp = rgrid(n_pairs_max);
+    shr_live LV;
+    memset(&LV, 0, sizeof(LV));
+    if (live && live->bits) LV = *live;
     hipLaunchKernelGGL(k_sparse_place, dim3(gp), dim3(RTPB), 0, st, pr_p, pr_r, pr_key, key_fill, ctr, key_off, dT, ts,
-                       l_p, l_r, l_te, l_q);
+                       l_p, l_r, l_te, l_q, LV);
     {
         shr_img none;
         memset(&none, 0, sizeof(none));
@@ -1027,11 +1133,11 @@ extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const in
         if (use_img)
             hipLaunchKernelGGL(k_sparse_take<true>, dim3((unsigned)tg), dim3(SPA_TPB), (size_t)I->lds, st, dT, ts, akeys,
                                n, dC, img, *I, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
-                               (const int64_t*)l_te, l_q, xcd, scale);
+                               (const int64_t*)l_te, l_q, xcd, scale, LV, pa0, pa1);
         else
             hipLaunchKernelGGL(k_sparse_take<false>, dim3((unsigned)tg), dim3(SPA_TPB), 0, st, dT, ts, akeys, n, dC,
                                (const uint8_t*)nullptr, none, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
-                               (const int64_t*)l_te, l_q, xcd, scale);
+                               (const int64_t*)l_te, l_q, xcd, scale, LV, pa0, pa1);
     }
     hipLaunchKernelGGL(k_sparse_rec, dim3(gp), dim3(256), 0, st, (const uint32_t*)l_p, (const uint32_t*)l_r,
                        (const uint32_t*)l_q, ctr, rec_p, rec_q, rec_r, rctr, rcap);
