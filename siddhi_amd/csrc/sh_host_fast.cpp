@@ -514,9 +514,12 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     shb_out O;
     memset(&O, 0, sizeof(O));
     O.n_out = P.n_out;
-    // the emitter's L2 warming of its row sources (SH_BK_WARM=0: off)
-    static const bool warm_off = getenv("SH_BK_WARM") && getenv("SH_BK_WARM")[0] == '0';
-    O.warm = warm_off ? 0 : 1;
+    // the emitter's L2 warming of its row sources: off unless SH_BK_WARM=1. It saves
+    // 0.12 ms of C2's 4.3 (profiles/r5_c2_warm_ab_*.json) but adds 1.77 GB of L2-miss
+    // fetch per step (profiles/pmc_c2.json, round 4) that no counter here can show to
+    // be Infinity-Cache hits rather than HBM traffic
+    static const bool warm_on = getenv("SH_BK_WARM") && getenv("SH_BK_WARM")[0] == '1';
+    O.warm = warm_on ? 1 : 0;
     int ms[SHB_MAX_MS], n_ms = 0;
     const int part_attr = h->part_attr0;
     for (int o = 0; o < P.n_out; o++) {
@@ -834,8 +837,8 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     shb_out O;
     memset(&O, 0, sizeof(O));
     O.n_out = Q.n_out;
-    static const bool warm_off = getenv("SH_BK_WARM") && getenv("SH_BK_WARM")[0] == '0';
-    O.warm = warm_off ? 0 : 1;  // the emitter's L2 warming (as the window engine's)
+    static const bool warm_on = getenv("SH_BK_WARM") && getenv("SH_BK_WARM")[0] == '1';
+    O.warm = warm_on ? 1 : 0;  // the emitter's L2 warming (as the window engine's: off by default)
     shb_s3 S;
     memset(&S, 0, sizeof(S));
     S.type = ty;
