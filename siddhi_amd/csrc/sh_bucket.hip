@@ -440,7 +440,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
             const uint32_t d = pw >> BK_PFX_BITS;
             const uint32_t ps = pw & BK_PFX_MASK;
             c = (pfx[s + 1] & BK_PFX_MASK) - ps;
-            mp[j] = ms0[d] + ps - (pfx[to[d]] & BK_PFX_MASK);
+            mp[j] = O.ms_slot ? (uint32_t)(b0 + s) : ms0[d] + ps - (pfx[to[d]] & BK_PFX_MASK);
         }
         if ((j & 3) == 0) cp[j >> 2] = 0u;
         cp[j >> 2] |= c << (8 * (j & 3));
@@ -839,6 +839,213 @@ __global__ void __launch_bounds__(S3B_TPB) k_s3b(shb_plan P, shb_s3 S) {
     if (S.warm) asm volatile("" ::"v"(warm));
 }
 
+// ---------------------------------------------------------------- sequence carry, sub-buckets
+// k_s3b with two workgroups per key bucket (S.sub = 1): workgroup (b, h) carries the
+// bucket's local keys of parity h (local key & 1 == h), so 512 workgroups of 512
+// threads and half-size chunks (72 KB of LDS: two per CU) replace 256 of 1,024 (131
+// KB: one per CU), and a CU overlaps one workgroup's carry walk with the other's
+// loads and sort. A chunk gathers up to S3C_RAW events of the bucket's segments and
+// keeps its parity's (~half: S3C_CH bounds it with > 50 sigma to spare on uniform
+// keys; more sets SHB_F_SPAN and the host runs k_s3b). The two workgroups of a bucket
+// interleave their events inside every (tile, bucket) segment, so a match's e1 /
+// last values go to the match stream AT ITS EVENT'S SLOT (one match per event at
+// most) and the emitter addresses them so (shb_out.ms_slot); per tile one atomic
+// per workgroup and chunk adds its matches.
+#define S3C_TPB 512
+#define S3C_CH 2048
+#define S3C_NR (S3C_CH / S3C_TPB)
+#define S3C_W (S3C_TPB / 64)
+#define S3C_NK (S3B_NK / 2)
+#define S3C_RAW 3584  // events of a chunk before the parity split
+
+__device__ __forceinline__ void s3c_sort_pass(const uint32_t* __restrict__ c_key, const uint16_t* in,
+                                              uint16_t* out, int L, int sh, uint32_t (*wc)[64], uint32_t* ws) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int c = threadIdx.x; c < S3C_W * 64; c += S3C_TPB) (&wc[0][0])[c] = 0u;
+    __syncthreads();
+    uint32_t rk[S3C_NR], dg[S3C_NR], ix[S3C_NR];
+#pragma unroll
+    for (int r = 0; r < S3C_NR; r++) {
+        const int pos = (w * S3C_NR + r) * 64 + lane;  // wave w owns positions [w * 256, w * 256 + 256)
+        const bool valid = pos < L;
+        ix[r] = valid ? (in ? (uint32_t)in[pos] : (uint32_t)pos) : 0u;
+        const uint32_t d = valid ? (c_key[ix[r]] >> sh) & 63u : 0u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bb = 0; bb < 6; bb++) {
+            const bool bit = (d >> bb) & 1u;
+            const uint64_t m = __ballot(valid && bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t r_ = (uint32_t)__popcll(peers & lt);
+        const uint32_t base = valid ? wc[w][d] : 0u;
+        if (valid && r_ == 0) wc[w][d] = base + (uint32_t)__popcll(peers);
+        rk[r] = valid ? base + r_ : ~0u;
+        dg[r] = d;
+    }
+    __syncthreads();
+    // (digit, wave) exclusive offsets: thread t = digit * 8 + wave
+    {
+        const int d = threadIdx.x >> 3, q = threadIdx.x & 7;
+        uint32_t tot;
+        const uint32_t ex = shw_block_excl<S3C_TPB>(wc[q][d], ws, &tot);
+        __syncthreads();
+        wc[q][d] = ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < S3C_NR; r++)
+        if (rk[r] != ~0u) out[wc[w][dg[r]] + rk[r]] = (uint16_t)ix[r];
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(S3C_TPB, 2) k_s3b2(shb_plan P, shb_s3 S) {
+    __shared__ uint32_t st_e1[S3C_NK], st_last[S3C_NK];
+    __shared__ uint8_t st_f[S3C_NK];  // bit 0: an e1, bit 1: a last e2
+    __shared__ uint32_t c_key[S3C_CH], c_val[S3C_CH], c_gi[S3C_CH];
+    __shared__ uint16_t o_a[S3C_CH], o_b[S3C_CH];
+    __shared__ uint32_t m_v0[S3C_CH], m_v1[S3C_CH];
+    __shared__ uint8_t m_hit[S3C_CH];
+    __shared__ uint32_t wc[S3C_W][64];
+    __shared__ uint32_t ws[S3C_W];
+    __shared__ uint32_t seg_p[SHB_CT_MAX + 1], seg_g[SHB_CT_MAX], t_sum[SHB_CT_MAX];
+    // the two workgroups of bucket b are blocks b and b + 256: the same XCD (round-robin
+    // dealing), so the bucket's segments are fetched into one L2
+    const int b = (int)(blockIdx.x & (SHB_NB - 1)), par = (int)(blockIdx.x >> 8);
+    const int kb = P.kb;
+    const uint32_t kmask = (1u << kb) - 1u;
+    const int t = S.type;
+    for (int k = threadIdx.x; k < S3C_NK; k += S3C_TPB) st_f[k] = 0;
+    const uint32_t* __restrict__ gcol = (const uint32_t*)P.st_dst[0];
+    unsigned long long t_prev = wall_clock64();
+#define S3C_PROF(ph)                                                                 \
+    if (P.prof && threadIdx.x == 0) {                                                \
+        const unsigned long long t_now = wall_clock64();                             \
+        atomicAdd(&P.prof[ph], t_now - t_prev);                                      \
+        t_prev = t_now;                                                              \
+    }
+    for (int a = 0; a < P.nt;) {
+        __syncthreads();
+        // the bucket's segments of tiles [a, a + SHB_CT_MAX), their prefix
+        const int nseg = P.nt - a < SHB_CT_MAX ? P.nt - a : SHB_CT_MAX;
+        uint32_t len = 0u, g = 0u;
+        if ((int)threadIdx.x < nseg) {
+            const int T = a + (int)threadIdx.x;
+            const uint32_t lo = P.tofft[(int64_t)b * P.tstride + T], hi = P.tofft[(int64_t)(b + 1) * P.tstride + T];
+            len = hi - lo;
+            g = ((uint32_t)T << SHB_TILE_SHIFT) + lo;
+        }
+        {
+            uint32_t tot;
+            const uint32_t pre = shw_block_excl<S3C_TPB>(len, ws, &tot);
+            if ((int)threadIdx.x < nseg) {
+                seg_p[threadIdx.x] = pre;
+                seg_g[threadIdx.x] = g;
+                t_sum[threadIdx.x] = 0u;
+            }
+            if ((int)threadIdx.x == nseg) seg_p[nseg] = tot;
+        }
+        __syncthreads();
+        // this chunk: tiles [a, a + ne), at most S3C_RAW events before the parity split
+        const int ne = __syncthreads_count((int)threadIdx.x < nseg && seg_p[threadIdx.x + 1] <= S3C_RAW);
+        if (ne == 0) {
+            if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_SPAN);
+            return;  // (uniform) the host reruns on k_s3b
+        }
+        const int Lraw = (int)seg_p[ne];
+        // this parity's events, compacted in arrival order (inside the bucket)
+        uint32_t L = 0u;
+        for (int i0 = 0; i0 < Lraw; i0 += S3C_TPB) {
+            const int i = i0 + (int)threadIdx.x;
+            uint32_t key = 0u, gi = 0u;
+            bool keep = false;
+            if (i < Lraw) {
+                int lo = 0, hi = ne - 1;  // the segment holding position i
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (seg_p[mid] <= (uint32_t)i) lo = mid;
+                    else hi = mid - 1;
+                }
+                gi = seg_g[lo] + ((uint32_t)i - seg_p[lo]);
+                key = P.w0[gi] & kmask;
+                keep = (int)(key & 1u) == par;
+            }
+            uint32_t tot;
+            const uint32_t pos = L + shw_block_excl<S3C_TPB>(keep ? 1u : 0u, ws, &tot);
+            if (keep && pos < S3C_CH) {
+                c_key[pos] = key >> 1;
+                c_val[pos] = gcol[gi];
+                c_gi[pos] = gi;
+            }
+            L += tot;
+        }
+        if (L > S3C_CH) {
+            if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_SPAN);
+            return;  // (uniform: L is the block total) the host reruns on k_s3b
+        }
+        __syncthreads();
+        S3C_PROF(0)
+        // stable sort by the parity's local key (kb - 1 bits)
+        const uint16_t* srt;
+        if (kb - 1 <= 6) {
+            s3c_sort_pass(c_key, nullptr, o_a, (int)L, 0, wc, ws);
+            srt = o_a;
+        } else {
+            s3c_sort_pass(c_key, nullptr, o_a, (int)L, 0, wc, ws);
+            s3c_sort_pass(c_key, o_a, o_b, (int)L, 6, wc, ws);
+            srt = o_b;
+        }
+        S3C_PROF(1)
+        // the first event of each key run steps through the run (k_s3b's step)
+        for (int q = threadIdx.x; q < (int)L; q += S3C_TPB) {
+            const uint32_t ci = srt[q];
+            const uint32_t key = c_key[ci];
+            if (q > 0 && c_key[srt[q - 1]] == key) continue;
+            uint32_t f = st_f[key], e1b = st_e1[key], lastb = st_last[key];
+            for (int r = q; r < (int)L; r++) {
+                const uint32_t cr = r == q ? ci : srt[r];
+                if (r > q && c_key[cr] != key) break;
+                const uint32_t xb = c_val[cr];
+                const NfVal x = s3b_val(xb, t);
+                const bool hit = (f & 2u) && nf_cmp(S.op3, S.dom3, x, s3b_val(lastb, t));
+                m_hit[cr] = hit ? 1 : 0;
+                m_v0[cr] = e1b;
+                m_v1[cr] = lastb;
+                if (!hit && (f & 1u) && nf_cmp(S.op2, S.dom2, x, s3b_val(e1b, t))) {
+                    f |= 2u;
+                    lastb = xb;
+                } else {
+                    f = 1u;
+                    e1b = xb;
+                }
+            }
+            st_f[key] = (uint8_t)f;
+            st_e1[key] = e1b;
+            st_last[key] = lastb;
+        }
+        __syncthreads();
+        S3C_PROF(2)
+        // counts at the slots, the match values at the matching event's slot, the
+        // chunk's matches per tile
+        for (int i = threadIdx.x; i < (int)L; i += S3C_TPB) {
+            const uint32_t gi = c_gi[i];
+            const uint32_t hit = m_hit[i];
+            P.cnt[gi] = (uint8_t)hit;
+            if (hit) {
+                for (int m = 0; m < S.n_ms; m++) ((uint32_t*)P.ms[m])[gi] = S.ms_slot[m] == 0 ? m_v0[i] : m_v1[i];
+                atomicAdd(&t_sum[(int)(gi >> SHB_TILE_SHIFT) - a], 1u);
+            }
+        }
+        __syncthreads();
+        for (int sg = threadIdx.x; sg < ne; sg += S3C_TPB)
+            if (t_sum[sg]) atomicAdd(&P.ttot[a + sg], t_sum[sg]);
+        S3C_PROF(3)
+        a += ne;
+    }
+#undef S3C_PROF
+}
+
 // ---------------------------------------------------------------- aggregate carry
 // Select-clause aggregators of the bucketed window engine (C2 select variant ii):
 // one running value per partition key and output, added in the reference's order
@@ -1115,7 +1322,12 @@ extern "C" int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream) {
 
 extern "C" int shb_s3_carry(const shb_plan* P, const shb_s3* S, void* stream) {
     if (P->kb > 12 || P->n_staged < 1 || P->st_width[0] != 4) return -1;
-    hipLaunchKernelGGL(k_s3b, dim3(SHB_NB), dim3(S3B_TPB), 0, (hipStream_t)stream, *P, *S);
+    if (S->sub) {
+        if (P->kb < 1) return -1;
+        hipLaunchKernelGGL(k_s3b2, dim3(2 * SHB_NB), dim3(S3C_TPB), 0, (hipStream_t)stream, *P, *S);
+    } else {
+        hipLaunchKernelGGL(k_s3b, dim3(SHB_NB), dim3(S3B_TPB), 0, (hipStream_t)stream, *P, *S);
+    }
     return bk_ok();
 }
 

@@ -143,6 +143,8 @@ struct shb_plan {
 struct shb_out {
     int32_t n_out;
     int32_t warm;                 // 1: the emitter warms L2 with its row sources first
+    int32_t ms_slot;              // 1: an event's (single) match-stream value sits at its own slot
+    int32_t pad;
     int32_t kind[SHB_MAX_OUT];
     int32_t type[SHB_MAX_OUT];    // sh_type: raw-value conversion
     const void* src[SHB_MAX_OUT]; // kind 0: match-stream column, kind 1: consumer column
@@ -158,7 +160,7 @@ struct shb_s3 {
     int32_t n_ms;
     int32_t ms_slot[2];
     int32_t warm;                 // 1: each chunk warms L2 with the next chunk's segments
-    int32_t pad;
+    int32_t sub;                  // 1: two workgroups per bucket (k_s3b2), match values at slots
 };
 
 // select-clause aggregators carried per key by the bucketed engine (k_bk_aggc):

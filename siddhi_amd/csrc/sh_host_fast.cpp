@@ -843,6 +843,13 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     memset(&S, 0, sizeof(S));
     S.type = ty;
     S.warm = getenv("SH_S3B_WARM") && getenv("SH_S3B_WARM")[0] == '0' ? 0 : 1;
+    // two workgroups per bucket (k_s3b2) unless SH_S3B_SUB=0 (read per call: A/B) or a
+    // previous call's chunk overflowed its parity split (h->s3b_sub_off)
+    {
+        const char* e = getenv("SH_S3B_SUB");
+        S.sub = (e && e[0] == '0') || h->s3b_sub_off || kb < 1 ? 0 : 1;
+    }
+    O.ms_slot = S.sub;
     S.op2 = Q.s3_op2;
     S.dom2 = Q.s3_dom2;
     S.op3 = Q.s3_op3;
@@ -942,6 +949,10 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
                 pr[0], pr[1], pr[2], pr[3]);
     }
     if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
+    if (flag == SHB_F_SPAN && S.sub) {
+        h->s3b_sub_off = true;  // a parity's chunk overflowed (skewed keys): one workgroup per bucket
+        return run_s3b(h, run, nkeys);
+    }
     if (flag) return 1;
     run->out_count = total;
     if (total > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
@@ -951,7 +962,7 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
     hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
     h->times.advance_launches = 1;
-    h->s3b_last = 1;
+    h->s3b_last = S.sub ? 2 : 1;
     return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "sequence engine");
 }
 

@@ -328,7 +328,8 @@ struct sh_handle {
     int bk_state = 0;
     int32_t part_attr0 = -1;  // stream-0 attribute keying query 0's partition
     int bk_last = 0;          // 1: the last sh_run_device ran on the bucketed engine
-    int s3b_last = 0;         // 1: ... on the sequence bucket-carry engine (k_s3b)
+    int s3b_last = 0;         // 1: ... on the sequence bucket-carry engine (k_s3b), 2: its sub-bucket form (k_s3b2)
+    bool s3b_sub_off = false; // a chunk's parity split overflowed once: k_s3b from then on
     shj_bucket bk{};
     std::string bk_err;
     DevBuf bk_w0, bk_sp, bk_toff, bk_tofft, bk_cnt, bk_mstart, bk_tpre, bk_tfirst, bk_hstart, bk_ttot, bk_flag, bk_prof;
