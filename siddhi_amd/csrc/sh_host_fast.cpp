@@ -843,11 +843,13 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     memset(&S, 0, sizeof(S));
     S.type = ty;
     S.warm = getenv("SH_S3B_WARM") && getenv("SH_S3B_WARM")[0] == '0' ? 0 : 1;
-    // two workgroups per bucket (k_s3b2) unless SH_S3B_SUB=0 (read per call: A/B) or a
-    // previous call's chunk overflowed its parity split (h->s3b_sub_off)
+    // two workgroups per bucket (k_s3b2) when SH_S3B_SUB=1 (read per call: A/B): exact,
+    // but on C3 its parity split costs more than the second workgroup per CU gains
+    // (5.28 vs 4.91 ms, profiles/r5_c3_s3b_sub_ab.txt); off after a chunk's parity
+    // split overflowed once (h->s3b_sub_off)
     {
         const char* e = getenv("SH_S3B_SUB");
-        S.sub = (e && e[0] == '0') || h->s3b_sub_off || kb < 1 ? 0 : 1;
+        S.sub = (e && e[0] == '1') && !h->s3b_sub_off && kb >= 1 ? 1 : 0;
     }
     O.ms_slot = S.sub;
     S.op2 = Q.s3_op2;
