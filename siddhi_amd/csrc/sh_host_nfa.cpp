@@ -1013,19 +1013,79 @@ int nf_next_due(sh_handle* h, int64_t* out) {
 // positions are global, so registration stamps and row order match one process.
 int nf_timers(sh_handle* h, int64_t now, bool wall) {
     HpScope hp_(h, 1);
-    {
-        int src = nf_settle(h);
-        if (src) return src;
-    }
-    if (!h->T->has_absent) return SH_OK;
-    if (h->n_nkeys == 0 && !h->coord_on) return SH_OK;
     hipStream_t st = h->stream;
-    if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
-    nf_put_cols(h, nf_store_cols(h));
     bool first_pass = true;
     int n_absent = 0;  // a key's armed flag may be cleared only when it has one scheduler
     for (int q = 0; q < h->T->n_queries; q++)
         for (int p = 0; p < h->T->q[q].n_proc; p++) n_absent += nf_has_sched(h->T->q[q].proc[p]);
+    // the due pass of scheduler (q, p): the candidate count and the first candidates
+    // into pinned memory, no sync (list: the armed-key list form; first: the pass
+    // that also folds the keys armed since the last one into the next list)
+    auto due_launch = [&](int q, int p, bool list, bool first) -> int {
+        const int32_t nkeys = h->n_nkeys;
+        if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");
+        if (h->pin_cand.ensure((size_t)kCandSpec * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "pinned staging");
+        const bool host_stamps = h->sm_on && !h->coord_on;
+        const uint64_t* rank = h->sm_on && !host_stamps ? h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>() : nullptr;
+        if (!(list && first)) hipMemsetAsync(h->n_ctr.p, 0, 8, st);
+        if (list) {
+            unsigned long long* ln = h->n_klist_n.as<unsigned long long>();
+            const int c = h->klist_cur;
+            if (first) {
+                nfd_zero2(h->n_ctr.p, 8, ln + (c ^ 1), 8, st);  // candidates + the next list's count
+                nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
+                             ln + c, h->n_arm_log.as<int32_t>(), h->n_arm_ctr.as<unsigned long long>(), now,
+                             h->n_cand.as<nfd_cand>(), h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h),
+                             n_absent == 1 ? 1 : 0, rank, h->n_klist[c ^ 1].as<int32_t>(), ln + (c ^ 1),
+                             (int64_t)nkeys, st);
+                hipMemsetAsync(h->n_arm_ctr.p, 0, 8, st);
+                h->klist_cur ^= 1;
+            } else {
+                nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
+                             ln + c, nullptr, nullptr, now, h->n_cand.as<nfd_cand>(),
+                             h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), 0, rank, nullptr, nullptr,
+                             (int64_t)nkeys, st);
+            }
+        } else {
+            nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, now, h->n_cand.as<nfd_cand>(),
+                    h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0, rank, st);
+        }
+        hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
+        // the first candidates come back with the count (most passes need no second copy)
+        hipMemcpyAsync(h->pin_cand.p, h->n_cand.p, (size_t)std::min<int64_t>(nkeys, kCandSpec) * sizeof(nfd_cand),
+                       hipMemcpyDeviceToHost, st);
+        return SH_OK;
+    };
+    // one sync for a pending event launch and the first due pass (SH_SPEC_DUE=1): with
+    // one scheduler, no coordinator and the stamps on the host, the due pass is queued
+    // behind the launch and comes back with it. A launch that had to be replayed
+    // (capacity growth) voids it: that scheduler's due pass then runs again over every
+    // key (the list it folded stays a superset of the armed keys). Off by default: on
+    // C4 it saves one sync per call (2.0 instead of 3.0) but the candidates' stamps
+    // then wait longer for the scheduler-map replay thread, and the call is slower
+    // (1,486-1,511 vs 1,377-1,379 ms per 3,000 calls, profiles/r5_c4_spec_due_ab.txt)
+    int spec = 0;  // 1: queued, 2: its results stand, 3: voided
+    {
+        static const bool spec_on = getenv("SH_SPEC_DUE") && getenv("SH_SPEC_DUE")[0] == '1';
+        if (spec_on && h->pend.on && !wall && !h->coord_on && h->sm_on && h->T->has_absent &&
+            h->T->n_queries == 1 && h->T->q[0].n_sched == 1 && h->n_nkeys > 0) {
+            if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
+            const bool list_pass = armed_flags(h) && h->n_arm_log.p;
+            const int rc = due_launch(0, h->T->q[0].sched_seq[0], list_pass, true);
+            if (rc) return rc;
+            if (list_pass) first_pass = false;
+            spec = 1;
+        }
+    }
+    {
+        int src = nf_settle(h);
+        if (src) return src;
+        if (spec == 1) spec = h->times.advance_launches == 1 ? 2 : 3;
+    }
+    if (!h->T->has_absent) return SH_OK;
+    if (h->n_nkeys == 0 && !h->coord_on) return SH_OK;
+    if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
+    nf_put_cols(h, nf_store_cols(h));
     for (int q = 0; q < h->T->n_queries; q++) {
         // Scheduler creation order (the TimestampGenerator's listener order)
         for (int si = 0; si < h->T->q[q].n_sched; si++) {
@@ -1042,43 +1102,16 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
             const int32_t nkeys = h->n_nkeys;
             unsigned long long nc = 0;
             if (nkeys > 0) {
-                // due keys
-                if (h->n_cand.ensure_fresh((size_t)nkeys * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "candidates");
-                const uint64_t* rank =
-                    h->sm_on && !host_stamps ? h->n_rank[q * NF_MAX_PROC + p].as<uint64_t>() : nullptr;
-                const bool list_pass = armed_flags(h) && h->n_arm_log.p;
-                if (!(list_pass && first_pass)) hipMemsetAsync(h->n_ctr.p, 0, 8, st);
-                if (list_pass) {
-                    // the armed-key list (+ the keys armed since the last pass on the
-                    // first scheduler's pass, which also rebuilds the list)
-                    unsigned long long* ln = h->n_klist_n.as<unsigned long long>();
-                    const int c = h->klist_cur;
-                    if (first_pass) {
-                        nfd_zero2(h->n_ctr.p, 8, ln + (c ^ 1), 8, st);  // candidates + the next list's count
-                        nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
-                                     ln + c, h->n_arm_log.as<int32_t>(), h->n_arm_ctr.as<unsigned long long>(), now,
-                                     h->n_cand.as<nfd_cand>(), h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h),
-                                     n_absent == 1 ? 1 : 0, rank, h->n_klist[c ^ 1].as<int32_t>(), ln + (c ^ 1),
-                                     (int64_t)nkeys, st);
-                        hipMemsetAsync(h->n_arm_ctr.p, 0, 8, st);
-                        h->klist_cur ^= 1;
-                        first_pass = false;
-                    } else {
-                        nfd_due_list(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), h->n_klist[c].as<int32_t>(),
-                                     ln + c, nullptr, nullptr, now, h->n_cand.as<nfd_cand>(),
-                                     h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), 0, rank, nullptr, nullptr,
-                                     (int64_t)nkeys, st);
-                    }
-                } else {
-                    nfd_due(h->d_T.as<nf_table>(), q, p, h->n_kstate.as<uint64_t>(), nkeys, now, h->n_cand.as<nfd_cand>(),
-                            h->n_ctr.as<unsigned long long>(), nkeys, armed_flags(h), n_absent == 1 ? 1 : 0, rank, st);
+                // due keys: the armed-key list (+ the keys armed since the last pass on
+                // the first scheduler's pass, which also rebuilds the list), or every key
+                // (a voided speculative pass: the list was folded on the replayed state)
+                if (!(spec == 2 && q == 0 && si == 0)) {
+                    const bool list_pass = armed_flags(h) && h->n_arm_log.p && !(spec == 3 && q == 0 && si == 0);
+                    const int rc = due_launch(q, p, list_pass, list_pass && first_pass);
+                    if (rc) return rc;
+                    if (list_pass) first_pass = false;
+                    if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
                 }
-                hipMemcpyAsync(h->pin_rd.as<void>(PR_NC), h->n_ctr.p, 8, hipMemcpyDeviceToHost, st);
-                // the first candidates come back with the count (most passes need no second copy)
-                if (h->pin_cand.ensure((size_t)kCandSpec * sizeof(nfd_cand))) return fail(h, SH_E_OOM, "pinned staging");
-                hipMemcpyAsync(h->pin_cand.p, h->n_cand.p, (size_t)std::min<int64_t>(nkeys, kCandSpec) * sizeof(nfd_cand),
-                               hipMemcpyDeviceToHost, st);
-                if (nf_sync(h, st) != hipSuccess) return fail(h, SH_E_HIP, "k_nfa_due");
                 nc = *h->pin_rd.as<unsigned long long>(PR_NC);
             }
             if (nc == 0 && !h->coord_on) continue;
