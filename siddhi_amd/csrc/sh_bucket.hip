@@ -1270,6 +1270,299 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggc(shb_plan P, shb_aggc A) {
 #undef AGC_PROF
 }
 
+// the aggregate carry with the additions in parallel (k_bk_aggp, the default carry):
+// the chunk's consumers sorted by local key as in k_bk_aggc, then their rows in that
+// order -- each key's rows of the chunk one contiguous run, in the reference's order --
+// get a block-wide segmented prefix per output plus the key's running value from the
+// earlier chunks. Exact by construction: sum(int | long) adds in 64-bit two's
+// complement (Java's long wrap-around); the double additions (sum of float / double,
+// avg of any type) run on 64-bit fixed point -- units of 2^-24 for float / double
+// arguments, of 1 for int / long -- and every addend and every running value must be
+// an integer number of units below 2^53 in magnitude, so each of Java's sequential
+// double additions is exact and equals this sum (SumAttributeAggregatorExecutor.java
+// :167-185, AvgAttributeAggregatorExecutor.java:145-155); a row that fails the test
+// sets SHB_F_AGG and the host takes the post-pass.
+#define AGP_ROWS 8192
+#define AGP_LIM 9007199254740992.0  // 2^53
+
+// output o's mode: 0 long wrap-around sum, 1 fixed-point double sum (avg: / count), 2 count
+__device__ __forceinline__ int agp_mode(const shb_aggc& A, int o, int* type) {
+    const int kind = A.kind[o];
+    if (kind == SH_AGG_COUNT) return 2;
+    const int sd = A.side[o];
+    *type = sd == 0 ? A.e1_type : A.e2_type[sd - 1];
+    if (kind == SH_AGG_SUM && (*type == SH_T_INT || *type == SH_T_LONG)) return 0;
+    return 1;
+}
+
+// an addend in the output's units; false: not an exact fixed-point value
+__device__ __forceinline__ bool agp_units(int mode, int type, int64_t x, int64_t* u) {
+    if (mode == 0) {
+        *u = type == SH_T_INT ? (int64_t)(int32_t)x : x;
+        return true;
+    }
+    double d;
+    switch (type) {
+        case SH_T_INT: d = (double)(int32_t)x; break;
+        case SH_T_LONG: d = (double)x; break;
+        case SH_T_FLOAT: d = (double)__uint_as_float((uint32_t)x); break;
+        default: d = __longlong_as_double(x);
+    }
+    if (type == SH_T_FLOAT || type == SH_T_DOUBLE) d *= 16777216.0;  // 2^24: exact
+    if (!(d == d) || fabs(d) >= AGP_LIM || d != trunc(d)) return false;
+    *u = (int64_t)d;
+    return true;
+}
+
+__global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
+    __shared__ int64_t st_acc[SHB_MAX_AGG][256];
+    __shared__ int64_t st_cnt[256];
+    __shared__ uint32_t c_key[AGC_CH];   // local key | count << 16
+    __shared__ uint16_t c_pre[AGC_CH];   // the consumer's first row in the chunk (arrival order)
+    __shared__ uint32_t c_mp[AGC_CH];    // ... its match-stream position
+    __shared__ uint32_t c_gi[AGC_CH];    // ... its slot
+    __shared__ uint16_t o_a[AGC_CH], o_b[AGC_CH];
+    __shared__ uint16_t rs[AGC_CH + 1];  // sorted consumer -> its first row in key order
+    __shared__ uint16_t run_q[257];      // key run -> its first sorted consumer
+    __shared__ int s_nruns;
+    __shared__ uint16_t rq[AGP_ROWS];    // row in key order -> its sorted consumer
+    __shared__ uint32_t wc[AGC_TPB / 64][64];
+    __shared__ uint32_t ws[AGC_TPB / 64];
+    __shared__ uint32_t seg_p[SHB_CT_MAX + 1], seg_g[SHB_CT_MAX];
+    __shared__ uint8_t seg_of[AGC_CH / 32];
+    __shared__ int s_bad;
+    const int b = blockIdx.x;
+    const int kb = P.kb;
+    const uint32_t kmask = (1u << kb) - 1u;
+    const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
+    for (int k = threadIdx.x; k < 256; k += AGC_TPB) {
+        st_cnt[k] = 0;
+        for (int o = 0; o < SHB_MAX_AGG; o++) st_acc[o][k] = 0;
+    }
+    if (threadIdx.x == 0) s_bad = 0;
+    const uint32_t* e1src = A.e1_col >= 0 ? (const uint32_t*)P.ms[A.e1_col] : nullptr;
+    const void* e2src = A.e2_col[0] >= 0 ? P.st_dst[A.e2_col[0]] : nullptr;
+    const uint32_t* e2srn = A.e2_col[1] >= 0 ? (const uint32_t*)P.st_dst[A.e2_col[1]] : nullptr;
+    unsigned long long t_prev = wall_clock64();
+#define AGP_PROF(ph)                                                                 \
+    if (P.prof && threadIdx.x == 0) {                                                \
+        const unsigned long long t_now = wall_clock64();                             \
+        atomicAdd(&P.prof[8 + (ph)], t_now - t_prev);                                \
+        t_prev = t_now;                                                              \
+    }
+    for (int a = 0; a < P.nt;) {
+        __syncthreads();
+        const int nseg = P.nt - a < SHB_CT_MAX ? P.nt - a : SHB_CT_MAX;
+        uint32_t len = 0u, g = 0u;
+        if ((int)threadIdx.x < nseg) {
+            const int T = a + (int)threadIdx.x;
+            const uint32_t lo = P.tofft[(int64_t)b * P.tstride + T], hi = P.tofft[(int64_t)(b + 1) * P.tstride + T];
+            len = hi - lo;
+            g = ((uint32_t)T << SHB_TILE_SHIFT) + lo;
+        }
+        {
+            uint32_t tot;
+            const uint32_t pre = shw_block_excl<AGC_TPB>(len, ws, &tot);
+            if ((int)threadIdx.x < nseg) {
+                seg_p[threadIdx.x] = pre;
+                seg_g[threadIdx.x] = g;
+            }
+            if ((int)threadIdx.x == nseg) seg_p[nseg] = tot;
+        }
+        __syncthreads();
+        const int ne = __syncthreads_count((int)threadIdx.x < nseg && seg_p[threadIdx.x + 1] <= AGC_CH);
+        if (ne == 0) {
+            if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_AGG);
+            return;  // (uniform) the host runs the post-pass instead
+        }
+        const int L = (int)seg_p[ne];
+        for (int j = (int)threadIdx.x; j * 32 < L; j += AGC_TPB) {
+            const uint32_t e = (uint32_t)j * 32u;
+            int lo = 0, hi = ne - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (seg_p[mid] <= e) lo = mid;
+                else hi = mid - 1;
+            }
+            seg_of[j] = (uint8_t)lo;
+        }
+        __syncthreads();
+        // the chunk's consumers (arrival order inside the bucket): key, count, slot
+        uint32_t cc[AGC_NR];
+        int sgi[AGC_NR];
+#pragma unroll
+        for (int k = 0; k < AGC_NR; k++) {
+            const int i = (int)threadIdx.x * AGC_NR + k;  // 4 consecutive events per thread
+            cc[k] = 0u;
+            sgi[k] = 0;
+            if (i < L) {
+                int sg = seg_of[i >> 5];
+                while (seg_p[sg + 1] <= (uint32_t)i) sg++;
+                sgi[k] = sg;
+                const uint32_t gi = seg_g[sg] + ((uint32_t)i - seg_p[sg]);
+                cc[k] = P.cnt[gi];
+                c_key[i] = (P.w0[gi] & kmask) | (cc[k] << 16);
+                c_gi[i] = gi;
+            }
+        }
+        uint32_t total;
+        {
+            uint32_t sum = 0;
+#pragma unroll
+            for (int k = 0; k < AGC_NR; k++) sum += cc[k];
+            uint32_t off = shw_block_excl<AGC_TPB>(sum, ws, &total);
+#pragma unroll
+            for (int k = 0; k < AGC_NR; k++) {
+                const int i = (int)threadIdx.x * AGC_NR + k;
+                if (i < L) c_pre[i] = (uint16_t)off;
+                off += cc[k];
+            }
+        }
+        if (total > AGP_ROWS) {
+            if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_AGG);
+            return;  // (uniform: total is the block sum)
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < AGC_NR; k++) {
+            const int i = (int)threadIdx.x * AGC_NR + k;
+            if (i >= L) continue;
+            const int sg = sgi[k];
+            c_mp[i] = P.mstart[(int64_t)(a + sg) * SHB_NB + b] + c_pre[i] - c_pre[seg_p[sg]];
+        }
+        __syncthreads();
+        AGP_PROF(0)
+        // stable sort by local key (kb <= 8: 6 bits, then the high bits)
+        const uint16_t* srt = o_a;
+        s3b_sort_pass(c_key, nullptr, o_a, L, 0, wc, ws);
+        if (kb > 6) {
+            s3b_sort_pass(c_key, o_a, o_b, L, 6, wc, ws);
+            srt = o_b;
+        }
+        AGP_PROF(1)
+        // rows in key order: each sorted consumer's first row, the row -> consumer map,
+        // and the key runs (one per local key present: <= 256)
+        {
+            uint32_t c4[AGC_NR], sum = 0, nst = 0, stb = 0;
+#pragma unroll
+            for (int k = 0; k < AGC_NR; k++) {
+                const int q = (int)threadIdx.x * AGC_NR + k;
+                c4[k] = 0u;
+                if (q < L) {
+                    const uint32_t kw = c_key[srt[q]];
+                    c4[k] = kw >> 16;
+                    if (q == 0 || (c_key[srt[q - 1]] & 0xFFFFu) != (kw & 0xFFFFu)) {
+                        stb |= 1u << k;
+                        nst++;
+                    }
+                }
+                sum += c4[k];
+            }
+            uint32_t tot2, nr;
+            uint32_t off = shw_block_excl<AGC_TPB>(sum, ws, &tot2);
+            uint32_t ro = shw_block_excl<AGC_TPB>(nst, ws, &nr);
+#pragma unroll
+            for (int k = 0; k < AGC_NR; k++) {
+                const int q = (int)threadIdx.x * AGC_NR + k;
+                if (q < L) {
+                    rs[q] = (uint16_t)off;
+                    for (uint32_t m = 0; m < c4[k]; m++) rq[off + m] = (uint16_t)q;
+                    if (stb >> k & 1u) run_q[ro++] = (uint16_t)q;
+                }
+                off += c4[k];
+            }
+            if (threadIdx.x == 0) {
+                run_q[nr] = (uint16_t)L;
+                s_nruns = (int)nr;
+            }
+            rs[L] = (uint16_t)total;  // (L <= AGC_CH: the sentinel slot)
+        }
+        __syncthreads();
+        AGP_PROF(2)
+        // one wave per key run: 64 rows at a time, the count from the row's place in the
+        // run, every sum an inclusive wave prefix on top of the key's running value
+        {
+            const int nruns = s_nruns;
+            int type[SHB_MAX_AGG], mode[SHB_MAX_AGG];
+#pragma unroll
+            for (int o = 0; o < SHB_MAX_AGG; o++) {
+                type[o] = SH_T_INT;
+                mode[o] = o < A.n ? agp_mode(A, o, &type[o]) : 2;
+            }
+            bool bad = false;
+            for (int ri = wv; ri < nruns; ri += AGC_TPB / 64) {
+                const int q0 = run_q[ri], q1 = run_q[ri + 1];
+                const int R0 = rs[q0], R1 = rs[q1];
+                const uint32_t key = c_key[srt[q0]] & 0xFFFFu;
+                int64_t acc[SHB_MAX_AGG];
+#pragma unroll
+                for (int o = 0; o < SHB_MAX_AGG; o++) acc[o] = st_acc[o][key];
+                const int64_t n0 = st_cnt[key];
+                for (int r0 = R0; r0 < R1; r0 += 64) {
+                    const int r = r0 + lane;
+                    const bool ok = r < R1;
+                    uint32_t mp = 0u, gi = 0u;
+                    int64_t x1 = 0, x2 = 0, x3 = 0;
+                    if (ok) {
+                        const uint32_t q = rq[r];
+                        const uint32_t cr = srt[q];
+                        mp = c_mp[cr] + (uint32_t)(r - rs[q]);
+                        gi = c_gi[cr];
+                        if (e1src) x1 = (int64_t)e1src[mp];
+                        if (e2src) x2 = agc_load(e2src, gi, A.e2_type[0]);
+                        if (e2srn) x3 = (int64_t)e2srn[gi];
+                    }
+                    const int64_t n = n0 + (r + 1 - R0);
+#pragma unroll
+                    for (int o = 0; o < SHB_MAX_AGG; o++) {
+                        if (o >= A.n) break;
+                        int64_t* out = (int64_t*)A.out[o];
+                        if (mode[o] == 2) {
+                            if (ok) out[mp] = n;
+                            continue;
+                        }
+                        const int sd = A.side[o];
+                        int64_t u = 0;
+                        if (ok) bad |= !agp_units(mode[o], type[o], sd == 0 ? x1 : (sd == 1 ? x2 : x3), &u);
+#pragma unroll
+                        for (int d = 1; d < 64; d <<= 1) {
+                            const int64_t t = __shfl_up(u, d);
+                            if (lane >= d) u = (int64_t)((uint64_t)u + (uint64_t)t);
+                        }
+                        const int64_t v = (int64_t)((uint64_t)acc[o] + (uint64_t)u);
+                        if (ok) {
+                            if (mode[o] == 0) {
+                                out[mp] = v;
+                            } else {
+                                double d = (double)v;
+                                bad |= fabs(d) >= AGP_LIM;
+                                if (type[o] == SH_T_FLOAT || type[o] == SH_T_DOUBLE) d *= 5.9604644775390625e-08;  // 2^-24: exact
+                                if (A.kind[o] == SH_AGG_AVG) d = d / (double)n;
+                                out[mp] = __double_as_longlong(d);
+                            }
+                        }
+                        acc[o] = __shfl(v, 63);  // (rows past the run add 0)
+                    }
+                }
+                if (lane == 0) {
+#pragma unroll
+                    for (int o = 0; o < SHB_MAX_AGG; o++) st_acc[o][key] = acc[o];
+                    st_cnt[key] = n0 + (R1 - R0);
+                }
+            }
+            if (bad) s_bad = 1;
+        }
+        __syncthreads();
+        if (s_bad) {
+            if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_AGG);
+            return;  // (uniform: read after the barrier) the host takes the post-pass
+        }
+        AGP_PROF(3)
+        a += ne;
+    }
+#undef AGP_PROF
+}
+
 // ---------------------------------------------------------------- launches
 static int bk_ok() { return hipGetLastError() == hipSuccess ? 0 : -3; }
 
@@ -1334,7 +1627,10 @@ extern "C" int shb_s3_carry(const shb_plan* P, const shb_s3* S, void* stream) {
 extern "C" int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream) {
     static_assert(AGC_TPB == S3B_TPB && AGC_CH == S3B_CH, "the sort pass shape");
     if (P->kb > 8 || A->n < 1 || A->n > SHB_MAX_AGG) return -1;
-    hipLaunchKernelGGL(k_bk_aggc, dim3(SHB_NB), dim3(AGC_TPB), 0, (hipStream_t)stream, *P, *A);
+    if (A->parallel)
+        hipLaunchKernelGGL(k_bk_aggp, dim3(SHB_NB), dim3(AGC_TPB), 0, (hipStream_t)stream, *P, *A);
+    else
+        hipLaunchKernelGGL(k_bk_aggc, dim3(SHB_NB), dim3(AGC_TPB), 0, (hipStream_t)stream, *P, *A);
     return bk_ok();
 }
 

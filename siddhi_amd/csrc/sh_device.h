@@ -176,6 +176,8 @@ struct shb_aggc {
     int32_t kind[SHB_MAX_AGG];    // SH_AGG_SUM / AVG / COUNT
     int32_t side[SHB_MAX_AGG];    // 0: e1, 1: e2 column 0, 2: e2 column 1, 3: none
     void* out[SHB_MAX_AGG];       // [match-stream positions] int64 / double bits
+    int32_t parallel;             // 1: k_bk_aggp (segmented prefix, exact fixed point), 0: k_bk_aggc
+    int32_t pad;
 };
 
 // typed output columns (sh_device_run.d_out_cols) instead of raw 8-byte rows

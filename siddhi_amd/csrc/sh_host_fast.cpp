@@ -628,10 +628,15 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     shb_aggc AG;
     memset(&AG, 0, sizeof(AG));
     AG.e1_col = AG.e2_col[0] = AG.e2_col[1] = -1;
-    // (k_bk_aggc walks every key of a bucket in one workgroup: C2's 40 keys per bucket
-    // leave most lanes idle -- 28 ms against the post-pass's 8.7 -- so it runs when the
-    // post-pass refuses (its double additions are not exact in parallel) or SH_BK_AGGC=1)
-    bool carry = P.agg_post && !getenv("SH_BK_AGG_POST") && (force_carry || getenv("SH_BK_AGGC"));
+    // k_bk_aggp first (the additions as a segmented prefix, exact in 64-bit fixed point,
+    // refused on the device by a value that is not); k_bk_aggc (every key of a bucket
+    // walked in one workgroup: C2's 40 keys per bucket leave most lanes idle -- 28 ms
+    // against the post-pass's 8.7) when the post-pass refuses too, or SH_BK_AGGC=1
+    const bool aggc_env = getenv("SH_BK_AGGC") != nullptr;
+    const bool aggp_off = getenv("SH_BK_AGGP") && getenv("SH_BK_AGGP")[0] == '0';
+    const bool par = !force_carry && !aggc_env && !aggp_off && !h->aggp_skip && run->n < ((int64_t)1 << 31);
+    bool carry = P.agg_post && !getenv("SH_BK_AGG_POST") && (force_carry || aggc_env || par);
+    AG.parallel = par ? 1 : 0;
     int agg_of[SHB_MAX_OUT];
     for (int o = 0; o < P.n_out; o++) agg_of[o] = -1;
     for (int o = 0; o < P.n_out && carry; o++) {
@@ -781,7 +786,11 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
         fprintf(stderr, "[shb_match clock ticks, sum over workgroups] table %llu load %llu rank %llu walk %llu "
                         "scan+psum %llu emit %llu\n",
                 pr[5], pr[0], pr[1], pr[2], pr[3], pr[4]);
-        if (carry)
+        if (carry && AG.parallel)
+            fprintf(stderr, "[k_bk_aggp clock ticks, sum over workgroups] table+load %llu sort %llu rows %llu "
+                            "scans %llu\n",
+                    pr[8], pr[9], pr[10], pr[11]);
+        else if (carry)
             fprintf(stderr, "[k_bk_aggc clock ticks, sum over workgroups] table %llu load+prefix %llu e1 %llu "
                             "sort %llu walk %llu\n",
                     pr[8], pr[9], pr[10], pr[11], pr[12]);
@@ -800,6 +809,14 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
         }
         return run_bucket(h, run, nkeys, force_carry);
     }
+    if (flag == SHB_F_AGG && carry && AG.parallel) {
+        // a value the fixed point cannot hold exactly (or a chunk too dense): the
+        // batch again without the carry, the post-pass (or k_bk_aggc) adding instead
+        h->aggp_skip = true;
+        const int rc = run_bucket(h, run, nkeys, force_carry);
+        h->aggp_skip = false;
+        return rc;
+    }
     if (flag) return 1;
     run->out_count = total;
     if (total > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
@@ -812,7 +829,7 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     h->bk_last = 1;
     h->stk_last = stk ? 1 : 0;
     h->bk_agg_carried = carry;
-    if (carry) h->agg_last = 4;
+    if (carry) h->agg_last = AG.parallel ? 5 : 4;
     return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "bucket engine");
 }
 

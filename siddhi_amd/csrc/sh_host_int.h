@@ -342,6 +342,7 @@ struct sh_handle {
     int stk_refused = 0;          // the device flags of the last refused stack-matcher run (diagnostics)
     shj_stack stk{};
     bool stk_skip = false;        // the next bucketed run takes the sort-and-walk matcher
+    bool aggp_skip = false;  // run_bucket: this batch without k_bk_aggp (it refused a value)
     int stk_cap = 0;              // spilled entries per key (0: from the first batch's rate)
     DevBuf k_spill;
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
@@ -357,7 +358,7 @@ struct sh_handle {
     // numbers when the caller wants none, and the last run's path
     DevBuf a_scratch, a_seq;
     int agg_last = 0;  // 1: post-pass done, 2: post-pass not exact -> sequential engine, 3: in the k_seq3s lanes,
-                       // 4: carried per key by the bucketed engine (k_bk_aggc)
+                       // 4: carried per key by the bucketed engine (k_bk_aggc), 5: ... in parallel (k_bk_aggp)
     std::vector<int32_t> out_types;  // per select position over the queries (-2: types differ)
     uint64_t fp = 0;                 // compiled-program fingerprint (snapshot images)
 };

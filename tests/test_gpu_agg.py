@@ -1,7 +1,8 @@
 """Select-clause aggregators on the fast engines. The bucketed engine (C2 shape)
-carries every key's running sum / avg / count across its buckets in arrival
-order (k_bk_aggc, agg_status 4: the reference's own sequence of additions) when the
-post-pass refuses or SH_BK_AGGC=1; the
+carries every key's running sum / avg / count across its buckets: by default as a
+segmented prefix in 64-bit fixed point, exact by construction (k_bk_aggp,
+agg_status 5), and in arrival order (k_bk_aggc, agg_status 4: the reference's own
+sequence of additions) when that and the post-pass refuse or SH_BK_AGGC=1; the
 window engine (C1), the rise-and-fall key-segment engine (C3) and the rule set
 (C5) write the aggregators' arguments and the sh_agg.hip post-pass forms the
 running values per (query, partition key) in match order after proving the
@@ -65,17 +66,20 @@ def _oracle(text, ts, cols, keys):
     return out
 
 
-@pytest.mark.parametrize("carry", [False, True])
+@pytest.mark.parametrize("carry", ["aggp", "post", "aggc"])
 @pytest.mark.parametrize("n,K", [(400_000, 2_000), (300_000, 20_000)])
 def test_c2_aggregates_bucketed_vs_oracle(n, K, carry, monkeypatch):
-    """default: the post-pass (status 1); SH_BK_AGGC=1: the per-key carry (status 4)"""
+    """default: the parallel fixed-point carry (k_bk_aggp, status 5); SH_BK_AGGP=0: the
+    post-pass (status 1); SH_BK_AGGC=1: the sequential per-key carry (status 4)"""
     from siddhi_amd import synth
-    if carry:
+    if carry == "aggc":
         monkeypatch.setenv("SH_BK_AGGC", "1")
+    if carry == "post":
+        monkeypatch.setenv("SH_BK_AGGP", "0")
     ts, k, p, v = synth.stock_stream(n, K, 100)
     (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], K)
     ref = _oracle(C2_AGG, ts, [k, p, v], k)
-    assert st["bucket"] == 1 and st["agg"] == (4 if carry else 1), st
+    assert st["bucket"] == 1 and st["agg"] == {"aggp": 5, "post": 1, "aggc": 4}[carry], st
     assert m == len(ref["seq"]) > 0
     assert np.array_equal(seq, ref["seq"].astype(np.int64))
     assert np.array_equal(vals, ref["values"])
@@ -124,8 +128,9 @@ def test_c5_aggregates_rule_set_vs_oracle():
 
 @pytest.mark.parametrize("post", [False, True])
 def test_rounding_additions_stay_exact(post, monkeypatch):
-    """prices spanning 2^-60 .. 2^60: the double additions round. The post-pass
-    refuses, and the carry adds in the reference's sequence instead (agg_status 4);
+    """prices spanning 2^-60 .. 2^60: the double additions round. The parallel carry
+    (k_bk_aggp) and the post-pass refuse, and the sequential carry adds in the
+    reference's sequence instead (agg_status 4);
     with SH_BK_AGG_POST=1 the sequential engine's sums are returned (agg_status 2);
     both == the oracle's"""
     from siddhi_amd import synth
@@ -151,7 +156,7 @@ def test_c2_aggregates_full_size_vs_restatement():
     from siddhi_amd import synth
     ts, k, p, v = synth.stock_stream(100_000_000, 10_000, 100)
     (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], 10_000)
-    assert st["bucket"] == 1 and st["agg"] == 1, st
+    assert st["bucket"] == 1 and st["agg"] == 5, st
     eseq, ev = c2_expected(ts, k, p, v)
     assert np.array_equal(seq, eseq)
     grp = k[eseq].astype(np.int64)
