@@ -589,9 +589,9 @@ def main():
     # + pad 4 + v2 8 = 32 B per match, two 16-byte stores) by default; raw rows
     # (seq 8 apart + four 8-byte words, 40 B) or typed columns (28 B in five
     # arrays: more store instructions, measured slower) on request
-    # (the aggregate variant's post-pass works on raw rows: packed rows would add a
-    # conversion pass, so --agg defaults to raw rows)
-    layout = (args.layout or ("columns" if args.columns else ("raw" if args.agg else "packed"))
+    # (--agg too: the bucketed engine's aggregate carry hands the running values to
+    # the emitter, which packs them like any 8-byte column: + total 8 + a1 8 = 48 B)
+    layout = (args.layout or ("columns" if args.columns else "packed")
               if args.config == "c2" else "raw")
     use_cols = layout == "columns"
     use_packed = layout == "packed"

@@ -1388,18 +1388,20 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
         }
         __syncthreads();
         // the chunk's consumers (arrival order inside the bucket): key, count, slot
-        uint32_t cc[AGC_NR];
+        uint32_t cc[AGC_NR], ms0[AGC_NR];
         int sgi[AGC_NR];
 #pragma unroll
         for (int k = 0; k < AGC_NR; k++) {
             const int i = (int)threadIdx.x * AGC_NR + k;  // 4 consecutive events per thread
             cc[k] = 0u;
             sgi[k] = 0;
+            ms0[k] = 0u;
             if (i < L) {
                 int sg = seg_of[i >> 5];
                 while (seg_p[sg + 1] <= (uint32_t)i) sg++;
                 sgi[k] = sg;
                 const uint32_t gi = seg_g[sg] + ((uint32_t)i - seg_p[sg]);
+                ms0[k] = P.mstart[(int64_t)(a + sg) * SHB_NB + b];
                 cc[k] = P.cnt[gi];
                 c_key[i] = (P.w0[gi] & kmask) | (cc[k] << 16);
                 c_gi[i] = gi;
@@ -1427,8 +1429,7 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
         for (int k = 0; k < AGC_NR; k++) {
             const int i = (int)threadIdx.x * AGC_NR + k;
             if (i >= L) continue;
-            const int sg = sgi[k];
-            c_mp[i] = P.mstart[(int64_t)(a + sg) * SHB_NB + b] + c_pre[i] - c_pre[seg_p[sg]];
+            c_mp[i] = ms0[k] + c_pre[i] - c_pre[seg_p[sgi[k]]];
         }
         __syncthreads();
         AGP_PROF(0)
@@ -1524,11 +1525,7 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
                         const int sd = A.side[o];
                         int64_t u = 0;
                         if (ok) bad |= !agp_units(mode[o], type[o], sd == 0 ? x1 : (sd == 1 ? x2 : x3), &u);
-#pragma unroll
-                        for (int d = 1; d < 64; d <<= 1) {
-                            const int64_t t = __shfl_up(u, d);
-                            if (lane >= d) u = (int64_t)((uint64_t)u + (uint64_t)t);
-                        }
+                        u = (int64_t)shw_incl_scan64((uint64_t)u);
                         const int64_t v = (int64_t)((uint64_t)acc[o] + (uint64_t)u);
                         if (ok) {
                             if (mode[o] == 0) {
@@ -1541,7 +1538,8 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
                                 out[mp] = __double_as_longlong(d);
                             }
                         }
-                        acc[o] = __shfl(v, 63);  // (rows past the run add 0)
+                        acc[o] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)v >> 32), 63) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readlane((int)v, 63));  // (rows past the run add 0)
                     }
                 }
                 if (lane == 0) {
@@ -1638,8 +1636,12 @@ template <int MODE, int NO>
 static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& OC, uint64_t seq_base,
                            uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
     // 6 rows per lane and round up to 4 values (1.505 vs 1.526 ms for 4 on C2,
-    // profiles/r4_c2_emit_ru_ab.txt), 4 beyond (registers)
-    constexpr int RU = (NO >= 1 && NO <= 4) ? 6 : 4;
+    // profiles/r4_c2_emit_ru_ab.txt), fewer beyond: as many as fit 128 VGPRs without
+    // spilling (packed rows and typed columns hold more per row than raw ones)
+    constexpr int RU = (NO >= 1 && NO <= 4) ? (MODE == SHB_OUT_COLS && NO == 4 ? 4 : 6)
+                                            : (MODE == SHB_OUT_RAW ? (NO <= 6 ? 4 : 3)
+                                                                   : (MODE == SHB_OUT_PACKED ? (NO <= 6 ? 2 : 1)
+                                                                                             : (NO <= 5 ? 2 : 1)));
     hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P, *O,
                        OC, seq_base, out_seq, out_vals, out_cap);
 }

@@ -1455,6 +1455,15 @@ static int run_device_impl(sh_handle* h, sh_device_run* run) {
     const bool aggp = h->prog.agg_post != 0;
     bool sequential = false;
     if (aggp) {
+        if (h->prog.window_ok && h->out_mode != SHB_OUT_RAW && !h->cols_rows && !getenv("SH_BK_AGG_POST")) {
+            // packed rows / typed columns straight from the bucketed engine when its
+            // parallel carry takes the batch (the post-pass works on raw rows)
+            h->aggp_only = true;
+            const int brc = run_bucket(h, run, nkeys);
+            h->aggp_only = false;
+            if (brc == SH_OK && h->bk_agg_carried) return SH_OK;
+            if (brc != SH_OK && brc != 1) return brc;
+        }
         const int crc = rows_for_cols(h, run);
         if (crc) return crc;
         if (!run->d_out_seq) {

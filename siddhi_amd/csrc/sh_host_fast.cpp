@@ -711,6 +711,7 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
                 O.type[o] = P.out_type[o];
             }
     }
+    if (h->aggp_only && !(carry && AG.parallel)) return 1;
     h->bk_agg_carried = false;
     shb_cols OC;
     memset(&OC, 0, sizeof(OC));
@@ -812,6 +813,7 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     if (flag == SHB_F_AGG && carry && AG.parallel) {
         // a value the fixed point cannot hold exactly (or a chunk too dense): the
         // batch again without the carry, the post-pass (or k_bk_aggc) adding instead
+        if (h->aggp_only) return 1;  // (the caller's raw rows first)
         h->aggp_skip = true;
         const int rc = run_bucket(h, run, nkeys, force_carry);
         h->aggp_skip = false;

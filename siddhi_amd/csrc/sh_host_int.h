@@ -343,6 +343,7 @@ struct sh_handle {
     shj_stack stk{};
     bool stk_skip = false;        // the next bucketed run takes the sort-and-walk matcher
     bool aggp_skip = false;  // run_bucket: this batch without k_bk_aggp (it refused a value)
+    bool aggp_only = false;  // run_bucket: k_bk_aggp or nothing (1), the caller's layout kept
     int stk_cap = 0;              // spilled entries per key (0: from the first batch's rate)
     DevBuf k_spill;
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows

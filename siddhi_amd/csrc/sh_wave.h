@@ -38,6 +38,32 @@ __device__ __forceinline__ uint32_t shw_incl_scan(uint32_t v) {
     return v;
 }
 
+template <int CTRL>
+__device__ __forceinline__ uint64_t shw_move64(uint64_t v) {
+    const uint32_t lo = shw_move<CTRL>((uint32_t)v), hi = shw_move<CTRL>((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// inclusive prefix sum of 64-bit values (two's complement: wraps like Java's long)
+__device__ __forceinline__ uint64_t shw_incl_scan64(uint64_t v) {
+    const int lane = threadIdx.x & 63;
+    const int rl = lane & 15;
+    uint64_t t;
+    t = shw_move64<SHW_ROW_SHR(1)>(v);
+    if (rl >= 1) v += t;
+    t = shw_move64<SHW_ROW_SHR(2)>(v);
+    if (rl >= 2) v += t;
+    t = shw_move64<SHW_ROW_SHR(4)>(v);
+    if (rl >= 4) v += t;
+    t = shw_move64<SHW_ROW_SHR(8)>(v);
+    if (rl >= 8) v += t;
+    t = shw_move64<SHW_ROW_BCAST15>(v);
+    if ((lane & 31) >= 16) v += t;
+    t = shw_move64<SHW_ROW_BCAST31>(v);
+    if (lane >= 32) v += t;
+    return v;
+}
+
 // value of lane 63 (the wave total after an inclusive scan)
 __device__ __forceinline__ uint32_t shw_last(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
 

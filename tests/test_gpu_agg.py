@@ -36,17 +36,22 @@ def _device():
         pytest.skip("no GPU")
 
 
-def _run(text, ts, k, cols, nkeys, with_query=False):
+def _run(text, ts, k, cols, nkeys, with_query=False, packed=False):
     import torch
     from siddhi_amd import compiler
-    from siddhi_amd.device_run import DeviceRunner
+    from siddhi_amd.device_run import DeviceRunner, packed_to_raw
     r = DeviceRunner(compiler.compile_app(text))
     dev = torch.device("cuda:0")
     tk = torch.from_numpy(k).to(dev)
     res = r.run(torch.from_numpy(ts).to(dev), tk, [torch.from_numpy(c).to(dev) for c in cols], nkeys,
-                with_query=with_query)
+                with_query=with_query, packed=packed)
     torch.cuda.synchronize()
-    out = [res[0]] + [x.cpu().numpy() for x in res[1:]]
+    if packed:
+        offs, rb = r.packed_layout()
+        oseq, ovals = packed_to_raw(res[1].cpu().numpy(), r.out_types, offs, rb)
+        out = [res[0], oseq.view(np.int64), ovals]
+    else:
+        out = [res[0]] + [x.cpu().numpy() for x in res[1:]]
     st = dict(agg=r.agg_status(), bucket=r.bucket_status(), seq3=r.seq3_status())
     r.close()
     return out, st
@@ -66,18 +71,21 @@ def _oracle(text, ts, cols, keys):
     return out
 
 
-@pytest.mark.parametrize("carry", ["aggp", "post", "aggc"])
+@pytest.mark.parametrize("carry", ["aggp", "post", "aggc", "aggp-packed", "aggc-packed"])
 @pytest.mark.parametrize("n,K", [(400_000, 2_000), (300_000, 20_000)])
 def test_c2_aggregates_bucketed_vs_oracle(n, K, carry, monkeypatch):
     """default: the parallel fixed-point carry (k_bk_aggp, status 5); SH_BK_AGGP=0: the
-    post-pass (status 1); SH_BK_AGGC=1: the sequential per-key carry (status 4)"""
+    post-pass (status 1); SH_BK_AGGC=1: the sequential per-key carry (status 4); the
+    carries into SH_OUT_PACKED rows too"""
     from siddhi_amd import synth
+    packed = carry.endswith("-packed")
+    carry = carry.replace("-packed", "")
     if carry == "aggc":
         monkeypatch.setenv("SH_BK_AGGC", "1")
     if carry == "post":
         monkeypatch.setenv("SH_BK_AGGP", "0")
     ts, k, p, v = synth.stock_stream(n, K, 100)
-    (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], K)
+    (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], K, packed=packed)
     ref = _oracle(C2_AGG, ts, [k, p, v], k)
     assert st["bucket"] == 1 and st["agg"] == {"aggp": 5, "post": 1, "aggc": 4}[carry], st
     assert m == len(ref["seq"]) > 0
