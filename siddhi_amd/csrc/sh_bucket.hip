@@ -261,14 +261,17 @@ __global__ void __launch_bounds__(TPB, MINW) k_bk_scatter(const int32_t* __restr
 #define BK_EROWS 1024  // rows the wave's map holds per pass (more: event-parallel writes)
 
 // select value o of a row (raw 8-byte form)
-#define BK_VAL(o, i, mp) bk_raw(O.src[o], O.kind[o] == 1 ? (i) : (mp), O.type[o])
+// (kind 0: by match-stream position, 1: by event, 2: by output row -- the aggregate carry's
+// running values, SHB_OUT_KIND_ROW)
+#define BK_VAL(o, i, mp, row) \
+    bk_raw(O.src[o], O.kind[o] == 1 ? (i) : (O.kind[o] == SHB_OUT_KIND_ROW ? (row) : (mp)), O.type[o])
 
 
 // the select values of a row (NO > 0: unrolled, the descriptors in scalar registers)
 template <int NO>
-__device__ __forceinline__ void bk_vals(const shb_out& O, int64_t i, int64_t mp, int64_t* v) {
+__device__ __forceinline__ void bk_vals(const shb_out& O, int64_t i, int64_t mp, int64_t row, int64_t* v) {
 #pragma unroll
-    for (int o = 0; o < NO; o++) v[o] = BK_VAL(o, i, mp);
+    for (int o = 0; o < NO; o++) v[o] = BK_VAL(o, i, mp, row);
 }
 
 
@@ -279,7 +282,7 @@ __device__ __forceinline__ void bk_row(const shb_out& O, const shb_cols& OC, con
                                        int64_t* __restrict__ out_vals) {
     if (NO > 0) {
         int64_t v[NO > 0 ? NO : 1];
-        bk_vals<NO>(O, i, mp, v);
+        bk_vals<NO>(O, i, mp, row, v);
         bk_store<MODE, NO>(OC, row, v, seq, out_seq, out_vals);
         return;
     }
@@ -294,7 +297,7 @@ __device__ __forceinline__ void bk_row(const shb_out& O, const shb_cols& OC, con
         out_seq[row] = seq;
     }
     for (int o = 0; o < no; o++) {
-        const int64_t v = bk_raw(o_src[o], o_kind[o] == 1 ? i : mp, o_type[o]);
+        const int64_t v = bk_raw(o_src[o], o_kind[o] == 1 ? i : (o_kind[o] == SHB_OUT_KIND_ROW ? row : mp), o_type[o]);
         if (MODE == SHB_OUT_PACKED) {
             uint32_t* r = (uint32_t*)OC.rows + row * OC.rw + OC.woff[o];
             r[0] = OC.colw[o] == 1 ? (uint32_t)(uint8_t)v : (uint32_t)v;
@@ -494,7 +497,7 @@ __global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, sh
                             const int e = rmap[w][t];
                             const uint32_t k = t - ero[w][e];
                             ii[u] = ib + e;
-                            bk_vals<NV>(O, ii[u], (int64_t)emp[w][e] + k, v[u]);
+                            bk_vals<NV>(O, ii[u], (int64_t)emp[w][e] + k, (int64_t)rb + t, v[u]);
                         }
                     }
 #pragma unroll
@@ -652,6 +655,60 @@ __device__ __forceinline__ void s3b_sort_pass(const uint32_t* __restrict__ c_key
 #pragma unroll
     for (int r = 0; r < S3B_NR; r++)
         if (rk[r] != ~0u) out[wc[w][dg[r]] + rk[r]] = (uint16_t)ix[r];
+    __syncthreads();
+}
+
+// one stable multisplit pass over the low 8 bits of the local key (kb <= 8: the whole
+// key in one pass instead of two 6-bit ones); wc8: S3B_W x 256 counters
+__device__ __forceinline__ void s3b_sort_pass8(const uint32_t* __restrict__ c_key, uint16_t* out, int L,
+                                               uint32_t (*wc8)[256], uint32_t* ws) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int c = threadIdx.x; c < S3B_W * 256; c += S3B_TPB) (&wc8[0][0])[c] = 0u;
+    __syncthreads();
+    uint32_t rk[S3B_NR], dg[S3B_NR];
+#pragma unroll
+    for (int r = 0; r < S3B_NR; r++) {
+        const int pos = (w * S3B_NR + r) * 64 + lane;  // wave w owns positions [w * 256, w * 256 + 256)
+        const bool valid = pos < L;
+        const uint32_t d = valid ? c_key[pos] & 255u : 0u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bb = 0; bb < 8; bb++) {
+            const bool bit = (d >> bb) & 1u;
+            const uint64_t m = __ballot(valid && bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t r_ = (uint32_t)__popcll(peers & lt);
+        const uint32_t base = valid ? wc8[w][d] : 0u;
+        if (valid && r_ == 0) wc8[w][d] = base + (uint32_t)__popcll(peers);
+        rk[r] = valid ? base + r_ : ~0u;
+        dg[r] = d;
+    }
+    __syncthreads();
+    // (digit, wave) exclusive offsets, digit-major: thread t takes digit t / 4, waves
+    // 4 (t % 4) .. 4 (t % 4) + 3
+    {
+        const int d = threadIdx.x >> 2, q0 = (threadIdx.x & 3) * 4;
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = wc8[q0 + k][d];
+            sum += v[k];
+        }
+        uint32_t tot;
+        uint32_t ex = shw_block_excl<S3B_TPB>(sum, ws, &tot);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            wc8[q0 + k][d] = ex;
+            ex += v[k];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < S3B_NR; r++)
+        if (rk[r] != ~0u) out[wc8[w][dg[r]] + rk[r]] = (uint16_t)((w * S3B_NR + r) * 64 + lane);
     __syncthreads();
 }
 
@@ -1321,12 +1378,13 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
     __shared__ uint16_t c_pre[AGC_CH];   // the consumer's first row in the chunk (arrival order)
     __shared__ uint32_t c_mp[AGC_CH];    // ... its match-stream position
     __shared__ uint32_t c_gi[AGC_CH];    // ... its slot
-    __shared__ uint16_t o_a[AGC_CH], o_b[AGC_CH];
+    __shared__ uint32_t c_wp[AGC_CH];    // ... its first row's output index (by_row) or position
+    __shared__ uint16_t o_a[AGC_CH];
     __shared__ uint16_t rs[AGC_CH + 1];  // sorted consumer -> its first row in key order
     __shared__ uint16_t run_q[257];      // key run -> its first sorted consumer
     __shared__ int s_nruns;
     __shared__ uint16_t rq[AGP_ROWS];    // row in key order -> its sorted consumer
-    __shared__ uint32_t wc[AGC_TPB / 64][64];
+    __shared__ uint32_t wc8[AGC_TPB / 64][256];
     __shared__ uint32_t ws[AGC_TPB / 64];
     __shared__ uint32_t seg_p[SHB_CT_MAX + 1], seg_g[SHB_CT_MAX];
     __shared__ uint8_t seg_of[AGC_CH / 32];
@@ -1430,16 +1488,13 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
             const int i = (int)threadIdx.x * AGC_NR + k;
             if (i >= L) continue;
             c_mp[i] = ms0[k] + c_pre[i] - c_pre[seg_p[sgi[k]]];
+            if (A.by_row) c_wp[i] = A.roff[c_gi[i]];
         }
         __syncthreads();
         AGP_PROF(0)
         // stable sort by local key (kb <= 8: 6 bits, then the high bits)
         const uint16_t* srt = o_a;
-        s3b_sort_pass(c_key, nullptr, o_a, L, 0, wc, ws);
-        if (kb > 6) {
-            s3b_sort_pass(c_key, o_a, o_b, L, 6, wc, ws);
-            srt = o_b;
-        }
+        s3b_sort_pass8(c_key, o_a, L, wc8, ws);
         AGP_PROF(1)
         // rows in key order: each sorted consumer's first row, the row -> consumer map,
         // and the key runs (one per local key present: <= 256)
@@ -1502,12 +1557,14 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
                 for (int r0 = R0; r0 < R1; r0 += 64) {
                     const int r = r0 + lane;
                     const bool ok = r < R1;
-                    uint32_t mp = 0u, gi = 0u;
+                    uint32_t mp = 0u, gi = 0u, wp = 0u;
                     int64_t x1 = 0, x2 = 0, x3 = 0;
                     if (ok) {
                         const uint32_t q = rq[r];
                         const uint32_t cr = srt[q];
-                        mp = c_mp[cr] + (uint32_t)(r - rs[q]);
+                        const uint32_t m = (uint32_t)(r - rs[q]);
+                        mp = c_mp[cr] + m;
+                        wp = A.by_row ? c_wp[cr] + m : mp;
                         gi = c_gi[cr];
                         if (e1src) x1 = (int64_t)e1src[mp];
                         if (e2src) x2 = agc_load(e2src, gi, A.e2_type[0]);
@@ -1519,7 +1576,7 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
                         if (o >= A.n) break;
                         int64_t* out = (int64_t*)A.out[o];
                         if (mode[o] == 2) {
-                            if (ok) out[mp] = n;
+                            if (ok) out[wp] = n;
                             continue;
                         }
                         const int sd = A.side[o];
@@ -1529,13 +1586,13 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
                         const int64_t v = (int64_t)((uint64_t)acc[o] + (uint64_t)u);
                         if (ok) {
                             if (mode[o] == 0) {
-                                out[mp] = v;
+                                out[wp] = v;
                             } else {
                                 double d = (double)v;
                                 bad |= fabs(d) >= AGP_LIM;
                                 if (type[o] == SH_T_FLOAT || type[o] == SH_T_DOUBLE) d *= 5.9604644775390625e-08;  // 2^-24: exact
                                 if (A.kind[o] == SH_AGG_AVG) d = d / (double)n;
-                                out[mp] = __double_as_longlong(d);
+                                out[wp] = __double_as_longlong(d);
                             }
                         }
                         acc[o] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)v >> 32), 63) << 32) |
@@ -1622,9 +1679,41 @@ extern "C" int shb_s3_carry(const shb_plan* P, const shb_s3* S, void* stream) {
     return bk_ok();
 }
 
+// each event's first output row, by slot: the tile's first row (ttot after shb_finish)
+// + the exclusive prefix of the counts in arrival order (the emitter's own row order), so
+// that the aggregate carry writes its running values where the emitter reads them row
+// by row (contiguous) instead of by match-stream position (one line per row)
+__global__ void __launch_bounds__(1024) k_bk_rowoff(shb_plan P, uint32_t* __restrict__ roff) {
+    __shared__ uint32_t ws[16];
+    const int T = blockIdx.x;
+    const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
+    const int tile_n = (int)((P.n - b0) < SHB_TILE ? (P.n - b0) : SHB_TILE);
+    constexpr int PER = SHB_TILE / 1024;
+    uint32_t sl[PER], c[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int l = (int)threadIdx.x * PER + k;  // consecutive arrivals per thread
+        sl[k] = l < tile_n ? (uint32_t)P.sp[b0 + l] : 0u;
+        c[k] = l < tile_n ? (uint32_t)P.cnt[b0 + sl[k]] : 0u;
+        sum += c[k];
+    }
+    uint32_t tot;
+    uint32_t off = P.ttot[T] + shw_block_excl<1024>(sum, ws, &tot);
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int l = (int)threadIdx.x * PER + k;
+        if (l < tile_n) roff[b0 + sl[k]] = off;
+        off += c[k];
+    }
+}
+
 extern "C" int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream) {
     static_assert(AGC_TPB == S3B_TPB && AGC_CH == S3B_CH, "the sort pass shape");
     if (P->kb > 8 || A->n < 1 || A->n > SHB_MAX_AGG) return -1;
+    if (A->by_row) {
+        if (!A->parallel || !A->roff) return -1;
+        hipLaunchKernelGGL(k_bk_rowoff, dim3(P->nt), dim3(1024), 0, (hipStream_t)stream, *P, A->roff);
+    }
     if (A->parallel)
         hipLaunchKernelGGL(k_bk_aggp, dim3(SHB_NB), dim3(AGC_TPB), 0, (hipStream_t)stream, *P, *A);
     else

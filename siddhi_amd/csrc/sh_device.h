@@ -147,8 +147,10 @@ struct shb_out {
     int32_t pad;
     int32_t kind[SHB_MAX_OUT];
     int32_t type[SHB_MAX_OUT];    // sh_type: raw-value conversion
-    const void* src[SHB_MAX_OUT]; // kind 0: match-stream column, kind 1: consumer column
+    const void* src[SHB_MAX_OUT]; // kind 0: match-stream column, kind 1: consumer column,
+                                  // kind 2 (SHB_OUT_KIND_ROW): a column by output row
 };
+#define SHB_OUT_KIND_ROW 2
 
 // the rise-and-fall sequence (nf_query.s3) for the bucket-carry engine: every
 // operand of f2 / f3 and every e1 / e2[last] select value is one 4-byte attribute
@@ -177,7 +179,9 @@ struct shb_aggc {
     int32_t side[SHB_MAX_AGG];    // 0: e1, 1: e2 column 0, 2: e2 column 1, 3: none
     void* out[SHB_MAX_AGG];       // [match-stream positions] int64 / double bits
     int32_t parallel;             // 1: k_bk_aggp (segmented prefix, exact fixed point), 0: k_bk_aggc
-    int32_t pad;
+    int32_t by_row;               // k_bk_aggp: out[] by output row (roff, after shb_finish), else by
+                                  // match-stream position
+    uint32_t* roff;               // [slot] the event's first output row (k_bk_rowoff), by_row only
 };
 
 // typed output columns (sh_device_run.d_out_cols) instead of raw 8-byte rows

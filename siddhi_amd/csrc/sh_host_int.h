@@ -342,6 +342,7 @@ struct sh_handle {
     int stk_refused = 0;          // the device flags of the last refused stack-matcher run (diagnostics)
     shj_stack stk{};
     bool stk_skip = false;        // the next bucketed run takes the sort-and-walk matcher
+    DevBuf bk_roff;          // [slot] first output row of each event (k_bk_rowoff)
     bool aggp_skip = false;  // run_bucket: this batch without k_bk_aggp (it refused a value)
     bool aggp_only = false;  // run_bucket: k_bk_aggp or nothing (1), the caller's layout kept
     int stk_cap = 0;              // spilled entries per key (0: from the first batch's rate)

@@ -71,7 +71,7 @@ def _oracle(text, ts, cols, keys):
     return out
 
 
-@pytest.mark.parametrize("carry", ["aggp", "post", "aggc", "aggp-packed", "aggc-packed"])
+@pytest.mark.parametrize("carry", ["aggp", "post", "aggc", "aggp-packed", "aggc-packed", "aggprow-packed"])
 @pytest.mark.parametrize("n,K", [(400_000, 2_000), (300_000, 20_000)])
 def test_c2_aggregates_bucketed_vs_oracle(n, K, carry, monkeypatch):
     """default: the parallel fixed-point carry (k_bk_aggp, status 5); SH_BK_AGGP=0: the
@@ -84,6 +84,9 @@ def test_c2_aggregates_bucketed_vs_oracle(n, K, carry, monkeypatch):
         monkeypatch.setenv("SH_BK_AGGC", "1")
     if carry == "post":
         monkeypatch.setenv("SH_BK_AGGP", "0")
+    if carry == "aggprow":  # the running values by output row (k_bk_rowoff), SH_AGGP_ROW=1
+        monkeypatch.setenv("SH_AGGP_ROW", "1")
+        carry = "aggp"
     ts, k, p, v = synth.stock_stream(n, K, 100)
     (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], K, packed=packed)
     ref = _oracle(C2_AGG, ts, [k, p, v], k)
