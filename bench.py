@@ -698,7 +698,7 @@ def main():
                        "path": "pageable host numpy -> HBM (torch .to), before the timed steps"},
             "config": {"workload": W["desc"], "events_per_gpu": n, W["key_name"]: args.keys,
                        "rate_ev_per_ms": args.rate,
-                       "output": {"packed": "packed rows (SH_OUT_PACKED, 32 B per match)",
+                       "output": {"packed": f"packed rows (SH_OUT_PACKED, {48 if args.agg else 32} B per match)",
                                   "columns": "typed columns (d_out_cols)",
                                   "raw": "raw 8-byte rows (d_out_values) + trigger_seq"}[layout],
                        "matches_per_gpu": int(m),

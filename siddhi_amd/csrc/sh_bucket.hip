@@ -1731,8 +1731,11 @@ static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& 
                                             : (MODE == SHB_OUT_RAW ? (NO <= 6 ? 4 : 3)
                                                                    : (MODE == SHB_OUT_PACKED ? (NO <= 6 ? 2 : 1)
                                                                                              : (NO <= 5 ? 2 : 1)));
-    hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P, *O,
-                       OC, seq_base, out_seq, out_vals, out_cap);
+    // (SH_EMIT_LDS_PAD=<bytes>: dynamic LDS that lowers the workgroups per CU -- an L2
+    // footprint experiment)
+    static const int pad = getenv("SH_EMIT_LDS_PAD") ? atoi(getenv("SH_EMIT_LDS_PAD")) : 0;
+    hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream, *P,
+                       *O, OC, seq_base, out_seq, out_vals, out_cap);
 }
 
 template <int MODE>
