@@ -1729,7 +1729,7 @@ static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& 
     // spilling (packed rows and typed columns hold more per row than raw ones)
     constexpr int RU = (NO >= 1 && NO <= 4) ? (MODE == SHB_OUT_COLS && NO == 4 ? 4 : 6)
                                             : (MODE == SHB_OUT_RAW ? (NO <= 6 ? 4 : 3)
-                                                                   : (MODE == SHB_OUT_PACKED ? (NO <= 6 ? 2 : 1)
+                                                                   : (MODE == SHB_OUT_PACKED ? (NO <= 6 ? 4 : (NO == 7 ? 2 : 1))
                                                                                              : (NO <= 5 ? 2 : 1)));
     // (SH_EMIT_LDS_PAD=<bytes>: dynamic LDS that lowers the workgroups per CU -- an L2
     // footprint experiment)

@@ -40,28 +40,31 @@ __device__ __forceinline__ void bk_put(void* col, int w, int64_t row, int64_t v)
 template <int NO>
 __device__ __forceinline__ void bk_pack(const shb_cols& OC, int64_t row, const int64_t* v, uint64_t seq) {
     constexpr int RW = ((2 + 2 * NO) + 3) & ~3;
-    uint32_t wv[RW];
-    wv[0] = (uint32_t)seq;
-    wv[1] = (uint32_t)(seq >> 32);
-#pragma unroll
-    for (int k = 2; k < RW; k++) wv[k] = 0u;
-#pragma unroll
-    for (int o = 0; o < NO; o++) {
-        const int wo = OC.woff[o];
-        const bool wide = OC.colw[o] == 8;
-        const uint32_t lo = OC.colw[o] == 1 ? (uint32_t)(uint8_t)v[o] : (uint32_t)v[o];
-        const uint32_t hi = (uint32_t)((uint64_t)v[o] >> 32);
-#pragma unroll
-        for (int k = 2 + o; k <= 2 + 2 * o && k < RW; k++)
-            if (k == wo) wv[k] = lo;
-#pragma unroll
-        for (int k = 3 + o; k <= 3 + 2 * o && k < RW; k++)
-            if (wide && k == wo + 1) wv[k] = hi;
-    }
     uint4* dst = (uint4*)((uint32_t*)OC.rows + row * OC.rw);
+    // one 16-byte store at a time: only its four words live (registers for more rows in flight)
 #pragma unroll
-    for (int q = 0; q < RW / 4; q++)
-        if (4 * q < OC.rw) dst[q] = make_uint4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
+    for (int q = 0; q < RW / 4; q++) {
+        if (4 * q >= OC.rw) break;
+        uint32_t wv[4] = {0u, 0u, 0u, 0u};
+        if (q == 0) {
+            wv[0] = (uint32_t)seq;
+            wv[1] = (uint32_t)(seq >> 32);
+        }
+#pragma unroll
+        for (int o = 0; o < NO; o++) {
+            const int wo = OC.woff[o];
+            const bool wide = OC.colw[o] == 8;
+            const uint32_t lo = OC.colw[o] == 1 ? (uint32_t)(uint8_t)v[o] : (uint32_t)v[o];
+            const uint32_t hi = (uint32_t)((uint64_t)v[o] >> 32);
+#pragma unroll
+            for (int k = 2 + o; k <= 2 + 2 * o && k < RW; k++)
+                if (k >= 4 * q && k < 4 * q + 4 && k == wo) wv[k - 4 * q] = lo;
+#pragma unroll
+            for (int k = 3 + o; k <= 3 + 2 * o && k < RW; k++)
+                if (k >= 4 * q && k < 4 * q + 4 && wide && k == wo + 1) wv[k - 4 * q] = hi;
+        }
+        dst[q] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    }
 }
 
 // one row in the caller's layout (MODE: SHB_OUT_RAW 8-byte words + out_seq,
