@@ -313,17 +313,23 @@ __device__ __forceinline__ void bk_row(const shb_out& O, const shb_cols& OC, con
 // rows per lane whose loads are issued before their stores (the template's RU:
 // 4 or 6; a half of 512 events has ~290 rows on C2, one round of 6 x 64 rows)
 
-template <int MODE, int NO, int BK_RU>
-__global__ void __launch_bounds__(BK_TPB, 4) k_bk_emit(shb_plan P, shb_out O, shb_cols OC, uint64_t seq_base,
+template <int MODE, int NO, int BK_RU, int BK_OCC = 4>
+__global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out O, shb_cols OC, uint64_t seq_base,
                                                     uint64_t* __restrict__ out_seq, int64_t* __restrict__ out_vals,
                                                     int64_t out_cap) {
-    __shared__ uint32_t pfx[SHB_TILE + 1];
+    // the slot prefix (phases 1-2) and the row maps (phase 3) share storage: phase 3
+    // starts after the barrier that ends every wave's phase 2 (42 KB instead of 75:
+    // three workgroups per CU when the registers allow)
+    constexpr int BK_MAPW = (BK_TPB / 64) * (BK_EROWS / 2 + BK_EHALF + BK_EHALF / 2);
+    __shared__ uint32_t pool[(SHB_TILE + 1) > BK_MAPW ? (SHB_TILE + 1) : BK_MAPW];
+    uint32_t* const pfx = pool;
+    uint16_t(*const rmap)[BK_EROWS] = (uint16_t(*)[BK_EROWS])pool;
+    uint32_t(*const emp)[BK_EHALF] = (uint32_t(*)[BK_EHALF])(pool + (BK_TPB / 64) * (BK_EROWS / 2));
+    uint16_t(*const ero)[BK_EHALF] =
+        (uint16_t(*)[BK_EHALF])(pool + (BK_TPB / 64) * (BK_EROWS / 2 + BK_EHALF));
     __shared__ uint32_t ms0[SHB_NB];
     __shared__ uint16_t to[SHB_NB + 1];
     __shared__ uint32_t wtot[BK_TPB / 64], ws[BK_TPB / 64];
-    __shared__ uint16_t rmap[BK_TPB / 64][BK_EROWS];
-    __shared__ uint32_t emp[BK_TPB / 64][BK_EHALF];
-    __shared__ uint16_t ero[BK_TPB / 64][BK_EHALF];
     __shared__ int32_t o_kind[SHB_MAX_OUT], o_type[SHB_MAX_OUT];
     __shared__ const void* o_src[SHB_MAX_OUT];
     __shared__ uint32_t s_tb;
@@ -1734,8 +1740,19 @@ static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& 
     // (SH_EMIT_LDS_PAD=<bytes>: dynamic LDS that lowers the workgroups per CU -- an L2
     // footprint experiment)
     static const int pad = getenv("SH_EMIT_LDS_PAD") ? atoi(getenv("SH_EMIT_LDS_PAD")) : 0;
-    hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream, *P,
-                       *O, OC, seq_base, out_seq, out_vals, out_cap);
+    // up to 4 values: 6 waves per SIMD (<= 80 VGPRs, 2 rows per lane: three workgroups per
+    // CU on the 42 KB of LDS), C2 emit 1.40 vs 1.46 ms at 4 waves x 6 rows
+    // (profiles/r5_c2_emit_occ_ab.txt); SH_EMIT_OCC=4 / 5 for the others
+    static const int occ = getenv("SH_EMIT_OCC") ? atoi(getenv("SH_EMIT_OCC")) : 6;
+    if (occ == 6 && NO >= 1 && NO <= 4)
+        hipLaunchKernelGGL((k_bk_emit<MODE, NO, 2, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream,
+                           *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
+    else if (occ == 5 && NO >= 1 && NO <= 4)
+        hipLaunchKernelGGL((k_bk_emit<MODE, NO, 3, 5>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream,
+                           *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
+    else
+        hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream, *P,
+                           *O, OC, seq_base, out_seq, out_vals, out_cap);
 }
 
 template <int MODE>
