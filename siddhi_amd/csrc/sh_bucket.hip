@@ -1747,6 +1747,9 @@ static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& 
     if (occ == 6 && NO >= 1 && NO <= 4)
         hipLaunchKernelGGL((k_bk_emit<MODE, NO, 2, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream,
                            *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
+    else if (occ == 66 && NO >= 5 && NO <= 6)  // (experiment: 5-6 values at 6 waves, 1 row per lane)
+        hipLaunchKernelGGL((k_bk_emit<MODE, NO, 1, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream,
+                           *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
     else if (occ == 5 && NO >= 1 && NO <= 4)
         hipLaunchKernelGGL((k_bk_emit<MODE, NO, 3, 5>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream,
                            *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
