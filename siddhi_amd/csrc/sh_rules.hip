@@ -929,8 +929,8 @@ __global__ void k_sparse_place(const uint32_t* __restrict__ pr_p, const uint32_t
     }
 }
 
-template <bool IMG>
-__global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __restrict__ RT,
+template <bool IMG, int TPB = SPA_TPB, int OCC = 1>
+__global__ void __launch_bounds__(TPB, OCC) k_sparse_take(const shr_table* __restrict__ RT,
                                                          const int64_t* __restrict__ ts,
                                                          const int32_t* __restrict__ akeys, int64_t n,
                                                          const shd_cols* __restrict__ C,
@@ -957,13 +957,13 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __rest
     const int64_t nw = xcd ? (int64_t)(gridDim.x >> 3) : (int64_t)gridDim.x;
     // SPA_U events per thread and round: their key, list bounds and first list
     // entry are loaded together (three dependent random reads per event otherwise)
-    const int64_t round = (int64_t)SPA_TPB * SPA_U;
+    const int64_t round = (int64_t)TPB * SPA_U;
     for (int64_t base = wb * round; base < n; base += nw * round) {
         int32_t key[SPA_U];
         int64_t tq[SPA_U];
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
-            const int64_t q = base + (int64_t)u * SPA_TPB + threadIdx.x;
+            const int64_t q = base + (int64_t)u * TPB + threadIdx.x;
             key[u] = q < n ? akeys[q] : -1;
             tq[u] = q < n ? ts[q] : 0;
             if (xcd && key[u] >= 0) {
@@ -999,7 +999,7 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __rest
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
             if (lo[u] == hi[u]) continue;
-            const int64_t q = base + (int64_t)u * SPA_TPB + threadIdx.x;
+            const int64_t q = base + (int64_t)u * TPB + threadIdx.x;
             // f2's most read attributes of the consumer, loaded once for its list
             RowPre rp;
             rp.slot = 1;
@@ -1130,7 +1130,19 @@ extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const in
         const int xcd = xenv && tg >= 64 ? 1 : 0;
         if (xcd) tg &= ~7LL;
         const float scale = 8.0f / (float)std::max(1, nkeys);
-        if (use_img)
+        // (SH_TAKE_512=1: 512-thread workgroups at <= 80 VGPRs, up to three per CU)
+        static const bool t512 = getenv("SH_TAKE_512") && getenv("SH_TAKE_512")[0] == '1';
+        static const int lim512 = t512 ? spa_img_attr(&k_sparse_take<true, 512, 6>) : 0;
+        if (use_img && t512 && I->lds <= lim512) {
+            int64_t tg2 = (n + 512 * SPA_U - 1) / (512 * SPA_U);
+            const int64_t gmax2 = 256LL * std::max(1, std::min(per_cu, 3));
+            if (tg2 > gmax2) tg2 = gmax2;
+            if (tg2 < 1) tg2 = 1;
+            if (xcd) tg2 &= ~7LL;
+            hipLaunchKernelGGL((k_sparse_take<true, 512, 6>), dim3((unsigned)tg2), dim3(512), (size_t)I->lds, st, dT, ts,
+                               akeys, n, dC, img, *I, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
+                               (const int64_t*)l_te, l_q, xcd, scale, LV, pa0, pa1);
+        } else if (use_img)
             hipLaunchKernelGGL(k_sparse_take<true>, dim3((unsigned)tg), dim3(SPA_TPB), (size_t)I->lds, st, dT, ts, akeys,
                                n, dC, img, *I, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
                                (const int64_t*)l_te, l_q, xcd, scale, LV, pa0, pa1);
