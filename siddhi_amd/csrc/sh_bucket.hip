@@ -1744,18 +1744,27 @@ static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& 
     // CU on the 42 KB of LDS), C2 emit 1.40 vs 1.46 ms at 4 waves x 6 rows
     // (profiles/r5_c2_emit_occ_ab.txt); SH_EMIT_OCC=4 / 5 for the others
     static const int occ = getenv("SH_EMIT_OCC") ? atoi(getenv("SH_EMIT_OCC")) : 6;
-    if (occ == 6 && NO >= 1 && NO <= 4)
-        hipLaunchKernelGGL((k_bk_emit<MODE, NO, 2, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream,
-                           *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
-    else if (occ == 66 && NO >= 5 && NO <= 6)  // (experiment: 5-6 values at 6 waves, 1 row per lane)
-        hipLaunchKernelGGL((k_bk_emit<MODE, NO, 1, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream,
-                           *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
-    else if (occ == 5 && NO >= 1 && NO <= 4)
-        hipLaunchKernelGGL((k_bk_emit<MODE, NO, 3, 5>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream,
-                           *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
-    else
-        hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream, *P,
-                           *O, OC, seq_base, out_seq, out_vals, out_cap);
+    if constexpr (NO >= 1 && NO <= 4) {
+        if (occ == 6) {
+            hipLaunchKernelGGL((k_bk_emit<MODE, NO, 2, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad,
+                               (hipStream_t)stream, *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
+            return;
+        }
+        if (occ == 5) {
+            hipLaunchKernelGGL((k_bk_emit<MODE, NO, 3, 5>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad,
+                               (hipStream_t)stream, *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
+            return;
+        }
+    }
+    if constexpr (NO >= 5 && NO <= 6) {
+        if (occ == 66) {  // (experiment: 5-6 values at 6 waves, 1 row per lane: slower)
+            hipLaunchKernelGGL((k_bk_emit<MODE, NO, 1, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad,
+                               (hipStream_t)stream, *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream, *P,
+                       *O, OC, seq_base, out_seq, out_vals, out_cap);
 }
 
 template <int MODE>
