@@ -1740,10 +1740,11 @@ static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& 
     // (SH_EMIT_LDS_PAD=<bytes>: dynamic LDS that lowers the workgroups per CU -- an L2
     // footprint experiment)
     static const int pad = getenv("SH_EMIT_LDS_PAD") ? atoi(getenv("SH_EMIT_LDS_PAD")) : 0;
-    // up to 4 values: 6 waves per SIMD (<= 80 VGPRs, 2 rows per lane: three workgroups per
-    // CU on the 42 KB of LDS), C2 emit 1.40 vs 1.46 ms at 4 waves x 6 rows
-    // (profiles/r5_c2_emit_occ_ab.txt); SH_EMIT_OCC=4 / 5 for the others
-    static const int occ = getenv("SH_EMIT_OCC") ? atoi(getenv("SH_EMIT_OCC")) : 6;
+    // SH_EMIT_OCC=6: up to 4 values at 6 waves per SIMD (<= 80 VGPRs, 2 rows per lane: three
+    // workgroups per CU on the 42 KB of LDS) -- C2 emit 1.40 vs 1.46 ms
+    // (profiles/r5_c2_emit_occ_ab.txt), but 22 VGPRs spill to scratch and the step moves
+    // 8.89 GB past L2 instead of 8.00 (profiles/r5_c2_emit_occ6_traffic.json): off by default
+    static const int occ = getenv("SH_EMIT_OCC") ? atoi(getenv("SH_EMIT_OCC")) : 4;
     if constexpr (NO >= 1 && NO <= 4) {
         if (occ == 6) {
             hipLaunchKernelGGL((k_bk_emit<MODE, NO, 2, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad,
