@@ -102,6 +102,7 @@ struct shd_window_ws {
 #define SHB_F_COUNT 8     // one consumer takes > 255 partials
 #define SHB_F_HALO 16     // a walk reached the halo start
 #define SHB_F_SPAN 32     // one tile's bucket segment exceeds a chunk
+#define SHB_F_CARRY 256   // the persistent matcher's carried partials overflow its LDS
 
 struct shb_plan {
     int64_t n;
@@ -197,33 +198,6 @@ struct shb_cols {
     void* rows;                   // packed: the rows
 };
 
-// ---- stack matcher (sh_stack.hip k_bk_stk) of the bucketed engine for partitioned
-// `every e1=S[f1] -> e2=S[x.a op e1.a] within W`: every pending partial of a key
-// is consumed by the first later event of the key with x_q op y_i, so a key's
-// pending partials form a monotone stack (consumers pop its top, expiry drops its
-// bottom). One wave per (bucket, run of tiles) replaces shb_match between
-// shb_partition and shb_finish; the staged column 0 is the ordering attribute.
-#define SHK_MAX_TERMS 4
-#define SHK_F_SPILL 128   // a key's spill stack overflowed
-struct shk_params {
-    int32_t dom;                  // compare domain: DOM_F32 or DOM_I32
-    int32_t run_tiles;            // arrival tiles per run (<= shk_max_run_tiles())
-    int32_t want_ms;              // 1: match-stream column 0 takes e1's ordering value
-    int32_t spill_cap;            // spilled entries per (wave, key) at most (else SHK_F_SPILL)
-    // order keys: stack entries hold key(x) ^ kflip (key: IEEE bits -> unsigned order,
-    // or int ^ sign bit), so every operator becomes `consume if cx > cy (or ==, ge)`
-    // on unsigned keys; zk1 -> zk0 merges -0.0 into +0.0 before a compare
-    uint32_t kflip, zk0, zk1;
-    int32_t ge;
-    // opening filter: every term compares the ordering column with a constant through
-    // order keys: result = lt & (v < c) | eq & (v == c) | gt & (v > c), f_nan for NaN
-    int32_t n_terms;
-    int32_t f_f32[SHK_MAX_TERMS], f_nan[SHK_MAX_TERMS], f_lt[SHK_MAX_TERMS], f_eq[SHK_MAX_TERMS],
-        f_gt[SHK_MAX_TERMS];
-    uint32_t f_ckey[SHK_MAX_TERMS];
-    uint64_t* spill;              // [grid * 4 waves][64 keys][spill_cap] entries below the LDS rings
-};
-
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -274,11 +248,6 @@ int shb_s3_carry(const shb_plan* P, const shb_s3* S, void* stream);
 int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream);
 int shb_emit(const shb_plan* P, const shb_out* O, const shb_cols* OC, uint64_t seq_base, uint64_t* out_seq,
              int64_t* out_vals, int64_t out_cap, void* stream);
-// stack matcher (sh_stack.hip): after shb_partition (ordering attribute staged as
-// column 0), before shb_finish; -1: a plan it does not take
-int shk_match(const shb_plan* P, const shk_params* K, void* stream);
-int shk_max_run_tiles(void);
-int shk_spill_keys(void);   // keys per workgroup (spill rows per workgroup)
 // raw 8-byte rows [m x n_out] -> typed columns of widths w[o] (8, 4 or 1 bytes)
 int shd_narrow_rows(const int64_t* vals, int32_t n_out, int64_t m, void* const* cols, const int32_t* w, void* stream);
 // raw rows + sequence numbers -> packed rows (SHB_OUT_PACKED; woff / rw as in shb_cols)

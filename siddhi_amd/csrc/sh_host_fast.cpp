@@ -432,62 +432,6 @@ int run_rules(sh_handle* h, sh_device_run* run) {
 // consumer-side form and a null-free projection; 0 ok, 1 = not applicable or a
 // premise failed on the device (the caller runs the general window path),
 // SH_E_MORE = output capacity too small (out_count = matches), <0 error
-// the stack matcher's parameters (sh_stack.hip) for a query of stack form: the
-// ordering term `e2.a op e1.a` (a 4-byte float or int) and an opening filter of
-// terms comparing a with constants; false: the sort-and-walk matcher instead
-static bool stack_params(const shj_stack& S, int64_t within, shk_params* K) {
-    memset(K, 0, sizeof(*K));
-    if (S.op != SH_OP_GT && S.op != SH_OP_GE && S.op != SH_OP_LT && S.op != SH_OP_LE) return false;
-    if (within < 0 || within > 0x7FFFFFFF) return false;
-    const bool f32 = S.dom == DOM_F32;
-    K->dom = S.dom;
-    // order keys: `consume if cx > cy` (GT / LT after a flip), `or equal` for GE / LE;
-    // -0.0 and +0.0 have adjacent keys (0x7FFFFFFF, 0x80000000 before the flip): the
-    // compares merge the first into the second; ints need no merge
-    K->kflip = (S.op == SH_OP_LT || S.op == SH_OP_LE) ? 0xFFFFFFFFu : 0u;
-    K->ge = (S.op == SH_OP_GE || S.op == SH_OP_LE) ? 1 : 0;
-    K->zk1 = f32 ? (0x7FFFFFFFu ^ K->kflip) : 0u;
-    K->zk0 = f32 ? (0x80000000u ^ K->kflip) : 0u;
-    K->n_terms = S.n_terms;
-    for (int k = 0; k < S.n_terms; k++) {
-        const shp_term& T = S.terms[k];
-        const bool fl = T.ltype == SH_T_FLOAT && T.dom == DOM_F32;
-        const bool in = T.ltype == SH_T_INT && T.dom == DOM_I32;
-        if (T.rkind != 1 || T.lattr != S.xattr || T.lslot != 0 || !(fl || in) || T.op < SH_OP_EQ || T.op > SH_OP_LE)
-            return false;
-        uint32_t cb;  // the constant in the compare domain (binary numeric promotion)
-        if (fl) {
-            float cf;
-            switch (T.ctype) {
-                case SH_T_INT: cf = (float)(int32_t)T.c; break;
-                case SH_T_LONG: cf = (float)T.c; break;
-                case SH_T_FLOAT: memcpy(&cf, &T.c, 4); break;
-                case SH_T_DOUBLE: {
-                    double d;
-                    memcpy(&d, &T.c, 8);
-                    cf = (float)d;
-                    break;
-                }
-                default: return false;
-            }
-            if (cf != cf) return false;  // a NaN constant
-            memcpy(&cb, &cf, 4);
-            cb = (cb & 0x80000000u) ? ~cb : (cb | 0x80000000u);
-            if (cb == 0x7FFFFFFFu) cb = 0x80000000u;
-        } else {
-            if (T.ctype != SH_T_INT) return false;
-            cb = (uint32_t)(int32_t)T.c ^ 0x80000000u;
-        }
-        K->f_f32[k] = fl ? 1 : 0;
-        K->f_ckey[k] = cb;
-        K->f_lt[k] = T.op == SH_OP_LT || T.op == SH_OP_LE || T.op == SH_OP_NE;
-        K->f_eq[k] = T.op == SH_OP_EQ || T.op == SH_OP_GE || T.op == SH_OP_LE;
-        K->f_gt[k] = T.op == SH_OP_GT || T.op == SH_OP_GE || T.op == SH_OP_NE;
-        K->f_nan[k] = T.op == SH_OP_NE;  // NaN: every compare false but !=
-    }
-    return true;
-}
-
 int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry) {
     static const bool off = getenv("SH_DISABLE_BUCKET") != nullptr;
     h->bk_last = 0;
@@ -496,19 +440,6 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     if (off || !h->partitioned || nkeys < 1024 || !P.out_fast || n < SHB_TILE) return 1;
     const int kb = std::max(0, bits_for((uint64_t)(nkeys - 1)) - 8);
     if (kb > 8) return 1;
-    // the stack matcher (sh_stack.hip) for queries of stack form when SH_STACK=1
-    // (read per call: tests A/B the matchers; on C2 it is the slower of the two,
-    // DESIGN.md "stack matcher"), the sort-and-walk one (shb_match, hipRTC)
-    // otherwise or when the stack matcher refuses on the device
-    h->stk_last = 0;
-    const char* on = getenv("SH_STACK");
-    bool stk = (on && on[0] && on[0] != '0') && !h->stk_skip && kb <= 6 && !P.agg_post && !force_carry;
-    h->stk_skip = false;
-    shk_params K;
-    if (stk) {
-        if (h->stk_state == 0) h->stk_state = shj_stack_form(&P, &h->stk) == 0 ? 1 : -1;
-        stk = h->stk_state == 1 && stack_params(h->stk, P.within_ms, &K);
-    }
     // select list: e2-side values (and e1's partition attribute, equal to e2's
     // for these types) from the consumer row; other e1-side values ride the match stream
     shb_out O;
@@ -540,16 +471,19 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
         O.kind[o] = 0;
         O.src[o] = (const void*)(intptr_t)m;  // resolved below
     }
-    // (the stack matcher's only e1-side value is the ordering attribute, through
-    // match-stream column 0)
-    if (stk && !(n_ms == 0 || (n_ms == 1 && ms[0] == h->stk.xattr))) stk = false;
-    if (!stk) {
-        if (h->bk_state == 0) {
-            const int lrc = shj_bucket_load(&P, ms, n_ms, &h->bk, &h->bk_err);
-            h->bk_state = lrc == 0 ? 1 : (lrc == -1 ? -2 : -1);  // -2: no consumer-side form (not applicable)
-        }
-        if (h->bk_state != 1) return 1;
+    if (h->bk_state == 0) {
+        const int lrc = shj_bucket_load(&P, ms, n_ms, &h->bk, &h->bk_err);
+        h->bk_state = lrc == 0 ? 1 : (lrc == -1 ? -2 : -1);  // -2: no consumer-side form (not applicable)
     }
+    if (h->bk_state != 1) return 1;
+    // the persistent matcher (shb_pmatch: one workgroup per bucket carrying its keys'
+    // pending partials across chunks) unless it refused this batch on the device
+    // (carry overflow) or SH_BK_PERSIST=0 (read per call: tests run both matchers);
+    // the per-pass sort-and-walk matcher (shb_match) otherwise
+    h->bk_refused = 0;
+    const char* pe = getenv("SH_BK_PERSIST");
+    const bool pm = h->bk.pmatch && !h->bk_pskip && !(pe && pe[0] == '0');
+    h->bk_pskip = false;
     hipStream_t st = h->stream;
     shb_plan B;
     memset(&B, 0, sizeof(B));
@@ -571,45 +505,20 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
         h->bk_hstart.ensure_fresh((int64_t)B.nt * 4) || h->bk_ttot.ensure_fresh(((int64_t)B.nt + 1) * 4) ||
         h->bk_flag.ensure_fresh(64) || h->bk_rd.ensure(64))
         return fail(h, SH_E_OOM, "bucket workspace");
-    B.n_staged = stk ? 1 : h->bk.n_staged;
+    B.n_staged = h->bk.n_staged;
     for (int k = 0; k < B.n_staged; k++) {
-        const int a = stk ? h->stk.xattr : h->bk.staged_attr[k];
+        const int a = h->bk.staged_attr[k];
         const int w = type_width(P.attr_type[0][a]);
         if (h->bk_st[k].ensure_fresh(slots * w)) return fail(h, SH_E_OOM, "bucket workspace");
         B.st_src[k] = run->d_cols[a];
         B.st_dst[k] = h->bk_st[k].p;
         B.st_width[k] = w;
     }
-    // match stream: one region of SHB_SPAN values per matcher workgroup (its first
-    // pass), then a shared tail for further passes; every partial is consumed at
-    // most once, so n values suffice for the tail
+    // match stream: shb_pmatch takes one region per chunk from a shared counter (every
+    // partial is consumed at most once, so n values hold them all); shb_match one
+    // region of SHB_SPAN values per workgroup (its first pass), then the shared tail
     B.n_ms = n_ms;
-    // the stack matcher's runs: a run and its halo (the window's tiles before it) in
-    // one pass of SHB_TILE-event tiles, each run at least SH_STK_RUN_H halo lengths
-    // (default 8) at the stream's mean rate, at least 24 runs (a few workgroups per
-    // CU slot); each run's region of the match stream bounds its halo by SHB_HMAX tiles
-    int run_tiles = 0;
-    if (stk) {
-        hipMemcpyAsync(h->bk_rd.p, run->d_ts, 8, hipMemcpyDeviceToHost, st);
-        hipMemcpyAsync(h->bk_rd.as<void>(8), run->d_ts + (n - 1), 8, hipMemcpyDeviceToHost, st);
-        if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "bucket: timestamp read");
-        const int64_t span = *h->bk_rd.as<int64_t>(8) - *h->bk_rd.as<int64_t>(0);
-        const double rate = (double)n / (double)(std::max<int64_t>(span, 0) + 1);  // events per ms
-        const int halo_t = (int)std::min(1e6, rate * (double)(P.within_ms + 1) / SHB_TILE) + 1;
-        static const int run_h = getenv("SH_STK_RUN_H") ? std::max(1, atoi(getenv("SH_STK_RUN_H"))) : 8;
-        static const int run_env = getenv("SH_STK_RUN") ? atoi(getenv("SH_STK_RUN")) : 0;
-        run_tiles = run_env > 0 ? run_env : (int)std::min<int64_t>((int64_t)run_h * halo_t, std::max(1, B.nt / 24));
-        run_tiles = std::max(1, std::min(run_tiles, shk_max_run_tiles()));
-        K.run_tiles = run_tiles;
-        K.want_ms = n_ms;
-        // spilled entries per key (below the LDS ring): twice a key's mean events per
-        // window, at least 8 (a deeper stack raises SHK_F_SPILL: the host retries)
-        if (h->stk_cap == 0)
-            h->stk_cap = (int)std::min(511.0, std::max(8.0, 2.0 * rate * (double)(P.within_ms + 1) / nkeys));
-        K.spill_cap = h->stk_cap;
-    }
-    const int64_t runs = stk ? (B.nt + run_tiles - 1) / run_tiles : 0;
-    const int64_t ms_vals = stk ? n + runs * SHB_HMAX * SHB_TILE : (int64_t)SHB_NB * B.n_chunks * SHB_SPAN + n;
+    const int64_t ms_vals = pm ? n + 64 : (int64_t)SHB_NB * B.n_chunks * SHB_SPAN + n;
     for (int m = 0; m < n_ms; m++) {
         const int w = type_width(P.attr_type[0][ms[m]]);
         if (h->bk_ms[m].ensure_fresh(ms_vals * w)) return fail(h, SH_E_OOM, "match stream");
@@ -755,23 +664,16 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     hipMemcpyAsync(h->bk_rd.p, run->d_ts, 8, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "bucket: timestamp read");
     B.tbase = *h->bk_rd.as<int64_t>() - ((int64_t)1 << (31 - kb));
-    if (stk) {
-        const size_t sb = (size_t)runs * (SHB_NB / 4) * shk_spill_keys() * K.spill_cap * 8;
-        if (h->k_spill.ensure(sb)) return fail(h, SH_E_OOM, "stack matcher spill");
-        K.spill = h->k_spill.as<uint64_t>();
-    }
     hipEventRecord(h->ev[0], st);
     hipMemsetAsync(B.flag, 0, 32, st);  // flag word + match-stream allocator
     hipMemsetAsync(B.ttot, 0, ((int64_t)B.nt + 1) * 4, st);
     if (shb_partition(run->d_keys, run->d_ts, nkeys, &B, st)) return fail(h, SH_E_HIP, "bucket partition launch failed");
     hipEventRecord(h->ev[1], st);
     void* args[] = {&B};
-    if (stk) {
-        if (shk_match(&B, &K, st)) return fail(h, SH_E_HIP, "stack matcher launch failed");
-    } else if (hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.n_chunks), 1, 1, 512, 1, 1, 0,
-                                     st, args, nullptr) != hipSuccess) {
-        return fail(h, SH_E_HIP, "shb_match launch failed");
-    }
+    if (pm ? hipModuleLaunchKernel((hipFunction_t)h->bk.pmatch, SHB_NB, 1, 1, 1024, 1, 1, 0, st, args, nullptr)
+           : hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.n_chunks), 1, 1, 512, 1, 1, 0,
+                                   st, args, nullptr))
+        return fail(h, SH_E_HIP, pm ? "shb_pmatch launch failed" : "shb_match launch failed");
     // (by output row: after the tiles' first rows are known)
     if (carry && !AG.by_row && shb_agg_carry(&B, &AG, st)) return fail(h, SH_E_HIP, "aggregate carry launch failed");
     if (shb_finish(&B, h->w_scan.as<uint32_t>(), st)) return fail(h, SH_E_HIP, "bucket scan launch failed");
@@ -785,15 +687,14 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     if (hipStreamSynchronize(st) != hipSuccess) return fail(h, SH_E_HIP, "device error in bucket engine");
     const int32_t flag = *h->bk_rd.as<int32_t>(0);
     const int64_t total = *h->bk_rd.as<uint32_t>(8);
-    if (B.prof && stk) {
+    if (B.prof) {
         unsigned long long pr[16];
         hipMemcpy(pr, B.prof, 128, hipMemcpyDeviceToHost);
-        fprintf(stderr, "[k_bk_stk clock ticks, sum over waves] setup %llu issue %llu sort %llu - %llu owner steps %llu "
-                        "rows %llu; batches %llu owner steps %llu; runs %lld of %d tiles\n",
-                pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], (long long)runs, run_tiles);
-    } else if (B.prof) {
-        unsigned long long pr[16];
-        hipMemcpy(pr, B.prof, 128, hipMemcpyDeviceToHost);
+        if (pm)
+            fprintf(stderr, "[shb_pmatch clock ticks, sum over workgroups] tiles %llu rank+span %llu next table+issue %llu "
+                            "walk %llu scan+carry %llu emit %llu\n",
+                    pr[5], pr[1], pr[0], pr[2], pr[3], pr[4]);
+        else
         fprintf(stderr, "[shb_match clock ticks, sum over workgroups] table %llu load %llu rank %llu walk %llu "
                         "scan+psum %llu emit %llu\n",
                 pr[5], pr[0], pr[1], pr[2], pr[3], pr[4]);
@@ -807,18 +708,14 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
                     pr[8], pr[9], pr[10], pr[11], pr[12]);
     }
     if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
-    if (flag && stk) {
-        static const bool dbg = getenv("SH_STK_DEBUG") != nullptr;
-        if (dbg) fprintf(stderr, "[stack matcher] refused on the device: flags 0x%x\n", flag);
-        h->stk_refused = flag;
-        if (flag == SHK_F_SPILL && h->stk_cap < 511) {
-            h->stk_cap = std::min(511, h->stk_cap * 4);  // deeper stacks than the mean rate suggests
-        } else if (flag & (SHB_F_TS | SHB_F_MONO)) {
-            return 1;  // neither matcher takes the batch
-        } else {
-            h->stk_skip = true;  // the sort-and-walk matcher once
+    if (flag && pm) {
+        h->bk_refused = flag;
+        if (flag & (SHB_F_TS | SHB_F_MONO | SHB_F_COUNT | SHB_F_SPAN))
+            return 1;  // the per-pass matcher refuses these too (its chunk is smaller)
+        if (flag & SHB_F_CARRY) {
+            h->bk_pskip = true;  // the per-pass matcher once
+            return run_bucket(h, run, nkeys, force_carry);
         }
-        return run_bucket(h, run, nkeys, force_carry);
     }
     if (flag == SHB_F_AGG && carry && AG.parallel) {
         // a value the fixed point cannot hold exactly (or a chunk too dense): the
@@ -838,8 +735,7 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
     hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
     h->times.advance_launches = 1;
-    h->bk_last = 1;
-    h->stk_last = stk ? 1 : 0;
+    h->bk_last = pm ? 3 : 1;
     h->bk_agg_carried = carry;
     if (carry) h->agg_last = AG.parallel ? 5 : 4;
     return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "bucket engine");

@@ -336,17 +336,12 @@ struct sh_handle {
     DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS], bk_agg[SHB_MAX_AGG];
     bool bk_agg_carried = false;  // the last bucketed run carried its aggregates (k_bk_aggc)
     PinBuf bk_rd;
-    // ---- the bucketed engine's stack matcher (sh_stack.hip): 0 untried, 1 applicable, -1 not
-    int stk_state = 0;
-    int stk_last = 0;             // 1: the last bucketed run matched on the stack matcher
-    int stk_refused = 0;          // the device flags of the last refused stack-matcher run (diagnostics)
-    shj_stack stk{};
-    bool stk_skip = false;        // the next bucketed run takes the sort-and-walk matcher
+    // ---- the bucketed engine's persistent matcher (shb_pmatch)
+    int bk_refused = 0;           // the device flags that sent the last run off it (diagnostics)
+    bool bk_pskip = false;        // the next bucketed run takes the per-pass matcher (shb_match)
     DevBuf bk_roff;          // [slot] first output row of each event (k_bk_rowoff)
     bool aggp_skip = false;  // run_bucket: this batch without k_bk_aggp (it refused a value)
     bool aggp_only = false;  // run_bucket: k_bk_aggp or nothing (1), the caller's layout kept
-    int stk_cap = 0;              // spilled entries per key (0: from the first batch's rate)
-    DevBuf k_spill;
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
     DevBuf w_colrows;
     bool cols_rows = false;
@@ -435,7 +430,7 @@ extern "C" {
 int shx_jit_status(sh_handle* h);
 int shx_jit_compile(sh_handle* h);
 int shx_bucket_status(sh_handle* h);
-int shx_stack_refused(sh_handle* h);
+int shx_bucket_refused(sh_handle* h);
 int shx_seq3_status(sh_handle* h);
 int shx_agg_status(sh_handle* h);
 int shx_rules_status(sh_handle* h);

@@ -32,21 +32,10 @@ int shj_bucket_chunk(void);
 // match stream carries (e1-side select values), in match-stream column order
 struct shj_bucket {
     void* match;          // hipFunction_t shb_match
+    void* pmatch;         // hipFunction_t shb_pmatch (persistent, one workgroup per bucket), NULL if absent
     int n_staged;         // columns the partition moves into bucket order
     int staged_attr[4];
 };
 int shj_bucket_load(const shp_program* hp, const int* ms_attrs, int n_ms, shj_bucket* out, std::string* err);
 int shj_bucket_source(const shp_program* hp, const int* ms_attrs, int n_ms, std::string* src);
 int shj_bucket_compile(const shp_program* hp, const int* ms_attrs, int n_ms, std::string* err);
-
-// the stack engine's form of a window program (sh_stack.hip): f2 is one ordering
-// term between the same 4-byte attribute of e2 and e1 (X(e2) op X(e1)) plus terms
-// on e1 alone; f1 and those terms become the opening filter. 0 ok, -1 no such form.
-struct shj_stack {
-    int op;               // consumed when cmp_op(op, x_e2, x_e1)
-    int dom;              // DOM_F32 / DOM_I32
-    int xattr;            // the ordering attribute
-    int n_terms;          // opening filter terms (f1 + e1-only terms of f2), slot 0 only
-    shp_term terms[4];
-};
-int shj_stack_form(const shp_program* hp, shj_stack* out);

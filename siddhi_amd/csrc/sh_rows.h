@@ -1,6 +1,6 @@
-// sh_rows.h — one output row in the caller's layout (device side), shared by the
-// bucketed emitter (sh_bucket.hip) and the stack engine (sh_stack.hip): raw 8-byte
-// rows + sequence numbers, typed natural-width columns, or packed rows.
+// sh_rows.h — one output row in the caller's layout (device side) for the
+// bucketed emitter (sh_bucket.hip): raw 8-byte rows + sequence numbers, typed
+// natural-width columns, or packed rows.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
