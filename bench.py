@@ -12,17 +12,21 @@ A step = one full pass of the matcher over the 100M events from fresh per-key
 state (radix segment -> per-key NFA advance -> ordered match placement), with
 the ordered match stream written to HBM.
 
-Multi-GPU (torchrun; C2, C3, C5): one process per GPU, strong scaling over
-ONE stream. Every rank ingests an arrival-contiguous slice (cut at send() call
-boundaries); a step routes the slice's events to the ranks owning their keys
-(mix32(key) % world, one RCCL all-to-all of packed records), runs the matcher on
-the owned events, sends every match row back to the rank holding its trigger
-event (a second all-to-all) and k-way merges the runs by trigger sequence (C5:
-by the trigger's PartitionStreamReceiver run, whose rows stay query-major)
-(siddhi_amd/shard.py, include/siddhi_shard.h). value = the stream's events /
-the max-over-ranks step time; the roofline is per GPU (all ranks' algorithmic
-matcher bytes / world / the slowest rank's matcher kernel time). C1 (no
-partition) runs replicas; C4 runs its streaming path per rank (main_c4).
+Multi-GPU (torchrun; C2, C3, C5): one process per GPU. The headline at N > 1 is
+the north-star design, strong scaling over ONE stream: every rank ingests an
+arrival-contiguous slice (cut at send() call boundaries); a step routes the
+slice's events to the ranks owning their keys (mix32(key) % world, one RCCL
+all-to-all of packed records), runs the matcher on the owned events, sends every
+match row back to the rank holding its trigger event (a second all-to-all) and
+k-way merges the runs by trigger sequence (C5: by the trigger's
+PartitionStreamReceiver run, whose rows stay query-major) (siddhi_amd/shard.py,
+include/siddhi_shard.h). value = the stream's events / the max-over-ranks step
+time; the roofline is per GPU (all ranks' algorithmic matcher bytes / world /
+the slowest rank's matcher kernel time). The same run then times the weak form
+(every GPU its own partition of the key space: its own stream over its own
+keys, no data-path collective) and prints it beside the headline as
+`weak_value` / `weak`. --strong / --weak run one form only. C1 (no partition)
+runs replicas; C4 runs its streaming path per rank (main_c4).
 """
 import argparse
 import json
@@ -61,10 +65,12 @@ def parse():
     ap.add_argument("--c4-every", action="store_true", help="c4: the `every (e1=Login and e2=Txn) -> ...` variant")
     ap.add_argument("--rules", type=int, default=1000, help="c5: rule count")
     ap.add_argument("--strong", action="store_true",
-                    help="N > 1: ONE stream over all ranks (c2 / c3 / c5: key-routed RCCL all-to-all + row return "
-                         "+ k-way merge; c4: key-sharded streaming with gloo coordination). Default: every GPU "
-                         "matches its own partition of the key space (its own stream over its own keys, no "
-                         "data-path collective; rank 0's stream is the canonical one), 'scaling': 'weak'")
+                    help="N > 1: only the ONE-stream form over all ranks (c2 / c3 / c5: key-routed RCCL all-to-all "
+                         "+ row return + k-way merge; c4: key-sharded streaming with gloo coordination). Default "
+                         "for c2 / c3 / c5: that form as the headline, then the weak form beside it (weak_value)")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: only the weak form (every GPU matches its own partition of the key space: its own "
+                         "stream over its own keys, no data-path collective; rank 0's stream is the canonical one)")
     args = ap.parse_args()
     args.seed_offset = 0  # (rank r of a weak-scaling run: its own partition's stream)
     if args.config == "c1":
@@ -507,15 +513,16 @@ def main_sharded(args, torch, dist, world, rank, dev):
         v = vals.cpu().numpy()
         oq = v[:, -1].astype(np.int32) if wq else None
         verified = check_rows(W, seq.cpu().numpy(), v[:, :-1] if wq else v, oq, (lo, hi))
-    cpu = cpu_baseline(args, W, n) if rank == 0 else None
+    cpu = cpu_baseline(args, W, n) if rank == 0 and args.cpu_sample else None
     # the same phase names as the one-GPU line (shard.KeyShardedStep.PHASES): the step's phases on
     # rank 0's launch stream, the matcher's own split inside unpack_match
     phases = dict(step.phase_ms() or {})
     last = kt_acc.get("last") or {}
     phases.update({"segment": last.get("segment_ms"), "advance": last.get("advance_ms"),
                    "emit": last.get("emit_ms")})
+    line = None
     if rank == 0:
-        print(json.dumps({
+        line = {
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
             "value": n * args.steps / dt, "unit": "events/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt * 1000.0 / args.steps, "higher_is_better": True,
@@ -534,9 +541,12 @@ def main_sharded(args, torch, dist, world, rank, dev):
                                    "algorithmic bytes of all ranks / world / slowest rank's matcher time",
                          "kernels_ms_per_step_max": kmax, "algorithmic_bytes_per_rank": b_alg.tolist()},
             "cpu_baseline": cpu,
-            "verified_vs_restatement": verified}))
+            "verified_vs_restatement": verified}
     runner.close()
-    dist.destroy_process_group()
+    del step, d_ts, d_cols, d_run
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return line
 
 
 def main():
@@ -556,15 +566,44 @@ def main():
         # rehearsal on one GPU: gloo through host memory (RCCL refuses duplicate devices)
         dist.init_process_group("gloo" if share else "nccl")
     dev = torch.device(f"cuda:{local}")
-    if world > 1 and not args.strong:
+    if args.config == "c4":
+        if world > 1 and not args.strong:
+            args.seed_offset = 7919 * rank  # each rank its own partition of the users
+        return main_c4(args, torch, dist, world, rank, dev)
+    if args.config in ("c2", "c3", "c5") and world > 1 and not args.weak:
+        # the north-star form first: one stream, key-routed over RCCL, rows merged back
+        strong = main_sharded(args, torch, dist, world, rank, dev)
+        if args.strong:
+            if rank == 0:
+                print(json.dumps(strong))
+            dist.destroy_process_group()
+            return
+        # then the weak form in the same run (its stream is rank 0's verified one at N = 1)
+        args.seed_offset = 7919 * rank
+        args.no_verify, args.cpu_sample = True, 0
+        weak = run_partitions(args, torch, dist, world, rank, dev)
+        if rank == 0:
+            strong["weak_value"] = weak["value"]
+            strong["weak"] = {k: weak[k] for k in ("value", "ms_per_step", "scaling", "roofline", "config",
+                                                   "phase_ms", "engine")}
+            print(json.dumps(strong))
+        dist.destroy_process_group()
+        return
+    if world > 1:
         # every rank matches its own partition of the key space (its own stream over
         # its own keys; rank 0's is the canonical one, verified)
         args.seed_offset = 7919 * rank
-    if args.config == "c4":
-        return main_c4(args, torch, dist, world, rank, dev)
-    if args.config in ("c2", "c3", "c5") and world > 1 and args.strong:
-        return main_sharded(args, torch, dist, world, rank, dev)
+    line = run_partitions(args, torch, dist, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
 
+
+def run_partitions(args, torch, dist, world, rank, dev):
+    """The one-GPU step, or at N > 1 the weak form: every rank its own partition of
+    the key space, ranks meeting only in the timing barrier and the max reduction.
+    Returns rank 0's line (None elsewhere)."""
     from siddhi_amd.device_run import DeviceRunner
 
     n, K = args.events, args.keys
@@ -683,8 +722,9 @@ def main():
         except Exception:
             traffic = None
 
-    cpu = cpu_baseline(args, W, n) if rank == 0 else None
+    cpu = cpu_baseline(args, W, n) if rank == 0 and args.cpu_sample else None
 
+    line = None
     if rank == 0:
         line = {
             "metric": "input events/sec (node) for partitioned pattern query; achieved HBM GB/s %",
@@ -725,10 +765,8 @@ def main():
             "cpu_baseline": cpu,
             "verified_vs_restatement": verified,
         }
-        print(json.dumps(line))
     runner.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return line
 
 
 if __name__ == "__main__":

@@ -170,8 +170,6 @@ def bind_product(lib):
     lib.shx_bucket_compile.restype = C.c_int
     lib.shx_bucket_status.argtypes = [C.c_void_p]
     lib.shx_bucket_status.restype = C.c_int
-    lib.shx_bucket_refused.argtypes = [C.c_void_p]
-    lib.shx_bucket_refused.restype = C.c_int
     lib.shx_seq3_status.argtypes = [C.c_void_p]
     lib.shx_seq3_status.restype = C.c_int
     lib.shx_agg_status.argtypes = [C.c_void_p]

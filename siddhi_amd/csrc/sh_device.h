@@ -102,7 +102,6 @@ struct shd_window_ws {
 #define SHB_F_COUNT 8     // one consumer takes > 255 partials
 #define SHB_F_HALO 16     // a walk reached the halo start
 #define SHB_F_SPAN 32     // one tile's bucket segment exceeds a chunk
-#define SHB_F_CARRY 256   // the persistent matcher's carried partials overflow its LDS
 
 struct shb_plan {
     int64_t n;

@@ -1715,9 +1715,8 @@ int shx_jit_compile(sh_handle* h) {
     return SH_OK;
 }
 
-// 3: the last sh_run_device ran on the bucketed engine's persistent matcher (shb_pmatch), 1: on
-// its per-pass matcher (shb_match); 0: another engine; -1: its matcher could not be built
-// (message in sh_last_error)
+// 1: the last sh_run_device ran on the bucketed engine; 0: another engine; -1: its matcher
+// could not be built (message in sh_last_error)
 int shx_bucket_status(sh_handle* h) {
     if (!h) return 0;
     if (h->bk_state == -2) return 0;  // no consumer-side form: not applicable
@@ -1727,9 +1726,6 @@ int shx_bucket_status(sh_handle* h) {
     }
     return h->bk_last;
 }
-
-// the device flags (SHB_F_*) that sent the last run off the persistent matcher
-int shx_bucket_refused(sh_handle* h) { return h ? h->bk_refused : 0; }
 
 // 1: the last general-engine sh_run_device took the rise-and-fall sequence engine
 int shx_seq3_status(sh_handle* h) { return h ? (h->s3b_last ? 2 : h->seq3_last) : 0; }

@@ -476,14 +476,6 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
         h->bk_state = lrc == 0 ? 1 : (lrc == -1 ? -2 : -1);  // -2: no consumer-side form (not applicable)
     }
     if (h->bk_state != 1) return 1;
-    // the persistent matcher (shb_pmatch: one workgroup per bucket carrying its keys'
-    // pending partials across chunks) unless it refused this batch on the device
-    // (carry overflow) or SH_BK_PERSIST=0 (read per call: tests run both matchers);
-    // the per-pass sort-and-walk matcher (shb_match) otherwise
-    h->bk_refused = 0;
-    const char* pe = getenv("SH_BK_PERSIST");
-    const bool pm = h->bk.pmatch && !h->bk_pskip && !(pe && pe[0] == '0');
-    h->bk_pskip = false;
     hipStream_t st = h->stream;
     shb_plan B;
     memset(&B, 0, sizeof(B));
@@ -514,11 +506,11 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
         B.st_dst[k] = h->bk_st[k].p;
         B.st_width[k] = w;
     }
-    // match stream: shb_pmatch takes one region per chunk from a shared counter (every
-    // partial is consumed at most once, so n values hold them all); shb_match one
-    // region of SHB_SPAN values per workgroup (its first pass), then the shared tail
+    // match stream: one region of SHB_SPAN values per matcher workgroup (its first
+    // pass), then a shared tail for further passes; every partial is consumed at
+    // most once, so n values suffice for the tail
     B.n_ms = n_ms;
-    const int64_t ms_vals = pm ? n + 64 : (int64_t)SHB_NB * B.n_chunks * SHB_SPAN + n;
+    const int64_t ms_vals = (int64_t)SHB_NB * B.n_chunks * SHB_SPAN + n;
     for (int m = 0; m < n_ms; m++) {
         const int w = type_width(P.attr_type[0][ms[m]]);
         if (h->bk_ms[m].ensure_fresh(ms_vals * w)) return fail(h, SH_E_OOM, "match stream");
@@ -670,10 +662,9 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     if (shb_partition(run->d_keys, run->d_ts, nkeys, &B, st)) return fail(h, SH_E_HIP, "bucket partition launch failed");
     hipEventRecord(h->ev[1], st);
     void* args[] = {&B};
-    if (pm ? hipModuleLaunchKernel((hipFunction_t)h->bk.pmatch, SHB_NB, 1, 1, 1024, 1, 1, 0, st, args, nullptr)
-           : hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.n_chunks), 1, 1, 512, 1, 1, 0,
-                                   st, args, nullptr))
-        return fail(h, SH_E_HIP, pm ? "shb_pmatch launch failed" : "shb_match launch failed");
+    if (hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.n_chunks), 1, 1, 512, 1, 1, 0, st, args,
+                              nullptr) != hipSuccess)
+        return fail(h, SH_E_HIP, "shb_match launch failed");
     // (by output row: after the tiles' first rows are known)
     if (carry && !AG.by_row && shb_agg_carry(&B, &AG, st)) return fail(h, SH_E_HIP, "aggregate carry launch failed");
     if (shb_finish(&B, h->w_scan.as<uint32_t>(), st)) return fail(h, SH_E_HIP, "bucket scan launch failed");
@@ -690,11 +681,6 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     if (B.prof) {
         unsigned long long pr[16];
         hipMemcpy(pr, B.prof, 128, hipMemcpyDeviceToHost);
-        if (pm)
-            fprintf(stderr, "[shb_pmatch clock ticks, sum over workgroups] tiles %llu rank+span %llu next table+issue %llu "
-                            "walk %llu scan+carry %llu emit %llu\n",
-                    pr[5], pr[1], pr[0], pr[2], pr[3], pr[4]);
-        else
         fprintf(stderr, "[shb_match clock ticks, sum over workgroups] table %llu load %llu rank %llu walk %llu "
                         "scan+psum %llu emit %llu\n",
                 pr[5], pr[0], pr[1], pr[2], pr[3], pr[4]);
@@ -708,15 +694,6 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
                     pr[8], pr[9], pr[10], pr[11], pr[12]);
     }
     if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
-    if (flag && pm) {
-        h->bk_refused = flag;
-        if (flag & (SHB_F_TS | SHB_F_MONO | SHB_F_COUNT | SHB_F_SPAN))
-            return 1;  // the per-pass matcher refuses these too (its chunk is smaller)
-        if (flag & SHB_F_CARRY) {
-            h->bk_pskip = true;  // the per-pass matcher once
-            return run_bucket(h, run, nkeys, force_carry);
-        }
-    }
     if (flag == SHB_F_AGG && carry && AG.parallel) {
         // a value the fixed point cannot hold exactly (or a chunk too dense): the
         // batch again without the carry, the post-pass (or k_bk_aggc) adding instead
@@ -735,7 +712,7 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
     hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
     h->times.advance_launches = 1;
-    h->bk_last = pm ? 3 : 1;
+    h->bk_last = 1;
     h->bk_agg_carried = carry;
     if (carry) h->agg_last = AG.parallel ? 5 : 4;
     return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "bucket engine");

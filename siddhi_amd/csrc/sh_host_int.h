@@ -336,9 +336,6 @@ struct sh_handle {
     DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS], bk_agg[SHB_MAX_AGG];
     bool bk_agg_carried = false;  // the last bucketed run carried its aggregates (k_bk_aggc)
     PinBuf bk_rd;
-    // ---- the bucketed engine's persistent matcher (shb_pmatch)
-    int bk_refused = 0;           // the device flags that sent the last run off it (diagnostics)
-    bool bk_pskip = false;        // the next bucketed run takes the per-pass matcher (shb_match)
     DevBuf bk_roff;          // [slot] first output row of each event (k_bk_rowoff)
     bool aggp_skip = false;  // run_bucket: this batch without k_bk_aggp (it refused a value)
     bool aggp_only = false;  // run_bucket: k_bk_aggp or nothing (1), the caller's layout kept
@@ -430,7 +427,6 @@ extern "C" {
 int shx_jit_status(sh_handle* h);
 int shx_jit_compile(sh_handle* h);
 int shx_bucket_status(sh_handle* h);
-int shx_bucket_refused(sh_handle* h);
 int shx_seq3_status(sh_handle* h);
 int shx_agg_status(sh_handle* h);
 int shx_rules_status(sh_handle* h);

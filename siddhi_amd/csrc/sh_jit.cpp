@@ -72,10 +72,12 @@ const int kMatchMinBlocks = env_int("SH_BK_MINB", 6, 1, 8);
 // a matcher pass's LDS span and consumer limit (events; multiples of its 512
 // threads, at most SHB_SPAN / SHB_CH): smaller passes take less LDS, so more
 // workgroups share a CU, at the price of more halo events per consumer. 3,072 /
-// 2,048 measured 4.44 vs 4.63 ms for 5,120 / 4,096 on C2 (profiles/r4_c2_span_ab.txt)
+// 2,048 measured 4.44 vs 4.63 ms for 5,120 / 4,096 on C2 (profiles/r4_c2_span_ab.txt);
+// 2,560 / 2,048 (the pass's 1,792 consumers and ~400 halo events fit) 1.98 vs 2.09 ms
+// for the matcher (profiles/r6_c2_span_ab.txt)
 const int kSpan = [] {
-    const int v = env_int("SH_BK_SPAN", 3072, 1024, SHB_SPAN);
-    return v % 512 ? 3072 : v;
+    const int v = env_int("SH_BK_SPAN", 2560, 1024, SHB_SPAN);
+    return v % 512 ? 2560 : v;
 }();
 // L2 warming of each pass's span (SH_BK_MWARM=0: off): the first line(s) of every
 // consumer / near-halo tile's segment are read as soon as the bucket starts arrive,
@@ -857,10 +859,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     // juggling on the CU's shared scalar unit); the block loop runs while any
     // lane of the wave still walks (a uniform exit). Consumed predecessors at
     // distance < 15 go to a 16-bit mask for the emit phase (SHB_MOVF: beyond).
-    // (mark: the persistent matcher records every consumed span position in s_used,
-    // from which it builds the carry of pending partials)
-    const std::string mark_s = "    if (cons) s_used[sp - 1 - step] = (uint8_t)1;\n";
-    auto walk_count = [&](bool mark) {
+    auto walk_count = [&]() {
         std::string s = head() + "uint32_t mask = 0u;\nuint32_t live = stopped ? 0u : 1u, mono = 0u;\n"
                                  "for (int base = 0; __ballot(live != 0u) != 0ull; base += SHB_D) {\n"
                                  "uint32_t wv[SHB_D];\n";
@@ -883,7 +882,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
         for (int a : need_r)
             s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
         s += "    {\n" + cand_fast +
-             "    const uint32_t cons = act & (ok ? 1u : 0u);\n    c_ += cons;\n" + (mark ? mark_s : std::string()) +
+             "    const uint32_t cons = act & (ok ? 1u : 0u);\n    c_ += cons;\n"
              "    mask |= step < SHB_MSTEPS ? (cons << step) : (cons ? SHB_MOVF : 0u);\n    }\n";
         s += "    {\n" + mid_fast + "    }\n    {\n    const uint32_t st = (act && (" + stop_cond +
              ")) ? 1u : 0u;\n    stopped |= st;\n    live = act & (st ^ 1u);\n    }\n}\n}\n"
@@ -896,7 +895,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     // `hasM` flag, the NaN tests on X and the per-step premise checks drop out;
     // times compare as the packed 32-bit values (in window: tr >= tq - W)
     const bool fdom = F.cross && (F.dom == DOM_F32 || F.dom == DOM_F64);
-    auto walk_count_f = [&](bool mark) {
+    auto walk_count_f = [&]() {
         const bool mx = F.op == SH_OP_GT || F.op == SH_OP_GE;
         const std::string opn = std::to_string(F.op);
         const std::string ext = F.dom == DOM_F32 ? (mx ? "__builtin_fmaxf" : "__builtin_fminf")
@@ -931,7 +930,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
         for (int a : need_r)
             s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
         s += "    {\n" + cand_f +
-             "    const uint32_t cons = act & (ok ? 1u : 0u);\n" + (mark ? mark_s : std::string()) +
+             "    const uint32_t cons = act & (ok ? 1u : 0u);\n"
              "    if (step < SHB_MSTEPS) mask |= cons << step;\n"
              "    else { cext += cons; mask |= cons ? SHB_MOVF : 0u; }\n    }\n";
         s += "    {\n" + mid_f + "    }\n    live = act & (cmp_op<" + DT + ">(" + (mx ? std::to_string(SH_OP_GE)
@@ -946,7 +945,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
     // result and takes the next consumer of the range (ballot rank), so a block of
     // SHB_D steps runs for busy lanes only instead of every lane waiting for the
     // wave's longest walk (C2: mean walk 3.4 steps, p90 9, wave max ~15)
-    auto walk_count_f_dyn = [&](bool mark) {
+    auto walk_count_f_dyn = [&]() {
         const bool mx = F.op == SH_OP_GT || F.op == SH_OP_GE;
         const std::string opn = std::to_string(F.op);
         const std::string ext = F.dom == DOM_F32 ? (mx ? "__builtin_fmaxf" : "__builtin_fminf")
@@ -1011,7 +1010,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
         for (int a : need_r)
             s += "    x0_" + std::to_string(a) + " = " + raw_of(P.attr_type[0][a], "av" + std::to_string(a) + "[u]") + ";\n";
         s += "    {\n" + cand_f +
-             "    const uint32_t cons = act & (ok ? 1u : 0u);\n" + (mark ? mark_s : std::string()) +
+             "    const uint32_t cons = act & (ok ? 1u : 0u);\n"
              "    if (step < SHB_MSTEPS) mask |= cons << step;\n"
              "    else { cext += cons; mask |= cons ? SHB_MOVF : 0u; }\n    }\n";
         s += "    {\n" + mid_f + "    }\n    live = act & (cmp_op<" + DT + ">(" + (mx ? std::to_string(SH_OP_GE)
@@ -1244,7 +1243,7 @@ SHB_PROF(1)
 )";
     if (fdom && kWalkDyn) {
         // consumers (chunk events): per-lane work hand-out over each wave's range
-        src += "// consumers (chunk events): partials taken per event\n" + walk_count_f_dyn(false) + "__syncthreads();\n";
+        src += "// consumers (chunk events): partials taken per event\n" + walk_count_f_dyn() + "__syncthreads();\n";
     } else {
         src += R"(// consumers (chunk events) in sorted order: partials taken per event
 for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {
@@ -1252,7 +1251,7 @@ const uint32_t cw = s_cons[ci];
 const int sp = (int)(cw & 0xFFFFu), i = hl + (int)(cw >> 16);
 uint32_t c_ = 0;
 )";
-        src += fdom ? walk_count_f(false) : walk_count(false);
+        src += fdom ? walk_count_f() : walk_count();
         src += R"(if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);
 s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);
 s_msk[i - hl] = (uint16_t)mask;
@@ -1347,355 +1346,6 @@ uint32_t k = 0;
     if (stage1) src += "}\n";
     src += "SHB_PROF(4)\na += ne;\n}\n#if SHB_WARMJ\nasm volatile(\"\" ::\"v\"(warm_));\n#endif\n}\n";
 
-    // ------------------------------------------------------------ shb_pmatch
-    // The persistent matcher: one 1,024-thread workgroup per bucket walks the
-    // bucket's tiles in chunks of at most SHP_CH events, in arrival order, and
-    // carries each local key's pending partials (plus its latest event) from one
-    // chunk to the next in LDS instead of re-reading a halo. The chunk's span is,
-    // per local key, the key's carried entries followed by its chunk events in
-    // arrival order, so the consumer walk above runs on it unchanged.
-    //   carry exactness: an entry i is dropped only when (a) it is not a partial
-    //   (f1 && e1-only terms fail: never consumable), (b) a chunk event consumed it,
-    //   or (c) it is outside the window of the key's latest event (every later
-    //   consumer of the key is at least as late). Any subsequence of a key's history
-    //   that holds all its pending partials gives the walk the same answer: an
-    //   event q between a pending partial i and the chunk's end did not consume i,
-    //   so X(q) op Y(i) fails and q cannot change ext op Y(i) (ExtForm above).
-    // Software pipeline: the next chunk's bucket starts are loaded while the
-    // current chunk is ranked, its events while the current chunk is walked.
-    {
-        size_t per_ev = 4 + 1;  // s_ws + s_used
-        for (int a : staged_out) per_ev += (size_t)type_width_of(P.attr_type[0][a]);
-        int ch = 4096, cc = 2048;
-        auto lds_bytes = [&](int c1, int c2) {
-            return (size_t)(c1 + c2) * per_ev + (size_t)c1 * (4 + 2) + 16u * 256u * 4u +
-                   (size_t)c2 * (per_ev - 1) + 3u * 257u * 4u + 2u * (257u + 256u) * 4u + 2u * (c1 / 32 + 1) * 2u + 256u;
-        };
-        while (ch > 1024 && lds_bytes(ch, cc) > 150u * 1024u) {
-            ch /= 2;
-            cc /= 2;
-        }
-        if (lds_bytes(ch, cc) > 150u * 1024u) return true;  // no persistent matcher (shb_match only)
-        SideGen gp;
-        gp.pfx[0] = gp.pfx[1] = "x0_";
-        gp.need[0] = gp.need[1] = &need_r;
-        gp.tmp = 5000;
-        const std::string part = "bool ok = true;\n" + unguard(gp.terms(F.f1, "ok")) + unguard(gp.terms(F.ionly, "ok"));
-        std::string ps = "\n#undef SHB_TPB\n#define SHB_TPB 1024\n#undef SHB_OFF\n#define SHB_OFF(t32) (false)\n"
-                         "#undef SHB_PROF\n#define SHP_CH " + std::to_string(ch) + "\n#define SHP_CC " + std::to_string(cc) +
-                         "\n#define SHP_SPAN (SHP_CH + SHP_CC)\n#define SHP_CTP 256\n#define SHP_NR (SHP_CH / SHB_TPB)\n"
-                         "#define SHP_SR (SHP_SPAN / SHB_TPB)\n"
-                         "static_assert(SHP_NR * SHB_TPB == SHP_CH && SHP_SR * SHB_TPB == SHP_SPAN && SHP_SPAN < 65536, \"pspan\");\n";
-        ps += R"(
-extern "C" __global__ void __launch_bounds__(SHB_TPB, 1) shb_pmatch(shb_plan P) {
-__shared__ uint32_t s_ws[SHP_SPAN];
-__shared__ __attribute__((aligned(16))) uint8_t s_used[SHP_SPAN];
-// the chunk's consumers in sorted order: sorted position | arrival index << 16
-__shared__ uint32_t s_cons[SHP_CH];
-__shared__ uint16_t s_pre[SHP_CH];
-__shared__ uint32_t u_buf[(SHB_TPB / 64) * 256];  // rank phase: per-wave key counts; then the u16 consumed masks
-uint32_t (*const wcnt)[256] = (uint32_t(*)[256])u_buf;
-uint16_t* const s_msk = (uint16_t*)u_buf;
-static_assert((SHB_TPB / 64) * 256 * 4 >= SHP_CH * 2, "masks fit u_buf");
-// the carry: pending partials (and each key's latest event) grouped by local key
-__shared__ uint32_t c_ws[SHP_CC];
-__shared__ uint32_t ccnt[256], kb0[257], cinc[256];
-// per chunk (double-buffered: the next chunk's table is built while the current
-// one is still in use): segment starts in span order, first slots, and the
-// segment of every 32nd chunk event
-__shared__ uint32_t seg_p[2][SHP_CTP + 1], seg_g[2][SHP_CTP];
-__shared__ uint16_t seg_of[2][SHP_CH / 32 + 1];
-__shared__ uint32_t ws[SHB_TPB / 64];
-__shared__ int s_i[4];
-)";
-        for (int a : staged_out) {
-            const std::string ct = col_ctype(P.attr_type[0][a]);
-            ps += "__shared__ " + ct + " " + lds(a) + "[SHP_SPAN];\n__shared__ " + ct + " c_a" + std::to_string(a) +
-                  "[SHP_CC];\n";
-        }
-        for (size_t k = 0; k < staged_out.size(); k++) {
-            const int a = staged_out[k];
-            const std::string ct = col_ctype(P.attr_type[0][a]);
-            ps += "const " + ct + "* __restrict__ g_a" + std::to_string(a) + " = (const " + ct + "*)P.st_dst[" +
-                  std::to_string(k) + "];\n";
-        }
-        ps += R"(
-const int b = (int)((blockIdx.x & 7u) * (SHB_NB / 8) + ((blockIdx.x >> 3) & (SHB_NB / 8 - 1)));
-const int kb = P.kb;
-const uint32_t kmask = (1u << kb) - 1u;
-const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
-const uint64_t lt_ = lane ? (~0ull >> (64 - lane)) : 0ull;
-const int64_t tsb0 = (int64_t)b * P.tstride, tsb1 = (int64_t)(b + 1) * P.tstride;
-if (threadIdx.x < 256) ccnt[threadIdx.x] = 0u;
-unsigned long long t_prev = wall_clock64();
-#define SHB_PROF(ph) if (P.prof && threadIdx.x == 0) { const unsigned long long t_now = wall_clock64(); atomicAdd(&P.prof[ph], t_now - t_prev); t_prev = t_now; }
-// the global slot of chunk event i (segments of table `bf` in span order)
-#define SHP_GIDX(bf, i, out) { int sg_ = seg_of[bf][(i) >> 5]; while (seg_p[bf][sg_ + 1] <= (uint32_t)(i)) sg_++; \
-    out = seg_g[bf][sg_] + ((uint32_t)(i) - seg_p[bf][sg_]); }
-// a chunk's tiles: this thread's tile (threads < SHP_CTP) -> its segment length and first slot
-uint32_t tlen_ = 0u, tgs_ = 0u;
-auto tiles_load = [&](int a0) {
-    tlen_ = 0u;
-    tgs_ = 0u;
-    const int T_ = a0 + (int)threadIdx.x;
-    if ((int)threadIdx.x < SHP_CTP && T_ < P.nt) {
-        const uint32_t lo_ = P.tofft[tsb0 + T_], hi_ = P.tofft[tsb1 + T_];
-        tlen_ = hi_ - lo_;
-        tgs_ = ((uint32_t)T_ << SHB_TILE_SHIFT) + lo_;
-    }
-};
-// the segment table of the chunk starting at tile a0: as many tiles as fit SHP_CH
-// events (0 with tiles left: one segment alone is larger, SHB_F_SPAN)
-auto seg_build = [&](int bf, int a0) -> int {
-    uint32_t tot;
-    const uint32_t pre = shw_block_excl<SHB_TPB>((int)threadIdx.x < SHP_CTP ? tlen_ : 0u, ws, &tot);
-    const int ne_ = __syncthreads_count((int)threadIdx.x < SHP_CTP && a0 + (int)threadIdx.x < P.nt &&
-                                        pre + tlen_ <= SHP_CH);
-    if ((int)threadIdx.x < ne_) {
-        seg_p[bf][threadIdx.x] = pre;
-        seg_g[bf][threadIdx.x] = tgs_;
-        for (uint32_t j = (pre + 31u) >> 5; (j << 5) < pre + tlen_; j++) seg_of[bf][j] = (uint16_t)threadIdx.x;
-    }
-    if ((int)threadIdx.x == ne_) seg_p[bf][ne_] = pre;
-    if (ne_ == 0 && a0 < P.nt && threadIdx.x == 0) atomicOr(P.flag, SHB_F_SPAN);
-    return ne_;
-};
-// the chunk's events into registers (all loads in flight together): wave v owns
-// the contiguous chunk events [v * SHP_NR * 64, (v + 1) * SHP_NR * 64)
-uint32_t wr[SHP_NR];
-)";
-        for (int a : staged_out) ps += std::string(col_ctype(P.attr_type[0][a])) + " vr" + std::to_string(a) + "[SHP_NR];\n";
-        ps += R"(auto issue = [&](int bf, int nc_) {
-#pragma unroll
-    for (int k = 0; k < SHP_NR; k++) {
-        const int i = (wv * SHP_NR + k) * 64 + lane;
-        uint32_t gi = 0u;
-        if (i < nc_) SHP_GIDX(bf, i, gi)
-        wr[k] = i < nc_ ? P.w0[gi] : 0u;
-)";
-        for (int a : staged_out)
-            ps += "        vr" + std::to_string(a) + "[k] = i < nc_ ? g_a" + std::to_string(a) + "[gi] : 0;\n";
-        ps += R"(    }
-};
-tiles_load(0);
-int ne = seg_build(0, 0);
-__syncthreads();
-int nc = (int)seg_p[0][ne];
-issue(0, nc);
-int a = 0, cur = 0;
-while (ne > 0) {
-const int an = a + ne, nxt = cur ^ 1;
-tiles_load(an);  // the next chunk's bucket starts, in flight while this chunk is ranked
-SHB_PROF(5)
-// stable sort by local key: each wave ranks its own events (kb ballots per round,
-// running per-key counts of the wave), one block pass combines the waves and
-// places every key's run after its carried entries
-for (int c = lane; c < 256; c += 64) wcnt[wv][c] = 0u;
-uint32_t rw[SHP_NR];
-#pragma unroll
-for (int k = 0; k < SHP_NR; k++) {
-    const int i = (wv * SHP_NR + k) * 64 + lane;
-    const bool valid = i < nc;
-    const uint32_t d = wr[k] & kmask;
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int bb = 0; bb < 8; bb++) {
-        if (bb < kb) {
-            const bool bit = (d >> bb) & 1u;
-            const uint64_t m = __ballot(valid && bit);
-            peers &= bit ? m : ~m;
-        }
-    }
-    const uint32_t r = (uint32_t)__popcll(peers & lt_);
-    const uint32_t base = valid ? wcnt[wv][d] : 0u;
-    rw[k] = valid ? ((base + r) | (d << 16)) : ~0u;
-    if (valid && r == 0) wcnt[wv][d] = base + (uint32_t)__popcll(peers);
-}
-__syncthreads();
-{
-    uint32_t tot = 0, all;
-    if (threadIdx.x < 256) {
-#pragma unroll
-        for (int q = 0; q < SHB_TPB / 64; q++) {
-            const uint32_t c = wcnt[q][threadIdx.x];
-            wcnt[q][threadIdx.x] = tot;
-            tot += c;
-        }
-    }
-    // one scan for both: the key's span length (low 16 bits) and its carried entries (high)
-    const uint32_t cc = threadIdx.x < 256 ? ccnt[threadIdx.x] : 0u;
-    const uint32_t ex = shw_block_excl<SHB_TPB>(threadIdx.x < 256 ? ((tot + cc) | (cc << 16)) : 0u, ws, &all);
-    if (threadIdx.x < 256) {
-        kb0[threadIdx.x] = ex & 0xFFFFu;
-        cinc[threadIdx.x] = (ex >> 16) + cc;
-    }
-    if (threadIdx.x == 0) kb0[256] = all & 0xFFFFu;
-}
-__syncthreads();
-const int L = (int)kb0[256];
-{
-#pragma unroll
-    for (int k = 0; k < SHP_NR; k++) {
-        if (rw[k] == ~0u) continue;
-        const int i = (wv * SHP_NR + k) * 64 + lane;
-        const uint32_t d = (rw[k] >> 16) & 0xFFu;
-        const int pos = (int)(kb0[d] + ccnt[d] + wcnt[wv][d] + (rw[k] & 0xFFFFu));
-        s_ws[pos] = wr[k];
-        s_cons[pos - (int)cinc[d]] = (uint32_t)pos | ((uint32_t)i << 16);
-)";
-        for (int a : staged_out) ps += "        " + lds(a) + "[pos] = vr" + std::to_string(a) + "[k];\n";
-        ps += R"(    }
-    const int ctot = (int)cinc[255];
-    for (int e = (int)threadIdx.x; e < ctot; e += SHB_TPB) {
-        const uint32_t w = c_ws[e];
-        const uint32_t d = w & kmask;
-        const int pos = (int)(kb0[d] + (uint32_t)e - (cinc[d] - ccnt[d]));
-        s_ws[pos] = w;
-)";
-        for (int a : staged_out) ps += "        " + lds(a) + "[pos] = c_a" + std::to_string(a) + "[e];\n";
-        ps += R"(    }
-    for (int p = (int)threadIdx.x * 4; p < L; p += SHB_TPB * 4) *(uint32_t*)(s_used + p) = 0u;
-}
-__syncthreads();
-SHB_PROF(1)
-// the next chunk's segment table, then its events in flight during the walk
-const int ne2 = seg_build(nxt, an);
-if (threadIdx.x < 256) ccnt[threadIdx.x] = 0u;  // (this chunk's carry counts are no longer read)
-__syncthreads();
-const int nc2 = (int)seg_p[nxt][ne2];
-issue(nxt, nc2);
-SHB_PROF(0)
-{
-const int hl = 0;
-)";
-        if (fdom && kWalkDyn) {
-            ps += walk_count_f_dyn(true);
-        } else {
-            ps += "for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {\nconst uint32_t cw = s_cons[ci];\n"
-                  "const int sp = (int)(cw & 0xFFFFu), i = hl + (int)(cw >> 16);\nuint32_t c_ = 0;\n";
-            ps += fdom ? walk_count_f(true) : walk_count(true);
-            ps += "if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);\ns_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);\n"
-                  "s_msk[i - hl] = (uint16_t)mask;\n}\n";
-        }
-        ps += R"(}
-__syncthreads();
-SHB_PROF(2)
-// the counts to the events' slots and their exclusive prefix over the chunk
-// (arrival order); the span entries the next chunk carries, compacted in span
-// order (so grouped by local key): one scan for both
-uint32_t total;
-{
-    const int p0 = (int)threadIdx.x * SHP_NR;
-    uint32_t v[SHP_NR];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int q = 0; q < SHP_NR; q++) {
-        v[q] = (p0 + q < nc) ? (uint32_t)s_pre[p0 + q] : 0u;
-        sum += v[q];
-    }
-    const int s0 = (int)threadIdx.x * SHP_SR;
-    uint32_t kp = 0u;
-#pragma unroll
-    for (int q = 0; q < SHP_SR; q++) {
-        const int p = s0 + q;
-        if (p < L) {
-            const uint32_t w = s_ws[p];
-            const uint32_t e = kb0[(w & kmask) + 1u] - 1u;  // the key's latest event
-            const uint32_t tl32 = s_ws[e] >> kb;
-            const uint32_t tlo = tl32 > SHB_WLIM ? tl32 - SHB_WLIM : 0u;
-            uint32_t keep = (uint32_t)p == e ? 1u : 0u;
-            if (!keep && !s_used[p] && (w >> kb) >= tlo) {
-)";
-        ps += decl_attrs(need_r, 0) + loads(need_r, "x0_", "p") + part + "keep = ok ? 1u : 0u;\n";
-        ps += R"(            }
-            kp |= keep << q;
-        }
-    }
-    uint32_t all;
-    const uint32_t ex = shw_block_excl<SHB_TPB>(sum | ((uint32_t)__popc(kp) << 16), ws, &all);
-    total = all & 0xFFFFu;
-    if (threadIdx.x == 0 && (all >> 16) > SHP_CC) atomicOr(P.flag, SHB_F_CARRY);
-    uint32_t off = ex & 0xFFFFu;
-#pragma unroll
-    for (int q = 0; q < SHP_NR; q++) {
-        if (p0 + q < nc) {
-            uint32_t gi;
-            SHP_GIDX(cur, p0 + q, gi)
-            P.cnt[gi] = (uint8_t)v[q];
-            s_pre[p0 + q] = (uint16_t)off;
-        }
-        off += v[q];
-    }
-    uint32_t ko = ex >> 16;
-#pragma unroll
-    for (int q = 0; q < SHP_SR; q++) {
-        if ((kp >> q) & 1u) {
-            const int p = s0 + q;
-            if (ko < SHP_CC) {
-                const uint32_t w = s_ws[p];
-                c_ws[ko] = w;
-)";
-        for (int a : staged_out) ps += "                c_a" + std::to_string(a) + "[ko] = " + lds(a) + "[p];\n";
-        ps += R"(                atomicAdd(&ccnt[w & kmask], 1u);
-            }
-            ko++;
-        }
-    }
-}
-// the chunk's match-stream region (every partial is consumed at most once: the
-// regions of all chunks fit n values)
-if (threadIdx.x == 0) s_i[1] = total ? (int)atomicAdd(P.ms_ctr, total) : 0;
-__syncthreads();
-const int64_t rbase = (int64_t)(uint32_t)s_i[1];
-// per chunk tile: the first match position of its segment, its matches
-for (int t = (int)threadIdx.x; t < ne; t += SHB_TPB) {
-    const uint32_t x0 = seg_p[cur][t], x1 = seg_p[cur][t + 1];
-    const uint32_t q0 = x0 < (uint32_t)nc ? (uint32_t)s_pre[x0] : total;
-    const uint32_t q1 = x1 < (uint32_t)nc ? (uint32_t)s_pre[x1] : total;
-    const int T = a + t;
-    P.mstart[(int64_t)T * SHB_NB + b] = (uint32_t)rbase + q0;
-    if (q1 > q0) atomicAdd(&P.ttot[T], q1 - q0);
-}
-SHB_PROF(3)
-{
-const int hl = 0;
-)";
-        // the e1-side values of the consumed partials into the region (staged in
-        // s_ws and written as one run when no walk needs the slow path: the span
-        // is no longer read, the carry holds what the next chunk needs)
-        if (stage1) {
-            const std::string a0 = lds(ms_attrs[0]);
-            ps += "int slow_ = 0;\nfor (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {\n"
-                  "    if (s_msk[ci] & SHB_MOVF) slow_ = 1;\n}\n"
-                  "if (!__syncthreads_or(slow_)) {\n"
-                  "for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {\n"
-                  "    const uint32_t cw = s_cons[ci];\n"
-                  "    const int sp = (int)(cw & 0xFFFFu), i = (int)(cw >> 16);\n"
-                  "    const uint32_t off = s_pre[i];\n"
-                  "    const uint32_t cn = ((i + 1 < nc) ? (uint32_t)s_pre[i + 1] : total) - off;\n"
-                  "    uint32_t m = s_msk[i], k = 0;\n"
-                  "    while (m) {\n"
-                  "        const int o = sp - __ffs(m);\n"
-                  "        m &= m - 1u;\n"
-                  "        s_ws[off + (cn - 1u - k)] = (uint32_t)" + a0 + "[o];\n"
-                  "        k++;\n"
-                  "    }\n}\n"
-                  "__syncthreads();\n"
-                  "for (int q = threadIdx.x; q < (int)total; q += SHB_TPB) ((uint32_t*)P.ms[0])[rbase + q] = s_ws[q];\n"
-                  "} else {\n";
-        }
-        ps += "for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {\nconst uint32_t cw = s_cons[ci];\n"
-              "const int sp = (int)(cw & 0xFFFFu), i = (int)(cw >> 16);\nconst uint32_t off = s_pre[i];\n"
-              "const uint32_t cn = ((i + 1 < nc) ? (uint32_t)s_pre[i + 1] : total) - off;\nif (cn == 0u) continue;\n"
-              "uint32_t k = 0;\n";
-        ps += "const uint32_t mk = s_msk[i];\nif (!(mk & SHB_MOVF)) {\n    uint32_t m = mk;\n"
-              "    while (m) {\n        const int o = sp - __ffs(m);\n        m &= m - 1u;\n"
-              "        const int64_t dst = rbase + (int64_t)off + (int64_t)(cn - 1u - k);\n        k++;\n" +
-              ms_put + "    }\n} else {\n" + walk(false, put) + "}\n}\n";
-        if (stage1) ps += "}\n";
-        ps += "}\n__syncthreads();\nSHB_PROF(4)\na = an;\ncur = nxt;\nne = ne2;\nnc = nc2;\n}\n}\n";
-        src += ps;
-    }
     return true;
 }
 
@@ -1822,14 +1472,8 @@ int shj_bucket_load(const shp_program* hp, const int* ms_attrs, int n_ms, shj_bu
             e->mod = nullptr;
             return -3;
         }
-        // the persistent matcher (absent when its LDS would not fit)
-        if (hipModuleGetFunction(&e->place, e->mod, "shb_pmatch") != hipSuccess) {
-            e->place = nullptr;
-            (void)hipGetLastError();
-        }
     }
     out->match = e->match;
-    out->pmatch = e->place;
     out->n_staged = (int)staged.size();
     for (size_t k = 0; k < staged.size(); k++) out->staged_attr[k] = staged[k];
     return 0;

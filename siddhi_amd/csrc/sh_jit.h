@@ -32,7 +32,6 @@ int shj_bucket_chunk(void);
 // match stream carries (e1-side select values), in match-stream column order
 struct shj_bucket {
     void* match;          // hipFunction_t shb_match
-    void* pmatch;         // hipFunction_t shb_pmatch (persistent, one workgroup per bucket), NULL if absent
     int n_staged;         // columns the partition moves into bucket order
     int staged_attr[4];
 };

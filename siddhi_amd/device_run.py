@@ -170,14 +170,9 @@ class DeviceRunner:
         return lib().shx_jit_status(self.handle.h)
 
     def bucket_status(self):
-        """3: the last run took the bucketed window engine (sh_bucket.hip) with its
-        persistent matcher (shb_pmatch), 1: with its per-pass matcher (shb_match),
-        0: another engine."""
+        """1: the last run took the bucketed window engine (sh_bucket.hip +
+        shb_match), 0: another engine."""
         return lib().shx_bucket_status(self.handle.h)
-
-    def bucket_refused(self):
-        """the device flags (SHB_F_*) that sent the last run off the persistent matcher"""
-        return lib().shx_bucket_refused(self.handle.h)
 
     def seq3_status(self):
         """1: the last run took the rise-and-fall sequence engine (k_seq3)."""

@@ -90,7 +90,7 @@ def test_c2_aggregates_bucketed_vs_oracle(n, K, carry, monkeypatch):
     ts, k, p, v = synth.stock_stream(n, K, 100)
     (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], K, packed=packed)
     ref = _oracle(C2_AGG, ts, [k, p, v], k)
-    assert st["bucket"] == 3 and st["agg"] == {"aggp": 5, "post": 1, "aggc": 4}[carry], st
+    assert st["bucket"] == 1 and st["agg"] == {"aggp": 5, "post": 1, "aggc": 4}[carry], st
     assert m == len(ref["seq"]) > 0
     assert np.array_equal(seq, ref["seq"].astype(np.int64))
     assert np.array_equal(vals, ref["values"])
@@ -167,7 +167,7 @@ def test_c2_aggregates_full_size_vs_restatement():
     from siddhi_amd import synth
     ts, k, p, v = synth.stock_stream(100_000_000, 10_000, 100)
     (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], 10_000)
-    assert st["bucket"] == 3 and st["agg"] == 5, st
+    assert st["bucket"] == 1 and st["agg"] == 5, st
     eseq, ev = c2_expected(ts, k, p, v)
     assert np.array_equal(seq, eseq)
     grp = k[eseq].astype(np.int64)

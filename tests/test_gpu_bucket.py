@@ -1,4 +1,4 @@
-"""GPU parity of the bucketed window engine (sh_bucket.hip + shb_pmatch / shb_match) through
+"""GPU parity of the bucketed window engine (sh_bucket.hip + shb_match) through
 the C-ABI (sh_run_device) against the CPU oracle: partitioned
 `every e1=S[f1] -> e2=S[f2] within W` with >= 1,024 keys. Bit-exact rows:
 trigger sequence numbers and raw select values. The engine's device premises
@@ -26,23 +26,10 @@ def _device():
         pytest.skip("no GPU")
 
 
-def _run(app, strings, ts, cols, keys, nk, columns=False, batch_events=4096, engine=None):
+def _run(app, strings, ts, cols, keys, nk, columns=False, batch_events=4096):
     """columns: typed output columns (d_out_cols), "packed": SH_OUT_PACKED rows;
-    both returned as raw rows for comparison. engine="walk": the bucketed engine's
-    per-pass matcher (shb_match) for the call (SH_BK_PERSIST=0), else the default
-    persistent matcher (shb_pmatch)"""
-    old = os.environ.get("SH_BK_PERSIST")
-    if engine == "walk":
-        os.environ["SH_BK_PERSIST"] = "0"
-    else:
-        os.environ.pop("SH_BK_PERSIST", None)
-    try:
-        return _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events)
-    finally:
-        if old is None:
-            os.environ.pop("SH_BK_PERSIST", None)
-        else:
-            os.environ["SH_BK_PERSIST"] = old
+    both returned as raw rows for comparison"""
+    return _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events)
 
 
 def _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events):
@@ -56,7 +43,7 @@ def _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events):
         m, rows = runner.run(torch.from_numpy(ts).to(dev), torch.from_numpy(keys).to(dev), tcols, nk,
                              packed=True, batch_events=batch_events)
         torch.cuda.synchronize()
-        status, err = runner.bucket_status(), runner.last_error() + f" (persistent matcher refused: {runner.bucket_refused()})"
+        status, err = runner.bucket_status(), runner.last_error()
         oseq, ovals = packed_to_raw(rows.cpu().numpy(), runner.out_types, offs, rb)
         runner.close()
         return (m, oseq.astype(np.int64), ovals), status, err
@@ -64,7 +51,7 @@ def _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events):
                                 columns=columns, batch_events=batch_events)
     torch.cuda.synchronize()
     status = runner.bucket_status()
-    err = runner.last_error() + f" (persistent matcher refused: {runner.bucket_refused()})"
+    err = runner.last_error()
     if columns:
         assert [c.dtype for c in ovals] == [{0: torch.int32, 1: torch.int32, 2: torch.int64, 3: torch.float32,
                                              4: torch.float64, 5: torch.uint8}[t] for t in runner.out_types]
@@ -75,26 +62,22 @@ def _run_inner(app, strings, ts, cols, keys, nk, columns, batch_events):
     return res, status, err
 
 
-@pytest.mark.parametrize("engine,expect", [(None, 3), ("walk", 1)])
-def test_c2_bucket_vs_oracle(engine, expect):
-    """status 3: the persistent matcher (default), 1: the per-pass matcher"""
+def test_c2_bucket_vs_oracle():
     n, nk = 400_000, 2_000
     ts, k, p, v = synth.stock_stream(n, nk, 100)
     ca = compiler.compile_app(synth.C2_QUERY)
     seq, _, vals, _ = run_stock_oracle(ca, ts, k, p, v)
-    (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk, engine=engine)
-    assert status == expect, err
+    (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk)
+    assert status == 1, err
     assert m == len(seq) > 0
     assert np.array_equal(oseq, seq.astype(np.int64))
     assert np.array_equal(ovals, vals)
 
 
-@pytest.mark.parametrize("n,nk,bucketed,columns,engine", [
-    (10_000_000, 10_000, 3, False, None), (10_000_000, 10_000, 1, False, "walk"),
-    (100_000_000, 10_000, 1, "packed", "walk"), (100_000_000, 10_000, 3, "packed", None),
-    (100_000_000, 10_000, 3, True, None), (3_000_000, 60_000, 1, False, "walk"),
-    (3_000_000, 60_000, 3, True, None), (3_000_000, 60_000, 3, "packed", None)])
-def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed, columns, engine):
+@pytest.mark.parametrize("n,nk,bucketed,columns", [
+    (10_000_000, 10_000, 1, False), (100_000_000, 10_000, 1, "packed"), (100_000_000, 10_000, 1, True),
+    (3_000_000, 60_000, 1, False), (3_000_000, 60_000, 1, True), (3_000_000, 60_000, 1, "packed")])
+def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed, columns):
     """60k symbols at 100 ev/ms: a key's previous event is often more than a
     window back, so many walks leave their key's run in the span; the halo covers
     the window in time and the check against the latest timestamp before the
@@ -102,7 +85,7 @@ def test_c2_bucket_full_size_vs_restatement(n, nk, bucketed, columns, engine):
     `columns`: typed output columns or packed rows (the bucketed engine writes them
     itself; "packed" at 100M is the bench's layout)"""
     ts, k, p, v = synth.stock_stream(n, nk, 100)
-    (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk, columns, engine=engine)
+    (m, oseq, ovals), status, err = _run(synth.C2_QUERY, None, ts, [k, p, v], k, nk, columns)
     assert status == bucketed, err
     eseq, evals = c2_expected(ts, k, p, v)
     assert m == len(eseq) > 0
@@ -140,7 +123,7 @@ def test_random_window_queries_bucket_vs_oracle(seed):
     seq, _, vals, nulls = run_columns_oracle(ca, ts, [keys, price, vol, x], keys)
     layout = [False, "packed", True][seed % 3]  # raw rows, packed rows, typed columns
     (m, oseq, ovals), status, err = _run(app, strings, ts, [keys, price, vol, x], keys, nk, layout)
-    assert status >= 0, err  # 3 / 1 bucketed, 0 another engine (not applicable / premise failed)
+    assert status >= 0, err  # 1 bucketed, 0 another engine (not applicable / premise failed)
     assert m == len(seq), app
     assert np.array_equal(oseq, seq.astype(np.int64)), app
     nn = ~nulls.astype(bool)
