@@ -483,11 +483,12 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     B.n = n;
     B.nt = (int32_t)((n + SHB_TILE - 1) / SHB_TILE);
     B.kb = kb;
-    // tiles per matcher chunk: 7/8 of the pass's consumer limit in events of a
-    // bucket at uniform keys (32 per tile; 56 tiles at 2,048), so a chunk and its
-    // halo fit the LDS span; denser buckets split
+    // tiles per matcher chunk: 15/16 of the pass's consumer limit in events of a
+    // bucket at uniform keys (32 per tile; 60 tiles at 2,048), so a chunk and its
+    // halo fit the LDS span; denser buckets split (C2: 60 tiles 1.90 ms, 56 1.97-1.99,
+    // 52 2.07, 64 2.50 in one call, profiles/r6_c2_ct_ab.txt)
     static const int ct_env = getenv("SH_BK_CT") ? atoi(getenv("SH_BK_CT")) : 0;
-    B.ct = ct_env > 0 ? std::min(ct_env, SHB_CT_MAX) : std::min(shj_bucket_chunk() * 7 / 256, SHB_CT_MAX);
+    B.ct = ct_env > 0 ? std::min(ct_env, SHB_CT_MAX) : std::min(shj_bucket_chunk() * 15 / 512, SHB_CT_MAX);
     B.n_chunks = (B.nt + B.ct - 1) / B.ct;
     const int64_t slots = (int64_t)B.nt * SHB_TILE;  // the tiles' bucket order
     if (ensure_ws(h, std::max<int64_t>(n, (int64_t)B.nt + 1)) || h->bk_w0.ensure_fresh(slots * 4) ||
