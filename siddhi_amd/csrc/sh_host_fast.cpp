@@ -213,6 +213,7 @@ static int run_rules_sparse(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     hipStream_t st = h->stream;
     const int64_t n = run->n;
     if (n <= 1 || n >= (int64_t)0xFFFFFFFFll || !run->d_keys) return 1;
+    if (h->r_rules.size() >= ((size_t)1 << 20)) return 1;  // (k_sparse_open's pairs hold 20-bit rule ids)
     const int64_t cap = std::max<int64_t>(65536, n / 8);
     const size_t nk1 = (size_t)nkeys + 1;
     if (h->rs_pr.ensure_fresh((size_t)cap * 16) || h->rs_key.ensure_fresh(nk1 * 12) ||

@@ -36,6 +36,7 @@
 #include "sh_device.h"
 #include "sh_rules.h"
 #include "sh_vm.h"
+#include "sh_wave.h"
 
 #define RTPB 256
 // a sorted timestamp: 32-bit offsets from tb when the run's range fits (s32), else int64
@@ -635,9 +636,10 @@ extern "C" int shr_ts_to32(const int64_t* ts, int64_t n, int64_t base, uint32_t*
 // later event q of its key with |ts_q - ts_p| <= W_r and f2_r(p, q) -- so with
 // non-decreasing timestamps (checked over the whole run) the consuming event is
 // the least such q:
-//   k_sparse_open: per event (arrival order) the index lookup and f1 of its
-//     candidate rules -> the partials (p, r), appended through an LDS buffer per
-//     workgroup, and per key a count (the partial's slot in its key's list);
+//   k_sparse_open: per event (arrival order) the index lookup of its candidate
+//     rules, the round's (event, rule) pairs expanded in LDS, f1 per pair (one
+//     lane each) -> the partials (p, r), appended through an LDS buffer per wave,
+//     and per key a count (the partial's slot in its key's list);
 //   scan of the per-key counts -> each key's list;
 //   k_sparse_place: the partials into their keys' lists, with their expiry time;
 //   k_sparse_take: per event q, its key's partials opened before it that are not
@@ -770,7 +772,8 @@ __device__ __forceinline__ bool spa_f2(const shr_table* __restrict__ RT, const s
     return rule_terms(R->t[1], R->nt[1], p, q, C);
 }
 
-#define SPA_WBUF 256  // partials a wave holds before it appends them (one global atomic per flush)
+#define SPA_WBUF 192  // partials a wave holds before it appends them (one global atomic per flush)
+#define SPA_PAIRS 6144  // (event, candidate rule) pairs of a round expanded in LDS, at most
 
 template <bool IMG>
 __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __restrict__ RT,
@@ -788,6 +791,10 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
     // waves run independently, no block barrier after the image is staged
     __shared__ uint32_t w_p[SPA_TPB / 64][SPA_WBUF], w_r[SPA_TPB / 64][SPA_WBUF], w_k[SPA_TPB / 64][SPA_WBUF];
     __shared__ uint32_t w_fill[SPA_TPB / 64];
+    // a round's (event, candidate rule) pairs: rule << 12 | the event's index in the round
+    __shared__ uint32_t s_pair[SPA_PAIRS];
+    __shared__ uint32_t s_ws[SPA_TPB / 64];
+    static_assert(SPA_TPB * SPA_U <= 4096, "12-bit event index in a pair");
     spa_stage<IMG>(img, I, C, s_img, s_col);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -828,18 +835,6 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
             key[u] = in ? akeys[p] : -1;
             xv[u] = (in && ix_col) ? rule_ix_key(ix_ty, rule_attr(s_col, ix_attr, ix_ty, (uint32_t)p)) : 0;
         }
-        // f1's most read attributes of the event, loaded with it (IMG: the terms
-        // come from LDS, so these are the chain's only global reads)
-        RowPre rp[SPA_U];
-#pragma unroll
-        for (int u = 0; u < SPA_U; u++) {
-            const int64_t p = base + (int64_t)u * SPA_TPB + threadIdx.x;
-            rp[u].slot = 0;
-            rp[u].a[0] = pa0;
-            rp[u].a[1] = pa1;
-            rp[u].v[0] = (pa0 >= 0 && p < n) ? rule_attr(s_col, pa0, RT->attr_type[pa0], (uint32_t)p) : 0;
-            rp[u].v[1] = (pa1 >= 0 && p < n) ? rule_attr(s_col, pa1, RT->attr_type[pa1], (uint32_t)p) : 0;
-        }
         uint32_t lo[SPA_U], hi[SPA_U];
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
@@ -848,39 +843,66 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
             lo[u] = hi[u] = 0;
             if (ix_col && key[u] >= 0 && key[u] < nkeys) spa_candidates<IMG>(RT, I, S, img, xv[u], &lo[u], &hi[u]);
         }
+        // the pairs of the round, expanded in LDS so that each lane evaluates f1 for
+        // one (event, rule) pair: no wave waits for its event with the most candidate
+        // rules (C5: ~1 candidate per event, ~5 for a wave's busiest). A round with
+        // more pairs than fit expands them in batches of SPA_PAIRS.
+        uint32_t tc = 0u;
 #pragma unroll
-        for (int u = 0; u < SPA_U; u++) {
-            const int64_t p = base + (int64_t)u * SPA_TPB + threadIdx.x;
-            const bool live = key[u] >= 0 && key[u] < nkeys;
-            const uint32_t total = live ? hi[u] - lo[u] + n_free : 0u;
-            const uint32_t nsel = hi[u] - lo[u];
-            // every lane of the wave takes the same number of steps (the wave's most
-            // candidate rules), so each step's partials are ranked by one ballot
-            uint32_t steps = total;
-            for (int o = 32; o > 0; o >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, o));
-            for (uint32_t k = 0; k < steps; k++) {
-                uint32_t r = 0u;
+        for (int u = 0; u < SPA_U; u++)
+            tc += (key[u] >= 0 && key[u] < nkeys) ? hi[u] - lo[u] + n_free : 0u;
+        uint32_t np_;
+        const uint32_t at0 = shw_block_excl<SPA_TPB>(tc, s_ws, &np_);
+        for (uint32_t b0 = 0; b0 < np_; b0 += SPA_PAIRS) {
+            const uint32_t b1 = b0 + SPA_PAIRS;
+            uint32_t at = at0;
+#pragma unroll
+            for (int u = 0; u < SPA_U; u++) {
+                const bool live = key[u] >= 0 && key[u] < nkeys;
+                const uint32_t total = live ? hi[u] - lo[u] + n_free : 0u;
+                const uint32_t nsel = hi[u] - lo[u];
+                for (uint32_t k = 0; k < total; k++, at++)
+                    if (at >= b0 && at < b1)
+                        s_pair[at - b0] = (spa_rule_id<IMG>(RT, I, S, lo[u], k, nsel) << 12) |
+                                          (uint32_t)(u * SPA_TPB + (int)threadIdx.x);
+            }
+            __syncthreads();
+            const uint32_t nb = min(np_ - b0, (uint32_t)SPA_PAIRS);
+            for (uint32_t q0 = 0; q0 < nb; q0 += SPA_TPB) {
+                const uint32_t q = q0 + threadIdx.x;
                 bool ok = false;
-                if (k < total) {
-                    r = spa_rule_id<IMG>(RT, I, S, lo[u], k, nsel);
-                    ok = spa_f1<IMG>(RT, I, S, C, r, (uint32_t)p, rp[u]);
+                uint32_t r = 0u, pp = 0u;
+                int32_t kk = 0;
+                if (q < nb) {
+                    const uint32_t w = s_pair[q];
+                    r = w >> 12;
+                    pp = (uint32_t)(base + (int64_t)(w & 4095u));
+                    // f1's most read attributes of the event (IMG: the terms come from LDS)
+                    RowPre rq;
+                    rq.slot = 0;
+                    rq.a[0] = pa0;
+                    rq.a[1] = pa1;
+                    rq.v[0] = pa0 >= 0 ? rule_attr(s_col, pa0, RT->attr_type[pa0], pp) : 0;
+                    rq.v[1] = pa1 >= 0 ? rule_attr(s_col, pa1, RT->attr_type[pa1], pp) : 0;
+                    kk = akeys[pp];
+                    ok = spa_f1<IMG>(RT, I, S, C, r, pp, rq);
                 }
                 const uint64_t m = __ballot(ok);
                 if (m == 0ull) continue;
                 const uint32_t fill = w_fill[wv];
-                const uint32_t at = fill + (uint32_t)__popcll(m & lt);
+                const uint32_t wat = fill + (uint32_t)__popcll(m & lt);
                 if (ok) {
-                    atomicAdd(&key_cnt[key[u]], 1u);  // (no return: the slot is taken at placement)
-                    if (at < SPA_WBUF) {
-                        w_p[wv][at] = (uint32_t)p;
-                        w_r[wv][at] = r;
-                        w_k[wv][at] = (uint32_t)key[u];
+                    atomicAdd(&key_cnt[kk], 1u);  // (no return: the slot is taken at placement)
+                    if (wat < SPA_WBUF) {
+                        w_p[wv][wat] = pp;
+                        w_r[wv][wat] = r;
+                        w_k[wv][wat] = (uint32_t)kk;
                     } else {
                         const unsigned long long g = atomicAdd(ctr, 1ull);  // (buffer full: straight out)
                         if ((int64_t)g < cap) {
-                            pr_p[g] = (uint32_t)p;
+                            pr_p[g] = pp;
                             pr_r[g] = r;
-                            pr_key[g] = (uint32_t)key[u];
+                            pr_key[g] = (uint32_t)kk;
                         }
                     }
                 }
@@ -891,6 +913,7 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
                     if (lane == 0) w_fill[wv] = 0u;
                 }
             }
+            __syncthreads();  // (the next batch or round rewrites the pairs)
         }
     }
     {
@@ -1077,7 +1100,7 @@ extern "C" int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int
     const int pa0 = pre ? pre[0] : -1, pa1 = pre ? pre[1] : -1;
     shr_img none;
     memset(&none, 0, sizeof(none));
-    const int buf = 3 * (SPA_TPB / 64) * SPA_WBUF * 4 + 512;
+    const int buf = 3 * (SPA_TPB / 64) * SPA_WBUF * 4 + SPA_PAIRS * 4 + 512;
     static const int lim = spa_img_attr(&k_sparse_open<true>);
     const bool use_img = spa_img_fits(img, I, buf) && I->lds <= lim &&
                          !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0');
