@@ -252,19 +252,13 @@ __global__ void __launch_bounds__(TPB, MINW) k_bk_scatter(const int32_t* __restr
 //     consumer-side values are read by arrival index, the e1-side values from
 //     the match stream
 #define BK_EHALF 512   // events of one row-map pass of a wave
-#ifndef BK_WARM_B
-#define BK_WARM_B 128  // bytes per warming read (one per 128-byte line; 64 measured 1.43 vs 1.405 ms)
-#endif
 #define BK_PFX_BITS 24  // pfx words: prefix in the low bits, the slot's bucket above
 #define BK_PFX_MASK ((1u << BK_PFX_BITS) - 1u)
 #define BK_NOSLOT 0xFFFFFFFFu
 #define BK_EROWS 1024  // rows the wave's map holds per pass (more: event-parallel writes)
 
-// select value o of a row (raw 8-byte form)
-// (kind 0: by match-stream position, 1: by event, 2: by output row -- the aggregate carry's
-// running values, SHB_OUT_KIND_ROW)
-#define BK_VAL(o, i, mp, row) \
-    bk_raw(O.src[o], O.kind[o] == 1 ? (i) : (O.kind[o] == SHB_OUT_KIND_ROW ? (row) : (mp)), O.type[o])
+// select value o of a row (raw 8-byte form; kind 0: by match-stream position, 1: by event)
+#define BK_VAL(o, i, mp, row) bk_raw(O.src[o], O.kind[o] == 1 ? (i) : (mp), O.type[o])
 
 
 // the select values of a row (NO > 0: unrolled, the descriptors in scalar registers)
@@ -297,7 +291,7 @@ __device__ __forceinline__ void bk_row(const shb_out& O, const shb_cols& OC, con
         out_seq[row] = seq;
     }
     for (int o = 0; o < no; o++) {
-        const int64_t v = bk_raw(o_src[o], o_kind[o] == 1 ? i : (o_kind[o] == SHB_OUT_KIND_ROW ? row : mp), o_type[o]);
+        const int64_t v = bk_raw(o_src[o], o_kind[o] == 1 ? i : mp, o_type[o]);
         if (MODE == SHB_OUT_PACKED) {
             uint32_t* r = (uint32_t*)OC.rows + row * OC.rw + OC.woff[o];
             r[0] = OC.colw[o] == 1 ? (uint32_t)(uint8_t)v : (uint32_t)v;
@@ -339,24 +333,6 @@ __global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out 
     const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
     const int tile_n = (int)((P.n - b0) < SHB_TILE ? (P.n - b0) : SHB_TILE);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // L2 warming (O.warm = 1): one read per 128-byte line of this wave's consumer-side
-    // columns, issued ahead of the loads the kernel first waits on, so that phase 3's
-    // row loads (rows -> their events, by arrival index) hit L2 instead of HBM; the
-    // values only feed an empty asm at the end (no memory effect)
-    uint32_t warm = 0u;
-    if (NO > 0 && O.warm) {
-        const int64_t e0 = b0 + (int64_t)w * (64 * BK_ITEMS);
-        const int nw = tile_n - w * (64 * BK_ITEMS);
-#pragma unroll
-        for (int o = 0; o < NV; o++) {
-            if (O.kind[o] != 1) continue;
-            const int wd = bk_width(O.type[o]);
-            const int per = BK_WARM_B / wd;  // events per warming read
-            for (int e = lane * per; e < nw && e < 64 * BK_ITEMS; e += 64 * per)
-                warm ^= wd == 1 ? (uint32_t)((const uint8_t*)O.src[o])[e0 + e]
-                                : ((const uint32_t*)O.src[o])[(e0 + e) * (wd / 4)];
-        }
-    }
     if (threadIdx.x <= SHB_NB) to[threadIdx.x] = P.toff[(int64_t)T * SHB_TOFF + threadIdx.x];
     if (threadIdx.x < SHB_NB) ms0[threadIdx.x] = P.mstart[(int64_t)T * SHB_NB + threadIdx.x];
     if (threadIdx.x == 0) s_tb = P.ttot[T];
@@ -419,22 +395,6 @@ __global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out 
         if (threadIdx.x == 0) pfx[SHB_TILE] = tot;
         __syncthreads();
     }
-    // L2 warming of the match stream: the first line (two when longer) of each of the
-    // tile's (tile, bucket) segments that has matches
-    if (NO > 0 && O.warm && threadIdx.x < SHB_NB) {
-        const int bb = threadIdx.x;
-        const uint32_t m0 = pfx[to[bb]] & BK_PFX_MASK, m1 = pfx[to[bb + 1]] & BK_PFX_MASK;
-        if (m1 > m0) {
-            const int64_t p0 = ms0[bb];
-#pragma unroll
-            for (int o = 0; o < NV; o++) {
-                if (O.kind[o] != 0) continue;
-                const int wd = bk_width(O.type[o]);
-                for (int64_t p1 = p0; p1 < p0 + (int64_t)(m1 - m0) && p1 < p0 + 2 * (BK_WARM_B / wd); p1 += BK_WARM_B / wd)
-                    warm ^= wd == 1 ? (uint32_t)((const uint8_t*)O.src[o])[p1] : ((const uint32_t*)O.src[o])[p1 * (wd / 4)];
-            }
-        }
-    }
     // 2. counts (4 packed per register) and match-stream positions of the wave's events
     uint32_t cp[BK_ITEMS / 4];
     uint32_t mp[BK_ITEMS];
@@ -449,7 +409,7 @@ __global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out 
             const uint32_t d = pw >> BK_PFX_BITS;
             const uint32_t ps = pw & BK_PFX_MASK;
             c = (pfx[s + 1] & BK_PFX_MASK) - ps;
-            mp[j] = O.ms_slot ? (uint32_t)(b0 + s) : ms0[d] + ps - (pfx[to[d]] & BK_PFX_MASK);
+            mp[j] = ms0[d] + ps - (pfx[to[d]] & BK_PFX_MASK);
         }
         if ((j & 3) == 0) cp[j >> 2] = 0u;
         cp[j >> 2] |= c << (8 * (j & 3));
@@ -544,7 +504,6 @@ __global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out 
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (NO > 0 && O.warm) asm volatile("" ::"v"(warm));
 }
 
 // ---------------------------------------------------------------- halo bound
@@ -902,213 +861,6 @@ __global__ void __launch_bounds__(S3B_TPB) k_s3b(shb_plan P, shb_s3 S) {
     if (S.warm) asm volatile("" ::"v"(warm));
 }
 
-// ---------------------------------------------------------------- sequence carry, sub-buckets
-// k_s3b with two workgroups per key bucket (S.sub = 1): workgroup (b, h) carries the
-// bucket's local keys of parity h (local key & 1 == h), so 512 workgroups of 512
-// threads and half-size chunks (72 KB of LDS: two per CU) replace 256 of 1,024 (131
-// KB: one per CU), and a CU overlaps one workgroup's carry walk with the other's
-// loads and sort. A chunk gathers up to S3C_RAW events of the bucket's segments and
-// keeps its parity's (~half: S3C_CH bounds it with > 50 sigma to spare on uniform
-// keys; more sets SHB_F_SPAN and the host runs k_s3b). The two workgroups of a bucket
-// interleave their events inside every (tile, bucket) segment, so a match's e1 /
-// last values go to the match stream AT ITS EVENT'S SLOT (one match per event at
-// most) and the emitter addresses them so (shb_out.ms_slot); per tile one atomic
-// per workgroup and chunk adds its matches.
-#define S3C_TPB 512
-#define S3C_CH 2048
-#define S3C_NR (S3C_CH / S3C_TPB)
-#define S3C_W (S3C_TPB / 64)
-#define S3C_NK (S3B_NK / 2)
-#define S3C_RAW 3584  // events of a chunk before the parity split
-
-__device__ __forceinline__ void s3c_sort_pass(const uint32_t* __restrict__ c_key, const uint16_t* in,
-                                              uint16_t* out, int L, int sh, uint32_t (*wc)[64], uint32_t* ws) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (int c = threadIdx.x; c < S3C_W * 64; c += S3C_TPB) (&wc[0][0])[c] = 0u;
-    __syncthreads();
-    uint32_t rk[S3C_NR], dg[S3C_NR], ix[S3C_NR];
-#pragma unroll
-    for (int r = 0; r < S3C_NR; r++) {
-        const int pos = (w * S3C_NR + r) * 64 + lane;  // wave w owns positions [w * 256, w * 256 + 256)
-        const bool valid = pos < L;
-        ix[r] = valid ? (in ? (uint32_t)in[pos] : (uint32_t)pos) : 0u;
-        const uint32_t d = valid ? (c_key[ix[r]] >> sh) & 63u : 0u;
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int bb = 0; bb < 6; bb++) {
-            const bool bit = (d >> bb) & 1u;
-            const uint64_t m = __ballot(valid && bit);
-            peers &= bit ? m : ~m;
-        }
-        const uint32_t r_ = (uint32_t)__popcll(peers & lt);
-        const uint32_t base = valid ? wc[w][d] : 0u;
-        if (valid && r_ == 0) wc[w][d] = base + (uint32_t)__popcll(peers);
-        rk[r] = valid ? base + r_ : ~0u;
-        dg[r] = d;
-    }
-    __syncthreads();
-    // (digit, wave) exclusive offsets: thread t = digit * 8 + wave
-    {
-        const int d = threadIdx.x >> 3, q = threadIdx.x & 7;
-        uint32_t tot;
-        const uint32_t ex = shw_block_excl<S3C_TPB>(wc[q][d], ws, &tot);
-        __syncthreads();
-        wc[q][d] = ex;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < S3C_NR; r++)
-        if (rk[r] != ~0u) out[wc[w][dg[r]] + rk[r]] = (uint16_t)ix[r];
-    __syncthreads();
-}
-
-__global__ void __launch_bounds__(S3C_TPB, 2) k_s3b2(shb_plan P, shb_s3 S) {
-    __shared__ uint32_t st_e1[S3C_NK], st_last[S3C_NK];
-    __shared__ uint8_t st_f[S3C_NK];  // bit 0: an e1, bit 1: a last e2
-    __shared__ uint32_t c_key[S3C_CH], c_val[S3C_CH], c_gi[S3C_CH];
-    __shared__ uint16_t o_a[S3C_CH], o_b[S3C_CH];
-    __shared__ uint32_t m_v0[S3C_CH], m_v1[S3C_CH];
-    __shared__ uint8_t m_hit[S3C_CH];
-    __shared__ uint32_t wc[S3C_W][64];
-    __shared__ uint32_t ws[S3C_W];
-    __shared__ uint32_t seg_p[SHB_CT_MAX + 1], seg_g[SHB_CT_MAX], t_sum[SHB_CT_MAX];
-    // the two workgroups of bucket b are blocks b and b + 256: the same XCD (round-robin
-    // dealing), so the bucket's segments are fetched into one L2
-    const int b = (int)(blockIdx.x & (SHB_NB - 1)), par = (int)(blockIdx.x >> 8);
-    const int kb = P.kb;
-    const uint32_t kmask = (1u << kb) - 1u;
-    const int t = S.type;
-    for (int k = threadIdx.x; k < S3C_NK; k += S3C_TPB) st_f[k] = 0;
-    const uint32_t* __restrict__ gcol = (const uint32_t*)P.st_dst[0];
-    unsigned long long t_prev = wall_clock64();
-#define S3C_PROF(ph)                                                                 \
-    if (P.prof && threadIdx.x == 0) {                                                \
-        const unsigned long long t_now = wall_clock64();                             \
-        atomicAdd(&P.prof[ph], t_now - t_prev);                                      \
-        t_prev = t_now;                                                              \
-    }
-    for (int a = 0; a < P.nt;) {
-        __syncthreads();
-        // the bucket's segments of tiles [a, a + SHB_CT_MAX), their prefix
-        const int nseg = P.nt - a < SHB_CT_MAX ? P.nt - a : SHB_CT_MAX;
-        uint32_t len = 0u, g = 0u;
-        if ((int)threadIdx.x < nseg) {
-            const int T = a + (int)threadIdx.x;
-            const uint32_t lo = P.tofft[(int64_t)b * P.tstride + T], hi = P.tofft[(int64_t)(b + 1) * P.tstride + T];
-            len = hi - lo;
-            g = ((uint32_t)T << SHB_TILE_SHIFT) + lo;
-        }
-        {
-            uint32_t tot;
-            const uint32_t pre = shw_block_excl<S3C_TPB>(len, ws, &tot);
-            if ((int)threadIdx.x < nseg) {
-                seg_p[threadIdx.x] = pre;
-                seg_g[threadIdx.x] = g;
-                t_sum[threadIdx.x] = 0u;
-            }
-            if ((int)threadIdx.x == nseg) seg_p[nseg] = tot;
-        }
-        __syncthreads();
-        // this chunk: tiles [a, a + ne), at most S3C_RAW events before the parity split
-        const int ne = __syncthreads_count((int)threadIdx.x < nseg && seg_p[threadIdx.x + 1] <= S3C_RAW);
-        if (ne == 0) {
-            if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_SPAN);
-            return;  // (uniform) the host reruns on k_s3b
-        }
-        const int Lraw = (int)seg_p[ne];
-        // this parity's events, compacted in arrival order (inside the bucket)
-        uint32_t L = 0u;
-        for (int i0 = 0; i0 < Lraw; i0 += S3C_TPB) {
-            const int i = i0 + (int)threadIdx.x;
-            uint32_t key = 0u, gi = 0u;
-            bool keep = false;
-            if (i < Lraw) {
-                int lo = 0, hi = ne - 1;  // the segment holding position i
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (seg_p[mid] <= (uint32_t)i) lo = mid;
-                    else hi = mid - 1;
-                }
-                gi = seg_g[lo] + ((uint32_t)i - seg_p[lo]);
-                key = P.w0[gi] & kmask;
-                keep = (int)(key & 1u) == par;
-            }
-            uint32_t tot;
-            const uint32_t pos = L + shw_block_excl<S3C_TPB>(keep ? 1u : 0u, ws, &tot);
-            if (keep && pos < S3C_CH) {
-                c_key[pos] = key >> 1;
-                c_val[pos] = gcol[gi];
-                c_gi[pos] = gi;
-            }
-            L += tot;
-        }
-        if (L > S3C_CH) {
-            if (threadIdx.x == 0) atomicOr(P.flag, SHB_F_SPAN);
-            return;  // (uniform: L is the block total) the host reruns on k_s3b
-        }
-        __syncthreads();
-        S3C_PROF(0)
-        // stable sort by the parity's local key (kb - 1 bits)
-        const uint16_t* srt;
-        if (kb - 1 <= 6) {
-            s3c_sort_pass(c_key, nullptr, o_a, (int)L, 0, wc, ws);
-            srt = o_a;
-        } else {
-            s3c_sort_pass(c_key, nullptr, o_a, (int)L, 0, wc, ws);
-            s3c_sort_pass(c_key, o_a, o_b, (int)L, 6, wc, ws);
-            srt = o_b;
-        }
-        S3C_PROF(1)
-        // the first event of each key run steps through the run (k_s3b's step)
-        for (int q = threadIdx.x; q < (int)L; q += S3C_TPB) {
-            const uint32_t ci = srt[q];
-            const uint32_t key = c_key[ci];
-            if (q > 0 && c_key[srt[q - 1]] == key) continue;
-            uint32_t f = st_f[key], e1b = st_e1[key], lastb = st_last[key];
-            for (int r = q; r < (int)L; r++) {
-                const uint32_t cr = r == q ? ci : srt[r];
-                if (r > q && c_key[cr] != key) break;
-                const uint32_t xb = c_val[cr];
-                const NfVal x = s3b_val(xb, t);
-                const bool hit = (f & 2u) && nf_cmp(S.op3, S.dom3, x, s3b_val(lastb, t));
-                m_hit[cr] = hit ? 1 : 0;
-                m_v0[cr] = e1b;
-                m_v1[cr] = lastb;
-                if (!hit && (f & 1u) && nf_cmp(S.op2, S.dom2, x, s3b_val(e1b, t))) {
-                    f |= 2u;
-                    lastb = xb;
-                } else {
-                    f = 1u;
-                    e1b = xb;
-                }
-            }
-            st_f[key] = (uint8_t)f;
-            st_e1[key] = e1b;
-            st_last[key] = lastb;
-        }
-        __syncthreads();
-        S3C_PROF(2)
-        // counts at the slots, the match values at the matching event's slot, the
-        // chunk's matches per tile
-        for (int i = threadIdx.x; i < (int)L; i += S3C_TPB) {
-            const uint32_t gi = c_gi[i];
-            const uint32_t hit = m_hit[i];
-            P.cnt[gi] = (uint8_t)hit;
-            if (hit) {
-                for (int m = 0; m < S.n_ms; m++) ((uint32_t*)P.ms[m])[gi] = S.ms_slot[m] == 0 ? m_v0[i] : m_v1[i];
-                atomicAdd(&t_sum[(int)(gi >> SHB_TILE_SHIFT) - a], 1u);
-            }
-        }
-        __syncthreads();
-        for (int sg = threadIdx.x; sg < ne; sg += S3C_TPB)
-            if (t_sum[sg]) atomicAdd(&P.ttot[a + sg], t_sum[sg]);
-        S3C_PROF(3)
-        a += ne;
-    }
-#undef S3C_PROF
-}
-
 // ---------------------------------------------------------------- aggregate carry
 // Select-clause aggregators of the bucketed window engine (C2 select variant ii):
 // one running value per partition key and output, added in the reference's order
@@ -1384,7 +1136,6 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
     __shared__ uint16_t c_pre[AGC_CH];   // the consumer's first row in the chunk (arrival order)
     __shared__ uint32_t c_mp[AGC_CH];    // ... its match-stream position
     __shared__ uint32_t c_gi[AGC_CH];    // ... its slot
-    __shared__ uint32_t c_wp[AGC_CH];    // ... its first row's output index (by_row) or position
     __shared__ uint16_t o_a[AGC_CH];
     __shared__ uint16_t rs[AGC_CH + 1];  // sorted consumer -> its first row in key order
     __shared__ uint16_t run_q[257];      // key run -> its first sorted consumer
@@ -1494,7 +1245,6 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
             const int i = (int)threadIdx.x * AGC_NR + k;
             if (i >= L) continue;
             c_mp[i] = ms0[k] + c_pre[i] - c_pre[seg_p[sgi[k]]];
-            if (A.by_row) c_wp[i] = A.roff[c_gi[i]];
         }
         __syncthreads();
         AGP_PROF(0)
@@ -1570,7 +1320,7 @@ __global__ void __launch_bounds__(AGC_TPB) k_bk_aggp(shb_plan P, shb_aggc A) {
                         const uint32_t cr = srt[q];
                         const uint32_t m = (uint32_t)(r - rs[q]);
                         mp = c_mp[cr] + m;
-                        wp = A.by_row ? c_wp[cr] + m : mp;
+                        wp = mp;
                         gi = c_gi[cr];
                         if (e1src) x1 = (int64_t)e1src[mp];
                         if (e2src) x2 = agc_load(e2src, gi, A.e2_type[0]);
@@ -1648,14 +1398,9 @@ __global__ void __launch_bounds__(256) k_bk_toff_t(const uint16_t* __restrict__ 
 
 extern "C" int shb_partition(const int32_t* keys, const int64_t* ts, int32_t nkeys, shb_plan* P, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    // SH_BK_SCAT: 8 (default) 1,024 threads, 8 events per lane: 61 VGPRs, 8 waves
-    // per SIMD (0.64 vs 0.79 ms on C2 in one call, profiles/r4_c2_scatter_ab.txt);
-    // 4: 512 threads, 16 events per lane, 94 VGPRs, 4 waves per SIMD
-    static const int scat = getenv("SH_BK_SCAT") ? atoi(getenv("SH_BK_SCAT")) : 8;
-    if (scat == 8)
-        hipLaunchKernelGGL((k_bk_scatter<2, 1024>), dim3(bk_grid(P->nt)), dim3(1024), 0, st, keys, ts, nkeys, *P);
-    else
-        hipLaunchKernelGGL((k_bk_scatter<4, BK_TPB>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, st, keys, ts, nkeys, *P);
+    // 1,024 threads, 8 events per lane: 61 VGPRs, 8 waves per SIMD (0.64 vs 0.79 ms on C2
+    // for 512 threads x 16 events at 94 VGPRs, profiles/r4_c2_scatter_ab.txt)
+    hipLaunchKernelGGL((k_bk_scatter<2, 1024>), dim3(bk_grid(P->nt)), dim3(1024), 0, st, keys, ts, nkeys, *P);
     if (bk_ok()) return -3;
     if (P->tstride < P->nt) return -1;
     hipLaunchKernelGGL(k_bk_toff_t, dim3((P->nt + TT_T - 1) / TT_T), dim3(256), 0, st, (const uint16_t*)P->toff, P->nt,
@@ -1676,50 +1421,13 @@ extern "C" int shb_finish(shb_plan* P, uint32_t* scan_tmp, void* stream) {
 
 extern "C" int shb_s3_carry(const shb_plan* P, const shb_s3* S, void* stream) {
     if (P->kb > 12 || P->n_staged < 1 || P->st_width[0] != 4) return -1;
-    if (S->sub) {
-        if (P->kb < 1) return -1;
-        hipLaunchKernelGGL(k_s3b2, dim3(2 * SHB_NB), dim3(S3C_TPB), 0, (hipStream_t)stream, *P, *S);
-    } else {
-        hipLaunchKernelGGL(k_s3b, dim3(SHB_NB), dim3(S3B_TPB), 0, (hipStream_t)stream, *P, *S);
-    }
+    hipLaunchKernelGGL(k_s3b, dim3(SHB_NB), dim3(S3B_TPB), 0, (hipStream_t)stream, *P, *S);
     return bk_ok();
-}
-
-// each event's first output row, by slot: the tile's first row (ttot after shb_finish)
-// + the exclusive prefix of the counts in arrival order (the emitter's own row order), so
-// that the aggregate carry writes its running values where the emitter reads them row
-// by row (contiguous) instead of by match-stream position (one line per row)
-__global__ void __launch_bounds__(1024) k_bk_rowoff(shb_plan P, uint32_t* __restrict__ roff) {
-    __shared__ uint32_t ws[16];
-    const int T = blockIdx.x;
-    const int64_t b0 = (int64_t)T << SHB_TILE_SHIFT;
-    const int tile_n = (int)((P.n - b0) < SHB_TILE ? (P.n - b0) : SHB_TILE);
-    constexpr int PER = SHB_TILE / 1024;
-    uint32_t sl[PER], c[PER], sum = 0;
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const int l = (int)threadIdx.x * PER + k;  // consecutive arrivals per thread
-        sl[k] = l < tile_n ? (uint32_t)P.sp[b0 + l] : 0u;
-        c[k] = l < tile_n ? (uint32_t)P.cnt[b0 + sl[k]] : 0u;
-        sum += c[k];
-    }
-    uint32_t tot;
-    uint32_t off = P.ttot[T] + shw_block_excl<1024>(sum, ws, &tot);
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const int l = (int)threadIdx.x * PER + k;
-        if (l < tile_n) roff[b0 + sl[k]] = off;
-        off += c[k];
-    }
 }
 
 extern "C" int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream) {
     static_assert(AGC_TPB == S3B_TPB && AGC_CH == S3B_CH, "the sort pass shape");
     if (P->kb > 8 || A->n < 1 || A->n > SHB_MAX_AGG) return -1;
-    if (A->by_row) {
-        if (!A->parallel || !A->roff) return -1;
-        hipLaunchKernelGGL(k_bk_rowoff, dim3(P->nt), dim3(1024), 0, (hipStream_t)stream, *P, A->roff);
-    }
     if (A->parallel)
         hipLaunchKernelGGL(k_bk_aggp, dim3(SHB_NB), dim3(AGC_TPB), 0, (hipStream_t)stream, *P, *A);
     else
@@ -1737,34 +1445,9 @@ static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& 
                                             : (MODE == SHB_OUT_RAW ? (NO <= 6 ? 4 : 3)
                                                                    : (MODE == SHB_OUT_PACKED ? (NO <= 6 ? 4 : (NO == 7 ? 2 : 1))
                                                                                              : (NO <= 5 ? 2 : 1)));
-    // (SH_EMIT_LDS_PAD=<bytes>: dynamic LDS that lowers the workgroups per CU -- an L2
-    // footprint experiment)
-    static const int pad = getenv("SH_EMIT_LDS_PAD") ? atoi(getenv("SH_EMIT_LDS_PAD")) : 0;
-    // SH_EMIT_OCC=6: up to 4 values at 6 waves per SIMD (<= 80 VGPRs, 2 rows per lane: three
-    // workgroups per CU on the 42 KB of LDS) -- C2 emit 1.40 vs 1.46 ms
-    // (profiles/r5_c2_emit_occ_ab.txt), but 22 VGPRs spill to scratch and the step moves
-    // 8.89 GB past L2 instead of 8.00 (profiles/r5_c2_emit_occ6_traffic.json): off by default
-    static const int occ = getenv("SH_EMIT_OCC") ? atoi(getenv("SH_EMIT_OCC")) : 4;
-    if constexpr (NO >= 1 && NO <= 4) {
-        if (occ == 6) {
-            hipLaunchKernelGGL((k_bk_emit<MODE, NO, 2, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad,
-                               (hipStream_t)stream, *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
-            return;
-        }
-        if (occ == 5) {
-            hipLaunchKernelGGL((k_bk_emit<MODE, NO, 3, 5>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad,
-                               (hipStream_t)stream, *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
-            return;
-        }
-    }
-    if constexpr (NO >= 5 && NO <= 6) {
-        if (occ == 66) {  // (experiment: 5-6 values at 6 waves, 1 row per lane: slower)
-            hipLaunchKernelGGL((k_bk_emit<MODE, NO, 1, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad,
-                               (hipStream_t)stream, *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
-            return;
-        }
-    }
-    hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), pad, (hipStream_t)stream, *P,
+    // (6 waves per SIMD at 2 rows per lane: 1.40 vs 1.46 ms on C2 but 22 VGPRs spilled
+    // and 0.9 GB more traffic per step, profiles/r5_c2_emit_occ_ab.txt: not kept)
+    hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P,
                        *O, OC, seq_base, out_seq, out_vals, out_cap);
 }
 

@@ -142,15 +142,11 @@ struct shb_plan {
 // (kind 0) or from the consumer event's attribute idx[o] (kind 1)
 struct shb_out {
     int32_t n_out;
-    int32_t warm;                 // 1: the emitter warms L2 with its row sources first
-    int32_t ms_slot;              // 1: an event's (single) match-stream value sits at its own slot
-    int32_t pad;
+    int32_t pad[3];
     int32_t kind[SHB_MAX_OUT];
     int32_t type[SHB_MAX_OUT];    // sh_type: raw-value conversion
-    const void* src[SHB_MAX_OUT]; // kind 0: match-stream column, kind 1: consumer column,
-                                  // kind 2 (SHB_OUT_KIND_ROW): a column by output row
+    const void* src[SHB_MAX_OUT]; // kind 0: match-stream column, kind 1: consumer column
 };
-#define SHB_OUT_KIND_ROW 2
 
 // the rise-and-fall sequence (nf_query.s3) for the bucket-carry engine: every
 // operand of f2 / f3 and every e1 / e2[last] select value is one 4-byte attribute
@@ -162,7 +158,6 @@ struct shb_s3 {
     int32_t n_ms;
     int32_t ms_slot[2];
     int32_t warm;                 // 1: each chunk warms L2 with the next chunk's segments
-    int32_t sub;                  // 1: two workgroups per bucket (k_s3b2), match values at slots
 };
 
 // select-clause aggregators carried per key by the bucketed engine (k_bk_aggc):
@@ -179,9 +174,6 @@ struct shb_aggc {
     int32_t side[SHB_MAX_AGG];    // 0: e1, 1: e2 column 0, 2: e2 column 1, 3: none
     void* out[SHB_MAX_AGG];       // [match-stream positions] int64 / double bits
     int32_t parallel;             // 1: k_bk_aggp (segmented prefix, exact fixed point), 0: k_bk_aggc
-    int32_t by_row;               // k_bk_aggp: out[] by output row (roff, after shb_finish), else by
-                                  // match-stream position
-    uint32_t* roff;               // [slot] the event's first output row (k_bk_rowoff), by_row only
 };
 
 // typed output columns (sh_device_run.d_out_cols) instead of raw 8-byte rows

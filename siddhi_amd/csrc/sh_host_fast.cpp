@@ -446,12 +446,6 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     shb_out O;
     memset(&O, 0, sizeof(O));
     O.n_out = P.n_out;
-    // the emitter's L2 warming of its row sources: off unless SH_BK_WARM=1. It saves
-    // 0.12 ms of C2's 4.3 (profiles/r5_c2_warm_ab_*.json) but adds 1.77 GB of L2-miss
-    // fetch per step (profiles/pmc_c2.json, round 4) that no counter here can show to
-    // be Infinity-Cache hits rather than HBM traffic
-    static const bool warm_on = getenv("SH_BK_WARM") && getenv("SH_BK_WARM")[0] == '1';
-    O.warm = warm_on ? 1 : 0;
     int ms[SHB_MAX_MS], n_ms = 0;
     const int part_attr = h->part_attr0;
     for (int o = 0; o < P.n_out; o++) {
@@ -537,13 +531,11 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     // against the post-pass's 8.7) when the post-pass refuses too, or SH_BK_AGGC=1
     const bool aggc_env = getenv("SH_BK_AGGC") != nullptr;
     const bool aggp_off = getenv("SH_BK_AGGP") && getenv("SH_BK_AGGP")[0] == '0';
-    const bool par = !force_carry && !aggc_env && !aggp_off && !h->aggp_skip && run->n < ((int64_t)1 << 31);
+    const bool par = !force_carry && !aggc_env && !aggp_off && !h->aggp_refused && run->n < ((int64_t)1 << 31);
     bool carry = P.agg_post && !getenv("SH_BK_AGG_POST") && (force_carry || aggc_env || par);
     AG.parallel = par ? 1 : 0;
-    // the running values by match-stream position; SH_AGGP_ROW=1: by output row
-    // (k_bk_rowoff's map, read contiguously by the emitter: emit 2.39 -> 2.04 ms, but the
-    // map 0.48 ms and the carry's scattered row writes 2.52 -> 3.07 ms, 8.39 vs 7.65 ms/step)
-    AG.by_row = par && getenv("SH_AGGP_ROW") && getenv("SH_AGGP_ROW")[0] == '1' ? 1 : 0;
+    // (the running values go by match-stream position; by output row, through a per-slot
+    // row map, measured 8.39 vs 7.65 ms/step in round 5: removed)
     int agg_of[SHB_MAX_OUT];
     for (int o = 0; o < P.n_out; o++) agg_of[o] = -1;
     for (int o = 0; o < P.n_out && carry; o++) {
@@ -611,13 +603,9 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
             if (h->bk_agg[i].ensure_fresh(ms_vals * 8)) return fail(h, SH_E_OOM, "aggregate columns");
             AG.out[i] = h->bk_agg[i].p;
         }
-        if (AG.by_row) {
-            if (h->bk_roff.ensure_fresh(std::max<int64_t>(1, run->n) * 4)) return fail(h, SH_E_OOM, "aggregate rows");
-            AG.roff = h->bk_roff.as<uint32_t>();
-        }
         for (int o = 0; o < O.n_out; o++)
             if (agg_of[o] >= 0) {
-                O.kind[o] = AG.by_row ? SHB_OUT_KIND_ROW : 0;
+                O.kind[o] = 0;
                 O.src[o] = AG.out[agg_of[o]];
                 O.type[o] = P.out_type[o];
             }
@@ -667,10 +655,8 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     if (hipModuleLaunchKernel((hipFunction_t)h->bk.match, (unsigned)(SHB_NB * B.n_chunks), 1, 1, 512, 1, 1, 0, st, args,
                               nullptr) != hipSuccess)
         return fail(h, SH_E_HIP, "shb_match launch failed");
-    // (by output row: after the tiles' first rows are known)
-    if (carry && !AG.by_row && shb_agg_carry(&B, &AG, st)) return fail(h, SH_E_HIP, "aggregate carry launch failed");
+    if (carry && shb_agg_carry(&B, &AG, st)) return fail(h, SH_E_HIP, "aggregate carry launch failed");
     if (shb_finish(&B, h->w_scan.as<uint32_t>(), st)) return fail(h, SH_E_HIP, "bucket scan launch failed");
-    if (carry && AG.by_row && shb_agg_carry(&B, &AG, st)) return fail(h, SH_E_HIP, "aggregate carry launch failed");
     hipEventRecord(h->ev[2], st);
     if (shb_emit(&B, &O, &OC, 0, run->d_out_seq, run->d_out_values, run->out_capacity, st))
         return fail(h, SH_E_HIP, "bucket emit launch failed");
@@ -699,11 +685,12 @@ int run_bucket(sh_handle* h, sh_device_run* run, int32_t nkeys, bool force_carry
     if (flag == SHB_F_AGG && carry && AG.parallel) {
         // a value the fixed point cannot hold exactly (or a chunk too dense): the
         // batch again without the carry, the post-pass (or k_bk_aggc) adding instead
+        // The refusal sticks to the handle: data that fails the fixed-point test once
+        // (a price such as 12.34) fails it in every batch, and each refused attempt costs
+        // a whole bucketed pipeline
+        h->aggp_refused = true;
         if (h->aggp_only) return 1;  // (the caller's raw rows first)
-        h->aggp_skip = true;
-        const int rc = run_bucket(h, run, nkeys, force_carry);
-        h->aggp_skip = false;
-        return rc;
+        return run_bucket(h, run, nkeys, force_carry);
     }
     if (flag) return 1;
     run->out_count = total;
@@ -741,21 +728,10 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     shb_out O;
     memset(&O, 0, sizeof(O));
     O.n_out = Q.n_out;
-    static const bool warm_on = getenv("SH_BK_WARM") && getenv("SH_BK_WARM")[0] == '1';
-    O.warm = warm_on ? 1 : 0;  // the emitter's L2 warming (as the window engine's: off by default)
     shb_s3 S;
     memset(&S, 0, sizeof(S));
     S.type = ty;
-    S.warm = getenv("SH_S3B_WARM") && getenv("SH_S3B_WARM")[0] == '0' ? 0 : 1;
-    // two workgroups per bucket (k_s3b2) when SH_S3B_SUB=1 (read per call: A/B): exact,
-    // but on C3 its parity split costs more than the second workgroup per CU gains
-    // (5.28 vs 4.91 ms, profiles/r5_c3_s3b_sub_ab.txt); off after a chunk's parity
-    // split overflowed once (h->s3b_sub_off)
-    {
-        const char* e = getenv("SH_S3B_SUB");
-        S.sub = (e && e[0] == '1') && !h->s3b_sub_off && kb >= 1 ? 1 : 0;
-    }
-    O.ms_slot = S.sub;
+    S.warm = 1;  // (the next chunk's gather overlaps the walk: 3.42 vs 3.52 ms, profiles/r4_c3_s3b_warm_ab.txt)
     S.op2 = Q.s3_op2;
     S.dom2 = Q.s3_dom2;
     S.op3 = Q.s3_op3;
@@ -855,10 +831,6 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
                 pr[0], pr[1], pr[2], pr[3]);
     }
     if (flag & SHB_F_KEY) return fail(h, SH_E_INVALID_ARG, "partition key id >= n_keys");
-    if (flag == SHB_F_SPAN && S.sub) {
-        h->s3b_sub_off = true;  // a parity's chunk overflowed (skewed keys): one workgroup per bucket
-        return run_s3b(h, run, nkeys);
-    }
     if (flag) return 1;
     run->out_count = total;
     if (total > run->out_capacity) return fail(h, SH_E_MORE, "output capacity too small");
@@ -868,7 +840,7 @@ int run_s3b(sh_handle* h, sh_device_run* run, int32_t nkeys) {
     hipEventElapsedTime(&h->times.emit_ms, h->ev[2], h->ev[3]);
     hipEventElapsedTime(&h->times.total_ms, h->ev[0], h->ev[3]);
     h->times.advance_launches = 1;
-    h->s3b_last = S.sub ? 2 : 1;
+    h->s3b_last = 1;
     return hipStreamSynchronize(st) == hipSuccess ? SH_OK : fail(h, SH_E_HIP, "sequence engine");
 }
 

@@ -328,16 +328,14 @@ struct sh_handle {
     int bk_state = 0;
     int32_t part_attr0 = -1;  // stream-0 attribute keying query 0's partition
     int bk_last = 0;          // 1: the last sh_run_device ran on the bucketed engine
-    int s3b_last = 0;         // 1: ... on the sequence bucket-carry engine (k_s3b), 2: its sub-bucket form (k_s3b2)
-    bool s3b_sub_off = false; // a chunk's parity split overflowed once: k_s3b from then on
+    int s3b_last = 0;         // 1: ... on the sequence bucket-carry engine (k_s3b)
     shj_bucket bk{};
     std::string bk_err;
     DevBuf bk_w0, bk_sp, bk_toff, bk_tofft, bk_cnt, bk_mstart, bk_tpre, bk_tfirst, bk_hstart, bk_ttot, bk_flag, bk_prof;
     DevBuf bk_st[SHB_MAX_STAGED], bk_ms[SHB_MAX_MS], bk_agg[SHB_MAX_AGG];
     bool bk_agg_carried = false;  // the last bucketed run carried its aggregates (k_bk_aggc)
     PinBuf bk_rd;
-    DevBuf bk_roff;          // [slot] first output row of each event (k_bk_rowoff)
-    bool aggp_skip = false;  // run_bucket: this batch without k_bk_aggp (it refused a value)
+    bool aggp_refused = false;  // run_bucket: k_bk_aggp refused a value once: the post-pass from then on
     bool aggp_only = false;  // run_bucket: k_bk_aggp or nothing (1), the caller's layout kept
     // typed output columns (sh_device_run.d_out_cols) for engines that write rows
     DevBuf w_colrows;

@@ -1056,31 +1056,12 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
                        hipMemcpyDeviceToHost, st);
         return SH_OK;
     };
-    // one sync for a pending event launch and the first due pass (SH_SPEC_DUE=1): with
-    // one scheduler, no coordinator and the stamps on the host, the due pass is queued
-    // behind the launch and comes back with it. A launch that had to be replayed
-    // (capacity growth) voids it: that scheduler's due pass then runs again over every
-    // key (the list it folded stays a superset of the armed keys). Off by default: on
-    // C4 it saves one sync per call (2.0 instead of 3.0) but the candidates' stamps
-    // then wait longer for the scheduler-map replay thread, and the call is slower
-    // (1,486-1,511 vs 1,377-1,379 ms per 3,000 calls, profiles/r5_c4_spec_due_ab.txt)
-    int spec = 0;  // 1: queued, 2: its results stand, 3: voided
-    {
-        static const bool spec_on = getenv("SH_SPEC_DUE") && getenv("SH_SPEC_DUE")[0] == '1';
-        if (spec_on && h->pend.on && !wall && !h->coord_on && h->sm_on && h->T->has_absent &&
-            h->T->n_queries == 1 && h->T->q[0].n_sched == 1 && h->n_nkeys > 0) {
-            if (pin_rd_ready(h)) return fail(h, SH_E_OOM, "pinned staging");
-            const bool list_pass = armed_flags(h) && h->n_arm_log.p;
-            const int rc = due_launch(0, h->T->q[0].sched_seq[0], list_pass, true);
-            if (rc) return rc;
-            if (list_pass) first_pass = false;
-            spec = 1;
-        }
-    }
+    // (queueing the first due pass behind a pending event launch saved a sync per call
+    // but made the candidates' stamps wait longer for the scheduler-map replay: 1,486-1,511
+    // vs 1,377-1,379 ms per 3,000 C4 calls, profiles/r5_c4_spec_due_ab.txt; removed)
     {
         int src = nf_settle(h);
         if (src) return src;
-        if (spec == 1) spec = h->times.advance_launches == 1 ? 2 : 3;
     }
     if (!h->T->has_absent) return SH_OK;
     if (h->n_nkeys == 0 && !h->coord_on) return SH_OK;
@@ -1103,10 +1084,9 @@ int nf_timers(sh_handle* h, int64_t now, bool wall) {
             unsigned long long nc = 0;
             if (nkeys > 0) {
                 // due keys: the armed-key list (+ the keys armed since the last pass on
-                // the first scheduler's pass, which also rebuilds the list), or every key
-                // (a voided speculative pass: the list was folded on the replayed state)
-                if (!(spec == 2 && q == 0 && si == 0)) {
-                    const bool list_pass = armed_flags(h) && h->n_arm_log.p && !(spec == 3 && q == 0 && si == 0);
+                // the first scheduler's pass, which also rebuilds the list)
+                {
+                    const bool list_pass = armed_flags(h) && h->n_arm_log.p;
                     const int rc = due_launch(q, p, list_pass, list_pass && first_pass);
                     if (rc) return rc;
                     if (list_pass) first_pass = false;

@@ -79,11 +79,6 @@ const int kSpan = [] {
     const int v = env_int("SH_BK_SPAN", 2560, 1024, SHB_SPAN);
     return v % 512 ? 2560 : v;
 }();
-// L2 warming of each pass's span (SH_BK_MWARM=0: off): the first line(s) of every
-// consumer / near-halo tile's segment are read as soon as the bucket starts arrive,
-// so the span loads after the segment table's barriers hit L2
-// (off by default: 2.21 vs 2.08 ms on C2 in one call, profiles/r4_c2_emit_warm_ab.txt)
-const int kSpanWarm = env_int("SH_BK_MWARM", 0, 0, 1);
 const int kChunk = [] {
     const int v = env_int("SH_BK_CH", 2048, 512, SHB_CH);
     return (v % 512 || v > kSpan) ? (kSpan < 2048 ? kSpan : 2048) : v;
@@ -1037,7 +1032,6 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
            "#define SHB_MINB " + std::to_string(kMatchMinBlocks) + "\n"
            "#define SHB_NSEG (SHB_CT_MAX + SHB_HMAX)\n"
            "#define SHB_SPANJ " + std::to_string(kSpan) + "\n#define SHB_CHJ " + std::to_string(kChunk) + "\n" +
-           "#define SHB_WARMJ " + std::to_string(kSpanWarm) + "\n"
            "#define SHB_NR (SHB_SPANJ / SHB_TPB)\nstatic_assert(SHB_SPANJ % SHB_TPB == 0 && SHB_NR * SHB_TPB == SHB_SPANJ && SHB_SPANJ <= SHB_SPAN && SHB_CHJ <= SHB_CH && SHB_CHJ % SHB_TPB == 0, \"span\");\n"
            "static_assert(SHB_NSEG < 256 && SHB_NSEG < SHB_TPB, \"segments\");\n";
     src += R"(
@@ -1077,7 +1071,6 @@ const int E = A + P.ct < P.nt ? A + P.ct : P.nt;
 const int kb = P.kb;
 const uint32_t kmask = (1u << kb) - 1u;
 const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
-uint32_t warm_ = 0u;  // (SHB_WARMJ: the warming reads, consumed by an empty asm at the end)
 for (int a = A; a < E;) {
 __syncthreads();
 unsigned long long t_prev = wall_clock64();
@@ -1091,17 +1084,9 @@ if (Tm >= 0 && Tm < E) {
     const uint32_t lo = P.tofft[(int64_t)b * P.tstride + Tm], hi = P.tofft[(int64_t)(b + 1) * P.tstride + Tm];
     len = hi - lo;
     g = ((uint32_t)Tm << SHB_TILE_SHIFT) + lo;
-#if SHB_WARMJ
-    if (Tm >= a - 16 && len) {
-        warm_ ^= P.w0[g];
-        if (len > 32u) warm_ ^= P.w0[g + 32u];
+
 )";
-    for (int a : staged_out)
-        src += "        warm_ ^= (uint32_t)g_a" + std::to_string(a) + "[g];\n        if (len > 32u) warm_ ^= (uint32_t)g_a" +
-               std::to_string(a) + "[g + 32u];\n";  // (integer column types: each element in bounds)
-    src += R"(    }
-#endif
-}
+    src += R"(}
 __syncthreads();
 const int h0 = s_i[0];  // first tile of the segment table
 const int nseg = E - h0;
@@ -1344,7 +1329,7 @@ uint32_t k = 0;
            ms_put + "    }\n} else {\n" + walk(false, put) + "}\n";
     src += "}\n";
     if (stage1) src += "}\n";
-    src += "SHB_PROF(4)\na += ne;\n}\n#if SHB_WARMJ\nasm volatile(\"\" ::\"v\"(warm_));\n#endif\n}\n";
+    src += "SHB_PROF(4)\na += ne;\n}\n}\n";
 
     return true;
 }

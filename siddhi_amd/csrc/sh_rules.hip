@@ -952,8 +952,8 @@ __global__ void k_sparse_place(const uint32_t* __restrict__ pr_p, const uint32_t
     }
 }
 
-template <bool IMG, int TPB = SPA_TPB, int OCC = 1>
-__global__ void __launch_bounds__(TPB, OCC) k_sparse_take(const shr_table* __restrict__ RT,
+template <bool IMG>
+__global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __restrict__ RT,
                                                          const int64_t* __restrict__ ts,
                                                          const int32_t* __restrict__ akeys, int64_t n,
                                                          const shd_cols* __restrict__ C,
@@ -962,22 +962,14 @@ __global__ void __launch_bounds__(TPB, OCC) k_sparse_take(const shr_table* __res
                                                          const uint32_t* __restrict__ l_p,
                                                          const uint32_t* __restrict__ l_r,
                                                          const int64_t* __restrict__ l_te, uint32_t* __restrict__ l_q,
-                                                         int xcd, float slice_scale, shr_live LV, int pa0,
-                                                         int pa1) {
+                                                         shr_live LV, int pa0, int pa1) {
     extern __shared__ uint4 s_img[];
     __shared__ const void* s_col[32];
     spa_stage<IMG>(img, I, C, s_img, s_col);
     __syncthreads();
     const SpaRules S{(const uint8_t*)s_img, img, s_col};
-    // XCD-sliced keys (xcd = 1, a grid of a multiple of 8): workgroups are dealt
-    // round-robin to the 8 XCDs, so workgroup w takes only the events whose key lies
-    // in the w % 8-th contiguous eighth of the key space. Each XCD's L2 then holds
-    // one eighth of the list offsets and lists (random reads per event) at the
-    // price of reading every key eight times (sequential). Any placement is
-    // correct (every event belongs to exactly one slice); this one is for speed.
-    const int xs = xcd ? (int)(blockIdx.x & 7u) : 0;
-    const int64_t wb = xcd ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
-    const int64_t nw = xcd ? (int64_t)(gridDim.x >> 3) : (int64_t)gridDim.x;
+    constexpr int TPB = SPA_TPB;
+    const int64_t wb = (int64_t)blockIdx.x, nw = (int64_t)gridDim.x;
     // SPA_U events per thread and round: their key, list bounds and first list
     // entry are loaded together (three dependent random reads per event otherwise)
     const int64_t round = (int64_t)TPB * SPA_U;
@@ -989,10 +981,6 @@ __global__ void __launch_bounds__(TPB, OCC) k_sparse_take(const shr_table* __res
             const int64_t q = base + (int64_t)u * TPB + threadIdx.x;
             key[u] = q < n ? akeys[q] : -1;
             tq[u] = q < n ? ts[q] : 0;
-            if (xcd && key[u] >= 0) {
-                const int sl = min(7, (int)((float)key[u] * slice_scale));
-                if (sl != xs) key[u] = -1;
-            }
         }
         // the live bitmap: an event whose key has no partial that can be consumed in
         // its time slice reads nothing else (a 128 KB slice of bits per 1M keys, in L2)
@@ -1146,33 +1134,16 @@ extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const in
         const int64_t gmax = 256LL * std::max(1, std::min(per_cu, 2));
         if (tg > gmax) tg = gmax;
         if (tg < 1) tg = 1;
-        // XCD-sliced keys: opt-in (SH_SPARSE_XCD=1). On C5 (1M cards) it measured
-        // 7.17 vs 2.94 ms for take in one call (profiles/r4_c5_xcd_ab.txt): reading
-        // every key eight times costs more than the list-bound misses it saves
-        static const bool xenv = getenv("SH_SPARSE_XCD") && getenv("SH_SPARSE_XCD")[0] == '1';
-        const int xcd = xenv && tg >= 64 ? 1 : 0;
-        if (xcd) tg &= ~7LL;
-        const float scale = 8.0f / (float)std::max(1, nkeys);
-        // (SH_TAKE_512=1: 512-thread workgroups at <= 80 VGPRs, up to three per CU)
-        static const bool t512 = getenv("SH_TAKE_512") && getenv("SH_TAKE_512")[0] == '1';
-        static const int lim512 = t512 ? spa_img_attr(&k_sparse_take<true, 512, 6>) : 0;
-        if (use_img && t512 && I->lds <= lim512) {
-            int64_t tg2 = (n + 512 * SPA_U - 1) / (512 * SPA_U);
-            const int64_t gmax2 = 256LL * std::max(1, std::min(per_cu, 3));
-            if (tg2 > gmax2) tg2 = gmax2;
-            if (tg2 < 1) tg2 = 1;
-            if (xcd) tg2 &= ~7LL;
-            hipLaunchKernelGGL((k_sparse_take<true, 512, 6>), dim3((unsigned)tg2), dim3(512), (size_t)I->lds, st, dT, ts,
-                               akeys, n, dC, img, *I, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
-                               (const int64_t*)l_te, l_q, xcd, scale, LV, pa0, pa1);
-        } else if (use_img)
+        // (slicing the keys by XCD measured 7.17 vs 2.94 ms for take on C5, and 512-thread
+        // workgroups lost too, profiles/r4_c5_xcd_ab.txt, r5_c5_take512_ab.txt: removed)
+        if (use_img)
             hipLaunchKernelGGL(k_sparse_take<true>, dim3((unsigned)tg), dim3(SPA_TPB), (size_t)I->lds, st, dT, ts, akeys,
                                n, dC, img, *I, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
-                               (const int64_t*)l_te, l_q, xcd, scale, LV, pa0, pa1);
+                               (const int64_t*)l_te, l_q, LV, pa0, pa1);
         else
             hipLaunchKernelGGL(k_sparse_take<false>, dim3((unsigned)tg), dim3(SPA_TPB), 0, st, dT, ts, akeys, n, dC,
                                (const uint8_t*)nullptr, none, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
-                               (const int64_t*)l_te, l_q, xcd, scale, LV, pa0, pa1);
+                               (const int64_t*)l_te, l_q, LV, pa0, pa1);
     }
     hipLaunchKernelGGL(k_sparse_rec, dim3(gp), dim3(256), 0, st, (const uint32_t*)l_p, (const uint32_t*)l_r,
                        (const uint32_t*)l_q, ctr, rec_p, rec_q, rec_r, rctr, rcap);

@@ -71,7 +71,7 @@ def _oracle(text, ts, cols, keys):
     return out
 
 
-@pytest.mark.parametrize("carry", ["aggp", "post", "aggc", "aggp-packed", "aggc-packed", "aggprow-packed"])
+@pytest.mark.parametrize("carry", ["aggp", "post", "aggc", "aggp-packed", "aggc-packed"])
 @pytest.mark.parametrize("n,K", [(400_000, 2_000), (300_000, 20_000)])
 def test_c2_aggregates_bucketed_vs_oracle(n, K, carry, monkeypatch):
     """default: the parallel fixed-point carry (k_bk_aggp, status 5); SH_BK_AGGP=0: the
@@ -84,9 +84,6 @@ def test_c2_aggregates_bucketed_vs_oracle(n, K, carry, monkeypatch):
         monkeypatch.setenv("SH_BK_AGGC", "1")
     if carry == "post":
         monkeypatch.setenv("SH_BK_AGGP", "0")
-    if carry == "aggprow":  # the running values by output row (k_bk_rowoff), SH_AGGP_ROW=1
-        monkeypatch.setenv("SH_AGGP_ROW", "1")
-        carry = "aggp"
     ts, k, p, v = synth.stock_stream(n, K, 100)
     (m, seq, vals), st = _run(C2_AGG, ts, k, [k, p, v], K, packed=packed)
     ref = _oracle(C2_AGG, ts, [k, p, v], k)
@@ -178,3 +175,31 @@ def test_c2_aggregates_full_size_vs_restatement():
     assert np.array_equal(vals[:, 2], raw_bits(running(grp, p1, "avg")))
     assert np.array_equal(vals[:, 3], running(grp, None, "count"))
     assert np.array_equal(vals[:, 4], running(grp, ev[:, 3], "sum"))
+
+
+def test_aggp_refusal_sticks_to_the_handle():
+    """double prices that are not whole units of 2^-24 (12.34): k_bk_aggp refuses the
+    first batch, the refusal is kept, and both runs on the handle come out
+    of the post-pass (agg_status 1) exactly as the oracle adds them, in packed rows"""
+    import torch
+    from siddhi_amd import compiler, synth
+    from siddhi_amd.device_run import DeviceRunner, packed_to_raw
+    text = C2_AGG.replace("price float", "price double")
+    n, K = 200_000, 2_048
+    ts, k, p, v = synth.stock_stream(n, K, 100)
+    pd = np.round(p.astype(np.float64) + 0.003, 2)  # two decimals as doubles: 12.34 etc.
+    ref = _oracle(text, ts, [k, pd, v], k)
+    r = DeviceRunner(compiler.compile_app(text))
+    dev = torch.device("cuda:0")
+    tk = torch.from_numpy(k).to(dev)
+    cols = [tk, torch.from_numpy(pd).to(dev), torch.from_numpy(v).to(dev)]
+    offs, rb = r.packed_layout()
+    for _ in range(2):
+        m, rows = r.run(torch.from_numpy(ts).to(dev), tk, cols, K, packed=True)
+        torch.cuda.synchronize()
+        oseq, ovals = packed_to_raw(rows.cpu().numpy(), r.out_types, offs, rb)
+        assert r.bucket_status() == 1 and r.agg_status() in (1, 2), (r.bucket_status(), r.agg_status())
+        assert m == len(ref["seq"]) > 0
+        assert np.array_equal(oseq.view(np.int64), ref["seq"].astype(np.int64))
+        assert np.array_equal(ovals, ref["values"])
+    r.close()

@@ -1,6 +1,6 @@
 """C3 (BASELINE.json configs[2]) through sh_run_device on its device forms:
 the bucket-carry engine (sh_bucket.hip, seq3 status 2: k_s3b, one workgroup per key
-bucket, the default; k_s3b2, two per bucket, SH_S3B_SUB=1 -- "s3b2"), the
+bucket, the default), the
 rise-and-fall key-segment engine (k_seq3s / k_seq3, sh_nfa.hip, status 1;
 SH_DISABLE_S3B=1) and the general engine (SH_NO_SEQ3=1, status 0): bit-exact
 against the oracle at 300k events (with price ties), against the vectorised
@@ -38,7 +38,7 @@ def _gpu(text, ts, cols, keys, nk):
     return r
 
 
-ENGINE = {"s3b": 2, "s3b2": 2, "seq3": 1, "general": 0}
+ENGINE = {"s3b": 2, "seq3": 1, "general": 0}
 
 
 def _engine(engine, monkeypatch):
@@ -46,12 +46,10 @@ def _engine(engine, monkeypatch):
         monkeypatch.setenv("SH_NO_SEQ3", "1")
     elif engine == "seq3":
         monkeypatch.setenv("SH_DISABLE_S3B", "1")
-    elif engine == "s3b2":
-        monkeypatch.setenv("SH_S3B_SUB", "1")
     return ENGINE[engine]
 
 
-@pytest.mark.parametrize("ties,engine", [(False, "s3b"), (True, "s3b"), (False, "s3b2"), (True, "s3b2"),
+@pytest.mark.parametrize("ties,engine", [(False, "s3b"), (True, "s3b"),
                                          (False, "seq3"), (True, "seq3"), (False, "general")])
 def test_c3_vs_oracle(ties, engine, monkeypatch):
     want = _engine(engine, monkeypatch)
@@ -66,7 +64,7 @@ def test_c3_vs_oracle(ties, engine, monkeypatch):
     assert np.array_equal(gseq, seq.astype(np.int64)) and np.array_equal(gvals, vals)
 
 
-@pytest.mark.parametrize("engine", ["s3b", "s3b2", "seq3"])
+@pytest.mark.parametrize("engine", ["s3b", "seq3"])
 def test_c3_full_size_vs_restatement(engine, monkeypatch):
     want = _engine(engine, monkeypatch)
     n, nk = 100_000_000, 1_000_000
