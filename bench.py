@@ -400,7 +400,7 @@ def check_rows(W, oseq, ovals, oq, sel_range=None):
 def engine_tag():
     """identifies the device pipeline a PMC profile was taken on (bumped when a
     pipeline's kernels change what they move)"""
-    return "r5"
+    return "r6"
 
 
 def cpu_baseline(args, W, n):
