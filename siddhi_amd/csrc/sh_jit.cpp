@@ -967,6 +967,7 @@ bool gen_bucket(const shp_program& P, const ExtForm& F, const std::vector<int>& 
             "        if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);\n"
             "        s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);\n"
             "        s_msk[i - hl] = (uint16_t)mask;\n"
+            "        slow_ |= (int)(mask & SHB_MOVF);\n"
             "        ci = -1;\n"
             "    }\n"
             "    const uint64_t im_ = __ballot(ci < 0);\n"
@@ -1226,6 +1227,9 @@ for (int k = 0; k < SHB_NR; k++) {
 __syncthreads();
 SHB_PROF(1)
 )";
+    // slow_: some consumer took a partial beyond the mask's SHB_MSTEPS steps (its
+    // match-stream values then come from a second walk)
+    src += "int slow_ = 0;\n";
     if (fdom && kWalkDyn) {
         // consumers (chunk events): per-lane work hand-out over each wave's range
         src += "// consumers (chunk events): partials taken per event\n" + walk_count_f_dyn() + "__syncthreads();\n";
@@ -1240,6 +1244,7 @@ uint32_t c_ = 0;
         src += R"(if (c_ > 255u) atomicOr(P.flag, SHB_F_COUNT);
 s_pre[i - hl] = (uint16_t)(c_ > 255u ? 255u : c_);
 s_msk[i - hl] = (uint16_t)mask;
+slow_ |= (int)(mask & SHB_MOVF);
 }
 __syncthreads();)";
     }
@@ -1292,18 +1297,24 @@ SHB_PROF(3)
     const bool stage1 = ms_attrs.size() == 1 && type_width_of(P.attr_type[0][ms_attrs[0]]) == 4;
     if (stage1) {
         const std::string a0 = lds(ms_attrs[0]);
-        src += "int slow_ = 0;\nfor (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {\n"
-               "    const int i = hl + (int)(s_cons[ci] >> 16);\n"
-               "    if (s_msk[i - hl] & SHB_MOVF) slow_ = 1;\n}\n"
-               "if (!__syncthreads_or(slow_)) {\n"
-               "for (int ci = threadIdx.x; ci < nc; ci += SHB_TPB) {\n"
-               "    const uint32_t cw = s_cons[ci];\n"
-               "    const int sp = (int)(cw & 0xFFFFu), i = hl + (int)(cw >> 16);\n"
-               "    const uint32_t off = s_pre[i - hl];\n"
-               "    const uint32_t cn = ((i + 1 < L) ? (uint32_t)s_pre[i + 1 - hl] : total) - off;\n"
-               "    uint32_t m = s_msk[i - hl], k = 0;\n"
+        // (every consumer's LDS words loaded before any value moves: one round
+        // trip for the chunk's at most SHB_CHJ / SHB_TPB consumers per thread)
+        src += "if (!__syncthreads_or(slow_)) {\n"
+               "int sp_[SHB_CHJ / SHB_TPB];\nuint32_t off_[SHB_CHJ / SHB_TPB], m_[SHB_CHJ / SHB_TPB], "
+               "nx_[SHB_CHJ / SHB_TPB];\n"
+               "#pragma unroll\nfor (int q = 0; q < SHB_CHJ / SHB_TPB; q++) {\n"
+               "    const int ci = (int)threadIdx.x + q * SHB_TPB;\n"
+               "    const uint32_t cw = ci < nc ? s_cons[ci] : 0u;\n"
+               "    const int i = hl + (int)(cw >> 16);\n"
+               "    sp_[q] = (int)(cw & 0xFFFFu);\n"
+               "    off_[q] = ci < nc ? (uint32_t)s_pre[i - hl] : 0u;\n"
+               "    nx_[q] = ci < nc && i + 1 < L ? (uint32_t)s_pre[i + 1 - hl] : total;\n"
+               "    m_[q] = ci < nc ? (uint32_t)s_msk[i - hl] : 0u;\n}\n"
+               "#pragma unroll\nfor (int q = 0; q < SHB_CHJ / SHB_TPB; q++) {\n"
+               "    const uint32_t off = off_[q], cn = nx_[q] - off;\n"
+               "    uint32_t m = m_[q], k = 0;\n"
                "    while (m) {\n"
-               "        const int o = sp - __ffs(m);\n"
+               "        const int o = sp_[q] - __ffs(m);\n"
                "        m &= m - 1u;\n"
                "        s_ws[off + (cn - 1u - k)] = (uint32_t)" + a0 + "[o];\n"
                "        k++;\n"
