@@ -83,6 +83,10 @@ int shr_keys(const uint32_t* rec_q, const uint32_t* rec_r, int64_t m, const uint
              uint32_t* k1, uint32_t* k2, void* stream,
              const int32_t* akeys = nullptr, const uint32_t* run_ids = nullptr,
              int32_t* long_run = nullptr);
+// after the passes by (run, rule, offset) of records taken in any order: each run
+// of equal keys (k2 may be NULL) put in rec_p order, in place
+int shr_order_ties(uint32_t* order, int64_t m, const uint32_t* k0, const uint32_t* k1, const uint32_t* k2,
+                   const uint32_t* rec_p, void* stream);
 // gk[i] = key[order[i]], gv[i] = order[i] (order NULL: identity)
 int shr_gather(const uint32_t* key, const uint32_t* order, int64_t m, uint32_t* gk, uint32_t* gv, void* stream);
 // ordered output rows from the sorted record order
