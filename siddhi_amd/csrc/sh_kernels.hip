@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(TPB, (B <= 8 ? 4 : 3)) k_digit_scatter(const u
                                                        uint32_t sentinel, const uint32_t* __restrict__ idx_in, int64_t n,
                                                        int shift, const uint32_t* __restrict__ offs, int64_t ntiles,
                                                        uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out,
-                                                       shd_payload PL, int sub_shift, int xcd) {
+                                                       shd_payload PL, int sub_shift, int xcd, int counts = 0) {
     // xcd: consecutive tiles go to one XCD (blocks are dealt round-robin over the 8
     // XCDs), so the short per-digit runs neighbouring tiles write into the same digit
     // region meet in one L2 and leave it as whole lines
@@ -204,7 +204,21 @@ __global__ void __launch_bounds__(TPB, (B <= 8 ? 4 : 3)) k_digit_scatter(const u
     for (int d = threadIdx.x; d < ND; d += TPB) {
 #pragma unroll
         for (int q = 0; q < TPB / 64; q++) wcnt[q][d] = 0;
-        gbase[d] = offs[hist_idx<B>(d, (uint32_t)tile, ntiles, sub_shift)];
+        if (!counts) gbase[d] = offs[hist_idx<B>(d, (uint32_t)tile, ntiles, sub_shift)];
+    }
+    if (B == 8 && counts) {
+        // offs holds the tiles' digit counts (digit-major, at most SMALL_TILES tiles):
+        // the digit's start (scan over the digits' totals) plus the earlier tiles'
+        // (8-bit digits: one per thread)
+        const uint32_t* c = offs + (int64_t)threadIdx.x * ntiles;
+        uint32_t tot = 0, before = 0;
+        for (int t = 0; t < (int)ntiles; t++) {
+            const uint32_t v = c[t];
+            before += t < (int)tile ? v : 0u;
+            tot += v;
+        }
+        uint32_t all;
+        gbase[threadIdx.x] = block_excl_scan(tot, &all) + before;
     }
     uint32_t key[RADIX_ITEMS];
 #pragma unroll
@@ -930,6 +944,7 @@ extern "C" int shd_segment_payload(const shd_batch* b, int32_t nkeys, shd_segmen
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+#define SMALL_TILES 16
 // stable LSD radix sort of (key, value) pairs by the low `bits` of the key
 // (vals NULL: identity); the result lies in the kbuf / vbuf ping-pong buffers,
 // which must not alias the inputs
@@ -947,11 +962,17 @@ extern "C" int shd_sort_pairs(const uint32_t* keys, const uint32_t* vals, int64_
         const int shift = ps * 8;
         hipLaunchKernelGGL(k_digit_hist<8>, dim3((unsigned)ntiles), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
                            0xFFFFFFFFu, n, shift, hist, ntiles, -1);
-        int rc = shd_exclusive_scan(hist, hist, 256 * ntiles, scan_tmp, stream);
-        if (rc) return rc;
+        // a few tiles (a rule run's records): every scatter workgroup sums the counts
+        // itself, no scan launches
+        // (profiles/r6_c5_sort_small_ab.txt: the record order 0.05 ms faster on C5)
+        const bool small = ntiles <= SMALL_TILES;
+        if (!small) {
+            int rc = shd_exclusive_scan(hist, hist, 256 * ntiles, scan_tmp, stream);
+            if (rc) return rc;
+        }
         hipLaunchKernelGGL(k_digit_scatter<8>, dim3(scatter_grid(ntiles)), dim3(TPB), 0, st, kin, (const int32_t*)nullptr,
                            0xFFFFFFFFu, vin, n, shift, (const uint32_t*)hist, ntiles, kbuf[ps & 1], vbuf[ps & 1], PL,
-                           -1, radix_xcd());
+                           -1, radix_xcd(), small ? 1 : 0);
         kin = kbuf[ps & 1];
         vin = vbuf[ps & 1];
     }
