@@ -742,6 +742,20 @@ __device__ __forceinline__ void spa_stage(const uint8_t* __restrict__ img, const
     if (threadIdx.x < 32) s_col[threadIdx.x] = C->col[0][threadIdx.x];
 }
 
+// open's image: everything but f2's terms (the host's descriptor for it has f1's
+// terms moved down over them: off_terms1 <= off_terms0 and the bytes between the
+// image's f2 terms and f1 terms skipped -- I.pad below)
+template <bool IMG>
+__device__ __forceinline__ void spa_stage_open(const uint8_t* __restrict__ img, const shr_img& I,
+                                               const shd_cols* __restrict__ C, uint4* s_img, const void** s_col) {
+    if (IMG) {
+        const int cut = I.off_terms1 / 16, skip = I.pad / 16;  // (pad: the f2 terms' bytes, a multiple of 16)
+        for (int i = threadIdx.x; i < I.lds / 16; i += blockDim.x)
+            s_img[i] = ((const uint4*)img)[i < cut ? i : i + skip];
+    }
+    if (threadIdx.x < 32) s_col[threadIdx.x] = C->col[0][threadIdx.x];
+}
+
 // candidate rule group of an index value: [lo, hi) of the rule ids
 template <bool IMG>
 __device__ __forceinline__ void spa_candidates(const shr_table* __restrict__ RT, const shr_img& I, const SpaRules& S,
@@ -813,10 +827,17 @@ __device__ __forceinline__ bool spa_f2(const shr_table* __restrict__ RT, const s
 }
 
 #define SPA_WBUF 192  // partials a wave holds before it appends them (one global atomic per flush)
-#define SPA_PAIRS 6144  // (event, candidate rule) pairs of a round expanded in LDS, at most
+// (event, candidate rule) pairs of a round expanded in LDS, at most: 1.5 per event
+#define SPO_TPB 512  // k_sparse_open's workgroup
+template <int TPB>
+struct SpaOpen {
+    static constexpr int PAIRS = TPB * SPA_U * 3 / 2;
+    static constexpr int WBUF = TPB >= 1024 ? SPA_WBUF : 128;
+    static constexpr int LDS = 3 * (TPB / 64) * WBUF * 4 + PAIRS * 4 + 512;  // static arrays, bytes (about)
+};
 
-template <bool IMG>
-__global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __restrict__ RT,
+template <bool IMG, int OTPB>
+__global__ void __launch_bounds__(OTPB) k_sparse_open(const shr_table* __restrict__ RT,
                                                          const int64_t* __restrict__ ts,
                                                          const int32_t* __restrict__ akeys, int64_t n, int32_t nkeys,
                                                          const shd_cols* __restrict__ C,
@@ -829,13 +850,16 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
     __shared__ const void* s_col[32];
     // per wave: its pending partials (opening event, rule, key) and their count --
     // waves run independently, no block barrier after the image is staged
-    __shared__ uint32_t w_p[SPA_TPB / 64][SPA_WBUF], w_r[SPA_TPB / 64][SPA_WBUF], w_k[SPA_TPB / 64][SPA_WBUF];
-    __shared__ uint32_t w_fill[SPA_TPB / 64];
+    __shared__ uint32_t w_p[OTPB / 64][SpaOpen<OTPB>::WBUF], w_r[OTPB / 64][SpaOpen<OTPB>::WBUF],
+        w_k[OTPB / 64][SpaOpen<OTPB>::WBUF];
+    __shared__ uint32_t w_fill[OTPB / 64];
     // a round's (event, candidate rule) pairs: rule << 12 | the event's index in the round
-    __shared__ uint32_t s_pair[SPA_PAIRS];
-    __shared__ uint32_t s_ws[SPA_TPB / 64];
-    static_assert(SPA_TPB * SPA_U <= 4096, "12-bit event index in a pair");
-    spa_stage<IMG>(img, I, C, s_img, s_col);
+    __shared__ uint32_t s_pair[SpaOpen<OTPB>::PAIRS];
+    constexpr int SPA_PAIRS = SpaOpen<OTPB>::PAIRS;
+    constexpr int SPA_WBUF_ = SpaOpen<OTPB>::WBUF;
+    __shared__ uint32_t s_ws[OTPB / 64];
+    static_assert(OTPB * SPA_U <= 4096, "12-bit event index in a pair");
+    spa_stage_open<IMG>(img, I, C, s_img, s_col);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     if (lane == 0) w_fill[wv] = 0u;
@@ -860,7 +884,7 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
             }
         }
     };
-    const int64_t round = (int64_t)SPA_TPB * SPA_U;
+    const int64_t round = (int64_t)OTPB * SPA_U;
     for (int64_t base = (int64_t)blockIdx.x * round; base < n; base += (int64_t)gridDim.x * round) {
         // SPA_U runs of the workgroup's events: ts, key, index value
         int64_t tv[SPA_U], tp[SPA_U];
@@ -868,7 +892,7 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
         int64_t xv[SPA_U];
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
-            const int64_t p = base + (int64_t)u * SPA_TPB + threadIdx.x;
+            const int64_t p = base + (int64_t)u * OTPB + threadIdx.x;
             const bool in = p < n;
             tv[u] = in ? ts[p] : 0;
             tp[u] = in && p > 0 ? ts[p - 1] : INT64_MIN;
@@ -892,7 +916,7 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
         for (int u = 0; u < SPA_U; u++)
             tc += (key[u] >= 0 && key[u] < nkeys) ? hi[u] - lo[u] + n_free : 0u;
         uint32_t np_;
-        const uint32_t at0 = shw_block_excl<SPA_TPB>(tc, s_ws, &np_);
+        const uint32_t at0 = shw_block_excl<OTPB>(tc, s_ws, &np_);
         for (uint32_t b0 = 0; b0 < np_; b0 += SPA_PAIRS) {
             const uint32_t b1 = b0 + SPA_PAIRS;
             uint32_t at = at0;
@@ -904,11 +928,11 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
                 for (uint32_t k = 0; k < total; k++, at++)
                     if (at >= b0 && at < b1)
                         s_pair[at - b0] = (spa_rule_id<IMG>(RT, I, S, lo[u], k, nsel) << 12) |
-                                          (uint32_t)(u * SPA_TPB + (int)threadIdx.x);
+                                          (uint32_t)(u * OTPB + (int)threadIdx.x);
             }
             __syncthreads();
             const uint32_t nb = min(np_ - b0, (uint32_t)SPA_PAIRS);
-            for (uint32_t q0 = 0; q0 < nb; q0 += SPA_TPB) {
+            for (uint32_t q0 = 0; q0 < nb; q0 += OTPB) {
                 const uint32_t q = q0 + threadIdx.x;
                 bool ok = false;
                 uint32_t r = 0u, pp = 0u;
@@ -933,7 +957,7 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
                 const uint32_t wat = fill + (uint32_t)__popcll(m & lt);
                 if (ok) {
                     atomicAdd(&key_cnt[kk], 1u);  // (no return: the slot is taken at placement)
-                    if (wat < SPA_WBUF) {
+                    if (wat < SPA_WBUF_) {
                         w_p[wv][wat] = pp;
                         w_r[wv][wat] = r;
                         w_k[wv][wat] = (uint32_t)kk;
@@ -946,9 +970,9 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_open(const shr_table* __rest
                         }
                     }
                 }
-                const uint32_t nf = min(fill + (uint32_t)__popcll(m), (uint32_t)SPA_WBUF);
+                const uint32_t nf = min(fill + (uint32_t)__popcll(m), (uint32_t)SPA_WBUF_);
                 if (lane == 0) w_fill[wv] = nf;
-                if (nf > SPA_WBUF - 64) {
+                if (nf > SPA_WBUF_ - 64) {
                     flush(nf);
                     if (lane == 0) w_fill[wv] = 0u;
                 }
@@ -1128,25 +1152,40 @@ extern "C" int shr_sparse_open(const shr_table* dT, const int64_t* ts, const int
                                unsigned long long* ctr, int64_t cap, int32_t* flag, const int32_t* pre,
                                void* stream) {
     const int pa0 = pre ? pre[0] : -1, pa1 = pre ? pre[1] : -1;
-    shr_img none;
-    memset(&none, 0, sizeof(none));
-    const int buf = 3 * (SPA_TPB / 64) * SPA_WBUF * 4 + SPA_PAIRS * 4 + 512;
-    static const int lim = spa_img_attr(&k_sparse_open<true>);
-    const bool use_img = spa_img_fits(img, I, buf) && I->lds <= lim &&
-                         !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0');
-    int64_t g = (n + SPA_TPB * SPA_U - 1) / (SPA_TPB * SPA_U);
-    const int per_cu = use_img ? (160 * 1024) / (I->lds + buf) : (160 * 1024) / buf;
-    const int64_t gmax = 256LL * std::max(1, std::min(per_cu, 2));
+    // 512-thread workgroups on an image without f2's terms: two per CU, whose block
+    // phases overlap (one 1,024-thread workgroup per CU on the whole image: segment
+    // 2.17 vs 2.06 ms on C5, profiles/r6_c5_open512_ab.txt)
+    shr_img IO;
+    memset(&IO, 0, sizeof(IO));
+    if (img && I && I->bytes > 0 && !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0')) {
+        IO = *I;
+        // f2's terms [off_terms1, off_terms0) left out; f1's terms moved down over them
+        const int t1 = I->off_terms0 - I->off_terms1;
+        IO.pad = 0;
+        if (t1 > 0 && I->off_terms0 < I->lds && t1 % 16 == 0) {
+            IO.pad = t1;
+            IO.off_terms0 = I->off_terms1;
+            IO.lds = I->lds - t1;
+        } else if (t1 > 0 && I->off_terms0 >= I->lds) {
+            IO.lds = I->off_terms1;  // (f1's terms in global memory: only the f2 terms cut)
+        }
+    }
+    constexpr int T = SPO_TPB;
+    const int buf = SpaOpen<T>::LDS;
+    static const int lim = spa_img_attr(&k_sparse_open<true, T>);
+    const bool use_img = IO.bytes > 0 && spa_img_fits(img, &IO, buf) && IO.lds <= lim;
+    int64_t g = (n + T * SPA_U - 1) / (T * SPA_U);
+    const int per_cu = use_img ? (160 * 1024) / (IO.lds + buf) : (160 * 1024) / buf;
+    const int64_t gmax = 256LL * std::max(1, std::min(per_cu, 4));
     if (g > gmax) g = gmax;  // each workgroup strides over the run (the image staged once, few buffer flushes)
     if (g < 1) g = 1;
     if (use_img)
-        hipLaunchKernelGGL(k_sparse_open<true>, dim3((unsigned)g), dim3(SPA_TPB), (size_t)I->lds, (hipStream_t)stream, dT,
-                           ts, akeys, n, nkeys, dC, img, *I, pr_p, pr_r, pr_key, key_cnt, ctr, cap, flag, pa0, pa1);
+        hipLaunchKernelGGL((k_sparse_open<true, T>), dim3((unsigned)g), dim3(T), (size_t)IO.lds, (hipStream_t)stream, dT,
+                           ts, akeys, n, nkeys, dC, img, IO, pr_p, pr_r, pr_key, key_cnt, ctr, cap, flag, pa0, pa1);
     else
-        hipLaunchKernelGGL(k_sparse_open<false>, dim3((unsigned)g), dim3(SPA_TPB), 0, (hipStream_t)stream, dT, ts, akeys,
-                           n, nkeys, dC, img && I && I->bytes > 0 ? img : (const uint8_t*)nullptr,
-                           img && I && I->bytes > 0 ? *I : none, pr_p, pr_r, pr_key, key_cnt, ctr, cap,
-                           flag, pa0, pa1);
+        hipLaunchKernelGGL((k_sparse_open<false, T>), dim3((unsigned)g), dim3(T), 0, (hipStream_t)stream, dT, ts, akeys,
+                           n, nkeys, dC, IO.bytes > 0 ? img : (const uint8_t*)nullptr, IO, pr_p, pr_r, pr_key, key_cnt,
+                           ctr, cap, flag, pa0, pa1);
     return rules_ok();
 }
 
