@@ -314,13 +314,19 @@ __global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out 
     // the slot prefix (phases 1-2) and the row maps (phase 3) share storage: phase 3
     // starts after the barrier that ends every wave's phase 2 (42 KB instead of 75:
     // three workgroups per CU when the registers allow)
-    constexpr int BK_MAPW = (BK_TPB / 64) * (BK_EROWS / 2 + BK_EHALF + BK_EHALF / 2);
+    // LM (6 waves per SIMD, <= 80 VGPRs): the wave's 1,024 match-stream positions go
+    // to LDS once (emp holds both halves) instead of living in registers through the
+    // row loop, and a half's row map holds 512 rows (more: the event-parallel path)
+    constexpr bool LM = BK_OCC >= 6;
+    constexpr int EROWS = LM ? 512 : BK_EROWS;
+    constexpr int EMPW = LM ? 2 * BK_EHALF : BK_EHALF;
+    constexpr int BK_MAPW = (BK_TPB / 64) * (EROWS / 2 + EMPW + BK_EHALF / 2);
     __shared__ uint32_t pool[(SHB_TILE + 1) > BK_MAPW ? (SHB_TILE + 1) : BK_MAPW];
     uint32_t* const pfx = pool;
-    uint16_t(*const rmap)[BK_EROWS] = (uint16_t(*)[BK_EROWS])pool;
-    uint32_t(*const emp)[BK_EHALF] = (uint32_t(*)[BK_EHALF])(pool + (BK_TPB / 64) * (BK_EROWS / 2));
+    uint16_t(*const rmap)[EROWS] = (uint16_t(*)[EROWS])pool;
+    uint32_t(*const emp)[EMPW] = (uint32_t(*)[EMPW])(pool + (BK_TPB / 64) * (EROWS / 2));
     uint16_t(*const ero)[BK_EHALF] =
-        (uint16_t(*)[BK_EHALF])(pool + (BK_TPB / 64) * (BK_EROWS / 2 + BK_EHALF));
+        (uint16_t(*)[BK_EHALF])(pool + (BK_TPB / 64) * (EROWS / 2 + EMPW));
     __shared__ uint32_t ms0[SHB_NB];
     __shared__ uint16_t to[SHB_NB + 1];
     __shared__ uint32_t wtot[BK_TPB / 64], ws[BK_TPB / 64];
@@ -420,6 +426,10 @@ __global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out 
         if (lane == 0) wtot[w] = wsum;
     }
     __syncthreads();
+    if (LM) {
+#pragma unroll
+        for (int j = 0; j < BK_ITEMS; j++) emp[w][j * 64 + lane] = mp[j];
+    }
     uint64_t rb = s_tb;  // this wave's first row
     for (int q = 0; q < w; q++) rb += wtot[q];
     // 3. rows, one half (512 events) at a time
@@ -433,12 +443,12 @@ __global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out 
             const uint32_t c = (cp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
             const uint32_t incl = shw_incl_scan(c);
             const uint32_t ro = carry + incl - c;
-            ro8[jj] = ro;
+            if (!LM) ro8[jj] = ro;
             const int e = jj * 64 + lane;
-            emp[w][e] = mp[j];
+            if (!LM) emp[w][e] = mp[j];
             ero[w][e] = (uint16_t)ro;
             for (uint32_t k = 0; k < c; k++)
-                if (ro + k < BK_EROWS) rmap[w][ro + k] = (uint16_t)e;
+                if (ro + k < EROWS) rmap[w][ro + k] = (uint16_t)e;
             carry += shw_last(incl);
         }
         const uint32_t R = carry;
@@ -446,7 +456,8 @@ __global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (R <= BK_EROWS) {
+        const int eo = LM ? hf * BK_EHALF : 0;  // the half's first entry of emp
+        if (R <= EROWS) {
             // row-parallel: lane t writes rows t, t + 64, ... (consecutive lanes,
             // consecutive rows); BK_RU rows' loads go out before their stores
             if (NO > 0) {
@@ -463,7 +474,7 @@ __global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out 
                             const int e = rmap[w][t];
                             const uint32_t k = t - ero[w][e];
                             ii[u] = ib + e;
-                            bk_vals<NV>(O, ii[u], (int64_t)emp[w][e] + k, (int64_t)rb + t, v[u]);
+                            bk_vals<NV>(O, ii[u], (int64_t)emp[w][eo + e] + k, (int64_t)rb + t, v[u]);
                         }
                     }
 #pragma unroll
@@ -479,21 +490,32 @@ __global__ void __launch_bounds__(BK_TPB, BK_OCC) k_bk_emit(shb_plan P, shb_out 
                     const int64_t i = ib + e;
                     const int64_t row = (int64_t)rb + t;
                     if (row >= out_cap) continue;  // the host reports SH_E_MORE
-                    bk_row<MODE, NO>(O, OC, o_kind, o_type, o_src, row, i, (int64_t)emp[w][e] + k,
+                    bk_row<MODE, NO>(O, OC, o_kind, o_type, o_src, row, i, (int64_t)emp[w][eo + e] + k,
                                      seq_base + (uint64_t)i, out_seq, out_vals);
                 }
             }
         } else {
             // a dense half (more rows than the map holds): each event writes its rows
+            // (LM: its first row from the same scan again, not kept in registers)
+            uint32_t carry2 = 0;
 #pragma unroll
             for (int jj = 0; jj < 8; jj++) {
                 const int j = hf * 8 + jj;
                 const uint32_t c = (cp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
                 const int64_t i = ib + jj * 64 + lane;
+                uint32_t ro = 0;
+                if (LM) {
+                    const uint32_t incl = shw_incl_scan(c);
+                    ro = carry2 + incl - c;
+                    carry2 += shw_last(incl);
+                } else {
+                    ro = ro8[jj];
+                }
                 for (uint32_t k = 0; k < c; k++) {
-                    const int64_t row = (int64_t)rb + ro8[jj] + k;
+                    const int64_t row = (int64_t)rb + ro + k;
                     if (row >= out_cap) break;
-                    bk_row<MODE, NO>(O, OC, o_kind, o_type, o_src, row, i, (int64_t)mp[j] + k,
+                    bk_row<MODE, NO>(O, OC, o_kind, o_type, o_src, row, i,
+                                     (int64_t)(LM ? emp[w][j * 64 + lane] : mp[j]) + k,
                                      seq_base + (uint64_t)i, out_seq, out_vals);
                 }
             }
@@ -1435,18 +1457,35 @@ extern "C" int shb_agg_carry(const shb_plan* P, const shb_aggc* A, void* stream)
     return bk_ok();
 }
 
+// rows per lane and round of the 6-waves-per-SIMD form (LM: match-stream positions
+// in LDS, <= 80 VGPRs): the most that compile without spilling VGPRs; 0 = that form
+// does not fit (more values per row: the 4-waves form below)
+template <int MODE, int NO>
+constexpr int bk_ru_lm() {
+    return NO == 0 ? 4
+         : MODE == SHB_OUT_COLS ? (NO <= 2 ? 4 : 0)
+                                : (NO <= 3 ? 4 : NO == 4 ? 3 : NO == 5 ? 2 : 1);
+}
+
 template <int MODE, int NO>
 static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& OC, uint64_t seq_base,
                            uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
-    // 6 rows per lane and round up to 4 values (1.505 vs 1.526 ms for 4 on C2,
-    // profiles/r4_c2_emit_ru_ab.txt), fewer beyond: as many as fit 128 VGPRs without
-    // spilling (packed rows and typed columns hold more per row than raw ones)
+    // 6 waves per SIMD where the row loop fits 80 VGPRs (profiles/r6_emit6_ab.txt):
+    // C2 (packed, 4 values) emit 1.47 -> 1.26 ms at 3 rows per lane, C3 (raw, 3
+    // values) 0.85 -> 0.75, C2 + aggregates (packed, 6 values, 1 row) 2.35 -> 2.31
+    constexpr int RL = bk_ru_lm<MODE, NO>();
+    if constexpr (RL > 0) {
+        hipLaunchKernelGGL((k_bk_emit<MODE, NO, RL, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream,
+                           *P, *O, OC, seq_base, out_seq, out_vals, out_cap);
+        return;
+    }
+    // otherwise 4 waves per SIMD: 6 rows per lane and round up to 4 values (1.505 vs
+    // 1.526 ms for 4 on C2, profiles/r4_c2_emit_ru_ab.txt), fewer beyond: as many as
+    // fit 128 VGPRs without spilling
     constexpr int RU = (NO >= 1 && NO <= 4) ? (MODE == SHB_OUT_COLS && NO == 4 ? 4 : 6)
                                             : (MODE == SHB_OUT_RAW ? (NO <= 6 ? 4 : 3)
                                                                    : (MODE == SHB_OUT_PACKED ? (NO <= 6 ? 4 : (NO == 7 ? 2 : 1))
                                                                                              : (NO <= 5 ? 2 : 1)));
-    // (6 waves per SIMD at 2 rows per lane: 1.40 vs 1.46 ms on C2 but 22 VGPRs spilled
-    // and 0.9 GB more traffic per step, profiles/r5_c2_emit_occ_ab.txt: not kept)
     hipLaunchKernelGGL((k_bk_emit<MODE, NO, RU>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream, *P,
                        *O, OC, seq_base, out_seq, out_vals, out_cap);
 }
