@@ -1464,7 +1464,7 @@ template <int MODE, int NO>
 constexpr int bk_ru_lm() {
     return NO == 0 ? 4
          : MODE == SHB_OUT_COLS ? (NO <= 2 ? 4 : 0)
-                                : (NO <= 3 ? 4 : NO == 4 ? 3 : NO == 5 ? 2 : 1);
+                                : (NO <= 3 ? 4 : NO == 4 ? 3 : NO == 5 ? 2 : 0);
 }
 
 template <int MODE, int NO>
@@ -1472,7 +1472,9 @@ static void bk_emit_launch(const shb_plan* P, const shb_out* O, const shb_cols& 
                            uint64_t* out_seq, int64_t* out_vals, int64_t out_cap, void* stream) {
     // 6 waves per SIMD where the row loop fits 80 VGPRs (profiles/r6_emit6_ab.txt):
     // C2 (packed, 4 values) emit 1.47 -> 1.26 ms at 3 rows per lane, C3 (raw, 3
-    // values) 0.85 -> 0.75, C2 + aggregates (packed, 6 values, 1 row) 2.35 -> 2.31
+    // values) 0.85 -> 0.75. Six values or more stay at 4 waves: C2 + aggregates at 6
+    // waves (1 row per lane) was 2.35 -> 2.31 ms but fetched 10.2 GB past L2 instead
+    // of 7.6 (its running values by match-stream position thrash L2 harder)
     constexpr int RL = bk_ru_lm<MODE, NO>();
     if constexpr (RL > 0) {
         hipLaunchKernelGGL((k_bk_emit<MODE, NO, RL, 6>), dim3(bk_grid(P->nt)), dim3(BK_TPB), 0, (hipStream_t)stream,
