@@ -222,6 +222,12 @@ __device__ __forceinline__ bool rule_terms_pre(const shp_term* T, int nt, uint32
         l.t = X.ltype;
         l.null = 0;
         l.b = rule_attr_pre(cols, X.lattr, X.ltype, lr, X.lslot, R);
+        // a float attribute against a double constant (Java compares as double): the
+        // same compare without the generic value / domain dispatch
+        if (X.rkind == 1 && X.dom == DOM_F64 && X.ltype == SH_T_FLOAT && X.ctype == SH_T_DOUBLE) {
+            if (!cmp_op<double>(X.op, (double)__uint_as_float((uint32_t)l.b), __longlong_as_double(X.c))) return false;
+            continue;
+        }
         if (X.rkind == 1) {
             r.t = X.ctype;
             r.null = 0;
