@@ -1022,6 +1022,7 @@ __global__ void k_sparse_place(const uint32_t* __restrict__ pr_p, const uint32_t
     }
 }
 
+#define SPA_TQ 256  // (event, list entry) pairs a wave queues at a time (k_sparse_take)
 template <bool IMG>
 __global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __restrict__ RT,
                                                          const int64_t* __restrict__ ts,
@@ -1035,10 +1036,12 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __rest
                                                          shr_live LV, int pa0, int pa1) {
     extern __shared__ uint4 s_img[];
     __shared__ const void* s_col[32];
+    __shared__ uint32_t s_tq[SPA_TPB / 64][SPA_TQ], s_tp[SPA_TPB / 64][SPA_TQ];
     spa_stage<IMG>(img, I, C, s_img, s_col);
     __syncthreads();
     const SpaRules S{(const uint8_t*)s_img, img, s_col};
     constexpr int TPB = SPA_TPB;
+    const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
     const int64_t wb = (int64_t)blockIdx.x, nw = (int64_t)gridDim.x;
     // SPA_U events per thread and round: their key, list bounds and first list
     // entry are loaded together (three dependent random reads per event otherwise)
@@ -1079,22 +1082,50 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __rest
                 hi[u] = key_off[key[u] + 1];
             }
         }
+        // the wave's (event, list entry) pairs of the round into its LDS queue, then one
+        // lane per pair: the few events whose key has live partials (~1% on C5) pay the
+        // list's dependent reads once per round together, not once per event slot u
+        // (C5 advance 2.43 -> 1.61 ms, profiles/r6_c5_take_queue_ab.txt)
+        uint32_t off[SPA_U], wtot = 0;
 #pragma unroll
         for (int u = 0; u < SPA_U; u++) {
-            if (lo[u] == hi[u]) continue;
-            const int64_t q = base + (int64_t)u * TPB + threadIdx.x;
-            // f2's most read attributes of the consumer, loaded once for its list
-            RowPre rp;
-            rp.slot = 1;
-            rp.a[0] = pa0;
-            rp.a[1] = pa1;
-            rp.v[0] = pa0 >= 0 ? rule_attr(S.cols, pa0, RT->attr_type[pa0], (uint32_t)q) : 0;
-            rp.v[1] = pa1 >= 0 ? rule_attr(S.cols, pa1, RT->attr_type[pa1], (uint32_t)q) : 0;
-            for (uint32_t pos = lo[u]; pos < hi[u]; pos++) {
-                const uint32_t p = l_p[pos];
-                if ((int64_t)p >= q || tq[u] > l_te[pos]) continue;
-                if (spa_f2<IMG>(RT, I, S, C, l_r[pos], p, (uint32_t)q, rp)) atomicMin(&l_q[pos], (uint32_t)q);
+            const uint32_t c = hi[u] - lo[u];
+            const uint32_t incl = shw_incl_scan(c);
+            off[u] = wtot + incl - c;
+            wtot += shw_last(incl);
+        }
+        for (uint32_t b0 = 0; b0 < wtot; b0 += SPA_TQ) {  // (uniform in the wave)
+#pragma unroll
+            for (int u = 0; u < SPA_U; u++) {
+                const uint32_t q = (uint32_t)(base + (int64_t)u * TPB + threadIdx.x);
+                for (uint32_t k = 0; k < hi[u] - lo[u]; k++) {
+                    const uint32_t at = off[u] + k;
+                    if (at >= b0 && at < b0 + SPA_TQ) {
+                        s_tq[wv][at - b0] = q;
+                        s_tp[wv][at - b0] = lo[u] + k;
+                    }
+                }
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t nb = wtot - b0 < SPA_TQ ? wtot - b0 : SPA_TQ;
+            for (uint32_t j = lane; j < nb; j += 64) {
+                const uint32_t q = s_tq[wv][j], pos = s_tp[wv][j];
+                const uint32_t p = l_p[pos], r = l_r[pos];
+                const int64_t te = l_te[pos], tqq = ts[q];
+                if (p >= q || tqq > te) continue;
+                RowPre rp;
+                rp.slot = 1;
+                rp.a[0] = pa0;
+                rp.a[1] = pa1;
+                rp.v[0] = pa0 >= 0 ? rule_attr(S.cols, pa0, RT->attr_type[pa0], q) : 0;
+                rp.v[1] = pa1 >= 0 ? rule_attr(S.cols, pa1, RT->attr_type[pa1], q) : 0;
+                if (spa_f2<IMG>(RT, I, S, C, r, p, q, rp)) atomicMin(&l_q[pos], q);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
 }
@@ -1214,22 +1245,23 @@ extern "C" int shr_sparse_match(const shr_table* dT, const int64_t* ts, const in
         shr_img none;
         memset(&none, 0, sizeof(none));
         static const int lim = spa_img_attr(&k_sparse_take<true>);
-        const bool use_img = spa_img_fits(img, I, 512) && I->lds <= lim &&
+        const int tstat = 2 * (SPA_TPB / 64) * SPA_TQ * 4 + 512;  // the pair queues + the column pointers
+        const bool use_img = spa_img_fits(img, I, tstat) && I->lds <= lim &&
                              !(getenv("SH_SPARSE_IMG") && getenv("SH_SPARSE_IMG")[0] == '0');
         int64_t tg = (n + SPA_TPB * SPA_U - 1) / (SPA_TPB * SPA_U);
-        const int per_cu = use_img ? (160 * 1024) / (I->lds + 512) : 2;
+        const int per_cu = use_img ? (160 * 1024) / (I->lds + tstat) : 2;
         const int64_t gmax = 256LL * std::max(1, std::min(per_cu, 2));
         if (tg > gmax) tg = gmax;
         if (tg < 1) tg = 1;
         // (slicing the keys by XCD measured 7.17 vs 2.94 ms for take on C5, and 512-thread
         // workgroups lost too, profiles/r4_c5_xcd_ab.txt, r5_c5_take512_ab.txt: removed)
         if (use_img)
-            hipLaunchKernelGGL(k_sparse_take<true>, dim3((unsigned)tg), dim3(SPA_TPB), (size_t)I->lds, st, dT, ts, akeys,
-                               n, dC, img, *I, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
+            hipLaunchKernelGGL((k_sparse_take<true>), dim3((unsigned)tg), dim3(SPA_TPB), (size_t)I->lds, st, dT, ts,
+                               akeys, n, dC, img, *I, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
                                (const int64_t*)l_te, l_q, LV, pa0, pa1);
         else
-            hipLaunchKernelGGL(k_sparse_take<false>, dim3((unsigned)tg), dim3(SPA_TPB), 0, st, dT, ts, akeys, n, dC,
-                               (const uint8_t*)nullptr, none, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
+            hipLaunchKernelGGL((k_sparse_take<false>), dim3((unsigned)tg), dim3(SPA_TPB), 0, st, dT, ts, akeys, n,
+                               dC, (const uint8_t*)nullptr, none, key_off, (const uint32_t*)l_p, (const uint32_t*)l_r,
                                (const int64_t*)l_te, l_q, LV, pa0, pa1);
     }
     hipLaunchKernelGGL(k_sparse_rec, dim3(gp), dim3(256), 0, st, (const uint32_t*)l_p, (const uint32_t*)l_r,
