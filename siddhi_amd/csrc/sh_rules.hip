@@ -513,14 +513,21 @@ __global__ void k_rules_ties(uint32_t* __restrict__ order, int64_t m, const uint
         if (i > 0 && tie_eq(k0, k1, k2, a, order[i - 1])) continue;  // not the run's first
         int64_t j = i + 1;
         while (j + 1 < m && tie_eq(k0, k1, k2, a, order[j + 1])) j++;
-        for (int64_t x = i + 1; x <= j; x++) {
-            const uint32_t v = order[x], pv = rec_p[v];
-            int64_t y = x - 1;
-            while (y >= i && rec_p[order[y]] > pv) {
-                order[y + 1] = order[y];
-                y--;
+        // shell sort of order[i..j] by rec_p (gap 1 alone: insertion sort for the
+        // usual run of 2-3; the gaps keep a hot key's long run near n log n)
+        const int64_t g = j - i + 1;
+        int64_t gap = 1;
+        while (gap * 9 / 4 + 1 < g) gap = gap * 9 / 4 + 1;
+        for (; gap >= 1; gap = gap == 1 ? 0 : (gap * 4) / 9) {
+            for (int64_t x = i + gap; x <= j; x++) {
+                const uint32_t v = order[x], pv = rec_p[v];
+                int64_t y = x - gap;
+                while (y >= i && rec_p[order[y]] > pv) {
+                    order[y + gap] = order[y];
+                    y -= gap;
+                }
+                order[y + gap] = v;
             }
-            order[y + 1] = v;
         }
     }
 }
@@ -1097,13 +1104,17 @@ __global__ void __launch_bounds__(SPA_TPB) k_sparse_take(const shr_table* __rest
         for (uint32_t b0 = 0; b0 < wtot; b0 += SPA_TQ) {  // (uniform in the wave)
 #pragma unroll
             for (int u = 0; u < SPA_U; u++) {
+                // this batch's part of the slot's list only (a hot key's long list costs
+                // its length once over all batches, not once per batch)
                 const uint32_t q = (uint32_t)(base + (int64_t)u * TPB + threadIdx.x);
-                for (uint32_t k = 0; k < hi[u] - lo[u]; k++) {
+                const uint32_t c = hi[u] - lo[u];
+                const uint32_t k0 = b0 > off[u] ? b0 - off[u] : 0u;
+                const uint32_t e = b0 + SPA_TQ > off[u] ? b0 + SPA_TQ - off[u] : 0u;
+                const uint32_t k1 = e < c ? e : c;
+                for (uint32_t k = k0; k < k1; k++) {
                     const uint32_t at = off[u] + k;
-                    if (at >= b0 && at < b0 + SPA_TQ) {
-                        s_tq[wv][at - b0] = q;
-                        s_tp[wv][at - b0] = lo[u] + k;
-                    }
+                    s_tq[wv][at - b0] = q;
+                    s_tp[wv][at - b0] = lo[u] + k;
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
