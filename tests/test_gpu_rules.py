@@ -87,6 +87,28 @@ def test_sparse_partials_vs_oracle(ci):
     assert np.array_equal(vals[:, :2], ref["values"][:, :2])
 
 
+def test_sparse_hot_card_vs_oracle():
+    """a skewed stream: half the transactions on one card and rules whose f2 factor
+    (2-4) lets partials pile up until a large amount takes many of one rule at once
+    (up to 17 per (event, rule) on this stream, 739 such runs), so that card's
+    partial list is long -- k_sparse_take's per-wave pair queue and k_rules_ties'
+    long runs (shell sort) against the oracle"""
+    n, cards, nr, seed = 24_000, 400, 12, 35
+    ts, card, amount, merchant = synth.txn_stream(n, cards, 4, n_merchants=4, seed=seed)
+    card = card.copy()
+    card[::2] = 0
+    rules = synth.c5_rules(nr, seed=seed, amount=(60.0, 400.0), merchants=4, factor=(2.0, 4.0), within=(100, 400))
+    text = synth.c5_query(rules, unit="milliseconds")
+    ref = oracle_run(text, cards, ts, card, amount, merchant, 4096, True)
+    st = []
+    seq, vals, q = _device_run(text, cards, ts, card, amount, merchant, 4096, True, status=st)
+    assert st == [1]
+    assert len(seq) == len(ref["seq"]) > 0
+    assert np.array_equal(seq, ref["seq"].astype(np.int64))
+    assert np.array_equal(q, ref["query"])
+    assert np.array_equal(vals[:, :2], ref["values"][:, :2])
+
+
 @pytest.mark.parametrize("n,cards,sparse", [(20_000_000, 200_000, "1"), (20_000_000, 200_000, "0"),
                                             (100_000_000, 1_000_000, "1")], ids=["20M", "20M-segment", "100M"])
 def test_c5_large_vs_vectorised_restatement(n, cards, sparse, monkeypatch):
