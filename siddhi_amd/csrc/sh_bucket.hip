@@ -827,8 +827,10 @@ __global__ void __launch_bounds__(S3B_TPB) k_s3b(shb_plan P, shb_s3 S) {
                     grow = !hit && (f & 1u) && nf_cmp(S.op2, S.dom2, x, s3b_val(e1b, t));
                 }
                 m_pre[cr] = hit ? 1 : 0;
-                m_v0[cr] = e1b;
-                m_v1[cr] = lastb;
+                if (hit) {  // (the outputs read the values of matching events only)
+                    m_v0[cr] = e1b;
+                    m_v1[cr] = lastb;
+                }
                 if (grow) {
                     f |= 2u;
                     lastb = xb;
